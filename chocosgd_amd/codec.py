@@ -1,0 +1,304 @@
+"""Tensor-level entry points of the MI355X CHOCO codec.
+
+Thin, allocation-light wrappers over the C ABI (include/choco_codec.h): they
+validate that every tensor is a contiguous ROCm device tensor, allocate the
+outputs with torch, pass raw pointers + the current HIP stream, and raise
+RuntimeError on any library error.  CPU tensors are rejected -- there is no CPU
+fallback anywhere in the product path.
+"""
+import ctypes
+import math
+import threading
+
+import torch
+
+from . import _lib
+
+_ws_lock = threading.Lock()
+_ws_cache = {}
+
+
+def _require(t, dtype=None, name="tensor"):
+    if not isinstance(t, torch.Tensor):
+        raise RuntimeError(f"{name} must be a torch.Tensor")
+    if not t.is_cuda:
+        raise RuntimeError(
+            f"chocosgd_amd runs on ROCm device tensors only; {name} is on {t.device}")
+    if dtype is not None and t.dtype != dtype:
+        raise RuntimeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be contiguous")
+    return t
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def workspace(dev, kind, nbytes):
+    """Per (device, stream, kind) scratch buffer; zero-filled on allocation.
+
+    The sign/qsgd accumulators rely on starting zeroed; every kernel that uses
+    them leaves them zeroed again (self-cleaning), so the buffer is reused as is.
+    """
+    nbytes = max(int(nbytes), 256)
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream, kind)
+    with _ws_lock:
+        buf = _ws_cache.get(key)
+        if buf is None or buf.numel() < nbytes:
+            if buf is not None:
+                torch.cuda.current_stream(dev).synchronize()
+            buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+            _ws_cache[key] = buf
+        return buf
+
+
+def lib():
+    return _lib.load()
+
+
+# ----------------------------------------------------------------------------- top-k
+def topk_k(n, ratio):
+    """k = max(1, int(n * (1 - ratio))) (sparsification.py:22,45)."""
+    return int(lib().choco_topk_k(int(n), float(ratio)))
+
+
+def topk(x, k, xhat=None, out=None):
+    """Exact top-k by |x - xhat| (signed values, int32 indices, ascending index).
+
+    `out=(values f32[k], indices i32[k])` writes into caller buffers (e.g. two views
+    of one wire message) instead of allocating."""
+    _require(x, torch.float32, "x")
+    if xhat is not None:
+        _require(xhat, torch.float32, "xhat")
+        if xhat.numel() != x.numel():
+            raise RuntimeError("x and xhat must have the same number of elements")
+    n = x.numel()
+    dev = x.device
+    if out is not None:
+        vals, idx = out
+        _require(vals, torch.float32, "out values")
+        _require(idx, torch.int32, "out indices")
+        if vals.numel() != k or idx.numel() != k:
+            raise RuntimeError("out buffers must hold exactly k elements")
+    else:
+        vals = torch.empty(k, dtype=torch.float32, device=dev)
+        idx = torch.empty(k, dtype=torch.int32, device=dev)
+    L = lib()
+    ws = workspace(dev, "topk", L.choco_topk_workspace_size(n))
+    _lib.check(L.choco_topk_compress(_ptr(x), _ptr(xhat), n, int(k), _ptr(vals), _ptr(idx), _ptr(ws),
+                                     ws.numel(), _stream(dev)), "choco_topk_compress")
+    return vals, idx
+
+
+class SegmentPlan:
+    """Host + device copies of the per-segment top-k plan {off, len, k, out_off}."""
+
+    def __init__(self, seg_lens, ratio, device):
+        L = lib()
+        self.seg_lens = [int(s) for s in seg_lens]
+        self.nseg = len(self.seg_lens)
+        offs = [0]
+        for s in self.seg_lens:
+            offs.append(offs[-1] + s)
+        self.seg_off = offs
+        p_off, self._off_keep = _lib.i64_array(offs)
+        self._plan_host = (ctypes.c_int64 * (4 * self.nseg))()
+        self.plan_host = ctypes.cast(self._plan_host, ctypes.POINTER(ctypes.c_int64))
+        total = L.choco_topk_segmented_plan(p_off, self.nseg, float(ratio), self.plan_host)
+        if total < 0:
+            raise RuntimeError(f"choco_topk_segmented_plan failed: {_lib.last_error()}")
+        self.k_total = int(total)
+        self.k_per_seg = [int(self._plan_host[4 * s + 2]) for s in range(self.nseg)]
+        self.plan_dev = torch.tensor(list(self._plan_host), dtype=torch.int64, device=device)
+        self.ws_bytes = int(L.choco_topk_segmented_workspace_size(self.plan_host, self.nseg))
+
+
+def topk_segmented(x, plan, xhat=None):
+    _require(x, torch.float32, "x")
+    if xhat is not None:
+        _require(xhat, torch.float32, "xhat")
+    dev = x.device
+    vals = torch.empty(plan.k_total, dtype=torch.float32, device=dev)
+    idx = torch.empty(plan.k_total, dtype=torch.int32, device=dev)
+    L = lib()
+    ws = workspace(dev, "topk", plan.ws_bytes)
+    _lib.check(L.choco_topk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
+                                               plan.nseg, _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(),
+                                               _stream(dev)), "choco_topk_compress_segmented")
+    return vals, idx
+
+
+# ----------------------------------------------------------------------------- random-k
+def randk(x, k, seed, is_biased=True, xhat=None):
+    _require(x, torch.float32, "x")
+    if xhat is not None:
+        _require(xhat, torch.float32, "xhat")
+    n = x.numel()
+    dev = x.device
+    vals = torch.empty(k, dtype=torch.float32, device=dev)
+    idx = torch.empty(k, dtype=torch.int32, device=dev)
+    L = lib()
+    ws = workspace(dev, "topk", L.choco_randk_workspace_size(n))
+    _lib.check(L.choco_randk_compress(_ptr(x), _ptr(xhat), n, int(k), int(seed) & (2**64 - 1),
+                                      1 if is_biased else 0, _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(),
+                                      _stream(dev)), "choco_randk_compress")
+    return vals, idx
+
+
+def gather(x, idx, scale=1.0, xhat=None):
+    _require(x, torch.float32, "x")
+    _require(idx, torch.int64, "idx")
+    out = torch.empty(idx.numel(), dtype=torch.float32, device=x.device)
+    _lib.check(lib().choco_gather(_ptr(x), _ptr(xhat), _ptr(idx), idx.numel(), float(scale), _ptr(out),
+                                  _stream(x.device)), "choco_gather")
+    return out
+
+
+def sparse_accumulate(values, indices, memory, weight, xhat_self=None):
+    _require(values, torch.float32, "values")
+    _require(indices, torch.int32, "indices")
+    _require(memory, torch.float32, "memory")
+    if xhat_self is not None:
+        _require(xhat_self, torch.float32, "xhat_self")
+    _lib.check(lib().choco_sparse_accumulate(_ptr(values), _ptr(indices), values.numel(), _ptr(xhat_self),
+                                             _ptr(memory), float(weight), _stream(memory.device)),
+               "choco_sparse_accumulate")
+
+
+# ----------------------------------------------------------------------------- sign
+def sign_words(n):
+    return int(lib().choco_sign_words(int(n)))
+
+
+def sign_compress(x, xhat=None, seg_off=None, nseg=1, want_norms=True):
+    """Pack sign bits in the (32, N') layout; optionally per-segment L1 norms (fp64-accumulated)."""
+    _require(x, torch.float32, "x")
+    if xhat is not None:
+        _require(xhat, torch.float32, "xhat")
+    if seg_off is not None:
+        _require(seg_off, torch.int64, "seg_off")
+    n = x.numel()
+    dev = x.device
+    L = lib()
+    packed = torch.empty(sign_words(n), dtype=torch.int32, device=dev)
+    norms = torch.empty(nseg, dtype=torch.float32, device=dev) if want_norms else None
+    ws = workspace(dev, "acc", L.choco_sign_workspace_size(nseg))
+    _lib.check(L.choco_sign_compress(_ptr(x), _ptr(xhat), n, _ptr(seg_off), int(nseg), _ptr(packed), _ptr(norms),
+                                     _ptr(ws), ws.numel(), _stream(dev)), "choco_sign_compress")
+    return packed, norms
+
+
+def sign_unpack(packed, n):
+    _require(packed, torch.int32, "packed")
+    out = torch.empty(n, dtype=torch.float32, device=packed.device)
+    _lib.check(lib().choco_sign_unpack(_ptr(packed), int(n), _ptr(out), _stream(packed.device)),
+               "choco_sign_unpack")
+    return out
+
+
+def sign_accumulate(messages, weights, self_slot, n, memory, xhat_self=None, seg_off=None, nseg=1):
+    """messages: list of (packed int32[N'], norms f32[nseg]) applied in order."""
+    _require(memory, torch.float32, "memory")
+    for p, nm in messages:
+        _require(p, torch.int32, "packed")
+        _require(nm, torch.float32, "norms")
+    pp, keep1 = _lib.ptr_array([p.data_ptr() for p, _ in messages])
+    nn, keep2 = _lib.ptr_array([nm.data_ptr() for _, nm in messages])
+    ww, keep3 = _lib.f32_array([float(w) for w in weights])
+    _lib.check(lib().choco_sign_decompress_accumulate(pp, nn, ww, len(messages), int(self_slot), int(n),
+                                                      _ptr(seg_off), int(nseg), _ptr(xhat_self), _ptr(memory),
+                                                      ctypes.c_void_p(0), 0, _stream(memory.device)),
+               "choco_sign_decompress_accumulate")
+
+
+# ----------------------------------------------------------------------------- QSGD
+def qsgd_levels_bits(quantize_level):
+    return int(quantize_level)
+
+
+def qsgd_packed_bytes(n, q):
+    return int(lib().choco_qsgd_packed_bytes(int(n), int(q)))
+
+
+def qsgd_compress(x, q, is_biased=False, xhat=None, seg_off=None, nseg=1, norm_in=None, u_in=None,
+                  seed=0, offset=0, want_dense=False):
+    """QSGD with s = 2^q - 1.  Returns (packed uint8, norms f32[nseg], dense f32[n] or None)."""
+    _require(x, torch.float32, "x")
+    if xhat is not None:
+        _require(xhat, torch.float32, "xhat")
+    if seg_off is not None:
+        _require(seg_off, torch.int64, "seg_off")
+    if norm_in is not None:
+        _require(norm_in, torch.float32, "norm_in")
+    if u_in is not None:
+        _require(u_in, torch.float32, "u_in")
+        if u_in.numel() != x.numel():
+            raise RuntimeError("u_in must have one uniform per element")
+    n = x.numel()
+    dev = x.device
+    L = lib()
+    packed = torch.empty(qsgd_packed_bytes(n, q), dtype=torch.uint8, device=dev)
+    norms = torch.empty(nseg, dtype=torch.float32, device=dev)
+    dense = torch.empty(n, dtype=torch.float32, device=dev) if want_dense else None
+    ws = workspace(dev, "acc", L.choco_qsgd_workspace_size(nseg))
+    _lib.check(L.choco_qsgd_compress(_ptr(x), _ptr(xhat), n, _ptr(seg_off), int(nseg), int(q),
+                                     1 if is_biased else 0, _ptr(norm_in), _ptr(u_in), int(seed) & (2**64 - 1),
+                                     int(offset) & (2**64 - 1), _ptr(packed), _ptr(norms), _ptr(dense), _ptr(ws),
+                                     ws.numel(), _stream(dev)), "choco_qsgd_compress")
+    return packed, norms, dense
+
+
+def qsgd_decode(packed, norms, n, q, is_biased=False, seg_off=None, nseg=1):
+    _require(packed, torch.uint8, "packed")
+    _require(norms, torch.float32, "norms")
+    out = torch.empty(n, dtype=torch.float32, device=packed.device)
+    _lib.check(lib().choco_qsgd_decode(_ptr(packed), _ptr(norms), int(n), _ptr(seg_off), int(nseg), int(q),
+                                       1 if is_biased else 0, _ptr(out), _stream(packed.device)),
+               "choco_qsgd_decode")
+    return out
+
+
+def qsgd_accumulate(messages, weights, self_slot, n, q, memory, xhat_self=None, is_biased=False, seg_off=None,
+                    nseg=1):
+    """messages: list of (packed uint8, norms f32[nseg]) applied in order."""
+    _require(memory, torch.float32, "memory")
+    pp, keep1 = _lib.ptr_array([p.data_ptr() for p, _ in messages])
+    nn, keep2 = _lib.ptr_array([nm.data_ptr() for _, nm in messages])
+    ww, keep3 = _lib.f32_array([float(w) for w in weights])
+    _lib.check(lib().choco_qsgd_decompress_accumulate(pp, nn, ww, len(messages), int(self_slot), int(n),
+                                                      _ptr(seg_off), int(nseg), int(q), 1 if is_biased else 0,
+                                                      _ptr(xhat_self), _ptr(memory), _stream(memory.device)),
+               "choco_qsgd_decompress_accumulate")
+
+
+# ----------------------------------------------------------------------------- gossip
+def gossip_step(x, memory, xhat, gamma):
+    for t, nm in ((x, "x"), (memory, "memory"), (xhat, "xhat")):
+        _require(t, torch.float32, nm)
+    _lib.check(lib().choco_gossip_step(_ptr(x), _ptr(memory), _ptr(xhat), float(gamma), x.numel(),
+                                       _stream(x.device)), "choco_gossip_step")
+
+
+# ----------------------------------------------------------------------------- profiling
+def profile_enable(on=True):
+    lib().choco_profile_enable(1 if on else 0)
+
+
+def profile_read(name):
+    total = ctypes.c_double(0.0)
+    cnt = ctypes.c_int64(0)
+    lib().choco_profile_read(name.encode(), ctypes.byref(total), ctypes.byref(cnt))
+    return total.value, cnt.value
+
+
+def profile_reset():
+    lib().choco_profile_reset()
+
+
+def is_pow2_minus1(s):
+    return s >= 1 and (s + 1) & s == 0 and int(math.log2(s + 1)) <= 16

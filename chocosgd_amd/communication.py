@@ -1,0 +1,101 @@
+"""Exchange step of the CHOCO gossip (drop-in for the decentralized half of
+dl_code/pcode/utils/communication.py).
+
+`DecentralizedAggregation._agg(data, op="get_raw_sync_data", force_wait=False)`
+keeps the reference's contract (communication.py:246-291): send `data` to every
+neighbour, receive each neighbour's message into a same-shaped buffer, return
+`(reqs, {rank: tensor})` with the local entry being `data` itself.  On ROCm the
+sends/receives are issued as ONE grouped batch (`dist.batch_isend_irecv`, i.e.
+ncclGroupStart/End over RCCL), so both ring directions run concurrently on
+their own xGMI links; on CPU the same code runs over gloo.
+
+Messages are whatever the CHOCO compressors pack (uint8 / int32 wire buffers);
+unlike the reference nothing is re-cast to the default float dtype.
+"""
+import torch
+import torch.distributed as dist
+
+
+def flatten(tensors, shapes=None, use_cuda=True):
+    from .tensor_buffer import flatten as _flatten
+    return _flatten(tensors, shapes=shapes, use_cuda=use_cuda)
+
+
+def unflatten(tensors, synced_tensors, shapes):
+    pointer = 0
+    for tensor, shape in zip(tensors, shapes):
+        param_size, nelement = shape
+        tensor.data[:] = synced_tensors[pointer:pointer + nelement].view(param_size)
+        pointer += nelement
+
+
+def recover_device(data, device=None):
+    return data.to(device) if device is not None else data
+
+
+def neighborhood(rank, world_size):
+    """Mixing-matrix row {rank: weight} incl. self, as the reference topologies give it.
+
+    world 1: {0: 1.0}; world 2: CompleteGraph (topology.py:122-162, weight 1/2,
+    RingGraph asserts n > 2 at topology.py:187); world >= 3: RingGraph
+    (topology.py:174-299, weights 1/3 for r-1, r, r+1, keys in ascending order).
+    """
+    if world_size == 1:
+        return {0: 1.0}
+    if world_size == 2:
+        return {0: 0.5, 1: 0.5}
+    ranks = sorted({(rank - 1) % world_size, rank, (rank + 1) % world_size})
+    return {r: 1.0 / 3 for r in ranks}
+
+
+class _Works:
+    def __init__(self, works):
+        self.works = list(works)
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+
+
+class DecentralizedAggregation(object):
+    """Aggregate updates in a decentralized manner (communication.py:230-291)."""
+
+    def __init__(self, rank, neighbors_info):
+        self.rank = rank
+        self.neighbors_info = neighbors_info
+        self.neighbor_ranks = [r for r in neighbors_info.keys() if r != rank]
+        self.world_size = float(len(self.neighbor_ranks))
+
+    def _agg(self, data, op, force_wait=True):
+        local_data = {i: torch.empty_like(data) for i in self.neighbor_ranks}
+        local_data[self.rank] = data
+        reqs = []
+        if self.neighbor_ranks:
+            ops = []
+            for node_rank in self.neighbor_ranks:
+                ops.append(dist.P2POp(dist.isend, data, node_rank))
+                ops.append(dist.P2POp(dist.irecv, local_data[node_rank], node_rank))
+            reqs = [_Works(dist.batch_isend_irecv(ops))]
+        if force_wait:
+            self.complete_wait(reqs)
+            if op == "avg":
+                return sum(local_data.values()) / (self.world_size + 1)
+            if op == "weighted":
+                return sum(t * self.neighbors_info[r] for r, t in local_data.items())
+            if op == "get_raw_sync_data":
+                return local_data
+            raise NotImplementedError("op {} is not supported yet.".format(op))
+        if op == "get_raw_sync_data":
+            return reqs, local_data
+        raise NotImplementedError("op {} is not supported yet.".format(op))
+
+    def complete_wait(self, reqs):
+        for req in reqs:
+            req.wait()
+
+
+def get_aggregators(cur_rank, world, neighbors_info, aggregator_type):
+    if aggregator_type == "decentralized":
+        return DecentralizedAggregation(cur_rank, neighbors_info)
+    raise NotImplementedError(
+        f"aggregator '{aggregator_type}' is outside the CHOCO compressor path (see DESIGN.md)")

@@ -1,0 +1,116 @@
+// Library-wide C-ABI plumbing: per-thread error text, version, profiling hooks.
+#include "choco_common.h"
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <atomic>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace choco {
+
+static thread_local char g_err[1024] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CHOCO_ERR_HIP, "launch of %s failed: %s", what, hipGetErrorString(e));
+  return CHOCO_OK;
+}
+
+// ---------------------------------------------------------------- profiling
+struct PendingEv {
+  std::string name;
+  hipEvent_t a, b;
+  bool closed;
+};
+static std::atomic<bool> g_prof_on{false};
+static std::mutex g_prof_mu;
+static std::vector<PendingEv> g_pending;
+static std::map<std::string, std::pair<double, int64_t>> g_acc;
+
+void profile_begin(const char* name, hipStream_t st) {
+  if (!g_prof_on.load(std::memory_order_relaxed)) return;
+  PendingEv p{name, nullptr, nullptr, false};
+  if (hipEventCreate(&p.a) != hipSuccess || hipEventCreate(&p.b) != hipSuccess) return;
+  (void)hipEventRecord(p.a, st);
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  g_pending.push_back(p);
+}
+
+void profile_end(const char* name, hipStream_t st) {
+  if (!g_prof_on.load(std::memory_order_relaxed)) return;
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  for (auto it = g_pending.rbegin(); it != g_pending.rend(); ++it) {
+    if (!it->closed && it->name == name) {
+      (void)hipEventRecord(it->b, st);
+      it->closed = true;
+      return;
+    }
+  }
+}
+
+static void profile_drain_locked() {
+  for (auto& p : g_pending) {
+    if (p.closed) {
+      float ms = 0.f;
+      (void)hipEventSynchronize(p.b);
+      if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+        auto& e = g_acc[p.name];
+        e.first += ms;
+        e.second += 1;
+      }
+    }
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  g_pending.clear();
+}
+
+}  // namespace choco
+
+using namespace choco;
+
+CHOCO_API int choco_version(void) { return 1; }
+
+CHOCO_API int choco_last_error(char* buf, size_t len) {
+  size_t n = strlen(g_err);
+  if (buf && len) {
+    size_t c = n < len - 1 ? n : len - 1;
+    memcpy(buf, g_err, c);
+    buf[c] = 0;
+  }
+  return (int)n;
+}
+
+CHOCO_API int choco_profile_enable(int32_t on) {
+  g_prof_on.store(on != 0);
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_profile_read(const char* name, double* total_ms, int64_t* count) {
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  profile_drain_locked();
+  auto it = g_acc.find(name ? name : "");
+  if (total_ms) *total_ms = it == g_acc.end() ? 0.0 : it->second.first;
+  if (count) *count = it == g_acc.end() ? 0 : it->second.second;
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_profile_reset(void) {
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  profile_drain_locked();
+  g_acc.clear();
+  return CHOCO_OK;
+}

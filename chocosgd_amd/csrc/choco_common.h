@@ -1,0 +1,190 @@
+// Shared device/host helpers for the CHOCO codec (gfx950 / CDNA4, wave64).
+//
+// Everything here is memory-bound per-element work: no MFMA.  Conventions used
+// by every kernel in this library:
+//   * `key(v)` = IEEE-754 bits of |v| (sign bit cleared).  For non-NaN floats the
+//     unsigned order of keys equals the order of magnitudes, so top-k by |v|
+//     (reference: torch.topk(x.abs(), k), dl_code/pcode/utils/sparsification.py:28)
+//     is top-k by key.  NaN keys sort above +inf, matching torch.topk's NaN order.
+//   * indices on the wire are int32 (the reference sends them as fp32 and loses
+//     exactness above 2^24: communication.py:69-72, sparsification.py:76).
+//   * Every arithmetic step whose rounding is observable follows the reference's
+//     fp32 op order; the library is built with -ffp-contract=off so no mul+add is
+//     silently fused (fmaf is written explicitly where torch itself fuses).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/choco_codec.h"
+
+#define CHOCO_DEV __device__ __forceinline__
+#define CHOCO_API extern "C" __attribute__((visibility("default")))
+
+namespace choco {
+
+// ---------------------------------------------------------------- errors
+int fail(int code, const char* fmt, ...);
+int check_launch(const char* what);
+
+#define CHOCO_HIP(expr)                                                     \
+  do {                                                                      \
+    hipError_t _e = (expr);                                                 \
+    if (_e != hipSuccess)                                                   \
+      return ::choco::fail(CHOCO_ERR_HIP, "%s failed: %s", #expr,           \
+                           hipGetErrorString(_e));                          \
+  } while (0)
+
+#define CHOCO_LAUNCHED(what)                                                \
+  do {                                                                      \
+    int _rc = ::choco::check_launch(what);                                  \
+    if (_rc) return _rc;                                                    \
+  } while (0)
+
+#define CHOCO_REQUIRE(cond, ...)                                            \
+  do {                                                                      \
+    if (!(cond)) return ::choco::fail(CHOCO_ERR_INVALID, __VA_ARGS__);      \
+  } while (0)
+
+// Optional hipEvent bracketing of a named kernel on its own stream (bench roofline).
+void profile_begin(const char* name, hipStream_t st);
+void profile_end(const char* name, hipStream_t st);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// ---------------------------------------------------------------- device helpers
+CHOCO_DEV uint32_t fkey(float v) { return __float_as_uint(v) & 0x7fffffffu; }
+
+CHOCO_DEV int lane_id() { return __lane_id(); }
+
+// number of set bits of `mask` strictly below this lane
+CHOCO_DEV uint32_t mask_prefix(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+CHOCO_DEV uint64_t ballot(bool p) { return __ballot(p); }
+
+template <typename T>
+CHOCO_DEV T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// inclusive prefix sum across the 64 lanes
+CHOCO_DEV uint32_t wave_incl_scan(uint32_t v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t t = __shfl_up(v, o);
+    if (l >= o) v += t;
+  }
+  return v;
+}
+
+// Block-wide exclusive scan of one u32 per thread.  `scratch` must hold
+// blockDim.x/64 + 1 words of LDS.  Returns the exclusive prefix; *total gets the
+// block sum.  All threads of the block must call it.
+CHOCO_DEV uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
+  const int l = lane_id();
+  const int w = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  uint32_t inc = wave_incl_scan(v);
+  if (l == 63) scratch[w] = inc;
+  __syncthreads();
+  if (w == 0) {
+    uint32_t t = (l < nw) ? scratch[l] : 0u;
+    uint32_t ti = wave_incl_scan(t);
+    if (l < nw) scratch[l] = ti - t;
+    if (l == 63) scratch[nw] = ti;
+  }
+  __syncthreads();
+  uint32_t r = scratch[w] + inc - v;
+  *total = scratch[nw];
+  __syncthreads();
+  return r;
+}
+
+// 64-bit reinterpret for double atomics through integer exchange
+CHOCO_DEV double atomic_exchange_double(double* p, double v) {
+  unsigned long long old = atomicExch(reinterpret_cast<unsigned long long*>(p),
+                                      (unsigned long long)__double_as_longlong(v));
+  return __longlong_as_double((long long)old);
+}
+
+// Producer side of a last-block-done ticket (MI355X guide §6 Guideline 16):
+// every wave drains its own memory ops, the block joins, one lane releases at
+// agent scope and draws a ticket.  Returns true in every thread of the block
+// that drew the last ticket; that block then acquires before reading.
+CHOCO_DEV bool last_block_ticket(unsigned int* ticket, unsigned int nblocks, unsigned int* lds_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned int t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *lds_flag = (t == nblocks - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  bool last = *lds_flag != 0u;
+  if (last) {
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
+  return last;
+}
+
+// ---------------------------------------------------------------- segments
+// seg_off: int64[nseg+1] monotone, seg_off[0] = 0, seg_off[nseg] = n.
+// Returns the segment containing flat element e (binary search, global memory).
+CHOCO_DEV int seg_of(const int64_t* __restrict__ seg_off, int nseg, int64_t e) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (seg_off[mid] <= e) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// ---------------------------------------------------------------- RNG
+// Philox4x32-10 (Salmon et al., SC'11).  u = (bits >> 8) * 2^-24 in [0,1).
+struct Philox4 { uint32_t x, y, z, w; };
+
+CHOCO_DEV Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
+    uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += W0; k1 += W1;
+  }
+  return Philox4{c0, c1, c2, c3};
+}
+
+CHOCO_DEV float u24(uint32_t b) { return (float)(b >> 8) * 5.9604644775390625e-08f; }
+
+// Seeded 32-bit bijective mixer used as the random-k ranking key
+// (murmur3 fmix32 of a seeded Weyl sequence).
+CHOCO_DEV uint32_t rank_hash(uint64_t seed, uint32_t i) {
+  uint32_t h = i * 0x9E3779B1u + (uint32_t)seed;
+  h ^= (uint32_t)(seed >> 32);
+  h ^= h >> 16; h *= 0x85EBCA6Bu;
+  h ^= h >> 13; h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
+}  // namespace choco

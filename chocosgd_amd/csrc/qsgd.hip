@@ -1,0 +1,536 @@
+// QSGD random quantization for the CHOCO gossip step on MI355X.
+//
+// Replaces QuantizationCompressor.get_qsgd / compress / uncompress
+// (reference dl_code/pcode/utils/sparsification.py:87-123) as applied per
+// parameter tensor by CHOCOQuantizationCompressor
+// (dl_code/pcode/optim/parallel_choco_v.py:375-433).
+//
+// The reference transmits the DEQUANTIZED dense fp32 tensor (4n bytes); here
+// the wire carries per-segment fp32 norms + a level plane (cw bits/element,
+// cw = the power of two >= q) + a sign plane (1 bit/element).  The receiver
+// rebuilds the reference's float bit-for-bit:
+//     ((scale * sign) * norm) * level / (float)s
+//
+// Two passes are unavoidable (the norm of a segment is needed before any of
+// its elements can be quantized):
+//   qsgd_norm_kernel    : fp64 sum of squares per segment (one fp64 atomic per
+//                         workgroup and segment), last workgroup rounds
+//                         sqrt() to fp32 and resets the accumulators.
+//   qsgd_quant_kernel   : levels + stochastic rounding + packing.  Workgroups
+//                         walk the buffer in REVERSE order, so the tail that the
+//                         norm pass streamed last is re-read from the 256 MB
+//                         Infinity Cache instead of HBM.
+#include "choco_common.h"
+
+#include <algorithm>
+#include <math.h>
+
+namespace choco {
+
+constexpr int kQThreads = 256;
+constexpr int kQPer = 8;                         // elements per thread in the quantize/decode passes
+constexpr int kQTile = kQThreads * kQPer;        // 2048
+constexpr int kNormTile = 32768;                 // elements per workgroup in the norm pass
+constexpr int kQMaxMsg = 8;
+
+struct QsgdWs {
+  unsigned int ticket;
+  unsigned int pad[63];
+  // double acc[nseg] at +256
+};
+
+static int container_bits(int q) {
+  int cw = 1;
+  while (cw < q) cw <<= 1;
+  return cw;
+}
+
+static int64_t plane_bytes(int64_t n, int cw) { return (int64_t)align_up((size_t)((n + 7) / 8) * cw, 16); }
+
+CHOCO_DEV float dval(const float* __restrict__ x, const float* __restrict__ xh, int64_t i) {
+  return xh ? x[i] - xh[i] : x[i];
+}
+
+// Per-segment quantizer parameters.
+struct QParam {
+  float norm, scale;
+};
+
+CHOCO_DEV QParam qparam(const float* __restrict__ norms, const int64_t* __restrict__ seg_off, int64_t n, int seg,
+                        int s_levels, bool biased) {
+  QParam p;
+  p.norm = norms[seg];
+  p.scale = 1.0f;
+  if (biased) {
+    const double d = (double)(seg_off ? seg_off[seg + 1] - seg_off[seg] : n);
+    const double s = (double)s_levels;
+    // 1.0 / (min(d / s**2, sqrt(d) / s) + 1.0)  in Python doubles (sparsification.py:96-97)
+    p.scale = (float)(1.0 / (fmin(d / (s * s), sqrt(d) / s) + 1.0));
+  }
+  return p;
+}
+
+// ---------------------------------------------------------------- pass 1: norms
+template <bool XH>
+__global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __restrict__ x,
+                                                              const float* __restrict__ xh, int64_t n,
+                                                              const int64_t* __restrict__ seg_off, int nseg,
+                                                              float* __restrict__ norms_out,
+                                                              QsgdWs* __restrict__ ws) {
+  __shared__ int s_seg[2];
+  __shared__ double s_red[kQThreads / 64];
+  __shared__ unsigned int s_flag;
+  double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int64_t t0 = (int64_t)blockIdx.x * kNormTile;
+  const int64_t t1 = std::min<int64_t>(t0 + kNormTile, n);
+  if (tid == 0) {
+    s_seg[0] = nseg > 1 ? seg_of(seg_off, nseg, t0) : 0;
+    s_seg[1] = nseg > 1 ? seg_of(seg_off, nseg, t1 - 1) : 0;
+  }
+  __syncthreads();
+  const int sg0 = s_seg[0], sg1 = s_seg[1];
+  if (sg0 == sg1) {
+    double p = 0.0;
+    for (int64_t e = t0 + 4 * tid; e < t1; e += 4 * kQThreads) {
+      if (e + 3 < t1) {
+        float4 a = *reinterpret_cast<const float4*>(x + e);
+        if (XH) {
+          const float4 h = *reinterpret_cast<const float4*>(xh + e);
+          a.x -= h.x; a.y -= h.y; a.z -= h.z; a.w -= h.w;
+        }
+        p += (double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z + (double)a.w * a.w;
+      } else {
+        for (int c = 0; c < 4 && e + c < t1; ++c) {
+          const double v = dval(x, XH ? xh : nullptr, e + c);
+          p += v * v;
+        }
+      }
+    }
+    p = wave_sum(p);
+    if (lane == 0) s_red[w] = p;
+    __syncthreads();
+    if (tid == 0) {
+      double t = 0.0;
+      for (int i = 0; i < kQThreads / 64; ++i) t += s_red[i];
+      if (t != 0.0) unsafeAtomicAdd(&acc[sg0], t);
+    }
+  } else {
+    // segment boundaries inside the tile: per-wave segmented reduction
+    for (int64_t base = t0 + 256 * w; base < t1; base += 256 * (kQThreads / 64)) {
+      const int64_t e = base + 4 * lane;
+      double v[4];
+      int sg[4];
+      int lo = 0x7fffffff, hi = -1;
+      for (int c = 0; c < 4; ++c) {
+        sg[c] = -1;
+        v[c] = 0.0;
+        if (e + c < t1) {
+          const double d = dval(x, XH ? xh : nullptr, e + c);
+          v[c] = d * d;
+          int s = sg0;
+          while (s + 1 < nseg && seg_off[s + 1] <= e + c) ++s;
+          sg[c] = s;
+          lo = min(lo, s);
+          hi = max(hi, s);
+        }
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, __shfl_xor(lo, o));
+        hi = max(hi, __shfl_xor(hi, o));
+      }
+      for (int q = lo; q <= hi; ++q) {
+        double p = 0.0;
+        for (int c = 0; c < 4; ++c)
+          if (sg[c] == q) p += v[c];
+        p = wave_sum(p);
+        if (lane == 0 && p != 0.0) unsafeAtomicAdd(&acc[q], p);
+      }
+    }
+  }
+  if (last_block_ticket(&ws->ticket, gridDim.x, &s_flag)) {
+    for (int q = threadIdx.x; q < nseg; q += blockDim.x)
+      norms_out[q] = (float)sqrt(atomic_exchange_double(&acc[q], 0.0));
+    if (threadIdx.x == 0) __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ---------------------------------------------------------------- pass 2: quantize + pack
+template <int CW>
+CHOCO_DEV void store_levels(uint8_t* __restrict__ plane, int64_t t, const uint32_t (&lv)[kQPer]) {
+  if (CW == 16) {
+    uint4 v;
+    v.x = lv[0] | (lv[1] << 16);
+    v.y = lv[2] | (lv[3] << 16);
+    v.z = lv[4] | (lv[5] << 16);
+    v.w = lv[6] | (lv[7] << 16);
+    reinterpret_cast<uint4*>(plane)[t] = v;
+  } else {
+    uint64_t acc = 0;
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) acc |= (uint64_t)lv[c] << (c * CW);
+    if (CW == 8) reinterpret_cast<uint64_t*>(plane)[t] = acc;
+    if (CW == 4) reinterpret_cast<uint32_t*>(plane)[t] = (uint32_t)acc;
+    if (CW == 2) reinterpret_cast<uint16_t*>(plane)[t] = (uint16_t)acc;
+    if (CW == 1) plane[t] = (uint8_t)acc;
+  }
+}
+
+template <int CW>
+CHOCO_DEV void load_levels(const uint8_t* __restrict__ plane, int64_t t, uint32_t (&lv)[kQPer]) {
+  if (CW == 16) {
+    const uint4 v = reinterpret_cast<const uint4*>(plane)[t];
+    lv[0] = v.x & 0xFFFFu; lv[1] = v.x >> 16;
+    lv[2] = v.y & 0xFFFFu; lv[3] = v.y >> 16;
+    lv[4] = v.z & 0xFFFFu; lv[5] = v.z >> 16;
+    lv[6] = v.w & 0xFFFFu; lv[7] = v.w >> 16;
+  } else {
+    uint64_t acc = 0;
+    if (CW == 8) acc = reinterpret_cast<const uint64_t*>(plane)[t];
+    if (CW == 4) acc = reinterpret_cast<const uint32_t*>(plane)[t];
+    if (CW == 2) acc = reinterpret_cast<const uint16_t*>(plane)[t];
+    if (CW == 1) acc = plane[t];
+    const uint32_t mask = (1u << CW) - 1u;
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) lv[c] = (uint32_t)(acc >> (c * CW)) & mask;
+  }
+}
+
+CHOCO_DEV int tile_seg(const int64_t* __restrict__ seg_off, int nseg, int64_t e0, int64_t e1, int* s_seg) {
+  if (threadIdx.x == 0) {
+    s_seg[0] = nseg > 1 ? seg_of(seg_off, nseg, e0) : 0;
+    s_seg[1] = nseg > 1 ? seg_of(seg_off, nseg, e1 - 1) : 0;
+  }
+  __syncthreads();
+  return s_seg[0];
+}
+
+template <int CW>
+__global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, const int64_t* __restrict__ seg_off,
+    int nseg, int s_levels, int biased, const float* __restrict__ norms, const float* __restrict__ u_in,
+    uint64_t seed, uint64_t offset, uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
+    float* __restrict__ dense_out, int64_t ntiles) {
+  __shared__ int s_seg[2];
+  const int64_t tile = ntiles - 1 - (int64_t)blockIdx.x;  // reverse walk: Infinity-Cache hits
+  const int64_t t_e0 = tile * kQTile;
+  const int64_t t_e1 = std::min<int64_t>(t_e0 + kQTile, n);
+  const int sg0 = tile_seg(seg_off, nseg, t_e0, t_e1, s_seg);
+  const bool uniform = s_seg[1] == sg0;
+  const int64_t e0 = t_e0 + (int64_t)threadIdx.x * kQPer;
+  if (e0 >= n) return;
+  const float sf = (float)s_levels;
+  const uint32_t smax = (uint32_t)s_levels;
+  float d[kQPer];
+  if (e0 + kQPer <= n) {
+    const float4 a0 = *reinterpret_cast<const float4*>(x + e0);
+    const float4 a1 = *reinterpret_cast<const float4*>(x + e0 + 4);
+    d[0] = a0.x; d[1] = a0.y; d[2] = a0.z; d[3] = a0.w; d[4] = a1.x; d[5] = a1.y; d[6] = a1.z; d[7] = a1.w;
+    if (xh) {
+      const float4 h0 = *reinterpret_cast<const float4*>(xh + e0);
+      const float4 h1 = *reinterpret_cast<const float4*>(xh + e0 + 4);
+      d[0] -= h0.x; d[1] -= h0.y; d[2] -= h0.z; d[3] -= h0.w;
+      d[4] -= h1.x; d[5] -= h1.y; d[6] -= h1.z; d[7] -= h1.w;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) d[c] = (e0 + c < n) ? dval(x, xh, e0 + c) : 0.f;
+  }
+  float u[kQPer];
+  if (u_in) {
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) u[c] = (e0 + c < n) ? u_in[e0 + c] : 0.f;
+  } else {
+    const uint64_t g = (uint64_t)e0 >> 2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const Philox4 r = philox4x32_10((uint32_t)(g + h), (uint32_t)((g + h) >> 32), (uint32_t)offset,
+                                      (uint32_t)(offset >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+      u[4 * h + 0] = u24(r.x); u[4 * h + 1] = u24(r.y); u[4 * h + 2] = u24(r.z); u[4 * h + 3] = u24(r.w);
+    }
+  }
+  QParam P = qparam(norms, seg_off, n, sg0, s_levels, biased != 0);
+  uint32_t lv[kQPer];
+  uint32_t sbits = 0;
+  float outv[kQPer];
+#pragma unroll
+  for (int c = 0; c < kQPer; ++c) {
+    const int64_t e = e0 + c;
+    if (!uniform && e < n) {
+      int s = sg0;
+      while (s + 1 < nseg && seg_off[s + 1] <= e) ++s;
+      P = qparam(norms, seg_off, n, s, s_levels, biased != 0);
+    }
+    const float a = fabsf(d[c]);
+    const float lf = (sf * a) / P.norm;            // s * x.abs() / norm
+    const float pl = floorf(lf);                   // previous_level
+    const float lvl = pl + ((u[c] < (lf - pl)) ? 1.0f : 0.0f);  // + is_next_level
+    const float sg = d[c] > 0.f ? 1.0f : (d[c] < 0.f ? -1.0f : 0.0f);  // torch.sign (NaN -> 0)
+    outv[c] = (((P.scale * sg) * P.norm) * lvl) / sf;
+    uint32_t li = 0;
+    if (lvl == lvl && e < n) li = lvl >= (float)smax ? smax : (uint32_t)lvl;
+    lv[c] = li;
+    sbits |= (d[c] < 0.f && e < n) ? (1u << c) : 0u;
+  }
+  const int64_t t = e0 / kQPer;
+  store_levels<CW>(lvl_plane, t, lv);
+  sign_plane[t] = (uint8_t)sbits;
+  if (dense_out) {
+    if (e0 + kQPer <= n) {
+      *reinterpret_cast<float4*>(dense_out + e0) = make_float4(outv[0], outv[1], outv[2], outv[3]);
+      *reinterpret_cast<float4*>(dense_out + e0 + 4) = make_float4(outv[4], outv[5], outv[6], outv[7]);
+    } else {
+      for (int c = 0; c < kQPer; ++c)
+        if (e0 + c < n) dense_out[e0 + c] = outv[c];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- decode / accumulate
+struct QMsgs {
+  const uint8_t* lvl[kQMaxMsg];
+  const uint8_t* sgn[kQMaxMsg];
+  const float* norms[kQMaxMsg];
+  float w[kQMaxMsg];
+  int nmsg;
+  int self_slot;
+};
+
+CHOCO_DEV float qdecode(uint32_t level, bool neg, const QParam& P, float sf) {
+  const float lvl = (P.norm == 0.0f) ? __int_as_float(0x7fc00000) : (float)level;  // ref: 0/0 -> NaN
+  const float sg = neg ? -1.0f : 1.0f;
+  return (((P.scale * sg) * P.norm) * lvl) / sf;
+}
+
+// MODE 0: out = decode(msg 0); MODE 1: accumulate all messages into hat/mem.
+template <int CW, int NM, int MODE>
+__global__ __launch_bounds__(kQThreads) void qsgd_decode_kernel(QMsgs M, int64_t n,
+                                                                const int64_t* __restrict__ seg_off, int nseg,
+                                                                int s_levels, int biased,
+                                                                float* __restrict__ hat, float* __restrict__ mem) {
+  __shared__ int s_seg[2];
+  const int64_t t_e0 = (int64_t)blockIdx.x * kQTile;
+  const int64_t t_e1 = std::min<int64_t>(t_e0 + kQTile, n);
+  const int sg0 = tile_seg(seg_off, nseg, t_e0, t_e1, s_seg);
+  const bool uniform = s_seg[1] == sg0;
+  const int64_t e0 = t_e0 + (int64_t)threadIdx.x * kQPer;
+  if (e0 >= n) return;
+  const float sf = (float)s_levels;
+  const int64_t t = e0 / kQPer;
+  const bool full = e0 + kQPer <= n;
+  float mv[kQPer], hv[kQPer];
+  const bool has_self = MODE == 1 && M.self_slot >= 0 && hat != nullptr;
+  if (MODE == 1) {
+    if (full) {
+      const float4 a0 = *reinterpret_cast<const float4*>(mem + e0);
+      const float4 a1 = *reinterpret_cast<const float4*>(mem + e0 + 4);
+      mv[0] = a0.x; mv[1] = a0.y; mv[2] = a0.z; mv[3] = a0.w; mv[4] = a1.x; mv[5] = a1.y; mv[6] = a1.z; mv[7] = a1.w;
+      if (has_self) {
+        const float4 b0 = *reinterpret_cast<const float4*>(hat + e0);
+        const float4 b1 = *reinterpret_cast<const float4*>(hat + e0 + 4);
+        hv[0] = b0.x; hv[1] = b0.y; hv[2] = b0.z; hv[3] = b0.w; hv[4] = b1.x; hv[5] = b1.y; hv[6] = b1.z; hv[7] = b1.w;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < kQPer; ++c) {
+        mv[c] = (e0 + c < n) ? mem[e0 + c] : 0.f;
+        hv[c] = (has_self && e0 + c < n) ? hat[e0 + c] : 0.f;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NM; ++q) {
+    uint32_t lv[kQPer];
+    load_levels<CW>(M.lvl[q], t, lv);
+    const uint32_t sb = M.sgn[q][t];
+    QParam P = qparam(M.norms[q], seg_off, n, sg0, s_levels, biased != 0);
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) {
+      const int64_t e = e0 + c;
+      if (!uniform && e < n) {
+        int s = sg0;
+        while (s + 1 < nseg && seg_off[s + 1] <= e) ++s;
+        P = qparam(M.norms[q], seg_off, n, s, s_levels, biased != 0);
+      }
+      const float v = qdecode(lv[c], (sb >> c) & 1u, P, sf);
+      if (MODE == 0) {
+        mv[c] = v;
+      } else {
+        if (has_self && q == M.self_slot) hv[c] = hv[c] + v;  // hat_params.buffer += q_values
+        const float wv = M.w[q] * v;                        // weight * q_values (rounded)
+        mv[c] = mv[c] + wv;                                  // memory += ...
+      }
+    }
+  }
+  float* dst = MODE == 0 ? hat : mem;  // MODE 0 writes the decoded floats to `hat` (= out)
+  if (full) {
+    *reinterpret_cast<float4*>(dst + e0) = make_float4(mv[0], mv[1], mv[2], mv[3]);
+    *reinterpret_cast<float4*>(dst + e0 + 4) = make_float4(mv[4], mv[5], mv[6], mv[7]);
+    if (has_self) {
+      *reinterpret_cast<float4*>(hat + e0) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+      *reinterpret_cast<float4*>(hat + e0 + 4) = make_float4(hv[4], hv[5], hv[6], hv[7]);
+    }
+  } else {
+    for (int c = 0; c < kQPer; ++c) {
+      if (e0 + c >= n) break;
+      dst[e0 + c] = mv[c];
+      if (has_self) hat[e0 + c] = hv[c];
+    }
+  }
+}
+
+template <int CW, int NM, int MODE>
+static void launch_decode(const QMsgs& M, int64_t n, const int64_t* seg_off, int nseg, int s_levels, int biased,
+                          float* hat, float* mem, hipStream_t st) {
+  const unsigned grid = (unsigned)((n + kQTile - 1) / kQTile);
+  hipLaunchKernelGGL((qsgd_decode_kernel<CW, NM, MODE>), dim3(grid), dim3(kQThreads), 0, st, M, n, seg_off, nseg,
+                     s_levels, biased, hat, mem);
+}
+
+template <int CW, int MODE>
+static void launch_decode_nm(const QMsgs& M, int64_t n, const int64_t* seg_off, int nseg, int s_levels,
+                             int biased, float* hat, float* mem, hipStream_t st) {
+  switch (M.nmsg) {
+    case 1: launch_decode<CW, 1, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+    case 2: launch_decode<CW, 2, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+    case 3: launch_decode<CW, 3, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+    case 4: launch_decode<CW, 4, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+    case 5: launch_decode<CW, 5, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+    case 6: launch_decode<CW, 6, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+    case 7: launch_decode<CW, 7, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+    default: launch_decode<CW, 8, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+  }
+}
+
+template <int MODE>
+static void launch_decode_cw(int cw, const QMsgs& M, int64_t n, const int64_t* seg_off, int nseg, int s_levels,
+                             int biased, float* hat, float* mem, hipStream_t st) {
+  switch (cw) {
+    case 1: launch_decode_nm<1, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+    case 2: launch_decode_nm<2, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+    case 4: launch_decode_nm<4, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+    case 8: launch_decode_nm<8, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+    default: launch_decode_nm<16, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+  }
+}
+
+}  // namespace choco
+
+using namespace choco;
+
+CHOCO_API int64_t choco_qsgd_packed_bytes(int64_t n, int32_t q) {
+  if (n <= 0 || q < 1 || q > 16) return 0;
+  return plane_bytes(n, container_bits(q)) + plane_bytes(n, 1);
+}
+
+CHOCO_API size_t choco_qsgd_workspace_size(int32_t nseg) {
+  return 256 + align_up((size_t)(nseg > 0 ? nseg : 1) * sizeof(double), 256);
+}
+
+CHOCO_API int choco_qsgd_compress(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
+                                  int32_t q, int32_t is_biased, const float* norm_in, const float* u_in,
+                                  uint64_t seed, uint64_t offset, uint8_t* packed, float* norms_out,
+                                  float* dense_out, void* ws, size_t ws_bytes, void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(x && packed, "null pointer argument");
+  CHOCO_REQUIRE(q >= 1 && q <= 16, "quantize level q must be in [1, 16] (q = 32 is a passthrough), got %d", q);
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
+  CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
+  CHOCO_REQUIRE(aligned16(x) && (!xhat || aligned16(xhat)) && aligned16(packed) &&
+                    (!dense_out || aligned16(dense_out)),
+                "buffers must be 16-byte aligned");
+  const int cw = container_bits(q);
+  const int s_levels = (1 << q) - 1;
+  const float* norms = norm_in;
+  if (!norms) {
+    CHOCO_REQUIRE(norms_out, "norms_out is required when norm_in is NULL");
+    CHOCO_REQUIRE(ws && ws_bytes >= choco_qsgd_workspace_size(nseg), "qsgd workspace too small");
+    const unsigned g1 = (unsigned)((n + kNormTile - 1) / kNormTile);
+    QsgdWs* w = static_cast<QsgdWs*>(ws);
+    profile_begin("qsgd_norm", st);
+    if (xhat)
+      hipLaunchKernelGGL((qsgd_norm_kernel<true>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
+                         norms_out, w);
+    else
+      hipLaunchKernelGGL((qsgd_norm_kernel<false>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
+                         norms_out, w);
+    profile_end("qsgd_norm", st);
+    CHOCO_LAUNCHED("qsgd_norm_kernel");
+    norms = norms_out;
+  } else if (norms_out && norms_out != norm_in) {
+    CHOCO_HIP(hipMemcpyAsync(norms_out, norm_in, sizeof(float) * nseg, hipMemcpyDeviceToDevice, st));
+  }
+  uint8_t* lvl_plane = packed;
+  uint8_t* sign_plane = packed + plane_bytes(n, cw);
+  const int64_t ntiles = (n + kQTile - 1) / kQTile;
+  profile_begin("qsgd_quantize", st);
+#define CHOCO_Q(CWV)                                                                                         \
+  case CWV:                                                                                                  \
+    hipLaunchKernelGGL((qsgd_quant_kernel<CWV>), dim3((unsigned)ntiles), dim3(kQThreads), 0, st, x, xhat, n, \
+                       seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane, sign_plane, \
+                       dense_out, ntiles);                                                                   \
+    break;
+  switch (cw) {
+    CHOCO_Q(1)
+    CHOCO_Q(2)
+    CHOCO_Q(4)
+    CHOCO_Q(8)
+    CHOCO_Q(16)
+  }
+#undef CHOCO_Q
+  profile_end("qsgd_quantize", st);
+  CHOCO_LAUNCHED("qsgd_quant_kernel");
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_qsgd_decode(const uint8_t* packed, const float* norms, int64_t n, const int64_t* seg_off,
+                                int32_t nseg, int32_t q, int32_t is_biased, float* out, void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(packed && norms && out, "null pointer argument");
+  CHOCO_REQUIRE(q >= 1 && q <= 16, "q must be in [1, 16]");
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
+  CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
+  CHOCO_REQUIRE(aligned16(packed) && aligned16(out), "buffers must be 16-byte aligned");
+  const int cw = container_bits(q);
+  QMsgs M{};
+  M.lvl[0] = packed;
+  M.sgn[0] = packed + plane_bytes(n, cw);
+  M.norms[0] = norms;
+  M.w[0] = 1.0f;
+  M.nmsg = 1;
+  M.self_slot = -1;
+  launch_decode_cw<0>(cw, M, n, seg_off, nseg, (1 << q) - 1, is_biased, out, nullptr, st);
+  CHOCO_LAUNCHED("qsgd_decode_kernel");
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_qsgd_decompress_accumulate(const uint8_t* const* packed_list, const float* const* norms_list,
+                                               const float* weights, int32_t nmsg, int32_t self_slot, int64_t n,
+                                               const int64_t* seg_off, int32_t nseg, int32_t q, int32_t is_biased,
+                                               float* xhat_self, float* memory, void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(packed_list && norms_list && weights && memory, "null pointer argument");
+  CHOCO_REQUIRE(nmsg >= 1 && nmsg <= kQMaxMsg, "nmsg must be in [1, %d]", kQMaxMsg);
+  CHOCO_REQUIRE(self_slot >= -1 && self_slot < nmsg, "bad self_slot");
+  CHOCO_REQUIRE(q >= 1 && q <= 16, "q must be in [1, 16]");
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
+  CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
+  CHOCO_REQUIRE(aligned16(memory) && (!xhat_self || aligned16(xhat_self)), "buffers must be 16-byte aligned");
+  const int cw = container_bits(q);
+  QMsgs M{};
+  for (int m = 0; m < nmsg; ++m) {
+    CHOCO_REQUIRE(packed_list[m] && norms_list[m], "null message pointer");
+    CHOCO_REQUIRE(aligned16(packed_list[m]), "packed messages must be 16-byte aligned");
+    M.lvl[m] = packed_list[m];
+    M.sgn[m] = packed_list[m] + plane_bytes(n, cw);
+    M.norms[m] = norms_list[m];
+    M.w[m] = weights[m];
+  }
+  M.nmsg = nmsg;
+  M.self_slot = self_slot;
+  profile_begin("qsgd_accumulate", st);
+  launch_decode_cw<1>(cw, M, n, seg_off, nseg, (1 << q) - 1, is_biased, xhat_self, memory, st);
+  profile_end("qsgd_accumulate", st);
+  CHOCO_LAUNCHED("qsgd_decode_kernel");
+  return CHOCO_OK;
+}

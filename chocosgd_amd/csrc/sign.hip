@@ -1,0 +1,498 @@
+// Sign(+norm) compression for the CHOCO gossip step on MI355X.
+//
+// Replaces SignCompressor.packing/unpacking (reference
+// dl_code/pcode/utils/sparsification.py:129-163, including the external
+// bit2byte extension) and the norm/sign halves of CHOCOSignCompressor
+// (dl_code/pcode/optim/parallel_choco_v.py:476-558).
+//
+// Layout (the reference's view(32, -1) of the zero-padded flat buffer):
+// N' = ceil(n/32) words; word j holds elements e = r*N' + j, r = 0..31, at
+// bit r; bit set <=> d < 0.
+//
+// Work decomposition ("column tiles"): a 256-thread workgroup owns 1024
+// consecutive words; each wave owns 256 words and lane l owns words
+// j0+4l .. j0+4l+3, so packed words are written once as 16-B stores and every
+// element is read exactly once.  For row r the wave's elements are the
+// contiguous flat run [r*N' + j0, +256); that run starts at an arbitrary
+// alignment m = (r*N' + j0) mod 4 (N' is 2 mod 4 for both BASELINE sign
+// configs), so each lane loads the ALIGNED float4 at A + 4l (A = run start
+// rounded down to 4), computes its 4 sign bits, and the wave realigns the
+// nibbles by one lane shuffle (lane 63 loads one extra float4 for the tail).
+// Per-segment L1 norms are accumulated in fp64: a run that lies inside one
+// segment is wave-reduced and merged per workgroup (one fp64 atomic per
+// segment per workgroup); runs that straddle a segment boundary are reduced
+// per segment inside the wave.  The last workgroup (agent-scope ticket)
+// rounds the sums to fp32 and zeroes the accumulators for the next call.
+#include "choco_common.h"
+
+#include <algorithm>
+
+namespace choco {
+
+constexpr int kSignThreads = 256;
+constexpr int kSignCols = 1024;  // words per workgroup
+
+struct SignWs {
+  unsigned int ticket;
+  unsigned int pad[63];
+  // double acc[nseg] follows at offset 256
+};
+
+CHOCO_DEV void load4g(const float* __restrict__ x, const float* __restrict__ xh, int64_t e, int64_t n,
+                      float (&v)[4]) {
+  if (e + 3 < n) {
+    float4 a = *reinterpret_cast<const float4*>(x + e);
+    if (xh) {
+      float4 h = *reinterpret_cast<const float4*>(xh + e);
+      a.x -= h.x; a.y -= h.y; a.z -= h.z; a.w -= h.w;
+    }
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int64_t i = e + c;
+      v[c] = (i < n && i >= 0) ? (xh ? x[i] - xh[i] : x[i]) : 0.f;
+    }
+  }
+}
+
+CHOCO_DEV uint32_t neg_bits4(const float (&v)[4]) {
+  return (v[0] < 0.f ? 1u : 0u) | (v[1] < 0.f ? 2u : 0u) | (v[2] < 0.f ? 4u : 0u) | (v[3] < 0.f ? 8u : 0u);
+}
+
+CHOCO_DEV int wave_min_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+CHOCO_DEV int wave_max_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+
+CHOCO_DEV int seg_walk(const int64_t* __restrict__ seg_off, int nseg, int s0, int64_t e) {
+  int s = s0;
+  while (s + 1 < nseg && seg_off[s + 1] <= e) ++s;
+  return s;
+}
+
+// Per-row segment info for this workgroup's 32 row runs.
+CHOCO_DEV void row_segments(const int64_t* __restrict__ seg_off, int nseg, int64_t n, int64_t Np, int64_t J0,
+                            int* s_lo, int* s_hi) {
+  if (threadIdx.x < 32) {
+    const int r = threadIdx.x;
+    const int64_t jend = std::min<int64_t>(J0 + kSignCols, Np);
+    const int64_t e0 = (int64_t)r * Np + J0;
+    const int64_t e1 = std::min<int64_t>((int64_t)r * Np + jend, n) - 1;
+    if (e0 < n && e1 >= e0) {
+      s_lo[r] = nseg > 1 ? seg_of(seg_off, nseg, e0) : 0;
+      s_hi[r] = nseg > 1 ? seg_of(seg_off, nseg, e1) : 0;
+    } else {
+      s_lo[r] = -1;
+      s_hi[r] = -1;
+    }
+  }
+}
+
+template <bool XH, bool NORM>
+__global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t Np,
+    const int64_t* __restrict__ seg_off, int nseg, uint32_t* __restrict__ packed, float* __restrict__ l1_out,
+    SignWs* __restrict__ ws) {
+  __shared__ int s_lo[32], s_hi[32];
+  __shared__ double s_rows[kSignThreads / 64][32];
+  __shared__ unsigned int s_flag;
+  double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int64_t J0 = (int64_t)blockIdx.x * kSignCols;
+  const int64_t j0 = J0 + 256 * w;
+  const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
+  if (NORM) row_segments(seg_off, nseg, n, Np, J0, s_lo, s_hi);
+  __syncthreads();
+
+  uint32_t wd[4] = {0u, 0u, 0u, 0u};
+  for (int r = 0; r < 32; ++r) {
+    const int64_t s = (int64_t)r * Np + j0;
+    double rowpart = 0.0;
+    if (ncol > 0 && s < n) {  // wave-uniform
+      const int64_t A = s & ~(int64_t)3;
+      const int m = (int)(s & 3);
+      const int64_t e = A + 4 * lane;
+      float v[4], t[4] = {0.f, 0.f, 0.f, 0.f};
+      load4g(x, XH ? xh : nullptr, e, n, v);
+      if (m != 0 && lane == 63) load4g(x, XH ? xh : nullptr, A + 256, n, t);
+      const uint32_t b4 = neg_bits4(v);
+      uint32_t nb4 = __shfl_down(b4, 1);
+      if (lane == 63) nb4 = neg_bits4(t);
+      const uint32_t w4 = m ? (((b4 >> m) | (nb4 << (4 - m))) & 15u) : b4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wd[c] |= ((w4 >> c) & 1u) << r;
+      if (NORM) {
+        const int64_t lim = std::min<int64_t>(s + ncol, n);
+        const bool uniform = s_lo[r] == s_hi[r];
+        if (uniform) {
+          double p = 0.0;
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (e + c >= s && e + c < lim) p += (double)fabsf(v[c]);
+          if (lane == 63)
+            for (int c = 0; c < m; ++c)
+              if (A + 256 + c < lim) p += (double)fabsf(t[c]);
+          rowpart = wave_sum(p);
+        } else {
+          int sg[4], tg[4];
+          int lo = 0x7fffffff, hi = -1;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            sg[c] = -1;
+            if (e + c >= s && e + c < lim) {
+              sg[c] = seg_walk(seg_off, nseg, s_lo[r], e + c);
+              lo = min(lo, sg[c]);
+              hi = max(hi, sg[c]);
+            }
+            tg[c] = -1;
+            if (lane == 63 && c < m && A + 256 + c < lim) {
+              tg[c] = seg_walk(seg_off, nseg, s_lo[r], A + 256 + c);
+              lo = min(lo, tg[c]);
+              hi = max(hi, tg[c]);
+            }
+          }
+          lo = wave_min_i(lo);
+          hi = wave_max_i(hi);
+          for (int q = lo; q <= hi; ++q) {
+            double p = 0.0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              if (sg[c] == q) p += (double)fabsf(v[c]);
+              if (tg[c] == q) p += (double)fabsf(t[c]);
+            }
+            p = wave_sum(p);
+            if (lane == 0 && p != 0.0) unsafeAtomicAdd(&acc[q], p);
+          }
+        }
+      }
+    }
+    if (NORM && lane == 0) s_rows[w][r] = rowpart;
+  }
+  // packed words: 16-B stores where possible
+  {
+    const int64_t j = j0 + 4 * lane;
+    if (j + 3 < Np) {
+      *reinterpret_cast<uint4*>(packed + j) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (j + c < Np) packed[j + c] = wd[c];
+    }
+  }
+  if (NORM) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int cur = -1;
+      double run = 0.0;
+      for (int r = 0; r < 32; ++r) {
+        if (s_lo[r] < 0 || s_lo[r] != s_hi[r]) continue;
+        double v = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < kSignThreads / 64; ++ww) v += s_rows[ww][r];
+        if (s_lo[r] != cur) {
+          if (cur >= 0 && run != 0.0) unsafeAtomicAdd(&acc[cur], run);
+          cur = s_lo[r];
+          run = 0.0;
+        }
+        run += v;
+      }
+      if (cur >= 0 && run != 0.0) unsafeAtomicAdd(&acc[cur], run);
+    }
+    if (last_block_ticket(&ws->ticket, gridDim.x, &s_flag)) {
+      for (int q = threadIdx.x; q < nseg; q += blockDim.x) l1_out[q] = (float)atomic_exchange_double(&acc[q], 0.0);
+      if (threadIdx.x == 0) __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Decode to +-1 floats (SignCompressor.unpacking).
+__global__ __launch_bounds__(kSignThreads) void sign_unpack_kernel(const uint32_t* __restrict__ packed,
+                                                                   int64_t n, int64_t Np,
+                                                                   float* __restrict__ out) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int64_t j0 = (int64_t)blockIdx.x * kSignCols + 256 * w;
+  const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
+  if (ncol == 0) return;
+  uint32_t wd[4];
+  {
+    const int64_t j = j0 + 4 * lane;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wd[c] = (j + c < Np) ? packed[j + c] : 0u;
+  }
+  for (int r = 0; r < 32; ++r) {
+    const int64_t s = (int64_t)r * Np + j0;
+    if (s >= n) break;
+    const int64_t A = s & ~(int64_t)3;
+    const int m = (int)(s & 3);
+    const int64_t e = A + 4 * lane;
+    const int64_t lim = std::min<int64_t>(s + ncol, n);
+    uint32_t own4 = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) own4 |= ((wd[c] >> r) & 1u) << c;
+    const uint32_t prev4 = __shfl_up(own4, 1);
+    const uint32_t x8 = (own4 << 4) | prev4;
+    float o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o[c] = ((x8 >> (4 + c - m)) & 1u) ? -1.f : 1.f;
+    if (e >= s && e + 3 < lim) {
+      *reinterpret_cast<float4*>(out + e) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (e + c >= s && e + c < lim) out[e + c] = o[c];
+    }
+    if (lane == 63)
+      for (int c = 0; c < m; ++c)
+        if (A + 256 + c < lim) out[A + 256 + c] = ((own4 >> (4 + c - m)) & 1u) ? -1.f : 1.f;
+  }
+}
+
+// Fused receiver update over up to 8 messages (CHOCOSignCompressor.uncompress).
+constexpr int kMaxMsg = 8;
+struct SignMsgs {
+  const uint32_t* packed[kMaxMsg];
+  const float* norms[kMaxMsg];
+  float w[kMaxMsg];
+  int nmsg;
+  int self_slot;
+};
+
+template <int NM>
+CHOCO_DEV void sign_apply(const SignMsgs& M, const float (&sc)[kMaxMsg], const uint32_t (&bits)[kMaxMsg],
+                          int shiftbit, float& h, float& mm) {
+#pragma unroll
+  for (int q = 0; q < NM; ++q) {
+    const float u = ((bits[q] >> shiftbit) & 1u) ? -sc[q] : sc[q];  // (norm/numel) * (+-1), exact
+    if (q == M.self_slot) h = h + u;
+    mm = fmaf(M.w[q], u, mm);  // torch add_(u, alpha=w) fuses on CPU (verified)
+  }
+}
+
+CHOCO_DEV float seg_scale(const float* __restrict__ norms, const int64_t* __restrict__ seg_off, int64_t n,
+                          int seg) {
+  const int64_t numel = seg_off ? seg_off[seg + 1] - seg_off[seg] : n;
+  return norms[seg] / (float)numel;
+}
+
+template <int NM>
+__global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs M, int64_t n, int64_t Np,
+                                                                       const int64_t* __restrict__ seg_off,
+                                                                       int nseg, float* __restrict__ hat,
+                                                                       float* __restrict__ mem) {
+  __shared__ int s_lo[32], s_hi[32];
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int64_t J0 = (int64_t)blockIdx.x * kSignCols;
+  const int64_t j0 = J0 + 256 * w;
+  const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
+  row_segments(seg_off, nseg, n, Np, J0, s_lo, s_hi);
+  __syncthreads();
+  if (ncol == 0) return;
+  uint32_t wd[NM][4];
+  {
+    const int64_t j = j0 + 4 * lane;
+#pragma unroll
+    for (int q = 0; q < NM; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wd[q][c] = (j + c < Np) ? M.packed[q][j + c] : 0u;
+  }
+  const bool has_self = M.self_slot >= 0 && hat != nullptr;
+  for (int r = 0; r < 32; ++r) {
+    const int64_t s = (int64_t)r * Np + j0;
+    if (s >= n) break;
+    const int64_t A = s & ~(int64_t)3;
+    const int m = (int)(s & 3);
+    const int64_t e = A + 4 * lane;
+    const int64_t lim = std::min<int64_t>(s + ncol, n);
+    uint32_t x8[kMaxMsg];
+#pragma unroll
+    for (int q = 0; q < NM; ++q) {
+      uint32_t own4 = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) own4 |= ((wd[q][c] >> r) & 1u) << c;
+      const uint32_t prev4 = __shfl_up(own4, 1);
+      x8[q] = (own4 << 4) | prev4;
+    }
+    const bool uniform = s_lo[r] == s_hi[r];
+    float sc[kMaxMsg];
+    if (uniform) {
+#pragma unroll
+      for (int q = 0; q < NM; ++q) sc[q] = seg_scale(M.norms[q], seg_off, n, s_lo[r]);
+    }
+    // main float4 of this lane
+    {
+      const bool full = e >= s && e + 3 < lim;
+      float hv[4] = {0.f, 0.f, 0.f, 0.f}, mv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (full) {
+        const float4 m4 = *reinterpret_cast<const float4*>(mem + e);
+        mv[0] = m4.x; mv[1] = m4.y; mv[2] = m4.z; mv[3] = m4.w;
+        if (has_self) {
+          const float4 h4 = *reinterpret_cast<const float4*>(hat + e);
+          hv[0] = h4.x; hv[1] = h4.y; hv[2] = h4.z; hv[3] = h4.w;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int64_t i = e + c;
+        const bool own = i >= s && i < lim;
+        if (!own) continue;
+        if (!full) {
+          mv[c] = mem[i];
+          if (has_self) hv[c] = hat[i];
+        }
+        float scl[kMaxMsg];
+        if (uniform) {
+#pragma unroll
+          for (int q = 0; q < NM; ++q) scl[q] = sc[q];
+        } else {
+          const int sg = seg_walk(seg_off, nseg, s_lo[r], i);
+#pragma unroll
+          for (int q = 0; q < NM; ++q) scl[q] = seg_scale(M.norms[q], seg_off, n, sg);
+        }
+        sign_apply<NM>(M, scl, x8, 4 + c - m, hv[c], mv[c]);
+        if (!full) {
+          mem[i] = mv[c];
+          if (has_self) hat[i] = hv[c];
+        }
+      }
+      if (full) {
+        *reinterpret_cast<float4*>(mem + e) = make_float4(mv[0], mv[1], mv[2], mv[3]);
+        if (has_self) *reinterpret_cast<float4*>(hat + e) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+      }
+    }
+    // tail elements of lane 63 (columns 256-m .. 255 of this run)
+    if (lane == 63) {
+      for (int c = 0; c < m; ++c) {
+        const int64_t i = A + 256 + c;
+        if (i >= lim) continue;
+        float hv = has_self ? hat[i] : 0.f, mv = mem[i];
+        float scl[kMaxMsg];
+        if (uniform) {
+#pragma unroll
+          for (int q = 0; q < NM; ++q) scl[q] = sc[q];
+        } else {
+          const int sg = seg_walk(seg_off, nseg, s_lo[r], i);
+#pragma unroll
+          for (int q = 0; q < NM; ++q) scl[q] = seg_scale(M.norms[q], seg_off, n, sg);
+        }
+        uint32_t own[kMaxMsg];
+#pragma unroll
+        for (int q = 0; q < NM; ++q) own[q] = x8[q] >> 4;  // this lane's own nibble
+        sign_apply<NM>(M, scl, own, 4 + c - m, hv, mv);
+        mem[i] = mv;
+        if (has_self) hat[i] = hv;
+      }
+    }
+  }
+}
+
+}  // namespace choco
+
+using namespace choco;
+
+CHOCO_API int64_t choco_sign_words(int64_t n) { return (n + 31) / 32; }
+
+CHOCO_API size_t choco_sign_workspace_size(int32_t nseg) {
+  return 256 + align_up((size_t)(nseg > 0 ? nseg : 1) * sizeof(double), 256);
+}
+
+CHOCO_API int choco_sign_compress(const float* x, const float* xhat, int64_t n, const int64_t* seg_off,
+                                  int32_t nseg, int32_t* packed, float* l1_norms, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(x && packed, "null pointer argument");
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
+  CHOCO_REQUIRE(aligned16(x) && (!xhat || aligned16(xhat)) && aligned16(packed),
+                "x/xhat/packed must be 16-byte aligned");
+  CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
+  const int64_t Np = choco_sign_words(n);
+  const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
+  uint32_t* pk = reinterpret_cast<uint32_t*>(packed);
+  SignWs* w = static_cast<SignWs*>(ws);
+  if (l1_norms) {
+    CHOCO_REQUIRE(ws && ws_bytes >= choco_sign_workspace_size(nseg), "sign workspace too small");
+  }
+  profile_begin("sign_pack", st);
+  if (xhat) {
+    if (l1_norms)
+      hipLaunchKernelGGL((sign_pack_kernel<true, true>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
+                         seg_off, nseg, pk, l1_norms, w);
+    else
+      hipLaunchKernelGGL((sign_pack_kernel<true, false>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
+                         seg_off, nseg, pk, l1_norms, w);
+  } else {
+    if (l1_norms)
+      hipLaunchKernelGGL((sign_pack_kernel<false, true>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
+                         seg_off, nseg, pk, l1_norms, w);
+    else
+      hipLaunchKernelGGL((sign_pack_kernel<false, false>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n,
+                         Np, seg_off, nseg, pk, l1_norms, w);
+  }
+  profile_end("sign_pack", st);
+  CHOCO_LAUNCHED("sign_pack_kernel");
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_sign_unpack(const int32_t* packed, int64_t n, float* out, void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(packed && out && n > 0 && n < (int64_t)INT32_MAX, "bad arguments");
+  CHOCO_REQUIRE(aligned16(out), "out must be 16-byte aligned");
+  const int64_t Np = choco_sign_words(n);
+  const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
+  hipLaunchKernelGGL(sign_unpack_kernel, dim3(grid), dim3(kSignThreads), 0, st,
+                     reinterpret_cast<const uint32_t*>(packed), n, Np, out);
+  CHOCO_LAUNCHED("sign_unpack_kernel");
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_sign_decompress_accumulate(const int32_t* const* packed_list, const float* const* norms_list,
+                                               const float* weights, int32_t nmsg, int32_t self_slot, int64_t n,
+                                               const int64_t* seg_off, int32_t nseg, float* xhat_self,
+                                               float* memory, void* ws, size_t ws_bytes, void* stream) {
+  (void)ws;
+  (void)ws_bytes;
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(packed_list && norms_list && weights && memory, "null pointer argument");
+  CHOCO_REQUIRE(nmsg >= 1 && nmsg <= kMaxMsg, "nmsg must be in [1, %d]", kMaxMsg);
+  CHOCO_REQUIRE(self_slot >= -1 && self_slot < nmsg, "bad self_slot");
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
+  CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
+  CHOCO_REQUIRE(aligned16(memory) && (!xhat_self || aligned16(xhat_self)), "buffers must be 16-byte aligned");
+  SignMsgs M{};
+  for (int q = 0; q < nmsg; ++q) {
+    CHOCO_REQUIRE(packed_list[q] && norms_list[q], "null message pointer");
+    M.packed[q] = reinterpret_cast<const uint32_t*>(packed_list[q]);
+    M.norms[q] = norms_list[q];
+    M.w[q] = weights[q];
+  }
+  M.nmsg = nmsg;
+  M.self_slot = self_slot;
+  const int64_t Np = choco_sign_words(n);
+  const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
+  profile_begin("sign_accumulate", st);
+#define CHOCO_SIGN_ACC(NM)                                                                                 \
+  case NM:                                                                                                  \
+    hipLaunchKernelGGL((sign_accumulate_kernel<NM>), dim3(grid), dim3(kSignThreads), 0, st, M, n, Np,      \
+                       seg_off, nseg, xhat_self, memory);                                                   \
+    break;
+  switch (nmsg) {
+    CHOCO_SIGN_ACC(1)
+    CHOCO_SIGN_ACC(2)
+    CHOCO_SIGN_ACC(3)
+    CHOCO_SIGN_ACC(4)
+    CHOCO_SIGN_ACC(5)
+    CHOCO_SIGN_ACC(6)
+    CHOCO_SIGN_ACC(7)
+    CHOCO_SIGN_ACC(8)
+  }
+#undef CHOCO_SIGN_ACC
+  profile_end("sign_accumulate", st);
+  CHOCO_LAUNCHED("sign_accumulate_kernel");
+  return CHOCO_OK;
+}

@@ -1,0 +1,835 @@
+// Top-k / random-k sparsification for the CHOCO gossip step on MI355X.
+//
+// Replaces SparsificationCompressor.get_top_k / get_random_k
+// (reference dl_code/pcode/utils/sparsification.py:18-54) and the per-tensor
+// compress loop of CHOCOSparsificationCompressor (parallel_choco_v.py:229-260).
+//
+// Exact semantics (both paths below produce bit-identical results):
+//   T  = k-th largest key(d) (key = |d| bits, see choco_common.h)
+//   out = { i : key_i > T }  U  { the (k - #{key > T}) lowest i with key_i == T },
+//   emitted as (d_i, i) in ascending i.
+//
+// Fast path for large n ("pipeline"), one HBM read of the delta:
+//   K1 topk_sample   : one workgroup histograms a 64K-element strided sample of
+//                      keys (32K bins = key>>16) and picks a candidate floor s_lo
+//                      (#{key >= s_lo} >= k with ~6 sigma margin) and a "sure"
+//                      ceiling s_hi (#{key >= s_hi} < k); [s_lo, s_hi) is split
+//                      into 63 equal key-buckets of width 2^shift.
+//   K2 topk_stream   : the streaming pass.  Each wave owns a contiguous range;
+//                      per float4 it ballots candidates (key >= s_lo), prefix-
+//                      counts them with bit-sliced ballots + mbcnt and writes
+//                      (value, index) in index order into its private slot of
+//                      the candidate buffer.  "maybe" candidates (key < s_hi)
+//                      are also kept in LDS and, at the end of the block,
+//                      counting-sorted by bucket into a per-block side list;
+//                      per-block bucket suffix counts go to a [64][nb] table
+//                      and, by one 256-B wave atomic, to global totals.
+//   K34 topk_finalize: every workgroup redundantly finds the bucket j* holding
+//                      the k-th key from the totals, gathers that bucket's keys
+//                      (a few thousand) from the side lists into LDS, radix-
+//                      selects T and the tie quota exactly, scans per-block
+//                      output offsets, then compacts its share of the candidate
+//                      buffer into the final ascending-index output.
+//   If the sample's guess was off (too few candidates, T in the "sure" range,
+//   bucket j* larger than LDS, or a wave's maybe-list overflowed), K34 falls
+//   back to an exact single-workgroup radix select over the full input
+//   (correct, slow, data-dependent only).
+// Small n (<= kSmallN) and every segment of the batched segmented path use
+// the same exact radix select (block_topk_exact) in one workgroup.
+#include "choco_common.h"
+
+#include <math.h>
+#include <algorithm>
+
+namespace choco {
+
+constexpr int kK2Threads = 256;
+constexpr int kK2Waves = kK2Threads / 64;
+constexpr int kK2Unroll = 4;
+constexpr int kNBucket = 64;            // 63 "maybe" buckets + 1 "sure"
+constexpr int kMaybeCap = 1024;         // maybe keys per wave kept in LDS
+constexpr int kSideCap = kK2Waves * kMaybeCap;
+constexpr int kNRep = 8;                // replicas of the global totals (per XCD group)
+constexpr int kNbMax = 4096;            // max K2 blocks (K34 keeps per-block arrays in LDS)
+constexpr int kMCap = 16384;            // max keys of bucket j* handled in LDS
+constexpr int kK34Threads = 256;
+constexpr int kSampleThreads = 1024;
+constexpr int kSampleN = 65536;
+constexpr int kSampleChunk = 256;
+constexpr int64_t kSmallN = 65536;
+constexpr int kExactThreads = 1024;
+
+enum SrcMode { kData = 0, kHash = 1 };
+
+struct TopkCtrl {
+  uint32_t s_lo, s_hi, shift, overflow;
+  uint32_t pad[12];
+  uint32_t G[kNRep][kNBucket];
+};
+
+struct TopkLayout {
+  int64_t n;
+  uint32_t tile, nb;
+  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, total;
+};
+
+static TopkLayout topk_layout(int64_t n) {
+  TopkLayout L{};
+  L.n = n;
+  uint32_t tile = 32768;
+  while ((int64_t)tile * kNbMax < n) tile <<= 1;
+  L.tile = tile;
+  L.nb = (uint32_t)((n + tile - 1) / tile);
+  size_t o = 0;
+  L.off_ctrl = o; o += align_up(sizeof(TopkCtrl), 256);
+  L.off_cum = o;  o += align_up((size_t)kNBucket * L.nb * 4, 256);
+  L.off_cntw = o; o += align_up((size_t)L.nb * kK2Waves * 4, 256);
+  L.off_side = o; o += align_up((size_t)L.nb * kSideCap * 4, 256);
+  L.off_cval = o; o += align_up((size_t)L.nb * tile * 4, 256);
+  L.off_cidx = o; o += align_up((size_t)L.nb * tile * 4, 256);
+  L.total = o;
+  return L;
+}
+
+// ----------------------------------------------------------------------------
+// key / value sources
+// ----------------------------------------------------------------------------
+template <int MODE, bool XH>
+struct Src {
+  const float* __restrict__ x;
+  const float* __restrict__ xh;
+  uint64_t seed;
+  CHOCO_DEV float val(int64_t i) const { return XH ? x[i] - xh[i] : x[i]; }
+  CHOCO_DEV uint32_t key_of(int64_t i, float v) const {
+    if (MODE == kHash) return rank_hash(seed, (uint32_t)i) >> 1;
+    return fkey(v);
+  }
+  CHOCO_DEV uint32_t key(int64_t i) const {
+    if (MODE == kHash) return rank_hash(seed, (uint32_t)i) >> 1;
+    return fkey(val(i));
+  }
+};
+
+// ----------------------------------------------------------------------------
+// exact single-workgroup select (small n, segments, fallback)
+// ----------------------------------------------------------------------------
+struct ExactSmem {
+  uint32_t hist[2048];
+  uint32_t scratch[24];
+  uint32_t bc[4];
+};
+
+// Returns T (k-th largest key) and the tie quota r via bc[0], bc[1]; bc[2] = #ties at T.
+template <class S>
+CHOCO_DEV void block_select_T(const S& src, int64_t n, int64_t k, ExactSmem& sm) {
+  const int tid = threadIdx.x, B = blockDim.x;
+  uint32_t prefix = 0, maskhi = 0;
+  uint32_t krem = (uint32_t)k;
+  const int shs[3] = {20, 9, 0};
+  const int wds[3] = {11, 11, 9};
+  for (int rd = 0; rd < 3; ++rd) {
+    const int sh = shs[rd];
+    const uint32_t dmask = (1u << wds[rd]) - 1u;
+    for (int i = tid; i < 2048; i += B) sm.hist[i] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < n; i += B) {
+      uint32_t key = src.key(i);
+      if ((key & maskhi) == prefix) atomicAdd(&sm.hist[(key >> sh) & dmask], 1u);
+    }
+    __syncthreads();
+    const int nbins = (int)dmask + 1;
+    const int per = (nbins + B - 1) / B;
+    const int b0 = tid * per;
+    uint32_t local = 0;
+    for (int j = 0; j < per; ++j)
+      if (b0 + j < nbins) local += sm.hist[b0 + j];
+    uint32_t total;
+    uint32_t pre = block_excl_scan(local, sm.scratch, &total);
+    uint32_t above = total - pre - local;  // matching keys in bins above my chunk
+    if (above < krem && krem <= above + local) {
+      uint32_t acc = above;
+      for (int j = per - 1; j >= 0; --j) {
+        int bin = b0 + j;
+        if (bin >= nbins) continue;
+        uint32_t c = sm.hist[bin];
+        if (acc + c >= krem) {
+          sm.bc[0] = (uint32_t)bin;
+          sm.bc[1] = krem - acc;
+          sm.bc[2] = c;
+          break;
+        }
+        acc += c;
+      }
+    }
+    __syncthreads();
+    prefix |= sm.bc[0] << sh;
+    maskhi |= dmask << sh;
+    krem = sm.bc[1];
+    __syncthreads();
+  }
+  if (tid == 0) { sm.bc[0] = prefix; sm.bc[1] = krem; }
+  __syncthreads();
+}
+
+// Ordered compaction of the selection defined by (T, r) over [0, n).
+template <class S>
+CHOCO_DEV void block_emit(const S& src, int64_t n, uint32_t T, uint32_t r, uint32_t ties_total,
+                          float scale, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
+                          int64_t idx_base, ExactSmem& sm) {
+  const int tid = threadIdx.x, B = blockDim.x;
+  const bool all_ties = (r == ties_total);
+  uint32_t out = 0, tie_run = 0;
+  for (int64_t base = 0; base < n; base += B) {
+    const int64_t i = base + tid;
+    const bool valid = i < n;
+    float v = 0.f;
+    uint32_t key = 0;
+    if (valid) { v = src.val(i); key = src.key_of(i, v); }
+    const bool gt = valid && key > T;
+    const bool eq = valid && key == T;
+    bool sel;
+    if (all_ties) {
+      sel = gt || eq;
+    } else {
+      uint32_t ntie;
+      uint32_t trank = tie_run + block_excl_scan(eq ? 1u : 0u, sm.scratch, &ntie);
+      sel = gt || (eq && trank < r);
+      tie_run += ntie;
+    }
+    uint32_t nsel;
+    uint32_t pos = out + block_excl_scan(sel ? 1u : 0u, sm.scratch, &nsel);
+    if (sel) {
+      out_val[pos] = v * scale;
+      out_idx[pos] = (int32_t)(i + idx_base);
+    }
+    out += nsel;
+  }
+}
+
+template <class S>
+CHOCO_DEV void block_topk_exact(const S& src, int64_t n, int64_t k, float scale,
+                                float* out_val, int32_t* out_idx, int64_t idx_base, ExactSmem& sm) {
+  if (k >= n) {
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+      out_val[i] = src.val(i) * scale;
+      out_idx[i] = (int32_t)(i + idx_base);
+    }
+    return;
+  }
+  block_select_T(src, n, k, sm);
+  const uint32_t T = sm.bc[0], r = sm.bc[1], ties = sm.bc[2];
+  __syncthreads();
+  block_emit(src, n, T, r, ties, scale, out_val, out_idx, idx_base, sm);
+}
+
+template <int MODE, bool XH>
+__global__ __launch_bounds__(kExactThreads) void topk_exact_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint64_t seed,
+    float scale, float* __restrict__ out_val, int32_t* __restrict__ out_idx, int64_t idx_base) {
+  __shared__ ExactSmem sm;
+  Src<MODE, XH> src{x, xh, seed};
+  block_topk_exact(src, n, k, scale, out_val, out_idx, idx_base, sm);
+}
+
+// Segmented: plan rows {off, len, k, out_off}; one workgroup per segment that
+// is not routed to the pipeline.
+CHOCO_DEV bool seg_uses_pipeline(int64_t off, int64_t len);
+
+template <bool XH>
+__global__ __launch_bounds__(kExactThreads) void topk_segmented_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ plan,
+    int32_t nseg, float* __restrict__ out_val, int32_t* __restrict__ out_idx) {
+  __shared__ ExactSmem sm;
+  const int s = blockIdx.x;
+  if (s >= nseg) return;
+  const int64_t off = plan[4 * s + 0], len = plan[4 * s + 1], k = plan[4 * s + 2], oo = plan[4 * s + 3];
+  if (seg_uses_pipeline(off, len) || len == 0) return;
+  Src<kData, XH> src{x + off, XH ? xh + off : nullptr, 0};
+  block_topk_exact(src, len, k, 1.0f, out_val + oo, out_idx + oo, off, sm);
+}
+
+// ----------------------------------------------------------------------------
+// K1: sample -> (s_lo, s_hi, shift)
+// ----------------------------------------------------------------------------
+CHOCO_DEV void write_params(TopkCtrl* ctrl, uint32_t s_lo, uint64_t s_hi_est) {
+  uint64_t width = s_hi_est > s_lo ? s_hi_est - s_lo : 1;
+  uint32_t shift = 0;
+  while ((63ull << shift) < width) ++shift;
+  uint64_t s_hi = (uint64_t)s_lo + (63ull << shift);
+  if (s_hi > 0xFFFFFFFFull) s_hi = 0xFFFFFFFFull;
+  ctrl->s_lo = s_lo;
+  ctrl->s_hi = (uint32_t)s_hi;
+  ctrl->shift = shift;
+}
+
+template <bool XH>
+__global__ __launch_bounds__(kSampleThreads) void topk_sample_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k,
+    TopkCtrl* __restrict__ ctrl) {
+  __shared__ uint32_t hist[32768];
+  __shared__ uint32_t scratch[24];
+  __shared__ uint32_t res[2];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 32768; i += kSampleThreads) hist[i] = 0;
+  for (int i = tid; i < kNRep * kNBucket; i += kSampleThreads) (&ctrl->G[0][0])[i] = 0;
+  if (tid == 0) { ctrl->overflow = 0; res[0] = 0; res[1] = 0xFFFFFFFFu; }
+  __syncthreads();
+  int64_t m;
+  if (n <= kSampleN) {
+    m = n;
+    for (int64_t i = tid; i < n; i += kSampleThreads) {
+      float v = XH ? x[i] - xh[i] : x[i];
+      atomicAdd(&hist[fkey(v) >> 16], 1u);
+    }
+  } else {
+    m = kSampleN;
+    constexpr int nchunk = kSampleN / kSampleChunk;          // 256 chunks
+    constexpr int f4_per_chunk = kSampleChunk / 4;            // 64 float4
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    const float4* h4 = reinterpret_cast<const float4*>(xh);
+    const int64_t stride4 = ((n - kSampleChunk) / (nchunk - 1)) >> 2;  // chunk stride in float4
+#pragma unroll 4
+    for (int it = 0; it < kSampleN / 4 / kSampleThreads; ++it) {   // 16 float4 per thread
+      int s = it * kSampleThreads + tid;
+      int c = s / f4_per_chunk;
+      int64_t q = (int64_t)c * stride4 + (s % f4_per_chunk);
+      float4 v = x4[q];
+      if (XH) { float4 h = h4[q]; v.x -= h.x; v.y -= h.y; v.z -= h.z; v.w -= h.w; }
+      atomicAdd(&hist[fkey(v.x) >> 16], 1u);
+      atomicAdd(&hist[fkey(v.y) >> 16], 1u);
+      atomicAdd(&hist[fkey(v.z) >> 16], 1u);
+      atomicAdd(&hist[fkey(v.w) >> 16], 1u);
+    }
+  }
+  __syncthreads();
+  // thread t owns bins [32t, 32t+32)
+  uint32_t local = 0;
+  for (int j = 0; j < 32; ++j) local += hist[tid * 32 + j];
+  uint32_t total;
+  uint32_t pre = block_excl_scan(local, scratch, &total);
+  uint32_t above = total - pre - local;
+  const double e = (double)k / (double)n * (double)m;
+  const double sd = sqrt(e);
+  const double rlo_d = ceil(e + 6.0 * sd + 4.0);
+  const double rhi_d = floor(e - 6.0 * sd - 4.0);
+  const uint32_t R_lo = rlo_d >= (double)m ? 0xFFFFFFFFu : (uint32_t)rlo_d;
+  const uint32_t R_hi = rhi_d < 1.0 ? 0u : (uint32_t)rhi_d;
+  // res[0] = bin_lo (0 if R_lo unreachable), res[1] = bin_hi (none -> 0xFFFFFFFF)
+  if (R_lo != 0xFFFFFFFFu && above < R_lo && R_lo <= above + local) {
+    uint32_t acc = above;
+    for (int j = 31; j >= 0; --j) {
+      acc += hist[tid * 32 + j];
+      if (acc >= R_lo) { res[0] = (uint32_t)(tid * 32 + j); break; }
+    }
+  }
+  if (R_hi != 0u && above < R_hi && R_hi <= above + local) {
+    uint32_t acc = above;
+    for (int j = 31; j >= 0; --j) {
+      acc += hist[tid * 32 + j];
+      if (acc >= R_hi) { res[1] = (uint32_t)(tid * 32 + j); break; }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t s_lo = res[0] << 16;
+    uint64_t s_hi_est = (res[1] == 0xFFFFFFFFu) ? 0x80000000ull : ((uint64_t)res[1] + 1) << 16;
+    write_params(ctrl, s_lo, s_hi_est);
+  }
+}
+
+// Random-k: keys are uniform on [0, 2^31); thresholds from the binomial tails.
+__global__ void topk_set_params_kernel(TopkCtrl* __restrict__ ctrl, uint32_t s_lo, uint64_t s_hi_est) {
+  for (int i = threadIdx.x; i < kNRep * kNBucket; i += blockDim.x) (&ctrl->G[0][0])[i] = 0;
+  if (threadIdx.x == 0) { ctrl->overflow = 0; write_params(ctrl, s_lo, s_hi_est); }
+}
+
+// ----------------------------------------------------------------------------
+// K2: streaming candidate compaction
+// ----------------------------------------------------------------------------
+template <int MODE, bool XH>
+__global__ __launch_bounds__(kK2Threads) void topk_stream_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, uint32_t tile, uint32_t nb,
+    uint64_t seed, TopkCtrl* __restrict__ ctrl, uint32_t* __restrict__ cum_tab,
+    uint32_t* __restrict__ cntw, uint32_t* __restrict__ side, float* __restrict__ cval,
+    uint32_t* __restrict__ cidx) {
+  __shared__ uint32_t s_maybe[kK2Waves][kMaybeCap];
+  __shared__ uint32_t s_hist[kNBucket];
+  __shared__ uint32_t s_cur[kNBucket];
+  __shared__ uint32_t s_cnt[kK2Waves];
+  __shared__ uint32_t s_mcnt[kK2Waves];
+
+  const uint32_t s_lo = ctrl->s_lo, s_hi = ctrl->s_hi, shift = ctrl->shift;
+  const int lane = lane_id();
+  const int w = threadIdx.x >> 6;
+  const int64_t b = blockIdx.x;
+  const int64_t wlen = tile / kK2Waves;
+  const int64_t wbeg = b * tile + w * wlen;
+  const int64_t wend = min(wbeg + wlen, n);
+  float* __restrict__ ov = cval + wbeg;
+  uint32_t* __restrict__ oi = cidx + wbeg;
+  Src<MODE, XH> src{x, xh, seed};
+
+  uint32_t ccount = 0;  // candidates written by this wave (wave-uniform)
+  uint32_t mcount = 0;  // maybe keys seen by this wave (wave-uniform, may exceed cap)
+
+  for (int64_t base = wbeg; base < wend; base += 256 * kK2Unroll) {
+    float v[kK2Unroll][4];
+    uint32_t kk[kK2Unroll][4];
+    if (MODE == kData) {
+#pragma unroll
+      for (int u = 0; u < kK2Unroll; ++u) {
+        const int64_t i = base + u * 256 + 4 * lane;
+        if (i + 3 < wend) {
+          float4 a = *reinterpret_cast<const float4*>(x + i);
+          if (XH) {
+            float4 h = *reinterpret_cast<const float4*>(xh + i);
+            a.x -= h.x; a.y -= h.y; a.z -= h.z; a.w -= h.w;
+          }
+          v[u][0] = a.x; v[u][1] = a.y; v[u][2] = a.z; v[u][3] = a.w;
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) v[u][c] = (i + c < wend) ? src.val(i + c) : 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kK2Unroll; ++u) {
+      const int64_t i = base + u * 256 + 4 * lane;
+      uint32_t cflags = 0, mflags = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const bool valid = i + c < wend;
+        uint32_t key = MODE == kData ? fkey(v[u][c]) : (valid ? src.key_of(i + c, 0.f) : 0u);
+        kk[u][c] = key;
+        const bool cand = valid && key >= s_lo;
+        cflags |= (cand ? 1u : 0u) << c;
+        mflags |= ((cand && key < s_hi) ? 1u : 0u) << c;
+      }
+      const uint32_t cn = __builtin_popcount(cflags);
+      const uint64_t b0 = ballot(cn & 1u), b1 = ballot(cn & 2u), b2 = ballot(cn & 4u);
+      if ((b0 | b1 | b2) == 0ull) continue;  // wave-uniform: no candidate in this float4 row
+      uint32_t pos = ccount + mask_prefix(b0) + 2u * mask_prefix(b1) + 4u * mask_prefix(b2);
+      ccount += (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+      const uint32_t mn = __builtin_popcount(mflags);
+      const uint64_t m0 = ballot(mn & 1u), m1 = ballot(mn & 2u), m2 = ballot(mn & 4u);
+      uint32_t mpos = mcount + mask_prefix(m0) + 2u * mask_prefix(m1) + 4u * mask_prefix(m2);
+      mcount += (uint32_t)(__popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2));
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (cflags & (1u << c)) {
+          float val = MODE == kData ? v[u][c] : src.val(i + c);
+          ov[pos] = val;
+          oi[pos] = (uint32_t)(i + c);
+          ++pos;
+          if (mflags & (1u << c)) {
+            if (mpos < kMaybeCap) s_maybe[w][mpos] = kk[u][c];
+            ++mpos;
+          }
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    s_cnt[w] = ccount;
+    s_mcnt[w] = mcount;
+    if (mcount > kMaybeCap) atomicOr(&ctrl->overflow, 1u);
+  }
+  if (threadIdx.x < kNBucket) s_hist[threadIdx.x] = 0;
+  __syncthreads();
+  // bucket histogram of the maybe keys (each wave bins its own list)
+  {
+    const uint32_t mc = min(s_mcnt[w], (uint32_t)kMaybeCap);
+    for (uint32_t j = lane; j < mc; j += 64) atomicAdd(&s_hist[(s_maybe[w][j] - s_lo) >> shift], 1u);
+  }
+  uint32_t csum = 0, msum = 0;
+#pragma unroll
+  for (int ww = 0; ww < kK2Waves; ++ww) {
+    csum += s_cnt[ww];
+    msum += min(s_mcnt[ww], (uint32_t)kMaybeCap);
+  }
+  __syncthreads();
+  if (w == 0) {
+    // bucket 63 = sure; cum[j] = sum_{i >= j} cnt[i]
+    uint32_t c = (lane == 63) ? (csum - msum) : s_hist[lane];
+    // reverse inclusive scan (suffix sums) via lane mirroring
+    uint32_t rv = __shfl(c, 63 - lane);
+    uint32_t inc = wave_incl_scan(rv);
+    uint32_t cum = __shfl(inc, 63 - lane);
+    cum_tab[(int64_t)lane * nb + b] = cum;
+    atomicAdd(&ctrl->G[b & (kNRep - 1)][lane], cum);
+    // counting-sort cursor: position of bucket j = #maybe with bucket > j
+    uint32_t cum_next = __shfl_down(cum, 1);
+    uint32_t sure = __shfl(cum, 63);
+    if (lane < 63) s_cur[lane] = cum_next - sure;
+    if (lane < kK2Waves) cntw[b * kK2Waves + lane] = s_cnt[lane];
+  }
+  __syncthreads();
+  uint32_t* __restrict__ sd = side + b * kSideCap;
+  {
+    const uint32_t mc = min(s_mcnt[w], (uint32_t)kMaybeCap);
+    for (uint32_t j = lane; j < mc; j += 64) {
+      uint32_t key = s_maybe[w][j];
+      uint32_t p = atomicAdd(&s_cur[(key - s_lo) >> shift], 1u);
+      sd[p] = key;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// K34: exact threshold + ordered output
+// ----------------------------------------------------------------------------
+struct FinSmem {
+  uint32_t keys[kMCap];
+  uint32_t A[kNbMax + 1];   // key start per K2 block (exclusive scan of bucket-j* counts)
+  uint32_t Bv[kNbMax];      // side offset of bucket j*, later selected-output offset
+  uint32_t Cv[kNbMax];      // #candidates in buckets > j*, later tie_before
+  uint32_t Dv[kNbMax];      // #keys == T per K2 block
+  uint32_t G[kNBucket];
+  uint32_t hist[256];
+  uint32_t scratch[24];
+  uint32_t bc[8];
+};
+
+template <int MODE, bool XH>
+__global__ __launch_bounds__(kK34Threads) void topk_finalize_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile,
+    uint32_t nb, uint64_t seed, float scale, const TopkCtrl* __restrict__ ctrl,
+    const uint32_t* __restrict__ cum_tab, const uint32_t* __restrict__ cntw,
+    const uint32_t* __restrict__ side, const float* __restrict__ cval,
+    const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
+    int64_t idx_base) {
+  __shared__ FinSmem fs;
+  __shared__ ExactSmem es;
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const uint32_t s_lo = ctrl->s_lo, shift = ctrl->shift;
+  Src<MODE, XH> src{x, xh, seed};
+
+  if (tid < kNBucket) {
+    uint32_t g = 0;
+#pragma unroll
+    for (int r = 0; r < kNRep; ++r) g += ctrl->G[r][tid];
+    fs.G[tid] = g;
+  }
+  __syncthreads();
+  // j* = max{ j <= 62 : G[j] >= k }
+  bool fallback = ctrl->overflow != 0 || fs.G[0] < (uint32_t)k || fs.G[63] >= (uint32_t)k;
+  uint32_t jstar = 0;
+  if (!fallback) {
+    for (int j = 62; j >= 0; --j)
+      if (fs.G[j] >= (uint32_t)k) { jstar = (uint32_t)j; break; }
+    const uint32_t M = fs.G[jstar] - fs.G[jstar + 1];
+    if (M > (uint32_t)kMCap) fallback = true;
+  }
+  if (fallback) {
+    if (blockIdx.x == 0) block_topk_exact(src, n, k, scale, out_val, out_idx, idx_base, es);
+    return;
+  }
+  const uint32_t rank_in = (uint32_t)k - fs.G[jstar + 1];  // 1 <= rank_in <= M
+
+  // per K2 block: bucket-j* count, side offset, count above bucket j*
+  const int per = (nb + kK34Threads - 1) / kK34Threads;
+  const int b0 = tid * per;
+  uint32_t local = 0;
+  for (int q = 0; q < per; ++q) {
+    const int b = b0 + q;
+    if (b >= (int)nb) break;
+    const uint32_t a = cum_tab[(int64_t)jstar * nb + b];
+    const uint32_t c = cum_tab[(int64_t)(jstar + 1) * nb + b];
+    const uint32_t s = cum_tab[(int64_t)63 * nb + b];
+    fs.A[b] = a - c;   // temporarily: count
+    fs.Bv[b] = c - s;  // side offset of bucket j*
+    fs.Cv[b] = c;      // candidates with bucket > j* (incl. sure)
+    local += a - c;
+  }
+  uint32_t M;
+  uint32_t pre = block_excl_scan(local, fs.scratch, &M);
+  for (int q = 0; q < per; ++q) {
+    const int b = b0 + q;
+    if (b >= (int)nb) break;
+    const uint32_t cnt = fs.A[b];
+    fs.A[b] = pre;
+    pre += cnt;
+  }
+  if (tid == 0) fs.A[nb] = M;
+  __syncthreads();
+  // gather bucket-j* keys (block order)
+  for (int q = 0; q < per; ++q) {
+    const int b = b0 + q;
+    if (b >= (int)nb) break;
+    const uint32_t st = fs.A[b], cnt = fs.A[b + 1] - st;
+    const uint32_t* sp = side + (int64_t)b * kSideCap + fs.Bv[b];
+    for (uint32_t j = 0; j < cnt; ++j) fs.keys[st + j] = sp[j];
+  }
+  __syncthreads();
+  // radix select inside the bucket: rel = key - base_j in [0, 2^shift)
+  const uint32_t base_j = s_lo + (jstar << shift);
+  uint32_t prefix = 0, krem = rank_in;
+  int sh = (int)shift;
+  while (sh > 0) {
+    const int dsh = sh > 8 ? sh - 8 : 0;
+    const uint32_t dmask = (1u << (sh - dsh)) - 1u;
+    fs.hist[tid] = 0;  // kK34Threads == 256 bins
+    __syncthreads();
+    for (uint32_t j = tid; j < M; j += kK34Threads) {
+      const uint32_t rel = fs.keys[j] - base_j;
+      if ((rel >> sh) == (prefix >> sh)) atomicAdd(&fs.hist[(rel >> dsh) & dmask], 1u);
+    }
+    __syncthreads();
+    if (w == 0) {
+      // suffix scan over 256 bins: lane l owns bins [4l, 4l+4)
+      uint32_t h0 = fs.hist[4 * lane], h1 = fs.hist[4 * lane + 1], h2 = fs.hist[4 * lane + 2],
+               h3 = fs.hist[4 * lane + 3];
+      uint32_t loc = h0 + h1 + h2 + h3;
+      uint32_t rv = __shfl(loc, 63 - lane);
+      uint32_t inc = wave_incl_scan(rv);
+      uint32_t suf_incl = __shfl(inc, 63 - lane);  // bins >= 4*lane
+      uint32_t above = suf_incl - loc;
+      if (above < krem && krem <= suf_incl) {
+        uint32_t acc = above;
+        uint32_t hs[4] = {h0, h1, h2, h3};
+        for (int t = 3; t >= 0; --t) {
+          if (acc + hs[t] >= krem) { fs.bc[0] = 4 * lane + t; fs.bc[1] = krem - acc; break; }
+          acc += hs[t];
+        }
+      }
+    }
+    __syncthreads();
+    prefix |= fs.bc[0] << dsh;
+    krem = fs.bc[1];
+    sh = dsh;
+    __syncthreads();
+  }
+  const uint32_t T = base_j + prefix;
+  const uint32_t r = krem;  // ties at T to take (>= 1)
+
+  // per K2 block: gt / eq counts of bucket j*, tie prefix, output offsets
+  uint32_t eq_local = 0;
+  for (int q = 0; q < per; ++q) {
+    const int b = b0 + q;
+    if (b >= (int)nb) break;
+    uint32_t eq = 0, gt = 0;
+    for (uint32_t j = fs.A[b]; j < fs.A[b + 1]; ++j) {
+      const uint32_t key = fs.keys[j];
+      gt += key > T;
+      eq += key == T;
+    }
+    fs.Bv[b] = gt;  // side offsets are no longer needed
+    fs.Dv[b] = eq;
+    eq_local += eq;
+  }
+  uint32_t tie_total;
+  uint32_t tb = block_excl_scan(eq_local, fs.scratch, &tie_total);
+  uint32_t sel_local = 0;
+  for (int q = 0; q < per; ++q) {
+    const int b = b0 + q;
+    if (b >= (int)nb) break;
+    const uint32_t eq = fs.Dv[b];
+    const uint32_t take = tb >= r ? 0u : min(eq, r - tb);
+    const uint32_t sel = fs.Cv[b] + fs.Bv[b] + take;
+    fs.Cv[b] = tb;   // tie_before
+    fs.Bv[b] = sel;  // selected count (scanned below)
+    tb += eq;
+    sel_local += sel;
+  }
+  uint32_t sel_total;
+  uint32_t sel_pre = block_excl_scan(sel_local, fs.scratch, &sel_total);
+  for (int q = 0; q < per; ++q) {
+    const int b = b0 + q;
+    if (b >= (int)nb) break;
+    const uint32_t c = fs.Bv[b];
+    fs.Bv[b] = sel_pre;
+    sel_pre += c;
+  }
+  __syncthreads();
+
+  // ordered compaction: each wave takes whole K2 blocks
+  const int nwaves_total = gridDim.x * (kK34Threads / 64);
+  for (int b = blockIdx.x * (kK34Threads / 64) + w; b < (int)nb; b += nwaves_total) {
+    uint32_t out = fs.Bv[b];
+    uint32_t tie_run = fs.Cv[b];
+    for (int w2 = 0; w2 < kK2Waves; ++w2) {
+      const uint32_t cnt = cntw[(int64_t)b * kK2Waves + w2];
+      const int64_t cb = (int64_t)b * tile + (int64_t)w2 * (tile / kK2Waves);
+      for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
+        const uint32_t j = c0 + lane;
+        const bool valid = j < cnt;
+        float v = 0.f;
+        uint32_t idx = 0, key = 0;
+        if (valid) {
+          v = cval[cb + j];
+          idx = cidx[cb + j];
+          key = MODE == kData ? fkey(v) : (rank_hash(seed, idx) >> 1);
+        }
+        const bool gt = valid && key > T;
+        const bool eq = valid && key == T;
+        const uint64_t eqm = ballot(eq);
+        const bool sel = gt || (eq && tie_run + mask_prefix(eqm) < r);
+        const uint64_t selm = ballot(sel);
+        if (sel) {
+          const uint32_t pos = out + mask_prefix(selm);
+          out_val[pos] = v * scale;
+          out_idx[pos] = (int32_t)((int64_t)idx + idx_base);
+        }
+        out += (uint32_t)__popcll(selm);
+        tie_run += (uint32_t)__popcll(eqm);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// host dispatch
+// ----------------------------------------------------------------------------
+constexpr int64_t kPipeMinSeg = 1 << 20;
+CHOCO_DEV bool seg_uses_pipeline(int64_t off, int64_t len) {
+  return len >= kPipeMinSeg && (off & 3) == 0;
+}
+static bool host_seg_uses_pipeline(int64_t off, int64_t len) {
+  return len >= kPipeMinSeg && (off & 3) == 0;
+}
+
+size_t topk_ws_bytes(int64_t n) { return n > kSmallN ? topk_layout(n).total : 256; }
+
+template <int MODE, bool XH>
+static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
+                       float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes,
+                       hipStream_t st) {
+  if (n <= kSmallN || k >= n) {
+    hipLaunchKernelGGL((topk_exact_kernel<MODE, XH>), dim3(1), dim3(kExactThreads), 0, st, x, xh, n, k,
+                       seed, scale, out_val, out_idx, idx_base);
+    CHOCO_LAUNCHED("topk_exact_kernel");
+    return CHOCO_OK;
+  }
+  const TopkLayout L = topk_layout(n);
+  CHOCO_REQUIRE(ws != nullptr && ws_bytes >= L.total, "top-k workspace too small: need %zu bytes, got %zu",
+                L.total, ws_bytes);
+  char* base = static_cast<char*>(ws);
+  TopkCtrl* ctrl = reinterpret_cast<TopkCtrl*>(base + L.off_ctrl);
+  uint32_t* cum = reinterpret_cast<uint32_t*>(base + L.off_cum);
+  uint32_t* cntw = reinterpret_cast<uint32_t*>(base + L.off_cntw);
+  uint32_t* side = reinterpret_cast<uint32_t*>(base + L.off_side);
+  float* cval = reinterpret_cast<float*>(base + L.off_cval);
+  uint32_t* cidx = reinterpret_cast<uint32_t*>(base + L.off_cidx);
+  if (MODE == kData) {
+    hipLaunchKernelGGL((topk_sample_kernel<XH>), dim3(1), dim3(kSampleThreads), 0, st, x, xh, n, k, ctrl);
+    CHOCO_LAUNCHED("topk_sample_kernel");
+  } else {
+    // keys uniform on [0, 2^31): P(key >= t) = (2^31 - t) / 2^31
+    const double nd = (double)n, kd = (double)k, sd = sqrt(kd);
+    const double c_lo = std::min(nd, kd + 6.0 * sd + 16.0);
+    const double c_hi = kd - 6.0 * sd - 16.0;
+    const double two31 = 2147483648.0;
+    uint32_t s_lo = (uint32_t)std::max(0.0, floor(two31 * (1.0 - c_lo / nd)));
+    uint64_t s_hi_est = c_hi < 1.0 ? 0x80000000ull : (uint64_t)ceil(two31 * (1.0 - c_hi / nd));
+    if (s_hi_est <= s_lo) s_hi_est = (uint64_t)s_lo + 1;
+    hipLaunchKernelGGL(topk_set_params_kernel, dim3(1), dim3(256), 0, st, ctrl, s_lo, s_hi_est);
+    CHOCO_LAUNCHED("topk_set_params_kernel");
+  }
+  profile_begin("topk_stream", st);
+  hipLaunchKernelGGL((topk_stream_kernel<MODE, XH>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, L.tile,
+                     L.nb, seed, ctrl, cum, cntw, side, cval, cidx);
+  profile_end("topk_stream", st);
+  CHOCO_LAUNCHED("topk_stream_kernel");
+  const uint32_t g34 = std::min<uint32_t>(256u, (L.nb + 3) / 4);
+  hipLaunchKernelGGL((topk_finalize_kernel<MODE, XH>), dim3(g34), dim3(kK34Threads), 0, st, x, xh, n, k,
+                     L.tile, L.nb, seed, scale, ctrl, cum, cntw, side, cval, cidx, out_val, out_idx, idx_base);
+  CHOCO_LAUNCHED("topk_finalize_kernel");
+  return CHOCO_OK;
+}
+
+template <int MODE>
+static int dispatch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
+                         float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes,
+                         hipStream_t st) {
+  CHOCO_REQUIRE(x != nullptr && out_val != nullptr && out_idx != nullptr, "null pointer argument");
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n must be in [1, 2^31-1), got %lld", (long long)n);
+  CHOCO_REQUIRE(k >= 1 && k <= n, "k must be in [1, n], got k=%lld n=%lld", (long long)k, (long long)n);
+  if (n > kSmallN && k < n) {
+    CHOCO_REQUIRE(aligned16(x) && (xh == nullptr || aligned16(xh)),
+                  "x/xhat must be 16-byte aligned for n > %lld", (long long)kSmallN);
+  }
+  if (xh) return launch_topk<MODE, true>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st);
+  return launch_topk<MODE, false>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st);
+}
+
+}  // namespace choco
+
+using namespace choco;
+
+CHOCO_API int64_t choco_topk_k(int64_t n, double ratio) {
+  // identical IEEE-double expression to max(1, int(x_len * (1 - ratio)))
+  double v = (double)n * (1.0 - ratio);
+  int64_t k = (int64_t)v;  // int() truncates toward zero
+  return k < 1 ? 1 : k;
+}
+
+CHOCO_API size_t choco_topk_workspace_size(int64_t n) { return topk_ws_bytes(n); }
+CHOCO_API size_t choco_randk_workspace_size(int64_t n) { return topk_ws_bytes(n); }
+
+CHOCO_API int choco_topk_compress(const float* x, const float* xhat, int64_t n, int64_t k, float* out_val,
+                                  int32_t* out_idx, void* ws, size_t ws_bytes, void* stream) {
+  return dispatch_topk<kData>(x, xhat, n, k, 0, 1.0f, out_val, out_idx, 0, ws, ws_bytes, as_stream(stream));
+}
+
+CHOCO_API int choco_randk_compress(const float* x, const float* xhat, int64_t n, int64_t k, uint64_t seed,
+                                   int32_t is_biased, float* out_val, int32_t* out_idx, void* ws,
+                                   size_t ws_bytes, void* stream) {
+  const float scale = is_biased ? 1.0f : (float)((double)n / (double)k);
+  return dispatch_topk<kHash>(x, xhat, n, k, seed, scale, out_val, out_idx, 0, ws, ws_bytes,
+                              as_stream(stream));
+}
+
+CHOCO_API int64_t choco_topk_segmented_plan(const int64_t* seg_off_host, int32_t nseg, double ratio,
+                                            int64_t* plan_host) {
+  if (seg_off_host == nullptr || nseg <= 0) return (int64_t)fail(CHOCO_ERR_INVALID, "bad segment table");
+  int64_t out = 0;
+  for (int s = 0; s < nseg; ++s) {
+    const int64_t off = seg_off_host[s], len = seg_off_host[s + 1] - seg_off_host[s];
+    if (len <= 0) return (int64_t)fail(CHOCO_ERR_INVALID, "segment %d has length %lld", s, (long long)len);
+    const int64_t k = choco_topk_k(len, ratio);
+    if (plan_host) {
+      plan_host[4 * s + 0] = off;
+      plan_host[4 * s + 1] = len;
+      plan_host[4 * s + 2] = k;
+      plan_host[4 * s + 3] = out;
+    }
+    out += k;
+  }
+  return out;
+}
+
+CHOCO_API size_t choco_topk_segmented_workspace_size(const int64_t* plan_host, int32_t nseg) {
+  size_t need = 256;
+  for (int s = 0; s < nseg; ++s) {
+    const int64_t off = plan_host[4 * s], len = plan_host[4 * s + 1];
+    if (host_seg_uses_pipeline(off, len)) need = std::max(need, topk_ws_bytes(len));
+  }
+  return need;
+}
+
+CHOCO_API int choco_topk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
+                                            const int64_t* plan_host, int32_t nseg, float* out_val,
+                                            int32_t* out_idx, void* ws, size_t ws_bytes, void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(x && plan_dev && plan_host && out_val && out_idx && nseg > 0, "null pointer argument");
+  CHOCO_REQUIRE(aligned16(x) && (xhat == nullptr || aligned16(xhat)), "x/xhat must be 16-byte aligned");
+  const int64_t ntot = plan_host[4 * (nseg - 1)] + plan_host[4 * (nseg - 1) + 1];
+  CHOCO_REQUIRE(ntot < (int64_t)INT32_MAX, "total length must be < 2^31");
+  // every segment that is not pipelined: one workgroup each, one launch
+  if (xhat)
+    hipLaunchKernelGGL((topk_segmented_kernel<true>), dim3(nseg), dim3(kExactThreads), 0, st, x, xhat,
+                       plan_dev, nseg, out_val, out_idx);
+  else
+    hipLaunchKernelGGL((topk_segmented_kernel<false>), dim3(nseg), dim3(kExactThreads), 0, st, x, xhat,
+                       plan_dev, nseg, out_val, out_idx);
+  CHOCO_LAUNCHED("topk_segmented_kernel");
+  for (int s = 0; s < nseg; ++s) {
+    const int64_t off = plan_host[4 * s], len = plan_host[4 * s + 1], k = plan_host[4 * s + 2],
+                  oo = plan_host[4 * s + 3];
+    if (!host_seg_uses_pipeline(off, len)) continue;
+    int rc = dispatch_topk<kData>(x + off, xhat ? xhat + off : nullptr, len, k, 0, 1.0f, out_val + oo,
+                                  out_idx + oo, off, ws, ws_bytes, st);
+    if (rc) return rc;
+  }
+  return CHOCO_OK;
+}

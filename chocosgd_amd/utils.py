@@ -1,0 +1,28 @@
+"""Gossip-step helpers: drop-in for the CHOCO half of dl_code/pcode/optim/utils.py."""
+from . import codec
+from .tensor_buffer import TensorBuffer
+
+
+def _get_data(param_groups, idx, is_get_grad):
+    if is_get_grad:
+        return param_groups[idx]["params"][0].grad
+    return param_groups[idx]["params"][0]
+
+
+def recover_params(param_groups, param_names, rank=None, neighbor_hat_params=None, get_hat_params=True):
+    """optim/utils.py:50-64: flat copies of the params (and of x_hat_i)."""
+    params = [_get_data(param_groups, idx, False) for idx, _ in param_names]
+    params = [p for p in params if p is not None]
+    flatten_params = TensorBuffer(params)
+    if get_hat_params:
+        assert neighbor_hat_params is not None and rank is not None
+        flatten_hat_params = TensorBuffer(params)
+        flatten_hat_params.buffer.data[:] = neighbor_hat_params[rank].buffer
+        return params, flatten_params, flatten_hat_params
+    return params, flatten_params
+
+
+def update_params_from_neighbor(neighbor_hat_params, flatten_params, consensus_stepsize, self_rank):
+    """optim/utils.py:67-72:  x += gamma * (memory - x_hat_i), one fused HIP pass."""
+    codec.gossip_step(flatten_params.buffer, neighbor_hat_params["memory"].buffer,
+                      neighbor_hat_params[self_rank].buffer, consensus_stepsize)

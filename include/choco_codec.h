@@ -1,0 +1,198 @@
+/*
+ * choco_codec.h -- C ABI of the MI355X (gfx950) CHOCO compressor codec.
+ *
+ * This is the drop-in boundary for ChocoSGD's compressor operator path
+ * (reference: epfml/ChocoSGD, dl_code/pcode).  Each entry point names the
+ * reference interface it replaces (file:line relative to the reference's
+ * dl_code/ directory).  All pointers are DEVICE pointers owned by the caller
+ * unless documented as host arrays; all work is enqueued on `stream`
+ * (a hipStream_t passed as void*), nothing allocates, nothing synchronises.
+ *
+ * Return value of every function: CHOCO_OK (0) or a negative CHOCO_ERR_*;
+ * choco_last_error() returns the per-thread message of the last failure.
+ *
+ * Element/index conventions:
+ *   - n counts fp32 elements; every n must be < 2^31 (indices are int32 on the
+ *     wire; the reference sends fp32 indices and is inexact above 2^24,
+ *     pcode/utils/communication.py:69-72 + pcode/utils/sparsification.py:76).
+ *   - "delta" inputs: if xhat != NULL the op works on d = x - xhat computed in
+ *     fp32 (pcode/optim/parallel_choco_v.py:236,382,482), else on d = x.
+ *   - segment tables `seg_off` are int64[nseg+1], seg_off[0] = 0,
+ *     seg_off[nseg] = n (the per-tensor layout of create_optimizer.py:15-24).
+ */
+#ifndef CHOCO_CODEC_H_
+#define CHOCO_CODEC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CHOCO_OK 0
+#define CHOCO_ERR_INVALID (-1)   /* bad argument / shape / alignment          */
+#define CHOCO_ERR_HIP (-2)       /* HIP runtime error                          */
+#define CHOCO_ERR_WORKSPACE (-3) /* workspace too small                        */
+
+/* ---------------------------------------------------------------- library */
+int choco_version(void);                          /* ABI version, currently 1 */
+int choco_last_error(char* buf, size_t len);      /* copies message, returns its length */
+
+/* k = max(1, int(n * (1 - ratio))) evaluated in IEEE double exactly as
+ * SparsificationCompressor.get_top_k / get_random_k do
+ * (pcode/utils/sparsification.py:22,45). */
+int64_t choco_topk_k(int64_t n, double ratio);
+
+/* --------------------------------------------------------------- top-k
+ * Replaces SparsificationCompressor.get_top_k (pcode/utils/sparsification.py:18-31)
+ * and the per-tensor loop of CHOCOSparsificationCompressor.compress
+ * (pcode/optim/parallel_choco_v.py:229-260).
+ * Output: exactly k (value, index) pairs of the largest |d|, SIGNED values,
+ * in ascending index order.  Ties at the k-th magnitude are broken towards the
+ * lowest index (the reference's k==1 path, torch.max, does the same; its
+ * torch.topk order is implementation-defined). */
+size_t choco_topk_workspace_size(int64_t n);
+int choco_topk_compress(const float* x, const float* xhat, int64_t n, int64_t k,
+                        float* out_val, int32_t* out_idx,
+                        void* ws, size_t ws_bytes, void* stream);
+
+/* Per-segment top-k (one tensor per segment, as the reference loops over
+ * parameter tensors): k_s = choco_topk_k(len_s, ratio), outputs concatenated in
+ * segment order, indices GLOBAL (segment offset added in integer arithmetic --
+ * the reference adds it in fp32, sparsification.py:76).
+ * choco_topk_segmented_plan fills a HOST plan of nseg rows {off, len, k_s, out_off}
+ * (int64 x 4) from the HOST table seg_off[nseg+1] and returns K = sum k_s (the
+ * reference's selected_shapes are the k_s, parallel_choco_v.py:245).  The caller
+ * keeps a DEVICE copy of the plan (plan_dev) and passes both on every call. */
+int64_t choco_topk_segmented_plan(const int64_t* seg_off_host, int32_t nseg, double ratio,
+                                  int64_t* plan_host);
+size_t choco_topk_segmented_workspace_size(const int64_t* plan_host, int32_t nseg);
+int choco_topk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
+                                  const int64_t* plan_host, int32_t nseg,
+                                  float* out_val, int32_t* out_idx,
+                                  void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------- random-k
+ * Replaces SparsificationCompressor.get_random_k (sparsification.py:40-54).
+ * The reference draws indices on the host with numpy's legacy RandomState;
+ * here k distinct indices are drawn on the device, uniformly without
+ * replacement, as the k highest values of a seeded bijective 32-bit hash of
+ * the index (ties -> lowest index).  Output in ascending index order.
+ * is_biased = 0 scales values by (float)(n / k) like the reference's
+ * unbiased branch (sparsification.py:54). */
+size_t choco_randk_workspace_size(int64_t n);
+int choco_randk_compress(const float* x, const float* xhat, int64_t n, int64_t k,
+                         uint64_t seed, int32_t is_biased,
+                         float* out_val, int32_t* out_idx,
+                         void* ws, size_t ws_bytes, void* stream);
+
+/* Gather at caller-given int64 indices (the reference's x_data[selected_indices],
+ * sparsification.py:31,52); scale = 1 for the biased path, (float)(n/k) otherwise. */
+int choco_gather(const float* x, const float* xhat, const int64_t* idx, int64_t k,
+                 float scale, float* out_val, void* stream);
+
+/* Receiver side of CHOCOSparsificationCompressor.uncompress
+ * (parallel_choco_v.py:307-310): for one message (val, idx) of k pairs,
+ *   if xhat_self != NULL:  xhat_self[idx] += val
+ *   memory[idx] += (float)weight * val        (two roundings, as torch does)
+ * Indices within one message must be unique (true for top-k / random-k). */
+int choco_sparse_accumulate(const float* val, const int32_t* idx, int64_t k,
+                            float* xhat_self, float* memory, float weight, void* stream);
+
+/* --------------------------------------------------------------- sign
+ * Replaces SignCompressor.packing (sparsification.py:129-145, incl. the external
+ * bit2byte.packing) and the per-tensor L1 norms of CHOCOSignCompressor.compress
+ * (parallel_choco_v.py:476-499).  Layout = the reference's (32, N') view of the
+ * zero-padded flat buffer, N' = ceil(n/32): word j holds elements j + r*N',
+ * r = 0..31, element r at bit r (LSB first: this repo's documented convention,
+ * the unvendored bit2byte's bit order is unpinned); bit set <=> d < 0
+ * (sign(0), -0.0, NaN and padding encode as "+").
+ * l1_norms (nullable) receives per-segment sum|d| accumulated in fp64 and
+ * rounded once to fp32.  seg_off is a DEVICE int64[nseg+1] (may be NULL when
+ * nseg == 1).  Workspace: choco_sign_workspace_size(nseg). */
+int64_t choco_sign_words(int64_t n);
+size_t choco_sign_workspace_size(int32_t nseg);
+int choco_sign_compress(const float* x, const float* xhat, int64_t n,
+                        const int64_t* seg_off, int32_t nseg,
+                        int32_t* packed, float* l1_norms,
+                        void* ws, size_t ws_bytes, void* stream);
+
+/* SignCompressor.unpacking (sparsification.py:147-163): +1.0 / -1.0 floats. */
+int choco_sign_unpack(const int32_t* packed, int64_t n, float* out, void* stream);
+
+/* Receiver side of CHOCOSignCompressor.uncompress (parallel_choco_v.py:524-558),
+ * fused over all messages in the given order (the reference's neighbors_info
+ * order).  For message m with per-segment norms norms[m][s] and packed signs:
+ *   upd = (norms[m][s] / (float)numel_s) * sign
+ *   if m == self_slot:  xhat_self += upd
+ *   memory = fmaf((float)weights[m], upd, memory)     (torch add_(.., alpha=w))
+ * packed_list/norms_list/weights are HOST arrays of length nmsg (<= 8) holding
+ * device pointers / weights.  self_slot = -1 when no message is the local one. */
+int choco_sign_decompress_accumulate(const int32_t* const* packed_list,
+                                     const float* const* norms_list,
+                                     const float* weights, int32_t nmsg, int32_t self_slot,
+                                     int64_t n, const int64_t* seg_off, int32_t nseg,
+                                     float* xhat_self, float* memory,
+                                     void* ws, size_t ws_bytes, void* stream);
+
+/* --------------------------------------------------------------- QSGD
+ * Replaces QuantizationCompressor.get_qsgd/compress (sparsification.py:87-98,114-120)
+ * applied per segment (parallel_choco_v.py:375-397).  s = 2^q - 1 levels.
+ *   norm_s  = ||d_s||_2 (fp64 accumulation, rounded once)   or norm_in[s] if given
+ *   lf      = ((float)s * |d|) / norm_s
+ *   level   = floor(lf) + (u < lf - floor(lf)),  u = u_in[e] if given, else
+ *             Philox4x32-10(seed, counter = offset + e)
+ * Wire format (packed, choco_qsgd_packed_bytes): level plane (container of
+ * cw = 1,2,4,8,16 bits >= q, little-endian within 32-bit words) followed by a
+ * sign plane (1 bit/element, bit set <=> d < 0), both padded to 16 bytes.
+ * dense_out (nullable) receives the reference's decoded floats
+ *   ((scale * sign(d)) * norm_s) * level / (float)s
+ * bit-for-bit; norms_out (nullable) the per-segment fp32 norms. q in [1,16]. */
+int64_t choco_qsgd_packed_bytes(int64_t n, int32_t q);
+size_t choco_qsgd_workspace_size(int32_t nseg);
+int choco_qsgd_compress(const float* x, const float* xhat, int64_t n,
+                        const int64_t* seg_off, int32_t nseg,
+                        int32_t q, int32_t is_biased,
+                        const float* norm_in, const float* u_in,
+                        uint64_t seed, uint64_t offset,
+                        uint8_t* packed, float* norms_out, float* dense_out,
+                        void* ws, size_t ws_bytes, void* stream);
+
+/* Decode a packed message to the reference's dense floats (the value that
+ * QuantizationCompressor.uncompress, sparsification.py:122-123, passes on). */
+int choco_qsgd_decode(const uint8_t* packed, const float* norms, int64_t n,
+                      const int64_t* seg_off, int32_t nseg, int32_t q, int32_t is_biased,
+                      float* out, void* stream);
+
+/* Receiver side of CHOCOQuantizationCompressor.uncompress (parallel_choco_v.py:415-433)
+ * fused over messages:  v = decode(m);  if m == self_slot: xhat_self += v;
+ * memory += (float)weights[m] * v   (two roundings). */
+int choco_qsgd_decompress_accumulate(const uint8_t* const* packed_list,
+                                     const float* const* norms_list,
+                                     const float* weights, int32_t nmsg, int32_t self_slot,
+                                     int64_t n, const int64_t* seg_off, int32_t nseg,
+                                     int32_t q, int32_t is_biased,
+                                     float* xhat_self, float* memory, void* stream);
+
+/* ------------------------------------------------------- gossip step
+ * update_params_from_neighbor (pcode/optim/utils.py:67-72):
+ *   x += (float)gamma * (memory - xhat)   (three roundings, as torch does). */
+int choco_gossip_step(float* x, const float* memory, const float* xhat, float gamma,
+                      int64_t n, void* stream);
+
+/* ------------------------------------------------------- profiling hooks
+ * Optional: when enabled, the library records hipEvents around the dominant
+ * kernel of each op on the op's own stream (the bench's roofline source). */
+int choco_profile_enable(int32_t on);
+/* Accumulated (sum of ms, count) of the named kernel since the last reset,
+ * after synchronising its events.  Names: "topk_stream", "sign_pack",
+ * "qsgd_quantize", "sparse_accumulate", ... */
+int choco_profile_read(const char* name, double* total_ms, int64_t* count);
+int choco_profile_reset(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CHOCO_CODEC_H_ */

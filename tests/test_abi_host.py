@@ -1,0 +1,138 @@
+"""C-ABI surface and host-side logic (no GPU needed: only host-only entry points are called)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, golden, golden_json
+from oracle import choco_oracle as O
+
+HEADER = os.path.join(ROOT, "include", "choco_codec.h")
+
+
+def _header_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|size_t)\s+(choco_[a-z0-9_]+)\s*\(", src, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from chocosgd_amd import _lib
+    return _lib.load()
+
+
+def test_library_exports_every_header_symbol(lib):
+    from chocosgd_amd import _lib
+    syms = _header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_lib.SIGNATURES), "ctypes table and header disagree"
+    assert lib.choco_version() == 1
+
+
+def test_exported_symbols_are_exactly_the_abi():
+    import subprocess
+    so = os.path.join(ROOT, "chocosgd_amd", "lib", "libchoco_codec.so")
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True).stdout
+    exported = sorted(l.split()[-1] for l in out.splitlines() if " T " in l and l.split()[-1].startswith("choco_"))
+    assert exported == _header_symbols()
+
+
+def test_topk_k_rule_matches_reference_table(lib):
+    for n, ratio, k in golden_json("k_table.json"):
+        assert lib.choco_topk_k(n, ratio) == k, (n, ratio)
+
+
+def test_sizes_and_formats(lib):
+    for n in [1, 31, 32, 33, 1_000_000, 345_000_000]:
+        assert lib.choco_sign_words(n) == O.sign_words(n)
+    for n in [1, 7, 8, 100003, 100_000_000]:
+        for q in [1, 2, 3, 4, 5, 8, 9, 16]:
+            cw = O.container_bits(q)
+            assert lib.choco_qsgd_packed_bytes(n, q) == O.plane_bytes(n, cw) + O.plane_bytes(n, 1)
+    assert lib.choco_qsgd_packed_bytes(10, 32) == 0
+    assert lib.choco_topk_workspace_size(100_000_000) > 8 * 100_000_000
+    assert lib.choco_topk_workspace_size(1000) >= 256
+    assert lib.choco_sign_workspace_size(161) >= 256 + 161 * 8
+
+
+def test_segmented_plan(lib):
+    from chocosgd_amd import _lib
+    lens = golden_json("layouts.json")["resnet50_imagenet"]
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    p_off, keep = _lib.i64_array(offs.tolist())
+    plan = (ctypes.c_int64 * (4 * len(lens)))()
+    total = lib.choco_topk_segmented_plan(p_off, len(lens), 0.99,
+                                          ctypes.cast(plan, ctypes.POINTER(ctypes.c_int64)))
+    rows = np.array(list(plan)).reshape(-1, 4)
+    ks = [O.topk_k(m, 0.99) for m in lens]
+    assert total == sum(ks)
+    assert rows[:, 0].tolist() == offs[:-1].tolist()
+    assert rows[:, 1].tolist() == lens
+    assert rows[:, 2].tolist() == ks
+    assert rows[:, 3].tolist() == np.concatenate([[0], np.cumsum(ks)[:-1]]).tolist()
+
+
+def test_error_reporting(lib):
+    from chocosgd_amd import _lib
+    rc = lib.choco_topk_compress(None, None, 10, 1, None, None, None, 0, None)
+    assert rc == -1
+    assert "null" in _lib.last_error()
+    with pytest.raises(RuntimeError):
+        _lib.check(rc, "choco_topk_compress")
+
+
+def test_cpu_tensors_are_rejected_loudly():
+    from chocosgd_amd import codec, sparsification
+    x = torch.randn(100)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        codec.topk(x, 5)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        sparsification.SparsificationCompressor().get_top_k(x, 0.9)
+    with pytest.raises(RuntimeError):
+        sparsification.SignCompressor().packing(x)
+
+
+def test_uncompress_exact_integer_offsets():
+    """SparsificationCompressor.uncompress: global index = local + segment start, in int64
+    (the reference adds in fp32 and is wrong above 2^24, sparsification.py:76)."""
+    from chocosgd_amd.sparsification import SparsificationCompressor
+    c = SparsificationCompressor()
+    big = 2 ** 24 + 5
+    shapes = [(torch.Size([big]), big), (torch.Size([10]), 10)]
+    values = torch.tensor([1.0, 2.0, 3.0])
+    local = torch.tensor([big - 1, 3, 9], dtype=torch.int64)
+    v, idx = c.uncompress(values, local, [1, 2], shapes)
+    assert idx.tolist() == [big - 1, big + 3, big + 9]
+    assert torch.equal(v, values)
+
+
+def test_tensor_buffer_keeps_dtype():
+    from chocosgd_amd.tensor_buffer import TensorBuffer
+    ints = [torch.tensor([16777217, 3], dtype=torch.int64), torch.tensor([5], dtype=torch.int64)]
+    tb = TensorBuffer(ints)
+    assert tb.buffer.dtype == torch.int64 and tb.buffer.tolist() == [16777217, 3, 5]
+    assert tb[1].tolist() == [5] and len(tb) == 2
+    flat = torch.arange(6, dtype=torch.float32)
+    tb2 = TensorBuffer.from_flat(flat, [(2, 2), (2,)])
+    assert tb2[0].shape == (2, 2) and tb2[1].tolist() == [4.0, 5.0]
+
+
+def test_neighborhood_matches_reference_topologies():
+    from chocosgd_amd.communication import neighborhood
+    assert neighborhood(0, 1) == {0: 1.0}
+    assert neighborhood(1, 2) == {0: 0.5, 1: 0.5}
+    assert neighborhood(0, 8) == {0: 1 / 3, 1: 1 / 3, 7: 1 / 3}
+    assert list(neighborhood(1, 3).keys()) == [0, 1, 2]
+    g = golden("choco_topk_mini_r09")
+    assert list(neighborhood(1, 3).values()) == g["weights"].tolist()
+
+
+def test_get_n_bits():
+    from chocosgd_amd.sparsification import get_n_bits
+    assert get_n_bits(torch.zeros(10, dtype=torch.float32)) == 320
+    assert get_n_bits(torch.zeros(10, dtype=torch.int32)) == 320

@@ -1,0 +1,212 @@
+"""GPU parity: QSGD, sign(+norm), gossip step through the C ABI vs the oracle and the
+reference's golden vectors.  Run on an MI355X with `pytest -m gpu`."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, golden_json, same_bits
+from oracle import choco_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def randn(n, seed, scale=1.0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return torch.randn(n, generator=g, device=DEV) * scale
+
+
+def seg_table(lens):
+    return dev(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)) if len(lens) > 1 else None
+
+
+# ------------------------------------------------------------------------------------ QSGD
+QCASES = [("qsgd_n32771_q4", 4, False), ("qsgd_n32771_q4_biased", 4, True), ("qsgd_n4099_q2", 2, False),
+          ("qsgd_n4099_q8", 8, False), ("qsgd_n257_q4_small", 4, False)]
+
+
+@pytest.mark.parametrize("name,q,biased", QCASES)
+def test_qsgd_golden_pinned(name, q, biased):
+    """Given the reference's uniforms and norm: dense output bit-exact, wire bit-exact vs
+    the oracle packer, decode(wire) == reference output."""
+    from chocosgd_amd import codec
+    g = golden(name)
+    x = dev(g["x"])
+    norm = dev(np.array([g["norm_ref"]], dtype=np.float32))
+    packed, norms, dense = codec.qsgd_compress(x, q, is_biased=biased, norm_in=norm, u_in=dev(g["u"]),
+                                               want_dense=True)
+    assert same_bits(host(dense), g["out"])
+    s = 2 ** q - 1
+    lvl = O.qsgd_levels(g["x"], s, g["u"], g["norm_ref"])
+    assert np.array_equal(host(packed), O.qsgd_pack(lvl, g["x"], q))
+    dec = codec.qsgd_decode(packed, norm, x.numel(), q, is_biased=biased)
+    assert same_bits(host(dec), g["out"])
+
+
+@pytest.mark.parametrize("n", [257, 100003, 4_000_001, 100_000_000])
+def test_qsgd_device_norm_vs_fp64(n):
+    from chocosgd_amd import codec
+    x = randn(n, 7)
+    _, norms, _ = codec.qsgd_compress(x, 4, seed=1)
+    exact = float(np.sqrt(np.sum(host(x).astype(np.float64) ** 2)))
+    assert abs(float(host(norms)[0]) - exact) <= 1e-6 * exact
+
+
+@pytest.mark.parametrize("q", [1, 2, 3, 4, 8, 16])
+@pytest.mark.parametrize("n", [1000, 262147])
+def test_qsgd_philox_mode_matches_oracle(q, n):
+    from chocosgd_amd import codec
+    x = randn(n, 100 + q)
+    seed, offset = 0x1234_5678_9ABC, 77
+    packed, norms, dense = codec.qsgd_compress(x, q, seed=seed, offset=offset, want_dense=True)
+    u = O.philox_uniforms(n, seed, offset)
+    s = 2 ** q - 1
+    nrm = host(norms)[0]
+    assert same_bits(host(dense), O.qsgd_dense(host(x), s, u, nrm))
+    assert np.array_equal(host(packed), O.qsgd_pack(O.qsgd_levels(host(x), s, u, nrm), host(x), q))
+
+
+def test_qsgd_zero_segment_nan():
+    from chocosgd_amd import codec
+    x = torch.zeros(64, device=DEV)
+    packed, norms, dense = codec.qsgd_compress(x, 4, seed=3, want_dense=True)
+    assert host(norms)[0] == 0 and np.all(np.isnan(host(dense)))
+    assert np.all(np.isnan(host(codec.qsgd_decode(packed, norms, 64, 4))))
+
+
+def test_choco_qsgd_round_trip_golden():
+    """Per-tensor QSGD of 3 workers (reference uniforms + norms pinned) -> fused accumulate."""
+    from chocosgd_amd import codec
+    g = golden("choco_qsgd_mini_q4")
+    lens = g["layout"].tolist()
+    so = seg_table(lens)
+    msgs = []
+    for r in range(3):
+        packed, _, dense = codec.qsgd_compress(dev(g["x"][r]), 4, xhat=dev(g["xhat"][r]), seg_off=so,
+                                               nseg=len(lens), norm_in=dev(g["norms_ref"][r]),
+                                               u_in=dev(g["u"][r]), want_dense=True)
+        assert same_bits(host(dense), g[f"msg{r}"])
+        msgs.append((packed, dev(g["norms_ref"][r])))
+    hat, mem = dev(g["hat0"]), dev(g["mem0"])
+    codec.qsgd_accumulate(msgs, g["weights"].tolist(), int(g["self_rank"]), sum(lens), 4, mem, xhat_self=hat,
+                          seg_off=so, nseg=len(lens))
+    assert same_bits(host(hat), g["hat1"])
+    assert same_bits(host(mem), g["mem1"])
+
+
+@pytest.mark.parametrize("layout", ["resnet20_cifar10", "resnet50_imagenet"])
+def test_qsgd_segmented_layout_norms_and_levels(layout):
+    from chocosgd_amd import codec
+    lens = golden_json("layouts.json")[layout]
+    n = sum(lens)
+    x, xh = randn(n, 21), randn(n, 22, 0.3)
+    so = seg_table(lens)
+    packed, norms, dense = codec.qsgd_compress(x, 4, xhat=xh, seg_off=so, nseg=len(lens), seed=9, offset=1,
+                                               want_dense=True)
+    d = host(x) - host(xh)
+    ref = O.l2_norms(d, lens)
+    assert np.allclose(host(norms), ref, rtol=1e-6, atol=0)
+    u = O.philox_uniforms(n, 9, 1)
+    off, outs = 0, []
+    for s, m in enumerate(lens):
+        outs.append(O.qsgd_dense(d[off:off + m], 15, u[off:off + m], host(norms)[s]))
+        off += m
+    assert same_bits(host(dense), np.concatenate(outs))
+    dec = codec.qsgd_decode(packed, norms, n, 4, seg_off=so, nseg=len(lens))
+    assert same_bits(host(dec), host(dense))
+
+
+# ------------------------------------------------------------------------------------ sign
+@pytest.mark.parametrize("name", ["sign_n4096", "sign_n40003_pad", "sign_n31"])
+def test_sign_golden(name):
+    from chocosgd_amd import codec
+    g = golden(name)
+    packed, _ = codec.sign_compress(dev(g["x"]), want_norms=False)
+    assert np.array_equal(host(packed), g["packed"])
+    out = codec.sign_unpack(packed, g["x"].size)
+    assert same_bits(host(out), g["decoded"])
+
+
+@pytest.mark.parametrize("n", [1, 5, 32, 33, 127, 1000, 4096 * 32 + 3, 1_000_000, 1_000_007, 10_781_250 * 4 + 1])
+def test_sign_random_sizes(n):
+    from chocosgd_amd import codec
+    x = randn(n, n % 1009)
+    xh = randn(n, 5, 0.5)
+    packed, norms = codec.sign_compress(x, xhat=xh)
+    d = host(x) - host(xh)
+    assert np.array_equal(host(packed), O.sign_pack(d))
+    assert host(norms)[0] == O.l1_norms(d, [n])[0] or np.isclose(host(norms)[0], O.l1_norms(d, [n])[0],
+                                                                  rtol=1e-7)
+    assert same_bits(host(codec.sign_unpack(packed, n)), O.sign_unpack(O.sign_pack(d), n))
+
+
+@pytest.mark.parametrize("layout", ["resnet20_cifar10", "resnet50_imagenet", "tiny_segments"])
+def test_sign_segmented_norms(layout):
+    from chocosgd_amd import codec
+    if layout == "tiny_segments":
+        rng = np.random.default_rng(0)
+        lens = rng.integers(1, 40, size=3000).tolist()
+    else:
+        lens = golden_json("layouts.json")[layout]
+    n = sum(lens)
+    x = randn(n, 31)
+    packed, norms = codec.sign_compress(x, seg_off=seg_table(lens), nseg=len(lens))
+    assert np.array_equal(host(packed), O.sign_pack(host(x)))
+    assert np.allclose(host(norms), O.l1_norms(host(x), lens), rtol=1e-7, atol=0)
+
+
+def test_choco_sign_round_trip_golden():
+    from chocosgd_amd import codec
+    g = golden("choco_sign_mini")
+    lens = g["layout"].tolist()
+    so = seg_table(lens)
+    msgs = []
+    for r in range(3):
+        packed, norms = codec.sign_compress(dev(g["x"][r]), xhat=dev(g["xhat"][r]), seg_off=so, nseg=len(lens))
+        assert np.array_equal(host(packed), g[f"signs{r}"])
+        assert np.allclose(host(norms), g[f"norms{r}"], rtol=1e-5, atol=0)
+        msgs.append((dev(g[f"signs{r}"]), dev(g[f"norms{r}"])))  # reference norms pinned
+    hat, mem = dev(g["hat0"]), dev(g["mem0"])
+    codec.sign_accumulate(msgs, g["weights"].tolist(), int(g["self_rank"]), sum(lens), mem, xhat_self=hat,
+                          seg_off=so, nseg=len(lens))
+    assert same_bits(host(hat), g["hat1"])
+    assert same_bits(host(mem), g["mem1"])
+
+
+@pytest.mark.parametrize("n,nseg", [(1_000_003, 1), (2_000_000, 7), (65, 3)])
+def test_sign_accumulate_vs_oracle(n, nseg):
+    from chocosgd_amd import codec
+    rng = np.random.default_rng(n)
+    cuts = np.sort(rng.choice(np.arange(1, n), size=nseg - 1, replace=False)) if nseg > 1 else np.array([])
+    lens = np.diff(np.concatenate([[0], cuts, [n]])).astype(np.int64).tolist()
+    so = seg_table(lens)
+    msgs_d, msgs_h = [], []
+    for r in range(3):
+        x = randn(n, 50 + r)
+        packed, norms = codec.sign_compress(x, seg_off=so, nseg=len(lens))
+        msgs_d.append((packed, norms))
+        msgs_h.append((host(packed), host(norms)))
+    hat, mem = randn(n, 60), randn(n, 61)
+    h0, m0 = host(hat), host(mem)
+    w = [1 / 3, 1 / 3, 1 / 3]
+    codec.sign_accumulate(msgs_d, w, 1, n, mem, xhat_self=hat, seg_off=so, nseg=len(lens))
+    O.sign_accumulate(h0, m0, msgs_h, w, 1, lens)
+    assert same_bits(host(hat), h0)
+    assert same_bits(host(mem), m0)
+
+
+# ------------------------------------------------------------------------------------ gossip
+def test_gossip_golden():
+    from chocosgd_amd import codec
+    g = golden("gossip_n10007")
+    x = dev(g["x"])
+    codec.gossip_step(x, dev(g["mem"]), dev(g["hat"]), float(g["gamma"]))
+    assert same_bits(host(x), g["out"])

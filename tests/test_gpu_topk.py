@@ -1,0 +1,166 @@
+"""GPU parity: top-k / random-k / sparse accumulate through the C ABI vs the oracle
+and the reference's golden vectors.  Run on an MI355X with `pytest -m gpu`."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, golden_json, same_bits
+from oracle import choco_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def randn(n, seed, scale=1.0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return torch.randn(n, generator=g, device=DEV) * scale
+
+
+TOPK_CASES = ["topk_n1000_r09", "topk_n65536_r099", "topk_n262144_r099", "topk_n30011_r09", "topk_n50_k1",
+              "topk_k1_tie", "topk_ties_n4096_r09"]
+
+
+@pytest.mark.parametrize("name", TOPK_CASES)
+def test_topk_golden(name):
+    from chocosgd_amd import codec
+    g = golden(name)
+    k = int(g["k"])
+    x = dev(g["x"])
+    xh = dev(g["xhat"]) if "xhat" in g else None
+    vals, idx = codec.topk(x, k, xhat=xh)
+    torch.cuda.synchronize()
+    d = (g["x"] - g["xhat"]).astype(np.float32) if "xhat" in g else g["x"]
+    ov, oi = O.topk(d, k)
+    assert np.array_equal(host(idx).astype(np.int64), oi)
+    assert same_bits(host(vals), ov)
+    if "ties" not in name:
+        assert np.array_equal(np.sort(g["indices"]), oi)  # the reference's own set
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 100, 4097, 65536, 65537, 100003, 1 << 20, 3_000_001, 25_000_000])
+@pytest.mark.parametrize("ratio", [0.99, 0.9, 0.5])
+def test_topk_random_sizes(n, ratio):
+    from chocosgd_amd import codec
+    x = randn(n, 1000 + n % 997)
+    k = codec.topk_k(n, ratio)
+    assert k == O.topk_k(n, ratio)
+    vals, idx = codec.topk(x, k)
+    ov, oi = O.topk(host(x), k)
+    assert np.array_equal(host(idx).astype(np.int64), oi)
+    assert same_bits(host(vals), ov)
+
+
+def test_topk_fused_delta():
+    from chocosgd_amd import codec
+    x, xh = randn(2_000_003, 5), randn(2_000_003, 6, 0.9)
+    k = codec.topk_k(x.numel(), 0.99)
+    v1, i1 = codec.topk(x, k, xhat=xh)
+    v2, i2 = codec.topk((x - xh).contiguous(), k)
+    assert torch.equal(i1, i2) and torch.equal(v1, v2)
+
+
+@pytest.mark.slow
+def test_topk_100M_bench_shape():
+    from chocosgd_amd import codec
+    n = 100_000_000
+    x = randn(n, 1000)
+    k = codec.topk_k(n, 0.99)
+    vals, idx = codec.topk(x, k)
+    ov, oi = O.topk(host(x), k)
+    assert np.array_equal(host(idx).astype(np.int64), oi)
+    assert same_bits(host(vals), ov)
+
+
+@pytest.mark.parametrize("kind", ["ties", "clustered", "zeros", "tiny_k", "k_equals_n", "nan"])
+def test_topk_fallback_and_edge_inputs(kind):
+    """Inputs that defeat the sampled threshold (heavy ties, values hidden between sample
+    chunks, all-zero tails) must still give the exact canonical answer."""
+    from chocosgd_amd import codec
+    n = 4_000_000
+    g = torch.Generator(device=DEV).manual_seed(77)
+    if kind == "ties":
+        x = torch.round(torch.randn(n, generator=g, device=DEV) * 4) / 4
+    elif kind == "clustered":
+        x = torch.zeros(n, device=DEV)
+        x[1_000_003:1_006_003] = torch.randn(6000, generator=g, device=DEV) + 10
+    elif kind == "zeros":
+        x = torch.zeros(n, device=DEV)
+        x[::1000] = 1.0
+    elif kind == "tiny_k":
+        x = torch.randn(n, generator=g, device=DEV)
+    elif kind == "k_equals_n":
+        x = torch.randn(100_000, generator=g, device=DEV)
+    else:
+        x = torch.randn(n, generator=g, device=DEV)
+        x[12345] = float("nan")
+    ratio = {"tiny_k": 0.999999, "k_equals_n": 0.0}.get(kind, 0.99)
+    k = codec.topk_k(x.numel(), ratio)
+    vals, idx = codec.topk(x.contiguous(), k)
+    ov, oi = O.topk(host(x), k)
+    assert np.array_equal(host(idx).astype(np.int64), oi)
+    assert same_bits(host(vals), ov)
+
+
+@pytest.mark.parametrize("layout", ["resnet20_cifar10", "resnet50_imagenet"])
+@pytest.mark.parametrize("ratio", [0.9, 0.99])
+def test_topk_segmented_model_layouts(layout, ratio):
+    from chocosgd_amd import codec
+    lens = golden_json("layouts.json")[layout]
+    n = sum(lens)
+    x, xh = randn(n, 11), randn(n, 12, 0.5)
+    plan = codec.SegmentPlan(lens, ratio, x.device)
+    vals, idx = codec.topk_segmented(x, plan, xhat=xh)
+    ov, oi, ks = O.topk_segmented(host(x) - host(xh), lens, ratio)
+    assert plan.k_per_seg == ks
+    assert np.array_equal(host(idx).astype(np.int64), oi)
+    assert same_bits(host(vals), ov)
+
+
+@pytest.mark.parametrize("n", [1000, 65536, 100003, 2_000_003])
+@pytest.mark.parametrize("seed", [1, 2 ** 40 + 3])
+def test_randk_matches_sampler_oracle(n, seed):
+    from chocosgd_amd import codec
+    x = randn(n, 3)
+    k = codec.topk_k(n, 0.95)
+    vals, idx = codec.randk(x, k, seed)
+    oi = O.randk_indices(n, k, seed)
+    assert np.array_equal(host(idx).astype(np.int64), oi)
+    assert same_bits(host(vals), host(x)[oi])
+    vu, iu = codec.randk(x, k, seed, is_biased=False)
+    assert torch.equal(iu, idx)
+    assert same_bits(host(vu), O.gather(host(x), oi, n, k, is_biased=False))
+
+
+def test_gather_golden():
+    from chocosgd_amd import codec
+    g = golden("randk_n20000_r095")
+    x = dev(g["x"])
+    n, k = g["x"].size, O.topk_k(g["x"].size, float(g["ratio"]))
+    out = codec.gather(x, dev(g["idx_biased"].astype(np.int64)))
+    assert same_bits(host(out), g["vals_biased"])
+    out = codec.gather(x, dev(g["idx_unbiased"].astype(np.int64)), scale=float(np.float32(n / k)))
+    assert same_bits(host(out), g["vals_unbiased"])
+
+
+@pytest.mark.parametrize("name,ratio", [("choco_topk_mini_r09", 0.9), ("choco_topk_mini_r099", 0.99)])
+def test_choco_topk_round_trip_golden(name, ratio):
+    """Per-tensor top-k of 3 workers -> accumulate into x_hat_1 / memory: bit-exact vs the reference."""
+    from chocosgd_amd import codec
+    g = golden(name)
+    lens = g["layout"].tolist()
+    self_rank = int(g["self_rank"])
+    hat, mem = dev(g["hat0"]), dev(g["mem0"])
+    plan = codec.SegmentPlan(lens, ratio, torch.device(DEV))
+    for r in range(3):
+        vals, idx = codec.topk_segmented(dev(g["x"][r]), plan, xhat=dev(g["xhat"][r]))
+        codec.sparse_accumulate(vals, idx, mem, float(g["weights"][r]), xhat_self=hat if r == self_rank else None)
+    assert same_bits(host(hat), g["hat1"])
+    assert same_bits(host(mem), g["mem1"])

@@ -1,0 +1,200 @@
+"""Pin the numpy oracle against golden vectors produced by the REFERENCE itself
+(tests/golden/gen_golden.py imports dl_code/pcode).  CPU only."""
+import numpy as np
+import pytest
+
+from conftest import golden, golden_json, same_bits
+from oracle import choco_oracle as O
+
+TOPK_CASES = ["topk_n1000_r09", "topk_n65536_r099", "topk_n262144_r099", "topk_n30011_r09", "topk_n50_k1",
+              "topk_k1_tie"]
+
+
+def _delta(g):
+    return g["x"] - g["xhat"] if "xhat" in g else g["x"]
+
+
+def test_k_rule_table():
+    for n, ratio, k in golden_json("k_table.json"):
+        assert O.topk_k(n, ratio) == k, (n, ratio)
+
+
+@pytest.mark.parametrize("name", TOPK_CASES)
+def test_topk_set_matches_reference(name):
+    g = golden(name)
+    d = _delta(g).astype(np.float32)
+    k = int(g["k"])
+    assert O.topk_k(d.size, float(g["ratio"])) == k
+    vals, idx = O.topk(d, k)
+    ref_idx = np.sort(g["indices"])
+    assert np.array_equal(idx, ref_idx)
+    order = np.argsort(g["indices"])
+    assert same_bits(vals, g["values"][order])
+
+
+def test_topk_k1_tie_first_index():
+    g = golden("topk_k1_tie")
+    _, idx = O.topk(g["x"], 1)
+    assert idx.tolist() == g["indices"].tolist() == [1]
+
+
+def test_topk_ties_multiset():
+    g = golden("topk_ties_n4096_r09")
+    d = g["x"]
+    k = int(g["k"])
+    vals, idx = O.topk(d, k)
+    assert np.array_equal(np.sort(np.abs(vals)), np.sort(np.abs(g["values"])))
+    thr = np.abs(vals).min()
+    assert np.all(np.abs(np.delete(d, idx)) <= thr)
+    # canonical tie rule: the lowest indices among |d| == thr are taken
+    eq = np.nonzero(np.abs(d) == thr)[0]
+    taken = np.intersect1d(idx, eq)
+    assert np.array_equal(taken, eq[:taken.size])
+
+
+def test_randk_gather_matches_reference():
+    g = golden("randk_n20000_r095")
+    x = g["x"]
+    n, k = x.size, O.topk_k(x.size, float(g["ratio"]))
+    assert same_bits(O.gather(x, g["idx_biased"]), g["vals_biased"])
+    assert same_bits(O.gather(x, g["idx_unbiased"], n, k, is_biased=False), g["vals_unbiased"])
+    assert len(np.unique(g["idx_biased"])) == k
+
+
+@pytest.mark.parametrize("name,q,biased", [("qsgd_n32771_q4", 4, False), ("qsgd_n32771_q4_biased", 4, True),
+                                           ("qsgd_n4099_q2", 2, False), ("qsgd_n4099_q8", 8, False),
+                                           ("qsgd_n257_q4_small", 4, False)])
+def test_qsgd_dense_matches_reference_with_pinned_norm(name, q, biased):
+    g = golden(name)
+    s = 2 ** q - 1
+    out = O.qsgd_dense(g["x"], s, g["u"], g["norm_ref"], is_biased=biased)
+    assert same_bits(out, g["out"])
+    # fp64-accumulated norm vs fp64 truth
+    nrm = O.l2_norms(g["x"], [g["x"].size])[0]
+    assert abs(float(nrm) - float(g["norm_f64"])) <= 1e-6 * float(g["norm_f64"])
+    # wire round trip decodes to the same floats
+    lvl = O.qsgd_levels(g["x"], s, g["u"], g["norm_ref"])
+    packed = O.qsgd_pack(lvl, g["x"], q)
+    levels, neg = O.qsgd_unpack(packed, g["x"].size, q)
+    dec = O.qsgd_decode(levels, neg, g["norm_ref"], s, g["x"].size, is_biased=biased)
+    assert same_bits(dec, g["out"])
+
+
+def test_qsgd_zero_tensor_is_nan_like_reference():
+    g = golden("qsgd_zeros")
+    out = O.qsgd_dense(g["x"], 15, g["u"], np.float32(0.0))
+    assert np.all(np.isnan(g["out"])) and np.all(np.isnan(out))
+    levels, neg = O.qsgd_unpack(O.qsgd_pack(O.qsgd_levels(g["x"], 15, g["u"], 0.0), g["x"], 4), 64, 4)
+    assert np.all(np.isnan(O.qsgd_decode(levels, neg, 0.0, 15, 64)))
+
+
+def test_qsgd_q32_passthrough():
+    g = golden("qsgd_q32_passthrough")
+    assert same_bits(g["x"], g["out"])
+
+
+@pytest.mark.parametrize("name", ["sign_n4096", "sign_n40003_pad", "sign_n31"])
+def test_sign_pack_unpack_matches_reference_wrapper(name):
+    g = golden(name)
+    packed = O.sign_pack(g["x"])
+    assert np.array_equal(packed, g["packed"])
+    assert same_bits(O.sign_unpack(packed, g["x"].size), g["decoded"])
+
+
+def _workers(g):
+    return [(g["x"][r] - g["xhat"][r]).astype(np.float32) for r in range(g["x"].shape[0])]
+
+
+@pytest.mark.parametrize("name,ratio", [("choco_topk_mini_r09", 0.9), ("choco_topk_mini_r099", 0.99)])
+def test_choco_topk_round_trip(name, ratio):
+    g = golden(name)
+    lens = g["layout"].tolist()
+    hat, mem = g["hat0"].copy(), g["mem0"].copy()
+    self_rank = int(g["self_rank"])
+    for r, d in enumerate(_workers(g)):
+        vals, idx, ks = O.topk_segmented(d, lens, ratio)
+        assert ks == g["selected_shapes"].tolist()
+        # the reference message: [values | local indices as fp32], per segment in topk order
+        msg = g[f"msg{r}"]
+        K = msg.size // 2
+        ref_local = msg[K:].astype(np.int64)
+        offs = np.repeat(np.cumsum([0] + lens[:-1]), ks)
+        ref_global = ref_local + offs
+        order = np.argsort(ref_global)
+        assert np.array_equal(idx, ref_global[order])
+        assert same_bits(vals, msg[:K][order])
+        O.sparse_accumulate(hat if r == self_rank else None, mem, vals, idx, g["weights"][r])
+    assert same_bits(hat, g["hat1"])
+    assert same_bits(mem, g["mem1"])
+    assert float(g["n_bits"]) == 64 * sum(ks)
+
+
+def test_choco_qsgd_round_trip():
+    g = golden("choco_qsgd_mini_q4")
+    lens = g["layout"].tolist()
+    s = 15
+    decoded = []
+    for r, d in enumerate(_workers(g)):
+        off, outs = 0, []
+        for si, m in enumerate(lens):
+            outs.append(O.qsgd_dense(d[off:off + m], s, g["u"][r][off:off + m], g["norms_ref"][r][si]))
+            off += m
+        dense = np.concatenate(outs)
+        assert same_bits(dense, g[f"msg{r}"])
+        decoded.append(dense)
+    hat, mem = g["hat0"].copy(), g["mem0"].copy()
+    O.qsgd_accumulate(hat, mem, decoded, g["weights"], int(g["self_rank"]))
+    assert same_bits(hat, g["hat1"])
+    assert same_bits(mem, g["mem1"])
+    assert float(g["n_bits"]) == 4 * sum(lens)
+
+
+def test_choco_sign_round_trip():
+    g = golden("choco_sign_mini")
+    lens = g["layout"].tolist()
+    msgs = []
+    for r, d in enumerate(_workers(g)):
+        ref_norms = g[f"norms{r}"]
+        ours = O.l1_norms(d, lens)
+        # the reference's fp32 CPU norm carries its own rounding drift (~6e-7 rel at 2304
+        # elements); the oracle is the fp64 sum rounded once
+        assert np.allclose(ours, ref_norms, rtol=1e-5, atol=0)
+        off = 0
+        for si, m in enumerate(lens):
+            exact = np.sum(np.abs(d[off:off + m].astype(np.float64)))
+            assert ours[si] == np.float32(exact)
+            off += m
+        assert np.array_equal(O.sign_pack(d), g[f"signs{r}"])
+        msgs.append((g[f"signs{r}"], ref_norms))
+    hat, mem = g["hat0"].copy(), g["mem0"].copy()
+    O.sign_accumulate(hat, mem, msgs, g["weights"], int(g["self_rank"]), lens)
+    assert same_bits(hat, g["hat1"])
+    assert same_bits(mem, g["mem1"])
+    assert float(g["n_bits"]) == 32 * len(lens) + 32 * O.sign_words(sum(lens))
+
+
+def test_gossip_step():
+    g = golden("gossip_n10007")
+    assert same_bits(O.gossip_step(g["x"], g["mem"], g["hat"], g["gamma"]), g["out"])
+    g2 = golden("choco_topk_mini_r09")
+    x = g2["x"][int(g2["self_rank"])]
+    assert same_bits(O.gossip_step(x, g2["mem1"], g2["hat1"], g2["gamma"]), g2["x_after_gossip"])
+
+
+def test_philox_known_answer():
+    # Random123 known-answer vector for philox4x32-10 (counter = key = 0)
+    r = O.philox4x32_10([0], [0], [0], [0], 0, 0)
+    assert [int(v[0]) for v in r] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    r = O.philox4x32_10([0xFFFFFFFF], [0xFFFFFFFF], [0xFFFFFFFF], [0xFFFFFFFF], 0xFFFFFFFF, 0xFFFFFFFF)
+    assert [int(v[0]) for v in r] == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+
+
+def test_randk_indices_distinct_and_uniformish():
+    n, k = 10000, 1000
+    counts = np.zeros(n)
+    for seed in range(40):
+        idx = O.randk_indices(n, k, seed)
+        assert idx.size == k and np.unique(idx).size == k
+        counts[idx] += 1
+    # each index selected ~ 40 * 0.1 = 4 times on average
+    assert 3.0 < counts.mean() < 5.0 and counts.max() < 20
