@@ -75,6 +75,7 @@ class Worker:
             nbytes = codec.qsgd_packed_bytes(self.n, self.param)
             self.msg = torch.empty(16 + nbytes, dtype=torch.uint8, device=dev)   # [norm (16 B) | planes]
         else:
+            self.k = None
             self.msg = torch.empty(4 + codec.sign_words(self.n), dtype=torch.int32, device=dev)
         self.recv = {r: torch.empty_like(self.msg) for r in self.peers}
         self.step_id = 0

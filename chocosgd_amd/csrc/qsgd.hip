@@ -217,6 +217,14 @@ __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
   const int64_t t_e1 = std::min<int64_t>(t_e0 + kQTile, n);
   const int sg0 = tile_seg(seg_off, nseg, t_e0, t_e1, s_seg);
   const bool uniform = s_seg[1] == sg0;
+  if (tile == ntiles - 1) {
+    // the wire is fully defined: zero the 16-byte padding tails of both planes
+    const int64_t groups = (n + kQPer - 1) / kQPer;
+    const int64_t lvl_used = groups * CW, lvl_end = (lvl_used + 15) / 16 * 16;
+    const int64_t sgn_used = groups, sgn_end = (sgn_used + 15) / 16 * 16;
+    for (int64_t b = lvl_used + threadIdx.x; b < lvl_end; b += kQThreads) lvl_plane[b] = 0;
+    for (int64_t b = sgn_used + threadIdx.x; b < sgn_end; b += kQThreads) sign_plane[b] = 0;
+  }
   const int64_t e0 = t_e0 + (int64_t)threadIdx.x * kQPer;
   if (e0 >= n) return;
   const float sf = (float)s_levels;
