@@ -92,20 +92,28 @@ __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __res
   const int sg0 = s_seg[0], sg1 = s_seg[1];
   if (sg0 == sg1) {
     double p = 0.0;
-    for (int64_t e = t0 + 4 * tid; e < t1; e += 4 * kQThreads) {
-      if (e + 3 < t1) {
-        float4 a = *reinterpret_cast<const float4*>(x + e);
-        if (XH) {
-          const float4 h = *reinterpret_cast<const float4*>(xh + e);
-          a.x -= h.x; a.y -= h.y; a.z -= h.z; a.w -= h.w;
-        }
-        p += (double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z + (double)a.w * a.w;
-      } else {
-        for (int c = 0; c < 4 && e + c < t1; ++c) {
-          const double v = dval(x, XH ? xh : nullptr, e + c);
-          p += v * v;
+    constexpr int U = 8;  // float4 loads in flight per thread
+    for (int64_t e0 = t0 + 4 * tid; e0 < t1; e0 += 4 * kQThreads * U) {
+      float4 a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t e = e0 + (int64_t)u * 4 * kQThreads;
+        if (e + 3 < t1) {
+          a[u] = *reinterpret_cast<const float4*>(x + e);
+          if (XH) {
+            const float4 h = *reinterpret_cast<const float4*>(xh + e);
+            a[u].x -= h.x; a[u].y -= h.y; a[u].z -= h.z; a[u].w -= h.w;
+          }
+        } else {
+          float t[4];
+          for (int c = 0; c < 4; ++c) t[c] = (e + c < t1) ? dval(x, XH ? xh : nullptr, e + c) : 0.f;
+          a[u] = make_float4(t[0], t[1], t[2], t[3]);
         }
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        p += (double)a[u].x * a[u].x + (double)a[u].y * a[u].y + (double)a[u].z * a[u].z +
+             (double)a[u].w * a[u].w;
     }
     p = wave_sum(p);
     if (lane == 0) s_red[w] = p;

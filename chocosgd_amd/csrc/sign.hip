@@ -112,16 +112,31 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
   __syncthreads();
 
   uint32_t wd[4] = {0u, 0u, 0u, 0u};
-  for (int r = 0; r < 32; ++r) {
+  constexpr int RU = 8;  // rows whose loads are in flight together
+  for (int r0 = 0; r0 < 32; r0 += RU) {
+  float vr[RU][4], tr[RU][4];
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int64_t s = (int64_t)(r0 + u) * Np + j0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) { vr[u][c] = 0.f; tr[u][c] = 0.f; }
+    if (ncol > 0 && s < n) {
+      const int64_t A = s & ~(int64_t)3;
+      load4g(x, XH ? xh : nullptr, A + 4 * lane, n, vr[u]);
+      if ((s & 3) != 0 && lane == 63) load4g(x, XH ? xh : nullptr, A + 256, n, tr[u]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int r = r0 + u;
     const int64_t s = (int64_t)r * Np + j0;
     double rowpart = 0.0;
     if (ncol > 0 && s < n) {  // wave-uniform
       const int64_t A = s & ~(int64_t)3;
       const int m = (int)(s & 3);
       const int64_t e = A + 4 * lane;
-      float v[4], t[4] = {0.f, 0.f, 0.f, 0.f};
-      load4g(x, XH ? xh : nullptr, e, n, v);
-      if (m != 0 && lane == 63) load4g(x, XH ? xh : nullptr, A + 256, n, t);
+      const float(&v)[4] = vr[u];
+      const float(&t)[4] = tr[u];
       const uint32_t b4 = neg_bits4(v);
       uint32_t nb4 = __shfl_down(b4, 1);
       if (lane == 63) nb4 = neg_bits4(t);
@@ -174,6 +189,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
       }
     }
     if (NORM && lane == 0) s_rows[w][r] = rowpart;
+  }
   }
   // packed words: 16-B stores where possible
   {
@@ -303,9 +319,26 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
       for (int c = 0; c < 4; ++c) wd[q][c] = (j + c < Np) ? M.packed[q][j + c] : 0u;
   }
   const bool has_self = M.self_slot >= 0 && hat != nullptr;
-  for (int r = 0; r < 32; ++r) {
+  constexpr int RU = 4;  // rows whose memory/x_hat loads are in flight together
+  for (int r0 = 0; r0 < 32; r0 += RU) {
+  float4 pm[RU], ph[RU];
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int64_t s = (int64_t)(r0 + u) * Np + j0;
+    const int64_t e = (s & ~(int64_t)3) + 4 * lane;
+    const int64_t lim = std::min<int64_t>(s + ncol, n);
+    pm[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    ph[u] = pm[u];
+    if (s < n && e >= s && e + 3 < lim) {
+      pm[u] = *reinterpret_cast<const float4*>(mem + e);
+      if (has_self) ph[u] = *reinterpret_cast<const float4*>(hat + e);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int r = r0 + u;
     const int64_t s = (int64_t)r * Np + j0;
-    if (s >= n) break;
+    if (s >= n) continue;
     const int64_t A = s & ~(int64_t)3;
     const int m = (int)(s & 3);
     const int64_t e = A + 4 * lane;
@@ -328,15 +361,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
     // main float4 of this lane
     {
       const bool full = e >= s && e + 3 < lim;
-      float hv[4] = {0.f, 0.f, 0.f, 0.f}, mv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (full) {
-        const float4 m4 = *reinterpret_cast<const float4*>(mem + e);
-        mv[0] = m4.x; mv[1] = m4.y; mv[2] = m4.z; mv[3] = m4.w;
-        if (has_self) {
-          const float4 h4 = *reinterpret_cast<const float4*>(hat + e);
-          hv[0] = h4.x; hv[1] = h4.y; hv[2] = h4.z; hv[3] = h4.w;
-        }
-      }
+      float hv[4] = {ph[u].x, ph[u].y, ph[u].z, ph[u].w}, mv[4] = {pm[u].x, pm[u].y, pm[u].z, pm[u].w};
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int64_t i = e + c;
@@ -389,6 +414,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
         if (has_self) hat[i] = hv;
       }
     }
+  }
   }
 }
 

@@ -4,36 +4,38 @@
 // (reference dl_code/pcode/utils/sparsification.py:18-54) and the per-tensor
 // compress loop of CHOCOSparsificationCompressor (parallel_choco_v.py:229-260).
 //
-// Exact semantics (both paths below produce bit-identical results):
+// Exact semantics (every path below produces bit-identical results):
 //   T  = k-th largest key(d) (key = |d| bits, see choco_common.h)
 //   out = { i : key_i > T }  U  { the (k - #{key > T}) lowest i with key_i == T },
 //   emitted as (d_i, i) in ascending i.
 //
-// Fast path for large n ("pipeline"), one HBM read of the delta:
-//   K1 topk_sample   : one workgroup histograms a 64K-element strided sample of
-//                      keys (32K bins = key>>16) and picks a candidate floor s_lo
-//                      (#{key >= s_lo} >= k with ~6 sigma margin) and a "sure"
-//                      ceiling s_hi (#{key >= s_hi} < k); [s_lo, s_hi) is split
-//                      into 63 equal key-buckets of width 2^shift.
-//   K2 topk_stream   : the streaming pass.  Each wave owns a contiguous range;
-//                      per float4 it ballots candidates (key >= s_lo), prefix-
-//                      counts them with bit-sliced ballots + mbcnt and writes
-//                      (value, index) in index order into its private slot of
-//                      the candidate buffer.  "maybe" candidates (key < s_hi)
-//                      are also kept in LDS and, at the end of the block,
-//                      counting-sorted by bucket into a per-block side list;
-//                      per-block bucket suffix counts go to a [64][nb] table
-//                      and, by one 256-B wave atomic, to global totals.
-//   K34 topk_finalize: every workgroup redundantly finds the bucket j* holding
-//                      the k-th key from the totals, gathers that bucket's keys
-//                      (a few thousand) from the side lists into LDS, radix-
-//                      selects T and the tie quota exactly, scans per-block
-//                      output offsets, then compacts its share of the candidate
-//                      buffer into the final ascending-index output.
+// Fast path for large n ("pipeline"); the delta is read from HBM ONCE:
+//   K1 topk_sample  : one workgroup histograms a 64K-element strided sample of
+//                     keys (32K bins = key>>16) and picks a candidate floor s_lo
+//                     (#{key >= s_lo} >= k with ~6 sigma margin) and a "sure"
+//                     ceiling s_hi (#{key >= s_hi} < k); [s_lo, s_hi) is split
+//                     into 63 equal key-buckets of width 2^shift.
+//   K2 topk_stream  : persistent streaming pass over 32K-element tiles (4 waves,
+//                     each a contiguous 8K range).  Loads are double-buffered in
+//                     registers; per float4 row the wave ballots candidates
+//                     (key >= s_lo), prefix-counts them with bit-sliced ballots
+//                     + mbcnt and appends (value, index) in index order to an LDS
+//                     stage that is flushed to the wave's slot of the candidate
+//                     buffer in coalesced 256-B stores.  "maybe" candidates
+//                     (key < s_hi) are also kept in LDS and, at the end of the
+//                     tile, counting-sorted by bucket into a per-tile side list;
+//                     per-tile bucket suffix counts go to a [64][nb] table and,
+//                     by one 256-B wave atomic, to replicated global totals.
+//   K3 topk_select  : one workgroup finds the bucket j* holding the k-th key from
+//                     the totals, gathers that bucket's keys (a few thousand)
+//                     from the side lists into LDS, radix-selects T and the tie
+//                     quota exactly and scans per-tile output offsets.
+//   K4 topk_emit    : one workgroup per tile compacts the tile's candidates into
+//                     the final ascending-index output.
 //   If the sample's guess was off (too few candidates, T in the "sure" range,
-//   bucket j* larger than LDS, or a wave's maybe-list overflowed), K34 falls
-//   back to an exact single-workgroup radix select over the full input
-//   (correct, slow, data-dependent only).
+//   bucket j* larger than LDS, or a wave's maybe-list overflowed), K3 runs an
+//   exact single-workgroup radix select over the full input instead (correct,
+//   slow, data-dependent only) and K4 exits.
 // Small n (<= kSmallN) and every segment of the batched segmented path use
 // the same exact radix select (block_topk_exact) in one workgroup.
 #include "choco_common.h"
@@ -45,14 +47,17 @@ namespace choco {
 
 constexpr int kK2Threads = 256;
 constexpr int kK2Waves = kK2Threads / 64;
-constexpr int kK2Unroll = 4;
+constexpr int kK2Unroll = 4;            // float4 rows per wave per pipeline stage
+constexpr int kK2BlocksPerCU = 4;
+constexpr int kStage = 512;             // LDS staging entries per wave
 constexpr int kNBucket = 64;            // 63 "maybe" buckets + 1 "sure"
-constexpr int kMaybeCap = 1024;         // maybe keys per wave kept in LDS
+constexpr int kMaybeCap = 512;          // maybe keys per wave kept in LDS
 constexpr int kSideCap = kK2Waves * kMaybeCap;
 constexpr int kNRep = 8;                // replicas of the global totals (per XCD group)
-constexpr int kNbMax = 4096;            // max K2 blocks (K34 keeps per-block arrays in LDS)
+constexpr int kNbMax = 4096;            // max tiles (K3 keeps per-tile arrays in LDS)
 constexpr int kMCap = 16384;            // max keys of bucket j* handled in LDS
-constexpr int kK34Threads = 256;
+constexpr int kK3Threads = 1024;
+constexpr int kK4Threads = 256;
 constexpr int kSampleThreads = 1024;
 constexpr int kSampleN = 65536;
 constexpr int kSampleChunk = 256;
@@ -60,17 +65,19 @@ constexpr int64_t kSmallN = 65536;
 constexpr int kExactThreads = 1024;
 
 enum SrcMode { kData = 0, kHash = 1 };
+enum TileMode { kTakeNone = 0, kTakeAll = 1, kTakePartial = 2 };
 
 struct TopkCtrl {
   uint32_t s_lo, s_hi, shift, overflow;
-  uint32_t pad[12];
+  uint32_t T, r, fallback;
+  uint32_t pad[9];
   uint32_t G[kNRep][kNBucket];
 };
 
 struct TopkLayout {
   int64_t n;
   uint32_t tile, nb;
-  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, total;
+  size_t off_ctrl, off_cum, off_cntw, off_side, off_tile, off_cval, off_cidx, total;
 };
 
 static TopkLayout topk_layout(int64_t n) {
@@ -85,6 +92,7 @@ static TopkLayout topk_layout(int64_t n) {
   L.off_cum = o;  o += align_up((size_t)kNBucket * L.nb * 4, 256);
   L.off_cntw = o; o += align_up((size_t)L.nb * kK2Waves * 4, 256);
   L.off_side = o; o += align_up((size_t)L.nb * kSideCap * 4, 256);
+  L.off_tile = o; o += align_up((size_t)L.nb * 3 * 4, 256);   // tile_off | tile_tieb | tile_mode
   L.off_cval = o; o += align_up((size_t)L.nb * tile * 4, 256);
   L.off_cidx = o; o += align_up((size_t)L.nb * tile * 4, 256);
   L.total = o;
@@ -262,15 +270,40 @@ CHOCO_DEV void write_params(TopkCtrl* ctrl, uint32_t s_lo, uint64_t s_hi_est) {
   ctrl->shift = shift;
 }
 
+// Highest bin b with #(samples in bins >= b) >= R, searched by one wave inside
+// its 2048-bin range given `above` = samples in bins above that range.
+CHOCO_DEV bool wave_find_bin(const uint32_t* hist, int w, uint32_t above, uint32_t R, uint32_t* out) {
+  const int lane = lane_id();
+  for (int i = 31; i >= 0; --i) {
+    const uint32_t h = hist[2048 * w + 64 * i + lane];
+    const uint32_t rv = __shfl(h, 63 - lane);
+    const uint32_t inc = wave_incl_scan(rv);
+    const uint32_t suf = __shfl(inc, 63 - lane);  // bins >= this lane, within the chunk
+    const uint32_t tot = __shfl(suf, 0);
+    if (above + tot >= R) {
+      const uint64_t m = ballot(above + suf >= R);
+      const int l = 63 - __clzll(m);
+      if (lane == 0) *out = (uint32_t)(2048 * w + 64 * i + l);
+      return true;
+    }
+    above += tot;
+  }
+  return false;
+}
+
 template <bool XH>
 __global__ __launch_bounds__(kSampleThreads) void topk_sample_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k,
     TopkCtrl* __restrict__ ctrl) {
   __shared__ uint32_t hist[32768];
-  __shared__ uint32_t scratch[24];
+  __shared__ uint32_t wsum[kSampleThreads / 64];
   __shared__ uint32_t res[2];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < 32768; i += kSampleThreads) hist[i] = 0;
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  {
+    uint4* h4 = reinterpret_cast<uint4*>(hist);
+#pragma unroll
+    for (int i = 0; i < 32768 / 4 / kSampleThreads; ++i) h4[i * kSampleThreads + tid] = make_uint4(0, 0, 0, 0);
+  }
   for (int i = tid; i < kNRep * kNBucket; i += kSampleThreads) (&ctrl->G[0][0])[i] = 0;
   if (tid == 0) { ctrl->overflow = 0; res[0] = 0; res[1] = 0xFFFFFFFFu; }
   __syncthreads();
@@ -283,56 +316,59 @@ __global__ __launch_bounds__(kSampleThreads) void topk_sample_kernel(
     }
   } else {
     m = kSampleN;
-    constexpr int nchunk = kSampleN / kSampleChunk;          // 256 chunks
-    constexpr int f4_per_chunk = kSampleChunk / 4;            // 64 float4
+    constexpr int nchunk = kSampleN / kSampleChunk;          // 256 chunks of 256 elements
+    constexpr int f4_per_chunk = kSampleChunk / 4;
+    constexpr int per = kSampleN / 4 / kSampleThreads;        // 16 float4 per thread
     const float4* x4 = reinterpret_cast<const float4*>(x);
     const float4* h4 = reinterpret_cast<const float4*>(xh);
     const int64_t stride4 = ((n - kSampleChunk) / (nchunk - 1)) >> 2;  // chunk stride in float4
-#pragma unroll 4
-    for (int it = 0; it < kSampleN / 4 / kSampleThreads; ++it) {   // 16 float4 per thread
-      int s = it * kSampleThreads + tid;
-      int c = s / f4_per_chunk;
-      int64_t q = (int64_t)c * stride4 + (s % f4_per_chunk);
-      float4 v = x4[q];
-      if (XH) { float4 h = h4[q]; v.x -= h.x; v.y -= h.y; v.z -= h.z; v.w -= h.w; }
-      atomicAdd(&hist[fkey(v.x) >> 16], 1u);
-      atomicAdd(&hist[fkey(v.y) >> 16], 1u);
-      atomicAdd(&hist[fkey(v.z) >> 16], 1u);
-      atomicAdd(&hist[fkey(v.w) >> 16], 1u);
+    float4 v[per];
+#pragma unroll
+    for (int it = 0; it < per; ++it) {  // every load issued before any is consumed
+      const int s = it * kSampleThreads + tid;
+      v[it] = x4[(int64_t)(s / f4_per_chunk) * stride4 + (s % f4_per_chunk)];
+    }
+    if (XH) {
+#pragma unroll
+      for (int it = 0; it < per; ++it) {
+        const int s = it * kSampleThreads + tid;
+        const float4 h = h4[(int64_t)(s / f4_per_chunk) * stride4 + (s % f4_per_chunk)];
+        v[it].x -= h.x; v[it].y -= h.y; v[it].z -= h.z; v[it].w -= h.w;
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < per; ++it) {
+      atomicAdd(&hist[fkey(v[it].x) >> 16], 1u);
+      atomicAdd(&hist[fkey(v[it].y) >> 16], 1u);
+      atomicAdd(&hist[fkey(v[it].z) >> 16], 1u);
+      atomicAdd(&hist[fkey(v[it].w) >> 16], 1u);
     }
   }
   __syncthreads();
-  // thread t owns bins [32t, 32t+32)
-  uint32_t local = 0;
-  for (int j = 0; j < 32; ++j) local += hist[tid * 32 + j];
-  uint32_t total;
-  uint32_t pre = block_excl_scan(local, scratch, &total);
-  uint32_t above = total - pre - local;
+  // wave w owns bins [2048 w, 2048 w + 2048); conflict-free strided sums
+  {
+    uint32_t s = 0;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) s += hist[2048 * w + 64 * i + lane];
+    s = wave_sum(s);
+    if (lane == 0) wsum[w] = s;
+  }
+  __syncthreads();
   const double e = (double)k / (double)n * (double)m;
   const double sd = sqrt(e);
   const double rlo_d = ceil(e + 6.0 * sd + 4.0);
   const double rhi_d = floor(e - 6.0 * sd - 4.0);
   const uint32_t R_lo = rlo_d >= (double)m ? 0xFFFFFFFFu : (uint32_t)rlo_d;
   const uint32_t R_hi = rhi_d < 1.0 ? 0u : (uint32_t)rhi_d;
-  // res[0] = bin_lo (0 if R_lo unreachable), res[1] = bin_hi (none -> 0xFFFFFFFF)
-  if (R_lo != 0xFFFFFFFFu && above < R_lo && R_lo <= above + local) {
-    uint32_t acc = above;
-    for (int j = 31; j >= 0; --j) {
-      acc += hist[tid * 32 + j];
-      if (acc >= R_lo) { res[0] = (uint32_t)(tid * 32 + j); break; }
-    }
-  }
-  if (R_hi != 0u && above < R_hi && R_hi <= above + local) {
-    uint32_t acc = above;
-    for (int j = 31; j >= 0; --j) {
-      acc += hist[tid * 32 + j];
-      if (acc >= R_hi) { res[1] = (uint32_t)(tid * 32 + j); break; }
-    }
-  }
+  uint32_t above = 0;
+  for (int ww = kSampleThreads / 64 - 1; ww > w; --ww) above += wsum[ww];
+  const uint32_t mine = wsum[w];
+  if (R_lo != 0xFFFFFFFFu && above < R_lo && R_lo <= above + mine) wave_find_bin(hist, w, above, R_lo, &res[0]);
+  if (R_hi != 0u && above < R_hi && R_hi <= above + mine) wave_find_bin(hist, w, above, R_hi, &res[1]);
   __syncthreads();
   if (tid == 0) {
-    uint32_t s_lo = res[0] << 16;
-    uint64_t s_hi_est = (res[1] == 0xFFFFFFFFu) ? 0x80000000ull : ((uint64_t)res[1] + 1) << 16;
+    const uint32_t s_lo = res[0] << 16;
+    const uint64_t s_hi_est = (res[1] == 0xFFFFFFFFu) ? 0x80000000ull : ((uint64_t)res[1] + 1) << 16;
     write_params(ctrl, s_lo, s_hi_est);
   }
 }
@@ -344,146 +380,189 @@ __global__ void topk_set_params_kernel(TopkCtrl* __restrict__ ctrl, uint32_t s_l
 }
 
 // ----------------------------------------------------------------------------
-// K2: streaming candidate compaction
+// K2: persistent streaming candidate compaction
 // ----------------------------------------------------------------------------
+struct StreamSmem {
+  float sv[kK2Waves][kStage];
+  uint32_t si[kK2Waves][kStage];
+  uint32_t maybe[kK2Waves][kMaybeCap];
+  uint32_t hist[kNBucket];
+  uint32_t cur[kNBucket];
+  uint32_t cnt[kK2Waves];
+  uint32_t mcnt[kK2Waves];
+};
+
+template <bool XH>
+CHOCO_DEV void load_rows(const float* __restrict__ x, const float* __restrict__ xh, int64_t base, int64_t wend,
+                         int lane, float4 (&r)[kK2Unroll]) {
+#pragma unroll
+  for (int u = 0; u < kK2Unroll; ++u) {
+    const int64_t i = base + u * 256 + 4 * lane;
+    if (i + 3 < wend) {
+      float4 a = *reinterpret_cast<const float4*>(x + i);
+      if (XH) {
+        const float4 h = *reinterpret_cast<const float4*>(xh + i);
+        a.x -= h.x; a.y -= h.y; a.z -= h.z; a.w -= h.w;
+      }
+      r[u] = a;
+    } else {
+      float t[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) t[c] = (i + c < wend) ? (XH ? x[i + c] - xh[i + c] : x[i + c]) : 0.f;
+      r[u] = make_float4(t[0], t[1], t[2], t[3]);
+    }
+  }
+}
+
 template <int MODE, bool XH>
 __global__ __launch_bounds__(kK2Threads) void topk_stream_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, uint32_t tile, uint32_t nb,
     uint64_t seed, TopkCtrl* __restrict__ ctrl, uint32_t* __restrict__ cum_tab,
     uint32_t* __restrict__ cntw, uint32_t* __restrict__ side, float* __restrict__ cval,
     uint32_t* __restrict__ cidx) {
-  __shared__ uint32_t s_maybe[kK2Waves][kMaybeCap];
-  __shared__ uint32_t s_hist[kNBucket];
-  __shared__ uint32_t s_cur[kNBucket];
-  __shared__ uint32_t s_cnt[kK2Waves];
-  __shared__ uint32_t s_mcnt[kK2Waves];
-
+  __shared__ StreamSmem sm;
   const uint32_t s_lo = ctrl->s_lo, s_hi = ctrl->s_hi, shift = ctrl->shift;
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
-  const int64_t b = blockIdx.x;
   const int64_t wlen = tile / kK2Waves;
-  const int64_t wbeg = b * tile + w * wlen;
-  const int64_t wend = min(wbeg + wlen, n);
-  float* __restrict__ ov = cval + wbeg;
-  uint32_t* __restrict__ oi = cidx + wbeg;
   Src<MODE, XH> src{x, xh, seed};
 
-  uint32_t ccount = 0;  // candidates written by this wave (wave-uniform)
-  uint32_t mcount = 0;  // maybe keys seen by this wave (wave-uniform, may exceed cap)
+  for (int64_t b = blockIdx.x; b < (int64_t)nb; b += gridDim.x) {
+    const int64_t wbeg = b * tile + w * wlen;
+    const int64_t wend = min(wbeg + wlen, n);
+    float* __restrict__ ov = cval + wbeg;
+    uint32_t* __restrict__ oi = cidx + wbeg;
+    uint32_t flushed = 0, staged = 0, mcount = 0;  // wave-uniform
 
-  for (int64_t base = wbeg; base < wend; base += 256 * kK2Unroll) {
-    float v[kK2Unroll][4];
-    uint32_t kk[kK2Unroll][4];
-    if (MODE == kData) {
+    float4 A[kK2Unroll];
+    if (MODE == kData && wbeg < wend) load_rows<XH>(x, xh, wbeg, wend, lane, A);
+    for (int64_t base = wbeg; base < wend; base += 256 * kK2Unroll) {
+      float4 B[kK2Unroll];
+      const int64_t nxt = base + 256 * kK2Unroll;
+      if (MODE == kData && nxt < wend) load_rows<XH>(x, xh, nxt, wend, lane, B);  // prefetch next stage
 #pragma unroll
       for (int u = 0; u < kK2Unroll; ++u) {
         const int64_t i = base + u * 256 + 4 * lane;
-        if (i + 3 < wend) {
-          float4 a = *reinterpret_cast<const float4*>(x + i);
-          if (XH) {
-            float4 h = *reinterpret_cast<const float4*>(xh + i);
-            a.x -= h.x; a.y -= h.y; a.z -= h.z; a.w -= h.w;
-          }
-          v[u][0] = a.x; v[u][1] = a.y; v[u][2] = a.z; v[u][3] = a.w;
-        } else {
+        const float vv[4] = {A[u].x, A[u].y, A[u].z, A[u].w};
+        uint32_t kk[4];
+        uint32_t cflags = 0, mflags = 0;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) v[u][c] = (i + c < wend) ? src.val(i + c) : 0.f;
+        for (int c = 0; c < 4; ++c) {
+          const bool valid = i + c < wend;
+          const uint32_t key = MODE == kData ? fkey(vv[c]) : (valid ? src.key_of(i + c, 0.f) : 0u);
+          kk[c] = key;
+          const bool cand = valid && key >= s_lo;
+          cflags |= (cand ? 1u : 0u) << c;
+          mflags |= ((cand && key < s_hi) ? 1u : 0u) << c;
         }
-      }
-    }
+        const uint32_t cn = __builtin_popcount(cflags);
+        const uint64_t b0 = ballot(cn & 1u), b1 = ballot(cn & 2u), b2 = ballot(cn & 4u);
+        if ((b0 | b1 | b2) == 0ull) continue;  // wave-uniform: no candidate in this row
+        uint32_t pos = staged + mask_prefix(b0) + 2u * mask_prefix(b1) + 4u * mask_prefix(b2);
+        staged += (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
 #pragma unroll
-    for (int u = 0; u < kK2Unroll; ++u) {
-      const int64_t i = base + u * 256 + 4 * lane;
-      uint32_t cflags = 0, mflags = 0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const bool valid = i + c < wend;
-        uint32_t key = MODE == kData ? fkey(v[u][c]) : (valid ? src.key_of(i + c, 0.f) : 0u);
-        kk[u][c] = key;
-        const bool cand = valid && key >= s_lo;
-        cflags |= (cand ? 1u : 0u) << c;
-        mflags |= ((cand && key < s_hi) ? 1u : 0u) << c;
-      }
-      const uint32_t cn = __builtin_popcount(cflags);
-      const uint64_t b0 = ballot(cn & 1u), b1 = ballot(cn & 2u), b2 = ballot(cn & 4u);
-      if ((b0 | b1 | b2) == 0ull) continue;  // wave-uniform: no candidate in this float4 row
-      uint32_t pos = ccount + mask_prefix(b0) + 2u * mask_prefix(b1) + 4u * mask_prefix(b2);
-      ccount += (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
-      const uint32_t mn = __builtin_popcount(mflags);
-      const uint64_t m0 = ballot(mn & 1u), m1 = ballot(mn & 2u), m2 = ballot(mn & 4u);
-      uint32_t mpos = mcount + mask_prefix(m0) + 2u * mask_prefix(m1) + 4u * mask_prefix(m2);
-      mcount += (uint32_t)(__popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2));
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (cflags & (1u << c)) {
-          float val = MODE == kData ? v[u][c] : src.val(i + c);
-          ov[pos] = val;
-          oi[pos] = (uint32_t)(i + c);
-          ++pos;
-          if (mflags & (1u << c)) {
-            if (mpos < kMaybeCap) s_maybe[w][mpos] = kk[u][c];
-            ++mpos;
+        for (int c = 0; c < 4; ++c) {
+          if (cflags & (1u << c)) {
+            sm.sv[w][pos] = MODE == kData ? vv[c] : src.val(i + c);
+            sm.si[w][pos] = (uint32_t)(i + c);
+            ++pos;
           }
         }
+        if (ballot(mflags != 0u)) {
+          const uint32_t mn = __builtin_popcount(mflags);
+          const uint64_t m0 = ballot(mn & 1u), m1 = ballot(mn & 2u), m2 = ballot(mn & 4u);
+          uint32_t mpos = mcount + mask_prefix(m0) + 2u * mask_prefix(m1) + 4u * mask_prefix(m2);
+          mcount += (uint32_t)(__popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2));
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (mflags & (1u << c)) {
+              if (mpos < kMaybeCap) sm.maybe[w][mpos] = kk[c];
+              ++mpos;
+            }
+          }
+        }
+        if (staged > kStage - 256) {  // flush the stage: coalesced 256-B stores
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          for (uint32_t j = lane; j < staged; j += 64) {
+            ov[flushed + j] = sm.sv[w][j];
+            oi[flushed + j] = sm.si[w][j];
+          }
+          flushed += staged;
+          staged = 0;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kK2Unroll; ++u) A[u] = B[u];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t j = lane; j < staged; j += 64) {
+      ov[flushed + j] = sm.sv[w][j];
+      oi[flushed + j] = sm.si[w][j];
+    }
+    flushed += staged;
+
+    // ---- end of tile: bucket counts, side list, totals
+    if (lane == 0) {
+      sm.cnt[w] = flushed;
+      sm.mcnt[w] = mcount;
+      if (mcount > kMaybeCap) atomicOr(&ctrl->overflow, 1u);
+    }
+    if (threadIdx.x < kNBucket) sm.hist[threadIdx.x] = 0;
+    __syncthreads();
+    {
+      const uint32_t mc = min(sm.mcnt[w], (uint32_t)kMaybeCap);
+      for (uint32_t j = lane; j < mc; j += 64) atomicAdd(&sm.hist[(sm.maybe[w][j] - s_lo) >> shift], 1u);
+    }
+    uint32_t csum = 0, msum = 0;
+#pragma unroll
+    for (int ww = 0; ww < kK2Waves; ++ww) {
+      csum += sm.cnt[ww];
+      msum += min(sm.mcnt[ww], (uint32_t)kMaybeCap);
+    }
+    __syncthreads();
+    if (w == 0) {
+      // bucket 63 = sure; cum[j] = sum_{i >= j} cnt[i]
+      const uint32_t c = (lane == 63) ? (csum - msum) : sm.hist[lane];
+      const uint32_t rv = __shfl(c, 63 - lane);
+      const uint32_t inc = wave_incl_scan(rv);
+      const uint32_t cum = __shfl(inc, 63 - lane);
+      cum_tab[(int64_t)lane * nb + b] = cum;
+      atomicAdd(&ctrl->G[b & (kNRep - 1)][lane], cum);
+      const uint32_t cum_next = __shfl_down(cum, 1);
+      const uint32_t sure = __shfl(cum, 63);
+      if (lane < 63) sm.cur[lane] = cum_next - sure;   // counting-sort cursor of bucket `lane`
+      if (lane < kK2Waves) cntw[b * kK2Waves + lane] = sm.cnt[lane];
+    }
+    __syncthreads();
+    {
+      uint32_t* __restrict__ sd = side + b * kSideCap;
+      const uint32_t mc = min(sm.mcnt[w], (uint32_t)kMaybeCap);
+      for (uint32_t j = lane; j < mc; j += 64) {
+        const uint32_t key = sm.maybe[w][j];
+        const uint32_t p = atomicAdd(&sm.cur[(key - s_lo) >> shift], 1u);
+        sd[p] = key;
       }
     }
-  }
-  if (lane == 0) {
-    s_cnt[w] = ccount;
-    s_mcnt[w] = mcount;
-    if (mcount > kMaybeCap) atomicOr(&ctrl->overflow, 1u);
-  }
-  if (threadIdx.x < kNBucket) s_hist[threadIdx.x] = 0;
-  __syncthreads();
-  // bucket histogram of the maybe keys (each wave bins its own list)
-  {
-    const uint32_t mc = min(s_mcnt[w], (uint32_t)kMaybeCap);
-    for (uint32_t j = lane; j < mc; j += 64) atomicAdd(&s_hist[(s_maybe[w][j] - s_lo) >> shift], 1u);
-  }
-  uint32_t csum = 0, msum = 0;
-#pragma unroll
-  for (int ww = 0; ww < kK2Waves; ++ww) {
-    csum += s_cnt[ww];
-    msum += min(s_mcnt[ww], (uint32_t)kMaybeCap);
-  }
-  __syncthreads();
-  if (w == 0) {
-    // bucket 63 = sure; cum[j] = sum_{i >= j} cnt[i]
-    uint32_t c = (lane == 63) ? (csum - msum) : s_hist[lane];
-    // reverse inclusive scan (suffix sums) via lane mirroring
-    uint32_t rv = __shfl(c, 63 - lane);
-    uint32_t inc = wave_incl_scan(rv);
-    uint32_t cum = __shfl(inc, 63 - lane);
-    cum_tab[(int64_t)lane * nb + b] = cum;
-    atomicAdd(&ctrl->G[b & (kNRep - 1)][lane], cum);
-    // counting-sort cursor: position of bucket j = #maybe with bucket > j
-    uint32_t cum_next = __shfl_down(cum, 1);
-    uint32_t sure = __shfl(cum, 63);
-    if (lane < 63) s_cur[lane] = cum_next - sure;
-    if (lane < kK2Waves) cntw[b * kK2Waves + lane] = s_cnt[lane];
-  }
-  __syncthreads();
-  uint32_t* __restrict__ sd = side + b * kSideCap;
-  {
-    const uint32_t mc = min(s_mcnt[w], (uint32_t)kMaybeCap);
-    for (uint32_t j = lane; j < mc; j += 64) {
-      uint32_t key = s_maybe[w][j];
-      uint32_t p = atomicAdd(&s_cur[(key - s_lo) >> shift], 1u);
-      sd[p] = key;
-    }
+    __syncthreads();  // LDS is reused by the next tile
   }
 }
 
 // ----------------------------------------------------------------------------
-// K34: exact threshold + ordered output
+// K3: exact threshold, tie quota and per-tile output offsets (one workgroup)
 // ----------------------------------------------------------------------------
-struct FinSmem {
+struct SelSmem {
   uint32_t keys[kMCap];
-  uint32_t A[kNbMax + 1];   // key start per K2 block (exclusive scan of bucket-j* counts)
-  uint32_t Bv[kNbMax];      // side offset of bucket j*, later selected-output offset
-  uint32_t Cv[kNbMax];      // #candidates in buckets > j*, later tie_before
-  uint32_t Dv[kNbMax];      // #keys == T per K2 block
+  uint32_t A[kNbMax + 1];   // key start per tile (exclusive scan of bucket-j* counts)
+  uint32_t Bv[kNbMax];      // side offset of bucket j*, later #keys > T in bucket j*
+  uint32_t Cv[kNbMax];      // #candidates in buckets > j* (incl. sure)
+  uint32_t Dv[kNbMax];      // #keys == T
   uint32_t G[kNBucket];
   uint32_t hist[256];
   uint32_t scratch[24];
@@ -491,18 +570,18 @@ struct FinSmem {
 };
 
 template <int MODE, bool XH>
-__global__ __launch_bounds__(kK34Threads) void topk_finalize_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile,
-    uint32_t nb, uint64_t seed, float scale, const TopkCtrl* __restrict__ ctrl,
-    const uint32_t* __restrict__ cum_tab, const uint32_t* __restrict__ cntw,
-    const uint32_t* __restrict__ side, const float* __restrict__ cval,
-    const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
-    int64_t idx_base) {
-  __shared__ FinSmem fs;
+__global__ __launch_bounds__(kK3Threads) void topk_select_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t nb,
+    uint64_t seed, float scale, TopkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ cum_tab,
+    const uint32_t* __restrict__ side, uint32_t* __restrict__ tile_info, float* __restrict__ out_val,
+    int32_t* __restrict__ out_idx, int64_t idx_base) {
+  __shared__ SelSmem fs;
   __shared__ ExactSmem es;
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const uint32_t s_lo = ctrl->s_lo, shift = ctrl->shift;
-  Src<MODE, XH> src{x, xh, seed};
+  uint32_t* __restrict__ tile_off = tile_info;
+  uint32_t* __restrict__ tile_tieb = tile_info + nb;
+  uint32_t* __restrict__ tile_mode = tile_info + 2 * nb;
 
   if (tid < kNBucket) {
     uint32_t g = 0;
@@ -517,17 +596,18 @@ __global__ __launch_bounds__(kK34Threads) void topk_finalize_kernel(
   if (!fallback) {
     for (int j = 62; j >= 0; --j)
       if (fs.G[j] >= (uint32_t)k) { jstar = (uint32_t)j; break; }
-    const uint32_t M = fs.G[jstar] - fs.G[jstar + 1];
-    if (M > (uint32_t)kMCap) fallback = true;
+    if (fs.G[jstar] - fs.G[jstar + 1] > (uint32_t)kMCap) fallback = true;
   }
   if (fallback) {
-    if (blockIdx.x == 0) block_topk_exact(src, n, k, scale, out_val, out_idx, idx_base, es);
+    Src<MODE, XH> src{x, xh, seed};
+    if (tid == 0) ctrl->fallback = 1u;
+    block_topk_exact(src, n, k, scale, out_val, out_idx, idx_base, es);
     return;
   }
   const uint32_t rank_in = (uint32_t)k - fs.G[jstar + 1];  // 1 <= rank_in <= M
 
-  // per K2 block: bucket-j* count, side offset, count above bucket j*
-  const int per = (nb + kK34Threads - 1) / kK34Threads;
+  // per tile: bucket-j* count, side offset, count above bucket j*
+  const int per = (nb + kK3Threads - 1) / kK3Threads;
   const int b0 = tid * per;
   uint32_t local = 0;
   for (int q = 0; q < per; ++q) {
@@ -538,7 +618,7 @@ __global__ __launch_bounds__(kK34Threads) void topk_finalize_kernel(
     const uint32_t s = cum_tab[(int64_t)63 * nb + b];
     fs.A[b] = a - c;   // temporarily: count
     fs.Bv[b] = c - s;  // side offset of bucket j*
-    fs.Cv[b] = c;      // candidates with bucket > j* (incl. sure)
+    fs.Cv[b] = c;
     local += a - c;
   }
   uint32_t M;
@@ -552,7 +632,7 @@ __global__ __launch_bounds__(kK34Threads) void topk_finalize_kernel(
   }
   if (tid == 0) fs.A[nb] = M;
   __syncthreads();
-  // gather bucket-j* keys (block order)
+  // gather bucket-j* keys in tile order
   for (int q = 0; q < per; ++q) {
     const int b = b0 + q;
     if (b >= (int)nb) break;
@@ -561,32 +641,31 @@ __global__ __launch_bounds__(kK34Threads) void topk_finalize_kernel(
     for (uint32_t j = 0; j < cnt; ++j) fs.keys[st + j] = sp[j];
   }
   __syncthreads();
-  // radix select inside the bucket: rel = key - base_j in [0, 2^shift)
+  // radix select inside the bucket: rel = key - base_j in [0, 2^shift), 8-bit digits
   const uint32_t base_j = s_lo + (jstar << shift);
   uint32_t prefix = 0, krem = rank_in;
   int sh = (int)shift;
   while (sh > 0) {
     const int dsh = sh > 8 ? sh - 8 : 0;
     const uint32_t dmask = (1u << (sh - dsh)) - 1u;
-    fs.hist[tid] = 0;  // kK34Threads == 256 bins
+    if (tid < 256) fs.hist[tid] = 0;
     __syncthreads();
-    for (uint32_t j = tid; j < M; j += kK34Threads) {
+    for (uint32_t j = tid; j < M; j += kK3Threads) {
       const uint32_t rel = fs.keys[j] - base_j;
       if ((rel >> sh) == (prefix >> sh)) atomicAdd(&fs.hist[(rel >> dsh) & dmask], 1u);
     }
     __syncthreads();
     if (w == 0) {
-      // suffix scan over 256 bins: lane l owns bins [4l, 4l+4)
-      uint32_t h0 = fs.hist[4 * lane], h1 = fs.hist[4 * lane + 1], h2 = fs.hist[4 * lane + 2],
-               h3 = fs.hist[4 * lane + 3];
-      uint32_t loc = h0 + h1 + h2 + h3;
-      uint32_t rv = __shfl(loc, 63 - lane);
-      uint32_t inc = wave_incl_scan(rv);
-      uint32_t suf_incl = __shfl(inc, 63 - lane);  // bins >= 4*lane
-      uint32_t above = suf_incl - loc;
+      const uint32_t h0 = fs.hist[4 * lane], h1 = fs.hist[4 * lane + 1], h2 = fs.hist[4 * lane + 2],
+                     h3 = fs.hist[4 * lane + 3];
+      const uint32_t loc = h0 + h1 + h2 + h3;
+      const uint32_t rv = __shfl(loc, 63 - lane);
+      const uint32_t inc = wave_incl_scan(rv);
+      const uint32_t suf_incl = __shfl(inc, 63 - lane);  // bins >= 4*lane
+      const uint32_t above = suf_incl - loc;
       if (above < krem && krem <= suf_incl) {
         uint32_t acc = above;
-        uint32_t hs[4] = {h0, h1, h2, h3};
+        const uint32_t hs[4] = {h0, h1, h2, h3};
         for (int t = 3; t >= 0; --t) {
           if (acc + hs[t] >= krem) { fs.bc[0] = 4 * lane + t; fs.bc[1] = krem - acc; break; }
           acc += hs[t];
@@ -602,7 +681,6 @@ __global__ __launch_bounds__(kK34Threads) void topk_finalize_kernel(
   const uint32_t T = base_j + prefix;
   const uint32_t r = krem;  // ties at T to take (>= 1)
 
-  // per K2 block: gt / eq counts of bucket j*, tie prefix, output offsets
   uint32_t eq_local = 0;
   for (int q = 0; q < per; ++q) {
     const int b = b0 + q;
@@ -613,7 +691,7 @@ __global__ __launch_bounds__(kK34Threads) void topk_finalize_kernel(
       gt += key > T;
       eq += key == T;
     }
-    fs.Bv[b] = gt;  // side offsets are no longer needed
+    fs.Bv[b] = gt;
     fs.Dv[b] = eq;
     eq_local += eq;
   }
@@ -626,8 +704,9 @@ __global__ __launch_bounds__(kK34Threads) void topk_finalize_kernel(
     const uint32_t eq = fs.Dv[b];
     const uint32_t take = tb >= r ? 0u : min(eq, r - tb);
     const uint32_t sel = fs.Cv[b] + fs.Bv[b] + take;
-    fs.Cv[b] = tb;   // tie_before
-    fs.Bv[b] = sel;  // selected count (scanned below)
+    tile_tieb[b] = tb;
+    tile_mode[b] = take == 0 ? kTakeNone : (take == eq ? kTakeAll : kTakePartial);
+    fs.Bv[b] = sel;
     tb += eq;
     sel_local += sel;
   }
@@ -636,44 +715,69 @@ __global__ __launch_bounds__(kK34Threads) void topk_finalize_kernel(
   for (int q = 0; q < per; ++q) {
     const int b = b0 + q;
     if (b >= (int)nb) break;
-    const uint32_t c = fs.Bv[b];
-    fs.Bv[b] = sel_pre;
-    sel_pre += c;
+    tile_off[b] = sel_pre;
+    sel_pre += fs.Bv[b];
   }
-  __syncthreads();
+  if (tid == 0) {
+    ctrl->T = T;
+    ctrl->r = r;
+    ctrl->fallback = 0u;
+  }
+}
 
-  // ordered compaction: each wave takes whole K2 blocks
-  const int nwaves_total = gridDim.x * (kK34Threads / 64);
-  for (int b = blockIdx.x * (kK34Threads / 64) + w; b < (int)nb; b += nwaves_total) {
-    uint32_t out = fs.Bv[b];
-    uint32_t tie_run = fs.Cv[b];
-    for (int w2 = 0; w2 < kK2Waves; ++w2) {
-      const uint32_t cnt = cntw[(int64_t)b * kK2Waves + w2];
-      const int64_t cb = (int64_t)b * tile + (int64_t)w2 * (tile / kK2Waves);
-      for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
-        const uint32_t j = c0 + lane;
-        const bool valid = j < cnt;
-        float v = 0.f;
-        uint32_t idx = 0, key = 0;
-        if (valid) {
-          v = cval[cb + j];
-          idx = cidx[cb + j];
-          key = MODE == kData ? fkey(v) : (rank_hash(seed, idx) >> 1);
-        }
-        const bool gt = valid && key > T;
-        const bool eq = valid && key == T;
-        const uint64_t eqm = ballot(eq);
-        const bool sel = gt || (eq && tie_run + mask_prefix(eqm) < r);
-        const uint64_t selm = ballot(sel);
-        if (sel) {
-          const uint32_t pos = out + mask_prefix(selm);
-          out_val[pos] = v * scale;
-          out_idx[pos] = (int32_t)((int64_t)idx + idx_base);
-        }
-        out += (uint32_t)__popcll(selm);
-        tie_run += (uint32_t)__popcll(eqm);
-      }
+// ----------------------------------------------------------------------------
+// K4: ordered compaction, one workgroup per tile
+// ----------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(kK4Threads) void topk_emit_kernel(
+    uint32_t tile, uint32_t nb, uint64_t seed, float scale, const TopkCtrl* __restrict__ ctrl,
+    const uint32_t* __restrict__ cntw, const uint32_t* __restrict__ tile_info, const float* __restrict__ cval,
+    const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
+    int64_t idx_base) {
+  __shared__ uint32_t scratch[24];
+  if (ctrl->fallback) return;
+  const int64_t b = blockIdx.x;
+  const uint32_t T = ctrl->T, r = ctrl->r;
+  uint32_t out = tile_info[b];
+  uint32_t tie_run = tile_info[nb + b];
+  const uint32_t mode = tile_info[2 * nb + b];
+  uint32_t c0 = cntw[b * kK2Waves + 0], c1 = cntw[b * kK2Waves + 1], c2 = cntw[b * kK2Waves + 2],
+           c3 = cntw[b * kK2Waves + 3];
+  const uint32_t e1 = c0, e2 = e1 + c1, e3 = e2 + c2, tot = e3 + c3;
+  const int64_t wlen = tile / kK2Waves;
+  const int64_t tb = b * tile;
+  for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads) {
+    const uint32_t p = p0 + threadIdx.x;
+    const bool valid = p < tot;
+    float v = 0.f;
+    uint32_t idx = 0, key = 0;
+    if (valid) {
+      // position p of the tile's concatenated wave runs
+      const int run = (p >= e1) + (p >= e2) + (p >= e3);
+      const uint32_t start = run == 0 ? 0u : (run == 1 ? e1 : (run == 2 ? e2 : e3));
+      const int64_t a = tb + run * wlen + (p - start);
+      v = cval[a];
+      idx = cidx[a];
+      key = MODE == kData ? fkey(v) : (rank_hash(seed, idx) >> 1);
     }
+    const bool gt = valid && key > T;
+    const bool eq = valid && key == T;
+    bool sel;
+    if (mode == kTakePartial) {
+      uint32_t neq;
+      const uint32_t rank = tie_run + block_excl_scan(eq ? 1u : 0u, scratch, &neq);
+      sel = gt || (eq && rank < r);
+      tie_run += neq;
+    } else {
+      sel = gt || (eq && mode == kTakeAll);
+    }
+    uint32_t nsel;
+    const uint32_t pos = out + block_excl_scan(sel ? 1u : 0u, scratch, &nsel);
+    if (sel) {
+      out_val[pos] = v * scale;
+      out_idx[pos] = (int32_t)((int64_t)idx + idx_base);
+    }
+    out += nsel;
   }
 }
 
@@ -689,6 +793,17 @@ static bool host_seg_uses_pipeline(int64_t off, int64_t len) {
 }
 
 size_t topk_ws_bytes(int64_t n) { return n > kSmallN ? topk_layout(n).total : 256; }
+
+static int num_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                   hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
 
 template <int MODE, bool XH>
 static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
@@ -708,6 +823,7 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   uint32_t* cum = reinterpret_cast<uint32_t*>(base + L.off_cum);
   uint32_t* cntw = reinterpret_cast<uint32_t*>(base + L.off_cntw);
   uint32_t* side = reinterpret_cast<uint32_t*>(base + L.off_side);
+  uint32_t* tinfo = reinterpret_cast<uint32_t*>(base + L.off_tile);
   float* cval = reinterpret_cast<float*>(base + L.off_cval);
   uint32_t* cidx = reinterpret_cast<uint32_t*>(base + L.off_cidx);
   if (MODE == kData) {
@@ -725,15 +841,18 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
     hipLaunchKernelGGL(topk_set_params_kernel, dim3(1), dim3(256), 0, st, ctrl, s_lo, s_hi_est);
     CHOCO_LAUNCHED("topk_set_params_kernel");
   }
+  const unsigned g2 = (unsigned)std::min<int64_t>(L.nb, (int64_t)num_cus() * kK2BlocksPerCU);
   profile_begin("topk_stream", st);
-  hipLaunchKernelGGL((topk_stream_kernel<MODE, XH>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, L.tile,
-                     L.nb, seed, ctrl, cum, cntw, side, cval, cidx);
+  hipLaunchKernelGGL((topk_stream_kernel<MODE, XH>), dim3(g2), dim3(kK2Threads), 0, st, x, xh, n, L.tile, L.nb,
+                     seed, ctrl, cum, cntw, side, cval, cidx);
   profile_end("topk_stream", st);
   CHOCO_LAUNCHED("topk_stream_kernel");
-  const uint32_t g34 = std::min<uint32_t>(256u, (L.nb + 3) / 4);
-  hipLaunchKernelGGL((topk_finalize_kernel<MODE, XH>), dim3(g34), dim3(kK34Threads), 0, st, x, xh, n, k,
-                     L.tile, L.nb, seed, scale, ctrl, cum, cntw, side, cval, cidx, out_val, out_idx, idx_base);
-  CHOCO_LAUNCHED("topk_finalize_kernel");
+  hipLaunchKernelGGL((topk_select_kernel<MODE, XH>), dim3(1), dim3(kK3Threads), 0, st, x, xh, n, k, L.nb, seed,
+                     scale, ctrl, cum, side, tinfo, out_val, out_idx, idx_base);
+  CHOCO_LAUNCHED("topk_select_kernel");
+  hipLaunchKernelGGL((topk_emit_kernel<MODE>), dim3(L.nb), dim3(kK4Threads), 0, st, L.tile, L.nb, seed, scale,
+                     ctrl, cntw, tinfo, cval, cidx, out_val, out_idx, idx_base);
+  CHOCO_LAUNCHED("topk_emit_kernel");
   return CHOCO_OK;
 }
 
