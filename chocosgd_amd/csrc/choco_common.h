@@ -143,6 +143,23 @@ CHOCO_DEV bool last_block_ticket(unsigned int* ticket, unsigned int nblocks, uns
   return last;
 }
 
+// Ticket for hand-offs whose payload travels ONLY through device-scope atomics
+// (performed at the memory side, coherent across XCDs): each wave waits until
+// its atomics are acknowledged, then one lane draws the ticket.  No release
+// fence (buffer_wbl2) per workgroup -- with thousands of workgroups that
+// write-back is what dominates -- and the last workgroup reads the payload with
+// atomic read-modify-writes, so it needs no acquire either.
+CHOCO_DEV bool last_block_ticket_atomics(unsigned int* ticket, unsigned int nblocks, unsigned int* lds_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned int t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *lds_flag = (t == nblocks - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  return *lds_flag != 0u;
+}
+
 // ---------------------------------------------------------------- segments
 // seg_off: int64[nseg+1] monotone, seg_off[0] = 0, seg_off[nseg] = n.
 // Returns the segment containing flat element e (binary search, global memory).

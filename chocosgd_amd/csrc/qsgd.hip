@@ -93,6 +93,25 @@ __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __res
   if (sg0 == sg1) {
     double p = 0.0;
     constexpr int U = 8;  // float4 loads in flight per thread
+    if (t1 - t0 == kNormTile) {
+      // full tile: unconditional loads (no branch around a load -> all U stay in flight)
+      for (int64_t e0 = t0 + 4 * tid; e0 < t1; e0 += 4 * kQThreads * U) {
+        float4 a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) a[u] = *reinterpret_cast<const float4*>(x + e0 + (int64_t)u * 4 * kQThreads);
+        if (XH) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const float4 h = *reinterpret_cast<const float4*>(xh + e0 + (int64_t)u * 4 * kQThreads);
+            a[u].x -= h.x; a[u].y -= h.y; a[u].z -= h.z; a[u].w -= h.w;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          p += (double)a[u].x * a[u].x + (double)a[u].y * a[u].y + (double)a[u].z * a[u].z +
+               (double)a[u].w * a[u].w;
+      }
+    } else
     for (int64_t e0 = t0 + 4 * tid; e0 < t1; e0 += 4 * kQThreads * U) {
       float4 a[U];
 #pragma unroll
@@ -156,7 +175,7 @@ __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __res
       }
     }
   }
-  if (last_block_ticket(&ws->ticket, gridDim.x, &s_flag)) {
+  if (last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
     for (int q = threadIdx.x; q < nseg; q += blockDim.x)
       norms_out[q] = (float)sqrt(atomic_exchange_double(&acc[q], 0.0));
     if (threadIdx.x == 0) __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

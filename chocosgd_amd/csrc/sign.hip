@@ -112,18 +112,39 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
   __syncthreads();
 
   uint32_t wd[4] = {0u, 0u, 0u, 0u};
+  // Interior workgroups (every row run, incl. the tail float4, inside [0, n)) use
+  // UNCONDITIONAL loads so all RU rows stay in flight (a branch around a load makes
+  // the compiler wait for it right away); only the last workgroups take the guarded path.
+  const bool interior = ncol == 256 && (int64_t)31 * Np + j0 + 260 <= n;
   constexpr int RU = 8;  // rows whose loads are in flight together
   for (int r0 = 0; r0 < 32; r0 += RU) {
   float vr[RU][4], tr[RU][4];
+  if (interior) {
 #pragma unroll
-  for (int u = 0; u < RU; ++u) {
-    const int64_t s = (int64_t)(r0 + u) * Np + j0;
+    for (int u = 0; u < RU; ++u) {
+      const int64_t A = ((int64_t)(r0 + u) * Np + j0) & ~(int64_t)3;
+      float4 a = *reinterpret_cast<const float4*>(x + A + 4 * lane);
+      float4 t = *reinterpret_cast<const float4*>(x + A + 256);  // tail (used by lane 63; broadcast)
+      if (XH) {
+        const float4 h = *reinterpret_cast<const float4*>(xh + A + 4 * lane);
+        const float4 ht = *reinterpret_cast<const float4*>(xh + A + 256);
+        a.x -= h.x; a.y -= h.y; a.z -= h.z; a.w -= h.w;
+        t.x -= ht.x; t.y -= ht.y; t.z -= ht.z; t.w -= ht.w;
+      }
+      vr[u][0] = a.x; vr[u][1] = a.y; vr[u][2] = a.z; vr[u][3] = a.w;
+      tr[u][0] = t.x; tr[u][1] = t.y; tr[u][2] = t.z; tr[u][3] = t.w;
+    }
+  } else {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) { vr[u][c] = 0.f; tr[u][c] = 0.f; }
-    if (ncol > 0 && s < n) {
-      const int64_t A = s & ~(int64_t)3;
-      load4g(x, XH ? xh : nullptr, A + 4 * lane, n, vr[u]);
-      if ((s & 3) != 0 && lane == 63) load4g(x, XH ? xh : nullptr, A + 256, n, tr[u]);
+    for (int u = 0; u < RU; ++u) {
+      const int64_t s = (int64_t)(r0 + u) * Np + j0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) { vr[u][c] = 0.f; tr[u][c] = 0.f; }
+      if (ncol > 0 && s < n) {
+        const int64_t A = s & ~(int64_t)3;
+        load4g(x, XH ? xh : nullptr, A + 4 * lane, n, vr[u]);
+        if ((s & 3) != 0 && lane == 63) load4g(x, XH ? xh : nullptr, A + 256, n, tr[u]);
+      }
     }
   }
 #pragma unroll
@@ -151,9 +172,11 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
 #pragma unroll
           for (int c = 0; c < 4; ++c)
             if (e + c >= s && e + c < lim) p += (double)fabsf(v[c]);
-          if (lane == 63)
-            for (int c = 0; c < m; ++c)
-              if (A + 256 + c < lim) p += (double)fabsf(t[c]);
+          if (lane == 63) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+              if (c < m && A + 256 + c < lim) p += (double)fabsf(t[c]);
+          }
           rowpart = wave_sum(p);
         } else {
           int sg[4], tg[4];
@@ -221,7 +244,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
       }
       if (cur >= 0 && run != 0.0) unsafeAtomicAdd(&acc[cur], run);
     }
-    if (last_block_ticket(&ws->ticket, gridDim.x, &s_flag)) {
+    if (last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
       for (int q = threadIdx.x; q < nseg; q += blockDim.x) l1_out[q] = (float)atomic_exchange_double(&acc[q], 0.0);
       if (threadIdx.x == 0) __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -297,17 +320,25 @@ CHOCO_DEV float seg_scale(const float* __restrict__ norms, const int64_t* __rest
   return norms[seg] / (float)numel;
 }
 
-template <int NM>
+template <int NM, bool HS>
 __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs M, int64_t n, int64_t Np,
                                                                        const int64_t* __restrict__ seg_off,
                                                                        int nseg, float* __restrict__ hat,
                                                                        float* __restrict__ mem) {
   __shared__ int s_lo[32], s_hi[32];
+  __shared__ float s_sc[kMaxMsg][32];
   const int lane = lane_id(), w = threadIdx.x >> 6;
   const int64_t J0 = (int64_t)blockIdx.x * kSignCols;
   const int64_t j0 = J0 + 256 * w;
   const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
   row_segments(seg_off, nseg, n, Np, J0, s_lo, s_hi);
+  __syncthreads();
+  // per-row (norm / numel) of every message for rows inside one segment: all global
+  // loads of the scales happen here, before the streaming loop
+  if (threadIdx.x < NM * 32) {
+    const int q = threadIdx.x >> 5, r = threadIdx.x & 31;
+    s_sc[q][r] = (s_lo[r] >= 0 && s_lo[r] == s_hi[r]) ? seg_scale(M.norms[q], seg_off, n, s_lo[r]) : 0.f;
+  }
   __syncthreads();
   if (ncol == 0) return;
   uint32_t wd[NM][4];
@@ -318,58 +349,139 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
 #pragma unroll
       for (int c = 0; c < 4; ++c) wd[q][c] = (j + c < Np) ? M.packed[q][j + c] : 0u;
   }
-  const bool has_self = M.self_slot >= 0 && hat != nullptr;
-  constexpr int RU = 4;  // rows whose memory/x_hat loads are in flight together
-  for (int r0 = 0; r0 < 32; r0 += RU) {
-  float4 pm[RU], ph[RU];
+  // interior workgroups: unconditional loads keep all RU rows in flight
+  const bool interior = ncol == 256 && (int64_t)31 * Np + j0 + 260 <= n;
+  constexpr int RU = 4;
+  bool all_uniform = true;
 #pragma unroll
-  for (int u = 0; u < RU; ++u) {
-    const int64_t s = (int64_t)(r0 + u) * Np + j0;
-    const int64_t e = (s & ~(int64_t)3) + 4 * lane;
-    const int64_t lim = std::min<int64_t>(s + ncol, n);
-    pm[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    ph[u] = pm[u];
-    if (s < n && e >= s && e + 3 < lim) {
-      pm[u] = *reinterpret_cast<const float4*>(mem + e);
-      if (has_self) ph[u] = *reinterpret_cast<const float4*>(hat + e);
+  for (int r = 0; r < 32; ++r) all_uniform &= s_lo[r] == s_hi[r];
+  if (interior && all_uniform) {
+    // fast path: no segment lookups, no global memory op besides the prefetch and the stores
+    for (int r0 = 0; r0 < 32; r0 += RU) {
+      float4 pm[RU], ph[RU], tm[RU], th[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int64_t A = ((int64_t)(r0 + u) * Np + j0) & ~(int64_t)3;
+        pm[u] = *reinterpret_cast<const float4*>(mem + A + 4 * lane);
+        tm[u] = *reinterpret_cast<const float4*>(mem + A + 256);
+        if (HS) {
+          ph[u] = *reinterpret_cast<const float4*>(hat + A + 4 * lane);
+          th[u] = *reinterpret_cast<const float4*>(hat + A + 256);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int r = r0 + u;
+        const int64_t s = (int64_t)r * Np + j0;
+        const int64_t A = s & ~(int64_t)3;
+        const int m = (int)(s & 3);
+        const int64_t e = A + 4 * lane;
+        uint32_t x8[kMaxMsg];
+        float sc[kMaxMsg];
+#pragma unroll
+        for (int q = 0; q < NM; ++q) {
+          uint32_t own4 = 0;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) own4 |= ((wd[q][c] >> r) & 1u) << c;
+          const uint32_t prev4 = __shfl_up(own4, 1);
+          x8[q] = (own4 << 4) | prev4;
+          sc[q] = s_sc[q][r];
+        }
+        float mv[4] = {pm[u].x, pm[u].y, pm[u].z, pm[u].w};
+        float hv[4] = {ph[u].x, ph[u].y, ph[u].z, ph[u].w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) sign_apply<NM>(M, sc, x8, 4 + c - m, hv[c], mv[c]);
+        if (lane != 0 || m == 0) {
+          *reinterpret_cast<float4*>(mem + e) = make_float4(mv[0], mv[1], mv[2], mv[3]);
+          if (HS) *reinterpret_cast<float4*>(hat + e) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+        } else {
+#pragma unroll
+          for (int c = 1; c < 4; ++c) {  // lane 0: elements before the run belong to the previous wave
+            if (c >= m) {
+              mem[e + c] = mv[c];
+              if (HS) hat[e + c] = hv[c];
+            }
+          }
+        }
+        if (lane == 63 && m > 0) {
+          const float tmv[4] = {tm[u].x, tm[u].y, tm[u].z, tm[u].w};
+          const float thv[4] = {th[u].x, th[u].y, th[u].z, th[u].w};
+          uint32_t own[kMaxMsg];
+#pragma unroll
+          for (int q = 0; q < NM; ++q) own[q] = x8[q] >> 4;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            if (c < m) {
+              float h1 = thv[c], m1 = tmv[c];
+              sign_apply<NM>(M, sc, own, 4 + c - m, h1, m1);
+              mem[A + 256 + c] = m1;
+              if (HS) hat[A + 256 + c] = h1;
+            }
+          }
+        }
+      }
     }
+    return;
   }
+  for (int r0 = 0; r0 < 32; r0 += RU) {
+    float4 pm[RU], ph[RU], tm[RU], th[RU];
+    if (interior) {
 #pragma unroll
-  for (int u = 0; u < RU; ++u) {
-    const int r = r0 + u;
-    const int64_t s = (int64_t)r * Np + j0;
-    if (s >= n) continue;
-    const int64_t A = s & ~(int64_t)3;
-    const int m = (int)(s & 3);
-    const int64_t e = A + 4 * lane;
-    const int64_t lim = std::min<int64_t>(s + ncol, n);
-    uint32_t x8[kMaxMsg];
+      for (int u = 0; u < RU; ++u) {
+        const int64_t A = ((int64_t)(r0 + u) * Np + j0) & ~(int64_t)3;
+        pm[u] = *reinterpret_cast<const float4*>(mem + A + 4 * lane);
+        tm[u] = *reinterpret_cast<const float4*>(mem + A + 256);  // tail float4 (lane 63; broadcast)
+        if (HS) {
+          ph[u] = *reinterpret_cast<const float4*>(hat + A + 4 * lane);
+          th[u] = *reinterpret_cast<const float4*>(hat + A + 256);
+        }
+      }
+    } else {
 #pragma unroll
-    for (int q = 0; q < NM; ++q) {
-      uint32_t own4 = 0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) own4 |= ((wd[q][c] >> r) & 1u) << c;
-      const uint32_t prev4 = __shfl_up(own4, 1);
-      x8[q] = (own4 << 4) | prev4;
+      for (int u = 0; u < RU; ++u) {
+        const int64_t s = (int64_t)(r0 + u) * Np + j0;
+        const int64_t e = (s & ~(int64_t)3) + 4 * lane;
+        const int64_t lim = std::min<int64_t>(s + ncol, n);
+        pm[u] = ph[u] = tm[u] = th[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (s < n && e >= s && e + 3 < lim) {
+          pm[u] = *reinterpret_cast<const float4*>(mem + e);
+          if (HS) ph[u] = *reinterpret_cast<const float4*>(hat + e);
+        }
+      }
     }
-    const bool uniform = s_lo[r] == s_hi[r];
-    float sc[kMaxMsg];
-    if (uniform) {
 #pragma unroll
-      for (int q = 0; q < NM; ++q) sc[q] = seg_scale(M.norms[q], seg_off, n, s_lo[r]);
-    }
-    // main float4 of this lane
-    {
+    for (int u = 0; u < RU; ++u) {
+      const int r = r0 + u;
+      const int64_t s = (int64_t)r * Np + j0;
+      if (s >= n) continue;
+      const int64_t A = s & ~(int64_t)3;
+      const int m = (int)(s & 3);
+      const int64_t e = A + 4 * lane;
+      const int64_t lim = std::min<int64_t>(s + ncol, n);
+      uint32_t x8[kMaxMsg];
+#pragma unroll
+      for (int q = 0; q < NM; ++q) {
+        uint32_t own4 = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) own4 |= ((wd[q][c] >> r) & 1u) << c;
+        const uint32_t prev4 = __shfl_up(own4, 1);
+        x8[q] = (own4 << 4) | prev4;
+      }
+      const bool uniform = s_lo[r] == s_hi[r];
+      float sc[kMaxMsg];
+#pragma unroll
+      for (int q = 0; q < NM; ++q) sc[q] = s_sc[q][r];
+      // main float4 of this lane
       const bool full = e >= s && e + 3 < lim;
-      float hv[4] = {ph[u].x, ph[u].y, ph[u].z, ph[u].w}, mv[4] = {pm[u].x, pm[u].y, pm[u].z, pm[u].w};
+      float mv[4] = {pm[u].x, pm[u].y, pm[u].z, pm[u].w};
+      float hv[4] = {ph[u].x, ph[u].y, ph[u].z, ph[u].w};
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int64_t i = e + c;
-        const bool own = i >= s && i < lim;
-        if (!own) continue;
-        if (!full) {
+        if (!(i >= s && i < lim)) continue;
+        if (!interior && !full) {
           mv[c] = mem[i];
-          if (has_self) hv[c] = hat[i];
+          if (HS) hv[c] = hat[i];
         }
         float scl[kMaxMsg];
         if (uniform) {
@@ -381,42 +493,51 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
           for (int q = 0; q < NM; ++q) scl[q] = seg_scale(M.norms[q], seg_off, n, sg);
         }
         sign_apply<NM>(M, scl, x8, 4 + c - m, hv[c], mv[c]);
-        if (!full) {
-          mem[i] = mv[c];
-          if (has_self) hat[i] = hv[c];
-        }
       }
       if (full) {
         *reinterpret_cast<float4*>(mem + e) = make_float4(mv[0], mv[1], mv[2], mv[3]);
-        if (has_self) *reinterpret_cast<float4*>(hat + e) = make_float4(hv[0], hv[1], hv[2], hv[3]);
-      }
-    }
-    // tail elements of lane 63 (columns 256-m .. 255 of this run)
-    if (lane == 63) {
-      for (int c = 0; c < m; ++c) {
-        const int64_t i = A + 256 + c;
-        if (i >= lim) continue;
-        float hv = has_self ? hat[i] : 0.f, mv = mem[i];
-        float scl[kMaxMsg];
-        if (uniform) {
+        if (HS) *reinterpret_cast<float4*>(hat + e) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+      } else {
 #pragma unroll
-          for (int q = 0; q < NM; ++q) scl[q] = sc[q];
-        } else {
-          const int sg = seg_walk(seg_off, nseg, s_lo[r], i);
-#pragma unroll
-          for (int q = 0; q < NM; ++q) scl[q] = seg_scale(M.norms[q], seg_off, n, sg);
+        for (int c = 0; c < 4; ++c) {
+          const int64_t i = e + c;
+          if (i >= s && i < lim) {
+            mem[i] = mv[c];
+            if (HS) hat[i] = hv[c];
+          }
         }
-        uint32_t own[kMaxMsg];
+      }
+      // tail elements of lane 63 (columns 256-m .. 255 of this run)
+      if (lane == 63 && m > 0) {
+        const float tmv[4] = {tm[u].x, tm[u].y, tm[u].z, tm[u].w};
+        const float thv[4] = {th[u].x, th[u].y, th[u].z, th[u].w};
 #pragma unroll
-        for (int q = 0; q < NM; ++q) own[q] = x8[q] >> 4;  // this lane's own nibble
-        sign_apply<NM>(M, scl, own, 4 + c - m, hv, mv);
-        mem[i] = mv;
-        if (has_self) hat[i] = hv;
+        for (int c = 0; c < 3; ++c) {
+          const int64_t i = A + 256 + c;
+          if (c >= m || i >= lim) continue;
+          float h1 = interior ? thv[c] : (HS ? hat[i] : 0.f);
+          float m1 = interior ? tmv[c] : mem[i];
+          float scl[kMaxMsg];
+          if (uniform) {
+#pragma unroll
+            for (int q = 0; q < NM; ++q) scl[q] = sc[q];
+          } else {
+            const int sg = seg_walk(seg_off, nseg, s_lo[r], i);
+#pragma unroll
+            for (int q = 0; q < NM; ++q) scl[q] = seg_scale(M.norms[q], seg_off, n, sg);
+          }
+          uint32_t own[kMaxMsg];
+#pragma unroll
+          for (int q = 0; q < NM; ++q) own[q] = x8[q] >> 4;  // this lane's own nibble
+          sign_apply<NM>(M, scl, own, 4 + c - m, h1, m1);
+          mem[i] = m1;
+          if (HS) hat[i] = h1;
+        }
       }
     }
-  }
   }
 }
+
 
 }  // namespace choco
 
@@ -504,8 +625,12 @@ CHOCO_API int choco_sign_decompress_accumulate(const int32_t* const* packed_list
   profile_begin("sign_accumulate", st);
 #define CHOCO_SIGN_ACC(NM)                                                                                 \
   case NM:                                                                                                  \
-    hipLaunchKernelGGL((sign_accumulate_kernel<NM>), dim3(grid), dim3(kSignThreads), 0, st, M, n, Np,      \
-                       seg_off, nseg, xhat_self, memory);                                                   \
+    if (self_slot >= 0 && xhat_self)                                                                        \
+      hipLaunchKernelGGL((sign_accumulate_kernel<NM, true>), dim3(grid), dim3(kSignThreads), 0, st, M, n,   \
+                         Np, seg_off, nseg, xhat_self, memory);                                             \
+    else                                                                                                    \
+      hipLaunchKernelGGL((sign_accumulate_kernel<NM, false>), dim3(grid), dim3(kSignThreads), 0, st, M, n,  \
+                         Np, seg_off, nseg, xhat_self, memory);                                             \
     break;
   switch (nmsg) {
     CHOCO_SIGN_ACC(1)

@@ -58,8 +58,10 @@ constexpr int kNbMax = 4096;            // max tiles (K3 keeps per-tile arrays i
 constexpr int kMCap = 16384;            // max keys of bucket j* handled in LDS
 constexpr int kK3Threads = 1024;
 constexpr int kK4Threads = 256;
-constexpr int kSampleThreads = 1024;
-constexpr int kSampleN = 65536;
+constexpr int kK1Blocks = 64;           // sample workgroups, 1024 samples each
+constexpr int kK1Threads = 256;
+constexpr int kK1ListCap = 256;         // per-workgroup tail-list capacity
+constexpr int kSampleN = kK1Blocks * kK1Threads * 4;   // 65536
 constexpr int kSampleChunk = 256;
 constexpr int64_t kSmallN = 65536;
 constexpr int kExactThreads = 1024;
@@ -69,15 +71,15 @@ enum TileMode { kTakeNone = 0, kTakeAll = 1, kTakePartial = 2 };
 
 struct TopkCtrl {
   uint32_t s_lo, s_hi, shift, overflow;
-  uint32_t T, r, fallback;
-  uint32_t pad[9];
+  uint32_t T, r, fallback, k1_ticket;
+  uint32_t pad[8];
   uint32_t G[kNRep][kNBucket];
 };
 
 struct TopkLayout {
   int64_t n;
   uint32_t tile, nb;
-  size_t off_ctrl, off_cum, off_cntw, off_side, off_tile, off_cval, off_cidx, total;
+  size_t off_ctrl, off_cum, off_cntw, off_side, off_tile, off_k1, off_cval, off_cidx, total;
 };
 
 static TopkLayout topk_layout(int64_t n) {
@@ -93,6 +95,7 @@ static TopkLayout topk_layout(int64_t n) {
   L.off_cntw = o; o += align_up((size_t)L.nb * kK2Waves * 4, 256);
   L.off_side = o; o += align_up((size_t)L.nb * kSideCap * 4, 256);
   L.off_tile = o; o += align_up((size_t)L.nb * 3 * 4, 256);   // tile_off | tile_tieb | tile_mode
+  L.off_k1 = o;   o += align_up((size_t)(kK1Blocks * kK1ListCap + kK1Blocks) * 4, 256);  // sample tail lists
   L.off_cval = o; o += align_up((size_t)L.nb * tile * 4, 256);
   L.off_cidx = o; o += align_up((size_t)L.nb * tile * 4, 256);
   L.total = o;
@@ -258,6 +261,13 @@ __global__ __launch_bounds__(kExactThreads) void topk_segmented_kernel(
 
 // ----------------------------------------------------------------------------
 // K1: sample -> (s_lo, s_hi, shift)
+//
+// 64 workgroups each take 1024 samples (4 contiguous 256-element chunks spread
+// over the buffer).  A workgroup keeps only its local tail -- the keys in the
+// coarse (key>>20) bins that hold its top ~4x(expected share) samples -- in a
+// global list; the last workgroup (agent-scope ticket) radix-selects the
+// R_lo-th / R_hi-th largest keys of the union exactly.  Truncating a list can
+// only lower those order statistics, i.e. make s_lo more conservative.
 // ----------------------------------------------------------------------------
 CHOCO_DEV void write_params(TopkCtrl* ctrl, uint32_t s_lo, uint64_t s_hi_est) {
   uint64_t width = s_hi_est > s_lo ? s_hi_est - s_lo : 1;
@@ -270,106 +280,160 @@ CHOCO_DEV void write_params(TopkCtrl* ctrl, uint32_t s_lo, uint64_t s_hi_est) {
   ctrl->shift = shift;
 }
 
-// Highest bin b with #(samples in bins >= b) >= R, searched by one wave inside
-// its 2048-bin range given `above` = samples in bins above that range.
-CHOCO_DEV bool wave_find_bin(const uint32_t* hist, int w, uint32_t above, uint32_t R, uint32_t* out) {
-  const int lane = lane_id();
-  for (int i = 31; i >= 0; --i) {
-    const uint32_t h = hist[2048 * w + 64 * i + lane];
-    const uint32_t rv = __shfl(h, 63 - lane);
-    const uint32_t inc = wave_incl_scan(rv);
-    const uint32_t suf = __shfl(inc, 63 - lane);  // bins >= this lane, within the chunk
-    const uint32_t tot = __shfl(suf, 0);
-    if (above + tot >= R) {
-      const uint64_t m = ballot(above + suf >= R);
-      const int l = 63 - __clzll(m);
-      if (lane == 0) *out = (uint32_t)(2048 * w + 64 * i + l);
-      return true;
-    }
-    above += tot;
-  }
-  return false;
-}
-
-template <bool XH>
-__global__ __launch_bounds__(kSampleThreads) void topk_sample_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k,
-    TopkCtrl* __restrict__ ctrl) {
-  __shared__ uint32_t hist[32768];
-  __shared__ uint32_t wsum[kSampleThreads / 64];
-  __shared__ uint32_t res[2];
+// rank-th largest (1-based) of keys[0..u) held in LDS; 4 rounds of 8-bit digits.
+CHOCO_DEV uint32_t lds_select_kth(const uint32_t* keys, uint32_t u, uint32_t rank, uint32_t* hist, uint32_t* bc) {
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  {
-    uint4* h4 = reinterpret_cast<uint4*>(hist);
-#pragma unroll
-    for (int i = 0; i < 32768 / 4 / kSampleThreads; ++i) h4[i * kSampleThreads + tid] = make_uint4(0, 0, 0, 0);
-  }
-  for (int i = tid; i < kNRep * kNBucket; i += kSampleThreads) (&ctrl->G[0][0])[i] = 0;
-  if (tid == 0) { ctrl->overflow = 0; res[0] = 0; res[1] = 0xFFFFFFFFu; }
-  __syncthreads();
-  int64_t m;
-  if (n <= kSampleN) {
-    m = n;
-    for (int64_t i = tid; i < n; i += kSampleThreads) {
-      float v = XH ? x[i] - xh[i] : x[i];
-      atomicAdd(&hist[fkey(v) >> 16], 1u);
+  uint32_t prefix = 0, maskhi = 0, krem = rank;
+  const int shs[4] = {23, 15, 7, 0};
+  const int wds[4] = {8, 8, 8, 7};
+  for (int rd = 0; rd < 4; ++rd) {
+    const int sh = shs[rd];
+    const uint32_t dmask = (1u << wds[rd]) - 1u;
+    for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (uint32_t j = tid; j < u; j += blockDim.x) {
+      const uint32_t key = keys[j];
+      if ((key & maskhi) == prefix) atomicAdd(&hist[(key >> sh) & dmask], 1u);
     }
-  } else {
-    m = kSampleN;
-    constexpr int nchunk = kSampleN / kSampleChunk;          // 256 chunks of 256 elements
-    constexpr int f4_per_chunk = kSampleChunk / 4;
-    constexpr int per = kSampleN / 4 / kSampleThreads;        // 16 float4 per thread
-    const float4* x4 = reinterpret_cast<const float4*>(x);
-    const float4* h4 = reinterpret_cast<const float4*>(xh);
-    const int64_t stride4 = ((n - kSampleChunk) / (nchunk - 1)) >> 2;  // chunk stride in float4
-    float4 v[per];
-#pragma unroll
-    for (int it = 0; it < per; ++it) {  // every load issued before any is consumed
-      const int s = it * kSampleThreads + tid;
-      v[it] = x4[(int64_t)(s / f4_per_chunk) * stride4 + (s % f4_per_chunk)];
-    }
-    if (XH) {
-#pragma unroll
-      for (int it = 0; it < per; ++it) {
-        const int s = it * kSampleThreads + tid;
-        const float4 h = h4[(int64_t)(s / f4_per_chunk) * stride4 + (s % f4_per_chunk)];
-        v[it].x -= h.x; v[it].y -= h.y; v[it].z -= h.z; v[it].w -= h.w;
+    __syncthreads();
+    if (w == 0) {
+      const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
+      const uint32_t loc = h0 + h1 + h2 + h3;
+      const uint32_t rv = __shfl(loc, 63 - lane);
+      const uint32_t inc = wave_incl_scan(rv);
+      const uint32_t suf_incl = __shfl(inc, 63 - lane);
+      const uint32_t above = suf_incl - loc;
+      if (above < krem && krem <= suf_incl) {
+        uint32_t acc = above;
+        const uint32_t hs[4] = {h0, h1, h2, h3};
+        for (int t = 3; t >= 0; --t) {
+          if (acc + hs[t] >= krem) { bc[0] = 4 * lane + t; bc[1] = krem - acc; break; }
+          acc += hs[t];
+        }
       }
     }
+    __syncthreads();
+    prefix |= bc[0] << sh;
+    maskhi |= dmask << sh;
+    krem = bc[1];
+    __syncthreads();
+  }
+  return prefix;
+}
+
+struct SampleSmem {
+  uint32_t hist[2048];
+  uint32_t keys[kK1Blocks * kK1ListCap];
+  uint32_t scratch[24];
+  uint32_t bc[4];
+  uint32_t flag;
+};
+
+template <bool XH>
+__global__ __launch_bounds__(kK1Threads) void topk_sample_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k,
+    TopkCtrl* __restrict__ ctrl, uint32_t* __restrict__ lists) {
+  __shared__ SampleSmem sm;
+  uint32_t* __restrict__ counts = lists + kK1Blocks * kK1ListCap;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 2048; i += kK1Threads) sm.hist[i] = 0;
+  // this thread's 4 samples: float4 s of chunk s/64 (64 float4 per 256-element chunk)
+  constexpr int nchunk = kSampleN / kSampleChunk;
+  const int64_t stride4 = ((n - kSampleChunk) / (nchunk - 1)) >> 2;
+  const int s = blockIdx.x * kK1Threads + tid;
+  const int64_t q = (int64_t)(s / 64) * stride4 + (s % 64);
+  float4 v = reinterpret_cast<const float4*>(x)[q];
+  if (XH) {
+    const float4 h = reinterpret_cast<const float4*>(xh)[q];
+    v.x -= h.x; v.y -= h.y; v.z -= h.z; v.w -= h.w;
+  }
+  const uint32_t kk[4] = {fkey(v.x), fkey(v.y), fkey(v.z), fkey(v.w)};
+  __syncthreads();
 #pragma unroll
-    for (int it = 0; it < per; ++it) {
-      atomicAdd(&hist[fkey(v[it].x) >> 16], 1u);
-      atomicAdd(&hist[fkey(v[it].y) >> 16], 1u);
-      atomicAdd(&hist[fkey(v[it].z) >> 16], 1u);
-      atomicAdd(&hist[fkey(v[it].w) >> 16], 1u);
+  for (int c = 0; c < 4; ++c) atomicAdd(&sm.hist[kk[c] >> 20], 1u);
+  __syncthreads();
+  // local cutoff: highest coarse bin whose suffix count reaches m_b
+  const double eb = (double)k / (double)n * (double)(kK1Threads * 4);
+  const uint32_t m_b = (uint32_t)fmin(4.0 * eb + 16.0, (double)(kK1Threads * 4));
+  {
+    uint32_t local = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) local += sm.hist[tid * 8 + j];
+    uint32_t total;
+    const uint32_t pre = block_excl_scan(local, sm.scratch, &total);
+    const uint32_t above = total - pre - local;
+    if (above < m_b && m_b <= above + local) {
+      uint32_t acc = above;
+      for (int j = 7; j >= 0; --j) {
+        acc += sm.hist[tid * 8 + j];
+        if (acc >= m_b) { sm.bc[0] = (uint32_t)(tid * 8 + j); break; }
+      }
+    }
+    __syncthreads();
+  }
+  const uint32_t cut = sm.bc[0];
+  uint32_t mine = 0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) mine += (kk[c] >> 20) >= cut;
+  uint32_t tot;
+  uint32_t pos = block_excl_scan(mine, sm.scratch, &tot);
+  uint32_t* __restrict__ my = lists + blockIdx.x * kK1ListCap;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if ((kk[c] >> 20) >= cut) {
+      if (pos < kK1ListCap) my[pos] = kk[c];
+      ++pos;
     }
   }
-  __syncthreads();
-  // wave w owns bins [2048 w, 2048 w + 2048); conflict-free strided sums
+  if (tid == 0) counts[blockIdx.x] = min(tot, (uint32_t)kK1ListCap);
+  if (!last_block_ticket(&ctrl->k1_ticket, gridDim.x, &sm.flag)) return;
+
+  // ---- last workgroup: exact order statistics of the union
+  // all counts in parallel, then one independent load per key slot
+  const uint32_t myc = tid < kK1Blocks ? counts[tid] : 0u;
+  uint32_t u;
+  const uint32_t mystart = block_excl_scan(myc, sm.scratch, &u);
   {
-    uint32_t s = 0;
-#pragma unroll 8
-    for (int i = 0; i < 32; ++i) s += hist[2048 * w + 64 * i + lane];
-    s = wave_sum(s);
-    if (lane == 0) wsum[w] = s;
+    // list starts in LDS (hist reused), then key slot p -> (list, offset) by binary search;
+    // G unconditional loads per thread in flight (clamped slot when p >= u)
+    if (tid < kK1Blocks) sm.hist[tid] = mystart;
+    __syncthreads();
+    constexpr int G = 16;
+    for (uint32_t base = 0; base < u; base += G * kK1Threads) {
+      uint32_t v[G];
+      int dst[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const uint32_t p = base + (uint32_t)g * kK1Threads + tid;
+        const uint32_t pc = p < u ? p : 0u;
+        int lo = 0, hi = kK1Blocks - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (sm.hist[mid] <= pc) lo = mid; else hi = mid - 1;
+        }
+        v[g] = lists[lo * kK1ListCap + (pc - sm.hist[lo])];
+        dst[g] = p < u ? (int)p : -1;
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (dst[g] >= 0) sm.keys[dst[g]] = v[g];
+    }
   }
+  for (int i = tid; i < kNRep * kNBucket; i += kK1Threads) (&ctrl->G[0][0])[i] = 0;
   __syncthreads();
-  const double e = (double)k / (double)n * (double)m;
+  const double m = (double)kSampleN;
+  const double e = (double)k / (double)n * m;
   const double sd = sqrt(e);
   const double rlo_d = ceil(e + 6.0 * sd + 4.0);
   const double rhi_d = floor(e - 6.0 * sd - 4.0);
-  const uint32_t R_lo = rlo_d >= (double)m ? 0xFFFFFFFFu : (uint32_t)rlo_d;
-  const uint32_t R_hi = rhi_d < 1.0 ? 0u : (uint32_t)rhi_d;
-  uint32_t above = 0;
-  for (int ww = kSampleThreads / 64 - 1; ww > w; --ww) above += wsum[ww];
-  const uint32_t mine = wsum[w];
-  if (R_lo != 0xFFFFFFFFu && above < R_lo && R_lo <= above + mine) wave_find_bin(hist, w, above, R_lo, &res[0]);
-  if (R_hi != 0u && above < R_hi && R_hi <= above + mine) wave_find_bin(hist, w, above, R_hi, &res[1]);
-  __syncthreads();
+  uint32_t s_lo = 0;
+  if (rlo_d <= (double)u) s_lo = lds_select_kth(sm.keys, u, (uint32_t)rlo_d, sm.hist, sm.bc);
+  uint64_t s_hi_est = 0x80000000ull;  // above every key: nothing is "sure"
+  if (rhi_d >= 1.0 && rhi_d <= (double)u) s_hi_est = (uint64_t)lds_select_kth(sm.keys, u, (uint32_t)rhi_d, sm.hist, sm.bc) + 1;
   if (tid == 0) {
-    const uint32_t s_lo = res[0] << 16;
-    const uint64_t s_hi_est = (res[1] == 0xFFFFFFFFu) ? 0x80000000ull : ((uint64_t)res[1] + 1) << 16;
+    ctrl->overflow = 0;
     write_params(ctrl, s_lo, s_hi_est);
+    __hip_atomic_store(&ctrl->k1_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -392,26 +456,111 @@ struct StreamSmem {
   uint32_t mcnt[kK2Waves];
 };
 
+// Unconditional (branch-free) float4 loads of kK2Unroll rows: keeps the
+// compiler's vmcnt accounting exact so the prefetch stays in flight.
 template <bool XH>
-CHOCO_DEV void load_rows(const float* __restrict__ x, const float* __restrict__ xh, int64_t base, int64_t wend,
-                         int lane, float4 (&r)[kK2Unroll]) {
+CHOCO_DEV void load_rows_full(const float* __restrict__ x, const float* __restrict__ xh, int64_t base, int lane,
+                              float4 (&r)[kK2Unroll]) {
 #pragma unroll
-  for (int u = 0; u < kK2Unroll; ++u) {
-    const int64_t i = base + u * 256 + 4 * lane;
-    if (i + 3 < wend) {
-      float4 a = *reinterpret_cast<const float4*>(x + i);
-      if (XH) {
-        const float4 h = *reinterpret_cast<const float4*>(xh + i);
-        a.x -= h.x; a.y -= h.y; a.z -= h.z; a.w -= h.w;
-      }
-      r[u] = a;
-    } else {
-      float t[4];
+  for (int u = 0; u < kK2Unroll; ++u) r[u] = *reinterpret_cast<const float4*>(x + base + u * 256 + 4 * lane);
+  if (XH) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) t[c] = (i + c < wend) ? (XH ? x[i + c] - xh[i + c] : x[i + c]) : 0.f;
-      r[u] = make_float4(t[0], t[1], t[2], t[3]);
+    for (int u = 0; u < kK2Unroll; ++u) {
+      const float4 h = *reinterpret_cast<const float4*>(xh + base + u * 256 + 4 * lane);
+      r[u].x -= h.x; r[u].y -= h.y; r[u].z -= h.z; r[u].w -= h.w;
     }
   }
+}
+
+// Per-wave compaction state (all wave-uniform).
+struct WaveAcc {
+  uint32_t flushed, staged, mcount;
+};
+
+// Flush exactly 256 staged candidates as 4 coalesced 256-B stores per array,
+// then move the (< 256) remainder to the front of the stage.
+CHOCO_DEV void flush256(StreamSmem& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
+                        uint32_t* __restrict__ oi) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  float fv[4];
+  uint32_t fi[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    fv[q] = sm.sv[w][q * 64 + lane];
+    fi[q] = sm.si[w][q * 64 + lane];
+  }
+  const uint32_t rem = a.staged - 256;
+  float rv[4];
+  uint32_t ri[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t j = q * 64 + lane;
+    rv[q] = j < rem ? sm.sv[w][256 + j] : 0.f;
+    ri[q] = j < rem ? sm.si[w][256 + j] : 0u;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t j = q * 64 + lane;
+    if (j < rem) {
+      sm.sv[w][j] = rv[q];
+      sm.si[w][j] = ri[q];
+    }
+    ov[a.flushed + j] = fv[q];
+    oi[a.flushed + j] = fi[q];
+  }
+  a.flushed += 256;
+  a.staged = rem;
+}
+
+// One float4 row per lane (256 elements per wave): ballot candidates into the stage.
+template <int MODE, bool XH, bool GUARD>
+CHOCO_DEV void process_row(const Src<MODE, XH>& src, const float4 v4, int64_t i, int64_t wend, uint32_t s_lo,
+                           uint32_t s_hi, StreamSmem& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
+                           uint32_t* __restrict__ oi) {
+  const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+  uint32_t kk[4];
+  uint32_t cflags = 0, mflags = 0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const bool valid = !GUARD || i + c < wend;
+    const uint32_t key = MODE == kData ? fkey(vv[c]) : (valid ? src.key_of(i + c, 0.f) : 0u);
+    kk[c] = key;
+    const bool cand = valid && key >= s_lo;
+    cflags |= (cand ? 1u : 0u) << c;
+    mflags |= ((cand && key < s_hi) ? 1u : 0u) << c;
+  }
+  const uint32_t cn = __builtin_popcount(cflags);
+  const uint64_t b0 = ballot(cn & 1u), b1 = ballot(cn & 2u), b2 = ballot(cn & 4u);
+  if ((b0 | b1 | b2) == 0ull) return;  // wave-uniform: no candidate in this row
+  uint32_t pos = a.staged + mask_prefix(b0) + 2u * mask_prefix(b1) + 4u * mask_prefix(b2);
+  a.staged += (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (cflags & (1u << c)) {
+      sm.sv[w][pos] = MODE == kData ? vv[c] : src.val(i + c);
+      sm.si[w][pos] = (uint32_t)(i + c);
+      ++pos;
+    }
+  }
+  if (ballot(mflags != 0u)) {
+    const uint32_t mn = __builtin_popcount(mflags);
+    const uint64_t m0 = ballot(mn & 1u), m1 = ballot(mn & 2u), m2 = ballot(mn & 4u);
+    uint32_t mpos = a.mcount + mask_prefix(m0) + 2u * mask_prefix(m1) + 4u * mask_prefix(m2);
+    a.mcount += (uint32_t)(__popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2));
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (mflags & (1u << c)) {
+        if (mpos < kMaybeCap) sm.maybe[w][mpos] = kk[c];
+        ++mpos;
+      }
+    }
+  }
+  if (a.staged >= 256) flush256(sm, w, lane, a, ov, oi);
 }
 
 template <int MODE, bool XH>
@@ -425,6 +574,7 @@ __global__ __launch_bounds__(kK2Threads) void topk_stream_kernel(
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   const int64_t wlen = tile / kK2Waves;
+  constexpr int64_t kStep = 256 * kK2Unroll;
   Src<MODE, XH> src{x, xh, seed};
 
   for (int64_t b = blockIdx.x; b < (int64_t)nb; b += gridDim.x) {
@@ -432,81 +582,55 @@ __global__ __launch_bounds__(kK2Threads) void topk_stream_kernel(
     const int64_t wend = min(wbeg + wlen, n);
     float* __restrict__ ov = cval + wbeg;
     uint32_t* __restrict__ oi = cidx + wbeg;
-    uint32_t flushed = 0, staged = 0, mcount = 0;  // wave-uniform
+    WaveAcc a{0u, 0u, 0u};
+    const int64_t full_end = wend > wbeg ? wbeg + (wend - wbeg) / kStep * kStep : wbeg;
 
-    float4 A[kK2Unroll];
-    if (MODE == kData && wbeg < wend) load_rows<XH>(x, xh, wbeg, wend, lane, A);
-    for (int64_t base = wbeg; base < wend; base += 256 * kK2Unroll) {
-      float4 B[kK2Unroll];
-      const int64_t nxt = base + 256 * kK2Unroll;
-      if (MODE == kData && nxt < wend) load_rows<XH>(x, xh, nxt, wend, lane, B);  // prefetch next stage
-#pragma unroll
-      for (int u = 0; u < kK2Unroll; ++u) {
-        const int64_t i = base + u * 256 + 4 * lane;
-        const float vv[4] = {A[u].x, A[u].y, A[u].z, A[u].w};
-        uint32_t kk[4];
-        uint32_t cflags = 0, mflags = 0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const bool valid = i + c < wend;
-          const uint32_t key = MODE == kData ? fkey(vv[c]) : (valid ? src.key_of(i + c, 0.f) : 0u);
-          kk[c] = key;
-          const bool cand = valid && key >= s_lo;
-          cflags |= (cand ? 1u : 0u) << c;
-          mflags |= ((cand && key < s_hi) ? 1u : 0u) << c;
+    // main loop: whole kStep blocks, double-buffered unconditional loads
+    if (full_end > wbeg) {
+      float4 A[kK2Unroll];
+      if (MODE == kData) load_rows_full<XH>(x, xh, wbeg, lane, A);
+      for (int64_t base = wbeg; base < full_end; base += kStep) {
+        float4 B[kK2Unroll];
+        if (MODE == kData) {
+          const int64_t nxt = base + kStep < full_end ? base + kStep : base;  // clamp: harmless reload
+          load_rows_full<XH>(x, xh, nxt, lane, B);
         }
-        const uint32_t cn = __builtin_popcount(cflags);
-        const uint64_t b0 = ballot(cn & 1u), b1 = ballot(cn & 2u), b2 = ballot(cn & 4u);
-        if ((b0 | b1 | b2) == 0ull) continue;  // wave-uniform: no candidate in this row
-        uint32_t pos = staged + mask_prefix(b0) + 2u * mask_prefix(b1) + 4u * mask_prefix(b2);
-        staged += (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          if (cflags & (1u << c)) {
-            sm.sv[w][pos] = MODE == kData ? vv[c] : src.val(i + c);
-            sm.si[w][pos] = (uint32_t)(i + c);
-            ++pos;
-          }
-        }
-        if (ballot(mflags != 0u)) {
-          const uint32_t mn = __builtin_popcount(mflags);
-          const uint64_t m0 = ballot(mn & 1u), m1 = ballot(mn & 2u), m2 = ballot(mn & 4u);
-          uint32_t mpos = mcount + mask_prefix(m0) + 2u * mask_prefix(m1) + 4u * mask_prefix(m2);
-          mcount += (uint32_t)(__popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2));
+        for (int u = 0; u < kK2Unroll; ++u)
+          process_row<MODE, XH, false>(src, MODE == kData ? A[u] : make_float4(0.f, 0.f, 0.f, 0.f),
+                                       base + u * 256 + 4 * lane, wend, s_lo, s_hi, sm, w, lane, a, ov, oi);
+        if (MODE == kData) {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            if (mflags & (1u << c)) {
-              if (mpos < kMaybeCap) sm.maybe[w][mpos] = kk[c];
-              ++mpos;
-            }
-          }
-        }
-        if (staged > kStage - 256) {  // flush the stage: coalesced 256-B stores
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          for (uint32_t j = lane; j < staged; j += 64) {
-            ov[flushed + j] = sm.sv[w][j];
-            oi[flushed + j] = sm.si[w][j];
-          }
-          flushed += staged;
-          staged = 0;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          for (int u = 0; u < kK2Unroll; ++u) A[u] = B[u];
         }
       }
-#pragma unroll
-      for (int u = 0; u < kK2Unroll; ++u) A[u] = B[u];
     }
+    // tail (< kStep elements): guarded loads
+    for (int64_t base = full_end; base < wend; base += 256) {
+      const int64_t i = base + 4 * lane;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (MODE == kData) {
+        float t[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) t[c] = (i + c < wend) ? src.val(i + c) : 0.f;
+        v = make_float4(t[0], t[1], t[2], t[3]);
+      }
+      process_row<MODE, XH, true>(src, v, i, wend, s_lo, s_hi, sm, w, lane, a, ov, oi);
+    }
+    // final partial flush (< 256 entries)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (uint32_t j = lane; j < staged; j += 64) {
-      ov[flushed + j] = sm.sv[w][j];
-      oi[flushed + j] = sm.si[w][j];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t j = q * 64 + lane;
+      if (j < a.staged) {
+        ov[a.flushed + j] = sm.sv[w][j];
+        oi[a.flushed + j] = sm.si[w][j];
+      }
     }
-    flushed += staged;
+    const uint32_t flushed = a.flushed + a.staged;
+    const uint32_t mcount = a.mcount;
 
     // ---- end of tile: bucket counts, side list, totals
     if (lane == 0) {
@@ -610,16 +734,26 @@ __global__ __launch_bounds__(kK3Threads) void topk_select_kernel(
   const int per = (nb + kK3Threads - 1) / kK3Threads;
   const int b0 = tid * per;
   uint32_t local = 0;
-  for (int q = 0; q < per; ++q) {
-    const int b = b0 + q;
-    if (b >= (int)nb) break;
-    const uint32_t a = cum_tab[(int64_t)jstar * nb + b];
-    const uint32_t c = cum_tab[(int64_t)(jstar + 1) * nb + b];
-    const uint32_t s = cum_tab[(int64_t)63 * nb + b];
-    fs.A[b] = a - c;   // temporarily: count
-    fs.Bv[b] = c - s;  // side offset of bucket j*
-    fs.Cv[b] = c;
-    local += a - c;
+  {
+    constexpr int PMAX = (kNbMax + kK3Threads - 1) / kK3Threads;
+    uint32_t a[PMAX], c[PMAX], s[PMAX];
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q) {  // unconditional (clamped) loads: all in flight together
+      const int bq = min(b0 + q, (int)nb - 1);
+      a[q] = cum_tab[(int64_t)jstar * nb + bq];
+      c[q] = cum_tab[(int64_t)(jstar + 1) * nb + bq];
+      s[q] = cum_tab[(int64_t)63 * nb + bq];
+    }
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q) {
+      const int b = b0 + q;
+      if (q < per && b < (int)nb) {
+        fs.A[b] = a[q] - c[q];   // temporarily: count
+        fs.Bv[b] = c[q] - s[q];  // side offset of bucket j*
+        fs.Cv[b] = c[q];
+        local += a[q] - c[q];
+      }
+    }
   }
   uint32_t M;
   uint32_t pre = block_excl_scan(local, fs.scratch, &M);
@@ -632,13 +766,35 @@ __global__ __launch_bounds__(kK3Threads) void topk_select_kernel(
   }
   if (tid == 0) fs.A[nb] = M;
   __syncthreads();
-  // gather bucket-j* keys in tile order
-  for (int q = 0; q < per; ++q) {
-    const int b = b0 + q;
-    if (b >= (int)nb) break;
-    const uint32_t st = fs.A[b], cnt = fs.A[b + 1] - st;
-    const uint32_t* sp = side + (int64_t)b * kSideCap + fs.Bv[b];
-    for (uint32_t j = 0; j < cnt; ++j) fs.keys[st + j] = sp[j];
+  // gather bucket-j* keys in tile order: one independent load per key slot
+  // (tile of slot p found by binary search over the LDS prefix array A)
+  {
+    constexpr int G = 8;
+    uint32_t v[G];
+    int dst[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const uint32_t p = tid + (uint32_t)g * kK3Threads;
+      const uint32_t pc = p < M ? p : 0u;  // clamped: the load below is unconditional
+      int lo = 0, hi = (int)nb - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (fs.A[mid] <= pc) lo = mid; else hi = mid - 1;
+      }
+      v[g] = side[(int64_t)lo * kSideCap + fs.Bv[lo] + (pc - fs.A[lo])];
+      dst[g] = p < M ? (int)p : -1;
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      if (dst[g] >= 0) fs.keys[dst[g]] = v[g];
+    for (uint32_t p = tid + G * kK3Threads; p < M; p += kK3Threads) {  // M > 8K: rare
+      int lo = 0, hi = (int)nb - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (fs.A[mid] <= p) lo = mid; else hi = mid - 1;
+      }
+      fs.keys[p] = side[(int64_t)lo * kSideCap + fs.Bv[lo] + (p - fs.A[lo])];
+    }
   }
   __syncthreads();
   // radix select inside the bucket: rel = key - base_j in [0, 2^shift), 8-bit digits
@@ -735,14 +891,15 @@ __global__ __launch_bounds__(kK4Threads) void topk_emit_kernel(
     const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
     int64_t idx_base) {
   __shared__ uint32_t scratch[24];
-  if (ctrl->fallback) return;
   const int64_t b = blockIdx.x;
-  const uint32_t T = ctrl->T, r = ctrl->r;
+  // every control word is independent: issue all loads before the first use
+  const uint32_t fallback = ctrl->fallback, T = ctrl->T, r = ctrl->r;
   uint32_t out = tile_info[b];
   uint32_t tie_run = tile_info[nb + b];
   const uint32_t mode = tile_info[2 * nb + b];
-  uint32_t c0 = cntw[b * kK2Waves + 0], c1 = cntw[b * kK2Waves + 1], c2 = cntw[b * kK2Waves + 2],
-           c3 = cntw[b * kK2Waves + 3];
+  const uint4 cw4 = *reinterpret_cast<const uint4*>(cntw + b * kK2Waves);
+  const uint32_t c0 = cw4.x, c1 = cw4.y, c2 = cw4.z, c3 = cw4.w;
+  if (fallback) return;
   const uint32_t e1 = c0, e2 = e1 + c1, e3 = e2 + c2, tot = e3 + c3;
   const int64_t wlen = tile / kK2Waves;
   const int64_t tb = b * tile;
@@ -827,7 +984,8 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   float* cval = reinterpret_cast<float*>(base + L.off_cval);
   uint32_t* cidx = reinterpret_cast<uint32_t*>(base + L.off_cidx);
   if (MODE == kData) {
-    hipLaunchKernelGGL((topk_sample_kernel<XH>), dim3(1), dim3(kSampleThreads), 0, st, x, xh, n, k, ctrl);
+    uint32_t* k1 = reinterpret_cast<uint32_t*>(base + L.off_k1);
+    hipLaunchKernelGGL((topk_sample_kernel<XH>), dim3(kK1Blocks), dim3(kK1Threads), 0, st, x, xh, n, k, ctrl, k1);
     CHOCO_LAUNCHED("topk_sample_kernel");
   } else {
     // keys uniform on [0, 2^31): P(key >= t) = (2^31 - t) / 2^31
