@@ -46,17 +46,21 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_library(force=False, verbose=False, jobs=None):
-    if not force and not _stale():
+def build_library(force=False, verbose=False, jobs=None, defines=(), lib=None):
+    """Build the codec.  `defines`/`lib` build a diagnostic variant (tools/) into its
+    own object dir and .so; the product library is always the default LIB."""
+    out = lib or LIB
+    if not force and not defines and not _stale():
         return LIB
     hipcc = _hipcc()
-    objdir = os.path.join(PKG, "build_obj")
+    tag = "_".join(d.replace("=", "") for d in defines)
+    objdir = os.path.join(PKG, "build_obj" + ("_" + tag if tag else ""))
     os.makedirs(objdir, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
-        cmd = [hipcc, *HIPCC_FLAGS, "-I", INCLUDE, "-c", src, "-o", obj]
+        cmd = [hipcc, *HIPCC_FLAGS, *[f"-D{d}" for d in defines], "-I", INCLUDE, "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr[-8000:]}")
@@ -68,13 +72,14 @@ def build_library(force=False, verbose=False, jobs=None):
     jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 2)), 8)
     with concurrent.futures.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, srcs))
-    tmp = LIB + ".tmp"
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-8000:]}")
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

@@ -40,33 +40,32 @@ static std::mutex g_prof_mu;
 static std::vector<PendingEv> g_pending;
 static std::map<std::string, std::pair<double, int64_t>> g_acc;
 
-void profile_begin(const char* name, hipStream_t st) {
+static thread_local ProfArm g_armed{nullptr, nullptr};
+
+void profile_begin(const char* name, hipStream_t) {
+  g_armed = ProfArm{nullptr, nullptr};
   if (!g_prof_on.load(std::memory_order_relaxed)) return;
-  PendingEv p{name, nullptr, nullptr, false};
+  PendingEv p{name, nullptr, nullptr, true};
   if (hipEventCreate(&p.a) != hipSuccess || hipEventCreate(&p.b) != hipSuccess) return;
-  (void)hipEventRecord(p.a, st);
+  g_armed = ProfArm{p.a, p.b};
   std::lock_guard<std::mutex> g(g_prof_mu);
   g_pending.push_back(p);
 }
 
-void profile_end(const char* name, hipStream_t st) {
-  if (!g_prof_on.load(std::memory_order_relaxed)) return;
-  std::lock_guard<std::mutex> g(g_prof_mu);
-  for (auto it = g_pending.rbegin(); it != g_pending.rend(); ++it) {
-    if (!it->closed && it->name == name) {
-      (void)hipEventRecord(it->b, st);
-      it->closed = true;
-      return;
-    }
-  }
+void profile_end(const char*, hipStream_t) { g_armed = ProfArm{nullptr, nullptr}; }
+
+ProfArm profile_take() {
+  const ProfArm r = g_armed;
+  g_armed = ProfArm{nullptr, nullptr};
+  return r;
 }
 
 static void profile_drain_locked() {
   for (auto& p : g_pending) {
     if (p.closed) {
       float ms = 0.f;
-      (void)hipEventSynchronize(p.b);
-      if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      // an armed pair that never reached a launch was never recorded: skipped
+      if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
         auto& e = g_acc[p.name];
         e.first += ms;
         e.second += 1;

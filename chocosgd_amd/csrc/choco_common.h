@@ -14,6 +14,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stddef.h>
 
@@ -47,9 +48,22 @@ int check_launch(const char* what);
     if (!(cond)) return ::choco::fail(CHOCO_ERR_INVALID, __VA_ARGS__);      \
   } while (0)
 
-// Optional hipEvent bracketing of a named kernel on its own stream (bench roofline).
+// Optional per-kernel timing (bench roofline).  profile_begin arms a pair of
+// events for the NEXT launch made by this thread; CHOCO_KLAUNCH attaches them to
+// the dispatch itself (hipExtLaunchKernelGGL), so they time the kernel and not
+// whatever is still queued ahead of it on the stream.  profile_end disarms.
+struct ProfArm {
+  hipEvent_t a, b;
+};
 void profile_begin(const char* name, hipStream_t st);
 void profile_end(const char* name, hipStream_t st);
+ProfArm profile_take();
+
+#define CHOCO_KLAUNCH(kernel, grid, block, shm, st, ...)                                     \
+  do {                                                                                      \
+    const ::choco::ProfArm _pa = ::choco::profile_take();                                   \
+    hipExtLaunchKernelGGL(kernel, grid, block, shm, st, _pa.a, _pa.b, 0u, __VA_ARGS__);     \
+  } while (0)
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -75,7 +75,7 @@ CHOCO_API int choco_gossip_step(float* x, const float* memory, const float* xhat
   CHOCO_REQUIRE(n > 0, "n must be positive");
   CHOCO_REQUIRE(aligned16(x) && aligned16(memory) && aligned16(xhat), "buffers must be 16-byte aligned");
   profile_begin("gossip_step", st);
-  hipLaunchKernelGGL(gossip_kernel, dim3(ew_grid(n, 4)), dim3(kEwThreads), 0, st, x, memory, xhat, gamma, n);
+  CHOCO_KLAUNCH(gossip_kernel, dim3(ew_grid(n, 4)), dim3(kEwThreads), 0, st, x, memory, xhat, gamma, n);
   profile_end("gossip_step", st);
   CHOCO_LAUNCHED("gossip_kernel");
   return CHOCO_OK;
@@ -87,7 +87,7 @@ CHOCO_API int choco_sparse_accumulate(const float* val, const int32_t* idx, int6
   CHOCO_REQUIRE(val && idx && memory, "null pointer argument");
   if (k <= 0) return CHOCO_OK;
   profile_begin("sparse_accumulate", st);
-  hipLaunchKernelGGL(sparse_acc_kernel, dim3(ew_grid(k, 1)), dim3(kEwThreads), 0, st, val, idx, k, xhat_self,
+  CHOCO_KLAUNCH(sparse_acc_kernel, dim3(ew_grid(k, 1)), dim3(kEwThreads), 0, st, val, idx, k, xhat_self,
                      memory, weight);
   profile_end("sparse_accumulate", st);
   CHOCO_LAUNCHED("sparse_acc_kernel");
@@ -99,7 +99,7 @@ CHOCO_API int choco_gather(const float* x, const float* xhat, const int64_t* idx
   hipStream_t st = as_stream(stream);
   CHOCO_REQUIRE(x && idx && out_val, "null pointer argument");
   if (k <= 0) return CHOCO_OK;
-  hipLaunchKernelGGL(gather_kernel, dim3(ew_grid(k, 1)), dim3(kEwThreads), 0, st, x, xhat, idx, k, scale, out_val);
+  CHOCO_KLAUNCH(gather_kernel, dim3(ew_grid(k, 1)), dim3(kEwThreads), 0, st, x, xhat, idx, k, scale, out_val);
   CHOCO_LAUNCHED("gather_kernel");
   return CHOCO_OK;
 }

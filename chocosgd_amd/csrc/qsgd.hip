@@ -418,7 +418,7 @@ template <int CW, int NM, int MODE>
 static void launch_decode(const QMsgs& M, int64_t n, const int64_t* seg_off, int nseg, int s_levels, int biased,
                           float* hat, float* mem, hipStream_t st) {
   const unsigned grid = (unsigned)((n + kQTile - 1) / kQTile);
-  hipLaunchKernelGGL((qsgd_decode_kernel<CW, NM, MODE>), dim3(grid), dim3(kQThreads), 0, st, M, n, seg_off, nseg,
+  CHOCO_KLAUNCH((qsgd_decode_kernel<CW, NM, MODE>), dim3(grid), dim3(kQThreads), 0, st, M, n, seg_off, nseg,
                      s_levels, biased, hat, mem);
 }
 
@@ -484,10 +484,10 @@ CHOCO_API int choco_qsgd_compress(const float* x, const float* xhat, int64_t n, 
     QsgdWs* w = static_cast<QsgdWs*>(ws);
     profile_begin("qsgd_norm", st);
     if (xhat)
-      hipLaunchKernelGGL((qsgd_norm_kernel<true>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
+      CHOCO_KLAUNCH((qsgd_norm_kernel<true>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
                          norms_out, w);
     else
-      hipLaunchKernelGGL((qsgd_norm_kernel<false>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
+      CHOCO_KLAUNCH((qsgd_norm_kernel<false>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
                          norms_out, w);
     profile_end("qsgd_norm", st);
     CHOCO_LAUNCHED("qsgd_norm_kernel");
@@ -501,7 +501,7 @@ CHOCO_API int choco_qsgd_compress(const float* x, const float* xhat, int64_t n, 
   profile_begin("qsgd_quantize", st);
 #define CHOCO_Q(CWV)                                                                                         \
   case CWV:                                                                                                  \
-    hipLaunchKernelGGL((qsgd_quant_kernel<CWV>), dim3((unsigned)ntiles), dim3(kQThreads), 0, st, x, xhat, n, \
+    CHOCO_KLAUNCH((qsgd_quant_kernel<CWV>), dim3((unsigned)ntiles), dim3(kQThreads), 0, st, x, xhat, n, \
                        seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane, sign_plane, \
                        dense_out, ntiles);                                                                   \
     break;

@@ -568,17 +568,17 @@ CHOCO_API int choco_sign_compress(const float* x, const float* xhat, int64_t n, 
   profile_begin("sign_pack", st);
   if (xhat) {
     if (l1_norms)
-      hipLaunchKernelGGL((sign_pack_kernel<true, true>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
+      CHOCO_KLAUNCH((sign_pack_kernel<true, true>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
                          seg_off, nseg, pk, l1_norms, w);
     else
-      hipLaunchKernelGGL((sign_pack_kernel<true, false>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
+      CHOCO_KLAUNCH((sign_pack_kernel<true, false>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
                          seg_off, nseg, pk, l1_norms, w);
   } else {
     if (l1_norms)
-      hipLaunchKernelGGL((sign_pack_kernel<false, true>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
+      CHOCO_KLAUNCH((sign_pack_kernel<false, true>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
                          seg_off, nseg, pk, l1_norms, w);
     else
-      hipLaunchKernelGGL((sign_pack_kernel<false, false>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n,
+      CHOCO_KLAUNCH((sign_pack_kernel<false, false>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n,
                          Np, seg_off, nseg, pk, l1_norms, w);
   }
   profile_end("sign_pack", st);
@@ -592,7 +592,7 @@ CHOCO_API int choco_sign_unpack(const int32_t* packed, int64_t n, float* out, vo
   CHOCO_REQUIRE(aligned16(out), "out must be 16-byte aligned");
   const int64_t Np = choco_sign_words(n);
   const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
-  hipLaunchKernelGGL(sign_unpack_kernel, dim3(grid), dim3(kSignThreads), 0, st,
+  CHOCO_KLAUNCH(sign_unpack_kernel, dim3(grid), dim3(kSignThreads), 0, st,
                      reinterpret_cast<const uint32_t*>(packed), n, Np, out);
   CHOCO_LAUNCHED("sign_unpack_kernel");
   return CHOCO_OK;
@@ -626,10 +626,10 @@ CHOCO_API int choco_sign_decompress_accumulate(const int32_t* const* packed_list
 #define CHOCO_SIGN_ACC(NM)                                                                                 \
   case NM:                                                                                                  \
     if (self_slot >= 0 && xhat_self)                                                                        \
-      hipLaunchKernelGGL((sign_accumulate_kernel<NM, true>), dim3(grid), dim3(kSignThreads), 0, st, M, n,   \
+      CHOCO_KLAUNCH((sign_accumulate_kernel<NM, true>), dim3(grid), dim3(kSignThreads), 0, st, M, n,   \
                          Np, seg_off, nseg, xhat_self, memory);                                             \
     else                                                                                                    \
-      hipLaunchKernelGGL((sign_accumulate_kernel<NM, false>), dim3(grid), dim3(kSignThreads), 0, st, M, n,  \
+      CHOCO_KLAUNCH((sign_accumulate_kernel<NM, false>), dim3(grid), dim3(kSignThreads), 0, st, M, n,  \
                          Np, seg_off, nseg, xhat_self, memory);                                             \
     break;
   switch (nmsg) {

@@ -10,32 +10,29 @@
 //   emitted as (d_i, i) in ascending i.
 //
 // Fast path for large n ("pipeline"); the delta is read from HBM ONCE:
-//   K1 topk_sample  : one workgroup histograms a 64K-element strided sample of
-//                     keys (32K bins = key>>16) and picks a candidate floor s_lo
-//                     (#{key >= s_lo} >= k with ~6 sigma margin) and a "sure"
-//                     ceiling s_hi (#{key >= s_hi} < k); [s_lo, s_hi) is split
-//                     into 63 equal key-buckets of width 2^shift.
-//   K2 topk_stream  : persistent streaming pass over 32K-element tiles (4 waves,
-//                     each a contiguous 8K range).  Loads are double-buffered in
-//                     registers; per float4 row the wave ballots candidates
-//                     (key >= s_lo), prefix-counts them with bit-sliced ballots
-//                     + mbcnt and appends (value, index) in index order to an LDS
-//                     stage that is flushed to the wave's slot of the candidate
-//                     buffer in coalesced 256-B stores.  "maybe" candidates
-//                     (key < s_hi) are also kept in LDS and, at the end of the
-//                     tile, counting-sorted by bucket into a per-tile side list;
-//                     per-tile bucket suffix counts go to a [64][nb] table and,
-//                     by one 256-B wave atomic, to replicated global totals.
-//   K3 topk_select  : one workgroup finds the bucket j* holding the k-th key from
-//                     the totals, gathers that bucket's keys (a few thousand)
-//                     from the side lists into LDS, radix-selects T and the tie
-//                     quota exactly and scans per-tile output offsets.
+//   K1 topk_sample  : 64 workgroups histogram a 64K-element strided sample and
+//                     keep their local tails; the last one picks a candidate
+//                     floor s_lo (#{key >= s_lo} >= k with a ~6 sigma margin)
+//                     and a "sure" ceiling s_hi (#{key >= s_hi} < k).
+//                     [s_lo, s_hi) is split into 255 key-buckets of width 2^shift.
+//   K2 topk_stream  : one workgroup per tile (4 waves, each a contiguous range);
+//                     per float4 row the wave ballots candidates (key >= s_lo)
+//                     and appends (value, index) in index order to an LDS ring
+//                     flushed to the wave's slot of the candidate buffer in
+//                     256-B stores.  At the end of the tile the "maybe" keys
+//                     (key < s_hi) are re-read, bucket-counted and counting-sorted
+//                     into a per-tile side list; per-tile bucket suffix counts go
+//                     to a [tile][256] table and to 16 replicated global totals.
+//   K3 topk_select  : one workgroup finds the bucket j* holding the k-th key
+//                     from the totals, copies every tile's bucket-j* keys (a few
+//                     thousand) into LDS, radix-selects T and the tie quota r
+//                     exactly and scans per-tile output offsets.
 //   K4 topk_emit    : one workgroup per tile compacts the tile's candidates into
 //                     the final ascending-index output.
 //   If the sample's guess was off (too few candidates, T in the "sure" range,
-//   bucket j* larger than LDS, or a wave's maybe-list overflowed), K3 runs an
-//   exact single-workgroup radix select over the full input instead (correct,
-//   slow, data-dependent only) and K4 exits.
+//   bucket j* larger than LDS, or a side list overflowed), K3 runs an exact
+//   single-workgroup radix select over the full input instead (correct, slow,
+//   data-dependent only) and K4 exits.
 // Small n (<= kSmallN) and every segment of the batched segmented path use
 // the same exact radix select (block_topk_exact) in one workgroup.
 #include "choco_common.h"
@@ -47,57 +44,90 @@ namespace choco {
 
 constexpr int kK2Threads = 256;
 constexpr int kK2Waves = kK2Threads / 64;
-constexpr int kK2Unroll = 4;            // float4 rows per wave per pipeline stage
-constexpr int kK2BlocksPerCU = 4;
-constexpr int kStage = 512;             // LDS staging entries per wave
-constexpr int kNBucket = 64;            // 63 "maybe" buckets + 1 "sure"
-constexpr int kMaybeCap = 512;          // maybe keys per wave kept in LDS
-constexpr int kSideCap = kK2Waves * kMaybeCap;
-constexpr int kNRep = 8;                // replicas of the global totals (per XCD group)
-constexpr int kNbMax = 4096;            // max tiles (K3 keeps per-tile arrays in LDS)
-constexpr int kMCap = 16384;            // max keys of bucket j* handled in LDS
+// Tuning knobs (tools/build_variants.py builds diagnostic variants of these).
+#ifndef CHOCO_K2_WPE     // stream-kernel waves per SIMD: VGPRs capped at 512 / WPE
+#define CHOCO_K2_WPE 8
+#endif
+#ifndef CHOCO_K2_ABLATE  // diagnostic: 1 no end-of-tile, 2 rows only folded (K3/K4 skipped)
+#define CHOCO_K2_ABLATE 0
+#endif
+#ifndef CHOCO_K2_TARGET  // tiles per launch: 256 CUs x 8 resident workgroups = one balanced round
+#define CHOCO_K2_TARGET 2048
+#endif
+constexpr int kK2Unroll = 4;            // float4 rows per wave per load batch
+constexpr int kK2Wpe = CHOCO_K2_WPE;
+constexpr int64_t kK2Target = CHOCO_K2_TARGET;
+constexpr int64_t kTileQuant = (int64_t)kK2Waves * kK2Unroll * 256;   // 4096 elements
+static_assert(kK2Target <= 2048, "K3 keeps two tiles per thread");
+constexpr int kRing = 512;              // LDS ring entries (value, index) per wave
+constexpr int kFlush = 64;              // ring -> HBM in 64-entry (2 x 256-B store) chunks
+constexpr int kNBucket = 256;           // 255 "maybe" buckets + 1 "sure"
+constexpr int kNMaybe = kNBucket - 1;
+constexpr int kNRep = 16;               // replicas of the global bucket totals
+constexpr int kMCap = 16384;            // max keys of bucket j* selected in LDS
 constexpr int kK3Threads = 1024;
 constexpr int kK4Threads = 256;
 constexpr int kK1Blocks = 64;           // sample workgroups, 1024 samples each
 constexpr int kK1Threads = 256;
-constexpr int kK1ListCap = 256;         // per-workgroup tail-list capacity
 constexpr int kSampleN = kK1Blocks * kK1Threads * 4;   // 65536
 constexpr int kSampleChunk = 256;
 constexpr int64_t kSmallN = 65536;
 constexpr int kExactThreads = 1024;
 
+// Diagnostic phase stamps (tools/stamps.py; never in the product build).
+#ifndef CHOCO_STAMPS
+#define CHOCO_STAMPS 0
+#endif
+#if CHOCO_STAMPS
+constexpr int kStampSlots = 40960;
+__device__ unsigned long long g_stamps[kStampSlots][4];
+#define STAMP(slot, j)                                                      \
+  do {                                                                      \
+    if (threadIdx.x == 0) g_stamps[(slot)][(j)] = wall_clock64();           \
+  } while (0)
+#else
+#define STAMP(slot, j) \
+  do {                 \
+  } while (0)
+#endif
+
 enum SrcMode { kData = 0, kHash = 1 };
 enum TileMode { kTakeNone = 0, kTakeAll = 1, kTakePartial = 2 };
 
 struct TopkCtrl {
-  uint32_t s_lo, s_hi, shift, overflow;
-  uint32_t T, r, fallback, k1_ticket;
+  uint32_t s_lo, s_hi, shift, overflow;          // K1 -> K2
+  uint32_t T, r, fallback, k1_ticket;            // K3 -> K4; K1b's self-resetting ticket
   uint32_t pad[8];
-  uint32_t G[kNRep][kNBucket];
+  uint32_t G[kNRep][kNBucket];                   // replicated bucket suffix totals
 };
 
 struct TopkLayout {
   int64_t n;
-  uint32_t tile, nb;
+  uint32_t tile, nb, side_cap;
   size_t off_ctrl, off_cum, off_cntw, off_side, off_tile, off_k1, off_cval, off_cidx, total;
 };
 
+// Tile = ceil(n / kK2Target) rounded up to 4096 elements, so one launch is one
+// balanced round of resident workgroups.  A tile's side list holds its "maybe"
+// keys: 1/16 of the tile, far above the sample's margin (~12 sqrt(k/n / 65536)
+// of the elements: 0.5 % at k = 1 %, 1.5 % at k = 10 %).
 static TopkLayout topk_layout(int64_t n) {
   TopkLayout L{};
   L.n = n;
-  uint32_t tile = 32768;
-  while ((int64_t)tile * kNbMax < n) tile <<= 1;
-  L.tile = tile;
+  int64_t tile = (n + kK2Target - 1) / kK2Target;
+  tile = std::max<int64_t>(kTileQuant, (tile + kTileQuant - 1) / kTileQuant * kTileQuant);
+  L.tile = (uint32_t)tile;
   L.nb = (uint32_t)((n + tile - 1) / tile);
+  L.side_cap = (uint32_t)std::max<int64_t>(2048, tile / 16);
   size_t o = 0;
-  L.off_ctrl = o; o += align_up(sizeof(TopkCtrl), 256);
-  L.off_cum = o;  o += align_up((size_t)kNBucket * L.nb * 4, 256);
-  L.off_cntw = o; o += align_up((size_t)L.nb * kK2Waves * 4, 256);
-  L.off_side = o; o += align_up((size_t)L.nb * kSideCap * 4, 256);
-  L.off_tile = o; o += align_up((size_t)L.nb * 3 * 4, 256);   // tile_off | tile_tieb | tile_mode
-  L.off_k1 = o;   o += align_up((size_t)(kK1Blocks * kK1ListCap + kK1Blocks) * 4, 256);  // sample tail lists
-  L.off_cval = o; o += align_up((size_t)L.nb * tile * 4, 256);
-  L.off_cidx = o; o += align_up((size_t)L.nb * tile * 4, 256);
+  L.off_ctrl = o;  o += align_up(sizeof(TopkCtrl), 256);
+  L.off_cum = o;   o += align_up((size_t)L.nb * kNBucket * 4, 256);
+  L.off_cntw = o;  o += align_up((size_t)L.nb * kK2Waves * 4, 256);
+  L.off_side = o;  o += align_up((size_t)L.nb * L.side_cap * 4, 256);
+  L.off_tile = o;  o += align_up((size_t)L.nb * 3 * 4, 256);        // tile_off | tile_tieb | tile_mode
+  L.off_k1 = o;    o += align_up((size_t)3 * 2048 * 4, 256);           // sample histograms (K1)
+  L.off_cval = o;  o += align_up((size_t)L.nb * tile * 4, 256);
+  L.off_cidx = o;  o += align_up((size_t)L.nb * tile * 4, 256);
   L.total = o;
   return L;
 }
@@ -260,180 +290,213 @@ __global__ __launch_bounds__(kExactThreads) void topk_segmented_kernel(
 }
 
 // ----------------------------------------------------------------------------
-// K1: sample -> (s_lo, s_hi, shift)
+// K1: sample -> (s_lo, s_hi, shift), two small kernels
 //
-// 64 workgroups each take 1024 samples (4 contiguous 256-element chunks spread
-// over the buffer).  A workgroup keeps only its local tail -- the keys in the
-// coarse (key>>20) bins that hold its top ~4x(expected share) samples -- in a
-// global list; the last workgroup (agent-scope ticket) radix-selects the
-// R_lo-th / R_hi-th largest keys of the union exactly.  Truncating a list can
-// only lower those order statistics, i.e. make s_lo more conservative.
+// 64 workgroups read a 64K-element strided sample (4 contiguous 256-element
+// chunks each).  K1a adds their coarse key histogram (key >> 20, 2048 bins) to
+// a global one.  K1b: every workgroup scans it for the coarse bins holding the
+// R_lo-th / R_hi-th largest sample keys, re-reads its samples and adds a fine
+// histogram (bits 19..9) of the keys in those two bins; the last workgroup
+// (fence-free ticket: the payload is atomics only) resolves both ranks to 512
+// keys -- s_lo rounded down, s_hi rounded up -- and clears the histograms for
+// the next call.  Both bounds are heuristics that K3 verifies (G[0] >= k,
+// G[sure] < k); any k/n works.
 // ----------------------------------------------------------------------------
 CHOCO_DEV void write_params(TopkCtrl* ctrl, uint32_t s_lo, uint64_t s_hi_est) {
-  uint64_t width = s_hi_est > s_lo ? s_hi_est - s_lo : 1;
+  const uint64_t width = s_hi_est > s_lo ? s_hi_est - s_lo : 1;
   uint32_t shift = 0;
-  while ((63ull << shift) < width) ++shift;
-  uint64_t s_hi = (uint64_t)s_lo + (63ull << shift);
+  while (((uint64_t)kNMaybe << shift) < width) ++shift;
+  uint64_t s_hi = (uint64_t)s_lo + ((uint64_t)kNMaybe << shift);
   if (s_hi > 0xFFFFFFFFull) s_hi = 0xFFFFFFFFull;
   ctrl->s_lo = s_lo;
   ctrl->s_hi = (uint32_t)s_hi;
   ctrl->shift = shift;
 }
 
-// rank-th largest (1-based) of keys[0..u) held in LDS; 4 rounds of 8-bit digits.
-CHOCO_DEV uint32_t lds_select_kth(const uint32_t* keys, uint32_t u, uint32_t rank, uint32_t* hist, uint32_t* bc) {
-  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  uint32_t prefix = 0, maskhi = 0, krem = rank;
-  const int shs[4] = {23, 15, 7, 0};
-  const int wds[4] = {8, 8, 8, 7};
-  for (int rd = 0; rd < 4; ++rd) {
-    const int sh = shs[rd];
-    const uint32_t dmask = (1u << wds[rd]) - 1u;
-    for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
-    __syncthreads();
-    for (uint32_t j = tid; j < u; j += blockDim.x) {
-      const uint32_t key = keys[j];
-      if ((key & maskhi) == prefix) atomicAdd(&hist[(key >> sh) & dmask], 1u);
-    }
-    __syncthreads();
-    if (w == 0) {
-      const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
-      const uint32_t loc = h0 + h1 + h2 + h3;
-      const uint32_t rv = __shfl(loc, 63 - lane);
-      const uint32_t inc = wave_incl_scan(rv);
-      const uint32_t suf_incl = __shfl(inc, 63 - lane);
-      const uint32_t above = suf_incl - loc;
-      if (above < krem && krem <= suf_incl) {
-        uint32_t acc = above;
-        const uint32_t hs[4] = {h0, h1, h2, h3};
-        for (int t = 3; t >= 0; --t) {
-          if (acc + hs[t] >= krem) { bc[0] = 4 * lane + t; bc[1] = krem - acc; break; }
-          acc += hs[t];
-        }
-      }
-    }
-    __syncthreads();
-    prefix |= bc[0] << sh;
-    maskhi |= dmask << sh;
-    krem = bc[1];
-    __syncthreads();
-  }
-  return prefix;
+CHOCO_DEV uint32_t ld_agent(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+CHOCO_DEV void st_agent(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-struct SampleSmem {
-  uint32_t hist[2048];
-  uint32_t keys[kK1Blocks * kK1ListCap];
-  uint32_t scratch[24];
-  uint32_t bc[4];
-  uint32_t flag;
+// Wave 0 of a workgroup: over a 256-bin LDS histogram (ascending value order),
+// find the bin holding the rank-th largest entry; returns (bin, rank inside bin)
+// via out[0], out[1].  Other waves must not call.
+CHOCO_DEV void wave_find_bin(const uint32_t* hist, uint32_t rank, uint32_t* out) {
+  const int lane = lane_id();
+  const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
+  const uint32_t loc = h0 + h1 + h2 + h3;
+  const uint32_t rv = __shfl(loc, 63 - lane);
+  const uint32_t inc = wave_incl_scan(rv);
+  const uint32_t suf_incl = __shfl(inc, 63 - lane);  // entries in bins >= 4*lane
+  const uint32_t above = suf_incl - loc;
+  if (above < rank && rank <= suf_incl) {
+    uint32_t acc = above;
+    const uint32_t hs[4] = {h0, h1, h2, h3};
+    for (int t = 3; t >= 0; --t) {
+      if (acc + hs[t] >= rank) { out[0] = 4 * lane + t; out[1] = rank - acc; break; }
+      acc += hs[t];
+    }
+  }
+}
+
+// Workgroup-wide: over hist[2048] in LDS (ascending value order), the bin holding
+// the rank-th largest entry and the rank inside it -> out[0], out[1].  Every
+// thread of the (kK1Threads) workgroup must call.
+CHOCO_DEV void block_find_bin2048(const uint32_t* hist, uint32_t rank, uint32_t* scratch, uint32_t* out) {
+  const int tid = threadIdx.x;
+  constexpr int per = 2048 / kK1Threads;
+  uint32_t hv[per];
+  uint32_t local = 0;
+#pragma unroll
+  for (int j = 0; j < per; ++j) {
+    hv[j] = hist[tid * per + j];
+    local += hv[j];
+  }
+  uint32_t total;
+  const uint32_t pre = block_excl_scan(local, scratch, &total);
+  const uint32_t above = total - pre - local;  // entries in bins above my chunk
+  if (above < rank && rank <= above + local) {
+    uint32_t acc = above;
+#pragma unroll
+    for (int j = per - 1; j >= 0; --j) {
+      if (acc < rank && rank <= acc + hv[j]) { out[0] = (uint32_t)(tid * per + j); out[1] = rank - acc; }
+      acc += hv[j];
+    }
+  }
+  __syncthreads();
+}
+
+struct SampleRanks {
+  uint32_t lo, hi;  // 1-based ranks from the top; 0 = none
 };
 
+// Ranks of the candidate floor / sure ceiling in the 64K sample (~6 sigma margins).
+CHOCO_DEV SampleRanks sample_ranks(int64_t n, int64_t k) {
+  const double m = (double)kSampleN;
+  const double e = (double)k / (double)n * m;
+  const double sd = sqrt(e);
+  const double rlo = ceil(e + 6.0 * sd + 4.0);
+  const double rhi = floor(e - 6.0 * sd - 4.0);
+  SampleRanks r;
+  r.lo = rlo <= m ? (uint32_t)rlo : 0u;  // 0: every key is a candidate
+  r.hi = rhi >= 1.0 ? (uint32_t)rhi : 0u;  // 0: no key is "sure"
+  return r;
+}
+
 template <bool XH>
-__global__ __launch_bounds__(kK1Threads) void topk_sample_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k,
-    TopkCtrl* __restrict__ ctrl, uint32_t* __restrict__ lists) {
-  __shared__ SampleSmem sm;
-  uint32_t* __restrict__ counts = lists + kK1Blocks * kK1ListCap;
-  const int tid = threadIdx.x;
-  for (int i = tid; i < 2048; i += kK1Threads) sm.hist[i] = 0;
-  // this thread's 4 samples: float4 s of chunk s/64 (64 float4 per 256-element chunk)
+CHOCO_DEV void load_sample(const float* __restrict__ x, const float* __restrict__ xh, int64_t n, uint32_t kk[4]) {
   constexpr int nchunk = kSampleN / kSampleChunk;
   const int64_t stride4 = ((n - kSampleChunk) / (nchunk - 1)) >> 2;
-  const int s = blockIdx.x * kK1Threads + tid;
-  const int64_t q = (int64_t)(s / 64) * stride4 + (s % 64);
+  const int s = blockIdx.x * kK1Threads + threadIdx.x;
+  const int64_t q = (int64_t)(s / 64) * stride4 + (s % 64);  // float4 s%64 of chunk s/64
   float4 v = reinterpret_cast<const float4*>(x)[q];
   if (XH) {
     const float4 h = reinterpret_cast<const float4*>(xh)[q];
     v.x -= h.x; v.y -= h.y; v.z -= h.z; v.w -= h.w;
   }
-  const uint32_t kk[4] = {fkey(v.x), fkey(v.y), fkey(v.z), fkey(v.w)};
+  kk[0] = fkey(v.x); kk[1] = fkey(v.y); kk[2] = fkey(v.z); kk[3] = fkey(v.w);
+}
+
+// K1a: global coarse histogram of the sample (hist = [coarse 2048 | fine lo 2048 | fine hi 2048]).
+template <bool XH>
+__global__ __launch_bounds__(kK1Threads) void topk_sample_hist_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[2048];
+  const int tid = threadIdx.x;
+  STAMP(blockIdx.x, 0);
+  for (int i = tid; i < 2048; i += kK1Threads) h[i] = 0;
+  uint32_t kk[4];
+  load_sample<XH>(x, xh, n, kk);
   __syncthreads();
 #pragma unroll
-  for (int c = 0; c < 4; ++c) atomicAdd(&sm.hist[kk[c] >> 20], 1u);
+  for (int c = 0; c < 4; ++c) atomicAdd(&h[kk[c] >> 20], 1u);
   __syncthreads();
-  // local cutoff: highest coarse bin whose suffix count reaches m_b
-  const double eb = (double)k / (double)n * (double)(kK1Threads * 4);
-  const uint32_t m_b = (uint32_t)fmin(4.0 * eb + 16.0, (double)(kK1Threads * 4));
-  {
-    uint32_t local = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) local += sm.hist[tid * 8 + j];
-    uint32_t total;
-    const uint32_t pre = block_excl_scan(local, sm.scratch, &total);
-    const uint32_t above = total - pre - local;
-    if (above < m_b && m_b <= above + local) {
-      uint32_t acc = above;
-      for (int j = 7; j >= 0; --j) {
-        acc += sm.hist[tid * 8 + j];
-        if (acc >= m_b) { sm.bc[0] = (uint32_t)(tid * 8 + j); break; }
-      }
-    }
-    __syncthreads();
+  for (int i = tid; i < 2048; i += kK1Threads) {
+    const uint32_t v = h[i];
+    if (v) atomicAdd(&hist[i], v);
   }
-  const uint32_t cut = sm.bc[0];
-  uint32_t mine = 0;
+  STAMP(blockIdx.x, 1);
+}
+
+struct BoundsSmem {
+  uint32_t h[2048];
+  uint32_t f[2][2048];
+  uint32_t scratch[24];
+  uint32_t bc[8];
+  uint32_t flag;
+};
+
+// K1b: fine histograms inside the two coarse bins, then the bounds.
+template <bool XH>
+__global__ __launch_bounds__(kK1Threads) void topk_sample_bounds_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k,
+    TopkCtrl* __restrict__ ctrl, uint32_t* __restrict__ hist) {
+  __shared__ BoundsSmem sm;
+  const int tid = threadIdx.x;
+  uint32_t* __restrict__ fine_lo = hist + 2048;
+  uint32_t* __restrict__ fine_hi = hist + 4096;
+  const SampleRanks R = sample_ranks(n, k);
+  uint32_t kk[4];
+  load_sample<XH>(x, xh, n, kk);
+  {
+    constexpr int per = 2048 / kK1Threads;
+    uint32_t hv[per];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) mine += (kk[c] >> 20) >= cut;
-  uint32_t tot;
-  uint32_t pos = block_excl_scan(mine, sm.scratch, &tot);
-  uint32_t* __restrict__ my = lists + blockIdx.x * kK1ListCap;
+    for (int j = 0; j < per; ++j) hv[j] = hist[tid + j * kK1Threads];  // written by K1a
+#pragma unroll
+    for (int j = 0; j < per; ++j) sm.h[tid + j * kK1Threads] = hv[j];
+  }
+  if (tid < 8) sm.bc[tid] = 0;
+  __syncthreads();
+  if (R.lo) block_find_bin2048(sm.h, R.lo, sm.scratch, sm.bc);
+  if (R.hi) block_find_bin2048(sm.h, R.hi, sm.scratch, sm.bc + 2);
+  const uint32_t c_lo = sm.bc[0], c_hi = sm.bc[2];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    if ((kk[c] >> 20) >= cut) {
-      if (pos < kK1ListCap) my[pos] = kk[c];
-      ++pos;
-    }
+    if (R.lo && (kk[c] >> 20) == c_lo) atomicAdd(&fine_lo[(kk[c] >> 9) & 2047u], 1u);
+    if (R.hi && (kk[c] >> 20) == c_hi) atomicAdd(&fine_hi[(kk[c] >> 9) & 2047u], 1u);
   }
-  if (tid == 0) counts[blockIdx.x] = min(tot, (uint32_t)kK1ListCap);
-  if (!last_block_ticket(&ctrl->k1_ticket, gridDim.x, &sm.flag)) return;
+  STAMP(blockIdx.x, 2);
+  const bool last = last_block_ticket_atomics(&ctrl->k1_ticket, gridDim.x, &sm.flag);
+  STAMP(blockIdx.x, 3);
+  if (!last) return;
 
-  // ---- last workgroup: exact order statistics of the union
-  // all counts in parallel, then one independent load per key slot
-  const uint32_t myc = tid < kK1Blocks ? counts[tid] : 0u;
-  uint32_t u;
-  const uint32_t mystart = block_excl_scan(myc, sm.scratch, &u);
+  // ---- last workgroup: resolve both ranks inside their coarse bins (one load round)
+  uint32_t s_lo = 0;
+  uint64_t s_hi_est = 0x80000000ull;  // above every key: nothing is "sure"
   {
-    // list starts in LDS (hist reused), then key slot p -> (list, offset) by binary search;
-    // G unconditional loads per thread in flight (clamped slot when p >= u)
-    if (tid < kK1Blocks) sm.hist[tid] = mystart;
-    __syncthreads();
-    constexpr int G = 16;
-    for (uint32_t base = 0; base < u; base += G * kK1Threads) {
-      uint32_t v[G];
-      int dst[G];
+    constexpr int per = 2048 / kK1Threads;
+    uint32_t fa[per], fb[per];
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const uint32_t p = base + (uint32_t)g * kK1Threads + tid;
-        const uint32_t pc = p < u ? p : 0u;
-        int lo = 0, hi = kK1Blocks - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (sm.hist[mid] <= pc) lo = mid; else hi = mid - 1;
-        }
-        v[g] = lists[lo * kK1ListCap + (pc - sm.hist[lo])];
-        dst[g] = p < u ? (int)p : -1;
-      }
+    for (int j = 0; j < per; ++j) {
+      fa[j] = R.lo ? ld_agent(&fine_lo[tid + j * kK1Threads]) : 0u;
+      fb[j] = R.hi ? ld_agent(&fine_hi[tid + j * kK1Threads]) : 0u;
+    }
 #pragma unroll
-      for (int g = 0; g < G; ++g)
-        if (dst[g] >= 0) sm.keys[dst[g]] = v[g];
+    for (int j = 0; j < per; ++j) {
+      sm.f[0][tid + j * kK1Threads] = fa[j];
+      sm.f[1][tid + j * kK1Threads] = fb[j];
     }
   }
-  for (int i = tid; i < kNRep * kNBucket; i += kK1Threads) (&ctrl->G[0][0])[i] = 0;
   __syncthreads();
-  const double m = (double)kSampleN;
-  const double e = (double)k / (double)n * m;
-  const double sd = sqrt(e);
-  const double rlo_d = ceil(e + 6.0 * sd + 4.0);
-  const double rhi_d = floor(e - 6.0 * sd - 4.0);
-  uint32_t s_lo = 0;
-  if (rlo_d <= (double)u) s_lo = lds_select_kth(sm.keys, u, (uint32_t)rlo_d, sm.hist, sm.bc);
-  uint64_t s_hi_est = 0x80000000ull;  // above every key: nothing is "sure"
-  if (rhi_d >= 1.0 && rhi_d <= (double)u) s_hi_est = (uint64_t)lds_select_kth(sm.keys, u, (uint32_t)rhi_d, sm.hist, sm.bc) + 1;
+  if (R.lo) {
+    block_find_bin2048(sm.f[0], sm.bc[1], sm.scratch, sm.bc + 4);
+    s_lo = (c_lo << 20) | (sm.bc[4] << 9);                                  // rounded down
+  }
+  if (R.hi) {
+    block_find_bin2048(sm.f[1], sm.bc[3], sm.scratch, sm.bc + 6);
+    s_hi_est = (uint64_t)((c_hi << 20) | (sm.bc[6] << 9)) + 512u;            // rounded up
+  }
+  STAMP(64, 0);
+  // clear the histograms and the bucket totals for K2 / the next call
+  for (int i = tid; i < 3 * 2048; i += kK1Threads) hist[i] = 0;
+  for (int i = tid; i < kNRep * kNBucket; i += kK1Threads) (&ctrl->G[0][0])[i] = 0;
   if (tid == 0) {
     ctrl->overflow = 0;
     write_params(ctrl, s_lo, s_hi_est);
-    __hip_atomic_store(&ctrl->k1_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_agent(&ctrl->k1_ticket, 0u);
   }
 }
 
@@ -444,20 +507,22 @@ __global__ void topk_set_params_kernel(TopkCtrl* __restrict__ ctrl, uint32_t s_l
 }
 
 // ----------------------------------------------------------------------------
-// K2: persistent streaming candidate compaction
+// K2: streaming candidate compaction, one workgroup per tile
+//
+// Sized for occupancy rather than software pipelining: 16.6 KB of LDS and
+// <= 64 VGPRs per thread let 8 workgroups (32 waves) share a CU, so ~128 KB of
+// loads per CU are in flight while the waves that own them compute.
 // ----------------------------------------------------------------------------
 struct StreamSmem {
-  float sv[kK2Waves][kStage];
-  uint32_t si[kK2Waves][kStage];
-  uint32_t maybe[kK2Waves][kMaybeCap];
-  uint32_t hist[kNBucket];
-  uint32_t cur[kNBucket];
+  uint2 ring[kK2Waves][kRing];  // (value bits, index) per wave, in index order
+  uint2 trash[kK2Waves][64];    // per-lane sink of the branch-free stage writes
+  uint32_t hist[kNBucket];      // maybe-key bucket counts, then counting-sort cursors
   uint32_t cnt[kK2Waves];
-  uint32_t mcnt[kK2Waves];
+  uint32_t scratch[8];
 };
 
-// Unconditional (branch-free) float4 loads of kK2Unroll rows: keeps the
-// compiler's vmcnt accounting exact so the prefetch stays in flight.
+// Unconditional float4 loads of kK2Unroll rows (no branch around a load: the
+// compiler's vmcnt accounting stays exact and all rows are in flight together).
 template <bool XH>
 CHOCO_DEV void load_rows_full(const float* __restrict__ x, const float* __restrict__ xh, int64_t base, int lane,
                               float4 (&r)[kK2Unroll]) {
@@ -472,221 +537,208 @@ CHOCO_DEV void load_rows_full(const float* __restrict__ x, const float* __restri
   }
 }
 
-// Per-wave compaction state (all wave-uniform).
-struct WaveAcc {
-  uint32_t flushed, staged, mcount;
-};
-
-// Flush exactly 256 staged candidates as 4 coalesced 256-B stores per array,
-// then move the (< 256) remainder to the front of the stage.
-CHOCO_DEV void flush256(StreamSmem& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
-                        uint32_t* __restrict__ oi) {
+CHOCO_DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  float fv[4];
-  uint32_t fi[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    fv[q] = sm.sv[w][q * 64 + lane];
-    fi[q] = sm.si[w][q * 64 + lane];
-  }
-  const uint32_t rem = a.staged - 256;
-  float rv[4];
-  uint32_t ri[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t j = q * 64 + lane;
-    rv[q] = j < rem ? sm.sv[w][256 + j] : 0.f;
-    ri[q] = j < rem ? sm.si[w][256 + j] : 0u;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t j = q * 64 + lane;
-    if (j < rem) {
-      sm.sv[w][j] = rv[q];
-      sm.si[w][j] = ri[q];
-    }
-    ov[a.flushed + j] = fv[q];
-    oi[a.flushed + j] = fi[q];
-  }
-  a.flushed += 256;
-  a.staged = rem;
 }
 
-// One float4 row per lane (256 elements per wave): ballot candidates into the stage.
+// Per-wave compaction state (wave-uniform): entries appended / written out.
+struct WaveAcc {
+  uint32_t staged, flushed;
+};
+
+// Write whole 64-entry chunks of the ring out (one 256-B store per array each).
+// The ring never holds more than 63 + 256 entries, so nothing is overwritten
+// before it is flushed.  Counters are wave-uniform; readfirstlane keeps them in
+// SGPRs so the flush test is a scalar branch.
+CHOCO_DEV void ring_flush(StreamSmem& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
+                          uint32_t* __restrict__ oi) {
+  wave_sync();
+  const uint32_t end = __builtin_amdgcn_readfirstlane(a.staged) & ~(uint32_t)(kFlush - 1);
+#pragma unroll 1
+  for (uint32_t f = __builtin_amdgcn_readfirstlane(a.flushed); f < end; f += kFlush) {
+    const uint2 e = sm.ring[w][(f + lane) & (kRing - 1)];
+    ov[f + lane] = __uint_as_float(e.x);
+    oi[f + lane] = e.y;
+  }
+  a.flushed = end;
+}
+
+// One float4 row per lane (256 elements per wave): append candidates to the ring.
+// Branch-free per lane: one ballot per component gives the lane prefix
+// (4 x mbcnt); every lane then writes its (value, index) pair either to its ring
+// slot or to its own trash slot, so the only branches are wave-uniform.
 template <int MODE, bool XH, bool GUARD>
 CHOCO_DEV void process_row(const Src<MODE, XH>& src, const float4 v4, int64_t i, int64_t wend, uint32_t s_lo,
-                           uint32_t s_hi, StreamSmem& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
+                           StreamSmem& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
                            uint32_t* __restrict__ oi) {
   const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
-  uint32_t kk[4];
-  uint32_t cflags = 0, mflags = 0;
+#if CHOCO_K2_ABLATE == 2
+  a.staged ^= __builtin_amdgcn_readfirstlane(fkey(vv[0]) ^ fkey(vv[1]) ^ fkey(vv[2]) ^ fkey(vv[3])) & 1u;
+  return;
+#endif
+  bool cand[4];
+  uint64_t m[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const bool valid = !GUARD || i + c < wend;
     const uint32_t key = MODE == kData ? fkey(vv[c]) : (valid ? src.key_of(i + c, 0.f) : 0u);
-    kk[c] = key;
-    const bool cand = valid && key >= s_lo;
-    cflags |= (cand ? 1u : 0u) << c;
-    mflags |= ((cand && key < s_hi) ? 1u : 0u) << c;
+    cand[c] = valid && key >= s_lo;
+    m[c] = ballot(cand[c]);
   }
-  const uint32_t cn = __builtin_popcount(cflags);
-  const uint64_t b0 = ballot(cn & 1u), b1 = ballot(cn & 2u), b2 = ballot(cn & 4u);
-  if ((b0 | b1 | b2) == 0ull) return;  // wave-uniform: no candidate in this row
-  uint32_t pos = a.staged + mask_prefix(b0) + 2u * mask_prefix(b1) + 4u * mask_prefix(b2);
-  a.staged += (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+  if ((m[0] | m[1] | m[2] | m[3]) == 0ull) return;  // wave-uniform: no candidate in this row
+  uint32_t pos = a.staged + mask_prefix(m[0]) + mask_prefix(m[1]) + mask_prefix(m[2]) + mask_prefix(m[3]);
+  a.staged += (uint32_t)(__popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]));
+  uint2* __restrict__ ring = sm.ring[w];
+  uint2* __restrict__ sink = &sm.trash[w][lane];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    if (cflags & (1u << c)) {
-      sm.sv[w][pos] = MODE == kData ? vv[c] : src.val(i + c);
-      sm.si[w][pos] = (uint32_t)(i + c);
-      ++pos;
+    if (m[c] != 0ull) {  // wave-uniform
+      const float v = MODE == kData ? vv[c] : (cand[c] ? src.val(i + c) : 0.f);
+      uint2* dst = cand[c] ? ring + (pos & (kRing - 1)) : sink;
+      *dst = make_uint2(__float_as_uint(v), (uint32_t)(i + c));
+      pos += cand[c] ? 1u : 0u;
     }
   }
-  if (ballot(mflags != 0u)) {
-    const uint32_t mn = __builtin_popcount(mflags);
-    const uint64_t m0 = ballot(mn & 1u), m1 = ballot(mn & 2u), m2 = ballot(mn & 4u);
-    uint32_t mpos = a.mcount + mask_prefix(m0) + 2u * mask_prefix(m1) + 4u * mask_prefix(m2);
-    a.mcount += (uint32_t)(__popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2));
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (mflags & (1u << c)) {
-        if (mpos < kMaybeCap) sm.maybe[w][mpos] = kk[c];
-        ++mpos;
-      }
-    }
-  }
-  if (a.staged >= 256) flush256(sm, w, lane, a, ov, oi);
+  a.staged = __builtin_amdgcn_readfirstlane(a.staged);
+  if (a.staged - a.flushed >= (uint32_t)kFlush) ring_flush(sm, w, lane, a, ov, oi);
+}
+
+// Key of candidate j of this wave's run, re-read from the run just written (L2).
+template <int MODE>
+CHOCO_DEV uint32_t cand_key(const float* __restrict__ ov, const uint32_t* __restrict__ oi, uint32_t j,
+                            uint64_t seed) {
+  return MODE == kData ? fkey(ov[j]) : (rank_hash(seed, oi[j]) >> 1);
 }
 
 template <int MODE, bool XH>
-__global__ __launch_bounds__(kK2Threads) void topk_stream_kernel(
+__global__ __launch_bounds__(kK2Threads, XH ? kK2Wpe - 2 : kK2Wpe) void topk_stream_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, uint32_t tile, uint32_t nb,
-    uint64_t seed, TopkCtrl* __restrict__ ctrl, uint32_t* __restrict__ cum_tab,
+    uint32_t side_cap, uint64_t seed, TopkCtrl* __restrict__ ctrl, uint32_t* __restrict__ cum_tab,
     uint32_t* __restrict__ cntw, uint32_t* __restrict__ side, float* __restrict__ cval,
     uint32_t* __restrict__ cidx) {
   __shared__ StreamSmem sm;
+  STAMP(1024 + blockIdx.x, 0);
   const uint32_t s_lo = ctrl->s_lo, s_hi = ctrl->s_hi, shift = ctrl->shift;
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
+  const int64_t b = blockIdx.x;
   const int64_t wlen = tile / kK2Waves;
   constexpr int64_t kStep = 256 * kK2Unroll;
   Src<MODE, XH> src{x, xh, seed};
 
-  for (int64_t b = blockIdx.x; b < (int64_t)nb; b += gridDim.x) {
-    const int64_t wbeg = b * tile + w * wlen;
-    const int64_t wend = min(wbeg + wlen, n);
-    float* __restrict__ ov = cval + wbeg;
-    uint32_t* __restrict__ oi = cidx + wbeg;
-    WaveAcc a{0u, 0u, 0u};
-    const int64_t full_end = wend > wbeg ? wbeg + (wend - wbeg) / kStep * kStep : wbeg;
+  const int64_t wbeg = b * tile + w * wlen;
+  const int64_t wend = min(wbeg + wlen, n);
+  float* __restrict__ ov = cval + wbeg;
+  uint32_t* __restrict__ oi = cidx + wbeg;
+  WaveAcc a{0u, 0u};
+  const int64_t full_end = wend > wbeg ? wbeg + (wend - wbeg) / kStep * kStep : wbeg;
+  for (int64_t base = wbeg; base < full_end; base += kStep) {
+    float4 A[kK2Unroll];
+    if (MODE == kData) load_rows_full<XH>(x, xh, base, lane, A);
+#pragma unroll
+    for (int u = 0; u < kK2Unroll; ++u)
+      process_row<MODE, XH, false>(src, MODE == kData ? A[u] : make_float4(0.f, 0.f, 0.f, 0.f),
+                                   base + u * 256 + 4 * lane, wend, s_lo, sm, w, lane, a, ov, oi);
+  }
+  // tail (< kStep elements, last tile only): guarded loads
+  for (int64_t base = full_end; base < wend; base += 256) {
+    const int64_t i = base + 4 * lane;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (MODE == kData) {
+      float t[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) t[c] = (i + c < wend) ? src.val(i + c) : 0.f;
+      v = make_float4(t[0], t[1], t[2], t[3]);
+    }
+    process_row<MODE, XH, true>(src, v, i, wend, s_lo, sm, w, lane, a, ov, oi);
+  }
+  // final partial chunk (< 64 entries)
+  wave_sync();
+  if (a.flushed + lane < a.staged) {
+    const uint2 e = sm.ring[w][(a.flushed + lane) & (kRing - 1)];
+    ov[a.flushed + lane] = __uint_as_float(e.x);
+    oi[a.flushed + lane] = e.y;
+  }
+  const uint32_t cnt = a.staged;
+  STAMP(1024 + b, 1);
+#if CHOCO_K2_ABLATE == 1
+  return;
+#endif
 
-    // main loop: whole kStep blocks, double-buffered unconditional loads
-    if (full_end > wbeg) {
-      float4 A[kK2Unroll];
-      if (MODE == kData) load_rows_full<XH>(x, xh, wbeg, lane, A);
-      for (int64_t base = wbeg; base < full_end; base += kStep) {
-        float4 B[kK2Unroll];
-        if (MODE == kData) {
-          const int64_t nxt = base + kStep < full_end ? base + kStep : base;  // clamp: harmless reload
-          load_rows_full<XH>(x, xh, nxt, lane, B);
-        }
-#pragma unroll
-        for (int u = 0; u < kK2Unroll; ++u)
-          process_row<MODE, XH, false>(src, MODE == kData ? A[u] : make_float4(0.f, 0.f, 0.f, 0.f),
-                                       base + u * 256 + 4 * lane, wend, s_lo, s_hi, sm, w, lane, a, ov, oi);
-        if (MODE == kData) {
-#pragma unroll
-          for (int u = 0; u < kK2Unroll; ++u) A[u] = B[u];
-        }
-      }
-    }
-    // tail (< kStep elements): guarded loads
-    for (int64_t base = full_end; base < wend; base += 256) {
-      const int64_t i = base + 4 * lane;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (MODE == kData) {
-        float t[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) t[c] = (i + c < wend) ? src.val(i + c) : 0.f;
-        v = make_float4(t[0], t[1], t[2], t[3]);
-      }
-      process_row<MODE, XH, true>(src, v, i, wend, s_lo, s_hi, sm, w, lane, a, ov, oi);
-    }
-    // final partial flush (< 256 entries)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // ---- end of tile: bucket counts of the "maybe" keys (s_lo <= key < s_hi),
+  // read back from the run this wave just wrote; then counting-sort them into
+  // the tile's side list (buckets from high to low).
+  if (lane == 0) sm.cnt[w] = cnt;
+  sm.hist[threadIdx.x] = 0;  // 256 threads <-> 256 buckets
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  for (uint32_t j0 = 0; j0 < cnt; j0 += 256) {
+    uint32_t kk[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const uint32_t j = q * 64 + lane;
-      if (j < a.staged) {
-        ov[a.flushed + j] = sm.sv[w][j];
-        oi[a.flushed + j] = sm.si[w][j];
-      }
+      const uint32_t j = j0 + q * 64 + lane;
+      kk[q] = cand_key<MODE>(ov, oi, j < cnt ? j : 0u, seed);
     }
-    const uint32_t flushed = a.flushed + a.staged;
-    const uint32_t mcount = a.mcount;
-
-    // ---- end of tile: bucket counts, side list, totals
-    if (lane == 0) {
-      sm.cnt[w] = flushed;
-      sm.mcnt[w] = mcount;
-      if (mcount > kMaybeCap) atomicOr(&ctrl->overflow, 1u);
-    }
-    if (threadIdx.x < kNBucket) sm.hist[threadIdx.x] = 0;
-    __syncthreads();
-    {
-      const uint32_t mc = min(sm.mcnt[w], (uint32_t)kMaybeCap);
-      for (uint32_t j = lane; j < mc; j += 64) atomicAdd(&sm.hist[(sm.maybe[w][j] - s_lo) >> shift], 1u);
-    }
-    uint32_t csum = 0, msum = 0;
 #pragma unroll
-    for (int ww = 0; ww < kK2Waves; ++ww) {
-      csum += sm.cnt[ww];
-      msum += min(sm.mcnt[ww], (uint32_t)kMaybeCap);
+    for (int q = 0; q < 4; ++q)
+      if (j0 + q * 64 + lane < cnt && kk[q] < s_hi) atomicAdd(&sm.hist[(kk[q] - s_lo) >> shift], 1u);
+  }
+  __syncthreads();
+  STAMP(1024 + b, 2);
+  {
+    // thread t <-> maybe bucket jb = 254 - t (t = 255: the "sure" bucket 255);
+    // cum[j] = #candidates with bucket >= j, sure included
+    const int t = threadIdx.x;
+    const int jb = t < kNMaybe ? kNMaybe - 1 - t : kNMaybe;
+    const uint32_t hv = t < kNMaybe ? sm.hist[jb] : 0u;
+    uint32_t msum;
+    const uint32_t above = block_excl_scan(hv, sm.scratch, &msum);  // maybe keys in buckets > jb
+    const uint32_t csum = sm.cnt[0] + sm.cnt[1] + sm.cnt[2] + sm.cnt[3];
+    const uint32_t sure = csum - msum;
+    if (t == 0 && msum > side_cap) atomicOr(&ctrl->overflow, 1u);
+    const uint32_t cum = t < kNMaybe ? sure + above + hv : sure;
+    cum_tab[b * kNBucket + jb] = cum;
+    atomicAdd(&ctrl->G[b & (kNRep - 1)][jb], cum);
+    if (t < kNMaybe) sm.hist[jb] = above;  // counting-sort cursor of bucket jb (hist is dead now)
+    if (t < kK2Waves) cntw[b * kK2Waves + t] = sm.cnt[t];
+  }
+  __syncthreads();
+  uint32_t* __restrict__ sd = side + b * side_cap;
+  for (uint32_t j0 = 0; j0 < cnt; j0 += 256) {
+    uint32_t kk[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t j = j0 + q * 64 + lane;
+      kk[q] = cand_key<MODE>(ov, oi, j < cnt ? j : 0u, seed);
     }
-    __syncthreads();
-    if (w == 0) {
-      // bucket 63 = sure; cum[j] = sum_{i >= j} cnt[i]
-      const uint32_t c = (lane == 63) ? (csum - msum) : sm.hist[lane];
-      const uint32_t rv = __shfl(c, 63 - lane);
-      const uint32_t inc = wave_incl_scan(rv);
-      const uint32_t cum = __shfl(inc, 63 - lane);
-      cum_tab[(int64_t)lane * nb + b] = cum;
-      atomicAdd(&ctrl->G[b & (kNRep - 1)][lane], cum);
-      const uint32_t cum_next = __shfl_down(cum, 1);
-      const uint32_t sure = __shfl(cum, 63);
-      if (lane < 63) sm.cur[lane] = cum_next - sure;   // counting-sort cursor of bucket `lane`
-      if (lane < kK2Waves) cntw[b * kK2Waves + lane] = sm.cnt[lane];
-    }
-    __syncthreads();
-    {
-      uint32_t* __restrict__ sd = side + b * kSideCap;
-      const uint32_t mc = min(sm.mcnt[w], (uint32_t)kMaybeCap);
-      for (uint32_t j = lane; j < mc; j += 64) {
-        const uint32_t key = sm.maybe[w][j];
-        const uint32_t p = atomicAdd(&sm.cur[(key - s_lo) >> shift], 1u);
-        sd[p] = key;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (j0 + q * 64 + lane < cnt && kk[q] < s_hi) {
+        const uint32_t p = atomicAdd(&sm.hist[(kk[q] - s_lo) >> shift], 1u);
+        if (p < side_cap) sd[p] = kk[q];
       }
     }
-    __syncthreads();  // LDS is reused by the next tile
   }
+  STAMP(1024 + b, 3);
 }
 
 // ----------------------------------------------------------------------------
-// K3: exact threshold, tie quota and per-tile output offsets (one workgroup)
+// K3: exact threshold T, tie quota r and per-tile output offsets (one workgroup)
+//
+// Latency-bound, so organised around three dependent global round trips: the
+// replicated bucket totals (-> bucket j* of the k-th key), two tiles' table
+// words per thread (-> bucket-j* key counts and side offsets), then the keys
+// themselves straight into their LDS slots.  T is radix-selected inside the
+// bucket in LDS; per-tile (#keys > T, #keys == T) and two block scans give every
+// tile's output offset and first-tie rank for K4.
 // ----------------------------------------------------------------------------
+constexpr int kK3PerThread = (kK2Target + kK3Threads - 1) / kK3Threads;   // tiles per thread
+
 struct SelSmem {
   uint32_t keys[kMCap];
-  uint32_t A[kNbMax + 1];   // key start per tile (exclusive scan of bucket-j* counts)
-  uint32_t Bv[kNbMax];      // side offset of bucket j*, later #keys > T in bucket j*
-  uint32_t Cv[kNbMax];      // #candidates in buckets > j* (incl. sure)
-  uint32_t Dv[kNbMax];      // #keys == T
   uint32_t G[kNBucket];
   uint32_t hist[256];
   uint32_t scratch[24];
@@ -696,110 +748,95 @@ struct SelSmem {
 template <int MODE, bool XH>
 __global__ __launch_bounds__(kK3Threads) void topk_select_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t nb,
-    uint64_t seed, float scale, TopkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ cum_tab,
-    const uint32_t* __restrict__ side, uint32_t* __restrict__ tile_info, float* __restrict__ out_val,
-    int32_t* __restrict__ out_idx, int64_t idx_base) {
+    uint32_t side_cap, uint64_t seed, float scale, TopkCtrl* __restrict__ ctrl,
+    const uint32_t* __restrict__ cum_tab, const uint32_t* __restrict__ side, uint32_t* __restrict__ tile_info,
+    float* __restrict__ out_val, int32_t* __restrict__ out_idx, int64_t idx_base) {
   __shared__ SelSmem fs;
   __shared__ ExactSmem es;
-  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  const uint32_t s_lo = ctrl->s_lo, shift = ctrl->shift;
-  uint32_t* __restrict__ tile_off = tile_info;
-  uint32_t* __restrict__ tile_tieb = tile_info + nb;
-  uint32_t* __restrict__ tile_mode = tile_info + 2 * nb;
-
+  const int tid = threadIdx.x, w = tid >> 6;
+  STAMP(100, 0);
+  const uint32_t s_lo = ctrl->s_lo, shift = ctrl->shift, overflow = ctrl->overflow;
+  const uint32_t ku = (uint32_t)k;
   if (tid < kNBucket) {
-    uint32_t g = 0;
+    uint32_t g[kNRep];
 #pragma unroll
-    for (int r = 0; r < kNRep; ++r) g += ctrl->G[r][tid];
-    fs.G[tid] = g;
+    for (int r = 0; r < kNRep; ++r) g[r] = ctrl->G[r][tid];
+    uint32_t s = 0;
+#pragma unroll
+    for (int r = 0; r < kNRep; ++r) s += g[r];
+    fs.G[tid] = s;
   }
+  if (tid == 0) fs.bc[0] = 0;
   __syncthreads();
-  // j* = max{ j <= 62 : G[j] >= k }
-  bool fallback = ctrl->overflow != 0 || fs.G[0] < (uint32_t)k || fs.G[63] >= (uint32_t)k;
-  uint32_t jstar = 0;
-  if (!fallback) {
-    for (int j = 62; j >= 0; --j)
-      if (fs.G[j] >= (uint32_t)k) { jstar = (uint32_t)j; break; }
-    if (fs.G[jstar] - fs.G[jstar + 1] > (uint32_t)kMCap) fallback = true;
-  }
+  // G[j] = #candidates in buckets >= j is non-increasing; j* = the unique
+  // j <= 254 with G[j] >= k > G[j+1]
+  bool fallback = overflow != 0 || fs.G[0] < ku || fs.G[kNMaybe] >= ku;
+  if (!fallback && tid < kNMaybe && fs.G[tid] >= ku && fs.G[tid + 1] < ku) fs.bc[0] = tid;
+  __syncthreads();
+  const uint32_t jstar = fs.bc[0];
+  if (!fallback && fs.G[jstar] - fs.G[jstar + 1] > (uint32_t)kMCap) fallback = true;
   if (fallback) {
+    // the sample's guess was off: exact single-workgroup selection (correct, slow)
     Src<MODE, XH> src{x, xh, seed};
     if (tid == 0) ctrl->fallback = 1u;
     block_topk_exact(src, n, k, scale, out_val, out_idx, idx_base, es);
     return;
   }
-  const uint32_t rank_in = (uint32_t)k - fs.G[jstar + 1];  // 1 <= rank_in <= M
-
-  // per tile: bucket-j* count, side offset, count above bucket j*
-  const int per = (nb + kK3Threads - 1) / kK3Threads;
-  const int b0 = tid * per;
-  uint32_t local = 0;
-  {
-    constexpr int PMAX = (kNbMax + kK3Threads - 1) / kK3Threads;
-    uint32_t a[PMAX], c[PMAX], s[PMAX];
+  STAMP(100, 1);
+  // ---- this thread's tiles: b = tid * kK3PerThread + q (contiguous, so the block
+  // scans below run in tile order)
+  uint32_t above[kK3PerThread], cb[kK3PerThread], off[kK3PerThread];
 #pragma unroll
-    for (int q = 0; q < PMAX; ++q) {  // unconditional (clamped) loads: all in flight together
-      const int bq = min(b0 + q, (int)nb - 1);
-      a[q] = cum_tab[(int64_t)jstar * nb + bq];
-      c[q] = cum_tab[(int64_t)(jstar + 1) * nb + bq];
-      s[q] = cum_tab[(int64_t)63 * nb + bq];
-    }
-#pragma unroll
-    for (int q = 0; q < PMAX; ++q) {
-      const int b = b0 + q;
-      if (q < per && b < (int)nb) {
-        fs.A[b] = a[q] - c[q];   // temporarily: count
-        fs.Bv[b] = c[q] - s[q];  // side offset of bucket j*
-        fs.Cv[b] = c[q];
-        local += a[q] - c[q];
-      }
-    }
+  for (int q = 0; q < kK3PerThread; ++q) {
+    const int64_t b = (int64_t)tid * kK3PerThread + q;
+    const int64_t bc = b < (int64_t)nb ? b : 0;  // clamped: the loads below are unconditional
+    const uint32_t* row = cum_tab + bc * kNBucket;
+    const uint32_t a = row[jstar], c = row[jstar + 1], s = row[kNMaybe];
+    above[q] = b < (int64_t)nb ? c : 0u;
+    cb[q] = b < (int64_t)nb ? a - c : 0u;  // keys of bucket j* in this tile
+    off[q] = c - s;                        // their side-list offset (buckets stored high to low)
   }
+  uint32_t mine = 0;
+#pragma unroll
+  for (int q = 0; q < kK3PerThread; ++q) mine += cb[q];
+  STAMP(102, 0);
   uint32_t M;
-  uint32_t pre = block_excl_scan(local, fs.scratch, &M);
-  for (int q = 0; q < per; ++q) {
-    const int b = b0 + q;
-    if (b >= (int)nb) break;
-    const uint32_t cnt = fs.A[b];
-    fs.A[b] = pre;
-    pre += cnt;
-  }
-  if (tid == 0) fs.A[nb] = M;
-  __syncthreads();
-  // gather bucket-j* keys in tile order: one independent load per key slot
-  // (tile of slot p found by binary search over the LDS prefix array A)
+  const uint32_t kpos = block_excl_scan(mine, fs.scratch, &M);  // M = G[j*] - G[j*+1]
+  STAMP(102, 1);
   {
-    constexpr int G = 8;
-    uint32_t v[G];
-    int dst[G];
+    // this thread's key slots [0, mine) over its tiles; loads in batches of 8
+    // issued before any LDS store, so each batch costs one round trip
+    const uint32_t* sd[kK3PerThread];
+    uint32_t first[kK3PerThread];
+    uint32_t acc = 0;
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const uint32_t p = tid + (uint32_t)g * kK3Threads;
-      const uint32_t pc = p < M ? p : 0u;  // clamped: the load below is unconditional
-      int lo = 0, hi = (int)nb - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (fs.A[mid] <= pc) lo = mid; else hi = mid - 1;
-      }
-      v[g] = side[(int64_t)lo * kSideCap + fs.Bv[lo] + (pc - fs.A[lo])];
-      dst[g] = p < M ? (int)p : -1;
+    for (int q = 0; q < kK3PerThread; ++q) {
+      sd[q] = side + ((int64_t)tid * kK3PerThread + q) * side_cap + off[q];
+      first[q] = acc;
+      acc += cb[q];
     }
+    constexpr int kB = 8;
+    for (uint32_t i0 = 0; i0 < mine; i0 += kB) {
+      uint32_t v[kB];
 #pragma unroll
-    for (int g = 0; g < G; ++g)
-      if (dst[g] >= 0) fs.keys[dst[g]] = v[g];
-    for (uint32_t p = tid + G * kK3Threads; p < M; p += kK3Threads) {  // M > 8K: rare
-      int lo = 0, hi = (int)nb - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (fs.A[mid] <= p) lo = mid; else hi = mid - 1;
+      for (int g = 0; g < kB; ++g) {
+        const uint32_t i = min(i0 + g, mine - 1);  // clamped: the load is unconditional
+        int q = 0;
+#pragma unroll
+        for (int t = 1; t < kK3PerThread; ++t) q += i >= first[t];
+        v[g] = sd[q][i - first[q]];
       }
-      fs.keys[p] = side[(int64_t)lo * kSideCap + fs.Bv[lo] + (p - fs.A[lo])];
+#pragma unroll
+      for (int g = 0; g < kB; ++g)
+        if (i0 + g < mine) fs.keys[kpos + i0 + g] = v[g];
     }
   }
+  STAMP(102, 2);
   __syncthreads();
-  // radix select inside the bucket: rel = key - base_j in [0, 2^shift), 8-bit digits
+  STAMP(100, 2);
+  // ---- radix select inside bucket j*: rel = key - base_j in [0, 2^shift)
   const uint32_t base_j = s_lo + (jstar << shift);
-  uint32_t prefix = 0, krem = rank_in;
+  uint32_t prefix = 0, krem = ku - fs.G[jstar + 1];  // 1 <= krem <= M
   int sh = (int)shift;
   while (sh > 0) {
     const int dsh = sh > 8 ? sh - 8 : 0;
@@ -811,74 +848,61 @@ __global__ __launch_bounds__(kK3Threads) void topk_select_kernel(
       if ((rel >> sh) == (prefix >> sh)) atomicAdd(&fs.hist[(rel >> dsh) & dmask], 1u);
     }
     __syncthreads();
-    if (w == 0) {
-      const uint32_t h0 = fs.hist[4 * lane], h1 = fs.hist[4 * lane + 1], h2 = fs.hist[4 * lane + 2],
-                     h3 = fs.hist[4 * lane + 3];
-      const uint32_t loc = h0 + h1 + h2 + h3;
-      const uint32_t rv = __shfl(loc, 63 - lane);
-      const uint32_t inc = wave_incl_scan(rv);
-      const uint32_t suf_incl = __shfl(inc, 63 - lane);  // bins >= 4*lane
-      const uint32_t above = suf_incl - loc;
-      if (above < krem && krem <= suf_incl) {
-        uint32_t acc = above;
-        const uint32_t hs[4] = {h0, h1, h2, h3};
-        for (int t = 3; t >= 0; --t) {
-          if (acc + hs[t] >= krem) { fs.bc[0] = 4 * lane + t; fs.bc[1] = krem - acc; break; }
-          acc += hs[t];
-        }
-      }
-    }
+    if (w == 0) wave_find_bin(fs.hist, krem, fs.bc + 2);
     __syncthreads();
-    prefix |= fs.bc[0] << dsh;
-    krem = fs.bc[1];
+    prefix |= fs.bc[2] << dsh;
+    krem = fs.bc[3];
     sh = dsh;
     __syncthreads();
   }
   const uint32_t T = base_j + prefix;
   const uint32_t r = krem;  // ties at T to take (>= 1)
-
-  uint32_t eq_local = 0;
-  for (int q = 0; q < per; ++q) {
-    const int b = b0 + q;
-    if (b >= (int)nb) break;
-    uint32_t eq = 0, gt = 0;
-    for (uint32_t j = fs.A[b]; j < fs.A[b + 1]; ++j) {
-      const uint32_t key = fs.keys[j];
-      gt += key > T;
-      eq += key == T;
+  STAMP(100, 3);
+  // ---- per tile: #keys > T (every key above bucket j* is) and #keys == T
+  uint32_t gt[kK3PerThread], eq[kK3PerThread];
+  uint32_t gsum = 0, esum = 0;
+  {
+    uint32_t p = kpos;
+#pragma unroll
+    for (int q = 0; q < kK3PerThread; ++q) {
+      uint32_t g = above[q], e = 0;
+      for (uint32_t i = 0; i < cb[q]; ++i) {
+        const uint32_t key = fs.keys[p + i];
+        g += key > T;
+        e += key == T;
+      }
+      p += cb[q];
+      gt[q] = g;
+      eq[q] = e;
+      gsum += g;
+      esum += e;
     }
-    fs.Bv[b] = gt;
-    fs.Dv[b] = eq;
-    eq_local += eq;
   }
-  uint32_t tie_total;
-  uint32_t tb = block_excl_scan(eq_local, fs.scratch, &tie_total);
-  uint32_t sel_local = 0;
-  for (int q = 0; q < per; ++q) {
-    const int b = b0 + q;
-    if (b >= (int)nb) break;
-    const uint32_t eq = fs.Dv[b];
-    const uint32_t take = tb >= r ? 0u : min(eq, r - tb);
-    const uint32_t sel = fs.Cv[b] + fs.Bv[b] + take;
-    tile_tieb[b] = tb;
-    tile_mode[b] = take == 0 ? kTakeNone : (take == eq ? kTakeAll : kTakePartial);
-    fs.Bv[b] = sel;
-    tb += eq;
-    sel_local += sel;
-  }
-  uint32_t sel_total;
-  uint32_t sel_pre = block_excl_scan(sel_local, fs.scratch, &sel_total);
-  for (int q = 0; q < per; ++q) {
-    const int b = b0 + q;
-    if (b >= (int)nb) break;
-    tile_off[b] = sel_pre;
-    sel_pre += fs.Bv[b];
+  uint32_t gtot, etot;
+  uint32_t gpre = block_excl_scan(gsum, fs.scratch, &gtot);
+  uint32_t epre = block_excl_scan(esum, fs.scratch, &etot);
+  uint32_t* __restrict__ tile_off = tile_info;
+  uint32_t* __restrict__ tile_tieb = tile_info + nb;
+  uint32_t* __restrict__ tile_mode = tile_info + 2 * nb;
+#pragma unroll
+  for (int q = 0; q < kK3PerThread; ++q) {
+    const int64_t b = (int64_t)tid * kK3PerThread + q;
+    if (b < (int64_t)nb) {
+      const uint32_t taken = min(r, epre);  // ties taken by earlier tiles (lowest index first)
+      const uint32_t take = min(eq[q], r - taken);
+      tile_off[b] = gpre + taken;
+      tile_tieb[b] = epre;
+      tile_mode[b] = take == 0 ? kTakeNone : (take == eq[q] ? kTakeAll : kTakePartial);
+    }
+    gpre += gt[q];
+    epre += eq[q];
   }
   if (tid == 0) {
     ctrl->T = T;
     ctrl->r = r;
     ctrl->fallback = 0u;
   }
+  STAMP(101, 0);
 }
 
 // ----------------------------------------------------------------------------
@@ -892,14 +916,15 @@ __global__ __launch_bounds__(kK4Threads) void topk_emit_kernel(
     int64_t idx_base) {
   __shared__ uint32_t scratch[24];
   const int64_t b = blockIdx.x;
+  STAMP(24576 + b, 0);
   // every control word is independent: issue all loads before the first use
   const uint32_t fallback = ctrl->fallback, T = ctrl->T, r = ctrl->r;
   uint32_t out = tile_info[b];
   uint32_t tie_run = tile_info[nb + b];
   const uint32_t mode = tile_info[2 * nb + b];
   const uint4 cw4 = *reinterpret_cast<const uint4*>(cntw + b * kK2Waves);
-  const uint32_t c0 = cw4.x, c1 = cw4.y, c2 = cw4.z, c3 = cw4.w;
   if (fallback) return;
+  const uint32_t c0 = cw4.x, c1 = cw4.y, c2 = cw4.z, c3 = cw4.w;
   const uint32_t e1 = c0, e2 = e1 + c1, e3 = e2 + c2, tot = e3 + c3;
   const int64_t wlen = tile / kK2Waves;
   const int64_t tb = b * tile;
@@ -936,6 +961,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_emit_kernel(
     }
     out += nsel;
   }
+  STAMP(24576 + b, 1);
 }
 
 // ----------------------------------------------------------------------------
@@ -951,23 +977,12 @@ static bool host_seg_uses_pipeline(int64_t off, int64_t len) {
 
 size_t topk_ws_bytes(int64_t n) { return n > kSmallN ? topk_layout(n).total : 256; }
 
-static int num_cus() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                   hipSuccess || cus <= 0)
-      cus = 256;
-  }
-  return cus;
-}
-
 template <int MODE, bool XH>
 static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                        float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes,
                        hipStream_t st) {
   if (n <= kSmallN || k >= n) {
-    hipLaunchKernelGGL((topk_exact_kernel<MODE, XH>), dim3(1), dim3(kExactThreads), 0, st, x, xh, n, k,
+    CHOCO_KLAUNCH((topk_exact_kernel<MODE, XH>), dim3(1), dim3(kExactThreads), 0, st, x, xh, n, k,
                        seed, scale, out_val, out_idx, idx_base);
     CHOCO_LAUNCHED("topk_exact_kernel");
     return CHOCO_OK;
@@ -985,8 +1000,11 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   uint32_t* cidx = reinterpret_cast<uint32_t*>(base + L.off_cidx);
   if (MODE == kData) {
     uint32_t* k1 = reinterpret_cast<uint32_t*>(base + L.off_k1);
-    hipLaunchKernelGGL((topk_sample_kernel<XH>), dim3(kK1Blocks), dim3(kK1Threads), 0, st, x, xh, n, k, ctrl, k1);
-    CHOCO_LAUNCHED("topk_sample_kernel");
+    CHOCO_KLAUNCH((topk_sample_hist_kernel<XH>), dim3(kK1Blocks), dim3(kK1Threads), 0, st, x, xh, n, k1);
+    CHOCO_LAUNCHED("topk_sample_hist_kernel");
+    CHOCO_KLAUNCH((topk_sample_bounds_kernel<XH>), dim3(kK1Blocks), dim3(kK1Threads), 0, st, x, xh, n, k, ctrl,
+                  k1);
+    CHOCO_LAUNCHED("topk_sample_bounds_kernel");
   } else {
     // keys uniform on [0, 2^31): P(key >= t) = (2^31 - t) / 2^31
     const double nd = (double)n, kd = (double)k, sd = sqrt(kd);
@@ -996,20 +1014,20 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
     uint32_t s_lo = (uint32_t)std::max(0.0, floor(two31 * (1.0 - c_lo / nd)));
     uint64_t s_hi_est = c_hi < 1.0 ? 0x80000000ull : (uint64_t)ceil(two31 * (1.0 - c_hi / nd));
     if (s_hi_est <= s_lo) s_hi_est = (uint64_t)s_lo + 1;
-    hipLaunchKernelGGL(topk_set_params_kernel, dim3(1), dim3(256), 0, st, ctrl, s_lo, s_hi_est);
+    CHOCO_KLAUNCH(topk_set_params_kernel, dim3(1), dim3(256), 0, st, ctrl, s_lo, s_hi_est);
     CHOCO_LAUNCHED("topk_set_params_kernel");
   }
-  const unsigned g2 = (unsigned)std::min<int64_t>(L.nb, (int64_t)num_cus() * kK2BlocksPerCU);
   profile_begin("topk_stream", st);
-  hipLaunchKernelGGL((topk_stream_kernel<MODE, XH>), dim3(g2), dim3(kK2Threads), 0, st, x, xh, n, L.tile, L.nb,
-                     seed, ctrl, cum, cntw, side, cval, cidx);
+  CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, L.tile, L.nb,
+                L.side_cap, seed, ctrl, cum, cntw, side, cval, cidx);
   profile_end("topk_stream", st);
   CHOCO_LAUNCHED("topk_stream_kernel");
-  hipLaunchKernelGGL((topk_select_kernel<MODE, XH>), dim3(1), dim3(kK3Threads), 0, st, x, xh, n, k, L.nb, seed,
-                     scale, ctrl, cum, side, tinfo, out_val, out_idx, idx_base);
+  if (CHOCO_K2_ABLATE) return CHOCO_OK;  // diagnostic builds: candidates are not valid
+  CHOCO_KLAUNCH((topk_select_kernel<MODE, XH>), dim3(1), dim3(kK3Threads), 0, st, x, xh, n, k, L.nb,
+                L.side_cap, seed, scale, ctrl, cum, side, tinfo, out_val, out_idx, idx_base);
   CHOCO_LAUNCHED("topk_select_kernel");
-  hipLaunchKernelGGL((topk_emit_kernel<MODE>), dim3(L.nb), dim3(kK4Threads), 0, st, L.tile, L.nb, seed, scale,
-                     ctrl, cntw, tinfo, cval, cidx, out_val, out_idx, idx_base);
+  CHOCO_KLAUNCH((topk_emit_kernel<MODE>), dim3(L.nb), dim3(kK4Threads), 0, st, L.tile, L.nb, seed, scale, ctrl,
+                cntw, tinfo, cval, cidx, out_val, out_idx, idx_base);
   CHOCO_LAUNCHED("topk_emit_kernel");
   return CHOCO_OK;
 }
@@ -1094,10 +1112,10 @@ CHOCO_API int choco_topk_compress_segmented(const float* x, const float* xhat, c
   CHOCO_REQUIRE(ntot < (int64_t)INT32_MAX, "total length must be < 2^31");
   // every segment that is not pipelined: one workgroup each, one launch
   if (xhat)
-    hipLaunchKernelGGL((topk_segmented_kernel<true>), dim3(nseg), dim3(kExactThreads), 0, st, x, xhat,
+    CHOCO_KLAUNCH((topk_segmented_kernel<true>), dim3(nseg), dim3(kExactThreads), 0, st, x, xhat,
                        plan_dev, nseg, out_val, out_idx);
   else
-    hipLaunchKernelGGL((topk_segmented_kernel<false>), dim3(nseg), dim3(kExactThreads), 0, st, x, xhat,
+    CHOCO_KLAUNCH((topk_segmented_kernel<false>), dim3(nseg), dim3(kExactThreads), 0, st, x, xhat,
                        plan_dev, nseg, out_val, out_idx);
   CHOCO_LAUNCHED("topk_segmented_kernel");
   for (int s = 0; s < nseg; ++s) {
@@ -1110,3 +1128,15 @@ CHOCO_API int choco_topk_compress_segmented(const float* x, const float* xhat, c
   }
   return CHOCO_OK;
 }
+
+#if CHOCO_STAMPS
+// Diagnostic builds only: copy out (and clear) the phase stamps.
+CHOCO_API int choco_dbg_stamps(unsigned long long* host, size_t bytes) {
+  const size_t all = sizeof(unsigned long long) * kStampSlots * 4;
+  if (bytes > all) bytes = all;
+  if (host) CHOCO_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost));
+  static unsigned long long zeros[kStampSlots * 4];
+  CHOCO_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zeros, all, 0, hipMemcpyHostToDevice));
+  return CHOCO_OK;
+}
+#endif

@@ -11,6 +11,12 @@
  * Return value of every function: CHOCO_OK (0) or a negative CHOCO_ERR_*;
  * choco_last_error() returns the per-thread message of the last failure.
  *
+ * Workspaces (`ws`, sized by the matching *_workspace_size): device memory the
+ * caller zero-fills ONCE before first use; every call leaves it ready for the
+ * next (self-resetting tickets and histograms).  A workspace carries state
+ * between the kernels of one call, so calls that may run concurrently need
+ * separate workspaces (one per stream).
+ *
  * Element/index conventions:
  *   - n counts fp32 elements; every n must be < 2^31 (indices are int32 on the
  *     wire; the reference sends fp32 indices and is inexact above 2^24,
@@ -182,8 +188,10 @@ int choco_gossip_step(float* x, const float* memory, const float* xhat, float ga
                       int64_t n, void* stream);
 
 /* ------------------------------------------------------- profiling hooks
- * Optional: when enabled, the library records hipEvents around the dominant
- * kernel of each op on the op's own stream (the bench's roofline source). */
+ * Optional: when enabled, the dominant kernel of each op is launched with a
+ * pair of hipEvents attached to the dispatch itself (hipExtLaunchKernelGGL), so
+ * the elapsed time is the kernel's own, not the queue ahead of it (the bench's
+ * roofline source; agrees with rocprofv3 --kernel-trace). */
 int choco_profile_enable(int32_t on);
 /* Accumulated (sum of ms, count) of the named kernel since the last reset,
  * after synchronising its events.  Names: "topk_stream", "sign_pack",

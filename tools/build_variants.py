@@ -1,0 +1,32 @@
+"""Build diagnostic variants of the codec (K2 ablations / tuning knobs) into
+chocosgd_amd/lib/variants/ for tools/diag_stream.py.  Never loaded by the product."""
+import os
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from chocosgd_amd import build  # noqa: E402
+
+VARIANTS = {
+    "wpe6": ["CHOCO_K2_WPE=6"],
+    "wpe7": ["CHOCO_K2_WPE=7"],
+    "t1024": ["CHOCO_K2_TARGET=1024"],
+    "stamps": ["CHOCO_STAMPS=1"],
+    "abl1": ["CHOCO_K2_ABLATE=1"],
+    "abl2": ["CHOCO_K2_ABLATE=2"],
+}
+
+
+def main(names):
+    out = os.path.join(build.LIBDIR, "variants")
+    names = names or list(VARIANTS)
+
+    def one(nm):
+        return build.build_library(force=True, defines=VARIANTS[nm], lib=os.path.join(out, f"lib_{nm}.so"), jobs=2)
+    with ThreadPoolExecutor(4) as ex:
+        for p in ex.map(one, names):
+            print(p)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -1,0 +1,83 @@
+"""Phase timeline of one top-k call from the CHOCO_STAMPS diagnostic build
+(wall_clock64, 100 MHz): per-kernel spans, per-workgroup durations.
+
+    python tools/stamps.py [--n 100000000] [--lib chocosgd_amd/lib/variants/lib_stamps.so]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from chocosgd_amd import _lib, codec  # noqa: E402
+
+TICK_US = 0.01  # 100 MHz
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=100_000_000)
+    ap.add_argument("--ratio", type=float, default=0.99)
+    ap.add_argument("--lib", default=os.path.join(ROOT, "chocosgd_amd/lib/variants/lib_stamps.so"))
+    ap.add_argument("--save", default=None, help="write the raw stamp table (.npy)")
+    a = ap.parse_args()
+    lib = _lib.load(a.lib)
+    fn = lib.choco_dbg_stamps
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    dev = torch.device("cuda", 0)
+    d = torch.randn(a.n, generator=torch.Generator(device=dev).manual_seed(1), device=dev)
+    k = codec.topk_k(a.n, a.ratio)
+    for _ in range(3):
+        codec.topk(d, k)
+    torch.cuda.synchronize()
+    buf = np.zeros((40960, 4), dtype=np.uint64)
+    fn(None, 0)
+    codec.topk(d, k)
+    torch.cuda.synchronize()
+    fn(buf.ctypes.data, buf.nbytes)
+    if a.save:
+        np.save(a.save, buf)
+    t = buf.astype(np.int64)
+    k1 = t[:64]
+    t0 = k1[:, 0][k1[:, 0] > 0].min()
+
+    def us(v):
+        return (v - t0) * TICK_US
+
+    def row(name, v):
+        v = v[v > 0]
+        if v.size == 0:
+            print(f"  {name:34s} (none)")
+            return
+        print(f"  {name:34s} min {us(v.min()):8.2f}  med {us(np.median(v)):8.2f}  max {us(v.max()):8.2f} us")
+
+    print(f"n={a.n} k={k}; times in us from the first K1 workgroup start")
+    print("K1 sample (64 workgroups x 2 kernels)")
+    row("K1a start", k1[:, 0]); row("K1a end", k1[:, 1]); row("K1b fine hist added", k1[:, 2])
+    row("K1b ticket drawn", k1[:, 3]); row("K1b last wg: bounds", t[64:65, 0])
+    k2 = t[1024:24576]
+    k2 = k2[k2[:, 0] > 0]
+    print(f"K2 stream ({len(k2)} workgroups)")
+    row("start", k2[:, 0]); row("streamed", k2[:, 1]); row("hist done", k2[:, 2]); row("end", k2[:, 3])
+    dur = (k2[:, 1] - k2[:, 0]) * TICK_US
+    tail = (k2[:, 3] - k2[:, 1]) * TICK_US
+    print(f"  per-wg stream time  min {dur.min():.2f} med {np.median(dur):.2f} max {dur.max():.2f} us;"
+          f" end-of-tile min {tail.min():.2f} med {np.median(tail):.2f} max {tail.max():.2f} us")
+    print("K3 select")
+    row("start", t[100:101, 0]); row("j* found", t[100:101, 1]); row("tid0: table words in", t[102:103, 0])
+    row("tid0: key slots scanned", t[102:103, 1]); row("tid0: keys stored", t[102:103, 2])
+    row("bucket keys in LDS", t[100:101, 2])
+    row("T selected", t[100:101, 3]); row("end", t[101:102, 0])
+    k4 = t[24576:40960]
+    k4 = k4[k4[:, 0] > 0]
+    print(f"K4 emit ({len(k4)} workgroups)")
+    row("start", k4[:, 0]); row("end", k4[:, 1])
+
+
+if __name__ == "__main__":
+    main()
