@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--n", type=int, default=0, help="override elements per worker")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--no-e2e", action="store_true", help="skip the host-resident (PCIe-inclusive) leg")
     return p.parse_args()
 
 
@@ -137,6 +138,43 @@ class Worker:
                 cw <<= 1
             return 4 * n + n * cw // 8 + n // 8          # read d, write level + sign planes
         return 4 * n + 4 * ((n + 31) // 32)              # read d, write packed sign words
+
+
+def e2e_rate(w, reps=5):
+    """Host-resident leg (north star: the path starts and ends in host memory):
+    pinned H2D of the worker's buffer -> compress -> D2H of the packed message
+    -> H2D of that message (the receiver's copy) -> decompress-accumulate.
+    Reported next to, never as, the device-resident value."""
+    host_x = w.d.cpu().pin_memory()
+    host_msg = torch.empty(w.msg.shape, dtype=w.msg.dtype).pin_memory()
+    parts = {"h2d": [], "device": [], "d2h": [], "total": []}
+    for i in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        w.d.copy_(host_x, non_blocking=True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        w.compress()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        host_msg.copy_(w.msg, non_blocking=True)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        w.msg.copy_(host_msg, non_blocking=True)
+        w.decompress()
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        if i:  # first round is a warm-up
+            parts["h2d"].append(t1 - t0)
+            parts["device"].append((t2 - t1) + (t4 - t3))
+            parts["d2h"].append(t3 - t2)
+            parts["total"].append(t4 - t0)
+    med = {k: statistics.median(v) for k, v in parts.items()}
+    return {"value": round(4 * w.n / med["total"] / 1e9, 3), "unit": "GB/s",
+            "ms": {k: round(v * 1e3, 3) for k, v in med.items()},
+            "msg_bytes": w.msg.numel() * w.msg.element_size(),
+            "note": "pinned host buffers; H2D x, compress, D2H message, H2D message + decompress; median of "
+                    f"{reps}"}
 
 
 def cpu_baseline(w, threads):
@@ -250,8 +288,11 @@ def main():
                          "traffic": traffic, "kernel": w.kernel, "kernel_us": round(avg_s * 1e6, 2),
                          "algorithmic_bytes_per_launch": w.kernel_bytes()},
             "kernels_us": kernels,
+            "e2e": None,
             "cpu_baseline": None,
         }
+        if world == 1 and not args.no_e2e:
+            out["e2e"] = e2e_rate(w)
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count())
             out["cpu_baseline"] = cpu_baseline(w, threads)

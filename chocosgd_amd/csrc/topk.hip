@@ -42,31 +42,28 @@
 
 namespace choco {
 
-constexpr int kK2Threads = 256;
+constexpr int kK2Threads = 1024;          // 16 waves, each a contiguous range of the tile
 constexpr int kK2Waves = kK2Threads / 64;
-// Tuning knobs (tools/build_variants.py builds diagnostic variants of these).
-#ifndef CHOCO_K2_WPE     // stream-kernel waves per SIMD: VGPRs capped at 512 / WPE
-#define CHOCO_K2_WPE 8
+// Diagnostic knob (tools/build_variants.py): tiles per launch.
+#ifndef CHOCO_K2_TARGET  // one workgroup per CU (256 CUs): no two tiles compete on a CU
+#define CHOCO_K2_TARGET 256
 #endif
-#ifndef CHOCO_K2_ABLATE  // diagnostic: 1 no end-of-tile, 2 rows only folded (K3/K4 skipped)
-#define CHOCO_K2_ABLATE 0
-#endif
-#ifndef CHOCO_K2_TARGET  // tiles per launch: 256 CUs x 8 resident workgroups = one balanced round
-#define CHOCO_K2_TARGET 2048
-#endif
-constexpr int kK2Unroll = 4;            // float4 rows per wave per load batch
-constexpr int kK2Wpe = CHOCO_K2_WPE;
+constexpr int kK2Unroll = 8;            // float4 rows per wave per load batch (8 KiB in flight)
 constexpr int64_t kK2Target = CHOCO_K2_TARGET;
-constexpr int64_t kTileQuant = (int64_t)kK2Waves * kK2Unroll * 256;   // 4096 elements
-static_assert(kK2Target <= 2048, "K3 keeps two tiles per thread");
+constexpr int64_t kTileQuant = (int64_t)kK2Waves * kK2Unroll * 256;   // 32768 elements
+static_assert(kK2Target <= 2048, "K3 keeps at most two tiles per thread");
+constexpr int64_t kChunk = 4096;        // elements a wave claims at a time (LDS counter)
+static_assert(kTileQuant % kChunk == 0 && kChunk % (256 * kK2Unroll) == 0, "chunk geometry");
+static_assert((int64_t(1) << 31) / kK2Target / kChunk <= 2 * 1024, "K4 scans <= 2 chunk counts per thread");
 constexpr int kRing = 512;              // LDS ring entries (value, index) per wave
 constexpr int kFlush = 64;              // ring -> HBM in 64-entry (2 x 256-B store) chunks
+constexpr int kMaybeCap = 16384;        // maybe keys per tile kept in LDS (= side-list capacity)
 constexpr int kNBucket = 256;           // 255 "maybe" buckets + 1 "sure"
 constexpr int kNMaybe = kNBucket - 1;
 constexpr int kNRep = 16;               // replicas of the global bucket totals
 constexpr int kMCap = 16384;            // max keys of bucket j* selected in LDS
 constexpr int kK3Threads = 1024;
-constexpr int kK4Threads = 256;
+constexpr int kK4Threads = 1024;
 constexpr int kK1Blocks = 64;           // sample workgroups, 1024 samples each
 constexpr int kK1Threads = 256;
 constexpr int kSampleN = kK1Blocks * kK1Threads * 4;   // 65536
@@ -107,10 +104,11 @@ struct TopkLayout {
   size_t off_ctrl, off_cum, off_cntw, off_side, off_tile, off_k1, off_cval, off_cidx, total;
 };
 
-// Tile = ceil(n / kK2Target) rounded up to 4096 elements, so one launch is one
-// balanced round of resident workgroups.  A tile's side list holds its "maybe"
-// keys: 1/16 of the tile, far above the sample's margin (~12 sqrt(k/n / 65536)
-// of the elements: 0.5 % at k = 1 %, 1.5 % at k = 10 %).
+// Tile = ceil(n / kK2Target) rounded up to 32768 elements: one tile per CU, all
+// resident at once (few tiles also keep K3's table reads short).  A tile's side
+// list holds its "maybe" keys (kMaybeCap, LDS-staged): the sample's margin is
+// ~12 sqrt(k/n / 65536) of the elements (0.5 % at k = 1 %, 1.5 % at k = 10 %,
+// 3.3 % at k = 50 % -> 13K of a 390K-element tile).
 static TopkLayout topk_layout(int64_t n) {
   TopkLayout L{};
   L.n = n;
@@ -118,11 +116,11 @@ static TopkLayout topk_layout(int64_t n) {
   tile = std::max<int64_t>(kTileQuant, (tile + kTileQuant - 1) / kTileQuant * kTileQuant);
   L.tile = (uint32_t)tile;
   L.nb = (uint32_t)((n + tile - 1) / tile);
-  L.side_cap = (uint32_t)std::max<int64_t>(2048, tile / 16);
+  L.side_cap = (uint32_t)std::min<int64_t>(kMaybeCap, tile);
   size_t o = 0;
   L.off_ctrl = o;  o += align_up(sizeof(TopkCtrl), 256);
   L.off_cum = o;   o += align_up((size_t)L.nb * kNBucket * 4, 256);
-  L.off_cntw = o;  o += align_up((size_t)L.nb * kK2Waves * 4, 256);
+  L.off_cntw = o;  o += align_up((size_t)L.nb * (tile / kChunk) * 4, 256);   // per-chunk candidate counts
   L.off_side = o;  o += align_up((size_t)L.nb * L.side_cap * 4, 256);
   L.off_tile = o;  o += align_up((size_t)L.nb * 3 * 4, 256);        // tile_off | tile_tieb | tile_mode
   L.off_k1 = o;    o += align_up((size_t)3 * 2048 * 4, 256);           // sample histograms (K1)
@@ -507,18 +505,25 @@ __global__ void topk_set_params_kernel(TopkCtrl* __restrict__ ctrl, uint32_t s_l
 }
 
 // ----------------------------------------------------------------------------
-// K2: streaming candidate compaction, one workgroup per tile
+// K2: streaming candidate compaction, one 16-wave workgroup per tile, one per CU
 //
-// Sized for occupancy rather than software pipelining: 16.6 KB of LDS and
-// <= 64 VGPRs per thread let 8 workgroups (32 waves) share a CU, so ~128 KB of
-// loads per CU are in flight while the waves that own them compute.
+// Measured (tools/probe_position.hip, probe_balance.hip): when two or more
+// workgroups share a CU, the one dispatched first streams first and the last
+// ones finish alone with few bytes in flight; with ONE workgroup per CU every
+// workgroup finishes within ~10 % of the others and the read runs at 6.4 TB/s.
+// 137 KiB of LDS enforces that placement.  Maybe keys (s_lo <= key < s_hi) are
+// binned and staged in LDS as the ring is flushed, so the end of the tile only
+// scans 256 bucket counts and counting-sorts the staged keys to the side list.
 // ----------------------------------------------------------------------------
 struct StreamSmem {
   uint2 ring[kK2Waves][kRing];  // (value bits, index) per wave, in index order
   uint2 trash[kK2Waves][64];    // per-lane sink of the branch-free stage writes
+  uint32_t maybe[kMaybeCap];    // the tile's maybe keys, in flush order
   uint32_t hist[kNBucket];      // maybe-key bucket counts, then counting-sort cursors
   uint32_t cnt[kK2Waves];
-  uint32_t scratch[8];
+  uint32_t scratch[24];
+  uint32_t mcount;
+  uint32_t next_chunk;          // the tile's chunk counter (waves claim chunks)
 };
 
 // Unconditional float4 loads of kK2Unroll rows (no branch around a load: the
@@ -548,12 +553,37 @@ struct WaveAcc {
   uint32_t staged, flushed;
 };
 
+// Per-tile bucket geometry, read once from the control block.
+struct Buckets {
+  uint32_t s_lo, s_hi, shift;
+  uint64_t seed;
+};
+
+// One flushed entry per lane: if its key is a "maybe" key, bin it and stage it
+// in the tile's LDS list (one LDS atomic per wave for the list slots).
+template <int MODE>
+CHOCO_DEV void note_maybe(StreamSmem& sm, uint2 e, bool valid, const Buckets& bk) {
+  const uint32_t key = MODE == kData ? fkey(__uint_as_float(e.x)) : (rank_hash(bk.seed, e.y) >> 1);
+  const bool mb = valid && key < bk.s_hi;  // every ring entry has key >= s_lo
+  const uint64_t bm = ballot(mb);
+  if (bm == 0ull) return;  // wave-uniform
+  uint32_t base = 0;
+  if (lane_id() == 0) base = atomicAdd(&sm.mcount, (uint32_t)__popcll(bm));
+  base = __builtin_amdgcn_readfirstlane(base);
+  if (mb) {
+    const uint32_t p = base + mask_prefix(bm);
+    if (p < (uint32_t)kMaybeCap) sm.maybe[p] = key;
+    atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
+  }
+}
+
 // Write whole 64-entry chunks of the ring out (one 256-B store per array each).
 // The ring never holds more than 63 + 256 entries, so nothing is overwritten
 // before it is flushed.  Counters are wave-uniform; readfirstlane keeps them in
 // SGPRs so the flush test is a scalar branch.
+template <int MODE>
 CHOCO_DEV void ring_flush(StreamSmem& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
-                          uint32_t* __restrict__ oi) {
+                          uint32_t* __restrict__ oi, const Buckets& bk) {
   wave_sync();
   const uint32_t end = __builtin_amdgcn_readfirstlane(a.staged) & ~(uint32_t)(kFlush - 1);
 #pragma unroll 1
@@ -561,6 +591,7 @@ CHOCO_DEV void ring_flush(StreamSmem& sm, int w, int lane, WaveAcc& a, float* __
     const uint2 e = sm.ring[w][(f + lane) & (kRing - 1)];
     ov[f + lane] = __uint_as_float(e.x);
     oi[f + lane] = e.y;
+    note_maybe<MODE>(sm, e, true, bk);
   }
   a.flushed = end;
 }
@@ -570,21 +601,17 @@ CHOCO_DEV void ring_flush(StreamSmem& sm, int w, int lane, WaveAcc& a, float* __
 // (4 x mbcnt); every lane then writes its (value, index) pair either to its ring
 // slot or to its own trash slot, so the only branches are wave-uniform.
 template <int MODE, bool XH, bool GUARD>
-CHOCO_DEV void process_row(const Src<MODE, XH>& src, const float4 v4, int64_t i, int64_t wend, uint32_t s_lo,
-                           StreamSmem& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
-                           uint32_t* __restrict__ oi) {
+CHOCO_DEV void process_row(const Src<MODE, XH>& src, const float4 v4, int64_t i, int64_t wend, StreamSmem& sm,
+                           int w, int lane, WaveAcc& a, float* __restrict__ ov, uint32_t* __restrict__ oi,
+                           const Buckets& bk) {
   const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
-#if CHOCO_K2_ABLATE == 2
-  a.staged ^= __builtin_amdgcn_readfirstlane(fkey(vv[0]) ^ fkey(vv[1]) ^ fkey(vv[2]) ^ fkey(vv[3])) & 1u;
-  return;
-#endif
   bool cand[4];
   uint64_t m[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const bool valid = !GUARD || i + c < wend;
     const uint32_t key = MODE == kData ? fkey(vv[c]) : (valid ? src.key_of(i + c, 0.f) : 0u);
-    cand[c] = valid && key >= s_lo;
+    cand[c] = valid && key >= bk.s_lo;
     m[c] = ballot(cand[c]);
   }
   if ((m[0] | m[1] | m[2] | m[3]) == 0ull) return;  // wave-uniform: no candidate in this row
@@ -602,124 +629,116 @@ CHOCO_DEV void process_row(const Src<MODE, XH>& src, const float4 v4, int64_t i,
     }
   }
   a.staged = __builtin_amdgcn_readfirstlane(a.staged);
-  if (a.staged - a.flushed >= (uint32_t)kFlush) ring_flush(sm, w, lane, a, ov, oi);
-}
-
-// Key of candidate j of this wave's run, re-read from the run just written (L2).
-template <int MODE>
-CHOCO_DEV uint32_t cand_key(const float* __restrict__ ov, const uint32_t* __restrict__ oi, uint32_t j,
-                            uint64_t seed) {
-  return MODE == kData ? fkey(ov[j]) : (rank_hash(seed, oi[j]) >> 1);
+  if (a.staged - a.flushed >= (uint32_t)kFlush) ring_flush<MODE>(sm, w, lane, a, ov, oi, bk);
 }
 
 template <int MODE, bool XH>
-__global__ __launch_bounds__(kK2Threads, XH ? kK2Wpe - 2 : kK2Wpe) void topk_stream_kernel(
+__global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, uint32_t tile, uint32_t nb,
     uint32_t side_cap, uint64_t seed, TopkCtrl* __restrict__ ctrl, uint32_t* __restrict__ cum_tab,
     uint32_t* __restrict__ cntw, uint32_t* __restrict__ side, float* __restrict__ cval,
     uint32_t* __restrict__ cidx) {
   __shared__ StreamSmem sm;
   STAMP(1024 + blockIdx.x, 0);
-  const uint32_t s_lo = ctrl->s_lo, s_hi = ctrl->s_hi, shift = ctrl->shift;
+  const Buckets bk{ctrl->s_lo, ctrl->s_hi, ctrl->shift, seed};
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   const int64_t b = blockIdx.x;
-  const int64_t wlen = tile / kK2Waves;
   constexpr int64_t kStep = 256 * kK2Unroll;
   Src<MODE, XH> src{x, xh, seed};
-
-  const int64_t wbeg = b * tile + w * wlen;
-  const int64_t wend = min(wbeg + wlen, n);
-  float* __restrict__ ov = cval + wbeg;
-  uint32_t* __restrict__ oi = cidx + wbeg;
-  WaveAcc a{0u, 0u};
-  const int64_t full_end = wend > wbeg ? wbeg + (wend - wbeg) / kStep * kStep : wbeg;
-  for (int64_t base = wbeg; base < full_end; base += kStep) {
-    float4 A[kK2Unroll];
-    if (MODE == kData) load_rows_full<XH>(x, xh, base, lane, A);
-#pragma unroll
-    for (int u = 0; u < kK2Unroll; ++u)
-      process_row<MODE, XH, false>(src, MODE == kData ? A[u] : make_float4(0.f, 0.f, 0.f, 0.f),
-                                   base + u * 256 + 4 * lane, wend, s_lo, sm, w, lane, a, ov, oi);
-  }
-  // tail (< kStep elements, last tile only): guarded loads
-  for (int64_t base = full_end; base < wend; base += 256) {
-    const int64_t i = base + 4 * lane;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (MODE == kData) {
-      float t[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) t[c] = (i + c < wend) ? src.val(i + c) : 0.f;
-      v = make_float4(t[0], t[1], t[2], t[3]);
-    }
-    process_row<MODE, XH, true>(src, v, i, wend, s_lo, sm, w, lane, a, ov, oi);
-  }
-  // final partial chunk (< 64 entries)
-  wave_sync();
-  if (a.flushed + lane < a.staged) {
-    const uint2 e = sm.ring[w][(a.flushed + lane) & (kRing - 1)];
-    ov[a.flushed + lane] = __uint_as_float(e.x);
-    oi[a.flushed + lane] = e.y;
-  }
-  const uint32_t cnt = a.staged;
-  STAMP(1024 + b, 1);
-#if CHOCO_K2_ABLATE == 1
-  return;
-#endif
-
-  // ---- end of tile: bucket counts of the "maybe" keys (s_lo <= key < s_hi),
-  // read back from the run this wave just wrote; then counting-sort them into
-  // the tile's side list (buckets from high to low).
-  if (lane == 0) sm.cnt[w] = cnt;
-  sm.hist[threadIdx.x] = 0;  // 256 threads <-> 256 buckets
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (threadIdx.x < kNBucket) sm.hist[threadIdx.x] = 0;
+  if (threadIdx.x == 0) { sm.mcount = 0; sm.next_chunk = 0; }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  for (uint32_t j0 = 0; j0 < cnt; j0 += 256) {
-    uint32_t kk[4];
+
+  // Waves claim the tile's kChunk-element chunks through an LDS counter: the
+  // CU's issue arbiter favours older waves, so a static split leaves the youngest
+  // waves finishing last with few bytes in flight.  Chunk c's candidates go to
+  // its own slot range and count, so the tile's output order is the chunk order.
+  const uint32_t nchunk = tile / (uint32_t)kChunk;
+  uint32_t total = 0;
+  uint32_t c = 0;
+  if (lane == 0) c = atomicAdd(&sm.next_chunk, 1u);
+  c = __builtin_amdgcn_readfirstlane(c);
+  while (c < nchunk) {
+    uint32_t nx = 0;
+    if (lane == 0) nx = atomicAdd(&sm.next_chunk, 1u);  // the next claim, used after this chunk
+    const int64_t cbeg = b * (int64_t)tile + (int64_t)c * kChunk;
+    const int64_t cend = min(cbeg + kChunk, n);
+    float* __restrict__ ov = cval + cbeg;
+    uint32_t* __restrict__ oi = cidx + cbeg;
+    WaveAcc a{0u, 0u};
+    const int64_t full_end = cend > cbeg ? cbeg + (cend - cbeg) / kStep * kStep : cbeg;
+    for (int64_t base = cbeg; base < full_end; base += kStep) {
+      float4 A[kK2Unroll];
+      if (MODE == kData) load_rows_full<XH>(x, xh, base, lane, A);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t j = j0 + q * 64 + lane;
-      kk[q] = cand_key<MODE>(ov, oi, j < cnt ? j : 0u, seed);
+      for (int u = 0; u < kK2Unroll; ++u)
+        process_row<MODE, XH, false>(src, MODE == kData ? A[u] : make_float4(0.f, 0.f, 0.f, 0.f),
+                                     base + u * 256 + 4 * lane, cend, sm, w, lane, a, ov, oi, bk);
     }
+    // tail (< kStep elements, last chunk only): guarded loads
+    for (int64_t base = full_end; base < cend; base += 256) {
+      const int64_t i = base + 4 * lane;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (MODE == kData) {
+        float t[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (j0 + q * 64 + lane < cnt && kk[q] < s_hi) atomicAdd(&sm.hist[(kk[q] - s_lo) >> shift], 1u);
+        for (int cc = 0; cc < 4; ++cc) t[cc] = (i + cc < cend) ? src.val(i + cc) : 0.f;
+        v = make_float4(t[0], t[1], t[2], t[3]);
+      }
+      process_row<MODE, XH, true>(src, v, i, cend, sm, w, lane, a, ov, oi, bk);
+    }
+    // the chunk's final partial ring chunk (< 64 entries)
+    wave_sync();
+    {
+      const bool valid = a.flushed + lane < a.staged;
+      uint2 e = make_uint2(0u, 0u);
+      if (valid) {
+        e = sm.ring[w][(a.flushed + lane) & (kRing - 1)];
+        ov[a.flushed + lane] = __uint_as_float(e.x);
+        oi[a.flushed + lane] = e.y;
+      }
+      note_maybe<MODE>(sm, e, valid, bk);
+    }
+    if (lane == 0) cntw[(int64_t)b * nchunk + c] = a.staged;
+    total += a.staged;
+    c = __builtin_amdgcn_readfirstlane(nx);
   }
+  if (lane == 0) sm.cnt[w] = total;
+  STAMP(1024 + b, 1);
   __syncthreads();
   STAMP(1024 + b, 2);
+
+  // ---- end of tile: bucket suffix counts, side list
+  const uint32_t msum = sm.mcount;
   {
     // thread t <-> maybe bucket jb = 254 - t (t = 255: the "sure" bucket 255);
     // cum[j] = #candidates with bucket >= j, sure included
     const int t = threadIdx.x;
     const int jb = t < kNMaybe ? kNMaybe - 1 - t : kNMaybe;
     const uint32_t hv = t < kNMaybe ? sm.hist[jb] : 0u;
-    uint32_t msum;
-    const uint32_t above = block_excl_scan(hv, sm.scratch, &msum);  // maybe keys in buckets > jb
-    const uint32_t csum = sm.cnt[0] + sm.cnt[1] + sm.cnt[2] + sm.cnt[3];
-    const uint32_t sure = csum - msum;
-    if (t == 0 && msum > side_cap) atomicOr(&ctrl->overflow, 1u);
-    const uint32_t cum = t < kNMaybe ? sure + above + hv : sure;
-    cum_tab[b * kNBucket + jb] = cum;
-    atomicAdd(&ctrl->G[b & (kNRep - 1)][jb], cum);
-    if (t < kNMaybe) sm.hist[jb] = above;  // counting-sort cursor of bucket jb (hist is dead now)
-    if (t < kK2Waves) cntw[b * kK2Waves + t] = sm.cnt[t];
+    uint32_t hsum;
+    const uint32_t above = block_excl_scan(hv, sm.scratch, &hsum);  // maybe keys in buckets > jb
+    uint32_t csum = 0;
+#pragma unroll
+    for (int ww = 0; ww < kK2Waves; ++ww) csum += sm.cnt[ww];
+    const uint32_t sure = csum - hsum;
+    if (t == 0 && (msum > side_cap || msum > (uint32_t)kMaybeCap)) atomicOr(&ctrl->overflow, 1u);
+    if (t < kNBucket) {
+      const uint32_t cum = t < kNMaybe ? sure + above + hv : sure;
+      cum_tab[b * kNBucket + jb] = cum;
+      atomicAdd(&ctrl->G[b & (kNRep - 1)][jb], cum);
+      if (t < kNMaybe) sm.hist[jb] = above;  // counting-sort cursor of bucket jb (hist is dead now)
+    }
   }
   __syncthreads();
-  uint32_t* __restrict__ sd = side + b * side_cap;
-  for (uint32_t j0 = 0; j0 < cnt; j0 += 256) {
-    uint32_t kk[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t j = j0 + q * 64 + lane;
-      kk[q] = cand_key<MODE>(ov, oi, j < cnt ? j : 0u, seed);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (j0 + q * 64 + lane < cnt && kk[q] < s_hi) {
-        const uint32_t p = atomicAdd(&sm.hist[(kk[q] - s_lo) >> shift], 1u);
-        if (p < side_cap) sd[p] = kk[q];
-      }
+  {
+    uint32_t* __restrict__ sd = side + b * side_cap;
+    const uint32_t mc = min(msum, min(side_cap, (uint32_t)kMaybeCap));
+    for (uint32_t j = threadIdx.x; j < mc; j += kK2Threads) {
+      const uint32_t key = sm.maybe[j];
+      const uint32_t p = atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
+      sd[p] = key;
     }
   }
   STAMP(1024 + b, 3);
@@ -915,6 +934,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_emit_kernel(
     const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
     int64_t idx_base) {
   __shared__ uint32_t scratch[24];
+  __shared__ uint32_t run_start[2 * kK4Threads + 1];
   const int64_t b = blockIdx.x;
   STAMP(24576 + b, 0);
   // every control word is independent: issue all loads before the first use
@@ -922,11 +942,21 @@ __global__ __launch_bounds__(kK4Threads) void topk_emit_kernel(
   uint32_t out = tile_info[b];
   uint32_t tie_run = tile_info[nb + b];
   const uint32_t mode = tile_info[2 * nb + b];
-  const uint4 cw4 = *reinterpret_cast<const uint4*>(cntw + b * kK2Waves);
+  const uint32_t nchunk = tile / (uint32_t)kChunk;  // <= 2 * kK4Threads (tile <= 2^31 / 256)
+  const uint32_t j0 = 2 * threadIdx.x, j1 = j0 + 1;
+  const uint32_t cw0 = j0 < nchunk ? cntw[b * nchunk + j0] : 0u;
+  const uint32_t cw1 = j1 < nchunk ? cntw[b * nchunk + j1] : 0u;
   if (fallback) return;
-  const uint32_t c0 = cw4.x, c1 = cw4.y, c2 = cw4.z, c3 = cw4.w;
-  const uint32_t e1 = c0, e2 = e1 + c1, e3 = e2 + c2, tot = e3 + c3;
-  const int64_t wlen = tile / kK2Waves;
+  {
+    // exclusive scan of the tile's per-chunk run lengths -> run_start[0..nchunk]
+    uint32_t tot;
+    const uint32_t pre = block_excl_scan(cw0 + cw1, scratch, &tot);
+    if (j0 < nchunk) run_start[j0] = pre;
+    if (j1 < nchunk) run_start[j1] = pre + cw0;
+    if (threadIdx.x == 0) run_start[nchunk] = tot;
+    __syncthreads();
+  }
+  const uint32_t tot = run_start[nchunk];
   const int64_t tb = b * tile;
   for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads) {
     const uint32_t p = p0 + threadIdx.x;
@@ -934,10 +964,13 @@ __global__ __launch_bounds__(kK4Threads) void topk_emit_kernel(
     float v = 0.f;
     uint32_t idx = 0, key = 0;
     if (valid) {
-      // position p of the tile's concatenated wave runs
-      const int run = (p >= e1) + (p >= e2) + (p >= e3);
-      const uint32_t start = run == 0 ? 0u : (run == 1 ? e1 : (run == 2 ? e2 : e3));
-      const int64_t a = tb + run * wlen + (p - start);
+      // position p of the tile's concatenated chunk runs: binary search of run_start
+      uint32_t lo = 0, hi = nchunk - 1;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (run_start[mid] <= p) lo = mid; else hi = mid - 1;
+      }
+      const int64_t a = tb + (int64_t)lo * kChunk + (p - run_start[lo]);
       v = cval[a];
       idx = cidx[a];
       key = MODE == kData ? fkey(v) : (rank_hash(seed, idx) >> 1);
@@ -1022,7 +1055,6 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
                 L.side_cap, seed, ctrl, cum, cntw, side, cval, cidx);
   profile_end("topk_stream", st);
   CHOCO_LAUNCHED("topk_stream_kernel");
-  if (CHOCO_K2_ABLATE) return CHOCO_OK;  // diagnostic builds: candidates are not valid
   CHOCO_KLAUNCH((topk_select_kernel<MODE, XH>), dim3(1), dim3(kK3Threads), 0, st, x, xh, n, k, L.nb,
                 L.side_cap, seed, scale, ctrl, cum, side, tinfo, out_val, out_idx, idx_base);
   CHOCO_LAUNCHED("topk_select_kernel");

@@ -8,12 +8,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from chocosgd_amd import build  # noqa: E402
 
 VARIANTS = {
-    "wpe6": ["CHOCO_K2_WPE=6"],
-    "wpe7": ["CHOCO_K2_WPE=7"],
-    "t1024": ["CHOCO_K2_TARGET=1024"],
     "stamps": ["CHOCO_STAMPS=1"],
-    "abl1": ["CHOCO_K2_ABLATE=1"],
-    "abl2": ["CHOCO_K2_ABLATE=2"],
+    "t512": ["CHOCO_K2_TARGET=512"],
 }
 
 

@@ -26,13 +26,18 @@ __device__ __forceinline__ unsigned fold(float4 v) {
 
 // tile t = TT float4 (4 waves x TT/4 contiguous); workgroup g processes tiles
 // g, g + G, g + 2G, ... (G = gridDim.x); interleave=false => one tile per workgroup
+// map: 0 = tile g; 1 = reversed (tile G-1-g); 2 = XCD-local (workgroups of XCD g%8
+// read the contiguous eighth g%8 of the tiles)
 template <int U>
 __global__ __launch_bounds__(256, 8) void k_tiles(const float4* __restrict__ x, long n4, long TT, long ntiles,
-                                                  unsigned* out, unsigned long long* st) {
+                                                  unsigned* out, unsigned long long* st, int map) {
   unsigned acc = 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (threadIdx.x == 0) st[2 * blockIdx.x] = wall_clock64();
-  for (long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  long first = blockIdx.x;
+  if (map == 1) first = gridDim.x - 1 - blockIdx.x;
+  if (map == 2) first = (long)(blockIdx.x % 8) * ((gridDim.x + 7) / 8) + blockIdx.x / 8;
+  for (long t = first; t < ntiles; t += gridDim.x) {
     const long beg = t * TT + w * (TT / 4);
     const long end = beg + TT / 4 < n4 ? beg + TT / 4 : n4;
     for (long b = beg; b + 64 * U <= end; b += 64 * U) {
@@ -73,35 +78,45 @@ static void report(const char* label, const std::vector<unsigned long long>& s, 
 
 int main() {
   const long n = 100000000, n4 = n / 4;
-  float4 *x, *junk;
+  float4* x;
   unsigned* out;
   unsigned long long* st;
   CK(hipMalloc(&x, n * 4));
-  CK(hipMalloc(&junk, 1024l * 1024 * 1024));
   CK(hipMalloc(&out, 4));
   CK(hipMalloc(&st, 2 * 65536 * sizeof(unsigned long long)));
   CK(hipMemset(x, 0x3c, n * 4));
   std::vector<unsigned long long> h(2 * 65536);
-  struct Cfg { const char* label; long TT; int G; };  // TT float4 per tile; G = 0 -> one wg per tile
-  const Cfg cfgs[] = {
-      {"contiguous 192KB tiles, 1/wg", 12288, 0},
-      {"interleaved 48KB tiles, G=2048", 3072, 2048},
-      {"interleaved 16KB tiles, G=2048", 1024, 2048},
-  };
-  for (int mode = 0; mode < 2; ++mode) {
-    for (const Cfg& c : cfgs) {
-      const long ntiles = (n4 + c.TT - 1) / c.TT;
-      const int G = c.G ? c.G : (int)ntiles;
-      for (int rep = 0; rep < 4; ++rep) {
-        if (mode == 1) CK(hipMemset(junk, rep, 1024l * 1024 * 1024));  // evict: 1 GiB of other lines
-        hipLaunchKernelGGL((k_tiles<4>), dim3(G), dim3(256), 0, 0, x, n4, c.TT, ntiles, out, st);
-        CK(hipGetLastError());
+  const long TT = 12288;  // 192 KB tiles, one per workgroup (top-k stream shape)
+  const long ntiles = (n4 + TT - 1) / TT;
+  const int G = (int)ntiles;
+  const char* names[3] = {"tile = wg id", "tile = reversed wg id", "XCD-local eighths"};
+  for (int map = 0; map < 3; ++map) {
+    for (int rep = 0; rep < 4; ++rep) {
+      hipLaunchKernelGGL((k_tiles<4>), dim3(G), dim3(256), 0, 0, x, n4, TT, ntiles, out, st, map);
+      CK(hipGetLastError());
+    }
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(h.data(), st, 2 * G * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    // per-eighth medians by WORKGROUP id (dispatch order) and by TILE position
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int g = 0; g < G; ++g) { t0 = std::min(t0, h[2 * g]); t1 = std::max(t1, h[2 * g + 1]); }
+    printf("%-24s span %7.2f us\n", names[map], (t1 - t0) * 0.01);
+    for (int by = 0; by < 3; ++by) {
+      printf("   median wg time by %-14s:", by == 0 ? "wg id eighth" : (by == 1 ? "tile eighth" : "XCD (wg%8)"));
+      for (int q = 0; q < 8; ++q) {
+        std::vector<double> d;
+        for (int g = 0; g < G; ++g) {
+          long tile = g;
+          if (map == 1) tile = G - 1 - g;
+          if (map == 2) tile = (long)(g % 8) * ((G + 7) / 8) + g / 8;
+          const int key = by == 0 ? (int)((long)g * 8 / G) : (by == 1 ? (int)(tile * 8 / ntiles) : g % 8);
+          if (key == q) d.push_back((h[2 * g + 1] - h[2 * g]) * 0.01);
+        }
+        if (d.empty()) { printf("     -"); continue; }
+        std::nth_element(d.begin(), d.begin() + d.size() / 2, d.end());
+        printf(" %5.1f", d[d.size() / 2]);
       }
-      CK(hipDeviceSynchronize());
-      CK(hipMemcpy(h.data(), st, 2 * G * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-      char lab[96];
-      snprintf(lab, sizeof lab, "%s %s", mode ? "[after 1GiB write]" : "[back to back]   ", c.label);
-      report(lab, h, G, c.G == 0);
+      printf("\n");
     }
   }
   return 0;
