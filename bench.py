@@ -272,7 +272,8 @@ def main():
         traffic = None
         tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tf):
-            traffic = json.load(open(tf)).get(f"{args.workload}:{w.n}")
+            entry = json.load(open(tf)).get(f"{args.workload}:{w.n}")
+            traffic = int(entry["bytes"]) if entry else None
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,

@@ -55,8 +55,6 @@ static_assert(kK2Target <= 2048, "K3 keeps at most two tiles per thread");
 constexpr int64_t kChunk = 4096;        // elements a wave claims at a time (LDS counter)
 static_assert(kTileQuant % kChunk == 0 && kChunk % (256 * kK2Unroll) == 0, "chunk geometry");
 static_assert((int64_t(1) << 31) / kK2Target / kChunk <= 2 * 1024, "K4 scans <= 2 chunk counts per thread");
-constexpr int kRing = 512;              // LDS ring entries (value, index) per wave
-constexpr int kFlush = 64;              // ring -> HBM in 64-entry (2 x 256-B store) chunks
 constexpr int kMaybeCap = 16384;        // maybe keys per tile kept in LDS (= side-list capacity)
 constexpr int kNBucket = 256;           // 255 "maybe" buckets + 1 "sure"
 constexpr int kNMaybe = kNBucket - 1;
@@ -510,20 +508,31 @@ __global__ void topk_set_params_kernel(TopkCtrl* __restrict__ ctrl, uint32_t s_l
 // Measured (tools/probe_position.hip, probe_balance.hip): when two or more
 // workgroups share a CU, the one dispatched first streams first and the last
 // ones finish alone with few bytes in flight; with ONE workgroup per CU every
-// workgroup finishes within ~10 % of the others and the read runs at 6.4 TB/s.
-// 137 KiB of LDS enforces that placement.  Maybe keys (s_lo <= key < s_hi) are
-// binned and staged in LDS as the ring is flushed, so the end of the tile only
-// scans 256 bucket counts and counting-sorts the staged keys to the side list.
+// workgroup finishes within ~10 % of the others.  LDS use (> 80 KiB) enforces
+// that placement.  Inside the workgroup the CU's issue arbiter favours older
+// waves, so waves claim kChunk-element chunks through an LDS counter.
+//
+// Two-level compaction, sized for k << n: per float4 row a wave only decides
+// which LANES hold a candidate (|v| >= s_lo, one ballot) and appends those lanes'
+// float4 + base index to a per-wave LDS entry ring (~3 of 64 lanes per row at
+// k = 1 %).  Every 64 entries are expanded to (value, index) pairs with the
+// exact integer key test and stored to the chunk's slot range; maybe keys
+// (s_lo <= key < s_hi) are binned and staged in LDS on the way, so the end of
+// the tile only scans 256 bucket counts and counting-sorts the staged keys.
 // ----------------------------------------------------------------------------
+constexpr int kEnt = 128;  // entry ring per wave (flush at 64: <= 63 + 64 pending)
+
 struct StreamSmem {
-  uint2 ring[kK2Waves][kRing];  // (value bits, index) per wave, in index order
-  uint2 trash[kK2Waves][64];    // per-lane sink of the branch-free stage writes
-  uint32_t maybe[kMaybeCap];    // the tile's maybe keys, in flush order
-  uint32_t hist[kNBucket];      // maybe-key bucket counts, then counting-sort cursors
+  float4 ent_v[kK2Waves][kEnt];   // staged lanes: the float4 row slice
+  uint32_t ent_i[kK2Waves][kEnt]; // ... and the index of its first element
+  float4 trash_v[kK2Waves][64];   // per-lane sinks of the branch-free batch writes
+  uint32_t trash_i[kK2Waves][64];
+  uint32_t maybe[kMaybeCap];      // the tile's maybe keys, in flush order
+  uint32_t hist[kNBucket];        // maybe-key bucket counts, then counting-sort cursors
   uint32_t cnt[kK2Waves];
   uint32_t scratch[24];
   uint32_t mcount;
-  uint32_t next_chunk;          // the tile's chunk counter (waves claim chunks)
+  uint32_t next_chunk;            // the tile's chunk counter (waves claim chunks)
 };
 
 // Unconditional float4 loads of kK2Unroll rows (no branch around a load: the
@@ -548,88 +557,133 @@ CHOCO_DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Per-wave compaction state (wave-uniform): entries appended / written out.
+// Per-wave compaction state of the current chunk (wave-uniform).
 struct WaveAcc {
-  uint32_t staged, flushed;
+  uint32_t estaged, eflushed;  // entry ring: appended / expanded
+  uint32_t staged;             // candidates written to the chunk's slot range
 };
 
 // Per-tile bucket geometry, read once from the control block.
 struct Buckets {
   uint32_t s_lo, s_hi, shift;
+  float s_lo_f;  // s_lo as a float: !(|v| < s_lo_f) is a superset test of key >= s_lo
   uint64_t seed;
 };
 
-// One flushed entry per lane: if its key is a "maybe" key, bin it and stage it
-// in the tile's LDS list (one LDS atomic per wave for the list slots).
-template <int MODE>
-CHOCO_DEV void note_maybe(StreamSmem& sm, uint2 e, bool valid, const Buckets& bk) {
-  const uint32_t key = MODE == kData ? fkey(__uint_as_float(e.x)) : (rank_hash(bk.seed, e.y) >> 1);
-  const bool mb = valid && key < bk.s_hi;  // every ring entry has key >= s_lo
-  const uint64_t bm = ballot(mb);
-  if (bm == 0ull) return;  // wave-uniform
-  uint32_t base = 0;
-  if (lane_id() == 0) base = atomicAdd(&sm.mcount, (uint32_t)__popcll(bm));
-  base = __builtin_amdgcn_readfirstlane(base);
-  if (mb) {
-    const uint32_t p = base + mask_prefix(bm);
-    if (p < (uint32_t)kMaybeCap) sm.maybe[p] = key;
-    atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
-  }
-}
-
-// Write whole 64-entry chunks of the ring out (one 256-B store per array each).
-// The ring never holds more than 63 + 256 entries, so nothing is overwritten
-// before it is flushed.  Counters are wave-uniform; readfirstlane keeps them in
-// SGPRs so the flush test is a scalar branch.
-template <int MODE>
-CHOCO_DEV void ring_flush(StreamSmem& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
-                          uint32_t* __restrict__ oi, const Buckets& bk) {
+// Expand entries [eflushed, eflushed + nent) (nent <= 64, one per lane) into
+// (value, index) candidates of the chunk [.., cend) in index order.
+template <int MODE, bool XH>
+CHOCO_DEV void expand_entries(const Src<MODE, XH>& src, StreamSmem& sm, int w, int lane, WaveAcc& a, uint32_t nent,
+                              int64_t cend, float* __restrict__ ov, uint32_t* __restrict__ oi, const Buckets& bk) {
   wave_sync();
-  const uint32_t end = __builtin_amdgcn_readfirstlane(a.staged) & ~(uint32_t)(kFlush - 1);
-#pragma unroll 1
-  for (uint32_t f = __builtin_amdgcn_readfirstlane(a.flushed); f < end; f += kFlush) {
-    const uint2 e = sm.ring[w][(f + lane) & (kRing - 1)];
-    ov[f + lane] = __uint_as_float(e.x);
-    oi[f + lane] = e.y;
-    note_maybe<MODE>(sm, e, true, bk);
-  }
-  a.flushed = end;
-}
-
-// One float4 row per lane (256 elements per wave): append candidates to the ring.
-// Branch-free per lane: one ballot per component gives the lane prefix
-// (4 x mbcnt); every lane then writes its (value, index) pair either to its ring
-// slot or to its own trash slot, so the only branches are wave-uniform.
-template <int MODE, bool XH, bool GUARD>
-CHOCO_DEV void process_row(const Src<MODE, XH>& src, const float4 v4, int64_t i, int64_t wend, StreamSmem& sm,
-                           int w, int lane, WaveAcc& a, float* __restrict__ ov, uint32_t* __restrict__ oi,
-                           const Buckets& bk) {
-  const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
-  bool cand[4];
+  const bool have = (uint32_t)lane < nent;
+  const uint32_t slot = (a.eflushed + lane) & (kEnt - 1);
+  const float4 ev = have ? sm.ent_v[w][slot] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const uint32_t ei = have ? sm.ent_i[w][slot] : 0u;
+  const float vv[4] = {ev.x, ev.y, ev.z, ev.w};
+  uint32_t kk[4];
+  bool f[4];
   uint64_t m[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    const bool valid = !GUARD || i + c < wend;
-    const uint32_t key = MODE == kData ? fkey(vv[c]) : (valid ? src.key_of(i + c, 0.f) : 0u);
-    cand[c] = valid && key >= bk.s_lo;
-    m[c] = ballot(cand[c]);
+    kk[c] = MODE == kData ? fkey(vv[c]) : (rank_hash(bk.seed, ei + c) >> 1);
+    f[c] = have && (int64_t)ei + c < cend && kk[c] >= bk.s_lo;
+    m[c] = ballot(f[c]);
   }
-  if ((m[0] | m[1] | m[2] | m[3]) == 0ull) return;  // wave-uniform: no candidate in this row
   uint32_t pos = a.staged + mask_prefix(m[0]) + mask_prefix(m[1]) + mask_prefix(m[2]) + mask_prefix(m[3]);
   a.staged += (uint32_t)(__popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]));
-  uint2* __restrict__ ring = sm.ring[w];
-  uint2* __restrict__ sink = &sm.trash[w][lane];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    if (m[c] != 0ull) {  // wave-uniform
-      const float v = MODE == kData ? vv[c] : (cand[c] ? src.val(i + c) : 0.f);
-      uint2* dst = cand[c] ? ring + (pos & (kRing - 1)) : sink;
-      *dst = make_uint2(__float_as_uint(v), (uint32_t)(i + c));
-      pos += cand[c] ? 1u : 0u;
+    if (m[c] == 0ull) continue;  // wave-uniform
+    if (f[c]) {
+      ov[pos] = MODE == kData ? vv[c] : src.val((int64_t)ei + c);
+      oi[pos] = ei + c;
+      ++pos;
+    }
+    // maybe keys: bin and stage (one LDS atomic per wave for the list slots)
+    const bool mb = f[c] && kk[c] < bk.s_hi;
+    const uint64_t bm = ballot(mb);
+    if (bm != 0ull) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&sm.mcount, (uint32_t)__popcll(bm));
+      base = __builtin_amdgcn_readfirstlane(base);
+      if (mb) {
+        const uint32_t p = base + mask_prefix(bm);
+        if (p < (uint32_t)kMaybeCap) sm.maybe[p] = kk[c];
+        atomicAdd(&sm.hist[(kk[c] - bk.s_lo) >> bk.shift], 1u);
+      }
     }
   }
   a.staged = __builtin_amdgcn_readfirstlane(a.staged);
-  if (a.staged - a.flushed >= (uint32_t)kFlush) ring_flush<MODE>(sm, w, lane, a, ov, oi, bk);
+  a.eflushed += nent;
+}
+
+// One float4 row per lane (256 elements per wave): stage the lanes that hold a
+// candidate.  The float test !(|v| < s_lo_f) is a superset of key >= s_lo (NaN
+// passes); expand_entries applies the exact test.
+template <int MODE, bool XH, bool GUARD>
+CHOCO_DEV void process_row(const Src<MODE, XH>& src, const float4 v4, int64_t i, int64_t cend, StreamSmem& sm,
+                           int w, int lane, WaveAcc& a, float* __restrict__ ov, uint32_t* __restrict__ oi,
+                           const Buckets& bk) {
+  bool any = false;
+  if (MODE == kData) {
+    const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) any |= (!GUARD || i + c < cend) && !(fabsf(vv[c]) < bk.s_lo_f);
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) any |= (!GUARD || i + c < cend) && src.key_of(i + c, 0.f) >= bk.s_lo;
+  }
+  const uint64_t M = ballot(any);
+  if (M == 0ull) return;  // wave-uniform: no candidate lane in this row
+  if (any) {
+    const uint32_t slot = (a.estaged + mask_prefix(M)) & (kEnt - 1);
+    sm.ent_v[w][slot] = v4;
+    sm.ent_i[w][slot] = (uint32_t)i;
+  }
+  a.estaged = __builtin_amdgcn_readfirstlane(a.estaged + (uint32_t)__popcll(M));
+  if (a.estaged - a.eflushed >= 64u) expand_entries<MODE, XH>(src, sm, w, lane, a, 64u, cend, ov, oi, bk);
+}
+
+// Eight full rows (one load batch) as ONE branch-free block, so the compiler can
+// interleave the rows' dependent compare -> ballot -> prefix -> LDS-store chains
+// (the kernel is otherwise issue-stall bound at 4 waves per SIMD).  Lanes
+// without a candidate store to their own trash slot.  If the batch could
+// overflow the entry ring (dense inputs), rows take the per-row path instead.
+template <bool XH>
+CHOCO_DEV void process_batch(const Src<kData, XH>& src, const float4 (&A)[kK2Unroll], int64_t base, int64_t cend,
+                             StreamSmem& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
+                             uint32_t* __restrict__ oi, const Buckets& bk) {
+  bool any[kK2Unroll];
+  uint64_t M[kK2Unroll];
+  uint32_t add = 0;
+#pragma unroll
+  for (int u = 0; u < kK2Unroll; ++u) {
+    any[u] = !(fabsf(A[u].x) < bk.s_lo_f) || !(fabsf(A[u].y) < bk.s_lo_f) || !(fabsf(A[u].z) < bk.s_lo_f) ||
+             !(fabsf(A[u].w) < bk.s_lo_f);
+    M[u] = ballot(any[u]);
+    add += (uint32_t)__popcll(M[u]);
+  }
+  add = __builtin_amdgcn_readfirstlane(add);
+  if (add == 0u) return;
+  if (a.estaged - a.eflushed + add <= (uint32_t)kEnt) {
+    uint32_t run = a.estaged;
+#pragma unroll
+    for (int u = 0; u < kK2Unroll; ++u) {
+      const uint32_t slot = (run + mask_prefix(M[u])) & (kEnt - 1);
+      float4* pv = any[u] ? &sm.ent_v[w][slot] : &sm.trash_v[w][lane];
+      uint32_t* pi = any[u] ? &sm.ent_i[w][slot] : &sm.trash_i[w][lane];
+      *pv = A[u];
+      *pi = (uint32_t)(base + u * 256 + 4 * lane);
+      run += (uint32_t)__popcll(M[u]);
+    }
+    a.estaged = __builtin_amdgcn_readfirstlane(run);
+    while (a.estaged - a.eflushed >= 64u) expand_entries<kData, XH>(src, sm, w, lane, a, 64u, cend, ov, oi, bk);
+  } else {
+#pragma unroll
+    for (int u = 0; u < kK2Unroll; ++u)
+      process_row<kData, XH, false>(src, A[u], base + u * 256 + 4 * lane, cend, sm, w, lane, a, ov, oi, bk);
+  }
 }
 
 template <int MODE, bool XH>
@@ -640,7 +694,12 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     uint32_t* __restrict__ cidx) {
   __shared__ StreamSmem sm;
   STAMP(1024 + blockIdx.x, 0);
-  const Buckets bk{ctrl->s_lo, ctrl->s_hi, ctrl->shift, seed};
+  Buckets bk;
+  bk.s_lo = ctrl->s_lo;
+  bk.s_hi = ctrl->s_hi;
+  bk.shift = ctrl->shift;
+  bk.s_lo_f = __uint_as_float(bk.s_lo);  // NaN when s_lo is a NaN key: then every lane is staged
+  bk.seed = seed;
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   const int64_t b = blockIdx.x;
@@ -650,10 +709,8 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   if (threadIdx.x == 0) { sm.mcount = 0; sm.next_chunk = 0; }
   __syncthreads();
 
-  // Waves claim the tile's kChunk-element chunks through an LDS counter: the
-  // CU's issue arbiter favours older waves, so a static split leaves the youngest
-  // waves finishing last with few bytes in flight.  Chunk c's candidates go to
-  // its own slot range and count, so the tile's output order is the chunk order.
+  // Chunk c's candidates go to its own slot range and count, so the tile's
+  // output order is the chunk order.
   const uint32_t nchunk = tile / (uint32_t)kChunk;
   uint32_t total = 0;
   uint32_t c = 0;
@@ -666,15 +723,19 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     const int64_t cend = min(cbeg + kChunk, n);
     float* __restrict__ ov = cval + cbeg;
     uint32_t* __restrict__ oi = cidx + cbeg;
-    WaveAcc a{0u, 0u};
+    WaveAcc a{0u, 0u, 0u};
     const int64_t full_end = cend > cbeg ? cbeg + (cend - cbeg) / kStep * kStep : cbeg;
     for (int64_t base = cbeg; base < full_end; base += kStep) {
       float4 A[kK2Unroll];
-      if (MODE == kData) load_rows_full<XH>(x, xh, base, lane, A);
+      if constexpr (MODE == kData) {
+        load_rows_full<XH>(x, xh, base, lane, A);
+        process_batch<XH>(src, A, base, cend, sm, w, lane, a, ov, oi, bk);
+      } else {
 #pragma unroll
-      for (int u = 0; u < kK2Unroll; ++u)
-        process_row<MODE, XH, false>(src, MODE == kData ? A[u] : make_float4(0.f, 0.f, 0.f, 0.f),
-                                     base + u * 256 + 4 * lane, cend, sm, w, lane, a, ov, oi, bk);
+        for (int u = 0; u < kK2Unroll; ++u)
+          process_row<MODE, XH, false>(src, make_float4(0.f, 0.f, 0.f, 0.f), base + u * 256 + 4 * lane, cend, sm,
+                                       w, lane, a, ov, oi, bk);
+      }
     }
     // tail (< kStep elements, last chunk only): guarded loads
     for (int64_t base = full_end; base < cend; base += 256) {
@@ -688,18 +749,9 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       }
       process_row<MODE, XH, true>(src, v, i, cend, sm, w, lane, a, ov, oi, bk);
     }
-    // the chunk's final partial ring chunk (< 64 entries)
-    wave_sync();
-    {
-      const bool valid = a.flushed + lane < a.staged;
-      uint2 e = make_uint2(0u, 0u);
-      if (valid) {
-        e = sm.ring[w][(a.flushed + lane) & (kRing - 1)];
-        ov[a.flushed + lane] = __uint_as_float(e.x);
-        oi[a.flushed + lane] = e.y;
-      }
-      note_maybe<MODE>(sm, e, valid, bk);
-    }
+    // the chunk's remaining entries (< 64)
+    const uint32_t rest = a.estaged - a.eflushed;
+    if (rest) expand_entries<MODE, XH>(src, sm, w, lane, a, rest, cend, ov, oi, bk);
     if (lane == 0) cntw[(int64_t)b * nchunk + c] = a.staged;
     total += a.staged;
     c = __builtin_amdgcn_readfirstlane(nx);
@@ -958,39 +1010,71 @@ __global__ __launch_bounds__(kK4Threads) void topk_emit_kernel(
   }
   const uint32_t tot = run_start[nchunk];
   const int64_t tb = b * tile;
-  for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads) {
-    const uint32_t p = p0 + threadIdx.x;
-    const bool valid = p < tot;
-    float v = 0.f;
-    uint32_t idx = 0, key = 0;
-    if (valid) {
-      // position p of the tile's concatenated chunk runs: binary search of run_start
-      uint32_t lo = 0, hi = nchunk - 1;
+  // Batches of kK4Threads * R candidates; thread t owns R consecutive positions
+  // (thread order = index order), loads them all at once, and one block scan of
+  // its count places them (two scans only when ties at T are split).
+  constexpr int R = 8;
+  for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads * R) {
+    const uint32_t pb = p0 + threadIdx.x * R;
+    uint32_t lo = 0;
+    if (pb < tot) {
+      uint32_t hi = nchunk - 1;
       while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
-        if (run_start[mid] <= p) lo = mid; else hi = mid - 1;
+        if (run_start[mid] <= pb) lo = mid; else hi = mid - 1;
       }
-      const int64_t a = tb + (int64_t)lo * kChunk + (p - run_start[lo]);
-      v = cval[a];
-      idx = cidx[a];
-      key = MODE == kData ? fkey(v) : (rank_hash(seed, idx) >> 1);
     }
-    const bool gt = valid && key > T;
-    const bool eq = valid && key == T;
-    bool sel;
-    if (mode == kTakePartial) {
-      uint32_t neq;
-      const uint32_t rank = tie_run + block_excl_scan(eq ? 1u : 0u, scratch, &neq);
-      sel = gt || (eq && rank < r);
-      tie_run += neq;
+    int64_t addr[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const uint32_t p = pb + i;
+      if (p < tot)
+        while (run_start[lo + 1] <= p) ++lo;  // the run of position p (runs may be empty)
+      addr[i] = p < tot ? tb + (int64_t)lo * kChunk + (p - run_start[lo]) : tb;  // clamped: loads are unconditional
+    }
+    float v[R];
+    uint32_t idx[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      v[i] = cval[addr[i]];
+      idx[i] = cidx[addr[i]];
+    }
+    bool gt[R], eq[R];
+    uint32_t neq = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const bool valid = pb + i < tot;
+      const uint32_t key = MODE == kData ? fkey(v[i]) : (rank_hash(seed, idx[i]) >> 1);
+      gt[i] = valid && key > T;
+      eq[i] = valid && key == T;
+      neq += eq[i] ? 1u : 0u;
+    }
+    bool sel[R];
+    if (mode == kTakePartial) {  // workgroup-uniform
+      uint32_t eq_total;
+      uint32_t rank = tie_run + block_excl_scan(neq, scratch, &eq_total);
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        sel[i] = gt[i] || (eq[i] && rank < r);
+        rank += eq[i] ? 1u : 0u;
+      }
+      tie_run += eq_total;
     } else {
-      sel = gt || (eq && mode == kTakeAll);
+#pragma unroll
+      for (int i = 0; i < R; ++i) sel[i] = gt[i] || (eq[i] && mode == kTakeAll);
     }
+    uint32_t nmine = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) nmine += sel[i] ? 1u : 0u;
     uint32_t nsel;
-    const uint32_t pos = out + block_excl_scan(sel ? 1u : 0u, scratch, &nsel);
-    if (sel) {
-      out_val[pos] = v * scale;
-      out_idx[pos] = (int32_t)((int64_t)idx + idx_base);
+    uint32_t pos = out + block_excl_scan(nmine, scratch, &nsel);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (sel[i]) {
+        out_val[pos] = v[i] * scale;
+        out_idx[pos] = (int32_t)((int64_t)idx[i] + idx_base);
+        ++pos;
+      }
     }
     out += nsel;
   }
@@ -1162,6 +1246,35 @@ CHOCO_API int choco_topk_compress_segmented(const float* x, const float* xhat, c
 }
 
 #if CHOCO_STAMPS
+// Diagnostic builds only: re-launch the stream kernel alone `reps` times back to
+// back (after one full choco_topk_compress on the same workspace set its
+// thresholds), timed with dispatch-attached events -> *avg_ms.
+CHOCO_API int choco_dbg_stream_only(const float* x, int64_t n, void* ws, size_t ws_bytes, int32_t reps,
+                                    double* avg_ms, void* stream) {
+  hipStream_t st = as_stream(stream);
+  const TopkLayout L = topk_layout(n);
+  CHOCO_REQUIRE(ws && ws_bytes >= L.total && reps > 0, "bad arguments");
+  char* base = static_cast<char*>(ws);
+  TopkCtrl* ctrl = reinterpret_cast<TopkCtrl*>(base + L.off_ctrl);
+  hipEvent_t a, b;
+  CHOCO_HIP(hipEventCreate(&a));
+  CHOCO_HIP(hipEventCreate(&b));
+  CHOCO_HIP(hipEventRecord(a, st));
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL((topk_stream_kernel<kData, false>), dim3(L.nb), dim3(kK2Threads), 0, st, x, nullptr, n,
+                       L.tile, L.nb, L.side_cap, (uint64_t)0, ctrl, reinterpret_cast<uint32_t*>(base + L.off_cum),
+                       reinterpret_cast<uint32_t*>(base + L.off_cntw), reinterpret_cast<uint32_t*>(base + L.off_side),
+                       reinterpret_cast<float*>(base + L.off_cval), reinterpret_cast<uint32_t*>(base + L.off_cidx));
+  CHOCO_HIP(hipEventRecord(b, st));
+  CHOCO_HIP(hipEventSynchronize(b));
+  float ms = 0.f;
+  CHOCO_HIP(hipEventElapsedTime(&ms, a, b));
+  *avg_ms = ms / reps;
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  return CHOCO_OK;
+}
+
 // Diagnostic builds only: copy out (and clear) the phase stamps.
 CHOCO_API int choco_dbg_stamps(unsigned long long* host, size_t bytes) {
   const size_t all = sizeof(unsigned long long) * kStampSlots * 4;
