@@ -46,9 +46,12 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--workload", default="topk", choices=sorted(WORKLOADS))
     p.add_argument("--n", type=int, default=0, help="override elements per worker")
+    p.add_argument("--nbuf", type=int, default=4, help="delta buffers compressed in rotation (one per step)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-e2e", action="store_true", help="skip the host-resident (PCIe-inclusive) leg")
+    p.add_argument("--lib", default=None, help=argparse.SUPPRESS)  # diagnostic variant (tools/build_variants.py)
+    p.add_argument("--diag-evict", action="store_true", help=argparse.SUPPRESS)  # 1 GiB read after each step
     return p.parse_args()
 
 
@@ -65,7 +68,11 @@ class Worker:
         self.nb = neighborhood(rank, world)
         self.peers = [r for r in self.nb if r != rank]
         g = torch.Generator(device=dev).manual_seed(1000 + rank)
-        self.d = torch.randn(self.n, generator=g, device=dev)            # the worker's delta x - x_hat
+        # The worker's delta x - x_hat.  Consecutive steps compress different
+        # buffers (args.nbuf, independent draws), so each step selects a new
+        # index set and the accumulate dirties new lines, as in training.
+        self.ds = [torch.randn(self.n, generator=g, device=dev) for _ in range(max(1, args.nbuf))]
+        self.d = self.ds[0]
         self.hat = torch.zeros(self.n, device=dev)
         self.mem = torch.zeros(self.n, device=dev)
         if self.op == "topk":
@@ -83,6 +90,7 @@ class Worker:
 
     def compress(self):
         c = self.codec
+        self.d = self.ds[self.step_id % len(self.ds)]
         if self.op == "topk":
             c.topk(self.d, self.k, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]))
         elif self.op == "qsgd":
@@ -151,7 +159,7 @@ def e2e_rate(w, reps=5):
     for i in range(reps + 1):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        w.d.copy_(host_x, non_blocking=True)
+        w.ds[w.step_id % len(w.ds)].copy_(host_x, non_blocking=True)  # the buffer compress() takes next
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         w.compress()
@@ -230,7 +238,9 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-    from chocosgd_amd import codec
+    from chocosgd_amd import _lib, codec
+    if args.lib:
+        _lib.load(args.lib)
     codec.lib()
     w = Worker(args, rank, world, dev)
 
@@ -240,6 +250,15 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    if args.diag_evict:
+        junk = torch.ones(256 * 1024 * 1024, device=dev)
+        sink = torch.empty(1, device=dev)
+        inner = w.step
+
+        def evicting_step():
+            inner()
+            torch.sum(junk, dim=0, keepdim=True, out=sink)
+        w.step = evicting_step
     for _ in range(args.warmup):
         w.step()
     barrier()
@@ -254,7 +273,7 @@ def main():
     codec.profile_enable(False)
     ktot, kcnt = codec.profile_read(w.kernel)
     kernels = {}
-    for name in ("topk_stream", "sparse_accumulate", "qsgd_norm", "qsgd_quantize", "qsgd_accumulate", "sign_pack",
+    for name in ("topk_stream", "topk_finish", "sparse_accumulate", "qsgd_norm", "qsgd_quantize", "qsgd_accumulate", "sign_pack",
                  "sign_accumulate"):
         t, c = codec.profile_read(name)
         if c:

@@ -14,6 +14,9 @@
 namespace choco {
 
 constexpr int kEwThreads = 256;
+#ifndef CHOCO_ACC_STORE  // diagnostic knob: 0 plain, 1 nt, 2 sc1 stores in the sparse accumulate
+#define CHOCO_ACC_STORE 0
+#endif
 
 __global__ __launch_bounds__(kEwThreads) void gossip_kernel(float* __restrict__ x, const float* __restrict__ mem,
                                                             const float* __restrict__ hat, float gamma, int64_t n) {
@@ -42,9 +45,17 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_kernel(const float* __r
   for (int64_t i = (int64_t)blockIdx.x * kEwThreads + threadIdx.x; i < k; i += stride) {
     const int64_t j = idx[i];
     const float v = val[i];
-    if (hat) hat[j] = hat[j] + v;
     const float wv = w * v;
+#if CHOCO_ACC_STORE == 0
+    if (hat) hat[j] = hat[j] + v;
     mem[j] = mem[j] + wv;
+#elif CHOCO_ACC_STORE == 1
+    if (hat) __builtin_nontemporal_store(hat[j] + v, &hat[j]);
+    __builtin_nontemporal_store(mem[j] + wv, &mem[j]);
+#else
+    if (hat) __hip_atomic_store(&hat[j], hat[j] + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&mem[j], mem[j] + wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
   }
 }
 

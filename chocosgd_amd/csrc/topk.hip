@@ -9,30 +9,31 @@
 //   out = { i : key_i > T }  U  { the (k - #{key > T}) lowest i with key_i == T },
 //   emitted as (d_i, i) in ascending i.
 //
-// Fast path for large n ("pipeline"); the delta is read from HBM ONCE:
-//   K1 topk_sample  : 64 workgroups histogram a 64K-element strided sample and
-//                     keep their local tails; the last one picks a candidate
-//                     floor s_lo (#{key >= s_lo} >= k with a ~6 sigma margin)
-//                     and a "sure" ceiling s_hi (#{key >= s_hi} < k).
-//                     [s_lo, s_hi) is split into 255 key-buckets of width 2^shift.
-//   K2 topk_stream  : one workgroup per tile (4 waves, each a contiguous range);
-//                     per float4 row the wave ballots candidates (key >= s_lo)
-//                     and appends (value, index) in index order to an LDS ring
-//                     flushed to the wave's slot of the candidate buffer in
-//                     256-B stores.  At the end of the tile the "maybe" keys
-//                     (key < s_hi) are re-read, bucket-counted and counting-sorted
-//                     into a per-tile side list; per-tile bucket suffix counts go
-//                     to a [tile][256] table and to 16 replicated global totals.
-//   K3 topk_select  : one workgroup finds the bucket j* holding the k-th key
-//                     from the totals, copies every tile's bucket-j* keys (a few
-//                     thousand) into LDS, radix-selects T and the tie quota r
-//                     exactly and scans per-tile output offsets.
-//   K4 topk_emit    : one workgroup per tile compacts the tile's candidates into
-//                     the final ascending-index output.
+// Fast path for large n ("pipeline"); the delta is read from HBM ONCE, in two
+// kernels:
+//   K2 topk_stream  : one 16-wave workgroup per tile, one per CU.  Prologue:
+//                     every workgroup histograms the same 32K-element strided
+//                     sample in LDS (while its first load batch is in flight)
+//                     and derives the candidate floor s_lo (#{key >= s_lo} >= k
+//                     with a ~6 sigma margin) and the "sure" ceiling s_hi
+//                     (#{key >= s_hi} < k); [s_lo, s_hi) is split into 255
+//                     key-buckets of width 2^shift.  Stream: per float4 row the
+//                     wave ballots candidates (key >= s_lo) and appends them in
+//                     index order to an LDS ring flushed to the chunk's slots of
+//                     the candidate buffer.  Tile end: the "maybe" keys
+//                     (key < s_hi) are bucket-counted and counting-sorted into a
+//                     per-tile side list; per-tile bucket suffix counts go to a
+//                     [tile][256] table and to 16 replicated global totals.
+//   K34 topk_finish : one workgroup per tile.  Each finds the bucket j* of the
+//                     k-th key from the totals, copies every tile's bucket-j*
+//                     keys (a few thousand) into LDS, radix-selects T and the tie
+//                     quota r exactly, scans all tiles' output offsets, and then
+//                     compacts its own tile's candidates into the final
+//                     ascending-index output.
 //   If the sample's guess was off (too few candidates, T in the "sure" range,
-//   bucket j* larger than LDS, or a side list overflowed), K3 runs an exact
-//   single-workgroup radix select over the full input instead (correct, slow,
-//   data-dependent only) and K4 exits.
+//   bucket j* larger than LDS, or a side list overflowed), K34's workgroup 0
+//   runs an exact single-workgroup radix select over the full input instead
+//   (correct, slow, data-dependent only).
 // Small n (<= kSmallN) and every segment of the batched segmented path use
 // the same exact radix select (block_topk_exact) in one workgroup.
 #include "choco_common.h"
@@ -51,21 +52,16 @@ constexpr int kK2Waves = kK2Threads / 64;
 constexpr int kK2Unroll = 8;            // float4 rows per wave per load batch (8 KiB in flight)
 constexpr int64_t kK2Target = CHOCO_K2_TARGET;
 constexpr int64_t kTileQuant = (int64_t)kK2Waves * kK2Unroll * 256;   // 32768 elements
-static_assert(kK2Target <= 2048, "K3 keeps at most two tiles per thread");
+static_assert(kK2Target <= 1024, "K34 keeps one tile per thread");
 constexpr int64_t kChunk = 4096;        // elements a wave claims at a time (LDS counter)
 static_assert(kTileQuant % kChunk == 0 && kChunk % (256 * kK2Unroll) == 0, "chunk geometry");
 static_assert((int64_t(1) << 31) / kK2Target / kChunk <= 2 * 1024, "K4 scans <= 2 chunk counts per thread");
-constexpr int kMaybeCap = 16384;        // maybe keys per tile kept in LDS (= side-list capacity)
+constexpr int kMaybeCap = 65536;        // side-list capacity per tile (maybe keys)
 constexpr int kNBucket = 256;           // 255 "maybe" buckets + 1 "sure"
 constexpr int kNMaybe = kNBucket - 1;
 constexpr int kNRep = 16;               // replicas of the global bucket totals
 constexpr int kMCap = 16384;            // max keys of bucket j* selected in LDS
-constexpr int kK3Threads = 1024;
 constexpr int kK4Threads = 1024;
-constexpr int kK1Blocks = 64;           // sample workgroups, 1024 samples each
-constexpr int kK1Threads = 256;
-constexpr int kSampleN = kK1Blocks * kK1Threads * 4;   // 65536
-constexpr int kSampleChunk = 256;
 constexpr int64_t kSmallN = 65536;
 constexpr int kExactThreads = 1024;
 
@@ -90,16 +86,16 @@ enum SrcMode { kData = 0, kHash = 1 };
 enum TileMode { kTakeNone = 0, kTakeAll = 1, kTakePartial = 2 };
 
 struct TopkCtrl {
-  uint32_t s_lo, s_hi, shift, overflow;          // K1 -> K2
-  uint32_t T, r, fallback, k1_ticket;            // K3 -> K4; K1b's self-resetting ticket
-  uint32_t pad[8];
+  uint32_t s_lo, s_hi, shift, overflow;          // K2 -> K34
+  uint32_t fin_ticket;                           // K34's self-resetting ticket
+  uint32_t pad[11];
   uint32_t G[kNRep][kNBucket];                   // replicated bucket suffix totals
 };
 
 struct TopkLayout {
   int64_t n;
   uint32_t tile, nb, side_cap;
-  size_t off_ctrl, off_cum, off_cntw, off_side, off_tile, off_k1, off_cval, off_cidx, total;
+  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, total;
 };
 
 // Tile = ceil(n / kK2Target) rounded up to 32768 elements: one tile per CU, all
@@ -120,10 +116,8 @@ static TopkLayout topk_layout(int64_t n) {
   L.off_cum = o;   o += align_up((size_t)L.nb * kNBucket * 4, 256);
   L.off_cntw = o;  o += align_up((size_t)L.nb * (tile / kChunk) * 4, 256);   // per-chunk candidate counts
   L.off_side = o;  o += align_up((size_t)L.nb * L.side_cap * 4, 256);
-  L.off_tile = o;  o += align_up((size_t)L.nb * 3 * 4, 256);        // tile_off | tile_tieb | tile_mode
-  L.off_k1 = o;    o += align_up((size_t)3 * 2048 * 4, 256);           // sample histograms (K1)
-  L.off_cval = o;  o += align_up((size_t)L.nb * tile * 4, 256);
-  L.off_cidx = o;  o += align_up((size_t)L.nb * tile * 4, 256);
+  L.off_cval = o;  o += align_up((size_t)L.nb * tile * 4, 256);   // candidate values, chunk slot ranges
+  L.off_cidx = o;  o += align_up((size_t)L.nb * tile * 4, 256);   // ... and indices
   L.total = o;
   return L;
 }
@@ -286,89 +280,27 @@ __global__ __launch_bounds__(kExactThreads) void topk_segmented_kernel(
 }
 
 // ----------------------------------------------------------------------------
-// K1: sample -> (s_lo, s_hi, shift), two small kernels
+// Sample bounds: the prologue of K2, computed identically by every workgroup
 //
-// 64 workgroups read a 64K-element strided sample (4 contiguous 256-element
-// chunks each).  K1a adds their coarse key histogram (key >> 20, 2048 bins) to
-// a global one.  K1b: every workgroup scans it for the coarse bins holding the
-// R_lo-th / R_hi-th largest sample keys, re-reads its samples and adds a fine
-// histogram (bits 19..9) of the keys in those two bins; the last workgroup
-// (fence-free ticket: the payload is atomics only) resolves both ranks to 512
-// keys -- s_lo rounded down, s_hi rounded up -- and clears the histograms for
-// the next call.  Both bounds are heuristics that K3 verifies (G[0] >= k,
-// G[sure] < k); any k/n works.
+// 128 runs of 256 contiguous elements (32768 keys, 128 KiB -- after the first
+// workgroup of an XCD misses, an L2 hit for the other 31) are histogrammed in
+// LDS, two levels: coarse key >> 20 (2048 bins), then bits 19..9 inside the two
+// coarse bins that hold the R_lo-th / R_hi-th largest sample keys.  s_lo is
+// rounded down and s_hi up to 512 keys.  Every workgroup reads the same sample
+// and counts it the same way, so all of them derive the same (s_lo, s_hi)
+// without a grid-wide hand-off.  Both bounds are heuristics that K34 verifies
+// (G[0] >= k, G[sure] < k); any k/n works.
 // ----------------------------------------------------------------------------
-CHOCO_DEV void write_params(TopkCtrl* ctrl, uint32_t s_lo, uint64_t s_hi_est) {
-  const uint64_t width = s_hi_est > s_lo ? s_hi_est - s_lo : 1;
-  uint32_t shift = 0;
-  while (((uint64_t)kNMaybe << shift) < width) ++shift;
-  uint64_t s_hi = (uint64_t)s_lo + ((uint64_t)kNMaybe << shift);
-  if (s_hi > 0xFFFFFFFFull) s_hi = 0xFFFFFFFFull;
-  ctrl->s_lo = s_lo;
-  ctrl->s_hi = (uint32_t)s_hi;
-  ctrl->shift = shift;
-}
-
-CHOCO_DEV uint32_t ld_agent(const uint32_t* p) {
-  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-CHOCO_DEV void st_agent(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Wave 0 of a workgroup: over a 256-bin LDS histogram (ascending value order),
-// find the bin holding the rank-th largest entry; returns (bin, rank inside bin)
-// via out[0], out[1].  Other waves must not call.
-CHOCO_DEV void wave_find_bin(const uint32_t* hist, uint32_t rank, uint32_t* out) {
-  const int lane = lane_id();
-  const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
-  const uint32_t loc = h0 + h1 + h2 + h3;
-  const uint32_t rv = __shfl(loc, 63 - lane);
-  const uint32_t inc = wave_incl_scan(rv);
-  const uint32_t suf_incl = __shfl(inc, 63 - lane);  // entries in bins >= 4*lane
-  const uint32_t above = suf_incl - loc;
-  if (above < rank && rank <= suf_incl) {
-    uint32_t acc = above;
-    const uint32_t hs[4] = {h0, h1, h2, h3};
-    for (int t = 3; t >= 0; --t) {
-      if (acc + hs[t] >= rank) { out[0] = 4 * lane + t; out[1] = rank - acc; break; }
-      acc += hs[t];
-    }
-  }
-}
-
-// Workgroup-wide: over hist[2048] in LDS (ascending value order), the bin holding
-// the rank-th largest entry and the rank inside it -> out[0], out[1].  Every
-// thread of the (kK1Threads) workgroup must call.
-CHOCO_DEV void block_find_bin2048(const uint32_t* hist, uint32_t rank, uint32_t* scratch, uint32_t* out) {
-  const int tid = threadIdx.x;
-  constexpr int per = 2048 / kK1Threads;
-  uint32_t hv[per];
-  uint32_t local = 0;
-#pragma unroll
-  for (int j = 0; j < per; ++j) {
-    hv[j] = hist[tid * per + j];
-    local += hv[j];
-  }
-  uint32_t total;
-  const uint32_t pre = block_excl_scan(local, scratch, &total);
-  const uint32_t above = total - pre - local;  // entries in bins above my chunk
-  if (above < rank && rank <= above + local) {
-    uint32_t acc = above;
-#pragma unroll
-    for (int j = per - 1; j >= 0; --j) {
-      if (acc < rank && rank <= acc + hv[j]) { out[0] = (uint32_t)(tid * per + j); out[1] = rank - acc; }
-      acc += hv[j];
-    }
-  }
-  __syncthreads();
-}
+constexpr int kSampleRuns = 128;
+constexpr int kSampleN = kSampleRuns * 256;                  // 32768
+constexpr int kSampleLoads = kSampleRuns * 64 / kK2Threads;  // float4 per thread (8)
+static_assert(kSampleLoads * kK2Threads == kSampleRuns * 64, "sample geometry");
 
 struct SampleRanks {
   uint32_t lo, hi;  // 1-based ranks from the top; 0 = none
 };
 
-// Ranks of the candidate floor / sure ceiling in the 64K sample (~6 sigma margins).
+// Ranks of the candidate floor / sure ceiling in the sample (~6 sigma margins).
 CHOCO_DEV SampleRanks sample_ranks(int64_t n, int64_t k) {
   const double m = (double)kSampleN;
   const double e = (double)k / (double)n * m;
@@ -381,129 +313,70 @@ CHOCO_DEV SampleRanks sample_ranks(int64_t n, int64_t k) {
   return r;
 }
 
-template <bool XH>
-CHOCO_DEV void load_sample(const float* __restrict__ x, const float* __restrict__ xh, int64_t n, uint32_t kk[4]) {
-  constexpr int nchunk = kSampleN / kSampleChunk;
-  const int64_t stride4 = ((n - kSampleChunk) / (nchunk - 1)) >> 2;
-  const int s = blockIdx.x * kK1Threads + threadIdx.x;
-  const int64_t q = (int64_t)(s / 64) * stride4 + (s % 64);  // float4 s%64 of chunk s/64
-  float4 v = reinterpret_cast<const float4*>(x)[q];
-  if (XH) {
-    const float4 h = reinterpret_cast<const float4*>(xh)[q];
-    v.x -= h.x; v.y -= h.y; v.z -= h.z; v.w -= h.w;
-  }
-  kk[0] = fkey(v.x); kk[1] = fkey(v.y); kk[2] = fkey(v.z); kk[3] = fkey(v.w);
-}
-
-// K1a: global coarse histogram of the sample (hist = [coarse 2048 | fine lo 2048 | fine hi 2048]).
-template <bool XH>
-__global__ __launch_bounds__(kK1Threads) void topk_sample_hist_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[2048];
-  const int tid = threadIdx.x;
-  STAMP(blockIdx.x, 0);
-  for (int i = tid; i < 2048; i += kK1Threads) h[i] = 0;
-  uint32_t kk[4];
-  load_sample<XH>(x, xh, n, kk);
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < 4; ++c) atomicAdd(&h[kk[c] >> 20], 1u);
-  __syncthreads();
-  for (int i = tid; i < 2048; i += kK1Threads) {
-    const uint32_t v = h[i];
-    if (v) atomicAdd(&hist[i], v);
-  }
-  STAMP(blockIdx.x, 1);
-}
-
-struct BoundsSmem {
-  uint32_t h[2048];
-  uint32_t f[2][2048];
-  uint32_t scratch[24];
-  uint32_t bc[8];
-  uint32_t flag;
+// Per-call bucket geometry: [s_lo, s_hi) is split into 255 "maybe" buckets of
+// width 2^shift; keys >= s_hi are "sure" (bucket 255).
+struct Buckets {
+  int64_t n;
+  uint32_t s_lo, s_hi, shift;
+  float s_lo_f;  // s_lo as a float: !(|v| < s_lo_f) is a superset test of key >= s_lo
+  uint64_t seed;
 };
 
-// K1b: fine histograms inside the two coarse bins, then the bounds.
-template <bool XH>
-__global__ __launch_bounds__(kK1Threads) void topk_sample_bounds_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k,
-    TopkCtrl* __restrict__ ctrl, uint32_t* __restrict__ hist) {
-  __shared__ BoundsSmem sm;
-  const int tid = threadIdx.x;
-  uint32_t* __restrict__ fine_lo = hist + 2048;
-  uint32_t* __restrict__ fine_hi = hist + 4096;
-  const SampleRanks R = sample_ranks(n, k);
-  uint32_t kk[4];
-  load_sample<XH>(x, xh, n, kk);
-  {
-    constexpr int per = 2048 / kK1Threads;
-    uint32_t hv[per];
-#pragma unroll
-    for (int j = 0; j < per; ++j) hv[j] = hist[tid + j * kK1Threads];  // written by K1a
-#pragma unroll
-    for (int j = 0; j < per; ++j) sm.h[tid + j * kK1Threads] = hv[j];
-  }
-  if (tid < 8) sm.bc[tid] = 0;
-  __syncthreads();
-  if (R.lo) block_find_bin2048(sm.h, R.lo, sm.scratch, sm.bc);
-  if (R.hi) block_find_bin2048(sm.h, R.hi, sm.scratch, sm.bc + 2);
-  const uint32_t c_lo = sm.bc[0], c_hi = sm.bc[2];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    if (R.lo && (kk[c] >> 20) == c_lo) atomicAdd(&fine_lo[(kk[c] >> 9) & 2047u], 1u);
-    if (R.hi && (kk[c] >> 20) == c_hi) atomicAdd(&fine_hi[(kk[c] >> 9) & 2047u], 1u);
-  }
-  STAMP(blockIdx.x, 2);
-  const bool last = last_block_ticket_atomics(&ctrl->k1_ticket, gridDim.x, &sm.flag);
-  STAMP(blockIdx.x, 3);
-  if (!last) return;
+CHOCO_DEV Buckets make_buckets(uint32_t s_lo, uint64_t s_hi_est, uint64_t seed) {
+  const uint64_t width = s_hi_est > s_lo ? s_hi_est - s_lo : 1;
+  uint32_t shift = 0;
+  while (((uint64_t)kNMaybe << shift) < width) ++shift;
+  uint64_t s_hi = (uint64_t)s_lo + ((uint64_t)kNMaybe << shift);
+  if (s_hi > 0xFFFFFFFFull) s_hi = 0xFFFFFFFFull;
+  Buckets bk;
+  bk.n = 0;
+  bk.s_lo = s_lo;
+  bk.s_hi = (uint32_t)s_hi;
+  bk.shift = shift;
+  bk.s_lo_f = __uint_as_float(s_lo);  // NaN when s_lo is a NaN key: then every lane is staged
+  bk.seed = seed;
+  return bk;
+}
 
-  // ---- last workgroup: resolve both ranks inside their coarse bins (one load round)
-  uint32_t s_lo = 0;
-  uint64_t s_hi_est = 0x80000000ull;  // above every key: nothing is "sure"
-  {
-    constexpr int per = 2048 / kK1Threads;
-    uint32_t fa[per], fb[per];
+template <bool XH>
+CHOCO_DEV void load_sample(const float* __restrict__ x, const float* __restrict__ xh, int64_t n,
+                           float4 (&s)[kSampleLoads], float4 (&h)[kSampleLoads]) {
+  const int64_t stride4 = ((n - 256) / (kSampleRuns - 1)) >> 2;  // float4 between run starts
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-    for (int j = 0; j < per; ++j) {
-      fa[j] = R.lo ? ld_agent(&fine_lo[tid + j * kK1Threads]) : 0u;
-      fb[j] = R.hi ? ld_agent(&fine_hi[tid + j * kK1Threads]) : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < per; ++j) {
-      sm.f[0][tid + j * kK1Threads] = fa[j];
-      sm.f[1][tid + j * kK1Threads] = fb[j];
-    }
-  }
-  __syncthreads();
-  if (R.lo) {
-    block_find_bin2048(sm.f[0], sm.bc[1], sm.scratch, sm.bc + 4);
-    s_lo = (c_lo << 20) | (sm.bc[4] << 9);                                  // rounded down
-  }
-  if (R.hi) {
-    block_find_bin2048(sm.f[1], sm.bc[3], sm.scratch, sm.bc + 6);
-    s_hi_est = (uint64_t)((c_hi << 20) | (sm.bc[6] << 9)) + 512u;            // rounded up
-  }
-  STAMP(64, 0);
-  // clear the histograms and the bucket totals for K2 / the next call
-  for (int i = tid; i < 3 * 2048; i += kK1Threads) hist[i] = 0;
-  for (int i = tid; i < kNRep * kNBucket; i += kK1Threads) (&ctrl->G[0][0])[i] = 0;
-  if (tid == 0) {
-    ctrl->overflow = 0;
-    write_params(ctrl, s_lo, s_hi_est);
-    st_agent(&ctrl->k1_ticket, 0u);
+  for (int j = 0; j < kSampleLoads; ++j) {
+    const int64_t q = (int64_t)(w + kK2Waves * j) * stride4 + lane;
+    s[j] = reinterpret_cast<const float4*>(x)[q];
+    if (XH) h[j] = reinterpret_cast<const float4*>(xh)[q];
   }
 }
 
-// Random-k: keys are uniform on [0, 2^31); thresholds from the binomial tails.
-__global__ void topk_set_params_kernel(TopkCtrl* __restrict__ ctrl, uint32_t s_lo, uint64_t s_hi_est) {
-  for (int i = threadIdx.x; i < kNRep * kNBucket; i += blockDim.x) (&ctrl->G[0][0])[i] = 0;
-  if (threadIdx.x == 0) { ctrl->overflow = 0; write_params(ctrl, s_lo, s_hi_est); }
+// Over hist[2048] in LDS (ascending key order), the bins holding the r0-th and
+// r1-th largest entries and the ranks inside them -> out[0..1], out[2..3] (a
+// rank of 0 is skipped).  Every thread of the kK2Threads workgroup calls it.
+CHOCO_DEV void block_find_two(const uint32_t* hist, uint32_t r0, uint32_t r1, uint32_t* scratch, uint32_t* out) {
+  static_assert(kK2Threads * 2 == 2048, "two bins per thread");
+  const int tid = threadIdx.x;
+  const uint32_t h0 = hist[2 * tid], h1 = hist[2 * tid + 1];
+  const uint32_t local = h0 + h1;
+  uint32_t total;
+  const uint32_t pre = block_excl_scan(local, scratch, &total);
+  const uint32_t above = total - pre - local;  // entries in bins above my two
+  const uint32_t rs[2] = {r0, r1};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const uint32_t r = rs[q];
+    if (r != 0u && above < r && r <= above + local) {
+      if (r <= above + h1) { out[2 * q] = 2 * tid + 1; out[2 * q + 1] = r - above; }
+      else { out[2 * q] = 2 * tid; out[2 * q + 1] = r - above - h1; }
+    }
+  }
+  __syncthreads();
 }
 
 // ----------------------------------------------------------------------------
-// K2: streaming candidate compaction, one 16-wave workgroup per tile, one per CU
+// K2: sample prologue + streaming candidate compaction, one 16-wave workgroup
+// per tile, one per CU
 //
 // Measured (tools/probe_position.hip, probe_balance.hip): when two or more
 // workgroups share a CU, the one dispatched first streams first and the last
@@ -512,40 +385,88 @@ __global__ void topk_set_params_kernel(TopkCtrl* __restrict__ ctrl, uint32_t s_l
 // that placement.  Inside the workgroup the CU's issue arbiter favours older
 // waves, so waves claim kChunk-element chunks through an LDS counter.
 //
-// Two-level compaction, sized for k << n: per float4 row a wave only decides
-// which LANES hold a candidate (|v| >= s_lo, one ballot) and appends those lanes'
-// float4 + base index to a per-wave LDS entry ring (~3 of 64 lanes per row at
-// k = 1 %).  Every 64 entries are expanded to (value, index) pairs with the
-// exact integer key test and stored to the chunk's slot range; maybe keys
-// (s_lo <= key < s_hi) are binned and staged in LDS on the way, so the end of
-// the tile only scans 256 bucket counts and counting-sorts the staged keys.
+// Each wave keeps its next load batch in flight while it works on the current
+// one (two register buffers A/B, 8 KiB each).  The first batch is issued
+// before the sample is counted, so the HBM is busy during the prologue.
+//
+// Candidates stay ON CHIP until the stream is over (tools/probe_wmix.hip: a
+// trickle of stores inside a saturated 400 MB read costs ~0.5 us per MB
+// written -- 3-4x its byte share, HBM read/write turnaround -- while LDS work
+// of the same shape costs nothing measurable):
+//   * per float4 row a wave decides which LANES hold a candidate (|v| >= s_lo,
+//     one ballot) and appends those lanes' float4 + first index ("entries", ~3
+//     of 64 lanes per row at k = 1 %) to a per-wave LDS ring;
+//   * every 64 entries are expanded with the exact key test into (value, index)
+//     pairs in the wave's region of an LDS pair buffer (chunk order), and the
+//     maybe keys (s_lo <= key < s_hi) are counted into the tile's bucket
+//     histogram;
+//   * a wave whose region is full writes further pairs straight to their
+//     chunk's global slots (dense inputs / large k: correct, slower);
+//   * at the end of the tile every chunk's LDS pairs leave in one burst to the
+//     chunk's global slots, and the maybe keys are counting-sorted into the
+//     tile's side list on the way.
 // ----------------------------------------------------------------------------
+#ifndef CHOCO_PRO_PREFETCH  // diagnostic knob: first batch issued before the sample histogram
+#define CHOCO_PRO_PREFETCH 1
+#endif
 constexpr int kEnt = 128;  // entry ring per wave (flush at 64: <= 63 + 64 pending)
+constexpr int kPairsPerWave = 640;  // LDS pair region per wave (~2x the k = 1 % share)
+constexpr int kMaxTileChunks = 2048;  // tile <= 2^31 / 256 elements
+static_assert((int64_t(1) << 31) / kK2Target / kChunk <= kMaxTileChunks, "chunk table");
+static_assert(kMaxTileChunks <= 2 * kK4Threads, "two chunk counts per thread");
+
+struct SampleHist {
+  uint32_t coarse[2048];
+  uint32_t fine[2][2048];
+};
 
 struct StreamSmem {
   float4 ent_v[kK2Waves][kEnt];   // staged lanes: the float4 row slice
   uint32_t ent_i[kK2Waves][kEnt]; // ... and the index of its first element
-  float4 trash_v[kK2Waves][64];   // per-lane sinks of the branch-free batch writes
-  uint32_t trash_i[kK2Waves][64];
-  uint32_t maybe[kMaybeCap];      // the tile's maybe keys, in flush order
+  float4 trash_v[64];             // per-lane sink of the branch-free batch writes (shared, never read)
+  uint32_t trash_i[64];
+  union {
+    uint2 pairs[kK2Waves * kPairsPerWave];  // (value bits, index) per candidate, per-wave regions
+    SampleHist sh;                          // prologue only
+  } u;
+  uint32_t cmeta[kMaxTileChunks];  // per chunk: LDS start | LDS count << 16
+  uint32_t ccnt[kMaxTileChunks];   // per chunk: candidates
   uint32_t hist[kNBucket];        // maybe-key bucket counts, then counting-sort cursors
   uint32_t cnt[kK2Waves];
   uint32_t scratch[24];
-  uint32_t mcount;
+  uint32_t bc[8];
   uint32_t next_chunk;            // the tile's chunk counter (waves claim chunks)
 };
+static_assert(sizeof(SampleHist) <= sizeof(uint2) * kK2Waves * kPairsPerWave, "sample histogram alias");
 
 // Unconditional float4 loads of kK2Unroll rows (no branch around a load: the
 // compiler's vmcnt accounting stays exact and all rows are in flight together).
+// The once-read stream uses non-temporal loads: they do not allocate in the
+// 256 MB Infinity Cache, so a previous kernel's dirty lines there are not
+// evicted (and written back) in the middle of the stream.  Measured in the
+// bench step (the previous step's sparse accumulate leaves ~120 MB dirty):
+// K2 130 -> 83 us; back to back, cold caches: 89.6 -> 82.9 us.
+#ifndef CHOCO_STREAM_NT
+#define CHOCO_STREAM_NT 1
+#endif
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+CHOCO_DEV float4 ld_stream(const float* p) {
+  if (CHOCO_STREAM_NT) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return *reinterpret_cast<const float4*>(p);
+}
+
 template <bool XH>
 CHOCO_DEV void load_rows_full(const float* __restrict__ x, const float* __restrict__ xh, int64_t base, int lane,
                               float4 (&r)[kK2Unroll]) {
 #pragma unroll
-  for (int u = 0; u < kK2Unroll; ++u) r[u] = *reinterpret_cast<const float4*>(x + base + u * 256 + 4 * lane);
+  for (int u = 0; u < kK2Unroll; ++u) r[u] = ld_stream(x + base + u * 256 + 4 * lane);
   if (XH) {
 #pragma unroll
     for (int u = 0; u < kK2Unroll; ++u) {
-      const float4 h = *reinterpret_cast<const float4*>(xh + base + u * 256 + 4 * lane);
+      const float4 h = ld_stream(xh + base + u * 256 + 4 * lane);
       r[u].x -= h.x; r[u].y -= h.y; r[u].z -= h.z; r[u].w -= h.w;
     }
   }
@@ -557,70 +478,78 @@ CHOCO_DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Per-wave compaction state of the current chunk (wave-uniform).
+// Per-wave state (wave-uniform).
 struct WaveAcc {
-  uint32_t estaged, eflushed;  // entry ring: appended / expanded
-  uint32_t staged;             // candidates written to the chunk's slot range
+  uint32_t estaged, eflushed;  // entry ring of the current chunk: appended / expanded
+  uint32_t staged;             // candidates of the current chunk
+  uint32_t lstart, lcnt;       // the current chunk's pairs kept in LDS: region offset, count
+  uint32_t lfill;              // pairs in the wave's LDS region
+  uint32_t cand;               // candidates, whole tile
 };
 
-// Per-tile bucket geometry, read once from the control block.
-struct Buckets {
-  uint32_t s_lo, s_hi, shift;
-  float s_lo_f;  // s_lo as a float: !(|v| < s_lo_f) is a superset test of key >= s_lo
-  uint64_t seed;
-};
-
-// Expand entries [eflushed, eflushed + nent) (nent <= 64, one per lane) into
-// (value, index) candidates of the chunk [.., cend) in index order.
+// Expand ring entries [eflushed, eflushed + nent) (nent <= 64, one per lane)
+// with the exact key test into the current chunk's candidates [staged, ..):
+// into the wave's LDS region while it has room, else straight to the chunk's
+// global slots (then for the rest of the chunk, so the LDS part stays a prefix
+// of the chunk's run).  Maybe keys are counted into the bucket histogram.
 template <int MODE, bool XH>
-CHOCO_DEV void expand_entries(const Src<MODE, XH>& src, StreamSmem& sm, int w, int lane, WaveAcc& a, uint32_t nent,
-                              int64_t cend, float* __restrict__ ov, uint32_t* __restrict__ oi, const Buckets& bk) {
+CHOCO_DEV void flush_entries(const Src<MODE, XH>& src, StreamSmem& sm, int w, int lane, WaveAcc& a, uint32_t nent,
+                             float* __restrict__ ov, uint32_t* __restrict__ oi, const Buckets& bk) {
   wave_sync();
   const bool have = (uint32_t)lane < nent;
   const uint32_t slot = (a.eflushed + lane) & (kEnt - 1);
-  const float4 ev = have ? sm.ent_v[w][slot] : make_float4(0.f, 0.f, 0.f, 0.f);
-  const uint32_t ei = have ? sm.ent_i[w][slot] : 0u;
-  const float vv[4] = {ev.x, ev.y, ev.z, ev.w};
-  uint32_t kk[4];
-  bool f[4];
-  uint64_t m[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    kk[c] = MODE == kData ? fkey(vv[c]) : (rank_hash(bk.seed, ei + c) >> 1);
-    f[c] = have && (int64_t)ei + c < cend && kk[c] >= bk.s_lo;
-    m[c] = ballot(f[c]);
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  uint32_t i0 = 0;
+  if (have) {
+    if (MODE == kData) v = sm.ent_v[w][slot];
+    i0 = sm.ent_i[w][slot];
   }
-  uint32_t pos = a.staged + mask_prefix(m[0]) + mask_prefix(m[1]) + mask_prefix(m[2]) + mask_prefix(m[3]);
-  a.staged += (uint32_t)(__popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]));
+  float vv[4] = {v.x, v.y, v.z, v.w};
+  bool ok[4];
+  uint32_t nc = 0;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    if (m[c] == 0ull) continue;  // wave-uniform
-    if (f[c]) {
-      ov[pos] = MODE == kData ? vv[c] : src.val((int64_t)ei + c);
-      oi[pos] = ei + c;
-      ++pos;
-    }
-    // maybe keys: bin and stage (one LDS atomic per wave for the list slots)
-    const bool mb = f[c] && kk[c] < bk.s_hi;
-    const uint64_t bm = ballot(mb);
-    if (bm != 0ull) {
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&sm.mcount, (uint32_t)__popcll(bm));
-      base = __builtin_amdgcn_readfirstlane(base);
-      if (mb) {
-        const uint32_t p = base + mask_prefix(bm);
-        if (p < (uint32_t)kMaybeCap) sm.maybe[p] = kk[c];
-        atomicAdd(&sm.hist[(kk[c] - bk.s_lo) >> bk.shift], 1u);
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t key = MODE == kData ? fkey(vv[q]) : (rank_hash(bk.seed, i0 + q) >> 1);
+    ok[q] = have && (int64_t)i0 + q < bk.n && key >= bk.s_lo;
+    nc += ok[q] ? 1u : 0u;
+    if (ok[q] && key < bk.s_hi) atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
+  }
+  if (MODE == kHash) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (ok[q]) vv[q] = src.val((int64_t)i0 + q);
+  }
+  const uint64_t b0 = ballot(nc & 1u), b1 = ballot(nc & 2u), b2 = ballot(nc & 4u);
+  const uint32_t tot = (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+  const uint32_t pre = mask_prefix(b0) + 2 * mask_prefix(b1) + 4 * mask_prefix(b2);
+  if (tot != 0u) {  // wave-uniform
+    const bool lds = a.lcnt == a.staged && a.lfill + tot <= (uint32_t)kPairsPerWave;  // LDS part still a prefix
+    uint32_t p = pre;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (ok[q]) {
+        if (lds) {
+          sm.u.pairs[w * kPairsPerWave + a.lfill + p] = make_uint2(__float_as_uint(vv[q]), i0 + q);
+        } else {
+          ov[a.staged + p] = vv[q];
+          oi[a.staged + p] = i0 + q;
+        }
+        ++p;
       }
     }
+    if (lds) {
+      a.lfill += tot;
+      a.lcnt += tot;
+    }
+    a.staged += tot;
   }
-  a.staged = __builtin_amdgcn_readfirstlane(a.staged);
+  a.cand += tot;
   a.eflushed += nent;
 }
 
 // One float4 row per lane (256 elements per wave): stage the lanes that hold a
 // candidate.  The float test !(|v| < s_lo_f) is a superset of key >= s_lo (NaN
-// passes); expand_entries applies the exact test.
+// passes); the flush applies the exact test.
 template <int MODE, bool XH, bool GUARD>
 CHOCO_DEV void process_row(const Src<MODE, XH>& src, const float4 v4, int64_t i, int64_t cend, StreamSmem& sm,
                            int w, int lane, WaveAcc& a, float* __restrict__ ov, uint32_t* __restrict__ oi,
@@ -638,18 +567,17 @@ CHOCO_DEV void process_row(const Src<MODE, XH>& src, const float4 v4, int64_t i,
   if (M == 0ull) return;  // wave-uniform: no candidate lane in this row
   if (any) {
     const uint32_t slot = (a.estaged + mask_prefix(M)) & (kEnt - 1);
-    sm.ent_v[w][slot] = v4;
+    if (MODE == kData) sm.ent_v[w][slot] = v4;
     sm.ent_i[w][slot] = (uint32_t)i;
   }
   a.estaged = __builtin_amdgcn_readfirstlane(a.estaged + (uint32_t)__popcll(M));
-  if (a.estaged - a.eflushed >= 64u) expand_entries<MODE, XH>(src, sm, w, lane, a, 64u, cend, ov, oi, bk);
+  if (a.estaged - a.eflushed >= 64u) flush_entries<MODE, XH>(src, sm, w, lane, a, 64u, ov, oi, bk);
 }
 
 // Eight full rows (one load batch) as ONE branch-free block, so the compiler can
-// interleave the rows' dependent compare -> ballot -> prefix -> LDS-store chains
-// (the kernel is otherwise issue-stall bound at 4 waves per SIMD).  Lanes
-// without a candidate store to their own trash slot.  If the batch could
-// overflow the entry ring (dense inputs), rows take the per-row path instead.
+// interleave the rows' dependent compare -> ballot -> prefix -> LDS-store chains.
+// Lanes without a candidate store to a trash slot.  If the batch could overflow
+// the entry ring (dense inputs), rows take the per-row path instead.
 template <bool XH>
 CHOCO_DEV void process_batch(const Src<kData, XH>& src, const float4 (&A)[kK2Unroll], int64_t base, int64_t cend,
                              StreamSmem& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
@@ -671,14 +599,15 @@ CHOCO_DEV void process_batch(const Src<kData, XH>& src, const float4 (&A)[kK2Unr
 #pragma unroll
     for (int u = 0; u < kK2Unroll; ++u) {
       const uint32_t slot = (run + mask_prefix(M[u])) & (kEnt - 1);
-      float4* pv = any[u] ? &sm.ent_v[w][slot] : &sm.trash_v[w][lane];
-      uint32_t* pi = any[u] ? &sm.ent_i[w][slot] : &sm.trash_i[w][lane];
+      float4* pv = any[u] ? &sm.ent_v[w][slot] : &sm.trash_v[lane];
+      uint32_t* pi = any[u] ? &sm.ent_i[w][slot] : &sm.trash_i[lane];
       *pv = A[u];
       *pi = (uint32_t)(base + u * 256 + 4 * lane);
       run += (uint32_t)__popcll(M[u]);
     }
     a.estaged = __builtin_amdgcn_readfirstlane(run);
-    while (a.estaged - a.eflushed >= 64u) expand_entries<kData, XH>(src, sm, w, lane, a, 64u, cend, ov, oi, bk);
+#pragma unroll 1
+    while (a.estaged - a.eflushed >= 64u) flush_entries<kData, XH>(src, sm, w, lane, a, 64u, ov, oi, bk);
   } else {
 #pragma unroll
     for (int u = 0; u < kK2Unroll; ++u)
@@ -687,86 +616,172 @@ CHOCO_DEV void process_batch(const Src<kData, XH>& src, const float4 (&A)[kK2Unr
 }
 
 template <int MODE, bool XH>
-__global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, uint32_t tile, uint32_t nb,
-    uint32_t side_cap, uint64_t seed, TopkCtrl* __restrict__ ctrl, uint32_t* __restrict__ cum_tab,
-    uint32_t* __restrict__ cntw, uint32_t* __restrict__ side, float* __restrict__ cval,
-    uint32_t* __restrict__ cidx) {
-  __shared__ StreamSmem sm;
-  STAMP(1024 + blockIdx.x, 0);
-  Buckets bk;
-  bk.s_lo = ctrl->s_lo;
-  bk.s_hi = ctrl->s_hi;
-  bk.shift = ctrl->shift;
-  bk.s_lo_f = __uint_as_float(bk.s_lo);  // NaN when s_lo is a NaN key: then every lane is staged
-  bk.seed = seed;
-  const int lane = lane_id();
-  const int w = threadIdx.x >> 6;
-  const int64_t b = blockIdx.x;
-  constexpr int64_t kStep = 256 * kK2Unroll;
-  Src<MODE, XH> src{x, xh, seed};
-  if (threadIdx.x < kNBucket) sm.hist[threadIdx.x] = 0;
-  if (threadIdx.x == 0) { sm.mcount = 0; sm.next_chunk = 0; }
-  __syncthreads();
+CHOCO_DEV void process_rows_hash(const Src<MODE, XH>& src, int64_t base, int64_t cend, StreamSmem& sm, int w,
+                                 int lane, WaveAcc& a, float* __restrict__ ov, uint32_t* __restrict__ oi,
+                                 const Buckets& bk) {
+#pragma unroll
+  for (int u = 0; u < kK2Unroll; ++u)
+    process_row<MODE, XH, false>(src, make_float4(0.f, 0.f, 0.f, 0.f), base + u * 256 + 4 * lane, cend, sm, w,
+                                 lane, a, ov, oi, bk);
+}
 
-  // Chunk c's candidates go to its own slot range and count, so the tile's
-  // output order is the chunk order.
-  const uint32_t nchunk = tile / (uint32_t)kChunk;
-  uint32_t total = 0;
+CHOCO_DEV uint32_t claim_chunk(StreamSmem& sm, int lane) {
   uint32_t c = 0;
   if (lane == 0) c = atomicAdd(&sm.next_chunk, 1u);
-  c = __builtin_amdgcn_readfirstlane(c);
+  return __builtin_amdgcn_readfirstlane(c);
+}
+
+// Random-k (MODE kHash): keys are uniform on [0, 2^31) and (s_lo, s_hi) come from
+// the binomial tails (host), passed as hs_lo / hs_hi.
+template <int MODE, bool XH>
+__global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile,
+    uint32_t side_cap, uint64_t seed, uint32_t hs_lo, uint64_t hs_hi, TopkCtrl* __restrict__ ctrl,
+    uint32_t* __restrict__ cum_tab, uint32_t* __restrict__ cntw, uint32_t* __restrict__ side,
+    float* __restrict__ cval, uint32_t* __restrict__ cidx) {
+  __shared__ StreamSmem sm;
+  STAMP(1024 + blockIdx.x, 0);
+  const int tid = threadIdx.x;
+  const int lane = lane_id();
+  const int w = tid >> 6;
+  const int64_t b = blockIdx.x;
+  constexpr int64_t kStep = 256 * kK2Unroll;
+  static_assert(kChunk == 2 * kStep, "a chunk is two load batches (A, B)");
+  const uint32_t nchunk = tile / (uint32_t)kChunk;
+  Src<MODE, XH> src{x, xh, seed};
+  // a full chunk's first batch, or a harmless re-read of the buffer start (n > kSmallN >= kChunk)
+  auto batch0 = [&](uint32_t c) -> int64_t {
+    const int64_t cb = b * (int64_t)tile + (int64_t)c * kChunk;
+    return (c < nchunk && cb + kChunk <= n) ? cb : 0;
+  };
+
+  // ---- prologue: the wave's first chunk is chunk w; its first batch goes out
+  // behind the sample loads, so the histogram work below overlaps HBM traffic
+  uint32_t c = (uint32_t)w;
+  float4 A[kK2Unroll], B[kK2Unroll];
+  Buckets bk;
+  if constexpr (MODE == kData) {
+    float4 s[kSampleLoads], sh[kSampleLoads];
+    load_sample<XH>(x, xh, n, s, sh);
+    if (!XH && CHOCO_PRO_PREFETCH) load_rows_full<XH>(x, xh, batch0(c), lane, A);  // XH: no registers to spare
+    for (int i = tid; i < 3 * 2048; i += kK2Threads) (&sm.u.sh.coarse[0])[i] = 0u;
+    if (tid < kNBucket) sm.hist[tid] = 0;
+    if (tid < 8) sm.bc[tid] = 0;
+    if (tid == 0) sm.next_chunk = kK2Waves;
+    __syncthreads();
+    uint32_t kk[kSampleLoads * 4];
+#pragma unroll
+    for (int j = 0; j < kSampleLoads; ++j) {
+      float4 v = s[j];
+      if (XH) { v.x -= sh[j].x; v.y -= sh[j].y; v.z -= sh[j].z; v.w -= sh[j].w; }
+      kk[4 * j + 0] = fkey(v.x); kk[4 * j + 1] = fkey(v.y); kk[4 * j + 2] = fkey(v.z); kk[4 * j + 3] = fkey(v.w);
+    }
+    STAMP(20000 + b, 0);
+#pragma unroll
+    for (int j = 0; j < kSampleLoads * 4; ++j) atomicAdd(&sm.u.sh.coarse[kk[j] >> 20], 1u);
+    __syncthreads();
+    STAMP(20000 + b, 1);
+    const SampleRanks R = sample_ranks(n, k);
+    block_find_two(sm.u.sh.coarse, R.lo, R.hi, sm.scratch, sm.bc);
+    const uint32_t c_lo = sm.bc[0], r_lo = sm.bc[1], c_hi = sm.bc[2], r_hi = sm.bc[3];
+#pragma unroll
+    for (int j = 0; j < kSampleLoads * 4; ++j) {
+      const uint32_t cb = kk[j] >> 20, fb = (kk[j] >> 9) & 2047u;
+      if (R.lo && cb == c_lo) atomicAdd(&sm.u.sh.fine[0][fb], 1u);
+      if (R.hi && cb == c_hi) atomicAdd(&sm.u.sh.fine[1][fb], 1u);
+    }
+    __syncthreads();
+    STAMP(20000 + b, 2);
+    block_find_two(sm.u.sh.fine[0], R.lo ? r_lo : 0u, 0u, sm.scratch, sm.bc + 4);
+    block_find_two(sm.u.sh.fine[1], R.hi ? r_hi : 0u, 0u, sm.scratch, sm.bc + 6);
+    const uint32_t s_lo = R.lo ? ((c_lo << 20) | (sm.bc[4] << 9)) : 0u;                       // rounded down
+    const uint64_t s_hi_est = R.hi ? (uint64_t)((c_hi << 20) | (sm.bc[6] << 9)) + 512u : 0x80000000ull;  // up
+    bk = make_buckets(s_lo, s_hi_est, seed);
+    if (XH || !CHOCO_PRO_PREFETCH) load_rows_full<XH>(x, xh, batch0(c), lane, A);
+    __syncthreads();  // the sample histograms (aliasing the pair buffer) are dead from here on
+    STAMP(20000 + b, 3);
+  } else {
+    if (tid < kNBucket) sm.hist[tid] = 0;
+    if (tid == 0) sm.next_chunk = kK2Waves;
+    bk = make_buckets(hs_lo, hs_hi, seed);
+    __syncthreads();
+  }
+  bk.n = n;
+  if (b == 0 && tid == 0) {
+    ctrl->s_lo = bk.s_lo;
+    ctrl->s_hi = bk.s_hi;
+    ctrl->shift = bk.shift;
+  }
+  STAMP(1024 + b, 1);
+
+  // ---- stream.  Chunk c's candidates get the global slot range [cbeg, ..) and
+  // a count, so the tile's candidates in chunk order are in index order.
+  // Invariant at the loop top: A holds (or is loading) chunk c's first batch
+  // when c is a full chunk.
+  const int64_t tb = b * (int64_t)tile;
+  WaveAcc a{};
+  uint32_t nx = claim_chunk(sm, lane);
   while (c < nchunk) {
-    uint32_t nx = 0;
-    if (lane == 0) nx = atomicAdd(&sm.next_chunk, 1u);  // the next claim, used after this chunk
-    const int64_t cbeg = b * (int64_t)tile + (int64_t)c * kChunk;
+    const uint32_t nn = claim_chunk(sm, lane);  // used after this chunk
+    const int64_t cbeg = tb + (int64_t)c * kChunk;
     const int64_t cend = min(cbeg + kChunk, n);
     float* __restrict__ ov = cval + cbeg;
     uint32_t* __restrict__ oi = cidx + cbeg;
-    WaveAcc a{0u, 0u, 0u};
-    const int64_t full_end = cend > cbeg ? cbeg + (cend - cbeg) / kStep * kStep : cbeg;
-    for (int64_t base = cbeg; base < full_end; base += kStep) {
-      float4 A[kK2Unroll];
-      if constexpr (MODE == kData) {
-        load_rows_full<XH>(x, xh, base, lane, A);
-        process_batch<XH>(src, A, base, cend, sm, w, lane, a, ov, oi, bk);
+    a.estaged = a.eflushed = a.staged = a.lcnt = 0u;
+    a.lstart = a.lfill;
+    if (cbeg + kChunk <= n) {
+      if constexpr (MODE == kData && !XH) {
+        // double-buffered: the next batch is always in flight
+        load_rows_full<XH>(x, xh, cbeg + kStep, lane, B);
+        process_batch<XH>(src, A, cbeg, cend, sm, w, lane, a, ov, oi, bk);
+        load_rows_full<XH>(x, xh, batch0(nx), lane, A);
+        process_batch<XH>(src, B, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk);
+      } else if constexpr (MODE == kData) {
+        // two input streams: one batch (16 KiB per wave) at a time
+        process_batch<XH>(src, A, cbeg, cend, sm, w, lane, a, ov, oi, bk);
+        load_rows_full<XH>(x, xh, cbeg + kStep, lane, A);
+        process_batch<XH>(src, A, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk);
+        load_rows_full<XH>(x, xh, batch0(nx), lane, A);
       } else {
-#pragma unroll
-        for (int u = 0; u < kK2Unroll; ++u)
-          process_row<MODE, XH, false>(src, make_float4(0.f, 0.f, 0.f, 0.f), base + u * 256 + 4 * lane, cend, sm,
-                                       w, lane, a, ov, oi, bk);
+        process_rows_hash<MODE, XH>(src, cbeg, cend, sm, w, lane, a, ov, oi, bk);
+        process_rows_hash<MODE, XH>(src, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk);
       }
-    }
-    // tail (< kStep elements, last chunk only): guarded loads
-    for (int64_t base = full_end; base < cend; base += 256) {
-      const int64_t i = base + 4 * lane;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (MODE == kData) {
-        float t[4];
+    } else {
+      // the buffer's last, partial chunk (or an empty one past n): guarded rows
+      for (int64_t base = cbeg; base < cend; base += 256) {
+        const int64_t i = base + 4 * lane;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (MODE == kData) {
+          float t[4];
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) t[cc] = (i + cc < cend) ? src.val(i + cc) : 0.f;
-        v = make_float4(t[0], t[1], t[2], t[3]);
+          for (int cc = 0; cc < 4; ++cc) t[cc] = (i + cc < cend) ? src.val(i + cc) : 0.f;
+          v = make_float4(t[0], t[1], t[2], t[3]);
+        }
+        process_row<MODE, XH, true>(src, v, i, cend, sm, w, lane, a, ov, oi, bk);
       }
-      process_row<MODE, XH, true>(src, v, i, cend, sm, w, lane, a, ov, oi, bk);
+      if constexpr (MODE == kData) load_rows_full<XH>(x, xh, batch0(nx), lane, A);
     }
     // the chunk's remaining entries (< 64)
     const uint32_t rest = a.estaged - a.eflushed;
-    if (rest) expand_entries<MODE, XH>(src, sm, w, lane, a, rest, cend, ov, oi, bk);
-    if (lane == 0) cntw[(int64_t)b * nchunk + c] = a.staged;
-    total += a.staged;
-    c = __builtin_amdgcn_readfirstlane(nx);
+    if (rest) flush_entries<MODE, XH>(src, sm, w, lane, a, rest, ov, oi, bk);
+    if (lane == 0) {
+      cntw[(int64_t)b * nchunk + c] = a.staged;
+      sm.ccnt[c] = a.staged;
+      sm.cmeta[c] = (w * kPairsPerWave + a.lstart) | (a.lcnt << 16);
+    }
+    c = nx;
+    nx = nn;
   }
-  if (lane == 0) sm.cnt[w] = total;
-  STAMP(1024 + b, 1);
-  __syncthreads();
+  if (lane == 0) sm.cnt[w] = a.cand;  // wave-uniform
   STAMP(1024 + b, 2);
+  __syncthreads();
 
-  // ---- end of tile: bucket suffix counts, side list
-  const uint32_t msum = sm.mcount;
+  // ---- end of tile: bucket suffix counts; then every chunk's LDS pairs leave to
+  // its global slots and the maybe keys are counting-sorted into the side list
   {
     // thread t <-> maybe bucket jb = 254 - t (t = 255: the "sure" bucket 255);
     // cum[j] = #candidates with bucket >= j, sure included
-    const int t = threadIdx.x;
+    const int t = tid;
     const int jb = t < kNMaybe ? kNMaybe - 1 - t : kNMaybe;
     const uint32_t hv = t < kNMaybe ? sm.hist[jb] : 0u;
     uint32_t hsum;
@@ -775,7 +790,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
 #pragma unroll
     for (int ww = 0; ww < kK2Waves; ++ww) csum += sm.cnt[ww];
     const uint32_t sure = csum - hsum;
-    if (t == 0 && (msum > side_cap || msum > (uint32_t)kMaybeCap)) atomicOr(&ctrl->overflow, 1u);
+    if (t == 0 && hsum > side_cap) atomicOr(&ctrl->overflow, 1u);
     if (t < kNBucket) {
       const uint32_t cum = t < kNMaybe ? sure + above + hv : sure;
       cum_tab[b * kNBucket + jb] = cum;
@@ -783,51 +798,117 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       if (t < kNMaybe) sm.hist[jb] = above;  // counting-sort cursor of bucket jb (hist is dead now)
     }
   }
+  STAMP(22000 + b, 0);
   __syncthreads();
   {
     uint32_t* __restrict__ sd = side + b * side_cap;
-    const uint32_t mc = min(msum, min(side_cap, (uint32_t)kMaybeCap));
-    for (uint32_t j = threadIdx.x; j < mc; j += kK2Threads) {
-      const uint32_t key = sm.maybe[j];
-      const uint32_t p = atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
-      sd[p] = key;
+    for (uint32_t cc = (uint32_t)w; cc < nchunk; cc += kK2Waves) {
+      const uint32_t meta = sm.cmeta[cc], cnt = sm.ccnt[cc];
+      const uint32_t ls = meta & 0xFFFFu, lc = meta >> 16;
+      float* __restrict__ ov = cval + tb + (int64_t)cc * kChunk;
+      uint32_t* __restrict__ oi = cidx + tb + (int64_t)cc * kChunk;
+      for (uint32_t j = lane; j < cnt; j += 64) {
+        uint32_t vb, ix;
+        if (j < lc) {
+          const uint2 pr = sm.u.pairs[ls + j];
+          vb = pr.x;
+          ix = pr.y;
+          ov[j] = __uint_as_float(vb);
+          oi[j] = ix;
+        } else {  // spilled during the stream
+          vb = __float_as_uint(ov[j]);
+          ix = oi[j];
+        }
+        const uint32_t key = MODE == kData ? (vb & 0x7fffffffu) : (rank_hash(seed, ix) >> 1);
+        if (key < bk.s_hi) {  // every candidate has key >= s_lo
+          const uint32_t p = atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
+          if (p < side_cap) sd[p] = key;
+        }
+      }
     }
   }
   STAMP(1024 + b, 3);
 }
 
 // ----------------------------------------------------------------------------
-// K3: exact threshold T, tie quota r and per-tile output offsets (one workgroup)
+// K34: exact threshold T, tie quota r, then this tile's ordered output; one
+// workgroup per tile
 //
-// Latency-bound, so organised around three dependent global round trips: the
-// replicated bucket totals (-> bucket j* of the k-th key), two tiles' table
-// words per thread (-> bucket-j* key counts and side offsets), then the keys
-// themselves straight into their LDS slots.  T is radix-selected inside the
-// bucket in LDS; per-tile (#keys > T, #keys == T) and two block scans give every
-// tile's output offset and first-tie rank for K4.
+// Every workgroup derives (T, r) and ALL tiles' output offsets itself from the
+// same inputs (the replicated bucket totals, two table words per tile, the few
+// thousand keys of bucket j* copied into LDS), then compacts its own tile.  The
+// redundant select is a handful of L2-served round trips; it replaces a
+// single-workgroup select kernel and a kernel boundary.
+//
+// The bucket totals are cleared for the next call by the workgroup that draws
+// the last ticket after reading them (fence-free: every workgroup's loads of
+// the totals have returned before it draws).
 // ----------------------------------------------------------------------------
-constexpr int kK3PerThread = (kK2Target + kK3Threads - 1) / kK3Threads;   // tiles per thread
+// Wave 0 of a workgroup: over a 256-bin LDS histogram (ascending value order),
+// find the bin holding the rank-th largest entry; returns (bin, rank inside bin)
+// via out[0], out[1].  Other waves must not call.
+CHOCO_DEV void wave_find_bin(const uint32_t* hist, uint32_t rank, uint32_t* out) {
+  const int lane = lane_id();
+  const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
+  const uint32_t loc = h0 + h1 + h2 + h3;
+  const uint32_t rv = __shfl(loc, 63 - lane);
+  const uint32_t inc = wave_incl_scan(rv);
+  const uint32_t suf_incl = __shfl(inc, 63 - lane);  // entries in bins >= 4*lane
+  const uint32_t above = suf_incl - loc;
+  if (above < rank && rank <= suf_incl) {
+    uint32_t acc = above;
+    const uint32_t hs[4] = {h0, h1, h2, h3};
+    for (int t = 3; t >= 0; --t) {
+      if (acc + hs[t] >= rank) { out[0] = 4 * lane + t; out[1] = rank - acc; break; }
+      acc += hs[t];
+    }
+  }
+}
 
-struct SelSmem {
+// Run starts of a tile's per-chunk candidate runs: counts (2 per thread) ->
+// exclusive starts, starts[nchunk] = total.  Every thread of the kK4Threads
+// workgroup calls it; ends with a barrier.
+CHOCO_DEV uint32_t chunk_run_starts(uint32_t c0, uint32_t c1, uint32_t nchunk, uint32_t* starts, uint32_t* scratch) {
+  const uint32_t j0 = 2 * threadIdx.x, j1 = j0 + 1;
+  uint32_t tot;
+  const uint32_t pre = block_excl_scan(c0 + c1, scratch, &tot);
+  if (j0 < nchunk) starts[j0] = pre;
+  if (j1 < nchunk) starts[j1] = pre + c0;
+  if (threadIdx.x == 0) starts[nchunk] = tot;
+  __syncthreads();
+  return tot;
+}
+
+struct FinSmem {
   uint32_t keys[kMCap];
   uint32_t G[kNBucket];
   uint32_t hist[256];
+  uint32_t run_start[kMaxTileChunks + 1];
   uint32_t scratch[24];
   uint32_t bc[8];
+  uint32_t flag;
 };
+static_assert(kK2Target <= kK4Threads, "K34 keeps one tile per thread");
 
 template <int MODE, bool XH>
-__global__ __launch_bounds__(kK3Threads) void topk_select_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t nb,
-    uint32_t side_cap, uint64_t seed, float scale, TopkCtrl* __restrict__ ctrl,
-    const uint32_t* __restrict__ cum_tab, const uint32_t* __restrict__ side, uint32_t* __restrict__ tile_info,
-    float* __restrict__ out_val, int32_t* __restrict__ out_idx, int64_t idx_base) {
-  __shared__ SelSmem fs;
+__global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
+    uint32_t side_cap, uint64_t seed, float scale, TopkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ cum_tab,
+    const uint32_t* __restrict__ cntw, const uint32_t* __restrict__ side, const float* __restrict__ cval,
+    const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
+    int64_t idx_base) {
+  __shared__ FinSmem fs;
   __shared__ ExactSmem es;
   const int tid = threadIdx.x, w = tid >> 6;
-  STAMP(100, 0);
+  const int64_t b = blockIdx.x;
+  STAMP(24576 + b, 0);
   const uint32_t s_lo = ctrl->s_lo, shift = ctrl->shift, overflow = ctrl->overflow;
   const uint32_t ku = (uint32_t)k;
+  // this tile's per-chunk entry counts (independent of everything below)
+  const uint32_t nchunk = tile / (uint32_t)kChunk;
+  const uint32_t j0 = 2 * tid, j1 = j0 + 1;
+  const uint32_t cw0 = j0 < nchunk ? cntw[b * nchunk + j0] : 0u;
+  const uint32_t cw1 = j1 < nchunk ? cntw[b * nchunk + j1] : 0u;
   if (tid < kNBucket) {
     uint32_t g[kNRep];
 #pragma unroll
@@ -839,6 +920,15 @@ __global__ __launch_bounds__(kK3Threads) void topk_select_kernel(
   }
   if (tid == 0) fs.bc[0] = 0;
   __syncthreads();
+  // every workgroup has read the totals and the overflow flag: the last one to
+  // draw a ticket clears them for the next call
+  if (last_block_ticket_atomics(&ctrl->fin_ticket, nb, &fs.flag)) {
+    for (int i = tid; i < kNRep * kNBucket; i += kK4Threads) (&ctrl->G[0][0])[i] = 0;
+    if (tid == 0) {
+      ctrl->overflow = 0;
+      ctrl->fin_ticket = 0;
+    }
+  }
   // G[j] = #candidates in buckets >= j is non-increasing; j* = the unique
   // j <= 254 with G[j] >= k > G[j+1]
   bool fallback = overflow != 0 || fs.G[0] < ku || fs.G[kNMaybe] >= ku;
@@ -848,63 +938,41 @@ __global__ __launch_bounds__(kK3Threads) void topk_select_kernel(
   if (!fallback && fs.G[jstar] - fs.G[jstar + 1] > (uint32_t)kMCap) fallback = true;
   if (fallback) {
     // the sample's guess was off: exact single-workgroup selection (correct, slow)
-    Src<MODE, XH> src{x, xh, seed};
-    if (tid == 0) ctrl->fallback = 1u;
-    block_topk_exact(src, n, k, scale, out_val, out_idx, idx_base, es);
+    if (b == 0) {
+      Src<MODE, XH> src{x, xh, seed};
+      block_topk_exact(src, n, k, scale, out_val, out_idx, idx_base, es);
+    }
     return;
   }
-  STAMP(100, 1);
-  // ---- this thread's tiles: b = tid * kK3PerThread + q (contiguous, so the block
-  // scans below run in tile order)
-  uint32_t above[kK3PerThread], cb[kK3PerThread], off[kK3PerThread];
-#pragma unroll
-  for (int q = 0; q < kK3PerThread; ++q) {
-    const int64_t b = (int64_t)tid * kK3PerThread + q;
-    const int64_t bc = b < (int64_t)nb ? b : 0;  // clamped: the loads below are unconditional
-    const uint32_t* row = cum_tab + bc * kNBucket;
-    const uint32_t a = row[jstar], c = row[jstar + 1], s = row[kNMaybe];
-    above[q] = b < (int64_t)nb ? c : 0u;
-    cb[q] = b < (int64_t)nb ? a - c : 0u;  // keys of bucket j* in this tile
-    off[q] = c - s;                        // their side-list offset (buckets stored high to low)
-  }
-  uint32_t mine = 0;
-#pragma unroll
-  for (int q = 0; q < kK3PerThread; ++q) mine += cb[q];
-  STAMP(102, 0);
-  uint32_t M;
-  const uint32_t kpos = block_excl_scan(mine, fs.scratch, &M);  // M = G[j*] - G[j*+1]
-  STAMP(102, 1);
+  // ---- thread t <-> tile t: bucket-j* key count and side-list offset
+  const bool mine_tile = tid < (int)nb;
+  uint32_t above = 0, cb = 0, off = 0;
   {
-    // this thread's key slots [0, mine) over its tiles; loads in batches of 8
-    // issued before any LDS store, so each batch costs one round trip
-    const uint32_t* sd[kK3PerThread];
-    uint32_t first[kK3PerThread];
-    uint32_t acc = 0;
-#pragma unroll
-    for (int q = 0; q < kK3PerThread; ++q) {
-      sd[q] = side + ((int64_t)tid * kK3PerThread + q) * side_cap + off[q];
-      first[q] = acc;
-      acc += cb[q];
+    const uint32_t* row = cum_tab + (int64_t)(mine_tile ? tid : 0) * kNBucket;  // clamped: loads unconditional
+    const uint32_t a = row[jstar], c = row[jstar + 1], s = row[kNMaybe];
+    if (mine_tile) {
+      above = c;
+      cb = a - c;     // keys of bucket j* in this tile
+      off = c - s;    // their side-list offset (buckets stored high to low)
     }
+  }
+  uint32_t M;
+  const uint32_t kpos = block_excl_scan(cb, fs.scratch, &M);  // M = G[j*] - G[j*+1]
+  {
+    // this tile's keys -> LDS slots [kpos, kpos + cb); loads in batches of 8
+    // issued before any LDS store, so each batch costs one round trip
+    const uint32_t* sd = side + (int64_t)(mine_tile ? tid : 0) * side_cap + off;
     constexpr int kB = 8;
-    for (uint32_t i0 = 0; i0 < mine; i0 += kB) {
+    for (uint32_t i0 = 0; i0 < cb; i0 += kB) {
       uint32_t v[kB];
 #pragma unroll
-      for (int g = 0; g < kB; ++g) {
-        const uint32_t i = min(i0 + g, mine - 1);  // clamped: the load is unconditional
-        int q = 0;
-#pragma unroll
-        for (int t = 1; t < kK3PerThread; ++t) q += i >= first[t];
-        v[g] = sd[q][i - first[q]];
-      }
+      for (int g = 0; g < kB; ++g) v[g] = sd[min(i0 + g, cb - 1)];  // clamped: the load is unconditional
 #pragma unroll
       for (int g = 0; g < kB; ++g)
-        if (i0 + g < mine) fs.keys[kpos + i0 + g] = v[g];
+        if (i0 + g < cb) fs.keys[kpos + i0 + g] = v[g];
     }
   }
-  STAMP(102, 2);
   __syncthreads();
-  STAMP(100, 2);
   // ---- radix select inside bucket j*: rel = key - base_j in [0, 2^shift)
   const uint32_t base_j = s_lo + (jstar << shift);
   uint32_t prefix = 0, krem = ku - fs.G[jstar + 1];  // 1 <= krem <= M
@@ -914,7 +982,7 @@ __global__ __launch_bounds__(kK3Threads) void topk_select_kernel(
     const uint32_t dmask = (1u << (sh - dsh)) - 1u;
     if (tid < 256) fs.hist[tid] = 0;
     __syncthreads();
-    for (uint32_t j = tid; j < M; j += kK3Threads) {
+    for (uint32_t j = tid; j < M; j += kK4Threads) {
       const uint32_t rel = fs.keys[j] - base_j;
       if ((rel >> sh) == (prefix >> sh)) atomicAdd(&fs.hist[(rel >> dsh) & dmask], 1u);
     }
@@ -928,100 +996,41 @@ __global__ __launch_bounds__(kK3Threads) void topk_select_kernel(
   }
   const uint32_t T = base_j + prefix;
   const uint32_t r = krem;  // ties at T to take (>= 1)
-  STAMP(100, 3);
   // ---- per tile: #keys > T (every key above bucket j* is) and #keys == T
-  uint32_t gt[kK3PerThread], eq[kK3PerThread];
-  uint32_t gsum = 0, esum = 0;
-  {
-    uint32_t p = kpos;
-#pragma unroll
-    for (int q = 0; q < kK3PerThread; ++q) {
-      uint32_t g = above[q], e = 0;
-      for (uint32_t i = 0; i < cb[q]; ++i) {
-        const uint32_t key = fs.keys[p + i];
-        g += key > T;
-        e += key == T;
-      }
-      p += cb[q];
-      gt[q] = g;
-      eq[q] = e;
-      gsum += g;
-      esum += e;
-    }
+  uint32_t gt = above, eq = 0;
+  for (uint32_t i = 0; i < cb; ++i) {
+    const uint32_t key = fs.keys[kpos + i];
+    gt += key > T;
+    eq += key == T;
   }
   uint32_t gtot, etot;
-  uint32_t gpre = block_excl_scan(gsum, fs.scratch, &gtot);
-  uint32_t epre = block_excl_scan(esum, fs.scratch, &etot);
-  uint32_t* __restrict__ tile_off = tile_info;
-  uint32_t* __restrict__ tile_tieb = tile_info + nb;
-  uint32_t* __restrict__ tile_mode = tile_info + 2 * nb;
-#pragma unroll
-  for (int q = 0; q < kK3PerThread; ++q) {
-    const int64_t b = (int64_t)tid * kK3PerThread + q;
-    if (b < (int64_t)nb) {
-      const uint32_t taken = min(r, epre);  // ties taken by earlier tiles (lowest index first)
-      const uint32_t take = min(eq[q], r - taken);
-      tile_off[b] = gpre + taken;
-      tile_tieb[b] = epre;
-      tile_mode[b] = take == 0 ? kTakeNone : (take == eq[q] ? kTakeAll : kTakePartial);
-    }
-    gpre += gt[q];
-    epre += eq[q];
+  const uint32_t gpre = block_excl_scan(gt, fs.scratch, &gtot);
+  const uint32_t epre = block_excl_scan(eq, fs.scratch, &etot);
+  if (tid == (int)b) {
+    const uint32_t taken = min(r, epre);  // ties taken by earlier tiles (lowest index first)
+    const uint32_t take = min(eq, r - taken);
+    fs.bc[4] = gpre + taken;
+    fs.bc[5] = epre;
+    fs.bc[6] = take == 0 ? kTakeNone : (take == eq ? kTakeAll : kTakePartial);
   }
-  if (tid == 0) {
-    ctrl->T = T;
-    ctrl->r = r;
-    ctrl->fallback = 0u;
-  }
-  STAMP(101, 0);
-}
-
-// ----------------------------------------------------------------------------
-// K4: ordered compaction, one workgroup per tile
-// ----------------------------------------------------------------------------
-template <int MODE>
-__global__ __launch_bounds__(kK4Threads) void topk_emit_kernel(
-    uint32_t tile, uint32_t nb, uint64_t seed, float scale, const TopkCtrl* __restrict__ ctrl,
-    const uint32_t* __restrict__ cntw, const uint32_t* __restrict__ tile_info, const float* __restrict__ cval,
-    const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
-    int64_t idx_base) {
-  __shared__ uint32_t scratch[24];
-  __shared__ uint32_t run_start[2 * kK4Threads + 1];
-  const int64_t b = blockIdx.x;
-  STAMP(24576 + b, 0);
-  // every control word is independent: issue all loads before the first use
-  const uint32_t fallback = ctrl->fallback, T = ctrl->T, r = ctrl->r;
-  uint32_t out = tile_info[b];
-  uint32_t tie_run = tile_info[nb + b];
-  const uint32_t mode = tile_info[2 * nb + b];
-  const uint32_t nchunk = tile / (uint32_t)kChunk;  // <= 2 * kK4Threads (tile <= 2^31 / 256)
-  const uint32_t j0 = 2 * threadIdx.x, j1 = j0 + 1;
-  const uint32_t cw0 = j0 < nchunk ? cntw[b * nchunk + j0] : 0u;
-  const uint32_t cw1 = j1 < nchunk ? cntw[b * nchunk + j1] : 0u;
-  if (fallback) return;
-  {
-    // exclusive scan of the tile's per-chunk run lengths -> run_start[0..nchunk]
-    uint32_t tot;
-    const uint32_t pre = block_excl_scan(cw0 + cw1, scratch, &tot);
-    if (j0 < nchunk) run_start[j0] = pre;
-    if (j1 < nchunk) run_start[j1] = pre + cw0;
-    if (threadIdx.x == 0) run_start[nchunk] = tot;
-    __syncthreads();
-  }
-  const uint32_t tot = run_start[nchunk];
-  const int64_t tb = b * tile;
+  const uint32_t tot = chunk_run_starts(cw0, cw1, nchunk, fs.run_start, fs.scratch);
+  STAMP(24576 + b, 1);
+  uint32_t out = fs.bc[4];
+  uint32_t tie_run = fs.bc[5];
+  const uint32_t mode = fs.bc[6];
+  const int64_t tb = b * (int64_t)tile;
   // Batches of kK4Threads * R candidates; thread t owns R consecutive positions
   // (thread order = index order), loads them all at once, and one block scan of
   // its count places them (two scans only when ties at T are split).
   constexpr int R = 8;
   for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads * R) {
-    const uint32_t pb = p0 + threadIdx.x * R;
+    const uint32_t pb = p0 + tid * R;
     uint32_t lo = 0;
     if (pb < tot) {
       uint32_t hi = nchunk - 1;
       while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
-        if (run_start[mid] <= pb) lo = mid; else hi = mid - 1;
+        if (fs.run_start[mid] <= pb) lo = mid; else hi = mid - 1;
       }
     }
     int64_t addr[R];
@@ -1029,8 +1038,8 @@ __global__ __launch_bounds__(kK4Threads) void topk_emit_kernel(
     for (int i = 0; i < R; ++i) {
       const uint32_t p = pb + i;
       if (p < tot)
-        while (run_start[lo + 1] <= p) ++lo;  // the run of position p (runs may be empty)
-      addr[i] = p < tot ? tb + (int64_t)lo * kChunk + (p - run_start[lo]) : tb;  // clamped: loads are unconditional
+        while (fs.run_start[lo + 1] <= p) ++lo;  // the run of position p (runs may be empty)
+      addr[i] = p < tot ? tb + (int64_t)lo * kChunk + (p - fs.run_start[lo]) : tb;  // clamped: loads unconditional
     }
     float v[R];
     uint32_t idx[R];
@@ -1039,35 +1048,35 @@ __global__ __launch_bounds__(kK4Threads) void topk_emit_kernel(
       v[i] = cval[addr[i]];
       idx[i] = cidx[addr[i]];
     }
-    bool gt[R], eq[R];
+    bool gtv[R], eqv[R];
     uint32_t neq = 0;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const bool valid = pb + i < tot;
       const uint32_t key = MODE == kData ? fkey(v[i]) : (rank_hash(seed, idx[i]) >> 1);
-      gt[i] = valid && key > T;
-      eq[i] = valid && key == T;
-      neq += eq[i] ? 1u : 0u;
+      gtv[i] = valid && key > T;
+      eqv[i] = valid && key == T;
+      neq += eqv[i] ? 1u : 0u;
     }
     bool sel[R];
     if (mode == kTakePartial) {  // workgroup-uniform
       uint32_t eq_total;
-      uint32_t rank = tie_run + block_excl_scan(neq, scratch, &eq_total);
+      uint32_t rank = tie_run + block_excl_scan(neq, fs.scratch, &eq_total);
 #pragma unroll
       for (int i = 0; i < R; ++i) {
-        sel[i] = gt[i] || (eq[i] && rank < r);
-        rank += eq[i] ? 1u : 0u;
+        sel[i] = gtv[i] || (eqv[i] && rank < r);
+        rank += eqv[i] ? 1u : 0u;
       }
       tie_run += eq_total;
     } else {
 #pragma unroll
-      for (int i = 0; i < R; ++i) sel[i] = gt[i] || (eq[i] && mode == kTakeAll);
+      for (int i = 0; i < R; ++i) sel[i] = gtv[i] || (eqv[i] && mode == kTakeAll);
     }
     uint32_t nmine = 0;
 #pragma unroll
     for (int i = 0; i < R; ++i) nmine += sel[i] ? 1u : 0u;
     uint32_t nsel;
-    uint32_t pos = out + block_excl_scan(nmine, scratch, &nsel);
+    uint32_t pos = out + block_excl_scan(nmine, fs.scratch, &nsel);
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       if (sel[i]) {
@@ -1078,7 +1087,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_emit_kernel(
     }
     out += nsel;
   }
-  STAMP(24576 + b, 1);
+  STAMP(24576 + b, 2);
 }
 
 // ----------------------------------------------------------------------------
@@ -1112,39 +1121,30 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   uint32_t* cum = reinterpret_cast<uint32_t*>(base + L.off_cum);
   uint32_t* cntw = reinterpret_cast<uint32_t*>(base + L.off_cntw);
   uint32_t* side = reinterpret_cast<uint32_t*>(base + L.off_side);
-  uint32_t* tinfo = reinterpret_cast<uint32_t*>(base + L.off_tile);
   float* cval = reinterpret_cast<float*>(base + L.off_cval);
   uint32_t* cidx = reinterpret_cast<uint32_t*>(base + L.off_cidx);
-  if (MODE == kData) {
-    uint32_t* k1 = reinterpret_cast<uint32_t*>(base + L.off_k1);
-    CHOCO_KLAUNCH((topk_sample_hist_kernel<XH>), dim3(kK1Blocks), dim3(kK1Threads), 0, st, x, xh, n, k1);
-    CHOCO_LAUNCHED("topk_sample_hist_kernel");
-    CHOCO_KLAUNCH((topk_sample_bounds_kernel<XH>), dim3(kK1Blocks), dim3(kK1Threads), 0, st, x, xh, n, k, ctrl,
-                  k1);
-    CHOCO_LAUNCHED("topk_sample_bounds_kernel");
-  } else {
+  uint32_t hs_lo = 0;
+  uint64_t hs_hi = 0;
+  if (MODE == kHash) {
     // keys uniform on [0, 2^31): P(key >= t) = (2^31 - t) / 2^31
     const double nd = (double)n, kd = (double)k, sd = sqrt(kd);
     const double c_lo = std::min(nd, kd + 6.0 * sd + 16.0);
     const double c_hi = kd - 6.0 * sd - 16.0;
     const double two31 = 2147483648.0;
-    uint32_t s_lo = (uint32_t)std::max(0.0, floor(two31 * (1.0 - c_lo / nd)));
-    uint64_t s_hi_est = c_hi < 1.0 ? 0x80000000ull : (uint64_t)ceil(two31 * (1.0 - c_hi / nd));
-    if (s_hi_est <= s_lo) s_hi_est = (uint64_t)s_lo + 1;
-    CHOCO_KLAUNCH(topk_set_params_kernel, dim3(1), dim3(256), 0, st, ctrl, s_lo, s_hi_est);
-    CHOCO_LAUNCHED("topk_set_params_kernel");
+    hs_lo = (uint32_t)std::max(0.0, floor(two31 * (1.0 - c_lo / nd)));
+    hs_hi = c_hi < 1.0 ? 0x80000000ull : (uint64_t)ceil(two31 * (1.0 - c_hi / nd));
+    if (hs_hi <= hs_lo) hs_hi = (uint64_t)hs_lo + 1;
   }
   profile_begin("topk_stream", st);
-  CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, L.tile, L.nb,
-                L.side_cap, seed, ctrl, cum, cntw, side, cval, cidx);
+  CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, k, L.tile,
+                L.side_cap, seed, hs_lo, hs_hi, ctrl, cum, cntw, side, cval, cidx);
   profile_end("topk_stream", st);
   CHOCO_LAUNCHED("topk_stream_kernel");
-  CHOCO_KLAUNCH((topk_select_kernel<MODE, XH>), dim3(1), dim3(kK3Threads), 0, st, x, xh, n, k, L.nb,
-                L.side_cap, seed, scale, ctrl, cum, side, tinfo, out_val, out_idx, idx_base);
-  CHOCO_LAUNCHED("topk_select_kernel");
-  CHOCO_KLAUNCH((topk_emit_kernel<MODE>), dim3(L.nb), dim3(kK4Threads), 0, st, L.tile, L.nb, seed, scale, ctrl,
-                cntw, tinfo, cval, cidx, out_val, out_idx, idx_base);
-  CHOCO_LAUNCHED("topk_emit_kernel");
+  profile_begin("topk_finish", st);
+  CHOCO_KLAUNCH((topk_finish_kernel<MODE, XH>), dim3(L.nb), dim3(kK4Threads), 0, st, x, xh, n, k, L.tile, L.nb,
+                L.side_cap, seed, scale, ctrl, cum, cntw, side, cval, cidx, out_val, out_idx, idx_base);
+  profile_end("topk_finish", st);
+  CHOCO_LAUNCHED("topk_finish_kernel");
   return CHOCO_OK;
 }
 
@@ -1249,7 +1249,7 @@ CHOCO_API int choco_topk_compress_segmented(const float* x, const float* xhat, c
 // Diagnostic builds only: re-launch the stream kernel alone `reps` times back to
 // back (after one full choco_topk_compress on the same workspace set its
 // thresholds), timed with dispatch-attached events -> *avg_ms.
-CHOCO_API int choco_dbg_stream_only(const float* x, int64_t n, void* ws, size_t ws_bytes, int32_t reps,
+CHOCO_API int choco_dbg_stream_only(const float* x, int64_t n, int64_t k, void* ws, size_t ws_bytes, int32_t reps,
                                     double* avg_ms, void* stream) {
   hipStream_t st = as_stream(stream);
   const TopkLayout L = topk_layout(n);
@@ -1262,7 +1262,8 @@ CHOCO_API int choco_dbg_stream_only(const float* x, int64_t n, void* ws, size_t 
   CHOCO_HIP(hipEventRecord(a, st));
   for (int r = 0; r < reps; ++r)
     hipLaunchKernelGGL((topk_stream_kernel<kData, false>), dim3(L.nb), dim3(kK2Threads), 0, st, x, nullptr, n,
-                       L.tile, L.nb, L.side_cap, (uint64_t)0, ctrl, reinterpret_cast<uint32_t*>(base + L.off_cum),
+                       k, L.tile, L.side_cap, (uint64_t)0, 0u, (uint64_t)0, ctrl,
+                       reinterpret_cast<uint32_t*>(base + L.off_cum),
                        reinterpret_cast<uint32_t*>(base + L.off_cntw), reinterpret_cast<uint32_t*>(base + L.off_side),
                        reinterpret_cast<float*>(base + L.off_cval), reinterpret_cast<uint32_t*>(base + L.off_cidx));
   CHOCO_HIP(hipEventRecord(b, st));

@@ -43,8 +43,11 @@ def main():
     if a.save:
         np.save(a.save, buf)
     t = buf.astype(np.int64)
-    k1 = t[:64]
-    t0 = k1[:, 0][k1[:, 0] > 0].min()
+    k2 = t[1024:1024 + 4096]
+    k2 = k2[k2[:, 0] > 0]
+    pro = t[20000:20000 + 2048]
+    pro = pro[pro[:, 0] > 0]
+    t0 = k2[:, 0].min()
 
     def us(v):
         return (v - t0) * TICK_US
@@ -56,27 +59,23 @@ def main():
             return
         print(f"  {name:34s} min {us(v.min()):8.2f}  med {us(np.median(v)):8.2f}  max {us(v.max()):8.2f} us")
 
-    print(f"n={a.n} k={k}; times in us from the first K1 workgroup start")
-    print("K1 sample (64 workgroups x 2 kernels)")
-    row("K1a start", k1[:, 0]); row("K1a end", k1[:, 1]); row("K1b fine hist added", k1[:, 2])
-    row("K1b ticket drawn", k1[:, 3]); row("K1b last wg: bounds", t[64:65, 0])
-    k2 = t[1024:24576]
-    k2 = k2[k2[:, 0] > 0]
-    print(f"K2 stream ({len(k2)} workgroups)")
-    row("start", k2[:, 0]); row("streamed", k2[:, 1]); row("hist done", k2[:, 2]); row("end", k2[:, 3])
-    dur = (k2[:, 1] - k2[:, 0]) * TICK_US
-    tail = (k2[:, 3] - k2[:, 1]) * TICK_US
-    print(f"  per-wg stream time  min {dur.min():.2f} med {np.median(dur):.2f} max {dur.max():.2f} us;"
+    print(f"n={a.n} k={k}; times in us from the first K2 workgroup start")
+    print(f"K2 sample + stream ({len(k2)} workgroups)")
+    row("start", k2[:, 0]); row("sample bounds", k2[:, 1]); row("streamed", k2[:, 2]); row("end", k2[:, 3])
+    row("  sample keys in registers", pro[:, 0]); row("  coarse histogram", pro[:, 1])
+    row("  fine histogram", pro[:, 2]); row("  bounds", pro[:, 3])
+    tb = t[22000:22000 + 2048]
+    row("  tile entries binned", tb[tb[:, 0] > 0][:, 0])
+    pro = (k2[:, 1] - k2[:, 0]) * TICK_US
+    dur = (k2[:, 2] - k2[:, 1]) * TICK_US
+    tail = (k2[:, 3] - k2[:, 2]) * TICK_US
+    print(f"  per-wg prologue min {pro.min():.2f} med {np.median(pro):.2f} max {pro.max():.2f} us;"
+          f" stream min {dur.min():.2f} med {np.median(dur):.2f} max {dur.max():.2f} us;"
           f" end-of-tile min {tail.min():.2f} med {np.median(tail):.2f} max {tail.max():.2f} us")
-    print("K3 select")
-    row("start", t[100:101, 0]); row("j* found", t[100:101, 1]); row("tid0: table words in", t[102:103, 0])
-    row("tid0: key slots scanned", t[102:103, 1]); row("tid0: keys stored", t[102:103, 2])
-    row("bucket keys in LDS", t[100:101, 2])
-    row("T selected", t[100:101, 3]); row("end", t[101:102, 0])
     k4 = t[24576:40960]
     k4 = k4[k4[:, 0] > 0]
-    print(f"K4 emit ({len(k4)} workgroups)")
-    row("start", k4[:, 0]); row("end", k4[:, 1])
+    print(f"K34 select + emit ({len(k4)} workgroups)")
+    row("start", k4[:, 0]); row("offsets known", k4[:, 1]); row("end", k4[:, 2])
 
 
 if __name__ == "__main__":
