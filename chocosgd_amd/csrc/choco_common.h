@@ -74,6 +74,16 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // ---------------------------------------------------------------- device helpers
 CHOCO_DEV uint32_t fkey(float v) { return __float_as_uint(v) & 0x7fffffffu; }
 
+// 16-byte non-temporal load (global_load_dwordx4 ... nt) for bytes a kernel
+// reads ONCE: they do not allocate in the Infinity Cache, so the stream neither
+// evicts a previous kernel's dirty lines there (their write-back would land in
+// the middle of the read stream) nor the data a later pass re-reads.
+typedef float choco_f32x4 __attribute__((ext_vector_type(4)));
+CHOCO_DEV float4 ld_nt4(const float* p) {
+  const choco_f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const choco_f32x4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 CHOCO_DEV int lane_id() { return __lane_id(); }
 
 // number of set bits of `mask` strictly below this lane
@@ -91,38 +101,46 @@ CHOCO_DEV T wave_sum(T v) {
   return v;
 }
 
-// inclusive prefix sum across the 64 lanes
+// DPP lane shift of a 32-bit value; lanes whose source is outside the row (or
+// whose row is masked off) get 0.
+template <int CTRL, int ROW_MASK = 0xf>
+CHOCO_DEV uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+
+// Inclusive prefix sum across the 64 lanes: Hillis-Steele inside each 16-lane
+// row (row_shr 1, 2, 4, 8), then row_bcast:15 / row_bcast:31 carry the row
+// totals -- six DPP adds, no LDS traffic (a __shfl_up version costs six
+// dependent ds_bpermute round trips).
 CHOCO_DEV uint32_t wave_incl_scan(uint32_t v) {
-  const int l = lane_id();
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t t = __shfl_up(v, o);
-    if (l >= o) v += t;
-  }
+  v += dpp_u32<0x111>(v);
+  v += dpp_u32<0x112>(v);
+  v += dpp_u32<0x114>(v);
+  v += dpp_u32<0x118>(v);
+  v += dpp_u32<0x142, 0xa>(v);
+  v += dpp_u32<0x143, 0xc>(v);
   return v;
 }
 
+CHOCO_DEV uint32_t wave_sum(uint32_t v) { return __builtin_amdgcn_readlane(wave_incl_scan(v), 63); }
+
 // Block-wide exclusive scan of one u32 per thread.  `scratch` must hold
 // blockDim.x/64 + 1 words of LDS.  Returns the exclusive prefix; *total gets the
-// block sum.  All threads of the block must call it.
+// block sum.  All threads of the block must call it.  Two barriers: every wave
+// scans the per-wave totals itself.
 CHOCO_DEV uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
   const int l = lane_id();
-  const int w = threadIdx.x >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = (blockDim.x + 63) >> 6;
-  uint32_t inc = wave_incl_scan(v);
+  const uint32_t inc = wave_incl_scan(v);
   if (l == 63) scratch[w] = inc;
   __syncthreads();
-  if (w == 0) {
-    uint32_t t = (l < nw) ? scratch[l] : 0u;
-    uint32_t ti = wave_incl_scan(t);
-    if (l < nw) scratch[l] = ti - t;
-    if (l == 63) scratch[nw] = ti;
-  }
-  __syncthreads();
-  uint32_t r = scratch[w] + inc - v;
-  *total = scratch[nw];
-  __syncthreads();
-  return r;
+  const uint32_t t = (l < nw) ? scratch[l] : 0u;
+  const uint32_t ti = wave_incl_scan(t);
+  const uint32_t base = __builtin_amdgcn_readlane(ti - t, w);
+  *total = __builtin_amdgcn_readlane(ti, nw - 1);
+  __syncthreads();  // scratch may be reused by the next call
+  return base + inc - v;
 }
 
 // 64-bit reinterpret for double atomics through integer exchange

@@ -123,10 +123,10 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int64_t A = ((int64_t)(r0 + u) * Np + j0) & ~(int64_t)3;
-      float4 a = *reinterpret_cast<const float4*>(x + A + 4 * lane);
+      float4 a = ld_nt4(x + A + 4 * lane);
       float4 t = *reinterpret_cast<const float4*>(x + A + 256);  // tail (used by lane 63; broadcast)
       if (XH) {
-        const float4 h = *reinterpret_cast<const float4*>(xh + A + 4 * lane);
+        const float4 h = ld_nt4(xh + A + 4 * lane);
         const float4 ht = *reinterpret_cast<const float4*>(xh + A + 256);
         a.x -= h.x; a.y -= h.y; a.z -= h.z; a.w -= h.w;
         t.x -= ht.x; t.y -= ht.y; t.z -= ht.z; t.w -= ht.w;

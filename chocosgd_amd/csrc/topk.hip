@@ -345,7 +345,7 @@ CHOCO_DEV void load_sample(const float* __restrict__ x, const float* __restrict_
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < kSampleLoads; ++j) {
-    const int64_t q = (int64_t)(w + kK2Waves * j) * stride4 + lane;
+    const int64_t q = (int64_t)(w * kSampleLoads + j) * stride4 + lane;  // wave w: runs 8w .. 8w+7
     s[j] = reinterpret_cast<const float4*>(x)[q];
     if (XH) h[j] = reinterpret_cast<const float4*>(xh)[q];
   }
@@ -406,6 +406,9 @@ CHOCO_DEV void block_find_two(const uint32_t* hist, uint32_t r0, uint32_t r1, ui
 //     chunk's global slots, and the maybe keys are counting-sorted into the
 //     tile's side list on the way.
 // ----------------------------------------------------------------------------
+#ifndef CHOCO_PRO_ONLY  // diagnostic knob: the stream kernel stops after the sample prologue
+#define CHOCO_PRO_ONLY 0
+#endif
 #ifndef CHOCO_PRO_PREFETCH  // diagnostic knob: first batch issued before the sample histogram
 #define CHOCO_PRO_PREFETCH 1
 #endif
@@ -415,9 +418,11 @@ constexpr int kMaxTileChunks = 2048;  // tile <= 2^31 / 256 elements
 static_assert((int64_t(1) << 31) / kK2Target / kChunk <= kMaxTileChunks, "chunk table");
 static_assert(kMaxTileChunks <= 2 * kK4Threads, "two chunk counts per thread");
 
+constexpr int kListPerWave = 256;  // sample keys >= F kept per wave (prologue)
 struct SampleHist {
-  uint32_t coarse[2048];
+  uint32_t coarse[4][2048];  // 4 copies (lane & 3): same-bin lanes of one atomic instruction serialize
   uint32_t fine[2][2048];
+  uint32_t list[kK2Waves][kListPerWave];
 };
 
 struct StreamSmem {
@@ -449,12 +454,8 @@ static_assert(sizeof(SampleHist) <= sizeof(uint2) * kK2Waves * kPairsPerWave, "s
 #ifndef CHOCO_STREAM_NT
 #define CHOCO_STREAM_NT 1
 #endif
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 CHOCO_DEV float4 ld_stream(const float* p) {
-  if (CHOCO_STREAM_NT) {
-    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-  }
+  if (CHOCO_STREAM_NT) return ld_nt4(p);
   return *reinterpret_cast<const float4*>(p);
 }
 
@@ -631,6 +632,103 @@ CHOCO_DEV uint32_t claim_chunk(StreamSmem& sm, int lane) {
   return __builtin_amdgcn_readfirstlane(c);
 }
 
+// The sample's candidate floor s_lo (the R_lo-th largest key, rounded down) and
+// sure ceiling s_hi (the R_hi-th largest, rounded up) -- every workgroup, same
+// sample, same answer.  LDS atomics cost ~16 cycles per wave instruction however
+// few lanes collide (measured: 32 per thread ~3 us per pass), so the fast path
+// counts few keys: a 1024-key subsample (one key per thread) in a coarse
+// histogram (16 runs spread over the buffer) gives a floor F safely below the R_lo-th largest key, the ~3 % of
+// keys >= F are compacted into per-wave LDS lists with ballots, and one fine
+// histogram of those (2048 bins over [F, subsample max]) resolves both ranks.
+// If a list overflows or fewer than R_lo keys pass F, the full two-level
+// histogram of all keys runs instead.
+CHOCO_DEV void sample_bounds_full(const uint32_t (&kk)[kSampleLoads * 4], const SampleRanks& R, int lane,
+                                  StreamSmem& sm, uint32_t& s_lo, uint64_t& s_hi_est) {
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 6 * 2048; i += kK2Threads) (&sm.u.sh.coarse[0][0])[i] = 0u;
+  if (tid < 8) sm.bc[tid] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSampleLoads * 4; ++j) atomicAdd(&sm.u.sh.coarse[lane & 3][kk[j] >> 20], 1u);
+  __syncthreads();
+  for (int i = tid; i < 2048; i += kK2Threads)
+    sm.u.sh.coarse[0][i] += sm.u.sh.coarse[1][i] + sm.u.sh.coarse[2][i] + sm.u.sh.coarse[3][i];
+  __syncthreads();
+  block_find_two(sm.u.sh.coarse[0], R.lo, R.hi, sm.scratch, sm.bc);
+  const uint32_t c_lo = sm.bc[0], r_lo = sm.bc[1], c_hi = sm.bc[2], r_hi = sm.bc[3];
+#pragma unroll
+  for (int j = 0; j < kSampleLoads * 4; ++j) {
+    const uint32_t cb = kk[j] >> 20, fb = (kk[j] >> 9) & 2047u;
+    if (R.lo && cb == c_lo) atomicAdd(&sm.u.sh.fine[0][fb], 1u);
+    if (R.hi && cb == c_hi) atomicAdd(&sm.u.sh.fine[1][fb], 1u);
+  }
+  __syncthreads();
+  block_find_two(sm.u.sh.fine[0], R.lo ? r_lo : 0u, 0u, sm.scratch, sm.bc + 4);
+  block_find_two(sm.u.sh.fine[1], R.hi ? r_hi : 0u, 0u, sm.scratch, sm.bc + 6);
+  s_lo = R.lo ? ((c_lo << 20) | (sm.bc[4] << 9)) : 0u;                                  // rounded down
+  s_hi_est = R.hi ? (uint64_t)((c_hi << 20) | (sm.bc[6] << 9)) + 512u : 0x80000000ull;  // rounded up
+}
+
+CHOCO_DEV void sample_bounds(const uint32_t (&kk)[kSampleLoads * 4], int64_t n, int64_t k, int lane, int w,
+                             StreamSmem& sm, uint32_t& s_lo, uint64_t& s_hi_est) {
+  const int tid = threadIdx.x;
+  const SampleRanks R = sample_ranks(n, k);
+  if (R.lo == 0) {  // every key is a candidate
+    s_lo = 0u;
+    s_hi_est = 0x80000000ull;
+    return;
+  }
+  // ---- stage A: subsample floor F and subsample maximum
+  uint32_t* coarse = sm.u.sh.coarse[0];
+  uint32_t* fine = sm.u.sh.fine[0];
+  for (int i = tid; i < 2048; i += kK2Threads) { coarse[i] = 0u; fine[i] = 0u; }
+  if (tid < 8) sm.bc[tid] = 0;
+  __syncthreads();
+  atomicAdd(&coarse[kk[0] >> 20], 1u);  // subsample: every thread's first key (wave w: run 8w)
+  __syncthreads();
+  const double e = (double)R.lo * (1024.0 / (double)kSampleN);
+  const uint32_t rA = (uint32_t)min(1024.0, ceil(e + 4.0 * sqrt(e) + 4.0));
+  STAMP(20000 + blockIdx.x, 1);
+  block_find_two(coarse, rA, 1u, sm.scratch, sm.bc);
+  const uint32_t F = sm.bc[0] << 20;
+  const uint32_t top = (sm.bc[2] + 1u) << 20;          // above the subsample maximum's bin
+  const uint32_t width = top - F;                      // >= 2^20
+  const int shiftB = max(0, 32 - (int)__clz(width - 1u) - 11);
+  // ---- keys >= F -> this wave's list (ballot compaction, no atomics)
+  uint32_t cnt = 0;  // wave-uniform
+#pragma unroll
+  for (int j = 0; j < kSampleLoads * 4; ++j) {
+    const bool p = kk[j] >= F;
+    const uint64_t M = ballot(p);
+    if (M != 0ull) {
+      const uint32_t pos = cnt + mask_prefix(M);
+      if (p && pos < (uint32_t)kListPerWave) sm.u.sh.list[w][pos] = kk[j];
+      cnt += (uint32_t)__popcll(M);
+    }
+  }
+  const uint32_t mine = min(cnt, (uint32_t)kListPerWave);
+  for (uint32_t i = lane; i < mine; i += 64) {
+    const uint32_t key = sm.u.sh.list[w][i];
+    atomicAdd(&fine[min((key - F) >> shiftB, 2047u)], 1u);
+  }
+  if (lane == 0) {
+    atomicAdd(&sm.bc[6], cnt);
+    if (cnt > (uint32_t)kListPerWave) atomicOr(&sm.bc[7], 1u);
+  }
+  __syncthreads();
+  STAMP(20000 + blockIdx.x, 2);
+  const uint32_t total = sm.bc[6], over = sm.bc[7];
+  __syncthreads();
+  if (over != 0u || total < R.lo) {  // workgroup-uniform
+    sample_bounds_full(kk, R, lane, sm, s_lo, s_hi_est);
+    return;
+  }
+  block_find_two(fine, R.lo, R.hi, sm.scratch, sm.bc);
+  const uint32_t j_lo = sm.bc[0], j_hi = sm.bc[2];
+  s_lo = F + (j_lo << shiftB);                                                     // rounded down
+  s_hi_est = (R.hi == 0u || j_hi == 2047u) ? 0x80000000ull : (uint64_t)F + ((uint64_t)(j_hi + 1u) << shiftB);
+}
+
 // Random-k (MODE kHash): keys are uniform on [0, 2^31) and (s_lo, s_hi) come from
 // the binomial tails (host), passed as hs_lo / hs_hi.
 template <int MODE, bool XH>
@@ -654,6 +752,10 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     const int64_t cb = b * (int64_t)tile + (int64_t)c * kChunk;
     return (c < nchunk && cb + kChunk <= n) ? cb : 0;
   };
+  auto batch1 = [&](uint32_t c) -> int64_t {
+    const int64_t cb = b * (int64_t)tile + (int64_t)c * kChunk;
+    return (c < nchunk && cb + kChunk <= n) ? cb + kStep : 0;
+  };
 
   // ---- prologue: the wave's first chunk is chunk w; its first batch goes out
   // behind the sample loads, so the histogram work below overlaps HBM traffic
@@ -663,12 +765,10 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   if constexpr (MODE == kData) {
     float4 s[kSampleLoads], sh[kSampleLoads];
     load_sample<XH>(x, xh, n, s, sh);
-    if (!XH && CHOCO_PRO_PREFETCH) load_rows_full<XH>(x, xh, batch0(c), lane, A);  // XH: no registers to spare
-    for (int i = tid; i < 3 * 2048; i += kK2Threads) (&sm.u.sh.coarse[0])[i] = 0u;
+    if (!XH && CHOCO_PRO_PREFETCH)  // the first chunk's first batch (XH: no registers to spare)
+      load_rows_full<XH>(x, xh, batch0(c), lane, A);
     if (tid < kNBucket) sm.hist[tid] = 0;
-    if (tid < 8) sm.bc[tid] = 0;
     if (tid == 0) sm.next_chunk = kK2Waves;
-    __syncthreads();
     uint32_t kk[kSampleLoads * 4];
 #pragma unroll
     for (int j = 0; j < kSampleLoads; ++j) {
@@ -677,27 +777,12 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       kk[4 * j + 0] = fkey(v.x); kk[4 * j + 1] = fkey(v.y); kk[4 * j + 2] = fkey(v.z); kk[4 * j + 3] = fkey(v.w);
     }
     STAMP(20000 + b, 0);
-#pragma unroll
-    for (int j = 0; j < kSampleLoads * 4; ++j) atomicAdd(&sm.u.sh.coarse[kk[j] >> 20], 1u);
-    __syncthreads();
-    STAMP(20000 + b, 1);
-    const SampleRanks R = sample_ranks(n, k);
-    block_find_two(sm.u.sh.coarse, R.lo, R.hi, sm.scratch, sm.bc);
-    const uint32_t c_lo = sm.bc[0], r_lo = sm.bc[1], c_hi = sm.bc[2], r_hi = sm.bc[3];
-#pragma unroll
-    for (int j = 0; j < kSampleLoads * 4; ++j) {
-      const uint32_t cb = kk[j] >> 20, fb = (kk[j] >> 9) & 2047u;
-      if (R.lo && cb == c_lo) atomicAdd(&sm.u.sh.fine[0][fb], 1u);
-      if (R.hi && cb == c_hi) atomicAdd(&sm.u.sh.fine[1][fb], 1u);
-    }
-    __syncthreads();
-    STAMP(20000 + b, 2);
-    block_find_two(sm.u.sh.fine[0], R.lo ? r_lo : 0u, 0u, sm.scratch, sm.bc + 4);
-    block_find_two(sm.u.sh.fine[1], R.hi ? r_hi : 0u, 0u, sm.scratch, sm.bc + 6);
-    const uint32_t s_lo = R.lo ? ((c_lo << 20) | (sm.bc[4] << 9)) : 0u;                       // rounded down
-    const uint64_t s_hi_est = R.hi ? (uint64_t)((c_hi << 20) | (sm.bc[6] << 9)) + 512u : 0x80000000ull;  // up
+    uint32_t s_lo;
+    uint64_t s_hi_est;
+    sample_bounds(kk, n, k, lane, w, sm, s_lo, s_hi_est);
     bk = make_buckets(s_lo, s_hi_est, seed);
     if (XH || !CHOCO_PRO_PREFETCH) load_rows_full<XH>(x, xh, batch0(c), lane, A);
+    if (!XH) load_rows_full<XH>(x, xh, batch1(c), lane, B);  // the sample keys are dead now
     __syncthreads();  // the sample histograms (aliasing the pair buffer) are dead from here on
     STAMP(20000 + b, 3);
   } else {
@@ -707,6 +792,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     __syncthreads();
   }
   bk.n = n;
+  if (CHOCO_PRO_ONLY) return;  // diagnostic builds only
   if (b == 0 && tid == 0) {
     ctrl->s_lo = bk.s_lo;
     ctrl->s_hi = bk.s_hi;
@@ -731,11 +817,12 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     a.lstart = a.lfill;
     if (cbeg + kChunk <= n) {
       if constexpr (MODE == kData && !XH) {
-        // double-buffered: the next batch is always in flight
-        load_rows_full<XH>(x, xh, cbeg + kStep, lane, B);
+        // double-buffered: A and B hold this chunk; each is refilled with the
+        // next chunk's batch as soon as it has been processed
         process_batch<XH>(src, A, cbeg, cend, sm, w, lane, a, ov, oi, bk);
         load_rows_full<XH>(x, xh, batch0(nx), lane, A);
         process_batch<XH>(src, B, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk);
+        load_rows_full<XH>(x, xh, batch1(nx), lane, B);
       } else if constexpr (MODE == kData) {
         // two input streams: one batch (16 KiB per wave) at a time
         process_batch<XH>(src, A, cbeg, cend, sm, w, lane, a, ov, oi, bk);
@@ -759,7 +846,10 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
         }
         process_row<MODE, XH, true>(src, v, i, cend, sm, w, lane, a, ov, oi, bk);
       }
-      if constexpr (MODE == kData) load_rows_full<XH>(x, xh, batch0(nx), lane, A);
+      if constexpr (MODE == kData) {
+        load_rows_full<XH>(x, xh, batch0(nx), lane, A);
+        if (!XH) load_rows_full<XH>(x, xh, batch1(nx), lane, B);
+      }
     }
     // the chunk's remaining entries (< 64)
     const uint32_t rest = a.estaged - a.eflushed;
