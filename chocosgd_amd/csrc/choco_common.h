@@ -143,6 +143,25 @@ CHOCO_DEV uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* tota
   return base + inc - v;
 }
 
+// block_excl_scan for two values at once (one set of barriers); `scratch` must
+// hold 2 * blockDim.x/64 words.
+CHOCO_DEV void block_excl_scan2(uint32_t v0, uint32_t v1, uint32_t* scratch, uint32_t* pre0, uint32_t* pre1,
+                                uint32_t* tot0, uint32_t* tot1) {
+  const int l = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = (blockDim.x + 63) >> 6;
+  const uint32_t i0 = wave_incl_scan(v0), i1 = wave_incl_scan(v1);
+  if (l == 63) { scratch[w] = i0; scratch[nw + w] = i1; }
+  __syncthreads();
+  const uint32_t t0 = (l < nw) ? scratch[l] : 0u, t1 = (l < nw) ? scratch[nw + l] : 0u;
+  const uint32_t s0 = wave_incl_scan(t0), s1 = wave_incl_scan(t1);
+  *pre0 = __builtin_amdgcn_readlane(s0 - t0, w) + i0 - v0;
+  *pre1 = __builtin_amdgcn_readlane(s1 - t1, w) + i1 - v1;
+  *tot0 = __builtin_amdgcn_readlane(s0, nw - 1);
+  *tot1 = __builtin_amdgcn_readlane(s1, nw - 1);
+  __syncthreads();
+}
+
 // 64-bit reinterpret for double atomics through integer exchange
 CHOCO_DEV double atomic_exchange_double(double* p, double v) {
   unsigned long long old = atomicExch(reinterpret_cast<unsigned long long*>(p),

@@ -291,17 +291,20 @@ __global__ __launch_bounds__(kExactThreads) void topk_segmented_kernel(
 // without a grid-wide hand-off.  Both bounds are heuristics that K34 verifies
 // (G[0] >= k, G[sure] < k); any k/n works.
 // ----------------------------------------------------------------------------
-constexpr int kSampleRuns = 128;
-constexpr int kSampleN = kSampleRuns * 256;                  // 32768
-constexpr int kSampleLoads = kSampleRuns * 64 / kK2Threads;  // float4 per thread (8)
-static_assert(kSampleLoads * kK2Threads == kSampleRuns * 64, "sample geometry");
+constexpr int kSampleRuns = 64;
+constexpr int kSampleN = kSampleRuns * 256;                  // 16384
+constexpr int kK1Threads = 1024;                              // the bounds kernel: one workgroup
+constexpr int kSampleLoads = kSampleRuns * 64 / kK1Threads;  // float4 per thread (4)
+static_assert(kSampleLoads * kK1Threads == kSampleRuns * 64, "sample geometry");
 
 struct SampleRanks {
   uint32_t lo, hi;  // 1-based ranks from the top; 0 = none
+  uint32_t sub;     // rank in the 1024-key subsample whose bin floors F (below rank lo w.h.p.)
 };
 
-// Ranks of the candidate floor / sure ceiling in the sample (~6 sigma margins).
-CHOCO_DEV SampleRanks sample_ranks(int64_t n, int64_t k) {
+// Ranks of the candidate floor / sure ceiling in the sample (~6 sigma margins),
+// computed on the host (they depend on n and k only) and passed to K2.
+static SampleRanks sample_ranks(int64_t n, int64_t k) {
   const double m = (double)kSampleN;
   const double e = (double)k / (double)n * m;
   const double sd = sqrt(e);
@@ -310,6 +313,8 @@ CHOCO_DEV SampleRanks sample_ranks(int64_t n, int64_t k) {
   SampleRanks r;
   r.lo = rlo <= m ? (uint32_t)rlo : 0u;  // 0: every key is a candidate
   r.hi = rhi >= 1.0 ? (uint32_t)rhi : 0u;  // 0: no key is "sure"
+  const double es = (double)r.lo * (1024.0 / m);
+  r.sub = (uint32_t)std::min(1024.0, ceil(es + 4.0 * sqrt(es) + 4.0));
   return r;
 }
 
@@ -338,6 +343,17 @@ CHOCO_DEV Buckets make_buckets(uint32_t s_lo, uint64_t s_hi_est, uint64_t seed) 
   return bk;
 }
 
+CHOCO_DEV Buckets make_buckets_from(uint32_t s_lo, uint32_t s_hi, uint32_t shift, uint64_t seed) {
+  Buckets bk;
+  bk.n = 0;
+  bk.s_lo = s_lo;
+  bk.s_hi = s_hi;
+  bk.shift = shift;
+  bk.s_lo_f = __uint_as_float(s_lo);
+  bk.seed = seed;
+  return bk;
+}
+
 template <bool XH>
 CHOCO_DEV void load_sample(const float* __restrict__ x, const float* __restrict__ xh, int64_t n,
                            float4 (&s)[kSampleLoads], float4 (&h)[kSampleLoads]) {
@@ -345,7 +361,7 @@ CHOCO_DEV void load_sample(const float* __restrict__ x, const float* __restrict_
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < kSampleLoads; ++j) {
-    const int64_t q = (int64_t)(w * kSampleLoads + j) * stride4 + lane;  // wave w: runs 8w .. 8w+7
+    const int64_t q = (int64_t)(w * kSampleLoads + j) * stride4 + lane;  // wave w: runs 4w .. 4w+3
     s[j] = reinterpret_cast<const float4*>(x)[q];
     if (XH) h[j] = reinterpret_cast<const float4*>(xh)[q];
   }
@@ -406,12 +422,6 @@ CHOCO_DEV void block_find_two(const uint32_t* hist, uint32_t r0, uint32_t r1, ui
 //     chunk's global slots, and the maybe keys are counting-sorted into the
 //     tile's side list on the way.
 // ----------------------------------------------------------------------------
-#ifndef CHOCO_PRO_ONLY  // diagnostic knob: the stream kernel stops after the sample prologue
-#define CHOCO_PRO_ONLY 0
-#endif
-#ifndef CHOCO_PRO_PREFETCH  // diagnostic knob: first batch issued before the sample histogram
-#define CHOCO_PRO_PREFETCH 1
-#endif
 constexpr int kEnt = 128;  // entry ring per wave (flush at 64: <= 63 + 64 pending)
 constexpr int kPairsPerWave = 640;  // LDS pair region per wave (~2x the k = 1 % share)
 constexpr int kMaxTileChunks = 2048;  // tile <= 2^31 / 256 elements
@@ -432,7 +442,6 @@ struct StreamSmem {
   uint32_t trash_i[64];
   union {
     uint2 pairs[kK2Waves * kPairsPerWave];  // (value bits, index) per candidate, per-wave regions
-    SampleHist sh;                          // prologue only
   } u;
   uint32_t cmeta[kMaxTileChunks];  // per chunk: LDS start | LDS count << 16
   uint32_t ccnt[kMaxTileChunks];   // per chunk: candidates
@@ -442,7 +451,6 @@ struct StreamSmem {
   uint32_t bc[8];
   uint32_t next_chunk;            // the tile's chunk counter (waves claim chunks)
 };
-static_assert(sizeof(SampleHist) <= sizeof(uint2) * kK2Waves * kPairsPerWave, "sample histogram alias");
 
 // Unconditional float4 loads of kK2Unroll rows (no branch around a load: the
 // compiler's vmcnt accounting stays exact and all rows are in flight together).
@@ -642,54 +650,58 @@ CHOCO_DEV uint32_t claim_chunk(StreamSmem& sm, int lane) {
 // histogram of those (2048 bins over [F, subsample max]) resolves both ranks.
 // If a list overflows or fewer than R_lo keys pass F, the full two-level
 // histogram of all keys runs instead.
+struct BoundsSmem {
+  SampleHist sh;
+  uint32_t scratch[40];
+  uint32_t bc[8];
+};
+
 CHOCO_DEV void sample_bounds_full(const uint32_t (&kk)[kSampleLoads * 4], const SampleRanks& R, int lane,
-                                  StreamSmem& sm, uint32_t& s_lo, uint64_t& s_hi_est) {
+                                  BoundsSmem& sm, uint32_t& s_lo, uint64_t& s_hi_est) {
   const int tid = threadIdx.x;
-  for (int i = tid; i < 6 * 2048; i += kK2Threads) (&sm.u.sh.coarse[0][0])[i] = 0u;
+  for (int i = tid; i < 6 * 2048; i += kK1Threads) (&sm.sh.coarse[0][0])[i] = 0u;
   if (tid < 8) sm.bc[tid] = 0;
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kSampleLoads * 4; ++j) atomicAdd(&sm.u.sh.coarse[lane & 3][kk[j] >> 20], 1u);
+  for (int j = 0; j < kSampleLoads * 4; ++j) atomicAdd(&sm.sh.coarse[lane & 3][kk[j] >> 20], 1u);
   __syncthreads();
-  for (int i = tid; i < 2048; i += kK2Threads)
-    sm.u.sh.coarse[0][i] += sm.u.sh.coarse[1][i] + sm.u.sh.coarse[2][i] + sm.u.sh.coarse[3][i];
+  for (int i = tid; i < 2048; i += kK1Threads)
+    sm.sh.coarse[0][i] += sm.sh.coarse[1][i] + sm.sh.coarse[2][i] + sm.sh.coarse[3][i];
   __syncthreads();
-  block_find_two(sm.u.sh.coarse[0], R.lo, R.hi, sm.scratch, sm.bc);
+  block_find_two(sm.sh.coarse[0], R.lo, R.hi, sm.scratch, sm.bc);
   const uint32_t c_lo = sm.bc[0], r_lo = sm.bc[1], c_hi = sm.bc[2], r_hi = sm.bc[3];
 #pragma unroll
   for (int j = 0; j < kSampleLoads * 4; ++j) {
     const uint32_t cb = kk[j] >> 20, fb = (kk[j] >> 9) & 2047u;
-    if (R.lo && cb == c_lo) atomicAdd(&sm.u.sh.fine[0][fb], 1u);
-    if (R.hi && cb == c_hi) atomicAdd(&sm.u.sh.fine[1][fb], 1u);
+    if (R.lo && cb == c_lo) atomicAdd(&sm.sh.fine[0][fb], 1u);
+    if (R.hi && cb == c_hi) atomicAdd(&sm.sh.fine[1][fb], 1u);
   }
   __syncthreads();
-  block_find_two(sm.u.sh.fine[0], R.lo ? r_lo : 0u, 0u, sm.scratch, sm.bc + 4);
-  block_find_two(sm.u.sh.fine[1], R.hi ? r_hi : 0u, 0u, sm.scratch, sm.bc + 6);
+  block_find_two(sm.sh.fine[0], R.lo ? r_lo : 0u, 0u, sm.scratch, sm.bc + 4);
+  block_find_two(sm.sh.fine[1], R.hi ? r_hi : 0u, 0u, sm.scratch, sm.bc + 6);
   s_lo = R.lo ? ((c_lo << 20) | (sm.bc[4] << 9)) : 0u;                                  // rounded down
   s_hi_est = R.hi ? (uint64_t)((c_hi << 20) | (sm.bc[6] << 9)) + 512u : 0x80000000ull;  // rounded up
 }
 
-CHOCO_DEV void sample_bounds(const uint32_t (&kk)[kSampleLoads * 4], int64_t n, int64_t k, int lane, int w,
-                             StreamSmem& sm, uint32_t& s_lo, uint64_t& s_hi_est) {
+CHOCO_DEV void sample_bounds(const uint32_t (&kk)[kSampleLoads * 4], const SampleRanks& R, int lane, int w,
+                             BoundsSmem& sm, uint32_t& s_lo, uint64_t& s_hi_est) {
   const int tid = threadIdx.x;
-  const SampleRanks R = sample_ranks(n, k);
   if (R.lo == 0) {  // every key is a candidate
     s_lo = 0u;
     s_hi_est = 0x80000000ull;
     return;
   }
   // ---- stage A: subsample floor F and subsample maximum
-  uint32_t* coarse = sm.u.sh.coarse[0];
-  uint32_t* fine = sm.u.sh.fine[0];
-  for (int i = tid; i < 2048; i += kK2Threads) { coarse[i] = 0u; fine[i] = 0u; }
+  uint32_t* coarse = sm.sh.coarse[0];
+  uint32_t* fine = sm.sh.fine[0];
+  for (int i = tid; i < 2048; i += kK1Threads) { coarse[i] = 0u; fine[i] = 0u; }
   if (tid < 8) sm.bc[tid] = 0;
   __syncthreads();
-  atomicAdd(&coarse[kk[0] >> 20], 1u);  // subsample: every thread's first key (wave w: run 8w)
+  atomicAdd(&coarse[kk[0] >> 20], 1u);  // subsample: every thread's first key (wave w: run 4w)
   __syncthreads();
-  const double e = (double)R.lo * (1024.0 / (double)kSampleN);
-  const uint32_t rA = (uint32_t)min(1024.0, ceil(e + 4.0 * sqrt(e) + 4.0));
-  STAMP(20000 + blockIdx.x, 1);
-  block_find_two(coarse, rA, 1u, sm.scratch, sm.bc);
+  STAMP(30001, 0);
+  block_find_two(coarse, R.sub, 1u, sm.scratch, sm.bc);
+  STAMP(30001, 1);
   const uint32_t F = sm.bc[0] << 20;
   const uint32_t top = (sm.bc[2] + 1u) << 20;          // above the subsample maximum's bin
   const uint32_t width = top - F;                      // >= 2^20
@@ -702,13 +714,14 @@ CHOCO_DEV void sample_bounds(const uint32_t (&kk)[kSampleLoads * 4], int64_t n, 
     const uint64_t M = ballot(p);
     if (M != 0ull) {
       const uint32_t pos = cnt + mask_prefix(M);
-      if (p && pos < (uint32_t)kListPerWave) sm.u.sh.list[w][pos] = kk[j];
+      if (p && pos < (uint32_t)kListPerWave) sm.sh.list[w][pos] = kk[j];
       cnt += (uint32_t)__popcll(M);
     }
   }
+  STAMP(30001, 2);
   const uint32_t mine = min(cnt, (uint32_t)kListPerWave);
   for (uint32_t i = lane; i < mine; i += 64) {
-    const uint32_t key = sm.u.sh.list[w][i];
+    const uint32_t key = sm.sh.list[w][i];
     atomicAdd(&fine[min((key - F) >> shiftB, 2047u)], 1u);
   }
   if (lane == 0) {
@@ -716,24 +729,63 @@ CHOCO_DEV void sample_bounds(const uint32_t (&kk)[kSampleLoads * 4], int64_t n, 
     if (cnt > (uint32_t)kListPerWave) atomicOr(&sm.bc[7], 1u);
   }
   __syncthreads();
-  STAMP(20000 + blockIdx.x, 2);
+  STAMP(30001, 3);
   const uint32_t total = sm.bc[6], over = sm.bc[7];
   __syncthreads();
   if (over != 0u || total < R.lo) {  // workgroup-uniform
     sample_bounds_full(kk, R, lane, sm, s_lo, s_hi_est);
     return;
   }
+  STAMP(30002, 0);
   block_find_two(fine, R.lo, R.hi, sm.scratch, sm.bc);
+  STAMP(30002, 1);
   const uint32_t j_lo = sm.bc[0], j_hi = sm.bc[2];
   s_lo = F + (j_lo << shiftB);                                                     // rounded down
   s_hi_est = (R.hi == 0u || j_hi == 2047u) ? 0x80000000ull : (uint64_t)F + ((uint64_t)(j_hi + 1u) << shiftB);
+}
+
+
+// K1: the sample bounds, ONE 1024-thread workgroup.  Measured: computed inside
+// the stream kernel's prologue by every workgroup they cost ~8-13 us of idle
+// HBM per call (the first prefetch batch cannot cover them: 255 CUs issuing
+// 8 KiB per wave at once block in the load-issue path until the flood
+// drains, so the histogram work does not start until it has); as their own
+// tiny kernel they take a few us and the stream kernel starts streaming at
+// once.
+template <bool XH>
+__global__ __launch_bounds__(kK1Threads) void topk_bounds_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ xh, int64_t n,
+                                                                 SampleRanks ranks, TopkCtrl* __restrict__ ctrl) {
+  __shared__ BoundsSmem sm;
+  STAMP(30000, 0);
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  float4 s[kSampleLoads], sh[kSampleLoads];
+  load_sample<XH>(x, xh, n, s, sh);
+  uint32_t kk[kSampleLoads * 4];
+#pragma unroll
+  for (int j = 0; j < kSampleLoads; ++j) {
+    float4 v = s[j];
+    if (XH) { v.x -= sh[j].x; v.y -= sh[j].y; v.z -= sh[j].z; v.w -= sh[j].w; }
+    kk[4 * j + 0] = fkey(v.x); kk[4 * j + 1] = fkey(v.y); kk[4 * j + 2] = fkey(v.z); kk[4 * j + 3] = fkey(v.w);
+  }
+  STAMP(30000, 1);
+  uint32_t s_lo;
+  uint64_t s_hi_est;
+  sample_bounds(kk, ranks, lane, w, sm, s_lo, s_hi_est);
+  if (threadIdx.x == 0) {
+    const Buckets bk = make_buckets(s_lo, s_hi_est, 0);
+    ctrl->s_lo = bk.s_lo;
+    ctrl->s_hi = bk.s_hi;
+    ctrl->shift = bk.shift;
+  }
+  STAMP(30000, 2);
 }
 
 // Random-k (MODE kHash): keys are uniform on [0, 2^31) and (s_lo, s_hi) come from
 // the binomial tails (host), passed as hs_lo / hs_hi.
 template <int MODE, bool XH>
 __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile,
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, uint32_t tile,
     uint32_t side_cap, uint64_t seed, uint32_t hs_lo, uint64_t hs_hi, TopkCtrl* __restrict__ ctrl,
     uint32_t* __restrict__ cum_tab, uint32_t* __restrict__ cntw, uint32_t* __restrict__ side,
     float* __restrict__ cval, uint32_t* __restrict__ cidx) {
@@ -757,43 +809,23 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     return (c < nchunk && cb + kChunk <= n) ? cb + kStep : 0;
   };
 
-  // ---- prologue: the wave's first chunk is chunk w; its first batch goes out
-  // behind the sample loads, so the histogram work below overlaps HBM traffic
+  // ---- prologue: the wave's first chunk is chunk w; both of its batches go out
+  // at once, then the bounds K1 left in the control block are read
   uint32_t c = (uint32_t)w;
   float4 A[kK2Unroll], B[kK2Unroll];
   Buckets bk;
   if constexpr (MODE == kData) {
-    float4 s[kSampleLoads], sh[kSampleLoads];
-    load_sample<XH>(x, xh, n, s, sh);
-    if (!XH && CHOCO_PRO_PREFETCH)  // the first chunk's first batch (XH: no registers to spare)
-      load_rows_full<XH>(x, xh, batch0(c), lane, A);
-    if (tid < kNBucket) sm.hist[tid] = 0;
-    if (tid == 0) sm.next_chunk = kK2Waves;
-    uint32_t kk[kSampleLoads * 4];
-#pragma unroll
-    for (int j = 0; j < kSampleLoads; ++j) {
-      float4 v = s[j];
-      if (XH) { v.x -= sh[j].x; v.y -= sh[j].y; v.z -= sh[j].z; v.w -= sh[j].w; }
-      kk[4 * j + 0] = fkey(v.x); kk[4 * j + 1] = fkey(v.y); kk[4 * j + 2] = fkey(v.z); kk[4 * j + 3] = fkey(v.w);
-    }
-    STAMP(20000 + b, 0);
-    uint32_t s_lo;
-    uint64_t s_hi_est;
-    sample_bounds(kk, n, k, lane, w, sm, s_lo, s_hi_est);
-    bk = make_buckets(s_lo, s_hi_est, seed);
-    if (XH || !CHOCO_PRO_PREFETCH) load_rows_full<XH>(x, xh, batch0(c), lane, A);
-    if (!XH) load_rows_full<XH>(x, xh, batch1(c), lane, B);  // the sample keys are dead now
-    __syncthreads();  // the sample histograms (aliasing the pair buffer) are dead from here on
-    STAMP(20000 + b, 3);
+    load_rows_full<XH>(x, xh, batch0(c), lane, A);
+    if (!XH) load_rows_full<XH>(x, xh, batch1(c), lane, B);
+    bk = make_buckets_from(ctrl->s_lo, ctrl->s_hi, ctrl->shift, seed);
   } else {
-    if (tid < kNBucket) sm.hist[tid] = 0;
-    if (tid == 0) sm.next_chunk = kK2Waves;
     bk = make_buckets(hs_lo, hs_hi, seed);
-    __syncthreads();
   }
+  if (tid < kNBucket) sm.hist[tid] = 0;
+  if (tid == 0) sm.next_chunk = kK2Waves;
+  __syncthreads();
   bk.n = n;
-  if (CHOCO_PRO_ONLY) return;  // diagnostic builds only
-  if (b == 0 && tid == 0) {
+  if (MODE == kHash && b == 0 && tid == 0) {
     ctrl->s_lo = bk.s_lo;
     ctrl->s_hi = bk.s_hi;
     ctrl->shift = bk.shift;
@@ -969,16 +1001,65 @@ CHOCO_DEV uint32_t chunk_run_starts(uint32_t c0, uint32_t c1, uint32_t nchunk, u
   return tot;
 }
 
+constexpr int kSelBits = 13;  // radix-select digit: one round for bucket widths <= 2^13
 struct FinSmem {
   uint32_t keys[kMCap];
+  uint32_t hist[1 << kSelBits];
   uint32_t G[kNBucket];
-  uint32_t hist[256];
   uint32_t run_start[kMaxTileChunks + 1];
-  uint32_t scratch[24];
+  uint32_t scratch[40];
   uint32_t bc[8];
-  uint32_t flag;
 };
 static_assert(kK2Target <= kK4Threads, "K34 keeps one tile per thread");
+
+// Over hist[1 << kSelBits] (ascending), the bin holding the rank-th largest
+// entry and the rank inside it -> out[0], out[1].  Every thread of the
+// kK4Threads workgroup calls it; ends with a barrier.
+CHOCO_DEV void block_find_rank8k(const uint32_t* hist, uint32_t rank, uint32_t* scratch, uint32_t* out) {
+  constexpr int per = (1 << kSelBits) / kK4Threads;
+  const int tid = threadIdx.x;
+  uint32_t hv[per];
+  uint32_t local = 0;
+#pragma unroll
+  for (int j = 0; j < per; ++j) {
+    hv[j] = hist[tid * per + j];
+    local += hv[j];
+  }
+  uint32_t total;
+  const uint32_t pre = block_excl_scan(local, scratch, &total);
+  const uint32_t above = total - pre - local;  // entries in bins above mine
+  if (above < rank && rank <= above + local) {
+    uint32_t acc = above;
+#pragma unroll
+    for (int j = per - 1; j >= 0; --j) {
+      if (acc < rank && rank <= acc + hv[j]) { out[0] = (uint32_t)(tid * per + j); out[1] = rank - acc; }
+      acc += hv[j];
+    }
+  }
+  __syncthreads();
+}
+
+// Emission of one batch: thread t owns R consecutive candidate positions
+// [pb, pb + R) of its tile (thread order = index order).
+constexpr int kEmitR = 8;
+CHOCO_DEV void emit_addresses(const uint32_t* run_start, uint32_t nchunk, uint32_t tot, uint32_t pb, int64_t tb,
+                              int64_t (&addr)[kEmitR]) {
+  uint32_t lo = 0;
+  if (pb < tot) {
+    uint32_t hi = nchunk - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (run_start[mid] <= pb) lo = mid; else hi = mid - 1;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kEmitR; ++i) {
+    const uint32_t p = pb + i;
+    if (p < tot)
+      while (run_start[lo + 1] <= p) ++lo;  // the run of position p (runs may be empty)
+    addr[i] = p < tot ? tb + (int64_t)lo * kChunk + (p - run_start[lo]) : tb;  // clamped: loads unconditional
+  }
+}
 
 template <int MODE, bool XH>
 __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
@@ -989,42 +1070,58 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     int64_t idx_base) {
   __shared__ FinSmem fs;
   __shared__ ExactSmem es;
-  const int tid = threadIdx.x, w = tid >> 6;
+  const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
   STAMP(24576 + b, 0);
-  const uint32_t s_lo = ctrl->s_lo, shift = ctrl->shift, overflow = ctrl->overflow;
+  // ---- first round trip, every load independent: control words (as vector
+  // loads, so they are issued here and not as late scalar loads), the totals,
+  // every tile's j*-independent "sure" count, this tile's chunk counts
   const uint32_t ku = (uint32_t)k;
-  // this tile's per-chunk entry counts (independent of everything below)
   const uint32_t nchunk = tile / (uint32_t)kChunk;
   const uint32_t j0 = 2 * tid, j1 = j0 + 1;
   const uint32_t cw0 = j0 < nchunk ? cntw[b * nchunk + j0] : 0u;
   const uint32_t cw1 = j1 < nchunk ? cntw[b * nchunk + j1] : 0u;
+  uint32_t cword = 0;
+  if (tid < 4) cword = __hip_atomic_load(&ctrl->s_lo + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool mine_tile = tid < (int)nb;
+  const uint32_t* row = cum_tab + (int64_t)(mine_tile ? tid : 0) * kNBucket;  // clamped: loads unconditional
+  const uint32_t sure_t = row[kNMaybe];
+  uint32_t g[kNRep];
   if (tid < kNBucket) {
-    uint32_t g[kNRep];
 #pragma unroll
     for (int r = 0; r < kNRep; ++r) g[r] = ctrl->G[r][tid];
+  }
+  if (tid < 4) fs.bc[tid] = cword;  // s_lo, s_hi, shift, overflow
+  const uint32_t tot = chunk_run_starts(cw0, cw1, nchunk, fs.run_start, fs.scratch);
+  const uint32_t s_lo = fs.bc[0], shift = fs.bc[2], overflow = fs.bc[3];
+  STAMP(26000 + b, 0);
+  // ---- the addresses of the tile's first emission batch (it does not depend on T)
+  const int64_t tb = b * (int64_t)tile;
+  int64_t addr[kEmitR];
+  emit_addresses(fs.run_start, nchunk, tot, (uint32_t)tid * kEmitR, tb, addr);
+  float v[kEmitR];
+  uint32_t idx[kEmitR];
+  if (tid < kNBucket) {
     uint32_t s = 0;
 #pragma unroll
     for (int r = 0; r < kNRep; ++r) s += g[r];
     fs.G[tid] = s;
   }
-  if (tid == 0) fs.bc[0] = 0;
+  if (tid == 0) fs.bc[4] = 0;
   __syncthreads();
-  // every workgroup has read the totals and the overflow flag: the last one to
-  // draw a ticket clears them for the next call
-  if (last_block_ticket_atomics(&ctrl->fin_ticket, nb, &fs.flag)) {
-    for (int i = tid; i < kNRep * kNBucket; i += kK4Threads) (&ctrl->G[0][0])[i] = 0;
-    if (tid == 0) {
-      ctrl->overflow = 0;
-      ctrl->fin_ticket = 0;
-    }
-  }
+  STAMP(26000 + b, 1);
+  // Every workgroup has read the totals and the overflow flag: draw a ticket
+  // now (its return is only looked at on the way out); the last drawer clears
+  // them for the next call.
+  uint32_t ticket = 0;
+  if (tid == 0) ticket = __hip_atomic_fetch_add(&ctrl->fin_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // G[j] = #candidates in buckets >= j is non-increasing; j* = the unique
   // j <= 254 with G[j] >= k > G[j+1]
   bool fallback = overflow != 0 || fs.G[0] < ku || fs.G[kNMaybe] >= ku;
-  if (!fallback && tid < kNMaybe && fs.G[tid] >= ku && fs.G[tid + 1] < ku) fs.bc[0] = tid;
+  if (!fallback && tid < kNMaybe && fs.G[tid] >= ku && fs.G[tid + 1] < ku) fs.bc[4] = tid;
   __syncthreads();
-  const uint32_t jstar = fs.bc[0];
+  const uint32_t jstar = fs.bc[4];
+  STAMP(26000 + b, 2);
   if (!fallback && fs.G[jstar] - fs.G[jstar + 1] > (uint32_t)kMCap) fallback = true;
   if (fallback) {
     // the sample's guess was off: exact single-workgroup selection (correct, slow)
@@ -1032,150 +1129,161 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
       Src<MODE, XH> src{x, xh, seed};
       block_topk_exact(src, n, k, scale, out_val, out_idx, idx_base, es);
     }
-    return;
-  }
-  // ---- thread t <-> tile t: bucket-j* key count and side-list offset
-  const bool mine_tile = tid < (int)nb;
-  uint32_t above = 0, cb = 0, off = 0;
-  {
-    const uint32_t* row = cum_tab + (int64_t)(mine_tile ? tid : 0) * kNBucket;  // clamped: loads unconditional
-    const uint32_t a = row[jstar], c = row[jstar + 1], s = row[kNMaybe];
-    if (mine_tile) {
-      above = c;
-      cb = a - c;     // keys of bucket j* in this tile
-      off = c - s;    // their side-list offset (buckets stored high to low)
+  } else {
+    // ---- thread t <-> tile t: bucket-j* key count and side-list offset
+    uint32_t above = 0, cb = 0, off = 0;
+    {
+      const uint32_t a = row[jstar], c = row[jstar + 1], s = sure_t;
+      if (mine_tile) {
+        above = c;
+        cb = a - c;   // keys of bucket j* in this tile
+        off = c - s;  // their side-list offset (buckets stored high to low)
+      }
+    }
+    uint32_t M;
+    const uint32_t kpos = block_excl_scan(cb, fs.scratch, &M);  // M = G[j*] - G[j*+1]
+    STAMP(26000 + b, 3);
+    {
+      // this tile's keys -> LDS slots [kpos, kpos + cb); loads in batches of 32
+      // issued before any LDS store, so each batch costs one round trip (a
+      // tile holds ~M / nb ~ 10-30 keys of bucket j*)
+      STAMP(27000 + b, 1);
+      const uint32_t* sd = side + (int64_t)(mine_tile ? tid : 0) * side_cap + off;
+      constexpr int kB = 32;
+      uint32_t kv[kB];
+      if (cb) {
+#pragma unroll
+        for (int q = 0; q < kB; ++q) kv[q] = sd[min((uint32_t)q, cb - 1)];
+      }
+      // The first emission batch's loads go out now, BEHIND the key loads: the
+      // vmcnt counter is in order, so waiting for the keys does not wait for
+      // them, and they land while T is being selected.
+#pragma unroll
+      for (int i = 0; i < kEmitR; ++i) {
+        v[i] = cval[addr[i]];
+        idx[i] = cidx[addr[i]];
+      }
+      if (cb) {
+#pragma unroll
+        for (int q = 0; q < kB; ++q)
+          if ((uint32_t)q < cb) fs.keys[kpos + q] = kv[q];
+      }
+      for (uint32_t i0 = kB; i0 < cb; i0 += kB) {
+        uint32_t kv[kB];
+#pragma unroll
+        for (int q = 0; q < kB; ++q) kv[q] = sd[min(i0 + q, cb - 1)];  // clamped: the load is unconditional
+#pragma unroll
+        for (int q = 0; q < kB; ++q)
+          if (i0 + q < cb) fs.keys[kpos + i0 + q] = kv[q];
+      }
+    }
+    // ---- radix select inside bucket j*: rel = key - base_j in [0, 2^shift),
+    // kSelBits per round (one round for shift <= kSelBits)
+    STAMP(27000 + b, 2);
+    const uint32_t base_j = s_lo + (jstar << shift);
+    uint32_t prefix = 0, krem = ku - fs.G[jstar + 1];  // 1 <= krem <= M
+    int sh = (int)shift;
+    while (sh > 0) {
+      const int dsh = sh > kSelBits ? sh - kSelBits : 0;
+      const uint32_t dmask = (1u << (sh - dsh)) - 1u;
+      for (int i = tid; i < (1 << kSelBits); i += kK4Threads) fs.hist[i] = 0;
+      __syncthreads();  // also: the bucket keys are in LDS
+      for (uint32_t j = tid; j < M; j += kK4Threads) {
+        const uint32_t rel = fs.keys[j] - base_j;
+        if (sh >= 32 || (rel >> sh) == (prefix >> sh)) atomicAdd(&fs.hist[(rel >> dsh) & dmask], 1u);
+      }
+      __syncthreads();
+      block_find_rank8k(fs.hist, krem, fs.scratch, fs.bc + 5);
+      prefix |= fs.bc[5] << dsh;
+      krem = fs.bc[6];
+      sh = dsh;
+    }
+    if (shift == 0) __syncthreads();  // the bucket keys are in LDS
+    STAMP(27000 + b, 0);
+    const uint32_t T = base_j + prefix;
+    const uint32_t r = krem;  // ties at T to take (>= 1)
+    // ---- per tile: #keys > T (every key above bucket j* is) and #keys == T
+    uint32_t gt = above, eq = 0;
+    for (uint32_t i = 0; i < cb; ++i) {
+      const uint32_t key = fs.keys[kpos + i];
+      gt += key > T;
+      eq += key == T;
+    }
+    uint32_t gpre, epre, gtot, etot;
+    block_excl_scan2(gt, eq, fs.scratch, &gpre, &epre, &gtot, &etot);
+    if (tid == (int)b) {
+      const uint32_t taken = min(r, epre);  // ties taken by earlier tiles (lowest index first)
+      const uint32_t take = min(eq, r - taken);
+      fs.bc[4] = gpre + taken;
+      fs.bc[5] = epre;
+      fs.bc[6] = take == 0 ? kTakeNone : (take == eq ? kTakeAll : kTakePartial);
+    }
+    __syncthreads();
+    STAMP(24576 + b, 1);
+    uint32_t out = fs.bc[4];
+    uint32_t tie_run = fs.bc[5];
+    const uint32_t mode = fs.bc[6];
+    // Batches of kK4Threads * kEmitR candidates; one block scan of each thread's
+    // count places them (two scans only when ties at T are split).
+    for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads * kEmitR) {
+      const uint32_t pb = p0 + tid * kEmitR;
+      if (p0 != 0) {  // workgroup-uniform: batches after the prefetched first one
+        emit_addresses(fs.run_start, nchunk, tot, pb, tb, addr);
+#pragma unroll
+        for (int i = 0; i < kEmitR; ++i) {
+          v[i] = cval[addr[i]];
+          idx[i] = cidx[addr[i]];
+        }
+      }
+      bool gtv[kEmitR], eqv[kEmitR];
+      uint32_t neq = 0;
+#pragma unroll
+      for (int i = 0; i < kEmitR; ++i) {
+        const bool valid = pb + i < tot;
+        const uint32_t key = MODE == kData ? fkey(v[i]) : (rank_hash(seed, idx[i]) >> 1);
+        gtv[i] = valid && key > T;
+        eqv[i] = valid && key == T;
+        neq += eqv[i] ? 1u : 0u;
+      }
+      bool sel[kEmitR];
+      if (mode == kTakePartial) {  // workgroup-uniform
+        uint32_t eq_total;
+        uint32_t rank = tie_run + block_excl_scan(neq, fs.scratch, &eq_total);
+#pragma unroll
+        for (int i = 0; i < kEmitR; ++i) {
+          sel[i] = gtv[i] || (eqv[i] && rank < r);
+          rank += eqv[i] ? 1u : 0u;
+        }
+        tie_run += eq_total;
+      } else {
+#pragma unroll
+        for (int i = 0; i < kEmitR; ++i) sel[i] = gtv[i] || (eqv[i] && mode == kTakeAll);
+      }
+      uint32_t nmine = 0;
+#pragma unroll
+      for (int i = 0; i < kEmitR; ++i) nmine += sel[i] ? 1u : 0u;
+      uint32_t nsel;
+      uint32_t pos = out + block_excl_scan(nmine, fs.scratch, &nsel);
+#pragma unroll
+      for (int i = 0; i < kEmitR; ++i) {
+        if (sel[i]) {
+          out_val[pos] = v[i] * scale;
+          out_idx[pos] = (int32_t)((int64_t)idx[i] + idx_base);
+          ++pos;
+        }
+      }
+      out += nsel;
     }
   }
-  uint32_t M;
-  const uint32_t kpos = block_excl_scan(cb, fs.scratch, &M);  // M = G[j*] - G[j*+1]
-  {
-    // this tile's keys -> LDS slots [kpos, kpos + cb); loads in batches of 8
-    // issued before any LDS store, so each batch costs one round trip
-    const uint32_t* sd = side + (int64_t)(mine_tile ? tid : 0) * side_cap + off;
-    constexpr int kB = 8;
-    for (uint32_t i0 = 0; i0 < cb; i0 += kB) {
-      uint32_t v[kB];
-#pragma unroll
-      for (int g = 0; g < kB; ++g) v[g] = sd[min(i0 + g, cb - 1)];  // clamped: the load is unconditional
-#pragma unroll
-      for (int g = 0; g < kB; ++g)
-        if (i0 + g < cb) fs.keys[kpos + i0 + g] = v[g];
-    }
-  }
+  // ---- the workgroup that drew the last ticket clears the totals for the next call
+  if (tid == 0) fs.bc[7] = ticket;
   __syncthreads();
-  // ---- radix select inside bucket j*: rel = key - base_j in [0, 2^shift)
-  const uint32_t base_j = s_lo + (jstar << shift);
-  uint32_t prefix = 0, krem = ku - fs.G[jstar + 1];  // 1 <= krem <= M
-  int sh = (int)shift;
-  while (sh > 0) {
-    const int dsh = sh > 8 ? sh - 8 : 0;
-    const uint32_t dmask = (1u << (sh - dsh)) - 1u;
-    if (tid < 256) fs.hist[tid] = 0;
-    __syncthreads();
-    for (uint32_t j = tid; j < M; j += kK4Threads) {
-      const uint32_t rel = fs.keys[j] - base_j;
-      if ((rel >> sh) == (prefix >> sh)) atomicAdd(&fs.hist[(rel >> dsh) & dmask], 1u);
+  if (fs.bc[7] == nb - 1u) {
+    for (int i = tid; i < kNRep * kNBucket; i += kK4Threads) (&ctrl->G[0][0])[i] = 0;
+    if (tid == 0) {
+      ctrl->overflow = 0;
+      ctrl->fin_ticket = 0;
     }
-    __syncthreads();
-    if (w == 0) wave_find_bin(fs.hist, krem, fs.bc + 2);
-    __syncthreads();
-    prefix |= fs.bc[2] << dsh;
-    krem = fs.bc[3];
-    sh = dsh;
-    __syncthreads();
-  }
-  const uint32_t T = base_j + prefix;
-  const uint32_t r = krem;  // ties at T to take (>= 1)
-  // ---- per tile: #keys > T (every key above bucket j* is) and #keys == T
-  uint32_t gt = above, eq = 0;
-  for (uint32_t i = 0; i < cb; ++i) {
-    const uint32_t key = fs.keys[kpos + i];
-    gt += key > T;
-    eq += key == T;
-  }
-  uint32_t gtot, etot;
-  const uint32_t gpre = block_excl_scan(gt, fs.scratch, &gtot);
-  const uint32_t epre = block_excl_scan(eq, fs.scratch, &etot);
-  if (tid == (int)b) {
-    const uint32_t taken = min(r, epre);  // ties taken by earlier tiles (lowest index first)
-    const uint32_t take = min(eq, r - taken);
-    fs.bc[4] = gpre + taken;
-    fs.bc[5] = epre;
-    fs.bc[6] = take == 0 ? kTakeNone : (take == eq ? kTakeAll : kTakePartial);
-  }
-  const uint32_t tot = chunk_run_starts(cw0, cw1, nchunk, fs.run_start, fs.scratch);
-  STAMP(24576 + b, 1);
-  uint32_t out = fs.bc[4];
-  uint32_t tie_run = fs.bc[5];
-  const uint32_t mode = fs.bc[6];
-  const int64_t tb = b * (int64_t)tile;
-  // Batches of kK4Threads * R candidates; thread t owns R consecutive positions
-  // (thread order = index order), loads them all at once, and one block scan of
-  // its count places them (two scans only when ties at T are split).
-  constexpr int R = 8;
-  for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads * R) {
-    const uint32_t pb = p0 + tid * R;
-    uint32_t lo = 0;
-    if (pb < tot) {
-      uint32_t hi = nchunk - 1;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (fs.run_start[mid] <= pb) lo = mid; else hi = mid - 1;
-      }
-    }
-    int64_t addr[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const uint32_t p = pb + i;
-      if (p < tot)
-        while (fs.run_start[lo + 1] <= p) ++lo;  // the run of position p (runs may be empty)
-      addr[i] = p < tot ? tb + (int64_t)lo * kChunk + (p - fs.run_start[lo]) : tb;  // clamped: loads unconditional
-    }
-    float v[R];
-    uint32_t idx[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      v[i] = cval[addr[i]];
-      idx[i] = cidx[addr[i]];
-    }
-    bool gtv[R], eqv[R];
-    uint32_t neq = 0;
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const bool valid = pb + i < tot;
-      const uint32_t key = MODE == kData ? fkey(v[i]) : (rank_hash(seed, idx[i]) >> 1);
-      gtv[i] = valid && key > T;
-      eqv[i] = valid && key == T;
-      neq += eqv[i] ? 1u : 0u;
-    }
-    bool sel[R];
-    if (mode == kTakePartial) {  // workgroup-uniform
-      uint32_t eq_total;
-      uint32_t rank = tie_run + block_excl_scan(neq, fs.scratch, &eq_total);
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        sel[i] = gtv[i] || (eqv[i] && rank < r);
-        rank += eqv[i] ? 1u : 0u;
-      }
-      tie_run += eq_total;
-    } else {
-#pragma unroll
-      for (int i = 0; i < R; ++i) sel[i] = gtv[i] || (eqv[i] && mode == kTakeAll);
-    }
-    uint32_t nmine = 0;
-#pragma unroll
-    for (int i = 0; i < R; ++i) nmine += sel[i] ? 1u : 0u;
-    uint32_t nsel;
-    uint32_t pos = out + block_excl_scan(nmine, fs.scratch, &nsel);
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      if (sel[i]) {
-        out_val[pos] = v[i] * scale;
-        out_idx[pos] = (int32_t)((int64_t)idx[i] + idx_base);
-        ++pos;
-      }
-    }
-    out += nsel;
   }
   STAMP(24576 + b, 2);
 }
@@ -1225,8 +1333,12 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
     hs_hi = c_hi < 1.0 ? 0x80000000ull : (uint64_t)ceil(two31 * (1.0 - c_hi / nd));
     if (hs_hi <= hs_lo) hs_hi = (uint64_t)hs_lo + 1;
   }
+  if (MODE == kData) {
+    CHOCO_KLAUNCH((topk_bounds_kernel<XH>), dim3(1), dim3(kK1Threads), 0, st, x, xh, n, sample_ranks(n, k), ctrl);
+    CHOCO_LAUNCHED("topk_bounds_kernel");
+  }
   profile_begin("topk_stream", st);
-  CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, k, L.tile,
+  CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, L.tile,
                 L.side_cap, seed, hs_lo, hs_hi, ctrl, cum, cntw, side, cval, cidx);
   profile_end("topk_stream", st);
   CHOCO_LAUNCHED("topk_stream_kernel");
@@ -1352,7 +1464,7 @@ CHOCO_API int choco_dbg_stream_only(const float* x, int64_t n, int64_t k, void* 
   CHOCO_HIP(hipEventRecord(a, st));
   for (int r = 0; r < reps; ++r)
     hipLaunchKernelGGL((topk_stream_kernel<kData, false>), dim3(L.nb), dim3(kK2Threads), 0, st, x, nullptr, n,
-                       k, L.tile, L.side_cap, (uint64_t)0, 0u, (uint64_t)0, ctrl,
+                       L.tile, L.side_cap, (uint64_t)0, 0u, (uint64_t)0, ctrl,
                        reinterpret_cast<uint32_t*>(base + L.off_cum),
                        reinterpret_cast<uint32_t*>(base + L.off_cntw), reinterpret_cast<uint32_t*>(base + L.off_side),
                        reinterpret_cast<float*>(base + L.off_cval), reinterpret_cast<uint32_t*>(base + L.off_cidx));

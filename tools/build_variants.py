@@ -9,9 +9,6 @@ from chocosgd_amd import build  # noqa: E402
 
 VARIANTS = {
     "stamps": ["CHOCO_STAMPS=1"],
-    "stamps_nopf": ["CHOCO_STAMPS=1", "CHOCO_PRO_PREFETCH=0"],
-    "stamps_proonly": ["CHOCO_STAMPS=1", "CHOCO_PRO_ONLY=1", "CHOCO_PRO_PREFETCH=0"],
-    "stamps_proonly_pf": ["CHOCO_STAMPS=1", "CHOCO_PRO_ONLY=1"],
     "acc_nt": ["CHOCO_ACC_STORE=1"],
     "acc_sc1": ["CHOCO_ACC_STORE=2"],
     "stream_nt": ["CHOCO_STREAM_NT=1"],

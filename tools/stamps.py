@@ -62,6 +62,14 @@ def main():
             return
         print(f"  {name:34s} min {us(v.min()):8.2f}  med {us(np.median(v)):8.2f}  max {us(v.max()):8.2f} us")
 
+    k1 = t[30000]
+    if k1[0] > 0:
+        print(f"K1 bounds: sample in {(k1[1] - k1[0]) * TICK_US:.2f} us, bounds {(k1[2] - k1[0]) * TICK_US:.2f} us "
+              f"after its start; K2 starts {(t0 - k1[2]) * TICK_US:.2f} us after K1's end")
+        s1, s2 = t[30001], t[30002]
+        print("  K1 phases (us after its start): subsample hist %.2f | F found %.2f | compacted %.2f | fine hist %.2f"
+              " | before find %.2f | ranks %.2f" % tuple((v - k1[0]) * TICK_US for v in
+                                                          (s1[0], s1[1], s1[2], s1[3], s2[0], s2[1])))
     print(f"n={a.n} k={k}; times in us from the first K2 workgroup start")
     print(f"K2 sample + stream ({len(k2)} workgroups)")
     row("start", k2[:, 0]); row("sample bounds", k2[:, 1]); row("streamed", k2[:, 2]); row("end", k2[:, 3])
@@ -75,10 +83,18 @@ def main():
     print(f"  per-wg prologue min {pro.min():.2f} med {np.median(pro):.2f} max {pro.max():.2f} us;"
           f" stream min {dur.min():.2f} med {np.median(dur):.2f} max {dur.max():.2f} us;"
           f" end-of-tile min {tail.min():.2f} med {np.median(tail):.2f} max {tail.max():.2f} us")
-    k4 = t[24576:40960]
+    k4 = t[24576:24576 + 1000]
     k4 = k4[k4[:, 0] > 0]
     print(f"K34 select + emit ({len(k4)} workgroups)")
-    row("start", k4[:, 0]); row("offsets known", k4[:, 1]); row("end", k4[:, 2])
+    row("start", k4[:, 0])
+    q = t[26000:26000 + 1000]
+    q = q[q[:, 0] > 0]
+    q2 = t[27000:27000 + 1000]
+    q2 = q2[q2[:, 0] > 0]
+    row("  run starts", q[:, 0]); row("  totals in LDS", q[:, 1]); row("  j* found", q[:, 2])
+    row("  table words + scan", q[:, 3]); row("  (key loads issued)", q2[:, 1])
+    row("  bucket keys stored", q2[:, 2]); row("  T selected", q2[:, 0])
+    row("offsets known", k4[:, 1]); row("end", k4[:, 2])
 
 
 if __name__ == "__main__":
