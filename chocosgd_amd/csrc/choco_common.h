@@ -84,6 +84,21 @@ CHOCO_DEV float4 ld_nt4(const float* p) {
   return make_float4(v.x, v.y, v.z, v.w);
 }
 
+// Raw buffer resource over [base, base + bytes) and a 16-byte load through it
+// (buffer_load_dwordx4, `nt` when NT).  A load whose offset is out of range
+// returns zeros WITHOUT a memory access: a prefetch that has nothing to fetch
+// can still be issued unconditionally (exact vmcnt accounting, no branch)
+// without costing a round trip.
+CHOCO_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+template <bool NT>
+CHOCO_DEV float4 ld_buf4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, NT ? 2 : 0);
+  const choco_f32x4 f = __builtin_bit_cast(choco_f32x4, v);
+  return make_float4(f.x, f.y, f.z, f.w);
+}
+
 CHOCO_DEV int lane_id() { return __lane_id(); }
 
 // number of set bits of `mask` strictly below this lane

@@ -76,9 +76,16 @@ __device__ unsigned long long g_stamps[kStampSlots][4];
   do {                                                                      \
     if (threadIdx.x == 0) g_stamps[(slot)][(j)] = wall_clock64();           \
   } while (0)
+#define WSTAMP(slot, j)                                                      \
+  do {                                                                      \
+    if (lane_id() == 0) g_stamps[(slot)][(j)] = wall_clock64();             \
+  } while (0)
 #else
 #define STAMP(slot, j) \
   do {                 \
+  } while (0)
+#define WSTAMP(slot, j) \
+  do {                  \
   } while (0)
 #endif
 
@@ -453,7 +460,12 @@ struct StreamSmem {
 };
 
 // Unconditional float4 loads of kK2Unroll rows (no branch around a load: the
-// compiler's vmcnt accounting stays exact and all rows are in flight together).
+// compiler's vmcnt accounting stays exact and all rows are in flight together),
+// through buffer resources based at the tile start (tile-relative byte offsets).
+// A chunk that does not exist is "loaded" from kNoChunk, out of the resource's
+// range: zeros, no memory access -- so the prefetch issued after a wave's last
+// chunk does not hold the tile's end for a round trip (the registers it targets
+// are reused there, which waits for it).
 // The once-read stream uses non-temporal loads: they do not allocate in the
 // 256 MB Infinity Cache, so a previous kernel's dirty lines there are not
 // evicted (and written back) in the middle of the stream.  Measured in the
@@ -462,20 +474,19 @@ struct StreamSmem {
 #ifndef CHOCO_STREAM_NT
 #define CHOCO_STREAM_NT 1
 #endif
-CHOCO_DEV float4 ld_stream(const float* p) {
-  if (CHOCO_STREAM_NT) return ld_nt4(p);
-  return *reinterpret_cast<const float4*>(p);
-}
+constexpr uint32_t kNoChunk = 0x80000000u;  // > any tile's bytes (tile <= 2^31 / 256 elements)
+struct TileRsrc {
+  __amdgpu_buffer_rsrc_t x, xh;
+};
 
 template <bool XH>
-CHOCO_DEV void load_rows_full(const float* __restrict__ x, const float* __restrict__ xh, int64_t base, int lane,
-                              float4 (&r)[kK2Unroll]) {
+CHOCO_DEV void load_rows_full(const TileRsrc& ts, uint32_t boff, int lane, float4 (&r)[kK2Unroll]) {
 #pragma unroll
-  for (int u = 0; u < kK2Unroll; ++u) r[u] = ld_stream(x + base + u * 256 + 4 * lane);
+  for (int u = 0; u < kK2Unroll; ++u) r[u] = ld_buf4<CHOCO_STREAM_NT>(ts.x, boff + (u * 256 + 4 * lane) * 4);
   if (XH) {
 #pragma unroll
     for (int u = 0; u < kK2Unroll; ++u) {
-      const float4 h = ld_stream(xh + base + u * 256 + 4 * lane);
+      const float4 h = ld_buf4<CHOCO_STREAM_NT>(ts.xh, boff + (u * 256 + 4 * lane) * 4);
       r[u].x -= h.x; r[u].y -= h.y; r[u].z -= h.z; r[u].w -= h.w;
     }
   }
@@ -799,15 +810,14 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   static_assert(kChunk == 2 * kStep, "a chunk is two load batches (A, B)");
   const uint32_t nchunk = tile / (uint32_t)kChunk;
   Src<MODE, XH> src{x, xh, seed};
-  // a full chunk's first batch, or a harmless re-read of the buffer start (n > kSmallN >= kChunk)
-  auto batch0 = [&](uint32_t c) -> int64_t {
-    const int64_t cb = b * (int64_t)tile + (int64_t)c * kChunk;
-    return (c < nchunk && cb + kChunk <= n) ? cb : 0;
+  // tile-relative byte offset of a full chunk's first / second batch, or kNoChunk
+  const int64_t tlen = min((int64_t)tile, n - b * (int64_t)tile);
+  const TileRsrc ts{buf_rsrc(x + b * (int64_t)tile, (uint32_t)(tlen * 4)),
+                    buf_rsrc((XH ? xh : x) + b * (int64_t)tile, (uint32_t)(tlen * 4))};
+  auto batch0 = [&](uint32_t c) -> uint32_t {
+    return (c < nchunk && (int64_t)(c + 1) * kChunk <= tlen) ? c * (uint32_t)kChunk * 4u : kNoChunk;
   };
-  auto batch1 = [&](uint32_t c) -> int64_t {
-    const int64_t cb = b * (int64_t)tile + (int64_t)c * kChunk;
-    return (c < nchunk && cb + kChunk <= n) ? cb + kStep : 0;
-  };
+  auto batch1 = [&](uint32_t c) -> uint32_t { return batch0(c) + (uint32_t)kStep * 4u; };
 
   // ---- prologue: the wave's first chunk is chunk w; both of its batches go out
   // at once, then the bounds K1 left in the control block are read
@@ -815,8 +825,8 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   float4 A[kK2Unroll], B[kK2Unroll];
   Buckets bk;
   if constexpr (MODE == kData) {
-    load_rows_full<XH>(x, xh, batch0(c), lane, A);
-    if (!XH) load_rows_full<XH>(x, xh, batch1(c), lane, B);
+    load_rows_full<XH>(ts, batch0(c), lane, A);
+    if (!XH) load_rows_full<XH>(ts, batch1(c), lane, B);
     bk = make_buckets_from(ctrl->s_lo, ctrl->s_hi, ctrl->shift, seed);
   } else {
     bk = make_buckets(hs_lo, hs_hi, seed);
@@ -852,15 +862,15 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
         // double-buffered: A and B hold this chunk; each is refilled with the
         // next chunk's batch as soon as it has been processed
         process_batch<XH>(src, A, cbeg, cend, sm, w, lane, a, ov, oi, bk);
-        load_rows_full<XH>(x, xh, batch0(nx), lane, A);
+        load_rows_full<XH>(ts, batch0(nx), lane, A);
         process_batch<XH>(src, B, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk);
-        load_rows_full<XH>(x, xh, batch1(nx), lane, B);
+        load_rows_full<XH>(ts, batch1(nx), lane, B);
       } else if constexpr (MODE == kData) {
         // two input streams: one batch (16 KiB per wave) at a time
         process_batch<XH>(src, A, cbeg, cend, sm, w, lane, a, ov, oi, bk);
-        load_rows_full<XH>(x, xh, cbeg + kStep, lane, A);
+        load_rows_full<XH>(ts, (uint32_t)(cbeg - b * (int64_t)tile + kStep) * 4u, lane, A);
         process_batch<XH>(src, A, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk);
-        load_rows_full<XH>(x, xh, batch0(nx), lane, A);
+        load_rows_full<XH>(ts, batch0(nx), lane, A);
       } else {
         process_rows_hash<MODE, XH>(src, cbeg, cend, sm, w, lane, a, ov, oi, bk);
         process_rows_hash<MODE, XH>(src, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk);
@@ -878,10 +888,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
         }
         process_row<MODE, XH, true>(src, v, i, cend, sm, w, lane, a, ov, oi, bk);
       }
-      if constexpr (MODE == kData) {
-        load_rows_full<XH>(x, xh, batch0(nx), lane, A);
-        if (!XH) load_rows_full<XH>(x, xh, batch1(nx), lane, B);
-      }
+      // the buffer's last chunk: every later chunk is past n, nothing to prefetch
     }
     // the chunk's remaining entries (< 64)
     const uint32_t rest = a.estaged - a.eflushed;
@@ -896,6 +903,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   }
   if (lane == 0) sm.cnt[w] = a.cand;  // wave-uniform
   STAMP(1024 + b, 2);
+  WSTAMP(32000 + b * 8 + (w >> 2), w & 3);
   __syncthreads();
 
   // ---- end of tile: bucket suffix counts; then every chunk's LDS pairs leave to
@@ -929,26 +937,27 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       const uint32_t ls = meta & 0xFFFFu, lc = meta >> 16;
       float* __restrict__ ov = cval + tb + (int64_t)cc * kChunk;
       uint32_t* __restrict__ oi = cidx + tb + (int64_t)cc * kChunk;
-      for (uint32_t j = lane; j < cnt; j += 64) {
-        uint32_t vb, ix;
-        if (j < lc) {
-          const uint2 pr = sm.u.pairs[ls + j];
-          vb = pr.x;
-          ix = pr.y;
-          ov[j] = __uint_as_float(vb);
-          oi[j] = ix;
-        } else {  // spilled during the stream
-          vb = __float_as_uint(ov[j]);
-          ix = oi[j];
-        }
+      auto to_side = [&](uint32_t vb, uint32_t ix) {
         const uint32_t key = MODE == kData ? (vb & 0x7fffffffu) : (rank_hash(seed, ix) >> 1);
         if (key < bk.s_hi) {  // every candidate has key >= s_lo
           const uint32_t p = atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
           if (p < side_cap) sd[p] = key;
         }
+      };
+      // Store-only loop: no global load may follow the stores inside it (vmcnt
+      // counts stores too, so a load's wait would wait for every store before it).
+      for (uint32_t j = lane; j < lc; j += 64) {
+        const uint2 pr = sm.u.pairs[ls + j];
+        ov[j] = __uint_as_float(pr.x);
+        oi[j] = pr.y;
+        to_side(pr.x, pr.y);
+      }
+      if (cnt > lc) {  // wave-uniform, rare: pairs spilled to global during the stream
+        for (uint32_t j = lc + lane; j < cnt; j += 64) to_side(__float_as_uint(ov[j]), oi[j]);
       }
     }
   }
+  WSTAMP(32000 + b * 8 + 4 + (w >> 2), w & 3);
   STAMP(1024 + b, 3);
 }
 

@@ -83,6 +83,17 @@ def main():
     print(f"  per-wg prologue min {pro.min():.2f} med {np.median(pro):.2f} max {pro.max():.2f} us;"
           f" stream min {dur.min():.2f} med {np.median(dur):.2f} max {dur.max():.2f} us;"
           f" end-of-tile min {tail.min():.2f} med {np.median(tail):.2f} max {tail.max():.2f} us")
+    ws = t[32000:32000 + 8 * len(k2)].reshape(len(k2), 8, 4)
+    se, be = ws[:, :4].reshape(len(k2), 16), ws[:, 4:].reshape(len(k2), 16)
+    if (se > 0).all():
+        spread = (se.max(1) - se.min(1)) * TICK_US
+        first_be = (be.min(1) - se.max(1)) * TICK_US
+        burst = (be.max(1) - be.min(1)) * TICK_US
+        print(f"  per-wave stream end spread (last - first wave) min {spread.min():.2f} med {np.median(spread):.2f}"
+              f" max {spread.max():.2f} us")
+        print(f"  last wave's stream end -> first wave's burst end: med {np.median(first_be):.2f} max {first_be.max():.2f};"
+              f" burst end spread med {np.median(burst):.2f} max {burst.max():.2f} us")
+        row("  last wave stream end", se.max(1)); row("  last wave burst end", be.max(1))
     k4 = t[24576:24576 + 1000]
     k4 = k4[k4[:, 0] > 0]
     print(f"K34 select + emit ({len(k4)} workgroups)")
