@@ -89,6 +89,25 @@ __device__ unsigned long long g_stamps[kStampSlots][4];
   } while (0)
 #endif
 
+// Diagnostic knobs: cache policy of the stream kernel's candidate/side stores
+// and of the finish kernel's output stores (0 plain, 1 nt, 2 sc1 write-through).
+#ifndef CHOCO_K2_STORE
+#define CHOCO_K2_STORE 0
+#endif
+#ifndef CHOCO_K34_STORE
+#define CHOCO_K34_STORE 0
+#endif
+template <int POL, class T>
+CHOCO_DEV void st_pol(T* p, T v) {
+  if constexpr (POL == 1) {
+    __builtin_nontemporal_store(v, p);
+  } else if constexpr (POL == 2) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *p = v;
+  }
+}
+
 enum SrcMode { kData = 0, kHash = 1 };
 enum TileMode { kTakeNone = 0, kTakeAll = 1, kTakePartial = 2 };
 
@@ -941,15 +960,15 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
         const uint32_t key = MODE == kData ? (vb & 0x7fffffffu) : (rank_hash(seed, ix) >> 1);
         if (key < bk.s_hi) {  // every candidate has key >= s_lo
           const uint32_t p = atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
-          if (p < side_cap) sd[p] = key;
+          if (p < side_cap) st_pol<CHOCO_K2_STORE>(&sd[p], key);
         }
       };
       // Store-only loop: no global load may follow the stores inside it (vmcnt
       // counts stores too, so a load's wait would wait for every store before it).
       for (uint32_t j = lane; j < lc; j += 64) {
         const uint2 pr = sm.u.pairs[ls + j];
-        ov[j] = __uint_as_float(pr.x);
-        oi[j] = pr.y;
+        st_pol<CHOCO_K2_STORE>(&ov[j], __uint_as_float(pr.x));
+        st_pol<CHOCO_K2_STORE>(&oi[j], pr.y);
         to_side(pr.x, pr.y);
       }
       if (cnt > lc) {  // wave-uniform, rare: pairs spilled to global during the stream
@@ -1276,8 +1295,8 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
 #pragma unroll
       for (int i = 0; i < kEmitR; ++i) {
         if (sel[i]) {
-          out_val[pos] = v[i] * scale;
-          out_idx[pos] = (int32_t)((int64_t)idx[i] + idx_base);
+          st_pol<CHOCO_K34_STORE>(&out_val[pos], v[i] * scale);
+          st_pol<CHOCO_K34_STORE>(&out_idx[pos], (int32_t)((int64_t)idx[i] + idx_base));
           ++pos;
         }
       }

@@ -12,6 +12,8 @@ for wl in topk qsgd sign; do
     > $O/pmc_w_$wl.log 2>&1 || exit $?
 done
 python tools/pmc_traffic.py $O/pmc_f_topk $O/pmc_w_topk topk_stream_kernel topk:100000000 && \
+python tools/pmc_traffic.py $O/pmc_f_topk $O/pmc_w_topk topk_finish_kernel topk_finish:100000000 && \
+python tools/pmc_traffic.py $O/pmc_f_topk $O/pmc_w_topk sparse_acc_kernel sparse_acc:1000000 && \
 python tools/pmc_traffic.py $O/pmc_f_qsgd $O/pmc_w_qsgd qsgd_quant_kernel qsgd:100000000 && \
 python tools/pmc_traffic.py $O/pmc_f_sign $O/pmc_w_sign sign_pack_kernel sign:345000000 && \
 cp profiles/pmc_traffic.json $O/ || exit 1

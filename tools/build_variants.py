@@ -12,6 +12,10 @@ VARIANTS = {
     "acc_nt": ["CHOCO_ACC_STORE=1"],
     "acc_sc1": ["CHOCO_ACC_STORE=2"],
     "stream_nt": ["CHOCO_STREAM_NT=1"],
+    "k2st_nt": ["CHOCO_K2_STORE=1"],
+    "k2st_sc1": ["CHOCO_K2_STORE=2"],
+    "st_nt": ["CHOCO_K2_STORE=1", "CHOCO_K34_STORE=1", "CHOCO_ACC_STORE=1"],
+    "st_sc1": ["CHOCO_K2_STORE=2", "CHOCO_K34_STORE=2", "CHOCO_ACC_STORE=2"],
 }
 
 
