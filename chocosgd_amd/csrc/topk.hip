@@ -53,9 +53,13 @@ constexpr int kK2Unroll = 8;            // float4 rows per wave per load batch (
 constexpr int64_t kK2Target = CHOCO_K2_TARGET;
 constexpr int64_t kTileQuant = (int64_t)kK2Waves * kK2Unroll * 256;   // 32768 elements
 static_assert(kK2Target <= 1024, "K34 keeps one tile per thread");
-constexpr int64_t kChunk = 4096;        // elements a wave claims at a time (LDS counter)
+// Elements a wave claims at a time (LDS counter): one load batch (2048) or two.
+#ifndef CHOCO_K2_CHUNK
+#define CHOCO_K2_CHUNK 2048
+#endif
+constexpr int64_t kChunk = CHOCO_K2_CHUNK;
 static_assert(kTileQuant % kChunk == 0 && kChunk % (256 * kK2Unroll) == 0, "chunk geometry");
-static_assert((int64_t(1) << 31) / kK2Target / kChunk <= 2 * 1024, "K4 scans <= 2 chunk counts per thread");
+static_assert(kChunk == 256 * kK2Unroll || kChunk == 512 * kK2Unroll, "a chunk is one or two load batches");
 constexpr int kMaybeCap = 65536;        // side-list capacity per tile (maybe keys)
 constexpr int kNBucket = 256;           // 255 "maybe" buckets + 1 "sure"
 constexpr int kNMaybe = kNBucket - 1;
@@ -450,9 +454,9 @@ CHOCO_DEV void block_find_two(const uint32_t* hist, uint32_t r0, uint32_t r1, ui
 // ----------------------------------------------------------------------------
 constexpr int kEnt = 128;  // entry ring per wave (flush at 64: <= 63 + 64 pending)
 constexpr int kPairsPerWave = 640;  // LDS pair region per wave (~2x the k = 1 % share)
-constexpr int kMaxTileChunks = 2048;  // tile <= 2^31 / 256 elements
-static_assert((int64_t(1) << 31) / kK2Target / kChunk <= kMaxTileChunks, "chunk table");
-static_assert(kMaxTileChunks <= 2 * kK4Threads, "two chunk counts per thread");
+constexpr int kMaxTileChunks = (int)((int64_t(1) << 31) / kK2Target / kChunk);  // tile <= 2^31 / 256 elements
+constexpr int kCPT = kMaxTileChunks / kK4Threads;  // chunk counts per K34 thread
+static_assert(kCPT * kK4Threads == kMaxTileChunks, "chunk table");
 
 constexpr int kListPerWave = 256;  // sample keys >= F kept per wave (prologue)
 struct SampleHist {
@@ -826,7 +830,8 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   const int w = tid >> 6;
   const int64_t b = blockIdx.x;
   constexpr int64_t kStep = 256 * kK2Unroll;
-  static_assert(kChunk == 2 * kStep, "a chunk is two load batches (A, B)");
+  constexpr bool kOneBatch = kChunk == kStep;  // a chunk is one load batch (else: two, A and B)
+  constexpr bool kTwoChunks = kOneBatch && MODE == kData && !XH;  // A and B hold the next two chunks
   const uint32_t nchunk = tile / (uint32_t)kChunk;
   Src<MODE, XH> src{x, xh, seed};
   // tile-relative byte offset of a full chunk's first / second batch, or kNoChunk
@@ -838,20 +843,22 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   };
   auto batch1 = [&](uint32_t c) -> uint32_t { return batch0(c) + (uint32_t)kStep * 4u; };
 
-  // ---- prologue: the wave's first chunk is chunk w; both of its batches go out
-  // at once, then the bounds K1 left in the control block are read
+  // ---- prologue: the wave's first chunk is chunk w (and with one-batch chunks
+  // its second is w + 16); both batches go out at once, then the bounds K1 left
+  // in the control block are read
   uint32_t c = (uint32_t)w;
   float4 A[kK2Unroll], B[kK2Unroll];
   Buckets bk;
   if constexpr (MODE == kData) {
     load_rows_full<XH>(ts, batch0(c), lane, A);
-    if (!XH) load_rows_full<XH>(ts, batch1(c), lane, B);
+    if (kTwoChunks) load_rows_full<XH>(ts, batch0(c + kK2Waves), lane, B);
+    else if (!kOneBatch && !XH) load_rows_full<XH>(ts, batch1(c), lane, B);
     bk = make_buckets_from(ctrl->s_lo, ctrl->s_hi, ctrl->shift, seed);
   } else {
     bk = make_buckets(hs_lo, hs_hi, seed);
   }
   if (tid < kNBucket) sm.hist[tid] = 0;
-  if (tid == 0) sm.next_chunk = kK2Waves;
+  if (tid == 0) sm.next_chunk = kTwoChunks ? 2 * kK2Waves : kK2Waves;
   __syncthreads();
   bk.n = n;
   if (MODE == kHash && b == 0 && tid == 0) {
@@ -867,6 +874,68 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   // when c is a full chunk.
   const int64_t tb = b * (int64_t)tile;
   WaveAcc a{};
+  // One chunk whose batch (one-batch chunks) is in R, or that loads itself
+  // (hash mode, the partial chunk); ends with the chunk's bookkeeping.
+  auto run_chunk = [&](uint32_t cc, const float4 (&R)[kK2Unroll]) {
+    const int64_t cbeg = tb + (int64_t)cc * kChunk;
+    const int64_t cend = min(cbeg + kChunk, n);
+    float* __restrict__ ov = cval + cbeg;
+    uint32_t* __restrict__ oi = cidx + cbeg;
+    a.estaged = a.eflushed = a.staged = a.lcnt = 0u;
+    a.lstart = a.lfill;
+    if (cbeg + kChunk <= n) {
+      if constexpr (MODE == kData) process_batch<XH>(src, R, cbeg, cend, sm, w, lane, a, ov, oi, bk);
+      else process_rows_hash<MODE, XH>(src, cbeg, cend, sm, w, lane, a, ov, oi, bk);
+    } else {
+      // the buffer's last, partial chunk (or an empty one past n): guarded rows
+      for (int64_t base = cbeg; base < cend; base += 256) {
+        const int64_t i = base + 4 * lane;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (MODE == kData) {
+          float tt[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) tt[q] = (i + q < cend) ? src.val(i + q) : 0.f;
+          v = make_float4(tt[0], tt[1], tt[2], tt[3]);
+        }
+        process_row<MODE, XH, true>(src, v, i, cend, sm, w, lane, a, ov, oi, bk);
+      }
+    }
+    // the chunk's remaining entries (< 64)
+    const uint32_t rest = a.estaged - a.eflushed;
+    if (rest) flush_entries<MODE, XH>(src, sm, w, lane, a, rest, ov, oi, bk);
+    if (lane == 0) {
+      cntw[(int64_t)b * nchunk + cc] = a.staged;
+      sm.ccnt[cc] = a.staged;
+      sm.cmeta[cc] = (w * kPairsPerWave + a.lstart) | (a.lcnt << 16);
+    }
+  };
+  if constexpr (kTwoChunks) {
+    // A and B hold the wave's next two chunks; a buffer is refilled with the
+    // next claimed chunk as soon as it has been processed.  Claims are
+    // increasing per wave (cA < cB at the loop top), so the first chunk past
+    // the tile ends the wave's stream.
+    uint32_t cA = c, cB = c + kK2Waves;
+    for (;;) {
+      if (cA >= nchunk) break;
+      const uint32_t nA = claim_chunk(sm, lane);
+      run_chunk(cA, A);
+      if constexpr (MODE == kData) load_rows_full<XH>(ts, batch0(nA), lane, A);
+      cA = nA;
+      if (cB >= nchunk) break;
+      const uint32_t nB = claim_chunk(sm, lane);
+      run_chunk(cB, B);
+      if constexpr (MODE == kData) load_rows_full<XH>(ts, batch0(nB), lane, B);
+      cB = nB;
+    }
+  } else if constexpr (kOneBatch) {
+    // one buffer (two input streams: x - xh is formed at load time; hash mode: no loads)
+    while (c < nchunk) {
+      const uint32_t nn = claim_chunk(sm, lane);
+      run_chunk(c, A);
+      if constexpr (MODE == kData) load_rows_full<XH>(ts, batch0(nn), lane, A);
+      c = nn;
+    }
+  } else {
   uint32_t nx = claim_chunk(sm, lane);
   while (c < nchunk) {
     const uint32_t nn = claim_chunk(sm, lane);  // used after this chunk
@@ -900,10 +969,10 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
         const int64_t i = base + 4 * lane;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (MODE == kData) {
-          float t[4];
+          float tt[4];
 #pragma unroll
-          for (int cc = 0; cc < 4; ++cc) t[cc] = (i + cc < cend) ? src.val(i + cc) : 0.f;
-          v = make_float4(t[0], t[1], t[2], t[3]);
+          for (int q = 0; q < 4; ++q) tt[q] = (i + q < cend) ? src.val(i + q) : 0.f;
+          v = make_float4(tt[0], tt[1], tt[2], tt[3]);
         }
         process_row<MODE, XH, true>(src, v, i, cend, sm, w, lane, a, ov, oi, bk);
       }
@@ -919,6 +988,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     }
     c = nx;
     nx = nn;
+  }
   }
   if (lane == 0) sm.cnt[w] = a.cand;  // wave-uniform
   STAMP(1024 + b, 2);
@@ -951,8 +1021,12 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   __syncthreads();
   {
     uint32_t* __restrict__ sd = side + b * side_cap;
-    for (uint32_t cc = (uint32_t)w; cc < nchunk; cc += kK2Waves) {
-      const uint32_t meta = sm.cmeta[cc], cnt = sm.ccnt[cc];
+    // a half wave per chunk (a chunk holds ~20-40 candidates at k = 1 %)
+    const uint32_t h = (uint32_t)lane & 31u;
+    for (uint32_t c0 = 2u * w; c0 < nchunk; c0 += 2u * kK2Waves) {
+      const uint32_t cc = c0 + ((uint32_t)lane >> 5);
+      const bool have = cc < nchunk;
+      const uint32_t meta = have ? sm.cmeta[cc] : 0u, cnt = have ? sm.ccnt[cc] : 0u;
       const uint32_t ls = meta & 0xFFFFu, lc = meta >> 16;
       float* __restrict__ ov = cval + tb + (int64_t)cc * kChunk;
       uint32_t* __restrict__ oi = cidx + tb + (int64_t)cc * kChunk;
@@ -965,15 +1039,14 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       };
       // Store-only loop: no global load may follow the stores inside it (vmcnt
       // counts stores too, so a load's wait would wait for every store before it).
-      for (uint32_t j = lane; j < lc; j += 64) {
+      for (uint32_t j = h; j < lc; j += 32) {
         const uint2 pr = sm.u.pairs[ls + j];
         st_pol<CHOCO_K2_STORE>(&ov[j], __uint_as_float(pr.x));
         st_pol<CHOCO_K2_STORE>(&oi[j], pr.y);
         to_side(pr.x, pr.y);
       }
-      if (cnt > lc) {  // wave-uniform, rare: pairs spilled to global during the stream
-        for (uint32_t j = lc + lane; j < cnt; j += 64) to_side(__float_as_uint(ov[j]), oi[j]);
-      }
+      // rare: pairs spilled to global during the stream (skipped when no lane has any)
+      for (uint32_t j = lc + h; j < cnt; j += 32) to_side(__float_as_uint(ov[j]), oi[j]);
     }
   }
   WSTAMP(32000 + b * 8 + 4 + (w >> 2), w & 3);
@@ -1015,15 +1088,22 @@ CHOCO_DEV void wave_find_bin(const uint32_t* hist, uint32_t rank, uint32_t* out)
   }
 }
 
-// Run starts of a tile's per-chunk candidate runs: counts (2 per thread) ->
+// Run starts of a tile's per-chunk candidate runs: counts (kCPT per thread) ->
 // exclusive starts, starts[nchunk] = total.  Every thread of the kK4Threads
 // workgroup calls it; ends with a barrier.
-CHOCO_DEV uint32_t chunk_run_starts(uint32_t c0, uint32_t c1, uint32_t nchunk, uint32_t* starts, uint32_t* scratch) {
-  const uint32_t j0 = 2 * threadIdx.x, j1 = j0 + 1;
+CHOCO_DEV uint32_t chunk_run_starts(const uint32_t (&cw)[kCPT], uint32_t nchunk, uint32_t* starts,
+                                    uint32_t* scratch) {
+  const uint32_t j0 = kCPT * threadIdx.x;
+  uint32_t s = 0;
+#pragma unroll
+  for (int q = 0; q < kCPT; ++q) s += cw[q];
   uint32_t tot;
-  const uint32_t pre = block_excl_scan(c0 + c1, scratch, &tot);
-  if (j0 < nchunk) starts[j0] = pre;
-  if (j1 < nchunk) starts[j1] = pre + c0;
+  uint32_t pre = block_excl_scan(s, scratch, &tot);
+#pragma unroll
+  for (int q = 0; q < kCPT; ++q) {
+    if (j0 + q < nchunk) starts[j0 + q] = pre;
+    pre += cw[q];
+  }
   if (threadIdx.x == 0) starts[nchunk] = tot;
   __syncthreads();
   return tot;
@@ -1106,9 +1186,12 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   // every tile's j*-independent "sure" count, this tile's chunk counts
   const uint32_t ku = (uint32_t)k;
   const uint32_t nchunk = tile / (uint32_t)kChunk;
-  const uint32_t j0 = 2 * tid, j1 = j0 + 1;
-  const uint32_t cw0 = j0 < nchunk ? cntw[b * nchunk + j0] : 0u;
-  const uint32_t cw1 = j1 < nchunk ? cntw[b * nchunk + j1] : 0u;
+  uint32_t cw[kCPT];
+#pragma unroll
+  for (int q = 0; q < kCPT; ++q) {
+    const uint32_t j = kCPT * tid + q;
+    cw[q] = j < nchunk ? cntw[b * nchunk + j] : 0u;
+  }
   uint32_t cword = 0;
   if (tid < 4) cword = __hip_atomic_load(&ctrl->s_lo + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool mine_tile = tid < (int)nb;
@@ -1120,7 +1203,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     for (int r = 0; r < kNRep; ++r) g[r] = ctrl->G[r][tid];
   }
   if (tid < 4) fs.bc[tid] = cword;  // s_lo, s_hi, shift, overflow
-  const uint32_t tot = chunk_run_starts(cw0, cw1, nchunk, fs.run_start, fs.scratch);
+  const uint32_t tot = chunk_run_starts(cw, nchunk, fs.run_start, fs.scratch);
   const uint32_t s_lo = fs.bc[0], shift = fs.bc[2], overflow = fs.bc[3];
   STAMP(26000 + b, 0);
   // ---- the addresses of the tile's first emission batch (it does not depend on T)

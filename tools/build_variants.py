@@ -12,6 +12,8 @@ VARIANTS = {
     "acc_nt": ["CHOCO_ACC_STORE=1"],
     "acc_sc1": ["CHOCO_ACC_STORE=2"],
     "stream_nt": ["CHOCO_STREAM_NT=1"],
+    "chunk4k": ["CHOCO_K2_CHUNK=4096"],
+    "stamps4k": ["CHOCO_STAMPS=1", "CHOCO_K2_CHUNK=4096"],
     "k2st_nt": ["CHOCO_K2_STORE=1"],
     "k2st_sc1": ["CHOCO_K2_STORE=2"],
     "st_nt": ["CHOCO_K2_STORE=1", "CHOCO_K34_STORE=1", "CHOCO_ACC_STORE=1"],
