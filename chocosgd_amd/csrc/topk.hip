@@ -454,6 +454,7 @@ CHOCO_DEV void block_find_two(const uint32_t* hist, uint32_t r0, uint32_t r1, ui
 // ----------------------------------------------------------------------------
 constexpr int kEnt = 128;  // entry ring per wave (flush at 64: <= 63 + 64 pending)
 constexpr int kPairsPerWave = 640;  // LDS pair region per wave (~2x the k = 1 % share)
+constexpr int kSideLds = kK2Waves * kEnt * 4;  // maybe keys sorted in LDS at tile end (in the dead entry ring)
 constexpr int kMaxTileChunks = (int)((int64_t(1) << 31) / kK2Target / kChunk);  // tile <= 2^31 / 256 elements
 constexpr int kCPT = kMaxTileChunks / kK4Threads;  // chunk counts per K34 thread
 static_assert(kCPT * kK4Threads == kMaxTileChunks, "chunk table");
@@ -474,12 +475,13 @@ struct StreamSmem {
     uint2 pairs[kK2Waves * kPairsPerWave];  // (value bits, index) per candidate, per-wave regions
   } u;
   uint32_t cmeta[kMaxTileChunks];  // per chunk: LDS start | LDS count << 16
-  uint32_t ccnt[kMaxTileChunks];   // per chunk: candidates
+  uint32_t ccnt[kMaxTileChunks + 1];  // per chunk: candidates; at tile end their exclusive prefix
   uint32_t hist[kNBucket];        // maybe-key bucket counts, then counting-sort cursors
   uint32_t cnt[kK2Waves];
-  uint32_t scratch[24];
+  uint32_t scratch[40];
   uint32_t bc[8];
   uint32_t next_chunk;            // the tile's chunk counter (waves claim chunks)
+  uint32_t spill;                 // some wave spilled pairs to global (tile end)
 };
 
 // Unconditional float4 loads of kK2Unroll rows (no branch around a load: the
@@ -858,7 +860,10 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     bk = make_buckets(hs_lo, hs_hi, seed);
   }
   if (tid < kNBucket) sm.hist[tid] = 0;
-  if (tid == 0) sm.next_chunk = kTwoChunks ? 2 * kK2Waves : kK2Waves;
+  if (tid == 0) {
+    sm.next_chunk = kTwoChunks ? 2 * kK2Waves : kK2Waves;
+    sm.spill = 0;
+  }
   __syncthreads();
   bk.n = n;
   if (MODE == kHash && b == 0 && tid == 0) {
@@ -904,7 +909,6 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     const uint32_t rest = a.estaged - a.eflushed;
     if (rest) flush_entries<MODE, XH>(src, sm, w, lane, a, rest, ov, oi, bk);
     if (lane == 0) {
-      cntw[(int64_t)b * nchunk + cc] = a.staged;
       sm.ccnt[cc] = a.staged;
       sm.cmeta[cc] = (w * kPairsPerWave + a.lstart) | (a.lcnt << 16);
     }
@@ -982,7 +986,6 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     const uint32_t rest = a.estaged - a.eflushed;
     if (rest) flush_entries<MODE, XH>(src, sm, w, lane, a, rest, ov, oi, bk);
     if (lane == 0) {
-      cntw[(int64_t)b * nchunk + c] = a.staged;
       sm.ccnt[c] = a.staged;
       sm.cmeta[c] = (w * kPairsPerWave + a.lstart) | (a.lcnt << 16);
     }
@@ -995,19 +998,41 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   WSTAMP(32000 + b * 8 + (w >> 2), w & 3);
   __syncthreads();
 
-  // ---- end of tile: bucket suffix counts; then every chunk's LDS pairs leave to
-  // its global slots and the maybe keys are counting-sorted into the side list
+  // ---- end of tile: bucket suffix counts and the chunks' candidate prefix;
+  // then the LDS pairs leave in one burst and the maybe keys are counting-sorted
+  // into the side list.  When no wave spilled (the usual case) the tile's
+  // candidates are written COMPACTLY, chunk after chunk from the tile start
+  // (full lines; cntw then says "one run": [total, 0, 0, ...]), and the sorted
+  // side list is staged in LDS and copied out coalesced.  Scattered partial-line
+  // stores while other CUs still stream cost ~0.5 us per MB (HBM turnaround).
+  uint32_t hsum, csum;
+  bool spilled;
   {
     // thread t <-> maybe bucket jb = 254 - t (t = 255: the "sure" bucket 255);
-    // cum[j] = #candidates with bucket >= j, sure included
+    // cum[j] = #candidates with bucket >= j, sure included.  And thread t <->
+    // chunks kCPT*t .. +kCPT-1 for the chunk prefix.
     const int t = tid;
     const int jb = t < kNMaybe ? kNMaybe - 1 - t : kNMaybe;
     const uint32_t hv = t < kNMaybe ? sm.hist[jb] : 0u;
-    uint32_t hsum;
-    const uint32_t above = block_excl_scan(hv, sm.scratch, &hsum);  // maybe keys in buckets > jb
-    uint32_t csum = 0;
+    uint32_t cc4[kCPT], cs = 0;
+    bool sp = false;
 #pragma unroll
-    for (int ww = 0; ww < kK2Waves; ++ww) csum += sm.cnt[ww];
+    for (int q = 0; q < kCPT; ++q) {
+      const uint32_t j = kCPT * (uint32_t)t + q;
+      cc4[q] = j < nchunk ? sm.ccnt[j] : 0u;
+      if (j < nchunk) sp |= cc4[q] != (sm.cmeta[j] >> 16);
+      cs += cc4[q];
+    }
+    if (ballot(sp) != 0ull && lane == 0) atomicOr(&sm.spill, 1u);  // (__syncthreads_or waits on vmcnt(0))
+    uint32_t above, cpre;
+    block_excl_scan2(hv, cs, sm.scratch, &above, &cpre, &hsum, &csum);  // maybe keys in buckets > jb
+#pragma unroll
+    for (int q = 0; q < kCPT; ++q) {
+      const uint32_t j = kCPT * (uint32_t)t + q;
+      if (j < nchunk) sm.ccnt[j] = cpre;
+      cpre += cc4[q];
+    }
+    if (t == 0) sm.ccnt[nchunk] = csum;
     const uint32_t sure = csum - hsum;
     if (t == 0 && hsum > side_cap) atomicOr(&ctrl->overflow, 1u);
     if (t < kNBucket) {
@@ -1016,37 +1041,55 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       atomicAdd(&ctrl->G[b & (kNRep - 1)][jb], cum);
       if (t < kNMaybe) sm.hist[jb] = above;  // counting-sort cursor of bucket jb (hist is dead now)
     }
+    STAMP(22000 + b, 0);
+    __syncthreads();
+    spilled = sm.spill != 0;
   }
-  STAMP(22000 + b, 0);
-  __syncthreads();
   {
     uint32_t* __restrict__ sd = side + b * side_cap;
-    // a half wave per chunk (a chunk holds ~20-40 candidates at k = 1 %)
+    uint32_t* __restrict__ skeys = reinterpret_cast<uint32_t*>(&sm.ent_v[0][0]);  // the ring is dead now
+    const bool sort_lds = hsum <= (uint32_t)kSideLds;
+    // a half wave per chunk (a chunk holds ~20 candidates at k = 1 %)
     const uint32_t h = (uint32_t)lane & 31u;
     for (uint32_t c0 = 2u * w; c0 < nchunk; c0 += 2u * kK2Waves) {
       const uint32_t cc = c0 + ((uint32_t)lane >> 5);
       const bool have = cc < nchunk;
-      const uint32_t meta = have ? sm.cmeta[cc] : 0u, cnt = have ? sm.ccnt[cc] : 0u;
+      const uint32_t meta = have ? sm.cmeta[cc] : 0u;
+      const uint32_t cp = have ? sm.ccnt[cc] : 0u, cnt = have ? sm.ccnt[cc + 1] - cp : 0u;
       const uint32_t ls = meta & 0xFFFFu, lc = meta >> 16;
-      float* __restrict__ ov = cval + tb + (int64_t)cc * kChunk;
-      uint32_t* __restrict__ oi = cidx + tb + (int64_t)cc * kChunk;
+      const int64_t o = tb + (spilled ? (int64_t)cc * kChunk : (int64_t)cp);
+      float* __restrict__ ov = cval + o;
+      uint32_t* __restrict__ oi = cidx + o;
       auto to_side = [&](uint32_t vb, uint32_t ix) {
         const uint32_t key = MODE == kData ? (vb & 0x7fffffffu) : (rank_hash(seed, ix) >> 1);
         if (key < bk.s_hi) {  // every candidate has key >= s_lo
           const uint32_t p = atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
-          if (p < side_cap) st_pol<CHOCO_K2_STORE>(&sd[p], key);
+          if (sort_lds) skeys[p] = key;
+          else if (p < side_cap) st_pol<CHOCO_K2_STORE>(&sd[p], key);
         }
       };
       // Store-only loop: no global load may follow the stores inside it (vmcnt
       // counts stores too, so a load's wait would wait for every store before it).
+#ifdef CHOCO_DIAG_NOBURST  // diagnostic only: no pair stores / no side list (wrong results)
+      if (CHOCO_DIAG_NOBURST == 1) continue;
+#endif
       for (uint32_t j = h; j < lc; j += 32) {
         const uint2 pr = sm.u.pairs[ls + j];
+#ifdef CHOCO_DIAG_NOBURST
+        if (CHOCO_DIAG_NOBURST == 2) { to_side(pr.x, pr.y); continue; }
+#endif
         st_pol<CHOCO_K2_STORE>(&ov[j], __uint_as_float(pr.x));
         st_pol<CHOCO_K2_STORE>(&oi[j], pr.y);
         to_side(pr.x, pr.y);
       }
-      // rare: pairs spilled to global during the stream (skipped when no lane has any)
+      if (have && h == 0) cntw[(int64_t)b * nchunk + cc] = spilled ? cnt : (cc == 0 ? csum : 0u);
+      // rare (a wave's LDS region overflowed): this tile keeps per-chunk slot
+      // ranges; the pairs spilled during the stream are only binned here
       for (uint32_t j = lc + h; j < cnt; j += 32) to_side(__float_as_uint(ov[j]), oi[j]);
+    }
+    if (sort_lds) {
+      __syncthreads();
+      for (uint32_t i = (uint32_t)tid; i < hsum; i += kK2Threads) sd[i] = skeys[i];
     }
   }
   WSTAMP(32000 + b * 8 + 4 + (w >> 2), w & 3);

@@ -14,6 +14,9 @@ VARIANTS = {
     "stream_nt": ["CHOCO_STREAM_NT=1"],
     "chunk4k": ["CHOCO_K2_CHUNK=4096"],
     "stamps4k": ["CHOCO_STAMPS=1", "CHOCO_K2_CHUNK=4096"],
+    "nob1": ["CHOCO_STAMPS=1", "CHOCO_DIAG_NOBURST=1"],
+    "nob2": ["CHOCO_STAMPS=1", "CHOCO_DIAG_NOBURST=2"],
+    "nob3": ["CHOCO_STAMPS=1", "CHOCO_DIAG_NOBURST=3"],
     "k2st_nt": ["CHOCO_K2_STORE=1"],
     "k2st_sc1": ["CHOCO_K2_STORE=2"],
     "st_nt": ["CHOCO_K2_STORE=1", "CHOCO_K34_STORE=1", "CHOCO_ACC_STORE=1"],
