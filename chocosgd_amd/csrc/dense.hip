@@ -52,6 +52,11 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_kernel(const float* __r
 #elif CHOCO_ACC_STORE == 1
     if (hat) __builtin_nontemporal_store(hat[j] + v, &hat[j]);
     __builtin_nontemporal_store(mem[j] + wv, &mem[j]);
+#elif CHOCO_ACC_STORE == 3
+    // the read-modify-write done in L2 (no-return fp32 atomics): the wave never
+    // waits for the old value (indices are distinct, so no two adds meet)
+    if (hat) unsafeAtomicAdd(&hat[j], v);
+    unsafeAtomicAdd(&mem[j], wv);
 #else
     if (hat) __hip_atomic_store(&hat[j], hat[j] + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&mem[j], mem[j] + wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

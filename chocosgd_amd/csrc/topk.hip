@@ -98,6 +98,9 @@ __device__ unsigned long long g_stamps[kStampSlots][4];
 #ifndef CHOCO_K2_STORE
 #define CHOCO_K2_STORE 0
 #endif
+#ifndef CHOCO_K34_PREFETCH
+#define CHOCO_K34_PREFETCH 1
+#endif
 #ifndef CHOCO_K34_STORE
 #define CHOCO_K34_STORE 0
 #endif
@@ -117,7 +120,7 @@ enum TileMode { kTakeNone = 0, kTakeAll = 1, kTakePartial = 2 };
 
 struct TopkCtrl {
   uint32_t s_lo, s_hi, shift, overflow;          // K2 -> K34
-  uint32_t fin_ticket;                           // K34's self-resetting ticket
+  uint32_t reserved;
   uint32_t pad[11];
   uint32_t G[kNRep][kNBucket];                   // replicated bucket suffix totals
 };
@@ -321,8 +324,11 @@ __global__ __launch_bounds__(kExactThreads) void topk_segmented_kernel(
 // without a grid-wide hand-off.  Both bounds are heuristics that K34 verifies
 // (G[0] >= k, G[sure] < k); any k/n works.
 // ----------------------------------------------------------------------------
-constexpr int kSampleRuns = 64;
-constexpr int kSampleN = kSampleRuns * 256;                  // 16384
+#ifndef CHOCO_SAMPLE_RUNS
+#define CHOCO_SAMPLE_RUNS 64
+#endif
+constexpr int kSampleRuns = CHOCO_SAMPLE_RUNS;  // runs of 256 contiguous elements
+constexpr int kSampleN = kSampleRuns * 256;                  // 16384 at 64 runs
 constexpr int kK1Threads = 1024;                              // the bounds kernel: one workgroup
 constexpr int kSampleLoads = kSampleRuns * 64 / kK1Threads;  // float4 per thread (4)
 static_assert(kSampleLoads * kK1Threads == kSampleRuns * 64, "sample geometry");
@@ -795,6 +801,9 @@ __global__ __launch_bounds__(kK1Threads) void topk_bounds_kernel(const float* __
   __shared__ BoundsSmem sm;
   STAMP(30000, 0);
   const int lane = lane_id(), w = threadIdx.x >> 6;
+  // this call's bucket totals and overflow flag start from zero (K2 adds to them)
+  for (int i = threadIdx.x; i < kNRep * kNBucket; i += kK1Threads) (&ctrl->G[0][0])[i] = 0u;
+  if (threadIdx.x == 0) ctrl->overflow = 0u;
   float4 s[kSampleLoads], sh[kSampleLoads];
   load_sample<XH>(x, xh, n, s, sh);
   uint32_t kk[kSampleLoads * 4];
@@ -1106,9 +1115,10 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
 // redundant select is a handful of L2-served round trips; it replaces a
 // single-workgroup select kernel and a kernel boundary.
 //
-// The bucket totals are cleared for the next call by the workgroup that draws
-// the last ticket after reading them (fence-free: every workgroup's loads of
-// the totals have returned before it draws).
+// The bucket totals and the overflow flag are zeroed at the START of each call
+// (K1, or a memset in hash mode), so K34 needs no last-workgroup ticket: a
+// returning atomic here was waited for on the spot (~1.8 us on the critical
+// path) because the atomic optimizer consumes its result right away.
 // ----------------------------------------------------------------------------
 // Wave 0 of a workgroup: over a 256-bin LDS histogram (ascending value order),
 // find the bin holding the rank-th largest entry; returns (bin, rank inside bin)
@@ -1155,6 +1165,7 @@ CHOCO_DEV uint32_t chunk_run_starts(const uint32_t (&cw)[kCPT], uint32_t nchunk,
 constexpr int kSelBits = 13;  // radix-select digit: one round for bucket widths <= 2^13
 struct FinSmem {
   uint32_t keys[kMCap];
+  uint32_t kbase[kK4Threads];  // per tile: side-list index of its first bucket-j* key - its first slot
   uint32_t hist[1 << kSelBits];
   uint32_t G[kNBucket];
   uint32_t run_start[kMaxTileChunks + 1];
@@ -1264,11 +1275,6 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   if (tid == 0) fs.bc[4] = 0;
   __syncthreads();
   STAMP(26000 + b, 1);
-  // Every workgroup has read the totals and the overflow flag: draw a ticket
-  // now (its return is only looked at on the way out); the last drawer clears
-  // them for the next call.
-  uint32_t ticket = 0;
-  if (tid == 0) ticket = __hip_atomic_fetch_add(&ctrl->fin_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // G[j] = #candidates in buckets >= j is non-increasing; j* = the unique
   // j <= 254 with G[j] >= k > G[j+1]
   bool fallback = overflow != 0 || fs.G[0] < ku || fs.G[kNMaybe] >= ku;
@@ -1297,38 +1303,50 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     uint32_t M;
     const uint32_t kpos = block_excl_scan(cb, fs.scratch, &M);  // M = G[j*] - G[j*+1]
     STAMP(26000 + b, 3);
+#if CHOCO_STAMPS
+    if (b == 0 && tid == 0) {
+      g_stamps[29000][0] = M; g_stamps[29000][1] = shift; g_stamps[29000][2] = jstar; g_stamps[29000][3] = fs.G[0];
+    }
+#endif
     {
-      // this tile's keys -> LDS slots [kpos, kpos + cb); loads in batches of 32
-      // issued before any LDS store, so each batch costs one round trip (a
-      // tile holds ~M / nb ~ 10-30 keys of bucket j*)
+      // All tiles' bucket-j* keys -> keys[0, M), tile after tile: key slot i
+      // belongs to tile tmap[i] (a slot -> tile map each tile writes for its
+      // own slots; it lives in the select histogram, which is not in use yet),
+      // so consecutive lanes load consecutive side-list words (a tile holds
+      // ~M / nb ~ 20 keys): a few lines per load instead of one per lane.
+      uint16_t* tmap = reinterpret_cast<uint16_t*>(fs.hist);
+      static_assert(sizeof(fs.hist) >= kMCap * sizeof(uint16_t), "tile map fits the histogram");
+      fs.kbase[tid] = (uint32_t)(mine_tile ? tid : 0) * side_cap + off - kpos;  // mod 2^32
+      for (uint32_t j = 0; j < cb; ++j) tmap[kpos + j] = (uint16_t)tid;
+      __syncthreads();
       STAMP(27000 + b, 1);
-      const uint32_t* sd = side + (int64_t)(mine_tile ? tid : 0) * side_cap + off;
-      constexpr int kB = 32;
-      uint32_t kv[kB];
-      if (cb) {
+      constexpr int kG = kMCap / kK4Threads;  // M <= kMCap: at most kG slots per thread
+      uint32_t ka[kG];
 #pragma unroll
-        for (int q = 0; q < kB; ++q) kv[q] = sd[min((uint32_t)q, cb - 1)];
+      for (int q = 0; q < kG; ++q) {
+        const uint32_t i = min((uint32_t)tid + (uint32_t)q * kK4Threads, M - 1u);
+        ka[q] = (uint32_t)q * kK4Threads < M ? fs.kbase[tmap[i]] + i : 0u;  // workgroup-uniform guard
       }
+      STAMP(28000 + b, 0);
+      uint32_t kv[kG];
+#pragma unroll
+      for (int q = 0; q < kG; ++q) kv[q] = (uint32_t)q * kK4Threads < M ? side[ka[q]] : 0u;  // clamped slots
       // The first emission batch's loads go out now, BEHIND the key loads: the
       // vmcnt counter is in order, so waiting for the keys does not wait for
       // them, and they land while T is being selected.
+      if (CHOCO_K34_PREFETCH) {
 #pragma unroll
-      for (int i = 0; i < kEmitR; ++i) {
-        v[i] = cval[addr[i]];
-        idx[i] = cidx[addr[i]];
+        for (int i = 0; i < kEmitR; ++i) {
+          v[i] = cval[addr[i]];
+          idx[i] = cidx[addr[i]];
+        }
       }
-      if (cb) {
+      STAMP(28000 + b, 1);
+      __syncthreads();  // the tile map (= histogram) is dead before the select clears it
 #pragma unroll
-        for (int q = 0; q < kB; ++q)
-          if ((uint32_t)q < cb) fs.keys[kpos + q] = kv[q];
-      }
-      for (uint32_t i0 = kB; i0 < cb; i0 += kB) {
-        uint32_t kv[kB];
-#pragma unroll
-        for (int q = 0; q < kB; ++q) kv[q] = sd[min(i0 + q, cb - 1)];  // clamped: the load is unconditional
-#pragma unroll
-        for (int q = 0; q < kB; ++q)
-          if (i0 + q < cb) fs.keys[kpos + i0 + q] = kv[q];
+      for (int q = 0; q < kG; ++q) {
+        const uint32_t i = (uint32_t)tid + (uint32_t)q * kK4Threads;
+        if (i < M) fs.keys[i] = kv[q];
       }
     }
     // ---- radix select inside bucket j*: rel = key - base_j in [0, 2^shift),
@@ -1347,7 +1365,9 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
         if (sh >= 32 || (rel >> sh) == (prefix >> sh)) atomicAdd(&fs.hist[(rel >> dsh) & dmask], 1u);
       }
       __syncthreads();
+      STAMP(28000 + b, 2);
       block_find_rank8k(fs.hist, krem, fs.scratch, fs.bc + 5);
+      STAMP(28000 + b, 3);
       prefix |= fs.bc[5] << dsh;
       krem = fs.bc[6];
       sh = dsh;
@@ -1358,10 +1378,15 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     const uint32_t r = krem;  // ties at T to take (>= 1)
     // ---- per tile: #keys > T (every key above bucket j* is) and #keys == T
     uint32_t gt = above, eq = 0;
-    for (uint32_t i = 0; i < cb; ++i) {
-      const uint32_t key = fs.keys[kpos + i];
-      gt += key > T;
-      eq += key == T;
+    for (uint32_t i0 = 0; i0 < cb; i0 += 8) {  // 8 independent LDS reads per round trip
+      uint32_t kk[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) kk[q] = fs.keys[kpos + min(i0 + q, cb - 1)];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        gt += (i0 + q < cb && kk[q] > T) ? 1u : 0u;
+        eq += (i0 + q < cb && kk[q] == T) ? 1u : 0u;
+      }
     }
     uint32_t gpre, epre, gtot, etot;
     block_excl_scan2(gt, eq, fs.scratch, &gpre, &epre, &gtot, &etot);
@@ -1381,7 +1406,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     // count places them (two scans only when ties at T are split).
     for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads * kEmitR) {
       const uint32_t pb = p0 + tid * kEmitR;
-      if (p0 != 0) {  // workgroup-uniform: batches after the prefetched first one
+      if (p0 != 0 || !CHOCO_K34_PREFETCH) {  // workgroup-uniform: batches after the prefetched first one
         emit_addresses(fs.run_start, nchunk, tot, pb, tb, addr);
 #pragma unroll
         for (int i = 0; i < kEmitR; ++i) {
@@ -1427,16 +1452,6 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
         }
       }
       out += nsel;
-    }
-  }
-  // ---- the workgroup that drew the last ticket clears the totals for the next call
-  if (tid == 0) fs.bc[7] = ticket;
-  __syncthreads();
-  if (fs.bc[7] == nb - 1u) {
-    for (int i = tid; i < kNRep * kNBucket; i += kK4Threads) (&ctrl->G[0][0])[i] = 0;
-    if (tid == 0) {
-      ctrl->overflow = 0;
-      ctrl->fin_ticket = 0;
     }
   }
   STAMP(24576 + b, 2);
@@ -1486,6 +1501,10 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
     hs_lo = (uint32_t)std::max(0.0, floor(two31 * (1.0 - c_lo / nd)));
     hs_hi = c_hi < 1.0 ? 0x80000000ull : (uint64_t)ceil(two31 * (1.0 - c_hi / nd));
     if (hs_hi <= hs_lo) hs_hi = (uint64_t)hs_lo + 1;
+  }
+  if (MODE == kHash) {
+    // this call's bucket totals and overflow flag start from zero (K1 does it in data mode)
+    CHOCO_REQUIRE(hipMemsetAsync(ctrl, 0, sizeof(TopkCtrl), st) == hipSuccess, "hipMemsetAsync failed");
   }
   if (MODE == kData) {
     CHOCO_KLAUNCH((topk_bounds_kernel<XH>), dim3(1), dim3(kK1Threads), 0, st, x, xh, n, sample_ranks(n, k), ctrl);

@@ -13,6 +13,11 @@ VARIANTS = {
     "acc_sc1": ["CHOCO_ACC_STORE=2"],
     "stream_nt": ["CHOCO_STREAM_NT=1"],
     "chunk4k": ["CHOCO_K2_CHUNK=4096"],
+    "nopf": ["CHOCO_K34_PREFETCH=0"],
+    "acc_atom": ["CHOCO_ACC_STORE=3"],
+    "s32k": ["CHOCO_SAMPLE_RUNS=128"],
+    "s32k_nopf": ["CHOCO_SAMPLE_RUNS=128", "CHOCO_K34_PREFETCH=0"],
+    "stamps_s32k": ["CHOCO_STAMPS=1", "CHOCO_SAMPLE_RUNS=128"],
     "stamps4k": ["CHOCO_STAMPS=1", "CHOCO_K2_CHUNK=4096"],
     "nob1": ["CHOCO_STAMPS=1", "CHOCO_DIAG_NOBURST=1"],
     "nob2": ["CHOCO_STAMPS=1", "CHOCO_DIAG_NOBURST=2"],

@@ -104,7 +104,16 @@ def main():
     q2 = q2[q2[:, 0] > 0]
     row("  run starts", q[:, 0]); row("  totals in LDS", q[:, 1]); row("  j* found", q[:, 2])
     row("  table words + scan", q[:, 3]); row("  (key loads issued)", q2[:, 1])
-    row("  bucket keys stored", q2[:, 2]); row("  T selected", q2[:, 0])
+    m = t[29000]
+    print(f"  bucket j*={m[2]} holds M={m[0]} keys (shift {m[1]}); candidates {m[3]}")
+    q3 = t[28000:28000 + 1000]
+    q3 = q3[q3[:, 0] > 0]
+    if len(q3):
+        row("  (gather addresses ready)", q3[:, 0]); row("  (gather + emit loads issued)", q3[:, 1])
+    row("  bucket keys stored", q2[:, 2])
+    if len(q3):
+        row("  (select histogram built)", q3[:, 2]); row("  (select rank found)", q3[:, 3])
+    row("  T selected", q2[:, 0])
     row("offsets known", k4[:, 1]); row("end", k4[:, 2])
 
 
