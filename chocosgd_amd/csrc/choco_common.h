@@ -99,6 +99,14 @@ CHOCO_DEV float4 ld_buf4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
   return make_float4(f.x, f.y, f.z, f.w);
 }
 
+// ... with a wave-uniform SGPR offset added (buffer_load_dwordx4 v, v_off, s[rsrc], s_off)
+template <bool NT>
+CHOCO_DEV float4 ld_buf4s(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, NT ? 2 : 0);
+  const choco_f32x4 f = __builtin_bit_cast(choco_f32x4, v);
+  return make_float4(f.x, f.y, f.z, f.w);
+}
+
 CHOCO_DEV int lane_id() { return __lane_id(); }
 
 // number of set bits of `mask` strictly below this lane

@@ -251,6 +251,119 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
   }
 }
 
+// One-segment pack (nseg == 1: the whole flat buffer has one norm): the same
+// column tiles, but each lane loads the float4 at its OWN run offset
+// s + 4l -- a dword-aligned (not 16-B aligned) global_load_dwordx4, which
+// gfx950 serves directly -- so there is no tail load and no realigning
+// shuffle.  Rows go in groups of RU with two groups in flight (A/B register
+// double buffer, non-temporal loads), and the L1 norm accumulates per lane in
+// fp64 over all 32 rows, with one wave reduction at the end.
+// Loads go through a raw buffer resource over the whole input (n * 4 < 2^32
+// bytes): the row offset is a wave-uniform SGPR operand and the lane offset
+// one VGPR, so the 2 x RU loads in flight need no 64-bit address registers.
+
+template <bool XH, bool NORM>
+__global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* __restrict__ x,
+                                                                  const float* __restrict__ xh, int64_t n,
+                                                                  int64_t Np, uint32_t* __restrict__ packed,
+                                                                  float* __restrict__ l1_out,
+                                                                  SignWs* __restrict__ ws) {
+  constexpr int RU = XH ? 4 : 8;  // rows per group (x and xh double the registers)
+  constexpr int NG = 32 / RU;
+  __shared__ double s_red[kSignThreads / 64];
+  __shared__ unsigned int s_flag;
+  double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int64_t j0 = (int64_t)blockIdx.x * kSignCols + 256 * w;
+  const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
+  // every row run of the wave (row 31's last float4 included) lies inside [0, n)
+  const bool interior = ncol == 256 && (int64_t)31 * Np + j0 + 256 <= n;
+  const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x, (uint32_t)(n * 4));
+  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(XH ? xh : x, (uint32_t)(n * 4));
+  const uint32_t voff = 16u * (uint32_t)lane;
+  auto row_off = [&](int r) -> uint32_t { return (uint32_t)(((int64_t)r * Np + j0) * 4); };  // wave-uniform
+  auto load_group = [&](int g, float4 (&R)[RU]) {
+#pragma unroll
+    for (int u = 0; u < RU; ++u) R[u] = ld_buf4s<true>(rx, voff, row_off(g * RU + u));
+    if (XH) {
+      float4 H[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) H[u] = ld_buf4s<true>(rh, voff, row_off(g * RU + u));
+#pragma unroll
+      for (int u = 0; u < RU; ++u) { R[u].x -= H[u].x; R[u].y -= H[u].y; R[u].z -= H[u].z; R[u].w -= H[u].w; }
+    }
+  };
+  uint32_t wd[4] = {0u, 0u, 0u, 0u};
+  double p = 0.0;
+  auto proc_group = [&](int g, const float4 (&R)[RU]) {
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int r = g * RU + u;
+      const float v[4] = {R[u].x, R[u].y, R[u].z, R[u].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wd[c] |= (v[c] < 0.f ? 1u : 0u) << r;
+      if (NORM) p += ((double)fabsf(v[0]) + (double)fabsf(v[1])) + ((double)fabsf(v[2]) + (double)fabsf(v[3]));
+      __builtin_amdgcn_sched_barrier(0);  // row by row: hoisted fp64 conversions of a whole group cost registers
+    }
+  };
+  // (sched_barrier: keep each group's loads where they are written -- hoisted,
+  // all 32 rows would be live at once)
+  if (interior) {
+    float4 A[RU], B[RU];
+    load_group(0, A);
+    load_group(1, B);
+#pragma unroll
+    for (int g = 0; g < NG; g += 2) {
+      proc_group(g, A);
+      if (g + 2 < NG) load_group(g + 2, A);
+      proc_group(g + 1, B);
+      if (g + 3 < NG) load_group(g + 3, B);
+    }
+  } else {
+    // the last workgroups: guarded element loads, one row at a time
+#pragma unroll 1
+    for (int r = 0; r < 32; ++r) {
+      const int64_t s = (int64_t)r * Np + j0 + 4 * lane;
+      float tt[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int64_t e = s + c;
+        tt[c] = (4 * lane + c < ncol && e < n) ? (XH ? x[e] - xh[e] : x[e]) : 0.f;
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wd[c] |= (tt[c] < 0.f ? 1u : 0u) << r;
+      if (NORM) p += ((double)fabsf(tt[0]) + (double)fabsf(tt[1])) + ((double)fabsf(tt[2]) + (double)fabsf(tt[3]));
+    }
+  }
+  {
+    const int64_t j = j0 + 4 * lane;
+    if (j + 3 < Np) {
+      *reinterpret_cast<uint4*>(packed + j) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (j + c < Np) packed[j + c] = wd[c];
+    }
+  }
+  if (NORM) {
+    p = wave_sum(p);
+    if (lane == 0) s_red[w] = p;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double tsum = 0.0;
+#pragma unroll
+      for (int i = 0; i < kSignThreads / 64; ++i) tsum += s_red[i];
+      if (tsum != 0.0) unsafeAtomicAdd(&acc[0], tsum);
+    }
+    if (last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
+      if (threadIdx.x == 0) {
+        l1_out[0] = (float)atomic_exchange_double(&acc[0], 0.0);
+        __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
 // Decode to +-1 floats (SignCompressor.unpacking).
 __global__ __launch_bounds__(kSignThreads) void sign_unpack_kernel(const uint32_t* __restrict__ packed,
                                                                    int64_t n, int64_t Np,
@@ -566,7 +679,23 @@ CHOCO_API int choco_sign_compress(const float* x, const float* xhat, int64_t n, 
     CHOCO_REQUIRE(ws && ws_bytes >= choco_sign_workspace_size(nseg), "sign workspace too small");
   }
   profile_begin("sign_pack", st);
-  if (xhat) {
+  if (nseg == 1 && n < (int64_t(1) << 30)) {  // buffer offsets: n * 4 < 2^32 bytes
+    if (xhat) {
+      if (l1_norms)
+        CHOCO_KLAUNCH((sign_pack1_kernel<true, true>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, pk,
+                      l1_norms, w);
+      else
+        CHOCO_KLAUNCH((sign_pack1_kernel<true, false>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, pk,
+                      l1_norms, w);
+    } else {
+      if (l1_norms)
+        CHOCO_KLAUNCH((sign_pack1_kernel<false, true>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, pk,
+                      l1_norms, w);
+      else
+        CHOCO_KLAUNCH((sign_pack1_kernel<false, false>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
+                      pk, l1_norms, w);
+    }
+  } else if (xhat) {
     if (l1_norms)
       CHOCO_KLAUNCH((sign_pack_kernel<true, true>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
                          seg_off, nseg, pk, l1_norms, w);

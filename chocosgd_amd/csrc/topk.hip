@@ -1206,6 +1206,11 @@ CHOCO_DEV void block_find_rank8k(const uint32_t* hist, uint32_t rank, uint32_t* 
 constexpr int kEmitR = 8;
 CHOCO_DEV void emit_addresses(const uint32_t* run_start, uint32_t nchunk, uint32_t tot, uint32_t pb, int64_t tb,
                               int64_t (&addr)[kEmitR]) {
+  if (run_start[1] >= tot) {  // one run (the compact layout): no search
+#pragma unroll
+    for (int i = 0; i < kEmitR; ++i) addr[i] = tb + (pb + i < tot ? (int64_t)(pb + i) : 0);
+    return;
+  }
   uint32_t lo = 0;
   if (pb < tot) {
     uint32_t hi = nchunk - 1;
