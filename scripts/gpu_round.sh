@@ -15,7 +15,7 @@ python tools/pmc_traffic.py $O/pmc_f_topk $O/pmc_w_topk topk_stream_kernel topk:
 python tools/pmc_traffic.py $O/pmc_f_topk $O/pmc_w_topk topk_finish_kernel topk_finish:100000000 && \
 python tools/pmc_traffic.py $O/pmc_f_topk $O/pmc_w_topk sparse_acc_kernel sparse_acc:1000000 && \
 python tools/pmc_traffic.py $O/pmc_f_qsgd $O/pmc_w_qsgd qsgd_quant_kernel qsgd:100000000 && \
-python tools/pmc_traffic.py $O/pmc_f_sign $O/pmc_w_sign sign_pack_kernel sign:345000000 && \
+python tools/pmc_traffic.py $O/pmc_f_sign $O/pmc_w_sign sign_pack sign:345000000 && \
 cp profiles/pmc_traffic.json $O/ || exit 1
 for wl in topk topk25m qsgd sign; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$wl -o run --output-format csv -- \
