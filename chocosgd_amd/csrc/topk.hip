@@ -99,7 +99,7 @@ __device__ unsigned long long g_stamps[kStampSlots][4];
 #define CHOCO_K2_STORE 0
 #endif
 #ifndef CHOCO_K34_PREFETCH
-#define CHOCO_K34_PREFETCH 1
+#define CHOCO_K34_PREFETCH 2
 #endif
 #ifndef CHOCO_K34_STORE
 #define CHOCO_K34_STORE 0
@@ -1162,10 +1162,13 @@ CHOCO_DEV uint32_t chunk_run_starts(const uint32_t (&cw)[kCPT], uint32_t nchunk,
   return tot;
 }
 
+constexpr int kEmitR = 8;  // emission batch: kEmitR rows of kK4Threads candidate positions
+constexpr int kEmitRows = kEmitR;
 constexpr int kSelBits = 13;  // radix-select digit: one round for bucket widths <= 2^13
 struct FinSmem {
   uint32_t keys[kMCap];
   uint32_t kbase[kK4Threads];  // per tile: side-list index of its first bucket-j* key - its first slot
+  uint32_t ecnt[2][kEmitRows * (kK4Threads / 64) + 1];  // emission: per (row, wave) counts -> bases, total
   uint32_t hist[1 << kSelBits];
   uint32_t G[kNBucket];
   uint32_t run_start[kMaxTileChunks + 1];
@@ -1201,32 +1204,50 @@ CHOCO_DEV void block_find_rank8k(const uint32_t* hist, uint32_t rank, uint32_t* 
   __syncthreads();
 }
 
-// Emission of one batch: thread t owns R consecutive candidate positions
-// [pb, pb + R) of its tile (thread order = index order).
-constexpr int kEmitR = 8;
-CHOCO_DEV void emit_addresses(const uint32_t* run_start, uint32_t nchunk, uint32_t tot, uint32_t pb, int64_t tb,
-                              int64_t (&addr)[kEmitR]) {
-  if (run_start[1] >= tot) {  // one run (the compact layout): no search
-#pragma unroll
-    for (int i = 0; i < kEmitR; ++i) addr[i] = tb + (pb + i < tot ? (int64_t)(pb + i) : 0);
-    return;
+// Emission: a batch is kEmitRows rows of kK4Threads candidate positions; in
+// row i thread t owns position p0 + i * kK4Threads + t, so every load and
+// store instruction is contiguous across the wave.
+// Candidate slot of tile position p (positions past the tile's total clamp to
+// the tile start: loads stay unconditional).  One run (the compact layout)
+// needs no search.
+CHOCO_DEV int64_t cand_addr(const uint32_t* run_start, uint32_t nchunk, uint32_t tot, uint32_t p, int64_t tb) {
+  if (p >= tot) return tb;
+  if (run_start[1] >= tot) return tb + p;
+  uint32_t lo = 0, hi = nchunk - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (run_start[mid] <= p) lo = mid; else hi = mid - 1;
   }
-  uint32_t lo = 0;
-  if (pb < tot) {
-    uint32_t hi = nchunk - 1;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1) >> 1;
-      if (run_start[mid] <= pb) lo = mid; else hi = mid - 1;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < kEmitR; ++i) {
-    const uint32_t p = pb + i;
-    if (p < tot)
-      while (run_start[lo + 1] <= p) ++lo;  // the run of position p (runs may be empty)
-    addr[i] = p < tot ? tb + (int64_t)lo * kChunk + (p - run_start[lo]) : tb;  // clamped: loads unconditional
-  }
+  return tb + (int64_t)lo * kChunk + (p - run_start[lo]);
 }
+
+// Exclusive ranks, in position order, of the flagged slots of one emission
+// batch (row-major: row i, then wave, then lane); returns the batch total.
+// `cnt` is one of two alternating LDS buffers; two barriers.
+CHOCO_DEV uint32_t batch_ranks(const bool (&f)[kEmitRows], uint32_t (&rk)[kEmitRows], uint32_t* cnt) {
+  constexpr int kW = kK4Threads / 64;
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  uint64_t bm[kEmitRows];
+#pragma unroll
+  for (int i = 0; i < kEmitRows; ++i) {
+    bm[i] = ballot(f[i]);
+    if (lane == 0) cnt[i * kW + w] = (uint32_t)__popcll(bm[i]);
+  }
+  __syncthreads();
+  if (w == 0) {  // wave 0 scans the kEmitRows * kW = 128 counts, two per lane
+    const uint32_t c0 = cnt[2 * lane], c1 = cnt[2 * lane + 1];
+    const uint32_t inc = wave_incl_scan(c0 + c1);
+    const uint32_t ex = inc - c0 - c1;
+    cnt[2 * lane] = ex;
+    cnt[2 * lane + 1] = ex + c0;
+    if (lane == 63) cnt[kEmitRows * kW] = inc;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kEmitRows; ++i) rk[i] = cnt[i * kW + w] + mask_prefix(bm[i]);
+  return cnt[kEmitRows * kW];
+}
+static_assert(kEmitRows * (kK4Threads / 64) == 128, "batch_ranks: wave 0 scans 2 counts per lane");
 
 template <int MODE, bool XH>
 __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
@@ -1268,7 +1289,8 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   // ---- the addresses of the tile's first emission batch (it does not depend on T)
   const int64_t tb = b * (int64_t)tile;
   int64_t addr[kEmitR];
-  emit_addresses(fs.run_start, nchunk, tot, (uint32_t)tid * kEmitR, tb, addr);
+#pragma unroll
+  for (int i = 0; i < kEmitR; ++i) addr[i] = cand_addr(fs.run_start, nchunk, tot, (uint32_t)(i * kK4Threads + tid), tb);
   float v[kEmitR];
   uint32_t idx[kEmitR];
   if (tid < kNBucket) {
@@ -1339,7 +1361,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
       // The first emission batch's loads go out now, BEHIND the key loads: the
       // vmcnt counter is in order, so waiting for the keys does not wait for
       // them, and they land while T is being selected.
-      if (CHOCO_K34_PREFETCH) {
+      if (CHOCO_K34_PREFETCH == 1) {
 #pragma unroll
         for (int i = 0; i < kEmitR; ++i) {
           v[i] = cval[addr[i]];
@@ -1352,6 +1374,16 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
       for (int q = 0; q < kG; ++q) {
         const uint32_t i = (uint32_t)tid + (uint32_t)q * kK4Threads;
         if (i < M) fs.keys[i] = kv[q];
+      }
+      if (CHOCO_K34_PREFETCH == 2) {
+        // late prefetch: the first emission batch goes out once the keys are in,
+        // so it does not queue in front of other workgroups' key gathers
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < kEmitR; ++i) {
+          v[i] = cval[addr[i]];
+          idx[i] = cidx[addr[i]];
+        }
       }
     }
     // ---- radix select inside bucket j*: rel = key - base_j in [0, 2^shift),
@@ -1407,12 +1439,14 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     uint32_t out = fs.bc[4];
     uint32_t tie_run = fs.bc[5];
     const uint32_t mode = fs.bc[6];
-    // Batches of kK4Threads * kEmitR candidates; one block scan of each thread's
-    // count places them (two scans only when ties at T are split).
+    // Batches of kEmitRows x kK4Threads candidates (row i, thread t <-> position
+    // p0 + i * kK4Threads + t); the ranks of the selected ones place them (the
+    // ties' ranks first, only when ties at T are split).
+    int eb = 0;  // alternating rank buffer
     for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads * kEmitR) {
-      const uint32_t pb = p0 + tid * kEmitR;
       if (p0 != 0 || !CHOCO_K34_PREFETCH) {  // workgroup-uniform: batches after the prefetched first one
-        emit_addresses(fs.run_start, nchunk, tot, pb, tb, addr);
+#pragma unroll
+        for (int i = 0; i < kEmitR; ++i) addr[i] = cand_addr(fs.run_start, nchunk, tot, p0 + i * kK4Threads + tid, tb);
 #pragma unroll
         for (int i = 0; i < kEmitR; ++i) {
           v[i] = cval[addr[i]];
@@ -1420,40 +1454,32 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
         }
       }
       bool gtv[kEmitR], eqv[kEmitR];
-      uint32_t neq = 0;
 #pragma unroll
       for (int i = 0; i < kEmitR; ++i) {
-        const bool valid = pb + i < tot;
+        const bool valid = p0 + i * kK4Threads + tid < tot;
         const uint32_t key = MODE == kData ? fkey(v[i]) : (rank_hash(seed, idx[i]) >> 1);
         gtv[i] = valid && key > T;
         eqv[i] = valid && key == T;
-        neq += eqv[i] ? 1u : 0u;
       }
       bool sel[kEmitR];
+      uint32_t rk[kEmitR];
       if (mode == kTakePartial) {  // workgroup-uniform
-        uint32_t eq_total;
-        uint32_t rank = tie_run + block_excl_scan(neq, fs.scratch, &eq_total);
+        const uint32_t eq_total = batch_ranks(eqv, rk, fs.ecnt[eb]);
+        eb ^= 1;
 #pragma unroll
-        for (int i = 0; i < kEmitR; ++i) {
-          sel[i] = gtv[i] || (eqv[i] && rank < r);
-          rank += eqv[i] ? 1u : 0u;
-        }
+        for (int i = 0; i < kEmitR; ++i) sel[i] = gtv[i] || (eqv[i] && tie_run + rk[i] < r);
         tie_run += eq_total;
       } else {
 #pragma unroll
         for (int i = 0; i < kEmitR; ++i) sel[i] = gtv[i] || (eqv[i] && mode == kTakeAll);
       }
-      uint32_t nmine = 0;
-#pragma unroll
-      for (int i = 0; i < kEmitR; ++i) nmine += sel[i] ? 1u : 0u;
-      uint32_t nsel;
-      uint32_t pos = out + block_excl_scan(nmine, fs.scratch, &nsel);
+      const uint32_t nsel = batch_ranks(sel, rk, fs.ecnt[eb]);
+      eb ^= 1;
 #pragma unroll
       for (int i = 0; i < kEmitR; ++i) {
         if (sel[i]) {
-          st_pol<CHOCO_K34_STORE>(&out_val[pos], v[i] * scale);
-          st_pol<CHOCO_K34_STORE>(&out_idx[pos], (int32_t)((int64_t)idx[i] + idx_base));
-          ++pos;
+          st_pol<CHOCO_K34_STORE>(&out_val[out + rk[i]], v[i] * scale);
+          st_pol<CHOCO_K34_STORE>(&out_idx[out + rk[i]], (int32_t)((int64_t)idx[i] + idx_base));
         }
       }
       out += nsel;

@@ -14,6 +14,7 @@ VARIANTS = {
     "stream_nt": ["CHOCO_STREAM_NT=1"],
     "chunk4k": ["CHOCO_K2_CHUNK=4096"],
     "nopf": ["CHOCO_K34_PREFETCH=0"],
+    "earlypf": ["CHOCO_K34_PREFETCH=1"],
     "acc_atom": ["CHOCO_ACC_STORE=3"],
     "s32k": ["CHOCO_SAMPLE_RUNS=128"],
     "s32k_nopf": ["CHOCO_SAMPLE_RUNS=128", "CHOCO_K34_PREFETCH=0"],
