@@ -70,6 +70,18 @@ CHOCO_DEV QParam qparam(const float* __restrict__ norms, const int64_t* __restri
   return p;
 }
 
+// Non-temporal loads in the norm pass (default; 0 for A/B runs): they keep the
+// previous decode's dirty Infinity-Cache lines from being written back in the
+// middle of this stream (bench step: 120 -> 72 us), though the decode then
+// meets them itself.
+#ifndef CHOCO_QNORM_NT
+#define CHOCO_QNORM_NT 1
+#endif
+CHOCO_DEV float4 ld_norm4(const float* p) {
+  if (CHOCO_QNORM_NT) return ld_nt4(p);
+  return *reinterpret_cast<const float4*>(p);
+}
+
 // ---------------------------------------------------------------- pass 1: norms
 template <bool XH>
 __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __restrict__ x,
@@ -98,11 +110,11 @@ __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __res
       for (int64_t e0 = t0 + 4 * tid; e0 < t1; e0 += 4 * kQThreads * U) {
         float4 a[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) a[u] = *reinterpret_cast<const float4*>(x + e0 + (int64_t)u * 4 * kQThreads);
+        for (int u = 0; u < U; ++u) a[u] = ld_norm4(x + e0 + (int64_t)u * 4 * kQThreads);
         if (XH) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            const float4 h = *reinterpret_cast<const float4*>(xh + e0 + (int64_t)u * 4 * kQThreads);
+            const float4 h = ld_norm4(xh + e0 + (int64_t)u * 4 * kQThreads);
             a[u].x -= h.x; a[u].y -= h.y; a[u].z -= h.z; a[u].w -= h.w;
           }
         }

@@ -15,6 +15,7 @@ VARIANTS = {
     "chunk4k": ["CHOCO_K2_CHUNK=4096"],
     "nopf": ["CHOCO_K34_PREFETCH=0"],
     "earlypf": ["CHOCO_K34_PREFETCH=1"],
+    "qn_plain": ["CHOCO_QNORM_NT=0"],
     "acc_atom": ["CHOCO_ACC_STORE=3"],
     "s32k": ["CHOCO_SAMPLE_RUNS=128"],
     "s32k_nopf": ["CHOCO_SAMPLE_RUNS=128", "CHOCO_K34_PREFETCH=0"],
