@@ -48,6 +48,7 @@ SIGNATURES = {
                                                   _c_i32, _c_i32, _vp, _vp, _vp]),
     "choco_gossip_step": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _vp]),
     "choco_profile_enable": (_c_i32, [_c_i32]),
+    "choco_profile_filter": (_c_i32, [ctypes.c_char_p]),
     "choco_profile_read": (_c_i32, [ctypes.c_char_p, ctypes.POINTER(_c_f64), ctypes.POINTER(_c_i64)]),
     "choco_profile_reset": (_c_i32, []),
 }

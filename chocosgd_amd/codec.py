@@ -289,6 +289,11 @@ def profile_enable(on=True):
     lib().choco_profile_enable(1 if on else 0)
 
 
+def profile_filter(name=None):
+    """Time only the launches named `name` (None = all)."""
+    lib().choco_profile_filter(name.encode() if name else None)
+
+
 def profile_read(name):
     total = ctypes.c_double(0.0)
     cnt = ctypes.c_int64(0)

@@ -39,16 +39,26 @@ static std::atomic<bool> g_prof_on{false};
 static std::mutex g_prof_mu;
 static std::vector<PendingEv> g_pending;
 static std::map<std::string, std::pair<double, int64_t>> g_acc;
+static std::string g_filter;               // only this kernel name is timed ("" = all)
+static std::vector<hipEvent_t> g_free_ev;  // events are reused: no create/destroy per launch
 
 static thread_local ProfArm g_armed{nullptr, nullptr};
 
 void profile_begin(const char* name, hipStream_t) {
   g_armed = ProfArm{nullptr, nullptr};
   if (!g_prof_on.load(std::memory_order_relaxed)) return;
-  PendingEv p{name, nullptr, nullptr, true};
-  if (hipEventCreate(&p.a) != hipSuccess || hipEventCreate(&p.b) != hipSuccess) return;
-  g_armed = ProfArm{p.a, p.b};
   std::lock_guard<std::mutex> g(g_prof_mu);
+  if (!g_filter.empty() && g_filter != name) return;
+  PendingEv p{name, nullptr, nullptr, false};  // closed once a launch takes the pair
+  for (hipEvent_t* e : {&p.a, &p.b}) {
+    if (!g_free_ev.empty()) {
+      *e = g_free_ev.back();
+      g_free_ev.pop_back();
+    } else if (hipEventCreate(e) != hipSuccess) {
+      return;
+    }
+  }
+  g_armed = ProfArm{p.a, p.b};
   g_pending.push_back(p);
 }
 
@@ -57,6 +67,14 @@ void profile_end(const char*, hipStream_t) { g_armed = ProfArm{nullptr, nullptr}
 ProfArm profile_take() {
   const ProfArm r = g_armed;
   g_armed = ProfArm{nullptr, nullptr};
+  if (r.a) {  // the launch records this pair: only now may it be read (events are reused)
+    std::lock_guard<std::mutex> g(g_prof_mu);
+    for (auto it = g_pending.rbegin(); it != g_pending.rend(); ++it)
+      if (it->a == r.a) {
+        it->closed = true;
+        break;
+      }
+  }
   return r;
 }
 
@@ -64,15 +82,15 @@ static void profile_drain_locked() {
   for (auto& p : g_pending) {
     if (p.closed) {
       float ms = 0.f;
-      // an armed pair that never reached a launch was never recorded: skipped
+      // (an armed pair that never reached a launch is not closed: skipped)
       if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
         auto& e = g_acc[p.name];
         e.first += ms;
         e.second += 1;
       }
     }
-    (void)hipEventDestroy(p.a);
-    (void)hipEventDestroy(p.b);
+    g_free_ev.push_back(p.a);
+    g_free_ev.push_back(p.b);
   }
   g_pending.clear();
 }
@@ -95,6 +113,12 @@ CHOCO_API int choco_last_error(char* buf, size_t len) {
 
 CHOCO_API int choco_profile_enable(int32_t on) {
   g_prof_on.store(on != 0);
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_profile_filter(const char* name) {
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  g_filter = name ? name : "";
   return CHOCO_OK;
 }
 

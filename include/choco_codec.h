@@ -196,6 +196,8 @@ int choco_profile_enable(int32_t on);
 /* Accumulated (sum of ms, count) of the named kernel since the last reset,
  * after synchronising its events.  Names: "topk_stream", "sign_pack",
  * "qsgd_quantize", "sparse_accumulate", ... */
+// Time only the launches named `name` (NULL or "" = all); events are reused.
+int choco_profile_filter(const char* name);
 int choco_profile_read(const char* name, double* total_ms, int64_t* count);
 int choco_profile_reset(void);
 
