@@ -9,14 +9,14 @@ from chocosgd_amd import build  # noqa: E402
 
 VARIANTS = {
     "stamps": ["CHOCO_STAMPS=1"],
-    "acc_nt": ["CHOCO_ACC_STORE=1"],
-    "acc_sc1": ["CHOCO_ACC_STORE=2"],
     "stream_nt": ["CHOCO_STREAM_NT=1"],
     "chunk4k": ["CHOCO_K2_CHUNK=4096"],
     "nopf": ["CHOCO_K34_PREFETCH=0"],
     "earlypf": ["CHOCO_K34_PREFETCH=1"],
     "qn_plain": ["CHOCO_QNORM_NT=0"],
-    "acc_atom": ["CHOCO_ACC_STORE=3"],
+    "acc_u4": ["CHOCO_ACC_U=4"],
+    "acc_u8": ["CHOCO_ACC_U=8"],
+    "acc_u16": ["CHOCO_ACC_U=16"],
     "s32k": ["CHOCO_SAMPLE_RUNS=128"],
     "s32k_nopf": ["CHOCO_SAMPLE_RUNS=128", "CHOCO_K34_PREFETCH=0"],
     "stamps_s32k": ["CHOCO_STAMPS=1", "CHOCO_SAMPLE_RUNS=128"],
@@ -26,8 +26,6 @@ VARIANTS = {
     "nob3": ["CHOCO_STAMPS=1", "CHOCO_DIAG_NOBURST=3"],
     "k2st_nt": ["CHOCO_K2_STORE=1"],
     "k2st_sc1": ["CHOCO_K2_STORE=2"],
-    "st_nt": ["CHOCO_K2_STORE=1", "CHOCO_K34_STORE=1", "CHOCO_ACC_STORE=1"],
-    "st_sc1": ["CHOCO_K2_STORE=2", "CHOCO_K34_STORE=2", "CHOCO_ACC_STORE=2"],
 }
 
 
