@@ -82,6 +82,14 @@ CHOCO_DEV float4 ld_norm4(const float* p) {
   return *reinterpret_cast<const float4*>(p);
 }
 
+#ifndef CHOCO_QQUANT_NT  // non-temporal loads in the quantize pass (off: the decode then runs 300 -> 270 us)
+#define CHOCO_QQUANT_NT 0
+#endif
+CHOCO_DEV float4 ld_quant4(const float* p) {
+  if (CHOCO_QQUANT_NT) return ld_nt4(p);
+  return *reinterpret_cast<const float4*>(p);
+}
+
 // ---------------------------------------------------------------- pass 1: norms
 template <bool XH>
 __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __restrict__ x,
@@ -270,12 +278,12 @@ __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
   const uint32_t smax = (uint32_t)s_levels;
   float d[kQPer];
   if (e0 + kQPer <= n) {
-    const float4 a0 = ld_nt4(x + e0);  // the delta's last read (the norm pass read it first)
-    const float4 a1 = ld_nt4(x + e0 + 4);
+    const float4 a0 = ld_quant4(x + e0);  // the delta's last read (the norm pass read it first)
+    const float4 a1 = ld_quant4(x + e0 + 4);
     d[0] = a0.x; d[1] = a0.y; d[2] = a0.z; d[3] = a0.w; d[4] = a1.x; d[5] = a1.y; d[6] = a1.z; d[7] = a1.w;
     if (xh) {
-      const float4 h0 = ld_nt4(xh + e0);
-      const float4 h1 = ld_nt4(xh + e0 + 4);
+      const float4 h0 = ld_quant4(xh + e0);
+      const float4 h1 = ld_quant4(xh + e0 + 4);
       d[0] -= h0.x; d[1] -= h0.y; d[2] -= h0.z; d[3] -= h0.w;
       d[4] -= h1.x; d[5] -= h1.y; d[6] -= h1.z; d[7] -= h1.w;
     }

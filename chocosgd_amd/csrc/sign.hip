@@ -262,6 +262,9 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
 // bytes): the row offset is a wave-uniform SGPR operand and the lane offset
 // one VGPR, so the 2 x RU loads in flight need no 64-bit address registers.
 
+#ifndef CHOCO_SIGN_NT  // non-temporal loads in the one-segment pack
+#define CHOCO_SIGN_NT 1
+#endif
 template <bool XH, bool NORM>
 __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* __restrict__ x,
                                                                   const float* __restrict__ xh, int64_t n,
@@ -284,11 +287,11 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
   auto row_off = [&](int r) -> uint32_t { return (uint32_t)(((int64_t)r * Np + j0) * 4); };  // wave-uniform
   auto load_group = [&](int g, float4 (&R)[RU]) {
 #pragma unroll
-    for (int u = 0; u < RU; ++u) R[u] = ld_buf4s<true>(rx, voff, row_off(g * RU + u));
+    for (int u = 0; u < RU; ++u) R[u] = ld_buf4s<CHOCO_SIGN_NT>(rx, voff, row_off(g * RU + u));
     if (XH) {
       float4 H[RU];
 #pragma unroll
-      for (int u = 0; u < RU; ++u) H[u] = ld_buf4s<true>(rh, voff, row_off(g * RU + u));
+      for (int u = 0; u < RU; ++u) H[u] = ld_buf4s<CHOCO_SIGN_NT>(rh, voff, row_off(g * RU + u));
 #pragma unroll
       for (int u = 0; u < RU; ++u) { R[u].x -= H[u].x; R[u].y -= H[u].y; R[u].z -= H[u].z; R[u].w -= H[u].w; }
     }

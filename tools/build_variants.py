@@ -14,6 +14,8 @@ VARIANTS = {
     "nopf": ["CHOCO_K34_PREFETCH=0"],
     "earlypf": ["CHOCO_K34_PREFETCH=1"],
     "qn_plain": ["CHOCO_QNORM_NT=0"],
+    "sign_plain": ["CHOCO_SIGN_NT=0"],
+    "qq_nt": ["CHOCO_QQUANT_NT=1"],
     "acc_u4": ["CHOCO_ACC_U=4"],
     "acc_u8": ["CHOCO_ACC_U=8"],
     "acc_u16": ["CHOCO_ACC_U=16"],
