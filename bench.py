@@ -7,22 +7,28 @@ message with its graph neighbours (RCCL send/recv over xGMI for N > 1), and
 decompress-accumulate every received message (self included) into x_hat_i and
 memory.  One process per GPU; each worker owns its own buffer (weak scaling).
 
-    python bench.py [--gpus N --steps K --warmup W --workload topk|topk25m|qsgd|sign]
+    python bench.py [--gpus N --steps K --warmup W --workload topk|...]
+
+`--gpus N` without a launcher starts N rank processes itself (before this
+process touches the GPU); under torch.distributed.run the ranks come from the
+environment.
 
 metric (BASELINE.json): compress+decompress GB/s = sum_r 4*n_r / max_r(step time).
-roofline: the dominant kernel's algorithmic bytes / its HIP-event-timed duration
-on its own stream, against 8 TB/s.  cpu_baseline: the reference's torch-CPU op
-sequence (oracle/torch_port.py) on the host cores, rank 0 only, N = 1 only.
+roofline: per STAGE of the step (compress, decompress), algorithmic bytes
+(SURVEY.md 8(d)) / the stage's kernel time from dispatch-attached HIP events;
+`roofline` is the stage that takes the most time (measured, not assumed): its
+kernels carry events inside the timed region, the other stage's in an untimed
+pass after it.  cpu_baseline: the reference's torch-CPU op sequence
+(oracle/torch_port.py) on the host cores, rank 0 only, N = 1 only.
 """
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
-
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -30,44 +36,90 @@ sys.path.insert(0, ROOT)
 METRIC = "compress+decompress GB/s (device-resident) on flat fp32 buffer, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 
+# name: op, elements per worker, parameter (ratio or q), config label
 WORKLOADS = {
-    # name: (op, n per worker, parameter, dominant kernel)
-    "topk": ("topk", 100_000_000, 0.99, "topk_stream"),
-    "topk25m": ("topk", 25_000_000, 0.99, "topk_stream"),
-    "qsgd": ("qsgd", 100_000_000, 4, "qsgd_quantize"),
-    "sign": ("sign", 345_000_000, None, "sign_pack"),
+    "topk": ("topk", 100_000_000, 0.99, "topk_k1pct_per_worker"),
+    "topk25m": ("topk", 25_000_000, 0.99, "topk_k1pct_25M"),
+    "topk_r50": ("topk_seg", 25_557_032, 0.99, "topk_k1pct_resnet50_161seg"),
+    "randk": ("randk", 100_000_000, 0.99, "randk_k1pct_per_worker"),
+    "qsgd": ("qsgd", 100_000_000, 4, "qsgd_q4_per_worker"),
+    "sign": ("sign", 345_000_000, None, "sign_norm_per_worker"),
+}
+
+# kernels (profile names) of each stage
+STAGES = {
+    "topk": (["topk_bounds", "topk_stream", "topk_finish", "topk_exact", "topk_all"], ["sparse_accumulate"]),
+    "topk_seg": (["topk_segmented", "topk_bounds", "topk_stream", "topk_finish"], ["sparse_accumulate"]),
+    "randk": (["topk_stream", "topk_finish", "topk_exact", "topk_all"], ["sparse_accumulate"]),
+    "qsgd": (["qsgd_norm", "qsgd_quantize"], ["qsgd_accumulate"]),
+    "sign": (["sign_pack"], ["sign_accumulate"]),
 }
 
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--workload", default="topk", choices=sorted(WORKLOADS))
     p.add_argument("--n", type=int, default=0, help="override elements per worker")
     p.add_argument("--nbuf", type=int, default=4, help="delta buffers compressed in rotation (one per step)")
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="gloo: messages staged through host memory (comm_device=cpu); lets ranks share a GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-e2e", action="store_true", help="skip the host-resident (PCIe-inclusive) leg")
     p.add_argument("--lib", default=None, help=argparse.SUPPRESS)
-    p.add_argument("--no-kernel-events", action="store_true", help=argparse.SUPPRESS)  # diagnostic  # diagnostic variant (tools/build_variants.py)
-    p.add_argument("--diag-evict", action="store_true", help=argparse.SUPPRESS)  # 1 GiB read after each step
+    p.add_argument("--no-kernel-events", action="store_true", help=argparse.SUPPRESS)  # diagnostic
     return p.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` with no launcher: one child process per rank, started
+    before this process makes any GPU call (it never makes one); exits with the worst rc."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
 
 
 class Worker:
     """Per-rank buffers and one compress -> exchange -> decompress round."""
 
     def __init__(self, args, rank, world, dev):
+        import torch
         from chocosgd_amd import codec
         from chocosgd_amd.communication import neighborhood
+        self.torch = torch
         self.codec = codec
-        self.op, n, self.param, self.kernel = WORKLOADS[args.workload]
-        self.n = args.n or n
+        self.op, n, self.param, self.label = WORKLOADS[args.workload]
+        self.backend = args.backend
         self.rank, self.world, self.dev = rank, world, dev
         self.nb = neighborhood(rank, world)
-        self.peers = [r for r in self.nb if r != rank]
+        self.ranks = list(self.nb.keys())
+        self.peers = [r for r in self.ranks if r != rank]
+        self.weights = [self.nb[r] for r in self.ranks]
+        self.self_slot = self.ranks.index(rank)
+        self.plan = None
+        if self.op == "topk_seg":
+            with open(os.path.join(ROOT, "tests", "golden", "layouts.json")) as f:
+                lens = json.load(f)["resnet50_imagenet"]
+            self.plan = codec.SegmentPlan(lens, self.param, dev)
+            n = sum(lens)
+        self.n = args.n or n
         g = torch.Generator(device=dev).manual_seed(1000 + rank)
         # The worker's delta x - x_hat.  Consecutive steps compress different
         # buffers (args.nbuf, independent draws), so each step selects a new
@@ -76,24 +128,36 @@ class Worker:
         self.d = self.ds[0]
         self.hat = torch.zeros(self.n, device=dev)
         self.mem = torch.zeros(self.n, device=dev)
-        if self.op == "topk":
+        self.k = None
+        if self.op in ("topk", "randk"):
             self.k = codec.topk_k(self.n, self.param)
             self.msg = torch.empty(2 * self.k, dtype=torch.int32, device=dev)
+        elif self.op == "topk_seg":
+            self.k = self.plan.k_total
+            self.msg = torch.empty(2 * self.k, dtype=torch.int32, device=dev)
         elif self.op == "qsgd":
-            self.k = None
             nbytes = codec.qsgd_packed_bytes(self.n, self.param)
             self.msg = torch.empty(16 + nbytes, dtype=torch.uint8, device=dev)   # [norm (16 B) | planes]
         else:
-            self.k = None
             self.msg = torch.empty(4 + codec.sign_words(self.n), dtype=torch.int32, device=dev)
         self.recv = {r: torch.empty_like(self.msg) for r in self.peers}
+        if self.backend == "gloo":
+            self.msg_h = torch.empty(self.msg.shape, dtype=self.msg.dtype).pin_memory()
+            self.recv_h = {r: torch.empty_like(self.msg_h).pin_memory() for r in self.peers}
         self.step_id = 0
 
     def compress(self):
         c = self.codec
+        torch = self.torch
         self.d = self.ds[self.step_id % len(self.ds)]
         if self.op == "topk":
             c.topk(self.d, self.k, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]))
+        elif self.op == "topk_seg":
+            c.topk_segmented(self.d, self.plan, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]))
+        elif self.op == "randk":
+            v, i = c.randk(self.d, self.k, seed=12345 + 7919 * self.step_id + self.rank)
+            self.msg[:self.k].view(torch.float32).copy_(v)
+            self.msg[self.k:].copy_(i)
         elif self.op == "qsgd":
             packed, norms, _ = c.qsgd_compress(self.d, self.param, seed=12345 + self.rank, offset=self.step_id)
             self.msg[16:].copy_(packed)
@@ -107,46 +171,77 @@ class Worker:
     def exchange(self):
         if not self.peers:
             return
+        import torch.distributed as dist
+        if self.backend == "gloo":  # comm_device=cpu: pinned host staging (parallel_choco_v.py:271-272)
+            self.msg_h.copy_(self.msg)
+            src, dst = self.msg_h, self.recv_h
+        else:
+            src, dst = self.msg, self.recv
         ops = []
         for r in self.peers:
-            ops.append(dist.P2POp(dist.isend, self.msg, r))
-            ops.append(dist.P2POp(dist.irecv, self.recv[r], r))
+            ops.append(dist.P2POp(dist.isend, src, r))
+            ops.append(dist.P2POp(dist.irecv, dst[r], r))
         for w in dist.batch_isend_irecv(ops):
             w.wait()
+        if self.backend == "gloo":
+            for r in self.peers:
+                self.recv[r].copy_(self.recv_h[r], non_blocking=True)
 
     def decompress(self):
         c = self.codec
-        ranks = list(self.nb.keys())
-        msgs = [self.msg if r == self.rank else self.recv[r] for r in ranks]
-        weights = [self.nb[r] for r in ranks]
-        self_slot = ranks.index(self.rank)
-        if self.op == "topk":
-            for r, m, w in zip(ranks, msgs, weights):
+        torch = self.torch
+        msgs = [self.msg if r == self.rank else self.recv[r] for r in self.ranks]
+        if self.op in ("topk", "topk_seg", "randk"):
+            for r, m, w in zip(self.ranks, msgs, self.weights):
                 c.sparse_accumulate(m[:self.k].view(torch.float32), m[self.k:], self.mem, w,
                                     xhat_self=self.hat if r == self.rank else None)
         elif self.op == "qsgd":
             parts = [(m[16:], m[:4].view(torch.float32)) for m in msgs]
-            c.qsgd_accumulate(parts, weights, self_slot, self.n, self.param, self.mem, xhat_self=self.hat)
+            c.qsgd_accumulate(parts, self.weights, self.self_slot, self.n, self.param, self.mem, xhat_self=self.hat)
         else:
             parts = [(m[4:], m[:1].view(torch.float32)) for m in msgs]
-            c.sign_accumulate(parts, weights, self_slot, self.n, self.mem, xhat_self=self.hat)
+            c.sign_accumulate(parts, self.weights, self.self_slot, self.n, self.mem, xhat_self=self.hat)
 
     def step(self):
         self.compress()
         self.exchange()
         self.decompress()
 
-    def kernel_bytes(self):
-        """Algorithmic HBM bytes of ONE launch of the dominant kernel."""
-        n = self.n
-        if self.op == "topk":
-            return 4 * n + 8 * self.k                    # read d once, write k (fp32 value, int32 index)
+    def stage_bytes(self):
+        """Algorithmic HBM bytes per step of each stage, and the
+        notes that say how they are counted."""
+        n, nm = self.n, len(self.ranks)
+        if self.op in ("topk", "topk_seg"):
+            comp = 4 * n + 8 * self.k                    # read d once, write k (fp32 value, int32 index)
+            dec = 8 * self.k * nm + 8 * self.k * (nm + 1)  # read each message; RMW mem per msg + x_hat (self)
+            return comp, dec, "compress 4n + 8k; decompress 8k read per message + 8k RMW per touched buffer"
+        if self.op == "randk":
+            comp = 4 * self.k + 8 * self.k                # gather k values + write k pairs (the sampler reads none)
+            dec = 8 * self.k * nm + 8 * self.k * (nm + 1)
+            return comp, dec, "compress 4k gather + 8k; decompress as top-k"
         if self.op == "qsgd":
             cw = 1
             while cw < self.param:
                 cw <<= 1
-            return 4 * n + n * cw // 8 + n // 8          # read d, write level + sign planes
-        return 4 * n + 4 * ((n + 31) // 32)              # read d, write packed sign words
+            wire = n * cw // 8 + n // 8
+            comp = 4 * n + wire + 4                       # read d, write level + sign planes + norm
+            dec = nm * wire + 8 * n + 8 * n               # read each message, RMW memory and x_hat
+            return comp, dec, "compress 4n + n(cw+1)/8 (the norm pass's second read of d is not counted); " \
+                              "decompress wire per message + 8n RMW memory + 8n RMW x_hat"
+        words = 4 * ((n + 31) // 32)
+        return 4 * n + words + 4, nm * words + 16 * n, "compress 4n + n/8; decompress n/8 per message + 16n RMW"
+
+    def granule_bytes_decompress(self):
+        """Sparse accumulate at HBM access granularity: every touched 64-B segment of
+        x_hat / memory is read and written whole (the bound a scattered RMW really pays)."""
+        if self.op not in ("topk", "topk_seg", "randk"):
+            return None
+        torch = self.torch
+        segs = 0
+        for m in [self.msg] + [self.recv[r] for r in self.peers]:
+            segs += int(torch.unique(m[self.k:].long() // 16).numel())
+        own = int(torch.unique(self.msg[self.k:].long() // 16).numel())
+        return 8 * self.k * len(self.ranks) + 128 * (segs + own)
 
 
 def e2e_rate(w, reps=5):
@@ -154,6 +249,7 @@ def e2e_rate(w, reps=5):
     pinned H2D of the worker's buffer -> compress -> D2H of the packed message
     -> H2D of that message (the receiver's copy) -> decompress-accumulate.
     Reported next to, never as, the device-resident value."""
+    import torch
     host_x = w.d.cpu().pin_memory()
     host_msg = torch.empty(w.msg.shape, dtype=w.msg.dtype).pin_memory()
     parts = {"h2d": [], "device": [], "d2h": [], "total": []}
@@ -186,64 +282,94 @@ def e2e_rate(w, reps=5):
                     f"{reps}"}
 
 
-def cpu_baseline(w, threads):
-    """Reference torch-CPU op sequence (oracle/torch_port.py) on the host cores."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(w):
+    """Reference torch-CPU op sequence (oracle/torch_port.py) on the host cores: the
+    process's usable CPUs (sched affinity), one thread, and os.cpu_count() threads."""
+    import torch
     from oracle import torch_port as P
-    torch.set_num_threads(threads)
-    n = w.n
-    if w.op == "topk":
-        d = w.d.cpu()
-        hat, mem = torch.zeros(n), torch.zeros(n)
 
-        def run():
-            v, i = P.topk_compress(d, w.param)
-            P.sparse_decompress(hat, mem, v, i, 1.0)
-        sample = f"full {n}-element delta, top-k ratio {w.param}, compress + self decompress"
-    elif w.op == "qsgd":
-        d = w.d.cpu()
-        hat, mem = torch.zeros(n), torch.zeros(n)
-
-        def run():
-            q = P.qsgd_compress(d, 2 ** w.param - 1)
-            P.dense_decompress(hat, mem, q, 1.0)
-        sample = f"full {n}-element delta, QSGD q={w.param}, compress + self decompress"
-    else:
-        m = min(n, 100_000_000)
+    def make(m):
         d = w.d[:m].cpu()
         hat, mem = torch.zeros(m), torch.zeros(m)
+        if w.op in ("topk", "topk_seg", "randk"):
+            if w.op == "randk":
+                return lambda: P.sparse_decompress(hat, mem, *P.randk_compress(d, w.param), 1.0)
+            return lambda: P.sparse_decompress(hat, mem, *P.topk_compress(d, w.param), 1.0)
+        if w.op == "qsgd":
+            return lambda: P.dense_decompress(hat, mem, P.qsgd_compress(d, 2 ** w.param - 1), 1.0)
+        return lambda: P.sign_decompress(hat, mem, *P.sign_compress(d), m, 1.0)
 
-        def run():
-            words, norm = P.sign_compress(d)
-            P.sign_decompress(hat, mem, words, norm, m, 1.0)
-        n = m
-        sample = f"first {m} elements of the delta, sign+L1 norm compress + self decompress"
-    run()  # warm-up
-    ts = []
-    budget = time.perf_counter() + 25.0
-    while len(ts) < 3 and (not ts or time.perf_counter() < budget):
-        t0 = time.perf_counter()
-        run()
-        ts.append(time.perf_counter() - t0)
-    med = statistics.median(ts)
-    return {"value": round(4 * n / med / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"{sample}; median of {len(ts)} after 1 warm-up; {med * 1e3:.1f} ms each"}
+    what = {"topk": "top-k (torch.topk) compress + self decompress",
+            "topk_seg": "top-k (torch.topk, flat) compress + self decompress",
+            "randk": "random-k (np.random.choice) compress + self decompress",
+            "qsgd": f"QSGD q={w.param} compress + self decompress",
+            "sign": "sign + L1 norm compress + self decompress"}[w.op]
+
+    def timed(threads, m, reps, budget_s):
+        torch.set_num_threads(threads)
+        run = make(m)
+        run()  # warm-up
+        ts = []
+        stop = time.perf_counter() + budget_s
+        while len(ts) < reps and (not ts or time.perf_counter() < stop):
+            t0 = time.perf_counter()
+            run()
+            ts.append(time.perf_counter() - t0)
+        med = statistics.median(ts)
+        return {"threads": threads, "n": m, "value": round(4 * m / med / 1e9, 4), "ms": round(med * 1e3, 1),
+                "reps": len(ts)}
+
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    big = min(w.n, 100_000_000)
+    small = min(w.n, 25_000_000)
+    rows = [timed(usable, big, 3, 20.0), timed(1, small, 2, 10.0)]
+    if (os.cpu_count() or usable) != usable:
+        rows.append(timed(os.cpu_count(), small, 2, 10.0))
+    main = rows[0]
+    return {"value": main["value"], "unit": "GB/s", "cores": usable, "kind": "port",
+            "sample": f"first {big} elements of the delta, {what}; median of {main['reps']} after 1 warm-up, "
+                      f"{main['ms']} ms each; rows: 1 thread and os.cpu_count() threads on {small} elements",
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(), "usable_cpus": usable, "rows": rows}
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    import torch
+    import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local % ndev)
+    dev = torch.device("cuda", local % ndev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
     from chocosgd_amd import _lib, codec
     if args.lib:
         _lib.load(args.lib)
     codec.lib()
     w = Worker(args, rank, world, dev)
+    comp_k, dec_k = STAGES[w.op]
 
     def barrier():
         torch.cuda.synchronize()
@@ -251,23 +377,31 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    if args.diag_evict:
-        junk = torch.ones(256 * 1024 * 1024, device=dev)
-        sink = torch.empty(1, device=dev)
-        inner = w.step
+    def stage_times(steps):
+        out = {}
+        for name in comp_k + dec_k:
+            t, c = codec.profile_read(name)
+            if c:
+                out[name] = (t / steps * 1e3, t / c * 1e3, c / steps)  # us per step, us per launch, launches/step
+        return out
 
-        def evicting_step():
-            inner()
-            torch.sum(junk, dim=0, keepdim=True, out=sink)
-        w.step = evicting_step
-    for _ in range(args.warmup):
+    # warm-up; its last steps time every kernel to find the dominant stage
+    codec.profile_reset()
+    for i in range(args.warmup):
+        codec.profile_enable(i >= args.warmup // 2)
         w.step()
     barrier()
-    # Only the dominant kernel's launches carry timing events inside the timed
-    # region: each event pair costs ~3 us of GPU time per launch (measured: all
-    # four kernels timed made the top-k step 13 us slower).
+    codec.profile_enable(False)
+    nw = args.warmup - args.warmup // 2
+    pre = stage_times(max(nw, 1))
+    t_comp = sum(pre[k][0] for k in comp_k if k in pre)
+    t_dec = sum(pre[k][0] for k in dec_k if k in pre)
+    dom_name, dom_k = ("decompress", dec_k) if t_dec > t_comp else ("compress", comp_k)
+
+    # timed region: only the dominant stage's kernels carry events (each event pair
+    # costs ~3 us of GPU time)
     codec.profile_reset()
-    codec.profile_filter(w.kernel)
+    codec.profile_filter(dom_k)
     codec.profile_enable(not args.no_kernel_events)
     barrier()
     t0 = time.perf_counter()
@@ -276,61 +410,96 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     codec.profile_enable(False)
-    ktot, kcnt = codec.profile_read(w.kernel)
-    # the other kernels of the step: an untimed pass with every launch timed
+    timed = stage_times(args.steps)
+
+    # untimed pass: every kernel, plus the exchange on its own events
     codec.profile_reset()
     codec.profile_filter(None)
     codec.profile_enable(True)
-    for _ in range(min(args.steps, 10)):
-        w.step()
+    npass = min(args.steps, 10)
+    ex_ms = []
+    for _ in range(npass):
+        w.compress()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        w.exchange()
+        e1.record()
+        w.decompress()
+        ex_ms.append((e0, e1))
     barrier()
     codec.profile_enable(False)
-    kernels = {}
-    for name in ("topk_stream", "topk_finish", "sparse_accumulate", "qsgd_norm", "qsgd_quantize", "qsgd_accumulate", "sign_pack",
-                 "sign_accumulate"):
-        t, c = (ktot, kcnt) if name == w.kernel else codec.profile_read(name)
-        if c:
-            kernels[name] = round(t / c * 1e3, 2)  # us per launch
+    untimed = stage_times(npass)
+    exchange_us = statistics.median(a.elapsed_time(b) * 1e3 for a, b in ex_ms) if w.peers else 0.0
+    granule = w.granule_bytes_decompress()
+
     t_max = elapsed
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
     ms_per_step = t_max / args.steps * 1e3
     value = world * 4 * w.n * args.steps / t_max / 1e9
     if rank == 0:
-        avg_s = ktot / max(kcnt, 1) / 1e3
-        achieved = w.kernel_bytes() / avg_s / 1e9 if kcnt else None
+        comp_b, dec_b, bytes_note = w.stage_bytes()
+
+        def stage_entry(name, kernels, nbytes, src):
+            us = sum(src[k][0] for k in kernels if k in src)
+            if us <= 0:
+                return None
+            ach = nbytes / (us * 1e-6) / 1e9
+            e = {"stage": name, "kernels": {k: {"us_per_launch": round(src[k][1], 2),
+                                                "launches_per_step": round(src[k][2], 2)}
+                                            for k in kernels if k in src},
+                 "us_per_step": round(us, 2), "algorithmic_bytes": nbytes, "achieved": round(ach, 1),
+                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}
+            return e
+
+        in_timed = {k: timed[k] for k in dom_k if k in timed}
+        src_comp = in_timed if dom_name == "compress" and in_timed else untimed
+        src_dec = in_timed if dom_name == "decompress" and in_timed else untimed
+        stages = [stage_entry("compress", comp_k, comp_b, src_comp), stage_entry("decompress", dec_k, dec_b, src_dec)]
+        stages = [s for s in stages if s]
+        if granule and len(stages) > 1:
+            s = stages[-1]
+            s["granule_bytes"] = granule
+            s["granule_achieved"] = round(granule / (s["us_per_step"] * 1e-6) / 1e9, 1)
+            s["granule_note"] = "every touched 64-B segment of x_hat / memory read + written whole, + messages"
+        dom = next((s for s in stages if s["stage"] == dom_name), stages[0] if stages else None)
         traffic = None
         tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(tf):
-            entry = json.load(open(tf)).get(f"{args.workload}:{w.n}")
-            traffic = int(entry["bytes"]) if entry else None
+        if os.path.exists(tf) and dom:
+            with open(tf) as f:
+                tab = json.load(f)
+            ks = [f"{k}:{args.workload}:{w.n}" for k in dom["kernels"]]
+            if all(k in tab for k in ks):
+                traffic = int(sum(tab[k]["bytes"] for k in ks))
+        roofline = None
+        if dom:
+            roofline = {"bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": dom["frac"], "traffic": traffic, "stage": dom["stage"],
+                        "kernels": sorted(dom["kernels"]), "kernel_us": dom["us_per_step"],
+                        "algorithmic_bytes_per_launch": dom["algorithmic_bytes"],
+                        "timed_in": "timed region (dispatch-attached events)" if in_timed else "untimed pass"}
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": {"topk": "topk_k1pct_per_worker", "topk25m": "topk_k1pct_25M",
-                                    "qsgd": "qsgd_q4_per_worker", "sign": "sign_norm_per_worker"}[args.workload],
-                       "n_per_worker": w.n, "k_per_worker": w.k,
+            "config": {"workload": w.label, "n_per_worker": w.n, "k_per_worker": w.k,
                        "graph": "self" if world == 1 else ("complete" if world == 2 else "ring"),
+                       "messages_per_step": len(w.ranks), "backend": args.backend if world > 1 else None,
                        "step": "compress+exchange+decompress-accumulate", "parallelism": f"gossip{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": traffic, "kernel": w.kernel, "kernel_us": round(avg_s * 1e6, 2),
-                         "algorithmic_bytes_per_launch": w.kernel_bytes()},
-            "kernels_us": kernels,
-            "kernels_note": "dispatch-attached HIP events: the dominant kernel inside the timed region (only its "
-                            "launches carry events there), the others in an untimed pass after it",
+            "roofline": roofline,
+            "stages": stages,
+            "stage_bytes_note": bytes_note,
+            "kernels_us": {k: round(v[1], 2) for k, v in untimed.items()},
+            "exchange_us": round(exchange_us, 1),
             "e2e": None,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_e2e:
             out["e2e"] = e2e_rate(w)
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count())
-            out["cpu_baseline"] = cpu_baseline(w, threads)
+            out["cpu_baseline"] = cpu_baseline(w)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

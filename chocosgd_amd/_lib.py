@@ -31,8 +31,10 @@ SIGNATURES = {
     "choco_topk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _p_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_randk_workspace_size": (_c_sz, [_c_i64]),
     "choco_randk_compress": (_c_i32, [_vp, _vp, _c_i64, _c_i64, _c_u64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
+    "choco_randk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _p_i64, _c_i32, _c_u64, _c_i32, _vp, _vp, _vp,
+                                                _c_sz, _vp]),
     "choco_gather": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_f32, _vp, _vp]),
-    "choco_sparse_accumulate": (_c_i32, [_vp, _vp, _c_i64, _vp, _vp, _c_f32, _vp]),
+    "choco_sparse_accumulate": (_c_i32, [_vp, _vp, _c_i64, _vp, _vp, _c_i64, _c_f32, _vp, _vp]),
     "choco_sign_words": (_c_i64, [_c_i64]),
     "choco_sign_workspace_size": (_c_sz, [_c_i32]),
     "choco_sign_compress": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),

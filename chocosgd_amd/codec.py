@@ -106,6 +106,7 @@ class SegmentPlan:
         for s in self.seg_lens:
             offs.append(offs[-1] + s)
         self.seg_off = offs
+        self.n = offs[-1]
         p_off, self._off_keep = _lib.i64_array(offs)
         self._plan_host = (ctypes.c_int64 * (4 * self.nseg))()
         self.plan_host = ctypes.cast(self._plan_host, ctypes.POINTER(ctypes.c_int64))
@@ -116,15 +117,41 @@ class SegmentPlan:
         self.k_per_seg = [int(self._plan_host[4 * s + 2]) for s in range(self.nseg)]
         self.plan_dev = torch.tensor(list(self._plan_host), dtype=torch.int64, device=device)
         self.ws_bytes = int(L.choco_topk_segmented_workspace_size(self.plan_host, self.nseg))
+        self._base = None
+
+    def selected_base(self):
+        """int32[K]: the segment start of every output slot (global -> local index)."""
+        if self._base is None:
+            offs = torch.tensor(self.seg_off[:-1], dtype=torch.int32, device=self.plan_dev.device)
+            ks = torch.tensor(self.k_per_seg, dtype=torch.int64, device=self.plan_dev.device)
+            self._base = torch.repeat_interleave(offs, ks)
+        return self._base
 
 
-def topk_segmented(x, plan, xhat=None):
+def _seg_outputs(x, xhat, plan, out):
     _require(x, torch.float32, "x")
+    if x.numel() != plan.n:
+        raise RuntimeError(f"x holds {x.numel()} elements, the segment plan {plan.n}")
     if xhat is not None:
         _require(xhat, torch.float32, "xhat")
+        if xhat.numel() != x.numel():
+            raise RuntimeError("x and xhat must have the same number of elements")
+    if out is not None:
+        vals, idx = out
+        _require(vals, torch.float32, "out values")
+        _require(idx, torch.int32, "out indices")
+        if vals.numel() != plan.k_total or idx.numel() != plan.k_total:
+            raise RuntimeError("out buffers must hold exactly the plan's K elements")
+        return vals, idx
+    return (torch.empty(plan.k_total, dtype=torch.float32, device=x.device),
+            torch.empty(plan.k_total, dtype=torch.int32, device=x.device))
+
+
+def topk_segmented(x, plan, xhat=None, out=None):
+    """Per-segment top-k (k_s of the plan), GLOBAL int32 indices; `out=(values, indices)`
+    writes into caller buffers (e.g. the two halves of a wire message)."""
+    vals, idx = _seg_outputs(x, xhat, plan, out)
     dev = x.device
-    vals = torch.empty(plan.k_total, dtype=torch.float32, device=dev)
-    idx = torch.empty(plan.k_total, dtype=torch.int32, device=dev)
     L = lib()
     ws = workspace(dev, "topk", plan.ws_bytes)
     _lib.check(L.choco_topk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
@@ -150,6 +177,20 @@ def randk(x, k, seed, is_biased=True, xhat=None):
     return vals, idx
 
 
+def randk_segmented(x, plan, seed, is_biased=True, xhat=None, out=None):
+    """Per-segment random-k over a SegmentPlan (k_s as top-k's), one batched call:
+    segment s ranked by the seeded hash with seed seg_seed(seed, s); GLOBAL indices."""
+    vals, idx = _seg_outputs(x, xhat, plan, out)
+    dev = x.device
+    L = lib()
+    ws = workspace(dev, "topk", plan.ws_bytes)
+    _lib.check(L.choco_randk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
+                                                plan.nseg, int(seed) & (2**64 - 1), 1 if is_biased else 0,
+                                                _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(), _stream(dev)),
+               "choco_randk_compress_segmented")
+    return vals, idx
+
+
 def gather(x, idx, scale=1.0, xhat=None):
     _require(x, torch.float32, "x")
     _require(idx, torch.int64, "idx")
@@ -159,14 +200,56 @@ def gather(x, idx, scale=1.0, xhat=None):
     return out
 
 
-def sparse_accumulate(values, indices, memory, weight, xhat_self=None):
+class IndexGuard:
+    """Lazy check of the out-of-range index count that the sparse accumulate
+    keeps in a device word (include/choco_codec.h): `arm()` queues a
+    non-blocking copy of the word to pinned host memory behind the launches;
+    `check()` raises RuntimeError -- the reference's index_put raises
+    IndexError -- once that copy has landed with a nonzero count.  No host
+    synchronisation on the hot path."""
+
+    def __init__(self, device):
+        self.device = device
+        self.word = torch.zeros(1, dtype=torch.int32, device=device)
+        self.host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self.event = None
+
+    def arm(self):
+        self.host.copy_(self.word, non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record(torch.cuda.current_stream(self.device))
+
+    def check(self, wait=False):
+        if self.event is None:
+            return
+        if wait:
+            self.event.synchronize()
+        elif not self.event.query():
+            return
+        self.event = None
+        bad = int(self.host.item())
+        if bad:
+            self.word.zero_()
+            raise RuntimeError(f"sparse accumulate: {bad} received indices out of range or not ascending (corrupt message "
+                               "or a peer with a different parameter layout)")
+
+
+def sparse_accumulate(values, indices, memory, weight, xhat_self=None, guard=None):
+    """x_hat[idx] += v (xhat_self given); memory[idx] += weight * v.  Indices
+    outside memory are skipped and counted into `guard` (an IndexGuard)."""
     _require(values, torch.float32, "values")
     _require(indices, torch.int32, "indices")
     _require(memory, torch.float32, "memory")
+    if indices.numel() != values.numel():
+        raise RuntimeError("values and indices must have the same length")
     if xhat_self is not None:
         _require(xhat_self, torch.float32, "xhat_self")
+        if xhat_self.numel() != memory.numel():
+            raise RuntimeError("xhat_self and memory must have the same length")
     _lib.check(lib().choco_sparse_accumulate(_ptr(values), _ptr(indices), values.numel(), _ptr(xhat_self),
-                                             _ptr(memory), float(weight), _stream(memory.device)),
+                                             _ptr(memory), memory.numel(), float(weight),
+                                             _ptr(guard.word) if guard is not None else ctypes.c_void_p(0),
+                                             _stream(memory.device)),
                "choco_sparse_accumulate")
 
 
@@ -201,26 +284,58 @@ def sign_unpack(packed, n):
     return out
 
 
+MAX_FUSED_MSGS = 8  # messages one fused accumulate launch takes (sign.hip kMaxMsg, qsgd.hip kQMaxMsg)
+
+
+def _msg_chunks(nmsg, self_slot):
+    """Consecutive chunks of <= MAX_FUSED_MSGS messages, in order, with the local
+    slot re-based into its chunk (-1 elsewhere).  memory is updated message by
+    message, so chunked launches give the same fp32 sequence as one launch."""
+    for c0 in range(0, nmsg, MAX_FUSED_MSGS):
+        c1 = min(nmsg, c0 + MAX_FUSED_MSGS)
+        yield c0, c1, (self_slot - c0) if c0 <= self_slot < c1 else -1
+
+
+def _check_layout(memory, xhat_self, n, seg_off, nseg):
+    if memory.numel() != n:
+        raise RuntimeError(f"memory holds {memory.numel()} elements, the messages describe {n}")
+    if xhat_self is not None:
+        _require(xhat_self, torch.float32, "xhat_self")
+        if xhat_self.numel() != n:
+            raise RuntimeError("xhat_self and memory must have the same length")
+    if nseg > 1:
+        _require(seg_off, torch.int64, "seg_off")
+        if seg_off.numel() != nseg + 1:
+            raise RuntimeError("seg_off must hold nseg + 1 offsets")
+
+
 def sign_accumulate(messages, weights, self_slot, n, memory, xhat_self=None, seg_off=None, nseg=1):
-    """messages: list of (packed int32[N'], norms f32[nseg]) applied in order."""
+    """messages: list of (packed int32[N'], norms f32[nseg]) applied in order; any count
+    (launched in fused chunks of MAX_FUSED_MSGS)."""
     _require(memory, torch.float32, "memory")
+    _check_layout(memory, xhat_self, n, seg_off, nseg)
+    if len(messages) != len(weights):
+        raise RuntimeError("one weight per message")
+    words = sign_words(n)
     for p, nm in messages:
         _require(p, torch.int32, "packed")
         _require(nm, torch.float32, "norms")
-    pp, keep1 = _lib.ptr_array([p.data_ptr() for p, _ in messages])
-    nn, keep2 = _lib.ptr_array([nm.data_ptr() for _, nm in messages])
-    ww, keep3 = _lib.f32_array([float(w) for w in weights])
-    _lib.check(lib().choco_sign_decompress_accumulate(pp, nn, ww, len(messages), int(self_slot), int(n),
-                                                      _ptr(seg_off), int(nseg), _ptr(xhat_self), _ptr(memory),
-                                                      ctypes.c_void_p(0), 0, _stream(memory.device)),
-               "choco_sign_decompress_accumulate")
+        if p.numel() != words or nm.numel() != nseg:
+            raise RuntimeError(f"sign message must hold {words} words and {nseg} norms, got {p.numel()} / "
+                               f"{nm.numel()}")
+    for c0, c1, slot in _msg_chunks(len(messages), int(self_slot)):
+        part = messages[c0:c1]
+        pp, keep1 = _lib.ptr_array([p.data_ptr() for p, _ in part])
+        nn, keep2 = _lib.ptr_array([nm.data_ptr() for _, nm in part])
+        ww, keep3 = _lib.f32_array([float(w) for w in weights[c0:c1]])
+        _lib.check(lib().choco_sign_decompress_accumulate(pp, nn, ww, len(part), slot, int(n), _ptr(seg_off),
+                                                          int(nseg), _ptr(xhat_self if slot >= 0 else None),
+                                                          _ptr(memory), ctypes.c_void_p(0), 0,
+                                                          _stream(memory.device)),
+                   "choco_sign_decompress_accumulate")
 
 
 # ----------------------------------------------------------------------------- QSGD
-def qsgd_levels_bits(quantize_level):
-    return int(quantize_level)
-
-
 def qsgd_packed_bytes(n, q):
     return int(lib().choco_qsgd_packed_bytes(int(n), int(q)))
 
@@ -265,15 +380,29 @@ def qsgd_decode(packed, norms, n, q, is_biased=False, seg_off=None, nseg=1):
 
 def qsgd_accumulate(messages, weights, self_slot, n, q, memory, xhat_self=None, is_biased=False, seg_off=None,
                     nseg=1):
-    """messages: list of (packed uint8, norms f32[nseg]) applied in order."""
+    """messages: list of (packed uint8, norms f32[nseg]) applied in order; any count
+    (launched in fused chunks of MAX_FUSED_MSGS)."""
     _require(memory, torch.float32, "memory")
-    pp, keep1 = _lib.ptr_array([p.data_ptr() for p, _ in messages])
-    nn, keep2 = _lib.ptr_array([nm.data_ptr() for _, nm in messages])
-    ww, keep3 = _lib.f32_array([float(w) for w in weights])
-    _lib.check(lib().choco_qsgd_decompress_accumulate(pp, nn, ww, len(messages), int(self_slot), int(n),
-                                                      _ptr(seg_off), int(nseg), int(q), 1 if is_biased else 0,
-                                                      _ptr(xhat_self), _ptr(memory), _stream(memory.device)),
-               "choco_qsgd_decompress_accumulate")
+    _check_layout(memory, xhat_self, n, seg_off, nseg)
+    if len(messages) != len(weights):
+        raise RuntimeError("one weight per message")
+    nbytes = qsgd_packed_bytes(n, q)
+    for p, nm in messages:
+        _require(p, torch.uint8, "packed")
+        _require(nm, torch.float32, "norms")
+        if p.numel() != nbytes or nm.numel() != nseg:
+            raise RuntimeError(f"QSGD message must hold {nbytes} bytes and {nseg} norms, got {p.numel()} / "
+                               f"{nm.numel()}")
+    for c0, c1, slot in _msg_chunks(len(messages), int(self_slot)):
+        part = messages[c0:c1]
+        pp, keep1 = _lib.ptr_array([p.data_ptr() for p, _ in part])
+        nn, keep2 = _lib.ptr_array([nm.data_ptr() for _, nm in part])
+        ww, keep3 = _lib.f32_array([float(w) for w in weights[c0:c1]])
+        _lib.check(lib().choco_qsgd_decompress_accumulate(pp, nn, ww, len(part), slot, int(n), _ptr(seg_off),
+                                                          int(nseg), int(q), 1 if is_biased else 0,
+                                                          _ptr(xhat_self if slot >= 0 else None), _ptr(memory),
+                                                          _stream(memory.device)),
+                   "choco_qsgd_decompress_accumulate")
 
 
 # ----------------------------------------------------------------------------- gossip
@@ -289,9 +418,11 @@ def profile_enable(on=True):
     lib().choco_profile_enable(1 if on else 0)
 
 
-def profile_filter(name=None):
-    """Time only the launches named `name` (None = all)."""
-    lib().choco_profile_filter(name.encode() if name else None)
+def profile_filter(names=None):
+    """Time only the launches named in `names` (a name or a list; None = all)."""
+    if isinstance(names, (list, tuple)):
+        names = ",".join(names)
+    lib().choco_profile_filter(names.encode() if names else None)
 
 
 def profile_read(name):

@@ -16,19 +16,6 @@ import torch
 import torch.distributed as dist
 
 
-def flatten(tensors, shapes=None, use_cuda=True):
-    from .tensor_buffer import flatten as _flatten
-    return _flatten(tensors, shapes=shapes, use_cuda=use_cuda)
-
-
-def unflatten(tensors, synced_tensors, shapes):
-    pointer = 0
-    for tensor, shape in zip(tensors, shapes):
-        param_size, nelement = shape
-        tensor.data[:] = synced_tensors[pointer:pointer + nelement].view(param_size)
-        pointer += nelement
-
-
 def recover_device(data, device=None):
     return data.to(device) if device is not None else data
 

@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <map>
 #include <mutex>
@@ -39,7 +40,7 @@ static std::atomic<bool> g_prof_on{false};
 static std::mutex g_prof_mu;
 static std::vector<PendingEv> g_pending;
 static std::map<std::string, std::pair<double, int64_t>> g_acc;
-static std::string g_filter;               // only this kernel name is timed ("" = all)
+static std::vector<std::string> g_filter;  // only these kernel names are timed (empty = all)
 static std::vector<hipEvent_t> g_free_ev;  // events are reused: no create/destroy per launch
 
 static thread_local ProfArm g_armed{nullptr, nullptr};
@@ -48,7 +49,7 @@ void profile_begin(const char* name, hipStream_t) {
   g_armed = ProfArm{nullptr, nullptr};
   if (!g_prof_on.load(std::memory_order_relaxed)) return;
   std::lock_guard<std::mutex> g(g_prof_mu);
-  if (!g_filter.empty() && g_filter != name) return;
+  if (!g_filter.empty() && std::find(g_filter.begin(), g_filter.end(), std::string(name)) == g_filter.end()) return;
   PendingEv p{name, nullptr, nullptr, false};  // closed once a launch takes the pair
   for (hipEvent_t* e : {&p.a, &p.b}) {
     if (!g_free_ev.empty()) {
@@ -116,9 +117,16 @@ CHOCO_API int choco_profile_enable(int32_t on) {
   return CHOCO_OK;
 }
 
-CHOCO_API int choco_profile_filter(const char* name) {
+CHOCO_API int choco_profile_filter(const char* names) {
   std::lock_guard<std::mutex> g(g_prof_mu);
-  g_filter = name ? name : "";
+  g_filter.clear();
+  std::string all = names ? names : "";
+  size_t p = 0;
+  while (p <= all.size()) {
+    const size_t q = std::min(all.find(',', p), all.size());
+    if (q > p) g_filter.push_back(all.substr(p, q - p));
+    p = q + 1;
+  }
   return CHOCO_OK;
 }
 

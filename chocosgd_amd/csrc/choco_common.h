@@ -68,6 +68,7 @@ ProfArm profile_take();
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+inline bool aligned4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 

@@ -43,18 +43,26 @@ __global__ __launch_bounds__(kEwThreads) void gossip_kernel(float* __restrict__ 
 #define CHOCO_ACC_U 1
 #endif
 constexpr int kAccU = CHOCO_ACC_U;
+// An index outside [0, n) (a corrupt message, or a peer with another layout) is
+// skipped and counted into *bad (nullable) -- the reference's index_put raises
+// IndexError there; the host checks the count lazily (codec.py).
 __global__ __launch_bounds__(kEwThreads) void sparse_acc_kernel(const float* __restrict__ val,
                                                                 const int32_t* __restrict__ idx, int64_t k,
                                                                 float* __restrict__ hat, float* __restrict__ mem,
-                                                                float w) {
+                                                                int64_t n, float w, uint32_t* __restrict__ bad) {
   const int64_t base = (int64_t)blockIdx.x * kEwThreads * kAccU + threadIdx.x;
+  uint32_t nbad = 0;
   if (base + (int64_t)(kAccU - 1) * kEwThreads < k) {
     int64_t j[kAccU];
     float v[kAccU], h[kAccU], m[kAccU];
+    bool ok[kAccU];
 #pragma unroll
     for (int u = 0; u < kAccU; ++u) {
       j[u] = idx[base + u * kEwThreads];
       v[u] = val[base + u * kEwThreads];
+      ok[u] = j[u] >= 0 && j[u] < n;
+      nbad += ok[u] ? 0u : 1u;
+      if (!ok[u]) j[u] = 0;
     }
 #pragma unroll
     for (int u = 0; u < kAccU; ++u) {
@@ -63,19 +71,115 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_kernel(const float* __r
     }
 #pragma unroll
     for (int u = 0; u < kAccU; ++u) {
+      if (!ok[u]) continue;
       if (hat) hat[j[u]] = h[u] + v[u];
       mem[j[u]] = m[u] + w * v[u];
     }
-    return;
+  } else {
+    for (int u = 0; u < kAccU; ++u) {
+      const int64_t i = base + u * kEwThreads;
+      if (i >= k) break;
+      const int64_t jj = idx[i];
+      if (jj < 0 || jj >= n) {
+        ++nbad;
+        continue;
+      }
+      const float vv = val[i];
+      if (hat) hat[jj] = hat[jj] + vv;
+      mem[jj] = mem[jj] + w * vv;
+    }
   }
-  for (int u = 0; u < kAccU; ++u) {
-    const int64_t i = base + u * kEwThreads;
-    if (i >= k) break;
-    const int64_t jj = idx[i];
-    const float vv = val[i];
-    if (hat) hat[jj] = hat[jj] + vv;
-    mem[jj] = mem[jj] + w * vv;
+  if (bad && nbad) atomicAdd(bad, nbad);
+}
+
+// Segment-owner form (default).  A message's indices are strictly ascending
+// (this codec's top-k / random-k wire), so the updates that fall into one
+// 64-B segment of x_hat / memory (16 floats) are consecutive in the message.
+// One QUAD of lanes per update: the quad of the segment's first update (the
+// "leader") loads the whole segment of each target buffer -- lane l4 its
+// float4 l4, so one wave instruction covers 16 segments -- applies every
+// update of that segment, and writes the whole segment back; the other quads
+// idle.  Whole-segment writes: no byte-masked partial writes reach the
+// memory side (a 4-B store dirties a sector that must be merged there).
+// A non-ascending pair (a corrupt message) is counted into *bad like an
+// out-of-range index.
+#ifndef CHOCO_ACC_MODE
+#define CHOCO_ACC_MODE 1
+#endif
+#ifndef CHOCO_ACC_SEGF
+#define CHOCO_ACC_SEGF 16
+#endif
+constexpr int kSegF = CHOCO_ACC_SEGF;  // floats per owned segment (16: 64 B)
+constexpr int kSegL = kSegF / 4;       // lanes per update (one float4 each)
+constexpr int kSegShift = kSegF == 32 ? 5 : (kSegF == 16 ? 4 : 3);
+static_assert((1 << kSegShift) == kSegF, "segment of 8, 16 or 32 floats");
+
+template <bool HS>
+__global__ __launch_bounds__(kEwThreads) void sparse_acc_seg_kernel(const float* __restrict__ val,
+                                                                    const int32_t* __restrict__ idx, int64_t k,
+                                                                    float* __restrict__ hat,
+                                                                    float* __restrict__ mem, int64_t n, float w,
+                                                                    uint32_t* __restrict__ bad) {
+  const int64_t t = (int64_t)blockIdx.x * kEwThreads + threadIdx.x;
+  const int64_t u = t / kSegL;
+  const int l4 = (int)(t % kSegL);
+  uint32_t nbad = 0;
+  if (u < k) {
+    const int64_t j = idx[u];
+    const int64_t jp = u > 0 ? (int64_t)idx[u - 1] : -1;
+    const bool ok = j >= 0 && j < n;
+    const int64_t seg = j >> kSegShift;
+    if (l4 == 0) nbad += (ok ? 0u : 1u) + ((u > 0 && jp >= j) ? 1u : 0u);
+    const bool leader = ok && (u == 0 || jp < 0 || (jp >> kSegShift) != seg);
+    if (leader) {
+      const int64_t base = seg * kSegF + 4 * l4;
+      const bool full = base + 4 <= n;
+      float hv[4] = {0.f, 0.f, 0.f, 0.f}, mv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (full) {
+        const float4 m4 = *reinterpret_cast<const float4*>(mem + base);
+        mv[0] = m4.x; mv[1] = m4.y; mv[2] = m4.z; mv[3] = m4.w;
+        if (HS) {
+          const float4 h4 = *reinterpret_cast<const float4*>(hat + base);
+          hv[0] = h4.x; hv[1] = h4.y; hv[2] = h4.z; hv[3] = h4.w;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (base + c < n) {
+            mv[c] = mem[base + c];
+            if (HS) hv[c] = hat[base + c];
+          }
+        }
+      }
+      int64_t je = j;
+      for (int64_t e = u; e < k && e < u + kSegF; ++e) {
+        if (e != u) je = idx[e];
+        if (je < 0 || je >= n || (je >> kSegShift) != seg) break;
+        const float v = val[e];
+        const int off = (int)(je - base);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (off == c) {
+            if (HS) hv[c] = hv[c] + v;
+            mv[c] = mv[c] + w * v;
+          }
+        }
+      }
+      if (full) {
+        *reinterpret_cast<float4*>(mem + base) = make_float4(mv[0], mv[1], mv[2], mv[3]);
+        if (HS) *reinterpret_cast<float4*>(hat + base) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (base + c < n) {
+            mem[base + c] = mv[c];
+            if (HS) hat[base + c] = hv[c];
+          }
+        }
+      }
+    }
   }
+  if (bad && nbad) atomicAdd(bad, nbad);
 }
 
 __global__ __launch_bounds__(kEwThreads) void gather_kernel(const float* __restrict__ x, const float* __restrict__ xh,
@@ -112,14 +216,25 @@ CHOCO_API int choco_gossip_step(float* x, const float* memory, const float* xhat
 }
 
 CHOCO_API int choco_sparse_accumulate(const float* val, const int32_t* idx, int64_t k, float* xhat_self,
-                                      float* memory, float weight, void* stream) {
+                                      float* memory, int64_t n, float weight, uint32_t* bad_count, void* stream) {
   hipStream_t st = as_stream(stream);
   CHOCO_REQUIRE(val && idx && memory, "null pointer argument");
+  CHOCO_REQUIRE(n > 0, "n must be positive");
   if (k <= 0) return CHOCO_OK;
   profile_begin("sparse_accumulate", st);
-  CHOCO_KLAUNCH(sparse_acc_kernel, dim3((unsigned)((k + (int64_t)kEwThreads * kAccU - 1) / ((int64_t)kEwThreads * kAccU))),
-                dim3(kEwThreads), 0, st, val, idx, k, xhat_self,
-                     memory, weight);
+  if (CHOCO_ACC_MODE == 1 && aligned16(memory) && (!xhat_self || aligned16(xhat_self))) {
+    const unsigned g = (unsigned)((kSegL * k + kEwThreads - 1) / kEwThreads);
+    if (xhat_self)
+      CHOCO_KLAUNCH((sparse_acc_seg_kernel<true>), dim3(g), dim3(kEwThreads), 0, st, val, idx, k, xhat_self, memory,
+                    n, weight, bad_count);
+    else
+      CHOCO_KLAUNCH((sparse_acc_seg_kernel<false>), dim3(g), dim3(kEwThreads), 0, st, val, idx, k, xhat_self,
+                    memory, n, weight, bad_count);
+  } else {
+    CHOCO_KLAUNCH(sparse_acc_kernel,
+                  dim3((unsigned)((k + (int64_t)kEwThreads * kAccU - 1) / ((int64_t)kEwThreads * kAccU))),
+                  dim3(kEwThreads), 0, st, val, idx, k, xhat_self, memory, n, weight, bad_count);
+  }
   profile_end("sparse_accumulate", st);
   CHOCO_LAUNCHED("sparse_acc_kernel");
   return CHOCO_OK;

@@ -295,21 +295,44 @@ __global__ __launch_bounds__(kExactThreads) void topk_exact_kernel(
   block_topk_exact(src, n, k, scale, out_val, out_idx, idx_base, sm);
 }
 
+// k >= n (ratio 0): every element, in index order -- a plain multi-workgroup copy.
+template <bool XH>
+__global__ __launch_bounds__(256) void topk_all_kernel(const float* __restrict__ x, const float* __restrict__ xh,
+                                                      int64_t n, float scale, float* __restrict__ out_val,
+                                                      int32_t* __restrict__ out_idx, int64_t idx_base) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    out_val[i] = (XH ? x[i] - xh[i] : x[i]) * scale;
+    out_idx[i] = (int32_t)(i + idx_base);
+  }
+}
+
+// Per-segment random-k seed (host and device agree; oracle/choco_oracle.py seg_seed):
+// splitmix64 of seed + (s + 1) * golden gamma, so every segment draws an independent
+// ranking (the reference calls np.random.choice once per tensor, sparsification.py:48).
+CHOCO_DEV __host__ inline uint64_t seg_seed(uint64_t seed, int64_t s) {
+  uint64_t z = seed + (uint64_t)(s + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
 // Segmented: plan rows {off, len, k, out_off}; one workgroup per segment that
 // is not routed to the pipeline.
-CHOCO_DEV bool seg_uses_pipeline(int64_t off, int64_t len);
+CHOCO_DEV bool seg_uses_pipeline(int64_t off, int64_t len, int mode);
 
-template <bool XH>
+template <int MODE, bool XH>
 __global__ __launch_bounds__(kExactThreads) void topk_segmented_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ plan,
-    int32_t nseg, float* __restrict__ out_val, int32_t* __restrict__ out_idx) {
+    int32_t nseg, uint64_t seed, int32_t is_biased, float* __restrict__ out_val, int32_t* __restrict__ out_idx) {
   __shared__ ExactSmem sm;
   const int s = blockIdx.x;
   if (s >= nseg) return;
   const int64_t off = plan[4 * s + 0], len = plan[4 * s + 1], k = plan[4 * s + 2], oo = plan[4 * s + 3];
-  if (seg_uses_pipeline(off, len) || len == 0) return;
-  Src<kData, XH> src{x + off, XH ? xh + off : nullptr, 0};
-  block_topk_exact(src, len, k, 1.0f, out_val + oo, out_idx + oo, off, sm);
+  if (seg_uses_pipeline(off, len, MODE) || len == 0) return;
+  Src<MODE, XH> src{x + off, XH ? xh + off : nullptr, MODE == kHash ? seg_seed(seed, s) : 0};
+  const float scale = (MODE == kHash && !is_biased) ? (float)((double)len / (double)k) : 1.0f;
+  block_topk_exact(src, len, k, scale, out_val + oo, out_idx + oo, off, sm);
 }
 
 // ----------------------------------------------------------------------------
@@ -395,11 +418,13 @@ CHOCO_DEV void load_sample(const float* __restrict__ x, const float* __restrict_
                            float4 (&s)[kSampleLoads], float4 (&h)[kSampleLoads]) {
   const int64_t stride4 = ((n - 256) / (kSampleRuns - 1)) >> 2;  // float4 between run starts
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // one 1 KiB buffer resource per run (wave-uniform base): dword-aligned 16-B
+  // buffer loads, so x / xh need only 4-byte alignment (unaligned segments)
 #pragma unroll
   for (int j = 0; j < kSampleLoads; ++j) {
-    const int64_t q = (int64_t)(w * kSampleLoads + j) * stride4 + lane;  // wave w: runs 4w .. 4w+3
-    s[j] = reinterpret_cast<const float4*>(x)[q];
-    if (XH) h[j] = reinterpret_cast<const float4*>(xh)[q];
+    const int64_t run0 = (int64_t)(w * kSampleLoads + j) * stride4 * 4;  // wave w: runs 4w .. 4w+3
+    s[j] = ld_buf4<false>(buf_rsrc(x + run0, 1024u), 16u * (uint32_t)lane);
+    if (XH) h[j] = ld_buf4<false>(buf_rsrc(xh + run0, 1024u), 16u * (uint32_t)lane);
   }
 }
 
@@ -1491,12 +1516,17 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
 // ----------------------------------------------------------------------------
 // host dispatch
 // ----------------------------------------------------------------------------
+// Segments of >= 1M elements take the multi-workgroup pipeline, at any 4-byte
+// alignment: every vector load of x / xhat there is a dword-aligned buffer load.
 constexpr int64_t kPipeMinSeg = 1 << 20;
-CHOCO_DEV bool seg_uses_pipeline(int64_t off, int64_t len) {
-  return len >= kPipeMinSeg && (off & 3) == 0;
+CHOCO_DEV bool seg_uses_pipeline(int64_t off, int64_t len, int mode) {
+  (void)off;
+  (void)mode;
+  return len >= kPipeMinSeg;
 }
 static bool host_seg_uses_pipeline(int64_t off, int64_t len) {
-  return len >= kPipeMinSeg && (off & 3) == 0;
+  (void)off;
+  return len >= kPipeMinSeg;
 }
 
 size_t topk_ws_bytes(int64_t n) { return n > kSmallN ? topk_layout(n).total : 256; }
@@ -1505,9 +1535,19 @@ template <int MODE, bool XH>
 static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                        float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes,
                        hipStream_t st) {
-  if (n <= kSmallN || k >= n) {
+  if (k >= n) {
+    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+    profile_begin("topk_all", st);
+    CHOCO_KLAUNCH((topk_all_kernel<XH>), dim3(g), dim3(256), 0, st, x, xh, n, scale, out_val, out_idx, idx_base);
+    profile_end("topk_all", st);
+    CHOCO_LAUNCHED("topk_all_kernel");
+    return CHOCO_OK;
+  }
+  if (n <= kSmallN) {
+    profile_begin("topk_exact", st);
     CHOCO_KLAUNCH((topk_exact_kernel<MODE, XH>), dim3(1), dim3(kExactThreads), 0, st, x, xh, n, k,
                        seed, scale, out_val, out_idx, idx_base);
+    profile_end("topk_exact", st);
     CHOCO_LAUNCHED("topk_exact_kernel");
     return CHOCO_OK;
   }
@@ -1538,7 +1578,9 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
     CHOCO_REQUIRE(hipMemsetAsync(ctrl, 0, sizeof(TopkCtrl), st) == hipSuccess, "hipMemsetAsync failed");
   }
   if (MODE == kData) {
+    profile_begin("topk_bounds", st);
     CHOCO_KLAUNCH((topk_bounds_kernel<XH>), dim3(1), dim3(kK1Threads), 0, st, x, xh, n, sample_ranks(n, k), ctrl);
+    profile_end("topk_bounds", st);
     CHOCO_LAUNCHED("topk_bounds_kernel");
   }
   profile_begin("topk_stream", st);
@@ -1561,10 +1603,7 @@ static int dispatch_topk(const float* x, const float* xh, int64_t n, int64_t k, 
   CHOCO_REQUIRE(x != nullptr && out_val != nullptr && out_idx != nullptr, "null pointer argument");
   CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n must be in [1, 2^31-1), got %lld", (long long)n);
   CHOCO_REQUIRE(k >= 1 && k <= n, "k must be in [1, n], got k=%lld n=%lld", (long long)k, (long long)n);
-  if (n > kSmallN && k < n) {
-    CHOCO_REQUIRE(aligned16(x) && (xh == nullptr || aligned16(xh)),
-                  "x/xhat must be 16-byte aligned for n > %lld", (long long)kSmallN);
-  }
+  CHOCO_REQUIRE(aligned4(x) && (xh == nullptr || aligned4(xh)), "x/xhat must be 4-byte aligned");
   if (xh) return launch_topk<MODE, true>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st);
   return launch_topk<MODE, false>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st);
 }
@@ -1624,31 +1663,54 @@ CHOCO_API size_t choco_topk_segmented_workspace_size(const int64_t* plan_host, i
   return need;
 }
 
-CHOCO_API int choco_topk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
-                                            const int64_t* plan_host, int32_t nseg, float* out_val,
-                                            int32_t* out_idx, void* ws, size_t ws_bytes, void* stream) {
-  hipStream_t st = as_stream(stream);
+template <int MODE>
+static int segmented(const float* x, const float* xhat, const int64_t* plan_dev, const int64_t* plan_host,
+                     int32_t nseg, uint64_t seed, int32_t is_biased, float* out_val, int32_t* out_idx, void* ws,
+                     size_t ws_bytes, hipStream_t st) {
   CHOCO_REQUIRE(x && plan_dev && plan_host && out_val && out_idx && nseg > 0, "null pointer argument");
-  CHOCO_REQUIRE(aligned16(x) && (xhat == nullptr || aligned16(xhat)), "x/xhat must be 16-byte aligned");
+  CHOCO_REQUIRE(aligned4(x) && (xhat == nullptr || aligned4(xhat)), "x/xhat must be 4-byte aligned");
   const int64_t ntot = plan_host[4 * (nseg - 1)] + plan_host[4 * (nseg - 1) + 1];
   CHOCO_REQUIRE(ntot < (int64_t)INT32_MAX, "total length must be < 2^31");
+  bool any_small = false;
+  for (int s = 0; s < nseg; ++s) any_small |= !host_seg_uses_pipeline(plan_host[4 * s], plan_host[4 * s + 1]);
   // every segment that is not pipelined: one workgroup each, one launch
-  if (xhat)
-    CHOCO_KLAUNCH((topk_segmented_kernel<true>), dim3(nseg), dim3(kExactThreads), 0, st, x, xhat,
-                       plan_dev, nseg, out_val, out_idx);
-  else
-    CHOCO_KLAUNCH((topk_segmented_kernel<false>), dim3(nseg), dim3(kExactThreads), 0, st, x, xhat,
-                       plan_dev, nseg, out_val, out_idx);
-  CHOCO_LAUNCHED("topk_segmented_kernel");
+  if (any_small) {
+    profile_begin("topk_segmented", st);
+    if (xhat)
+      CHOCO_KLAUNCH((topk_segmented_kernel<MODE, true>), dim3(nseg), dim3(kExactThreads), 0, st, x, xhat,
+                    plan_dev, nseg, seed, is_biased, out_val, out_idx);
+    else
+      CHOCO_KLAUNCH((topk_segmented_kernel<MODE, false>), dim3(nseg), dim3(kExactThreads), 0, st, x, xhat,
+                    plan_dev, nseg, seed, is_biased, out_val, out_idx);
+    profile_end("topk_segmented", st);
+    CHOCO_LAUNCHED("topk_segmented_kernel");
+  }
   for (int s = 0; s < nseg; ++s) {
     const int64_t off = plan_host[4 * s], len = plan_host[4 * s + 1], k = plan_host[4 * s + 2],
                   oo = plan_host[4 * s + 3];
     if (!host_seg_uses_pipeline(off, len)) continue;
-    int rc = dispatch_topk<kData>(x + off, xhat ? xhat + off : nullptr, len, k, 0, 1.0f, out_val + oo,
-                                  out_idx + oo, off, ws, ws_bytes, st);
+    const uint64_t sd = MODE == kHash ? seg_seed(seed, s) : 0;
+    const float scale = (MODE == kHash && !is_biased) ? (float)((double)len / (double)k) : 1.0f;
+    int rc = dispatch_topk<MODE>(x + off, xhat ? xhat + off : nullptr, len, k, sd, scale, out_val + oo,
+                                 out_idx + oo, off, ws, ws_bytes, st);
     if (rc) return rc;
   }
   return CHOCO_OK;
+}
+
+CHOCO_API int choco_topk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
+                                            const int64_t* plan_host, int32_t nseg, float* out_val,
+                                            int32_t* out_idx, void* ws, size_t ws_bytes, void* stream) {
+  return segmented<kData>(x, xhat, plan_dev, plan_host, nseg, 0, 1, out_val, out_idx, ws, ws_bytes,
+                          as_stream(stream));
+}
+
+CHOCO_API int choco_randk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
+                                             const int64_t* plan_host, int32_t nseg, uint64_t seed,
+                                             int32_t is_biased, float* out_val, int32_t* out_idx, void* ws,
+                                             size_t ws_bytes, void* stream) {
+  return segmented<kHash>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, ws, ws_bytes,
+                          as_stream(stream));
 }
 
 #if CHOCO_STAMPS

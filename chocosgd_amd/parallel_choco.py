@@ -141,52 +141,67 @@ class _CHOCOBase(object):
 
 
 class CHOCOSparsificationCompressor(_CHOCOBase):
-    """top-k / random-k  (parallel_choco_v.py:189-332)."""
+    """top-k / random-k  (parallel_choco_v.py:189-332).
+
+    compress writes values and GLOBAL int32 indices straight into the wire
+    message [fp32 values | int32 indices]; `flatten_selected_indices` holds the
+    reference's LOCAL per-tensor indices (parallel_choco_v.py:248-249), derived
+    from the wire with the plan's cached segment starts."""
+
+    def __init__(self, *args, **kargs):
+        super().__init__(*args, **kargs)
+        self._guards = {}
 
     def compress(self, sync_buffer):
         x, xh, lay = self._flat_inputs(sync_buffer)
+        plan = lay.topk_plan(float(self.compress_ratio))
+        K = plan.k_total
+        message = torch.empty(2 * K, dtype=torch.int32, device=x.device)
+        values, indices = message[:K].view(torch.float32), message[K:]
         if "top_k" in self.comm_op:
-            plan = lay.topk_plan(float(self.compress_ratio))
-            values, indices = codec.topk_segmented(x, plan, xhat=xh)
-            selected_shapes = list(plan.k_per_seg)
+            codec.topk_segmented(x, plan, xhat=xh, out=(values, indices))
         elif "random_k" in self.comm_op:
-            vals, idxs, selected_shapes = [], [], []
-            for s in range(lay.nseg):
-                a, b = lay.seg_off_list[s], lay.seg_off_list[s + 1]
-                k = codec.topk_k(b - a, self.compress_ratio)
-                v, i = codec.randk(x[a:b], k, _draw_seed(), is_biased=True, xhat=xh[a:b])
-                vals.append(v)
-                idxs.append(i + a)
-                selected_shapes.append(k)
-            values, indices = torch.cat(vals), torch.cat(idxs).to(torch.int32)
+            # the reference never forwards is_biased to get_random_k (sparsification.py:60)
+            codec.randk_segmented(x, plan, _draw_seed(), is_biased=True, xhat=xh, out=(values, indices))
         else:
             raise NotImplementedError
+        selected_shapes = list(plan.k_per_seg)
+        local = torch.sub(indices, plan.selected_base())
         sync_buffer["selected_shapes"] = selected_shapes
         sync_buffer["flatten_selected_values"] = TensorBuffer.from_flat(values, [(k,) for k in selected_shapes])
-        sync_buffer["flatten_selected_indices"] = TensorBuffer.from_flat(indices, [(k,) for k in selected_shapes])
+        sync_buffer["flatten_selected_indices"] = TensorBuffer.from_flat(local, [(k,) for k in selected_shapes])
+        sync_buffer["wire_message"] = message
         # nominal bits as in parallel_choco_v.py:252-254 (32-bit values + 32-bit indices)
-        sync_buffer["n_bits"] = get_n_bits(values) + get_n_bits(indices)
+        sync_buffer["n_bits"] = get_n_bits(values) + get_n_bits(local)
 
     def sync(self, sync_buffer):
-        values = sync_buffer["flatten_selected_values"].buffer
-        indices = sync_buffer["flatten_selected_indices"].buffer
-        message = torch.cat([values.view(torch.int32), indices])
+        message = sync_buffer["wire_message"]
         reqs, synced = self._send(sync_buffer, message)
         sync_buffer["sync_reqs"] = reqs
         sync_buffer["synced_message"] = synced
         sync_buffer["sycned_message_size"] = len(message)
 
+    def _guard(self, device):
+        g = self._guards.get(device)
+        if g is None:
+            g = self._guards[device] = codec.IndexGuard(device)
+        return g
+
     def uncompress(self, sync_buffer, neighbor_hat_params, neighbors_info):
         self.aggregator_fn.complete_wait(sync_buffer["sync_reqs"])
         K = int(sync_buffer["sycned_message_size"] / 2)
         memory = neighbor_hat_params["memory"]
+        guard = self._guard(memory.buffer.device)
+        guard.check()  # out-of-range indices of an EARLIER step (lazy, no sync)
         for rank, weight in neighbors_info.items():
             hat_params = neighbor_hat_params[rank if rank in neighbor_hat_params else "memory"]
             msg = recover_device(sync_buffer["synced_message"][rank], device=hat_params.buffer.device)
             q_values = msg[:K].view(torch.float32)
             q_indices = msg[K:]
             codec.sparse_accumulate(q_values, q_indices, memory.buffer, weight,
-                                    xhat_self=hat_params.buffer if rank in neighbor_hat_params else None)
+                                    xhat_self=hat_params.buffer if rank in neighbor_hat_params else None,
+                                    guard=guard)
+        guard.arm()
 
 
 class CHOCOQuantizationCompressor(_CHOCOBase):
@@ -262,6 +277,11 @@ class CHOCOSignCompressor(_CHOCOBase):
         sync_buffer["sync_reqs_1"] = reqs
         sync_buffer["sync_reqs_2"] = []
         sync_buffer["synced_message"] = synced
+        # the reference's two received dicts (parallel_choco_v.py:521-522), as views of
+        # the one message per rank: [fp32 norms (16-B padded) | int32 words]
+        nseg = norms.numel()
+        sync_buffer["synced_flatten_norms"] = {r: m[:hw].view(torch.float32)[:nseg] for r, m in synced.items()}
+        sync_buffer["synced_signs"] = {r: m[hw:] for r, m in synced.items()}
 
     def uncompress(self, sync_buffer, neighbor_hat_params, neighbors_info):
         self.aggregator_fn.complete_wait(sync_buffer["sync_reqs_1"])
@@ -273,15 +293,10 @@ class CHOCOSignCompressor(_CHOCOBase):
         weights = [neighbors_info[r] for r in ranks]
         self_slot = self._self_slot(ranks, neighbor_hat_params)
         xhat_self = neighbor_hat_params[ranks[self_slot]].buffer if self_slot >= 0 else None
-        hw = _hdr_words(lay.nseg)
-        parts, norms_by_rank, signs_by_rank = [], {}, {}
+        parts = []
         for r in ranks:
-            m = recover_device(sync_buffer["synced_message"][r], device=dev)
-            nm = m[:hw].view(torch.float32)[:lay.nseg].contiguous()
-            sg = m[hw:]
-            norms_by_rank[r], signs_by_rank[r] = nm, sg
+            nm = recover_device(sync_buffer["synced_flatten_norms"][r], device=dev).contiguous()
+            sg = recover_device(sync_buffer["synced_signs"][r], device=dev)
             parts.append((sg, nm))
-        sync_buffer["synced_flatten_norms"] = norms_by_rank
-        sync_buffer["synced_signs"] = signs_by_rank
         codec.sign_accumulate(parts, weights, self_slot, lay.n, memory.buffer, xhat_self=xhat_self,
                               seg_off=lay.seg_off, nseg=lay.nseg)

@@ -98,13 +98,30 @@ int choco_randk_compress(const float* x, const float* xhat, int64_t n, int64_t k
 int choco_gather(const float* x, const float* xhat, const int64_t* idx, int64_t k,
                  float scale, float* out_val, void* stream);
 
+/* Per-segment random-k (CHOCOSparsificationCompressor.compress with
+ * comm_op "random_k", parallel_choco_v.py:229-260 -> sparsification.py:40-54 per
+ * tensor): the plan of choco_topk_segmented_plan (k_s = max(1, int(len_s*(1-ratio)))),
+ * segment s ranked by the hash with seed seg_seed(seed, s) (splitmix64 of
+ * seed + (s+1) * 0x9E3779B97F4A7C15), outputs concatenated in segment order with
+ * GLOBAL indices.  Any 4-byte alignment; workspace:
+ * choco_topk_segmented_workspace_size. */
+int choco_randk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
+                                   const int64_t* plan_host, int32_t nseg,
+                                   uint64_t seed, int32_t is_biased,
+                                   float* out_val, int32_t* out_idx,
+                                   void* ws, size_t ws_bytes, void* stream);
+
 /* Receiver side of CHOCOSparsificationCompressor.uncompress
  * (parallel_choco_v.py:307-310): for one message (val, idx) of k pairs,
  *   if xhat_self != NULL:  xhat_self[idx] += val
  *   memory[idx] += (float)weight * val        (two roundings, as torch does)
- * Indices within one message must be unique (true for top-k / random-k). */
+ * Indices within one message must be unique (true for top-k / random-k).
+ * n = length of xhat_self / memory: an index outside [0, n) is skipped and
+ * counted into *bad_count (device uint32, nullable) -- the reference's
+ * index_put raises IndexError there. */
 int choco_sparse_accumulate(const float* val, const int32_t* idx, int64_t k,
-                            float* xhat_self, float* memory, float weight, void* stream);
+                            float* xhat_self, float* memory, int64_t n, float weight,
+                            uint32_t* bad_count, void* stream);
 
 /* --------------------------------------------------------------- sign
  * Replaces SignCompressor.packing (sparsification.py:129-145, incl. the external
@@ -196,8 +213,9 @@ int choco_profile_enable(int32_t on);
 /* Accumulated (sum of ms, count) of the named kernel since the last reset,
  * after synchronising its events.  Names: "topk_stream", "sign_pack",
  * "qsgd_quantize", "sparse_accumulate", ... */
-// Time only the launches named `name` (NULL or "" = all); events are reused.
-int choco_profile_filter(const char* name);
+/* Time only the launches whose name is in the comma-separated list `names`
+ * (NULL or "" = all); events are reused. */
+int choco_profile_filter(const char* names);
 int choco_profile_read(const char* name, double* total_ms, int64_t* count);
 int choco_profile_reset(void);
 

@@ -4,6 +4,7 @@ The reference never travels to the GPU box, so the CPU baseline that bench.py
 times next to the GPU numbers is this restatement of the reference's own torch
 op sequences, run with torch on the host cores:
   top-k     : SparsificationCompressor.get_top_k        (sparsification.py:18-31)
+  random-k  : SparsificationCompressor.get_random_k     (sparsification.py:40-54)
               + receiver x_hat[idx] += v; memory[idx] += w * v
                                                          (parallel_choco_v.py:307-310)
   QSGD      : QuantizationCompressor.get_qsgd           (sparsification.py:87-98)
@@ -25,6 +26,17 @@ def topk_compress(d, ratio):
     else:
         _, idx = torch.topk(x_data.abs(), top_k, largest=True, sorted=False)
     return x_data[idx], idx
+
+
+def randk_compress(d, ratio):
+    """SparsificationCompressor.get_random_k (sparsification.py:40-54), biased branch."""
+    import numpy as np
+    x_data = d.view(-1)
+    x_len = x_data.nelement()
+    top_k = max(1, int(x_len * (1 - ratio)))
+    selected_indices = np.random.choice(x_len, top_k, replace=False)
+    selected_indices = torch.LongTensor(selected_indices)
+    return x_data[selected_indices], selected_indices
 
 
 def sparse_decompress(hat, mem, values, idx, weight):

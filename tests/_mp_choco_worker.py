@@ -1,0 +1,98 @@
+"""Multi-process CHOCO gossip round for tests/test_gpu_multiproc.py (not a test module).
+
+    python tests/_mp_choco_worker.py <comm_op> <world> <outdir>
+
+This launcher process never touches the GPU: it starts `world` rank processes
+(spawn), each of which builds the drop-in CHOCOCompressor with the reference's
+DecentralizedAggregation over gloo and comm_device="cpu" (pinned host staging,
+parallel_choco_v.py:271-272), runs compress -> sync -> uncompress on the one
+GPU, and saves its x_hat / memory and every received message to <outdir>.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LENS = [3, 70_001, 5, 1_100_003, 17, 300]
+RATIO = 0.9
+
+
+def inputs(rank):
+    """Worker `rank`'s x, x_hat (its own flatten_hat_params), and its x_hat_i / memory state."""
+    n = sum(LENS)
+    rng = np.random.default_rng(100 + rank)
+    x = rng.standard_normal(n).astype(np.float32)
+    xh = (rng.standard_normal(n) * 0.5).astype(np.float32)
+    hat0 = rng.standard_normal(n).astype(np.float32)
+    mem0 = rng.standard_normal(n).astype(np.float32)
+    return x, xh, hat0, mem0
+
+
+def _rank_main(rank, world, port, comm_op, outdir):
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from chocosgd_amd import parallel_choco
+        from chocosgd_amd.communication import DecentralizedAggregation, neighborhood
+        from chocosgd_amd.parallel_choco import CHOCOCompressor
+        from chocosgd_amd.tensor_buffer import TensorBuffer
+        parallel_choco._draw_seed = lambda: 1000 + rank  # pinned per-worker seeds (random-k, QSGD)
+        nb = neighborhood(rank, world)
+        agg = DecentralizedAggregation(rank, nb)
+        comp = CHOCOCompressor(aggregator=agg, comm_op=comm_op, comm_device="cpu", compress_ratio=RATIO,
+                               quantize_level=4, is_biased=False, backend="gloo", use_ipc=False)
+        x, xh, hat0, mem0 = inputs(rank)
+
+        def split(a):
+            t = torch.from_numpy(a).cuda()
+            out, p = [], 0
+            for m in LENS:
+                out.append(t[p:p + m].clone())
+                p += m
+            return out
+        sb = {"original_shapes": [(torch.Size([m]), m) for m in LENS],
+              "flatten_params": TensorBuffer(split(x)), "flatten_hat_params": TensorBuffer(split(xh))}
+        nhp = {rank: TensorBuffer(split(hat0)), "memory": TensorBuffer(split(mem0))}
+        # pipeline() without its except-and-print, so a failure fails the test
+        with torch.cuda.stream(comp.compressor_fn.gossip_stream):
+            comp.compress(sb)
+            comp.sync(sb)
+            comp.uncompress(sb, nhp, nb)
+        torch.cuda.synchronize()
+        out = {"hat": nhp[rank].buffer.cpu().numpy(), "mem": nhp["memory"].buffer.cpu().numpy()}
+        for r, m in sb["synced_message"].items():
+            out[f"msg{r}"] = m.cpu().numpy()
+        np.savez(os.path.join(outdir, f"rank{rank}.npz"), **out)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def main():
+    comm_op, world, outdir = sys.argv[1], int(sys.argv[2]), sys.argv[3]
+    import multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, comm_op, outdir)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    codes = [p.exitcode for p in procs]
+    if any(c != 0 for c in codes):
+        print(f"rank exit codes {codes}", file=sys.stderr)
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

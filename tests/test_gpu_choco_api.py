@@ -152,3 +152,118 @@ def test_reference_named_primitives():
     out = qc.compress(d, "quantize_qsgd", 4, False)
     assert out.shape == d.shape and torch.isfinite(out).all()
     assert qc.compress(d, "quantize_qsgd", 32, False) is d
+
+
+def _run_synthetic(comm_op, lens, ratio, seeds, monkeypatch, world=3, self_rank=1):
+    """CHOCOCompressor compress -> sync -> uncompress for `world` workers on synthetic
+    inputs; the per-worker random-k seeds are pinned through _draw_seed."""
+    from chocosgd_amd import parallel_choco
+    from chocosgd_amd.parallel_choco import CHOCOCompressor
+    from chocosgd_amd.tensor_buffer import TensorBuffer
+    it = iter(seeds)
+    monkeypatch.setattr(parallel_choco, "_draw_seed", lambda: next(it))
+    n = sum(lens)
+    rng = np.random.default_rng(sum(lens) + len(comm_op))
+    xs = rng.standard_normal((world, n)).astype(np.float32)
+    xhs = (rng.standard_normal((world, n)) * 0.5).astype(np.float32)
+    hat0 = rng.standard_normal(n).astype(np.float32)
+    mem0 = rng.standard_normal(n).astype(np.float32)
+    shapes = [(torch.Size([m]), m) for m in lens]
+    args = dict(aggregator=None, comm_op=comm_op, comm_device="gpu", compress_ratio=ratio, quantize_level=4,
+                is_biased=False, backend="nccl", use_ipc=False)
+    sent, comps = [], []
+    for r in range(world):
+        comp = CHOCOCompressor(**args)
+        sb = {"original_shapes": shapes,
+              "flatten_params": TensorBuffer(_split(dev(xs[r]), lens)),
+              "flatten_hat_params": TensorBuffer(_split(dev(xhs[r]), lens))}
+        comp.compress(sb)
+        comp.compressor_fn.aggregator_fn = CaptureAgg()
+        comp.sync(sb)
+        sent.append(comp.compressor_fn.aggregator_fn.sent)
+        comps.append((comp, sb))
+    comp, sb = comps[self_rank]
+    nhp = {self_rank: TensorBuffer(_split(dev(hat0), lens)), "memory": TensorBuffer(_split(dev(mem0), lens))}
+    comp.compressor_fn.aggregator_fn = ReplayAgg([{r: sent[r][c] for r in range(world)}
+                                                  for c in range(len(sent[0]))])
+    comp.sync(sb)
+    weights = [1.0 / world] * world
+    comp.uncompress(sb, nhp, {r: w for r, w in enumerate(weights)})
+    return xs, xhs, hat0, mem0, weights, sb, nhp
+
+
+def test_choco_random_k_round_trip(monkeypatch):
+    """random_k through the drop-in: a non-multiple-of-4 tensor ahead of segments over 64K
+    and over 1M elements; messages and the accumulate vs the oracle sampler, bit-exact."""
+    lens = [3, 70_001, 5, 1_200_003, 17, 300]
+    seeds = [11, 22, 33]
+    xs, xhs, hat0, mem0, weights, sb, nhp = _run_synthetic("compress_random_k", lens, 0.95, seeds, monkeypatch)
+    hat, mem = hat0.copy(), mem0.copy()
+    K = sum(O.topk_k(m, 0.95) for m in lens)
+    for r in range(3):
+        ov, oi = O.randk_segmented(xs[r] - xhs[r], lens, 0.95, seeds[r])
+        m = host(sb["synced_message"][r])
+        assert np.array_equal(m[K:].astype(np.int64), oi)
+        assert same_bits(m[:K].view(np.float32), ov)
+        O.sparse_accumulate(hat if r == 1 else None, mem, ov, oi, weights[r])
+    assert same_bits(host(nhp[1].buffer), hat)
+    assert same_bits(host(nhp["memory"].buffer), mem)
+    # the contract's local per-tensor indices (parallel_choco_v.py:248-249)
+    ov, oi = O.randk_segmented(xs[1] - xhs[1], lens, 0.95, seeds[1])
+    starts = np.repeat(np.concatenate([[0], np.cumsum(lens)[:-1]]), [O.topk_k(m, 0.95) for m in lens])
+    assert np.array_equal(host(sb["flatten_selected_indices"].buffer).astype(np.int64), oi - starts)
+
+
+def test_choco_top_k_local_indices(monkeypatch):
+    lens = [3, 70_001, 5, 1_200_003]
+    xs, xhs, hat0, mem0, weights, sb, nhp = _run_synthetic("compress_top_k", lens, 0.99, [0] * 3, monkeypatch)
+    ov, oi, ks = O.topk_segmented(xs[1] - xhs[1], lens, 0.99)
+    starts = np.repeat(np.concatenate([[0], np.cumsum(lens)[:-1]]), ks)
+    assert np.array_equal(host(sb["flatten_selected_indices"].buffer).astype(np.int64), oi - starts)
+    assert same_bits(host(sb["flatten_selected_values"].buffer), ov)
+
+
+def test_sparse_accumulate_out_of_range_raises():
+    from chocosgd_amd import codec
+    n = 1000
+    mem, hat = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    guard = codec.IndexGuard(mem.device)
+    vals = torch.ones(4, device=DEV)
+    idx = torch.tensor([1, 5, n + 3, -2], dtype=torch.int32, device=DEV)
+    codec.sparse_accumulate(vals, idx, mem, 0.5, xhat_self=hat, guard=guard)
+    guard.arm()
+    with pytest.raises(RuntimeError, match="out of range"):
+        guard.check(wait=True)
+    assert host(hat)[[1, 5]].tolist() == [1.0, 1.0] and host(hat).sum() == 2.0
+    assert host(mem).sum() == 1.0
+    guard.arm()
+    guard.check(wait=True)  # the word was reset
+
+
+@pytest.mark.parametrize("kind", ["sign", "qsgd"])
+def test_accumulate_more_than_8_messages(kind):
+    """A 10-neighbour mixing row: applied in fused chunks of 8, same fp32 sequence."""
+    from chocosgd_amd import codec
+    n, nmsg, self_slot = 100_003, 10, 9
+    w = [1.0 / nmsg] * nmsg
+    hat, mem = torch.randn(n, device=DEV), torch.randn(n, device=DEV)
+    h0, m0 = host(hat), host(mem)
+    msgs_d, decoded = [], []
+    for r in range(nmsg):
+        x = torch.randn(n, device=DEV)
+        if kind == "sign":
+            packed, norms = codec.sign_compress(x)
+            msgs_d.append((packed, norms))
+            decoded.append((host(packed), host(norms)))
+        else:
+            packed, norms, dense = codec.qsgd_compress(x, 4, seed=r, want_dense=True)
+            msgs_d.append((packed, norms))
+            decoded.append(host(dense))
+    if kind == "sign":
+        codec.sign_accumulate(msgs_d, w, self_slot, n, mem, xhat_self=hat)
+        O.sign_accumulate(h0, m0, decoded, w, self_slot, [n])
+    else:
+        codec.qsgd_accumulate(msgs_d, w, self_slot, n, 4, mem, xhat_self=hat)
+        O.qsgd_accumulate(h0, m0, decoded, w, self_slot)
+    assert same_bits(host(hat), h0)
+    assert same_bits(host(mem), m0)

@@ -1,0 +1,96 @@
+"""The CHOCO gossip round across PROCESSES: CHOCOCompressor compress -> sync ->
+uncompress on 2 and 3 ranks sharing the one GPU, exchanging through the
+reference's DecentralizedAggregation over gloo with comm_device="cpu"
+(communication.py:246-291, parallel_choco_v.py:262-310).  Every worker's
+x_hat / memory is compared with the oracle's round over the same inputs.
+
+The ranks are started by tests/_mp_choco_worker.py in a fresh interpreter, so
+the processes that use the GPU are not forked from this (GPU-initialised) one.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, same_bits
+from oracle import choco_oracle as O
+
+pytestmark = pytest.mark.gpu
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import _mp_choco_worker as W  # noqa: E402
+
+
+def _neighborhood(rank, world):
+    if world == 2:
+        return {0: 0.5, 1: 0.5}
+    ranks = sorted({(rank - 1) % world, rank, (rank + 1) % world})
+    return {r: 1.0 / 3 for r in ranks}
+
+
+def _hdr(nseg):
+    return (nseg + 3) // 4 * 4
+
+
+@pytest.mark.parametrize("comm_op,world", [("compress_top_k", 2), ("compress_top_k", 3), ("compress_random_k", 3),
+                                           ("sign", 2), ("sign", 3), ("quantize_qsgd", 3)])
+def test_choco_round_across_processes(comm_op, world, tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_mp_choco_worker.py"), comm_op, str(world),
+                        str(tmp_path)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lens, nseg = W.LENS, len(W.LENS)
+    n = sum(lens)
+    ins = [W.inputs(q) for q in range(world)]
+    deltas = [(x - xh).astype(np.float32) for x, xh, _, _ in ins]
+    got = [dict(np.load(tmp_path / f"rank{q}.npz")) for q in range(world)]
+    # every worker's message, checked once against the oracle (as its neighbours received it)
+    msgs = {}
+    for q in range(world):
+        rcv = next(g[f"msg{q}"] for g in got if f"msg{q}" in g)
+        d = deltas[q]
+        if "top_k" in comm_op or "random_k" in comm_op:
+            if "top_k" in comm_op:
+                ov, oi, _ = O.topk_segmented(d, lens, W.RATIO)
+            else:
+                ov, oi = O.randk_segmented(d, lens, W.RATIO, 1000 + q)
+            K = ov.size
+            assert np.array_equal(rcv[K:].astype(np.int64), oi)
+            assert same_bits(rcv[:K].view(np.float32), ov)
+            msgs[q] = (ov, oi)
+        elif comm_op == "sign":
+            hw = _hdr(nseg)
+            norms = rcv[:hw].view(np.float32)[:nseg]
+            assert np.array_equal(rcv[hw:], O.sign_pack(d))
+            assert np.allclose(norms, O.l1_norms(d, lens), rtol=1e-6, atol=0)
+            msgs[q] = (rcv[hw:], norms)
+        else:
+            hb = 4 * _hdr(nseg)
+            norms = rcv[:hb].view(np.float32)[:nseg]
+            assert np.allclose(norms, O.l2_norms(d, lens), rtol=1e-6, atol=0)
+            u = O.philox_uniforms(n, 1000 + q, 0)
+            lvl, dec, off = [], [], 0
+            for s, m in enumerate(lens):
+                lvl.append(O.qsgd_levels(d[off:off + m], 15, u[off:off + m], norms[s]))
+                off += m
+            assert np.array_equal(rcv[hb:], O.qsgd_pack(np.concatenate(lvl), d, 4))
+            levels, neg = O.qsgd_unpack(rcv[hb:], n, 4)
+            off = 0
+            for s, m in enumerate(lens):
+                dec.append(O.qsgd_decode(levels[off:off + m], neg[off:off + m], norms[s], 15, m))
+                off += m
+            msgs[q] = np.concatenate(dec)
+    # every worker's accumulate, in its neighbors_info order
+    for rank in range(world):
+        _, _, hat, mem = (a.copy() for a in ins[rank])
+        nb = _neighborhood(rank, world)
+        ranks = list(nb)
+        if "top_k" in comm_op or "random_k" in comm_op:
+            for q in ranks:
+                O.sparse_accumulate(hat if q == rank else None, mem, msgs[q][0], msgs[q][1], nb[q])
+        elif comm_op == "sign":
+            O.sign_accumulate(hat, mem, [msgs[q] for q in ranks], [nb[q] for q in ranks], ranks.index(rank), lens)
+        else:
+            O.qsgd_accumulate(hat, mem, [msgs[q] for q in ranks], [nb[q] for q in ranks], ranks.index(rank))
+        assert same_bits(got[rank]["hat"], hat), f"rank {rank} x_hat"
+        assert same_bits(got[rank]["mem"], mem), f"rank {rank} memory"

@@ -59,12 +59,38 @@ def test_topk_random_sizes(n, ratio):
 
 
 def test_topk_fused_delta():
+    """d = x - xhat formed inside the kernel vs the oracle's top-k of the host delta."""
     from chocosgd_amd import codec
     x, xh = randn(2_000_003, 5), randn(2_000_003, 6, 0.9)
     k = codec.topk_k(x.numel(), 0.99)
     v1, i1 = codec.topk(x, k, xhat=xh)
-    v2, i2 = codec.topk((x - xh).contiguous(), k)
-    assert torch.equal(i1, i2) and torch.equal(v1, v2)
+    ov, oi = O.topk(host(x) - host(xh), k)
+    assert np.array_equal(host(i1).astype(np.int64), oi)
+    assert same_bits(host(v1), ov)
+
+
+@pytest.mark.parametrize("n", [2_000_003, 100_003])
+def test_topk_k_equals_n_large(n):
+    """ratio 0 (k = n): a multi-workgroup copy with iota indices."""
+    from chocosgd_amd import codec
+    x, xh = randn(n, 8), randn(n, 9)
+    vals, idx = codec.topk(x, n, xhat=xh)
+    assert np.array_equal(host(idx), np.arange(n, dtype=np.int32))
+    assert same_bits(host(vals), host(x) - host(xh))
+
+
+def test_topk_unaligned_base_pipeline():
+    """A 3M-element view starting 1 and 3 floats past a 16-byte boundary runs the
+    multi-workgroup pipeline (dword-aligned buffer loads)."""
+    from chocosgd_amd import codec
+    base, bh = randn(3_000_010, 13), randn(3_000_010, 14, 0.5)
+    for off in (1, 3):
+        x, xh = base[off:off + 3_000_000], bh[off:off + 3_000_000]
+        k = codec.topk_k(x.numel(), 0.99)
+        vals, idx = codec.topk(x, k, xhat=xh)
+        ov, oi = O.topk(host(x) - host(xh), k)
+        assert np.array_equal(host(idx).astype(np.int64), oi)
+        assert same_bits(host(vals), ov)
 
 
 @pytest.mark.slow
@@ -120,6 +146,38 @@ def test_topk_segmented_model_layouts(layout, ratio):
     vals, idx = codec.topk_segmented(x, plan, xhat=xh)
     ov, oi, ks = O.topk_segmented(host(x) - host(xh), lens, ratio)
     assert plan.k_per_seg == ks
+    assert np.array_equal(host(idx).astype(np.int64), oi)
+    assert same_bits(host(vals), ov)
+
+
+UNALIGNED_LAYOUT = [3, 70_001, 5, 1_200_003, 17, 300, 1_048_577, 2]
+
+
+@pytest.mark.parametrize("ratio", [0.9, 0.99])
+def test_topk_segmented_unaligned_large(ratio):
+    """Segments over 64K and over 1M elements that start off a 16-byte boundary."""
+    from chocosgd_amd import codec
+    lens = UNALIGNED_LAYOUT
+    n = sum(lens)
+    x, xh = randn(n, 41), randn(n, 42, 0.5)
+    plan = codec.SegmentPlan(lens, ratio, x.device)
+    vals, idx = codec.topk_segmented(x, plan, xhat=xh)
+    ov, oi, ks = O.topk_segmented(host(x) - host(xh), lens, ratio)
+    assert np.array_equal(host(idx).astype(np.int64), oi)
+    assert same_bits(host(vals), ov)
+
+
+@pytest.mark.parametrize("layout", ["unaligned", "resnet20_cifar10"])
+@pytest.mark.parametrize("is_biased", [True, False])
+def test_randk_segmented_vs_oracle(layout, is_biased):
+    from chocosgd_amd import codec
+    lens = UNALIGNED_LAYOUT if layout == "unaligned" else golden_json("layouts.json")[layout]
+    n = sum(lens)
+    x, xh = randn(n, 51), randn(n, 52, 0.5)
+    seed = 0xDEADBEEF12345
+    plan = codec.SegmentPlan(lens, 0.95, x.device)
+    vals, idx = codec.randk_segmented(x, plan, seed, is_biased=is_biased, xhat=xh)
+    ov, oi = O.randk_segmented(host(x) - host(xh), lens, 0.95, seed, is_biased=is_biased)
     assert np.array_equal(host(idx).astype(np.int64), oi)
     assert same_bits(host(vals), ov)
 

@@ -198,3 +198,37 @@ def test_randk_indices_distinct_and_uniformish():
         counts[idx] += 1
     # each index selected ~ 40 * 0.1 = 4 times on average
     assert 3.0 < counts.mean() < 5.0 and counts.max() < 20
+
+
+def test_oracle_sampled_helpers_agree_with_full_forms():
+    """philox_uniforms_at / qsgd_wire_at (the sampled checks at BASELINE sizes) restate the
+    full-array forms exactly."""
+    n, seed, offset = 10_007, 0x1234_5678_9ABC, 5
+    u = O.philox_uniforms(n, seed, offset)
+    idx = np.array([0, 1, 2, 3, 4, 777, 4096, n - 2, n - 1])
+    assert np.array_equal(O.philox_uniforms_at(idx, seed, offset), u[idx])
+    rng = np.random.default_rng(0)
+    d = rng.standard_normal(n).astype(np.float32)
+    for q in (1, 2, 4, 8, 16):
+        s = 2 ** q - 1
+        lvl = O.qsgd_levels(d, s, u, np.float32(np.sqrt(np.sum(d.astype(np.float64) ** 2))) / 40)
+        packed = O.qsgd_pack(lvl, d, q)
+        levels, neg = O.qsgd_unpack(packed, n, q)
+        gl, gn = O.qsgd_wire_at(packed, n, q, idx)
+        assert np.array_equal(gl, levels[idx].astype(np.int64)) and np.array_equal(gn, neg[idx])
+
+
+def test_oracle_segmented_randk():
+    lens = [3, 70, 5, 1000, 17]
+    d = np.random.default_rng(1).standard_normal(sum(lens)).astype(np.float32)
+    v, i = O.randk_segmented(d, lens, 0.9, 42)
+    ks = [O.topk_k(m, 0.9) for m in lens]
+    assert v.size == i.size == sum(ks)
+    off = 0
+    for s, (m, k) in enumerate(zip(lens, ks)):
+        part = i[sum(ks[:s]):sum(ks[:s + 1])]
+        assert np.all(np.diff(part) > 0) and part[0] >= off and part[-1] < off + m
+        assert np.array_equal(part - off, O.randk_indices(m, k, O.seg_seed(42, s)))
+        off += m
+    assert same_bits(v, d[i])
+    assert O.seg_seed(42, 0) != O.seg_seed(42, 1) and O.seg_seed(42, 0) < 2 ** 64

@@ -1,11 +1,14 @@
-"""HBM traffic of the bench's dominant kernel from rocprofv3 --pmc passes.
+"""HBM traffic per dispatch of every codec kernel from two rocprofv3 --pmc passes.
 
-FETCH_SIZE and WRITE_SIZE are reported in KB per dispatch (summed over the
-TCC instances).  gfx950 correction (MI355X_MICROARCH.md, HBM section):
-FETCH_SIZE counts exactly half of the bytes of a wide coalesced streaming read,
-so it is doubled.  Writes profiles/pmc_traffic.json {"<workload>:<n>": bytes}.
+FETCH_SIZE and WRITE_SIZE are reported in KB per dispatch (summed over the TCC
+instances).  gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE
+counts exactly half of the bytes of a wide coalesced STREAMING read, so it is
+doubled for the streaming kernels -- and NOT for the scattered read-modify-write
+of the sparse accumulate (4-B gathers; the correction is uncalibrated there, so
+its raw count is kept).  Writes profiles/pmc_traffic.json
+{"<profile name>:<workload>:<n>": {...}}, the keys bench.py reads.
 
-    python tools/pmc_traffic.py <fetch_dir> <write_dir> <kernel-substring> <workload:n>
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <workload> <n>
 """
 import collections
 import csv
@@ -14,32 +17,52 @@ import json
 import os
 import sys
 
+# bench/profile stage name -> (rocprof kernel-name substring, fetch correction)
+KERNELS = {
+    "topk_bounds": ("topk_bounds_kernel", 2.0),
+    "topk_stream": ("topk_stream_kernel", 2.0),
+    "topk_finish": ("topk_finish_kernel", 2.0),
+    "topk_fused": ("topk_fused_kernel", 2.0),
+    "topk_segmented": ("topk_segmented_kernel", 2.0),
+    "sparse_accumulate": ("sparse_acc", 1.0),
+    "qsgd_norm": ("qsgd_norm_kernel", 2.0),
+    "qsgd_quantize": ("qsgd_quant_kernel", 2.0),
+    "qsgd_accumulate": ("qsgd_decode_kernel", 2.0),
+    "sign_pack": ("sign_pack", 2.0),
+    "sign_accumulate": ("sign_accumulate_kernel", 2.0),
+    "gossip_step": ("gossip_kernel", 2.0),
+}
+
 
 def per_dispatch(root, counter, kernel):
     vals = collections.defaultdict(float)
     for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(path)):
-            if r["Counter_Name"] == counter and kernel in r.get("Kernel_Name", ""):
-                vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                if r["Counter_Name"] == counter and kernel in r.get("Kernel_Name", ""):
+                    vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
     return sorted(vals.values())
 
 
 def main():
-    fdir, wdir, kernel, key = sys.argv[1:5]
-    f = per_dispatch(fdir, "FETCH_SIZE", kernel)
-    w = per_dispatch(wdir, "WRITE_SIZE", kernel)
-    if not f or not w:
-        sys.exit(f"no {kernel} dispatches found")
-    fmed, wmed = f[len(f) // 2], w[len(w) // 2]
-    out = {"fetch_bytes": 2 * fmed * 1024, "write_bytes": wmed * 1024}
-    out["bytes"] = out["fetch_bytes"] + out["write_bytes"]
-    out["note"] = ("median over %d/%d dispatches; FETCH_SIZE x2 (gfx950 streaming-read correction) + WRITE_SIZE, "
-                   "KB units x1024" % (len(f), len(w)))
+    fdir, wdir, workload, n = sys.argv[1:5]
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
     data = json.load(open(path)) if os.path.exists(path) else {}
-    data[key] = out
+    for name, (kernel, corr) in KERNELS.items():
+        f = per_dispatch(fdir, "FETCH_SIZE", kernel)
+        w = per_dispatch(wdir, "WRITE_SIZE", kernel)
+        if not f or not w:
+            continue
+        fmed, wmed = f[len(f) // 2], w[len(w) // 2]
+        out = {"fetch_bytes": corr * fmed * 1024, "write_bytes": wmed * 1024}
+        out["bytes"] = out["fetch_bytes"] + out["write_bytes"]
+        out["note"] = (f"median over {len(f)}/{len(w)} dispatches; FETCH_SIZE x{corr:g} "
+                       f"({'gfx950 streaming-read correction' if corr != 1 else 'scattered: raw'}) + WRITE_SIZE, "
+                       "KB units x1024")
+        key = f"{name}:{workload}:{n}"
+        data[key] = out
+        print(key, out)
     json.dump(data, open(path, "w"), indent=1, sort_keys=True)
-    print(key, out)
 
 
 if __name__ == "__main__":
