@@ -293,9 +293,33 @@ def cpu_model():
     return "unknown"
 
 
+def usable_cpus():
+    """CPUs this process may actually use: the affinity mask, capped by a cgroup v2/v1
+    CPU quota (a GPU box grants a 16-CPU share of a machine whose os.cpu_count() is far
+    larger; oversubscribing that share only slows torch down)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+            if path.endswith("cpu.max") and parts and parts[0] != "max":
+                n = min(n, max(1, int(int(parts[0]) / int(parts[1]))))
+            elif path.endswith("quota_us") and int(parts[0]) > 0:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    n = min(n, max(1, int(int(parts[0]) / int(f.read()))))
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    return n
+
+
 def cpu_baseline(w):
     """Reference torch-CPU op sequence (oracle/torch_port.py) on the host cores: the
-    process's usable CPUs (sched affinity), one thread, and os.cpu_count() threads."""
+    process's usable CPUs (affinity and cgroup quota), one thread, and os.cpu_count()
+    threads."""
     import torch
     from oracle import torch_port as P
 
@@ -330,10 +354,7 @@ def cpu_baseline(w):
         return {"threads": threads, "n": m, "value": round(4 * m / med / 1e9, 4), "ms": round(med * 1e3, 1),
                 "reps": len(ts)}
 
-    try:
-        usable = len(os.sched_getaffinity(0))
-    except AttributeError:
-        usable = os.cpu_count()
+    usable = usable_cpus()
     big = min(w.n, 100_000_000)
     small = min(w.n, 25_000_000)
     rows = [timed(usable, big, 3, 20.0), timed(1, small, 2, 10.0)]
