@@ -96,7 +96,8 @@ def topk(x, k, xhat=None, out=None):
 
 
 class SegmentPlan:
-    """Host + device copies of the per-segment top-k plan {off, len, k, out_off}."""
+    """Host + device copies of the per-segment top-k plan (include/choco_codec.h):
+    rows {off, len, k, out_off, first tile, tiles, ..} + the tile -> segment map."""
 
     def __init__(self, seg_lens, ratio, device):
         L = lib()
@@ -108,16 +109,32 @@ class SegmentPlan:
         self.seg_off = offs
         self.n = offs[-1]
         p_off, self._off_keep = _lib.i64_array(offs)
-        self._plan_host = (ctypes.c_int64 * (4 * self.nseg))()
+        plen = L.choco_topk_segmented_plan_len(p_off, self.nseg)
+        if plen < 0:
+            raise RuntimeError(f"choco_topk_segmented_plan_len failed: {_lib.last_error()}")
+        self._plan_host = (ctypes.c_int64 * int(plen))()
         self.plan_host = ctypes.cast(self._plan_host, ctypes.POINTER(ctypes.c_int64))
         total = L.choco_topk_segmented_plan(p_off, self.nseg, float(ratio), self.plan_host)
         if total < 0:
             raise RuntimeError(f"choco_topk_segmented_plan failed: {_lib.last_error()}")
         self.k_total = int(total)
-        self.k_per_seg = [int(self._plan_host[4 * s + 2]) for s in range(self.nseg)]
+        self.k_per_seg = [int(self._plan_host[8 * s + 2]) for s in range(self.nseg)]
+        self.ntile = int(self._plan_host[6])
         self.plan_dev = torch.tensor(list(self._plan_host), dtype=torch.int64, device=device)
         self.ws_bytes = int(L.choco_topk_segmented_workspace_size(self.plan_host, self.nseg))
         self._base = None
+        self._ws = {}
+
+    def workspace(self, dev):
+        """This plan's own zero-filled workspace per stream: the batched select keeps
+        per-segment histograms there that every call leaves zeroed for the NEXT call of
+        the same plan (include/choco_codec.h), so no other call may share it."""
+        key = torch.cuda.current_stream(dev).cuda_stream
+        with _ws_lock:
+            buf = self._ws.get(key)
+            if buf is None:
+                buf = self._ws[key] = torch.zeros(max(self.ws_bytes, 256), dtype=torch.uint8, device=dev)
+            return buf
 
     def selected_base(self):
         """int32[K]: the segment start of every output slot (global -> local index)."""
@@ -153,7 +170,7 @@ def topk_segmented(x, plan, xhat=None, out=None):
     vals, idx = _seg_outputs(x, xhat, plan, out)
     dev = x.device
     L = lib()
-    ws = workspace(dev, "topk", plan.ws_bytes)
+    ws = plan.workspace(dev)
     _lib.check(L.choco_topk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
                                                plan.nseg, _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(),
                                                _stream(dev)), "choco_topk_compress_segmented")
@@ -183,7 +200,7 @@ def randk_segmented(x, plan, seed, is_biased=True, xhat=None, out=None):
     vals, idx = _seg_outputs(x, xhat, plan, out)
     dev = x.device
     L = lib()
-    ws = workspace(dev, "topk", plan.ws_bytes)
+    ws = plan.workspace(dev)
     _lib.check(L.choco_randk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
                                                 plan.nseg, int(seed) & (2**64 - 1), 1 if is_biased else 0,
                                                 _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(), _stream(dev)),

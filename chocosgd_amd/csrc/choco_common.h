@@ -279,4 +279,22 @@ CHOCO_DEV uint32_t rank_hash(uint64_t seed, uint32_t i) {
   return h;
 }
 
+// Per-segment random-k seed (host and device agree; oracle/choco_oracle.py seg_seed):
+// splitmix64 of seed + (s + 1) * golden gamma, so every segment draws an independent
+// ranking (the reference calls np.random.choice once per tensor, sparsification.py:48).
+CHOCO_DEV __host__ inline uint64_t seg_seed(uint64_t seed, int64_t s) {
+  uint64_t z = seed + (uint64_t)(s + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// ---------------------------------------------------------------- top-k internals
+// (topk.hip: the flat multi-workgroup pipeline; topk_seg.hip: the batched
+// segmented select).  mode: 0 = data keys |d|, 1 = random-k hash keys.
+enum TopkMode { kData = 0, kHash = 1 };
+size_t topk_ws_bytes(int64_t n);
+int topk_pipeline(int mode, const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
+                  float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes, hipStream_t st);
+
 }  // namespace choco

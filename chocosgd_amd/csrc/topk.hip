@@ -34,8 +34,8 @@
 //   bucket j* larger than LDS, or a side list overflowed), K34's workgroup 0
 //   runs an exact single-workgroup radix select over the full input instead
 //   (correct, slow, data-dependent only).
-// Small n (<= kSmallN) and every segment of the batched segmented path use
-// the same exact radix select (block_topk_exact) in one workgroup.
+// Small n (<= kSmallN) uses an exact radix select (block_topk_exact) in one
+// workgroup; per-tensor (segmented) calls are batched in topk_seg.hip.
 #include "choco_common.h"
 
 #include <math.h>
@@ -115,7 +115,6 @@ CHOCO_DEV void st_pol(T* p, T v) {
   }
 }
 
-enum SrcMode { kData = 0, kHash = 1 };
 enum TileMode { kTakeNone = 0, kTakeAll = 1, kTakePartial = 2 };
 
 struct TopkCtrl {
@@ -305,34 +304,6 @@ __global__ __launch_bounds__(256) void topk_all_kernel(const float* __restrict__
     out_val[i] = (XH ? x[i] - xh[i] : x[i]) * scale;
     out_idx[i] = (int32_t)(i + idx_base);
   }
-}
-
-// Per-segment random-k seed (host and device agree; oracle/choco_oracle.py seg_seed):
-// splitmix64 of seed + (s + 1) * golden gamma, so every segment draws an independent
-// ranking (the reference calls np.random.choice once per tensor, sparsification.py:48).
-CHOCO_DEV __host__ inline uint64_t seg_seed(uint64_t seed, int64_t s) {
-  uint64_t z = seed + (uint64_t)(s + 1) * 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-// Segmented: plan rows {off, len, k, out_off}; one workgroup per segment that
-// is not routed to the pipeline.
-CHOCO_DEV bool seg_uses_pipeline(int64_t off, int64_t len, int mode);
-
-template <int MODE, bool XH>
-__global__ __launch_bounds__(kExactThreads) void topk_segmented_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ plan,
-    int32_t nseg, uint64_t seed, int32_t is_biased, float* __restrict__ out_val, int32_t* __restrict__ out_idx) {
-  __shared__ ExactSmem sm;
-  const int s = blockIdx.x;
-  if (s >= nseg) return;
-  const int64_t off = plan[4 * s + 0], len = plan[4 * s + 1], k = plan[4 * s + 2], oo = plan[4 * s + 3];
-  if (seg_uses_pipeline(off, len, MODE) || len == 0) return;
-  Src<MODE, XH> src{x + off, XH ? xh + off : nullptr, MODE == kHash ? seg_seed(seed, s) : 0};
-  const float scale = (MODE == kHash && !is_biased) ? (float)((double)len / (double)k) : 1.0f;
-  block_topk_exact(src, len, k, scale, out_val + oo, out_idx + oo, off, sm);
 }
 
 // ----------------------------------------------------------------------------
@@ -1516,19 +1487,6 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
 // ----------------------------------------------------------------------------
 // host dispatch
 // ----------------------------------------------------------------------------
-// Segments of >= 1M elements take the multi-workgroup pipeline, at any 4-byte
-// alignment: every vector load of x / xhat there is a dword-aligned buffer load.
-constexpr int64_t kPipeMinSeg = 1 << 20;
-CHOCO_DEV bool seg_uses_pipeline(int64_t off, int64_t len, int mode) {
-  (void)off;
-  (void)mode;
-  return len >= kPipeMinSeg;
-}
-static bool host_seg_uses_pipeline(int64_t off, int64_t len) {
-  (void)off;
-  return len >= kPipeMinSeg;
-}
-
 size_t topk_ws_bytes(int64_t n) { return n > kSmallN ? topk_layout(n).total : 256; }
 
 template <int MODE, bool XH>
@@ -1608,6 +1566,12 @@ static int dispatch_topk(const float* x, const float* xh, int64_t n, int64_t k, 
   return launch_topk<MODE, false>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st);
 }
 
+int topk_pipeline(int mode, const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
+                  float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (mode == kHash) return dispatch_topk<kHash>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st);
+  return dispatch_topk<kData>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st);
+}
+
 }  // namespace choco
 
 using namespace choco;
@@ -1633,84 +1597,6 @@ CHOCO_API int choco_randk_compress(const float* x, const float* xhat, int64_t n,
   const float scale = is_biased ? 1.0f : (float)((double)n / (double)k);
   return dispatch_topk<kHash>(x, xhat, n, k, seed, scale, out_val, out_idx, 0, ws, ws_bytes,
                               as_stream(stream));
-}
-
-CHOCO_API int64_t choco_topk_segmented_plan(const int64_t* seg_off_host, int32_t nseg, double ratio,
-                                            int64_t* plan_host) {
-  if (seg_off_host == nullptr || nseg <= 0) return (int64_t)fail(CHOCO_ERR_INVALID, "bad segment table");
-  int64_t out = 0;
-  for (int s = 0; s < nseg; ++s) {
-    const int64_t off = seg_off_host[s], len = seg_off_host[s + 1] - seg_off_host[s];
-    if (len <= 0) return (int64_t)fail(CHOCO_ERR_INVALID, "segment %d has length %lld", s, (long long)len);
-    const int64_t k = choco_topk_k(len, ratio);
-    if (plan_host) {
-      plan_host[4 * s + 0] = off;
-      plan_host[4 * s + 1] = len;
-      plan_host[4 * s + 2] = k;
-      plan_host[4 * s + 3] = out;
-    }
-    out += k;
-  }
-  return out;
-}
-
-CHOCO_API size_t choco_topk_segmented_workspace_size(const int64_t* plan_host, int32_t nseg) {
-  size_t need = 256;
-  for (int s = 0; s < nseg; ++s) {
-    const int64_t off = plan_host[4 * s], len = plan_host[4 * s + 1];
-    if (host_seg_uses_pipeline(off, len)) need = std::max(need, topk_ws_bytes(len));
-  }
-  return need;
-}
-
-template <int MODE>
-static int segmented(const float* x, const float* xhat, const int64_t* plan_dev, const int64_t* plan_host,
-                     int32_t nseg, uint64_t seed, int32_t is_biased, float* out_val, int32_t* out_idx, void* ws,
-                     size_t ws_bytes, hipStream_t st) {
-  CHOCO_REQUIRE(x && plan_dev && plan_host && out_val && out_idx && nseg > 0, "null pointer argument");
-  CHOCO_REQUIRE(aligned4(x) && (xhat == nullptr || aligned4(xhat)), "x/xhat must be 4-byte aligned");
-  const int64_t ntot = plan_host[4 * (nseg - 1)] + plan_host[4 * (nseg - 1) + 1];
-  CHOCO_REQUIRE(ntot < (int64_t)INT32_MAX, "total length must be < 2^31");
-  bool any_small = false;
-  for (int s = 0; s < nseg; ++s) any_small |= !host_seg_uses_pipeline(plan_host[4 * s], plan_host[4 * s + 1]);
-  // every segment that is not pipelined: one workgroup each, one launch
-  if (any_small) {
-    profile_begin("topk_segmented", st);
-    if (xhat)
-      CHOCO_KLAUNCH((topk_segmented_kernel<MODE, true>), dim3(nseg), dim3(kExactThreads), 0, st, x, xhat,
-                    plan_dev, nseg, seed, is_biased, out_val, out_idx);
-    else
-      CHOCO_KLAUNCH((topk_segmented_kernel<MODE, false>), dim3(nseg), dim3(kExactThreads), 0, st, x, xhat,
-                    plan_dev, nseg, seed, is_biased, out_val, out_idx);
-    profile_end("topk_segmented", st);
-    CHOCO_LAUNCHED("topk_segmented_kernel");
-  }
-  for (int s = 0; s < nseg; ++s) {
-    const int64_t off = plan_host[4 * s], len = plan_host[4 * s + 1], k = plan_host[4 * s + 2],
-                  oo = plan_host[4 * s + 3];
-    if (!host_seg_uses_pipeline(off, len)) continue;
-    const uint64_t sd = MODE == kHash ? seg_seed(seed, s) : 0;
-    const float scale = (MODE == kHash && !is_biased) ? (float)((double)len / (double)k) : 1.0f;
-    int rc = dispatch_topk<MODE>(x + off, xhat ? xhat + off : nullptr, len, k, sd, scale, out_val + oo,
-                                 out_idx + oo, off, ws, ws_bytes, st);
-    if (rc) return rc;
-  }
-  return CHOCO_OK;
-}
-
-CHOCO_API int choco_topk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
-                                            const int64_t* plan_host, int32_t nseg, float* out_val,
-                                            int32_t* out_idx, void* ws, size_t ws_bytes, void* stream) {
-  return segmented<kData>(x, xhat, plan_dev, plan_host, nseg, 0, 1, out_val, out_idx, ws, ws_bytes,
-                          as_stream(stream));
-}
-
-CHOCO_API int choco_randk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
-                                             const int64_t* plan_host, int32_t nseg, uint64_t seed,
-                                             int32_t is_biased, float* out_val, int32_t* out_idx, void* ws,
-                                             size_t ws_bytes, void* stream) {
-  return segmented<kHash>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, ws, ws_bytes,
-                          as_stream(stream));
 }
 
 #if CHOCO_STAMPS

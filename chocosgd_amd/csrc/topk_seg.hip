@@ -1,0 +1,512 @@
+// Batched per-tensor (segmented) top-k / random-k on MI355X.
+//
+// Replaces the per-parameter-tensor loop of CHOCOSparsificationCompressor.compress
+// (reference dl_code/pcode/optim/parallel_choco_v.py:229-260), which calls
+// SparsificationCompressor.get_top_k / get_random_k (sparsification.py:18-54)
+// once per tensor of the layout that create_optimizer.py:15-24 defines (one
+// parameter per group: 65 tensors for ResNet-20, 161 for ResNet-50).
+//
+// Per segment s the answer is the exact selection of the flat path (topk.hip):
+//   T_s = k_s-th largest key, out = {key > T_s} U {the lowest-index ties at T_s},
+//   (value, GLOBAL index) in ascending index order, segments concatenated.
+//
+// Every segment of up to kSegMaxTiles tiles (16M elements) is cut into tiles of
+// kSegTile = 16384 elements; ALL tiles of ALL such segments run in the same
+// launches (a 2,048-element BN vector and a 2.4M-element conv weight alike),
+// four of them per call:
+//   S1 seg_hist     (tile)   : 2048-bin histogram of key >> 20 (sign-free
+//                              exponent + 3 mantissa bits) -> hist1[s].
+//   S2 seg_collect  (tile)   : every tile finds its segment's coarse bin b1 of
+//                              the k-th key from hist1[s] (same data, same
+//                              answer), re-reads its tile (an Infinity-Cache hit
+//                              when the layout fits 256 MB) and compacts the
+//                              candidates (key >= b1 << 20) in index order into
+//                              its own slot range; keys in bin b1 feed a
+//                              histogram of bits 19..9 -> hist2[s].
+//   S3 seg_select   (segment): bin b2 from hist2[s], then bits 8..0 over the
+//                              segment's candidates (~1-2 % of it) -> exact T_s
+//                              and tie quota r_s; per-tile counts (> T, == T)
+//                              scanned into each tile's output offset and tie
+//                              share; resets hist1[s], hist2[s] for the next call.
+//   S4 seg_emit     (tile)   : ordered compaction of the tile's candidates
+//                              (key > T, plus its share of ties) to the output.
+// Two passes over the input (the first from HBM, the second usually from the
+// Infinity Cache) instead of one workgroup per segment doing four.  Segments
+// over 16M elements take the flat multi-workgroup pipeline (topk.hip).
+#include "choco_common.h"
+
+#include <algorithm>
+
+namespace choco {
+
+constexpr int kSegTile = 16384;                       // elements per tile
+constexpr int kSegThreads = 1024;                     // 4 rows of 1024 float4 = one tile
+constexpr int kSegRows = kSegTile / (4 * kSegThreads);
+constexpr int kSegMaxTiles = 1024;                    // tiles per batched segment (S3: one per thread)
+constexpr int64_t kSegBatchMax = (int64_t)kSegTile * kSegMaxTiles;
+constexpr int kRow = 8;                               // plan row width (int64)
+constexpr int kH = 2048;                              // histogram bins (S1, S2)
+static_assert(kSegRows * 4 * kSegThreads == kSegTile, "tile geometry");
+
+// plan (host + device copies, int64):
+//   rows[nseg][8] = {off, len, k, out_off, t0, ntile, 0, 0}; row 0 also carries
+//   [6] = total tiles, [7] = batched segments;
+//   then tile -> segment map [total tiles]; then batched segment ids [batched].
+struct SegRow {
+  int64_t off, len, k, out_off, t0, ntile;
+};
+CHOCO_DEV SegRow seg_row(const int64_t* __restrict__ plan, int s) {
+  const int64_t* p = plan + (int64_t)kRow * s;
+  return SegRow{p[0], p[1], p[2], p[3], p[4], p[5]};
+}
+
+struct SegWs {
+  uint32_t *hist1, *hist2, *info, *tilecnt, *tileout;
+  float* cval;
+  uint32_t* cidx;
+};
+
+struct SegLayout {
+  size_t off_h1, off_h2, off_info, off_cnt, off_out, off_cval, off_cidx, total;
+};
+
+static SegLayout seg_layout(int nseg, int64_t ntile) {
+  SegLayout L{};
+  size_t o = 0;
+  L.off_h1 = o;   o += align_up((size_t)nseg * kH * 4, 256);
+  L.off_h2 = o;   o += align_up((size_t)nseg * kH * 4, 256);
+  L.off_info = o; o += align_up((size_t)nseg * 4 * 4, 256);
+  L.off_cnt = o;  o += align_up((size_t)ntile * 4, 256);
+  L.off_out = o;  o += align_up((size_t)ntile * 8, 256);
+  L.off_cval = o; o += align_up((size_t)ntile * kSegTile * 4, 256);
+  L.off_cidx = o; o += align_up((size_t)ntile * kSegTile * 4, 256);
+  L.total = o;
+  return L;
+}
+
+// This tile: its segment, the segment's row, its first element and length.
+struct TileCtx {
+  int s;
+  SegRow R;
+  int64_t j, start, slot;  // tile number inside the segment, first element, candidate slot base
+  int tl;
+};
+CHOCO_DEV TileCtx tile_ctx(const int64_t* __restrict__ plan, int nseg, int64_t b) {
+  TileCtx c;
+  c.s = (int)plan[(int64_t)kRow * nseg + b];
+  c.R = seg_row(plan, c.s);
+  c.j = b - c.R.t0;
+  c.start = c.R.off + c.j * kSegTile;
+  c.slot = b * kSegTile;
+  c.tl = (int)min((int64_t)kSegTile, c.R.len - c.j * kSegTile);
+  return c;
+}
+
+// The tile's values: row r, thread t <-> elements r * 4096 + 4t .. +3 (dword-
+// aligned buffer loads: x + start needs only 4-byte alignment; past the tile
+// the loads return zeros and the elements are masked by `valid`).
+template <bool XH>
+CHOCO_DEV void tile_load(const float* __restrict__ x, const float* __restrict__ xh, const TileCtx& c,
+                         float (&v)[kSegRows][4]) {
+  const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x + c.start, (uint32_t)c.tl * 4u);
+  const __amdgpu_buffer_rsrc_t rh = buf_rsrc((XH ? xh : x) + c.start, (uint32_t)c.tl * 4u);
+  float4 a[kSegRows], h[kSegRows];
+#pragma unroll
+  for (int r = 0; r < kSegRows; ++r) a[r] = ld_buf4<false>(rx, (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u);
+  if (XH) {
+#pragma unroll
+    for (int r = 0; r < kSegRows; ++r) h[r] = ld_buf4<false>(rh, (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u);
+  }
+#pragma unroll
+  for (int r = 0; r < kSegRows; ++r) {
+    v[r][0] = a[r].x; v[r][1] = a[r].y; v[r][2] = a[r].z; v[r][3] = a[r].w;
+    if (XH) { v[r][0] -= h[r].x; v[r][1] -= h[r].y; v[r][2] -= h[r].z; v[r][3] -= h[r].w; }
+  }
+}
+
+CHOCO_DEV int tile_elem(int r, int q) { return r * 4 * kSegThreads + 4 * (int)threadIdx.x + q; }
+
+template <int MODE>
+CHOCO_DEV uint32_t tile_key(const TileCtx& c, uint64_t sseed, int e, float v) {
+  if (MODE == kHash) return rank_hash(sseed, (uint32_t)(c.start - c.R.off + e)) >> 1;
+  return fkey(v);
+}
+
+// Over hist[kH] in LDS or global memory (ascending key order), the bin holding
+// the rank-th largest entry and the rank inside it -> out[0], out[1].  Two bins
+// per thread of the kSegThreads workgroup; ends with a barrier.
+CHOCO_DEV void block_find_rank2k(uint32_t h0, uint32_t h1, uint32_t rank, uint32_t* scratch, uint32_t* out) {
+  const int tid = threadIdx.x;
+  const uint32_t local = h0 + h1;
+  uint32_t total;
+  const uint32_t pre = block_excl_scan(local, scratch, &total);
+  const uint32_t above = total - pre - local;  // entries in bins above my two
+  if (above < rank && rank <= above + local) {
+    if (rank <= above + h1) { out[0] = 2 * tid + 1; out[1] = rank - above; }
+    else { out[0] = 2 * tid; out[1] = rank - above - h1; }
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------- S1: coarse histogram
+template <int MODE, bool XH>
+__global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __restrict__ x,
+                                                               const float* __restrict__ xh,
+                                                               const int64_t* __restrict__ plan, int nseg,
+                                                               uint64_t seed, uint32_t* __restrict__ hist1) {
+  __shared__ uint32_t h[kH];
+  const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+  float v[kSegRows][4] = {};
+  if (MODE == kData) tile_load<XH>(x, xh, c, v);
+  for (int i = threadIdx.x; i < kH; i += kSegThreads) h[i] = 0u;
+  __syncthreads();
+  const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
+#pragma unroll
+  for (int r = 0; r < kSegRows; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tile_elem(r, q);
+      if (e < c.tl) atomicAdd(&h[tile_key<MODE>(c, sseed, e, v[r][q]) >> 20], 1u);
+    }
+  __syncthreads();
+  uint32_t* __restrict__ g = hist1 + (int64_t)c.s * kH;
+  for (int i = threadIdx.x; i < kH; i += kSegThreads)
+    if (h[i]) atomicAdd(&g[i], h[i]);
+}
+
+// ---------------------------------------------------------------- S2: coarse select + candidates
+template <int MODE, bool XH>
+__global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ plan, int nseg,
+    uint64_t seed, const uint32_t* __restrict__ hist1, uint32_t* __restrict__ hist2, uint32_t* __restrict__ info,
+    uint32_t* __restrict__ tilecnt, float* __restrict__ cval, uint32_t* __restrict__ cidx) {
+  __shared__ uint32_t h2[kH];
+  __shared__ uint32_t scratch[40];
+  __shared__ uint32_t bc[4];
+  const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+  const int tid = threadIdx.x;
+  float v[kSegRows][4] = {};
+  if (MODE == kData) tile_load<XH>(x, xh, c, v);  // in flight while b1 is found
+  const uint32_t* __restrict__ g1 = hist1 + (int64_t)c.s * kH;
+  const uint32_t c0 = g1[2 * tid], c1 = g1[2 * tid + 1];
+  for (int i = tid; i < kH; i += kSegThreads) h2[i] = 0u;
+  block_find_rank2k(c0, c1, (uint32_t)c.R.k, scratch, bc);
+  const uint32_t b1 = bc[0], kb = bc[1];
+  if (c.j == 0 && tid == 0) {
+    info[4 * c.s + 0] = b1;
+    info[4 * c.s + 1] = kb;
+  }
+  const uint32_t floor_key = b1 << 20;
+  const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
+  uint32_t run = 0;
+#pragma unroll
+  for (int r = 0; r < kSegRows; ++r) {
+    bool cand[4];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tile_elem(r, q);
+      const uint32_t key = tile_key<MODE>(c, sseed, e, v[r][q]);
+      cand[q] = e < c.tl && key >= floor_key;
+      cnt += cand[q] ? 1u : 0u;
+      if (cand[q] && (key >> 20) == b1) atomicAdd(&h2[(key >> 9) & (kH - 1)], 1u);
+    }
+    uint32_t tot;
+    uint32_t pos = run + block_excl_scan(cnt, scratch, &tot);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (cand[q]) {
+        const int e = tile_elem(r, q);
+        float val = v[r][q];
+        if (MODE == kHash) val = XH ? x[c.start + e] - xh[c.start + e] : x[c.start + e];
+        cval[c.slot + pos] = val;
+        cidx[c.slot + pos] = (uint32_t)(c.start + e);
+        ++pos;
+      }
+    }
+    run += tot;
+  }
+  __syncthreads();
+  uint32_t* __restrict__ g2 = hist2 + (int64_t)c.s * kH;
+  for (int i = tid; i < kH; i += kSegThreads)
+    if (h2[i]) atomicAdd(&g2[i], h2[i]);
+  if (tid == 0) tilecnt[blockIdx.x] = run;
+}
+
+// ---------------------------------------------------------------- S3: exact T per segment
+template <int MODE>
+__global__ __launch_bounds__(kSegThreads) void seg_select_kernel(
+    const int64_t* __restrict__ plan, int nseg, uint64_t seed, uint32_t* __restrict__ hist1,
+    uint32_t* __restrict__ hist2, uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt,
+    const float* __restrict__ cval, const uint32_t* __restrict__ cidx, uint32_t* __restrict__ tileout) {
+  __shared__ uint32_t h3[512];
+  __shared__ uint32_t tg[kSegMaxTiles], te[kSegMaxTiles];
+  __shared__ uint32_t scratch[40];
+  __shared__ uint32_t bc[4];
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int64_t ntile_all = plan[6];
+  const int s = (int)plan[(int64_t)kRow * nseg + ntile_all + blockIdx.x];
+  const SegRow R = seg_row(plan, s);
+  const uint64_t sseed = MODE == kHash ? seg_seed(seed, s) : 0;
+  const uint32_t b1 = info[4 * s + 0], kb = info[4 * s + 1];
+  uint32_t* __restrict__ g1 = hist1 + (int64_t)s * kH;
+  uint32_t* __restrict__ g2 = hist2 + (int64_t)s * kH;
+  const uint32_t c0 = g2[2 * tid], c1 = g2[2 * tid + 1];
+  if (tid < 512) h3[tid] = 0u;
+  block_find_rank2k(c0, c1, kb, scratch, bc);
+  const uint32_t b2 = bc[0], kc = bc[1];
+  // every tile of this segment has read hist1 / hist2 (earlier launches): reset them
+  g1[2 * tid] = 0u; g1[2 * tid + 1] = 0u;
+  g2[2 * tid] = 0u; g2[2 * tid + 1] = 0u;
+  const uint32_t P = (b1 << 20) | (b2 << 9);
+  auto key_at = [&](int64_t slot) -> uint32_t {
+    return MODE == kHash ? (rank_hash(sseed, cidx[slot] - (uint32_t)R.off) >> 1) : fkey(cval[slot]);
+  };
+  // bits 8..0 of the keys in fine bin (b1, b2): one wave per tile
+  for (int64_t t = w; t < R.ntile; t += kSegThreads / 64) {
+    const int64_t base = (R.t0 + t) * kSegTile;
+    const uint32_t cnt = tilecnt[R.t0 + t];
+    for (uint32_t i = lane; i < cnt; i += 64) {
+      const uint32_t key = key_at(base + i);
+      if ((key >> 9) == (P >> 9)) atomicAdd(&h3[key & 511u], 1u);
+    }
+  }
+  __syncthreads();
+  {
+    const uint32_t hv = tid < 512 ? h3[tid] : 0u;
+    uint32_t total;
+    const uint32_t pre = block_excl_scan(hv, scratch, &total);
+    const uint32_t above = total - pre - hv;
+    if (tid < 512 && above < kc && kc <= above + hv) { bc[2] = (uint32_t)tid; bc[3] = kc - above; }
+    __syncthreads();
+  }
+  const uint32_t T = P | bc[2];
+  const uint32_t r = bc[3];  // ties at T to take (>= 1)
+  // per tile: #keys > T, #keys == T (one wave per tile)
+  for (int64_t t = w; t < R.ntile; t += kSegThreads / 64) {
+    const int64_t base = (R.t0 + t) * kSegTile;
+    const uint32_t cnt = tilecnt[R.t0 + t];
+    uint32_t gt = 0, eq = 0;
+    for (uint32_t i = lane; i < cnt; i += 64) {
+      const uint32_t key = key_at(base + i);
+      gt += key > T ? 1u : 0u;
+      eq += key == T ? 1u : 0u;
+    }
+    gt = wave_sum(gt);
+    eq = wave_sum(eq);
+    if (lane == 0) { tg[t] = gt; te[t] = eq; }
+  }
+  __syncthreads();
+  {
+    const bool mine = tid < R.ntile;
+    const uint32_t gv = mine ? tg[tid] : 0u, ev = mine ? te[tid] : 0u;
+    uint32_t gpre, epre, gtot, etot;
+    block_excl_scan2(gv, ev, scratch, &gpre, &epre, &gtot, &etot);
+    if (mine) {
+      const uint32_t taken = min(r, epre);  // ties taken by earlier tiles (lowest index first)
+      const uint32_t share = min(ev, r - taken);
+      tileout[2 * (R.t0 + tid)] = gpre + taken;
+      tileout[2 * (R.t0 + tid) + 1] = share | (share == ev ? 0x80000000u : 0u);  // bit 31: every tie
+    }
+  }
+  if (tid == 0) info[4 * s + 2] = T;
+}
+
+// ---------------------------------------------------------------- S4: ordered emission
+template <int MODE>
+__global__ __launch_bounds__(kSegThreads) void seg_emit_kernel(
+    const int64_t* __restrict__ plan, int nseg, uint64_t seed, int32_t is_biased, const uint32_t* __restrict__ info,
+    const uint32_t* __restrict__ tilecnt, const uint32_t* __restrict__ tileout, const float* __restrict__ cval,
+    const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx) {
+  __shared__ uint32_t scratch[40];
+  const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+  const int tid = threadIdx.x;
+  const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
+  const uint32_t T = info[4 * c.s + 2];
+  const uint32_t cnt = tilecnt[blockIdx.x];
+  const uint32_t o = tileout[2 * blockIdx.x], tw = tileout[2 * blockIdx.x + 1];
+  const uint32_t quota = tw & 0x7fffffffu;
+  const bool all_ties = (tw >> 31) != 0u;
+  const float scale = (MODE == kHash && !is_biased) ? (float)((double)c.R.len / (double)c.R.k) : 1.0f;
+  float* __restrict__ ov = out_val + c.R.out_off + o;
+  int32_t* __restrict__ oi = out_idx + c.R.out_off + o;
+  uint32_t run = 0, tie_run = 0;
+  for (uint32_t p0 = 0; p0 < cnt; p0 += kSegThreads) {  // workgroup-uniform
+    const uint32_t p = p0 + tid;
+    const bool valid = p < cnt;
+    const float v = valid ? cval[c.slot + p] : 0.f;
+    const uint32_t ix = valid ? cidx[c.slot + p] : 0u;
+    const uint32_t key = MODE == kHash ? (rank_hash(sseed, ix - (uint32_t)c.R.off) >> 1) : fkey(v);
+    const bool gt = valid && key > T, eq = valid && key == T;
+    bool sel;
+    if (all_ties || quota == 0u) {
+      sel = gt || (eq && all_ties);
+    } else {
+      uint32_t ntie;
+      const uint32_t trank = tie_run + block_excl_scan(eq ? 1u : 0u, scratch, &ntie);
+      sel = gt || (eq && trank < quota);
+      tie_run += ntie;
+    }
+    uint32_t nsel;
+    const uint32_t pos = run + block_excl_scan(sel ? 1u : 0u, scratch, &nsel);
+    if (sel) {
+      ov[pos] = v * scale;
+      oi[pos] = (int32_t)ix;
+    }
+    run += nsel;
+  }
+}
+
+// ---------------------------------------------------------------- host side
+static int64_t plan_tiles(const int64_t* plan_host) { return plan_host[6]; }
+static int64_t plan_batched(const int64_t* plan_host) { return plan_host[7]; }
+
+template <int MODE, bool XH>
+static int launch_batched(const float* x, const float* xh, const int64_t* plan_dev, const int64_t* plan_host,
+                          int nseg, uint64_t seed, int32_t is_biased, float* out_val, int32_t* out_idx,
+                          const SegWs& W, hipStream_t st) {
+  const unsigned ntile = (unsigned)plan_tiles(plan_host);
+  const unsigned nbat = (unsigned)plan_batched(plan_host);
+  profile_begin("topk_seg_hist", st);
+  CHOCO_KLAUNCH((seg_hist_kernel<MODE, XH>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg, seed,
+                W.hist1);
+  profile_end("topk_seg_hist", st);
+  CHOCO_LAUNCHED("seg_hist_kernel");
+  profile_begin("topk_seg_collect", st);
+  CHOCO_KLAUNCH((seg_collect_kernel<MODE, XH>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg, seed,
+                W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx);
+  profile_end("topk_seg_collect", st);
+  CHOCO_LAUNCHED("seg_collect_kernel");
+  profile_begin("topk_seg_select", st);
+  CHOCO_KLAUNCH((seg_select_kernel<MODE>), dim3(nbat), dim3(kSegThreads), 0, st, plan_dev, nseg, seed, W.hist1,
+                W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.tileout);
+  profile_end("topk_seg_select", st);
+  CHOCO_LAUNCHED("seg_select_kernel");
+  profile_begin("topk_seg_emit", st);
+  CHOCO_KLAUNCH((seg_emit_kernel<MODE>), dim3(ntile), dim3(kSegThreads), 0, st, plan_dev, nseg, seed, is_biased,
+                W.info, W.tilecnt, W.tileout, W.cval, W.cidx, out_val, out_idx);
+  profile_end("topk_seg_emit", st);
+  CHOCO_LAUNCHED("seg_emit_kernel");
+  return CHOCO_OK;
+}
+
+static size_t pipeline_ws(const int64_t* plan_host, int nseg) {
+  size_t need = 0;
+  for (int s = 0; s < nseg; ++s) {
+    const int64_t* p = plan_host + (int64_t)kRow * s;
+    if (p[5] == 0) need = std::max(need, topk_ws_bytes(p[1]));
+  }
+  return need;
+}
+
+template <int MODE>
+static int segmented(const float* x, const float* xhat, const int64_t* plan_dev, const int64_t* plan_host,
+                     int32_t nseg, uint64_t seed, int32_t is_biased, float* out_val, int32_t* out_idx, void* ws,
+                     size_t ws_bytes, hipStream_t st) {
+  CHOCO_REQUIRE(x && plan_dev && plan_host && out_val && out_idx && nseg > 0, "null pointer argument");
+  CHOCO_REQUIRE(aligned4(x) && (xhat == nullptr || aligned4(xhat)), "x/xhat must be 4-byte aligned");
+  const int64_t* last = plan_host + (int64_t)kRow * (nseg - 1);
+  CHOCO_REQUIRE(last[0] + last[1] < (int64_t)INT32_MAX, "total length must be < 2^31");
+  const int64_t ntile = plan_tiles(plan_host);
+  const SegLayout L = seg_layout(nseg, ntile);
+  const size_t need = L.total + pipeline_ws(plan_host, nseg);
+  CHOCO_REQUIRE(ws != nullptr && ws_bytes >= need, "segmented top-k workspace too small: need %zu bytes, got %zu",
+                need, ws_bytes);
+  char* base = static_cast<char*>(ws);
+  if (ntile > 0) {
+    SegWs W{reinterpret_cast<uint32_t*>(base + L.off_h1), reinterpret_cast<uint32_t*>(base + L.off_h2),
+            reinterpret_cast<uint32_t*>(base + L.off_info), reinterpret_cast<uint32_t*>(base + L.off_cnt),
+            reinterpret_cast<uint32_t*>(base + L.off_out), reinterpret_cast<float*>(base + L.off_cval),
+            reinterpret_cast<uint32_t*>(base + L.off_cidx)};
+    const int rc = xhat ? launch_batched<MODE, true>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val,
+                                                     out_idx, W, st)
+                        : launch_batched<MODE, false>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val,
+                                                      out_idx, W, st);
+    if (rc) return rc;
+  }
+  // segments over kSegBatchMax elements: the flat pipeline, one after another
+  // (its workspace follows the batched one: the batched histograms must stay zero)
+  for (int s = 0; s < nseg; ++s) {
+    const int64_t* p = plan_host + (int64_t)kRow * s;
+    if (p[5] != 0) continue;
+    const uint64_t sd = MODE == kHash ? seg_seed(seed, s) : 0;
+    const float scale = (MODE == kHash && !is_biased) ? (float)((double)p[1] / (double)p[2]) : 1.0f;
+    const int rc = topk_pipeline(MODE, x + p[0], xhat ? xhat + p[0] : nullptr, p[1], p[2], sd, scale,
+                                 out_val + p[3], out_idx + p[3], p[0], base + L.total, ws_bytes - L.total, st);
+    if (rc) return rc;
+  }
+  return CHOCO_OK;
+}
+
+}  // namespace choco
+
+using namespace choco;
+
+static int seg_plan_scan(const int64_t* seg_off_host, int32_t nseg, int64_t* ntile, int64_t* nbat) {
+  if (seg_off_host == nullptr || nseg <= 0) return fail(CHOCO_ERR_INVALID, "bad segment table");
+  *ntile = 0;
+  *nbat = 0;
+  for (int s = 0; s < nseg; ++s) {
+    const int64_t len = seg_off_host[s + 1] - seg_off_host[s];
+    if (len <= 0) return fail(CHOCO_ERR_INVALID, "segment %d has length %lld", s, (long long)len);
+    if (len <= kSegBatchMax) {
+      *ntile += (len + kSegTile - 1) / kSegTile;
+      *nbat += 1;
+    }
+  }
+  return CHOCO_OK;
+}
+
+CHOCO_API int64_t choco_topk_segmented_plan_len(const int64_t* seg_off_host, int32_t nseg) {
+  int64_t ntile, nbat;
+  const int rc = seg_plan_scan(seg_off_host, nseg, &ntile, &nbat);
+  if (rc) return rc;
+  return (int64_t)kRow * nseg + ntile + nbat;
+}
+
+CHOCO_API int64_t choco_topk_segmented_plan(const int64_t* seg_off_host, int32_t nseg, double ratio,
+                                            int64_t* plan_host) {
+  int64_t ntile, nbat;
+  const int rc = seg_plan_scan(seg_off_host, nseg, &ntile, &nbat);
+  if (rc) return rc;
+  CHOCO_REQUIRE(ratio >= 0.0 && ratio < 1.0, "compress ratio must be in [0, 1), got %g", ratio);
+  int64_t out = 0, t0 = 0, b = 0;
+  for (int s = 0; s < nseg; ++s) {
+    const int64_t off = seg_off_host[s], len = seg_off_host[s + 1] - seg_off_host[s];
+    const int64_t k = choco_topk_k(len, ratio);
+    const int64_t nt = len <= kSegBatchMax ? (len + kSegTile - 1) / kSegTile : 0;
+    if (plan_host) {
+      int64_t* p = plan_host + (int64_t)kRow * s;
+      p[0] = off; p[1] = len; p[2] = k; p[3] = out; p[4] = t0; p[5] = nt; p[6] = 0; p[7] = 0;
+      for (int64_t t = 0; t < nt; ++t) plan_host[(int64_t)kRow * nseg + t0 + t] = s;
+      if (nt) plan_host[(int64_t)kRow * nseg + ntile + b++] = s;
+    }
+    t0 += nt;
+    out += k;
+  }
+  if (plan_host) {
+    plan_host[6] = ntile;
+    plan_host[7] = nbat;
+  }
+  return out;
+}
+
+CHOCO_API size_t choco_topk_segmented_workspace_size(const int64_t* plan_host, int32_t nseg) {
+  if (!plan_host || nseg <= 0) return 256;
+  return seg_layout(nseg, plan_tiles(plan_host)).total + pipeline_ws(plan_host, nseg) + 256;
+}
+
+CHOCO_API int choco_topk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
+                                            const int64_t* plan_host, int32_t nseg, float* out_val,
+                                            int32_t* out_idx, void* ws, size_t ws_bytes, void* stream) {
+  return segmented<kData>(x, xhat, plan_dev, plan_host, nseg, 0, 1, out_val, out_idx, ws, ws_bytes,
+                          as_stream(stream));
+}
+
+CHOCO_API int choco_randk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
+                                             const int64_t* plan_host, int32_t nseg, uint64_t seed,
+                                             int32_t is_biased, float* out_val, int32_t* out_idx, void* ws,
+                                             size_t ws_bytes, void* stream) {
+  return segmented<kHash>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, ws, ws_bytes,
+                          as_stream(stream));
+}

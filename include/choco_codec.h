@@ -66,11 +66,21 @@ int choco_topk_compress(const float* x, const float* xhat, int64_t n, int64_t k,
 /* Per-segment top-k (one tensor per segment, as the reference loops over
  * parameter tensors): k_s = choco_topk_k(len_s, ratio), outputs concatenated in
  * segment order, indices GLOBAL (segment offset added in integer arithmetic --
- * the reference adds it in fp32, sparsification.py:76).
- * choco_topk_segmented_plan fills a HOST plan of nseg rows {off, len, k_s, out_off}
- * (int64 x 4) from the HOST table seg_off[nseg+1] and returns K = sum k_s (the
- * reference's selected_shapes are the k_s, parallel_choco_v.py:245).  The caller
- * keeps a DEVICE copy of the plan (plan_dev) and passes both on every call. */
+ * the reference adds it in fp32, sparsification.py:76).  Every segment of up to
+ * 16M elements is cut into 16K-element tiles and ALL of them are selected in the
+ * same four launches (topk_seg.hip); longer segments run the flat pipeline.
+ * choco_topk_segmented_plan fills a HOST int64 plan of
+ * choco_topk_segmented_plan_len(seg_off, nseg) entries from the HOST table
+ * seg_off[nseg+1]: nseg rows of 8 {off, len, k_s, out_off, first tile, tiles, ., .}
+ * (row 0's last two = total tiles, batched segments), then the tile -> segment
+ * map, then the batched segment ids.  It returns K = sum k_s (the reference's
+ * selected_shapes are the k_s, parallel_choco_v.py:245); ratio must be in [0, 1).
+ * The caller keeps a DEVICE copy of the whole plan (plan_dev) and passes both on
+ * every call.  x / xhat need only 4-byte alignment.  The workspace
+ * (choco_topk_segmented_workspace_size) is bound to ONE plan: its per-segment
+ * histograms are left zeroed for the next call of that plan, so a workspace that
+ * served another plan or call must be zero-filled again first. */
+int64_t choco_topk_segmented_plan_len(const int64_t* seg_off_host, int32_t nseg);
 int64_t choco_topk_segmented_plan(const int64_t* seg_off_host, int32_t nseg, double ratio,
                                   int64_t* plan_host);
 size_t choco_topk_segmented_workspace_size(const int64_t* plan_host, int32_t nseg);

@@ -66,16 +66,31 @@ def test_segmented_plan(lib):
     lens = golden_json("layouts.json")["resnet50_imagenet"]
     offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     p_off, keep = _lib.i64_array(offs.tolist())
-    plan = (ctypes.c_int64 * (4 * len(lens)))()
+    plen = lib.choco_topk_segmented_plan_len(p_off, len(lens))
+    tiles = [(m + 16383) // 16384 for m in lens]  # every ResNet-50 tensor is batched (< 16M)
+    assert plen == 8 * len(lens) + sum(tiles) + len(lens)
+    plan = (ctypes.c_int64 * plen)()
     total = lib.choco_topk_segmented_plan(p_off, len(lens), 0.99,
                                           ctypes.cast(plan, ctypes.POINTER(ctypes.c_int64)))
-    rows = np.array(list(plan)).reshape(-1, 4)
+    flat = np.array(list(plan))
+    rows = flat[:8 * len(lens)].reshape(-1, 8)
     ks = [O.topk_k(m, 0.99) for m in lens]
     assert total == sum(ks)
     assert rows[:, 0].tolist() == offs[:-1].tolist()
     assert rows[:, 1].tolist() == lens
     assert rows[:, 2].tolist() == ks
     assert rows[:, 3].tolist() == np.concatenate([[0], np.cumsum(ks)[:-1]]).tolist()
+    assert rows[:, 4].tolist() == np.concatenate([[0], np.cumsum(tiles)[:-1]]).tolist()
+    assert rows[:, 5].tolist() == tiles
+    assert rows[0, 6] == sum(tiles) and rows[0, 7] == len(lens)
+    tmap = flat[8 * len(lens):8 * len(lens) + sum(tiles)]
+    assert tmap.tolist() == np.repeat(np.arange(len(lens)), tiles).tolist()
+    assert flat[8 * len(lens) + sum(tiles):].tolist() == list(range(len(lens)))
+    # a segment over 16M elements is routed to the flat pipeline (no tiles)
+    big = np.array([0, 5, 5 + 20_000_000], dtype=np.int64)
+    pb, keep2 = _lib.i64_array(big.tolist())
+    assert lib.choco_topk_segmented_plan_len(pb, 2) == 16 + 1 + 1
+    assert lib.choco_topk_segmented_plan(pb, 2, 1.5, None) < 0  # ratio outside [0, 1)
 
 
 def test_error_reporting(lib):

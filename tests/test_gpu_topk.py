@@ -167,6 +167,49 @@ def test_topk_segmented_unaligned_large(ratio):
     assert same_bits(host(vals), ov)
 
 
+@pytest.mark.parametrize("case", ["ties", "ratio0", "ratio05", "nan", "tile_edges", "huge_mixed"])
+def test_topk_segmented_edge_layouts(case):
+    """The batched segmented select (topk_seg.hip) on tie-heavy tensors, k = len, k = len/2,
+    NaN, tensors at tile edges (16384 +- 1, exactly 1024 tiles) and a tensor over 16M
+    elements that takes the flat pipeline next to batched ones."""
+    from chocosgd_amd import codec
+    ratio = {"ratio0": 0.0, "ratio05": 0.5}.get(case, 0.99)
+    if case == "tile_edges":
+        lens = [16383, 16384, 16385, 1, 16_777_216, 32768]
+    elif case == "huge_mixed":
+        lens = [7, 20_000_001, 3000, 1_100_001]
+    else:
+        lens = [100, 50_000, 16384, 16385, 3, 700_001]
+    n = sum(lens)
+    x, xh = randn(n, 61), randn(n, 62, 0.5)
+    if case == "ties":
+        x = torch.round(x * 2) / 2
+        xh = torch.zeros_like(x)
+    if case == "nan":
+        x[[5, 60_000, 90_000]] = float("nan")
+    plan = codec.SegmentPlan(lens, ratio, x.device)
+    vals, idx = codec.topk_segmented(x, plan, xhat=xh)
+    ov, oi, ks = O.topk_segmented(host(x) - host(xh), lens, ratio)
+    assert plan.k_per_seg == ks
+    assert np.array_equal(host(idx).astype(np.int64), oi)
+    assert same_bits(host(vals), ov)
+
+
+def test_topk_segmented_repeat_calls_self_clean():
+    """Workspace histograms are reset by every call: repeated calls on new data stay exact."""
+    from chocosgd_amd import codec
+    layouts = [golden_json("layouts.json")["resnet20_cifar10"], UNALIGNED_LAYOUT]
+    plans = [codec.SegmentPlan(lens, r, torch.device(DEV)) for lens, r in zip(layouts, (0.9, 0.99))]
+    for seed in range(4):  # two plans interleaved, each on new data
+        lens, plan = layouts[seed % 2], plans[seed % 2]
+        x = randn(sum(lens), 70 + seed)
+        vals, idx = codec.topk_segmented(x, plan)
+        ov, oi, _ = O.topk_segmented(host(x), lens, (0.9, 0.99)[seed % 2])
+        assert np.array_equal(host(idx).astype(np.int64), oi)
+        assert same_bits(host(vals), ov)
+        codec.topk(x, codec.topk_k(x.numel(), 0.99))  # the flat path's workspace is separate
+
+
 @pytest.mark.parametrize("layout", ["unaligned", "resnet20_cifar10"])
 @pytest.mark.parametrize("is_biased", [True, False])
 def test_randk_segmented_vs_oracle(layout, is_biased):
