@@ -248,25 +248,30 @@ CHOCO_DEV int seg_of(const int64_t* __restrict__ seg_off, int nseg, int64_t e) {
 }
 
 // ---------------------------------------------------------------- RNG
-// Philox4x32-10 (Salmon et al., SC'11).  u = (bits >> 8) * 2^-24 in [0,1).
-struct Philox4 { uint32_t x, y, z, w; };
-
-CHOCO_DEV Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                uint32_t k0, uint32_t k1) {
-  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
-  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
-    uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
-    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
-    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
-    k0 += W0; k1 += W1;
-  }
-  return Philox4{c0, c1, c2, c3};
+// SplitMix64 (Steele, Lea & Flood, OOPSLA 2014; passes BigCrush): the output
+// function of the splitmix64 generator, used in counter mode -- the value at
+// counter c of stream `key` is mix(key + (c + 1) * gamma), exactly the
+// generator's own sequence from state `key`.  Integer multiplies are quarter
+// rate on CDNA: two 64-bit mixes per 4 uniforms cost ~3x less VALU time than
+// Philox4x32-10 (40 32-bit multiplies per 4 uniforms), which made the QSGD
+// quantize pass ALU-bound.
+constexpr uint64_t kGoldenGamma = 0x9E3779B97F4A7C15ull;
+CHOCO_DEV __host__ inline uint64_t splitmix64_mix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
 }
-
-CHOCO_DEV float u24(uint32_t b) { return (float)(b >> 8) * 5.9604644775390625e-08f; }
+// QSGD uniform stream of (seed, offset): key = mix(seed + (offset + 1) * 0xD1B54A32D192ED03);
+// elements 2p and 2p+1 take bits 63..40 and 31..8 of mix(key + (p + 1) * gamma), * 2^-24.
+CHOCO_DEV __host__ inline uint64_t qrng_key(uint64_t seed, uint64_t offset) {
+  return splitmix64_mix(seed + (offset + 1) * 0xD1B54A32D192ED03ull);
+}
+CHOCO_DEV float u24(uint32_t b24) { return (float)b24 * 5.9604644775390625e-08f; }
+CHOCO_DEV void qrng_pair(uint64_t key, uint64_t p, float& u0, float& u1) {
+  const uint64_t z = splitmix64_mix(key + (p + 1) * kGoldenGamma);
+  u0 = u24((uint32_t)(z >> 40));
+  u1 = u24((uint32_t)(z >> 8) & 0xFFFFFFu);
+}
 
 // Seeded 32-bit bijective mixer used as the random-k ranking key
 // (murmur3 fmix32 of a seeded Weyl sequence).
@@ -283,10 +288,7 @@ CHOCO_DEV uint32_t rank_hash(uint64_t seed, uint32_t i) {
 // splitmix64 of seed + (s + 1) * golden gamma, so every segment draws an independent
 // ranking (the reference calls np.random.choice once per tensor, sparsification.py:48).
 CHOCO_DEV __host__ inline uint64_t seg_seed(uint64_t seed, int64_t s) {
-  uint64_t z = seed + (uint64_t)(s + 1) * 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
+  return splitmix64_mix(seed + (uint64_t)(s + 1) * kGoldenGamma);
 }
 
 // ---------------------------------------------------------------- top-k internals

@@ -252,6 +252,13 @@ CHOCO_DEV int tile_seg(const int64_t* __restrict__ seg_off, int nseg, int64_t e0
   return s_seg[0];
 }
 
+// 8 elements per thread: one 4*CW-bit level store and one sign byte.  Measured
+// against a wave-batch form that transposes the outputs through LDS into 16-B
+// level / 4-B sign stores per lane: 123 vs 135 us at 100M in the bench step --
+// this pass is bound by the stream (and by the write-back of the dirty lines
+// the previous step's receiver left in the Infinity Cache), not by its stores.
+// Its VALU work is dominated by the uniforms: SplitMix64 (choco_common.h) took
+// the pass from 126 to 123 us against Philox4x32-10.
 template <int CW>
 __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, const int64_t* __restrict__ seg_off,
@@ -296,13 +303,10 @@ __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
 #pragma unroll
     for (int c = 0; c < kQPer; ++c) u[c] = (e0 + c < n) ? u_in[e0 + c] : 0.f;
   } else {
-    const uint64_t g = (uint64_t)e0 >> 2;
+    const uint64_t key = qrng_key(seed, offset);
+    const uint64_t p = (uint64_t)e0 >> 1;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const Philox4 r = philox4x32_10((uint32_t)(g + h), (uint32_t)((g + h) >> 32), (uint32_t)offset,
-                                      (uint32_t)(offset >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
-      u[4 * h + 0] = u24(r.x); u[4 * h + 1] = u24(r.y); u[4 * h + 2] = u24(r.z); u[4 * h + 3] = u24(r.w);
-    }
+    for (int h = 0; h < 4; ++h) qrng_pair(key, p + h, u[2 * h], u[2 * h + 1]);
   }
   QParam P = qparam(norms, seg_off, n, sg0, s_levels, biased != 0);
   uint32_t lv[kQPer];
@@ -519,11 +523,11 @@ CHOCO_API int choco_qsgd_compress(const float* x, const float* xhat, int64_t n, 
   uint8_t* sign_plane = packed + plane_bytes(n, cw);
   const int64_t ntiles = (n + kQTile - 1) / kQTile;
   profile_begin("qsgd_quantize", st);
-#define CHOCO_Q(CWV)                                                                                         \
-  case CWV:                                                                                                  \
-    CHOCO_KLAUNCH((qsgd_quant_kernel<CWV>), dim3((unsigned)ntiles), dim3(kQThreads), 0, st, x, xhat, n, \
-                       seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane, sign_plane, \
-                       dense_out, ntiles);                                                                   \
+#define CHOCO_Q(CWV)                                                                                          \
+  case CWV:                                                                                                   \
+    CHOCO_KLAUNCH((qsgd_quant_kernel<CWV>), dim3((unsigned)ntiles), dim3(kQThreads), 0, st, x, xhat, n,      \
+                  seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane, sign_plane,        \
+                  dense_out, ntiles);                                                                         \
     break;
   switch (cw) {
     CHOCO_Q(1)

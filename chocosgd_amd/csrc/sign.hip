@@ -654,6 +654,134 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
   }
 }
 
+// One-segment receiver (nseg == 1, the flat buffer; n * 4 < 2^32 bytes).  A wave
+// owns 1024 consecutive columns (words) as 4 sub-runs of 256: lane l holds words
+// j0 + 256s + 4l .. +3 of every message, so in row r its elements are the 1024
+// CONSECUTIVE floats r*N' + j0 .. +1023 -- 4 KiB runs instead of 1 KiB ones.
+// Every lane loads and stores the float4 at its OWN element offset with
+// dword-aligned buffer loads / stores (N' = 2 mod 4 at both BASELINE sizes, so
+// half the rows start 8 B off a 16-B boundary): no realigning shuffle, no tail
+// element, and a line shared with the neighbouring wave only at the two ends of
+// each 4 KiB run.  Rows go in pairs with two pairs in flight (A/B).
+// Measured SLOWER than the column-tile receiver (1208 vs 1127 us at 345M, one
+// message): the dword-aligned 16-B stores cost more than the longer runs save.
+// Kept as a diagnostic variant (CHOCO_SIGN_ACC1=1).
+#ifndef CHOCO_SIGN_ACC1
+#define CHOCO_SIGN_ACC1 0
+#endif
+constexpr int kSA1Cols = 1024;               // columns per wave
+constexpr int kSA1Waves = 4;
+constexpr int kSA1WgCols = kSA1Cols * kSA1Waves;
+constexpr int kSA1RU = 2;                    // rows per group
+
+CHOCO_DEV void st_buf4s(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, float4 v) {
+  choco_f32x4 f;
+  f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, f), r,
+                                         voff, soff, 0);
+}
+
+template <int NM, bool HS>
+__global__ __launch_bounds__(64 * kSA1Waves) void sign_accumulate1_kernel(SignMsgs M, int64_t n, int64_t Np,
+                                                                          float* __restrict__ hat,
+                                                                          float* __restrict__ mem) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int64_t j0 = (int64_t)blockIdx.x * kSA1WgCols + (int64_t)w * kSA1Cols;
+  if (j0 >= Np) return;  // wave-uniform; no workgroup barrier in this kernel
+  const int ncol = (int)std::min<int64_t>(kSA1Cols, Np - j0);
+  float sc[kMaxMsg];
+#pragma unroll
+  for (int q = 0; q < NM; ++q) sc[q] = M.norms[q][0] / (float)n;  // (norm / numel), exact per message
+  uint32_t wd[NM][4][4];
+#pragma unroll
+  for (int q = 0; q < NM; ++q)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int64_t j = j0 + 256 * s + 4 * lane;
+      if (j + 3 < Np) {
+        const uint4 v = *reinterpret_cast<const uint4*>(M.packed[q] + j);
+        wd[q][s][0] = v.x; wd[q][s][1] = v.y; wd[q][s][2] = v.z; wd[q][s][3] = v.w;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wd[q][s][c] = (j + c < Np) ? M.packed[q][j + c] : 0u;
+      }
+    }
+  auto apply = [&](int r, int s, float4 h4, float4 m4, float4& ho, float4& mo) {
+    float hv[4] = {h4.x, h4.y, h4.z, h4.w}, mv[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int q = 0; q < NM; ++q) {
+        const float u = ((wd[q][s][c] >> r) & 1u) ? -sc[q] : sc[q];
+        if (HS && q == M.self_slot) hv[c] = hv[c] + u;
+        mv[c] = fmaf(M.w[q], u, mv[c]);  // torch add_(u, alpha=w) fuses on CPU (verified)
+      }
+    }
+    ho = make_float4(hv[0], hv[1], hv[2], hv[3]);
+    mo = make_float4(mv[0], mv[1], mv[2], mv[3]);
+  };
+  const bool interior = ncol == kSA1Cols && (int64_t)31 * Np + j0 + kSA1Cols <= n;
+  if (interior) {
+    const __amdgpu_buffer_rsrc_t rm = buf_rsrc(mem, (uint32_t)(n * 4));
+    const __amdgpu_buffer_rsrc_t rh = buf_rsrc(HS ? hat : mem, (uint32_t)(n * 4));
+    const uint32_t voff = 16u * (uint32_t)lane;
+    auto row_off = [&](int r) -> uint32_t { return (uint32_t)(((int64_t)r * Np + j0) * 4); };  // wave-uniform
+    auto load = [&](int g, float4 (&Mr)[kSA1RU][4], float4 (&Hr)[kSA1RU][4]) {
+#pragma unroll
+      for (int u = 0; u < kSA1RU; ++u)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          Mr[u][s] = ld_buf4s<false>(rm, voff + 1024u * s, row_off(g * kSA1RU + u));
+          if (HS) Hr[u][s] = ld_buf4s<false>(rh, voff + 1024u * s, row_off(g * kSA1RU + u));
+        }
+    };
+    auto proc = [&](int g, const float4 (&Mr)[kSA1RU][4], const float4 (&Hr)[kSA1RU][4]) {
+#pragma unroll
+      for (int u = 0; u < kSA1RU; ++u)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          float4 ho, mo;
+          apply(g * kSA1RU + u, s, HS ? Hr[u][s] : Mr[u][s], Mr[u][s], ho, mo);
+          st_buf4s(rm, voff + 1024u * s, row_off(g * kSA1RU + u), mo);
+          if (HS) st_buf4s(rh, voff + 1024u * s, row_off(g * kSA1RU + u), ho);
+        }
+    };
+    constexpr int NG = 32 / kSA1RU;
+    float4 MA[kSA1RU][4], HA[kSA1RU][4], MB[kSA1RU][4], HB[kSA1RU][4];
+    load(0, MA, HA);
+    load(1, MB, HB);
+#pragma unroll 1
+    for (int g = 0; g < NG; g += 2) {
+      proc(g, MA, HA);
+      if (g + 2 < NG) load(g + 2, MA, HA);
+      proc(g + 1, MB, HB);
+      if (g + 3 < NG) load(g + 3, MB, HB);
+    }
+    return;
+  }
+  // the last waves: guarded element path
+#pragma unroll 1
+  for (int r = 0; r < 32; ++r) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int col = 256 * s + 4 * lane;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int64_t e = (int64_t)r * Np + j0 + col + c;
+        if (col + c >= ncol || e >= n) continue;
+        float h = HS ? hat[e] : 0.f, m = mem[e];
+#pragma unroll
+        for (int q = 0; q < NM; ++q) {
+          const float u = ((wd[q][s][c] >> r) & 1u) ? -sc[q] : sc[q];
+          if (HS && q == M.self_slot) h = h + u;
+          m = fmaf(M.w[q], u, m);
+        }
+        mem[e] = m;
+        if (HS) hat[e] = h;
+      }
+    }
+  }
+}
 
 }  // namespace choco
 
@@ -755,6 +883,32 @@ CHOCO_API int choco_sign_decompress_accumulate(const int32_t* const* packed_list
   const int64_t Np = choco_sign_words(n);
   const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
   profile_begin("sign_accumulate", st);
+  if (nseg == 1 && n < (int64_t(1) << 30) && CHOCO_SIGN_ACC1) {
+    const unsigned g1 = (unsigned)((Np + kSA1WgCols - 1) / kSA1WgCols);
+#define CHOCO_SIGN_ACC1_CASE(NM)                                                                            \
+  case NM:                                                                                                  \
+    if (self_slot >= 0 && xhat_self)                                                                        \
+      CHOCO_KLAUNCH((sign_accumulate1_kernel<NM, true>), dim3(g1), dim3(64 * kSA1Waves), 0, st, M, n, Np,   \
+                    xhat_self, memory);                                                                     \
+    else                                                                                                    \
+      CHOCO_KLAUNCH((sign_accumulate1_kernel<NM, false>), dim3(g1), dim3(64 * kSA1Waves), 0, st, M, n, Np,  \
+                    xhat_self, memory);                                                                     \
+    break;
+    switch (nmsg) {
+      CHOCO_SIGN_ACC1_CASE(1)
+      CHOCO_SIGN_ACC1_CASE(2)
+      CHOCO_SIGN_ACC1_CASE(3)
+      CHOCO_SIGN_ACC1_CASE(4)
+      CHOCO_SIGN_ACC1_CASE(5)
+      CHOCO_SIGN_ACC1_CASE(6)
+      CHOCO_SIGN_ACC1_CASE(7)
+      CHOCO_SIGN_ACC1_CASE(8)
+    }
+#undef CHOCO_SIGN_ACC1_CASE
+    profile_end("sign_accumulate", st);
+    CHOCO_LAUNCHED("sign_accumulate1_kernel");
+    return CHOCO_OK;
+  }
 #define CHOCO_SIGN_ACC(NM)                                                                                 \
   case NM:                                                                                                  \
     if (self_slot >= 0 && xhat_self)                                                                        \

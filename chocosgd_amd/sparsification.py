@@ -11,7 +11,7 @@ Deliberate differences (all documented in DESIGN.md):
   * random-k indices are drawn on the device from a seeded hash ranking instead of
     the host's numpy RandomState (sparsification.py:48); the seed is taken from
     torch's default generator, so torch.manual_seed makes runs reproducible.
-  * QSGD uniforms come from an in-kernel Philox4x32-10 stream instead of
+  * QSGD uniforms come from an in-kernel SplitMix64 counter stream instead of
     torch.rand_like (sparsification.py:91); norms are fp64-accumulated (the
     reference's fp32 CPU norm drifts by up to 1e-2 relative at 1e8 elements).
 """

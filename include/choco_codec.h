@@ -175,7 +175,10 @@ int choco_sign_decompress_accumulate(const int32_t* const* packed_list,
  *   norm_s  = ||d_s||_2 (fp64 accumulation, rounded once)   or norm_in[s] if given
  *   lf      = ((float)s * |d|) / norm_s
  *   level   = floor(lf) + (u < lf - floor(lf)),  u = u_in[e] if given, else
- *             Philox4x32-10(seed, counter = offset + e)
+ *             this codec's SplitMix64 counter stream: key = mix(seed + (offset+1) *
+ *             0xD1B54A32D192ED03), z = mix(key + (e/2 + 1) * 0x9E3779B97F4A7C15),
+ *             u = (even e: z >> 40, odd e: (z >> 8) & 0xFFFFFF) * 2^-24
+ *             (the reference draws torch.rand_like, sparsification.py:91)
  * Wire format (packed, choco_qsgd_packed_bytes): level plane (container of
  * cw = 1,2,4,8,16 bits >= q, little-endian within 32-bit words) followed by a
  * sign plane (1 bit/element, bit set <=> d < 0), both padded to 16 bytes.

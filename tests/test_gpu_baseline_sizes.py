@@ -80,7 +80,7 @@ def test_sign_345M_words_norm_accumulate():
 
 def test_qsgd_100M_levels_wire_decode():
     """cfg 3: n = 100,000,000, q = 4 (s = 15).  Sampled levels and signs on the wire vs the
-    oracle (device Philox uniforms restated), the dense decode of those elements bit-exact,
+    oracle (the device SplitMix64 uniforms restated), the dense decode of those elements bit-exact,
     and the norm vs fp64."""
     from chocosgd_amd import codec
     n, q = 100_000_000, 4
@@ -93,7 +93,7 @@ def test_qsgd_100M_levels_wire_decode():
     assert abs(nrm - exact) <= 1e-6 * exact
     idx = _sample(0, n, 1 << 20, 9)
     d = host(x[torch.from_numpy(idx).to(DEV)])
-    u = O.philox_uniforms_at(idx, seed, offset)
+    u = O.qsgd_uniforms_at(idx, seed, offset)
     lvl = O.qsgd_levels(d, s, u, nrm)
     exp_lvl = np.minimum(lvl, s).astype(np.int64)
     got_lvl, got_neg = O.qsgd_wire_at(host(packed), n, q, idx)

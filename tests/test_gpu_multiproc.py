@@ -68,7 +68,7 @@ def test_choco_round_across_processes(comm_op, world, tmp_path):
             hb = 4 * _hdr(nseg)
             norms = rcv[:hb].view(np.float32)[:nseg]
             assert np.allclose(norms, O.l2_norms(d, lens), rtol=1e-6, atol=0)
-            u = O.philox_uniforms(n, 1000 + q, 0)
+            u = O.qsgd_uniforms(n, 1000 + q, 0)
             lvl, dec, off = [], [], 0
             for s, m in enumerate(lens):
                 lvl.append(O.qsgd_levels(d[off:off + m], 15, u[off:off + m], norms[s]))

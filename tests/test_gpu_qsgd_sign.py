@@ -62,12 +62,12 @@ def test_qsgd_device_norm_vs_fp64(n):
 
 @pytest.mark.parametrize("q", [1, 2, 3, 4, 8, 16])
 @pytest.mark.parametrize("n", [1000, 262147])
-def test_qsgd_philox_mode_matches_oracle(q, n):
+def test_qsgd_device_rng_matches_oracle(q, n):
     from chocosgd_amd import codec
     x = randn(n, 100 + q)
     seed, offset = 0x1234_5678_9ABC, 77
     packed, norms, dense = codec.qsgd_compress(x, q, seed=seed, offset=offset, want_dense=True)
-    u = O.philox_uniforms(n, seed, offset)
+    u = O.qsgd_uniforms(n, seed, offset)
     s = 2 ** q - 1
     nrm = host(norms)[0]
     assert same_bits(host(dense), O.qsgd_dense(host(x), s, u, nrm))
@@ -114,7 +114,7 @@ def test_qsgd_segmented_layout_norms_and_levels(layout):
     d = host(x) - host(xh)
     ref = O.l2_norms(d, lens)
     assert np.allclose(host(norms), ref, rtol=1e-6, atol=0)
-    u = O.philox_uniforms(n, 9, 1)
+    u = O.qsgd_uniforms(n, 9, 1)
     off, outs = 0, []
     for s, m in enumerate(lens):
         outs.append(O.qsgd_dense(d[off:off + m], 15, u[off:off + m], host(norms)[s]))

@@ -181,12 +181,13 @@ def test_gossip_step():
     assert same_bits(O.gossip_step(x, g2["mem1"], g2["hat1"], g2["gamma"]), g2["x_after_gossip"])
 
 
-def test_philox_known_answer():
-    # Random123 known-answer vector for philox4x32-10 (counter = key = 0)
-    r = O.philox4x32_10([0], [0], [0], [0], 0, 0)
-    assert [int(v[0]) for v in r] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
-    r = O.philox4x32_10([0xFFFFFFFF], [0xFFFFFFFF], [0xFFFFFFFF], [0xFFFFFFFF], 0xFFFFFFFF, 0xFFFFFFFF)
-    assert [int(v[0]) for v in r] == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+def test_splitmix64_known_answer():
+    # the first outputs of the splitmix64 generator from state 0 (Vigna's reference
+    # implementation: state += gamma; return mix(state))
+    z = O.splitmix64_mix(np.array([O.GAMMA, 2 * O.GAMMA % 2 ** 64], dtype=np.uint64))
+    assert z.tolist() == [16294208416658607535, 7960286522194355700]
+    u = O.qsgd_uniforms(6, 7, 3)
+    assert u.dtype == np.float32 and np.all((u >= 0) & (u < 1))
 
 
 def test_randk_indices_distinct_and_uniformish():
@@ -201,12 +202,12 @@ def test_randk_indices_distinct_and_uniformish():
 
 
 def test_oracle_sampled_helpers_agree_with_full_forms():
-    """philox_uniforms_at / qsgd_wire_at (the sampled checks at BASELINE sizes) restate the
+    """qsgd_uniforms_at / qsgd_wire_at (the sampled checks at BASELINE sizes) restate the
     full-array forms exactly."""
     n, seed, offset = 10_007, 0x1234_5678_9ABC, 5
-    u = O.philox_uniforms(n, seed, offset)
+    u = O.qsgd_uniforms(n, seed, offset)
     idx = np.array([0, 1, 2, 3, 4, 777, 4096, n - 2, n - 1])
-    assert np.array_equal(O.philox_uniforms_at(idx, seed, offset), u[idx])
+    assert np.array_equal(O.qsgd_uniforms_at(idx, seed, offset), u[idx])
     rng = np.random.default_rng(0)
     d = rng.standard_normal(n).astype(np.float32)
     for q in (1, 2, 4, 8, 16):

@@ -12,6 +12,9 @@ VARIANTS = {
     "acc_elem": ["CHOCO_ACC_MODE=0"],
     "acc_seg8": ["CHOCO_ACC_SEGF=8"],
     "acc_seg32": ["CHOCO_ACC_SEGF=32"],
+    "qq_nt": ["CHOCO_QQUANT_NT=1"],
+    "qn_plain": ["CHOCO_QNORM_NT=0"],
+    "sign_acc1": ["CHOCO_SIGN_ACC1=1"],
 }
 
 
