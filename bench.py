@@ -48,9 +48,10 @@ WORKLOADS = {
 
 # kernels (profile names) of each stage
 STAGES = {
-    "topk": (["topk_bounds", "topk_stream", "topk_finish", "topk_exact", "topk_all"], ["sparse_accumulate"]),
-    "topk_seg": (["topk_seg_hist", "topk_seg_collect", "topk_seg_select", "topk_seg_emit", "topk_bounds",
-                  "topk_stream", "topk_finish"], ["sparse_accumulate"]),
+    "topk": (["topk_fused", "topk_bounds", "topk_stream", "topk_finish", "topk_exact", "topk_all"],
+             ["sparse_accumulate"]),
+    "topk_seg": (["topk_seg_hist", "topk_seg_collect", "topk_seg_select", "topk_seg_emit", "topk_fused",
+                  "topk_bounds", "topk_stream", "topk_finish"], ["sparse_accumulate"]),
     "randk": (["topk_stream", "topk_finish", "topk_exact", "topk_all"], ["sparse_accumulate"]),
     "qsgd": (["qsgd_norm", "qsgd_quantize"], ["qsgd_accumulate"]),
     "sign": (["sign_pack"], ["sign_accumulate"]),

@@ -357,11 +357,11 @@ struct Buckets {
   uint64_t seed;
 };
 
-CHOCO_DEV Buckets make_buckets(uint32_t s_lo, uint64_t s_hi_est, uint64_t seed) {
+CHOCO_DEV Buckets make_buckets(uint32_t s_lo, uint64_t s_hi_est, uint64_t seed, uint32_t nmaybe = kNMaybe) {
   const uint64_t width = s_hi_est > s_lo ? s_hi_est - s_lo : 1;
   uint32_t shift = 0;
-  while (((uint64_t)kNMaybe << shift) < width) ++shift;
-  uint64_t s_hi = (uint64_t)s_lo + ((uint64_t)kNMaybe << shift);
+  while (((uint64_t)nmaybe << shift) < width) ++shift;
+  uint64_t s_hi = (uint64_t)s_lo + ((uint64_t)nmaybe << shift);
   if (s_hi > 0xFFFFFFFFull) s_hi = 0xFFFFFFFFull;
   Buckets bk;
   bk.n = 0;
@@ -539,8 +539,8 @@ struct WaveAcc {
 // into the wave's LDS region while it has room, else straight to the chunk's
 // global slots (then for the rest of the chunk, so the LDS part stays a prefix
 // of the chunk's run).  Maybe keys are counted into the bucket histogram.
-template <int MODE, bool XH>
-CHOCO_DEV void flush_entries(const Src<MODE, XH>& src, StreamSmem& sm, int w, int lane, WaveAcc& a, uint32_t nent,
+template <int MODE, bool XH, class SM>
+CHOCO_DEV void flush_entries(const Src<MODE, XH>& src, SM& sm, int w, int lane, WaveAcc& a, uint32_t nent,
                              float* __restrict__ ov, uint32_t* __restrict__ oi, const Buckets& bk) {
   wave_sync();
   const bool have = (uint32_t)lane < nent;
@@ -597,8 +597,8 @@ CHOCO_DEV void flush_entries(const Src<MODE, XH>& src, StreamSmem& sm, int w, in
 // One float4 row per lane (256 elements per wave): stage the lanes that hold a
 // candidate.  The float test !(|v| < s_lo_f) is a superset of key >= s_lo (NaN
 // passes); the flush applies the exact test.
-template <int MODE, bool XH, bool GUARD>
-CHOCO_DEV void process_row(const Src<MODE, XH>& src, const float4 v4, int64_t i, int64_t cend, StreamSmem& sm,
+template <int MODE, bool XH, bool GUARD, class SM>
+CHOCO_DEV void process_row(const Src<MODE, XH>& src, const float4 v4, int64_t i, int64_t cend, SM& sm,
                            int w, int lane, WaveAcc& a, float* __restrict__ ov, uint32_t* __restrict__ oi,
                            const Buckets& bk) {
   bool any = false;
@@ -618,16 +618,16 @@ CHOCO_DEV void process_row(const Src<MODE, XH>& src, const float4 v4, int64_t i,
     sm.ent_i[w][slot] = (uint32_t)i;
   }
   a.estaged = __builtin_amdgcn_readfirstlane(a.estaged + (uint32_t)__popcll(M));
-  if (a.estaged - a.eflushed >= 64u) flush_entries<MODE, XH>(src, sm, w, lane, a, 64u, ov, oi, bk);
+  if (a.estaged - a.eflushed >= 64u) flush_entries(src, sm, w, lane, a, 64u, ov, oi, bk);
 }
 
 // Eight full rows (one load batch) as ONE branch-free block, so the compiler can
 // interleave the rows' dependent compare -> ballot -> prefix -> LDS-store chains.
 // Lanes without a candidate store to a trash slot.  If the batch could overflow
 // the entry ring (dense inputs), rows take the per-row path instead.
-template <bool XH>
+template <bool XH, class SM>
 CHOCO_DEV void process_batch(const Src<kData, XH>& src, const float4 (&A)[kK2Unroll], int64_t base, int64_t cend,
-                             StreamSmem& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
+                             SM& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
                              uint32_t* __restrict__ oi, const Buckets& bk) {
   bool any[kK2Unroll];
   uint64_t M[kK2Unroll];
@@ -654,7 +654,7 @@ CHOCO_DEV void process_batch(const Src<kData, XH>& src, const float4 (&A)[kK2Unr
     }
     a.estaged = __builtin_amdgcn_readfirstlane(run);
 #pragma unroll 1
-    while (a.estaged - a.eflushed >= 64u) flush_entries<kData, XH>(src, sm, w, lane, a, 64u, ov, oi, bk);
+    while (a.estaged - a.eflushed >= 64u) flush_entries(src, sm, w, lane, a, 64u, ov, oi, bk);
   } else {
 #pragma unroll
     for (int u = 0; u < kK2Unroll; ++u)
@@ -662,8 +662,8 @@ CHOCO_DEV void process_batch(const Src<kData, XH>& src, const float4 (&A)[kK2Unr
   }
 }
 
-template <int MODE, bool XH>
-CHOCO_DEV void process_rows_hash(const Src<MODE, XH>& src, int64_t base, int64_t cend, StreamSmem& sm, int w,
+template <int MODE, bool XH, class SM>
+CHOCO_DEV void process_rows_hash(const Src<MODE, XH>& src, int64_t base, int64_t cend, SM& sm, int w,
                                  int lane, WaveAcc& a, float* __restrict__ ov, uint32_t* __restrict__ oi,
                                  const Buckets& bk) {
 #pragma unroll
@@ -672,7 +672,8 @@ CHOCO_DEV void process_rows_hash(const Src<MODE, XH>& src, int64_t base, int64_t
                                  lane, a, ov, oi, bk);
 }
 
-CHOCO_DEV uint32_t claim_chunk(StreamSmem& sm, int lane) {
+template <class SM>
+CHOCO_DEV uint32_t claim_chunk(SM& sm, int lane) {
   uint32_t c = 0;
   if (lane == 0) c = atomicAdd(&sm.next_chunk, 1u);
   return __builtin_amdgcn_readfirstlane(c);
@@ -694,8 +695,9 @@ struct BoundsSmem {
   uint32_t bc[8];
 };
 
+template <class BS>
 CHOCO_DEV void sample_bounds_full(const uint32_t (&kk)[kSampleLoads * 4], const SampleRanks& R, int lane,
-                                  BoundsSmem& sm, uint32_t& s_lo, uint64_t& s_hi_est) {
+                                  BS& sm, uint32_t& s_lo, uint64_t& s_hi_est) {
   const int tid = threadIdx.x;
   for (int i = tid; i < 6 * 2048; i += kK1Threads) (&sm.sh.coarse[0][0])[i] = 0u;
   if (tid < 8) sm.bc[tid] = 0;
@@ -721,8 +723,9 @@ CHOCO_DEV void sample_bounds_full(const uint32_t (&kk)[kSampleLoads * 4], const 
   s_hi_est = R.hi ? (uint64_t)((c_hi << 20) | (sm.bc[6] << 9)) + 512u : 0x80000000ull;  // rounded up
 }
 
+template <class BS>
 CHOCO_DEV void sample_bounds(const uint32_t (&kk)[kSampleLoads * 4], const SampleRanks& R, int lane, int w,
-                             BoundsSmem& sm, uint32_t& s_lo, uint64_t& s_hi_est) {
+                             BS& sm, uint32_t& s_lo, uint64_t& s_hi_est) {
   const int tid = threadIdx.x;
   if (R.lo == 0) {  // every key is a candidate
     s_lo = 0u;
@@ -1485,9 +1488,658 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
 }
 
 // ----------------------------------------------------------------------------
+// Fused one-launch top-k (kData): bounds + stream + select + emit
+//
+// One launch of nb + 1 workgroups (nb <= 255 tiles: every workgroup has a CU of
+// its own on MI355X).  Workgroups take TICKETS from a counter: ticket 0 computes
+// the sample bounds (K1's job) and publishes them; ticket t >= 1 streams tile
+// t - 1 (K2's job), keeping its candidates in LDS; when the tickets run out a
+// workgroup waits until every tile has published its bucket counts and side
+// list, then -- like K34, redundantly in every workgroup -- selects the exact
+// threshold T and each tile's output offset, and finally emits the candidates
+// of its OWN tile(s) straight from LDS to the output.  Against K1 + K2 + K34:
+// no candidate write and re-read (~14 MB at k = 1 %), no kernel boundaries.
+//
+// Deadlock-free by construction: a workgroup only waits on work owned by
+// workgroups that have already taken a ticket, i.e. are running (the bounds
+// and every claimed tile), never on a workgroup that may not be resident.
+// When fewer workgroups are resident than tiles (another kernel or process
+// holds CUs), the running ones take more tickets and process those extra tiles
+// in "spill" mode: candidates go to their global chunk slots (K2's layout) and
+// are emitted from there.  The same happens to a tile whose candidates
+// overflow a wave's LDS region (dense inputs / large k).
+//
+// Counters are reset by the last workgroup to finish; the bucket totals are
+// double-buffered by call parity and the idle set is zeroed by the bounds
+// workgroup, so no workgroup clears state another may still read.
+// ----------------------------------------------------------------------------
+#ifndef CHOCO_FUSED_PRE  // batches per wave issued before the bounds are known (1 or 2)
+#define CHOCO_FUSED_PRE 2
+#endif
+#ifndef CHOCO_FUSED_DIAG  // register-pressure diagnostics only (1: no emission)
+#define CHOCO_FUSED_DIAG 0
+#endif
+constexpr int kFB = 1024;                  // buckets: 1023 "maybe" + 1 "sure"
+constexpr int kFMaybe = kFB - 1;
+constexpr int kFMaxChunks = 512;           // tile <= 512 chunks (1M elements)
+constexpr int kFMCap = 8192;               // bucket-j* keys selected in LDS
+constexpr int kFSelBits = 12;
+constexpr int kFMaxOwn = 256;              // tiles one workgroup may process
+constexpr int64_t kFTileTarget = 255;      // + the bounds workgroup = 256 CUs
+static_assert(kFB == kK2Threads, "one bucket per thread at the tile end");
+
+struct FusedCtrl {
+  uint32_t claim, done, exitc, ready;      // tickets, tiles published, workgroups done, bounds published
+  uint32_t s_lo, s_hi, shift, epoch;
+  uint32_t overflow, pad[55];
+  uint32_t G[2][kNRep][kFB];               // replicated bucket suffix totals, by call parity
+};
+
+struct FusedLayout {
+  int64_t n;
+  uint32_t tile, nb, side_cap, nchunk;
+  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, total;
+};
+
+static FusedLayout fused_layout(int64_t n) {
+  FusedLayout L{};
+  L.n = n;
+  int64_t tile = (n + kFTileTarget - 1) / kFTileTarget;
+  tile = std::max<int64_t>(kTileQuant, (tile + kTileQuant - 1) / kTileQuant * kTileQuant);
+  L.tile = (uint32_t)tile;
+  L.nb = (uint32_t)((n + tile - 1) / tile);
+  L.nchunk = (uint32_t)(tile / kChunk);
+  L.side_cap = (uint32_t)std::min<int64_t>(kMaybeCap, tile);
+  size_t o = 0;
+  L.off_cum = o;   o += align_up((size_t)L.nb * kFB * 4, 256);
+  L.off_cntw = o;  o += align_up((size_t)L.nb * L.nchunk * 4, 256);
+  L.off_side = o;  o += align_up((size_t)L.nb * L.side_cap * 4, 256);
+  L.off_cval = o;  o += align_up((size_t)L.nb * tile * 4, 256);
+  L.off_cidx = o;  o += align_up((size_t)L.nb * tile * 4, 256);
+  // the control block lies past everything the three-kernel path (random-k on the
+  // same workspace) writes, so its counters stay as the last fused call left them
+  L.off_ctrl = std::max(o, topk_layout(n).total);
+  L.total = L.off_ctrl + align_up(sizeof(FusedCtrl), 256);
+  return L;
+}
+
+static bool fused_fits(int64_t n) {
+  return n > kSmallN && (int64_t)fused_layout(n).nchunk <= kFMaxChunks;
+}
+
+struct FusedSmem {
+  union {
+    struct {  // stream: per-wave entry rings
+      float4 ent_v[kK2Waves][kEnt];
+      uint32_t ent_i[kK2Waves][kEnt];
+    };
+    struct {  // select: bucket-j* keys + radix histogram (tile map / tile info before / after)
+      uint32_t keys[kFMCap];
+      uint32_t shist[1 << kFSelBits];
+    };
+  };
+  union {
+    uint2 pairs[kK2Waves * kPairsPerWave];  // candidates of the LDS tile, per-wave regions
+    SampleHist sh;                           // bounds workgroup, before any tile
+    ExactSmem es;                            // single-workgroup fallback
+  } u;
+  float4 trash_v[64];
+  uint32_t trash_i[64];
+  uint32_t cmeta[kFMaxChunks];       // LDS tile, per chunk: LDS start | LDS count << 16
+  uint32_t ccnt[kFMaxChunks + 1];    // LDS tile, per chunk: candidates, then their exclusive prefix
+  uint32_t cmeta2[kFMaxChunks];      // the same for spill-mode tiles
+  uint32_t ccnt2[kFMaxChunks + 1];
+  uint32_t hist[kFB];                // maybe-key bucket counts, then counting-sort cursors
+  uint32_t kbase[kK4Threads];
+  uint32_t G[kFB];
+  uint32_t ecnt[2][kEmitRows * (kK4Threads / 64) + 1];
+  uint32_t own[kFMaxOwn];            // tiles of this workgroup: tile | (in LDS) << 31
+  uint32_t cnt[kK2Waves];
+  uint32_t scratch[40];
+  uint32_t bc[8];
+  uint32_t next_chunk, spill, ticket, nown;
+};
+
+struct BoundsView {
+  SampleHist& sh;
+  uint32_t* scratch;
+  uint32_t* bc;
+};
+
+// Hand-offs between workgroups (bounds, tile tables, side lists) use the
+// fence-free form of MI355X_MICROARCH.md "Valid forms": every handed-off word is
+// stored write-through (relaxed agent-scope atomic store = sc1) and read with
+// sc1 loads; each storing wave drains (vmcnt(0)) before a workgroup barrier,
+// behind which one lane adds to the counter; the consumer polls that counter.
+// No release fence: a buffer_wbl2 writes back the whole XCD L2 and cost
+// 10-30 us per tile in the middle of everyone else's stream (measured).
+CHOCO_DEV void st_sc1(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+CHOCO_DEV uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// bounded poll of a counter written by running workgroups (s_sleep between
+// polls); returns when *p >= want
+CHOCO_DEV void poll_ge(const uint32_t* p, uint32_t want) {
+  for (uint32_t it = 0; it < (1u << 26); ++it) {
+    if (ld_sc1(p) >= want) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// every wave's stores drained, the workgroup joined, one lane adds
+CHOCO_DEV void publish_add(uint32_t* counter) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Over hist[1 << kFSelBits] (ascending), the bin of the rank-th largest entry and
+// the rank inside it -> out[0], out[1]; ends with a barrier.
+CHOCO_DEV void block_find_rank4k(const uint32_t* hist, uint32_t rank, uint32_t* scratch, uint32_t* out) {
+  constexpr int per = (1 << kFSelBits) / kK4Threads;
+  const int tid = threadIdx.x;
+  uint32_t hv[per];
+  uint32_t local = 0;
+#pragma unroll
+  for (int j = 0; j < per; ++j) {
+    hv[j] = hist[tid * per + j];
+    local += hv[j];
+  }
+  uint32_t total;
+  const uint32_t pre = block_excl_scan(local, scratch, &total);
+  const uint32_t above = total - pre - local;
+  if (above < rank && rank <= above + local) {
+    uint32_t acc = above;
+#pragma unroll
+    for (int j = per - 1; j >= 0; --j) {
+      if (acc < rank && rank <= acc + hv[j]) { out[0] = (uint32_t)(tid * per + j); out[1] = rank - acc; }
+      acc += hv[j];
+    }
+  }
+  __syncthreads();
+}
+
+// Stream one tile (K2's body).  lds_mode: candidates may stay in the waves' LDS
+// regions; otherwise every candidate goes to its chunk's global slots.
+template <bool XH>
+CHOCO_DEV void fused_stream_tile(const Src<kData, XH>& src, const float* __restrict__ x, const float* __restrict__ xh,
+                                 int64_t n, uint32_t tile, uint32_t b, bool lds_mode, const Buckets& bk,
+                                 FusedSmem& sm, uint32_t* ccnt, uint32_t* cmeta, float* __restrict__ cval,
+                                 uint32_t* __restrict__ cidx, float4 (&A)[kK2Unroll], float4 (&B)[kK2Unroll],
+                                 const TileRsrc& ts) {
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  constexpr bool kTwoChunks = !XH;  // A and B hold the wave's next two chunks
+  const uint32_t nchunk = tile / (uint32_t)kChunk;
+  const int64_t tb = (int64_t)b * tile;
+  const int64_t tlen = min((int64_t)tile, n - tb);
+  auto batch0 = [&](uint32_t c) -> uint32_t {
+    return (c < nchunk && (int64_t)(c + 1) * kChunk <= tlen) ? c * (uint32_t)kChunk * 4u : kNoChunk;
+  };
+  WaveAcc a{};
+  if (!lds_mode) a.lfill = (uint32_t)kPairsPerWave;  // no LDS room: every pair spills
+  auto run_chunk = [&](uint32_t cc, const float4 (&R)[kK2Unroll]) {
+    const int64_t cbeg = tb + (int64_t)cc * kChunk;
+    const int64_t cend = min(cbeg + kChunk, n);
+    float* __restrict__ ov = cval + cbeg;
+    uint32_t* __restrict__ oi = cidx + cbeg;
+    a.estaged = a.eflushed = a.staged = a.lcnt = 0u;
+    a.lstart = a.lfill;
+    if (cbeg + kChunk <= n) {
+      process_batch<XH>(src, R, cbeg, cend, sm, w, lane, a, ov, oi, bk);
+    } else {
+      for (int64_t base = cbeg; base < cend; base += 256) {
+        const int64_t i = base + 4 * lane;
+        float tt[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tt[q] = (i + q < cend) ? src.val(i + q) : 0.f;
+        process_row<kData, XH, true>(src, make_float4(tt[0], tt[1], tt[2], tt[3]), i, cend, sm, w, lane, a, ov, oi,
+                                     bk);
+      }
+    }
+    const uint32_t rest = a.estaged - a.eflushed;
+    if (rest) flush_entries(src, sm, w, lane, a, rest, ov, oi, bk);
+    if (lane == 0) {
+      ccnt[cc] = a.staged;
+      cmeta[cc] = (w * kPairsPerWave + (a.lstart < (uint32_t)kPairsPerWave ? a.lstart : 0u)) | (a.lcnt << 16);
+    }
+  };
+  uint32_t c = (uint32_t)w;
+  if constexpr (kTwoChunks) {
+    uint32_t cA = c, cB = c + kK2Waves;
+    for (;;) {
+      if (cA >= nchunk) break;
+      const uint32_t nA = claim_chunk(sm, lane);
+      run_chunk(cA, A);
+      load_rows_full<XH>(ts, batch0(nA), lane, A);
+      cA = nA;
+      if (cB >= nchunk) break;
+      const uint32_t nB = claim_chunk(sm, lane);
+      run_chunk(cB, B);
+      load_rows_full<XH>(ts, batch0(nB), lane, B);
+      cB = nB;
+    }
+  } else {
+    while (c < nchunk) {
+      const uint32_t nn = claim_chunk(sm, lane);
+      run_chunk(c, A);
+      load_rows_full<XH>(ts, batch0(nn), lane, A);
+      c = nn;
+    }
+  }
+  if (lane == 0) sm.cnt[w] = a.cand;
+  __syncthreads();
+}
+
+template <bool XH>
+__global__ __launch_bounds__(kK2Threads) void topk_fused_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
+    uint32_t side_cap, SampleRanks ranks, FusedCtrl* __restrict__ ctrl, uint32_t* __restrict__ cum_tab,
+    uint32_t* __restrict__ cntw, uint32_t* __restrict__ side, float* __restrict__ cval, uint32_t* __restrict__ cidx,
+    float* __restrict__ out_val, int32_t* __restrict__ out_idx, int64_t idx_base) {
+  __shared__ FusedSmem sm;
+  STAMP(36000 + blockIdx.x, 0);
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const uint32_t nchunk = tile / (uint32_t)kChunk;
+  const uint32_t ku = (uint32_t)k;
+  Src<kData, XH> src{x, xh, 0};
+  if (tid == 0) {
+    sm.nown = 0;
+    sm.bc[7] = __hip_atomic_load(&ctrl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const uint32_t epoch = __builtin_amdgcn_readfirstlane(sm.bc[7]);
+  uint32_t* __restrict__ G = &ctrl->G[epoch & 1u][0][0];
+  bool have_bounds = false;
+  bool bounds_wg = false;
+  Buckets bk{};
+
+  // ---------------- tickets: bounds duty (ticket 0), then tiles (ticket t <-> tile t - 1).
+  // LDS-carried values are re-read with readfirstlane: the compiler must see them
+  // wave-uniform (the buffer descriptors built from them live in SGPRs)
+  auto claim = [&]() -> uint32_t {
+    if (tid == 0) sm.ticket = __hip_atomic_fetch_add(&ctrl->claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t t = __builtin_amdgcn_readfirstlane(sm.ticket);
+    __syncthreads();
+    return t;
+  };
+  uint32_t ticket = claim();
+  STAMP(36000 + blockIdx.x, 1);
+#if CHOCO_STAMPS
+  if (tid == 0) g_stamps[38000 + blockIdx.x][0] = ticket + 1;
+#endif
+  if (ticket == 0) {
+    {
+      // the sample bounds (K1), published for every tile; then the idle parity
+      // of the bucket totals is cleared for the next call
+      bounds_wg = true;
+      float4 sv[kSampleLoads], shv[kSampleLoads];
+      load_sample<XH>(x, xh, n, sv, shv);
+      uint32_t kk[kSampleLoads * 4];
+#pragma unroll
+      for (int j = 0; j < kSampleLoads; ++j) {
+        float4 v = sv[j];
+        if (XH) { v.x -= shv[j].x; v.y -= shv[j].y; v.z -= shv[j].z; v.w -= shv[j].w; }
+        kk[4 * j + 0] = fkey(v.x); kk[4 * j + 1] = fkey(v.y); kk[4 * j + 2] = fkey(v.z); kk[4 * j + 3] = fkey(v.w);
+      }
+      uint32_t s_lo;
+      uint64_t s_hi_est;
+      BoundsView bv{sm.u.sh, sm.scratch, sm.bc};
+      sample_bounds(kk, ranks, lane, w, bv, s_lo, s_hi_est);
+      bk = make_buckets(s_lo, s_hi_est, 0, kFMaybe);
+      bk.n = n;
+      have_bounds = true;
+      if (tid == 0) {
+        __hip_atomic_store(&ctrl->s_lo, bk.s_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctrl->s_hi, bk.s_hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctrl->shift, bk.shift, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&ctrl->ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      STAMP(36000 + blockIdx.x, 2);
+      uint32_t* __restrict__ Gn = &ctrl->G[(epoch + 1u) & 1u][0][0];
+      for (int i = tid; i < kNRep * kFB; i += kK2Threads) Gn[i] = 0u;
+    }
+    ticket = claim();
+  }
+  for (; ticket <= nb; ticket = claim()) {
+    // ---- tile b = ticket - 1: its first loads go out before the bounds are read
+    const uint32_t b = ticket - 1;
+    const bool lds_mode = __builtin_amdgcn_readfirstlane(sm.nown) == 0;
+    uint32_t* ccnt = lds_mode ? sm.ccnt : sm.ccnt2;
+    uint32_t* cmeta = lds_mode ? sm.cmeta : sm.cmeta2;
+    const int64_t tb = (int64_t)b * tile;
+    const int64_t tlen = min((int64_t)tile, n - tb);
+    const TileRsrc ts{buf_rsrc(x + tb, (uint32_t)(tlen * 4)), buf_rsrc((XH ? xh : x) + tb, (uint32_t)(tlen * 4))};
+    auto batch0 = [&](uint32_t c) -> uint32_t {
+      return (c < nchunk && (int64_t)(c + 1) * kChunk <= tlen) ? c * (uint32_t)kChunk * 4u : kNoChunk;
+    };
+    // The first batches go out before the bounds are known -- except wave 0's:
+    // its lane 0 polls, and a poll queued behind the wave's own 16 KiB of loads
+    // would only return once they have landed (vmcnt is in order).
+    const bool early = have_bounds || w != 0;
+    float4 A[kK2Unroll], B[kK2Unroll];
+    if (early) {
+      load_rows_full<XH>(ts, batch0((uint32_t)w), lane, A);
+      if (!XH && CHOCO_FUSED_PRE == 2) load_rows_full<XH>(ts, batch0((uint32_t)w + kK2Waves), lane, B);
+    }
+    sm.hist[tid] = 0u;
+    if (tid == 0) {
+      sm.next_chunk = XH ? kK2Waves : 2 * kK2Waves;
+      sm.spill = 0;
+      if (!have_bounds) {
+        poll_ge(&ctrl->ready, 1u);
+        sm.bc[0] = __hip_atomic_load(&ctrl->s_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sm.bc[1] = __hip_atomic_load(&ctrl->s_hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sm.bc[2] = __hip_atomic_load(&ctrl->shift, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+    STAMP(36000 + blockIdx.x, 2);
+    if (!early) load_rows_full<XH>(ts, batch0((uint32_t)w), lane, A);
+    if (!XH && (!early || CHOCO_FUSED_PRE != 2)) load_rows_full<XH>(ts, batch0((uint32_t)w + kK2Waves), lane, B);
+    if (!have_bounds) {
+      bk = make_buckets_from(__builtin_amdgcn_readfirstlane(sm.bc[0]), __builtin_amdgcn_readfirstlane(sm.bc[1]),
+                             __builtin_amdgcn_readfirstlane(sm.bc[2]), 0);
+      bk.n = n;
+      have_bounds = true;
+    }
+    fused_stream_tile<XH>(src, x, xh, n, tile, b, lds_mode, bk, sm, ccnt, cmeta, cval, cidx, A, B, ts);
+    STAMP(36000 + blockIdx.x, 3);
+
+    // ---- tile end: bucket suffix counts -> cum_tab row + totals; chunk prefix;
+    // the maybe keys counting-sorted into the side list (pairs stay in LDS)
+    uint32_t hsum, csum;
+    bool spilled;
+    {
+      const int t = tid;
+      const int jb = t < kFMaybe ? kFMaybe - 1 - t : kFMaybe;
+      const uint32_t hv = t < kFMaybe ? sm.hist[jb] : 0u;
+      const uint32_t cs = (uint32_t)t < nchunk ? ccnt[t] : 0u;
+      const bool sp = (uint32_t)t < nchunk && cs != (cmeta[t] >> 16);
+      if (ballot(sp) != 0ull && lane == 0) atomicOr(&sm.spill, 1u);
+      uint32_t above, cpre;
+      block_excl_scan2(hv, cs, sm.scratch, &above, &cpre, &hsum, &csum);
+      if ((uint32_t)t < nchunk) ccnt[t] = cpre;
+      if (t == 0) ccnt[nchunk] = csum;
+      const uint32_t sure = csum - hsum;
+      if (t == 0 && hsum > side_cap) atomicOr(&ctrl->overflow, 1u);
+      const uint32_t cum = t < kFMaybe ? sure + above + hv : sure;
+      st_sc1(&cum_tab[(int64_t)b * kFB + jb], cum);
+      atomicAdd(&G[(b & (kNRep - 1)) * kFB + jb], cum);
+      if (t < kFMaybe) sm.hist[jb] = above;  // counting-sort cursor of bucket jb
+      __syncthreads();
+      spilled = sm.spill != 0 || !lds_mode;
+    }
+    {
+      uint32_t* __restrict__ sd = side + (int64_t)b * side_cap;
+      uint32_t* __restrict__ skeys = reinterpret_cast<uint32_t*>(&sm.ent_v[0][0]);  // the ring is dead now
+      const bool sort_lds = hsum <= (uint32_t)kSideLds;
+      const uint32_t h = (uint32_t)lane & 31u;
+      const int64_t tbase = (int64_t)b * tile;
+      for (uint32_t c0 = 2u * w; c0 < nchunk; c0 += 2u * kK2Waves) {
+        const uint32_t cc = c0 + ((uint32_t)lane >> 5);
+        const bool have = cc < nchunk;
+        const uint32_t meta = have ? cmeta[cc] : 0u;
+        const uint32_t cnt = have ? ccnt[cc + 1] - ccnt[cc] : 0u;
+        const uint32_t ls = meta & 0xFFFFu, lc = have ? (meta >> 16) : 0u;
+        float* __restrict__ ov = cval + tbase + (int64_t)cc * kChunk;
+        uint32_t* __restrict__ oi = cidx + tbase + (int64_t)cc * kChunk;
+        auto to_side = [&](uint32_t vb, uint32_t ix) {
+          const uint32_t key = vb & 0x7fffffffu;
+          if (key < bk.s_hi) {
+            const uint32_t p = atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
+            if (sort_lds) skeys[p] = key;
+            else if (p < side_cap) st_sc1(&sd[p], key);
+          }
+        };
+        for (uint32_t j = h; j < lc; j += 32) {
+          const uint2 pr = sm.u.pairs[ls + j];
+          if (spilled) {  // this tile is emitted from global memory: its LDS pairs go to their slots
+            ov[j] = __uint_as_float(pr.x);
+            oi[j] = pr.y;
+          }
+          to_side(pr.x, pr.y);
+        }
+        if (spilled && have && h == 0) cntw[(int64_t)b * nchunk + cc] = cnt;
+        for (uint32_t j = lc + h; j < cnt; j += 32) to_side(__float_as_uint(ov[j]), oi[j]);
+      }
+      if (sort_lds) {
+        __syncthreads();
+        for (uint32_t i = (uint32_t)tid; i < hsum; i += kK2Threads) st_sc1(&sd[i], skeys[i]);
+      }
+    }
+    if (tid == 0 && sm.nown < (uint32_t)kFMaxOwn) sm.own[sm.nown++] = b | (spilled ? 0u : 0x80000000u);
+#if CHOCO_STAMPS
+    if (tid == 0) { g_stamps[38000 + blockIdx.x][1] = sm.nown; g_stamps[38000 + blockIdx.x][2] = spilled ? 1 : 0;
+                    g_stamps[38000 + blockIdx.x][3] = hsum; }
+#endif
+    publish_add(&ctrl->done);  // (ends with this tile's stores drained and released)
+    STAMP(37000 + blockIdx.x, 0);
+  }
+
+  // ---------------- every tile published -> exact T, offsets (K34's select)
+  if (tid == 0) {
+    poll_ge(&ctrl->done, nb);
+    sm.bc[0] = __hip_atomic_load(&ctrl->s_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm.bc[2] = __hip_atomic_load(&ctrl->shift, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm.bc[3] = __hip_atomic_load(&ctrl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm.bc[4] = 0;
+  }
+  __syncthreads();
+  STAMP(37000 + blockIdx.x, 1);
+  const uint32_t s_lo = __builtin_amdgcn_readfirstlane(sm.bc[0]), shift = __builtin_amdgcn_readfirstlane(sm.bc[2]),
+                 overflow = __builtin_amdgcn_readfirstlane(sm.bc[3]);
+  {
+    uint32_t g = 0;
+#pragma unroll
+    for (int r = 0; r < kNRep; ++r) g += __hip_atomic_load(&G[r * kFB + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm.G[tid] = g;
+  }
+  const bool mine_tile = (uint32_t)tid < nb;
+  const uint32_t* row = cum_tab + (int64_t)(mine_tile ? tid : 0) * kFB;
+  const uint32_t sure_t = ld_sc1(&row[kFMaybe]);
+  __syncthreads();
+  bool fallback = overflow != 0 || sm.G[0] < ku || sm.G[kFMaybe] >= ku;
+  if (!fallback && tid < kFMaybe && sm.G[tid] >= ku && sm.G[tid + 1] < ku) sm.bc[4] = (uint32_t)tid;
+  __syncthreads();
+  const uint32_t jstar = __builtin_amdgcn_readfirstlane(sm.bc[4]);
+  if (!fallback && sm.G[jstar] - sm.G[jstar + 1] > (uint32_t)kFMCap) fallback = true;
+  if (fallback) {
+    // the sample's guess was off: exact single-workgroup selection by the bounds
+    // workgroup (correct, slow)
+    if (bounds_wg) {
+      __syncthreads();
+      block_topk_exact(src, n, k, 1.0f, out_val, out_idx, idx_base, sm.u.es);
+    }
+  } else {
+    uint32_t above = 0, cb = 0, off = 0;
+    if (mine_tile) {
+      const uint32_t a = ld_sc1(&row[jstar]), c = ld_sc1(&row[jstar + 1]);
+      above = c;
+      cb = a - c;
+      off = c - sure_t;
+    }
+    uint32_t M;
+    const uint32_t kpos = block_excl_scan(cb, sm.scratch, &M);
+    {
+      uint16_t* tmap = reinterpret_cast<uint16_t*>(sm.shist);
+      static_assert(sizeof(sm.shist) >= kFMCap * sizeof(uint16_t), "tile map fits the histogram");
+      sm.kbase[tid] = (uint32_t)(mine_tile ? tid : 0) * side_cap + off - kpos;  // mod 2^32
+      for (uint32_t j = 0; j < cb; ++j) tmap[kpos + j] = (uint16_t)tid;
+      __syncthreads();
+      constexpr int kG = kFMCap / kK4Threads;
+      uint32_t kv[kG];
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        const uint32_t i = min((uint32_t)tid + (uint32_t)q * kK4Threads, M - 1u);
+        kv[q] = (uint32_t)q * kK4Threads < M ? ld_sc1(&side[sm.kbase[tmap[i]] + i]) : 0u;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        const uint32_t i = (uint32_t)tid + (uint32_t)q * kK4Threads;
+        if (i < M) sm.keys[i] = kv[q];
+      }
+    }
+    const uint32_t base_j = s_lo + (jstar << shift);
+    uint32_t prefix = 0, krem = ku - sm.G[jstar + 1];
+    int sh = (int)shift;
+    while (sh > 0) {
+      const int dsh = sh > kFSelBits ? sh - kFSelBits : 0;
+      const uint32_t dmask = (1u << (sh - dsh)) - 1u;
+      for (int i = tid; i < (1 << kFSelBits); i += kK4Threads) sm.shist[i] = 0;
+      __syncthreads();
+      for (uint32_t j = tid; j < M; j += kK4Threads) {
+        const uint32_t rel = sm.keys[j] - base_j;
+        if (sh >= 32 || (rel >> sh) == (prefix >> sh)) atomicAdd(&sm.shist[(rel >> dsh) & dmask], 1u);
+      }
+      __syncthreads();
+      block_find_rank4k(sm.shist, krem, sm.scratch, sm.bc + 5);
+      prefix |= __builtin_amdgcn_readfirstlane(sm.bc[5]) << dsh;
+      krem = __builtin_amdgcn_readfirstlane(sm.bc[6]);
+      sh = dsh;
+    }
+    __syncthreads();
+    const uint32_t T = base_j + prefix;
+    const uint32_t r = krem;  // ties at T to take (>= 1)
+    uint32_t gt = above, eq = 0;
+    for (uint32_t i0 = 0; i0 < cb; i0 += 8) {
+      uint32_t kk8[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) kk8[q] = sm.keys[kpos + min(i0 + q, cb - 1)];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        gt += (i0 + q < cb && kk8[q] > T) ? 1u : 0u;
+        eq += (i0 + q < cb && kk8[q] == T) ? 1u : 0u;
+      }
+    }
+    uint32_t gpre, epre, gtot, etot;
+    block_excl_scan2(gt, eq, sm.scratch, &gpre, &epre, &gtot, &etot);
+    // per tile: output offset, ties before it, tie mode (in the dead histogram)
+    STAMP(37000 + blockIdx.x, 2);
+    uint32_t* tinfo = sm.shist;
+    if (mine_tile) {
+      const uint32_t taken = min(r, epre);
+      const uint32_t take = min(eq, r - taken);
+      tinfo[3 * tid + 0] = gpre + taken;
+      tinfo[3 * tid + 1] = epre;
+      tinfo[3 * tid + 2] = take == 0 ? kTakeNone : (take == eq ? kTakeAll : kTakePartial);
+    }
+    __syncthreads();
+
+    // ---------------- emit this workgroup's tiles
+    const uint32_t nown = __builtin_amdgcn_readfirstlane(sm.nown);
+    for (uint32_t oi_ = 0; oi_ < (CHOCO_FUSED_DIAG == 1 ? 0u : nown); ++oi_) {
+      const uint32_t ent = __builtin_amdgcn_readfirstlane(sm.own[oi_]);
+      const uint32_t b = ent & 0x7fffffffu;
+      const bool in_lds = (ent >> 31) != 0u;
+      const int64_t tb = (int64_t)b * tile;
+      uint32_t out = __builtin_amdgcn_readfirstlane(tinfo[3 * b + 0]);
+      uint32_t tie_run = __builtin_amdgcn_readfirstlane(tinfo[3 * b + 1]);
+      const uint32_t mode = __builtin_amdgcn_readfirstlane(tinfo[3 * b + 2]);
+      uint32_t tot;
+      if (in_lds) {
+        tot = __builtin_amdgcn_readfirstlane(sm.ccnt[nchunk]);
+      } else {
+        uint32_t cw1[kCPT];
+#pragma unroll
+        for (int q = 0; q < kCPT; ++q) {
+          const uint32_t j = kCPT * tid + q;
+          cw1[q] = j < nchunk ? cntw[(int64_t)b * nchunk + j] : 0u;
+        }
+        tot = chunk_run_starts(cw1, nchunk, sm.ccnt2, sm.scratch);
+      }
+      int eb = 0;
+      for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads * kEmitR) {
+        float v[kEmitR];
+        uint32_t idx[kEmitR];
+#pragma unroll
+        for (int i = 0; i < kEmitR; ++i) {
+          const uint32_t p = p0 + i * kK4Threads + tid;
+          if (in_lds) {
+            // chunk of position p (LDS prefix search), then its LDS pair
+            uint32_t lo = 0, hi = nchunk - 1, pp = p < tot ? p : 0u;
+            while (lo < hi) {
+              const uint32_t mid = (lo + hi + 1) >> 1;
+              if (sm.ccnt[mid] <= pp) lo = mid; else hi = mid - 1;
+            }
+            const uint2 pr = sm.u.pairs[(sm.cmeta[lo] & 0xFFFFu) + (pp - sm.ccnt[lo])];
+            v[i] = __uint_as_float(pr.x);
+            idx[i] = pr.y;
+          } else {
+            const int64_t ad = cand_addr(sm.ccnt2, nchunk, tot, p, tb);
+            v[i] = cval[ad];
+            idx[i] = cidx[ad];
+          }
+        }
+        bool gtv[kEmitR], eqv[kEmitR];
+#pragma unroll
+        for (int i = 0; i < kEmitR; ++i) {
+          const bool valid = p0 + i * kK4Threads + tid < tot;
+          const uint32_t key = fkey(v[i]);
+          gtv[i] = valid && key > T;
+          eqv[i] = valid && key == T;
+        }
+        bool sel[kEmitR];
+        uint32_t rk[kEmitR];
+        if (mode == kTakePartial) {
+          const uint32_t eq_total = batch_ranks(eqv, rk, sm.ecnt[eb]);
+          eb ^= 1;
+#pragma unroll
+          for (int i = 0; i < kEmitR; ++i) sel[i] = gtv[i] || (eqv[i] && tie_run + rk[i] < r);
+          tie_run += eq_total;
+        } else {
+#pragma unroll
+          for (int i = 0; i < kEmitR; ++i) sel[i] = gtv[i] || (eqv[i] && mode == kTakeAll);
+        }
+        const uint32_t nsel = batch_ranks(sel, rk, sm.ecnt[eb]);
+        eb ^= 1;
+#pragma unroll
+        for (int i = 0; i < kEmitR; ++i) {
+          if (sel[i]) {
+            out_val[out + rk[i]] = v[i];
+            out_idx[out + rk[i]] = (int32_t)((int64_t)idx[i] + idx_base);
+          }
+        }
+        out += nsel;
+      }
+      __syncthreads();  // ccnt2 / ecnt reuse by the next tile
+    }
+  }
+  // ---------------- the last workgroup out resets the counters for the next call
+  __syncthreads();
+  STAMP(37000 + blockIdx.x, 3);
+  if (tid == 0) {
+    const uint32_t e = __hip_atomic_fetch_add(&ctrl->exitc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e == gridDim.x - 1) {
+      __hip_atomic_store(&ctrl->claim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctrl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctrl->ready, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctrl->overflow, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctrl->epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ctrl->exitc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
 // host dispatch
 // ----------------------------------------------------------------------------
-size_t topk_ws_bytes(int64_t n) { return n > kSmallN ? topk_layout(n).total : 256; }
+// The fused one-launch kernel (topk_fused_kernel) is parity-green but measured
+// SLOWER than K1 + K2 + K34 at 100M, k = 1 % (119 vs 92 us, tools/fused_stamps.py;
+// DESIGN.md): the bounds workgroup's sample competes with the tiles' prefetch
+// flood (bounds at 10-18 us vs K1's 5.5), write-through tile publishing waits
+// on memory acks (~8 us), the in-kernel "all tiles done" poll costs ~3 us, and
+// the redundant select + LDS emission cost as much as K34.  Diagnostic variant.
+#ifndef CHOCO_TOPK_FUSED
+#define CHOCO_TOPK_FUSED 0
+#endif
+size_t topk_ws_bytes(int64_t n) {
+  if (n <= kSmallN) return 256;
+  return CHOCO_TOPK_FUSED && fused_fits(n) ? fused_layout(n).total : topk_layout(n).total;
+}
 
 template <int MODE, bool XH>
 static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
@@ -1507,6 +2159,22 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
                        seed, scale, out_val, out_idx, idx_base);
     profile_end("topk_exact", st);
     CHOCO_LAUNCHED("topk_exact_kernel");
+    return CHOCO_OK;
+  }
+  if (MODE == kData && CHOCO_TOPK_FUSED && fused_fits(n)) {
+    const FusedLayout F = fused_layout(n);
+    CHOCO_REQUIRE(ws != nullptr && ws_bytes >= F.total, "top-k workspace too small: need %zu bytes, got %zu",
+                  F.total, ws_bytes);
+    CHOCO_REQUIRE(scale == 1.0f, "fused top-k takes scale 1");
+    char* fb = static_cast<char*>(ws);
+    profile_begin("topk_fused", st);
+    CHOCO_KLAUNCH((topk_fused_kernel<XH>), dim3(F.nb + 1), dim3(kK2Threads), 0, st, x, xh, n, k, F.tile, F.nb,
+                  F.side_cap, sample_ranks(n, k), reinterpret_cast<FusedCtrl*>(fb + F.off_ctrl),
+                  reinterpret_cast<uint32_t*>(fb + F.off_cum), reinterpret_cast<uint32_t*>(fb + F.off_cntw),
+                  reinterpret_cast<uint32_t*>(fb + F.off_side), reinterpret_cast<float*>(fb + F.off_cval),
+                  reinterpret_cast<uint32_t*>(fb + F.off_cidx), out_val, out_idx, idx_base);
+    profile_end("topk_fused", st);
+    CHOCO_LAUNCHED("topk_fused_kernel");
     return CHOCO_OK;
   }
   const TopkLayout L = topk_layout(n);

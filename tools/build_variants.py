@@ -15,6 +15,8 @@ VARIANTS = {
     "qq_nt": ["CHOCO_QQUANT_NT=1"],
     "qn_plain": ["CHOCO_QNORM_NT=0"],
     "sign_acc1": ["CHOCO_SIGN_ACC1=1"],
+    "fused": ["CHOCO_TOPK_FUSED=1"],
+    "fused_stamps": ["CHOCO_TOPK_FUSED=1", "CHOCO_STAMPS=1"],
 }
 
 
