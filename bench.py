@@ -13,6 +13,12 @@ memory.  One process per GPU; each worker owns its own buffer (weak scaling).
 process touches the GPU); under torch.distributed.run the ranks come from the
 environment.
 
+The step_* workloads run the whole CHOCO step of ParallelCHOCO_V (parallel_choco_v.py:
+116-155, after apply_gradient): the consensus step x += gamma (memory - x_hat) FUSED into
+the compressor's first pass (include/choco_codec.h), compress of d = x_new - x_hat,
+exchange, accumulate; `--unfused` runs the consensus step as its own pass first, as the
+reference does (optim/utils.py:67-72), for the A/B.
+
 metric (BASELINE.json): compress+decompress GB/s = sum_r 4*n_r / max_r(step time).
 roofline: per STAGE of the step (compress, decompress), algorithmic bytes
 (SURVEY.md 8(d)) / the stage's kernel time from dispatch-attached HIP events;
@@ -44,7 +50,11 @@ WORKLOADS = {
     "randk": ("randk", 100_000_000, 0.99, "randk_k1pct_per_worker"),
     "qsgd": ("qsgd", 100_000_000, 4, "qsgd_q4_per_worker"),
     "sign": ("sign", 345_000_000, None, "sign_norm_per_worker"),
+    "step_topk": ("topk", 100_000_000, 0.99, "choco_step_gossip_topk_k1pct"),
+    "step_sign": ("sign", 345_000_000, None, "choco_step_gossip_sign_norm"),
+    "step_qsgd": ("qsgd", 100_000_000, 4, "choco_step_gossip_qsgd_q4"),
 }
+GAMMA = 0.9  # consensus_stepsize (parameters.py:126 default)
 
 # kernels (profile names) of each stage
 STAGES = {
@@ -68,6 +78,8 @@ def parse():
     p.add_argument("--nbuf", type=int, default=4, help="delta buffers compressed in rotation (one per step)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="gloo: messages staged through host memory (comm_device=cpu); lets ranks share a GPU")
+    p.add_argument("--unfused", action="store_true",
+                   help="step_* workloads: the consensus step as its own pass (the reference's order)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the host-resident (PCIe-inclusive) leg")
     p.add_argument("--lib", default=None, help=argparse.SUPPRESS)
@@ -108,6 +120,10 @@ class Worker:
         self.torch = torch
         self.codec = codec
         self.op, n, self.param, self.label = WORKLOADS[args.workload]
+        self.step_mode = args.workload.startswith("step_")
+        self.unfused = self.step_mode and args.unfused
+        if self.unfused:
+            self.label += "_unfused"
         self.backend = args.backend
         self.rank, self.world, self.dev = rank, world, dev
         self.nb = neighborhood(rank, world)
@@ -126,10 +142,18 @@ class Worker:
         # The worker's delta x - x_hat.  Consecutive steps compress different
         # buffers (args.nbuf, independent draws), so each step selects a new
         # index set and the accumulate dirties new lines, as in training.
-        self.ds = [torch.randn(self.n, generator=g, device=dev) for _ in range(max(1, args.nbuf))]
+        if self.step_mode:
+            # x, x_hat, memory resident; x moves every step (the consensus step), so every
+            # step selects a new index set
+            self.x = torch.randn(self.n, generator=g, device=dev)
+            self.hat = self.x + 0.1 * torch.randn(self.n, generator=g, device=dev)
+            self.mem = self.hat + 0.05 * torch.randn(self.n, generator=g, device=dev)
+            self.ds = [self.x]
+        else:
+            self.ds = [torch.randn(self.n, generator=g, device=dev) for _ in range(max(1, args.nbuf))]
+            self.hat = torch.zeros(self.n, device=dev)
+            self.mem = torch.zeros(self.n, device=dev)
         self.d = self.ds[0]
-        self.hat = torch.zeros(self.n, device=dev)
-        self.mem = torch.zeros(self.n, device=dev)
         self.k = None
         if self.op in ("topk", "randk"):
             self.k = codec.topk_k(self.n, self.param)
@@ -152,7 +176,9 @@ class Worker:
         c = self.codec
         torch = self.torch
         self.d = self.ds[self.step_id % len(self.ds)]
-        if self.op == "topk":
+        if self.step_mode:
+            self.compress_step()
+        elif self.op == "topk":
             c.topk(self.d, self.k, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]))
         elif self.op == "topk_seg":
             c.topk_segmented(self.d, self.plan, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]))
@@ -169,6 +195,26 @@ class Worker:
             self.msg[4:].copy_(packed)
             self.msg[:1].view(torch.float32).copy_(norms)
         self.step_id += 1
+
+    def compress_step(self):
+        """consensus step (fused, or its own pass with --unfused) + compress of x - x_hat"""
+        c, torch = self.codec, self.torch
+        g = (self.mem, GAMMA)
+        if self.unfused:
+            c.gossip_step(self.x, self.mem, self.hat, GAMMA)
+            g = None
+        if self.op == "topk":
+            c.topk(self.x, self.k, xhat=self.hat, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]),
+                   gossip=g)
+        elif self.op == "qsgd":
+            packed, norms, _ = c.qsgd_compress(self.x, self.param, xhat=self.hat, seed=12345 + self.rank,
+                                               offset=self.step_id, gossip=g)
+            self.msg[16:].copy_(packed)
+            self.msg[:4].view(torch.float32).copy_(norms)
+        else:
+            packed, norms = c.sign_compress(self.x, xhat=self.hat, gossip=g)
+            self.msg[4:].copy_(packed)
+            self.msg[:1].view(torch.float32).copy_(norms)
 
     def exchange(self):
         if not self.peers:
@@ -213,6 +259,14 @@ class Worker:
         """Algorithmic HBM bytes per step of each stage, and the
         notes that say how they are counted."""
         n, nm = self.n, len(self.ranks)
+        if self.step_mode:
+            comp, dec, note = self._codec_bytes(n, nm)
+            # the consensus step reads x, memory, x_hat and writes x (16n) in place of the
+            # 4n read of a resident delta: the compulsory bytes of the fused pass
+            return comp + 12 * n, dec, "consensus step + compress 16n + codec output; " + note
+        return self._codec_bytes(n, nm)
+
+    def _codec_bytes(self, n, nm):
         if self.op in ("topk", "topk_seg"):
             comp = 4 * n + 8 * self.k                    # read d once, write k (fp32 value, int32 index)
             dec = 8 * self.k * nm + 8 * self.k * (nm + 1)  # read each message; RMW mem per msg + x_hat (self)
@@ -326,21 +380,35 @@ def cpu_baseline(w):
     from oracle import torch_port as P
 
     def make(m):
-        d = w.d[:m].cpu()
-        hat, mem = torch.zeros(m), torch.zeros(m)
+        if w.step_mode:  # the reference's step: consensus step, then compress x - x_hat
+            x0, hat, mem = w.x[:m].cpu(), w.hat[:m].cpu(), w.mem[:m].cpu()
+            codec_run = make_codec(m, hat, mem, None)
+
+            def run():
+                x = x0.clone()  # (the copy is outside the reference's work but cheap next to it)
+                P.gossip_step(x, mem, hat, GAMMA)
+                codec_run(x - hat)
+            return run
+        return make_codec(m, torch.zeros(m), torch.zeros(m), w.d[:m].cpu())
+
+    def make_codec(m, hat, mem, d_fixed):
+        def wrap(f):
+            return (lambda: f(d_fixed)) if d_fixed is not None else f
         if w.op in ("topk", "topk_seg", "randk"):
             if w.op == "randk":
-                return lambda: P.sparse_decompress(hat, mem, *P.randk_compress(d, w.param), 1.0)
-            return lambda: P.sparse_decompress(hat, mem, *P.topk_compress(d, w.param), 1.0)
+                return wrap(lambda d: P.sparse_decompress(hat, mem, *P.randk_compress(d, w.param), 1.0))
+            return wrap(lambda d: P.sparse_decompress(hat, mem, *P.topk_compress(d, w.param), 1.0))
         if w.op == "qsgd":
-            return lambda: P.dense_decompress(hat, mem, P.qsgd_compress(d, 2 ** w.param - 1), 1.0)
-        return lambda: P.sign_decompress(hat, mem, *P.sign_compress(d), m, 1.0)
+            return wrap(lambda d: P.dense_decompress(hat, mem, P.qsgd_compress(d, 2 ** w.param - 1), 1.0))
+        return wrap(lambda d: P.sign_decompress(hat, mem, *P.sign_compress(d), m, 1.0))
 
     what = {"topk": "top-k (torch.topk) compress + self decompress",
             "topk_seg": "top-k (torch.topk, flat) compress + self decompress",
             "randk": "random-k (np.random.choice) compress + self decompress",
             "qsgd": f"QSGD q={w.param} compress + self decompress",
             "sign": "sign + L1 norm compress + self decompress"}[w.op]
+    if w.step_mode:
+        what = "consensus step x += gamma (memory - x_hat) + " + what
 
     def timed(threads, m, reps, budget_s):
         torch.set_num_threads(threads)
@@ -393,6 +461,8 @@ def main():
     codec.lib()
     w = Worker(args, rank, world, dev)
     comp_k, dec_k = STAGES[w.op]
+    if w.step_mode:
+        comp_k = comp_k + ["gossip_step"]
 
     def barrier():
         torch.cuda.synchronize()
@@ -519,7 +589,7 @@ def main():
             "e2e": None,
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_e2e:
+        if world == 1 and not args.no_e2e and not w.step_mode:
             out["e2e"] = e2e_rate(w)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(w)

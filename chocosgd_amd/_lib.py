@@ -50,6 +50,14 @@ SIGNATURES = {
     "choco_qsgd_decompress_accumulate": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i32, _c_i64, _vp, _c_i32,
                                                   _c_i32, _c_i32, _vp, _vp, _vp]),
     "choco_gossip_step": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _vp]),
+    "choco_gossip_topk_compress": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+    "choco_gossip_topk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _c_f32, _vp, _p_i64, _c_i32, _vp, _vp, _vp,
+                                                      _c_sz, _vp]),
+    "choco_gossip_randk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _c_f32, _vp, _p_i64, _c_i32, _c_u64, _c_i32,
+                                                       _vp, _vp, _vp, _c_sz, _vp]),
+    "choco_gossip_sign_compress": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _vp, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
+    "choco_gossip_qsgd_compress": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _vp, _c_i32, _c_i32, _c_i32, _c_u64,
+                                            _c_u64, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_profile_enable": (_c_i32, [_c_i32]),
     "choco_profile_filter": (_c_i32, [ctypes.c_char_p]),
     "choco_profile_read": (_c_i32, [ctypes.c_char_p, ctypes.POINTER(_c_f64), ctypes.POINTER(_c_i64)]),

@@ -61,17 +61,33 @@ def lib():
     return _lib.load()
 
 
+def _gossip(gossip, x, xhat):
+    """`gossip=(memory, gamma)`: the fused consensus step x += gamma * (memory - xhat)
+    (optim/utils.py:67-72) in the compressor's first pass; x is written in place and
+    the codec compresses d = x_new - xhat (include/choco_codec.h)."""
+    if gossip is None:
+        return None
+    memory, gamma = gossip
+    _require(memory, torch.float32, "memory")
+    if xhat is None:
+        raise RuntimeError("the fused gossip step needs xhat")
+    if memory.numel() != x.numel():
+        raise RuntimeError("memory and x must have the same number of elements")
+    return memory, float(gamma)
+
+
 # ----------------------------------------------------------------------------- top-k
 def topk_k(n, ratio):
     """k = max(1, int(n * (1 - ratio))) (sparsification.py:22,45)."""
     return int(lib().choco_topk_k(int(n), float(ratio)))
 
 
-def topk(x, k, xhat=None, out=None):
+def topk(x, k, xhat=None, out=None, gossip=None):
     """Exact top-k by |x - xhat| (signed values, int32 indices, ascending index).
 
     `out=(values f32[k], indices i32[k])` writes into caller buffers (e.g. two views
-    of one wire message) instead of allocating."""
+    of one wire message) instead of allocating; `gossip=(memory, gamma)` fuses the
+    consensus step (x is updated in place first)."""
     _require(x, torch.float32, "x")
     if xhat is not None:
         _require(xhat, torch.float32, "xhat")
@@ -90,6 +106,12 @@ def topk(x, k, xhat=None, out=None):
         idx = torch.empty(k, dtype=torch.int32, device=dev)
     L = lib()
     ws = workspace(dev, "topk", L.choco_topk_workspace_size(n))
+    g = _gossip(gossip, x, xhat)
+    if g is not None:
+        _lib.check(L.choco_gossip_topk_compress(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1], n, int(k), _ptr(vals),
+                                                _ptr(idx), _ptr(ws), ws.numel(), _stream(dev)),
+                   "choco_gossip_topk_compress")
+        return vals, idx
     _lib.check(L.choco_topk_compress(_ptr(x), _ptr(xhat), n, int(k), _ptr(vals), _ptr(idx), _ptr(ws),
                                      ws.numel(), _stream(dev)), "choco_topk_compress")
     return vals, idx
@@ -164,13 +186,21 @@ def _seg_outputs(x, xhat, plan, out):
             torch.empty(plan.k_total, dtype=torch.int32, device=x.device))
 
 
-def topk_segmented(x, plan, xhat=None, out=None):
+def topk_segmented(x, plan, xhat=None, out=None, gossip=None):
     """Per-segment top-k (k_s of the plan), GLOBAL int32 indices; `out=(values, indices)`
-    writes into caller buffers (e.g. the two halves of a wire message)."""
+    writes into caller buffers (e.g. the two halves of a wire message);
+    `gossip=(memory, gamma)` fuses the consensus step."""
     vals, idx = _seg_outputs(x, xhat, plan, out)
     dev = x.device
     L = lib()
     ws = plan.workspace(dev)
+    g = _gossip(gossip, x, xhat)
+    if g is not None:
+        _lib.check(L.choco_gossip_topk_compress_segmented(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1], _ptr(plan.plan_dev),
+                                                          plan.plan_host, plan.nseg, _ptr(vals), _ptr(idx), _ptr(ws),
+                                                          ws.numel(), _stream(dev)),
+                   "choco_gossip_topk_compress_segmented")
+        return vals, idx
     _lib.check(L.choco_topk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
                                                plan.nseg, _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(),
                                                _stream(dev)), "choco_topk_compress_segmented")
@@ -194,13 +224,21 @@ def randk(x, k, seed, is_biased=True, xhat=None):
     return vals, idx
 
 
-def randk_segmented(x, plan, seed, is_biased=True, xhat=None, out=None):
+def randk_segmented(x, plan, seed, is_biased=True, xhat=None, out=None, gossip=None):
     """Per-segment random-k over a SegmentPlan (k_s as top-k's), one batched call:
     segment s ranked by the seeded hash with seed seg_seed(seed, s); GLOBAL indices."""
     vals, idx = _seg_outputs(x, xhat, plan, out)
     dev = x.device
     L = lib()
     ws = plan.workspace(dev)
+    g = _gossip(gossip, x, xhat)
+    if g is not None:
+        _lib.check(L.choco_gossip_randk_compress_segmented(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1],
+                                                           _ptr(plan.plan_dev), plan.plan_host, plan.nseg,
+                                                           int(seed) & (2**64 - 1), 1 if is_biased else 0,
+                                                           _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(), _stream(dev)),
+                   "choco_gossip_randk_compress_segmented")
+        return vals, idx
     _lib.check(L.choco_randk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
                                                 plan.nseg, int(seed) & (2**64 - 1), 1 if is_biased else 0,
                                                 _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(), _stream(dev)),
@@ -275,8 +313,9 @@ def sign_words(n):
     return int(lib().choco_sign_words(int(n)))
 
 
-def sign_compress(x, xhat=None, seg_off=None, nseg=1, want_norms=True):
-    """Pack sign bits in the (32, N') layout; optionally per-segment L1 norms (fp64-accumulated)."""
+def sign_compress(x, xhat=None, seg_off=None, nseg=1, want_norms=True, gossip=None):
+    """Pack sign bits in the (32, N') layout; optionally per-segment L1 norms (fp64-accumulated).
+    `gossip=(memory, gamma)` fuses the consensus step."""
     _require(x, torch.float32, "x")
     if xhat is not None:
         _require(xhat, torch.float32, "xhat")
@@ -288,6 +327,12 @@ def sign_compress(x, xhat=None, seg_off=None, nseg=1, want_norms=True):
     packed = torch.empty(sign_words(n), dtype=torch.int32, device=dev)
     norms = torch.empty(nseg, dtype=torch.float32, device=dev) if want_norms else None
     ws = workspace(dev, "acc", L.choco_sign_workspace_size(nseg))
+    g = _gossip(gossip, x, xhat)
+    if g is not None:
+        _lib.check(L.choco_gossip_sign_compress(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1], n, _ptr(seg_off), int(nseg),
+                                                _ptr(packed), _ptr(norms), _ptr(ws), ws.numel(), _stream(dev)),
+                   "choco_gossip_sign_compress")
+        return packed, norms
     _lib.check(L.choco_sign_compress(_ptr(x), _ptr(xhat), n, _ptr(seg_off), int(nseg), _ptr(packed), _ptr(norms),
                                      _ptr(ws), ws.numel(), _stream(dev)), "choco_sign_compress")
     return packed, norms
@@ -358,8 +403,9 @@ def qsgd_packed_bytes(n, q):
 
 
 def qsgd_compress(x, q, is_biased=False, xhat=None, seg_off=None, nseg=1, norm_in=None, u_in=None,
-                  seed=0, offset=0, want_dense=False):
-    """QSGD with s = 2^q - 1.  Returns (packed uint8, norms f32[nseg], dense f32[n] or None)."""
+                  seed=0, offset=0, want_dense=False, gossip=None):
+    """QSGD with s = 2^q - 1.  Returns (packed uint8, norms f32[nseg], dense f32[n] or None).
+    `gossip=(memory, gamma)` fuses the consensus step (device norms and uniforms only)."""
     _require(x, torch.float32, "x")
     if xhat is not None:
         _require(xhat, torch.float32, "xhat")
@@ -378,6 +424,15 @@ def qsgd_compress(x, q, is_biased=False, xhat=None, seg_off=None, nseg=1, norm_i
     norms = torch.empty(nseg, dtype=torch.float32, device=dev)
     dense = torch.empty(n, dtype=torch.float32, device=dev) if want_dense else None
     ws = workspace(dev, "acc", L.choco_qsgd_workspace_size(nseg))
+    g = _gossip(gossip, x, xhat)
+    if g is not None:
+        if norm_in is not None or u_in is not None:
+            raise RuntimeError("the fused gossip step takes the device norms and uniforms")
+        _lib.check(L.choco_gossip_qsgd_compress(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1], n, _ptr(seg_off), int(nseg),
+                                                int(q), 1 if is_biased else 0, int(seed) & (2**64 - 1),
+                                                int(offset) & (2**64 - 1), _ptr(packed), _ptr(norms), _ptr(dense),
+                                                _ptr(ws), ws.numel(), _stream(dev)), "choco_gossip_qsgd_compress")
+        return packed, norms, dense
     _lib.check(L.choco_qsgd_compress(_ptr(x), _ptr(xhat), n, _ptr(seg_off), int(nseg), int(q),
                                      1 if is_biased else 0, _ptr(norm_in), _ptr(u_in), int(seed) & (2**64 - 1),
                                      int(offset) & (2**64 - 1), _ptr(packed), _ptr(norms), _ptr(dense), _ptr(ws),

@@ -108,6 +108,35 @@ CHOCO_DEV float4 ld_buf4s(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff
   return make_float4(f.x, f.y, f.z, f.w);
 }
 
+// 16-byte store through a buffer resource (`nt` when NT); an out-of-range
+// offset is dropped without a memory access.
+template <bool NT>
+CHOCO_DEV void st_buf4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, float4 v) {
+  choco_f32x4 f;
+  f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, f), r,
+                                         byte_off, 0, NT ? 2 : 0);
+}
+
+// ---------------------------------------------------------------- fused gossip step
+// The CHOCO consensus step x += gamma * (memory - x_hat) (optim/utils.py:67-72,
+// three fp32 roundings as torch does) fused into the FIRST full pass of a
+// compressor: that pass reads x, memory and x_hat, writes x_new back in place
+// and works on d = x_new - x_hat (parallel_choco_v.py:236); later passes of the
+// same call read (x_new, x_hat) like any delta input.
+struct Gossip {
+  const float* mem;  // nullptr: no gossip step
+  float gamma;
+};
+CHOCO_DEV float gossip1(float x, float m, float h, float g) { return x + g * (m - h); }
+CHOCO_DEV float4 gossip4(float4 x, float4 m, float4 h, float g) {
+  return make_float4(gossip1(x.x, m.x, h.x, g), gossip1(x.y, m.y, h.y, g), gossip1(x.z, m.z, h.z, g),
+                     gossip1(x.w, m.w, h.w, g));
+}
+CHOCO_DEV float4 sub4(float4 a, float4 b) { return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
+// the standalone step (dense.hip), for paths that have no full first pass to fuse into
+int gossip_launch(float* x, const float* mem, const float* xh, float gamma, int64_t n, hipStream_t st);
+
 CHOCO_DEV int lane_id() { return __lane_id(); }
 
 // number of set bits of `mask` strictly below this lane
@@ -256,14 +285,14 @@ CHOCO_DEV int seg_of(const int64_t* __restrict__ seg_off, int nseg, int64_t e) {
 // Philox4x32-10 (40 32-bit multiplies per 4 uniforms), which made the QSGD
 // quantize pass ALU-bound.
 constexpr uint64_t kGoldenGamma = 0x9E3779B97F4A7C15ull;
-CHOCO_DEV __host__ inline uint64_t splitmix64_mix(uint64_t z) {
+CHOCO_DEV __host__ uint64_t splitmix64_mix(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
 // QSGD uniform stream of (seed, offset): key = mix(seed + (offset + 1) * 0xD1B54A32D192ED03);
 // elements 2p and 2p+1 take bits 63..40 and 31..8 of mix(key + (p + 1) * gamma), * 2^-24.
-CHOCO_DEV __host__ inline uint64_t qrng_key(uint64_t seed, uint64_t offset) {
+CHOCO_DEV __host__ uint64_t qrng_key(uint64_t seed, uint64_t offset) {
   return splitmix64_mix(seed + (offset + 1) * 0xD1B54A32D192ED03ull);
 }
 CHOCO_DEV float u24(uint32_t b24) { return (float)b24 * 5.9604644775390625e-08f; }
@@ -287,7 +316,7 @@ CHOCO_DEV uint32_t rank_hash(uint64_t seed, uint32_t i) {
 // Per-segment random-k seed (host and device agree; oracle/choco_oracle.py seg_seed):
 // splitmix64 of seed + (s + 1) * golden gamma, so every segment draws an independent
 // ranking (the reference calls np.random.choice once per tensor, sparsification.py:48).
-CHOCO_DEV __host__ inline uint64_t seg_seed(uint64_t seed, int64_t s) {
+CHOCO_DEV __host__ uint64_t seg_seed(uint64_t seed, int64_t s) {
   return splitmix64_mix(seed + (uint64_t)(s + 1) * kGoldenGamma);
 }
 
@@ -296,7 +325,10 @@ CHOCO_DEV __host__ inline uint64_t seg_seed(uint64_t seed, int64_t s) {
 // segmented select).  mode: 0 = data keys |d|, 1 = random-k hash keys.
 enum TopkMode { kData = 0, kHash = 1 };
 size_t topk_ws_bytes(int64_t n);
+// gs.mem != nullptr: the gossip step is applied to x[0, n) first (fused into the
+// stream pass where the path has one); x is then written.
 int topk_pipeline(int mode, const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
-                  float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes, hipStream_t st);
+                  float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes, hipStream_t st,
+                  Gossip gs = Gossip{nullptr, 0.f});
 
 }  // namespace choco

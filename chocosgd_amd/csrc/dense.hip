@@ -198,22 +198,94 @@ static unsigned ew_grid(int64_t work, int per_thread) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 8192));
 }
 
+// One-shot form: each thread owns kGossipU float4 of every stream (no grid-stride
+// loop), all loads issued before any arithmetic; `nt` policy knob for the A/B.
+#ifndef CHOCO_GOSSIP_FORM  // 0: grid-stride gossip_kernel; 1: one-shot gossipu_kernel
+#define CHOCO_GOSSIP_FORM 1
+#endif
+#ifndef CHOCO_GOSSIP_U  // measured at 100M (tools/gossip_probe.py): U=4 + nt 258 us (6.2 TB/s)
+#define CHOCO_GOSSIP_U 4    // against 320 us for the grid-stride form and 291 us for U=2 plain
+#endif
+#ifndef CHOCO_GOSSIP_NT
+#define CHOCO_GOSSIP_NT 1
+#endif
+constexpr int kGossipU = CHOCO_GOSSIP_U;
+__global__ __launch_bounds__(kEwThreads) void gossipu_kernel(float* __restrict__ x, const float* __restrict__ mem,
+                                                             const float* __restrict__ hat, float gamma, int64_t n) {
+  const int64_t e0 = ((int64_t)blockIdx.x * kEwThreads * kGossipU + threadIdx.x) * 4;
+  constexpr int64_t kStep = (int64_t)kEwThreads * 4;  // consecutive threads: consecutive float4
+  if (e0 + (kGossipU - 1) * kStep + 3 < n) {
+    float4 a[kGossipU], m[kGossipU], h[kGossipU];
+#pragma unroll
+    for (int u = 0; u < kGossipU; ++u) {
+      if (CHOCO_GOSSIP_NT) {
+        a[u] = ld_nt4(x + e0 + u * kStep);
+        m[u] = ld_nt4(mem + e0 + u * kStep);
+        h[u] = ld_nt4(hat + e0 + u * kStep);
+      } else {
+        a[u] = *reinterpret_cast<const float4*>(x + e0 + u * kStep);
+        m[u] = *reinterpret_cast<const float4*>(mem + e0 + u * kStep);
+        h[u] = *reinterpret_cast<const float4*>(hat + e0 + u * kStep);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kGossipU; ++u) {
+      const float4 v = gossip4(a[u], m[u], h[u], gamma);
+      if (CHOCO_GOSSIP_NT) {
+        choco_f32x4 f;
+        f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
+        __builtin_nontemporal_store(f, reinterpret_cast<choco_f32x4*>(x + e0 + u * kStep));
+      } else {
+        *reinterpret_cast<float4*>(x + e0 + u * kStep) = v;
+      }
+    }
+  } else {
+    for (int u = 0; u < kGossipU; ++u)
+      for (int c = 0; c < 4; ++c) {
+        const int64_t i = e0 + u * kStep + c;
+        if (i < n) x[i] = gossip1(x[i], mem[i], hat[i], gamma);
+      }
+  }
+}
+
+// any 4-byte alignment (segments of a flat buffer): one element per thread
+__global__ __launch_bounds__(kEwThreads) void gossip1_kernel(float* __restrict__ x, const float* __restrict__ mem,
+                                                             const float* __restrict__ hat, float gamma, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * kEwThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kEwThreads + threadIdx.x; i < n; i += stride)
+    x[i] = gossip1(x[i], mem[i], hat[i], gamma);
+}
+
+int gossip_launch(float* x, const float* mem, const float* xh, float gamma, int64_t n, hipStream_t st) {
+  CHOCO_REQUIRE(x && mem && xh, "null pointer argument");
+  CHOCO_REQUIRE(n > 0, "n must be positive");
+  CHOCO_REQUIRE(aligned4(x) && aligned4(mem) && aligned4(xh), "buffers must be 4-byte aligned");
+  profile_begin("gossip_step", st);
+  if (aligned16(x) && aligned16(mem) && aligned16(xh)) {
+    if (CHOCO_GOSSIP_FORM == 1) {
+      const int64_t per = (int64_t)kEwThreads * 4 * kGossipU;
+      CHOCO_KLAUNCH(gossipu_kernel, dim3((unsigned)((n + per - 1) / per)), dim3(kEwThreads), 0, st, x, mem, xh,
+                    gamma, n);
+    } else {
+      CHOCO_KLAUNCH(gossip_kernel, dim3(ew_grid(n, 4)), dim3(kEwThreads), 0, st, x, mem, xh, gamma, n);
+    }
+  } else {
+    CHOCO_KLAUNCH(gossip1_kernel, dim3(ew_grid(n, 1)), dim3(kEwThreads), 0, st, x, mem, xh, gamma, n);
+  }
+  profile_end("gossip_step", st);
+  CHOCO_LAUNCHED("gossip_kernel");
+  return CHOCO_OK;
+}
+
 }  // namespace choco
 
 using namespace choco;
 
 CHOCO_API int choco_gossip_step(float* x, const float* memory, const float* xhat, float gamma, int64_t n,
                                 void* stream) {
-  hipStream_t st = as_stream(stream);
-  CHOCO_REQUIRE(x && memory && xhat, "null pointer argument");
-  CHOCO_REQUIRE(n > 0, "n must be positive");
-  CHOCO_REQUIRE(aligned16(x) && aligned16(memory) && aligned16(xhat), "buffers must be 16-byte aligned");
-  profile_begin("gossip_step", st);
-  CHOCO_KLAUNCH(gossip_kernel, dim3(ew_grid(n, 4)), dim3(kEwThreads), 0, st, x, memory, xhat, gamma, n);
-  profile_end("gossip_step", st);
-  CHOCO_LAUNCHED("gossip_kernel");
-  return CHOCO_OK;
+  return gossip_launch(x, memory, xhat, gamma, n, as_stream(stream));
 }
+
 
 CHOCO_API int choco_sparse_accumulate(const float* val, const int32_t* idx, int64_t k, float* xhat_self,
                                       float* memory, int64_t n, float weight, uint32_t* bad_count, void* stream) {

@@ -90,13 +90,46 @@ CHOCO_DEV float4 ld_quant4(const float* p) {
   return *reinterpret_cast<const float4*>(p);
 }
 
+// The fused gossip step's xh loads and x_new stores in the norm pass:
+// non-temporal (default; measured at 100M in the step: norm 343 -> 315 us, step
+// 0.827 -> 0.785 ms) or plain (A/B knob: lets the quantize pass's backward walk
+// hit the Infinity Cache, but the dirty lines cost more than that saves).
+#ifndef CHOCO_QNORM_GS_NT
+#define CHOCO_QNORM_GS_NT 1
+#endif
+CHOCO_DEV float4 ld_gs4(const float* p) {
+  if (CHOCO_QNORM_GS_NT) return ld_nt4(p);
+  return *reinterpret_cast<const float4*>(p);
+}
+CHOCO_DEV void st_gs4(float* p, float4 v) {
+  if (CHOCO_QNORM_GS_NT) {
+    choco_f32x4 f;
+    f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
+    __builtin_nontemporal_store(f, reinterpret_cast<choco_f32x4*>(p));
+  } else {
+    *reinterpret_cast<float4*>(p) = v;
+  }
+}
+
 // ---------------------------------------------------------------- pass 1: norms
-template <bool XH>
+// GS: the fused gossip step (x_new = x + gamma (memory - xh) written back, the
+// norm is of d = x_new - xh; the quantize pass then reads (x_new, xh)).
+template <bool XH, bool GS = false>
 __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __restrict__ x,
                                                               const float* __restrict__ xh, int64_t n,
                                                               const int64_t* __restrict__ seg_off, int nseg,
                                                               float* __restrict__ norms_out,
-                                                              QsgdWs* __restrict__ ws) {
+                                                              QsgdWs* __restrict__ ws, Gossip gs) {
+  static_assert(!GS || XH, "the gossip step needs x_hat");
+  // one element's delta (and, GS, its gossip step)
+  auto dv = [&](int64_t i) -> float {
+    if (GS) {
+      const float xn = gossip1(x[i], gs.mem[i], xh[i], gs.gamma);
+      const_cast<float*>(x)[i] = xn;
+      return xn - xh[i];
+    }
+    return dval(x, XH ? xh : nullptr, i);
+  };
   __shared__ int s_seg[2];
   __shared__ double s_red[kQThreads / 64];
   __shared__ unsigned int s_flag;
@@ -119,7 +152,19 @@ __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __res
         float4 a[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) a[u] = ld_norm4(x + e0 + (int64_t)u * 4 * kQThreads);
-        if (XH) {
+        if (GS) {
+          float4 h[U], m[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) m[u] = ld_norm4(gs.mem + e0 + (int64_t)u * 4 * kQThreads);
+#pragma unroll
+          for (int u = 0; u < U; ++u) h[u] = ld_gs4(xh + e0 + (int64_t)u * 4 * kQThreads);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const float4 xn = gossip4(a[u], m[u], h[u], gs.gamma);
+            st_gs4(const_cast<float*>(x) + e0 + (int64_t)u * 4 * kQThreads, xn);
+            a[u] = sub4(xn, h[u]);
+          }
+        } else if (XH) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const float4 h = ld_norm4(xh + e0 + (int64_t)u * 4 * kQThreads);
@@ -137,7 +182,7 @@ __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __res
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t e = e0 + (int64_t)u * 4 * kQThreads;
-        if (e + 3 < t1) {
+        if (e + 3 < t1 && !GS) {
           a[u] = *reinterpret_cast<const float4*>(x + e);
           if (XH) {
             const float4 h = *reinterpret_cast<const float4*>(xh + e);
@@ -145,7 +190,7 @@ __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __res
           }
         } else {
           float t[4];
-          for (int c = 0; c < 4; ++c) t[c] = (e + c < t1) ? dval(x, XH ? xh : nullptr, e + c) : 0.f;
+          for (int c = 0; c < 4; ++c) t[c] = (e + c < t1) ? dv(e + c) : 0.f;
           a[u] = make_float4(t[0], t[1], t[2], t[3]);
         }
       }
@@ -173,7 +218,7 @@ __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __res
         sg[c] = -1;
         v[c] = 0.0;
         if (e + c < t1) {
-          const double d = dval(x, XH ? xh : nullptr, e + c);
+          const double d = dv(e + c);
           v[c] = d * d;
           int s = sg0;
           while (s + 1 < nseg && seg_off[s + 1] <= e + c) ++s;
@@ -486,12 +531,12 @@ CHOCO_API size_t choco_qsgd_workspace_size(int32_t nseg) {
   return 256 + align_up((size_t)(nseg > 0 ? nseg : 1) * sizeof(double), 256);
 }
 
-CHOCO_API int choco_qsgd_compress(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
-                                  int32_t q, int32_t is_biased, const float* norm_in, const float* u_in,
-                                  uint64_t seed, uint64_t offset, uint8_t* packed, float* norms_out,
-                                  float* dense_out, void* ws, size_t ws_bytes, void* stream) {
-  hipStream_t st = as_stream(stream);
+static int qsgd_compress(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
+                         int32_t q, int32_t is_biased, const float* norm_in, const float* u_in, uint64_t seed,
+                         uint64_t offset, uint8_t* packed, float* norms_out, float* dense_out, void* ws,
+                         size_t ws_bytes, hipStream_t st, Gossip gs) {
   CHOCO_REQUIRE(x && packed, "null pointer argument");
+  CHOCO_REQUIRE(!gs.mem || (xhat && aligned16(gs.mem)), "the gossip step needs x_hat and a 16-byte aligned memory");
   CHOCO_REQUIRE(q >= 1 && q <= 16, "quantize level q must be in [1, 16] (q = 32 is a passthrough), got %d", q);
   CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
   CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
@@ -507,17 +552,26 @@ CHOCO_API int choco_qsgd_compress(const float* x, const float* xhat, int64_t n, 
     const unsigned g1 = (unsigned)((n + kNormTile - 1) / kNormTile);
     QsgdWs* w = static_cast<QsgdWs*>(ws);
     profile_begin("qsgd_norm", st);
-    if (xhat)
+    if (gs.mem)
+      CHOCO_KLAUNCH((qsgd_norm_kernel<true, true>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
+                    norms_out, w, gs);
+    else if (xhat)
       CHOCO_KLAUNCH((qsgd_norm_kernel<true>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
-                         norms_out, w);
+                    norms_out, w, gs);
     else
       CHOCO_KLAUNCH((qsgd_norm_kernel<false>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
-                         norms_out, w);
+                    norms_out, w, gs);
     profile_end("qsgd_norm", st);
     CHOCO_LAUNCHED("qsgd_norm_kernel");
     norms = norms_out;
-  } else if (norms_out && norms_out != norm_in) {
-    CHOCO_HIP(hipMemcpyAsync(norms_out, norm_in, sizeof(float) * nseg, hipMemcpyDeviceToDevice, st));
+  } else {
+    // pinned norms (parity mode): no norm pass to fuse the gossip step into
+    if (gs.mem) {
+      const int rc = gossip_launch(const_cast<float*>(x), gs.mem, xhat, gs.gamma, n, st);
+      if (rc) return rc;
+    }
+    if (norms_out && norms_out != norm_in)
+      CHOCO_HIP(hipMemcpyAsync(norms_out, norm_in, sizeof(float) * nseg, hipMemcpyDeviceToDevice, st));
   }
   uint8_t* lvl_plane = packed;
   uint8_t* sign_plane = packed + plane_bytes(n, cw);
@@ -540,6 +594,23 @@ CHOCO_API int choco_qsgd_compress(const float* x, const float* xhat, int64_t n, 
   profile_end("qsgd_quantize", st);
   CHOCO_LAUNCHED("qsgd_quant_kernel");
   return CHOCO_OK;
+}
+
+CHOCO_API int choco_qsgd_compress(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
+                                  int32_t q, int32_t is_biased, const float* norm_in, const float* u_in,
+                                  uint64_t seed, uint64_t offset, uint8_t* packed, float* norms_out,
+                                  float* dense_out, void* ws, size_t ws_bytes, void* stream) {
+  return qsgd_compress(x, xhat, n, seg_off, nseg, q, is_biased, norm_in, u_in, seed, offset, packed, norms_out,
+                       dense_out, ws, ws_bytes, as_stream(stream), Gossip{nullptr, 0.f});
+}
+
+CHOCO_API int choco_gossip_qsgd_compress(float* x, const float* memory, const float* xhat, float gamma, int64_t n,
+                                         const int64_t* seg_off, int32_t nseg, int32_t q, int32_t is_biased,
+                                         uint64_t seed, uint64_t offset, uint8_t* packed, float* norms_out,
+                                         float* dense_out, void* ws, size_t ws_bytes, void* stream) {
+  CHOCO_REQUIRE(memory != nullptr && xhat != nullptr, "the gossip step needs memory and x_hat");
+  return qsgd_compress(x, xhat, n, seg_off, nseg, q, is_biased, nullptr, nullptr, seed, offset, packed, norms_out,
+                       dense_out, ws, ws_bytes, as_stream(stream), Gossip{memory, gamma});
 }
 
 CHOCO_API int choco_qsgd_decode(const uint8_t* packed, const float* norms, int64_t n, const int64_t* seg_off,

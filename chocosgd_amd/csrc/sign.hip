@@ -38,6 +38,14 @@ struct SignWs {
   // double acc[nseg] follows at offset 256
 };
 
+template <bool NT = false>
+CHOCO_DEV void st_buf4s(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, float4 v) {
+  choco_f32x4 f;
+  f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, f), r,
+                                         voff, soff, NT ? 2 : 0);
+}
+
 CHOCO_DEV void load4g(const float* __restrict__ x, const float* __restrict__ xh, int64_t e, int64_t n,
                       float (&v)[4]) {
   if (e + 3 < n) {
@@ -53,6 +61,43 @@ CHOCO_DEV void load4g(const float* __restrict__ x, const float* __restrict__ xh,
       const int64_t i = e + c;
       v[c] = (i < n && i >= 0) ? (xh ? x[i] - xh[i] : x[i]) : 0.f;
     }
+  }
+}
+
+// load4g with the fused gossip step (GS): x_new = x + gamma (memory - xh) for the
+// four elements e..e+3, stored back for the elements this wave owns ([own0, own1)
+// -- the realigned loads also read neighbours' elements, which are never used),
+// v = x_new - xh.
+CHOCO_DEV void load4g_gossip(const float* __restrict__ x, const float* __restrict__ xh, const Gossip& gs, int64_t e,
+                             int64_t n, int64_t own0, int64_t own1, float (&v)[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int64_t i = e + c;
+    v[c] = 0.f;
+    if (i < n && i >= 0) {
+      const float xn = gossip1(x[i], gs.mem[i], xh[i], gs.gamma);
+      if (i >= own0 && i < own1) const_cast<float*>(x)[i] = xn;
+      v[c] = xn - xh[i];
+    }
+  }
+}
+
+// store x_new of lane-owned elements A+4l+c (c >= m for lane 0) and, for lane 63,
+// of the tail A+256+c (c < m): the owned run is [A+m, A+m+256)
+CHOCO_DEV void store_owned_gossip(float* __restrict__ x, int64_t A, int m, int lane, float4 a, float4 t) {
+  if (lane > 0 || m == 0) {
+    *reinterpret_cast<float4*>(x + A + 4 * lane) = a;
+  } else {
+    const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int c = 1; c < 4; ++c)
+      if (c >= m) x[A + c] = av[c];
+  }
+  if (lane == 63 && m > 0) {
+    const float tv[3] = {t.x, t.y, t.z};
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      if (c < m) x[A + 256 + c] = tv[c];
   }
 }
 
@@ -95,11 +140,13 @@ CHOCO_DEV void row_segments(const int64_t* __restrict__ seg_off, int nseg, int64
   }
 }
 
-template <bool XH, bool NORM>
+// GS: the fused gossip step (x_new written back for the wave's own elements).
+template <bool XH, bool NORM, bool GS = false>
 __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t Np,
     const int64_t* __restrict__ seg_off, int nseg, uint32_t* __restrict__ packed, float* __restrict__ l1_out,
-    SignWs* __restrict__ ws) {
+    SignWs* __restrict__ ws, Gossip gs) {
+  static_assert(!GS || XH, "the gossip step needs x_hat");
   __shared__ int s_lo[32], s_hi[32];
   __shared__ double s_rows[kSignThreads / 64][32];
   __shared__ unsigned int s_flag;
@@ -128,6 +175,13 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
       if (XH) {
         const float4 h = ld_nt4(xh + A + 4 * lane);
         const float4 ht = *reinterpret_cast<const float4*>(xh + A + 256);
+        if (GS) {
+          const float4 am = ld_nt4(gs.mem + A + 4 * lane);
+          const float4 tm = *reinterpret_cast<const float4*>(gs.mem + A + 256);
+          a = gossip4(a, am, h, gs.gamma);
+          t = gossip4(t, tm, ht, gs.gamma);
+          store_owned_gossip(const_cast<float*>(x), A, (int)(((int64_t)(r0 + u) * Np + j0) & 3), lane, a, t);
+        }
         a.x -= h.x; a.y -= h.y; a.z -= h.z; a.w -= h.w;
         t.x -= ht.x; t.y -= ht.y; t.z -= ht.z; t.w -= ht.w;
       }
@@ -142,8 +196,13 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
       for (int c = 0; c < 4; ++c) { vr[u][c] = 0.f; tr[u][c] = 0.f; }
       if (ncol > 0 && s < n) {
         const int64_t A = s & ~(int64_t)3;
-        load4g(x, XH ? xh : nullptr, A + 4 * lane, n, vr[u]);
-        if ((s & 3) != 0 && lane == 63) load4g(x, XH ? xh : nullptr, A + 256, n, tr[u]);
+        if (GS) {
+          load4g_gossip(x, xh, gs, A + 4 * lane, n, s, s + ncol, vr[u]);
+          if ((s & 3) != 0 && lane == 63) load4g_gossip(x, xh, gs, A + 256, n, s, s + ncol, tr[u]);
+        } else {
+          load4g(x, XH ? xh : nullptr, A + 4 * lane, n, vr[u]);
+          if ((s & 3) != 0 && lane == 63) load4g(x, XH ? xh : nullptr, A + 256, n, tr[u]);
+        }
       }
     }
   }
@@ -262,16 +321,25 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
 // bytes): the row offset is a wave-uniform SGPR operand and the lane offset
 // one VGPR, so the 2 x RU loads in flight need no 64-bit address registers.
 
+#ifndef CHOCO_SIGN_GS_RU  // rows per group with the fused gossip step (3 streams)
+#define CHOCO_SIGN_GS_RU 8
+#endif
+#ifndef CHOCO_SIGN_GS_FUSE  // 0: the standalone consensus step, then the x - x_hat pack (A/B)
+#define CHOCO_SIGN_GS_FUSE 1
+#endif
 #ifndef CHOCO_SIGN_NT  // non-temporal loads in the one-segment pack
 #define CHOCO_SIGN_NT 1
 #endif
-template <bool XH, bool NORM>
+// GS: the fused gossip step -- x, memory and xh rows in flight, x_new stored back
+// (each lane owns its float4 of every row run: no overlap), d = x_new - xh.
+template <bool XH, bool NORM, bool GS = false>
 __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* __restrict__ x,
                                                                   const float* __restrict__ xh, int64_t n,
                                                                   int64_t Np, uint32_t* __restrict__ packed,
                                                                   float* __restrict__ l1_out,
-                                                                  SignWs* __restrict__ ws) {
-  constexpr int RU = XH ? 4 : 8;  // rows per group (x and xh double the registers)
+                                                                  SignWs* __restrict__ ws, Gossip gs) {
+  static_assert(!GS || XH, "the gossip step needs x_hat");
+  constexpr int RU = GS ? CHOCO_SIGN_GS_RU : (XH ? 4 : 8);  // rows per group (more streams, more registers)
   constexpr int NG = 32 / RU;
   __shared__ double s_red[kSignThreads / 64];
   __shared__ unsigned int s_flag;
@@ -283,26 +351,44 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
   const bool interior = ncol == 256 && (int64_t)31 * Np + j0 + 256 <= n;
   const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x, (uint32_t)(n * 4));
   const __amdgpu_buffer_rsrc_t rh = buf_rsrc(XH ? xh : x, (uint32_t)(n * 4));
+  const __amdgpu_buffer_rsrc_t rm = buf_rsrc(GS ? gs.mem : x, (uint32_t)(n * 4));
   const uint32_t voff = 16u * (uint32_t)lane;
   auto row_off = [&](int r) -> uint32_t { return (uint32_t)(((int64_t)r * Np + j0) * 4); };  // wave-uniform
-  auto load_group = [&](int g, float4 (&R)[RU]) {
+  // A group's raw rows (x; xh; memory) stay in flight until the group is processed:
+  // the delta and the gossip step's x_new are formed in proc_group, so the other
+  // group's loads are not waited for early.
+  struct Group {
+    float4 x[RU], h[RU], m[RU];
+  };
+  auto load_group = [&](int g, Group& G) {
 #pragma unroll
-    for (int u = 0; u < RU; ++u) R[u] = ld_buf4s<CHOCO_SIGN_NT>(rx, voff, row_off(g * RU + u));
+    for (int u = 0; u < RU; ++u) G.x[u] = ld_buf4s<CHOCO_SIGN_NT>(rx, voff, row_off(g * RU + u));
     if (XH) {
-      float4 H[RU];
 #pragma unroll
-      for (int u = 0; u < RU; ++u) H[u] = ld_buf4s<CHOCO_SIGN_NT>(rh, voff, row_off(g * RU + u));
+      for (int u = 0; u < RU; ++u) G.h[u] = ld_buf4s<CHOCO_SIGN_NT>(rh, voff, row_off(g * RU + u));
+    }
+    if (GS) {
 #pragma unroll
-      for (int u = 0; u < RU; ++u) { R[u].x -= H[u].x; R[u].y -= H[u].y; R[u].z -= H[u].z; R[u].w -= H[u].w; }
+      for (int u = 0; u < RU; ++u) G.m[u] = ld_buf4s<CHOCO_SIGN_NT>(rm, voff, row_off(g * RU + u));
     }
   };
   uint32_t wd[4] = {0u, 0u, 0u, 0u};
   double p = 0.0;
-  auto proc_group = [&](int g, const float4 (&R)[RU]) {
+  auto proc_group = [&](int g, Group& G) {
+    if (GS) {
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        G.x[u] = gossip4(G.x[u], G.m[u], G.h[u], gs.gamma);
+        // non-temporal: x_new is not re-read by this step, and dirty Infinity-Cache
+        // lines would be written back in the middle of the receiver's pass
+        st_buf4s<true>(rx, voff, row_off(g * RU + u), G.x[u]);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int r = g * RU + u;
-      const float v[4] = {R[u].x, R[u].y, R[u].z, R[u].w};
+      const float4 R = XH ? sub4(G.x[u], G.h[u]) : G.x[u];
+      const float v[4] = {R.x, R.y, R.z, R.w};
 #pragma unroll
       for (int c = 0; c < 4; ++c) wd[c] |= (v[c] < 0.f ? 1u : 0u) << r;
       if (NORM) p += ((double)fabsf(v[0]) + (double)fabsf(v[1])) + ((double)fabsf(v[2]) + (double)fabsf(v[3]));
@@ -312,7 +398,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
   // (sched_barrier: keep each group's loads where they are written -- hoisted,
   // all 32 rows would be live at once)
   if (interior) {
-    float4 A[RU], B[RU];
+    Group A, B;
     load_group(0, A);
     load_group(1, B);
 #pragma unroll
@@ -331,7 +417,16 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int64_t e = s + c;
-        tt[c] = (4 * lane + c < ncol && e < n) ? (XH ? x[e] - xh[e] : x[e]) : 0.f;
+        if (GS) {
+          tt[c] = 0.f;
+          if (4 * lane + c < ncol && e < n) {
+            const float xn = gossip1(x[e], gs.mem[e], xh[e], gs.gamma);
+            const_cast<float*>(x)[e] = xn;
+            tt[c] = xn - xh[e];
+          }
+        } else {
+          tt[c] = (4 * lane + c < ncol && e < n) ? (XH ? x[e] - xh[e] : x[e]) : 0.f;
+        }
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c) wd[c] |= (tt[c] < 0.f ? 1u : 0u) << r;
@@ -674,12 +769,6 @@ constexpr int kSA1Waves = 4;
 constexpr int kSA1WgCols = kSA1Cols * kSA1Waves;
 constexpr int kSA1RU = 2;                    // rows per group
 
-CHOCO_DEV void st_buf4s(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, float4 v) {
-  choco_f32x4 f;
-  f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, f), r,
-                                         voff, soff, 0);
-}
 
 template <int NM, bool HS>
 __global__ __launch_bounds__(64 * kSA1Waves) void sign_accumulate1_kernel(SignMsgs M, int64_t n, int64_t Np,
@@ -793,14 +882,25 @@ CHOCO_API size_t choco_sign_workspace_size(int32_t nseg) {
   return 256 + align_up((size_t)(nseg > 0 ? nseg : 1) * sizeof(double), 256);
 }
 
-CHOCO_API int choco_sign_compress(const float* x, const float* xhat, int64_t n, const int64_t* seg_off,
-                                  int32_t nseg, int32_t* packed, float* l1_norms, void* ws, size_t ws_bytes,
-                                  void* stream) {
-  hipStream_t st = as_stream(stream);
+template <bool XH, bool NORM, bool GS>
+static void launch_pack(bool one, unsigned grid, hipStream_t st, const float* x, const float* xhat, int64_t n,
+                        int64_t Np, const int64_t* seg_off, int32_t nseg, uint32_t* pk, float* l1, SignWs* w,
+                        Gossip gs) {
+  if (one)
+    CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, pk, l1,
+                  w, gs);
+  else
+    CHOCO_KLAUNCH((sign_pack_kernel<XH, NORM, GS>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, seg_off,
+                  nseg, pk, l1, w, gs);
+}
+
+static int sign_compress(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
+                         int32_t* packed, float* l1_norms, void* ws, size_t ws_bytes, hipStream_t st, Gossip gs) {
   CHOCO_REQUIRE(x && packed, "null pointer argument");
   CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
   CHOCO_REQUIRE(aligned16(x) && (!xhat || aligned16(xhat)) && aligned16(packed),
                 "x/xhat/packed must be 16-byte aligned");
+  CHOCO_REQUIRE(!gs.mem || (xhat && aligned16(gs.mem)), "the gossip step needs x_hat and a 16-byte aligned memory");
   CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
   const int64_t Np = choco_sign_words(n);
   const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
@@ -809,41 +909,41 @@ CHOCO_API int choco_sign_compress(const float* x, const float* xhat, int64_t n, 
   if (l1_norms) {
     CHOCO_REQUIRE(ws && ws_bytes >= choco_sign_workspace_size(nseg), "sign workspace too small");
   }
+  const bool one = nseg == 1 && n < (int64_t(1) << 30);  // one segment, buffer offsets: n * 4 < 2^32 bytes
+  if (gs.mem && !CHOCO_SIGN_GS_FUSE) {
+    const int rc = gossip_launch(const_cast<float*>(x), gs.mem, xhat, gs.gamma, n, st);
+    if (rc) return rc;
+    gs.mem = nullptr;
+  }
   profile_begin("sign_pack", st);
-  if (nseg == 1 && n < (int64_t(1) << 30)) {  // buffer offsets: n * 4 < 2^32 bytes
-    if (xhat) {
-      if (l1_norms)
-        CHOCO_KLAUNCH((sign_pack1_kernel<true, true>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, pk,
-                      l1_norms, w);
-      else
-        CHOCO_KLAUNCH((sign_pack1_kernel<true, false>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, pk,
-                      l1_norms, w);
-    } else {
-      if (l1_norms)
-        CHOCO_KLAUNCH((sign_pack1_kernel<false, true>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, pk,
-                      l1_norms, w);
-      else
-        CHOCO_KLAUNCH((sign_pack1_kernel<false, false>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
-                      pk, l1_norms, w);
-    }
+  if (gs.mem) {
+    if (l1_norms) launch_pack<true, true, true>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs);
+    else launch_pack<true, false, true>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs);
   } else if (xhat) {
-    if (l1_norms)
-      CHOCO_KLAUNCH((sign_pack_kernel<true, true>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
-                         seg_off, nseg, pk, l1_norms, w);
-    else
-      CHOCO_KLAUNCH((sign_pack_kernel<true, false>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
-                         seg_off, nseg, pk, l1_norms, w);
+    if (l1_norms) launch_pack<true, true, false>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs);
+    else launch_pack<true, false, false>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs);
   } else {
-    if (l1_norms)
-      CHOCO_KLAUNCH((sign_pack_kernel<false, true>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
-                         seg_off, nseg, pk, l1_norms, w);
-    else
-      CHOCO_KLAUNCH((sign_pack_kernel<false, false>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n,
-                         Np, seg_off, nseg, pk, l1_norms, w);
+    if (l1_norms) launch_pack<false, true, false>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs);
+    else launch_pack<false, false, false>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs);
   }
   profile_end("sign_pack", st);
   CHOCO_LAUNCHED("sign_pack_kernel");
   return CHOCO_OK;
+}
+
+CHOCO_API int choco_sign_compress(const float* x, const float* xhat, int64_t n, const int64_t* seg_off,
+                                  int32_t nseg, int32_t* packed, float* l1_norms, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  return sign_compress(x, xhat, n, seg_off, nseg, packed, l1_norms, ws, ws_bytes, as_stream(stream),
+                       Gossip{nullptr, 0.f});
+}
+
+CHOCO_API int choco_gossip_sign_compress(float* x, const float* memory, const float* xhat, float gamma, int64_t n,
+                                         const int64_t* seg_off, int32_t nseg, int32_t* packed, float* l1_norms,
+                                         void* ws, size_t ws_bytes, void* stream) {
+  CHOCO_REQUIRE(memory != nullptr && xhat != nullptr, "the gossip step needs memory and x_hat");
+  return sign_compress(x, xhat, n, seg_off, nseg, packed, l1_norms, ws, ws_bytes, as_stream(stream),
+                       Gossip{memory, gamma});
 }
 
 CHOCO_API int choco_sign_unpack(const int32_t* packed, int64_t n, float* out, void* stream) {

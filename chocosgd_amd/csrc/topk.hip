@@ -163,6 +163,12 @@ struct Src {
   const float* __restrict__ xh;
   uint64_t seed;
   CHOCO_DEV float val(int64_t i) const { return XH ? x[i] - xh[i] : x[i]; }
+  // the fused gossip step on one element: x[i] <- x_new, returns x_new - xh[i]
+  CHOCO_DEV float val_gossip(int64_t i, const Gossip& g) const {
+    const float xn = gossip1(x[i], g.mem[i], xh[i], g.gamma);
+    const_cast<float*>(x)[i] = xn;
+    return xn - xh[i];
+  }
   CHOCO_DEV uint32_t key_of(int64_t i, float v) const {
     if (MODE == kHash) return rank_hash(seed, (uint32_t)i) >> 1;
     return fkey(v);
@@ -384,9 +390,10 @@ CHOCO_DEV Buckets make_buckets_from(uint32_t s_lo, uint32_t s_hi, uint32_t shift
   return bk;
 }
 
-template <bool XH>
-CHOCO_DEV void load_sample(const float* __restrict__ x, const float* __restrict__ xh, int64_t n,
-                           float4 (&s)[kSampleLoads], float4 (&h)[kSampleLoads]) {
+template <bool XH, bool GS>
+CHOCO_DEV void load_sample(const float* __restrict__ x, const float* __restrict__ xh, const float* __restrict__ mem,
+                           int64_t n, float4 (&s)[kSampleLoads], float4 (&h)[kSampleLoads],
+                           float4 (&m)[kSampleLoads]) {
   const int64_t stride4 = ((n - 256) / (kSampleRuns - 1)) >> 2;  // float4 between run starts
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   // one 1 KiB buffer resource per run (wave-uniform base): dword-aligned 16-B
@@ -396,6 +403,7 @@ CHOCO_DEV void load_sample(const float* __restrict__ x, const float* __restrict_
     const int64_t run0 = (int64_t)(w * kSampleLoads + j) * stride4 * 4;  // wave w: runs 4w .. 4w+3
     s[j] = ld_buf4<false>(buf_rsrc(x + run0, 1024u), 16u * (uint32_t)lane);
     if (XH) h[j] = ld_buf4<false>(buf_rsrc(xh + run0, 1024u), 16u * (uint32_t)lane);
+    if (GS) m[j] = ld_buf4<false>(buf_rsrc(mem + run0, 1024u), 16u * (uint32_t)lane);
   }
 }
 
@@ -503,7 +511,7 @@ struct StreamSmem {
 #endif
 constexpr uint32_t kNoChunk = 0x80000000u;  // > any tile's bytes (tile <= 2^31 / 256 elements)
 struct TileRsrc {
-  __amdgpu_buffer_rsrc_t x, xh;
+  __amdgpu_buffer_rsrc_t x, xh, m;  // m: the gossip step's memory (GS only)
 };
 
 template <bool XH>
@@ -516,6 +524,30 @@ CHOCO_DEV void load_rows_full(const TileRsrc& ts, uint32_t boff, int lane, float
       const float4 h = ld_buf4<CHOCO_STREAM_NT>(ts.xh, boff + (u * 256 + 4 * lane) * 4);
       r[u].x -= h.x; r[u].y -= h.y; r[u].z -= h.z; r[u].w -= h.w;
     }
+  }
+}
+
+// The fused gossip step on one load batch (GS): x, memory and xh rows in flight
+// together, x_new = x + gamma (memory - xh) stored back in place (a chunk that
+// does not exist loads zeros and its stores are dropped: out of the resource's
+// range), and r = x_new - xh.  No cross-chunk prefetch: three streams per wave
+// keep 24 KiB in flight, 16 waves per CU are plenty to cover the latency.
+#ifndef CHOCO_GS_STORE_NT  // cache policy of the x_new stores (A/B knob)
+#define CHOCO_GS_STORE_NT 1
+#endif
+CHOCO_DEV void gossip_rows(const TileRsrc& ts, uint32_t boff, int lane, float gamma, float4 (&r)[kK2Unroll]) {
+  float4 M[kK2Unroll], H[kK2Unroll];
+#pragma unroll
+  for (int u = 0; u < kK2Unroll; ++u) r[u] = ld_buf4<CHOCO_STREAM_NT>(ts.x, boff + (u * 256 + 4 * lane) * 4);
+#pragma unroll
+  for (int u = 0; u < kK2Unroll; ++u) M[u] = ld_buf4<CHOCO_STREAM_NT>(ts.m, boff + (u * 256 + 4 * lane) * 4);
+#pragma unroll
+  for (int u = 0; u < kK2Unroll; ++u) H[u] = ld_buf4<CHOCO_STREAM_NT>(ts.xh, boff + (u * 256 + 4 * lane) * 4);
+#pragma unroll
+  for (int u = 0; u < kK2Unroll; ++u) {
+    const float4 xn = gossip4(r[u], M[u], H[u], gamma);
+    st_buf4<CHOCO_GS_STORE_NT>(ts.x, boff + (u * 256 + 4 * lane) * 4, xn);
+    r[u] = sub4(xn, H[u]);
   }
 }
 
@@ -793,22 +825,25 @@ CHOCO_DEV void sample_bounds(const uint32_t (&kk)[kSampleLoads * 4], const Sampl
 // drains, so the histogram work does not start until it has); as their own
 // tiny kernel they take a few us and the stream kernel starts streaming at
 // once.
-template <bool XH>
+// GS: the sample is of d = (x + gamma (memory - xh)) - xh (K2 writes x_new later).
+template <bool XH, bool GS>
 __global__ __launch_bounds__(kK1Threads) void topk_bounds_kernel(const float* __restrict__ x,
                                                                  const float* __restrict__ xh, int64_t n,
-                                                                 SampleRanks ranks, TopkCtrl* __restrict__ ctrl) {
+                                                                 SampleRanks ranks, TopkCtrl* __restrict__ ctrl,
+                                                                 Gossip gs) {
   __shared__ BoundsSmem sm;
   STAMP(30000, 0);
   const int lane = lane_id(), w = threadIdx.x >> 6;
   // this call's bucket totals and overflow flag start from zero (K2 adds to them)
   for (int i = threadIdx.x; i < kNRep * kNBucket; i += kK1Threads) (&ctrl->G[0][0])[i] = 0u;
   if (threadIdx.x == 0) ctrl->overflow = 0u;
-  float4 s[kSampleLoads], sh[kSampleLoads];
-  load_sample<XH>(x, xh, n, s, sh);
+  float4 s[kSampleLoads], sh[kSampleLoads], sm_[kSampleLoads];
+  load_sample<XH, GS>(x, xh, gs.mem, n, s, sh, sm_);
   uint32_t kk[kSampleLoads * 4];
 #pragma unroll
   for (int j = 0; j < kSampleLoads; ++j) {
     float4 v = s[j];
+    if (GS) v = gossip4(v, sm_[j], sh[j], gs.gamma);
     if (XH) { v.x -= sh[j].x; v.y -= sh[j].y; v.z -= sh[j].z; v.w -= sh[j].w; }
     kk[4 * j + 0] = fkey(v.x); kk[4 * j + 1] = fkey(v.y); kk[4 * j + 2] = fkey(v.z); kk[4 * j + 3] = fkey(v.w);
   }
@@ -827,12 +862,15 @@ __global__ __launch_bounds__(kK1Threads) void topk_bounds_kernel(const float* __
 
 // Random-k (MODE kHash): keys are uniform on [0, 2^31) and (s_lo, s_hi) come from
 // the binomial tails (host), passed as hs_lo / hs_hi.
-template <int MODE, bool XH>
+// GS (kData, XH): the fused gossip step -- the stream reads x, memory and xh,
+// writes x_new back and selects on d = x_new - xh.
+template <int MODE, bool XH, bool GS = false>
 __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, uint32_t tile,
     uint32_t side_cap, uint64_t seed, uint32_t hs_lo, uint64_t hs_hi, TopkCtrl* __restrict__ ctrl,
     uint32_t* __restrict__ cum_tab, uint32_t* __restrict__ cntw, uint32_t* __restrict__ side,
-    float* __restrict__ cval, uint32_t* __restrict__ cidx) {
+    float* __restrict__ cval, uint32_t* __restrict__ cidx, Gossip gs) {
+  static_assert(!GS || (MODE == kData && XH), "the gossip step needs x_hat and data keys");
   __shared__ StreamSmem sm;
   STAMP(1024 + blockIdx.x, 0);
   const int tid = threadIdx.x;
@@ -842,12 +880,14 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   constexpr int64_t kStep = 256 * kK2Unroll;
   constexpr bool kOneBatch = kChunk == kStep;  // a chunk is one load batch (else: two, A and B)
   constexpr bool kTwoChunks = kOneBatch && MODE == kData && !XH;  // A and B hold the next two chunks
+  static_assert(!GS || kOneBatch, "the gossip stream processes one-batch chunks");
   const uint32_t nchunk = tile / (uint32_t)kChunk;
   Src<MODE, XH> src{x, xh, seed};
   // tile-relative byte offset of a full chunk's first / second batch, or kNoChunk
   const int64_t tlen = min((int64_t)tile, n - b * (int64_t)tile);
   const TileRsrc ts{buf_rsrc(x + b * (int64_t)tile, (uint32_t)(tlen * 4)),
-                    buf_rsrc((XH ? xh : x) + b * (int64_t)tile, (uint32_t)(tlen * 4))};
+                    buf_rsrc((XH ? xh : x) + b * (int64_t)tile, (uint32_t)(tlen * 4)),
+                    buf_rsrc((GS ? gs.mem : x) + b * (int64_t)tile, (uint32_t)(tlen * 4))};
   auto batch0 = [&](uint32_t c) -> uint32_t {
     return (c < nchunk && (int64_t)(c + 1) * kChunk <= tlen) ? c * (uint32_t)kChunk * 4u : kNoChunk;
   };
@@ -860,7 +900,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   float4 A[kK2Unroll], B[kK2Unroll];
   Buckets bk;
   if constexpr (MODE == kData) {
-    load_rows_full<XH>(ts, batch0(c), lane, A);
+    if (!GS) load_rows_full<XH>(ts, batch0(c), lane, A);
     if (kTwoChunks) load_rows_full<XH>(ts, batch0(c + kK2Waves), lane, B);
     else if (!kOneBatch && !XH) load_rows_full<XH>(ts, batch1(c), lane, B);
     bk = make_buckets_from(ctrl->s_lo, ctrl->s_hi, ctrl->shift, seed);
@@ -907,7 +947,8 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
         if (MODE == kData) {
           float tt[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) tt[q] = (i + q < cend) ? src.val(i + q) : 0.f;
+          for (int q = 0; q < 4; ++q)
+            tt[q] = (i + q < cend) ? (GS ? src.val_gossip(i + q, gs) : src.val(i + q)) : 0.f;
           v = make_float4(tt[0], tt[1], tt[2], tt[3]);
         }
         process_row<MODE, XH, true>(src, v, i, cend, sm, w, lane, a, ov, oi, bk);
@@ -943,8 +984,9 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     // one buffer (two input streams: x - xh is formed at load time; hash mode: no loads)
     while (c < nchunk) {
       const uint32_t nn = claim_chunk(sm, lane);
+      if constexpr (GS) gossip_rows(ts, batch0(c), lane, gs.gamma, A);
       run_chunk(c, A);
-      if constexpr (MODE == kData) load_rows_full<XH>(ts, batch0(nn), lane, A);
+      if constexpr (MODE == kData && !GS) load_rows_full<XH>(ts, batch0(nn), lane, A);
       c = nn;
     }
   } else {
@@ -983,7 +1025,8 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
         if (MODE == kData) {
           float tt[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) tt[q] = (i + q < cend) ? src.val(i + q) : 0.f;
+          for (int q = 0; q < 4; ++q)
+            tt[q] = (i + q < cend) ? (GS ? src.val_gossip(i + q, gs) : src.val(i + q)) : 0.f;
           v = make_float4(tt[0], tt[1], tt[2], tt[3]);
         }
         process_row<MODE, XH, true>(src, v, i, cend, sm, w, lane, a, ov, oi, bk);
@@ -1775,7 +1818,8 @@ __global__ __launch_bounds__(kK2Threads) void topk_fused_kernel(
       // of the bucket totals is cleared for the next call
       bounds_wg = true;
       float4 sv[kSampleLoads], shv[kSampleLoads];
-      load_sample<XH>(x, xh, n, sv, shv);
+      float4 smv[kSampleLoads];
+      load_sample<XH, false>(x, xh, nullptr, n, sv, shv, smv);
       uint32_t kk[kSampleLoads * 4];
 #pragma unroll
       for (int j = 0; j < kSampleLoads; ++j) {
@@ -2141,10 +2185,12 @@ size_t topk_ws_bytes(int64_t n) {
   return CHOCO_TOPK_FUSED && fused_fits(n) ? fused_layout(n).total : topk_layout(n).total;
 }
 
-template <int MODE, bool XH>
+// GS: the gossip step fused into K1's sample and K2's stream (x written by K2);
+// K34 and its exact fallback then read (x_new, xh).
+template <int MODE, bool XH, bool GS = false>
 static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                        float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes,
-                       hipStream_t st) {
+                       hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}) {
   if (k >= n) {
     const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
     profile_begin("topk_all", st);
@@ -2161,7 +2207,7 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
     CHOCO_LAUNCHED("topk_exact_kernel");
     return CHOCO_OK;
   }
-  if (MODE == kData && CHOCO_TOPK_FUSED && fused_fits(n)) {
+  if (MODE == kData && !GS && CHOCO_TOPK_FUSED && fused_fits(n)) {
     const FusedLayout F = fused_layout(n);
     CHOCO_REQUIRE(ws != nullptr && ws_bytes >= F.total, "top-k workspace too small: need %zu bytes, got %zu",
                   F.total, ws_bytes);
@@ -2205,13 +2251,14 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   }
   if (MODE == kData) {
     profile_begin("topk_bounds", st);
-    CHOCO_KLAUNCH((topk_bounds_kernel<XH>), dim3(1), dim3(kK1Threads), 0, st, x, xh, n, sample_ranks(n, k), ctrl);
+    CHOCO_KLAUNCH((topk_bounds_kernel<XH, GS>), dim3(1), dim3(kK1Threads), 0, st, x, xh, n, sample_ranks(n, k), ctrl,
+                  gs);
     profile_end("topk_bounds", st);
     CHOCO_LAUNCHED("topk_bounds_kernel");
   }
   profile_begin("topk_stream", st);
-  CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, L.tile,
-                L.side_cap, seed, hs_lo, hs_hi, ctrl, cum, cntw, side, cval, cidx);
+  CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH, GS>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, L.tile,
+                L.side_cap, seed, hs_lo, hs_hi, ctrl, cum, cntw, side, cval, cidx, gs);
   profile_end("topk_stream", st);
   CHOCO_LAUNCHED("topk_stream_kernel");
   profile_begin("topk_finish", st);
@@ -2225,19 +2272,31 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
 template <int MODE>
 static int dispatch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                          float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes,
-                         hipStream_t st) {
+                         hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}) {
   CHOCO_REQUIRE(x != nullptr && out_val != nullptr && out_idx != nullptr, "null pointer argument");
   CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n must be in [1, 2^31-1), got %lld", (long long)n);
   CHOCO_REQUIRE(k >= 1 && k <= n, "k must be in [1, n], got k=%lld n=%lld", (long long)k, (long long)n);
   CHOCO_REQUIRE(aligned4(x) && (xh == nullptr || aligned4(xh)), "x/xhat must be 4-byte aligned");
+  if (gs.mem) {
+    CHOCO_REQUIRE(xh != nullptr && aligned4(gs.mem), "the gossip step needs x_hat and a 4-byte aligned memory");
+    if (MODE == kData && k < n && n > kSmallN)
+      return launch_topk<kData, true, true>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st,
+                                            gs);
+    // no full stream pass to fuse into (random-k gathers k elements; small n and
+    // k == n are one-workgroup / copy paths): the standalone step, then the codec
+    const int rc = gossip_launch(const_cast<float*>(x), gs.mem, xh, gs.gamma, n, st);
+    if (rc) return rc;
+  }
   if (xh) return launch_topk<MODE, true>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st);
   return launch_topk<MODE, false>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st);
 }
 
 int topk_pipeline(int mode, const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
-                  float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes, hipStream_t st) {
-  if (mode == kHash) return dispatch_topk<kHash>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st);
-  return dispatch_topk<kData>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st);
+                  float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes, hipStream_t st,
+                  Gossip gs) {
+  if (mode == kHash)
+    return dispatch_topk<kHash>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st, gs);
+  return dispatch_topk<kData>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st, gs);
 }
 
 }  // namespace choco
@@ -2257,6 +2316,14 @@ CHOCO_API size_t choco_randk_workspace_size(int64_t n) { return topk_ws_bytes(n)
 CHOCO_API int choco_topk_compress(const float* x, const float* xhat, int64_t n, int64_t k, float* out_val,
                                   int32_t* out_idx, void* ws, size_t ws_bytes, void* stream) {
   return dispatch_topk<kData>(x, xhat, n, k, 0, 1.0f, out_val, out_idx, 0, ws, ws_bytes, as_stream(stream));
+}
+
+CHOCO_API int choco_gossip_topk_compress(float* x, const float* memory, const float* xhat, float gamma, int64_t n,
+                                         int64_t k, float* out_val, int32_t* out_idx, void* ws, size_t ws_bytes,
+                                         void* stream) {
+  CHOCO_REQUIRE(memory != nullptr && xhat != nullptr, "the gossip step needs memory and x_hat");
+  return dispatch_topk<kData>(x, xhat, n, k, 0, 1.0f, out_val, out_idx, 0, ws, ws_bytes, as_stream(stream),
+                              Gossip{memory, gamma});
 }
 
 CHOCO_API int choco_randk_compress(const float* x, const float* xhat, int64_t n, int64_t k, uint64_t seed,
@@ -2287,7 +2354,8 @@ CHOCO_API int choco_dbg_stream_only(const float* x, int64_t n, int64_t k, void* 
                        L.tile, L.side_cap, (uint64_t)0, 0u, (uint64_t)0, ctrl,
                        reinterpret_cast<uint32_t*>(base + L.off_cum),
                        reinterpret_cast<uint32_t*>(base + L.off_cntw), reinterpret_cast<uint32_t*>(base + L.off_side),
-                       reinterpret_cast<float*>(base + L.off_cval), reinterpret_cast<uint32_t*>(base + L.off_cidx));
+                       reinterpret_cast<float*>(base + L.off_cval), reinterpret_cast<uint32_t*>(base + L.off_cidx),
+                       Gossip{nullptr, 0.f});
   CHOCO_HIP(hipEventRecord(b, st));
   CHOCO_HIP(hipEventSynchronize(b));
   float ms = 0.f;

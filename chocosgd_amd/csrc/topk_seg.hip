@@ -124,6 +124,31 @@ CHOCO_DEV void tile_load(const float* __restrict__ x, const float* __restrict__ 
   }
 }
 
+// S1 with the fused gossip step: x, memory and xh of the tile in flight
+// together, x_new = x + gamma (memory - xh) stored back (the buffer resources
+// end at the tile: nothing past it is read or written), v = x_new - xh.
+CHOCO_DEV void tile_load_gossip(const float* __restrict__ x, const float* __restrict__ xh, const Gossip& gs,
+                                const TileCtx& c, float (&v)[kSegRows][4]) {
+  const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x + c.start, (uint32_t)c.tl * 4u);
+  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(xh + c.start, (uint32_t)c.tl * 4u);
+  const __amdgpu_buffer_rsrc_t rm = buf_rsrc(gs.mem + c.start, (uint32_t)c.tl * 4u);
+  float4 a[kSegRows], h[kSegRows], m[kSegRows];
+#pragma unroll
+  for (int r = 0; r < kSegRows; ++r) {
+    const uint32_t off = (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u;
+    a[r] = ld_buf4<true>(rx, off);
+    m[r] = ld_buf4<true>(rm, off);
+    h[r] = ld_buf4<false>(rh, off);  // S2 re-reads xh (and x_new): keep them in the Infinity Cache
+  }
+#pragma unroll
+  for (int r = 0; r < kSegRows; ++r) {
+    const uint32_t off = (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u;
+    const float4 xn = gossip4(a[r], m[r], h[r], gs.gamma);
+    st_buf4<false>(rx, off, xn);
+    v[r][0] = xn.x - h[r].x; v[r][1] = xn.y - h[r].y; v[r][2] = xn.z - h[r].z; v[r][3] = xn.w - h[r].w;
+  }
+}
+
 CHOCO_DEV int tile_elem(int r, int q) { return r * 4 * kSegThreads + 4 * (int)threadIdx.x + q; }
 
 template <int MODE>
@@ -149,15 +174,18 @@ CHOCO_DEV void block_find_rank2k(uint32_t h0, uint32_t h1, uint32_t rank, uint32
 }
 
 // ---------------------------------------------------------------- S1: coarse histogram
-template <int MODE, bool XH>
+template <int MODE, bool XH, bool GS = false>
 __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ xh,
                                                                const int64_t* __restrict__ plan, int nseg,
-                                                               uint64_t seed, uint32_t* __restrict__ hist1) {
+                                                               uint64_t seed, uint32_t* __restrict__ hist1,
+                                                               Gossip gs) {
+  static_assert(!GS || (MODE == kData && XH), "the gossip step needs x_hat and data keys");
   __shared__ uint32_t h[kH];
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
   float v[kSegRows][4] = {};
-  if (MODE == kData) tile_load<XH>(x, xh, c, v);
+  if (GS) tile_load_gossip(x, xh, gs, c, v);
+  else if (MODE == kData) tile_load<XH>(x, xh, c, v);
   for (int i = threadIdx.x; i < kH; i += kSegThreads) h[i] = 0u;
   __syncthreads();
   const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
@@ -361,15 +389,15 @@ __global__ __launch_bounds__(kSegThreads) void seg_emit_kernel(
 static int64_t plan_tiles(const int64_t* plan_host) { return plan_host[6]; }
 static int64_t plan_batched(const int64_t* plan_host) { return plan_host[7]; }
 
-template <int MODE, bool XH>
+template <int MODE, bool XH, bool GS = false>
 static int launch_batched(const float* x, const float* xh, const int64_t* plan_dev, const int64_t* plan_host,
                           int nseg, uint64_t seed, int32_t is_biased, float* out_val, int32_t* out_idx,
-                          const SegWs& W, hipStream_t st) {
+                          const SegWs& W, hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}) {
   const unsigned ntile = (unsigned)plan_tiles(plan_host);
   const unsigned nbat = (unsigned)plan_batched(plan_host);
   profile_begin("topk_seg_hist", st);
-  CHOCO_KLAUNCH((seg_hist_kernel<MODE, XH>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg, seed,
-                W.hist1);
+  CHOCO_KLAUNCH((seg_hist_kernel<MODE, XH, GS>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg, seed,
+                W.hist1, gs);
   profile_end("topk_seg_hist", st);
   CHOCO_LAUNCHED("seg_hist_kernel");
   profile_begin("topk_seg_collect", st);
@@ -399,14 +427,25 @@ static size_t pipeline_ws(const int64_t* plan_host, int nseg) {
   return need;
 }
 
+// gs.mem != nullptr: the fused gossip step (top-k: inside S1 and the flat
+// pipeline's stream; random-k, which reads only k elements: the standalone step
+// over the whole buffer first).
 template <int MODE>
 static int segmented(const float* x, const float* xhat, const int64_t* plan_dev, const int64_t* plan_host,
                      int32_t nseg, uint64_t seed, int32_t is_biased, float* out_val, int32_t* out_idx, void* ws,
-                     size_t ws_bytes, hipStream_t st) {
+                     size_t ws_bytes, hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}) {
   CHOCO_REQUIRE(x && plan_dev && plan_host && out_val && out_idx && nseg > 0, "null pointer argument");
   CHOCO_REQUIRE(aligned4(x) && (xhat == nullptr || aligned4(xhat)), "x/xhat must be 4-byte aligned");
   const int64_t* last = plan_host + (int64_t)kRow * (nseg - 1);
   CHOCO_REQUIRE(last[0] + last[1] < (int64_t)INT32_MAX, "total length must be < 2^31");
+  if (gs.mem) {
+    CHOCO_REQUIRE(xhat != nullptr && aligned4(gs.mem), "the gossip step needs x_hat and a 4-byte aligned memory");
+    if (MODE == kHash) {
+      const int rc = gossip_launch(const_cast<float*>(x), gs.mem, xhat, gs.gamma, last[0] + last[1], st);
+      if (rc) return rc;
+      gs.mem = nullptr;
+    }
+  }
   const int64_t ntile = plan_tiles(plan_host);
   const SegLayout L = seg_layout(nseg, ntile);
   const size_t need = L.total + pipeline_ws(plan_host, nseg);
@@ -418,10 +457,14 @@ static int segmented(const float* x, const float* xhat, const int64_t* plan_dev,
             reinterpret_cast<uint32_t*>(base + L.off_info), reinterpret_cast<uint32_t*>(base + L.off_cnt),
             reinterpret_cast<uint32_t*>(base + L.off_out), reinterpret_cast<float*>(base + L.off_cval),
             reinterpret_cast<uint32_t*>(base + L.off_cidx)};
-    const int rc = xhat ? launch_batched<MODE, true>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val,
-                                                     out_idx, W, st)
-                        : launch_batched<MODE, false>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val,
-                                                      out_idx, W, st);
+    int rc;
+    if (MODE == kData && gs.mem)
+      rc = launch_batched<kData, true, true>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, W,
+                                             st, gs);
+    else if (xhat)
+      rc = launch_batched<MODE, true>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, W, st);
+    else
+      rc = launch_batched<MODE, false>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, W, st);
     if (rc) return rc;
   }
   // segments over kSegBatchMax elements: the flat pipeline, one after another
@@ -431,8 +474,9 @@ static int segmented(const float* x, const float* xhat, const int64_t* plan_dev,
     if (p[5] != 0) continue;
     const uint64_t sd = MODE == kHash ? seg_seed(seed, s) : 0;
     const float scale = (MODE == kHash && !is_biased) ? (float)((double)p[1] / (double)p[2]) : 1.0f;
+    const Gossip gseg{gs.mem ? gs.mem + p[0] : nullptr, gs.gamma};
     const int rc = topk_pipeline(MODE, x + p[0], xhat ? xhat + p[0] : nullptr, p[1], p[2], sd, scale,
-                                 out_val + p[3], out_idx + p[3], p[0], base + L.total, ws_bytes - L.total, st);
+                                 out_val + p[3], out_idx + p[3], p[0], base + L.total, ws_bytes - L.total, st, gseg);
     if (rc) return rc;
   }
   return CHOCO_OK;
@@ -509,4 +553,22 @@ CHOCO_API int choco_randk_compress_segmented(const float* x, const float* xhat, 
                                              size_t ws_bytes, void* stream) {
   return segmented<kHash>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, ws, ws_bytes,
                           as_stream(stream));
+}
+
+CHOCO_API int choco_gossip_topk_compress_segmented(float* x, const float* memory, const float* xhat, float gamma,
+                                                   const int64_t* plan_dev, const int64_t* plan_host, int32_t nseg,
+                                                   float* out_val, int32_t* out_idx, void* ws, size_t ws_bytes,
+                                                   void* stream) {
+  CHOCO_REQUIRE(memory != nullptr && xhat != nullptr, "the gossip step needs memory and x_hat");
+  return segmented<kData>(x, xhat, plan_dev, plan_host, nseg, 0, 1, out_val, out_idx, ws, ws_bytes,
+                          as_stream(stream), Gossip{memory, gamma});
+}
+
+CHOCO_API int choco_gossip_randk_compress_segmented(float* x, const float* memory, const float* xhat, float gamma,
+                                                    const int64_t* plan_dev, const int64_t* plan_host, int32_t nseg,
+                                                    uint64_t seed, int32_t is_biased, float* out_val,
+                                                    int32_t* out_idx, void* ws, size_t ws_bytes, void* stream) {
+  CHOCO_REQUIRE(memory != nullptr && xhat != nullptr, "the gossip step needs memory and x_hat");
+  return segmented<kHash>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, ws, ws_bytes,
+                          as_stream(stream), Gossip{memory, gamma});
 }

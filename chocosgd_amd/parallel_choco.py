@@ -17,7 +17,11 @@ What changes underneath:
     QSGD = [fp32 norms | level plane | sign plane]; sign = [fp32 norms | packed
     words] in ONE message (the reference sends norms and signs separately);
   * uncompress applies all neighbour messages with fused kernels in
-    `neighbors_info` order, reproducing the reference's fp32 rounding sequence.
+    `neighbors_info` order, reproducing the reference's fp32 rounding sequence;
+  * optional input key `gossip` = (memory buffer, consensus_stepsize): compress
+    first applies ParallelCHOCO_V.step's update_params_from_neighbor
+    (optim/utils.py:67-72) to `flatten_params` inside its own first pass
+    (utils.fused_step drives it; include/choco_codec.h "fused gossip step").
 """
 import torch
 
@@ -127,6 +131,11 @@ class _CHOCOBase(object):
             raise RuntimeError("original_shapes do not match flatten_params")
         return x, xh, lay
 
+    @staticmethod
+    def _gossip(sync_buffer):
+        g = sync_buffer.get("gossip")
+        return None if g is None else (g[0], float(g[1]))
+
     def _send(self, sync_buffer, message):
         if self.comm_device == "cpu":
             message = message.cpu().pin_memory()
@@ -158,11 +167,12 @@ class CHOCOSparsificationCompressor(_CHOCOBase):
         K = plan.k_total
         message = torch.empty(2 * K, dtype=torch.int32, device=x.device)
         values, indices = message[:K].view(torch.float32), message[K:]
+        g = self._gossip(sync_buffer)
         if "top_k" in self.comm_op:
-            codec.topk_segmented(x, plan, xhat=xh, out=(values, indices))
+            codec.topk_segmented(x, plan, xhat=xh, out=(values, indices), gossip=g)
         elif "random_k" in self.comm_op:
             # the reference never forwards is_biased to get_random_k (sparsification.py:60)
-            codec.randk_segmented(x, plan, _draw_seed(), is_biased=True, xhat=xh, out=(values, indices))
+            codec.randk_segmented(x, plan, _draw_seed(), is_biased=True, xhat=xh, out=(values, indices), gossip=g)
         else:
             raise NotImplementedError
         selected_shapes = list(plan.k_per_seg)
@@ -211,11 +221,14 @@ class CHOCOQuantizationCompressor(_CHOCOBase):
         x, xh, lay = self._flat_inputs(sync_buffer)
         q = int(self.quantize_level)
         hw = _hdr_words(lay.nseg)
+        g = self._gossip(sync_buffer)
         if q == 32:  # the reference sends the raw delta (sparsification.py:118-119)
+            if g is not None:
+                codec.gossip_step(x, g[0], xh, g[1])
             message = torch.sub(x, xh).view(torch.uint8)
         else:
             packed, norms, _ = codec.qsgd_compress(x, q, is_biased=self.is_biased, xhat=xh, seg_off=lay.seg_off,
-                                                   nseg=lay.nseg, seed=_draw_seed())
+                                                   nseg=lay.nseg, seed=_draw_seed(), gossip=g)
             header = torch.zeros(hw, dtype=torch.float32, device=x.device)
             header[:lay.nseg] = norms
             message = torch.cat([header.view(torch.uint8), packed])
@@ -258,7 +271,8 @@ class CHOCOSignCompressor(_CHOCOBase):
 
     def compress(self, sync_buffer):
         x, xh, lay = self._flat_inputs(sync_buffer)
-        signs, norms = codec.sign_compress(x, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg, want_norms=True)
+        signs, norms = codec.sign_compress(x, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg, want_norms=True,
+                                           gossip=self._gossip(sync_buffer))
         sync_buffer["flatten_norms"] = TensorBuffer.from_flat(norms, [() for _ in range(lay.nseg)])
         sync_buffer["flatten_directions"] = None  # the delta is never materialised (fused)
         sync_buffer["signs"] = signs

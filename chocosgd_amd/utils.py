@@ -22,6 +22,23 @@ def recover_params(param_groups, param_names, rank=None, neighbor_hat_params=Non
     return params, flatten_params
 
 
+def fused_step(compressor, param_groups, param_names, shapes, neighbor_hat_params, neighbors_info,
+               consensus_stepsize, rank):
+    """ParallelCHOCO_V.step after apply_gradient (parallel_choco_v.py:115-155), with the
+    consensus step fused into the compressor's first pass: recover_params, then
+    compress (x += gamma * (memory - x_hat_i) and d = x_new - x_hat_i in one pass), sync,
+    uncompress, and the updated x unpacked into the model.  Returns the sync_buffer.
+    The reference runs update_params_from_neighbor as its own pass before compress."""
+    params, flatten_params, flatten_hat_params = recover_params(param_groups, param_names, rank,
+                                                                neighbor_hat_params, get_hat_params=True)
+    sync_buffer = {"original_shapes": shapes, "flatten_params": flatten_params,
+                   "flatten_hat_params": flatten_hat_params,
+                   "gossip": (neighbor_hat_params["memory"].buffer, consensus_stepsize)}
+    compressor.pipeline(sync_buffer, neighbor_hat_params, neighbors_info)
+    flatten_params.unpack(params)
+    return sync_buffer
+
+
 def update_params_from_neighbor(neighbor_hat_params, flatten_params, consensus_stepsize, self_rank):
     """optim/utils.py:67-72:  x += gamma * (memory - x_hat_i), one fused HIP pass."""
     codec.gossip_step(flatten_params.buffer, neighbor_hat_params["memory"].buffer,

@@ -217,6 +217,39 @@ int choco_qsgd_decompress_accumulate(const uint8_t* const* packed_list,
 int choco_gossip_step(float* x, const float* memory, const float* xhat, float gamma,
                       int64_t n, void* stream);
 
+/* ------------------------------------------- fused gossip step + compress
+ * ParallelCHOCO_V.step's update_params_from_neighbor -> compress sequence
+ * (pcode/optim/parallel_choco_v.py:116-142 -> :229-240, optim/utils.py:67-72) in
+ * the codec's own passes: the FIRST full pass of the compressor reads x, memory
+ * and xhat, writes x_new = x + (float)gamma * (memory - xhat) back into x (bit-
+ * identical to choco_gossip_step) and compresses d = x_new - xhat, so the step
+ * costs one pass of 12 B read + 4 B written per element less than
+ * choco_gossip_step followed by the compressor.  Outputs, workspaces, plans and
+ * alignment rules are those of the matching non-gossip entry point.  Paths with
+ * no full first pass (random-k, which gathers k elements; pinned-norm QSGD; tiny
+ * or k == n top-k) run choco_gossip_step first. */
+int choco_gossip_topk_compress(float* x, const float* memory, const float* xhat, float gamma,
+                               int64_t n, int64_t k, float* out_val, int32_t* out_idx,
+                               void* ws, size_t ws_bytes, void* stream);
+int choco_gossip_topk_compress_segmented(float* x, const float* memory, const float* xhat, float gamma,
+                                         const int64_t* plan_dev, const int64_t* plan_host, int32_t nseg,
+                                         float* out_val, int32_t* out_idx,
+                                         void* ws, size_t ws_bytes, void* stream);
+int choco_gossip_randk_compress_segmented(float* x, const float* memory, const float* xhat, float gamma,
+                                          const int64_t* plan_dev, const int64_t* plan_host, int32_t nseg,
+                                          uint64_t seed, int32_t is_biased,
+                                          float* out_val, int32_t* out_idx,
+                                          void* ws, size_t ws_bytes, void* stream);
+int choco_gossip_sign_compress(float* x, const float* memory, const float* xhat, float gamma,
+                               int64_t n, const int64_t* seg_off, int32_t nseg,
+                               int32_t* packed, float* l1_norms,
+                               void* ws, size_t ws_bytes, void* stream);
+int choco_gossip_qsgd_compress(float* x, const float* memory, const float* xhat, float gamma,
+                               int64_t n, const int64_t* seg_off, int32_t nseg,
+                               int32_t q, int32_t is_biased, uint64_t seed, uint64_t offset,
+                               uint8_t* packed, float* norms_out, float* dense_out,
+                               void* ws, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------- profiling hooks
  * Optional: when enabled, the dominant kernel of each op is launched with a
  * pair of hipEvents attached to the dispatch itself (hipExtLaunchKernelGGL), so

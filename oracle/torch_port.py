@@ -89,3 +89,9 @@ def sign_decompress(hat, mem, words, norm, n, weight):
     if hat is not None:
         hat.add_(upd)
     mem.add_(upd, alpha=weight)
+
+
+def gossip_step(x, mem, hat, gamma):
+    """optim/utils.py:70-72 (update_params_from_neighbor), as torch ops."""
+    x.add_(gamma * (mem - hat))
+    return x

@@ -16,7 +16,7 @@ therefore pin the wrapper semantics (sign, pad-to-32, (32, N') split, decode
 rule, per-tensor L1 norms, accumulate), while the bit position inside a word
 is this repo's convention ("parity unpinned" at that one boundary).
 
-Usage:  python tests/golden/gen_golden.py
+Usage:  python tests/golden/gen_golden.py [generator ...]   (no argument: all)
 """
 import json
 import os
@@ -329,6 +329,47 @@ def gen_choco(kind, name, layout, comm_op, **kw):
     save(name, **arrays)
 
 
+def gen_choco_step(kind, name, layout, comm_op, **kw):
+    """ParallelCHOCO_V.step after apply_gradient (parallel_choco_v.py:116-155) for a ring
+    of 3: every worker r runs update_params_from_neighbor (optim/utils.py:67-72) on its
+    own x_r, x_hat_r, memory_r, then compress + sync; worker 1 replays the three
+    messages through uncompress.  Pins the fused gossip + compress entry points."""
+    cls = {"topk": ref_pcv.CHOCOSparsificationCompressor,
+           "sign": ref_pcv.CHOCOSignCompressor}[kind]
+    n = sum(layout)
+    shapes = [(torch.Size([m]), m) for m in layout]
+    W, self_rank, gamma = 3, 1, 0.9
+    neighbors_info = {0: 1.0 / 3, 1: 1.0 / 3, 2: 1.0 / 3}
+    xs = [randn(n, 1500 + 10 * r) for r in range(W)]
+    hats = [xs[r] + randn(n, 1501 + 10 * r, 0.1) for r in range(W)]
+    mems = [hats[r] + randn(n, 1502 + 10 * r, 0.05) for r in range(W)]
+    sent, sbs, x_after = [], [], []
+    for r in range(W):
+        comp = make_comp(cls, comm_op, **kw)
+        nhp = {r: TensorBuffer(split(hats[r], layout)), "memory": TensorBuffer(split(mems[r], layout))}
+        fp = TensorBuffer(split(xs[r], layout))
+        ref_ou.update_params_from_neighbor(nhp, fp, gamma, r)
+        x_after.append(fp.buffer.clone())
+        sb = {"original_shapes": shapes, "flatten_params": fp,
+              "flatten_hat_params": TensorBuffer(split(hats[r], layout))}
+        comp.compress(sb)
+        comp.aggregator_fn = CaptureAgg()
+        comp.sync(sb)
+        sent.append(comp.aggregator_fn.sent)
+        sbs.append((comp, sb, nhp))
+    comp, sb, nhp = sbs[self_rank]
+    ncalls = len(sent[0])
+    comp.aggregator_fn = ReplayAgg([{r: sent[r][c] for r in range(W)} for c in range(ncalls)])
+    comp.sync(sb)
+    comp.uncompress(sb, nhp, neighbors_info)
+    save(name, layout=np.array(layout, dtype=np.int64), gamma=np.float64(gamma),
+         x=np.stack([x.numpy() for x in xs]), xhat=np.stack([h.numpy() for h in hats]),
+         mem=np.stack([m.numpy() for m in mems]), x_after_gossip=np.stack([x.numpy() for x in x_after]),
+         hat1=nhp[self_rank].buffer.numpy(), mem1=nhp["memory"].buffer.numpy(),
+         weights=np.array([neighbors_info[r] for r in range(W)]), self_rank=np.int64(self_rank),
+         n_bits=np.float64(sb["n_bits"]))
+
+
 def gen_gossip():
     x, mem, hat = randn(10007, 61), randn(10007, 62), randn(10007, 63)
     fp = TensorBuffer([x.clone()])
@@ -354,8 +395,20 @@ def gen_layouts():
     print("wrote layouts.json", {k: (len(v), sum(v)) for k, v in res.items()})
 
 
+STEP_LAYOUT = MINI_LAYOUT + [1029, 3]
+
+
+def gen_choco_steps():
+    gen_choco_step("topk", "choco_step_topk_r099", STEP_LAYOUT, "compress_top_k", ratio=0.99)
+    gen_choco_step("sign", "choco_step_sign", STEP_LAYOUT, "sign")
+
+
 if __name__ == "__main__":
     torch.set_num_threads(min(8, os.cpu_count() or 1))
+    if len(sys.argv) > 1:  # only the named generators, e.g. gen_choco_steps
+        for nm in sys.argv[1:]:
+            globals()[nm]()
+        sys.exit(0)
     gen_k_table()
     gen_topk()
     gen_randk()
@@ -366,4 +419,5 @@ if __name__ == "__main__":
     gen_choco("qsgd", "choco_qsgd_mini_q4", MINI_LAYOUT, "quantize_qsgd", qlevel=4)
     gen_choco("sign", "choco_sign_mini", MINI_LAYOUT, "sign")
     gen_gossip()
+    gen_choco_steps()
     gen_layouts()

@@ -181,6 +181,33 @@ def test_gossip_step():
     assert same_bits(O.gossip_step(x, g2["mem1"], g2["hat1"], g2["gamma"]), g2["x_after_gossip"])
 
 
+@pytest.mark.parametrize("name", ["choco_step_topk_r099", "choco_step_sign"])
+def test_choco_step_fixture(name):
+    """ParallelCHOCO_V.step (consensus step, then compress, ring of 3, receiver 1) as the
+    reference ran it: the oracle's gossip step is bit-exact for every worker, and the
+    oracle's codec on d = x_after - x_hat reproduces the receiver's x_hat / memory."""
+    g = golden(name)
+    lens = g["layout"].tolist()
+    s = int(g["self_rank"])
+    ds = []
+    for r in range(3):
+        xa = O.gossip_step(g["x"][r], g["mem"][r], g["xhat"][r], g["gamma"])
+        assert same_bits(xa, g["x_after_gossip"][r])
+        ds.append((xa - g["xhat"][r]).astype(np.float32))
+    hat, mem = g["xhat"][s].copy(), g["mem"][s].copy()
+    if "topk" in name:
+        for r in range(3):
+            ov, oi, _ = O.topk_segmented(ds[r], lens, 0.99)
+            O.sparse_accumulate(hat if r == s else None, mem, ov, oi, g["weights"][r])
+        assert same_bits(hat, g["hat1"])
+        assert same_bits(mem, g["mem1"])
+    else:
+        msgs = [(O.sign_pack(d), O.l1_norms(d, lens)) for d in ds]
+        O.sign_accumulate(hat, mem, msgs, g["weights"], s, lens)
+        assert np.allclose(hat, g["hat1"], rtol=1e-5, atol=1e-6)
+        assert np.allclose(mem, g["mem1"], rtol=1e-5, atol=1e-6)
+
+
 def test_splitmix64_known_answer():
     # the first outputs of the splitmix64 generator from state 0 (Vigna's reference
     # implementation: state += gamma; return mix(state))

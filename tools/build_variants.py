@@ -17,6 +17,10 @@ VARIANTS = {
     "sign_acc1": ["CHOCO_SIGN_ACC1=1"],
     "fused": ["CHOCO_TOPK_FUSED=1"],
     "fused_stamps": ["CHOCO_TOPK_FUSED=1", "CHOCO_STAMPS=1"],
+    "g_form0": ["CHOCO_GOSSIP_FORM=0"],
+    "gs_st_plain": ["CHOCO_GS_STORE_NT=0"],
+    "sgs_ru4": ["CHOCO_SIGN_GS_RU=4"],
+    "sgs_split": ["CHOCO_SIGN_GS_FUSE=0"],
 }
 
 
