@@ -42,6 +42,12 @@ SIGNATURES = {
     "choco_sign_unpack": (_c_i32, [_vp, _c_i64, _vp, _vp]),
     "choco_sign_decompress_accumulate": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i32, _c_i64, _vp, _c_i32,
                                                   _vp, _vp, _vp, _c_sz, _vp]),
+    "choco_sign_decompress_axpy": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i64, _vp, _c_i32, _c_i32, _vp, _vp]),
+    "choco_sign_decompress_extrapolate": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _c_f32, _c_f32, _vp, _vp]),
+    "choco_qsgd_decompress_extrapolate": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _c_i32, _c_i32, _c_f32, _c_f32,
+                                                   _vp, _vp]),
+    "choco_sparse_extrapolate": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i64, _c_f32, _c_f32, _vp, _vp]),
+    "choco_sign_local_decode": (_c_i32, [_vp, _c_i64, _vp, _c_i32, _vp, _vp, _vp]),
     "choco_qsgd_packed_bytes": (_c_i64, [_c_i64, _c_i32]),
     "choco_qsgd_workspace_size": (_c_sz, [_c_i32]),
     "choco_qsgd_compress": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _c_i32, _c_i32, _vp, _vp, _c_u64, _c_u64,

@@ -308,6 +308,19 @@ def sparse_accumulate(values, indices, memory, weight, xhat_self=None, guard=Non
                "choco_sparse_accumulate")
 
 
+def sparse_extrapolate(values, indices, target, a, b, guard=None):
+    """target[idx] = fmaf(b, v, target[idx] * a): ECD's replica update (ecd_psgd.py:299-303)."""
+    _require(values, torch.float32, "values")
+    _require(indices, torch.int32, "indices")
+    _require(target, torch.float32, "target")
+    if indices.numel() != values.numel():
+        raise RuntimeError("values and indices must have the same length")
+    _lib.check(lib().choco_sparse_extrapolate(_ptr(values), _ptr(indices), values.numel(), _ptr(target),
+                                              target.numel(), float(a), float(b),
+                                              _ptr(guard.word) if guard is not None else ctypes.c_void_p(0),
+                                              _stream(target.device)), "choco_sparse_extrapolate")
+
+
 # ----------------------------------------------------------------------------- sign
 def sign_words(n):
     return int(lib().choco_sign_words(int(n)))
@@ -397,6 +410,51 @@ def sign_accumulate(messages, weights, self_slot, n, memory, xhat_self=None, seg
                    "choco_sign_decompress_accumulate")
 
 
+def sign_axpy(messages, weights, n, target, seg_off=None, nseg=1, two_roundings=False):
+    """target += w_m * decode(m) for each (packed, norms) message in order -- the receiver of
+    the DCD / DeepSqueeze sign compressors; `two_roundings` selects torch's add_(w * u)
+    over add_(u, alpha=w) (include/choco_codec.h)."""
+    _require(target, torch.float32, "target")
+    _check_layout(target, None, n, seg_off, nseg)
+    if len(messages) != len(weights):
+        raise RuntimeError("one weight per message")
+    words = sign_words(n)
+    for p, nm in messages:
+        _require(p, torch.int32, "packed")
+        _require(nm, torch.float32, "norms")
+        if p.numel() != words or nm.numel() != nseg:
+            raise RuntimeError(f"sign message must hold {words} words and {nseg} norms")
+    for c0, c1, _ in _msg_chunks(len(messages), -1):
+        part = messages[c0:c1]
+        pp, keep1 = _lib.ptr_array([p.data_ptr() for p, _ in part])
+        nn, keep2 = _lib.ptr_array([nm.data_ptr() for _, nm in part])
+        ww, keep3 = _lib.f32_array([float(w) for w in weights[c0:c1]])
+        _lib.check(lib().choco_sign_decompress_axpy(pp, nn, ww, len(part), int(n), _ptr(seg_off), int(nseg),
+                                                    1 if two_roundings else 0, _ptr(target),
+                                                    _stream(target.device)), "choco_sign_decompress_axpy")
+
+
+def sign_extrapolate(packed, norms, n, target, a, b, seg_off=None, nseg=1):
+    """target_s = target_s * a + ((b * norm_s) / numel_s) * sign: ECD (ecd_psgd.py:448-454)."""
+    _require(packed, torch.int32, "packed")
+    _require(norms, torch.float32, "norms")
+    _require(target, torch.float32, "target")
+    _check_layout(target, None, n, seg_off, nseg)
+    _lib.check(lib().choco_sign_decompress_extrapolate(_ptr(packed), _ptr(norms), int(n), _ptr(seg_off), int(nseg),
+                                                       float(a), float(b), _ptr(target), _stream(target.device)),
+               "choco_sign_decompress_extrapolate")
+
+
+def sign_local_decode(x, norms, seg_off=None, nseg=1):
+    """(norm_s * torch.sign(x)) / numel_s: DeepSqueeze's local copy of its sign message."""
+    _require(x, torch.float32, "x")
+    _require(norms, torch.float32, "norms")
+    out = torch.empty_like(x)
+    _lib.check(lib().choco_sign_local_decode(_ptr(x), x.numel(), _ptr(seg_off), int(nseg), _ptr(norms), _ptr(out),
+                                             _stream(x.device)), "choco_sign_local_decode")
+    return out
+
+
 # ----------------------------------------------------------------------------- QSGD
 def qsgd_packed_bytes(n, q):
     return int(lib().choco_qsgd_packed_bytes(int(n), int(q)))
@@ -475,6 +533,18 @@ def qsgd_accumulate(messages, weights, self_slot, n, q, memory, xhat_self=None, 
                                                           _ptr(xhat_self if slot >= 0 else None), _ptr(memory),
                                                           _stream(memory.device)),
                    "choco_qsgd_decompress_accumulate")
+
+
+def qsgd_extrapolate(packed, norms, n, q, target, a, b, is_biased=False, seg_off=None, nseg=1):
+    """target = fmaf(b, decode(m), target * a): ECD (ecd_psgd.py:415-423)."""
+    _require(packed, torch.uint8, "packed")
+    _require(norms, torch.float32, "norms")
+    _require(target, torch.float32, "target")
+    _check_layout(target, None, n, seg_off, nseg)
+    _lib.check(lib().choco_qsgd_decompress_extrapolate(_ptr(packed), _ptr(norms), int(n), _ptr(seg_off), int(nseg),
+                                                       int(q), 1 if is_biased else 0, float(a), float(b),
+                                                       _ptr(target), _stream(target.device)),
+               "choco_qsgd_decompress_extrapolate")
 
 
 # ----------------------------------------------------------------------------- gossip

@@ -193,6 +193,23 @@ __global__ __launch_bounds__(kEwThreads) void gather_kernel(const float* __restr
   }
 }
 
+// ECDSparsificationCompressor.uncompress (ecd_psgd.py:299-303):
+//   target[idx] = target[idx].mul(a).add(b, v)  ->  fmaf(b, v, target[idx] * a)
+// (torch's vectorized add with alpha fuses).  Indices unique per message.
+__global__ __launch_bounds__(kEwThreads) void sparse_extrap_kernel(const float* __restrict__ val,
+                                                                   const int32_t* __restrict__ idx, int64_t k,
+                                                                   float* __restrict__ target, int64_t n, float a,
+                                                                   float b, uint32_t* __restrict__ bad) {
+  const int64_t i = (int64_t)blockIdx.x * kEwThreads + threadIdx.x;
+  if (i >= k) return;
+  const int64_t j = idx[i];
+  if (j < 0 || j >= n) {
+    if (bad) atomicAdd(bad, 1u);
+    return;
+  }
+  target[j] = fmaf(b, val[i], target[j] * a);
+}
+
 static unsigned ew_grid(int64_t work, int per_thread) {
   int64_t g = (work + (int64_t)kEwThreads * per_thread - 1) / ((int64_t)kEwThreads * per_thread);
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 8192));
@@ -319,5 +336,19 @@ CHOCO_API int choco_gather(const float* x, const float* xhat, const int64_t* idx
   if (k <= 0) return CHOCO_OK;
   CHOCO_KLAUNCH(gather_kernel, dim3(ew_grid(k, 1)), dim3(kEwThreads), 0, st, x, xhat, idx, k, scale, out_val);
   CHOCO_LAUNCHED("gather_kernel");
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_sparse_extrapolate(const float* val, const int32_t* idx, int64_t k, float* target, int64_t n,
+                                       float a, float b, uint32_t* bad_count, void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(val && idx && target, "null pointer argument");
+  CHOCO_REQUIRE(n > 0, "n must be positive");
+  if (k <= 0) return CHOCO_OK;
+  profile_begin("sparse_accumulate", st);
+  CHOCO_KLAUNCH(sparse_extrap_kernel, dim3((unsigned)((k + kEwThreads - 1) / kEwThreads)), dim3(kEwThreads), 0, st,
+                val, idx, k, target, n, a, b, bad_count);
+  profile_end("sparse_accumulate", st);
+  CHOCO_LAUNCHED("sparse_extrap_kernel");
   return CHOCO_OK;
 }

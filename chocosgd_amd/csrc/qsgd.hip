@@ -398,6 +398,8 @@ struct QMsgs {
   float w[kQMaxMsg];
   int nmsg;
   int self_slot;
+  int extrap;  // 1: memory = fmaf(w, v, memory * a) (ECD, ecd_psgd.py:421-423)
+  float a;
 };
 
 CHOCO_DEV float qdecode(uint32_t level, bool neg, const QParam& P, float sf) {
@@ -461,8 +463,12 @@ __global__ __launch_bounds__(kQThreads) void qsgd_decode_kernel(QMsgs M, int64_t
         mv[c] = v;
       } else {
         if (has_self && q == M.self_slot) hv[c] = hv[c] + v;  // hat_params.buffer += q_values
-        const float wv = M.w[q] * v;                        // weight * q_values (rounded)
-        mv[c] = mv[c] + wv;                                  // memory += ...
+        if (M.extrap) {
+          mv[c] = fmaf(M.w[q], v, mv[c] * M.a);  // hat.mul_(a).add_(q, alpha=b)
+        } else {
+          const float wv = M.w[q] * v;                        // weight * q_values (rounded)
+          mv[c] = mv[c] + wv;                                  // memory += ...
+        }
       }
     }
   }
@@ -660,6 +666,32 @@ CHOCO_API int choco_qsgd_decompress_accumulate(const uint8_t* const* packed_list
   M.self_slot = self_slot;
   profile_begin("qsgd_accumulate", st);
   launch_decode_cw<1>(cw, M, n, seg_off, nseg, (1 << q) - 1, is_biased, xhat_self, memory, st);
+  profile_end("qsgd_accumulate", st);
+  CHOCO_LAUNCHED("qsgd_decode_kernel");
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_qsgd_decompress_extrapolate(const uint8_t* packed, const float* norms, int64_t n,
+                                                const int64_t* seg_off, int32_t nseg, int32_t q, int32_t is_biased,
+                                                float a, float b, float* target, void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(packed && norms && target, "null pointer argument");
+  CHOCO_REQUIRE(q >= 1 && q <= 16, "q must be in [1, 16]");
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
+  CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
+  CHOCO_REQUIRE(aligned16(packed) && aligned16(target), "buffers must be 16-byte aligned");
+  const int cw = container_bits(q);
+  QMsgs M{};
+  M.lvl[0] = packed;
+  M.sgn[0] = packed + plane_bytes(n, cw);
+  M.norms[0] = norms;
+  M.w[0] = b;
+  M.nmsg = 1;
+  M.self_slot = -1;
+  M.extrap = 1;
+  M.a = a;
+  profile_begin("qsgd_accumulate", st);
+  launch_decode_cw<1>(cw, M, n, seg_off, nseg, (1 << q) - 1, is_biased, nullptr, target, st);
   profile_end("qsgd_accumulate", st);
   CHOCO_LAUNCHED("qsgd_decode_kernel");
   return CHOCO_OK;

@@ -512,7 +512,17 @@ struct SignMsgs {
   float w[kMaxMsg];
   int nmsg;
   int self_slot;
+  // memory update: 0 = fmaf(w, u, memory) (torch add_(u, alpha=w)); 1 = memory + (w * u)
+  // (add_(w * u)); 2 = (memory * a) + u with u = ((b * norm) / numel) * sign (ECD's
+  // extrapolation, ecd_psgd.py:448-454; w unused)
+  int mode;
+  float a, b;
 };
+
+CHOCO_DEV float sign_axpy(const SignMsgs& M, int q, float u, float m) {
+  if (M.mode == 2) return m * M.a + u;
+  return M.mode == 1 ? m + M.w[q] * u : fmaf(M.w[q], u, m);
+}
 
 template <int NM>
 CHOCO_DEV void sign_apply(const SignMsgs& M, const float (&sc)[kMaxMsg], const uint32_t (&bits)[kMaxMsg],
@@ -521,14 +531,14 @@ CHOCO_DEV void sign_apply(const SignMsgs& M, const float (&sc)[kMaxMsg], const u
   for (int q = 0; q < NM; ++q) {
     const float u = ((bits[q] >> shiftbit) & 1u) ? -sc[q] : sc[q];  // (norm/numel) * (+-1), exact
     if (q == M.self_slot) h = h + u;
-    mm = fmaf(M.w[q], u, mm);  // torch add_(u, alpha=w) fuses on CPU (verified)
+    mm = sign_axpy(M, q, u, mm);  // torch add_(u, alpha=w) fuses on CPU (verified)
   }
 }
 
-CHOCO_DEV float seg_scale(const float* __restrict__ norms, const int64_t* __restrict__ seg_off, int64_t n,
-                          int seg) {
+CHOCO_DEV float seg_scale(const SignMsgs& M, int q, const int64_t* __restrict__ seg_off, int64_t n, int seg) {
   const int64_t numel = seg_off ? seg_off[seg + 1] - seg_off[seg] : n;
-  return norms[seg] / (float)numel;
+  const float nm = M.mode == 2 ? M.b * M.norms[q][seg] : M.norms[q][seg];
+  return nm / (float)numel;
 }
 
 template <int NM, bool HS>
@@ -548,7 +558,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
   // loads of the scales happen here, before the streaming loop
   if (threadIdx.x < NM * 32) {
     const int q = threadIdx.x >> 5, r = threadIdx.x & 31;
-    s_sc[q][r] = (s_lo[r] >= 0 && s_lo[r] == s_hi[r]) ? seg_scale(M.norms[q], seg_off, n, s_lo[r]) : 0.f;
+    s_sc[q][r] = (s_lo[r] >= 0 && s_lo[r] == s_hi[r]) ? seg_scale(M, q, seg_off, n, s_lo[r]) : 0.f;
   }
   __syncthreads();
   if (ncol == 0) return;
@@ -701,7 +711,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
         } else {
           const int sg = seg_walk(seg_off, nseg, s_lo[r], i);
 #pragma unroll
-          for (int q = 0; q < NM; ++q) scl[q] = seg_scale(M.norms[q], seg_off, n, sg);
+          for (int q = 0; q < NM; ++q) scl[q] = seg_scale(M, q, seg_off, n, sg);
         }
         sign_apply<NM>(M, scl, x8, 4 + c - m, hv[c], mv[c]);
       }
@@ -735,7 +745,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
           } else {
             const int sg = seg_walk(seg_off, nseg, s_lo[r], i);
 #pragma unroll
-            for (int q = 0; q < NM; ++q) scl[q] = seg_scale(M.norms[q], seg_off, n, sg);
+            for (int q = 0; q < NM; ++q) scl[q] = seg_scale(M, q, seg_off, n, sg);
           }
           uint32_t own[kMaxMsg];
 #pragma unroll
@@ -803,7 +813,7 @@ __global__ __launch_bounds__(64 * kSA1Waves) void sign_accumulate1_kernel(SignMs
       for (int q = 0; q < NM; ++q) {
         const float u = ((wd[q][s][c] >> r) & 1u) ? -sc[q] : sc[q];
         if (HS && q == M.self_slot) hv[c] = hv[c] + u;
-        mv[c] = fmaf(M.w[q], u, mv[c]);  // torch add_(u, alpha=w) fuses on CPU (verified)
+        mv[c] = sign_axpy(M, q, u, mv[c]);  // torch add_(u, alpha=w) fuses on CPU (verified)
       }
     }
     ho = make_float4(hv[0], hv[1], hv[2], hv[3]);
@@ -863,12 +873,47 @@ __global__ __launch_bounds__(64 * kSA1Waves) void sign_accumulate1_kernel(SignMs
         for (int q = 0; q < NM; ++q) {
           const float u = ((wd[q][s][c] >> r) & 1u) ? -sc[q] : sc[q];
           if (HS && q == M.self_slot) h = h + u;
-          m = fmaf(M.w[q], u, m);
+          m = sign_axpy(M, q, u, m);
         }
         mem[e] = m;
         if (HS) hat[e] = h;
       }
     }
+  }
+}
+
+// DeepSqueezeSignCompressor.compress's local copy of the message
+// (deep_squeeze.py:416-422): out = (norm_s * torch.sign(x)) / numel_s -- sign(0) = 0
+// and NaN stays NaN, unlike the wire's decode (zero encodes as "+").  One float4
+// per thread; the segment is found once per workgroup and walked per element only
+// when the workgroup straddles a boundary.
+constexpr int kLocalTile = kSignThreads * 4;
+__global__ __launch_bounds__(kSignThreads) void sign_local_kernel(const float* __restrict__ x, int64_t n,
+                                                                  const int64_t* __restrict__ seg_off, int nseg,
+                                                                  const float* __restrict__ norms,
+                                                                  float* __restrict__ out) {
+  __shared__ int s_seg[2];
+  const int64_t t0 = (int64_t)blockIdx.x * kLocalTile;
+  const int64_t t1 = std::min<int64_t>(t0 + kLocalTile, n);
+  if (threadIdx.x == 0) {
+    s_seg[0] = nseg > 1 ? seg_of(seg_off, nseg, t0) : 0;
+    s_seg[1] = nseg > 1 ? seg_of(seg_off, nseg, t1 - 1) : 0;
+  }
+  __syncthreads();
+  const int sg0 = s_seg[0];
+  const bool uniform = s_seg[1] == sg0;
+  const int64_t e0 = t0 + 4 * (int64_t)threadIdx.x;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int64_t e = e0 + c;
+    if (e >= n) break;
+    int sgi = sg0;
+    if (!uniform)
+      while (sgi + 1 < nseg && seg_off[sgi + 1] <= e) ++sgi;
+    const int64_t numel = nseg > 1 ? seg_off[sgi + 1] - seg_off[sgi] : n;
+    const float v = x[e];
+    const float sg = v > 0.f ? 1.0f : (v < 0.f ? -1.0f : (v == v ? 0.0f : v));  // torch.sign: NaN -> NaN
+    out[e] = (norms[sgi] * sg) / (float)numel;
   }
 }
 
@@ -1029,6 +1074,88 @@ CHOCO_API int choco_sign_decompress_accumulate(const int32_t* const* packed_list
     CHOCO_SIGN_ACC(8)
   }
 #undef CHOCO_SIGN_ACC
+  profile_end("sign_accumulate", st);
+  CHOCO_LAUNCHED("sign_accumulate_kernel");
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_sign_decompress_axpy(const int32_t* const* packed_list, const float* const* norms_list,
+                                         const float* weights, int32_t nmsg, int64_t n, const int64_t* seg_off,
+                                         int32_t nseg, int32_t two_roundings, float* target, void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(packed_list && norms_list && weights && target, "null pointer argument");
+  CHOCO_REQUIRE(nmsg >= 1 && nmsg <= kMaxMsg, "nmsg must be in [1, %d]", kMaxMsg);
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
+  CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
+  CHOCO_REQUIRE(aligned16(target), "target must be 16-byte aligned");
+  SignMsgs M{};
+  for (int q = 0; q < nmsg; ++q) {
+    CHOCO_REQUIRE(packed_list[q] && norms_list[q], "null message pointer");
+    M.packed[q] = reinterpret_cast<const uint32_t*>(packed_list[q]);
+    M.norms[q] = norms_list[q];
+    M.w[q] = weights[q];
+  }
+  M.nmsg = nmsg;
+  M.self_slot = -1;
+  M.mode = two_roundings ? 1 : 0;
+  const int64_t Np = choco_sign_words(n);
+  const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
+  profile_begin("sign_accumulate", st);
+#define CHOCO_SIGN_AXPY(NM)                                                                                 \
+  case NM:                                                                                                  \
+    CHOCO_KLAUNCH((sign_accumulate_kernel<NM, false>), dim3(grid), dim3(kSignThreads), 0, st, M, n, Np, seg_off, \
+                  nseg, nullptr, target);                                                                   \
+    break;
+  switch (nmsg) {
+    CHOCO_SIGN_AXPY(1)
+    CHOCO_SIGN_AXPY(2)
+    CHOCO_SIGN_AXPY(3)
+    CHOCO_SIGN_AXPY(4)
+    CHOCO_SIGN_AXPY(5)
+    CHOCO_SIGN_AXPY(6)
+    CHOCO_SIGN_AXPY(7)
+    CHOCO_SIGN_AXPY(8)
+  }
+#undef CHOCO_SIGN_AXPY
+  profile_end("sign_accumulate", st);
+  CHOCO_LAUNCHED("sign_accumulate_kernel");
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_sign_local_decode(const float* x, int64_t n, const int64_t* seg_off, int32_t nseg,
+                                      const float* norms, float* out, void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(x && norms && out, "null pointer argument");
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
+  CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
+  const unsigned grid = (unsigned)((n + kLocalTile - 1) / kLocalTile);
+  CHOCO_KLAUNCH(sign_local_kernel, dim3(grid), dim3(kSignThreads), 0, st, x, n, seg_off, nseg, norms, out);
+  CHOCO_LAUNCHED("sign_local_kernel");
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_sign_decompress_extrapolate(const int32_t* packed, const float* norms, int64_t n,
+                                                const int64_t* seg_off, int32_t nseg, float a, float b, float* target,
+                                                void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(packed && norms && target, "null pointer argument");
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
+  CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
+  CHOCO_REQUIRE(aligned16(target), "target must be 16-byte aligned");
+  SignMsgs M{};
+  M.packed[0] = reinterpret_cast<const uint32_t*>(packed);
+  M.norms[0] = norms;
+  M.w[0] = 1.0f;
+  M.nmsg = 1;
+  M.self_slot = -1;
+  M.mode = 2;
+  M.a = a;
+  M.b = b;
+  const int64_t Np = choco_sign_words(n);
+  const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
+  profile_begin("sign_accumulate", st);
+  CHOCO_KLAUNCH((sign_accumulate_kernel<1, false>), dim3(grid), dim3(kSignThreads), 0, st, M, n, Np, seg_off, nseg,
+                nullptr, target);
   profile_end("sign_accumulate", st);
   CHOCO_LAUNCHED("sign_accumulate_kernel");
   return CHOCO_OK;

@@ -133,6 +133,12 @@ int choco_sparse_accumulate(const float* val, const int32_t* idx, int64_t k,
                             float* xhat_self, float* memory, int64_t n, float weight,
                             uint32_t* bad_count, void* stream);
 
+/* ECDSparsificationCompressor.uncompress (ecd_psgd.py:287-303) for one message:
+ * target[idx] = fmaf(b, val, target[idx] * a)   (hat[idx].mul(a).add(b, q_values),
+ * a = 1 - 2/t, b = 2/t); out-of-range indices are skipped and counted as above. */
+int choco_sparse_extrapolate(const float* val, const int32_t* idx, int64_t k, float* target,
+                             int64_t n, float a, float b, uint32_t* bad_count, void* stream);
+
 /* --------------------------------------------------------------- sign
  * Replaces SignCompressor.packing (sparsification.py:129-145, incl. the external
  * bit2byte.packing) and the per-tensor L1 norms of CHOCOSignCompressor.compress
@@ -168,6 +174,28 @@ int choco_sign_decompress_accumulate(const int32_t* const* packed_list,
                                      int64_t n, const int64_t* seg_off, int32_t nseg,
                                      float* xhat_self, float* memory,
                                      void* ws, size_t ws_bytes, void* stream);
+
+/* Receiver side of the other consumers of the sign codec: for each message m in
+ * order, target += weights[m] * decode(m) per element, with the reference's
+ * rounding: two_roundings = 0 -> fmaf(w, u, target) (torch add_(u, alpha=w):
+ * DCDSignCompressor.uncompress, dcd_psgd.py:442-446, w = 1); 1 -> target + (w * u)
+ * (torch add_(w * u): DeepSqueezeSignCompressor.uncompress, deep_squeeze.py:481-488,
+ * w = consensus_stepsize * (w_r - [r == self])).  u = (norms[m][s] / numel_s) * sign. */
+int choco_sign_decompress_axpy(const int32_t* const* packed_list, const float* const* norms_list,
+                               const float* weights, int32_t nmsg, int64_t n,
+                               const int64_t* seg_off, int32_t nseg, int32_t two_roundings,
+                               float* target, void* stream);
+
+/* ECDSignCompressor.uncompress (ecd_psgd.py:448-454) for one message:
+ * target_s = (target_s * a) + ((b * norm_s) / numel_s) * sign   (a = 1 - 2/t, b = 2/t). */
+int choco_sign_decompress_extrapolate(const int32_t* packed, const float* norms, int64_t n,
+                                      const int64_t* seg_off, int32_t nseg, float a, float b,
+                                      float* target, void* stream);
+
+/* DeepSqueezeSignCompressor.compress's local compressed copy (deep_squeeze.py:416-422):
+ * out = (norms[s] * torch.sign(x)) / numel_s, sign(0) = 0, NaN stays NaN. */
+int choco_sign_local_decode(const float* x, int64_t n, const int64_t* seg_off, int32_t nseg,
+                            const float* norms, float* out, void* stream);
 
 /* --------------------------------------------------------------- QSGD
  * Replaces QuantizationCompressor.get_qsgd/compress (sparsification.py:87-98,114-120)
@@ -210,6 +238,12 @@ int choco_qsgd_decompress_accumulate(const uint8_t* const* packed_list,
                                      int64_t n, const int64_t* seg_off, int32_t nseg,
                                      int32_t q, int32_t is_biased,
                                      float* xhat_self, float* memory, void* stream);
+
+/* ECDQuantizationCompressor.uncompress (ecd_psgd.py:415-423) for one message:
+ * target = fmaf(b, decode(m), target * a)   (hat.mul_(a).add_(q, alpha=b)). */
+int choco_qsgd_decompress_extrapolate(const uint8_t* packed, const float* norms, int64_t n,
+                                      const int64_t* seg_off, int32_t nseg, int32_t q, int32_t is_biased,
+                                      float a, float b, float* target, void* stream);
 
 /* ------------------------------------------------------- gossip step
  * update_params_from_neighbor (pcode/optim/utils.py:67-72):

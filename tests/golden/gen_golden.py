@@ -395,6 +395,182 @@ def gen_layouts():
     print("wrote layouts.json", {k: (len(v), sum(v)) for k, v in res.items()})
 
 
+def _consumer(cls, comm_op, ratio=0.9, qlevel=4, biased=False, **extra):
+    """A reference DCD / DeepSqueeze compressor (its __init__ only stores arguments)."""
+    return cls(aggregator=None, comm_op=comm_op, comm_device="gpu", compress_ratio=ratio,
+               quantize_level=qlevel, is_biased=biased, backend="nccl", use_ipc=False, **extra)
+
+
+class SyncCapture:
+    """force_wait=True aggregator: returns {rank: data}; records what was sent."""
+
+    def __init__(self, rank):
+        self.rank, self.sent = rank, []
+
+    def _agg(self, data, op, force_wait=True):
+        assert op == "get_raw_sync_data" and force_wait is True
+        self.sent.append(data.clone())
+        return {self.rank: data}
+
+
+class SyncReplay:
+    def __init__(self, per_call):
+        self.per_call = list(per_call)
+
+    def _agg(self, data, op, force_wait=True):
+        return self.per_call.pop(0)
+
+
+def gen_dcd(kind, name, layout, comm_op, **kw):
+    """DCD_PSGD's compressor (dcd_psgd.py:150-446) for a ring of 3: worker r compresses
+    d = half_r - x_r; worker 1 replays the three messages into its replicas of every
+    neighbour's model (neighbor_hat_params, one per rank)."""
+    import pcode.optim.dcd_psgd as ref_dcd
+    cls = {"topk": ref_dcd.DCDSparsificationCompressor, "qsgd": ref_dcd.DCDQuantizationCompressor,
+           "sign": ref_dcd.DCDSignCompressor}[kind]
+    n = sum(layout)
+    shapes = [(torch.Size([m]), m) for m in layout]
+    W, self_rank = 3, 1
+    xs = [randn(n, 2500 + 10 * r) for r in range(W)]
+    halfs = [xs[r] + randn(n, 2501 + 10 * r, 0.1) for r in range(W)]
+    sent, draws, last = [], [], None
+    for r in range(W):
+        comp = _consumer(cls, comm_op, **kw)
+        sb = {"original_shapes": shapes, "flatten_half_params": TensorBuffer(split(halfs[r], layout)),
+              "flatten_params": TensorBuffer(split(xs[r], layout))}
+        torch.manual_seed(2900 + r)
+        with RandCapture() as cap:
+            comp.compress(sb)
+        draws.append(torch.cat(cap.draws) if cap.draws else torch.zeros(0))
+        comp.aggregator_fn = SyncCapture(r)
+        comp.sync(sb)
+        sent.append(comp.aggregator_fn.sent)
+        if r == self_rank:
+            last = (comp, sb)
+    comp, sb = last
+    hats0 = [randn(n, 2600 + r, 0.5) for r in range(W)]
+    nhp = {r: TensorBuffer(split(hats0[r], layout)) for r in range(W)}
+    comp.aggregator_fn = SyncReplay([{r: sent[r][c] for r in range(W)} for c in range(len(sent[0]))])
+    comp.sync(sb)
+    comp.uncompress(sb, nhp)
+    arrays = dict(layout=np.array(layout, dtype=np.int64), x=np.stack([x.numpy() for x in xs]),
+                  half=np.stack([h.numpy() for h in halfs]), hats0=np.stack([h.numpy() for h in hats0]),
+                  hats1=np.stack([nhp[r].buffer.numpy() for r in range(W)]), self_rank=np.int64(self_rank),
+                  n_bits=np.float64(sb["n_bits"]))
+    if kind == "qsgd":
+        arrays["u"] = np.stack([d.numpy() for d in draws])
+        for r in range(W):
+            arrays[f"msg{r}"] = sent[r][0].numpy()
+    save(name, **arrays)
+
+
+def gen_deepsqueeze(kind, name, layout, comm_op, **kw):
+    """DeepSqueeze's compressor (deep_squeeze.py:133-489) for a ring of 3: worker r
+    compresses its error-compensated memory_r and returns the local compressed copy;
+    worker 1 aggregates consensus_stepsize * (w_r - [r == 1]) * decode(msg_r)."""
+    import pcode.optim.deep_squeeze as ref_ds
+    cls = {"topk": ref_ds.DeepSqueezeSparsificationCompressor, "qsgd": ref_ds.DeepSqueezeQuantizationCompressor,
+           "sign": ref_ds.DeepSqueezeSignCompressor}[kind]
+    n = sum(layout)
+    shapes = [(torch.Size([m]), m) for m in layout]
+    W, self_rank, gamma = 3, 1, 0.5
+    neighbors_info = {0: 1.0 / 3, 1: 1.0 / 3, 2: 1.0 / 3}
+    mems = [randn(n, 3500 + 10 * r) for r in range(W)]
+    if kind == "sign":
+        for m in mems:
+            m[::101] = 0.0  # torch.sign(0) = 0 in the local copy, "+" on the wire
+    sent, draws, local, last = [], [], [], None
+    for r in range(W):
+        comp = _consumer(cls, comm_op, rank=r, consensus_stepsize=gamma, **kw)
+        sb = {"original_shapes": shapes, "params_tb": TensorBuffer(split(mems[r], layout))}
+        torch.manual_seed(3900 + r)
+        with RandCapture() as cap:
+            lc = comp.compress(sb)
+        draws.append(torch.cat(cap.draws) if cap.draws else torch.zeros(0))
+        local.append(lc.buffer.clone())
+        comp.aggregator_fn = SyncCapture(r)
+        comp.sync(sb)
+        sent.append(comp.aggregator_fn.sent)
+        if r == self_rank:
+            last = (comp, sb)
+    comp, sb = last
+    comp.aggregator_fn = SyncReplay([{r: sent[r][c] for r in range(W)} for c in range(len(sent[0]))])
+    comp.sync(sb)
+    agg = comp.uncompress(sb, neighbors_info)
+    arrays = dict(layout=np.array(layout, dtype=np.int64), mem=np.stack([m.numpy() for m in mems]),
+                  local=np.stack([m.numpy() for m in local]), agg=agg.buffer.numpy(), gamma=np.float64(gamma),
+                  weights=np.array([neighbors_info[r] for r in range(W)]), self_rank=np.int64(self_rank),
+                  n_bits=np.float64(sb["n_bits"]))
+    if kind == "qsgd":
+        arrays["u"] = np.stack([d.numpy() for d in draws])
+        for r in range(W):
+            arrays[f"msg{r}"] = sent[r][0].numpy()
+    if kind == "sign":
+        for r in range(W):
+            arrays[f"norms{r}"] = sent[r][0].numpy()
+    save(name, **arrays)
+
+
+def gen_ecd(kind, name, layout, comm_op, local_index=5, **kw):
+    """ECD_PSGD's compressor (ecd_psgd.py:186-455) for a ring of 3: worker r compresses
+    its extrapolated model z_r; worker 1 extrapolates its replica of every neighbour,
+    hat <- (1 - 2/t) hat + (2/t) q, t = local_index."""
+    import pcode.optim.ecd_psgd as ref_ecd
+    cls = {"topk": ref_ecd.ECDSparsificationCompressor, "qsgd": ref_ecd.ECDQuantizationCompressor,
+           "sign": ref_ecd.ECDSignCompressor}[kind]
+    n = sum(layout)
+    shapes = [(torch.Size([m]), m) for m in layout]
+    W, self_rank = 3, 1
+    zs = [randn(n, 4500 + 10 * r) for r in range(W)]
+    sent, draws, last = [], [], None
+    for r in range(W):
+        comp = _consumer(cls, comm_op, **kw)
+        sb = {"original_shapes": shapes, "flatten_updated_params": TensorBuffer(split(zs[r], layout))}
+        torch.manual_seed(4900 + r)
+        with RandCapture() as cap:
+            comp.compress(sb)
+        draws.append(torch.cat(cap.draws) if cap.draws else torch.zeros(0))
+        comp.aggregator_fn = SyncCapture(r)
+        comp.sync(sb)
+        sent.append(comp.aggregator_fn.sent)
+        if r == self_rank:
+            last = (comp, sb)
+    comp, sb = last
+    hats0 = [randn(n, 4600 + r, 0.5) for r in range(W)]
+    nhp = {r: TensorBuffer(split(hats0[r], layout)) for r in range(W)}
+    comp.aggregator_fn = SyncReplay([{r: sent[r][c] for r in range(W)} for c in range(len(sent[0]))])
+    comp.sync(sb)
+    comp.uncompress(sb, nhp, local_index)
+    arrays = dict(layout=np.array(layout, dtype=np.int64), z=np.stack([z.numpy() for z in zs]),
+                  hats0=np.stack([h.numpy() for h in hats0]),
+                  hats1=np.stack([nhp[r].buffer.numpy() for r in range(W)]), local_index=np.int64(local_index),
+                  self_rank=np.int64(self_rank), n_bits=np.float64(sb["n_bits"]))
+    if kind == "qsgd":
+        arrays["u"] = np.stack([d.numpy() for d in draws])
+        for r in range(W):
+            arrays[f"msg{r}"] = sent[r][0].numpy()
+    if kind == "sign":
+        for r in range(W):
+            arrays[f"norms{r}"] = sent[r][0].numpy()
+    save(name, **arrays)
+
+
+def gen_consumers():
+    gen_dcd("topk", "dcd_topk_mini_r09", MINI_LAYOUT, "compress_top_k", ratio=0.9)
+    gen_dcd("qsgd", "dcd_qsgd_mini_q4", MINI_LAYOUT, "quantize_qsgd", qlevel=4)
+    gen_dcd("sign", "dcd_sign_mini", MINI_LAYOUT, "sign")
+    gen_deepsqueeze("topk", "deepsqueeze_topk_mini_r09", MINI_LAYOUT, "compress_top_k", ratio=0.9)
+    gen_deepsqueeze("qsgd", "deepsqueeze_qsgd_mini_q4", MINI_LAYOUT, "quantize_qsgd", qlevel=4)
+    gen_deepsqueeze("sign", "deepsqueeze_sign_mini", MINI_LAYOUT, "sign")
+    gen_ecd_all()
+
+
+def gen_ecd_all():
+    gen_ecd("topk", "ecd_topk_mini_r09", MINI_LAYOUT, "compress_top_k", ratio=0.9)
+    gen_ecd("qsgd", "ecd_qsgd_mini_q4", MINI_LAYOUT, "quantize_qsgd", qlevel=4)
+    gen_ecd("sign", "ecd_sign_mini", MINI_LAYOUT, "sign")
+
+
 STEP_LAYOUT = MINI_LAYOUT + [1029, 3]
 
 
@@ -420,4 +596,5 @@ if __name__ == "__main__":
     gen_choco("sign", "choco_sign_mini", MINI_LAYOUT, "sign")
     gen_gossip()
     gen_choco_steps()
+    gen_consumers()
     gen_layouts()

@@ -1,0 +1,259 @@
+"""The other consumers of the codec through their drop-ins:
+DCD (chocosgd_amd/dcd.py, reference dcd_psgd.py:150-446), DeepSqueeze
+(chocosgd_amd/deep_squeeze.py, reference deep_squeeze.py:133-489) and ECD
+(chocosgd_amd/ecd.py, reference ecd_psgd.py:186-455), driven on the GPU with
+capturing / replaying aggregators against the reference's own round trips
+(tests/golden/gen_golden.py gen_dcd, gen_deepsqueeze, gen_ecd).
+
+Top-k: bit-exact.  Sign: the device L1 norms are fp64 sums (the reference's fp32 CPU
+norms drift ~1e-6), so results agree to 1e-5 and are bit-exact against the oracle fed
+the device norms.  QSGD: the device draws its own uniforms, so every message is checked
+against the oracle with the device's norms and uniforms, then the receiver bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, same_bits
+from oracle import choco_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def _split(flat, lens):
+    out, p = [], 0
+    for m in lens:
+        out.append(flat[p:p + m].clone())
+        p += m
+    return out
+
+
+class _Capture:
+    def __init__(self, rank):
+        self.rank, self.sent = rank, []
+
+    def _agg(self, data, op, force_wait=True):
+        assert op == "get_raw_sync_data" and force_wait is True
+        self.sent.append(data.clone())
+        return {self.rank: data}
+
+
+class _Replay:
+    def __init__(self, per_call):
+        self.per_call = list(per_call)
+
+    def _agg(self, data, op, force_wait=True):
+        return self.per_call.pop(0)
+
+
+def _args(comm_op, **kw):
+    return dict(aggregator=None, comm_op=comm_op, comm_device="gpu", compress_ratio=kw.get("ratio", 0.9),
+                quantize_level=kw.get("q", 4), is_biased=False, backend="nccl", use_ipc=False)
+
+
+# ------------------------------------------------------------------------------ DCD
+def run_dcd(g, comm_op, **kw):
+    from chocosgd_amd.dcd import DCDCompressor
+    from chocosgd_amd.tensor_buffer import TensorBuffer
+    lens = g["layout"].tolist()
+    shapes = [(torch.Size([m]), m) for m in lens]
+    s = int(g["self_rank"])
+    sent, mine = [], None
+    for r in range(3):
+        comp = DCDCompressor(**_args(comm_op, **kw))
+        sb = {"original_shapes": shapes, "flatten_half_params": TensorBuffer(_split(dev(g["half"][r]), lens)),
+              "flatten_params": TensorBuffer(_split(dev(g["x"][r]), lens))}
+        comp.compress(sb)
+        comp.compressor_fn.aggregator_fn = _Capture(r)
+        comp.sync(sb)
+        sent.append(comp.compressor_fn.aggregator_fn.sent)
+        if r == s:
+            mine = (comp, sb)
+    comp, sb = mine
+    nhp = {r: TensorBuffer(_split(dev(g["hats0"][r]), lens)) for r in range(3)}
+    comp.compressor_fn.aggregator_fn = _Replay([{r: sent[r][c] for r in range(3)} for c in range(len(sent[0]))])
+    comp.sync(sb)
+    comp.uncompress(sb, nhp)
+    return sb, nhp, sent
+
+
+def test_dcd_topk_golden():
+    g = golden("dcd_topk_mini_r09")
+    sb, nhp, _ = run_dcd(g, "compress_top_k", ratio=0.9)
+    for r in range(3):
+        assert same_bits(host(nhp[r].buffer), g["hats1"][r]), f"replica {r}"
+    assert sb["n_bits"] == float(g["n_bits"])
+
+
+def test_dcd_sign_golden():
+    g = golden("dcd_sign_mini")
+    lens = g["layout"].tolist()
+    sb, nhp, sent = run_dcd(g, "sign")
+    hw = (len(lens) + 3) // 4 * 4
+    for r in range(3):
+        assert np.allclose(host(nhp[r].buffer), g["hats1"][r], rtol=1e-5, atol=1e-6)
+        m = host(sent[r][0])
+        hat = g["hats0"][r].copy()
+        O.sign_axpy(hat, m[hw:], m[:hw].view(np.float32)[:len(lens)], lens, 1.0, two_roundings=False)
+        assert same_bits(host(nhp[r].buffer), hat)
+    assert sb["n_bits"] == float(g["n_bits"])
+
+
+def _qsgd_decoded(msg, lens, q=4):
+    n = sum(lens)
+    hb = 4 * ((len(lens) + 3) // 4 * 4)
+    norms = msg[:hb].view(np.float32)[:len(lens)]
+    levels, neg = O.qsgd_unpack(msg[hb:], n, q)
+    off, parts = 0, []
+    for si, m in enumerate(lens):
+        parts.append(O.qsgd_decode(levels[off:off + m], neg[off:off + m], norms[si], 2 ** q - 1, m))
+        off += m
+    return np.concatenate(parts)
+
+
+def test_dcd_qsgd_consistent():
+    g = golden("dcd_qsgd_mini_q4")
+    lens = g["layout"].tolist()
+    sb, nhp, sent = run_dcd(g, "quantize_qsgd", q=4)
+    for r in range(3):
+        dec = _qsgd_decoded(host(sent[r][0]), lens)
+        assert same_bits(host(nhp[r].buffer), (g["hats0"][r] + dec).astype(np.float32))
+        d = (g["half"][r] - g["x"][r]).astype(np.float64)
+        assert np.corrcoef(dec, d)[0, 1] > 0.3  # an unbiased quantization of the delta
+    assert sb["n_bits"] == float(g["n_bits"])
+
+
+# ------------------------------------------------------------------------------ DeepSqueeze
+def run_deepsqueeze(g, comm_op, **kw):
+    from chocosgd_amd.deep_squeeze import DeepSqueezeCompressor
+    from chocosgd_amd.tensor_buffer import TensorBuffer
+    lens = g["layout"].tolist()
+    shapes = [(torch.Size([m]), m) for m in lens]
+    s = int(g["self_rank"])
+    neighbors_info = {r: float(w) for r, w in enumerate(g["weights"])}
+    sent, local, mine = [], [], None
+    for r in range(3):
+        comp = DeepSqueezeCompressor(rank=r, consensus_stepsize=float(g["gamma"]), **_args(comm_op, **kw))
+        sb = {"original_shapes": shapes, "params_tb": TensorBuffer(_split(dev(g["mem"][r]), lens))}
+        local.append(host(comp.compress(sb).buffer))
+        comp.compressor_fn.aggregator_fn = _Capture(r)
+        comp.sync(sb)
+        sent.append(comp.compressor_fn.aggregator_fn.sent)
+        if r == s:
+            mine = (comp, sb)
+    comp, sb = mine
+    comp.compressor_fn.aggregator_fn = _Replay([{r: sent[r][c] for r in range(3)} for c in range(len(sent[0]))])
+    comp.sync(sb)
+    agg = host(comp.uncompress(sb, neighbors_info).buffer)
+    return sb, local, agg, sent
+
+
+def test_deepsqueeze_topk_golden():
+    g = golden("deepsqueeze_topk_mini_r09")
+    sb, local, agg, _ = run_deepsqueeze(g, "compress_top_k", ratio=0.9)
+    for r in range(3):
+        assert same_bits(local[r], g["local"][r]), f"local {r}"
+    assert same_bits(agg, g["agg"])
+    assert sb["n_bits"] == float(g["n_bits"])
+
+
+def test_deepsqueeze_sign_golden():
+    g = golden("deepsqueeze_sign_mini")
+    lens = g["layout"].tolist()
+    s = int(g["self_rank"])
+    sb, local, agg, sent = run_deepsqueeze(g, "sign")
+    hw = (len(lens) + 3) // 4 * 4
+    want = np.zeros_like(g["agg"])
+    for r in range(3):
+        m = host(sent[r][0])
+        norms = m[:hw].view(np.float32)[:len(lens)]
+        assert np.allclose(norms, g[f"norms{r}"], rtol=1e-5, atol=0)
+        assert np.array_equal(m[hw:], O.sign_pack(g["mem"][r]))
+        assert same_bits(local[r], O.sign_local(g["mem"][r], norms, lens))  # sign(0) = 0 kept
+        assert np.allclose(local[r], g["local"][r], rtol=1e-5, atol=1e-7)
+        c = O.deepsqueeze_weight(float(g["gamma"]), float(g["weights"][r]), r == s)
+        O.sign_axpy(want, m[hw:], norms, lens, c, two_roundings=True)
+    assert same_bits(agg, want)
+    # the aggregate sums terms of both signs (c_self < 0): absolute tolerance at the terms' scale
+    assert np.allclose(agg, g["agg"], rtol=1e-5, atol=1e-6)
+
+
+def test_deepsqueeze_qsgd_consistent():
+    g = golden("deepsqueeze_qsgd_mini_q4")
+    lens = g["layout"].tolist()
+    s = int(g["self_rank"])
+    sb, local, agg, sent = run_deepsqueeze(g, "quantize_qsgd", q=4)
+    want = np.zeros_like(g["agg"])
+    for r in range(3):
+        dec = _qsgd_decoded(host(sent[r][0]), lens)
+        assert same_bits(local[r], dec)  # the local copy is the decoded message
+        c = O.deepsqueeze_weight(float(g["gamma"]), float(g["weights"][r]), r == s)
+        want = (want + (c * dec).astype(np.float32)).astype(np.float32)
+    assert same_bits(agg, want)
+    assert sb["n_bits"] == float(g["n_bits"])
+
+
+# ------------------------------------------------------------------------------ ECD
+def run_ecd(g, comm_op, **kw):
+    from chocosgd_amd.ecd import ECDCompressor
+    from chocosgd_amd.tensor_buffer import TensorBuffer
+    lens = g["layout"].tolist()
+    shapes = [(torch.Size([m]), m) for m in lens]
+    s = int(g["self_rank"])
+    sent, mine = [], None
+    for r in range(3):
+        comp = ECDCompressor(**_args(comm_op, **kw))
+        sb = {"original_shapes": shapes, "flatten_updated_params": TensorBuffer(_split(dev(g["z"][r]), lens))}
+        comp.compress(sb)
+        comp.compressor_fn.aggregator_fn = _Capture(r)
+        comp.sync(sb)
+        sent.append(comp.compressor_fn.aggregator_fn.sent)
+        if r == s:
+            mine = (comp, sb)
+    comp, sb = mine
+    nhp = {r: TensorBuffer(_split(dev(g["hats0"][r]), lens)) for r in range(3)}
+    comp.compressor_fn.aggregator_fn = _Replay([{r: sent[r][c] for r in range(3)} for c in range(len(sent[0]))])
+    comp.sync(sb)
+    comp.uncompress(sb, nhp, int(g["local_index"]))
+    return sb, nhp, sent
+
+
+def test_ecd_topk_golden():
+    g = golden("ecd_topk_mini_r09")
+    sb, nhp, _ = run_ecd(g, "compress_top_k", ratio=0.9)
+    for r in range(3):
+        assert same_bits(host(nhp[r].buffer), g["hats1"][r]), f"replica {r}"
+    assert sb["n_bits"] == float(g["n_bits"])
+
+
+def test_ecd_sign_golden():
+    g = golden("ecd_sign_mini")
+    lens = g["layout"].tolist()
+    t = int(g["local_index"])
+    sb, nhp, sent = run_ecd(g, "sign")
+    hw = (len(lens) + 3) // 4 * 4
+    for r in range(3):
+        m = host(sent[r][0])
+        want = O.ecd_sign_extrapolate(g["hats0"][r], m[hw:], m[:hw].view(np.float32)[:len(lens)], lens, t)
+        assert same_bits(host(nhp[r].buffer), want)
+        assert np.allclose(host(nhp[r].buffer), g["hats1"][r], rtol=1e-5, atol=1e-6)
+
+
+def test_ecd_qsgd_consistent():
+    g = golden("ecd_qsgd_mini_q4")
+    lens = g["layout"].tolist()
+    t = int(g["local_index"])
+    sb, nhp, sent = run_ecd(g, "quantize_qsgd", q=4)
+    for r in range(3):
+        dec = _qsgd_decoded(host(sent[r][0]), lens)
+        assert same_bits(host(nhp[r].buffer), O.ecd_extrapolate(g["hats0"][r], dec, t))
+    assert sb["n_bits"] == float(g["n_bits"])

@@ -208,6 +208,122 @@ def test_choco_step_fixture(name):
         assert np.allclose(mem, g["mem1"], rtol=1e-5, atol=1e-6)
 
 
+def test_dcd_topk_fixture():
+    """DCD (dcd_psgd.py:175-275): every replica hat_r[idx_r] += v_r, v_r = top-k of
+    half_r - x_r per tensor."""
+    g = golden("dcd_topk_mini_r09")
+    lens = g["layout"].tolist()
+    for r in range(3):
+        d = (g["half"][r] - g["x"][r]).astype(np.float32)
+        ov, oi, _ = O.topk_segmented(d, lens, 0.9)
+        hat = g["hats0"][r].copy()
+        hat[oi] = hat[oi] + ov
+        assert same_bits(hat, g["hats1"][r])
+
+
+def test_dcd_qsgd_fixture():
+    import torch
+    g = golden("dcd_qsgd_mini_q4")
+    lens = g["layout"].tolist()
+    for r in range(3):
+        d = (g["half"][r] - g["x"][r]).astype(np.float32)
+        # the message is the reference's dense floats: the oracle rebuilds it from the captured
+        # uniforms and the reference's own fp32 norm (torch CPU, as dcd_psgd.py:310 computes it)
+        dense = g[f"msg{r}"]
+        assert same_bits((g["hats0"][r] + dense).astype(np.float32), g["hats1"][r])
+        off, outs = 0, []
+        for m in lens:
+            nrm = np.float32(torch.from_numpy(d[off:off + m].copy()).norm(p=2).item())
+            outs.append(O.qsgd_dense(d[off:off + m], 15, g["u"][r][off:off + m], nrm))
+            off += m
+        assert same_bits(np.concatenate(outs), dense)
+
+
+def test_dcd_sign_fixture():
+    g = golden("dcd_sign_mini")
+    lens = g["layout"].tolist()
+    for r in range(3):
+        d = (g["half"][r] - g["x"][r]).astype(np.float32)
+        hat = g["hats0"][r].copy()
+        O.sign_axpy(hat, O.sign_pack(d), O.l1_norms(d, lens), lens, 1.0, two_roundings=False)
+        assert np.allclose(hat, g["hats1"][r], rtol=1e-5, atol=1e-6)
+
+
+def test_deepsqueeze_topk_fixture():
+    """DeepSqueeze (deep_squeeze.py:187-279): local copy = message scattered into zeros;
+    aggregate = sum_r c_r * v_r at idx_r, c_r = gamma (w_r - [r == self]), two roundings."""
+    g = golden("deepsqueeze_topk_mini_r09")
+    lens = g["layout"].tolist()
+    s = int(g["self_rank"])
+    agg = np.zeros_like(g["agg"])
+    for r in range(3):
+        ov, oi, _ = O.topk_segmented(g["mem"][r], lens, 0.9)
+        local = np.zeros_like(g["mem"][r])
+        local[oi] = ov
+        assert same_bits(local, g["local"][r])
+        c = O.deepsqueeze_weight(float(g["gamma"]), float(g["weights"][r]), r == s)
+        agg[oi] = agg[oi] + (c * ov).astype(np.float32)
+    assert same_bits(agg, g["agg"])
+
+
+def test_deepsqueeze_qsgd_fixture():
+    g = golden("deepsqueeze_qsgd_mini_q4")
+    s = int(g["self_rank"])
+    agg = np.zeros_like(g["agg"])
+    for r in range(3):
+        assert same_bits(g["local"][r], g[f"msg{r}"])  # the local copy IS the dense message
+        c = O.deepsqueeze_weight(float(g["gamma"]), float(g["weights"][r]), r == s)
+        agg = (agg + (c * g[f"msg{r}"]).astype(np.float32)).astype(np.float32)
+    assert same_bits(agg, g["agg"])
+
+
+def test_deepsqueeze_sign_fixture():
+    """With the reference's own fp32 norms (its message) the local copy and the aggregate
+    are bit-exact; the oracle's fp64 norms agree with them to 1e-5."""
+    g = golden("deepsqueeze_sign_mini")
+    lens = g["layout"].tolist()
+    s = int(g["self_rank"])
+    agg = np.zeros_like(g["agg"])
+    for r in range(3):
+        x = g["mem"][r]
+        norms = g[f"norms{r}"]
+        assert np.allclose(O.l1_norms(x, lens), norms, rtol=1e-5, atol=0)
+        assert same_bits(O.sign_local(x, norms, lens), g["local"][r])
+        c = O.deepsqueeze_weight(float(g["gamma"]), float(g["weights"][r]), r == s)
+        O.sign_axpy(agg, O.sign_pack(x), norms, lens, c, two_roundings=True)
+    assert same_bits(agg, g["agg"])
+
+
+def test_ecd_topk_fixture():
+    """ECD (ecd_psgd.py:211-303): replica r extrapolated with the top-k of z_r."""
+    g = golden("ecd_topk_mini_r09")
+    lens = g["layout"].tolist()
+    t = int(g["local_index"])
+    for r in range(3):
+        ov, oi, _ = O.topk_segmented(g["z"][r], lens, 0.9)
+        hat = g["hats0"][r].copy()
+        hat[oi] = O.ecd_extrapolate(hat[oi], ov, t)
+        assert same_bits(hat, g["hats1"][r])
+
+
+def test_ecd_qsgd_fixture():
+    g = golden("ecd_qsgd_mini_q4")
+    t = int(g["local_index"])
+    for r in range(3):
+        assert same_bits(O.ecd_extrapolate(g["hats0"][r], g[f"msg{r}"], t), g["hats1"][r])
+
+
+def test_ecd_sign_fixture():
+    g = golden("ecd_sign_mini")
+    lens = g["layout"].tolist()
+    t = int(g["local_index"])
+    for r in range(3):
+        norms = g[f"norms{r}"]
+        assert np.allclose(O.l1_norms(g["z"][r], lens), norms, rtol=1e-5, atol=0)
+        got = O.ecd_sign_extrapolate(g["hats0"][r], O.sign_pack(g["z"][r]), norms, lens, t)
+        assert same_bits(got, g["hats1"][r])
+
+
 def test_splitmix64_known_answer():
     # the first outputs of the splitmix64 generator from state 0 (Vigna's reference
     # implementation: state += gamma; return mix(state))
