@@ -81,8 +81,39 @@ class DecentralizedAggregation(object):
             req.wait()
 
 
+class CentralizedAggregation(object):
+    """The all-gather / all-reduce half of communication.py:138-226 that the
+    EF-sign and DGC consumers use (`_agg(data, op=, communication_scheme=,
+    async_op=)`): RCCL collectives on ROCm, gloo on CPU."""
+
+    def __init__(self, rank, world, neighbors_info=None, group=None):
+        self.rank = rank
+        self.group = group
+        self.world_size = float(world)
+
+    def _agg(self, data, op=None, distributed=True, communication_scheme="all_reduce", async_op=False, **kargs):
+        if not distributed:
+            return data
+        if communication_scheme == "all_reduce":
+            if op not in ("avg", "sum"):
+                raise NotImplementedError
+            req = dist.all_reduce(data, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+            if async_op:
+                return data, req
+            return data / self.world_size if op == "avg" else data
+        if communication_scheme == "all_gather":
+            gathered = [torch.empty_like(data) for _ in range(int(self.world_size))]
+            req = dist.all_gather(gathered, data, group=self.group, async_op=async_op)
+            return (gathered, req) if async_op else gathered
+        raise NotImplementedError
+
+    def complete_wait(self, req):
+        req.wait()
+
+
 def get_aggregators(cur_rank, world, neighbors_info, aggregator_type):
     if aggregator_type == "decentralized":
         return DecentralizedAggregation(cur_rank, neighbors_info)
-    raise NotImplementedError(
-        f"aggregator '{aggregator_type}' is outside the CHOCO compressor path (see DESIGN.md)")
+    if aggregator_type == "centralized":
+        return CentralizedAggregation(cur_rank, world, neighbors_info)
+    raise NotImplementedError(f"aggregator '{aggregator_type}' is outside the compressor path (see DESIGN.md)")

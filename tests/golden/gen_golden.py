@@ -555,6 +555,80 @@ def gen_ecd(kind, name, layout, comm_op, local_index=5, **kw):
     save(name, **arrays)
 
 
+class GatherCapture:
+    """centralized all-gather aggregator over W simulated ranks: returns the list of
+    every rank's data (filled in from the recorded messages)."""
+
+    def __init__(self, msgs):
+        self.msgs = msgs  # per call: list over ranks
+
+    def _agg(self, data, op=None, communication_scheme="all_gather", **kw):
+        return self.msgs.pop(0)
+
+
+def gen_ef_sign(name, layout):
+    """EFSignCompressor (ef_sign_sgd.py:126-219) for 3 ranks: rank 1 decompresses."""
+    import pcode.optim.ef_sign_sgd as ref_ef
+    W, me = 3, 1
+    n = sum(layout)
+    grads = [randn(n, 5500 + r) for r in range(W)]
+    grads[0][::97] = 0.0
+    bufs, sent = [], []
+    for r in range(W):
+        comp = ref_ef.EFSignCompressor(rank=r, world_size=W, aggregator=None, comm_op="sign", comm_device="gpu",
+                                       use_ipc=False)
+        sb = comp.compress(TensorBuffer(split(grads[r], layout)))
+        bufs.append((comp, sb))
+        sent.append((sb["grad_norms_tb"].buffer.clone(), sb["signs"].clone()))
+    comp, sb = bufs[me]
+    local = sb["synced_grads_tb"].buffer.clone()
+    comp.aggregator_fn = GatherCapture([[s[0] for s in sent], [s[1] for s in sent]])
+    comp.sync(sb)
+    out = comp.decompress(sb)
+    save(name, layout=np.array(layout, dtype=np.int64), grads=np.stack([g.numpy() for g in grads]),
+         local=local.numpy(), out=out.buffer.numpy(), norms=np.stack([s[0].numpy() for s in sent]),
+         rank=np.int64(me), n_bits=np.float64(sb["n_bits"]))
+
+
+def gen_dgc(name, layout, ratio=0.9):
+    """DGC._compress / _sync / _recover_info (dgc.py:153-252) with top-k, 3 ranks."""
+    import pcode.optim.dgc as ref_dgc
+    W, me, lr = 3, 1, 0.1
+    n = sum(layout)
+    names = [f"p{i}" for i in range(len(layout))]
+    grads = [randn(n, 6500 + r) for r in range(W)]
+    mems = [randn(n, 6600 + r, 0.3) for r in range(W)]
+    msgs, outs = [], {}
+    for r in range(W):
+        opt = object.__new__(ref_dgc.DGC)
+        opt.param_names = list(enumerate(names))
+        opt.memory_of_grads = {nm: m.clone() for nm, m in zip(names, split(mems[r], layout))}
+        opt._get_compress_ratio = lambda: ratio
+        opt.comm_op = "compress_top_k"
+        opt.compressor_fn = ref_sp.SparsificationCompressor()
+        opt.quantize_level = 32
+        opt.is_biased = False
+        opt.is_compress_op = True
+        opt.mask_momentum = False
+        opt.comm_device = "gpu"
+        vals, idx, n_bits = opt._compress(split(grads[r], layout))
+        msgs.append(torch.cat([vals, idx]))
+        outs[r] = (opt, vals, idx, n_bits, torch.cat([opt.memory_of_grads[nm] for nm in names]))
+    opt, vals, idx, n_bits, mem_after = outs[me]
+    opt.world_aggregator = GatherCapture([list(msgs)])
+    synced, size = opt._sync(vals, idx)
+    opt.n_nodes = W
+    opt.param_groups = [{"lr": lr}]
+    params = randn(n, 6700, 1.0)
+    shapes = [(torch.Size([m]), m) for m in layout]
+    upd = opt._recover_info(params, synced, size, opt.selected_shapes, shapes)
+    save(name, layout=np.array(layout, dtype=np.int64), grads=np.stack([g.numpy() for g in grads]),
+         mems=np.stack([m.numpy() for m in mems]),
+         mems_after=np.stack([outs[r][4].numpy() for r in range(W)]), params=params.numpy(),
+         params_after=upd.numpy(), lr=np.float64(lr), ratio=np.float64(ratio), rank=np.int64(me),
+         n_bits=np.float64(n_bits))
+
+
 def gen_consumers():
     gen_dcd("topk", "dcd_topk_mini_r09", MINI_LAYOUT, "compress_top_k", ratio=0.9)
     gen_dcd("qsgd", "dcd_qsgd_mini_q4", MINI_LAYOUT, "quantize_qsgd", qlevel=4)
@@ -563,6 +637,12 @@ def gen_consumers():
     gen_deepsqueeze("qsgd", "deepsqueeze_qsgd_mini_q4", MINI_LAYOUT, "quantize_qsgd", qlevel=4)
     gen_deepsqueeze("sign", "deepsqueeze_sign_mini", MINI_LAYOUT, "sign")
     gen_ecd_all()
+    gen_central()
+
+
+def gen_central():
+    gen_ef_sign("efsign_mini", MINI_LAYOUT)
+    gen_dgc("dgc_topk_mini_r09", MINI_LAYOUT)
 
 
 def gen_ecd_all():

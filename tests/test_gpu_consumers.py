@@ -257,3 +257,81 @@ def test_ecd_qsgd_consistent():
         dec = _qsgd_decoded(host(sent[r][0]), lens)
         assert same_bits(host(nhp[r].buffer), O.ecd_extrapolate(g["hats0"][r], dec, t))
     assert sb["n_bits"] == float(g["n_bits"])
+
+
+# ------------------------------------------------------------------------------ EF-sign, DGC
+class _Gather:
+    """all-gather stand-in: every rank's message, in rank order, per call."""
+
+    def __init__(self, per_call):
+        self.per_call = list(per_call)
+
+    def _agg(self, data, op=None, communication_scheme="all_gather", **kw):
+        return self.per_call.pop(0)
+
+
+def test_ef_sign_golden():
+    from chocosgd_amd.ef_sign import EFSignCompressor
+    from chocosgd_amd.tensor_buffer import TensorBuffer
+    g = golden("efsign_mini")
+    lens = g["layout"].tolist()
+    me = int(g["rank"])
+    hw = (len(lens) + 3) // 4 * 4
+    msgs, bufs = [], []
+    for r in range(3):
+        comp = EFSignCompressor(rank=r, world_size=3, aggregator=None, comm_op="sign", comm_device="gpu",
+                                use_ipc=False)
+        sb = comp.compress(TensorBuffer(_split(dev(g["grads"][r]), lens)))
+        bufs.append((comp, sb))
+        norms = sb["grad_norms_tb"].buffer
+        header = torch.zeros(hw, dtype=torch.float32, device=DEV)
+        header[:len(lens)] = norms
+        msgs.append(torch.cat([header.view(torch.int32), sb["signs"]]))
+    comp, sb = bufs[me]
+    nm_me = host(sb["grad_norms_tb"].buffer)
+    assert np.allclose(nm_me, g["norms"][me], rtol=1e-5, atol=0)
+    local = host(sb["synced_grads_tb"].buffer)
+    assert same_bits(local, O.sign_local(g["grads"][me], nm_me, lens))
+    comp.aggregator_fn = _Gather([msgs])
+    comp.sync(sb)
+    out = host(comp.decompress(sb).buffer)
+    want = local.copy()
+    for r in range(3):
+        if r != me:
+            m = host(msgs[r])
+            O.sign_axpy(want, m[hw:], m[:hw].view(np.float32)[:len(lens)], lens, 1.0, two_roundings=False)
+    assert same_bits(out, (want / np.float32(3.0)).astype(np.float32))
+    assert np.allclose(out, g["out"], rtol=1e-5, atol=1e-6)
+    assert sb["n_bits"] == float(g["n_bits"])
+
+
+def test_dgc_topk():
+    """Compress (memory keeps the unselected entries: the intended `_grad * nmask`, see
+    test_oracle_golden.test_dgc_fixture for the reference's uint8-NOT defect) and the
+    recovered parameters bit-exact against the reference's fixture."""
+    from chocosgd_amd.dgc import DGCCodec
+    from chocosgd_amd.tensor_buffer import TensorBuffer
+    g = golden("dgc_topk_mini_r09")
+    lens = g["layout"].tolist()
+    me = int(g["rank"])
+    ratio = float(g["ratio"])
+    msgs, mine = [], None
+    for r in range(3):
+        codec_r = DGCCodec(world_aggregator=None, comm_op="compress_top_k", comm_device="gpu", n_nodes=3)
+        mem = TensorBuffer(_split(dev(g["mems"][r]), lens))
+        grads = _split(dev(g["grads"][r]), lens)
+        vals, idx, n_bits = codec_r.compress(grads, mem, ratio)
+        x = (g["grads"][r] + g["mems"][r]).astype(np.float32)
+        ov, oi, _ = O.topk_segmented(x, lens, ratio)
+        assert np.array_equal(host(idx).astype(np.int64), oi) and same_bits(host(vals), ov)
+        x[oi] = 0.0
+        assert same_bits(host(mem.buffer), x)
+        msgs.append(torch.cat([vals.view(torch.int32), idx]))
+        if r == me:
+            mine = (codec_r, vals, idx, n_bits)
+    codec_r, vals, idx, n_bits = mine
+    assert n_bits == float(g["n_bits"])
+    codec_r.world_aggregator = _Gather([msgs])
+    synced, size = codec_r.sync(vals, idx)
+    out = codec_r.recover_info(dev(g["params"]), synced, size, float(g["lr"]))
+    assert same_bits(host(out), g["params_after"])

@@ -324,6 +324,46 @@ def test_ecd_sign_fixture():
         assert same_bits(got, g["hats1"][r])
 
 
+def test_ef_sign_fixture():
+    """EFSignCompressor (ef_sign_sgd.py:140-219): the local copy norm * sign(g) / numel
+    (sign(0) = 0) plus every other rank's decoded signs, divided by the world size."""
+    g = golden("efsign_mini")
+    lens = g["layout"].tolist()
+    me = int(g["rank"])
+    local = O.sign_local(g["grads"][me], g["norms"][me], lens)
+    assert same_bits(local, g["local"])
+    out = local.copy()
+    for r in range(3):
+        if r != me:
+            O.sign_axpy(out, O.sign_pack(g["grads"][r]), g["norms"][r], lens, 1.0, two_roundings=False)
+    assert same_bits((out / np.float32(3.0)).astype(np.float32), g["out"])
+
+
+def test_dgc_fixture():
+    """DGC._compress / _recover_info (dgc.py:153-252): error-feedback top-k and the averaged
+    sparse update of all ranks' messages, bit-exact.
+
+    The memory update is NOT reproduced: the reference's get_mask returns
+    (~mask.byte()).float() (sparsification.py:33-38), a BITWISE not of uint8 under the
+    PyTorch it pins (>= 1.2), i.e. 255 / 254 instead of 1 / 0, so its memory becomes
+    255 * _grad (254 * at the selected entries).  The drop-in keeps the intended
+    `_grad * nmask` (selected entries zeroed); this test pins what the
+    fixture holds so the deviation is explicit."""
+    g = golden("dgc_topk_mini_r09")
+    lens = g["layout"].tolist()
+    grads = np.zeros_like(g["params"])
+    for r in range(3):
+        x = (g["grads"][r] + g["mems"][r]).astype(np.float32)
+        ov, oi, _ = O.topk_segmented(x, lens, float(g["ratio"]))
+        factor = np.full(x.size, np.float32(255.0), dtype=np.float32)
+        factor[oi] = np.float32(254.0)
+        assert same_bits((x * factor).astype(np.float32), g["mems_after"][r])
+        grads[oi] = grads[oi] + ov
+    upd = (grads / np.float32(3)).astype(np.float32)
+    want = O.fma32(np.float32(-float(g["lr"])), upd, g["params"])
+    assert same_bits(want, g["params_after"])
+
+
 def test_splitmix64_known_answer():
     # the first outputs of the splitmix64 generator from state 0 (Vigna's reference
     # implementation: state += gamma; return mix(state))
