@@ -23,14 +23,17 @@ KERNELS = {
     "topk_stream": ("topk_stream_kernel", 2.0),
     "topk_finish": ("topk_finish_kernel", 2.0),
     "topk_fused": ("topk_fused_kernel", 2.0),
-    "topk_segmented": ("topk_segmented_kernel", 2.0),
+    "topk_seg_hist": ("seg_hist_kernel", 2.0),
+    "topk_seg_collect": ("seg_collect_kernel", 2.0),
+    "topk_seg_select": ("seg_select_kernel", 2.0),
+    "topk_seg_emit": ("seg_emit_kernel", 2.0),
     "sparse_accumulate": ("sparse_acc", 1.0),
     "qsgd_norm": ("qsgd_norm_kernel", 2.0),
     "qsgd_quantize": ("qsgd_quant_kernel", 2.0),
     "qsgd_accumulate": ("qsgd_decode_kernel", 2.0),
     "sign_pack": ("sign_pack", 2.0),
     "sign_accumulate": ("sign_accumulate_kernel", 2.0),
-    "gossip_step": ("gossip_kernel", 2.0),
+    "gossip_step": ("gossip", 2.0),
 }
 
 
