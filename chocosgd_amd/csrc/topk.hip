@@ -65,6 +65,7 @@ constexpr int kNBucket = 256;           // 255 "maybe" buckets + 1 "sure"
 constexpr int kNMaybe = kNBucket - 1;
 constexpr int kNRep = 16;               // replicas of the global bucket totals
 constexpr int kMCap = 16384;            // max keys of bucket j* selected in LDS
+constexpr size_t kWideBytes = 4 * (64 + 3 * 2048);  // sizeof(WideCtrl), rounded to 256 below
 constexpr int kK4Threads = 1024;
 constexpr int64_t kSmallN = 65536;
 constexpr int kExactThreads = 1024;
@@ -127,7 +128,7 @@ struct TopkCtrl {
 struct TopkLayout {
   int64_t n;
   uint32_t tile, nb, side_cap;
-  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, total;
+  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, off_wide, off_gcnt, total;
 };
 
 // Tile = ceil(n / kK2Target) rounded up to 32768 elements: one tile per CU, all
@@ -143,13 +144,18 @@ static TopkLayout topk_layout(int64_t n) {
   L.tile = (uint32_t)tile;
   L.nb = (uint32_t)((n + tile - 1) / tile);
   L.side_cap = (uint32_t)std::min<int64_t>(kMaybeCap, tile);
+  // A fixed header at the start of every top-k workspace (any n): the control block
+  // and the exact-fallback queue (WideCtrl), whose counters rely on starting zeroed --
+  // calls of different n sharing one workspace must not move them.
   size_t o = 0;
   L.off_ctrl = o;  o += align_up(sizeof(TopkCtrl), 256);
+  L.off_wide = o;  o += kWideBytes;
   L.off_cum = o;   o += align_up((size_t)L.nb * kNBucket * 4, 256);
   L.off_cntw = o;  o += align_up((size_t)L.nb * (tile / kChunk) * 4, 256);   // per-chunk candidate counts
   L.off_side = o;  o += align_up((size_t)L.nb * L.side_cap * 4, 256);
   L.off_cval = o;  o += align_up((size_t)L.nb * tile * 4, 256);   // candidate values, chunk slot ranges
   L.off_cidx = o;  o += align_up((size_t)L.nb * tile * 4, 256);   // ... and indices
+  L.off_gcnt = o;  o += align_up((size_t)L.nb * 8, 256);              // ... its per-tile (#>T, #==T)
   L.total = o;
   return L;
 }
@@ -184,7 +190,7 @@ struct Src {
 // ----------------------------------------------------------------------------
 struct ExactSmem {
   uint32_t hist[2048];
-  uint32_t scratch[24];
+  uint32_t scratch[40];  // block_excl_scan2: 2 words per wave
   uint32_t bc[4];
 };
 
@@ -851,11 +857,21 @@ __global__ __launch_bounds__(kK1Threads) void topk_bounds_kernel(const float* __
   uint32_t s_lo;
   uint64_t s_hi_est;
   sample_bounds(kk, ranks, lane, w, sm, s_lo, s_hi_est);
+  const Buckets bk = make_buckets(s_lo, s_hi_est, 0);
+  // Degenerate input: more than a quarter of the sample lies in the "maybe" range (an
+  // all-equal buffer, a huge tie cluster at the k-th magnitude): the bucket select
+  // cannot succeed, so flag it (overflow bit 1) -- K2 then skips the candidate stream
+  // and K34 goes straight to the exact fallback.
+  uint32_t nmaybe = 0;
+#pragma unroll
+  for (int j = 0; j < kSampleLoads * 4; ++j) nmaybe += (kk[j] >= bk.s_lo && kk[j] < bk.s_hi) ? 1u : 0u;
+  uint32_t tot_maybe;
+  block_excl_scan(nmaybe, sm.scratch, &tot_maybe);
   if (threadIdx.x == 0) {
-    const Buckets bk = make_buckets(s_lo, s_hi_est, 0);
     ctrl->s_lo = bk.s_lo;
     ctrl->s_hi = bk.s_hi;
     ctrl->shift = bk.shift;
+    if (tot_maybe > (uint32_t)(kSampleN / 4)) ctrl->overflow = 2u;
   }
   STAMP(30000, 2);
 }
@@ -904,6 +920,9 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     if (kTwoChunks) load_rows_full<XH>(ts, batch0(c + kK2Waves), lane, B);
     else if (!kOneBatch && !XH) load_rows_full<XH>(ts, batch1(c), lane, B);
     bk = make_buckets_from(ctrl->s_lo, ctrl->s_hi, ctrl->shift, seed);
+    // K1 flagged a degenerate sample: K34 will take the exact fallback, which needs
+    // nothing from this kernel (with the fused gossip step the stream must still run)
+    if (!GS && (ctrl->overflow & 2u) != 0u) return;
   } else {
     bk = make_buckets(hs_lo, hs_hi, seed);
   }
@@ -1291,15 +1310,289 @@ CHOCO_DEV uint32_t batch_ranks(const bool (&f)[kEmitRows], uint32_t (&rk)[kEmitR
 }
 static_assert(kEmitRows * (kK4Threads / 64) == 128, "batch_ranks: wave 0 scans 2 counts per lane");
 
+// Hand-offs between workgroups (bounds, tile tables, side lists) use the
+// fence-free form of MI355X_MICROARCH.md "Valid forms": every handed-off word is
+// stored write-through (relaxed agent-scope atomic store = sc1) and read with
+// sc1 loads; each storing wave drains (vmcnt(0)) before a workgroup barrier,
+// behind which one lane adds to the counter; the consumer polls that counter.
+// No release fence: a buffer_wbl2 writes back the whole XCD L2 and cost
+// 10-30 us per tile in the middle of everyone else's stream (measured).
+CHOCO_DEV void st_sc1(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+CHOCO_DEV uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// bounded poll of a counter written by running workgroups (s_sleep between
+// polls); returns when *p >= want
+CHOCO_DEV void poll_ge(const uint32_t* p, uint32_t want) {
+  for (uint32_t it = 0; it < (1u << 22); ++it) {
+    if (ld_sc1(p) >= want) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// every wave's stores drained, the workgroup joined, one lane adds
+CHOCO_DEV void publish_add(uint32_t* counter) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ----------------------------------------------------------------------------
+// Wide exact fallback (K34, when the sample's bucket guess failed: bucket j* larger
+// than LDS -- tie clusters, exact zeros where x = x_hat --, too few candidates, or a
+// side list overflow).  Instead of one workgroup radix-selecting the whole input,
+// every K34 workgroup takes TICKETS from a work queue of 5 * nb items:
+//   phases 0-2: histogram of one tile's keys for radix digit 0/1/2 (bits 30..20,
+//               19..9, 8..0; only keys matching the digits found so far),
+//   phase 3   : one tile's (#key > T, #key == T),
+//   phase 4   : one tile's ordered emission at its offset (counts of earlier tiles).
+// An item of phase p waits until every item of phase p-1 is done; those are held by
+// workgroups that drew earlier tickets and are therefore running, so the queue is
+// deadlock-free whatever number of workgroups is resident.  The digits are
+// re-derived from the global histograms by whoever needs them (a 2048-bin scan).
+// The last workgroup to leave resets the queue and zeroes the histograms.
+// Five streaming passes over the input by all CUs instead of ~4 by one CU.
+// ----------------------------------------------------------------------------
+struct WideCtrl {
+  uint32_t ticket, exitc, pad0[6];
+  uint32_t done[8];  // items completed per phase
+  uint32_t pad1[48];
+  uint32_t hist[3][2048];
+};
+static_assert(sizeof(WideCtrl) == kWideBytes && kWideBytes % 256 == 0, "topk_layout reserves WideCtrl");
+constexpr int kWidePhases = 5;
+#ifndef CHOCO_WIDE_DEBUG  // printf trace of the fallback queue (diagnostic builds)
+#define CHOCO_WIDE_DEBUG 0
+#endif
+constexpr int kWideU = 4;  // float4 loads per stream per thread in flight
+
+// Queue hand-offs made by ALL lanes of wave 0 (no lane-divergent region inside the
+// ticket loop: with `if (threadIdx.x == 0)` around the atomic and the poll, the
+// compiler split the loop so that wave 0 executed extra barriers -- measured hang).
+CHOCO_DEV uint32_t wave0_fetch_add(uint32_t* p, uint32_t v) {
+  const uint32_t r = __hip_atomic_fetch_add(p, lane_id() == 0 ? v : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_amdgcn_readfirstlane(r);
+}
+CHOCO_DEV void wave0_poll_ge(const uint32_t* p, uint32_t want) {
+  for (uint32_t it = 0; it < (1u << 22); ++it) {
+    if (__builtin_amdgcn_readfirstlane(ld_sc1(p)) >= want) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+CHOCO_DEV constexpr int wide_shift(int r) { return r == 0 ? 20 : (r == 1 ? 9 : 0); }
+CHOCO_DEV constexpr uint32_t wide_mask(int r) { return r == 2 ? 511u : 2047u; }
+
+// Digits 0 .. upto-1 from the global histograms -> (prefix, maskhi, krem).
+CHOCO_DEV void wide_digits(WideCtrl* W, int upto, uint32_t k, ExactSmem& es, uint32_t& prefix, uint32_t& maskhi,
+                           uint32_t& krem) {
+  prefix = 0u;
+  maskhi = 0u;
+  krem = k;
+  for (int r = 0; r < upto; ++r) {
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x) es.hist[i] = ld_sc1(&W->hist[r][i]);
+    __syncthreads();
+    block_find_two(es.hist, krem, 0u, es.scratch, es.bc);
+    const uint32_t bin = es.bc[0];
+    krem = es.bc[1];
+    prefix |= bin << wide_shift(r);
+    maskhi |= wide_mask(r) << wide_shift(r);
+    __syncthreads();
+  }
+}
+
+// The keys (and values) of tile [lo, hi) row by row (a row = 4 consecutive elements
+// per thread, kK4Threads * 4 per row, kWideU rows' loads in flight):
+// fn(i0, n_in, keys[4], vals[4]) for every row, by every thread (block-uniform).
+template <int MODE, bool XH, class F>
+CHOCO_DEV void wide_tile(const Src<MODE, XH>& src, int64_t lo, int64_t hi, F&& fn) {
+  const uint32_t len = (uint32_t)(hi - lo);
+  const __amdgpu_buffer_rsrc_t rx = buf_rsrc(src.x + lo, len * 4u);
+  const __amdgpu_buffer_rsrc_t rh = buf_rsrc((XH ? src.xh : src.x) + lo, len * 4u);
+  constexpr uint32_t kStep = kK4Threads * 4u;
+  for (uint32_t b0 = 0; b0 < len; b0 += kStep * kWideU) {
+    float4 v[kWideU], h[kWideU];
+#pragma unroll
+    for (int u = 0; u < kWideU; ++u) {
+      const uint32_t off = (b0 + (uint32_t)u * kStep + 4u * threadIdx.x) * 4u;
+      if (MODE == kData) {
+        v[u] = ld_buf4<true>(rx, off);
+        if (XH) h[u] = ld_buf4<true>(rh, off);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kWideU; ++u) {
+      if (b0 + (uint32_t)u * kStep >= len) break;  // block-uniform
+      const uint32_t e0 = b0 + (uint32_t)u * kStep + 4u * threadIdx.x;
+      float vv[4] = {0.f, 0.f, 0.f, 0.f};
+      uint32_t kk[4];
+      if (MODE == kData) {
+        const float4 d = XH ? sub4(v[u], h[u]) : v[u];
+        vv[0] = d.x; vv[1] = d.y; vv[2] = d.z; vv[3] = d.w;
+      }
+      const int nin = e0 >= len ? 0 : (int)min(4u, len - e0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int64_t i = lo + e0 + c;
+        if (MODE == kHash && c < nin) vv[c] = src.val(i);
+        kk[c] = c < nin ? src.key_of(i, vv[c]) : 0u;
+      }
+      fn(lo + (int64_t)e0, nin, kk, vv);
+    }
+  }
+}
+
+template <int MODE, bool XH>
+CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
+                             float scale, WideCtrl* W, uint32_t* __restrict__ gcnt, float* __restrict__ out_val,
+                             int32_t* __restrict__ out_idx, int64_t idx_base, ExactSmem& es, uint32_t* s_tk) {
+  const int tid = threadIdx.x;
+  const bool w0 = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;  // wave-uniform
+  for (;;) {
+    if (w0) *s_tk = wave0_fetch_add(&W->ticket, 1u);  // every lane of wave 0 writes the same value
+    __syncthreads();
+    const uint32_t tk = __builtin_amdgcn_readfirstlane(*s_tk);
+    __syncthreads();
+    if (tk >= (uint32_t)kWidePhases * nb) break;  // workgroup-uniform
+    const int phase = (int)(tk / nb);
+    const uint32_t t = tk % nb;
+#if CHOCO_WIDE_DEBUG
+    if (tid == 0) printf("wg %d ticket %u phase %d tile %u done %u %u %u %u %u\n", (int)blockIdx.x, tk, phase, t,
+                         ld_sc1(&W->done[0]), ld_sc1(&W->done[1]), ld_sc1(&W->done[2]), ld_sc1(&W->done[3]),
+                         ld_sc1(&W->done[4]));
+#endif
+    if (phase > 0) {
+      if (w0) wave0_poll_ge(&W->done[phase - 1], nb);
+      __syncthreads();
+    }
+    const int64_t lo = (int64_t)t * tile, hi = min(lo + (int64_t)tile, n);
+    uint32_t prefix, maskhi, krem;
+    wide_digits(W, phase < 3 ? phase : 3, (uint32_t)k, es, prefix, maskhi, krem);
+    if (phase < 3) {
+      const int sh = wide_shift(phase);
+      const uint32_t dm = wide_mask(phase);
+      for (int i = tid; i < 2048; i += kK4Threads) es.hist[i] = 0u;
+      __syncthreads();
+#if CHOCO_WIDE_DEBUG
+      if (tid == 0) printf("wg %d item %u: digits done, tile [%lld, %lld)\n", (int)blockIdx.x, tk, (long long)lo,
+                           (long long)hi);
+#endif
+      const int lane = lane_id();
+      wide_tile(src, lo, hi, [&](int64_t, int nin, const uint32_t (&kk)[4], const float (&)[4]) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          // tie-heavy inputs put most lanes in one bin: the lanes of the wave's first
+          // bin add with one atomic, the rest one by one
+          const bool on = c < nin && (kk[c] & maskhi) == prefix;
+          const uint32_t bin = (kk[c] >> sh) & dm;
+          const uint64_t live = ballot(on);
+          if (live == 0ull) continue;  // wave-uniform
+          const int first = __builtin_ctzll(live);
+          const uint32_t b0 = __builtin_amdgcn_readlane(bin, first);
+          const uint64_t same = ballot(on && bin == b0);
+          if (lane == first) atomicAdd(&es.hist[b0], (uint32_t)__popcll(same));
+          if (on && bin != b0) atomicAdd(&es.hist[bin], 1u);
+        }
+      });
+      __syncthreads();
+#if CHOCO_WIDE_DEBUG
+      if (tid == 0) printf("wg %d item %u: histogram done\n", (int)blockIdx.x, tk);
+#endif
+      for (int i = tid; i < 2048; i += kK4Threads)
+        if (es.hist[i]) __hip_atomic_fetch_add(&W->hist[phase][i], es.hist[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if CHOCO_WIDE_DEBUG
+      if (es.hist[1008] && tid == 1008) printf("wg %d item %u: flushed bin 1008 += %u\n", (int)blockIdx.x, tk, es.hist[1008]);
+      if (tid == 0) printf("wg %d item %u: flush loop done (thread 0)\n", (int)blockIdx.x, tk);
+      __syncthreads();
+      if (tid == 0) printf("wg %d item %u: barrier after flush\n", (int)blockIdx.x, tk);
+#endif
+    } else {
+      const uint32_t T = prefix;  // all digits known: T = the k-th largest key, krem = ties to take
+      const uint32_t r = krem;
+      if (phase == 3) {
+        uint32_t gt = 0, eq = 0;
+        wide_tile(src, lo, hi, [&](int64_t, int nin, const uint32_t (&kk)[4], const float (&)[4]) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            gt += (c < nin && kk[c] > T) ? 1u : 0u;
+            eq += (c < nin && kk[c] == T) ? 1u : 0u;
+          }
+        });
+        uint32_t gtot, etot, gp, ep;
+        block_excl_scan2(gt, eq, es.scratch, &gp, &ep, &gtot, &etot);
+        if (w0) { st_sc1(&gcnt[2 * t], gtot); st_sc1(&gcnt[2 * t + 1], etot); }  // same value from every lane
+      } else {
+        // this tile's output offset and tie start: counts of the tiles before it
+        const bool mine = (uint32_t)tid < nb;
+        const uint32_t gv = mine && (uint32_t)tid < t ? ld_sc1(&gcnt[2 * tid]) : 0u;
+        const uint32_t ev = mine && (uint32_t)tid < t ? ld_sc1(&gcnt[2 * tid + 1]) : 0u;
+        uint32_t gp, ep, gtot, etot;
+        block_excl_scan2(gv, ev, es.scratch, &gp, &ep, &gtot, &etot);
+        const uint32_t taken = min(r, etot);  // ties taken by the earlier tiles
+        uint32_t out = gtot + taken, tie_run = etot;
+        // ordered compaction, row by row: ties by global rank (lowest index first)
+        wide_tile(src, lo, hi, [&](int64_t i0, int nin, const uint32_t (&kk)[4], const float (&vv)[4]) {
+          uint32_t neq = 0;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) neq += (c < nin && kk[c] == T) ? 1u : 0u;
+          uint32_t tp, tt;
+          tp = block_excl_scan(neq, es.scratch, &tt);
+          bool sel[4];
+          uint32_t ns = 0, q = tie_run + tp;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const bool in = c < nin;
+            const bool eqc = in && kk[c] == T;
+            sel[c] = (in && kk[c] > T) || (eqc && q < r);
+            q += eqc ? 1u : 0u;
+            ns += sel[c] ? 1u : 0u;
+          }
+          uint32_t st;
+          uint32_t pos = out + block_excl_scan(ns, es.scratch, &st);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (sel[c]) {
+              out_val[pos] = vv[c] * scale;
+              out_idx[pos] = (int32_t)(i0 + c + idx_base);
+              ++pos;
+            }
+          }
+          out += st;
+          tie_run += tt;
+        });
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (w0) wave0_fetch_add(&W->done[phase], 1u);
+#if CHOCO_WIDE_DEBUG
+    if (tid == 0) printf("wg %d item %u published\n", (int)blockIdx.x, tk);
+#endif
+  }
+  // the last workgroup out resets the queue for the next call
+  if (w0) {
+    const uint32_t e = wave0_fetch_add(&W->exitc, 1u);
+    *s_tk = e == nb - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (*s_tk) {
+    for (int i = tid; i < 3 * 2048; i += kK4Threads) st_sc1(&W->hist[0][0] + i, 0u);
+    if (tid < 8) st_sc1(&W->done[tid], 0u);
+    if (tid == 0) { st_sc1(&W->ticket, 0u); st_sc1(&W->exitc, 0u); }
+  }
+}
+
 template <int MODE, bool XH>
 __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
     uint32_t side_cap, uint64_t seed, float scale, TopkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ cum_tab,
     const uint32_t* __restrict__ cntw, const uint32_t* __restrict__ side, const float* __restrict__ cval,
     const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
-    int64_t idx_base) {
+    int64_t idx_base, WideCtrl* __restrict__ wide, uint32_t* __restrict__ gcnt) {
   __shared__ FinSmem fs;
   __shared__ ExactSmem es;
+  __shared__ uint32_t s_tk;
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
   STAMP(24576 + b, 0);
@@ -1353,11 +1646,10 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   STAMP(26000 + b, 2);
   if (!fallback && fs.G[jstar] - fs.G[jstar + 1] > (uint32_t)kMCap) fallback = true;
   if (fallback) {
-    // the sample's guess was off: exact single-workgroup selection (correct, slow)
-    if (b == 0) {
-      Src<MODE, XH> src{x, xh, seed};
-      block_topk_exact(src, n, k, scale, out_val, out_idx, idx_base, es);
-    }
+    // the sample's guess was off: the exact radix select over the whole input, shared
+    // by every workgroup through the ticketed queue (wide_fallback)
+    Src<MODE, XH> src{x, xh, seed};
+    wide_fallback(src, n, k, tile, nb, scale, wide, gcnt, out_val, out_idx, idx_base, es, &s_tk);
   } else {
     // ---- thread t <-> tile t: bucket-j* key count and side-list offset
     uint32_t above = 0, cb = 0, off = 0;
@@ -1593,7 +1885,7 @@ static FusedLayout fused_layout(int64_t n) {
   L.nb = (uint32_t)((n + tile - 1) / tile);
   L.nchunk = (uint32_t)(tile / kChunk);
   L.side_cap = (uint32_t)std::min<int64_t>(kMaybeCap, tile);
-  size_t o = 0;
+  size_t o = topk_layout(n).off_cum;  // past the fixed header (TopkCtrl + WideCtrl) of every top-k workspace
   L.off_cum = o;   o += align_up((size_t)L.nb * kFB * 4, 256);
   L.off_cntw = o;  o += align_up((size_t)L.nb * L.nchunk * 4, 256);
   L.off_side = o;  o += align_up((size_t)L.nb * L.side_cap * 4, 256);
@@ -1648,34 +1940,6 @@ struct BoundsView {
   uint32_t* scratch;
   uint32_t* bc;
 };
-
-// Hand-offs between workgroups (bounds, tile tables, side lists) use the
-// fence-free form of MI355X_MICROARCH.md "Valid forms": every handed-off word is
-// stored write-through (relaxed agent-scope atomic store = sc1) and read with
-// sc1 loads; each storing wave drains (vmcnt(0)) before a workgroup barrier,
-// behind which one lane adds to the counter; the consumer polls that counter.
-// No release fence: a buffer_wbl2 writes back the whole XCD L2 and cost
-// 10-30 us per tile in the middle of everyone else's stream (measured).
-CHOCO_DEV void st_sc1(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-CHOCO_DEV uint32_t ld_sc1(const uint32_t* p) {
-  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// bounded poll of a counter written by running workgroups (s_sleep between
-// polls); returns when *p >= want
-CHOCO_DEV void poll_ge(const uint32_t* p, uint32_t want) {
-  for (uint32_t it = 0; it < (1u << 26); ++it) {
-    if (ld_sc1(p) >= want) break;
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
-
-// every wave's stores drained, the workgroup joined, one lane adds
-CHOCO_DEV void publish_add(uint32_t* counter) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Over hist[1 << kFSelBits] (ascending), the bin of the rank-th largest entry and
 // the rank inside it -> out[0], out[1]; ends with a barrier.
@@ -2263,7 +2527,8 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   CHOCO_LAUNCHED("topk_stream_kernel");
   profile_begin("topk_finish", st);
   CHOCO_KLAUNCH((topk_finish_kernel<MODE, XH>), dim3(L.nb), dim3(kK4Threads), 0, st, x, xh, n, k, L.tile, L.nb,
-                L.side_cap, seed, scale, ctrl, cum, cntw, side, cval, cidx, out_val, out_idx, idx_base);
+                L.side_cap, seed, scale, ctrl, cum, cntw, side, cval, cidx, out_val, out_idx, idx_base,
+                reinterpret_cast<WideCtrl*>(base + L.off_wide), reinterpret_cast<uint32_t*>(base + L.off_gcnt));
   profile_end("topk_finish", st);
   CHOCO_LAUNCHED("topk_finish_kernel");
   return CHOCO_OK;

@@ -135,6 +135,33 @@ def test_topk_fallback_and_edge_inputs(kind):
     assert same_bits(host(vals), ov)
 
 
+@pytest.mark.parametrize("kind", ["ties", "all_equal", "zeros_xhat"])
+def test_topk_wide_fallback_100M(kind):
+    """The exact fallback at BASELINE size (every K34 workgroup on the ticketed radix
+    select, csrc/topk.hip wide_fallback): tie clusters, an all-equal buffer (side
+    lists overflow), and x == x_hat on most elements (exact zeros), bit-exact against
+    the oracle; run twice so the queue's self-reset is exercised."""
+    from chocosgd_amd import codec
+    n = 100_000_000
+    g = torch.Generator(device=DEV).manual_seed(91)
+    xh = None
+    if kind == "ties":
+        x = torch.round(torch.randn(n, generator=g, device=DEV) * 8) / 8
+    elif kind == "all_equal":
+        x = torch.full((n,), 0.5, device=DEV)
+    else:
+        x = torch.randn(n, generator=g, device=DEV)
+        xh = x.clone()
+        xh[::97] += 1.0  # d = 0 except every 97th element (-1)
+    k = codec.topk_k(n, 0.99)
+    d = host(x) if xh is None else (host(x) - host(xh)).astype(np.float32)
+    ov, oi = O.topk(d, k)
+    for _ in range(2):
+        vals, idx = codec.topk(x, k, xhat=xh)
+        assert np.array_equal(host(idx).astype(np.int64), oi)
+        assert same_bits(host(vals), ov)
+
+
 @pytest.mark.parametrize("layout", ["resnet20_cifar10", "resnet50_imagenet"])
 @pytest.mark.parametrize("ratio", [0.9, 0.99])
 def test_topk_segmented_model_layouts(layout, ratio):
