@@ -163,9 +163,11 @@ class Worker:
             self.msg = torch.empty(2 * self.k, dtype=torch.int32, device=dev)
         elif self.op == "qsgd":
             nbytes = codec.qsgd_packed_bytes(self.n, self.param)
-            self.msg = torch.empty(16 + nbytes, dtype=torch.uint8, device=dev)   # [norm (16 B) | planes]
+            self.msg = torch.zeros(16 + nbytes, dtype=torch.uint8, device=dev)   # [norm (16 B) | planes]
+            self.wire = (self.msg[16:], self.msg[:4].view(torch.float32)[:1])  # compress writes in place
         else:
-            self.msg = torch.empty(4 + codec.sign_words(self.n), dtype=torch.int32, device=dev)
+            self.msg = torch.zeros(4 + codec.sign_words(self.n), dtype=torch.int32, device=dev)
+            self.wire = (self.msg[4:], self.msg[:4].view(torch.float32)[:1])
         self.recv = {r: torch.empty_like(self.msg) for r in self.peers}
         if self.backend == "gloo":
             self.msg_h = torch.empty(self.msg.shape, dtype=self.msg.dtype).pin_memory()
@@ -187,13 +189,9 @@ class Worker:
             self.msg[:self.k].view(torch.float32).copy_(v)
             self.msg[self.k:].copy_(i)
         elif self.op == "qsgd":
-            packed, norms, _ = c.qsgd_compress(self.d, self.param, seed=12345 + self.rank, offset=self.step_id)
-            self.msg[16:].copy_(packed)
-            self.msg[:4].view(torch.float32).copy_(norms)
+            c.qsgd_compress(self.d, self.param, seed=12345 + self.rank, offset=self.step_id, out=self.wire)
         else:
-            packed, norms = c.sign_compress(self.d)
-            self.msg[4:].copy_(packed)
-            self.msg[:1].view(torch.float32).copy_(norms)
+            c.sign_compress(self.d, out=self.wire)
         self.step_id += 1
 
     def compress_step(self):
@@ -207,14 +205,10 @@ class Worker:
             c.topk(self.x, self.k, xhat=self.hat, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]),
                    gossip=g)
         elif self.op == "qsgd":
-            packed, norms, _ = c.qsgd_compress(self.x, self.param, xhat=self.hat, seed=12345 + self.rank,
-                                               offset=self.step_id, gossip=g)
-            self.msg[16:].copy_(packed)
-            self.msg[:4].view(torch.float32).copy_(norms)
+            c.qsgd_compress(self.x, self.param, xhat=self.hat, seed=12345 + self.rank, offset=self.step_id,
+                            gossip=g, out=self.wire)
         else:
-            packed, norms = c.sign_compress(self.x, xhat=self.hat, gossip=g)
-            self.msg[4:].copy_(packed)
-            self.msg[:1].view(torch.float32).copy_(norms)
+            c.sign_compress(self.x, xhat=self.hat, gossip=g, out=self.wire)
 
     def exchange(self):
         if not self.peers:

@@ -326,9 +326,38 @@ def sign_words(n):
     return int(lib().choco_sign_words(int(n)))
 
 
-def sign_compress(x, xhat=None, seg_off=None, nseg=1, want_norms=True, gossip=None):
+def _out_views(out, packed_n, packed_dtype, nseg, dev):
+    """Caller-provided (packed, norms) buffers -- e.g. views into one wire message, so the
+    kernels write the message in place instead of a torch.cat copying it afterwards."""
+    packed, norms = out
+    _require(packed, packed_dtype, "out packed")
+    if packed.numel() != packed_n or packed.device != dev:
+        raise RuntimeError(f"out packed must hold {packed_n} elements on {dev}")
+    if norms is not None:
+        _require(norms, torch.float32, "out norms")
+        if norms.numel() != nseg or norms.device != dev:
+            raise RuntimeError(f"out norms must hold {nseg} floats on {dev}")
+    return packed, norms
+
+
+def wire_header_words(nseg):
+    """int32 words of a wire message's fp32 norms header (16-byte aligned)."""
+    return (int(nseg) + 3) // 4 * 4
+
+
+def sign_wire(n, nseg, dev):
+    """One sign wire message [fp32 norms (16-B padded) | int32 words[N']] and the
+    (packed, norms) views sign_compress(out=...) fills in place (header pad zeroed)."""
+    hw = wire_header_words(nseg)
+    msg = torch.empty(hw + sign_words(n), dtype=torch.int32, device=dev)
+    msg[:hw].zero_()
+    return msg, (msg[hw:], msg[:hw].view(torch.float32)[:nseg])
+
+
+def sign_compress(x, xhat=None, seg_off=None, nseg=1, want_norms=True, gossip=None, out=None):
     """Pack sign bits in the (32, N') layout; optionally per-segment L1 norms (fp64-accumulated).
-    `gossip=(memory, gamma)` fuses the consensus step."""
+    `gossip=(memory, gamma)` fuses the consensus step; `out=(packed int32[N'], norms f32[nseg])`
+    writes into caller buffers."""
     _require(x, torch.float32, "x")
     if xhat is not None:
         _require(xhat, torch.float32, "xhat")
@@ -337,8 +366,11 @@ def sign_compress(x, xhat=None, seg_off=None, nseg=1, want_norms=True, gossip=No
     n = x.numel()
     dev = x.device
     L = lib()
-    packed = torch.empty(sign_words(n), dtype=torch.int32, device=dev)
-    norms = torch.empty(nseg, dtype=torch.float32, device=dev) if want_norms else None
+    if out is not None:
+        packed, norms = _out_views(out, sign_words(n), torch.int32, nseg, dev)
+    else:
+        packed = torch.empty(sign_words(n), dtype=torch.int32, device=dev)
+        norms = torch.empty(nseg, dtype=torch.float32, device=dev) if want_norms else None
     ws = workspace(dev, "acc", L.choco_sign_workspace_size(nseg))
     g = _gossip(gossip, x, xhat)
     if g is not None:
@@ -460,10 +492,20 @@ def qsgd_packed_bytes(n, q):
     return int(lib().choco_qsgd_packed_bytes(int(n), int(q)))
 
 
+def qsgd_wire(n, q, nseg, dev):
+    """One QSGD wire message [fp32 norms (16-B padded) | level plane | sign plane] (uint8)
+    and the (packed, norms) views qsgd_compress(out=...) fills in place (header pad zeroed)."""
+    hb = 4 * wire_header_words(nseg)
+    msg = torch.empty(hb + qsgd_packed_bytes(n, q), dtype=torch.uint8, device=dev)
+    msg[:hb].zero_()
+    return msg, (msg[hb:], msg[:hb].view(torch.float32)[:nseg])
+
+
 def qsgd_compress(x, q, is_biased=False, xhat=None, seg_off=None, nseg=1, norm_in=None, u_in=None,
-                  seed=0, offset=0, want_dense=False, gossip=None):
+                  seed=0, offset=0, want_dense=False, gossip=None, out=None):
     """QSGD with s = 2^q - 1.  Returns (packed uint8, norms f32[nseg], dense f32[n] or None).
-    `gossip=(memory, gamma)` fuses the consensus step (device norms and uniforms only)."""
+    `gossip=(memory, gamma)` fuses the consensus step (device norms and uniforms only);
+    `out=(packed uint8[qsgd_packed_bytes], norms f32[nseg])` writes into caller buffers."""
     _require(x, torch.float32, "x")
     if xhat is not None:
         _require(xhat, torch.float32, "xhat")
@@ -478,8 +520,13 @@ def qsgd_compress(x, q, is_biased=False, xhat=None, seg_off=None, nseg=1, norm_i
     n = x.numel()
     dev = x.device
     L = lib()
-    packed = torch.empty(qsgd_packed_bytes(n, q), dtype=torch.uint8, device=dev)
-    norms = torch.empty(nseg, dtype=torch.float32, device=dev)
+    if out is not None:
+        packed, norms = _out_views(out, qsgd_packed_bytes(n, q), torch.uint8, nseg, dev)
+        if norms is None:
+            raise RuntimeError("out norms is required")
+    else:
+        packed = torch.empty(qsgd_packed_bytes(n, q), dtype=torch.uint8, device=dev)
+        norms = torch.empty(nseg, dtype=torch.float32, device=dev)
     dense = torch.empty(n, dtype=torch.float32, device=dev) if want_dense else None
     ws = workspace(dev, "acc", L.choco_qsgd_workspace_size(nseg))
     g = _gossip(gossip, x, xhat)

@@ -281,26 +281,47 @@ CHOCO_DEV int seg_of(const int64_t* __restrict__ seg_off, int nseg, int64_t e) {
 // function of the splitmix64 generator, used in counter mode -- the value at
 // counter c of stream `key` is mix(key + (c + 1) * gamma), exactly the
 // generator's own sequence from state `key`.  Integer multiplies are quarter
-// rate on CDNA: two 64-bit mixes per 4 uniforms cost ~3x less VALU time than
-// Philox4x32-10 (40 32-bit multiplies per 4 uniforms), which made the QSGD
-// quantize pass ALU-bound.
+// rate on CDNA (Philox4x32-10 spends 40 32-bit multiplies per 4 uniforms), so
+// SplitMix64 only keys the streams and seeds xoroshiro128+ below.
 constexpr uint64_t kGoldenGamma = 0x9E3779B97F4A7C15ull;
 CHOCO_DEV __host__ uint64_t splitmix64_mix(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
-// QSGD uniform stream of (seed, offset): key = mix(seed + (offset + 1) * 0xD1B54A32D192ED03);
-// elements 2p and 2p+1 take bits 63..40 and 31..8 of mix(key + (p + 1) * gamma), * 2^-24.
+// QSGD uniform stream of (seed, offset): key = mix(seed + (offset + 1) * 0xD1B54A32D192ED03).
 CHOCO_DEV __host__ uint64_t qrng_key(uint64_t seed, uint64_t offset) {
   return splitmix64_mix(seed + (offset + 1) * 0xD1B54A32D192ED03ull);
 }
 CHOCO_DEV float u24(uint32_t b24) { return (float)b24 * 5.9604644775390625e-08f; }
-CHOCO_DEV void qrng_pair(uint64_t key, uint64_t p, float& u0, float& u1) {
-  const uint64_t z = splitmix64_mix(key + (p + 1) * kGoldenGamma);
-  u0 = u24((uint32_t)(z >> 40));
-  u1 = u24((uint32_t)(z >> 8) & 0xFFFFFFu);
-}
+
+// The uniforms themselves come from xoroshiro128+ (Blackman & Vigna 2018, the
+// a=24 b=16 c=37 parameters) run for 16 steps per 32-element STREAM, its state
+// seeded by SplitMix64 as its authors prescribe: stream `sid` starts at
+// (mix(key + (2 sid + 1) gamma), mix(key + (2 sid + 2) gamma)).  One step (two
+// 64-bit adds/xors/rotates, no multiply) yields two uniforms: bits 63..40 and
+// 39..16 of s0 + s1, * 2^-24.  Amortising the seeding over 32 elements takes the
+// generator from ~20 to ~8 VALU operations per element (the quantize pass is
+// VALU-bound).  Stream of element e (qsgd.hip kQStreamTile): tile T = e >> 13,
+// o = e & 8191, sid = (T << 8) | ((o >> 3) & 255), position (o >> 11) * 8 + (o & 7).
+CHOCO_DEV __host__ uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+struct Xoro128 {
+  uint64_t s0, s1;
+  CHOCO_DEV void seed(uint64_t key, uint64_t sid) {
+    const uint64_t z = key + (2 * sid + 1) * kGoldenGamma;
+    s0 = splitmix64_mix(z);
+    s1 = splitmix64_mix(z + kGoldenGamma);
+  }
+  // next output; u0/u1 = its two 24-bit uniforms
+  CHOCO_DEV void next2(float& u0, float& u1) {
+    const uint64_t a = s0, r = a + s1, t = s1 ^ a;
+    s0 = rotl64(a, 24) ^ t ^ (t << 16);
+    s1 = rotl64(t, 37);
+    const uint32_t hi = (uint32_t)(r >> 32), lo = (uint32_t)r;
+    u0 = u24(hi >> 8);
+    u1 = u24(__builtin_amdgcn_alignbit(hi, lo, 16) & 0xFFFFFFu);
+  }
+};
 
 // Seeded 32-bit bijective mixer used as the random-k ranking key
 // (murmur3 fmix32 of a seeded Weyl sequence).

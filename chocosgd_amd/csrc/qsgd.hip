@@ -297,13 +297,105 @@ CHOCO_DEV int tile_seg(const int64_t* __restrict__ seg_off, int nseg, int64_t e0
   return s_seg[0];
 }
 
-// 8 elements per thread: one 4*CW-bit level store and one sign byte.  Measured
-// against a wave-batch form that transposes the outputs through LDS into 16-B
-// level / 4-B sign stores per lane: 123 vs 135 us at 100M in the bench step --
-// this pass is bound by the stream (and by the write-back of the dirty lines
-// the previous step's receiver left in the Infinity Cache), not by its stores.
-// Its VALU work is dominated by the uniforms: SplitMix64 (choco_common.h) took
-// the pass from 126 to 123 us against Philox4x32-10.
+// s * |d| / norm, correctly rounded, without the IEEE division expansion per
+// element.  With y = RN(1/norm) (one real division per thread) and q0 = RN(t * y)
+// (within one ulp of t / norm), r = fma(-q0, norm, t) is exact and
+// RN(q0 + r * y) is RN(t / norm) (Markstein's theorem) as long as nothing
+// underflows or overflows: the fast form is taken for norm in [2^-30, 2^96] and
+// q0 in [2^-60, 2^7] (then t >= 2^-90 and r stays normal), zeros give +0 as
+// 0/norm does, and everything else (tiny quotients, NaN/inf, extreme norms, a
+// pinned norm below |d|) takes the real division.  Checked against fp32 division on 3e9 (t, norm) pairs (random over
+// the guarded range + exhaustive t for 12 norm mantissas) and bit-exact against
+// the oracle in the GPU tests.
+struct QDiv {
+  float norm, y;
+  bool fast;
+  CHOCO_DEV void init(float nrm) {
+    norm = nrm;
+    y = 1.0f / nrm;
+    fast = nrm >= 0x1p-30f && nrm <= 0x1p96f;
+  }
+  // returns t / norm; *slow set when this element needs the real division
+  CHOCO_DEV float quot(float t, bool& slow) const {
+    const float q0 = t * y;
+    const float r = fmaf(-q0, norm, t);
+    slow = !(fast && ((q0 >= 0x1p-60f && q0 <= 0x1p7f) || t == 0.0f));
+    return t == 0.0f ? 0.0f : fmaf(r, y, q0);
+  }
+};
+
+// One quantized element: level (clamped container value, 0 for NaN), sign bit.
+CHOCO_DEV float qlevel(float lf, float u) {
+  const float pl = floorf(lf);                                // previous_level
+  return pl + ((u < (lf - pl)) ? 1.0f : 0.0f);                // + is_next_level
+}
+
+// Quantize + pack.  A 256-thread workgroup owns an 8192-element tile; thread t
+// owns the four 8-element groups t_e0 + g*2048 + 8t (g = 0..3): one 4*CW-bit
+// level store and one sign byte per group (the wire of the decode kernel),
+// two float4 loads per group, all eight in flight before any arithmetic.  The
+// thread's 32 elements are one uniform stream (xoroshiro128+, choco_common.h).
+// VALU-bound, not HBM-bound, in its round-1 form (SplitMix64 per pair + the
+// IEEE division per element: 123 us at 100M with the tail re-read from the
+// Infinity Cache); see DESIGN.md §4 for the measured steps.
+constexpr int kQG = 4;                                  // groups per thread
+constexpr int kQStreamTile = kQThreads * kQPer * kQG;   // 8192 elements per workgroup
+static_assert(kQStreamTile == 8192, "the uniform-stream mapping (choco_common.h) assumes 8192-element tiles");
+
+// A tile that crosses a segment boundary or ends the buffer: element by element,
+// in stream order (the same uniforms as the fast path), per-element segment
+// parameters and the real division.  Kept out of line: it is rare and would
+// otherwise unroll into the hot kernel.
+template <int CW>
+__device__ __noinline__ void qsgd_quant_tile_slow(const float* __restrict__ x, const float* __restrict__ xh, int64_t n,
+                                                  const int64_t* __restrict__ seg_off, int nseg, int s_levels,
+                                                  int biased, const float* __restrict__ norms,
+                                                  const float* __restrict__ u_in, uint64_t seed, uint64_t offset,
+                                                  uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
+                                                  float* __restrict__ dense_out, int64_t tile, int sg0) {
+  const float sf = (float)s_levels;
+  const uint32_t smax = (uint32_t)s_levels;
+  const int64_t eb = tile * kQStreamTile + (int64_t)threadIdx.x * kQPer;
+  Xoro128 rng;
+  if (!u_in) rng.seed(qrng_key(seed, offset), ((uint64_t)tile << 8) | threadIdx.x);
+  int s = sg0;
+#pragma unroll 1
+  for (int g = 0; g < kQG; ++g) {
+    const int64_t e0 = eb + (int64_t)g * kQThreads * kQPer;
+    uint64_t lacc[2] = {0, 0};  // 8 * CW <= 128 level bits
+    uint32_t sbits = 0;
+#pragma unroll 1
+    for (int c = 0; c < kQPer; c += 2) {
+      float uu[2];
+      if (!u_in) rng.next2(uu[0], uu[1]);
+      for (int h = 0; h < 2; ++h) {
+        const int64_t e = e0 + c + h;
+        if (e >= n) continue;
+        if (u_in) uu[h] = u_in[e];
+        while (s + 1 < nseg && seg_off[s + 1] <= e) ++s;
+        const QParam Q = qparam(norms, seg_off, n, s, s_levels, biased != 0);
+        const float dv = dval(x, xh, e);
+        const float lvl = qlevel((sf * fabsf(dv)) / Q.norm, uu[h]);  // s * x.abs() / norm
+        const uint32_t li = lvl == lvl ? (lvl >= sf ? smax : (uint32_t)lvl) : 0u;
+        const int bp = (c + h) * CW;
+        if (bp < 64) lacc[0] |= (uint64_t)li << bp; else lacc[1] |= (uint64_t)li << (bp - 64);
+        sbits |= dv < 0.f ? (1u << (c + h)) : 0u;
+        if (dense_out) {
+          const float sg = dv > 0.f ? 1.0f : (dv < 0.f ? -1.0f : 0.0f);  // torch.sign (NaN -> 0)
+          dense_out[e] = (((Q.scale * sg) * Q.norm) * lvl) / sf;
+        }
+      }
+    }
+    if (e0 >= n) break;
+    uint32_t lv[kQPer];
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c)
+      lv[c] = (uint32_t)(c * CW < 64 ? lacc[0] >> (c * CW) : lacc[1] >> (c * CW - 64)) & ((1u << CW) - 1u);
+    store_levels<CW>(lvl_plane, e0 / kQPer, lv);
+    sign_plane[e0 / kQPer] = (uint8_t)sbits;
+  }
+}
+
 template <int CW>
 __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, const int64_t* __restrict__ seg_off,
@@ -312,8 +404,8 @@ __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
     float* __restrict__ dense_out, int64_t ntiles) {
   __shared__ int s_seg[2];
   const int64_t tile = ntiles - 1 - (int64_t)blockIdx.x;  // reverse walk: Infinity-Cache hits
-  const int64_t t_e0 = tile * kQTile;
-  const int64_t t_e1 = std::min<int64_t>(t_e0 + kQTile, n);
+  const int64_t t_e0 = tile * kQStreamTile;
+  const int64_t t_e1 = std::min<int64_t>(t_e0 + kQStreamTile, n);
   const int sg0 = tile_seg(seg_off, nseg, t_e0, t_e1, s_seg);
   const bool uniform = s_seg[1] == sg0;
   if (tile == ntiles - 1) {
@@ -324,68 +416,95 @@ __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
     for (int64_t b = lvl_used + threadIdx.x; b < lvl_end; b += kQThreads) lvl_plane[b] = 0;
     for (int64_t b = sgn_used + threadIdx.x; b < sgn_end; b += kQThreads) sign_plane[b] = 0;
   }
-  const int64_t e0 = t_e0 + (int64_t)threadIdx.x * kQPer;
-  if (e0 >= n) return;
   const float sf = (float)s_levels;
   const uint32_t smax = (uint32_t)s_levels;
-  float d[kQPer];
-  if (e0 + kQPer <= n) {
-    const float4 a0 = ld_quant4(x + e0);  // the delta's last read (the norm pass read it first)
-    const float4 a1 = ld_quant4(x + e0 + 4);
-    d[0] = a0.x; d[1] = a0.y; d[2] = a0.z; d[3] = a0.w; d[4] = a1.x; d[5] = a1.y; d[6] = a1.z; d[7] = a1.w;
-    if (xh) {
-      const float4 h0 = ld_quant4(xh + e0);
-      const float4 h1 = ld_quant4(xh + e0 + 4);
-      d[0] -= h0.x; d[1] -= h0.y; d[2] -= h0.z; d[3] -= h0.w;
-      d[4] -= h1.x; d[5] -= h1.y; d[6] -= h1.z; d[7] -= h1.w;
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < kQPer; ++c) d[c] = (e0 + c < n) ? dval(x, xh, e0 + c) : 0.f;
+  const int64_t eb = t_e0 + (int64_t)threadIdx.x * kQPer;  // group g starts at eb + g * 2048
+  constexpr int GS = kQThreads * kQPer;                    // 2048
+  if (!uniform || t_e1 - t_e0 != kQStreamTile) {
+    qsgd_quant_tile_slow<CW>(x, xh, n, seg_off, nseg, s_levels, biased, norms, u_in, seed, offset, lvl_plane,
+                             sign_plane, dense_out, tile, sg0);
+    return;
   }
-  float u[kQPer];
+  // full one-segment tile: unconditional loads, all in flight (the delta's last
+  // read: the norm pass read it first)
+  float d[kQG][kQPer];
+  {
+    float4 a[kQG][2];
+#pragma unroll
+    for (int g = 0; g < kQG; ++g) {
+      a[g][0] = ld_quant4(x + eb + g * GS);
+      a[g][1] = ld_quant4(x + eb + g * GS + 4);
+    }
+    if (xh) {
+#pragma unroll
+      for (int g = 0; g < kQG; ++g) {
+        const float4 h0 = ld_quant4(xh + eb + g * GS), h1 = ld_quant4(xh + eb + g * GS + 4);
+        a[g][0] = sub4(a[g][0], h0);
+        a[g][1] = sub4(a[g][1], h1);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < kQG; ++g) {
+      d[g][0] = a[g][0].x; d[g][1] = a[g][0].y; d[g][2] = a[g][0].z; d[g][3] = a[g][0].w;
+      d[g][4] = a[g][1].x; d[g][5] = a[g][1].y; d[g][6] = a[g][1].z; d[g][7] = a[g][1].w;
+    }
+  }
+  float u[kQG][kQPer];
   if (u_in) {
 #pragma unroll
-    for (int c = 0; c < kQPer; ++c) u[c] = (e0 + c < n) ? u_in[e0 + c] : 0.f;
-  } else {
-    const uint64_t key = qrng_key(seed, offset);
-    const uint64_t p = (uint64_t)e0 >> 1;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) qrng_pair(key, p + h, u[2 * h], u[2 * h + 1]);
-  }
-  QParam P = qparam(norms, seg_off, n, sg0, s_levels, biased != 0);
-  uint32_t lv[kQPer];
-  uint32_t sbits = 0;
-  float outv[kQPer];
-#pragma unroll
-  for (int c = 0; c < kQPer; ++c) {
-    const int64_t e = e0 + c;
-    if (!uniform && e < n) {
-      int s = sg0;
-      while (s + 1 < nseg && seg_off[s + 1] <= e) ++s;
-      P = qparam(norms, seg_off, n, s, s_levels, biased != 0);
+    for (int g = 0; g < kQG; ++g) {
+      const float4 u0 = *reinterpret_cast<const float4*>(u_in + eb + g * GS);
+      const float4 u1 = *reinterpret_cast<const float4*>(u_in + eb + g * GS + 4);
+      u[g][0] = u0.x; u[g][1] = u0.y; u[g][2] = u0.z; u[g][3] = u0.w;
+      u[g][4] = u1.x; u[g][5] = u1.y; u[g][6] = u1.z; u[g][7] = u1.w;
     }
-    const float a = fabsf(d[c]);
-    const float lf = (sf * a) / P.norm;            // s * x.abs() / norm
-    const float pl = floorf(lf);                   // previous_level
-    const float lvl = pl + ((u[c] < (lf - pl)) ? 1.0f : 0.0f);  // + is_next_level
-    const float sg = d[c] > 0.f ? 1.0f : (d[c] < 0.f ? -1.0f : 0.0f);  // torch.sign (NaN -> 0)
-    outv[c] = (((P.scale * sg) * P.norm) * lvl) / sf;
-    uint32_t li = 0;
-    if (lvl == lvl && e < n) li = lvl >= (float)smax ? smax : (uint32_t)lvl;
-    lv[c] = li;
-    sbits |= (d[c] < 0.f && e < n) ? (1u << c) : 0u;
+  } else {
+    Xoro128 rng;
+    rng.seed(qrng_key(seed, offset), ((uint64_t)tile << 8) | threadIdx.x);
+#pragma unroll
+    for (int g = 0; g < kQG; ++g)
+#pragma unroll
+      for (int c = 0; c < kQPer; c += 2) rng.next2(u[g][c], u[g][c + 1]);
   }
-  const int64_t t = e0 / kQPer;
-  store_levels<CW>(lvl_plane, t, lv);
-  sign_plane[t] = (uint8_t)sbits;
-  if (dense_out) {
-    if (e0 + kQPer <= n) {
+  const QParam P = qparam(norms, seg_off, n, sg0, s_levels, biased != 0);
+  QDiv D;
+  D.init(P.norm);
+  const bool dense = dense_out != nullptr;
+#pragma unroll
+  for (int g = 0; g < kQG; ++g) {
+    const int64_t e0 = eb + g * GS;
+    float lf[kQPer];
+    bool slow[kQPer];
+    bool any = false;
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) {
+      lf[c] = D.quot(sf * fabsf(d[g][c]), slow[c]);  // s * x.abs() / norm
+      any |= slow[c];
+    }
+    if (__builtin_expect(__ballot(any) != 0, 0)) {
+#pragma unroll
+      for (int c = 0; c < kQPer; ++c)
+        if (slow[c]) lf[c] = (sf * fabsf(d[g][c])) / P.norm;
+    }
+    uint32_t lv[kQPer];
+    uint32_t sbits = 0;
+    float outv[kQPer];
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) {
+      const float lvl = qlevel(lf[c], u[g][c]);
+      if (dense) {
+        const float sg = d[g][c] > 0.f ? 1.0f : (d[g][c] < 0.f ? -1.0f : 0.0f);  // torch.sign (NaN -> 0)
+        outv[c] = (((P.scale * sg) * P.norm) * lvl) / sf;
+      }
+      lv[c] = lvl == lvl ? (lvl >= sf ? smax : (uint32_t)lvl) : 0u;
+      sbits |= d[g][c] < 0.f ? (1u << c) : 0u;
+    }
+    const int64_t t = e0 / kQPer;
+    store_levels<CW>(lvl_plane, t, lv);
+    sign_plane[t] = (uint8_t)sbits;
+    if (dense) {
       *reinterpret_cast<float4*>(dense_out + e0) = make_float4(outv[0], outv[1], outv[2], outv[3]);
       *reinterpret_cast<float4*>(dense_out + e0 + 4) = make_float4(outv[4], outv[5], outv[6], outv[7]);
-    } else {
-      for (int c = 0; c < kQPer; ++c)
-        if (e0 + c < n) dense_out[e0 + c] = outv[c];
     }
   }
 }
@@ -406,6 +525,19 @@ CHOCO_DEV float qdecode(uint32_t level, bool neg, const QParam& P, float sf) {
   const float lvl = (P.norm == 0.0f) ? __int_as_float(0x7fc00000) : (float)level;  // ref: 0/0 -> NaN
   const float sg = neg ? -1.0f : 1.0f;
   return (((P.scale * sg) * P.norm) * lvl) / sf;
+}
+
+#ifndef CHOCO_QDEC_ST_NT  // non-temporal x_hat / memory stores in the decode (A/B knob)
+#define CHOCO_QDEC_ST_NT 0
+#endif
+CHOCO_DEV void st_dec4(float* p, float4 v) {
+  if (CHOCO_QDEC_ST_NT) {
+    choco_f32x4 f;
+    f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
+    __builtin_nontemporal_store(f, reinterpret_cast<choco_f32x4*>(p));
+  } else {
+    *reinterpret_cast<float4*>(p) = v;
+  }
 }
 
 // MODE 0: out = decode(msg 0); MODE 1: accumulate all messages into hat/mem.
@@ -474,11 +606,11 @@ __global__ __launch_bounds__(kQThreads) void qsgd_decode_kernel(QMsgs M, int64_t
   }
   float* dst = MODE == 0 ? hat : mem;  // MODE 0 writes the decoded floats to `hat` (= out)
   if (full) {
-    *reinterpret_cast<float4*>(dst + e0) = make_float4(mv[0], mv[1], mv[2], mv[3]);
-    *reinterpret_cast<float4*>(dst + e0 + 4) = make_float4(mv[4], mv[5], mv[6], mv[7]);
+    st_dec4(dst + e0, make_float4(mv[0], mv[1], mv[2], mv[3]));
+    st_dec4(dst + e0 + 4, make_float4(mv[4], mv[5], mv[6], mv[7]));
     if (has_self) {
-      *reinterpret_cast<float4*>(hat + e0) = make_float4(hv[0], hv[1], hv[2], hv[3]);
-      *reinterpret_cast<float4*>(hat + e0 + 4) = make_float4(hv[4], hv[5], hv[6], hv[7]);
+      st_dec4(hat + e0, make_float4(hv[0], hv[1], hv[2], hv[3]));
+      st_dec4(hat + e0 + 4, make_float4(hv[4], hv[5], hv[6], hv[7]));
     }
   } else {
     for (int c = 0; c < kQPer; ++c) {
@@ -581,7 +713,7 @@ static int qsgd_compress(const float* x, const float* xhat, int64_t n, const int
   }
   uint8_t* lvl_plane = packed;
   uint8_t* sign_plane = packed + plane_bytes(n, cw);
-  const int64_t ntiles = (n + kQTile - 1) / kQTile;
+  const int64_t ntiles = (n + kQStreamTile - 1) / kQStreamTile;
   profile_begin("qsgd_quantize", st);
 #define CHOCO_Q(CWV)                                                                                          \
   case CWV:                                                                                                   \

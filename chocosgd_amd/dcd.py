@@ -97,28 +97,27 @@ class _ConsumerBase(object):
             message = d.contiguous().view(torch.uint8)
             dense = d
         else:
-            packed, norms, dense = codec.qsgd_compress(x, q, is_biased=self.is_biased, xhat=xh, seg_off=lay.seg_off,
-                                                       nseg=lay.nseg, seed=_draw_seed(), want_dense=want_dense)
-            header = torch.zeros(_hdr_words(lay.nseg), dtype=torch.float32, device=x.device)
-            header[:lay.nseg] = norms
-            message = torch.cat([header.view(torch.uint8), packed])
+            message, out = codec.qsgd_wire(lay.n, q, lay.nseg, x.device)  # written in place by the kernels
+            _, _, dense = codec.qsgd_compress(x, q, is_biased=self.is_biased, xhat=xh, seg_off=lay.seg_off,
+                                              nseg=lay.nseg, seed=_draw_seed(), want_dense=want_dense, out=out)
         sync_buffer["flatten_updates"] = TensorBuffer.from_flat(message, [(message.numel(),)])
         sync_buffer["n_bits"] = get_n_bits(x) * self.quantize_level / 32  # nominal, as the reference
         sync_buffer["n_bits_wire"] = 8 * message.numel()
         return dense
 
     def _sign_message(self, sync_buffer, x, xh, lay):
-        signs, norms = codec.sign_compress(x, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg, want_norms=True)
+        message, (signs, norms) = codec.sign_wire(lay.n, lay.nseg, x.device)  # written in place by the kernels
+        codec.sign_compress(x, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg, want_norms=True, out=(signs, norms))
+        sync_buffer["sign_message"] = message
         sync_buffer["signs"] = signs
         sync_buffer["sign_size"] = torch.Size([lay.n])
         sync_buffer["n_bits"] = get_n_bits(norms) + get_n_bits(signs)
         return signs, norms
 
-    def _sign_wire(self, norms, signs):
-        hw = _hdr_words(norms.numel())
-        header = torch.zeros(hw, dtype=torch.float32, device=signs.device)
-        header[:norms.numel()] = norms
-        return torch.cat([header.view(torch.int32), signs])
+    @staticmethod
+    def _sign_wire(sync_buffer):
+        """[norms | signs]: the norms and signs of _sign_message are views of this one message."""
+        return sync_buffer["sign_message"]
 
     @staticmethod
     def _sign_parts(synced, nseg):
@@ -201,7 +200,7 @@ class DCDSignCompressor(_ConsumerBase):
 
     def sync(self, sync_buffer):
         norms = sync_buffer["flatten_norms"].buffer
-        synced = self._send(self._sign_wire(norms, sync_buffer["signs"]))
+        synced = self._send(self._sign_wire(sync_buffer))
         sync_buffer["synced_message"] = synced
         sync_buffer["synced_flatten_norms"], sync_buffer["synced_signs"] = self._sign_parts(synced, norms.numel())
 

@@ -154,7 +154,7 @@ class DeepSqueezeSignCompressor(_DeepSqueezeBase):
 
     def sync(self, sync_buffer):
         norms = sync_buffer["param_norms_tb"].buffer
-        synced = self._send(self._sign_wire(norms, sync_buffer["signs"]))
+        synced = self._send(self._sign_wire(sync_buffer))
         sync_buffer["synced_message"] = synced
         sync_buffer["synced_param_norms"], sync_buffer["synced_signs"] = self._sign_parts(synced, norms.numel())
 

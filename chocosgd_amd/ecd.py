@@ -117,7 +117,7 @@ class ECDSignCompressor(_ECDBase):
 
     def sync(self, sync_buffer):
         norms = sync_buffer["flatten_norms"].buffer
-        synced = self._send(self._sign_wire(norms, sync_buffer["signs"]))
+        synced = self._send(self._sign_wire(sync_buffer))
         sync_buffer["synced_message"] = synced
         sync_buffer["synced_flatten_norms"], sync_buffer["synced_signs"] = self._sign_parts(synced, norms.numel())
 

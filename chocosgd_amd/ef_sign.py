@@ -38,20 +38,19 @@ class EFSignCompressor(object):
     def compress(self, grads_tb):
         g = grads_tb.buffer
         lay = self._layout(grads_tb)
-        signs, norms = codec.sign_compress(g, seg_off=lay.seg_off, nseg=lay.nseg, want_norms=True)
+        message, (signs, norms) = codec.sign_wire(lay.n, lay.nseg, g.device)  # written in place by the kernels
+        codec.sign_compress(g, seg_off=lay.seg_off, nseg=lay.nseg, want_norms=True, out=(signs, norms))
         local = codec.sign_local_decode(g, norms, seg_off=lay.seg_off, nseg=lay.nseg)
         return {"grad_norms_tb": TensorBuffer.from_flat(norms, [() for _ in range(lay.nseg)]),
                 "grads_tb": grads_tb,
                 "synced_grads_tb": TensorBuffer.from_flat(local, grads_tb._tensors_sizes),
-                "signs": signs, "sign_size": torch.Size([lay.n]),
+                "signs": signs, "sign_message": message, "sign_size": torch.Size([lay.n]),
                 "n_bits": get_n_bits(norms) + get_n_bits(signs)}
 
     def sync(self, sync_buffer):
         norms = sync_buffer["grad_norms_tb"].buffer
         hw = _hdr_words(norms.numel())
-        header = torch.zeros(hw, dtype=torch.float32, device=norms.device)
-        header[:norms.numel()] = norms
-        message = torch.cat([header.view(torch.int32), sync_buffer["signs"]])
+        message = sync_buffer["sign_message"]  # [norms | signs]: written in place by compress
         if self.comm_device == "cpu":
             message = message.cpu().pin_memory()
         synced = self.aggregator_fn._agg(message, communication_scheme="all_gather", async_op=False)

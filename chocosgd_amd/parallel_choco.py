@@ -69,9 +69,7 @@ class _Layout:
         return p
 
 
-def _hdr_words(nseg):
-    """int32 words reserved for the fp32 norms header (16-byte aligned)."""
-    return (nseg + 3) // 4 * 4
+_hdr_words = codec.wire_header_words  # int32 words of the fp32 norms header (16-byte aligned)
 
 
 class CHOCOCompressor(object):
@@ -220,18 +218,15 @@ class CHOCOQuantizationCompressor(_CHOCOBase):
     def compress(self, sync_buffer):
         x, xh, lay = self._flat_inputs(sync_buffer)
         q = int(self.quantize_level)
-        hw = _hdr_words(lay.nseg)
         g = self._gossip(sync_buffer)
         if q == 32:  # the reference sends the raw delta (sparsification.py:118-119)
             if g is not None:
                 codec.gossip_step(x, g[0], xh, g[1])
             message = torch.sub(x, xh).view(torch.uint8)
         else:
-            packed, norms, _ = codec.qsgd_compress(x, q, is_biased=self.is_biased, xhat=xh, seg_off=lay.seg_off,
-                                                   nseg=lay.nseg, seed=_draw_seed(), gossip=g)
-            header = torch.zeros(hw, dtype=torch.float32, device=x.device)
-            header[:lay.nseg] = norms
-            message = torch.cat([header.view(torch.uint8), packed])
+            message, out = codec.qsgd_wire(lay.n, q, lay.nseg, x.device)  # written in place by the kernels
+            codec.qsgd_compress(x, q, is_biased=self.is_biased, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg,
+                                seed=_draw_seed(), gossip=g, out=out)
         sync_buffer["flatten_updates"] = TensorBuffer.from_flat(message, [(message.numel(),)])
         # nominal bits as in parallel_choco_v.py:393
         sync_buffer["n_bits"] = get_n_bits(x) * self.quantize_level / 32
@@ -271,8 +266,10 @@ class CHOCOSignCompressor(_CHOCOBase):
 
     def compress(self, sync_buffer):
         x, xh, lay = self._flat_inputs(sync_buffer)
-        signs, norms = codec.sign_compress(x, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg, want_norms=True,
-                                           gossip=self._gossip(sync_buffer))
+        message, (signs, norms) = codec.sign_wire(lay.n, lay.nseg, x.device)  # written in place by the kernels
+        codec.sign_compress(x, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg, want_norms=True,
+                            gossip=self._gossip(sync_buffer), out=(signs, norms))
+        sync_buffer["sign_message"] = message
         sync_buffer["flatten_norms"] = TensorBuffer.from_flat(norms, [() for _ in range(lay.nseg)])
         sync_buffer["flatten_directions"] = None  # the delta is never materialised (fused)
         sync_buffer["signs"] = signs
@@ -284,9 +281,7 @@ class CHOCOSignCompressor(_CHOCOBase):
         norms = sync_buffer["flatten_norms"].buffer
         signs = sync_buffer["signs"]
         hw = _hdr_words(norms.numel())
-        header = torch.zeros(hw, dtype=torch.float32, device=signs.device)
-        header[:norms.numel()] = norms
-        message = torch.cat([header.view(torch.int32), signs])
+        message = sync_buffer["sign_message"]  # [norms | signs]: the two buffers above are views of it
         reqs, synced = self._send(sync_buffer, message)
         sync_buffer["sync_reqs_1"] = reqs
         sync_buffer["sync_reqs_2"] = []

@@ -373,6 +373,49 @@ def test_splitmix64_known_answer():
     assert u.dtype == np.float32 and np.all((u >= 0) & (u < 1))
 
 
+def _xoro_scalar_stream(key, sid, count):
+    """xoroshiro128+ written out sequentially in Python ints (Blackman & Vigna 2018,
+    a=24 b=16 c=37), seeded by two SplitMix64 outputs: an independent restatement of the
+    vectorised oracle form."""
+    M = (1 << 64) - 1
+
+    def mix(z):
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return z ^ (z >> 31)
+
+    def rotl(x, k):
+        return ((x << k) | (x >> (64 - k))) & M
+    z = (key + (2 * sid + 1) * O.GAMMA) & M
+    s0, s1 = mix(z), mix((z + O.GAMMA) & M)
+    out = []
+    for _ in range(count):
+        out.append((s0 + s1) & M)
+        t = s1 ^ s0
+        s0 = rotl(s0, 24) ^ t ^ ((t << 16) & M)
+        s1 = rotl(t, 37)
+    return out
+
+
+def test_qsgd_uniform_stream_mapping():
+    """The device stream layout (qsgd.hip kQStreamTile): element e is position
+    ((e & 8191) >> 11) * 8 + (e & 7) of stream ((e >> 13) << 8) | ((e & 8191) >> 3 & 255)."""
+    seed, offset = 0xABCDEF, 2
+    key = O.qrng_key(seed, offset)
+    for tile, t in ((0, 0), (0, 255), (3, 17)):
+        r = _xoro_scalar_stream(key, (tile << 8) | t, 16)
+        idx = np.array([tile * 8192 + g * 2048 + 8 * t + c for g in range(4) for c in range(8)])
+        want = []
+        for p in range(32):
+            v = r[p // 2]
+            want.append(((v >> 40) if p % 2 == 0 else (v >> 16) & 0xFFFFFF) * 2.0 ** -24)
+        assert np.array_equal(O.qsgd_uniforms_at(idx, seed, offset), np.array(want, dtype=np.float32))
+    # distribution: 2^20 uniforms, 64 bins within 5 sigma, mean 1/2
+    u = O.qsgd_uniforms(1 << 20, 11, 0)
+    h = np.bincount((u * 64).astype(np.int64), minlength=64)
+    assert abs(u.mean() - 0.5) < 2e-3 and np.all(np.abs(h - 16384) < 5 * 128)
+
+
 def test_randk_indices_distinct_and_uniformish():
     n, k = 10000, 1000
     counts = np.zeros(n)

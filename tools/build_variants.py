@@ -20,11 +20,8 @@ VARIANTS = {
     "g_form0": ["CHOCO_GOSSIP_FORM=0"],
     "gs_st_plain": ["CHOCO_GS_STORE_NT=0"],
     "wide_debug": ["CHOCO_WIDE_DEBUG=1"],
-    "qq_norng": ["CHOCO_QQUANT_DIAG=1"],
-    "ieee_div": ["CHOCO_IEEE_DIV=1"],
-    "sacc_rg32": ["CHOCO_SIGN_ACC_RG=32"],
-    "sacc_rg16": ["CHOCO_SIGN_ACC_RG=16"],
-    "sacc_rg4": ["CHOCO_SIGN_ACC_RG=4"],
+    "qdec_nt": ["CHOCO_QDEC_ST_NT=1"],
+    "qn_plain_qdec_nt": ["CHOCO_QNORM_NT=0", "CHOCO_QDEC_ST_NT=1"],
     "sgs_ru4": ["CHOCO_SIGN_GS_RU=4"],
     "sgs_split": ["CHOCO_SIGN_GS_FUSE=0"],
 }
