@@ -54,6 +54,7 @@ WORKLOADS = {
     "step_sign": ("sign", 345_000_000, None, "choco_step_gossip_sign_norm"),
     "step_qsgd": ("qsgd", 100_000_000, 4, "choco_step_gossip_qsgd_q4"),
 }
+SCATTER_TX_CEILING = 49.0  # G 64-B line transactions/s, best scattered RMW rate measured (tools/probe_scatter.hip)
 GAMMA = 0.9  # consensus_stepsize (parameters.py:126 default)
 
 # kernels (profile names) of each stage
@@ -551,6 +552,14 @@ def main():
             s["granule_bytes"] = granule
             s["granule_achieved"] = round(granule / (s["us_per_step"] * 1e-6) / 1e9, 1)
             s["granule_note"] = "every touched 64-B segment of x_hat / memory read + written whole, + messages"
+            # the bound a scattered RMW really meets: HBM line transactions per second (a read
+            # and a write-back per touched 64-B line); ceiling = the best rate tools/probe_scatter.hip
+            # measured for any scattered RMW pattern on MI355X (profiles/r02_probe_scatter.txt)
+            tx = (granule - 8 * w.k * len(w.ranks)) / 64
+            s["line_tx_rate"] = round(tx / (s["us_per_step"] * 1e-6) / 1e9, 2)
+            s["line_tx_ceiling"] = SCATTER_TX_CEILING
+            s["line_tx_frac"] = round(s["line_tx_rate"] / SCATTER_TX_CEILING, 3)
+            s["line_tx_unit"] = "G line-transactions/s"
         dom = next((s for s in stages if s["stage"] == dom_name), stages[0] if stages else None)
         traffic = None
         tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")

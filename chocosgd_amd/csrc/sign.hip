@@ -541,6 +541,33 @@ CHOCO_DEV float seg_scale(const SignMsgs& M, int q, const int64_t* __restrict__ 
   return nm / (float)numel;
 }
 
+#ifndef CHOCO_SIGN_ACC_RU  // rows per load group in the receiver (A/B knob)
+#define CHOCO_SIGN_ACC_RU 4
+#endif
+// Rows of the (32, N') view one receiver workgroup covers (32 / kSAccRows workgroups
+// per 1024-column block).  Block L -> (column block, row block) keeps the row blocks
+// of one column block on ONE XCD (linear ids congruent mod 8), so their word loads
+// hit that XCD's L2.
+#ifndef CHOCO_SIGN_ACC_RG
+#define CHOCO_SIGN_ACC_RG 8
+#endif
+constexpr int kSAccRows = CHOCO_SIGN_ACC_RG;
+constexpr int kSAccRB = 32 / kSAccRows;  // row blocks per column block
+static_assert(kSAccRows % CHOCO_SIGN_ACC_RU == 0 && 32 % kSAccRows == 0, "row blocking");
+CHOCO_DEV void sign_acc_block(uint32_t L, int64_t& cb, int& rb) {
+  if (kSAccRB == 1) {
+    cb = L;
+    rb = 0;
+    return;
+  }
+  const uint32_t rest = L / 8;
+  rb = (int)(rest % kSAccRB) * kSAccRows;
+  cb = (int64_t)(L % 8) + 8 * (int64_t)(rest / kSAccRB);
+}
+static unsigned sign_acc_grid(int64_t Np) {
+  const int64_t ncb = (Np + kSignCols - 1) / kSignCols;
+  return kSAccRB == 1 ? (unsigned)ncb : (unsigned)((ncb + 7) / 8 * 8 * kSAccRB);
+}
 template <int NM, bool HS>
 __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs M, int64_t n, int64_t Np,
                                                                        const int64_t* __restrict__ seg_off,
@@ -549,7 +576,11 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
   __shared__ int s_lo[32], s_hi[32];
   __shared__ float s_sc[kMaxMsg][32];
   const int lane = lane_id(), w = threadIdx.x >> 6;
-  const int64_t J0 = (int64_t)blockIdx.x * kSignCols;
+  int64_t cb;
+  int rb;
+  sign_acc_block(blockIdx.x, cb, rb);
+  if (cb * kSignCols >= Np) return;  // workgroup-uniform (grid padded to a multiple of 8 column blocks)
+  const int64_t J0 = cb * kSignCols;
   const int64_t j0 = J0 + 256 * w;
   const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
   row_segments(seg_off, nseg, n, Np, J0, s_lo, s_hi);
@@ -572,13 +603,13 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
   }
   // interior workgroups: unconditional loads keep all RU rows in flight
   const bool interior = ncol == 256 && (int64_t)31 * Np + j0 + 260 <= n;
-  constexpr int RU = 4;
+  constexpr int RU = CHOCO_SIGN_ACC_RU;
   bool all_uniform = true;
 #pragma unroll
-  for (int r = 0; r < 32; ++r) all_uniform &= s_lo[r] == s_hi[r];
+  for (int r = 0; r < kSAccRows; ++r) all_uniform &= s_lo[rb + r] == s_hi[rb + r];
   if (interior && all_uniform) {
     // fast path: no segment lookups, no global memory op besides the prefetch and the stores
-    for (int r0 = 0; r0 < 32; r0 += RU) {
+    for (int r0 = rb; r0 < rb + kSAccRows; r0 += RU) {
       float4 pm[RU], ph[RU], tm[RU], th[RU];
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
@@ -644,7 +675,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
     }
     return;
   }
-  for (int r0 = 0; r0 < 32; r0 += RU) {
+  for (int r0 = rb; r0 < rb + kSAccRows; r0 += RU) {
     float4 pm[RU], ph[RU], tm[RU], th[RU];
     if (interior) {
 #pragma unroll
@@ -1026,7 +1057,7 @@ CHOCO_API int choco_sign_decompress_accumulate(const int32_t* const* packed_list
   M.nmsg = nmsg;
   M.self_slot = self_slot;
   const int64_t Np = choco_sign_words(n);
-  const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
+  const unsigned grid = sign_acc_grid(Np);
   profile_begin("sign_accumulate", st);
   if (nseg == 1 && n < (int64_t(1) << 30) && CHOCO_SIGN_ACC1) {
     const unsigned g1 = (unsigned)((Np + kSA1WgCols - 1) / kSA1WgCols);
@@ -1099,7 +1130,7 @@ CHOCO_API int choco_sign_decompress_axpy(const int32_t* const* packed_list, cons
   M.self_slot = -1;
   M.mode = two_roundings ? 1 : 0;
   const int64_t Np = choco_sign_words(n);
-  const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
+  const unsigned grid = sign_acc_grid(Np);
   profile_begin("sign_accumulate", st);
 #define CHOCO_SIGN_AXPY(NM)                                                                                 \
   case NM:                                                                                                  \
@@ -1152,7 +1183,7 @@ CHOCO_API int choco_sign_decompress_extrapolate(const int32_t* packed, const flo
   M.a = a;
   M.b = b;
   const int64_t Np = choco_sign_words(n);
-  const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
+  const unsigned grid = sign_acc_grid(Np);
   profile_begin("sign_accumulate", st);
   CHOCO_KLAUNCH((sign_accumulate_kernel<1, false>), dim3(grid), dim3(kSignThreads), 0, st, M, n, Np, seg_off, nseg,
                 nullptr, target);

@@ -22,6 +22,9 @@ VARIANTS = {
     "wide_debug": ["CHOCO_WIDE_DEBUG=1"],
     "qdec_nt": ["CHOCO_QDEC_ST_NT=1"],
     "qn_plain_qdec_nt": ["CHOCO_QNORM_NT=0", "CHOCO_QDEC_ST_NT=1"],
+    "sacc_rg32": ["CHOCO_SIGN_ACC_RG=32"],
+    "sacc_rg16": ["CHOCO_SIGN_ACC_RG=16"],
+    "sacc_rg4": ["CHOCO_SIGN_ACC_RG=4"],
     "sgs_ru4": ["CHOCO_SIGN_GS_RU=4"],
     "sgs_split": ["CHOCO_SIGN_GS_FUSE=0"],
 }
