@@ -23,13 +23,17 @@
 //                              candidates (key >= b1 << 20) in index order into
 //                              its own slot range; keys in bin b1 feed a
 //                              histogram of bits 19..9 -> hist2[s].
-//   S3 seg_select   (segment): bin b2 from hist2[s], then bits 8..0 over the
-//                              segment's candidates (~1-2 % of it) -> exact T_s
-//                              and tie quota r_s; per-tile counts (> T, == T)
-//                              scanned into each tile's output offset and tie
-//                              share; resets hist1[s], hist2[s] for the next call.
-//   S4 seg_emit     (tile)   : ordered compaction of the tile's candidates
-//                              (key > T, plus its share of ties) to the output.
+//   S3a seg_fine    (tile)   : bin b2 of the k-th key from hist2[s]; bits 8..0
+//                              of the tile's candidates in fine bin (b1, b2) ->
+//                              hist3[s].
+//   S3b seg_count   (tile)   : exact T_s and tie quota r_s from hist3[s]; the
+//                              tile's counts (> T_s, == T_s).
+//   S4 seg_emit     (tile)   : offset and tie share from the counts of the
+//                              segment's earlier tiles, then the ordered
+//                              compaction of the tile's candidates (key > T_s,
+//                              plus its share of ties) to the output.
+// Every launch is tile-parallel; each histogram is reset by the first tile of
+// its segment in the launch after its last reader.
 // Two passes over the input (the first from HBM, the second usually from the
 // Infinity Cache) instead of one workgroup per segment doing four.  Segments
 // over 16M elements take the flat multi-workgroup pipeline (topk.hip).
@@ -61,13 +65,13 @@ CHOCO_DEV SegRow seg_row(const int64_t* __restrict__ plan, int s) {
 }
 
 struct SegWs {
-  uint32_t *hist1, *hist2, *info, *tilecnt, *tileout;
+  uint32_t *hist1, *hist2, *hist3, *info, *tilecnt, *tcount;
   float* cval;
   uint32_t* cidx;
 };
 
 struct SegLayout {
-  size_t off_h1, off_h2, off_info, off_cnt, off_out, off_cval, off_cidx, total;
+  size_t off_h1, off_h2, off_h3, off_info, off_cnt, off_out, off_cval, off_cidx, total;
 };
 
 static SegLayout seg_layout(int nseg, int64_t ntile) {
@@ -75,7 +79,8 @@ static SegLayout seg_layout(int nseg, int64_t ntile) {
   size_t o = 0;
   L.off_h1 = o;   o += align_up((size_t)nseg * kH * 4, 256);
   L.off_h2 = o;   o += align_up((size_t)nseg * kH * 4, 256);
-  L.off_info = o; o += align_up((size_t)nseg * 4 * 4, 256);
+  L.off_h3 = o;   o += align_up((size_t)nseg * 512 * 4, 256);
+  L.off_info = o; o += align_up((size_t)nseg * 8 * 4, 256);
   L.off_cnt = o;  o += align_up((size_t)ntile * 4, 256);
   L.off_out = o;  o += align_up((size_t)ntile * 8, 256);
   L.off_cval = o; o += align_up((size_t)ntile * kSegTile * 4, 256);
@@ -221,8 +226,8 @@ __global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
   block_find_rank2k(c0, c1, (uint32_t)c.R.k, scratch, bc);
   const uint32_t b1 = bc[0], kb = bc[1];
   if (c.j == 0 && tid == 0) {
-    info[4 * c.s + 0] = b1;
-    info[4 * c.s + 1] = kb;
+    info[8 * c.s + 0] = b1;
+    info[8 * c.s + 1] = kb;
   }
   const uint32_t floor_key = b1 << 20;
   const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
@@ -262,99 +267,175 @@ __global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
 }
 
 // ---------------------------------------------------------------- S3: exact T per segment
+// Tile-parallel (every tile of every segment in one launch, like S1/S2): a
+// per-segment select in ONE workgroup was latency-bound on the largest segment
+// (a 2.4M-element conv weight: ~50K candidates walked by 16 waves, a dependent
+// load per step).  Both kernels use 256-thread workgroups; every tile derives
+// its segment's bins from the complete global histograms of the previous launch.
+//   S3a seg_fine : bin b2 (bits 19..9) of the k-th key from hist2[s]; bits 8..0
+//                  of this tile's candidates in fine bin (b1, b2) -> hist3[s].
+//   S3b seg_count: T_s from hist3[s]; this tile's (#key > T_s, #key == T_s).
+// S4 then places each tile from the counts of the tiles before it.
+constexpr int kS3Threads = 256;
+constexpr int kH3 = 512;  // bits 8..0
+
+// Over hist[nb] in global memory (ascending key order), the bin holding the
+// rank-th largest entry and the rank inside it -> out[0], out[1]; PER bins per
+// thread of a kS3Threads workgroup.  Ends with a barrier.
+template <int PER>
+CHOCO_DEV void block_find_rank_g(const uint32_t* __restrict__ hist, uint32_t rank, uint32_t* scratch, uint32_t* out) {
+  const int tid = threadIdx.x;
+  uint32_t hv[PER];
+  uint32_t local = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    hv[j] = hist[tid * PER + j];
+    local += hv[j];
+  }
+  uint32_t total;
+  const uint32_t pre = block_excl_scan(local, scratch, &total);
+  const uint32_t above = total - pre - local;  // entries in bins above mine
+  if (above < rank && rank <= above + local) {
+    uint32_t acc = above;
+#pragma unroll
+    for (int j = PER - 1; j >= 0; --j) {
+      if (acc < rank && rank <= acc + hv[j]) { out[0] = (uint32_t)(tid * PER + j); out[1] = rank - acc; }
+      acc += hv[j];
+    }
+  }
+  __syncthreads();
+}
+
 template <int MODE>
-__global__ __launch_bounds__(kSegThreads) void seg_select_kernel(
+CHOCO_DEV uint32_t cand_key(const float* __restrict__ cval, const uint32_t* __restrict__ cidx, int64_t slot,
+                            uint64_t sseed, int64_t seg_off) {
+  return MODE == kHash ? (rank_hash(sseed, cidx[slot] - (uint32_t)seg_off) >> 1) : fkey(cval[slot]);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kS3Threads) void seg_fine_kernel(
     const int64_t* __restrict__ plan, int nseg, uint64_t seed, uint32_t* __restrict__ hist1,
-    uint32_t* __restrict__ hist2, uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt,
-    const float* __restrict__ cval, const uint32_t* __restrict__ cidx, uint32_t* __restrict__ tileout) {
-  __shared__ uint32_t h3[512];
-  __shared__ uint32_t tg[kSegMaxTiles], te[kSegMaxTiles];
+    const uint32_t* __restrict__ hist2, uint32_t* __restrict__ hist3, uint32_t* __restrict__ info,
+    const uint32_t* __restrict__ tilecnt, const float* __restrict__ cval, const uint32_t* __restrict__ cidx) {
+  __shared__ uint32_t h3[kH3];
   __shared__ uint32_t scratch[40];
   __shared__ uint32_t bc[4];
-  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  const int64_t ntile_all = plan[6];
-  const int s = (int)plan[(int64_t)kRow * nseg + ntile_all + blockIdx.x];
-  const SegRow R = seg_row(plan, s);
-  const uint64_t sseed = MODE == kHash ? seg_seed(seed, s) : 0;
-  const uint32_t b1 = info[4 * s + 0], kb = info[4 * s + 1];
-  uint32_t* __restrict__ g1 = hist1 + (int64_t)s * kH;
-  uint32_t* __restrict__ g2 = hist2 + (int64_t)s * kH;
-  const uint32_t c0 = g2[2 * tid], c1 = g2[2 * tid + 1];
-  if (tid < 512) h3[tid] = 0u;
-  block_find_rank2k(c0, c1, kb, scratch, bc);
-  const uint32_t b2 = bc[0], kc = bc[1];
-  // every tile of this segment has read hist1 / hist2 (earlier launches): reset them
-  g1[2 * tid] = 0u; g1[2 * tid + 1] = 0u;
-  g2[2 * tid] = 0u; g2[2 * tid + 1] = 0u;
-  const uint32_t P = (b1 << 20) | (b2 << 9);
-  auto key_at = [&](int64_t slot) -> uint32_t {
-    return MODE == kHash ? (rank_hash(sseed, cidx[slot] - (uint32_t)R.off) >> 1) : fkey(cval[slot]);
-  };
-  // bits 8..0 of the keys in fine bin (b1, b2): one wave per tile
-  for (int64_t t = w; t < R.ntile; t += kSegThreads / 64) {
-    const int64_t base = (R.t0 + t) * kSegTile;
-    const uint32_t cnt = tilecnt[R.t0 + t];
-    for (uint32_t i = lane; i < cnt; i += 64) {
-      const uint32_t key = key_at(base + i);
-      if ((key >> 9) == (P >> 9)) atomicAdd(&h3[key & 511u], 1u);
+  const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+  const int tid = threadIdx.x;
+  const uint32_t cnt = tilecnt[blockIdx.x];
+  const uint32_t b1 = info[8 * c.s + 0], kb = info[8 * c.s + 1];
+  for (int i = tid; i < kH3; i += kS3Threads) h3[i] = 0u;
+  block_find_rank_g<kH / kS3Threads>(hist2 + (int64_t)c.s * kH, kb, scratch, bc);
+  const uint32_t b2 = bc[0];
+  if (c.j == 0 && tid == 0) {
+    info[8 * c.s + 3] = b2;
+    info[8 * c.s + 4] = bc[1];  // rank of the k-th key inside fine bin (b1, b2)
+  }
+  if (c.j == 0) {  // every tile of the segment read hist1 in S2: reset it for the next call
+    uint32_t* __restrict__ g1 = hist1 + (int64_t)c.s * kH;
+    for (int i = tid; i < kH; i += kS3Threads) g1[i] = 0u;
+  }
+  const uint32_t P9 = (b1 << 11) | b2;  // key >> 9 of the fine bin
+  const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
+  constexpr int U = 4;
+  for (uint32_t i0 = 0; i0 < cnt; i0 += U * kS3Threads) {  // workgroup-uniform
+    uint32_t key[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * kS3Threads + tid;
+      key[u] = i < cnt ? cand_key<MODE>(cval, cidx, c.slot + i, sseed, c.R.off) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * kS3Threads + tid;
+      if (i < cnt && (key[u] >> 9) == P9) atomicAdd(&h3[key[u] & (kH3 - 1)], 1u);
     }
   }
   __syncthreads();
-  {
-    const uint32_t hv = tid < 512 ? h3[tid] : 0u;
-    uint32_t total;
-    const uint32_t pre = block_excl_scan(hv, scratch, &total);
-    const uint32_t above = total - pre - hv;
-    if (tid < 512 && above < kc && kc <= above + hv) { bc[2] = (uint32_t)tid; bc[3] = kc - above; }
-    __syncthreads();
-  }
-  const uint32_t T = P | bc[2];
-  const uint32_t r = bc[3];  // ties at T to take (>= 1)
-  // per tile: #keys > T, #keys == T (one wave per tile)
-  for (int64_t t = w; t < R.ntile; t += kSegThreads / 64) {
-    const int64_t base = (R.t0 + t) * kSegTile;
-    const uint32_t cnt = tilecnt[R.t0 + t];
-    uint32_t gt = 0, eq = 0;
-    for (uint32_t i = lane; i < cnt; i += 64) {
-      const uint32_t key = key_at(base + i);
-      gt += key > T ? 1u : 0u;
-      eq += key == T ? 1u : 0u;
+  uint32_t* __restrict__ g3 = hist3 + (int64_t)c.s * kH3;
+  for (int i = tid; i < kH3; i += kS3Threads)
+    if (h3[i]) atomicAdd(&g3[i], h3[i]);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
+    const int64_t* __restrict__ plan, int nseg, uint64_t seed, uint32_t* __restrict__ hist2,
+    const uint32_t* __restrict__ hist3, uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt,
+    const float* __restrict__ cval, const uint32_t* __restrict__ cidx, uint32_t* __restrict__ tcount) {
+  __shared__ uint32_t scratch[40];
+  __shared__ uint32_t bc[4];
+  const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+  const int tid = threadIdx.x;
+  const uint32_t cnt = tilecnt[blockIdx.x];
+  const uint32_t b1 = info[8 * c.s + 0], b2 = info[8 * c.s + 3], kc = info[8 * c.s + 4];
+  block_find_rank_g<kH3 / kS3Threads>(hist3 + (int64_t)c.s * kH3, kc, scratch, bc);
+  const uint32_t T = (b1 << 20) | (b2 << 9) | bc[0];
+  if (c.j == 0) {
+    if (tid == 0) {
+      info[8 * c.s + 2] = T;
+      info[8 * c.s + 5] = bc[1];  // ties at T to take (>= 1)
     }
-    gt = wave_sum(gt);
-    eq = wave_sum(eq);
-    if (lane == 0) { tg[t] = gt; te[t] = eq; }
+    uint32_t* __restrict__ g2 = hist2 + (int64_t)c.s * kH;  // read by every tile in S3a
+    for (int i = tid; i < kH; i += kS3Threads) g2[i] = 0u;
   }
-  __syncthreads();
-  {
-    const bool mine = tid < R.ntile;
-    const uint32_t gv = mine ? tg[tid] : 0u, ev = mine ? te[tid] : 0u;
-    uint32_t gpre, epre, gtot, etot;
-    block_excl_scan2(gv, ev, scratch, &gpre, &epre, &gtot, &etot);
-    if (mine) {
-      const uint32_t taken = min(r, epre);  // ties taken by earlier tiles (lowest index first)
-      const uint32_t share = min(ev, r - taken);
-      tileout[2 * (R.t0 + tid)] = gpre + taken;
-      tileout[2 * (R.t0 + tid) + 1] = share | (share == ev ? 0x80000000u : 0u);  // bit 31: every tie
+  const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
+  constexpr int U = 4;
+  uint32_t gt = 0, eq = 0;
+  for (uint32_t i0 = 0; i0 < cnt; i0 += U * kS3Threads) {  // workgroup-uniform
+    uint32_t key[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * kS3Threads + tid;
+      key[u] = i < cnt ? cand_key<MODE>(cval, cidx, c.slot + i, sseed, c.R.off) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * kS3Threads + tid;
+      gt += (i < cnt && key[u] > T) ? 1u : 0u;
+      eq += (i < cnt && key[u] == T) ? 1u : 0u;
     }
   }
-  if (tid == 0) info[4 * s + 2] = T;
+  uint32_t g0, e0, gtot, etot;
+  block_excl_scan2(gt, eq, scratch, &g0, &e0, &gtot, &etot);
+  if (tid == 0) {
+    tcount[2 * blockIdx.x] = gtot;
+    tcount[2 * blockIdx.x + 1] = etot;
+  }
 }
 
 // ---------------------------------------------------------------- S4: ordered emission
+// The tile's output offset and tie share from the counts of the segment's
+// earlier tiles (<= kSegMaxTiles - 1: one per thread), then the ordered
+// compaction of its candidates.
 template <int MODE>
 __global__ __launch_bounds__(kSegThreads) void seg_emit_kernel(
     const int64_t* __restrict__ plan, int nseg, uint64_t seed, int32_t is_biased, const uint32_t* __restrict__ info,
-    const uint32_t* __restrict__ tilecnt, const uint32_t* __restrict__ tileout, const float* __restrict__ cval,
-    const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx) {
+    const uint32_t* __restrict__ tilecnt, const uint32_t* __restrict__ tcount, uint32_t* __restrict__ hist3,
+    const float* __restrict__ cval, const uint32_t* __restrict__ cidx, float* __restrict__ out_val,
+    int32_t* __restrict__ out_idx) {
   __shared__ uint32_t scratch[40];
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
   const int tid = threadIdx.x;
   const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
-  const uint32_t T = info[4 * c.s + 2];
+  const uint32_t T = info[8 * c.s + 2], r = info[8 * c.s + 5];
   const uint32_t cnt = tilecnt[blockIdx.x];
-  const uint32_t o = tileout[2 * blockIdx.x], tw = tileout[2 * blockIdx.x + 1];
-  const uint32_t quota = tw & 0x7fffffffu;
-  const bool all_ties = (tw >> 31) != 0u;
+  const uint32_t ev = tcount[2 * blockIdx.x + 1];
+  uint32_t o, quota;
+  {
+    const bool before = tid < c.j;  // the segment's tiles ahead of this one
+    const int64_t bt = c.R.t0 + tid;
+    const uint32_t g = before ? tcount[2 * bt] : 0u, e = before ? tcount[2 * bt + 1] : 0u;
+    uint32_t gp, ep, gsum, esum;
+    block_excl_scan2(g, e, scratch, &gp, &ep, &gsum, &esum);
+    const uint32_t taken = min(r, esum);  // ties taken by earlier tiles (lowest index first)
+    o = gsum + taken;
+    quota = min(ev, r - taken);
+  }
+  if (c.j == 0) {  // every tile of the segment read hist3 in S3b: reset it for the next call
+    uint32_t* __restrict__ g3 = hist3 + (int64_t)c.s * kH3;
+    for (int i = tid; i < kH3; i += kSegThreads) g3[i] = 0u;
+  }
+  const bool all_ties = quota == ev;
   const float scale = (MODE == kHash && !is_biased) ? (float)((double)c.R.len / (double)c.R.k) : 1.0f;
   float* __restrict__ ov = out_val + c.R.out_off + o;
   int32_t* __restrict__ oi = out_idx + c.R.out_off + o;
@@ -394,7 +475,6 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
                           int nseg, uint64_t seed, int32_t is_biased, float* out_val, int32_t* out_idx,
                           const SegWs& W, hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}) {
   const unsigned ntile = (unsigned)plan_tiles(plan_host);
-  const unsigned nbat = (unsigned)plan_batched(plan_host);
   profile_begin("topk_seg_hist", st);
   CHOCO_KLAUNCH((seg_hist_kernel<MODE, XH, GS>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg, seed,
                 W.hist1, gs);
@@ -405,14 +485,19 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
                 W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx);
   profile_end("topk_seg_collect", st);
   CHOCO_LAUNCHED("seg_collect_kernel");
-  profile_begin("topk_seg_select", st);
-  CHOCO_KLAUNCH((seg_select_kernel<MODE>), dim3(nbat), dim3(kSegThreads), 0, st, plan_dev, nseg, seed, W.hist1,
-                W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.tileout);
-  profile_end("topk_seg_select", st);
-  CHOCO_LAUNCHED("seg_select_kernel");
+  profile_begin("topk_seg_fine", st);
+  CHOCO_KLAUNCH((seg_fine_kernel<MODE>), dim3(ntile), dim3(kS3Threads), 0, st, plan_dev, nseg, seed, W.hist1,
+                W.hist2, W.hist3, W.info, W.tilecnt, W.cval, W.cidx);
+  profile_end("topk_seg_fine", st);
+  CHOCO_LAUNCHED("seg_fine_kernel");
+  profile_begin("topk_seg_count", st);
+  CHOCO_KLAUNCH((seg_count_kernel<MODE>), dim3(ntile), dim3(kS3Threads), 0, st, plan_dev, nseg, seed, W.hist2,
+                W.hist3, W.info, W.tilecnt, W.cval, W.cidx, W.tcount);
+  profile_end("topk_seg_count", st);
+  CHOCO_LAUNCHED("seg_count_kernel");
   profile_begin("topk_seg_emit", st);
   CHOCO_KLAUNCH((seg_emit_kernel<MODE>), dim3(ntile), dim3(kSegThreads), 0, st, plan_dev, nseg, seed, is_biased,
-                W.info, W.tilecnt, W.tileout, W.cval, W.cidx, out_val, out_idx);
+                W.info, W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx);
   profile_end("topk_seg_emit", st);
   CHOCO_LAUNCHED("seg_emit_kernel");
   return CHOCO_OK;
@@ -454,6 +539,7 @@ static int segmented(const float* x, const float* xhat, const int64_t* plan_dev,
   char* base = static_cast<char*>(ws);
   if (ntile > 0) {
     SegWs W{reinterpret_cast<uint32_t*>(base + L.off_h1), reinterpret_cast<uint32_t*>(base + L.off_h2),
+            reinterpret_cast<uint32_t*>(base + L.off_h3),
             reinterpret_cast<uint32_t*>(base + L.off_info), reinterpret_cast<uint32_t*>(base + L.off_cnt),
             reinterpret_cast<uint32_t*>(base + L.off_out), reinterpret_cast<float*>(base + L.off_cval),
             reinterpret_cast<uint32_t*>(base + L.off_cidx)};

@@ -25,7 +25,8 @@ KERNELS = {
     "topk_fused": ("topk_fused_kernel", 2.0),
     "topk_seg_hist": ("seg_hist_kernel", 2.0),
     "topk_seg_collect": ("seg_collect_kernel", 2.0),
-    "topk_seg_select": ("seg_select_kernel", 2.0),
+    "topk_seg_fine": ("seg_fine_kernel", 2.0),
+    "topk_seg_count": ("seg_count_kernel", 2.0),
     "topk_seg_emit": ("seg_emit_kernel", 2.0),
     "sparse_accumulate": ("sparse_acc", 1.0),
     "qsgd_norm": ("qsgd_norm_kernel", 2.0),
