@@ -179,6 +179,12 @@ CHOCO_DEV void block_find_rank2k(uint32_t h0, uint32_t h1, uint32_t rank, uint32
 }
 
 // ---------------------------------------------------------------- S1: coarse histogram
+#ifndef CHOCO_S1_COPIES
+#define CHOCO_S1_COPIES 1
+#endif
+#ifndef CHOCO_S1_DIAG  // 1: no histogram (load-path timing only; results invalid)
+#define CHOCO_S1_DIAG 0
+#endif
 template <int MODE, bool XH, bool GS = false>
 __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ xh,
@@ -186,25 +192,35 @@ __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __re
                                                                uint64_t seed, uint32_t* __restrict__ hist1,
                                                                Gossip gs) {
   static_assert(!GS || (MODE == kData && XH), "the gossip step needs x_hat and data keys");
-  __shared__ uint32_t h[kH];
+  constexpr int NC = CHOCO_S1_COPIES;  // histogram copies (wave w -> copy w % NC): less same-bin contention
+  __shared__ uint32_t h[NC][kH];
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
   float v[kSegRows][4] = {};
   if (GS) tile_load_gossip(x, xh, gs, c, v);
   else if (MODE == kData) tile_load<XH>(x, xh, c, v);
-  for (int i = threadIdx.x; i < kH; i += kSegThreads) h[i] = 0u;
+  for (int i = threadIdx.x; i < NC * kH; i += kSegThreads) (&h[0][0])[i] = 0u;
   __syncthreads();
   const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
+  uint32_t* __restrict__ hw = h[(threadIdx.x >> 6) % NC];
+  uint32_t dsum = 0;
 #pragma unroll
   for (int r = 0; r < kSegRows; ++r)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = tile_elem(r, q);
-      if (e < c.tl) atomicAdd(&h[tile_key<MODE>(c, sseed, e, v[r][q]) >> 20], 1u);
+      const uint32_t key = tile_key<MODE>(c, sseed, e, v[r][q]);
+      if (CHOCO_S1_DIAG) dsum += key;
+      else if (e < c.tl) atomicAdd(&hw[key >> 20], 1u);
     }
+  if (CHOCO_S1_DIAG && dsum == 0x12345u) hw[0] = dsum;  // keep the loads (diagnostic build only)
   __syncthreads();
   uint32_t* __restrict__ g = hist1 + (int64_t)c.s * kH;
-  for (int i = threadIdx.x; i < kH; i += kSegThreads)
-    if (h[i]) atomicAdd(&g[i], h[i]);
+  for (int i = threadIdx.x; i < kH; i += kSegThreads) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) t += h[k][i];
+    if (t) atomicAdd(&g[i], t);
+  }
 }
 
 // ---------------------------------------------------------------- S2: coarse select + candidates
@@ -216,6 +232,8 @@ __global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
   __shared__ uint32_t h2[kH];
   __shared__ uint32_t scratch[40];
   __shared__ uint32_t bc[4];
+  __shared__ uint32_t rc_cnt[kSegRows * (kSegThreads / 64) + 1];
+  static_assert(kSegRows * (kSegThreads / 64) == 64, "one wave scans the (row, wave) counts");
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
   const int tid = threadIdx.x;
   float v[kSegRows][4] = {};
@@ -231,24 +249,42 @@ __global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
   }
   const uint32_t floor_key = b1 << 20;
   const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
-  uint32_t run = 0;
+  // candidate flags of all rows, then ONE scan of the (row, wave) counts places
+  // them in index order (row-major: row r, wave w, lane, element)
+  constexpr int kW = kSegThreads / 64;
+  const int lane = lane_id(), w = tid >> 6;
+  uint32_t cm[kSegRows];    // candidate bits of this lane's 4 elements per row
+  uint32_t lpre[kSegRows];  // exclusive count of candidates of lower lanes (same row, wave)
 #pragma unroll
   for (int r = 0; r < kSegRows; ++r) {
-    bool cand[4];
-    uint32_t cnt = 0;
+    cm[r] = 0u;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = tile_elem(r, q);
       const uint32_t key = tile_key<MODE>(c, sseed, e, v[r][q]);
-      cand[q] = e < c.tl && key >= floor_key;
-      cnt += cand[q] ? 1u : 0u;
-      if (cand[q] && (key >> 20) == b1) atomicAdd(&h2[(key >> 9) & (kH - 1)], 1u);
+      const bool cand = e < c.tl && key >= floor_key;
+      cm[r] |= cand ? (1u << q) : 0u;
+      if (cand && (key >> 20) == b1) atomicAdd(&h2[(key >> 9) & (kH - 1)], 1u);
     }
-    uint32_t tot;
-    uint32_t pos = run + block_excl_scan(cnt, scratch, &tot);
+    const uint32_t cnt = (uint32_t)__popc(cm[r]);
+    const uint32_t inc = wave_incl_scan(cnt);
+    lpre[r] = inc - cnt;
+    if (lane == 63) rc_cnt[r * kW + w] = inc;
+  }
+  __syncthreads();
+  if (w == 0) {  // wave 0: exclusive scan of the kSegRows * kW = 64 counts (row-major)
+    const uint32_t cv = rc_cnt[lane];
+    const uint32_t inc = wave_incl_scan(cv);
+    rc_cnt[lane] = inc - cv;
+    if (lane == 63) rc_cnt[kSegRows * kW] = inc;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kSegRows; ++r) {
+    uint32_t pos = rc_cnt[r * kW + w] + lpre[r];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      if (cand[q]) {
+      if (cm[r] & (1u << q)) {
         const int e = tile_elem(r, q);
         float val = v[r][q];
         if (MODE == kHash) val = XH ? x[c.start + e] - xh[c.start + e] : x[c.start + e];
@@ -257,13 +293,11 @@ __global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
         ++pos;
       }
     }
-    run += tot;
   }
-  __syncthreads();
   uint32_t* __restrict__ g2 = hist2 + (int64_t)c.s * kH;
   for (int i = tid; i < kH; i += kSegThreads)
     if (h2[i]) atomicAdd(&g2[i], h2[i]);
-  if (tid == 0) tilecnt[blockIdx.x] = run;
+  if (tid == 0) tilecnt[blockIdx.x] = rc_cnt[kSegRows * kW];
 }
 
 // ---------------------------------------------------------------- S3: exact T per segment

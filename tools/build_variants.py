@@ -22,6 +22,9 @@ VARIANTS = {
     "wide_debug": ["CHOCO_WIDE_DEBUG=1"],
     "qdec_nt": ["CHOCO_QDEC_ST_NT=1"],
     "qn_plain_qdec_nt": ["CHOCO_QNORM_NT=0", "CHOCO_QDEC_ST_NT=1"],
+    "s1_c2": ["CHOCO_S1_COPIES=2"],
+    "s1_c4": ["CHOCO_S1_COPIES=4"],
+    "s1_diag": ["CHOCO_S1_DIAG=1"],
     "sacc_rg32": ["CHOCO_SIGN_ACC_RG=32"],
     "sacc_rg16": ["CHOCO_SIGN_ACC_RG=16"],
     "sacc_rg4": ["CHOCO_SIGN_ACC_RG=4"],
