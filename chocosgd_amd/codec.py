@@ -57,6 +57,25 @@ def workspace(dev, kind, nbytes):
         return buf
 
 
+def workspace_bytes():
+    """Device bytes held by the cached scratch buffers (top-k: ~9 bytes per element of
+    the largest flat input, sized for 288 GB HBM rather than packed)."""
+    with _ws_lock:
+        return sum(b.numel() for b in _ws_cache.values())
+
+
+def release_workspaces(dev=None):
+    """Drop the cached scratch buffers (all devices, or `dev`) after synchronising the
+    streams that used them; the next call on that stream allocates a fresh, zeroed one.
+    SegmentPlan workspaces belong to their plan and go with it."""
+    with _ws_lock:
+        for key in list(_ws_cache):
+            if dev is not None and key[0] != torch.device(dev).index:
+                continue
+            torch.cuda.synchronize(key[0])
+            del _ws_cache[key]
+
+
 def lib():
     return _lib.load()
 

@@ -292,3 +292,21 @@ def test_choco_topk_round_trip_golden(name, ratio):
         codec.sparse_accumulate(vals, idx, mem, float(g["weights"][r]), xhat_self=hat if r == self_rank else None)
     assert same_bits(host(hat), g["hat1"])
     assert same_bits(host(mem), g["mem1"])
+
+
+def test_release_workspaces_then_recompute():
+    """codec.release_workspaces frees the cached scratch; the next call allocates a fresh
+    zeroed one and gives the same exact answer."""
+    from chocosgd_amd import codec
+    d = randn(3_000_000, 77)
+    k = codec.topk_k(d.numel(), 0.99)
+    v1, i1 = codec.topk(d, k)
+    torch.cuda.synchronize()
+    assert codec.workspace_bytes() > 0
+    codec.release_workspaces()
+    assert codec.workspace_bytes() == 0
+    v2, i2 = codec.topk(d, k)
+    torch.cuda.synchronize()
+    assert torch.equal(i1, i2) and torch.equal(v1.view(torch.int32), v2.view(torch.int32))
+    ov, oi = O.topk(host(d), k)
+    assert np.array_equal(host(i2).astype(np.int64), oi)
