@@ -212,8 +212,12 @@ class Worker:
             c.sign_compress(self.x, xhat=self.hat, gossip=g, out=self.wire)
 
     def exchange(self):
+        self.exchange_finish(self.exchange_start())
+
+    def exchange_start(self):
+        """Post the grouped sends/recvs; returns the works (None without peers)."""
         if not self.peers:
-            return
+            return None
         import torch.distributed as dist
         if self.backend == "gloo":  # comm_device=cpu: pinned host staging (parallel_choco_v.py:271-272)
             self.msg_h.copy_(self.msg)
@@ -224,20 +228,32 @@ class Worker:
         for r in self.peers:
             ops.append(dist.P2POp(dist.isend, src, r))
             ops.append(dist.P2POp(dist.irecv, dst[r], r))
-        for w in dist.batch_isend_irecv(ops):
+        return dist.batch_isend_irecv(ops)
+
+    def exchange_finish(self, works):
+        if works is None:
+            return
+        for w in works:
             w.wait()
         if self.backend == "gloo":
             for r in self.peers:
                 self.recv[r].copy_(self.recv_h[r], non_blocking=True)
 
-    def decompress(self):
+    def hat_self_update(self):
+        """x_hat += own message (sparse codecs): it needs no remote message, so with peers
+        it runs while the exchange is in flight (bit-identical: x_hat takes only the
+        local message; memory's updates stay in neighbour order, parallel_choco_v.py:307-310)."""
+        torch = self.torch
+        self.codec.sparse_accumulate(self.msg[:self.k].view(torch.float32), self.msg[self.k:], self.hat, 1.0)
+
+    def decompress(self, hat_done=False):
         c = self.codec
         torch = self.torch
         msgs = [self.msg if r == self.rank else self.recv[r] for r in self.ranks]
         if self.op in ("topk", "topk_seg", "randk"):
             for r, m, w in zip(self.ranks, msgs, self.weights):
                 c.sparse_accumulate(m[:self.k].view(torch.float32), m[self.k:], self.mem, w,
-                                    xhat_self=self.hat if r == self.rank else None)
+                                    xhat_self=self.hat if r == self.rank and not hat_done else None)
         elif self.op == "qsgd":
             parts = [(m[16:], m[:4].view(torch.float32)) for m in msgs]
             c.qsgd_accumulate(parts, self.weights, self.self_slot, self.n, self.param, self.mem, xhat_self=self.hat)
@@ -247,8 +263,12 @@ class Worker:
 
     def step(self):
         self.compress()
-        self.exchange()
-        self.decompress()
+        works = self.exchange_start()
+        overlap = works is not None and self.op in ("topk", "topk_seg", "randk")
+        if overlap:
+            self.hat_self_update()
+        self.exchange_finish(works)
+        self.decompress(hat_done=overlap)
 
     def stage_bytes(self):
         """Algorithmic HBM bytes per step of each stage, and the

@@ -196,19 +196,29 @@ class CHOCOSparsificationCompressor(_CHOCOBase):
         return g
 
     def uncompress(self, sync_buffer, neighbor_hat_params, neighbors_info):
-        self.aggregator_fn.complete_wait(sync_buffer["sync_reqs"])
         K = int(sync_buffer["sycned_message_size"] / 2)
         memory = neighbor_hat_params["memory"]
         guard = self._guard(memory.buffer.device)
         guard.check()  # out-of-range indices of an EARLIER step (lazy, no sync)
+        # x_hat takes only the local message (hat_params.buffer += q_values,
+        # parallel_choco_v.py:307-308): with remote messages pending, its scatter is
+        # queued BEFORE waiting for them, so it runs while the exchange is in flight.
+        # Bit-identical: memory's updates keep the neighbour order below.
+        local = [r for r in neighbors_info if r in neighbor_hat_params]
+        hat_early = len(local) == 1 and len(neighbors_info) > 1
+        if hat_early:
+            hat = neighbor_hat_params[local[0]].buffer
+            msg = sync_buffer["wire_message"]
+            codec.sparse_accumulate(msg[:K].view(torch.float32), msg[K:], hat, 1.0, guard=guard)
+        self.aggregator_fn.complete_wait(sync_buffer["sync_reqs"])
         for rank, weight in neighbors_info.items():
             hat_params = neighbor_hat_params[rank if rank in neighbor_hat_params else "memory"]
             msg = recover_device(sync_buffer["synced_message"][rank], device=hat_params.buffer.device)
             q_values = msg[:K].view(torch.float32)
             q_indices = msg[K:]
+            own = rank in neighbor_hat_params and not hat_early
             codec.sparse_accumulate(q_values, q_indices, memory.buffer, weight,
-                                    xhat_self=hat_params.buffer if rank in neighbor_hat_params else None,
-                                    guard=guard)
+                                    xhat_self=hat_params.buffer if own else None, guard=guard)
         guard.arm()
 
 
