@@ -182,7 +182,8 @@ CHOCO_DEV void block_find_rank2k(uint32_t h0, uint32_t h1, uint32_t rank, uint32
 #ifndef CHOCO_S1_COPIES
 #define CHOCO_S1_COPIES 1
 #endif
-#ifndef CHOCO_S1_DIAG  // 1: no histogram (load-path timing only; results invalid)
+#ifndef CHOCO_S1_DIAG  // 1: no histogram (load-path timing only); 2: no S1 read at all, one
+                       // synthetic bin (S2 from HBM); results invalid, S4 stores nothing
 #define CHOCO_S1_DIAG 0
 #endif
 template <int MODE, bool XH, bool GS = false>
@@ -196,6 +197,10 @@ __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __re
   __shared__ uint32_t h[NC][kH];
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
   float v[kSegRows][4] = {};
+  if (CHOCO_S1_DIAG == 2) {  // diagnostic: every element counted in the bin of |v| = 2.5
+    if (threadIdx.x == 0) atomicAdd(&hist1[(int64_t)c.s * kH + 0x402], (uint32_t)c.tl);
+    return;
+  }
   if (GS) tile_load_gossip(x, xh, gs, c, v);
   else if (MODE == kData) tile_load<XH>(x, xh, c, v);
   for (int i = threadIdx.x; i < NC * kH; i += kSegThreads) (&h[0][0])[i] = 0u;
@@ -439,10 +444,18 @@ __global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
 
 // ---------------------------------------------------------------- S4: ordered emission
 // The tile's output offset and tie share from the counts of the segment's
-// earlier tiles (<= kSegMaxTiles - 1: one per thread), then the ordered
-// compaction of its candidates.
+// earlier tiles (<= kSegMaxTiles - 1: kS4Per per thread), then the ordered
+// compaction of its candidates (a few hundred at k = 1 %: one or two rounds).
+// Latency-bound like S3: 256-thread workgroups (cheaper block scans, more
+// workgroups resident); CHOCO_S4_THREADS=1024 is the previous form.
+#ifndef CHOCO_S4_THREADS
+#define CHOCO_S4_THREADS 256
+#endif
+constexpr int kS4Threads = CHOCO_S4_THREADS;
+constexpr int kS4Per = kSegMaxTiles / kS4Threads;
+static_assert(kS4Per * kS4Threads == kSegMaxTiles, "S4 tile-count geometry");
 template <int MODE>
-__global__ __launch_bounds__(kSegThreads) void seg_emit_kernel(
+__global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
     const int64_t* __restrict__ plan, int nseg, uint64_t seed, int32_t is_biased, const uint32_t* __restrict__ info,
     const uint32_t* __restrict__ tilecnt, const uint32_t* __restrict__ tcount, uint32_t* __restrict__ hist3,
     const float* __restrict__ cval, const uint32_t* __restrict__ cidx, float* __restrict__ out_val,
@@ -451,14 +464,21 @@ __global__ __launch_bounds__(kSegThreads) void seg_emit_kernel(
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
   const int tid = threadIdx.x;
   const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
+  if (CHOCO_S1_DIAG == 2) return;
   const uint32_t T = info[8 * c.s + 2], r = info[8 * c.s + 5];
   const uint32_t cnt = tilecnt[blockIdx.x];
   const uint32_t ev = tcount[2 * blockIdx.x + 1];
   uint32_t o, quota;
   {
-    const bool before = tid < c.j;  // the segment's tiles ahead of this one
-    const int64_t bt = c.R.t0 + tid;
-    const uint32_t g = before ? tcount[2 * bt] : 0u, e = before ? tcount[2 * bt + 1] : 0u;
+    uint32_t g = 0u, e = 0u;  // over the segment's tiles ahead of this one
+#pragma unroll
+    for (int q = 0; q < kS4Per; ++q) {
+      const int t = q * kS4Threads + tid;
+      if (t < c.j) {
+        g += tcount[2 * (c.R.t0 + t)];
+        e += tcount[2 * (c.R.t0 + t) + 1];
+      }
+    }
     uint32_t gp, ep, gsum, esum;
     block_excl_scan2(g, e, scratch, &gp, &ep, &gsum, &esum);
     const uint32_t taken = min(r, esum);  // ties taken by earlier tiles (lowest index first)
@@ -467,14 +487,14 @@ __global__ __launch_bounds__(kSegThreads) void seg_emit_kernel(
   }
   if (c.j == 0) {  // every tile of the segment read hist3 in S3b: reset it for the next call
     uint32_t* __restrict__ g3 = hist3 + (int64_t)c.s * kH3;
-    for (int i = tid; i < kH3; i += kSegThreads) g3[i] = 0u;
+    for (int i = tid; i < kH3; i += kS4Threads) g3[i] = 0u;
   }
   const bool all_ties = quota == ev;
   const float scale = (MODE == kHash && !is_biased) ? (float)((double)c.R.len / (double)c.R.k) : 1.0f;
   float* __restrict__ ov = out_val + c.R.out_off + o;
   int32_t* __restrict__ oi = out_idx + c.R.out_off + o;
   uint32_t run = 0, tie_run = 0;
-  for (uint32_t p0 = 0; p0 < cnt; p0 += kSegThreads) {  // workgroup-uniform
+  for (uint32_t p0 = 0; p0 < cnt; p0 += kS4Threads) {  // workgroup-uniform
     const uint32_t p = p0 + tid;
     const bool valid = p < cnt;
     const float v = valid ? cval[c.slot + p] : 0.f;
@@ -530,7 +550,7 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
   profile_end("topk_seg_count", st);
   CHOCO_LAUNCHED("seg_count_kernel");
   profile_begin("topk_seg_emit", st);
-  CHOCO_KLAUNCH((seg_emit_kernel<MODE>), dim3(ntile), dim3(kSegThreads), 0, st, plan_dev, nseg, seed, is_biased,
+  CHOCO_KLAUNCH((seg_emit_kernel<MODE>), dim3(ntile), dim3(kS4Threads), 0, st, plan_dev, nseg, seed, is_biased,
                 W.info, W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx);
   profile_end("topk_seg_emit", st);
   CHOCO_LAUNCHED("seg_emit_kernel");

@@ -25,11 +25,17 @@ VARIANTS = {
     "s1_c2": ["CHOCO_S1_COPIES=2"],
     "s1_c4": ["CHOCO_S1_COPIES=4"],
     "s1_diag": ["CHOCO_S1_DIAG=1"],
+    "s1_diag2": ["CHOCO_S1_DIAG=2"],
+    "s4_1024": ["CHOCO_S4_THREADS=1024"],
     "sacc_rg32": ["CHOCO_SIGN_ACC_RG=32"],
     "sacc_rg16": ["CHOCO_SIGN_ACC_RG=16"],
     "sacc_rg4": ["CHOCO_SIGN_ACC_RG=4"],
     "sgs_ru4": ["CHOCO_SIGN_GS_RU=4"],
     "sgs_split": ["CHOCO_SIGN_GS_FUSE=0"],
+    "k2t384": ["CHOCO_K2_TARGET=384"],
+    "k2t512": ["CHOCO_K2_TARGET=512"],
+    "k2t768": ["CHOCO_K2_TARGET=768"],
+    "k2t1024": ["CHOCO_K2_TARGET=1024"],
 }
 
 
