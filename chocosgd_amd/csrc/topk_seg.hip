@@ -315,7 +315,10 @@ __global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
 //                  of this tile's candidates in fine bin (b1, b2) -> hist3[s].
 //   S3b seg_count: T_s from hist3[s]; this tile's (#key > T_s, #key == T_s).
 // S4 then places each tile from the counts of the tiles before it.
-constexpr int kS3Threads = 256;
+#ifndef CHOCO_S3_THREADS
+#define CHOCO_S3_THREADS 256
+#endif
+constexpr int kS3Threads = CHOCO_S3_THREADS;
 constexpr int kH3 = 512;  // bits 8..0
 
 // Over hist[nb] in global memory (ascending key order), the bin holding the

@@ -27,6 +27,10 @@ VARIANTS = {
     "s1_diag": ["CHOCO_S1_DIAG=1"],
     "s1_diag2": ["CHOCO_S1_DIAG=2"],
     "s4_1024": ["CHOCO_S4_THREADS=1024"],
+    "s4_128": ["CHOCO_S4_THREADS=128"],
+    "s4_64": ["CHOCO_S4_THREADS=64"],
+    "s3_128": ["CHOCO_S3_THREADS=128"],
+    "s3_64": ["CHOCO_S3_THREADS=64"],
     "sacc_rg32": ["CHOCO_SIGN_ACC_RG=32"],
     "sacc_rg16": ["CHOCO_SIGN_ACC_RG=16"],
     "sacc_rg4": ["CHOCO_SIGN_ACC_RG=4"],
