@@ -194,22 +194,26 @@ def test_topk_segmented_unaligned_large(ratio):
     assert same_bits(host(vals), ov)
 
 
-@pytest.mark.parametrize("case", ["ties", "ratio0", "ratio05", "nan", "tile_edges", "huge_mixed"])
+@pytest.mark.parametrize("case", ["ties", "ties_many_tiles", "ratio0", "ratio05", "nan", "tile_edges", "huge_mixed"])
 def test_topk_segmented_edge_layouts(case):
     """The batched segmented select (topk_seg.hip) on tie-heavy tensors, k = len, k = len/2,
     NaN, tensors at tile edges (16384 +- 1, exactly 1024 tiles) and a tensor over 16M
-    elements that takes the flat pipeline next to batched ones."""
+    elements that takes the flat pipeline next to batched ones.  ties_many_tiles: the tie
+    quota of a 306-tile tensor is split over tiles past the first 256 (S4 sums the
+    earlier tiles' counts four per thread)."""
     from chocosgd_amd import codec
     ratio = {"ratio0": 0.0, "ratio05": 0.5}.get(case, 0.99)
     if case == "tile_edges":
         lens = [16383, 16384, 16385, 1, 16_777_216, 32768]
     elif case == "huge_mixed":
         lens = [7, 20_000_001, 3000, 1_100_001]
+    elif case == "ties_many_tiles":
+        lens = [5_000_003, 16384, 9]
     else:
         lens = [100, 50_000, 16384, 16385, 3, 700_001]
     n = sum(lens)
     x, xh = randn(n, 61), randn(n, 62, 0.5)
-    if case == "ties":
+    if case in ("ties", "ties_many_tiles"):
         x = torch.round(x * 2) / 2
         xh = torch.zeros_like(x)
     if case == "nan":
