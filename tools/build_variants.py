@@ -27,6 +27,10 @@ VARIANTS = {
     "s1_diag": ["CHOCO_S1_DIAG=1"],
     "s1_diag2": ["CHOCO_S1_DIAG=2"],
     "s4_1024": ["CHOCO_S4_THREADS=1024"],
+    "k2st_nt": ["CHOCO_K2_STORE=1"],
+    "k2st_wt": ["CHOCO_K2_STORE=2"],
+    "k34st_nt": ["CHOCO_K34_STORE=1"],
+    "k34st_wt": ["CHOCO_K34_STORE=2"],
     "s4_128": ["CHOCO_S4_THREADS=128"],
     "s4_64": ["CHOCO_S4_THREADS=64"],
     "s3_128": ["CHOCO_S3_THREADS=128"],
