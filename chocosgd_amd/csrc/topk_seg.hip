@@ -182,6 +182,12 @@ CHOCO_DEV void block_find_rank2k(uint32_t h0, uint32_t h1, uint32_t rank, uint32
 #ifndef CHOCO_S1_COPIES
 #define CHOCO_S1_COPIES 1
 #endif
+#ifndef CHOCO_S2_DIAG  // 1: fixed coarse bin (no hist1 read, no scan): S2 chain-latency probe; results invalid
+#define CHOCO_S2_DIAG 0
+#endif
+#ifndef CHOCO_S1_LANEC
+#define CHOCO_S1_LANEC 1
+#endif
 #ifndef CHOCO_S1_DIAG  // 1: no histogram (load-path timing only); 2: no S1 read at all, one
                        // synthetic bin (S2 from HBM); results invalid, S4 stores nothing
 #define CHOCO_S1_DIAG 0
@@ -193,7 +199,9 @@ __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __re
                                                                uint64_t seed, uint32_t* __restrict__ hist1,
                                                                Gossip gs) {
   static_assert(!GS || (MODE == kData && XH), "the gossip step needs x_hat and data keys");
-  constexpr int NC = CHOCO_S1_COPIES;  // histogram copies (wave w -> copy w % NC): less same-bin contention
+  // histogram copies: wave w -> copy w % NC (CHOCO_S1_COPIES), or lane l -> copy
+  // l % NC (CHOCO_S1_LANEC: same-bin lanes of ONE atomic instruction split over copies)
+  constexpr int NC = CHOCO_S1_LANEC > 1 ? CHOCO_S1_LANEC : CHOCO_S1_COPIES;
   __shared__ uint32_t h[NC][kH];
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
   float v[kSegRows][4] = {};
@@ -206,7 +214,7 @@ __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __re
   for (int i = threadIdx.x; i < NC * kH; i += kSegThreads) (&h[0][0])[i] = 0u;
   __syncthreads();
   const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
-  uint32_t* __restrict__ hw = h[(threadIdx.x >> 6) % NC];
+  uint32_t* __restrict__ hw = h[CHOCO_S1_LANEC > 1 ? lane_id() % NC : (threadIdx.x >> 6) % NC];
   uint32_t dsum = 0;
 #pragma unroll
   for (int r = 0; r < kSegRows; ++r)
@@ -244,9 +252,14 @@ __global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
   float v[kSegRows][4] = {};
   if (MODE == kData) tile_load<XH>(x, xh, c, v);  // in flight while b1 is found
   const uint32_t* __restrict__ g1 = hist1 + (int64_t)c.s * kH;
-  const uint32_t c0 = g1[2 * tid], c1 = g1[2 * tid + 1];
+  const uint32_t c0 = CHOCO_S2_DIAG ? 0u : g1[2 * tid], c1 = CHOCO_S2_DIAG ? 0u : g1[2 * tid + 1];
   for (int i = tid; i < kH; i += kSegThreads) h2[i] = 0u;
-  block_find_rank2k(c0, c1, (uint32_t)c.R.k, scratch, bc);
+  if (CHOCO_S2_DIAG) {
+    if (tid == 0) { bc[0] = 0x402u; bc[1] = (uint32_t)c.R.k; }
+    __syncthreads();
+  } else {
+    block_find_rank2k(c0, c1, (uint32_t)c.R.k, scratch, bc);
+  }
   const uint32_t b1 = bc[0], kb = bc[1];
   if (c.j == 0 && tid == 0) {
     info[8 * c.s + 0] = b1;
@@ -467,7 +480,7 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
   const int tid = threadIdx.x;
   const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
-  if (CHOCO_S1_DIAG == 2) return;
+  if (CHOCO_S1_DIAG == 2 || CHOCO_S2_DIAG) return;
   const uint32_t T = info[8 * c.s + 2], r = info[8 * c.s + 5];
   const uint32_t cnt = tilecnt[blockIdx.x];
   const uint32_t ev = tcount[2 * blockIdx.x + 1];

@@ -27,6 +27,10 @@ VARIANTS = {
     "s1_diag": ["CHOCO_S1_DIAG=1"],
     "s1_diag2": ["CHOCO_S1_DIAG=2"],
     "s4_1024": ["CHOCO_S4_THREADS=1024"],
+    "s1_lc2": ["CHOCO_S1_LANEC=2"],
+    "s1_lc4": ["CHOCO_S1_LANEC=4"],
+    "s1_lc8": ["CHOCO_S1_LANEC=8"],
+    "s2_diag": ["CHOCO_S2_DIAG=1"],
     "k2st_nt": ["CHOCO_K2_STORE=1"],
     "k2st_wt": ["CHOCO_K2_STORE=2"],
     "k34st_nt": ["CHOCO_K34_STORE=1"],
