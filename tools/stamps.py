@@ -73,6 +73,12 @@ def main():
     print(f"n={a.n} k={k}; times in us from the first K2 workgroup start")
     print(f"K2 sample + stream ({len(k2)} workgroups)")
     row("start", k2[:, 0]); row("sample bounds", k2[:, 1]); row("streamed", k2[:, 2]); row("end", k2[:, 3])
+    # per XCD (workgroup b runs on XCD b % 8): full tiles only (the last tile is partial)
+    full = t[1024:1024 + 4096]
+    nb = int((full[:, 0] > 0).sum())
+    ends = {x: [us(full[b, 3]) for b in range(x, nb - 1, 8)] for x in range(8)}
+    print("  per-XCD end of the full tiles (median / max us): " +
+          "  ".join(f"X{x} {np.median(v):.1f}/{max(v):.1f}" for x, v in ends.items() if v))
     row("  sample keys in registers", pro[:, 0]); row("  subsample histogram", pro[:, 1])
     row("  keys >= F listed + fine histogram", pro[:, 2]); row("  bounds", pro[:, 3])
     tb = t[22000:22000 + 2048]
