@@ -12,6 +12,9 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libchoco_codec.so")
 
+TOPK_STATUS_OFFSET = 0        # CHOCO_TOPK_STATUS_OFFSET
+TOPK_STATUS_POLL_TIMEOUT = 1  # CHOCO_TOPK_STATUS_POLL_TIMEOUT
+
 _c_i32, _c_i64, _c_u64, _c_f32, _c_f64 = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
                                            ctypes.c_float, ctypes.c_double)
 _c_sz, _vp = ctypes.c_size_t, ctypes.c_void_p
@@ -25,6 +28,8 @@ SIGNATURES = {
     "choco_last_error": (_c_i32, [ctypes.c_char_p, _c_sz]),
     "choco_topk_k": (_c_i64, [_c_i64, _c_f64]),
     "choco_topk_workspace_size": (_c_sz, [_c_i64]),
+    "choco_topk_workspace_reset": (_c_i32, [_vp, _c_sz]),
+    "choco_topk_set_warm_start": (_c_i32, [_c_i32]),
     "choco_topk_compress": (_c_i32, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_topk_segmented_plan_len": (_c_i64, [_p_i64, _c_i32]),
     "choco_topk_segmented_plan": (_c_i64, [_p_i64, _c_i32, _c_f64, _p_i64]),

@@ -39,11 +39,21 @@ def _stream(dev):
     return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
 
+def _new_workspace(dev, nbytes):
+    """A zero-filled workspace; the library forgets any warm-start record it kept for
+    that address range (a freed workspace's address can come back)."""
+    buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+    lib().choco_topk_workspace_reset(_ptr(buf), buf.numel())
+    return buf
+
+
 def workspace(dev, kind, nbytes):
     """Per (device, stream, kind) scratch buffer; zero-filled on allocation.
 
     The sign/qsgd accumulators rely on starting zeroed; every kernel that uses
     them leaves them zeroed again (self-cleaning), so the buffer is reused as is.
+    A top-k workspace also carries the warm-start window from one call to the next
+    (include/choco_codec.h).
     """
     nbytes = max(int(nbytes), 256)
     key = (dev.index, torch.cuda.current_stream(dev).cuda_stream, kind)
@@ -52,9 +62,69 @@ def workspace(dev, kind, nbytes):
         if buf is None or buf.numel() < nbytes:
             if buf is not None:
                 torch.cuda.current_stream(dev).synchronize()
-            buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+                _status.pop(buf.data_ptr(), None)
+            buf = _new_workspace(dev, nbytes)
             _ws_cache[key] = buf
         return buf
+
+
+class TopkStatus:
+    """Lazy check of a top-k workspace's sticky status word (include/choco_codec.h,
+    CHOCO_TOPK_STATUS_OFFSET): every `every`-th call queues a non-blocking copy of the
+    word to pinned host memory behind its launches (a 4-byte copy per call would sit in
+    the stream of every step); `check()` raises RuntimeError once such a copy has landed
+    nonzero -- the output of the call that set it is invalid -- and clears the word.
+    `check(wait=True)` copies and waits (end of training, checkpoints)."""
+
+    def __init__(self, ws, every=16):
+        self.word = ws[_lib.TOPK_STATUS_OFFSET:_lib.TOPK_STATUS_OFFSET + 4].view(torch.int32)
+        self.host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self.event = None
+        self.every = every
+        self.calls = 0
+
+    def arm(self):
+        self.host.copy_(self.word, non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record(torch.cuda.current_stream(self.word.device))
+
+    def after_call(self):
+        self.calls += 1
+        if self.event is None and self.calls % self.every == 0:
+            self.arm()
+
+    def check(self, wait=False):
+        if wait and self.event is None:
+            self.arm()
+        if self.event is None:
+            return
+        if wait:
+            self.event.synchronize()
+        elif not self.event.query():
+            return
+        self.event = None
+        bad = int(self.host.item())
+        if bad:
+            self.word.zero_()
+            raise RuntimeError(f"top-k: status word {bad:#x}: a bounded wait of the exact fallback gave up, so the "
+                               "output of an earlier call on this workspace is invalid")
+
+
+_status = {}
+
+
+def topk_status(ws):
+    """The TopkStatus of a workspace tensor (one per workspace)."""
+    st = _status.get(ws.data_ptr())
+    if st is None:
+        st = _status[ws.data_ptr()] = TopkStatus(ws)
+    return st
+
+
+def check_topk_status(wait=True):
+    """Check every top-k workspace's status word now (raises RuntimeError)."""
+    for st in list(_status.values()):
+        st.check(wait=wait)
 
 
 def workspace_bytes():
@@ -73,7 +143,9 @@ def release_workspaces(dev=None):
             if dev is not None and key[0] != torch.device(dev).index:
                 continue
             torch.cuda.synchronize(key[0])
-            del _ws_cache[key]
+            buf = _ws_cache.pop(key)
+            _status.pop(buf.data_ptr(), None)
+            lib().choco_topk_workspace_reset(_ptr(buf), buf.numel())
 
 
 def lib():
@@ -125,14 +197,17 @@ def topk(x, k, xhat=None, out=None, gossip=None):
         idx = torch.empty(k, dtype=torch.int32, device=dev)
     L = lib()
     ws = workspace(dev, "topk", L.choco_topk_workspace_size(n))
+    st = topk_status(ws)
+    st.check()
     g = _gossip(gossip, x, xhat)
     if g is not None:
         _lib.check(L.choco_gossip_topk_compress(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1], n, int(k), _ptr(vals),
                                                 _ptr(idx), _ptr(ws), ws.numel(), _stream(dev)),
                    "choco_gossip_topk_compress")
-        return vals, idx
-    _lib.check(L.choco_topk_compress(_ptr(x), _ptr(xhat), n, int(k), _ptr(vals), _ptr(idx), _ptr(ws),
-                                     ws.numel(), _stream(dev)), "choco_topk_compress")
+    else:
+        _lib.check(L.choco_topk_compress(_ptr(x), _ptr(xhat), n, int(k), _ptr(vals), _ptr(idx), _ptr(ws),
+                                         ws.numel(), _stream(dev)), "choco_topk_compress")
+    st.after_call()
     return vals, idx
 
 
@@ -170,11 +245,11 @@ class SegmentPlan:
         """This plan's own zero-filled workspace per stream: the batched select keeps
         per-segment histograms there that every call leaves zeroed for the NEXT call of
         the same plan (include/choco_codec.h), so no other call may share it."""
-        key = torch.cuda.current_stream(dev).cuda_stream
+        key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
         with _ws_lock:
             buf = self._ws.get(key)
             if buf is None:
-                buf = self._ws[key] = torch.zeros(max(self.ws_bytes, 256), dtype=torch.uint8, device=dev)
+                buf = self._ws[key] = _new_workspace(dev, max(self.ws_bytes, 256))
             return buf
 
     def selected_base(self):
@@ -213,16 +288,19 @@ def topk_segmented(x, plan, xhat=None, out=None, gossip=None):
     dev = x.device
     L = lib()
     ws = plan.workspace(dev)
+    st = topk_status(ws)
+    st.check()
     g = _gossip(gossip, x, xhat)
     if g is not None:
         _lib.check(L.choco_gossip_topk_compress_segmented(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1], _ptr(plan.plan_dev),
                                                           plan.plan_host, plan.nseg, _ptr(vals), _ptr(idx), _ptr(ws),
                                                           ws.numel(), _stream(dev)),
                    "choco_gossip_topk_compress_segmented")
-        return vals, idx
-    _lib.check(L.choco_topk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
-                                               plan.nseg, _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(),
-                                               _stream(dev)), "choco_topk_compress_segmented")
+    else:
+        _lib.check(L.choco_topk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
+                                                   plan.nseg, _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(),
+                                                   _stream(dev)), "choco_topk_compress_segmented")
+    st.after_call()
     return vals, idx
 
 
@@ -237,9 +315,12 @@ def randk(x, k, seed, is_biased=True, xhat=None):
     idx = torch.empty(k, dtype=torch.int32, device=dev)
     L = lib()
     ws = workspace(dev, "topk", L.choco_randk_workspace_size(n))
+    st = topk_status(ws)
+    st.check()
     _lib.check(L.choco_randk_compress(_ptr(x), _ptr(xhat), n, int(k), int(seed) & (2**64 - 1),
                                       1 if is_biased else 0, _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(),
                                       _stream(dev)), "choco_randk_compress")
+    st.after_call()
     return vals, idx
 
 
@@ -250,6 +331,8 @@ def randk_segmented(x, plan, seed, is_biased=True, xhat=None, out=None, gossip=N
     dev = x.device
     L = lib()
     ws = plan.workspace(dev)
+    st = topk_status(ws)
+    st.check()
     g = _gossip(gossip, x, xhat)
     if g is not None:
         _lib.check(L.choco_gossip_randk_compress_segmented(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1],
@@ -257,11 +340,12 @@ def randk_segmented(x, plan, seed, is_biased=True, xhat=None, out=None, gossip=N
                                                            int(seed) & (2**64 - 1), 1 if is_biased else 0,
                                                            _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(), _stream(dev)),
                    "choco_gossip_randk_compress_segmented")
-        return vals, idx
-    _lib.check(L.choco_randk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
-                                                plan.nseg, int(seed) & (2**64 - 1), 1 if is_biased else 0,
-                                                _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(), _stream(dev)),
-               "choco_randk_compress_segmented")
+    else:
+        _lib.check(L.choco_randk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
+                                                    plan.nseg, int(seed) & (2**64 - 1), 1 if is_biased else 0,
+                                                    _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(), _stream(dev)),
+                   "choco_randk_compress_segmented")
+    st.after_call()
     return vals, idx
 
 

@@ -82,14 +82,33 @@ class DecentralizedAggregation(object):
 
 
 class CentralizedAggregation(object):
-    """The all-gather / all-reduce half of communication.py:138-226 that the
-    EF-sign and DGC consumers use (`_agg(data, op=, communication_scheme=,
-    async_op=)`): RCCL collectives on ROCm, gloo on CPU."""
+    """The all-gather / all-reduce / reduce half of communication.py:138-226 that the
+    EF-sign and DGC consumers use (`_agg(data, op=, communication_scheme=, async_op=)`):
+    RCCL collectives on ROCm, gloo on CPU.
 
-    def __init__(self, rank, world, neighbors_info=None, group=None):
+    Built as the reference builds it (communication.py:141-151; dgc.py:53-59 and
+    ef_sign_sgd.py:41-47 pass `world=conf.graph.ranks`, a list, which the reference
+    ignores): the group is `dist.new_group` of the neighbour ranks (every rank must make
+    the same call, as with the reference) and the world size is the number of neighbour
+    ranks.  `group=` overrides the group (e.g. an existing one); no neighbours -> the
+    default group."""
+
+    def __init__(self, rank, world=None, neighbors_info=None, group=None):
         self.rank = rank
-        self.group = group
-        self.world_size = float(world)
+        neighbor_ranks = list(neighbors_info.keys()) if neighbors_info else []
+        if group is not None:
+            self.group = group
+        elif neighbor_ranks and dist.is_initialized():
+            self.group = dist.new_group(neighbor_ranks)
+        else:
+            self.group = None
+        if neighbor_ranks:
+            self.world_size = float(len(neighbor_ranks))
+        elif isinstance(world, (list, tuple)):
+            self.world_size = float(len(world))
+        else:
+            self.world_size = float(world if world is not None else (dist.get_world_size() if dist.is_initialized()
+                                                                      else 1))
 
     def _agg(self, data, op=None, distributed=True, communication_scheme="all_reduce", async_op=False, **kargs):
         if not distributed:
@@ -101,6 +120,11 @@ class CentralizedAggregation(object):
             if async_op:
                 return data, req
             return data / self.world_size if op == "avg" else data
+        if communication_scheme == "reduce":
+            if op != "sum":
+                raise NotImplementedError
+            req = dist.reduce(data, dst=kargs["dst_rank"], op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+            return (data, req) if async_op else data
         if communication_scheme == "all_gather":
             gathered = [torch.empty_like(data) for _ in range(int(self.world_size))]
             req = dist.all_gather(gathered, data, group=self.group, async_op=async_op)

@@ -39,7 +39,11 @@
 #include "choco_common.h"
 
 #include <math.h>
+#include <stddef.h>
 #include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <unordered_map>
 
 namespace choco {
 
@@ -118,17 +122,40 @@ CHOCO_DEV void st_pol(T* p, T v) {
 
 enum TileMode { kTakeNone = 0, kTakeAll = 1, kTakePartial = 2 };
 
-struct TopkCtrl {
-  uint32_t s_lo, s_hi, shift, overflow;          // K2 -> K34
-  uint32_t reserved;
-  uint32_t pad[11];
-  uint32_t G[kNRep][kNBucket];                   // replicated bucket suffix totals
+// Candidate window of one call: keys >= s_lo are candidates, [s_lo, s_hi) is
+// split into 255 "maybe" buckets of width 2^shift, keys >= s_hi are "sure".
+// Written by K1 (cold call: the sample) or by the previous call's K34 (warm
+// call: the previous exact threshold and bucket counts, margin m / 1024 of k),
+// for the (n, k) it was made for.
+struct TopkBounds {
+  uint32_t s_lo, s_hi, shift, m1024;  // m1024 = 0: a sample / fallback window (no count targets)
+  int64_t n, k;
+  uint32_t valid, pad;
 };
+
+// The control block at the start of every top-k workspace.  Per-call state is
+// double-buffered by call parity `par` (the host keeps the call count of each
+// workspace, topk_warm_*): call c reads bounds[par], adds into G[par] and
+// overflow[par]; its K2 zeroes G[par ^ 1] / overflow[par ^ 1] for call c + 1
+// and its K34 writes bounds[par ^ 1] -- no kernel of call c touches state that
+// another kernel of call c still reads.
+struct TopkCtrl {
+  uint32_t status;                               // sticky error bits (kStatus*), read by the host lazily
+  uint32_t pad0[15];
+  uint32_t overflow[2];                          // bit 0: a side list overflowed; bit 1: take the exact fallback
+  uint32_t pad1[14];
+  TopkBounds bounds[2];
+  uint32_t pad2[16];
+  uint32_t G[2][kNRep][kNBucket];                // replicated bucket suffix totals
+};
+static_assert(offsetof(TopkCtrl, status) == CHOCO_TOPK_STATUS_OFFSET, "status word at the documented offset");
+constexpr uint32_t kStatusPollTimeout = 1u;    // a bounded wait of the exact fallback gave up: output invalid
+constexpr uint32_t kNoCandKey = 0x7F800000u;   // window that admits only inf / NaN keys (invalid bounds)
 
 struct TopkLayout {
   int64_t n;
   uint32_t tile, nb, side_cap;
-  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, off_wide, off_gcnt, total;
+  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, off_wide, off_gcnt, off_tinfo, total;
 };
 
 // Tile = ceil(n / kK2Target) rounded up to 32768 elements: one tile per CU, all
@@ -156,6 +183,7 @@ static TopkLayout topk_layout(int64_t n) {
   L.off_cval = o;  o += align_up((size_t)L.nb * tile * 4, 256);   // candidate values, chunk slot ranges
   L.off_cidx = o;  o += align_up((size_t)L.nb * tile * 4, 256);   // ... and indices
   L.off_gcnt = o;  o += align_up((size_t)L.nb * 8, 256);              // ... its per-tile (#>T, #==T)
+  L.off_tinfo = o; o += align_up((size_t)L.nb * 4, 256);              // per tile: candidates (compact) or ~0 (spilled)
   L.total = o;
   return L;
 }
@@ -834,15 +862,16 @@ CHOCO_DEV void sample_bounds(const uint32_t (&kk)[kSampleLoads * 4], const Sampl
 // GS: the sample is of d = (x + gamma (memory - xh)) - xh (K2 writes x_new later).
 template <bool XH, bool GS>
 __global__ __launch_bounds__(kK1Threads) void topk_bounds_kernel(const float* __restrict__ x,
-                                                                 const float* __restrict__ xh, int64_t n,
-                                                                 SampleRanks ranks, TopkCtrl* __restrict__ ctrl,
-                                                                 Gossip gs) {
+                                                                 const float* __restrict__ xh, int64_t n, int64_t k,
+                                                                 uint32_t par, SampleRanks ranks,
+                                                                 TopkCtrl* __restrict__ ctrl, Gossip gs) {
   __shared__ BoundsSmem sm;
   STAMP(30000, 0);
   const int lane = lane_id(), w = threadIdx.x >> 6;
-  // this call's bucket totals and overflow flag start from zero (K2 adds to them)
-  for (int i = threadIdx.x; i < kNRep * kNBucket; i += kK1Threads) (&ctrl->G[0][0])[i] = 0u;
-  if (threadIdx.x == 0) ctrl->overflow = 0u;
+  // this call's bucket totals and overflow flag start from zero (K2 adds to them);
+  // a cold call makes no assumption about what an earlier call left
+  for (int i = threadIdx.x; i < kNRep * kNBucket; i += kK1Threads) (&ctrl->G[par][0][0])[i] = 0u;
+  if (threadIdx.x == 0) ctrl->overflow[par] = 0u;
   float4 s[kSampleLoads], sh[kSampleLoads], sm_[kSampleLoads];
   load_sample<XH, GS>(x, xh, gs.mem, n, s, sh, sm_);
   uint32_t kk[kSampleLoads * 4];
@@ -868,10 +897,15 @@ __global__ __launch_bounds__(kK1Threads) void topk_bounds_kernel(const float* __
   uint32_t tot_maybe;
   block_excl_scan(nmaybe, sm.scratch, &tot_maybe);
   if (threadIdx.x == 0) {
-    ctrl->s_lo = bk.s_lo;
-    ctrl->s_hi = bk.s_hi;
-    ctrl->shift = bk.shift;
-    if (tot_maybe > (uint32_t)(kSampleN / 4)) ctrl->overflow = 2u;
+    TopkBounds& B = ctrl->bounds[par];
+    B.s_lo = bk.s_lo;
+    B.s_hi = bk.s_hi;
+    B.shift = bk.shift;
+    B.m1024 = 0u;  // a sample window: no count targets to measure the next call's drift against
+    B.n = n;
+    B.k = k;
+    B.valid = 1u;
+    if (tot_maybe > (uint32_t)(kSampleN / 4)) ctrl->overflow[par] = 2u;
   }
   STAMP(30000, 2);
 }
@@ -882,10 +916,10 @@ __global__ __launch_bounds__(kK1Threads) void topk_bounds_kernel(const float* __
 // writes x_new back and selects on d = x_new - xh.
 template <int MODE, bool XH, bool GS = false>
 __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, uint32_t tile,
-    uint32_t side_cap, uint64_t seed, uint32_t hs_lo, uint64_t hs_hi, TopkCtrl* __restrict__ ctrl,
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
+    uint32_t par, uint32_t side_cap, uint64_t seed, uint32_t hs_lo, uint64_t hs_hi, TopkCtrl* __restrict__ ctrl,
     uint32_t* __restrict__ cum_tab, uint32_t* __restrict__ cntw, uint32_t* __restrict__ side,
-    float* __restrict__ cval, uint32_t* __restrict__ cidx, Gossip gs) {
+    float* __restrict__ cval, uint32_t* __restrict__ cidx, uint32_t* __restrict__ tinfo, Gossip gs) {
   static_assert(!GS || (MODE == kData && XH), "the gossip step needs x_hat and data keys");
   __shared__ StreamSmem sm;
   STAMP(1024 + blockIdx.x, 0);
@@ -915,14 +949,24 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   uint32_t c = (uint32_t)w;
   float4 A[kK2Unroll], B[kK2Unroll];
   Buckets bk;
+  // the NEXT call's bucket totals and overflow word start from zero (no kernel of
+  // this call reads them: this call's are G[par] / overflow[par])
+  for (int i = (int)b * kK2Threads + tid; i < kNRep * kNBucket; i += (int)nb * kK2Threads)
+    (&ctrl->G[par ^ 1u][0][0])[i] = 0u;
+  if (b == 0 && tid == 0) ctrl->overflow[par ^ 1u] = 0u;
   if constexpr (MODE == kData) {
     if (!GS) load_rows_full<XH>(ts, batch0(c), lane, A);
     if (kTwoChunks) load_rows_full<XH>(ts, batch0(c + kK2Waves), lane, B);
     else if (!kOneBatch && !XH) load_rows_full<XH>(ts, batch1(c), lane, B);
-    bk = make_buckets_from(ctrl->s_lo, ctrl->s_hi, ctrl->shift, seed);
+    // this call's window: K1's sample (cold call) or the previous call's (warm call)
+    const TopkBounds W = ctrl->bounds[par];
+    const bool ok = W.valid != 0u && W.n == n && W.k == k && W.shift < 32u;
+    bk = ok ? make_buckets_from(W.s_lo, W.s_hi, W.shift, seed) : make_buckets_from(kNoCandKey, kNoCandKey, 0u, seed);
+    // no window for this (n, k) (a workspace the host believed warm): the exact fallback
+    if (!ok && b == 0 && tid == 0) atomicOr(&ctrl->overflow[par], 2u);
     // K1 flagged a degenerate sample: K34 will take the exact fallback, which needs
     // nothing from this kernel (with the fused gossip step the stream must still run)
-    if (!GS && (ctrl->overflow & 2u) != 0u) return;
+    if (!GS && (!ok || (ctrl->overflow[par] & 2u) != 0u)) return;
   } else {
     bk = make_buckets(hs_lo, hs_hi, seed);
   }
@@ -934,9 +978,14 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   __syncthreads();
   bk.n = n;
   if (MODE == kHash && b == 0 && tid == 0) {
-    ctrl->s_lo = bk.s_lo;
-    ctrl->s_hi = bk.s_hi;
-    ctrl->shift = bk.shift;
+    TopkBounds& W = ctrl->bounds[par];
+    W.s_lo = bk.s_lo;
+    W.s_hi = bk.s_hi;
+    W.shift = bk.shift;
+    W.m1024 = 0u;
+    W.n = n;
+    W.k = k;
+    W.valid = 1u;
   }
   STAMP(1024 + b, 1);
 
@@ -1104,11 +1153,11 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     }
     if (t == 0) sm.ccnt[nchunk] = csum;
     const uint32_t sure = csum - hsum;
-    if (t == 0 && hsum > side_cap) atomicOr(&ctrl->overflow, 1u);
+    if (t == 0 && hsum > side_cap) atomicOr(&ctrl->overflow[par], 1u);
     if (t < kNBucket) {
       const uint32_t cum = t < kNMaybe ? sure + above + hv : sure;
       cum_tab[b * kNBucket + jb] = cum;
-      atomicAdd(&ctrl->G[b & (kNRep - 1)][jb], cum);
+      atomicAdd(&ctrl->G[par][b & (kNRep - 1)][jb], cum);
       if (t < kNMaybe) sm.hist[jb] = above;  // counting-sort cursor of bucket jb (hist is dead now)
     }
     STAMP(22000 + b, 0);
@@ -1140,19 +1189,14 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       };
       // Store-only loop: no global load may follow the stores inside it (vmcnt
       // counts stores too, so a load's wait would wait for every store before it).
-#ifdef CHOCO_DIAG_NOBURST  // diagnostic only: no pair stores / no side list (wrong results)
-      if (CHOCO_DIAG_NOBURST == 1) continue;
-#endif
       for (uint32_t j = h; j < lc; j += 32) {
         const uint2 pr = sm.u.pairs[ls + j];
-#ifdef CHOCO_DIAG_NOBURST
-        if (CHOCO_DIAG_NOBURST == 2) { to_side(pr.x, pr.y); continue; }
-#endif
         st_pol<CHOCO_K2_STORE>(&ov[j], __uint_as_float(pr.x));
         st_pol<CHOCO_K2_STORE>(&oi[j], pr.y);
         to_side(pr.x, pr.y);
       }
       if (have && h == 0) cntw[(int64_t)b * nchunk + cc] = spilled ? cnt : (cc == 0 ? csum : 0u);
+      if (cc == 0 && lane == 0) tinfo[b] = spilled ? 0xFFFFFFFFu : csum;
       // rare (a wave's LDS region overflowed): this tile keeps per-chunk slot
       // ranges; the pairs spilled during the stream are only binned here
       for (uint32_t j = lc + h; j < cnt; j += 32) to_side(__float_as_uint(ov[j]), oi[j]);
@@ -1235,6 +1279,7 @@ struct FinSmem {
   uint32_t run_start[kMaxTileChunks + 1];
   uint32_t scratch[40];
   uint32_t bc[8];
+  uint32_t ctl[8];  // this call's window (s_lo, s_hi, shift), overflow word, margin m1024
 };
 static_assert(kK2Target <= kK4Threads, "K34 keeps one tile per thread");
 
@@ -1265,15 +1310,28 @@ CHOCO_DEV void block_find_rank8k(const uint32_t* hist, uint32_t rank, uint32_t* 
   __syncthreads();
 }
 
+// The same over hist[nbins], nbins <= kK4Threads: one bin per thread.
+CHOCO_DEV void block_find_rank1k(const uint32_t* hist, uint32_t nbins, uint32_t rank, uint32_t* scratch,
+                                  uint32_t* out) {
+  const int tid = threadIdx.x;
+  const uint32_t hv = (uint32_t)tid < nbins ? hist[tid] : 0u;
+  uint32_t total;
+  const uint32_t pre = block_excl_scan(hv, scratch, &total);
+  const uint32_t above = total - pre - hv;  // entries in bins above mine
+  if (above < rank && rank <= above + hv) { out[0] = (uint32_t)tid; out[1] = rank - above; }
+  __syncthreads();
+}
+
 // Emission: a batch is kEmitRows rows of kK4Threads candidate positions; in
 // row i thread t owns position p0 + i * kK4Threads + t, so every load and
 // store instruction is contiguous across the wave.
 // Candidate slot of tile position p (positions past the tile's total clamp to
 // the tile start: loads stay unconditional).  One run (the compact layout)
 // needs no search.
-CHOCO_DEV int64_t cand_addr(const uint32_t* run_start, uint32_t nchunk, uint32_t tot, uint32_t p, int64_t tb) {
+CHOCO_DEV int64_t cand_addr(const uint32_t* run_start, uint32_t nchunk, uint32_t tot, uint32_t p, int64_t tb,
+                            bool compact) {
   if (p >= tot) return tb;
-  if (run_start[1] >= tot) return tb + p;
+  if (compact || run_start[1] >= tot) return tb + p;
   uint32_t lo = 0, hi = nchunk - 1;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) >> 1;
@@ -1322,14 +1380,6 @@ CHOCO_DEV uint32_t ld_sc1(const uint32_t* p) {
   return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// bounded poll of a counter written by running workgroups (s_sleep between
-// polls); returns when *p >= want
-CHOCO_DEV void poll_ge(const uint32_t* p, uint32_t want) {
-  for (uint32_t it = 0; it < (1u << 22); ++it) {
-    if (ld_sc1(p) >= want) break;
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
 
 // every wave's stores drained, the workgroup joined, one lane adds
 CHOCO_DEV void publish_add(uint32_t* counter) {
@@ -1374,11 +1424,17 @@ CHOCO_DEV uint32_t wave0_fetch_add(uint32_t* p, uint32_t v) {
   const uint32_t r = __hip_atomic_fetch_add(p, lane_id() == 0 ? v : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return __builtin_amdgcn_readfirstlane(r);
 }
-CHOCO_DEV void wave0_poll_ge(const uint32_t* p, uint32_t want) {
-  for (uint32_t it = 0; it < (1u << 22); ++it) {
-    if (__builtin_amdgcn_readfirstlane(ld_sc1(p)) >= want) break;
+// Bounded: false when the budget ran out (a stuck producer must not hang the GPU;
+// the caller flags the call's output invalid in the workspace status word).
+#ifndef CHOCO_POLL_BUDGET  // diagnostic builds only (tools/build_variants.py "poll1")
+#define CHOCO_POLL_BUDGET (1u << 22)
+#endif
+CHOCO_DEV bool wave0_poll_ge(const uint32_t* p, uint32_t want) {
+  for (uint32_t it = 0; it < (uint32_t)CHOCO_POLL_BUDGET; ++it) {
+    if (__builtin_amdgcn_readfirstlane(ld_sc1(p)) >= want) return true;
     __builtin_amdgcn_s_sleep(2);
   }
+  return __builtin_amdgcn_readfirstlane(ld_sc1(p)) >= want;
 }
 
 CHOCO_DEV constexpr int wide_shift(int r) { return r == 0 ? 20 : (r == 1 ? 9 : 0); }
@@ -1443,10 +1499,36 @@ CHOCO_DEV void wide_tile(const Src<MODE, XH>& src, int64_t lo, int64_t hi, F&& f
   }
 }
 
+// The next call's window after a fallback: keys at count levels k (1 +- 1/8) from the
+// complete coarse histogram hist[0] (key >> 20 of every key), bin-rounded outward.
+CHOCO_DEV void fallback_window(WideCtrl* W, int64_t n, int64_t k, ExactSmem& es, TopkBounds* next) {
+  for (int i = threadIdx.x; i < 2048; i += blockDim.x) es.hist[i] = ld_sc1(&W->hist[0][i]);
+  if (threadIdx.x < 4) es.bc[threadIdx.x] = 0u;
+  __syncthreads();
+  const uint64_t lo_t = std::min<uint64_t>((uint64_t)n, (uint64_t)k + (uint64_t)k / 8);
+  const uint64_t hi_t = std::max<uint64_t>(1, (uint64_t)k - (uint64_t)k / 8);
+  block_find_two(es.hist, (uint32_t)lo_t, (uint32_t)hi_t, es.scratch, es.bc);
+  if (threadIdx.x == 0) {
+    const uint64_t x_lo = (uint64_t)es.bc[0] << 20, x_hi = ((uint64_t)es.bc[2] + 1) << 20;
+    const uint64_t width = x_hi > x_lo + 255 ? x_hi - x_lo : 255;
+    uint32_t sh = 0;
+    while (((uint64_t)kNMaybe << sh) < width) ++sh;
+    next->s_lo = (uint32_t)x_lo;
+    next->s_hi = (uint32_t)std::min<uint64_t>(x_lo + ((uint64_t)kNMaybe << sh), 0xFFFFFFFFull);
+    next->shift = sh;
+    next->m1024 = 0u;
+    next->n = n;
+    next->k = k;
+    next->valid = 1u;
+  }
+  __syncthreads();
+}
+
 template <int MODE, bool XH>
 CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
                              float scale, WideCtrl* W, uint32_t* __restrict__ gcnt, float* __restrict__ out_val,
-                             int32_t* __restrict__ out_idx, int64_t idx_base, ExactSmem& es, uint32_t* s_tk) {
+                             int32_t* __restrict__ out_idx, int64_t idx_base, ExactSmem& es, uint32_t* s_tk,
+                             uint32_t* __restrict__ status, TopkBounds* next) {
   const int tid = threadIdx.x;
   const bool w0 = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;  // wave-uniform
   for (;;) {
@@ -1463,7 +1545,8 @@ CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uin
                          ld_sc1(&W->done[4]));
 #endif
     if (phase > 0) {
-      if (w0) wave0_poll_ge(&W->done[phase - 1], nb);
+      if (w0 && !wave0_poll_ge(&W->done[phase - 1], nb) && lane_id() == 0)
+        atomicOr(status, kStatusPollTimeout);
       __syncthreads();
     }
     const int64_t lo = (int64_t)t * tile, hi = min(lo + (int64_t)tile, n);
@@ -1510,6 +1593,7 @@ CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uin
     } else {
       const uint32_t T = prefix;  // all digits known: T = the k-th largest key, krem = ties to take
       const uint32_t r = krem;
+      if (phase == 3 && t == 0 && next != nullptr) fallback_window(W, n, k, es, next);
       if (phase == 3) {
         uint32_t gt = 0, eq = 0;
         wide_tile(src, lo, hi, [&](int64_t, int nin, const uint32_t (&kk)[4], const float (&)[4]) {
@@ -1583,13 +1667,81 @@ CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uin
   }
 }
 
+// ----------------------------------------------------------------------------
+// Warm start: the NEXT call's window from this call's bucket counts
+//
+// G[j] = #{key >= s_lo + j 2^shift} (j = 0..255, G[255] = #{key >= s_hi}) is
+// this call's key distribution around T.  The next window puts its candidate
+// floor where this call had k (1 + m) keys above, and its sure ceiling where it
+// had k (1 - m): if the next delta's distribution moved by less than m the next
+// call selects inside it.  m (in 1/1024 of k) is twice the miss of the edges
+// this call aimed at, decaying by half per call to kWarmM0.  Edges outside the
+// window are extrapolated from its density (G[0] - k keys over [s_lo, T]).
+// Wave 0 of one workgroup; ~0.3 us, after that workgroup's emission.
+// ----------------------------------------------------------------------------
+constexpr uint32_t kWarmM0 = 20;     // ~2 % of k (the bench's randn deltas drift ~0.1 %)
+constexpr uint32_t kWarmMMax = 512;  // 50 %
+CHOCO_DEV void next_window(const uint32_t* G, uint32_t s_lo, uint32_t s_hi, uint32_t shift, uint32_t m_prev,
+                           uint32_t T, int64_t n, int64_t k, TopkBounds* __restrict__ out) {
+  const int lane = lane_id();
+  const double kd = (double)k;
+  uint32_t m = kWarmM0;
+  if (m_prev != 0u) {  // this call's window aimed at k (1 + m_prev) / k (1 - m_prev)
+    const double e = fmax(fabs((double)G[0] - kd * (1.0 + m_prev / 1024.0)),
+                          fabs((double)G[kNMaybe] - kd * (1.0 - m_prev / 1024.0)));
+    const double me = ceil(2.0 * e / kd * 1024.0);
+    m = (uint32_t)fmin((double)kWarmMMax, fmax(fmax((double)kWarmM0, me), (double)(m_prev / 2)));
+  }
+  const uint64_t lo_t = (uint64_t)k + (uint64_t)k * m / 1024u;
+  const uint64_t hi_t = (uint64_t)k - std::min<uint64_t>((uint64_t)k, (uint64_t)k * m / 1024u);
+  uint32_t nlo = 0, nhi = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t g = G[4 * lane + q];
+    nlo += (uint64_t)g >= lo_t ? 1u : 0u;  // G is non-increasing: a prefix of the buckets
+    nhi += (uint64_t)g > hi_t ? 1u : 0u;
+  }
+  nlo = wave_sum(nlo);
+  nhi = wave_sum(nhi);
+  if (lane != 0) return;
+  const uint64_t w0 = (uint64_t)s_hi - s_lo;
+  uint64_t x_lo, x_hi;
+  if (nlo >= 1u) {
+    x_lo = (uint64_t)s_lo + ((uint64_t)(nlo - 1u) << shift);
+  } else {  // fewer than k (1 + m) keys in the whole window: extend it downwards
+    const double D = (double)(T - s_lo), C = (double)G[0] - kd, need = (double)lo_t - (double)G[0];
+    const double dl = C >= fmax(kd / 1024.0, 16.0) ? 2.0 * D * need / C + (double)(1u << shift)
+                                                   : 2.0 * (double)w0 + D;
+    x_lo = dl >= (double)s_lo ? 0ull : (uint64_t)((double)s_lo - dl);
+  }
+  if (nhi <= (uint32_t)kNMaybe) {
+    x_hi = std::min<uint64_t>((uint64_t)s_lo + ((uint64_t)nhi << shift), s_hi);
+  } else {  // more than k (1 - m) keys are "sure": extend it upwards
+    const double D = (double)(s_hi - T), C = kd - (double)G[kNMaybe], need = (double)G[kNMaybe] - (double)hi_t;
+    const double dh = C >= fmax(kd / 1024.0, 16.0) ? 2.0 * D * need / C + (double)(1u << shift)
+                                                   : 2.0 * (double)w0 + D;
+    x_hi = (uint64_t)fmin((double)s_hi + dh, 2147483648.0);
+  }
+  const uint64_t width = x_hi > x_lo + kNMaybe ? x_hi - x_lo : (uint64_t)kNMaybe;
+  uint32_t sh = 0;
+  while (((uint64_t)kNMaybe << sh) < width) ++sh;
+  out->s_lo = (uint32_t)x_lo;
+  out->s_hi = (uint32_t)std::min<uint64_t>(x_lo + ((uint64_t)kNMaybe << sh), 0xFFFFFFFFull);
+  out->shift = sh;
+  out->m1024 = m;
+  out->n = n;
+  out->k = k;
+  out->valid = 1u;
+}
+
 template <int MODE, bool XH>
 __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
     uint32_t side_cap, uint64_t seed, float scale, TopkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ cum_tab,
     const uint32_t* __restrict__ cntw, const uint32_t* __restrict__ side, const float* __restrict__ cval,
     const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
-    int64_t idx_base, WideCtrl* __restrict__ wide, uint32_t* __restrict__ gcnt) {
+    int64_t idx_base, WideCtrl* __restrict__ wide, uint32_t* __restrict__ gcnt, uint32_t par,
+    uint32_t* __restrict__ status, const uint32_t* __restrict__ tinfo) {
   __shared__ FinSmem fs;
   __shared__ ExactSmem es;
   __shared__ uint32_t s_tk;
@@ -1601,31 +1753,39 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   // every tile's j*-independent "sure" count, this tile's chunk counts
   const uint32_t ku = (uint32_t)k;
   const uint32_t nchunk = tile / (uint32_t)kChunk;
+  // the tile's candidates: one compact run (the usual case) or per-chunk slot runs
+  const uint32_t ti = tinfo[b];
+  const bool compact = ti != 0xFFFFFFFFu;
   uint32_t cw[kCPT];
 #pragma unroll
   for (int q = 0; q < kCPT; ++q) {
     const uint32_t j = kCPT * tid + q;
-    cw[q] = j < nchunk ? cntw[b * nchunk + j] : 0u;
+    cw[q] = (!compact && j < nchunk) ? cntw[b * nchunk + j] : 0u;
   }
   uint32_t cword = 0;
-  if (tid < 4) cword = __hip_atomic_load(&ctrl->s_lo + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  {
+    const TopkBounds& Bw = ctrl->bounds[par];
+    const uint32_t* src = tid == 0 ? &Bw.s_lo : tid == 1 ? &Bw.s_hi : tid == 2 ? &Bw.shift
+                        : tid == 3 ? &ctrl->overflow[par] : &Bw.m1024;
+    if (tid < 5) cword = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   const bool mine_tile = tid < (int)nb;
   const uint32_t* row = cum_tab + (int64_t)(mine_tile ? tid : 0) * kNBucket;  // clamped: loads unconditional
   const uint32_t sure_t = row[kNMaybe];
   uint32_t g[kNRep];
   if (tid < kNBucket) {
 #pragma unroll
-    for (int r = 0; r < kNRep; ++r) g[r] = ctrl->G[r][tid];
+    for (int r = 0; r < kNRep; ++r) g[r] = ctrl->G[par][r][tid];
   }
-  if (tid < 4) fs.bc[tid] = cword;  // s_lo, s_hi, shift, overflow
-  const uint32_t tot = chunk_run_starts(cw, nchunk, fs.run_start, fs.scratch);
-  const uint32_t s_lo = fs.bc[0], shift = fs.bc[2], overflow = fs.bc[3];
+  if (tid < 5) fs.ctl[tid] = cword;  // s_lo, s_hi, shift, overflow, m1024
+  const uint32_t tot = compact ? ti : chunk_run_starts(cw, nchunk, fs.run_start, fs.scratch);
+  const uint32_t s_lo = fs.ctl[0], shift = fs.ctl[2], overflow = fs.ctl[3];
   STAMP(26000 + b, 0);
   // ---- the addresses of the tile's first emission batch (it does not depend on T)
   const int64_t tb = b * (int64_t)tile;
   int64_t addr[kEmitR];
 #pragma unroll
-  for (int i = 0; i < kEmitR; ++i) addr[i] = cand_addr(fs.run_start, nchunk, tot, (uint32_t)(i * kK4Threads + tid), tb);
+  for (int i = 0; i < kEmitR; ++i) addr[i] = cand_addr(fs.run_start, nchunk, tot, (uint32_t)(i * kK4Threads + tid), tb, compact);
   float v[kEmitR];
   uint32_t idx[kEmitR];
   if (tid < kNBucket) {
@@ -1649,7 +1809,8 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     // the sample's guess was off: the exact radix select over the whole input, shared
     // by every workgroup through the ticketed queue (wide_fallback)
     Src<MODE, XH> src{x, xh, seed};
-    wide_fallback(src, n, k, tile, nb, scale, wide, gcnt, out_val, out_idx, idx_base, es, &s_tk);
+    wide_fallback(src, n, k, tile, nb, scale, wide, gcnt, out_val, out_idx, idx_base, es, &s_tk, status,
+                  MODE == kData ? &ctrl->bounds[par ^ 1u] : nullptr);
   } else {
     // ---- thread t <-> tile t: bucket-j* key count and side-list offset
     uint32_t above = 0, cb = 0, off = 0;
@@ -1729,7 +1890,9 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     while (sh > 0) {
       const int dsh = sh > kSelBits ? sh - kSelBits : 0;
       const uint32_t dmask = (1u << (sh - dsh)) - 1u;
-      for (int i = tid; i < (1 << kSelBits); i += kK4Threads) fs.hist[i] = 0;
+      // a digit of <= 10 bits (the warm window's buckets): one bin per thread
+      const bool narrow = dmask < (uint32_t)kK4Threads;
+      for (int i = tid; i < (narrow ? (int)dmask + 1 : (1 << kSelBits)); i += kK4Threads) fs.hist[i] = 0;
       __syncthreads();  // also: the bucket keys are in LDS
       for (uint32_t j = tid; j < M; j += kK4Threads) {
         const uint32_t rel = fs.keys[j] - base_j;
@@ -1737,7 +1900,8 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
       }
       __syncthreads();
       STAMP(28000 + b, 2);
-      block_find_rank8k(fs.hist, krem, fs.scratch, fs.bc + 5);
+      if (narrow) block_find_rank1k(fs.hist, dmask + 1, krem, fs.scratch, fs.bc + 5);
+      else block_find_rank8k(fs.hist, krem, fs.scratch, fs.bc + 5);
       STAMP(28000 + b, 3);
       prefix |= fs.bc[5] << dsh;
       krem = fs.bc[6];
@@ -1780,7 +1944,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads * kEmitR) {
       if (p0 != 0 || !CHOCO_K34_PREFETCH) {  // workgroup-uniform: batches after the prefetched first one
 #pragma unroll
-        for (int i = 0; i < kEmitR; ++i) addr[i] = cand_addr(fs.run_start, nchunk, tot, p0 + i * kK4Threads + tid, tb);
+        for (int i = 0; i < kEmitR; ++i) addr[i] = cand_addr(fs.run_start, nchunk, tot, p0 + i * kK4Threads + tid, tb, compact);
 #pragma unroll
         for (int i = 0; i < kEmitR; ++i) {
           v[i] = cval[addr[i]];
@@ -1818,643 +1982,67 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
       }
       out += nsel;
     }
+    if (MODE == kData && b == 0 && tid < 64)
+      next_window(fs.G, s_lo, fs.ctl[1], shift, fs.ctl[4], T, n, k, &ctrl->bounds[par ^ 1u]);
   }
+  // random-k windows come from the host each call: nothing for the next call to reuse
+  if (MODE == kHash && b == 0 && tid == 0) ctrl->bounds[par ^ 1u].valid = 0u;
   STAMP(24576 + b, 2);
-}
-
-// ----------------------------------------------------------------------------
-// Fused one-launch top-k (kData): bounds + stream + select + emit
-//
-// One launch of nb + 1 workgroups (nb <= 255 tiles: every workgroup has a CU of
-// its own on MI355X).  Workgroups take TICKETS from a counter: ticket 0 computes
-// the sample bounds (K1's job) and publishes them; ticket t >= 1 streams tile
-// t - 1 (K2's job), keeping its candidates in LDS; when the tickets run out a
-// workgroup waits until every tile has published its bucket counts and side
-// list, then -- like K34, redundantly in every workgroup -- selects the exact
-// threshold T and each tile's output offset, and finally emits the candidates
-// of its OWN tile(s) straight from LDS to the output.  Against K1 + K2 + K34:
-// no candidate write and re-read (~14 MB at k = 1 %), no kernel boundaries.
-//
-// Deadlock-free by construction: a workgroup only waits on work owned by
-// workgroups that have already taken a ticket, i.e. are running (the bounds
-// and every claimed tile), never on a workgroup that may not be resident.
-// When fewer workgroups are resident than tiles (another kernel or process
-// holds CUs), the running ones take more tickets and process those extra tiles
-// in "spill" mode: candidates go to their global chunk slots (K2's layout) and
-// are emitted from there.  The same happens to a tile whose candidates
-// overflow a wave's LDS region (dense inputs / large k).
-//
-// Counters are reset by the last workgroup to finish; the bucket totals are
-// double-buffered by call parity and the idle set is zeroed by the bounds
-// workgroup, so no workgroup clears state another may still read.
-// ----------------------------------------------------------------------------
-#ifndef CHOCO_FUSED_PRE  // batches per wave issued before the bounds are known (1 or 2)
-#define CHOCO_FUSED_PRE 2
-#endif
-#ifndef CHOCO_FUSED_DIAG  // register-pressure diagnostics only (1: no emission)
-#define CHOCO_FUSED_DIAG 0
-#endif
-constexpr int kFB = 1024;                  // buckets: 1023 "maybe" + 1 "sure"
-constexpr int kFMaybe = kFB - 1;
-constexpr int kFMaxChunks = 512;           // tile <= 512 chunks (1M elements)
-constexpr int kFMCap = 8192;               // bucket-j* keys selected in LDS
-constexpr int kFSelBits = 12;
-constexpr int kFMaxOwn = 256;              // tiles one workgroup may process
-constexpr int64_t kFTileTarget = 255;      // + the bounds workgroup = 256 CUs
-static_assert(kFB == kK2Threads, "one bucket per thread at the tile end");
-
-struct FusedCtrl {
-  uint32_t claim, done, exitc, ready;      // tickets, tiles published, workgroups done, bounds published
-  uint32_t s_lo, s_hi, shift, epoch;
-  uint32_t overflow, pad[55];
-  uint32_t G[2][kNRep][kFB];               // replicated bucket suffix totals, by call parity
-};
-
-struct FusedLayout {
-  int64_t n;
-  uint32_t tile, nb, side_cap, nchunk;
-  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, total;
-};
-
-static FusedLayout fused_layout(int64_t n) {
-  FusedLayout L{};
-  L.n = n;
-  int64_t tile = (n + kFTileTarget - 1) / kFTileTarget;
-  tile = std::max<int64_t>(kTileQuant, (tile + kTileQuant - 1) / kTileQuant * kTileQuant);
-  L.tile = (uint32_t)tile;
-  L.nb = (uint32_t)((n + tile - 1) / tile);
-  L.nchunk = (uint32_t)(tile / kChunk);
-  L.side_cap = (uint32_t)std::min<int64_t>(kMaybeCap, tile);
-  size_t o = topk_layout(n).off_cum;  // past the fixed header (TopkCtrl + WideCtrl) of every top-k workspace
-  L.off_cum = o;   o += align_up((size_t)L.nb * kFB * 4, 256);
-  L.off_cntw = o;  o += align_up((size_t)L.nb * L.nchunk * 4, 256);
-  L.off_side = o;  o += align_up((size_t)L.nb * L.side_cap * 4, 256);
-  L.off_cval = o;  o += align_up((size_t)L.nb * tile * 4, 256);
-  L.off_cidx = o;  o += align_up((size_t)L.nb * tile * 4, 256);
-  // the control block lies past everything the three-kernel path (random-k on the
-  // same workspace) writes, so its counters stay as the last fused call left them
-  L.off_ctrl = std::max(o, topk_layout(n).total);
-  L.total = L.off_ctrl + align_up(sizeof(FusedCtrl), 256);
-  return L;
-}
-
-static bool fused_fits(int64_t n) {
-  return n > kSmallN && (int64_t)fused_layout(n).nchunk <= kFMaxChunks;
-}
-
-struct FusedSmem {
-  union {
-    struct {  // stream: per-wave entry rings
-      float4 ent_v[kK2Waves][kEnt];
-      uint32_t ent_i[kK2Waves][kEnt];
-    };
-    struct {  // select: bucket-j* keys + radix histogram (tile map / tile info before / after)
-      uint32_t keys[kFMCap];
-      uint32_t shist[1 << kFSelBits];
-    };
-  };
-  union {
-    uint2 pairs[kK2Waves * kPairsPerWave];  // candidates of the LDS tile, per-wave regions
-    SampleHist sh;                           // bounds workgroup, before any tile
-    ExactSmem es;                            // single-workgroup fallback
-  } u;
-  float4 trash_v[64];
-  uint32_t trash_i[64];
-  uint32_t cmeta[kFMaxChunks];       // LDS tile, per chunk: LDS start | LDS count << 16
-  uint32_t ccnt[kFMaxChunks + 1];    // LDS tile, per chunk: candidates, then their exclusive prefix
-  uint32_t cmeta2[kFMaxChunks];      // the same for spill-mode tiles
-  uint32_t ccnt2[kFMaxChunks + 1];
-  uint32_t hist[kFB];                // maybe-key bucket counts, then counting-sort cursors
-  uint32_t kbase[kK4Threads];
-  uint32_t G[kFB];
-  uint32_t ecnt[2][kEmitRows * (kK4Threads / 64) + 1];
-  uint32_t own[kFMaxOwn];            // tiles of this workgroup: tile | (in LDS) << 31
-  uint32_t cnt[kK2Waves];
-  uint32_t scratch[40];
-  uint32_t bc[8];
-  uint32_t next_chunk, spill, ticket, nown;
-};
-
-struct BoundsView {
-  SampleHist& sh;
-  uint32_t* scratch;
-  uint32_t* bc;
-};
-
-// Over hist[1 << kFSelBits] (ascending), the bin of the rank-th largest entry and
-// the rank inside it -> out[0], out[1]; ends with a barrier.
-CHOCO_DEV void block_find_rank4k(const uint32_t* hist, uint32_t rank, uint32_t* scratch, uint32_t* out) {
-  constexpr int per = (1 << kFSelBits) / kK4Threads;
-  const int tid = threadIdx.x;
-  uint32_t hv[per];
-  uint32_t local = 0;
-#pragma unroll
-  for (int j = 0; j < per; ++j) {
-    hv[j] = hist[tid * per + j];
-    local += hv[j];
-  }
-  uint32_t total;
-  const uint32_t pre = block_excl_scan(local, scratch, &total);
-  const uint32_t above = total - pre - local;
-  if (above < rank && rank <= above + local) {
-    uint32_t acc = above;
-#pragma unroll
-    for (int j = per - 1; j >= 0; --j) {
-      if (acc < rank && rank <= acc + hv[j]) { out[0] = (uint32_t)(tid * per + j); out[1] = rank - acc; }
-      acc += hv[j];
-    }
-  }
-  __syncthreads();
-}
-
-// Stream one tile (K2's body).  lds_mode: candidates may stay in the waves' LDS
-// regions; otherwise every candidate goes to its chunk's global slots.
-template <bool XH>
-CHOCO_DEV void fused_stream_tile(const Src<kData, XH>& src, const float* __restrict__ x, const float* __restrict__ xh,
-                                 int64_t n, uint32_t tile, uint32_t b, bool lds_mode, const Buckets& bk,
-                                 FusedSmem& sm, uint32_t* ccnt, uint32_t* cmeta, float* __restrict__ cval,
-                                 uint32_t* __restrict__ cidx, float4 (&A)[kK2Unroll], float4 (&B)[kK2Unroll],
-                                 const TileRsrc& ts) {
-  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  constexpr bool kTwoChunks = !XH;  // A and B hold the wave's next two chunks
-  const uint32_t nchunk = tile / (uint32_t)kChunk;
-  const int64_t tb = (int64_t)b * tile;
-  const int64_t tlen = min((int64_t)tile, n - tb);
-  auto batch0 = [&](uint32_t c) -> uint32_t {
-    return (c < nchunk && (int64_t)(c + 1) * kChunk <= tlen) ? c * (uint32_t)kChunk * 4u : kNoChunk;
-  };
-  WaveAcc a{};
-  if (!lds_mode) a.lfill = (uint32_t)kPairsPerWave;  // no LDS room: every pair spills
-  auto run_chunk = [&](uint32_t cc, const float4 (&R)[kK2Unroll]) {
-    const int64_t cbeg = tb + (int64_t)cc * kChunk;
-    const int64_t cend = min(cbeg + kChunk, n);
-    float* __restrict__ ov = cval + cbeg;
-    uint32_t* __restrict__ oi = cidx + cbeg;
-    a.estaged = a.eflushed = a.staged = a.lcnt = 0u;
-    a.lstart = a.lfill;
-    if (cbeg + kChunk <= n) {
-      process_batch<XH>(src, R, cbeg, cend, sm, w, lane, a, ov, oi, bk);
-    } else {
-      for (int64_t base = cbeg; base < cend; base += 256) {
-        const int64_t i = base + 4 * lane;
-        float tt[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) tt[q] = (i + q < cend) ? src.val(i + q) : 0.f;
-        process_row<kData, XH, true>(src, make_float4(tt[0], tt[1], tt[2], tt[3]), i, cend, sm, w, lane, a, ov, oi,
-                                     bk);
-      }
-    }
-    const uint32_t rest = a.estaged - a.eflushed;
-    if (rest) flush_entries(src, sm, w, lane, a, rest, ov, oi, bk);
-    if (lane == 0) {
-      ccnt[cc] = a.staged;
-      cmeta[cc] = (w * kPairsPerWave + (a.lstart < (uint32_t)kPairsPerWave ? a.lstart : 0u)) | (a.lcnt << 16);
-    }
-  };
-  uint32_t c = (uint32_t)w;
-  if constexpr (kTwoChunks) {
-    uint32_t cA = c, cB = c + kK2Waves;
-    for (;;) {
-      if (cA >= nchunk) break;
-      const uint32_t nA = claim_chunk(sm, lane);
-      run_chunk(cA, A);
-      load_rows_full<XH>(ts, batch0(nA), lane, A);
-      cA = nA;
-      if (cB >= nchunk) break;
-      const uint32_t nB = claim_chunk(sm, lane);
-      run_chunk(cB, B);
-      load_rows_full<XH>(ts, batch0(nB), lane, B);
-      cB = nB;
-    }
-  } else {
-    while (c < nchunk) {
-      const uint32_t nn = claim_chunk(sm, lane);
-      run_chunk(c, A);
-      load_rows_full<XH>(ts, batch0(nn), lane, A);
-      c = nn;
-    }
-  }
-  if (lane == 0) sm.cnt[w] = a.cand;
-  __syncthreads();
-}
-
-template <bool XH>
-__global__ __launch_bounds__(kK2Threads) void topk_fused_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
-    uint32_t side_cap, SampleRanks ranks, FusedCtrl* __restrict__ ctrl, uint32_t* __restrict__ cum_tab,
-    uint32_t* __restrict__ cntw, uint32_t* __restrict__ side, float* __restrict__ cval, uint32_t* __restrict__ cidx,
-    float* __restrict__ out_val, int32_t* __restrict__ out_idx, int64_t idx_base) {
-  __shared__ FusedSmem sm;
-  STAMP(36000 + blockIdx.x, 0);
-  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  const uint32_t nchunk = tile / (uint32_t)kChunk;
-  const uint32_t ku = (uint32_t)k;
-  Src<kData, XH> src{x, xh, 0};
-  if (tid == 0) {
-    sm.nown = 0;
-    sm.bc[7] = __hip_atomic_load(&ctrl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  const uint32_t epoch = __builtin_amdgcn_readfirstlane(sm.bc[7]);
-  uint32_t* __restrict__ G = &ctrl->G[epoch & 1u][0][0];
-  bool have_bounds = false;
-  bool bounds_wg = false;
-  Buckets bk{};
-
-  // ---------------- tickets: bounds duty (ticket 0), then tiles (ticket t <-> tile t - 1).
-  // LDS-carried values are re-read with readfirstlane: the compiler must see them
-  // wave-uniform (the buffer descriptors built from them live in SGPRs)
-  auto claim = [&]() -> uint32_t {
-    if (tid == 0) sm.ticket = __hip_atomic_fetch_add(&ctrl->claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint32_t t = __builtin_amdgcn_readfirstlane(sm.ticket);
-    __syncthreads();
-    return t;
-  };
-  uint32_t ticket = claim();
-  STAMP(36000 + blockIdx.x, 1);
-#if CHOCO_STAMPS
-  if (tid == 0) g_stamps[38000 + blockIdx.x][0] = ticket + 1;
-#endif
-  if (ticket == 0) {
-    {
-      // the sample bounds (K1), published for every tile; then the idle parity
-      // of the bucket totals is cleared for the next call
-      bounds_wg = true;
-      float4 sv[kSampleLoads], shv[kSampleLoads];
-      float4 smv[kSampleLoads];
-      load_sample<XH, false>(x, xh, nullptr, n, sv, shv, smv);
-      uint32_t kk[kSampleLoads * 4];
-#pragma unroll
-      for (int j = 0; j < kSampleLoads; ++j) {
-        float4 v = sv[j];
-        if (XH) { v.x -= shv[j].x; v.y -= shv[j].y; v.z -= shv[j].z; v.w -= shv[j].w; }
-        kk[4 * j + 0] = fkey(v.x); kk[4 * j + 1] = fkey(v.y); kk[4 * j + 2] = fkey(v.z); kk[4 * j + 3] = fkey(v.w);
-      }
-      uint32_t s_lo;
-      uint64_t s_hi_est;
-      BoundsView bv{sm.u.sh, sm.scratch, sm.bc};
-      sample_bounds(kk, ranks, lane, w, bv, s_lo, s_hi_est);
-      bk = make_buckets(s_lo, s_hi_est, 0, kFMaybe);
-      bk.n = n;
-      have_bounds = true;
-      if (tid == 0) {
-        __hip_atomic_store(&ctrl->s_lo, bk.s_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctrl->s_hi, bk.s_hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ctrl->shift, bk.shift, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&ctrl->ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      STAMP(36000 + blockIdx.x, 2);
-      uint32_t* __restrict__ Gn = &ctrl->G[(epoch + 1u) & 1u][0][0];
-      for (int i = tid; i < kNRep * kFB; i += kK2Threads) Gn[i] = 0u;
-    }
-    ticket = claim();
-  }
-  for (; ticket <= nb; ticket = claim()) {
-    // ---- tile b = ticket - 1: its first loads go out before the bounds are read
-    const uint32_t b = ticket - 1;
-    const bool lds_mode = __builtin_amdgcn_readfirstlane(sm.nown) == 0;
-    uint32_t* ccnt = lds_mode ? sm.ccnt : sm.ccnt2;
-    uint32_t* cmeta = lds_mode ? sm.cmeta : sm.cmeta2;
-    const int64_t tb = (int64_t)b * tile;
-    const int64_t tlen = min((int64_t)tile, n - tb);
-    const TileRsrc ts{buf_rsrc(x + tb, (uint32_t)(tlen * 4)), buf_rsrc((XH ? xh : x) + tb, (uint32_t)(tlen * 4))};
-    auto batch0 = [&](uint32_t c) -> uint32_t {
-      return (c < nchunk && (int64_t)(c + 1) * kChunk <= tlen) ? c * (uint32_t)kChunk * 4u : kNoChunk;
-    };
-    // The first batches go out before the bounds are known -- except wave 0's:
-    // its lane 0 polls, and a poll queued behind the wave's own 16 KiB of loads
-    // would only return once they have landed (vmcnt is in order).
-    const bool early = have_bounds || w != 0;
-    float4 A[kK2Unroll], B[kK2Unroll];
-    if (early) {
-      load_rows_full<XH>(ts, batch0((uint32_t)w), lane, A);
-      if (!XH && CHOCO_FUSED_PRE == 2) load_rows_full<XH>(ts, batch0((uint32_t)w + kK2Waves), lane, B);
-    }
-    sm.hist[tid] = 0u;
-    if (tid == 0) {
-      sm.next_chunk = XH ? kK2Waves : 2 * kK2Waves;
-      sm.spill = 0;
-      if (!have_bounds) {
-        poll_ge(&ctrl->ready, 1u);
-        sm.bc[0] = __hip_atomic_load(&ctrl->s_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sm.bc[1] = __hip_atomic_load(&ctrl->s_hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sm.bc[2] = __hip_atomic_load(&ctrl->shift, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    __syncthreads();
-    STAMP(36000 + blockIdx.x, 2);
-    if (!early) load_rows_full<XH>(ts, batch0((uint32_t)w), lane, A);
-    if (!XH && (!early || CHOCO_FUSED_PRE != 2)) load_rows_full<XH>(ts, batch0((uint32_t)w + kK2Waves), lane, B);
-    if (!have_bounds) {
-      bk = make_buckets_from(__builtin_amdgcn_readfirstlane(sm.bc[0]), __builtin_amdgcn_readfirstlane(sm.bc[1]),
-                             __builtin_amdgcn_readfirstlane(sm.bc[2]), 0);
-      bk.n = n;
-      have_bounds = true;
-    }
-    fused_stream_tile<XH>(src, x, xh, n, tile, b, lds_mode, bk, sm, ccnt, cmeta, cval, cidx, A, B, ts);
-    STAMP(36000 + blockIdx.x, 3);
-
-    // ---- tile end: bucket suffix counts -> cum_tab row + totals; chunk prefix;
-    // the maybe keys counting-sorted into the side list (pairs stay in LDS)
-    uint32_t hsum, csum;
-    bool spilled;
-    {
-      const int t = tid;
-      const int jb = t < kFMaybe ? kFMaybe - 1 - t : kFMaybe;
-      const uint32_t hv = t < kFMaybe ? sm.hist[jb] : 0u;
-      const uint32_t cs = (uint32_t)t < nchunk ? ccnt[t] : 0u;
-      const bool sp = (uint32_t)t < nchunk && cs != (cmeta[t] >> 16);
-      if (ballot(sp) != 0ull && lane == 0) atomicOr(&sm.spill, 1u);
-      uint32_t above, cpre;
-      block_excl_scan2(hv, cs, sm.scratch, &above, &cpre, &hsum, &csum);
-      if ((uint32_t)t < nchunk) ccnt[t] = cpre;
-      if (t == 0) ccnt[nchunk] = csum;
-      const uint32_t sure = csum - hsum;
-      if (t == 0 && hsum > side_cap) atomicOr(&ctrl->overflow, 1u);
-      const uint32_t cum = t < kFMaybe ? sure + above + hv : sure;
-      st_sc1(&cum_tab[(int64_t)b * kFB + jb], cum);
-      atomicAdd(&G[(b & (kNRep - 1)) * kFB + jb], cum);
-      if (t < kFMaybe) sm.hist[jb] = above;  // counting-sort cursor of bucket jb
-      __syncthreads();
-      spilled = sm.spill != 0 || !lds_mode;
-    }
-    {
-      uint32_t* __restrict__ sd = side + (int64_t)b * side_cap;
-      uint32_t* __restrict__ skeys = reinterpret_cast<uint32_t*>(&sm.ent_v[0][0]);  // the ring is dead now
-      const bool sort_lds = hsum <= (uint32_t)kSideLds;
-      const uint32_t h = (uint32_t)lane & 31u;
-      const int64_t tbase = (int64_t)b * tile;
-      for (uint32_t c0 = 2u * w; c0 < nchunk; c0 += 2u * kK2Waves) {
-        const uint32_t cc = c0 + ((uint32_t)lane >> 5);
-        const bool have = cc < nchunk;
-        const uint32_t meta = have ? cmeta[cc] : 0u;
-        const uint32_t cnt = have ? ccnt[cc + 1] - ccnt[cc] : 0u;
-        const uint32_t ls = meta & 0xFFFFu, lc = have ? (meta >> 16) : 0u;
-        float* __restrict__ ov = cval + tbase + (int64_t)cc * kChunk;
-        uint32_t* __restrict__ oi = cidx + tbase + (int64_t)cc * kChunk;
-        auto to_side = [&](uint32_t vb, uint32_t ix) {
-          const uint32_t key = vb & 0x7fffffffu;
-          if (key < bk.s_hi) {
-            const uint32_t p = atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
-            if (sort_lds) skeys[p] = key;
-            else if (p < side_cap) st_sc1(&sd[p], key);
-          }
-        };
-        for (uint32_t j = h; j < lc; j += 32) {
-          const uint2 pr = sm.u.pairs[ls + j];
-          if (spilled) {  // this tile is emitted from global memory: its LDS pairs go to their slots
-            ov[j] = __uint_as_float(pr.x);
-            oi[j] = pr.y;
-          }
-          to_side(pr.x, pr.y);
-        }
-        if (spilled && have && h == 0) cntw[(int64_t)b * nchunk + cc] = cnt;
-        for (uint32_t j = lc + h; j < cnt; j += 32) to_side(__float_as_uint(ov[j]), oi[j]);
-      }
-      if (sort_lds) {
-        __syncthreads();
-        for (uint32_t i = (uint32_t)tid; i < hsum; i += kK2Threads) st_sc1(&sd[i], skeys[i]);
-      }
-    }
-    if (tid == 0 && sm.nown < (uint32_t)kFMaxOwn) sm.own[sm.nown++] = b | (spilled ? 0u : 0x80000000u);
-#if CHOCO_STAMPS
-    if (tid == 0) { g_stamps[38000 + blockIdx.x][1] = sm.nown; g_stamps[38000 + blockIdx.x][2] = spilled ? 1 : 0;
-                    g_stamps[38000 + blockIdx.x][3] = hsum; }
-#endif
-    publish_add(&ctrl->done);  // (ends with this tile's stores drained and released)
-    STAMP(37000 + blockIdx.x, 0);
-  }
-
-  // ---------------- every tile published -> exact T, offsets (K34's select)
-  if (tid == 0) {
-    poll_ge(&ctrl->done, nb);
-    sm.bc[0] = __hip_atomic_load(&ctrl->s_lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sm.bc[2] = __hip_atomic_load(&ctrl->shift, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sm.bc[3] = __hip_atomic_load(&ctrl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sm.bc[4] = 0;
-  }
-  __syncthreads();
-  STAMP(37000 + blockIdx.x, 1);
-  const uint32_t s_lo = __builtin_amdgcn_readfirstlane(sm.bc[0]), shift = __builtin_amdgcn_readfirstlane(sm.bc[2]),
-                 overflow = __builtin_amdgcn_readfirstlane(sm.bc[3]);
-  {
-    uint32_t g = 0;
-#pragma unroll
-    for (int r = 0; r < kNRep; ++r) g += __hip_atomic_load(&G[r * kFB + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sm.G[tid] = g;
-  }
-  const bool mine_tile = (uint32_t)tid < nb;
-  const uint32_t* row = cum_tab + (int64_t)(mine_tile ? tid : 0) * kFB;
-  const uint32_t sure_t = ld_sc1(&row[kFMaybe]);
-  __syncthreads();
-  bool fallback = overflow != 0 || sm.G[0] < ku || sm.G[kFMaybe] >= ku;
-  if (!fallback && tid < kFMaybe && sm.G[tid] >= ku && sm.G[tid + 1] < ku) sm.bc[4] = (uint32_t)tid;
-  __syncthreads();
-  const uint32_t jstar = __builtin_amdgcn_readfirstlane(sm.bc[4]);
-  if (!fallback && sm.G[jstar] - sm.G[jstar + 1] > (uint32_t)kFMCap) fallback = true;
-  if (fallback) {
-    // the sample's guess was off: exact single-workgroup selection by the bounds
-    // workgroup (correct, slow)
-    if (bounds_wg) {
-      __syncthreads();
-      block_topk_exact(src, n, k, 1.0f, out_val, out_idx, idx_base, sm.u.es);
-    }
-  } else {
-    uint32_t above = 0, cb = 0, off = 0;
-    if (mine_tile) {
-      const uint32_t a = ld_sc1(&row[jstar]), c = ld_sc1(&row[jstar + 1]);
-      above = c;
-      cb = a - c;
-      off = c - sure_t;
-    }
-    uint32_t M;
-    const uint32_t kpos = block_excl_scan(cb, sm.scratch, &M);
-    {
-      uint16_t* tmap = reinterpret_cast<uint16_t*>(sm.shist);
-      static_assert(sizeof(sm.shist) >= kFMCap * sizeof(uint16_t), "tile map fits the histogram");
-      sm.kbase[tid] = (uint32_t)(mine_tile ? tid : 0) * side_cap + off - kpos;  // mod 2^32
-      for (uint32_t j = 0; j < cb; ++j) tmap[kpos + j] = (uint16_t)tid;
-      __syncthreads();
-      constexpr int kG = kFMCap / kK4Threads;
-      uint32_t kv[kG];
-#pragma unroll
-      for (int q = 0; q < kG; ++q) {
-        const uint32_t i = min((uint32_t)tid + (uint32_t)q * kK4Threads, M - 1u);
-        kv[q] = (uint32_t)q * kK4Threads < M ? ld_sc1(&side[sm.kbase[tmap[i]] + i]) : 0u;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int q = 0; q < kG; ++q) {
-        const uint32_t i = (uint32_t)tid + (uint32_t)q * kK4Threads;
-        if (i < M) sm.keys[i] = kv[q];
-      }
-    }
-    const uint32_t base_j = s_lo + (jstar << shift);
-    uint32_t prefix = 0, krem = ku - sm.G[jstar + 1];
-    int sh = (int)shift;
-    while (sh > 0) {
-      const int dsh = sh > kFSelBits ? sh - kFSelBits : 0;
-      const uint32_t dmask = (1u << (sh - dsh)) - 1u;
-      for (int i = tid; i < (1 << kFSelBits); i += kK4Threads) sm.shist[i] = 0;
-      __syncthreads();
-      for (uint32_t j = tid; j < M; j += kK4Threads) {
-        const uint32_t rel = sm.keys[j] - base_j;
-        if (sh >= 32 || (rel >> sh) == (prefix >> sh)) atomicAdd(&sm.shist[(rel >> dsh) & dmask], 1u);
-      }
-      __syncthreads();
-      block_find_rank4k(sm.shist, krem, sm.scratch, sm.bc + 5);
-      prefix |= __builtin_amdgcn_readfirstlane(sm.bc[5]) << dsh;
-      krem = __builtin_amdgcn_readfirstlane(sm.bc[6]);
-      sh = dsh;
-    }
-    __syncthreads();
-    const uint32_t T = base_j + prefix;
-    const uint32_t r = krem;  // ties at T to take (>= 1)
-    uint32_t gt = above, eq = 0;
-    for (uint32_t i0 = 0; i0 < cb; i0 += 8) {
-      uint32_t kk8[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) kk8[q] = sm.keys[kpos + min(i0 + q, cb - 1)];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        gt += (i0 + q < cb && kk8[q] > T) ? 1u : 0u;
-        eq += (i0 + q < cb && kk8[q] == T) ? 1u : 0u;
-      }
-    }
-    uint32_t gpre, epre, gtot, etot;
-    block_excl_scan2(gt, eq, sm.scratch, &gpre, &epre, &gtot, &etot);
-    // per tile: output offset, ties before it, tie mode (in the dead histogram)
-    STAMP(37000 + blockIdx.x, 2);
-    uint32_t* tinfo = sm.shist;
-    if (mine_tile) {
-      const uint32_t taken = min(r, epre);
-      const uint32_t take = min(eq, r - taken);
-      tinfo[3 * tid + 0] = gpre + taken;
-      tinfo[3 * tid + 1] = epre;
-      tinfo[3 * tid + 2] = take == 0 ? kTakeNone : (take == eq ? kTakeAll : kTakePartial);
-    }
-    __syncthreads();
-
-    // ---------------- emit this workgroup's tiles
-    const uint32_t nown = __builtin_amdgcn_readfirstlane(sm.nown);
-    for (uint32_t oi_ = 0; oi_ < (CHOCO_FUSED_DIAG == 1 ? 0u : nown); ++oi_) {
-      const uint32_t ent = __builtin_amdgcn_readfirstlane(sm.own[oi_]);
-      const uint32_t b = ent & 0x7fffffffu;
-      const bool in_lds = (ent >> 31) != 0u;
-      const int64_t tb = (int64_t)b * tile;
-      uint32_t out = __builtin_amdgcn_readfirstlane(tinfo[3 * b + 0]);
-      uint32_t tie_run = __builtin_amdgcn_readfirstlane(tinfo[3 * b + 1]);
-      const uint32_t mode = __builtin_amdgcn_readfirstlane(tinfo[3 * b + 2]);
-      uint32_t tot;
-      if (in_lds) {
-        tot = __builtin_amdgcn_readfirstlane(sm.ccnt[nchunk]);
-      } else {
-        uint32_t cw1[kCPT];
-#pragma unroll
-        for (int q = 0; q < kCPT; ++q) {
-          const uint32_t j = kCPT * tid + q;
-          cw1[q] = j < nchunk ? cntw[(int64_t)b * nchunk + j] : 0u;
-        }
-        tot = chunk_run_starts(cw1, nchunk, sm.ccnt2, sm.scratch);
-      }
-      int eb = 0;
-      for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads * kEmitR) {
-        float v[kEmitR];
-        uint32_t idx[kEmitR];
-#pragma unroll
-        for (int i = 0; i < kEmitR; ++i) {
-          const uint32_t p = p0 + i * kK4Threads + tid;
-          if (in_lds) {
-            // chunk of position p (LDS prefix search), then its LDS pair
-            uint32_t lo = 0, hi = nchunk - 1, pp = p < tot ? p : 0u;
-            while (lo < hi) {
-              const uint32_t mid = (lo + hi + 1) >> 1;
-              if (sm.ccnt[mid] <= pp) lo = mid; else hi = mid - 1;
-            }
-            const uint2 pr = sm.u.pairs[(sm.cmeta[lo] & 0xFFFFu) + (pp - sm.ccnt[lo])];
-            v[i] = __uint_as_float(pr.x);
-            idx[i] = pr.y;
-          } else {
-            const int64_t ad = cand_addr(sm.ccnt2, nchunk, tot, p, tb);
-            v[i] = cval[ad];
-            idx[i] = cidx[ad];
-          }
-        }
-        bool gtv[kEmitR], eqv[kEmitR];
-#pragma unroll
-        for (int i = 0; i < kEmitR; ++i) {
-          const bool valid = p0 + i * kK4Threads + tid < tot;
-          const uint32_t key = fkey(v[i]);
-          gtv[i] = valid && key > T;
-          eqv[i] = valid && key == T;
-        }
-        bool sel[kEmitR];
-        uint32_t rk[kEmitR];
-        if (mode == kTakePartial) {
-          const uint32_t eq_total = batch_ranks(eqv, rk, sm.ecnt[eb]);
-          eb ^= 1;
-#pragma unroll
-          for (int i = 0; i < kEmitR; ++i) sel[i] = gtv[i] || (eqv[i] && tie_run + rk[i] < r);
-          tie_run += eq_total;
-        } else {
-#pragma unroll
-          for (int i = 0; i < kEmitR; ++i) sel[i] = gtv[i] || (eqv[i] && mode == kTakeAll);
-        }
-        const uint32_t nsel = batch_ranks(sel, rk, sm.ecnt[eb]);
-        eb ^= 1;
-#pragma unroll
-        for (int i = 0; i < kEmitR; ++i) {
-          if (sel[i]) {
-            out_val[out + rk[i]] = v[i];
-            out_idx[out + rk[i]] = (int32_t)((int64_t)idx[i] + idx_base);
-          }
-        }
-        out += nsel;
-      }
-      __syncthreads();  // ccnt2 / ecnt reuse by the next tile
-    }
-  }
-  // ---------------- the last workgroup out resets the counters for the next call
-  __syncthreads();
-  STAMP(37000 + blockIdx.x, 3);
-  if (tid == 0) {
-    const uint32_t e = __hip_atomic_fetch_add(&ctrl->exitc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (e == gridDim.x - 1) {
-      __hip_atomic_store(&ctrl->claim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ctrl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ctrl->ready, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ctrl->overflow, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ctrl->epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ctrl->exitc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 // ----------------------------------------------------------------------------
 // host dispatch
 // ----------------------------------------------------------------------------
-// The fused one-launch kernel (topk_fused_kernel) is parity-green but measured
-// SLOWER than K1 + K2 + K34 at 100M, k = 1 % (119 vs 92 us, tools/fused_stamps.py;
-// DESIGN.md): the bounds workgroup's sample competes with the tiles' prefetch
-// flood (bounds at 10-18 us vs K1's 5.5), write-through tile publishing waits
-// on memory acks (~8 us), the in-kernel "all tiles done" poll costs ~3 us, and
-// the redundant select + LDS emission cost as much as K34.  Diagnostic variant.
-#ifndef CHOCO_TOPK_FUSED
-#define CHOCO_TOPK_FUSED 0
-#endif
 size_t topk_ws_bytes(int64_t n) {
   if (n <= kSmallN) return 256;
-  return CHOCO_TOPK_FUSED && fused_fits(n) ? fused_layout(n).total : topk_layout(n).total;
+  return topk_layout(n).total;
+}
+
+// ---- warm-start bookkeeping (host): per workspace pointer, the (n, k, mode) and
+// call count of the last pipeline call made on it.  The call count gives each
+// call its parity (TopkCtrl); a data-mode call with the same (n, k) as the
+// previous call on the workspace is warm (no K1).  K2 re-checks the window's
+// (n, k) on the device, so a stale entry costs one exact fallback, never a
+// wrong answer.
+struct WarmEntry {
+  int64_t n, k;
+  uint64_t calls;
+  bool data;
+};
+static std::mutex g_warm_mu;
+static std::unordered_map<const void*, WarmEntry> g_warm;
+static std::atomic<bool> g_warm_on{true};
+
+struct WarmClaim {
+  uint32_t par;
+  bool known;  // an earlier pipeline call on this workspace left G[par] / overflow[par] zeroed
+  bool warm;   // ... and its window is for this (n, k): skip K1
+};
+static WarmClaim warm_claim(const void* ws, int64_t n, int64_t k, bool data) {
+  std::lock_guard<std::mutex> g(g_warm_mu);
+  auto it = g_warm.find(ws);
+  if (it == g_warm.end()) {
+    g_warm.emplace(ws, WarmEntry{n, k, 1u, data});
+    return WarmClaim{0u, false, false};
+  }
+  WarmEntry& e = it->second;
+  WarmClaim c{(uint32_t)(e.calls & 1u), true,
+              data && e.data && e.n == n && e.k == k && g_warm_on.load(std::memory_order_relaxed)};
+  e.n = n;
+  e.k = k;
+  e.data = data;
+  e.calls += 1;
+  return c;
 }
 
 // GS: the gossip step fused into K1's sample and K2's stream (x written by K2);
 // K34 and its exact fallback then read (x_new, xh).
+// status: where the exact fallback flags a bounded wait that gave up (the
+// workspace's own status word, or the segmented workspace's).
 template <int MODE, bool XH, bool GS = false>
 static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                        float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes,
-                       hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}) {
+                       hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}, uint32_t* status = nullptr) {
   if (k >= n) {
     const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
     profile_begin("topk_all", st);
@@ -2471,22 +2059,6 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
     CHOCO_LAUNCHED("topk_exact_kernel");
     return CHOCO_OK;
   }
-  if (MODE == kData && !GS && CHOCO_TOPK_FUSED && fused_fits(n)) {
-    const FusedLayout F = fused_layout(n);
-    CHOCO_REQUIRE(ws != nullptr && ws_bytes >= F.total, "top-k workspace too small: need %zu bytes, got %zu",
-                  F.total, ws_bytes);
-    CHOCO_REQUIRE(scale == 1.0f, "fused top-k takes scale 1");
-    char* fb = static_cast<char*>(ws);
-    profile_begin("topk_fused", st);
-    CHOCO_KLAUNCH((topk_fused_kernel<XH>), dim3(F.nb + 1), dim3(kK2Threads), 0, st, x, xh, n, k, F.tile, F.nb,
-                  F.side_cap, sample_ranks(n, k), reinterpret_cast<FusedCtrl*>(fb + F.off_ctrl),
-                  reinterpret_cast<uint32_t*>(fb + F.off_cum), reinterpret_cast<uint32_t*>(fb + F.off_cntw),
-                  reinterpret_cast<uint32_t*>(fb + F.off_side), reinterpret_cast<float*>(fb + F.off_cval),
-                  reinterpret_cast<uint32_t*>(fb + F.off_cidx), out_val, out_idx, idx_base);
-    profile_end("topk_fused", st);
-    CHOCO_LAUNCHED("topk_fused_kernel");
-    return CHOCO_OK;
-  }
   const TopkLayout L = topk_layout(n);
   CHOCO_REQUIRE(ws != nullptr && ws_bytes >= L.total, "top-k workspace too small: need %zu bytes, got %zu",
                 L.total, ws_bytes);
@@ -2497,6 +2069,7 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   uint32_t* side = reinterpret_cast<uint32_t*>(base + L.off_side);
   float* cval = reinterpret_cast<float*>(base + L.off_cval);
   uint32_t* cidx = reinterpret_cast<uint32_t*>(base + L.off_cidx);
+  if (status == nullptr) status = &ctrl->status;
   uint32_t hs_lo = 0;
   uint64_t hs_hi = 0;
   if (MODE == kHash) {
@@ -2509,26 +2082,32 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
     hs_hi = c_hi < 1.0 ? 0x80000000ull : (uint64_t)ceil(two31 * (1.0 - c_hi / nd));
     if (hs_hi <= hs_lo) hs_hi = (uint64_t)hs_lo + 1;
   }
-  if (MODE == kHash) {
-    // this call's bucket totals and overflow flag start from zero (K1 does it in data mode)
-    CHOCO_REQUIRE(hipMemsetAsync(ctrl, 0, sizeof(TopkCtrl), st) == hipSuccess, "hipMemsetAsync failed");
+  const WarmClaim wc = warm_claim(ws, n, k, MODE == kData);
+  const uint32_t par = wc.par;
+  if (MODE == kHash && !wc.known) {
+    // this call's bucket totals and overflow word start from zero (K1 does it in data mode)
+    CHOCO_REQUIRE(hipMemsetAsync(&ctrl->G[par][0][0], 0, sizeof(ctrl->G[par]), st) == hipSuccess &&
+                      hipMemsetAsync(&ctrl->overflow[par], 0, sizeof(uint32_t), st) == hipSuccess,
+                  "hipMemsetAsync failed");
   }
-  if (MODE == kData) {
+  if (MODE == kData && !wc.warm) {
     profile_begin("topk_bounds", st);
-    CHOCO_KLAUNCH((topk_bounds_kernel<XH, GS>), dim3(1), dim3(kK1Threads), 0, st, x, xh, n, sample_ranks(n, k), ctrl,
-                  gs);
+    CHOCO_KLAUNCH((topk_bounds_kernel<XH, GS>), dim3(1), dim3(kK1Threads), 0, st, x, xh, n, k, par,
+                  sample_ranks(n, k), ctrl, gs);
     profile_end("topk_bounds", st);
     CHOCO_LAUNCHED("topk_bounds_kernel");
   }
   profile_begin("topk_stream", st);
-  CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH, GS>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, L.tile,
-                L.side_cap, seed, hs_lo, hs_hi, ctrl, cum, cntw, side, cval, cidx, gs);
+  CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH, GS>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, k, L.tile, L.nb,
+                par, L.side_cap, seed, hs_lo, hs_hi, ctrl, cum, cntw, side, cval, cidx,
+                reinterpret_cast<uint32_t*>(base + L.off_tinfo), gs);
   profile_end("topk_stream", st);
   CHOCO_LAUNCHED("topk_stream_kernel");
   profile_begin("topk_finish", st);
   CHOCO_KLAUNCH((topk_finish_kernel<MODE, XH>), dim3(L.nb), dim3(kK4Threads), 0, st, x, xh, n, k, L.tile, L.nb,
                 L.side_cap, seed, scale, ctrl, cum, cntw, side, cval, cidx, out_val, out_idx, idx_base,
-                reinterpret_cast<WideCtrl*>(base + L.off_wide), reinterpret_cast<uint32_t*>(base + L.off_gcnt));
+                reinterpret_cast<WideCtrl*>(base + L.off_wide), reinterpret_cast<uint32_t*>(base + L.off_gcnt), par,
+                status, reinterpret_cast<const uint32_t*>(base + L.off_tinfo));
   profile_end("topk_finish", st);
   CHOCO_LAUNCHED("topk_finish_kernel");
   return CHOCO_OK;
@@ -2537,7 +2116,7 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
 template <int MODE>
 static int dispatch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                          float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes,
-                         hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}) {
+                         hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}, uint32_t* status = nullptr) {
   CHOCO_REQUIRE(x != nullptr && out_val != nullptr && out_idx != nullptr, "null pointer argument");
   CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n must be in [1, 2^31-1), got %lld", (long long)n);
   CHOCO_REQUIRE(k >= 1 && k <= n, "k must be in [1, n], got k=%lld n=%lld", (long long)k, (long long)n);
@@ -2546,22 +2125,35 @@ static int dispatch_topk(const float* x, const float* xh, int64_t n, int64_t k, 
     CHOCO_REQUIRE(xh != nullptr && aligned4(gs.mem), "the gossip step needs x_hat and a 4-byte aligned memory");
     if (MODE == kData && k < n && n > kSmallN)
       return launch_topk<kData, true, true>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st,
-                                            gs);
+                                            gs, status);
     // no full stream pass to fuse into (random-k gathers k elements; small n and
     // k == n are one-workgroup / copy paths): the standalone step, then the codec
     const int rc = gossip_launch(const_cast<float*>(x), gs.mem, xh, gs.gamma, n, st);
     if (rc) return rc;
   }
-  if (xh) return launch_topk<MODE, true>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st);
-  return launch_topk<MODE, false>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st);
+  if (xh)
+    return launch_topk<MODE, true>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st,
+                                   Gossip{nullptr, 0.f}, status);
+  return launch_topk<MODE, false>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st,
+                                  Gossip{nullptr, 0.f}, status);
 }
 
 int topk_pipeline(int mode, const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                   float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes, hipStream_t st,
-                  Gossip gs) {
+                  Gossip gs, uint32_t* status) {
   if (mode == kHash)
-    return dispatch_topk<kHash>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st, gs);
-  return dispatch_topk<kData>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st, gs);
+    return dispatch_topk<kHash>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st, gs, status);
+  return dispatch_topk<kData>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st, gs, status);
+}
+
+void topk_warm_forget(const void* ws, size_t bytes) {
+  std::lock_guard<std::mutex> g(g_warm_mu);
+  const char* lo = static_cast<const char*>(ws);
+  for (auto it = g_warm.begin(); it != g_warm.end();) {
+    const char* p = static_cast<const char*>(it->first);
+    if (p == lo || (p > lo && p < lo + bytes)) it = g_warm.erase(it);
+    else ++it;
+  }
 }
 
 }  // namespace choco
@@ -2576,6 +2168,16 @@ CHOCO_API int64_t choco_topk_k(int64_t n, double ratio) {
 }
 
 CHOCO_API size_t choco_topk_workspace_size(int64_t n) { return topk_ws_bytes(n); }
+
+CHOCO_API int choco_topk_workspace_reset(const void* ws, size_t ws_bytes) {
+  topk_warm_forget(ws, ws_bytes);
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_topk_set_warm_start(int32_t enable) {
+  g_warm_on.store(enable != 0);
+  return CHOCO_OK;
+}
 CHOCO_API size_t choco_randk_workspace_size(int64_t n) { return topk_ws_bytes(n); }
 
 CHOCO_API int choco_topk_compress(const float* x, const float* xhat, int64_t n, int64_t k, float* out_val,
@@ -2610,17 +2212,26 @@ CHOCO_API int choco_dbg_stream_only(const float* x, int64_t n, int64_t k, void* 
   CHOCO_REQUIRE(ws && ws_bytes >= L.total && reps > 0, "bad arguments");
   char* base = static_cast<char*>(ws);
   TopkCtrl* ctrl = reinterpret_cast<TopkCtrl*>(base + L.off_ctrl);
+  // the window the next call would use; the totals it accumulates are garbage afterwards,
+  // so the workspace is forgotten (its next call is cold: K1 re-zeroes them)
+  uint32_t par = 0;
+  {
+    std::lock_guard<std::mutex> g(g_warm_mu);
+    auto it = g_warm.find(ws);
+    CHOCO_REQUIRE(it != g_warm.end(), "run choco_topk_compress on this workspace first");
+    par = (uint32_t)(it->second.calls & 1u);
+  }
   hipEvent_t a, b;
   CHOCO_HIP(hipEventCreate(&a));
   CHOCO_HIP(hipEventCreate(&b));
   CHOCO_HIP(hipEventRecord(a, st));
   for (int r = 0; r < reps; ++r)
-    hipLaunchKernelGGL((topk_stream_kernel<kData, false>), dim3(L.nb), dim3(kK2Threads), 0, st, x, nullptr, n,
-                       L.tile, L.side_cap, (uint64_t)0, 0u, (uint64_t)0, ctrl,
+    hipLaunchKernelGGL((topk_stream_kernel<kData, false>), dim3(L.nb), dim3(kK2Threads), 0, st, x, nullptr, n, k,
+                       L.tile, L.nb, par, L.side_cap, (uint64_t)0, 0u, (uint64_t)0, ctrl,
                        reinterpret_cast<uint32_t*>(base + L.off_cum),
                        reinterpret_cast<uint32_t*>(base + L.off_cntw), reinterpret_cast<uint32_t*>(base + L.off_side),
                        reinterpret_cast<float*>(base + L.off_cval), reinterpret_cast<uint32_t*>(base + L.off_cidx),
-                       Gossip{nullptr, 0.f});
+                       reinterpret_cast<uint32_t*>(base + L.off_tinfo), Gossip{nullptr, 0.f});
   CHOCO_HIP(hipEventRecord(b, st));
   CHOCO_HIP(hipEventSynchronize(b));
   float ms = 0.f;
@@ -2628,6 +2239,7 @@ CHOCO_API int choco_dbg_stream_only(const float* x, int64_t n, int64_t k, void* 
   *avg_ms = ms / reps;
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
+  topk_warm_forget(ws, 1);
   return CHOCO_OK;
 }
 

@@ -76,7 +76,7 @@ struct SegLayout {
 
 static SegLayout seg_layout(int nseg, int64_t ntile) {
   SegLayout L{};
-  size_t o = 0;
+  size_t o = 256;  // [0, 256): the sticky status word (CHOCO_TOPK_STATUS_OFFSET) of the whole call
   L.off_h1 = o;   o += align_up((size_t)nseg * kH * 4, 256);
   L.off_h2 = o;   o += align_up((size_t)nseg * kH * 4, 256);
   L.off_h3 = o;   o += align_up((size_t)nseg * 512 * 4, 256);
@@ -182,15 +182,8 @@ CHOCO_DEV void block_find_rank2k(uint32_t h0, uint32_t h1, uint32_t rank, uint32
 #ifndef CHOCO_S1_COPIES
 #define CHOCO_S1_COPIES 1
 #endif
-#ifndef CHOCO_S2_DIAG  // 1: fixed coarse bin (no hist1 read, no scan): S2 chain-latency probe; results invalid
-#define CHOCO_S2_DIAG 0
-#endif
 #ifndef CHOCO_S1_LANEC
 #define CHOCO_S1_LANEC 1
-#endif
-#ifndef CHOCO_S1_DIAG  // 1: no histogram (load-path timing only); 2: no S1 read at all, one
-                       // synthetic bin (S2 from HBM); results invalid, S4 stores nothing
-#define CHOCO_S1_DIAG 0
 #endif
 template <int MODE, bool XH, bool GS = false>
 __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __restrict__ x,
@@ -205,27 +198,20 @@ __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __re
   __shared__ uint32_t h[NC][kH];
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
   float v[kSegRows][4] = {};
-  if (CHOCO_S1_DIAG == 2) {  // diagnostic: every element counted in the bin of |v| = 2.5
-    if (threadIdx.x == 0) atomicAdd(&hist1[(int64_t)c.s * kH + 0x402], (uint32_t)c.tl);
-    return;
-  }
   if (GS) tile_load_gossip(x, xh, gs, c, v);
   else if (MODE == kData) tile_load<XH>(x, xh, c, v);
   for (int i = threadIdx.x; i < NC * kH; i += kSegThreads) (&h[0][0])[i] = 0u;
   __syncthreads();
   const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
   uint32_t* __restrict__ hw = h[CHOCO_S1_LANEC > 1 ? lane_id() % NC : (threadIdx.x >> 6) % NC];
-  uint32_t dsum = 0;
 #pragma unroll
   for (int r = 0; r < kSegRows; ++r)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = tile_elem(r, q);
       const uint32_t key = tile_key<MODE>(c, sseed, e, v[r][q]);
-      if (CHOCO_S1_DIAG) dsum += key;
-      else if (e < c.tl) atomicAdd(&hw[key >> 20], 1u);
+      if (e < c.tl) atomicAdd(&hw[key >> 20], 1u);
     }
-  if (CHOCO_S1_DIAG && dsum == 0x12345u) hw[0] = dsum;  // keep the loads (diagnostic build only)
   __syncthreads();
   uint32_t* __restrict__ g = hist1 + (int64_t)c.s * kH;
   for (int i = threadIdx.x; i < kH; i += kSegThreads) {
@@ -252,14 +238,9 @@ __global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
   float v[kSegRows][4] = {};
   if (MODE == kData) tile_load<XH>(x, xh, c, v);  // in flight while b1 is found
   const uint32_t* __restrict__ g1 = hist1 + (int64_t)c.s * kH;
-  const uint32_t c0 = CHOCO_S2_DIAG ? 0u : g1[2 * tid], c1 = CHOCO_S2_DIAG ? 0u : g1[2 * tid + 1];
+  const uint32_t c0 = g1[2 * tid], c1 = g1[2 * tid + 1];
   for (int i = tid; i < kH; i += kSegThreads) h2[i] = 0u;
-  if (CHOCO_S2_DIAG) {
-    if (tid == 0) { bc[0] = 0x402u; bc[1] = (uint32_t)c.R.k; }
-    __syncthreads();
-  } else {
-    block_find_rank2k(c0, c1, (uint32_t)c.R.k, scratch, bc);
-  }
+  block_find_rank2k(c0, c1, (uint32_t)c.R.k, scratch, bc);
   const uint32_t b1 = bc[0], kb = bc[1];
   if (c.j == 0 && tid == 0) {
     info[8 * c.s + 0] = b1;
@@ -480,7 +461,6 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
   const int tid = threadIdx.x;
   const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
-  if (CHOCO_S1_DIAG == 2 || CHOCO_S2_DIAG) return;
   const uint32_t T = info[8 * c.s + 2], r = info[8 * c.s + 5];
   const uint32_t cnt = tilecnt[blockIdx.x];
   const uint32_t ev = tcount[2 * blockIdx.x + 1];
@@ -573,11 +553,13 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
   return CHOCO_OK;
 }
 
+// Segments over kSegBatchMax elements: one flat-pipeline workspace EACH (after the
+// batched one), so each keeps its own warm-start window between calls.
 static size_t pipeline_ws(const int64_t* plan_host, int nseg) {
   size_t need = 0;
   for (int s = 0; s < nseg; ++s) {
     const int64_t* p = plan_host + (int64_t)kRow * s;
-    if (p[5] == 0) need = std::max(need, topk_ws_bytes(p[1]));
+    if (p[5] == 0) need += align_up(topk_ws_bytes(p[1]), 256);
   }
   return need;
 }
@@ -623,17 +605,22 @@ static int segmented(const float* x, const float* xhat, const int64_t* plan_dev,
       rc = launch_batched<MODE, false>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, W, st);
     if (rc) return rc;
   }
-  // segments over kSegBatchMax elements: the flat pipeline, one after another
-  // (its workspace follows the batched one: the batched histograms must stay zero)
+  // segments over kSegBatchMax elements: the flat pipeline, one after another, each
+  // in its own workspace after the batched one (the batched histograms must stay
+  // zero); their fallbacks flag this call's status word
+  size_t fo = L.total;
   for (int s = 0; s < nseg; ++s) {
     const int64_t* p = plan_host + (int64_t)kRow * s;
     if (p[5] != 0) continue;
     const uint64_t sd = MODE == kHash ? seg_seed(seed, s) : 0;
     const float scale = (MODE == kHash && !is_biased) ? (float)((double)p[1] / (double)p[2]) : 1.0f;
     const Gossip gseg{gs.mem ? gs.mem + p[0] : nullptr, gs.gamma};
+    const size_t fb = align_up(topk_ws_bytes(p[1]), 256);
     const int rc = topk_pipeline(MODE, x + p[0], xhat ? xhat + p[0] : nullptr, p[1], p[2], sd, scale,
-                                 out_val + p[3], out_idx + p[3], p[0], base + L.total, ws_bytes - L.total, st, gseg);
+                                 out_val + p[3], out_idx + p[3], p[0], base + fo, fb, st, gseg,
+                                 reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_STATUS_OFFSET));
     if (rc) return rc;
+    fo += fb;
   }
   return CHOCO_OK;
 }

@@ -59,6 +59,28 @@ int64_t choco_topk_k(int64_t n, double ratio);
  * lowest index (the reference's k==1 path, torch.max, does the same; its
  * torch.topk order is implementation-defined). */
 size_t choco_topk_workspace_size(int64_t n);
+/* Warm start.  A top-k workspace keeps the previous call's exact threshold and
+ * bucket counts, and the library keeps (host side, per workspace pointer) the
+ * (n, k) and the call count of the last call made on it.  A call with the same
+ * (n, k) as the previous call on the same workspace skips the sampling kernel
+ * and selects inside a candidate window around the previous threshold (its
+ * margin follows the drift observed between calls); a call whose window misses
+ * takes the exact fallback, and leaves a fresh window for the next call.  The
+ * output is identical on every path.  Calls on one workspace must be issued in
+ * stream order (one stream per workspace, as above).
+ * choco_topk_workspace_reset forgets every workspace inside [ws, ws + ws_bytes)
+ * (call it whenever a top-k / random-k / segmented workspace is allocated or
+ * zero-filled again: its next call is cold); choco_topk_set_warm_start(0) turns
+ * the warm path off library-wide (every call samples). */
+int choco_topk_workspace_reset(const void* ws, size_t ws_bytes);
+int choco_topk_set_warm_start(int32_t enable);
+/* Byte offset, in every top-k / random-k / segmented workspace, of a sticky uint32
+ * status word.  Bit 0: a bounded wait inside the exact fallback gave up, so the
+ * output of that call is invalid (never expected; the wait is bounded so that a
+ * stuck producer cannot hang the GPU).  The caller reads it without blocking
+ * (e.g. an async copy checked later), raises, and writes 0 back. */
+#define CHOCO_TOPK_STATUS_OFFSET 0
+#define CHOCO_TOPK_STATUS_POLL_TIMEOUT 1
 int choco_topk_compress(const float* x, const float* xhat, int64_t n, int64_t k,
                         float* out_val, int32_t* out_idx,
                         void* ws, size_t ws_bytes, void* stream);

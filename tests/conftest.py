@@ -32,10 +32,11 @@ def load_golden():
 
 
 def same_bits(a, b):
-    """Bit-exact float comparison that treats NaN == NaN and +0 == -0."""
-    a = np.asarray(a, dtype=np.float32)
-    b = np.asarray(b, dtype=np.float32)
+    """Bit-exact float comparison: identical fp32 bit patterns (so +0 != -0), except
+    that a NaN matches any NaN (payloads are not part of the contract)."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
     if a.shape != b.shape:
         return False
     both_nan = np.isnan(a) & np.isnan(b)
-    return bool(np.all(both_nan | (a == b)))
+    return bool(np.all(both_nan | (a.view(np.uint32) == b.view(np.uint32))))

@@ -314,3 +314,86 @@ def test_release_workspaces_then_recompute():
     assert torch.equal(i1, i2) and torch.equal(v1.view(torch.int32), v2.view(torch.int32))
     ov, oi = O.topk(host(d), k)
     assert np.array_equal(host(i2).astype(np.int64), oi)
+
+
+def _check_topk(x, k, xh=None):
+    from chocosgd_amd import codec
+    vals, idx = codec.topk(x, k, xhat=xh)
+    d = host(x) if xh is None else (host(x) - host(xh)).astype(np.float32)
+    ov, oi = O.topk(d, k)
+    assert np.array_equal(host(idx).astype(np.int64), oi)
+    assert same_bits(host(vals), ov)
+
+
+@pytest.mark.parametrize("n", [3_000_000, 25_000_000])
+def test_topk_warm_start_badly_wrong_windows(n):
+    """Warm start (include/choco_codec.h): consecutive calls with the same (n, k) on one
+    workspace select inside the window the previous call left.  Every call stays exact,
+    including those whose window is badly wrong: the buffer scaled x100, then all zeros,
+    then random again, x1e-3, a tie-heavy buffer, a constant buffer, and random."""
+    from chocosgd_amd import codec
+    k = codec.topk_k(n, 0.99)
+    g = torch.Generator(device=DEV).manual_seed(400)
+    seq = [randn(n, 401), randn(n, 402), randn(n, 403) * 100, torch.zeros(n, device=DEV), randn(n, 404),
+           randn(n, 405) * 1e-3, torch.round(torch.randn(n, generator=g, device=DEV) * 4) / 4,
+           torch.full((n,), -2.5, device=DEV), randn(n, 406), randn(n, 407)]
+    for x in seq:
+        _check_topk(x, k)
+
+
+def test_topk_warm_start_drift_and_cold_equal():
+    """A slowly drifting delta (the CHOCO case: scale shrinks 3 % per call) stays exact on
+    the warm path, and the warm and cold (workspace reset / warm start off) answers agree."""
+    from chocosgd_amd import codec, _lib
+    n = 4_000_037
+    k = codec.topk_k(n, 0.99)
+    base = randn(n, 410)
+    for step in range(12):
+        x = base * (0.97 ** step) + randn(n, 411 + step, 0.05)
+        _check_topk(x, k)
+    lib = _lib.load()
+    x = randn(n, 430)
+    v_w, i_w = codec.topk(x, k)
+    lib.choco_topk_set_warm_start(0)
+    try:
+        v_c, i_c = codec.topk(x, k)
+    finally:
+        lib.choco_topk_set_warm_start(1)
+    assert torch.equal(i_w, i_c) and torch.equal(v_w.view(torch.int32), v_c.view(torch.int32))
+
+
+def test_topk_warm_start_alternating_shapes():
+    """Calls of different (n, k) on the shared workspace alternate: each is cold (the window
+    is keyed by (n, k)), then warm again; all exact."""
+    from chocosgd_amd import codec
+    for i in range(6):
+        n = (2_000_003, 3_000_017)[i % 2]
+        ratio = (0.99, 0.9)[(i // 2) % 2]
+        _check_topk(randn(n, 440 + i), codec.topk_k(n, ratio))
+
+
+def test_topk_warm_start_gossip_sequence():
+    """The fused consensus step on the warm path: x, memory, x_hat evolve over calls."""
+    from chocosgd_amd import codec
+    n = 3_000_011
+    k = codec.topk_k(n, 0.99)
+    g = torch.Generator(device=DEV).manual_seed(450)
+    x = torch.randn(n, generator=g, device=DEV)
+    hat = x + 0.1 * torch.randn(n, generator=g, device=DEV)
+    mem = hat + 0.05 * torch.randn(n, generator=g, device=DEV)
+    for step in range(5):
+        xa = O.gossip_step(host(x), host(mem), host(hat), 0.9)
+        d = (xa - host(hat)).astype(np.float32)
+        vals, idx = codec.topk(x, k, xhat=hat, gossip=(mem, 0.9))
+        assert same_bits(host(x), xa)
+        ov, oi = O.topk(d, k)
+        assert np.array_equal(host(idx).astype(np.int64), oi)
+        assert same_bits(host(vals), ov)
+        codec.sparse_accumulate(vals, idx, mem, 1.0, xhat_self=hat)
+
+
+def test_topk_status_word_clean_after_calls():
+    """No call of this module left the workspace status word set (bounded waits never gave up)."""
+    from chocosgd_amd import codec
+    _check_topk(randn(2_000_003, 460), codec.topk_k(2_000_003, 0.99))
+    codec.check_topk_status(wait=True)

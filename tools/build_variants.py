@@ -15,8 +15,6 @@ VARIANTS = {
     "qq_nt": ["CHOCO_QQUANT_NT=1"],
     "qn_plain": ["CHOCO_QNORM_NT=0"],
     "sign_acc1": ["CHOCO_SIGN_ACC1=1"],
-    "fused": ["CHOCO_TOPK_FUSED=1"],
-    "fused_stamps": ["CHOCO_TOPK_FUSED=1", "CHOCO_STAMPS=1"],
     "g_form0": ["CHOCO_GOSSIP_FORM=0"],
     "gs_st_plain": ["CHOCO_GS_STORE_NT=0"],
     "wide_debug": ["CHOCO_WIDE_DEBUG=1"],
@@ -24,13 +22,10 @@ VARIANTS = {
     "qn_plain_qdec_nt": ["CHOCO_QNORM_NT=0", "CHOCO_QDEC_ST_NT=1"],
     "s1_c2": ["CHOCO_S1_COPIES=2"],
     "s1_c4": ["CHOCO_S1_COPIES=4"],
-    "s1_diag": ["CHOCO_S1_DIAG=1"],
-    "s1_diag2": ["CHOCO_S1_DIAG=2"],
     "s4_1024": ["CHOCO_S4_THREADS=1024"],
     "s1_lc2": ["CHOCO_S1_LANEC=2"],
     "s1_lc4": ["CHOCO_S1_LANEC=4"],
     "s1_lc8": ["CHOCO_S1_LANEC=8"],
-    "s2_diag": ["CHOCO_S2_DIAG=1"],
     "k2st_nt": ["CHOCO_K2_STORE=1"],
     "k2st_wt": ["CHOCO_K2_STORE=2"],
     "k34st_nt": ["CHOCO_K34_STORE=1"],

@@ -24,21 +24,25 @@ def main():
     ap.add_argument("--ratio", type=float, default=0.99)
     ap.add_argument("--lib", default=os.path.join(ROOT, "chocosgd_amd/lib/variants/lib_stamps.so"))
     ap.add_argument("--save", default=None, help="write the raw stamp table (.npy)")
+    ap.add_argument("--nbuf", type=int, default=4, help="buffers compressed in rotation (the bench's warm path)")
+    ap.add_argument("--cold", action="store_true", help="stamp a cold call (warm start off: K1 runs)")
     a = ap.parse_args()
     lib = _lib.load(a.lib)
     fn = lib.choco_dbg_stamps
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     dev = torch.device("cuda", 0)
-    d = torch.randn(a.n, generator=torch.Generator(device=dev).manual_seed(1), device=dev)
+    g = torch.Generator(device=dev).manual_seed(1)
+    ds = [torch.randn(a.n, generator=g, device=dev) for _ in range(max(1, a.nbuf))]
     k = codec.topk_k(a.n, a.ratio)
-    for _ in range(3):
-        codec.topk(d, k)
+    lib.choco_topk_set_warm_start(0 if a.cold else 1)
+    for i in range(6):
+        codec.topk(ds[i % len(ds)], k)
     torch.cuda.synchronize()
     buf = np.zeros((40960, 4), dtype=np.uint64)
     fn(None, 0)
     try:
-        codec.topk(d, k)
+        codec.topk(ds[6 % len(ds)], k)
     except RuntimeError as e:  # diagnostic builds that stop early
         print("(call failed:", e, ")")
     torch.cuda.synchronize()
