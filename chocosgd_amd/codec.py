@@ -363,14 +363,19 @@ class IndexGuard:
     keeps in a device word (include/choco_codec.h): `arm()` queues a
     non-blocking copy of the word to pinned host memory behind the launches;
     `check()` raises RuntimeError -- the reference's index_put raises
-    IndexError -- once that copy has landed with a nonzero count.  No host
-    synchronisation on the hot path."""
+    IndexError -- once that copy has landed with a count above what was already
+    reported.  The count is cumulative (never reset on the device), so no error is
+    lost between copies.  No host synchronisation on the hot path; callers check
+    AFTER their own step's work is queued (a bad index of an earlier step must not
+    stop this step's valid messages from being applied), and `check(wait=True)`
+    copies and waits (teardown, checkpoints)."""
 
     def __init__(self, device):
         self.device = device
         self.word = torch.zeros(1, dtype=torch.int32, device=device)
         self.host = torch.zeros(1, dtype=torch.int32).pin_memory()
         self.event = None
+        self.reported = 0
 
     def arm(self):
         self.host.copy_(self.word, non_blocking=True)
@@ -378,6 +383,8 @@ class IndexGuard:
         self.event.record(torch.cuda.current_stream(self.device))
 
     def check(self, wait=False):
+        if wait and self.event is None:
+            self.arm()
         if self.event is None:
             return
         if wait:
@@ -385,11 +392,20 @@ class IndexGuard:
         elif not self.event.query():
             return
         self.event = None
-        bad = int(self.host.item())
-        if bad:
-            self.word.zero_()
-            raise RuntimeError(f"sparse accumulate: {bad} received indices out of range or not ascending (corrupt message "
-                               "or a peer with a different parameter layout)")
+        bad = int(self.host.item()) & 0xFFFFFFFF
+        if bad > self.reported:
+            new, self.reported = bad - self.reported, bad
+            raise RuntimeError(f"sparse accumulate: {new} received indices out of range or not ascending (corrupt "
+                               "message or a peer with a different parameter layout); a corrupt message may already "
+                               "have been applied")
+
+    def check_then_arm(self):
+        """End of a receiver step: report an EARLIER step's bad indices (this step's
+        messages are already applied), then queue this step's copy."""
+        try:
+            self.check()
+        finally:
+            self.arm()
 
 
 def sparse_accumulate(values, indices, memory, weight, xhat_self=None, guard=None):

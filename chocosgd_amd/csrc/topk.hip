@@ -1779,6 +1779,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   }
   if (tid < 5) fs.ctl[tid] = cword;  // s_lo, s_hi, shift, overflow, m1024
   const uint32_t tot = compact ? ti : chunk_run_starts(cw, nchunk, fs.run_start, fs.scratch);
+  if (compact) __syncthreads();  // fs.ctl (chunk_run_starts ends with this barrier)
   const uint32_t s_lo = fs.ctl[0], shift = fs.ctl[2], overflow = fs.ctl[3];
   STAMP(26000 + b, 0);
   // ---- the addresses of the tile's first emission batch (it does not depend on T)
@@ -1975,7 +1976,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
       eb ^= 1;
 #pragma unroll
       for (int i = 0; i < kEmitR; ++i) {
-        if (sel[i]) {
+        if (sel[i] && out + rk[i] < ku) {  // (bounded: an inconsistent select cannot write past k)
           st_pol<CHOCO_K34_STORE>(&out_val[out + rk[i]], v[i] * scale);
           st_pol<CHOCO_K34_STORE>(&out_idx[out + rk[i]], (int32_t)((int64_t)idx[i] + idx_base));
         }

@@ -154,11 +154,11 @@ class DCDSparsificationCompressor(_ConsumerBase):
             guard = self._guards.get(dev)
             if guard is None:
                 guard = self._guards[dev] = codec.IndexGuard(dev)
-            guard.check()
             msg = recover_device(sync_buffer["synced_message"][rank], device=dev)
             # hat[idx] += v  (dcd_psgd.py:275) == hat[idx] + 1.0f * v
             codec.sparse_accumulate(msg[:K].view(torch.float32), msg[K:], hat_params.buffer, 1.0, guard=guard)
-            guard.arm()
+        for guard in self._guards.values():  # bad indices of an earlier step, after this step's work
+            guard.check_then_arm()
 
 
 class DCDQuantizationCompressor(_ConsumerBase):

@@ -101,13 +101,12 @@ class DeepSqueezeSparsificationCompressor(_DeepSqueezeBase):
         agg = torch.zeros_like(tb.buffer)
         K = int(sync_buffer["sycned_message_size"] / 2)
         guard = self._guard(dev)
-        guard.check()
         for rank in neighbors_info.keys():
             msg = recover_device(sync_buffer["synced_message"][rank], device=dev)
             # agg[idx] += c * v  (two roundings, deep_squeeze.py:274-278)
             codec.sparse_accumulate(msg[:K].view(torch.float32), msg[K:], agg, self._weight(neighbors_info, rank),
                                     guard=guard)
-        guard.arm()
+        guard.check_then_arm()  # bad indices of an earlier step, after this step's work
         return self._like(tb, agg)
 
 

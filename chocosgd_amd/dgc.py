@@ -3,13 +3,20 @@ compress_or_quantize at :327-343): error-feedback top-k / random-k of every
 gradient tensor, an all-gather of the [values | indices] messages and the
 averaged sparse update -- or, for a quantize op, the QSGD dense floats all-reduced.
 
-`DGCCodec(world_aggregator, comm_op, comm_device, n_nodes, quantize_level=, is_biased=)`
-keeps the reference's three steps as methods:
+`DGCCodec(world_aggregator, comm_op, comm_device, n_nodes, quantize_level=, is_biased=,
+strict_reference=True)` keeps the reference's three steps as methods:
   * `compress(grads, memory_tb, compress_ratio)` -> (values, indices, n_bits):
-    _grad = grad + memory per tensor, top-k of _grad, memory <- _grad with the
-    selected entries zeroed (the reference's `_grad * nmask`); the error-feedback
-    memory is ONE flat TensorBuffer (the reference keeps a dict of per-parameter
-    vectors) so the whole layout is one batched launch; `indices` are GLOBAL int32;
+    _grad = grad + memory per tensor, top-k of _grad, memory <- `_grad * nmask`
+    (dgc.py:174-176).  The reference's nmask is `(~mask.byte()).float()`
+    (sparsification.py:33-38): a bitwise NOT of uint8 under the PyTorch this
+    runs on, i.e. 255 for unselected and 254 for selected entries, and
+    `strict_reference=True` (the default) reproduces exactly that, bit for bit.
+    `strict_reference=False` applies the evident intent instead (1 - mask, what `~`
+    gave for a ByteTensor in PyTorch <= 1.1: the selected entries zeroed, the rest
+    kept).  The error-feedback memory is ONE flat TensorBuffer (the reference keeps a
+    dict of per-parameter vectors) so the whole layout is one batched launch;
+    `indices` are GLOBAL int32.  For a quantize op the reference leaves memory alone
+    (dgc.py:183-185): _grad = grad + memory is a temporary;
   * `sync(values, indices)` -> (synced_message, message_size);
   * `recover_info(flatten_params, synced_message, message_size, lr)` -> params - lr *
     (sum of messages) / n_nodes.
@@ -26,7 +33,9 @@ from .tensor_buffer import flatten
 
 
 class DGCCodec(object):
-    def __init__(self, world_aggregator, comm_op, comm_device, n_nodes, quantize_level=None, is_biased=False):
+    def __init__(self, world_aggregator, comm_op, comm_device, n_nodes, quantize_level=None, is_biased=False,
+                 strict_reference=True):
+        self.strict_reference = strict_reference
         self.world_aggregator = world_aggregator
         self.comm_op = comm_op
         self.comm_device = comm_device
@@ -38,11 +47,12 @@ class DGCCodec(object):
         self.last_indices = None
 
     def compress(self, grads, memory_tb, compress_ratio):
-        x = memory_tb.buffer
+        memory = memory_tb.buffer
         lens = tuple(int(g.nelement()) for g in grads)
-        lay = _Layout.get(lens, x.device)
-        x.add_(flatten(grads))  # _grad = grad + memory (dgc.py:157; fp32 add commutes)
+        lay = _Layout.get(lens, memory.device)
         if self.is_compress_op:
+            x = memory
+            x.add_(flatten(grads))  # _grad = grad + memory (dgc.py:157; fp32 add commutes), in place
             plan = lay.topk_plan(float(compress_ratio))
             if "top_k" in self.comm_op:
                 values, indices = codec.topk_segmented(x, plan)
@@ -50,14 +60,20 @@ class DGCCodec(object):
                 values, indices = codec.randk_segmented(x, plan, _draw_seed(), is_biased=True)
             else:
                 raise NotImplementedError
-            # memory = _grad * nmask: the selected entries (values == x[idx]) become 0
-            codec.sparse_accumulate(torch.neg(values), indices, x, 1.0)
+            if self.strict_reference:
+                # _grad * nmask with nmask = (~mask.byte()).float(): 255 unselected, 254 selected
+                x.mul_(255.0)
+                x.index_put_((indices.long(),), values * 254.0)
+            else:
+                # _grad * (1 - mask): the selected entries (values == x[idx]) become 0
+                codec.sparse_accumulate(torch.neg(values), indices, x, 1.0)
             self.selected_shapes = list(plan.k_per_seg)
             self.last_indices = indices
             # nominal bits as compress_or_quantize counts them (dgc.py:335-337): fp32 values and
             # the int64 indices torch.topk returns (the wire here carries int32)
             return values, indices, 32 * values.numel() + 64 * indices.numel()
         if "quantize" in self.comm_op:
+            x = memory + flatten(grads)  # _grad: a temporary, memory keeps its value (dgc.py:183-185)
             q = int(self.quantize_level)
             if q == 32:
                 dense = x.clone()

@@ -74,10 +74,10 @@ class ECDSparsificationCompressor(_ECDBase):
             guard = self._guards.get(dev)
             if guard is None:
                 guard = self._guards[dev] = codec.IndexGuard(dev)
-            guard.check()
             msg = recover_device(sync_buffer["synced_message"][rank], device=dev)
             codec.sparse_extrapolate(msg[:K].view(torch.float32), msg[K:], hat_params.buffer, a, b, guard=guard)
-            guard.arm()
+        for guard in self._guards.values():  # bad indices of an earlier step, after this step's work
+            guard.check_then_arm()
 
 
 class ECDQuantizationCompressor(_ECDBase):

@@ -199,7 +199,6 @@ class CHOCOSparsificationCompressor(_CHOCOBase):
         K = int(sync_buffer["sycned_message_size"] / 2)
         memory = neighbor_hat_params["memory"]
         guard = self._guard(memory.buffer.device)
-        guard.check()  # out-of-range indices of an EARLIER step (lazy, no sync)
         # x_hat takes only the local message (hat_params.buffer += q_values,
         # parallel_choco_v.py:307-308): with remote messages pending, its scatter is
         # queued BEFORE waiting for them, so it runs while the exchange is in flight.
@@ -219,7 +218,14 @@ class CHOCOSparsificationCompressor(_CHOCOBase):
             own = rank in neighbor_hat_params and not hat_early
             codec.sparse_accumulate(q_values, q_indices, memory.buffer, weight,
                                     xhat_self=hat_params.buffer if own else None, guard=guard)
-        guard.arm()
+        # out-of-range indices of an EARLIER step (lazy, no sync), reported once this step's
+        # messages are applied; pipeline() prints it as the reference prints its RuntimeErrors
+        guard.check_then_arm()
+
+    def check(self, wait=True):
+        """Report bad received indices now (teardown / checkpoint): raises RuntimeError."""
+        for g in self._guards.values():
+            g.check(wait=wait)
 
 
 class CHOCOQuantizationCompressor(_CHOCOBase):

@@ -237,7 +237,7 @@ def test_sparse_accumulate_out_of_range_raises():
     assert host(hat)[[1, 5]].tolist() == [1.0, 1.0] and host(hat).sum() == 2.0
     assert host(mem).sum() == 1.0
     guard.arm()
-    guard.check(wait=True)  # the word was reset
+    guard.check(wait=True)  # the count is cumulative: nothing new since it was reported
 
 
 @pytest.mark.parametrize("kind", ["sign", "qsgd"])
@@ -256,9 +256,11 @@ def test_accumulate_more_than_8_messages(kind):
             msgs_d.append((packed, norms))
             decoded.append((host(packed), host(norms)))
         else:
-            packed, norms, dense = codec.qsgd_compress(x, 4, seed=r, want_dense=True)
+            packed, norms = codec.qsgd_compress(x, 4, seed=r)[:2]
             msgs_d.append((packed, norms))
-            decoded.append(host(dense))
+            # the oracle's own decode of the wire (not the device's dense output)
+            levels, neg = O.qsgd_unpack(host(packed), n, 4)
+            decoded.append(O.qsgd_decode(levels, neg, host(norms)[0], 15, n))
     if kind == "sign":
         codec.sign_accumulate(msgs_d, w, self_slot, n, mem, xhat_self=hat)
         O.sign_accumulate(h0, m0, decoded, w, self_slot, [n])

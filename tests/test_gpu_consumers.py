@@ -19,6 +19,22 @@ from oracle import choco_oracle as O
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+SEED0 = 5000  # torch.manual_seed(SEED0 + rank) before each rank's compress
+
+
+def drawn_seed(r):
+    """The seed sparsification._draw_seed takes from torch's generator after manual_seed(SEED0 + r)."""
+    torch.manual_seed(SEED0 + r)
+    return int(torch.randint(0, 2**62, (1,)).item())
+
+
+def randk_expected(d, lens, ratio, r):
+    """(values, global indices) the device sampler draws for rank r (oracle restatement)."""
+    return O.randk_segmented(np.asarray(d, dtype=np.float32), lens, ratio, drawn_seed(r), is_biased=True)
+
+
+def wire(vals, idx):
+    return np.concatenate([np.asarray(vals, dtype=np.float32).view(np.int32), np.asarray(idx).astype(np.int32)])
 
 
 def dev(a):
@@ -72,6 +88,7 @@ def run_dcd(g, comm_op, **kw):
         comp = DCDCompressor(**_args(comm_op, **kw))
         sb = {"original_shapes": shapes, "flatten_half_params": TensorBuffer(_split(dev(g["half"][r]), lens)),
               "flatten_params": TensorBuffer(_split(dev(g["x"][r]), lens))}
+        torch.manual_seed(SEED0 + r)  # the random-k sampler's seed (sparsification._draw_seed)
         comp.compress(sb)
         comp.compressor_fn.aggregator_fn = _Capture(r)
         comp.sync(sb)
@@ -144,6 +161,7 @@ def run_deepsqueeze(g, comm_op, **kw):
     for r in range(3):
         comp = DeepSqueezeCompressor(rank=r, consensus_stepsize=float(g["gamma"]), **_args(comm_op, **kw))
         sb = {"original_shapes": shapes, "params_tb": TensorBuffer(_split(dev(g["mem"][r]), lens))}
+        torch.manual_seed(SEED0 + r)
         local.append(host(comp.compress(sb).buffer))
         comp.compressor_fn.aggregator_fn = _Capture(r)
         comp.sync(sb)
@@ -213,6 +231,7 @@ def run_ecd(g, comm_op, **kw):
     for r in range(3):
         comp = ECDCompressor(**_args(comm_op, **kw))
         sb = {"original_shapes": shapes, "flatten_updated_params": TensorBuffer(_split(dev(g["z"][r]), lens))}
+        torch.manual_seed(SEED0 + r)
         comp.compress(sb)
         comp.compressor_fn.aggregator_fn = _Capture(r)
         comp.sync(sb)
@@ -306,9 +325,9 @@ def test_ef_sign_golden():
 
 
 def test_dgc_topk():
-    """Compress (memory keeps the unselected entries: the intended `_grad * nmask`, see
-    test_oracle_golden.test_dgc_fixture for the reference's uint8-NOT defect) and the
-    recovered parameters bit-exact against the reference's fixture."""
+    """strict_reference=False: the intended memory update (selected entries zeroed, what `~`
+    on a ByteTensor gave in PyTorch <= 1.1); the selection and the recovered parameters
+    bit-exact against the reference's fixture."""
     from chocosgd_amd.dgc import DGCCodec
     from chocosgd_amd.tensor_buffer import TensorBuffer
     g = golden("dgc_topk_mini_r09")
@@ -317,7 +336,8 @@ def test_dgc_topk():
     ratio = float(g["ratio"])
     msgs, mine = [], None
     for r in range(3):
-        codec_r = DGCCodec(world_aggregator=None, comm_op="compress_top_k", comm_device="gpu", n_nodes=3)
+        codec_r = DGCCodec(world_aggregator=None, comm_op="compress_top_k", comm_device="gpu", n_nodes=3,
+                           strict_reference=False)
         mem = TensorBuffer(_split(dev(g["mems"][r]), lens))
         grads = _split(dev(g["grads"][r]), lens)
         vals, idx, n_bits = codec_r.compress(grads, mem, ratio)
@@ -335,3 +355,121 @@ def test_dgc_topk():
     synced, size = codec_r.sync(vals, idx)
     out = codec_r.recover_info(dev(g["params"]), synced, size, float(g["lr"]))
     assert same_bits(host(out), g["params_after"])
+
+
+# ------------------------------------------------------------------------------ random-k consumers
+def test_dcd_random_k():
+    """DCDSparsificationCompressor with random_k (dcd_psgd.py:150-275): each rank's message is
+    the device sampler's draw (oracle restatement of the seeded hash, seed from torch's
+    generator) of half - x, and every replica gets hat[idx] += v."""
+    g = golden("dcd_topk_mini_r09")
+    lens = g["layout"].tolist()
+    sb, nhp, sent = run_dcd(g, "compress_random_k", ratio=0.9)
+    for r in range(3):
+        ov, oi = randk_expected((g["half"][r] - g["x"][r]).astype(np.float32), lens, 0.9, r)
+        assert np.array_equal(host(sent[r][0]), wire(ov, oi)), f"message {r}"
+        want = g["hats0"][r].copy()
+        want[oi] = (want[oi] + ov).astype(np.float32)
+        assert same_bits(host(nhp[r].buffer), want), f"replica {r}"
+
+
+def test_ecd_random_k():
+    """ECDSparsificationCompressor with random_k (ecd_psgd.py:211-303): messages of z, every
+    replica extrapolated hat[idx] = fmaf(2/t, v, hat[idx] * (1 - 2/t))."""
+    g = golden("ecd_topk_mini_r09")
+    lens = g["layout"].tolist()
+    t = int(g["local_index"])
+    a, b = O.ecd_coeffs(t)
+    sb, nhp, sent = run_ecd(g, "compress_random_k", ratio=0.9)
+    for r in range(3):
+        ov, oi = randk_expected(g["z"][r], lens, 0.9, r)
+        assert np.array_equal(host(sent[r][0]), wire(ov, oi)), f"message {r}"
+        want = g["hats0"][r].copy()
+        want[oi] = O.fma32(b, ov, (want[oi] * a).astype(np.float32))
+        assert same_bits(host(nhp[r].buffer), want), f"replica {r}"
+
+
+def test_deepsqueeze_random_k():
+    """DeepSqueezeSparsificationCompressor with random_k (deep_squeeze.py:158-279): the local
+    copy holds the drawn values, the aggregate sums c_r * v in neighbour order."""
+    g = golden("deepsqueeze_topk_mini_r09")
+    lens = g["layout"].tolist()
+    s = int(g["self_rank"])
+    sb, local, agg, sent = run_deepsqueeze(g, "compress_random_k", ratio=0.9)
+    want = np.zeros_like(g["agg"])
+    for r in range(3):
+        ov, oi = randk_expected(g["mem"][r], lens, 0.9, r)
+        assert np.array_equal(host(sent[r][0]), wire(ov, oi)), f"message {r}"
+        loc = np.zeros_like(g["mem"][r])
+        loc[oi] = ov
+        assert same_bits(local[r], loc)
+        c = O.deepsqueeze_weight(float(g["gamma"]), float(g["weights"][r]), r == s)
+        want[oi] = (want[oi] + (c * ov).astype(np.float32)).astype(np.float32)
+    assert same_bits(agg, want)
+
+
+# ------------------------------------------------------------------------------ DGC: strict / intended / quantize
+def test_dgc_topk_strict_reference_memory():
+    """strict_reference=True (the default): memory <- _grad * nmask with the reference's
+    nmask = (~mask.byte()).float() = 255 / 254 (dgc.py:174-176, sparsification.py:33-38),
+    bit-exact against the reference's own fixture; get_mask agrees."""
+    from chocosgd_amd.dgc import DGCCodec
+    from chocosgd_amd.sparsification import SparsificationCompressor
+    from chocosgd_amd.tensor_buffer import TensorBuffer
+    g = golden("dgc_topk_mini_r09")
+    lens = g["layout"].tolist()
+    ratio = float(g["ratio"])
+    for r in range(3):
+        c = DGCCodec(world_aggregator=None, comm_op="compress_top_k", comm_device="gpu", n_nodes=3)
+        assert c.strict_reference
+        mem = TensorBuffer(_split(dev(g["mems"][r]), lens))
+        vals, idx, _ = c.compress(_split(dev(g["grads"][r]), lens), mem, ratio)
+        assert same_bits(host(mem.buffer), g["mems_after"][r])
+        x = dev((g["grads"][r] + g["mems"][r]).astype(np.float32))
+        _, nmask = SparsificationCompressor().get_mask(x, idx.long())
+        assert same_bits(host(x * nmask), g["mems_after"][r])
+
+
+@pytest.mark.parametrize("q", [32, 4])
+def test_dgc_quantize_multistep(q):
+    """DGC's quantize branch (dgc.py:183-185, 336-340) over three steps: the memory is left
+    alone (the reference's `pass`), the message is QSGD of grad + memory (q = 32: the floats
+    themselves), and recover_info applies params - lr * sum / n_nodes."""
+    from chocosgd_amd.dgc import DGCCodec
+    from chocosgd_amd.tensor_buffer import TensorBuffer
+    g = golden("dgc_topk_mini_r09")
+    lens = g["layout"].tolist()
+    n = sum(lens)
+    c = DGCCodec(world_aggregator=None, comm_op="quantize_qsgd", comm_device="gpu", n_nodes=3, quantize_level=q)
+    mem0 = g["mems"][0]
+    mem = TensorBuffer(_split(dev(mem0), lens))
+    params = g["params"].copy()
+    for step in range(3):
+        grads = (g["grads"][step] * np.float32(0.5 + step)).astype(np.float32)
+        seed = drawn_seed(step)
+        torch.manual_seed(SEED0 + step)
+        dense, idx, n_bits = c.compress(_split(dev(grads), lens), mem, None)
+        assert idx is None
+        assert same_bits(host(mem.buffer), mem0), "memory must keep its value"
+        x = (grads + mem0).astype(np.float32)
+        if q == 32:
+            want = x
+        else:
+            s = 2 ** q - 1
+            u = O.qsgd_uniforms(n, seed, 0)
+            off, parts = 0, []
+            for si, m in enumerate(lens):
+                nd = np.float32(np.sqrt(np.sum(x[off:off + m].astype(np.float64) ** 2)))
+                parts.append(O.qsgd_dense(x[off:off + m], s, u[off:off + m], nd))
+                off += m
+            want = np.concatenate(parts)
+        assert same_bits(host(dense), want)
+        others = [dense, dense * 2, dense * 3]
+        summed = others[0] + others[1] + others[2]
+        c.world_aggregator = _Gather([summed])
+        synced, size = c.sync(dense, None)
+        out = c.recover_info(dev(params), synced, size, 0.1)
+        upd = (host(summed) / np.float32(3)).astype(np.float32)
+        params_next = O.fma32(np.float32(-0.1), upd, params)
+        assert same_bits(host(out), params_next)
+        params = params_next

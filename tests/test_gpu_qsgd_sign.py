@@ -121,7 +121,13 @@ def test_qsgd_segmented_layout_norms_and_levels(layout):
         off += m
     assert same_bits(host(dense), np.concatenate(outs))
     dec = codec.qsgd_decode(packed, norms, n, 4, seg_off=so, nseg=len(lens))
-    assert same_bits(host(dec), host(dense))
+    levels, neg = O.qsgd_unpack(host(packed), n, 4)  # the oracle's decode of the wire itself
+    off, want = 0, []
+    for s, m in enumerate(lens):
+        want.append(O.qsgd_decode(levels[off:off + m], neg[off:off + m], host(norms)[s], 15, m))
+        off += m
+    assert same_bits(host(dec), np.concatenate(want))
+    assert same_bits(host(dense), np.concatenate(want))
 
 
 # ------------------------------------------------------------------------------------ sign
