@@ -59,11 +59,11 @@ GAMMA = 0.9  # consensus_stepsize (parameters.py:126 default)
 
 # kernels (profile names) of each stage
 STAGES = {
-    "topk": (["topk_fused", "topk_bounds", "topk_stream", "topk_finish", "topk_exact", "topk_all"],
+    "topk": (["topk_bounds", "topk_stream", "topk_finish", "topk_exact", "topk_all"],
              ["sparse_accumulate"]),
-    "topk_seg": (["topk_seg_hist", "topk_seg_collect", "topk_seg_fine", "topk_seg_count", "topk_seg_emit", "topk_fused",
+    "topk_seg": (["topk_seg_hist", "topk_seg_collect", "topk_seg_fine", "topk_seg_count", "topk_seg_emit",
                   "topk_bounds", "topk_stream", "topk_finish"], ["sparse_accumulate"]),
-    "randk": (["topk_stream", "topk_finish", "topk_exact", "topk_all"], ["sparse_accumulate"]),
+    "randk": (["randk_count", "randk_tile"], ["sparse_accumulate"]),
     "qsgd": (["qsgd_norm", "qsgd_quantize"], ["qsgd_accumulate"]),
     "sign": (["sign_pack"], ["sign_accumulate"]),
 }
@@ -186,9 +186,9 @@ class Worker:
         elif self.op == "topk_seg":
             c.topk_segmented(self.d, self.plan, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]))
         elif self.op == "randk":
-            v, i = c.randk(self.d, self.k, seed=12345 + 7919 * self.step_id + self.rank)
-            self.msg[:self.k].view(torch.float32).copy_(v)
-            self.msg[self.k:].copy_(i)
+            # one seed per worker, the step number as the stream offset (include/choco_codec.h)
+            c.randk(self.d, self.k, seed=12345 + self.rank, offset=self.step_id,
+                    out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]))
         elif self.op == "qsgd":
             c.qsgd_compress(self.d, self.param, seed=12345 + self.rank, offset=self.step_id, out=self.wire)
         else:

@@ -36,8 +36,8 @@ SIGNATURES = {
     "choco_topk_segmented_workspace_size": (_c_sz, [_p_i64, _c_i32]),
     "choco_topk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _p_i64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_randk_workspace_size": (_c_sz, [_c_i64]),
-    "choco_randk_compress": (_c_i32, [_vp, _vp, _c_i64, _c_i64, _c_u64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
-    "choco_randk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _p_i64, _c_i32, _c_u64, _c_i32, _vp, _vp, _vp,
+    "choco_randk_compress": (_c_i32, [_vp, _vp, _c_i64, _c_i64, _c_u64, _c_u64, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
+    "choco_randk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _p_i64, _c_i32, _c_u64, _c_u64, _c_i32, _vp, _vp, _vp,
                                                 _c_sz, _vp]),
     "choco_gather": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_f32, _vp, _vp]),
     "choco_sparse_accumulate": (_c_i32, [_vp, _vp, _c_i64, _vp, _vp, _c_i64, _c_f32, _vp, _vp]),
@@ -64,8 +64,8 @@ SIGNATURES = {
     "choco_gossip_topk_compress": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_gossip_topk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _c_f32, _vp, _p_i64, _c_i32, _vp, _vp, _vp,
                                                       _c_sz, _vp]),
-    "choco_gossip_randk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _c_f32, _vp, _p_i64, _c_i32, _c_u64, _c_i32,
-                                                       _vp, _vp, _vp, _c_sz, _vp]),
+    "choco_gossip_randk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _c_f32, _vp, _p_i64, _c_i32, _c_u64, _c_u64,
+                                                       _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_gossip_sign_compress": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _vp, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_gossip_qsgd_compress": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _vp, _c_i32, _c_i32, _c_i32, _c_u64,
                                             _c_u64, _vp, _vp, _vp, _vp, _c_sz, _vp]),

@@ -305,47 +305,54 @@ def topk_segmented(x, plan, xhat=None, out=None, gossip=None):
 
 
 # ----------------------------------------------------------------------------- random-k
-def randk(x, k, seed, is_biased=True, xhat=None):
+def randk(x, k, seed, is_biased=True, xhat=None, offset=0, out=None):
+    """Uniform random k-subset (include/choco_codec.h: the device sampler of (seed, offset)),
+    values x[i] (- xhat[i]) (* n / k unbiased), int32 indices in ascending order;
+    `out=(values f32[k], indices i32[k])` writes into caller buffers."""
     _require(x, torch.float32, "x")
     if xhat is not None:
         _require(xhat, torch.float32, "xhat")
+        if xhat.numel() != x.numel():
+            raise RuntimeError("x and xhat must have the same number of elements")
     n = x.numel()
     dev = x.device
-    vals = torch.empty(k, dtype=torch.float32, device=dev)
-    idx = torch.empty(k, dtype=torch.int32, device=dev)
+    if out is not None:
+        vals, idx = out
+        _require(vals, torch.float32, "out values")
+        _require(idx, torch.int32, "out indices")
+        if vals.numel() != k or idx.numel() != k:
+            raise RuntimeError("out buffers must hold exactly k elements")
+    else:
+        vals = torch.empty(k, dtype=torch.float32, device=dev)
+        idx = torch.empty(k, dtype=torch.int32, device=dev)
     L = lib()
-    ws = workspace(dev, "topk", L.choco_randk_workspace_size(n))
-    st = topk_status(ws)
-    st.check()
+    ws = workspace(dev, "randk", L.choco_randk_workspace_size(n))
     _lib.check(L.choco_randk_compress(_ptr(x), _ptr(xhat), n, int(k), int(seed) & (2**64 - 1),
-                                      1 if is_biased else 0, _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(),
-                                      _stream(dev)), "choco_randk_compress")
-    st.after_call()
+                                      int(offset) & (2**64 - 1), 1 if is_biased else 0, _ptr(vals), _ptr(idx),
+                                      _ptr(ws), ws.numel(), _stream(dev)), "choco_randk_compress")
     return vals, idx
 
 
-def randk_segmented(x, plan, seed, is_biased=True, xhat=None, out=None, gossip=None):
+def randk_segmented(x, plan, seed, is_biased=True, xhat=None, out=None, gossip=None, offset=0):
     """Per-segment random-k over a SegmentPlan (k_s as top-k's), one batched call:
-    segment s ranked by the seeded hash with seed seg_seed(seed, s); GLOBAL indices."""
+    segment s drawn with key derive(key(seed, offset), s); GLOBAL indices."""
     vals, idx = _seg_outputs(x, xhat, plan, out)
     dev = x.device
     L = lib()
     ws = plan.workspace(dev)
-    st = topk_status(ws)
-    st.check()
     g = _gossip(gossip, x, xhat)
+    sd, off = int(seed) & (2**64 - 1), int(offset) & (2**64 - 1)
     if g is not None:
         _lib.check(L.choco_gossip_randk_compress_segmented(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1],
-                                                           _ptr(plan.plan_dev), plan.plan_host, plan.nseg,
-                                                           int(seed) & (2**64 - 1), 1 if is_biased else 0,
-                                                           _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(), _stream(dev)),
+                                                           _ptr(plan.plan_dev), plan.plan_host, plan.nseg, sd, off,
+                                                           1 if is_biased else 0, _ptr(vals), _ptr(idx), _ptr(ws),
+                                                           ws.numel(), _stream(dev)),
                    "choco_gossip_randk_compress_segmented")
     else:
         _lib.check(L.choco_randk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
-                                                    plan.nseg, int(seed) & (2**64 - 1), 1 if is_biased else 0,
-                                                    _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(), _stream(dev)),
+                                                    plan.nseg, sd, off, 1 if is_biased else 0, _ptr(vals), _ptr(idx),
+                                                    _ptr(ws), ws.numel(), _stream(dev)),
                    "choco_randk_compress_segmented")
-    st.after_call()
     return vals, idx
 
 

@@ -356,4 +356,14 @@ int topk_pipeline(int mode, const float* x, const float* xh, int64_t n, int64_t 
 // forget the warm-start records of the top-k workspaces in [ws, ws + bytes) (include/choco_codec.h)
 void topk_warm_forget(const void* ws, size_t bytes);
 
+// random-k (randk.hip): tiles of a segment, the counts buffer, the two launches
+// (plan_dev == nullptr: the flat call over [0, n) with k; else the segmented plan's
+// random-k table at rk_base with R tiles)
+int64_t randk_tiles(int64_t len);
+size_t randk_counts_bytes(int64_t R);
+int randk_launch(const float* x, const float* xh, const int64_t* plan_dev, int64_t rk_base, int64_t R, int64_t n,
+                 int64_t k, uint64_t seed, uint64_t offset, int32_t is_biased, float* out_val, int32_t* out_idx,
+                 void* counts, size_t counts_bytes, hipStream_t st);
+void randk_forget(const void* ws, size_t bytes);
+
 }  // namespace choco

@@ -1,0 +1,348 @@
+// Random-k sparsification on MI355X: a direct sampler.
+//
+// Replaces SparsificationCompressor.get_random_k (reference
+// dl_code/pcode/utils/sparsification.py:40-54: np.random.choice(n, k,
+// replace=False), then x_data[selected_indices], scaled by n / k when
+// unbiased) and the random_k branch of CHOCOSparsificationCompressor.compress
+// (parallel_choco_v.py:229-260, one draw per parameter tensor).
+//
+// The sample is a uniform k-subset of [0, N) drawn WITHOUT touching the N - k
+// unselected elements (round 2 hashed and ranked all N indices):
+//   * pi_N(.; K) is a seeded bijection of [0, N): four rounds of
+//     (add a_r, multiply by odd m_r, x ^= x >> h) on the B-bit domain
+//     (2^B >= N, h = (B + 1) / 2), cycle-walked back into [0, N);
+//   * the segment is cut into tiles of 2^18 elements; tile t's count c_t is
+//     #{ j < k : pi_N(j; K) >> 18 == t } -- the counts of the first k values of
+//     a random permutation, i.e. exactly the multivariate hypergeometric split
+//     of a uniform k-subset over the tiles (one pass over k, not N);
+//   * inside tile t the c_t positions are pi_{L_t}(j; K_t), j < c_t -- a fresh
+//     uniform c_t-subset of the tile (conditioned on its count, a uniform
+//     k-subset is uniform inside every tile and independent across tiles), set
+//     in a 32 KB LDS bitmap and emitted in ascending order with a gather of
+//     x[i] (- xhat[i]) (* n / k).
+// Keys: K = derive(qrng_key(seed, offset), s) for segment s (the flat call is
+// segment 0), K_t = derive(K, 8 + t), round keys of pi(.; K): a_r = derive(K, 2r),
+// m_r = derive(K, 2r + 1) | 1, masked to B bits, derive(K, i) =
+// splitmix64_mix(K + (i + 1) * 0x9E3779B97F4A7C15).  oracle/choco_oracle.py
+// restates every step (randk_indices, randk_segmented).
+//
+// Two launches: R1 (tile counts; only for segments of more than one tile) and
+// R2 (per tile: bitmap sample, ordered emission, gather).  Bytes: 4k gathered
+// (8k with xhat) + 8k written; the sampler itself reads nothing.
+#include "choco_common.h"
+
+#include <algorithm>
+#include <mutex>
+#include <unordered_map>
+
+namespace choco {
+
+constexpr int kRkTileBits = 18;
+constexpr int64_t kRkTile = int64_t(1) << kRkTileBits;  // elements per tile: a 32 KB bitmap
+constexpr int kRkThreads = 1024;
+constexpr int kRkWords = (int)(kRkTile / 32);            // 8192 bitmap words
+constexpr int kRkWpt = kRkWords / kRkThreads;            // 8 words (256 bits) per thread
+constexpr int kRkMaxSegTiles = (int)((int64_t(1) << 31) >> kRkTileBits);  // 8192 tiles of one segment
+constexpr int64_t kRkCountWgs = 32;  // flat count pass: workgroups sharing [0, k)
+constexpr int kRkWalkCap = 4096;  // cycle-walk bound (P(walk > 64) < 2^-64 per draw): a GPU loop must end
+static_assert(kRkWpt * 32 * kRkThreads == kRkTile, "bitmap geometry");
+
+CHOCO_DEV __host__ uint64_t rk_derive(uint64_t K, uint64_t i) { return splitmix64_mix(K + (i + 1) * kGoldenGamma); }
+
+// Seeded bijection of [0, N), N in [1, 2^31).
+struct RkPerm {
+  uint32_t N, mask, h;
+  uint32_t a[4], m[4];
+  CHOCO_DEV void init(uint64_t K, uint32_t n) {
+    N = n;
+    uint32_t B = 1;
+    while ((1u << B) < n) ++B;
+    mask = (1u << B) - 1u;
+    h = (B + 1u) / 2u;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      a[r] = (uint32_t)rk_derive(K, 2 * r) & mask;
+      m[r] = ((uint32_t)rk_derive(K, 2 * r + 1) | 1u) & mask;
+    }
+  }
+  CHOCO_DEV uint32_t rounds(uint32_t x) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      x = (x + a[r]) & mask;
+      x = (x * m[r]) & mask;
+      x ^= x >> h;
+    }
+    return x;
+  }
+  CHOCO_DEV uint32_t operator()(uint32_t j) const {
+    uint32_t y = rounds(j);
+    for (int it = 0; y >= N && it < kRkWalkCap; ++it) y = rounds(y);
+    return y;
+  }
+};
+
+// One tile of one segment: where it is, what its segment is.
+struct RkTile {
+  int64_t seg_off, seg_len, k, out_off;  // the segment (plan row)
+  int64_t t, ntile, first;               // tile index in the segment, its tile count, global id of its tile 0
+  uint64_t K;                            // the segment's key
+};
+
+// plan (int64): the segmented top-k plan (topk_seg.hip) followed by the random-k
+// tile table at rk_base: [R] then R x {segment, tile in segment, first tile of the
+// segment, tiles of the segment}.
+CHOCO_DEV RkTile rk_tile_seg(const int64_t* __restrict__ plan, int64_t rk_base, uint64_t key, int64_t b) {
+  const int64_t* e = plan + rk_base + 1 + 4 * b;
+  const int64_t s = e[0];
+  const int64_t* row = plan + 8 * s;
+  RkTile T;
+  T.seg_off = row[0];
+  T.seg_len = row[1];
+  T.k = row[2];
+  T.out_off = row[3];
+  T.t = e[1];
+  T.first = e[2];
+  T.ntile = e[3];
+  T.K = rk_derive(key, (uint64_t)s);
+  return T;
+}
+CHOCO_DEV RkTile rk_tile_flat(int64_t n, int64_t k, uint64_t key, int64_t b) {
+  RkTile T;
+  T.seg_off = 0;
+  T.seg_len = n;
+  T.k = k;
+  T.out_off = 0;
+  T.t = b;
+  T.ntile = (n + kRkTile - 1) >> kRkTileBits;
+  T.first = 0;
+  T.K = rk_derive(key, 0);
+  return T;
+}
+
+// R1: this tile's share of j in [0, k) of its segment -> pi_N(j) -> tile histogram
+// -> the counts of the call (cnt[par]); the NEXT call's counts are zeroed here.
+template <bool FLAT>
+__global__ __launch_bounds__(kRkThreads) void randk_count_kernel(const int64_t* __restrict__ plan, int64_t rk_base,
+                                                                 int64_t n, int64_t k, uint64_t key,
+                                                                 uint32_t* __restrict__ cnt_cur,
+                                                                 uint32_t* __restrict__ cnt_next, int64_t cap) {
+  __shared__ uint32_t hist[kRkMaxSegTiles];
+  const int64_t b = blockIdx.x;
+  // flat: gridDim.x <= tiles workgroups share [0, k) (fewer flushes of the tile histogram:
+  // every flush is up to `tiles` global atomics onto the same `tiles` words); segmented:
+  // one workgroup per tile of the plan
+  const RkTile T = FLAT ? rk_tile_flat(n, k, key, 0) : rk_tile_seg(plan, rk_base, key, b);
+  // the NEXT call's counts, over the buffer's whole capacity (it may draw more tiles)
+  for (int64_t i = b * kRkThreads + threadIdx.x; i < cap; i += (int64_t)gridDim.x * kRkThreads) cnt_next[i] = 0u;
+  if (T.ntile <= 1 || T.k >= T.seg_len) return;  // one tile, or every element: no split to draw
+  const int nt = (int)T.ntile;
+  for (int i = threadIdx.x; i < nt; i += kRkThreads) hist[i] = 0u;
+  __syncthreads();
+  RkPerm P;
+  P.init(T.K, (uint32_t)T.seg_len);
+  const int64_t parts = FLAT ? (int64_t)gridDim.x : T.ntile, part = FLAT ? b : T.t;
+  const int64_t j0 = T.k * part / parts, j1 = T.k * (part + 1) / parts;
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += kRkThreads) atomicAdd(&hist[P((uint32_t)j) >> kRkTileBits], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < nt; i += kRkThreads)
+    if (hist[i]) atomicAdd(&cnt_cur[T.first + i], hist[i]);
+}
+
+CHOCO_DEV uint32_t pick_word(const uint32_t (&w)[kRkWpt], int q) {  // w[q] by selects (no scratch)
+  uint32_t r = w[0];
+#pragma unroll
+  for (int i = 1; i < kRkWpt; ++i) r = q == i ? w[i] : r;
+  return r;
+}
+
+// R2: one tile -> its count and output offset, the bitmap sample, the ordered
+// emission with the gather.
+template <bool FLAT, bool XH>
+__global__ __launch_bounds__(kRkThreads) void randk_tile_kernel(const float* __restrict__ x, const float* __restrict__ xh,
+                                                                const int64_t* __restrict__ plan, int64_t rk_base,
+                                                                int64_t n, int64_t k, uint64_t key, int32_t is_biased,
+                                                                const uint32_t* __restrict__ cnt,
+                                                                float* __restrict__ out_val,
+                                                                int32_t* __restrict__ out_idx) {
+  __shared__ uint32_t bm[kRkWords];
+  __shared__ uint32_t scratch[40];
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const RkTile T = FLAT ? rk_tile_flat(n, k, key, b) : rk_tile_seg(plan, rk_base, key, b);
+  const int64_t start = T.t << kRkTileBits;  // within the segment
+  const uint32_t L = (uint32_t)std::min<int64_t>(kRkTile, T.seg_len - start);
+  const bool all = T.k >= T.seg_len;
+  // this tile's count and the counts of the segment's earlier tiles
+  uint32_t c, pre;
+  if (all) {
+    c = L;
+    pre = (uint32_t)start;
+  } else if (T.ntile == 1) {
+    c = (uint32_t)T.k;
+    pre = 0u;
+  } else {
+    uint32_t part = 0;
+    for (int64_t i = tid; i < T.t; i += kRkThreads) part += cnt[T.first + i];
+    uint32_t tot;
+    block_excl_scan(part, scratch, &tot);
+    pre = tot;
+    c = cnt[T.first + T.t];
+  }
+  // the c positions of this tile: a bitmap in LDS
+  if (all) {
+#pragma unroll
+    for (int q = 0; q < kRkWpt; ++q) {
+      const uint32_t w0 = (uint32_t)(tid * kRkWpt + q) * 32u;
+      bm[tid * kRkWpt + q] = w0 + 32u <= L ? 0xFFFFFFFFu : (w0 >= L ? 0u : ((1u << (L - w0)) - 1u));
+    }
+    __syncthreads();
+  } else {
+#pragma unroll
+    for (int q = 0; q < kRkWpt; ++q) bm[tid * kRkWpt + q] = 0u;
+    __syncthreads();
+    RkPerm P;
+    P.init(rk_derive(T.K, 8 + (uint64_t)T.t), L);
+    for (uint32_t j = tid; j < c; j += kRkThreads) {
+      const uint32_t p = P(j);
+      atomicOr(&bm[p >> 5], 1u << (p & 31u));
+    }
+    __syncthreads();
+  }
+  // thread t owns bits [256 t, 256 t + 256): rank of its first set bit
+  uint32_t w[kRkWpt];
+  uint32_t mine = 0;
+#pragma unroll
+  for (int q = 0; q < kRkWpt; ++q) {
+    w[q] = bm[tid * kRkWpt + q];
+    mine += (uint32_t)__popc(w[q]);
+  }
+  uint32_t tot;
+  uint32_t rank = block_excl_scan(mine, scratch, &tot);
+  const float scale = is_biased ? 1.0f : (float)((double)T.seg_len / (double)T.k);
+  const int64_t gbase = T.seg_off + start;                 // global index of the tile's first element
+  float* __restrict__ ov = out_val + T.out_off + pre;
+  int32_t* __restrict__ oi = out_idx + T.out_off + pre;
+  // ascending set bits, kG gathers in flight per batch (every register index static)
+  constexpr int kG = 8;
+  int q = 0;
+  uint32_t cur = w[0];
+  for (;;) {
+    uint32_t pos[kG];
+    bool ok[kG];
+#pragma unroll
+    for (int i = 0; i < kG; ++i) {
+      while (cur == 0u && q + 1 < kRkWpt) cur = pick_word(w, ++q);
+      ok[i] = cur != 0u;
+      pos[i] = ok[i] ? (uint32_t)(tid * kRkWpt + q) * 32u + (uint32_t)__builtin_ctz(cur) : 0u;
+      if (ok[i]) cur &= cur - 1u;
+    }
+    if (!ok[0]) break;
+    float v[kG];
+#pragma unroll
+    for (int i = 0; i < kG; ++i) {
+      v[i] = 0.f;
+      if (ok[i]) {
+        const int64_t e = gbase + pos[i];
+        v[i] = XH ? x[e] - xh[e] : x[e];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kG; ++i) {
+      if (ok[i] && rank + (uint32_t)i < c) {  // (bounded: never past the tile's count)
+        ov[rank + i] = v[i] * scale;
+        oi[rank + i] = (int32_t)(gbase + pos[i]);
+      }
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < kG; ++i) m += ok[i] ? 1u : 0u;
+    rank += m;
+  }
+}
+
+// ---------------------------------------------------------------- host side
+// call parity per counts buffer: call c adds into cnt[c & 1] and zeroes the other
+static std::mutex g_rk_mu;
+static std::unordered_map<const void*, uint64_t> g_rk_calls;
+static uint32_t rk_parity(const void* cnt) {
+  std::lock_guard<std::mutex> g(g_rk_mu);
+  auto it = g_rk_calls.find(cnt);
+  if (it == g_rk_calls.end()) {
+    g_rk_calls.emplace(cnt, 1u);
+    return 0u;
+  }
+  return (uint32_t)(it->second++ & 1u);
+}
+void randk_forget(const void* ws, size_t bytes) {
+  std::lock_guard<std::mutex> g(g_rk_mu);
+  const char* lo = static_cast<const char*>(ws);
+  for (auto it = g_rk_calls.begin(); it != g_rk_calls.end();) {
+    const char* p = static_cast<const char*>(it->first);
+    if (p == lo || (p > lo && p < lo + bytes)) it = g_rk_calls.erase(it);
+    else ++it;
+  }
+}
+
+int64_t randk_tiles(int64_t len) { return (len + kRkTile - 1) >> kRkTileBits; }
+
+// counts: [256-B header (status word) | cnt[2][R]]
+size_t randk_counts_bytes(int64_t R) { return 256 + align_up((size_t)(2 * R) * 4, 256); }
+
+// The flat call (plan == nullptr) or the segmented one (plan_dev / rk_base / R).
+int randk_launch(const float* x, const float* xh, const int64_t* plan_dev, int64_t rk_base, int64_t R, int64_t n,
+                 int64_t k, uint64_t seed, uint64_t offset, int32_t is_biased, float* out_val, int32_t* out_idx,
+                 void* counts, size_t counts_bytes, hipStream_t st) {
+  const uint64_t key = qrng_key(seed, offset);
+  CHOCO_REQUIRE(counts_bytes >= randk_counts_bytes(R), "random-k counts buffer too small");
+  const int64_t cap = (int64_t)((counts_bytes - 256) / 8);  // tiles per parity the buffer holds
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(counts) + 256);
+  // first call on a buffer: parity 0, zero (the workspace contract); R1 zeroes the other
+  const uint32_t par = rk_parity(cnt);
+  const bool flat = plan_dev == nullptr;
+  profile_begin("randk_count", st);
+  if (flat)
+    CHOCO_KLAUNCH((randk_count_kernel<true>), dim3((unsigned)std::min<int64_t>(R, kRkCountWgs)), dim3(kRkThreads), 0,
+                  st, plan_dev, rk_base, n, k, key,
+                  cnt + par * cap, cnt + (par ^ 1u) * cap, cap);
+  else
+    CHOCO_KLAUNCH((randk_count_kernel<false>), dim3((unsigned)R), dim3(kRkThreads), 0, st, plan_dev, rk_base, n, k,
+                  key, cnt + par * cap, cnt + (par ^ 1u) * cap, cap);
+  profile_end("randk_count", st);
+  CHOCO_LAUNCHED("randk_count_kernel");
+  profile_begin("randk_tile", st);
+  if (flat && xh)
+    CHOCO_KLAUNCH((randk_tile_kernel<true, true>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
+                  rk_base, n, k, key, is_biased, cnt + par * cap, out_val, out_idx);
+  else if (flat)
+    CHOCO_KLAUNCH((randk_tile_kernel<true, false>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
+                  rk_base, n, k, key, is_biased, cnt + par * cap, out_val, out_idx);
+  else if (xh)
+    CHOCO_KLAUNCH((randk_tile_kernel<false, true>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
+                  rk_base, n, k, key, is_biased, cnt + par * cap, out_val, out_idx);
+  else
+    CHOCO_KLAUNCH((randk_tile_kernel<false, false>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
+                  rk_base, n, k, key, is_biased, cnt + par * cap, out_val, out_idx);
+  profile_end("randk_tile", st);
+  CHOCO_LAUNCHED("randk_tile_kernel");
+  return CHOCO_OK;
+}
+
+}  // namespace choco
+
+using namespace choco;
+
+CHOCO_API size_t choco_randk_workspace_size(int64_t n) { return n > 0 ? randk_counts_bytes(randk_tiles(n)) : 256; }
+
+CHOCO_API int choco_randk_compress(const float* x, const float* xhat, int64_t n, int64_t k, uint64_t seed,
+                                   uint64_t offset, int32_t is_biased, float* out_val, int32_t* out_idx, void* ws,
+                                   size_t ws_bytes, void* stream) {
+  CHOCO_REQUIRE(x != nullptr && out_val != nullptr && out_idx != nullptr, "null pointer argument");
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n must be in [1, 2^31-1), got %lld", (long long)n);
+  CHOCO_REQUIRE(k >= 1 && k <= n, "k must be in [1, n], got k=%lld n=%lld", (long long)k, (long long)n);
+  CHOCO_REQUIRE(aligned4(x) && (xhat == nullptr || aligned4(xhat)), "x/xhat must be 4-byte aligned");
+  const int64_t R = randk_tiles(n);
+  CHOCO_REQUIRE(ws != nullptr && ws_bytes >= randk_counts_bytes(R),
+                "random-k workspace too small: need %zu bytes, got %zu", randk_counts_bytes(R), ws_bytes);
+  return randk_launch(x, xhat, nullptr, 0, R, n, k, seed, offset, is_biased, out_val, out_idx, ws, ws_bytes,
+                      as_stream(stream));
+}

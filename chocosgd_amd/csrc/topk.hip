@@ -2172,6 +2172,7 @@ CHOCO_API size_t choco_topk_workspace_size(int64_t n) { return topk_ws_bytes(n);
 
 CHOCO_API int choco_topk_workspace_reset(const void* ws, size_t ws_bytes) {
   topk_warm_forget(ws, ws_bytes);
+  randk_forget(ws, ws_bytes);
   return CHOCO_OK;
 }
 
@@ -2179,7 +2180,6 @@ CHOCO_API int choco_topk_set_warm_start(int32_t enable) {
   g_warm_on.store(enable != 0);
   return CHOCO_OK;
 }
-CHOCO_API size_t choco_randk_workspace_size(int64_t n) { return topk_ws_bytes(n); }
 
 CHOCO_API int choco_topk_compress(const float* x, const float* xhat, int64_t n, int64_t k, float* out_val,
                                   int32_t* out_idx, void* ws, size_t ws_bytes, void* stream) {
@@ -2192,14 +2192,6 @@ CHOCO_API int choco_gossip_topk_compress(float* x, const float* memory, const fl
   CHOCO_REQUIRE(memory != nullptr && xhat != nullptr, "the gossip step needs memory and x_hat");
   return dispatch_topk<kData>(x, xhat, n, k, 0, 1.0f, out_val, out_idx, 0, ws, ws_bytes, as_stream(stream),
                               Gossip{memory, gamma});
-}
-
-CHOCO_API int choco_randk_compress(const float* x, const float* xhat, int64_t n, int64_t k, uint64_t seed,
-                                   int32_t is_biased, float* out_val, int32_t* out_idx, void* ws,
-                                   size_t ws_bytes, void* stream) {
-  const float scale = is_biased ? 1.0f : (float)((double)n / (double)k);
-  return dispatch_topk<kHash>(x, xhat, n, k, seed, scale, out_val, out_idx, 0, ws, ws_bytes,
-                              as_stream(stream));
 }
 
 #if CHOCO_STAMPS

@@ -644,11 +644,17 @@ static int seg_plan_scan(const int64_t* seg_off_host, int32_t nseg, int64_t* nti
   return CHOCO_OK;
 }
 
+static int64_t rk_plan_tiles(const int64_t* seg_off_host, int32_t nseg) {
+  int64_t R = 0;
+  for (int s = 0; s < nseg; ++s) R += randk_tiles(seg_off_host[s + 1] - seg_off_host[s]);
+  return R;
+}
+
 CHOCO_API int64_t choco_topk_segmented_plan_len(const int64_t* seg_off_host, int32_t nseg) {
   int64_t ntile, nbat;
   const int rc = seg_plan_scan(seg_off_host, nseg, &ntile, &nbat);
   if (rc) return rc;
-  return (int64_t)kRow * nseg + ntile + nbat;
+  return (int64_t)kRow * nseg + ntile + nbat + 1 + 4 * rk_plan_tiles(seg_off_host, nseg);
 }
 
 CHOCO_API int64_t choco_topk_segmented_plan(const int64_t* seg_off_host, int32_t nseg, double ratio,
@@ -674,13 +680,56 @@ CHOCO_API int64_t choco_topk_segmented_plan(const int64_t* seg_off_host, int32_t
   if (plan_host) {
     plan_host[6] = ntile;
     plan_host[7] = nbat;
+    // the random-k tile table (randk.hip): [R] then R x {segment, tile, first tile, tiles}
+    int64_t* rk = plan_host + (int64_t)kRow * nseg + ntile + nbat;
+    int64_t r = 0;
+    for (int s = 0; s < nseg; ++s) {
+      const int64_t nt = randk_tiles(seg_off_host[s + 1] - seg_off_host[s]);
+      for (int64_t t = 0; t < nt; ++t) {
+        int64_t* e = rk + 1 + 4 * (r + t);
+        e[0] = s; e[1] = t; e[2] = r; e[3] = nt;
+      }
+      r += nt;
+    }
+    rk[0] = r;
   }
   return out;
 }
 
+static int64_t rk_base_of(const int64_t* plan_host, int32_t nseg) {
+  return (int64_t)kRow * nseg + plan_tiles(plan_host) + plan_batched(plan_host);
+}
+
 CHOCO_API size_t choco_topk_segmented_workspace_size(const int64_t* plan_host, int32_t nseg) {
   if (!plan_host || nseg <= 0) return 256;
-  return seg_layout(nseg, plan_tiles(plan_host)).total + pipeline_ws(plan_host, nseg) + 256;
+  return seg_layout(nseg, plan_tiles(plan_host)).total + pipeline_ws(plan_host, nseg) +
+         randk_counts_bytes(plan_host[rk_base_of(plan_host, nseg)]) + 256;
+}
+
+// Per-segment random-k (randk.hip): the counts buffer follows the top-k regions.
+static int randk_segmented_call(const float* x, const float* xhat, const int64_t* plan_dev, const int64_t* plan_host,
+                                int32_t nseg, uint64_t seed, uint64_t offset, int32_t is_biased, float* out_val,
+                                int32_t* out_idx, void* ws, size_t ws_bytes, hipStream_t st,
+                                Gossip gs = Gossip{nullptr, 0.f}) {
+  CHOCO_REQUIRE(x && plan_dev && plan_host && out_val && out_idx && nseg > 0, "null pointer argument");
+  CHOCO_REQUIRE(aligned4(x) && (xhat == nullptr || aligned4(xhat)), "x/xhat must be 4-byte aligned");
+  const int64_t* last = plan_host + (int64_t)kRow * (nseg - 1);
+  const int64_t n = last[0] + last[1];
+  CHOCO_REQUIRE(n < (int64_t)INT32_MAX, "total length must be < 2^31");
+  const int64_t rk_base = rk_base_of(plan_host, nseg);
+  const int64_t R = plan_host[rk_base];
+  const size_t off = seg_layout(nseg, plan_tiles(plan_host)).total + pipeline_ws(plan_host, nseg);
+  CHOCO_REQUIRE(ws != nullptr && ws_bytes >= off + randk_counts_bytes(R),
+                "segmented random-k workspace too small: need %zu bytes, got %zu", off + randk_counts_bytes(R),
+                ws_bytes);
+  if (gs.mem) {
+    // random-k reads only k elements: no full pass to fuse the consensus step into
+    CHOCO_REQUIRE(xhat != nullptr && aligned4(gs.mem), "the gossip step needs x_hat and a 4-byte aligned memory");
+    const int rc = gossip_launch(const_cast<float*>(x), gs.mem, xhat, gs.gamma, n, st);
+    if (rc) return rc;
+  }
+  return randk_launch(x, xhat, plan_dev, rk_base, R, n, 0, seed, offset, is_biased, out_val, out_idx,
+                      static_cast<char*>(ws) + off, ws_bytes - off, st);
 }
 
 CHOCO_API int choco_topk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
@@ -691,11 +740,11 @@ CHOCO_API int choco_topk_compress_segmented(const float* x, const float* xhat, c
 }
 
 CHOCO_API int choco_randk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
-                                             const int64_t* plan_host, int32_t nseg, uint64_t seed,
+                                             const int64_t* plan_host, int32_t nseg, uint64_t seed, uint64_t offset,
                                              int32_t is_biased, float* out_val, int32_t* out_idx, void* ws,
                                              size_t ws_bytes, void* stream) {
-  return segmented<kHash>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, ws, ws_bytes,
-                          as_stream(stream));
+  return randk_segmented_call(x, xhat, plan_dev, plan_host, nseg, seed, offset, is_biased, out_val, out_idx, ws,
+                              ws_bytes, as_stream(stream));
 }
 
 CHOCO_API int choco_gossip_topk_compress_segmented(float* x, const float* memory, const float* xhat, float gamma,
@@ -709,9 +758,10 @@ CHOCO_API int choco_gossip_topk_compress_segmented(float* x, const float* memory
 
 CHOCO_API int choco_gossip_randk_compress_segmented(float* x, const float* memory, const float* xhat, float gamma,
                                                     const int64_t* plan_dev, const int64_t* plan_host, int32_t nseg,
-                                                    uint64_t seed, int32_t is_biased, float* out_val,
-                                                    int32_t* out_idx, void* ws, size_t ws_bytes, void* stream) {
+                                                    uint64_t seed, uint64_t offset, int32_t is_biased,
+                                                    float* out_val, int32_t* out_idx, void* ws, size_t ws_bytes,
+                                                    void* stream) {
   CHOCO_REQUIRE(memory != nullptr && xhat != nullptr, "the gossip step needs memory and x_hat");
-  return segmented<kHash>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, ws, ws_bytes,
-                          as_stream(stream), Gossip{memory, gamma});
+  return randk_segmented_call(x, xhat, plan_dev, plan_host, nseg, seed, offset, is_biased, out_val, out_idx, ws,
+                              ws_bytes, as_stream(stream), Gossip{memory, gamma});
 }

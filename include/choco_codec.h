@@ -113,15 +113,26 @@ int choco_topk_compress_segmented(const float* x, const float* xhat, const int64
 
 /* ------------------------------------------------------------- random-k
  * Replaces SparsificationCompressor.get_random_k (sparsification.py:40-54).
- * The reference draws indices on the host with numpy's legacy RandomState;
- * here k distinct indices are drawn on the device, uniformly without
- * replacement, as the k highest values of a seeded bijective 32-bit hash of
- * the index (ties -> lowest index).  Output in ascending index order.
- * is_biased = 0 scales values by (float)(n / k) like the reference's
- * unbiased branch (sparsification.py:54). */
+ * The reference draws np.random.choice(n, k, replace=False) on the host (legacy
+ * RandomState); here a uniform k-subset of [0, n) is drawn on the device, and
+ * only the k selected elements are read (randk.hip):
+ *   derive(K, i) = splitmix64_mix(K + (i + 1) * 0x9E3779B97F4A7C15);
+ *   K = derive(key, 0), key = splitmix64_mix(seed + (offset + 1) * 0xD1B54A32D192ED03);
+ *   pi_N(j; K): on B bits (2^B >= N, h = (B + 1) / 2), four rounds of
+ *     x = (x + a_r) & mask; x = (x * m_r) & mask; x ^= x >> h,
+ *     a_r = (u32)derive(K, 2r) & mask, m_r = ((u32)derive(K, 2r + 1) | 1) & mask,
+ *     repeated while x >= N (cycle walking: a bijection of [0, N));
+ *   tiles of 2^18 elements; tile t holds c_t = #{ j < k : pi_n(j; K) >> 18 == t }
+ *     of the selected indices (one tile: c_0 = k; k >= n: every index);
+ *   its positions are pi_{L_t}(j; derive(K, 8 + t)), j < c_t (L_t = the tile length).
+ * Output in ascending index order.  `offset` selects an independent stream for the
+ * same seed (e.g. the step number).  is_biased = 0 scales values by
+ * (float)(n / k) like the reference's unbiased branch (sparsification.py:54).
+ * Workspace: choco_randk_workspace_size(n) (zero-filled once; see the top-k
+ * workspace rules; choco_topk_workspace_reset also resets it). */
 size_t choco_randk_workspace_size(int64_t n);
 int choco_randk_compress(const float* x, const float* xhat, int64_t n, int64_t k,
-                         uint64_t seed, int32_t is_biased,
+                         uint64_t seed, uint64_t offset, int32_t is_biased,
                          float* out_val, int32_t* out_idx,
                          void* ws, size_t ws_bytes, void* stream);
 
@@ -132,14 +143,13 @@ int choco_gather(const float* x, const float* xhat, const int64_t* idx, int64_t 
 
 /* Per-segment random-k (CHOCOSparsificationCompressor.compress with
  * comm_op "random_k", parallel_choco_v.py:229-260 -> sparsification.py:40-54 per
- * tensor): the plan of choco_topk_segmented_plan (k_s = max(1, int(len_s*(1-ratio)))),
- * segment s ranked by the hash with seed seg_seed(seed, s) (splitmix64 of
- * seed + (s+1) * 0x9E3779B97F4A7C15), outputs concatenated in segment order with
- * GLOBAL indices.  Any 4-byte alignment; workspace:
- * choco_topk_segmented_workspace_size. */
+ * tensor): the plan of choco_topk_segmented_plan (k_s = max(1, int(len_s*(1-ratio))),
+ * which also carries the random-k tile table), segment s drawn as above with
+ * K_s = derive(key, s), outputs concatenated in segment order with GLOBAL
+ * indices.  Any 4-byte alignment; workspace: choco_topk_segmented_workspace_size. */
 int choco_randk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
                                    const int64_t* plan_host, int32_t nseg,
-                                   uint64_t seed, int32_t is_biased,
+                                   uint64_t seed, uint64_t offset, int32_t is_biased,
                                    float* out_val, int32_t* out_idx,
                                    void* ws, size_t ws_bytes, void* stream);
 
@@ -293,7 +303,7 @@ int choco_gossip_topk_compress_segmented(float* x, const float* memory, const fl
                                          void* ws, size_t ws_bytes, void* stream);
 int choco_gossip_randk_compress_segmented(float* x, const float* memory, const float* xhat, float gamma,
                                           const int64_t* plan_dev, const int64_t* plan_host, int32_t nseg,
-                                          uint64_t seed, int32_t is_biased,
+                                          uint64_t seed, uint64_t offset, int32_t is_biased,
                                           float* out_val, int32_t* out_idx,
                                           void* ws, size_t ws_bytes, void* stream);
 int choco_gossip_sign_compress(float* x, const float* memory, const float* xhat, float gamma,

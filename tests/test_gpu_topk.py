@@ -256,9 +256,11 @@ def test_randk_segmented_vs_oracle(layout, is_biased):
     assert same_bits(host(vals), ov)
 
 
-@pytest.mark.parametrize("n", [1000, 65536, 100003, 2_000_003])
+@pytest.mark.parametrize("n", [1, 2, 1000, 65536, 100003, 262144, 262145, 2_000_003])
 @pytest.mark.parametrize("seed", [1, 2 ** 40 + 3])
 def test_randk_matches_sampler_oracle(n, seed):
+    """The direct sampler (csrc/randk.hip) against its restatement: single- and multi-tile
+    (2^18) draws, exact tile edges."""
     from chocosgd_amd import codec
     x = randn(n, 3)
     k = codec.topk_k(n, 0.95)
@@ -397,3 +399,49 @@ def test_topk_status_word_clean_after_calls():
     from chocosgd_amd import codec
     _check_topk(randn(2_000_003, 460), codec.topk_k(2_000_003, 0.99))
     codec.check_topk_status(wait=True)
+
+
+@pytest.mark.parametrize("case", ["offsets", "k1", "all", "xhat_unaligned"])
+def test_randk_sampler_cases(case):
+    """(seed, offset) streams, k = 1, k = n (every index), and x - xhat on an unaligned view."""
+    from chocosgd_amd import codec
+    n = 1_000_003
+    if case == "offsets":
+        x = randn(n, 31)
+        k = codec.topk_k(n, 0.99)
+        seen = []
+        for off in (0, 1, 2):
+            vals, idx = codec.randk(x, k, 77, offset=off)
+            oi = O.randk_indices(n, k, 77, off)
+            assert np.array_equal(host(idx).astype(np.int64), oi)
+            assert same_bits(host(vals), host(x)[oi])
+            seen.append(oi)
+        assert not np.array_equal(seen[0], seen[1])
+    elif case in ("k1", "all"):
+        x = randn(n, 32)
+        k = 1 if case == "k1" else n
+        vals, idx = codec.randk(x, k, 5, is_biased=False)
+        oi = O.randk_indices(n, k, 5)
+        assert np.array_equal(host(idx).astype(np.int64), oi)
+        assert same_bits(host(vals), O.gather(host(x), oi, n, k, is_biased=False))
+    else:
+        base, bh = randn(n + 3, 33), randn(n + 3, 34)
+        x, xh = base[3:], bh[1:n + 1]
+        k = codec.topk_k(n, 0.9)
+        vals, idx = codec.randk(x, k, 6, xhat=xh)
+        oi = O.randk_indices(n, k, 6)
+        assert np.array_equal(host(idx).astype(np.int64), oi)
+        assert same_bits(host(vals), (host(x) - host(xh))[oi])
+
+
+@pytest.mark.slow
+def test_randk_100M_bench_shape():
+    """BASELINE cfg-4 shape (100M, k = 1M): 382 tiles, the count pass and the per-tile draws."""
+    from chocosgd_amd import codec
+    n = 100_000_000
+    x = randn(n, 1000)
+    k = codec.topk_k(n, 0.99)
+    vals, idx = codec.randk(x, k, 12345, offset=3)
+    oi = O.randk_indices(n, k, 12345, 3)
+    assert np.array_equal(host(idx).astype(np.int64), oi)
+    assert same_bits(host(vals), host(x)[oi])

@@ -421,10 +421,49 @@ def test_randk_indices_distinct_and_uniformish():
     counts = np.zeros(n)
     for seed in range(40):
         idx = O.randk_indices(n, k, seed)
-        assert idx.size == k and np.unique(idx).size == k
+        assert idx.size == k and np.unique(idx).size == k and np.all(np.diff(idx) > 0)
         counts[idx] += 1
     # each index selected ~ 40 * 0.1 = 4 times on average
     assert 3.0 < counts.mean() < 5.0 and counts.max() < 20
+    # (seed, offset) streams are distinct
+    assert not np.array_equal(O.randk_indices(n, k, 7, 0), O.randk_indices(n, k, 7, 1))
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 5, 17, 1000, 65537, 262144, 300001])
+def test_randk_permutation_is_a_bijection(N):
+    """pi_N (csrc/randk.hip RkPerm) maps [0, N) onto [0, N) for every key."""
+    for K in (0, 1, 0xDEADBEEF12345678):
+        y = O.rk_perm(np.arange(N), N, K)
+        assert np.array_equal(np.sort(y), np.arange(N))
+
+
+def test_randk_multi_tile_counts_hypergeometric():
+    """Over tiles of 2^18, the per-tile counts of a multi-tile draw follow the
+    multivariate hypergeometric law of a uniform k-subset (mean k L_t / N, variance
+    k p (1 - p) (N - k) / (N - 1)); every index distinct, ascending, in range."""
+    N, k = 1_000_003, 30_000
+    T = 1 << O.RK_TILE_BITS
+    nt = (N + T - 1) // T
+    lens = np.array([min(T, N - t * T) for t in range(nt)], dtype=np.float64)
+    cs = []
+    for seed in range(60):
+        idx = O.randk_indices(N, k, seed)
+        assert idx.size == k and np.unique(idx).size == k and idx[0] >= 0 and idx[-1] < N
+        cs.append(np.bincount(idx // T, minlength=nt))
+    cs = np.array(cs, dtype=np.float64)
+    p = lens / N
+    mean, var = k * p, k * p * (1 - p) * (N - k) / (N - 1)
+    assert np.all(np.abs(cs.mean(0) - mean) < 5 * np.sqrt(var / len(cs)))
+    assert np.all(np.abs(cs.var(0) / var - 1) < 0.6)
+
+
+def test_randk_all_and_tiny():
+    assert np.array_equal(O.randk_indices(5, 5, 3), np.arange(5))
+    assert np.array_equal(O.randk_indices(600_000, 600_000, 3), np.arange(600_000))
+    i = O.randk_indices(1, 1, 9)
+    assert i.tolist() == [0]
+    i = O.randk_indices(700_001, 1, 9)
+    assert i.size == 1 and 0 <= i[0] < 700_001
 
 
 def test_oracle_sampled_helpers_agree_with_full_forms():
@@ -455,7 +494,8 @@ def test_oracle_segmented_randk():
     for s, (m, k) in enumerate(zip(lens, ks)):
         part = i[sum(ks[:s]):sum(ks[:s + 1])]
         assert np.all(np.diff(part) > 0) and part[0] >= off and part[-1] < off + m
-        assert np.array_equal(part - off, O.randk_indices(m, k, O.seg_seed(42, s)))
+        assert np.array_equal(part - off, O.randk_segment_indices(m, k, O.rk_derive(O.randk_key(42), s)))
         off += m
     assert same_bits(v, d[i])
-    assert O.seg_seed(42, 0) != O.seg_seed(42, 1) and O.seg_seed(42, 0) < 2 ** 64
+    # the flat draw is segment 0 of the same key
+    assert np.array_equal(O.randk_indices(1000, 100, 42), O.randk_segment_indices(1000, 100, O.rk_derive(O.randk_key(42), 0)))
