@@ -8,10 +8,12 @@ Deliberate differences (all documented in DESIGN.md):
     order is implementation-defined, sparsification.py:28-30); the selected SET is
     identical for tie-free inputs; ties at the k-th magnitude go to the lowest
     index (what the reference's k == 1 path, torch.max, does).
-  * random-k indices are drawn on the device from a seeded hash ranking instead of
-    the host's numpy RandomState (sparsification.py:48); the seed is taken from
-    torch's default generator, so torch.manual_seed makes runs reproducible.
-  * QSGD uniforms come from an in-kernel SplitMix64 counter stream instead of
+  * random-k indices are a uniform k-subset drawn on the device (a seeded bijection
+    gives the per-tile counts and the in-tile positions, include/choco_codec.h)
+    instead of the host's numpy RandomState (sparsification.py:48); the seed is taken
+    from torch's default generator, so torch.manual_seed makes runs reproducible.
+  * QSGD uniforms come from in-kernel xoroshiro128+ streams (seeded by SplitMix64,
+    include/choco_codec.h) instead of
     torch.rand_like (sparsification.py:91); norms are fp64-accumulated (the
     reference's fp32 CPU norm drifts by up to 1e-2 relative at 1e8 elements).
 """

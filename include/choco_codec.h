@@ -90,7 +90,7 @@ int choco_topk_compress(const float* x, const float* xhat, int64_t n, int64_t k,
  * segment order, indices GLOBAL (segment offset added in integer arithmetic --
  * the reference adds it in fp32, sparsification.py:76).  Every segment of up to
  * 16M elements is cut into 16K-element tiles and ALL of them are selected in the
- * same four launches (topk_seg.hip); longer segments run the flat pipeline.
+ * same five launches (topk_seg.hip); longer segments run the flat pipeline.
  * choco_topk_segmented_plan fills a HOST int64 plan of
  * choco_topk_segmented_plan_len(seg_off, nseg) entries from the HOST table
  * seg_off[nseg+1]: nseg rows of 8 {off, len, k_s, out_off, first tile, tiles, ., .}
@@ -235,10 +235,16 @@ int choco_sign_local_decode(const float* x, int64_t n, const int64_t* seg_off, i
  *   norm_s  = ||d_s||_2 (fp64 accumulation, rounded once)   or norm_in[s] if given
  *   lf      = ((float)s * |d|) / norm_s
  *   level   = floor(lf) + (u < lf - floor(lf)),  u = u_in[e] if given, else
- *             this codec's SplitMix64 counter stream: key = mix(seed + (offset+1) *
- *             0xD1B54A32D192ED03), z = mix(key + (e/2 + 1) * 0x9E3779B97F4A7C15),
- *             u = (even e: z >> 40, odd e: (z >> 8) & 0xFFFFFF) * 2^-24
- *             (the reference draws torch.rand_like, sparsification.py:91)
+ *             this codec's stream (the reference draws torch.rand_like,
+ *             sparsification.py:91): key = splitmix64_mix(seed + (offset+1) *
+ *             0xD1B54A32D192ED03); element e belongs to stream
+ *             sid = ((e >> 13) << 8) | ((e & 8191) >> 3 & 255) at position
+ *             p = ((e & 8191) >> 11) * 8 + (e & 7); stream sid is xoroshiro128+
+ *             (a=24, b=16, c=37) started from (splitmix64_mix(z),
+ *             splitmix64_mix(z + 0x9E3779B97F4A7C15)), z = key + (2 sid + 1) *
+ *             0x9E3779B97F4A7C15; its output number p / 2, r = s0 + s1, gives
+ *             u = (even p: r >> 40, odd p: (r >> 16) & 0xFFFFFF) * 2^-24
+ *             (restated in oracle/choco_oracle.py qsgd_uniforms_at)
  * Wire format (packed, choco_qsgd_packed_bytes): level plane (container of
  * cw = 1,2,4,8,16 bits >= q, little-endian within 32-bit words) followed by a
  * sign plane (1 bit/element, bit set <=> d < 0), both padded to 16 bytes.

@@ -104,7 +104,7 @@ def test_choco_sign_api_close():
 
 def test_choco_qsgd_api_consistent():
     """Device uniforms differ from torch.rand_like, so compare with the oracle driven by the
-    same Philox stream: re-decode every message and re-accumulate on the host."""
+    same device uniform stream: re-decode every message and re-accumulate on the host."""
     g = golden("choco_qsgd_mini_q4")
     sb, nhp, s = run_choco(g, "quantize_qsgd", q=4)
     assert sb["n_bits"] == float(g["n_bits"])

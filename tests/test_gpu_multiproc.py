@@ -39,6 +39,24 @@ def test_choco_round_across_processes(comm_op, world, tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_mp_choco_worker.py"), comm_op, str(world),
                         str(tmp_path)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
+    _verify_round(comm_op, world, tmp_path)
+
+
+@pytest.mark.parametrize("comm_op,world", [("compress_top_k", 2), ("sign", 2), ("quantize_qsgd", 2)])
+def test_parallel_choco_sync_process_ipc(comm_op, world, tmp_path):
+    """ParallelCHOCO's process variant (parallel_choco.py:64-87,95-187): each trainer hands
+    its CUDA x / x_hat / memory to a spawned sync process over torch.multiprocessing IPC;
+    the sync processes run CHOCOCompressor.pipeline over gloo (comm_device="cpu") on the
+    shared tensors; the trainers' own tensors then hold the oracle's x_hat / memory
+    (tests/_mp_ipc_worker.py)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_mp_ipc_worker.py"), comm_op, str(world),
+                        str(tmp_path)], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    _verify_round(comm_op, world, tmp_path)
+
+
+def _verify_round(comm_op, world, tmp_path):
     lens, nseg = W.LENS, len(W.LENS)
     n = sum(lens)
     ins = [W.inputs(q) for q in range(world)]
