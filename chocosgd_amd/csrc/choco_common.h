@@ -355,6 +355,8 @@ int topk_pipeline(int mode, const float* x, const float* xh, int64_t n, int64_t 
                   Gossip gs = Gossip{nullptr, 0.f}, uint32_t* status = nullptr);
 // forget the warm-start records of the top-k workspaces in [ws, ws + bytes) (include/choco_codec.h)
 void topk_warm_forget(const void* ws, size_t bytes);
+void seg_forget(const void* ws, size_t bytes);  // ... of the segmented workspaces (topk_seg.hip)
+bool topk_warm_enabled();                        // choco_topk_set_warm_start
 
 // random-k (randk.hip): tiles of a segment, the counts buffer, the two launches
 // (plan_dev == nullptr: the flat call over [0, n) with k; else the segmented plan's

@@ -1,10 +1,10 @@
-// Batched per-tensor (segmented) top-k / random-k on MI355X.
+// Batched per-tensor (segmented) top-k on MI355X.
 //
 // Replaces the per-parameter-tensor loop of CHOCOSparsificationCompressor.compress
 // (reference dl_code/pcode/optim/parallel_choco_v.py:229-260), which calls
-// SparsificationCompressor.get_top_k / get_random_k (sparsification.py:18-54)
-// once per tensor of the layout that create_optimizer.py:15-24 defines (one
-// parameter per group: 65 tensors for ResNet-20, 161 for ResNet-50).
+// SparsificationCompressor.get_top_k (sparsification.py:18-31) once per tensor of
+// the layout that create_optimizer.py:15-24 defines (one parameter per group: 65
+// tensors for ResNet-20, 161 for ResNet-50).  (Per-segment random-k: randk.hip.)
 //
 // Per segment s the answer is the exact selection of the flat path (topk.hip):
 //   T_s = k_s-th largest key, out = {key > T_s} U {the lowest-index ties at T_s},
@@ -12,34 +12,41 @@
 //
 // Every segment of up to kSegMaxTiles tiles (16M elements) is cut into tiles of
 // kSegTile = 16384 elements; ALL tiles of ALL such segments run in the same
-// launches (a 2,048-element BN vector and a 2.4M-element conv weight alike),
-// four of them per call:
-//   S1 seg_hist     (tile)   : 2048-bin histogram of key >> 20 (sign-free
-//                              exponent + 3 mantissa bits) -> hist1[s].
-//   S2 seg_collect  (tile)   : every tile finds its segment's coarse bin b1 of
-//                              the k-th key from hist1[s] (same data, same
-//                              answer), re-reads its tile (an Infinity-Cache hit
-//                              when the layout fits 256 MB) and compacts the
-//                              candidates (key >= b1 << 20) in index order into
-//                              its own slot range; keys in bin b1 feed a
-//                              histogram of bits 19..9 -> hist2[s].
-//   S3a seg_fine    (tile)   : bin b2 of the k-th key from hist2[s]; bits 8..0
-//                              of the tile's candidates in fine bin (b1, b2) ->
-//                              hist3[s].
-//   S3b seg_count   (tile)   : exact T_s and tie quota r_s from hist3[s]; the
-//                              tile's counts (> T_s, == T_s).
-//   S4 seg_emit     (tile)   : offset and tie share from the counts of the
-//                              segment's earlier tiles, then the ordered
-//                              compaction of the tile's candidates (key > T_s,
-//                              plus its share of ties) to the output.
-// Every launch is tile-parallel; each histogram is reset by the first tile of
-// its segment in the launch after its last reader.
-// Two passes over the input (the first from HBM, the second usually from the
-// Infinity Cache) instead of one workgroup per segment doing four.  Segments
-// over 16M elements take the flat multi-workgroup pipeline (topk.hip).
+// launches.  Two sequences, chosen per call on the host (a workspace's first call
+// is cold, later calls warm; include/choco_codec.h "warm start"):
+//
+// COLD (five launches, two reads of the input):
+//   S1 seg_hist     : 2048-bin histogram of key >> 20 -> hist1[s].
+//   S2 seg_collect  : coarse bin b1 of the k_s-th key from hist1[s]; candidates
+//                     key >= b1 << 20 compacted in index order into the tile's
+//                     slots; keys in bin b1 -> hist2[s] (bits 19..9).
+//   S3a seg_fine    : bin b2 of the k_s-th key from hist2[s]; bits 8..0 of the
+//                     tile's candidates in bin (b1, b2) -> hist3[s].
+//   S3b seg_count   : T_s and the tie quota from hist3[s]; the tile's (#> T_s,
+//                     #== T_s); tile 0 of the segment writes the NEXT call's window.
+//   S4 seg_emit     : offset and tie share from the segment's earlier tiles, then
+//                     the ordered compaction of the tile's candidates.
+// WARM (four launches, ONE read): each segment carries a window [lo_s, lo_s +
+// 2048 << sh_s) from the previous call (around that call's T_s, margins at
+// k_s (1 +- m_s) keys), so
+//   W2 seg_collect  : candidates key >= lo_s, compacted; their window bin
+//                     min((key - lo_s) >> sh_s, 2047) -> hist2[s]  (no S1);
+//   S3a / S3b / S4  : as above with (window bin, low sh_s bits) in place of
+//                     (b2, bits 8..0).  A segment whose T_s is not inside its
+//                     window (fewer than k_s candidates, or T_s in the clamped
+//                     top bin) is flagged in S3a and selected exactly by ONE
+//                     workgroup in S4 (slow, correct), which also re-centres its
+//                     window; k_s >= len_s segments take every element.
+// Every histogram is reset by the first tile of its segment in the launch after
+// its last reader.  Segments over 16M elements take the flat pipeline (topk.hip),
+// each in its own workspace (its own warm window).
 #include "choco_common.h"
+#include "select.h"
 
+#include <math.h>
 #include <algorithm>
+#include <mutex>
+#include <unordered_map>
 
 namespace choco {
 
@@ -50,12 +57,14 @@ constexpr int kSegMaxTiles = 1024;                    // tiles per batched segme
 constexpr int64_t kSegBatchMax = (int64_t)kSegTile * kSegMaxTiles;
 constexpr int kRow = 8;                               // plan row width (int64)
 constexpr int kH = 2048;                              // histogram bins (S1, S2)
+constexpr uint32_t kWinShMax = 9;                     // warm window bin <= 2^9 keys (hist3: 512 bins)
 static_assert(kSegRows * 4 * kSegThreads == kSegTile, "tile geometry");
 
 // plan (host + device copies, int64):
 //   rows[nseg][8] = {off, len, k, out_off, t0, ntile, 0, 0}; row 0 also carries
 //   [6] = total tiles, [7] = batched segments;
-//   then tile -> segment map [total tiles]; then batched segment ids [batched].
+//   then tile -> segment map [total tiles]; then batched segment ids [batched];
+//   then the random-k tile table (randk.hip).
 struct SegRow {
   int64_t off, len, k, out_off, t0, ntile;
 };
@@ -64,14 +73,23 @@ CHOCO_DEV SegRow seg_row(const int64_t* __restrict__ plan, int s) {
   return SegRow{p[0], p[1], p[2], p[3], p[4], p[5]};
 }
 
+// A segment's warm window: candidates key >= lo, bins of 2^sh keys.
+struct SegWin {
+  uint32_t lo, sh, valid, pad;
+};
+
+// info[8 s + i]: 0 b1 (cold), 1 rank inside b1 (cold), 2 T, 3 bin of the k-th key
+// (S3a), 4 rank inside that bin, 5 ties at T to take, 6 mode (0 select, 1 window
+// missed: exact fallback in S4, 2 take every element)
 struct SegWs {
   uint32_t *hist1, *hist2, *hist3, *info, *tilecnt, *tcount;
   float* cval;
   uint32_t* cidx;
+  SegWin* win;
 };
 
 struct SegLayout {
-  size_t off_h1, off_h2, off_h3, off_info, off_cnt, off_out, off_cval, off_cidx, total;
+  size_t off_h1, off_h2, off_h3, off_info, off_cnt, off_out, off_cval, off_cidx, off_win, total;
 };
 
 static SegLayout seg_layout(int nseg, int64_t ntile) {
@@ -85,6 +103,7 @@ static SegLayout seg_layout(int nseg, int64_t ntile) {
   L.off_out = o;  o += align_up((size_t)ntile * 8, 256);
   L.off_cval = o; o += align_up((size_t)ntile * kSegTile * 4, 256);
   L.off_cidx = o; o += align_up((size_t)ntile * kSegTile * 4, 256);
+  L.off_win = o;  o += align_up((size_t)nseg * sizeof(SegWin), 256);
   L.total = o;
   return L;
 }
@@ -129,9 +148,12 @@ CHOCO_DEV void tile_load(const float* __restrict__ x, const float* __restrict__ 
   }
 }
 
-// S1 with the fused gossip step: x, memory and xh of the tile in flight
-// together, x_new = x + gamma (memory - xh) stored back (the buffer resources
-// end at the tile: nothing past it is read or written), v = x_new - xh.
+// The first read with the fused gossip step: x, memory and xh of the tile in
+// flight together, x_new = x + gamma (memory - xh) stored back (the buffer
+// resources end at the tile: nothing past it is read or written), v = x_new - xh.
+// NT: the cold sequence re-reads x_new and xh in S2 (keep them in the Infinity
+// Cache); the warm one reads them once.
+template <bool NT>
 CHOCO_DEV void tile_load_gossip(const float* __restrict__ x, const float* __restrict__ xh, const Gossip& gs,
                                 const TileCtx& c, float (&v)[kSegRows][4]) {
   const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x + c.start, (uint32_t)c.tl * 4u);
@@ -143,24 +165,18 @@ CHOCO_DEV void tile_load_gossip(const float* __restrict__ x, const float* __rest
     const uint32_t off = (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u;
     a[r] = ld_buf4<true>(rx, off);
     m[r] = ld_buf4<true>(rm, off);
-    h[r] = ld_buf4<false>(rh, off);  // S2 re-reads xh (and x_new): keep them in the Infinity Cache
+    h[r] = ld_buf4<NT>(rh, off);
   }
 #pragma unroll
   for (int r = 0; r < kSegRows; ++r) {
     const uint32_t off = (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u;
     const float4 xn = gossip4(a[r], m[r], h[r], gs.gamma);
-    st_buf4<false>(rx, off, xn);
+    st_buf4<NT>(rx, off, xn);
     v[r][0] = xn.x - h[r].x; v[r][1] = xn.y - h[r].y; v[r][2] = xn.z - h[r].z; v[r][3] = xn.w - h[r].w;
   }
 }
 
 CHOCO_DEV int tile_elem(int r, int q) { return r * 4 * kSegThreads + 4 * (int)threadIdx.x + q; }
-
-template <int MODE>
-CHOCO_DEV uint32_t tile_key(const TileCtx& c, uint64_t sseed, int e, float v) {
-  if (MODE == kHash) return rank_hash(sseed, (uint32_t)(c.start - c.R.off + e)) >> 1;
-  return fkey(v);
-}
 
 // Over hist[kH] in LDS or global memory (ascending key order), the bin holding
 // the rank-th largest entry and the rank inside it -> out[0], out[1].  Two bins
@@ -178,39 +194,38 @@ CHOCO_DEV void block_find_rank2k(uint32_t h0, uint32_t h1, uint32_t rank, uint32
   __syncthreads();
 }
 
-// ---------------------------------------------------------------- S1: coarse histogram
+// ---------------------------------------------------------------- S1: coarse histogram (cold)
 #ifndef CHOCO_S1_COPIES
 #define CHOCO_S1_COPIES 1
 #endif
 #ifndef CHOCO_S1_LANEC
 #define CHOCO_S1_LANEC 1
 #endif
-template <int MODE, bool XH, bool GS = false>
+template <bool XH, bool GS = false>
 __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ xh,
                                                                const int64_t* __restrict__ plan, int nseg,
-                                                               uint64_t seed, uint32_t* __restrict__ hist1,
-                                                               Gossip gs) {
-  static_assert(!GS || (MODE == kData && XH), "the gossip step needs x_hat and data keys");
+                                                               uint32_t* __restrict__ hist1, Gossip gs) {
+  static_assert(!GS || XH, "the gossip step needs x_hat");
   // histogram copies: wave w -> copy w % NC (CHOCO_S1_COPIES), or lane l -> copy
   // l % NC (CHOCO_S1_LANEC: same-bin lanes of ONE atomic instruction split over copies)
   constexpr int NC = CHOCO_S1_LANEC > 1 ? CHOCO_S1_LANEC : CHOCO_S1_COPIES;
   __shared__ uint32_t h[NC][kH];
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
   float v[kSegRows][4] = {};
-  if (GS) tile_load_gossip(x, xh, gs, c, v);
-  else if (MODE == kData) tile_load<XH>(x, xh, c, v);
+  if (GS) tile_load_gossip<false>(x, xh, gs, c, v);
+  else if (c.R.ntile == 1) return;  // a single-tile segment is selected in S2 (no histogram)
+  else tile_load<XH>(x, xh, c, v);
+  if (c.R.ntile == 1) return;  // (GS: its consensus step is applied; S2 selects it)
   for (int i = threadIdx.x; i < NC * kH; i += kSegThreads) (&h[0][0])[i] = 0u;
   __syncthreads();
-  const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
   uint32_t* __restrict__ hw = h[CHOCO_S1_LANEC > 1 ? lane_id() % NC : (threadIdx.x >> 6) % NC];
 #pragma unroll
   for (int r = 0; r < kSegRows; ++r)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = tile_elem(r, q);
-      const uint32_t key = tile_key<MODE>(c, sseed, e, v[r][q]);
-      if (e < c.tl) atomicAdd(&hw[key >> 20], 1u);
+      if (e < c.tl) atomicAdd(&hw[fkey(v[r][q]) >> 20], 1u);
     }
   __syncthreads();
   uint32_t* __restrict__ g = hist1 + (int64_t)c.s * kH;
@@ -222,12 +237,127 @@ __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __re
   }
 }
 
-// ---------------------------------------------------------------- S2: coarse select + candidates
-template <int MODE, bool XH>
-__global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
+// ---------------------------------------------------------------- single-tile segments
+// A segment of at most one tile (the many small tensors of a CNN layout: BN scales and
+// biases, small convs) is selected EXACTLY by the workgroup that holds it, in S2, from
+// its registers: a three-digit radix select (bits 30..20, 19..9, 8..0) in the LDS
+// histogram, then the ordered compaction (ties at T by index).  No window, no S3/S4
+// work: their k-th key moves by many ranks from call to call, so a warm window would
+// miss often.  Exclusive ranks of the set bits of `bits` in row-major order (row r,
+// wave, lane, element q) -> base[r] (+ popc of the lane's lower bits); two barriers.
+CHOCO_DEV void tile_ranks(const uint32_t (&bits)[kSegRows], uint32_t (&base)[kSegRows], uint32_t* rc_cnt,
+                          uint32_t* total) {
+  constexpr int kW = kSegThreads / 64;
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+#pragma unroll
+  for (int r = 0; r < kSegRows; ++r) {
+    const uint32_t cnt = (uint32_t)__popc(bits[r]);
+    const uint32_t inc = wave_incl_scan(cnt);
+    base[r] = inc - cnt;
+    if (lane == 63) rc_cnt[r * kW + w] = inc;
+  }
+  __syncthreads();
+  if (w == 0) {
+    const uint32_t cv = rc_cnt[lane];
+    const uint32_t inc = wave_incl_scan(cv);
+    rc_cnt[lane] = inc - cv;
+    if (lane == 63) rc_cnt[kSegRows * kW] = inc;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kSegRows; ++r) base[r] += rc_cnt[r * kW + w];
+  *total = rc_cnt[kSegRows * kW];
+  __syncthreads();  // rc_cnt is reused
+}
+
+CHOCO_DEV void seg_exact_tile(const float (&v)[kSegRows][4], const TileCtx& c, uint32_t* h, uint32_t* scratch,
+                              uint32_t* bc, uint32_t* rc_cnt, float* __restrict__ out_val,
+                              int32_t* __restrict__ out_idx) {
+  const int tid = threadIdx.x;
+  const uint32_t k = (uint32_t)c.R.k;
+  uint32_t key[kSegRows][4];
+#pragma unroll
+  for (int r = 0; r < kSegRows; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) key[r][q] = fkey(v[r][q]);
+  const bool all = k >= (uint32_t)c.tl;
+  uint32_t prefix = 0, maskhi = 0, krem = k;
+  if (!all) {
+    const int shs[3] = {20, 9, 0};
+    const uint32_t dms[3] = {2047u, 2047u, 511u};
+#pragma unroll
+    for (int rd = 0; rd < 3; ++rd) {
+      for (int i = tid; i < kH; i += kSegThreads) h[i] = 0u;
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < kSegRows; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (tile_elem(r, q) < c.tl && (key[r][q] & maskhi) == prefix)
+            atomicAdd(&h[(key[r][q] >> shs[rd]) & dms[rd]], 1u);
+      __syncthreads();
+      block_find_rank2k(h[2 * tid], h[2 * tid + 1], krem, scratch, bc);
+      prefix |= bc[0] << shs[rd];
+      maskhi |= dms[rd] << shs[rd];
+      krem = bc[1];
+      __syncthreads();  // bc is rewritten by the next round
+    }
+  }
+  const uint32_t T = prefix, r_take = krem;  // the k-th key and the ties at it to take
+  uint32_t eqb[kSegRows], selb[kSegRows], base[kSegRows], tot;
+#pragma unroll
+  for (int r = 0; r < kSegRows; ++r) {
+    eqb[r] = 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      eqb[r] |= (!all && tile_elem(r, q) < c.tl && key[r][q] == T) ? (1u << q) : 0u;
+  }
+  tile_ranks(eqb, base, rc_cnt, &tot);  // tie ranks in index order
+#pragma unroll
+  for (int r = 0; r < kSegRows; ++r) {
+    selb[r] = 0u;
+    uint32_t tr = base[r];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool in = tile_elem(r, q) < c.tl;
+      const bool eq = (eqb[r] >> q) & 1u;
+      selb[r] |= (in && (all || key[r][q] > T || (eq && tr < r_take))) ? (1u << q) : 0u;
+      tr += eq ? 1u : 0u;
+    }
+  }
+  tile_ranks(selb, base, rc_cnt, &tot);
+  float* __restrict__ ov = out_val + c.R.out_off;
+  int32_t* __restrict__ oi = out_idx + c.R.out_off;
+#pragma unroll
+  for (int r = 0; r < kSegRows; ++r) {
+    uint32_t pos = base[r];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if ((selb[r] >> q) & 1u) {
+        if (pos < k) {  // (bounded)
+          ov[pos] = v[r][q];
+          oi[pos] = (int32_t)(c.start + tile_elem(r, q));
+        }
+        ++pos;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- S2 / W2: candidates
+// Cold: the floor is the coarse bin b1 of the k_s-th key (from hist1), keys of bin b1
+// feed hist2 by bits 19..9.  Warm: the floor is the window's lo, every candidate
+// feeds hist2 by its window bin min((key - lo) >> sh, 2047); GS: the fused gossip
+// step happens here (the one read).
+// (8 waves per SIMD = two workgroups per CU: <= 64 VGPRs; one per CU measured ~10 us
+// slower at ResNet-50)
+template <bool XH, bool WARM, bool GS = false>
+__global__ __launch_bounds__(kSegThreads, 8) void seg_collect_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ plan, int nseg,
-    uint64_t seed, const uint32_t* __restrict__ hist1, uint32_t* __restrict__ hist2, uint32_t* __restrict__ info,
-    uint32_t* __restrict__ tilecnt, float* __restrict__ cval, uint32_t* __restrict__ cidx) {
+    const uint32_t* __restrict__ hist1, uint32_t* __restrict__ hist2, uint32_t* __restrict__ info,
+    uint32_t* __restrict__ tilecnt, float* __restrict__ cval, uint32_t* __restrict__ cidx,
+    const SegWin* __restrict__ win, Gossip gs, float* __restrict__ out_val, int32_t* __restrict__ out_idx) {
+  static_assert(!GS || (XH && WARM), "the gossip step is fused into S2 on the warm path only (S1 on the cold)");
   __shared__ uint32_t h2[kH];
   __shared__ uint32_t scratch[40];
   __shared__ uint32_t bc[4];
@@ -236,18 +366,32 @@ __global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
   const int tid = threadIdx.x;
   float v[kSegRows][4] = {};
-  if (MODE == kData) tile_load<XH>(x, xh, c, v);  // in flight while b1 is found
-  const uint32_t* __restrict__ g1 = hist1 + (int64_t)c.s * kH;
-  const uint32_t c0 = g1[2 * tid], c1 = g1[2 * tid + 1];
-  for (int i = tid; i < kH; i += kSegThreads) h2[i] = 0u;
-  block_find_rank2k(c0, c1, (uint32_t)c.R.k, scratch, bc);
-  const uint32_t b1 = bc[0], kb = bc[1];
-  if (c.j == 0 && tid == 0) {
-    info[8 * c.s + 0] = b1;
-    info[8 * c.s + 1] = kb;
+  if (GS) tile_load_gossip<true>(x, xh, gs, c, v);  // in flight while the floor is found
+  else tile_load<XH>(x, xh, c, v);
+  if (c.R.ntile == 1) {  // workgroup-uniform: the whole segment is here
+    seg_exact_tile(v, c, h2, scratch, bc, rc_cnt, out_val, out_idx);
+    return;
   }
-  const uint32_t floor_key = b1 << 20;
-  const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
+  for (int i = tid; i < kH; i += kSegThreads) h2[i] = 0u;
+  uint32_t floor_key, b1 = 0, sh = 0;
+  if (WARM) {
+    const SegWin w = win[c.s];
+    // no window (never expected after a cold call): no candidates -> S3a flags the miss
+    floor_key = w.valid ? w.lo : 0xFFFFFFFFu;
+    sh = w.valid ? min(w.sh, kWinShMax) : 0u;
+    if (c.R.k >= c.R.len) floor_key = 0u;  // every element
+    __syncthreads();
+  } else {
+    const uint32_t* __restrict__ g1 = hist1 + (int64_t)c.s * kH;
+    const uint32_t c0 = g1[2 * tid], c1 = g1[2 * tid + 1];
+    block_find_rank2k(c0, c1, (uint32_t)c.R.k, scratch, bc);
+    b1 = bc[0];
+    if (c.j == 0 && tid == 0) {
+      info[8 * c.s + 0] = b1;
+      info[8 * c.s + 1] = bc[1];
+    }
+    floor_key = b1 << 20;
+  }
   // candidate flags of all rows, then ONE scan of the (row, wave) counts places
   // them in index order (row-major: row r, wave w, lane, element)
   constexpr int kW = kSegThreads / 64;
@@ -260,10 +404,14 @@ __global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = tile_elem(r, q);
-      const uint32_t key = tile_key<MODE>(c, sseed, e, v[r][q]);
+      const uint32_t key = fkey(v[r][q]);
       const bool cand = e < c.tl && key >= floor_key;
       cm[r] |= cand ? (1u << q) : 0u;
-      if (cand && (key >> 20) == b1) atomicAdd(&h2[(key >> 9) & (kH - 1)], 1u);
+      if (WARM) {
+        if (cand) atomicAdd(&h2[min((key - floor_key) >> sh, (uint32_t)(kH - 1))], 1u);
+      } else {
+        if (cand && (key >> 20) == b1) atomicAdd(&h2[(key >> 9) & (kH - 1)], 1u);
+      }
     }
     const uint32_t cnt = (uint32_t)__popc(cm[r]);
     const uint32_t inc = wave_incl_scan(cnt);
@@ -285,9 +433,7 @@ __global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
     for (int q = 0; q < 4; ++q) {
       if (cm[r] & (1u << q)) {
         const int e = tile_elem(r, q);
-        float val = v[r][q];
-        if (MODE == kHash) val = XH ? x[c.start + e] - xh[c.start + e] : x[c.start + e];
-        cval[c.slot + pos] = val;
+        cval[c.slot + pos] = v[r][q];
         cidx[c.slot + pos] = (uint32_t)(c.start + e);
         ++pos;
       }
@@ -305,19 +451,22 @@ __global__ __launch_bounds__(kSegThreads) void seg_collect_kernel(
 // (a 2.4M-element conv weight: ~50K candidates walked by 16 waves, a dependent
 // load per step).  Both kernels use 256-thread workgroups; every tile derives
 // its segment's bins from the complete global histograms of the previous launch.
-//   S3a seg_fine : bin b2 (bits 19..9) of the k-th key from hist2[s]; bits 8..0
-//                  of this tile's candidates in fine bin (b1, b2) -> hist3[s].
-//   S3b seg_count: T_s from hist3[s]; this tile's (#key > T_s, #key == T_s).
+//   S3a seg_fine : bin of the k-th key from hist2[s]; the low bits of this tile's
+//                  candidates in that bin -> hist3[s].
+//   S3b seg_count: T_s from hist3[s]; this tile's (#key > T_s, #key == T_s);
+//                  tile 0: the next call's window.
 // S4 then places each tile from the counts of the tiles before it.
 #ifndef CHOCO_S3_THREADS
 #define CHOCO_S3_THREADS 256
 #endif
 constexpr int kS3Threads = CHOCO_S3_THREADS;
-constexpr int kH3 = 512;  // bits 8..0
+constexpr int kH3 = 512;  // bits 8..0 (cold) / the low sh <= 9 bits of a window bin (warm)
+enum SegMode { kSegSelect = 0, kSegMissed = 1, kSegAll = 2 };
 
 // Over hist[nb] in global memory (ascending key order), the bin holding the
-// rank-th largest entry and the rank inside it -> out[0], out[1]; PER bins per
-// thread of a kS3Threads workgroup.  Ends with a barrier.
+// rank-th largest entry and the rank inside it -> out[0], out[1], and the
+// histogram total -> out[2]; PER bins per thread of a kS3Threads workgroup.
+// Ends with a barrier.
 template <int PER>
 CHOCO_DEV void block_find_rank_g(const uint32_t* __restrict__ hist, uint32_t rank, uint32_t* scratch, uint32_t* out) {
   const int tid = threadIdx.x;
@@ -331,6 +480,7 @@ CHOCO_DEV void block_find_rank_g(const uint32_t* __restrict__ hist, uint32_t ran
   uint32_t total;
   const uint32_t pre = block_excl_scan(local, scratch, &total);
   const uint32_t above = total - pre - local;  // entries in bins above mine
+  if (tid == 0) out[2] = total;
   if (above < rank && rank <= above + local) {
     uint32_t acc = above;
 #pragma unroll
@@ -342,49 +492,64 @@ CHOCO_DEV void block_find_rank_g(const uint32_t* __restrict__ hist, uint32_t ran
   __syncthreads();
 }
 
-template <int MODE>
-CHOCO_DEV uint32_t cand_key(const float* __restrict__ cval, const uint32_t* __restrict__ cidx, int64_t slot,
-                            uint64_t sseed, int64_t seg_off) {
-  return MODE == kHash ? (rank_hash(sseed, cidx[slot] - (uint32_t)seg_off) >> 1) : fkey(cval[slot]);
-}
-
-template <int MODE>
+template <bool WARM>
 __global__ __launch_bounds__(kS3Threads) void seg_fine_kernel(
-    const int64_t* __restrict__ plan, int nseg, uint64_t seed, uint32_t* __restrict__ hist1,
-    const uint32_t* __restrict__ hist2, uint32_t* __restrict__ hist3, uint32_t* __restrict__ info,
-    const uint32_t* __restrict__ tilecnt, const float* __restrict__ cval, const uint32_t* __restrict__ cidx) {
+    const int64_t* __restrict__ plan, int nseg, uint32_t* __restrict__ hist1, const uint32_t* __restrict__ hist2,
+    uint32_t* __restrict__ hist3, uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt,
+    const float* __restrict__ cval, const SegWin* __restrict__ win) {
   __shared__ uint32_t h3[kH3];
   __shared__ uint32_t scratch[40];
   __shared__ uint32_t bc[4];
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+  if (c.R.ntile == 1) return;  // selected in S2
   const int tid = threadIdx.x;
   const uint32_t cnt = tilecnt[blockIdx.x];
-  const uint32_t b1 = info[8 * c.s + 0], kb = info[8 * c.s + 1];
   for (int i = tid; i < kH3; i += kS3Threads) h3[i] = 0u;
-  block_find_rank_g<kH / kS3Threads>(hist2 + (int64_t)c.s * kH, kb, scratch, bc);
+  if (tid < 4) bc[tid] = 0u;
+  __syncthreads();
+  uint32_t lo = 0, sh = 0, b1 = 0;
+  uint32_t rank;
+  if (WARM) {
+    const SegWin w = win[c.s];
+    lo = w.lo;
+    sh = min(w.sh, kWinShMax);
+    rank = (uint32_t)c.R.k;
+  } else {
+    b1 = info[8 * c.s + 0];
+    rank = info[8 * c.s + 1];
+  }
+  block_find_rank_g<kH / kS3Threads>(hist2 + (int64_t)c.s * kH, rank, scratch, bc);
   const uint32_t b2 = bc[0];
+  uint32_t mode = kSegSelect;
+  if (WARM) {
+    if (c.R.k >= c.R.len) mode = kSegAll;
+    else if (bc[2] < rank || b2 == (uint32_t)(kH - 1)) mode = kSegMissed;  // T below the window or in its clamped top
+  }
   if (c.j == 0 && tid == 0) {
     info[8 * c.s + 3] = b2;
-    info[8 * c.s + 4] = bc[1];  // rank of the k-th key inside fine bin (b1, b2)
+    info[8 * c.s + 4] = bc[1];  // rank of the k-th key inside that bin
+    info[8 * c.s + 6] = mode;
   }
-  if (c.j == 0) {  // every tile of the segment read hist1 in S2: reset it for the next call
+  if (!WARM && c.j == 0) {  // every tile of the segment read hist1 in S2: reset it for the next call
     uint32_t* __restrict__ g1 = hist1 + (int64_t)c.s * kH;
     for (int i = tid; i < kH; i += kS3Threads) g1[i] = 0u;
   }
-  const uint32_t P9 = (b1 << 11) | b2;  // key >> 9 of the fine bin
-  const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
+  if (mode != kSegSelect) return;  // workgroup-uniform
+  const uint32_t fmask = WARM ? (1u << sh) - 1u : (uint32_t)(kH3 - 1);
   constexpr int U = 4;
   for (uint32_t i0 = 0; i0 < cnt; i0 += U * kS3Threads) {  // workgroup-uniform
     uint32_t key[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + u * kS3Threads + tid;
-      key[u] = i < cnt ? cand_key<MODE>(cval, cidx, c.slot + i, sseed, c.R.off) : 0u;
+      key[u] = i < cnt ? fkey(cval[c.slot + i]) : 0u;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + u * kS3Threads + tid;
-      if (i < cnt && (key[u] >> 9) == P9) atomicAdd(&h3[key[u] & (kH3 - 1)], 1u);
+      const bool in = WARM ? (key[u] - lo) >> sh == b2 : key[u] >> 9 == ((b1 << 11) | b2);
+      const uint32_t f = WARM ? (key[u] - lo) & fmask : key[u] & fmask;
+      if (i < cnt && in) atomicAdd(&h3[f], 1u);
     }
   }
   __syncthreads();
@@ -393,43 +558,116 @@ __global__ __launch_bounds__(kS3Threads) void seg_fine_kernel(
     if (h3[i]) atomicAdd(&g3[i], h3[i]);
 }
 
-template <int MODE>
+// Next call's window of one segment (S3b, tile 0; every thread of the workgroup):
+// over hist[kH] of bins of 2^shb keys from `base`, with `above` keys above the
+// range, the keys at count levels k + delta and k - delta (delta = 0.03 k +
+// 4 sqrt(k) + 8: the k-th key of a small segment moves by many ranks from one
+// call to the next), bin-rounded outward; a window wider than 2048 << kWinShMax
+// keys is centred on T instead.
+CHOCO_DEV void seg_next_window(const uint32_t* __restrict__ hist, uint32_t base, uint32_t shb, uint32_t above,
+                               uint32_t k, uint32_t T, SegWin* __restrict__ out, uint32_t* scratch) {
+  constexpr int PER = kH / kS3Threads;
+  const int tid = threadIdx.x;
+  const uint64_t delta = (uint64_t)(0.03 * (double)k + 4.0 * sqrt((double)k)) + 8u;
+  const uint64_t lo_t = (uint64_t)k + delta, hi_t = (uint64_t)k > delta ? (uint64_t)k - delta : 0u;
+  uint32_t hv[PER], local = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    hv[j] = hist[tid * PER + j];
+    local += hv[j];
+  }
+  uint32_t total;
+  const uint32_t pre = block_excl_scan(local, scratch, &total);
+  // C(j) = #keys >= base + (j << shb) = above + total - (keys in bins below j)
+  uint32_t nlo = 0, nhi = 0, below = pre;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint64_t C = (uint64_t)above + total - below;
+    nlo += C >= lo_t ? 1u : 0u;
+    nhi += C > hi_t ? 1u : 0u;
+    below += hv[j];
+  }
+  uint32_t tlo, thi;
+  block_excl_scan2(nlo, nhi, scratch, &tlo, &thi, &nlo, &nhi);  // (totals in nlo, nhi)
+  if (tid == 0) {
+    uint64_t x_lo = (uint64_t)base + ((uint64_t)(nlo ? nlo - 1u : 0u) << shb);
+    uint64_t x_hi = (uint64_t)base + ((uint64_t)nhi << shb);
+    uint32_t sh = 0;
+    while (((uint64_t)kH << sh) < x_hi - x_lo && sh < kWinShMax) ++sh;
+    if (((uint64_t)kH << sh) < x_hi - x_lo) {  // too wide for the finest bins: centre on T
+      sh = kWinShMax;
+      x_lo = T > (1u << 18) ? (uint64_t)T - (1u << 18) : 0u;
+    }
+    out->lo = (uint32_t)x_lo;
+    out->sh = sh;
+    out->valid = 1u;
+  }
+}
+
+template <bool WARM>
 __global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
-    const int64_t* __restrict__ plan, int nseg, uint64_t seed, uint32_t* __restrict__ hist2,
-    const uint32_t* __restrict__ hist3, uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt,
-    const float* __restrict__ cval, const uint32_t* __restrict__ cidx, uint32_t* __restrict__ tcount) {
+    const int64_t* __restrict__ plan, int nseg, uint32_t* __restrict__ hist2, const uint32_t* __restrict__ hist3,
+    uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt, const float* __restrict__ cval,
+    uint32_t* __restrict__ tcount, SegWin* __restrict__ win) {
   __shared__ uint32_t scratch[40];
   __shared__ uint32_t bc[4];
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+  if (c.R.ntile == 1) return;  // selected in S2
   const int tid = threadIdx.x;
   const uint32_t cnt = tilecnt[blockIdx.x];
-  const uint32_t b1 = info[8 * c.s + 0], b2 = info[8 * c.s + 3], kc = info[8 * c.s + 4];
-  block_find_rank_g<kH3 / kS3Threads>(hist3 + (int64_t)c.s * kH3, kc, scratch, bc);
-  const uint32_t T = (b1 << 20) | (b2 << 9) | bc[0];
+  const uint32_t mode = WARM ? info[8 * c.s + 6] : (uint32_t)kSegSelect;
+  const uint32_t b2 = info[8 * c.s + 3], kc = info[8 * c.s + 4];
+  SegWin w{0u, 9u, 0u, 0u};
+  uint32_t b1 = 0;
+  if (WARM) {
+    w = win[c.s];
+    w.sh = min(w.sh, kWinShMax);
+  } else {
+    b1 = info[8 * c.s + 0];
+  }
+  uint32_t T = 0;
+  if (mode == kSegSelect) {  // workgroup-uniform
+    block_find_rank_g<kH3 / kS3Threads>(hist3 + (int64_t)c.s * kH3, kc, scratch, bc);
+    T = WARM ? w.lo + (b2 << w.sh) + bc[0] : ((b1 << 20) | (b2 << 9) | bc[0]);
+  }
   if (c.j == 0) {
-    if (tid == 0) {
+    if (tid == 0 && mode == kSegSelect) {
       info[8 * c.s + 2] = T;
       info[8 * c.s + 5] = bc[1];  // ties at T to take (>= 1)
     }
     uint32_t* __restrict__ g2 = hist2 + (int64_t)c.s * kH;  // read by every tile in S3a
+    if (mode == kSegSelect) {
+      // the next call's window, from this call's hist2 (cold: bits 19..9 inside b1,
+      // with the keys of the bins above b1; warm: the window's own bins)
+      const uint32_t base = WARM ? w.lo : (b1 << 20);
+      const uint32_t shb = WARM ? w.sh : 9u;
+      const uint32_t above = WARM ? 0u : (uint32_t)c.R.k - info[8 * c.s + 1];
+      seg_next_window(g2, base, shb, above, (uint32_t)c.R.k, T, &win[c.s], scratch);
+      __syncthreads();
+    } else if (mode == kSegAll && tid == 0) {
+      win[c.s] = SegWin{0u, kWinShMax, 1u, 0u};
+    }
     for (int i = tid; i < kH; i += kS3Threads) g2[i] = 0u;
   }
-  const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
-  constexpr int U = 4;
   uint32_t gt = 0, eq = 0;
-  for (uint32_t i0 = 0; i0 < cnt; i0 += U * kS3Threads) {  // workgroup-uniform
-    uint32_t key[U];
+  if (mode == kSegSelect) {
+    constexpr int U = 4;
+    for (uint32_t i0 = 0; i0 < cnt; i0 += U * kS3Threads) {  // workgroup-uniform
+      uint32_t key[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t i = i0 + u * kS3Threads + tid;
-      key[u] = i < cnt ? cand_key<MODE>(cval, cidx, c.slot + i, sseed, c.R.off) : 0u;
-    }
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = i0 + u * kS3Threads + tid;
+        key[u] = i < cnt ? fkey(cval[c.slot + i]) : 0u;
+      }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t i = i0 + u * kS3Threads + tid;
-      gt += (i < cnt && key[u] > T) ? 1u : 0u;
-      eq += (i < cnt && key[u] == T) ? 1u : 0u;
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = i0 + u * kS3Threads + tid;
+        gt += (i < cnt && key[u] > T) ? 1u : 0u;
+        eq += (i < cnt && key[u] == T) ? 1u : 0u;
+      }
     }
+  } else if (mode == kSegAll) {
+    gt = tid == 0 ? cnt : 0u;
   }
   uint32_t g0, e0, gtot, etot;
   block_excl_scan2(gt, eq, scratch, &g0, &e0, &gtot, &etot);
@@ -444,24 +682,42 @@ __global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
 // earlier tiles (<= kSegMaxTiles - 1: kS4Per per thread), then the ordered
 // compaction of its candidates (a few hundred at k = 1 %: one or two rounds).
 // Latency-bound like S3: 256-thread workgroups (cheaper block scans, more
-// workgroups resident); CHOCO_S4_THREADS=1024 is the previous form.
+// workgroups resident).  A warm segment whose window missed: tile 0 selects the
+// whole segment exactly (select.h; the segment's candidates were not all kept)
+// and re-centres the window on its T.
 #ifndef CHOCO_S4_THREADS
 #define CHOCO_S4_THREADS 256
 #endif
 constexpr int kS4Threads = CHOCO_S4_THREADS;
 constexpr int kS4Per = kSegMaxTiles / kS4Threads;
 static_assert(kS4Per * kS4Threads == kSegMaxTiles, "S4 tile-count geometry");
-template <int MODE>
+template <bool WARM, bool XH>
 __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
-    const int64_t* __restrict__ plan, int nseg, uint64_t seed, int32_t is_biased, const uint32_t* __restrict__ info,
-    const uint32_t* __restrict__ tilecnt, const uint32_t* __restrict__ tcount, uint32_t* __restrict__ hist3,
-    const float* __restrict__ cval, const uint32_t* __restrict__ cidx, float* __restrict__ out_val,
-    int32_t* __restrict__ out_idx) {
+    const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ plan, int nseg,
+    const uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt, const uint32_t* __restrict__ tcount,
+    uint32_t* __restrict__ hist3, const float* __restrict__ cval, const uint32_t* __restrict__ cidx,
+    float* __restrict__ out_val, int32_t* __restrict__ out_idx, SegWin* __restrict__ win) {
   __shared__ uint32_t scratch[40];
+  __shared__ ExactSmem es;
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+  if (c.R.ntile == 1) return;  // selected in S2
   const int tid = threadIdx.x;
-  const uint64_t sseed = MODE == kHash ? seg_seed(seed, c.s) : 0;
-  const uint32_t T = info[8 * c.s + 2], r = info[8 * c.s + 5];
+  if (c.j == 0) {  // every tile of the segment read hist3 in S3b: reset it for the next call
+    uint32_t* __restrict__ g3 = hist3 + (int64_t)c.s * kH3;
+    for (int i = tid; i < kH3; i += kS4Threads) g3[i] = 0u;
+  }
+  const uint32_t mode = WARM ? info[8 * c.s + 6] : (uint32_t)kSegSelect;
+  if (mode == kSegMissed) {  // workgroup-uniform
+    if (c.j != 0) return;
+    Src<kData, XH> src{x + c.R.off, XH ? xh + c.R.off : nullptr, 0};
+    block_select_T(src, c.R.len, c.R.k, es);
+    const uint32_t T = es.bc[0], r = es.bc[1], ties = es.bc[2];
+    __syncthreads();
+    block_emit(src, c.R.len, T, r, ties, 1.0f, out_val + c.R.out_off, out_idx + c.R.out_off, c.R.off, es);
+    if (tid == 0) win[c.s] = SegWin{T > (1u << 18) ? T - (1u << 18) : 0u, kWinShMax, 1u, 0u};
+    return;
+  }
+  const uint32_t T = info[8 * c.s + 2], r = mode == kSegAll ? 0u : info[8 * c.s + 5];
   const uint32_t cnt = tilecnt[blockIdx.x];
   const uint32_t ev = tcount[2 * blockIdx.x + 1];
   uint32_t o, quota;
@@ -481,22 +737,18 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
     o = gsum + taken;
     quota = min(ev, r - taken);
   }
-  if (c.j == 0) {  // every tile of the segment read hist3 in S3b: reset it for the next call
-    uint32_t* __restrict__ g3 = hist3 + (int64_t)c.s * kH3;
-    for (int i = tid; i < kH3; i += kS4Threads) g3[i] = 0u;
-  }
   const bool all_ties = quota == ev;
-  const float scale = (MODE == kHash && !is_biased) ? (float)((double)c.R.len / (double)c.R.k) : 1.0f;
   float* __restrict__ ov = out_val + c.R.out_off + o;
   int32_t* __restrict__ oi = out_idx + c.R.out_off + o;
+  const uint32_t room = (uint32_t)c.R.k - min(o, (uint32_t)c.R.k);  // (bounded: never past the segment's k)
   uint32_t run = 0, tie_run = 0;
   for (uint32_t p0 = 0; p0 < cnt; p0 += kS4Threads) {  // workgroup-uniform
     const uint32_t p = p0 + tid;
     const bool valid = p < cnt;
     const float v = valid ? cval[c.slot + p] : 0.f;
     const uint32_t ix = valid ? cidx[c.slot + p] : 0u;
-    const uint32_t key = MODE == kHash ? (rank_hash(sseed, ix - (uint32_t)c.R.off) >> 1) : fkey(v);
-    const bool gt = valid && key > T, eq = valid && key == T;
+    const uint32_t key = fkey(v);
+    const bool gt = valid && (mode == kSegAll || key > T), eq = valid && mode != kSegAll && key == T;
     bool sel;
     if (all_ties || quota == 0u) {
       sel = gt || (eq && all_ties);
@@ -508,8 +760,8 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
     }
     uint32_t nsel;
     const uint32_t pos = run + block_excl_scan(sel ? 1u : 0u, scratch, &nsel);
-    if (sel) {
-      ov[pos] = v * scale;
+    if (sel && pos < room) {
+      ov[pos] = v;
       oi[pos] = (int32_t)ix;
     }
     run += nsel;
@@ -520,34 +772,76 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
 static int64_t plan_tiles(const int64_t* plan_host) { return plan_host[6]; }
 static int64_t plan_batched(const int64_t* plan_host) { return plan_host[7]; }
 
-template <int MODE, bool XH, bool GS = false>
+// warm bookkeeping: per segmented workspace, whether an earlier call left windows
+static std::mutex g_seg_mu;
+static std::unordered_map<const void*, uint64_t> g_seg_calls;
+static bool seg_claim_warm(const void* ws) {
+  std::lock_guard<std::mutex> g(g_seg_mu);
+  auto it = g_seg_calls.find(ws);
+  if (it == g_seg_calls.end()) {
+    g_seg_calls.emplace(ws, 1u);
+    return false;
+  }
+  ++it->second;
+  return topk_warm_enabled();
+}
+void seg_forget(const void* ws, size_t bytes) {
+  std::lock_guard<std::mutex> g(g_seg_mu);
+  const char* lo = static_cast<const char*>(ws);
+  for (auto it = g_seg_calls.begin(); it != g_seg_calls.end();) {
+    const char* p = static_cast<const char*>(it->first);
+    if (p == lo || (p > lo && p < lo + bytes)) it = g_seg_calls.erase(it);
+    else ++it;
+  }
+}
+
+template <bool XH, bool GS>
 static int launch_batched(const float* x, const float* xh, const int64_t* plan_dev, const int64_t* plan_host,
-                          int nseg, uint64_t seed, int32_t is_biased, float* out_val, int32_t* out_idx,
-                          const SegWs& W, hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}) {
+                          int nseg, float* out_val, int32_t* out_idx, const SegWs& W, bool warm, hipStream_t st,
+                          Gossip gs) {
   const unsigned ntile = (unsigned)plan_tiles(plan_host);
-  profile_begin("topk_seg_hist", st);
-  CHOCO_KLAUNCH((seg_hist_kernel<MODE, XH, GS>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg, seed,
-                W.hist1, gs);
-  profile_end("topk_seg_hist", st);
-  CHOCO_LAUNCHED("seg_hist_kernel");
-  profile_begin("topk_seg_collect", st);
-  CHOCO_KLAUNCH((seg_collect_kernel<MODE, XH>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg, seed,
-                W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx);
+  if (!warm) {
+    profile_begin("topk_seg_hist", st);
+    CHOCO_KLAUNCH((seg_hist_kernel<XH, GS>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg, W.hist1,
+                  gs);
+    profile_end("topk_seg_hist", st);
+    CHOCO_LAUNCHED("seg_hist_kernel");
+    profile_begin("topk_seg_collect", st);
+    CHOCO_KLAUNCH((seg_collect_kernel<XH, false, false>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev,
+                  nseg, W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.win, Gossip{nullptr, 0.f}, out_val,
+                  out_idx);
+  } else {
+    profile_begin("topk_seg_collect", st);
+    CHOCO_KLAUNCH((seg_collect_kernel<XH, true, GS>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg,
+                  W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.win, gs, out_val, out_idx);
+  }
   profile_end("topk_seg_collect", st);
   CHOCO_LAUNCHED("seg_collect_kernel");
   profile_begin("topk_seg_fine", st);
-  CHOCO_KLAUNCH((seg_fine_kernel<MODE>), dim3(ntile), dim3(kS3Threads), 0, st, plan_dev, nseg, seed, W.hist1,
-                W.hist2, W.hist3, W.info, W.tilecnt, W.cval, W.cidx);
+  if (warm)
+    CHOCO_KLAUNCH((seg_fine_kernel<true>), dim3(ntile), dim3(kS3Threads), 0, st, plan_dev, nseg, W.hist1, W.hist2,
+                  W.hist3, W.info, W.tilecnt, W.cval, W.win);
+  else
+    CHOCO_KLAUNCH((seg_fine_kernel<false>), dim3(ntile), dim3(kS3Threads), 0, st, plan_dev, nseg, W.hist1, W.hist2,
+                  W.hist3, W.info, W.tilecnt, W.cval, W.win);
   profile_end("topk_seg_fine", st);
   CHOCO_LAUNCHED("seg_fine_kernel");
   profile_begin("topk_seg_count", st);
-  CHOCO_KLAUNCH((seg_count_kernel<MODE>), dim3(ntile), dim3(kS3Threads), 0, st, plan_dev, nseg, seed, W.hist2,
-                W.hist3, W.info, W.tilecnt, W.cval, W.cidx, W.tcount);
+  if (warm)
+    CHOCO_KLAUNCH((seg_count_kernel<true>), dim3(ntile), dim3(kS3Threads), 0, st, plan_dev, nseg, W.hist2, W.hist3,
+                  W.info, W.tilecnt, W.cval, W.tcount, W.win);
+  else
+    CHOCO_KLAUNCH((seg_count_kernel<false>), dim3(ntile), dim3(kS3Threads), 0, st, plan_dev, nseg, W.hist2, W.hist3,
+                  W.info, W.tilecnt, W.cval, W.tcount, W.win);
   profile_end("topk_seg_count", st);
   CHOCO_LAUNCHED("seg_count_kernel");
   profile_begin("topk_seg_emit", st);
-  CHOCO_KLAUNCH((seg_emit_kernel<MODE>), dim3(ntile), dim3(kS4Threads), 0, st, plan_dev, nseg, seed, is_biased,
-                W.info, W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx);
+  if (warm)
+    CHOCO_KLAUNCH((seg_emit_kernel<true, XH>), dim3(ntile), dim3(kS4Threads), 0, st, x, xh, plan_dev, nseg, W.info,
+                  W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win);
+  else
+    CHOCO_KLAUNCH((seg_emit_kernel<false, XH>), dim3(ntile), dim3(kS4Threads), 0, st, x, xh, plan_dev, nseg, W.info,
+                  W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win);
   profile_end("topk_seg_emit", st);
   CHOCO_LAUNCHED("seg_emit_kernel");
   return CHOCO_OK;
@@ -564,25 +858,16 @@ static size_t pipeline_ws(const int64_t* plan_host, int nseg) {
   return need;
 }
 
-// gs.mem != nullptr: the fused gossip step (top-k: inside S1 and the flat
-// pipeline's stream; random-k, which reads only k elements: the standalone step
-// over the whole buffer first).
-template <int MODE>
+// gs.mem != nullptr: the fused gossip step (cold: inside S1; warm: inside S2; the
+// flat pipeline: inside its stream).
 static int segmented(const float* x, const float* xhat, const int64_t* plan_dev, const int64_t* plan_host,
-                     int32_t nseg, uint64_t seed, int32_t is_biased, float* out_val, int32_t* out_idx, void* ws,
-                     size_t ws_bytes, hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}) {
+                     int32_t nseg, float* out_val, int32_t* out_idx, void* ws, size_t ws_bytes, hipStream_t st,
+                     Gossip gs = Gossip{nullptr, 0.f}) {
   CHOCO_REQUIRE(x && plan_dev && plan_host && out_val && out_idx && nseg > 0, "null pointer argument");
   CHOCO_REQUIRE(aligned4(x) && (xhat == nullptr || aligned4(xhat)), "x/xhat must be 4-byte aligned");
   const int64_t* last = plan_host + (int64_t)kRow * (nseg - 1);
   CHOCO_REQUIRE(last[0] + last[1] < (int64_t)INT32_MAX, "total length must be < 2^31");
-  if (gs.mem) {
-    CHOCO_REQUIRE(xhat != nullptr && aligned4(gs.mem), "the gossip step needs x_hat and a 4-byte aligned memory");
-    if (MODE == kHash) {
-      const int rc = gossip_launch(const_cast<float*>(x), gs.mem, xhat, gs.gamma, last[0] + last[1], st);
-      if (rc) return rc;
-      gs.mem = nullptr;
-    }
-  }
+  if (gs.mem) CHOCO_REQUIRE(xhat != nullptr && aligned4(gs.mem), "the gossip step needs x_hat and a 4-byte aligned memory");
   const int64_t ntile = plan_tiles(plan_host);
   const SegLayout L = seg_layout(nseg, ntile);
   const size_t need = L.total + pipeline_ws(plan_host, nseg);
@@ -594,15 +879,15 @@ static int segmented(const float* x, const float* xhat, const int64_t* plan_dev,
             reinterpret_cast<uint32_t*>(base + L.off_h3),
             reinterpret_cast<uint32_t*>(base + L.off_info), reinterpret_cast<uint32_t*>(base + L.off_cnt),
             reinterpret_cast<uint32_t*>(base + L.off_out), reinterpret_cast<float*>(base + L.off_cval),
-            reinterpret_cast<uint32_t*>(base + L.off_cidx)};
+            reinterpret_cast<uint32_t*>(base + L.off_cidx), reinterpret_cast<SegWin*>(base + L.off_win)};
+    const bool warm = seg_claim_warm(base + L.off_win);
     int rc;
-    if (MODE == kData && gs.mem)
-      rc = launch_batched<kData, true, true>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, W,
-                                             st, gs);
+    if (gs.mem)
+      rc = launch_batched<true, true>(x, xhat, plan_dev, plan_host, nseg, out_val, out_idx, W, warm, st, gs);
     else if (xhat)
-      rc = launch_batched<MODE, true>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, W, st);
+      rc = launch_batched<true, false>(x, xhat, plan_dev, plan_host, nseg, out_val, out_idx, W, warm, st, gs);
     else
-      rc = launch_batched<MODE, false>(x, xhat, plan_dev, plan_host, nseg, seed, is_biased, out_val, out_idx, W, st);
+      rc = launch_batched<false, false>(x, xhat, plan_dev, plan_host, nseg, out_val, out_idx, W, warm, st, gs);
     if (rc) return rc;
   }
   // segments over kSegBatchMax elements: the flat pipeline, one after another, each
@@ -612,11 +897,9 @@ static int segmented(const float* x, const float* xhat, const int64_t* plan_dev,
   for (int s = 0; s < nseg; ++s) {
     const int64_t* p = plan_host + (int64_t)kRow * s;
     if (p[5] != 0) continue;
-    const uint64_t sd = MODE == kHash ? seg_seed(seed, s) : 0;
-    const float scale = (MODE == kHash && !is_biased) ? (float)((double)p[1] / (double)p[2]) : 1.0f;
     const Gossip gseg{gs.mem ? gs.mem + p[0] : nullptr, gs.gamma};
     const size_t fb = align_up(topk_ws_bytes(p[1]), 256);
-    const int rc = topk_pipeline(MODE, x + p[0], xhat ? xhat + p[0] : nullptr, p[1], p[2], sd, scale,
+    const int rc = topk_pipeline(kData, x + p[0], xhat ? xhat + p[0] : nullptr, p[1], p[2], 0, 1.0f,
                                  out_val + p[3], out_idx + p[3], p[0], base + fo, fb, st, gseg,
                                  reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_STATUS_OFFSET));
     if (rc) return rc;
@@ -735,8 +1018,7 @@ static int randk_segmented_call(const float* x, const float* xhat, const int64_t
 CHOCO_API int choco_topk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
                                             const int64_t* plan_host, int32_t nseg, float* out_val,
                                             int32_t* out_idx, void* ws, size_t ws_bytes, void* stream) {
-  return segmented<kData>(x, xhat, plan_dev, plan_host, nseg, 0, 1, out_val, out_idx, ws, ws_bytes,
-                          as_stream(stream));
+  return segmented(x, xhat, plan_dev, plan_host, nseg, out_val, out_idx, ws, ws_bytes, as_stream(stream));
 }
 
 CHOCO_API int choco_randk_compress_segmented(const float* x, const float* xhat, const int64_t* plan_dev,
@@ -752,8 +1034,8 @@ CHOCO_API int choco_gossip_topk_compress_segmented(float* x, const float* memory
                                                    float* out_val, int32_t* out_idx, void* ws, size_t ws_bytes,
                                                    void* stream) {
   CHOCO_REQUIRE(memory != nullptr && xhat != nullptr, "the gossip step needs memory and x_hat");
-  return segmented<kData>(x, xhat, plan_dev, plan_host, nseg, 0, 1, out_val, out_idx, ws, ws_bytes,
-                          as_stream(stream), Gossip{memory, gamma});
+  return segmented(x, xhat, plan_dev, plan_host, nseg, out_val, out_idx, ws, ws_bytes, as_stream(stream),
+                   Gossip{memory, gamma});
 }
 
 CHOCO_API int choco_gossip_randk_compress_segmented(float* x, const float* memory, const float* xhat, float gamma,

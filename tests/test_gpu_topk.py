@@ -445,3 +445,64 @@ def test_randk_100M_bench_shape():
     oi = O.randk_indices(n, k, 12345, 3)
     assert np.array_equal(host(idx).astype(np.int64), oi)
     assert same_bits(host(vals), host(x)[oi])
+
+
+def _check_seg(x, plan, lens, ratio, xh=None):
+    from chocosgd_amd import codec
+    vals, idx = codec.topk_segmented(x, plan, xhat=xh)
+    d = host(x) if xh is None else (host(x) - host(xh)).astype(np.float32)
+    ov, oi, _ = O.topk_segmented(d, lens, ratio)
+    assert np.array_equal(host(idx).astype(np.int64), oi)
+    assert same_bits(host(vals), ov)
+
+
+@pytest.mark.parametrize("layout", ["resnet20_cifar10", "resnet50_imagenet", "edges"])
+def test_topk_segmented_warm_sequence(layout):
+    """Warm segmented calls (one read: each segment's window from the previous call):
+    drifting data, then windows that are badly wrong -- x100, all zeros (k_s-th key 0),
+    tie-heavy, x1e-3, back to random -- every call exact (misses take the exact
+    one-workgroup fallback in S4 and re-centre the window)."""
+    from chocosgd_amd import codec
+    lens = ([16383, 16384, 16385, 1, 3, 700_001, 32768, 2_500_007] if layout == "edges"
+            else golden_json("layouts.json")[layout])
+    n = sum(lens)
+    ratio = 0.99
+    plan = codec.SegmentPlan(lens, ratio, torch.device(DEV))
+    base = randn(n, 500)
+    g = torch.Generator(device=DEV).manual_seed(501)
+    seq = [base, base * 0.98 + randn(n, 502, 0.05), base * 0.95 + randn(n, 503, 0.05), randn(n, 504) * 100,
+           torch.zeros(n, device=DEV), torch.round(torch.randn(n, generator=g, device=DEV) * 4) / 4,
+           randn(n, 505) * 1e-3, randn(n, 506), randn(n, 507)]
+    for x in seq:
+        _check_seg(x, plan, lens, ratio)
+
+
+def test_topk_segmented_warm_ratio0_and_half():
+    """k_s = len_s (every element) and k_s = len_s / 2 on the warm path."""
+    from chocosgd_amd import codec
+    lens = [100, 50_000, 16384, 16385, 3, 700_001]
+    n = sum(lens)
+    for ratio in (0.0, 0.5):
+        plan = codec.SegmentPlan(lens, ratio, torch.device(DEV))
+        for i in range(3):
+            _check_seg(randn(n, 510 + i), plan, lens, ratio, xh=randn(n, 520 + i, 0.5))
+
+
+def test_topk_segmented_gossip_warm_sequence():
+    """The consensus step fused into the warm path's single read (S2) over several steps."""
+    from chocosgd_amd import codec
+    lens = golden_json("layouts.json")["resnet20_cifar10"] + [1_100_003]
+    n = sum(lens)
+    plan = codec.SegmentPlan(lens, 0.99, torch.device(DEV))
+    g = torch.Generator(device=DEV).manual_seed(530)
+    x = torch.randn(n, generator=g, device=DEV)
+    hat = x + 0.1 * torch.randn(n, generator=g, device=DEV)
+    mem = hat + 0.05 * torch.randn(n, generator=g, device=DEV)
+    for step in range(4):
+        xa = O.gossip_step(host(x), host(mem), host(hat), 0.9)
+        vals, idx = codec.topk_segmented(x, plan, xhat=hat, gossip=(mem, 0.9))
+        assert same_bits(host(x), xa)
+        ov, oi, _ = O.topk_segmented((xa - host(hat)).astype(np.float32), lens, 0.99)
+        assert np.array_equal(host(idx).astype(np.int64), oi)
+        assert same_bits(host(vals), ov)
+        codec.sparse_accumulate(vals, idx, mem, 1.0, xhat_self=hat)
