@@ -43,7 +43,7 @@ constexpr int kRkThreads = 1024;
 constexpr int kRkWords = (int)(kRkTile / 32);            // 8192 bitmap words
 constexpr int kRkWpt = kRkWords / kRkThreads;            // 8 words (256 bits) per thread
 constexpr int kRkMaxSegTiles = (int)((int64_t(1) << 31) >> kRkTileBits);  // 8192 tiles of one segment
-constexpr int64_t kRkCountWgs = 32;  // flat count pass: workgroups sharing [0, k)
+constexpr int64_t kRkPad = 32;  // one tile counter per 128-B line
 constexpr int kRkWalkCap = 4096;  // cycle-walk bound (P(walk > 64) < 2^-64 per draw): a GPU loop must end
 static_assert(kRkWpt * 32 * kRkThreads == kRkTile, "bitmap geometry");
 
@@ -128,24 +128,23 @@ __global__ __launch_bounds__(kRkThreads) void randk_count_kernel(const int64_t* 
                                                                  uint32_t* __restrict__ cnt_next, int64_t cap) {
   __shared__ uint32_t hist[kRkMaxSegTiles];
   const int64_t b = blockIdx.x;
-  // flat: gridDim.x <= tiles workgroups share [0, k) (fewer flushes of the tile histogram:
-  // every flush is up to `tiles` global atomics onto the same `tiles` words); segmented:
-  // one workgroup per tile of the plan
-  const RkTile T = FLAT ? rk_tile_flat(n, k, key, 0) : rk_tile_seg(plan, rk_base, key, b);
+  const RkTile T = FLAT ? rk_tile_flat(n, k, key, b) : rk_tile_seg(plan, rk_base, key, b);
   // the NEXT call's counts, over the buffer's whole capacity (it may draw more tiles)
-  for (int64_t i = b * kRkThreads + threadIdx.x; i < cap; i += (int64_t)gridDim.x * kRkThreads) cnt_next[i] = 0u;
+  for (int64_t i = b * kRkThreads + threadIdx.x; i < cap; i += (int64_t)gridDim.x * kRkThreads)
+    cnt_next[i * kRkPad] = 0u;
   if (T.ntile <= 1 || T.k >= T.seg_len) return;  // one tile, or every element: no split to draw
   const int nt = (int)T.ntile;
   for (int i = threadIdx.x; i < nt; i += kRkThreads) hist[i] = 0u;
   __syncthreads();
   RkPerm P;
   P.init(T.K, (uint32_t)T.seg_len);
-  const int64_t parts = FLAT ? (int64_t)gridDim.x : T.ntile, part = FLAT ? b : T.t;
-  const int64_t j0 = T.k * part / parts, j1 = T.k * (part + 1) / parts;
+  const int64_t j0 = T.k * T.t / T.ntile, j1 = T.k * (T.t + 1) / T.ntile;
   for (int64_t j = j0 + threadIdx.x; j < j1; j += kRkThreads) atomicAdd(&hist[P((uint32_t)j) >> kRkTileBits], 1u);
   __syncthreads();
+  // every workgroup adds into every tile's counter: one 128-B line per counter (adders
+  // on one line serialize, MI355X_MICROARCH.md "Global float atomics", contention)
   for (int i = threadIdx.x; i < nt; i += kRkThreads)
-    if (hist[i]) atomicAdd(&cnt_cur[T.first + i], hist[i]);
+    if (hist[i]) atomicAdd(&cnt_cur[(T.first + i) * kRkPad], hist[i]);
 }
 
 CHOCO_DEV uint32_t pick_word(const uint32_t (&w)[kRkWpt], int q) {  // w[q] by selects (no scratch)
@@ -182,11 +181,11 @@ __global__ __launch_bounds__(kRkThreads) void randk_tile_kernel(const float* __r
     pre = 0u;
   } else {
     uint32_t part = 0;
-    for (int64_t i = tid; i < T.t; i += kRkThreads) part += cnt[T.first + i];
+    for (int64_t i = tid; i < T.t; i += kRkThreads) part += cnt[(T.first + i) * kRkPad];
     uint32_t tot;
     block_excl_scan(part, scratch, &tot);
     pre = tot;
-    c = cnt[T.first + T.t];
+    c = cnt[(T.first + T.t) * kRkPad];
   }
   // the c positions of this tile: a bitmap in LDS
   if (all) {
@@ -285,8 +284,8 @@ void randk_forget(const void* ws, size_t bytes) {
 
 int64_t randk_tiles(int64_t len) { return (len + kRkTile - 1) >> kRkTileBits; }
 
-// counts: [256-B header (status word) | cnt[2][R]]
-size_t randk_counts_bytes(int64_t R) { return 256 + align_up((size_t)(2 * R) * 4, 256); }
+// counts: [256-B header (status word) | cnt[2][R] (one 128-B line each)]
+size_t randk_counts_bytes(int64_t R) { return 256 + align_up((size_t)(2 * R) * 4 * kRkPad, 256); }
 
 // The flat call (plan == nullptr) or the segmented one (plan_dev / rk_base / R).
 int randk_launch(const float* x, const float* xh, const int64_t* plan_dev, int64_t rk_base, int64_t R, int64_t n,
@@ -294,34 +293,34 @@ int randk_launch(const float* x, const float* xh, const int64_t* plan_dev, int64
                  void* counts, size_t counts_bytes, hipStream_t st) {
   const uint64_t key = qrng_key(seed, offset);
   CHOCO_REQUIRE(counts_bytes >= randk_counts_bytes(R), "random-k counts buffer too small");
-  const int64_t cap = (int64_t)((counts_bytes - 256) / 8);  // tiles per parity the buffer holds
+  const int64_t cap = (int64_t)((counts_bytes - 256) / (8 * kRkPad));  // tiles per parity the buffer holds
   uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(counts) + 256);
   // first call on a buffer: parity 0, zero (the workspace contract); R1 zeroes the other
   const uint32_t par = rk_parity(cnt);
   const bool flat = plan_dev == nullptr;
   profile_begin("randk_count", st);
   if (flat)
-    CHOCO_KLAUNCH((randk_count_kernel<true>), dim3((unsigned)std::min<int64_t>(R, kRkCountWgs)), dim3(kRkThreads), 0,
-                  st, plan_dev, rk_base, n, k, key,
-                  cnt + par * cap, cnt + (par ^ 1u) * cap, cap);
+    CHOCO_KLAUNCH((randk_count_kernel<true>), dim3((unsigned)R), dim3(kRkThreads), 0, st, plan_dev, rk_base, n, k,
+                  key,
+                  cnt + par * cap * kRkPad, cnt + (par ^ 1u) * cap * kRkPad, cap);
   else
     CHOCO_KLAUNCH((randk_count_kernel<false>), dim3((unsigned)R), dim3(kRkThreads), 0, st, plan_dev, rk_base, n, k,
-                  key, cnt + par * cap, cnt + (par ^ 1u) * cap, cap);
+                  key, cnt + par * cap * kRkPad, cnt + (par ^ 1u) * cap * kRkPad, cap);
   profile_end("randk_count", st);
   CHOCO_LAUNCHED("randk_count_kernel");
   profile_begin("randk_tile", st);
   if (flat && xh)
     CHOCO_KLAUNCH((randk_tile_kernel<true, true>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
-                  rk_base, n, k, key, is_biased, cnt + par * cap, out_val, out_idx);
+                  rk_base, n, k, key, is_biased, cnt + par * cap * kRkPad, out_val, out_idx);
   else if (flat)
     CHOCO_KLAUNCH((randk_tile_kernel<true, false>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
-                  rk_base, n, k, key, is_biased, cnt + par * cap, out_val, out_idx);
+                  rk_base, n, k, key, is_biased, cnt + par * cap * kRkPad, out_val, out_idx);
   else if (xh)
     CHOCO_KLAUNCH((randk_tile_kernel<false, true>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
-                  rk_base, n, k, key, is_biased, cnt + par * cap, out_val, out_idx);
+                  rk_base, n, k, key, is_biased, cnt + par * cap * kRkPad, out_val, out_idx);
   else
     CHOCO_KLAUNCH((randk_tile_kernel<false, false>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
-                  rk_base, n, k, key, is_biased, cnt + par * cap, out_val, out_idx);
+                  rk_base, n, k, key, is_biased, cnt + par * cap * kRkPad, out_val, out_idx);
   profile_end("randk_tile", st);
   CHOCO_LAUNCHED("randk_tile_kernel");
   return CHOCO_OK;

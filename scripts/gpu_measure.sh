@@ -16,7 +16,7 @@ for wl in $WLS; do
   rm -rf /tmp/pk
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/pk -o k -- python3 bench.py --workload $wl --steps 20 \
     --warmup 5 --no-cpu-baseline --no-e2e > $O/prof_$wl.json 2> $O/prof_$wl.err || { tail -5 $O/prof_$wl.err; exit 1; }
-  cp $(find /tmp/pk -name "*kernel_stats.csv" | head -1) $O/r02_${wl}_kernel_stats.csv || exit 1
+  cp $(find /tmp/pk -name "*kernel_stats.csv" | head -1) $O/${R:-r03}_${wl}_kernel_stats.csv || exit 1
   timeout -k 10 300 python3 bench.py --workload $wl > $O/bench_$wl.json 2> $O/bench_$wl.err \
     || { tail -5 $O/bench_$wl.err; exit 1; }
   echo "$wl done: $(python3 -c "import json; d=json.loads(open('$O/bench_$wl.json').read().splitlines()[-1]); r=d['roofline']; print(d['value'], d['ms_per_step'], r['stage'], r['frac'], r['traffic'])")"

@@ -22,13 +22,14 @@ KERNELS = {
     "topk_bounds": ("topk_bounds_kernel", 2.0),
     "topk_stream": ("topk_stream_kernel", 2.0),
     "topk_finish": ("topk_finish_kernel", 2.0),
-    "topk_fused": ("topk_fused_kernel", 2.0),
     "topk_seg_hist": ("seg_hist_kernel", 2.0),
     "topk_seg_collect": ("seg_collect_kernel", 2.0),
     "topk_seg_fine": ("seg_fine_kernel", 2.0),
     "topk_seg_count": ("seg_count_kernel", 2.0),
     "topk_seg_emit": ("seg_emit_kernel", 2.0),
     "sparse_accumulate": ("sparse_acc", 1.0),
+    "randk_count": ("randk_count_kernel", 1.0),
+    "randk_tile": ("randk_tile_kernel", 1.0),  # 4-B gathers: raw count (uncalibrated, like the accumulate)
     "qsgd_norm": ("qsgd_norm_kernel", 2.0),
     "qsgd_quantize": ("qsgd_quant_kernel", 2.0),
     "qsgd_accumulate": ("qsgd_decode_kernel", 2.0),
