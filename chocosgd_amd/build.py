@@ -58,8 +58,25 @@ def build_library(force=False, verbose=False, jobs=None, defines=(), lib=None):
     os.makedirs(objdir, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
 
+    headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+    flags_stamp = os.path.join(objdir, "flags.txt")
+    flags = " ".join(HIPCC_FLAGS + [f"-D{d}" for d in defines])
+    same_flags = os.path.exists(flags_stamp) and open(flags_stamp).read() == flags
+
+    macros = [d.split("=")[0] for d in defines]
+    in_headers = any(m in open(h).read() for h in headers for m in macros)
+
     def compile_one(src):
+        # a variant's macros that only one source names: the other objects are the
+        # product build's (built first, below)
+        if defines and not in_headers and not any(m in open(src).read() for m in macros):
+            return os.path.join(PKG, "build_obj", os.path.basename(src) + ".o")
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        # an object newer than its source and every header, built with the same flags, is kept
+        if same_flags and os.path.exists(obj):
+            t = os.path.getmtime(obj)
+            if all(os.path.getmtime(d) <= t for d in [src] + headers):
+                return obj
         cmd = [hipcc, *HIPCC_FLAGS, *[f"-D{d}" for d in defines], "-I", INCLUDE, "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
@@ -69,9 +86,13 @@ def build_library(force=False, verbose=False, jobs=None, defines=(), lib=None):
         return obj
 
     srcs = sources()
+    if defines:
+        build_library(jobs=jobs)  # the product objects a variant reuses
     jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 2)), 8)
     with concurrent.futures.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, srcs))
+    with open(flags_stamp, "w") as f:
+        f.write(flags)
     os.makedirs(os.path.dirname(out), exist_ok=True)
     tmp = out + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]

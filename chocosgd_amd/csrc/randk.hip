@@ -26,9 +26,15 @@
 // splitmix64_mix(K + (i + 1) * 0x9E3779B97F4A7C15).  oracle/choco_oracle.py
 // restates every step (randk_indices, randk_segmented).
 //
-// Two launches: R1 (tile counts; only for segments of more than one tile) and
-// R2 (per tile: bitmap sample, ordered emission, gather).  Bytes: 4k gathered
-// (8k with xhat) + 8k written; the sampler itself reads nothing.
+// Two launches: R1 (tile counts; only for segments of more than one tile) and R2
+// (per tile: bitmap sample, ordered emission, gather).  Bytes: 4k gathered (8k
+// with xhat) + 8k written; the sampler itself reads nothing.
+//
+// R1 spreads a segment's k draws over G = min(tiles, 256) workgroups; each writes
+// its column of a [tile][256] count matrix (draws per tile, draws in earlier
+// tiles) with plain stores, and an R2 tile sums its own row (count and output
+// offset) -- no atomics (round 3's per-tile counters, one 128-B line each, took
+// 382 device-scope adders per line at 100M: 12-27 us).
 #include "choco_common.h"
 
 #include <algorithm>
@@ -37,13 +43,32 @@
 
 namespace choco {
 
+// Diagnostic phase stamps (tools/rk_stamps.py; never in the product build).
+#ifndef CHOCO_STAMPS
+#define CHOCO_STAMPS 0
+#endif
+#if CHOCO_STAMPS
+constexpr int kRkStampSlots = 16384;
+__device__ unsigned long long g_rk_stamps[kRkStampSlots][8];
+#define RKSTAMP(slot, j)                                                     \
+  do {                                                                      \
+    if (threadIdx.x == 0) g_rk_stamps[(slot)][(j)] = wall_clock64();        \
+  } while (0)
+#else
+#define RKSTAMP(slot, j) \
+  do {                   \
+  } while (0)
+#endif
+
 constexpr int kRkTileBits = 18;
 constexpr int64_t kRkTile = int64_t(1) << kRkTileBits;  // elements per tile: a 32 KB bitmap
 constexpr int kRkThreads = 1024;
 constexpr int kRkWords = (int)(kRkTile / 32);            // 8192 bitmap words
 constexpr int kRkWpt = kRkWords / kRkThreads;            // 8 words (256 bits) per thread
 constexpr int kRkMaxSegTiles = (int)((int64_t(1) << 31) >> kRkTileBits);  // 8192 tiles of one segment
-constexpr int64_t kRkPad = 32;  // one tile counter per 128-B line
+constexpr int kRkGroups = 256;   // R1 workgroups drawing one segment's counts (count-matrix row length)
+constexpr int kRkList = 8192;    // R2: positions listed in LDS (denser tiles emit per thread)
+constexpr int kRkGU = 4;         // R2: list gathers in flight per thread
 constexpr int kRkWalkCap = 4096;  // cycle-walk bound (P(walk > 64) < 2^-64 per draw): a GPU loop must end
 static_assert(kRkWpt * 32 * kRkThreads == kRkTile, "bitmap geometry");
 
@@ -119,32 +144,53 @@ CHOCO_DEV RkTile rk_tile_flat(int64_t n, int64_t k, uint64_t key, int64_t b) {
   return T;
 }
 
-// R1: this tile's share of j in [0, k) of its segment -> pi_N(j) -> tile histogram
-// -> the counts of the call (cnt[par]); the NEXT call's counts are zeroed here.
+// R1: group g < G = min(tiles, kRkGroups) of a multi-tile segment draws j in
+// [k g / G, k (g + 1) / G) -> pi_N(j) -> a tile histogram in LDS, and writes its
+// column of the segment's count matrix: H[tile][g] (this group's draws in the
+// tile) and P[tile][g] (its draws in the segment's earlier tiles).  No atomics:
+// an R2 tile sums its own row of H and of P (G contiguous words each).  Workgroup
+// b is plan tile b; tiles past their segment's G (and single-tile segments) idle.
 template <bool FLAT>
 __global__ __launch_bounds__(kRkThreads) void randk_count_kernel(const int64_t* __restrict__ plan, int64_t rk_base,
                                                                  int64_t n, int64_t k, uint64_t key,
-                                                                 uint32_t* __restrict__ cnt_cur,
-                                                                 uint32_t* __restrict__ cnt_next, int64_t cap) {
+                                                                 uint32_t* __restrict__ H, uint32_t* __restrict__ P) {
   __shared__ uint32_t hist[kRkMaxSegTiles];
+  __shared__ uint32_t scratch[40];
   const int64_t b = blockIdx.x;
+  RKSTAMP(b, 0);
   const RkTile T = FLAT ? rk_tile_flat(n, k, key, b) : rk_tile_seg(plan, rk_base, key, b);
-  // the NEXT call's counts, over the buffer's whole capacity (it may draw more tiles)
-  for (int64_t i = b * kRkThreads + threadIdx.x; i < cap; i += (int64_t)gridDim.x * kRkThreads)
-    cnt_next[i * kRkPad] = 0u;
-  if (T.ntile <= 1 || T.k >= T.seg_len) return;  // one tile, or every element: no split to draw
+  const int64_t G = std::min<int64_t>(T.ntile, kRkGroups);
+  if (T.ntile <= 1 || T.k >= T.seg_len || T.t >= G) return;  // workgroup-uniform
   const int nt = (int)T.ntile;
   for (int i = threadIdx.x; i < nt; i += kRkThreads) hist[i] = 0u;
   __syncthreads();
-  RkPerm P;
-  P.init(T.K, (uint32_t)T.seg_len);
-  const int64_t j0 = T.k * T.t / T.ntile, j1 = T.k * (T.t + 1) / T.ntile;
-  for (int64_t j = j0 + threadIdx.x; j < j1; j += kRkThreads) atomicAdd(&hist[P((uint32_t)j) >> kRkTileBits], 1u);
+  RkPerm Pm;
+  Pm.init(T.K, (uint32_t)T.seg_len);
+  const int64_t j0 = T.k * T.t / G, j1 = T.k * (T.t + 1) / G;
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += kRkThreads) atomicAdd(&hist[Pm((uint32_t)j) >> kRkTileBits], 1u);
   __syncthreads();
-  // every workgroup adds into every tile's counter: one 128-B line per counter (adders
-  // on one line serialize, MI355X_MICROARCH.md "Global float atomics", contention)
-  for (int i = threadIdx.x; i < nt; i += kRkThreads)
-    if (hist[i]) atomicAdd(&cnt_cur[(T.first + i) * kRkPad], hist[i]);
+  RKSTAMP(b, 1);
+  // column g of rows first .. first + nt - 1: kRkPer tiles per thread per round
+  constexpr int kRkPer = kRkMaxSegTiles / kRkThreads;
+  uint32_t c[kRkPer], sum = 0;
+#pragma unroll
+  for (int q = 0; q < kRkPer; ++q) {
+    const int i = (int)threadIdx.x * kRkPer + q;
+    c[q] = i < nt ? hist[i] : 0u;
+    sum += c[q];
+  }
+  uint32_t tot;
+  uint32_t pre = block_excl_scan(sum, scratch, &tot);
+#pragma unroll
+  for (int q = 0; q < kRkPer; ++q) {
+    const int i = (int)threadIdx.x * kRkPer + q;
+    if (i < nt) {
+      H[(T.first + i) * kRkGroups + T.t] = c[q];
+      P[(T.first + i) * kRkGroups + T.t] = pre;
+    }
+    pre += c[q];
+  }
+  RKSTAMP(b, 2);
 }
 
 CHOCO_DEV uint32_t pick_word(const uint32_t (&w)[kRkWpt], int q) {  // w[q] by selects (no scratch)
@@ -154,24 +200,29 @@ CHOCO_DEV uint32_t pick_word(const uint32_t (&w)[kRkWpt], int q) {  // w[q] by s
   return r;
 }
 
-// R2: one tile -> its count and output offset, the bitmap sample, the ordered
-// emission with the gather.
+// R2: one tile -> its count and output offset (its rows of H and P), the bitmap
+// sample, the ordered emission with the gather.  Up to kRkList positions are
+// listed in LDS in ascending order and gathered by consecutive lanes (coalesced
+// stores, kRkGU loads in flight per thread); denser tiles emit per thread.
 template <bool FLAT, bool XH>
 __global__ __launch_bounds__(kRkThreads) void randk_tile_kernel(const float* __restrict__ x, const float* __restrict__ xh,
                                                                 const int64_t* __restrict__ plan, int64_t rk_base,
                                                                 int64_t n, int64_t k, uint64_t key, int32_t is_biased,
-                                                                const uint32_t* __restrict__ cnt,
+                                                                const uint32_t* __restrict__ H,
+                                                                const uint32_t* __restrict__ P,
                                                                 float* __restrict__ out_val,
                                                                 int32_t* __restrict__ out_idx) {
   __shared__ uint32_t bm[kRkWords];
+  __shared__ uint32_t list[kRkList];
   __shared__ uint32_t scratch[40];
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
+  RKSTAMP(8192 + b, 0);
   const RkTile T = FLAT ? rk_tile_flat(n, k, key, b) : rk_tile_seg(plan, rk_base, key, b);
   const int64_t start = T.t << kRkTileBits;  // within the segment
   const uint32_t L = (uint32_t)std::min<int64_t>(kRkTile, T.seg_len - start);
   const bool all = T.k >= T.seg_len;
-  // this tile's count and the counts of the segment's earlier tiles
+  // this tile's count and the draws of the segment's earlier tiles
   uint32_t c, pre;
   if (all) {
     c = L;
@@ -180,13 +231,13 @@ __global__ __launch_bounds__(kRkThreads) void randk_tile_kernel(const float* __r
     c = (uint32_t)T.k;
     pre = 0u;
   } else {
-    uint32_t part = 0;
-    for (int64_t i = tid; i < T.t; i += kRkThreads) part += cnt[(T.first + i) * kRkPad];
-    uint32_t tot;
-    block_excl_scan(part, scratch, &tot);
-    pre = tot;
-    c = cnt[(T.first + T.t) * kRkPad];
+    const int64_t G = std::min<int64_t>(T.ntile, kRkGroups);
+    const int64_t row = (T.first + T.t) * kRkGroups;
+    const uint32_t h = tid < G ? H[row + tid] : 0u, p = tid < G ? P[row + tid] : 0u;
+    uint32_t x0, x1;
+    block_excl_scan2(h, p, scratch, &x0, &x1, &c, &pre);
   }
+  RKSTAMP(8192 + b, 1);
   // the c positions of this tile: a bitmap in LDS
   if (all) {
 #pragma unroll
@@ -199,14 +250,15 @@ __global__ __launch_bounds__(kRkThreads) void randk_tile_kernel(const float* __r
 #pragma unroll
     for (int q = 0; q < kRkWpt; ++q) bm[tid * kRkWpt + q] = 0u;
     __syncthreads();
-    RkPerm P;
-    P.init(rk_derive(T.K, 8 + (uint64_t)T.t), L);
+    RkPerm Pm;
+    Pm.init(rk_derive(T.K, 8 + (uint64_t)T.t), L);
     for (uint32_t j = tid; j < c; j += kRkThreads) {
-      const uint32_t p = P(j);
+      const uint32_t p = Pm(j);
       atomicOr(&bm[p >> 5], 1u << (p & 31u));
     }
     __syncthreads();
   }
+  RKSTAMP(8192 + b, 2);
   // thread t owns bits [256 t, 256 t + 256): rank of its first set bit
   uint32_t w[kRkWpt];
   uint32_t mine = 0;
@@ -217,75 +269,100 @@ __global__ __launch_bounds__(kRkThreads) void randk_tile_kernel(const float* __r
   }
   uint32_t tot;
   uint32_t rank = block_excl_scan(mine, scratch, &tot);
+  RKSTAMP(8192 + b, 3);
   const float scale = is_biased ? 1.0f : (float)((double)T.seg_len / (double)T.k);
   const int64_t gbase = T.seg_off + start;                 // global index of the tile's first element
   float* __restrict__ ov = out_val + T.out_off + pre;
   int32_t* __restrict__ oi = out_idx + T.out_off + pre;
-  // ascending set bits, kG gathers in flight per batch (every register index static)
-  constexpr int kG = 8;
-  int q = 0;
-  uint32_t cur = w[0];
-  for (;;) {
-    uint32_t pos[kG];
-    bool ok[kG];
+  if (c <= (uint32_t)kRkList) {  // workgroup-uniform
+    // ascending positions -> list[rank ..], then lanes gather consecutive entries
+    uint32_t r = rank;
 #pragma unroll
-    for (int i = 0; i < kG; ++i) {
-      while (cur == 0u && q + 1 < kRkWpt) cur = pick_word(w, ++q);
-      ok[i] = cur != 0u;
-      pos[i] = ok[i] ? (uint32_t)(tid * kRkWpt + q) * 32u + (uint32_t)__builtin_ctz(cur) : 0u;
-      if (ok[i]) cur &= cur - 1u;
-    }
-    if (!ok[0]) break;
-    float v[kG];
-#pragma unroll
-    for (int i = 0; i < kG; ++i) {
-      v[i] = 0.f;
-      if (ok[i]) {
-        const int64_t e = gbase + pos[i];
-        v[i] = XH ? x[e] - xh[e] : x[e];
+    for (int q = 0; q < kRkWpt; ++q) {
+      uint32_t wq = w[q];
+      while (wq != 0u) {
+        if (r < c) list[r] = (uint32_t)(tid * kRkWpt + q) * 32u + (uint32_t)__builtin_ctz(wq);
+        ++r;
+        wq &= wq - 1u;
       }
     }
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < c; i0 += kRkThreads * kRkGU) {
+      uint32_t pos[kRkGU];
+      float v[kRkGU];
 #pragma unroll
-    for (int i = 0; i < kG; ++i) {
-      if (ok[i] && rank + (uint32_t)i < c) {  // (bounded: never past the tile's count)
-        ov[rank + i] = v[i] * scale;
-        oi[rank + i] = (int32_t)(gbase + pos[i]);
+      for (int u = 0; u < kRkGU; ++u) {
+        const uint32_t i = i0 + (uint32_t)u * kRkThreads + (uint32_t)tid;
+        pos[u] = list[min(i, c - 1u)];
+      }
+#pragma unroll
+      for (int u = 0; u < kRkGU; ++u) {
+        const uint32_t i = i0 + (uint32_t)u * kRkThreads + (uint32_t)tid;
+        const int64_t e = gbase + pos[u];
+        v[u] = 0.f;
+        if (i < c) v[u] = XH ? x[e] - xh[e] : x[e];
+      }
+#pragma unroll
+      for (int u = 0; u < kRkGU; ++u) {
+        const uint32_t i = i0 + (uint32_t)u * kRkThreads + (uint32_t)tid;
+        if (i < c) {
+          ov[i] = v[u] * scale;
+          oi[i] = (int32_t)(gbase + pos[u]);
+        }
       }
     }
-    uint32_t m = 0;
+  } else {
+    // dense tile: each thread emits its own ascending positions, kG gathers in flight
+    constexpr int kG = 8;
+    int q = 0;
+    uint32_t cur = w[0];
+    for (;;) {
+      uint32_t pos[kG];
+      bool ok[kG];
 #pragma unroll
-    for (int i = 0; i < kG; ++i) m += ok[i] ? 1u : 0u;
-    rank += m;
+      for (int i = 0; i < kG; ++i) {
+        while (cur == 0u && q + 1 < kRkWpt) cur = pick_word(w, ++q);
+        ok[i] = cur != 0u;
+        pos[i] = ok[i] ? (uint32_t)(tid * kRkWpt + q) * 32u + (uint32_t)__builtin_ctz(cur) : 0u;
+        if (ok[i]) cur &= cur - 1u;
+      }
+      if (!ok[0]) break;
+      float v[kG];
+#pragma unroll
+      for (int i = 0; i < kG; ++i) {
+        v[i] = 0.f;
+        if (ok[i]) {
+          const int64_t e = gbase + pos[i];
+          v[i] = XH ? x[e] - xh[e] : x[e];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kG; ++i) {
+        if (ok[i] && rank + (uint32_t)i < c) {  // (bounded: never past the tile's count)
+          ov[rank + i] = v[i] * scale;
+          oi[rank + i] = (int32_t)(gbase + pos[i]);
+        }
+      }
+      uint32_t m = 0;
+#pragma unroll
+      for (int i = 0; i < kG; ++i) m += ok[i] ? 1u : 0u;
+      rank += m;
+    }
   }
+#if CHOCO_STAMPS
+  __syncthreads();
+  RKSTAMP(8192 + b, 4);
+#endif
 }
 
 // ---------------------------------------------------------------- host side
-// call parity per counts buffer: call c adds into cnt[c & 1] and zeroes the other
-static std::mutex g_rk_mu;
-static std::unordered_map<const void*, uint64_t> g_rk_calls;
-static uint32_t rk_parity(const void* cnt) {
-  std::lock_guard<std::mutex> g(g_rk_mu);
-  auto it = g_rk_calls.find(cnt);
-  if (it == g_rk_calls.end()) {
-    g_rk_calls.emplace(cnt, 1u);
-    return 0u;
-  }
-  return (uint32_t)(it->second++ & 1u);
-}
-void randk_forget(const void* ws, size_t bytes) {
-  std::lock_guard<std::mutex> g(g_rk_mu);
-  const char* lo = static_cast<const char*>(ws);
-  for (auto it = g_rk_calls.begin(); it != g_rk_calls.end();) {
-    const char* p = static_cast<const char*>(it->first);
-    if (p == lo || (p > lo && p < lo + bytes)) it = g_rk_calls.erase(it);
-    else ++it;
-  }
-}
+void randk_forget(const void*, size_t) {}  // no per-workspace host state
 
 int64_t randk_tiles(int64_t len) { return (len + kRkTile - 1) >> kRkTileBits; }
 
-// counts: [256-B header (status word) | cnt[2][R] (one 128-B line each)]
-size_t randk_counts_bytes(int64_t R) { return 256 + align_up((size_t)(2 * R) * 4 * kRkPad, 256); }
+// counts: [256-B header (status word at 0) | H[R][256] | P[R][256]] (u32); every entry
+// an R2 tile reads is written by this call's R1 (no zero-fill needed between calls)
+size_t randk_counts_bytes(int64_t R) { return 256 + 2 * align_up((size_t)R * kRkGroups * 4, 256); }
 
 // The flat call (plan == nullptr) or the segmented one (plan_dev / rk_base / R).
 int randk_launch(const float* x, const float* xh, const int64_t* plan_dev, int64_t rk_base, int64_t R, int64_t n,
@@ -293,34 +370,31 @@ int randk_launch(const float* x, const float* xh, const int64_t* plan_dev, int64
                  void* counts, size_t counts_bytes, hipStream_t st) {
   const uint64_t key = qrng_key(seed, offset);
   CHOCO_REQUIRE(counts_bytes >= randk_counts_bytes(R), "random-k counts buffer too small");
-  const int64_t cap = (int64_t)((counts_bytes - 256) / (8 * kRkPad));  // tiles per parity the buffer holds
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(counts) + 256);
-  // first call on a buffer: parity 0, zero (the workspace contract); R1 zeroes the other
-  const uint32_t par = rk_parity(cnt);
+  uint32_t* H = reinterpret_cast<uint32_t*>(static_cast<char*>(counts) + 256);
+  uint32_t* P = reinterpret_cast<uint32_t*>(static_cast<char*>(counts) + 256 + align_up((size_t)R * kRkGroups * 4, 256));
   const bool flat = plan_dev == nullptr;
   profile_begin("randk_count", st);
   if (flat)
     CHOCO_KLAUNCH((randk_count_kernel<true>), dim3((unsigned)R), dim3(kRkThreads), 0, st, plan_dev, rk_base, n, k,
-                  key,
-                  cnt + par * cap * kRkPad, cnt + (par ^ 1u) * cap * kRkPad, cap);
+                  key, H, P);
   else
     CHOCO_KLAUNCH((randk_count_kernel<false>), dim3((unsigned)R), dim3(kRkThreads), 0, st, plan_dev, rk_base, n, k,
-                  key, cnt + par * cap * kRkPad, cnt + (par ^ 1u) * cap * kRkPad, cap);
+                  key, H, P);
   profile_end("randk_count", st);
   CHOCO_LAUNCHED("randk_count_kernel");
   profile_begin("randk_tile", st);
   if (flat && xh)
     CHOCO_KLAUNCH((randk_tile_kernel<true, true>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
-                  rk_base, n, k, key, is_biased, cnt + par * cap * kRkPad, out_val, out_idx);
+                  rk_base, n, k, key, is_biased, H, P, out_val, out_idx);
   else if (flat)
     CHOCO_KLAUNCH((randk_tile_kernel<true, false>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
-                  rk_base, n, k, key, is_biased, cnt + par * cap * kRkPad, out_val, out_idx);
+                  rk_base, n, k, key, is_biased, H, P, out_val, out_idx);
   else if (xh)
     CHOCO_KLAUNCH((randk_tile_kernel<false, true>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
-                  rk_base, n, k, key, is_biased, cnt + par * cap * kRkPad, out_val, out_idx);
+                  rk_base, n, k, key, is_biased, H, P, out_val, out_idx);
   else
     CHOCO_KLAUNCH((randk_tile_kernel<false, false>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
-                  rk_base, n, k, key, is_biased, cnt + par * cap * kRkPad, out_val, out_idx);
+                  rk_base, n, k, key, is_biased, H, P, out_val, out_idx);
   profile_end("randk_tile", st);
   CHOCO_LAUNCHED("randk_tile_kernel");
   return CHOCO_OK;
@@ -329,6 +403,18 @@ int randk_launch(const float* x, const float* xh, const int64_t* plan_dev, int64
 }  // namespace choco
 
 using namespace choco;
+
+#if CHOCO_STAMPS
+// Diagnostic builds only: copy out (and clear) the random-k phase stamps.
+CHOCO_API int choco_dbg_rk_stamps(unsigned long long* host, size_t bytes) {
+  const size_t all = sizeof(unsigned long long) * kRkStampSlots * 8;
+  if (bytes > all) bytes = all;
+  if (host) CHOCO_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rk_stamps), bytes, 0, hipMemcpyDeviceToHost));
+  static unsigned long long zeros[kRkStampSlots * 8];
+  CHOCO_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_rk_stamps), zeros, all, 0, hipMemcpyHostToDevice));
+  return CHOCO_OK;
+}
+#endif
 
 CHOCO_API size_t choco_randk_workspace_size(int64_t n) { return n > 0 ? randk_counts_bytes(randk_tiles(n)) : 256; }
 

@@ -555,10 +555,13 @@ CHOCO_DEV void process_row(const Src<MODE, XH>& src, const float4 v4, int64_t i,
 // interleave the rows' dependent compare -> ballot -> prefix -> LDS-store chains.
 // Lanes without a candidate store to a trash slot.  If the batch could overflow
 // the entry ring (dense inputs), rows take the per-row path instead.
-template <bool XH, class SM>
+// `reload` is called once A is dead (the batch is staged in LDS), BEFORE the ring
+// is expanded: the wave's next load batch then flies during the expansion, so
+// both of its buffers are in flight for most of the batch's work.
+template <bool XH, class SM, class RL>
 CHOCO_DEV void process_batch(const Src<kData, XH>& src, const float4 (&A)[kK2Unroll], int64_t base, int64_t cend,
                              SM& sm, int w, int lane, WaveAcc& a, float* __restrict__ ov,
-                             uint32_t* __restrict__ oi, const Buckets& bk) {
+                             uint32_t* __restrict__ oi, const Buckets& bk, RL&& reload) {
   bool any[kK2Unroll];
   uint64_t M[kK2Unroll];
   uint32_t add = 0;
@@ -570,7 +573,10 @@ CHOCO_DEV void process_batch(const Src<kData, XH>& src, const float4 (&A)[kK2Unr
     add += (uint32_t)__popcll(M[u]);
   }
   add = __builtin_amdgcn_readfirstlane(add);
-  if (add == 0u) return;
+  if (add == 0u) {
+    reload();
+    return;
+  }
   if (a.estaged - a.eflushed + add <= (uint32_t)kEnt) {
     uint32_t run = a.estaged;
 #pragma unroll
@@ -583,12 +589,14 @@ CHOCO_DEV void process_batch(const Src<kData, XH>& src, const float4 (&A)[kK2Unr
       run += (uint32_t)__popcll(M[u]);
     }
     a.estaged = __builtin_amdgcn_readfirstlane(run);
+    reload();
 #pragma unroll 1
     while (a.estaged - a.eflushed >= 64u) flush_entries(src, sm, w, lane, a, 64u, ov, oi, bk);
   } else {
 #pragma unroll
     for (int u = 0; u < kK2Unroll; ++u)
       process_row<kData, XH, false>(src, A[u], base + u * 256 + 4 * lane, cend, sm, w, lane, a, ov, oi, bk);
+    reload();
   }
 }
 
@@ -861,7 +869,8 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   WaveAcc a{};
   // One chunk whose batch (one-batch chunks) is in R, or that loads itself
   // (hash mode, the partial chunk); ends with the chunk's bookkeeping.
-  auto run_chunk = [&](uint32_t cc, const float4 (&R)[kK2Unroll]) {
+  // `reload` refills R (the wave's next chunk) as soon as R is dead.
+  auto run_chunk = [&](uint32_t cc, const float4 (&R)[kK2Unroll], auto&& reload) {
     const int64_t cbeg = tb + (int64_t)cc * kChunk;
     const int64_t cend = min(cbeg + kChunk, n);
     float* __restrict__ ov = cval + cbeg;
@@ -869,9 +878,14 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     a.estaged = a.eflushed = a.staged = a.lcnt = 0u;
     a.lstart = a.lfill;
     if (cbeg + kChunk <= n) {
-      if constexpr (MODE == kData) process_batch<XH>(src, R, cbeg, cend, sm, w, lane, a, ov, oi, bk);
-      else process_rows_hash<MODE, XH>(src, cbeg, cend, sm, w, lane, a, ov, oi, bk);
+      if constexpr (MODE == kData) {
+        process_batch<XH>(src, R, cbeg, cend, sm, w, lane, a, ov, oi, bk, reload);
+      } else {
+        reload();
+        process_rows_hash<MODE, XH>(src, cbeg, cend, sm, w, lane, a, ov, oi, bk);
+      }
     } else {
+      reload();  // (R unused: the partial chunk loads itself)
       // the buffer's last, partial chunk (or an empty one past n): guarded rows
       for (int64_t base = cbeg; base < cend; base += 256) {
         const int64_t i = base + 4 * lane;
@@ -903,13 +917,15 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     for (;;) {
       if (cA >= nchunk) break;
       const uint32_t nA = claim_chunk(sm, lane);
-      run_chunk(cA, A);
-      if constexpr (MODE == kData) load_rows_full<XH>(ts, batch0(nA), lane, A);
+      run_chunk(cA, A, [&] {
+        if constexpr (MODE == kData) load_rows_full<XH>(ts, batch0(nA), lane, A);
+      });
       cA = nA;
       if (cB >= nchunk) break;
       const uint32_t nB = claim_chunk(sm, lane);
-      run_chunk(cB, B);
-      if constexpr (MODE == kData) load_rows_full<XH>(ts, batch0(nB), lane, B);
+      run_chunk(cB, B, [&] {
+        if constexpr (MODE == kData) load_rows_full<XH>(ts, batch0(nB), lane, B);
+      });
       cB = nB;
     }
   } else if constexpr (kOneBatch) {
@@ -917,8 +933,9 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     while (c < nchunk) {
       const uint32_t nn = claim_chunk(sm, lane);
       if constexpr (GS) gossip_rows(ts, batch0(c), lane, gs.gamma, A);
-      run_chunk(c, A);
-      if constexpr (MODE == kData && !GS) load_rows_full<XH>(ts, batch0(nn), lane, A);
+      run_chunk(c, A, [&] {
+        if constexpr (MODE == kData && !GS) load_rows_full<XH>(ts, batch0(nn), lane, A);
+      });
       c = nn;
     }
   } else {
@@ -935,16 +952,17 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       if constexpr (MODE == kData && !XH) {
         // double-buffered: A and B hold this chunk; each is refilled with the
         // next chunk's batch as soon as it has been processed
-        process_batch<XH>(src, A, cbeg, cend, sm, w, lane, a, ov, oi, bk);
-        load_rows_full<XH>(ts, batch0(nx), lane, A);
-        process_batch<XH>(src, B, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk);
-        load_rows_full<XH>(ts, batch1(nx), lane, B);
+        process_batch<XH>(src, A, cbeg, cend, sm, w, lane, a, ov, oi, bk,
+                          [&] { load_rows_full<XH>(ts, batch0(nx), lane, A); });
+        process_batch<XH>(src, B, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk,
+                          [&] { load_rows_full<XH>(ts, batch1(nx), lane, B); });
       } else if constexpr (MODE == kData) {
         // two input streams: one batch (16 KiB per wave) at a time
-        process_batch<XH>(src, A, cbeg, cend, sm, w, lane, a, ov, oi, bk);
-        load_rows_full<XH>(ts, (uint32_t)(cbeg - b * (int64_t)tile + kStep) * 4u, lane, A);
-        process_batch<XH>(src, A, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk);
-        load_rows_full<XH>(ts, batch0(nx), lane, A);
+        process_batch<XH>(src, A, cbeg, cend, sm, w, lane, a, ov, oi, bk, [&] {
+          load_rows_full<XH>(ts, (uint32_t)(cbeg - b * (int64_t)tile + kStep) * 4u, lane, A);
+        });
+        process_batch<XH>(src, A, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk,
+                          [&] { load_rows_full<XH>(ts, batch0(nx), lane, A); });
       } else {
         process_rows_hash<MODE, XH>(src, cbeg, cend, sm, w, lane, a, ov, oi, bk);
         process_rows_hash<MODE, XH>(src, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk);
