@@ -252,6 +252,17 @@ class SegmentPlan:
                 buf = self._ws[key] = _new_workspace(dev, max(self.ws_bytes, 256))
             return buf
 
+    def drop_workspace(self, dev):
+        """Forget this plan's workspace on the current stream of `dev` (after a failed
+        call: its histograms may not be zeroed any more); the next call starts cold on
+        a fresh zero-filled one."""
+        key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+        with _ws_lock:
+            buf = self._ws.pop(key, None)
+        if buf is not None:
+            _status.pop(buf.data_ptr(), None)
+            lib().choco_topk_workspace_reset(_ptr(buf), buf.numel())
+
     def selected_base(self):
         """int32[K]: the segment start of every output slot (global -> local index)."""
         if self._base is None:
@@ -291,15 +302,22 @@ def topk_segmented(x, plan, xhat=None, out=None, gossip=None):
     st = topk_status(ws)
     st.check()
     g = _gossip(gossip, x, xhat)
-    if g is not None:
-        _lib.check(L.choco_gossip_topk_compress_segmented(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1], _ptr(plan.plan_dev),
-                                                          plan.plan_host, plan.nseg, _ptr(vals), _ptr(idx), _ptr(ws),
-                                                          ws.numel(), _stream(dev)),
-                   "choco_gossip_topk_compress_segmented")
-    else:
-        _lib.check(L.choco_topk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
-                                                   plan.nseg, _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(),
-                                                   _stream(dev)), "choco_topk_compress_segmented")
+    try:
+        if g is not None:
+            _lib.check(L.choco_gossip_topk_compress_segmented(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1],
+                                                              _ptr(plan.plan_dev), plan.plan_host, plan.nseg,
+                                                              _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(),
+                                                              _stream(dev)),
+                       "choco_gossip_topk_compress_segmented")
+        else:
+            _lib.check(L.choco_topk_compress_segmented(_ptr(x), _ptr(xhat), _ptr(plan.plan_dev), plan.plan_host,
+                                                       plan.nseg, _ptr(vals), _ptr(idx), _ptr(ws), ws.numel(),
+                                                       _stream(dev)), "choco_topk_compress_segmented")
+    except RuntimeError:
+        # a call that failed part-way may leave the plan's histograms non-zero
+        torch.cuda.synchronize(dev)
+        plan.drop_workspace(dev)
+        raise
     st.after_call()
     return vals, idx
 

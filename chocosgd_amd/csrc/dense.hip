@@ -102,7 +102,12 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_kernel(const float* __r
 // idle.  Whole-segment writes: no byte-masked partial writes reach the
 // memory side (a 4-B store dirties a sector that must be merged there).
 // A non-ascending pair (a corrupt message) is counted into *bad like an
-// out-of-range index.
+// out-of-range index.  Such a message is applied before the count is seen: with
+// indices out of order two leaders can own the same segment (e.g. [20, 3, 21])
+// and one whole-segment write overwrites the other's update, so x_hat / memory
+// of that step may already be wrong when the host reports the bad count
+// (IndexGuard, one step later; INTEGRATION.md "corrupt messages").  Messages
+// from this codec are always ascending.
 #ifndef CHOCO_ACC_MODE
 #define CHOCO_ACC_MODE 1
 #endif

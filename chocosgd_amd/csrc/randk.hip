@@ -52,7 +52,7 @@ constexpr int kRkStampSlots = 16384;
 __device__ unsigned long long g_rk_stamps[kRkStampSlots][8];
 #define RKSTAMP(slot, j)                                                     \
   do {                                                                      \
-    if (threadIdx.x == 0) g_rk_stamps[(slot)][(j)] = wall_clock64();        \
+    if (threadIdx.x == 0 && (slot) < kRkStampSlots) g_rk_stamps[(slot)][(j)] = wall_clock64(); \
   } while (0)
 #else
 #define RKSTAMP(slot, j) \
@@ -62,15 +62,22 @@ __device__ unsigned long long g_rk_stamps[kRkStampSlots][8];
 
 constexpr int kRkTileBits = 18;
 constexpr int64_t kRkTile = int64_t(1) << kRkTileBits;  // elements per tile: a 32 KB bitmap
-constexpr int kRkThreads = 1024;
-constexpr int kRkWords = (int)(kRkTile / 32);            // 8192 bitmap words
-constexpr int kRkWpt = kRkWords / kRkThreads;            // 8 words (256 bits) per thread
+constexpr int kRkThreads = 1024;                         // R1
+constexpr int kRkWords = (int)(kRkTile / 32);            // 8192 bitmap words per tile
+// R2: kRkQ workgroups per tile, each one quarter of the tile's bitmap (2^16 bits,
+// 8 KB of LDS) with kRkQThreads threads of 8 words (256 bits) each: ~6 small
+// workgroups per CU instead of 1-2 large ones (382 tiles on 256 CUs left half the
+// CUs with two 1024-thread tiles and set the tail: 44.7 us at 100M).
+constexpr int kRkQ = 4;
+constexpr int kRkQThreads = 256;
+constexpr int kRkQWords = kRkWords / kRkQ;               // 2048
+constexpr int kRkWpt = kRkQWords / kRkQThreads;          // 8 words (256 bits) per thread
 constexpr int kRkMaxSegTiles = (int)((int64_t(1) << 31) >> kRkTileBits);  // 8192 tiles of one segment
 constexpr int kRkGroups = 256;   // R1 workgroups drawing one segment's counts (count-matrix row length)
-constexpr int kRkList = 8192;    // R2: positions listed in LDS (denser tiles emit per thread)
+constexpr int kRkList = 4096;    // R2: positions of a quarter listed in LDS (denser quarters emit per thread)
 constexpr int kRkGU = 4;         // R2: list gathers in flight per thread
 constexpr int kRkWalkCap = 4096;  // cycle-walk bound (P(walk > 64) < 2^-64 per draw): a GPU loop must end
-static_assert(kRkWpt * 32 * kRkThreads == kRkTile, "bitmap geometry");
+static_assert(kRkWpt * 32 * kRkQThreads * kRkQ == kRkTile, "bitmap geometry");
 
 CHOCO_DEV __host__ uint64_t rk_derive(uint64_t K, uint64_t i) { return splitmix64_mix(K + (i + 1) * kGoldenGamma); }
 
@@ -200,24 +207,28 @@ CHOCO_DEV uint32_t pick_word(const uint32_t (&w)[kRkWpt], int q) {  // w[q] by s
   return r;
 }
 
-// R2: one tile -> its count and output offset (its rows of H and P), the bitmap
-// sample, the ordered emission with the gather.  Up to kRkList positions are
-// listed in LDS in ascending order and gathered by consecutive lanes (coalesced
-// stores, kRkGU loads in flight per thread); denser tiles emit per thread.
+// R2: one quarter of a tile -> the tile's count and output offset (its rows of H
+// and P), the quarter's bitmap (every draw of the tile is evaluated; the ones
+// below the quarter are counted, which places the quarter inside the tile without
+// any exchange between workgroups), the ordered emission with the gather.  Up to
+// kRkList positions are listed in LDS in ascending order and gathered by
+// consecutive lanes (coalesced stores, kRkGU loads in flight per thread); denser
+// quarters emit per thread.
 template <bool FLAT, bool XH>
-__global__ __launch_bounds__(kRkThreads) void randk_tile_kernel(const float* __restrict__ x, const float* __restrict__ xh,
-                                                                const int64_t* __restrict__ plan, int64_t rk_base,
-                                                                int64_t n, int64_t k, uint64_t key, int32_t is_biased,
-                                                                const uint32_t* __restrict__ H,
-                                                                const uint32_t* __restrict__ P,
-                                                                float* __restrict__ out_val,
-                                                                int32_t* __restrict__ out_idx) {
-  __shared__ uint32_t bm[kRkWords];
+__global__ __launch_bounds__(kRkQThreads) void randk_tile_kernel(const float* __restrict__ x, const float* __restrict__ xh,
+                                                                 const int64_t* __restrict__ plan, int64_t rk_base,
+                                                                 int64_t n, int64_t k, uint64_t key, int32_t is_biased,
+                                                                 const uint32_t* __restrict__ H,
+                                                                 const uint32_t* __restrict__ P,
+                                                                 float* __restrict__ out_val,
+                                                                 int32_t* __restrict__ out_idx) {
+  __shared__ uint32_t bm[kRkQWords];
   __shared__ uint32_t list[kRkList];
   __shared__ uint32_t scratch[40];
   const int tid = threadIdx.x;
-  const int64_t b = blockIdx.x;
-  RKSTAMP(8192 + b, 0);
+  const int64_t b = blockIdx.x / kRkQ;
+  const uint32_t qb = (uint32_t)(blockIdx.x % kRkQ) * (uint32_t)(kRkQWords * 32);  // quarter's first bit
+  RKSTAMP(8192 + blockIdx.x, 0);
   const RkTile T = FLAT ? rk_tile_flat(n, k, key, b) : rk_tile_seg(plan, rk_base, key, b);
   const int64_t start = T.t << kRkTileBits;  // within the segment
   const uint32_t L = (uint32_t)std::min<int64_t>(kRkTile, T.seg_len - start);
@@ -237,14 +248,17 @@ __global__ __launch_bounds__(kRkThreads) void randk_tile_kernel(const float* __r
     uint32_t x0, x1;
     block_excl_scan2(h, p, scratch, &x0, &x1, &c, &pre);
   }
-  RKSTAMP(8192 + b, 1);
-  // the c positions of this tile: a bitmap in LDS
+  RKSTAMP(8192 + blockIdx.x, 1);
+  if (qb >= L) return;  // a quarter past the segment's end (workgroup-uniform)
+  // the quarter's positions: a bitmap in LDS; `below` = the tile's positions before it
+  uint32_t below;
   if (all) {
 #pragma unroll
     for (int q = 0; q < kRkWpt; ++q) {
-      const uint32_t w0 = (uint32_t)(tid * kRkWpt + q) * 32u;
+      const uint32_t w0 = qb + (uint32_t)(tid * kRkWpt + q) * 32u;
       bm[tid * kRkWpt + q] = w0 + 32u <= L ? 0xFFFFFFFFu : (w0 >= L ? 0u : ((1u << (L - w0)) - 1u));
     }
+    below = qb;
     __syncthreads();
   } else {
 #pragma unroll
@@ -252,14 +266,20 @@ __global__ __launch_bounds__(kRkThreads) void randk_tile_kernel(const float* __r
     __syncthreads();
     RkPerm Pm;
     Pm.init(rk_derive(T.K, 8 + (uint64_t)T.t), L);
-    for (uint32_t j = tid; j < c; j += kRkThreads) {
-      const uint32_t p = Pm(j);
-      atomicOr(&bm[p >> 5], 1u << (p & 31u));
+    uint32_t nb = 0;
+    for (uint32_t j = tid; j < c; j += kRkQThreads) {
+      const uint32_t pos = Pm(j);
+      if (pos < qb) {
+        ++nb;
+      } else if (pos - qb < (uint32_t)(kRkQWords * 32)) {
+        const uint32_t p = pos - qb;
+        atomicOr(&bm[p >> 5], 1u << (p & 31u));
+      }
     }
-    __syncthreads();
+    block_excl_scan(nb, scratch, &below);  // (ends with a barrier: the bitmap is complete)
   }
-  RKSTAMP(8192 + b, 2);
-  // thread t owns bits [256 t, 256 t + 256): rank of its first set bit
+  RKSTAMP(8192 + blockIdx.x, 2);
+  // thread t owns bits [256 t, 256 t + 256) of the quarter: rank of its first set bit
   uint32_t w[kRkWpt];
   uint32_t mine = 0;
 #pragma unroll
@@ -267,52 +287,53 @@ __global__ __launch_bounds__(kRkThreads) void randk_tile_kernel(const float* __r
     w[q] = bm[tid * kRkWpt + q];
     mine += (uint32_t)__popc(w[q]);
   }
-  uint32_t tot;
-  uint32_t rank = block_excl_scan(mine, scratch, &tot);
-  RKSTAMP(8192 + b, 3);
+  uint32_t cq;
+  uint32_t rank = block_excl_scan(mine, scratch, &cq);
+  RKSTAMP(8192 + blockIdx.x, 3);
   const float scale = is_biased ? 1.0f : (float)((double)T.seg_len / (double)T.k);
-  const int64_t gbase = T.seg_off + start;                 // global index of the tile's first element
-  float* __restrict__ ov = out_val + T.out_off + pre;
-  int32_t* __restrict__ oi = out_idx + T.out_off + pre;
-  if (c <= (uint32_t)kRkList) {  // workgroup-uniform
+  const int64_t gbase = T.seg_off + start + qb;            // global index of the quarter's first element
+  const uint32_t room = c - min(below, c);                 // (bounded: never past the tile's count)
+  float* __restrict__ ov = out_val + T.out_off + pre + below;
+  int32_t* __restrict__ oi = out_idx + T.out_off + pre + below;
+  if (cq <= (uint32_t)kRkList) {  // workgroup-uniform
     // ascending positions -> list[rank ..], then lanes gather consecutive entries
     uint32_t r = rank;
 #pragma unroll
     for (int q = 0; q < kRkWpt; ++q) {
       uint32_t wq = w[q];
       while (wq != 0u) {
-        if (r < c) list[r] = (uint32_t)(tid * kRkWpt + q) * 32u + (uint32_t)__builtin_ctz(wq);
+        list[r] = (uint32_t)(tid * kRkWpt + q) * 32u + (uint32_t)__builtin_ctz(wq);
         ++r;
         wq &= wq - 1u;
       }
     }
     __syncthreads();
-    for (uint32_t i0 = 0; i0 < c; i0 += kRkThreads * kRkGU) {
+    for (uint32_t i0 = 0; i0 < cq; i0 += kRkQThreads * kRkGU) {
       uint32_t pos[kRkGU];
       float v[kRkGU];
 #pragma unroll
       for (int u = 0; u < kRkGU; ++u) {
-        const uint32_t i = i0 + (uint32_t)u * kRkThreads + (uint32_t)tid;
-        pos[u] = list[min(i, c - 1u)];
+        const uint32_t i = i0 + (uint32_t)u * kRkQThreads + (uint32_t)tid;
+        pos[u] = list[min(i, cq - 1u)];
       }
 #pragma unroll
       for (int u = 0; u < kRkGU; ++u) {
-        const uint32_t i = i0 + (uint32_t)u * kRkThreads + (uint32_t)tid;
+        const uint32_t i = i0 + (uint32_t)u * kRkQThreads + (uint32_t)tid;
         const int64_t e = gbase + pos[u];
         v[u] = 0.f;
-        if (i < c) v[u] = XH ? x[e] - xh[e] : x[e];
+        if (i < cq) v[u] = XH ? x[e] - xh[e] : x[e];
       }
 #pragma unroll
       for (int u = 0; u < kRkGU; ++u) {
-        const uint32_t i = i0 + (uint32_t)u * kRkThreads + (uint32_t)tid;
-        if (i < c) {
+        const uint32_t i = i0 + (uint32_t)u * kRkQThreads + (uint32_t)tid;
+        if (i < cq && i < room) {
           ov[i] = v[u] * scale;
           oi[i] = (int32_t)(gbase + pos[u]);
         }
       }
     }
   } else {
-    // dense tile: each thread emits its own ascending positions, kG gathers in flight
+    // dense quarter: each thread emits its own ascending positions, kG gathers in flight
     constexpr int kG = 8;
     int q = 0;
     uint32_t cur = w[0];
@@ -338,7 +359,7 @@ __global__ __launch_bounds__(kRkThreads) void randk_tile_kernel(const float* __r
       }
 #pragma unroll
       for (int i = 0; i < kG; ++i) {
-        if (ok[i] && rank + (uint32_t)i < c) {  // (bounded: never past the tile's count)
+        if (ok[i] && rank + (uint32_t)i < room) {
           ov[rank + i] = v[i] * scale;
           oi[rank + i] = (int32_t)(gbase + pos[i]);
         }
@@ -351,7 +372,7 @@ __global__ __launch_bounds__(kRkThreads) void randk_tile_kernel(const float* __r
   }
 #if CHOCO_STAMPS
   __syncthreads();
-  RKSTAMP(8192 + b, 4);
+  RKSTAMP(8192 + blockIdx.x, 4);
 #endif
 }
 
@@ -384,16 +405,16 @@ int randk_launch(const float* x, const float* xh, const int64_t* plan_dev, int64
   CHOCO_LAUNCHED("randk_count_kernel");
   profile_begin("randk_tile", st);
   if (flat && xh)
-    CHOCO_KLAUNCH((randk_tile_kernel<true, true>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
+    CHOCO_KLAUNCH((randk_tile_kernel<true, true>), dim3((unsigned)(R * kRkQ)), dim3(kRkQThreads), 0, st, x, xh, plan_dev,
                   rk_base, n, k, key, is_biased, H, P, out_val, out_idx);
   else if (flat)
-    CHOCO_KLAUNCH((randk_tile_kernel<true, false>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
+    CHOCO_KLAUNCH((randk_tile_kernel<true, false>), dim3((unsigned)(R * kRkQ)), dim3(kRkQThreads), 0, st, x, xh, plan_dev,
                   rk_base, n, k, key, is_biased, H, P, out_val, out_idx);
   else if (xh)
-    CHOCO_KLAUNCH((randk_tile_kernel<false, true>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
+    CHOCO_KLAUNCH((randk_tile_kernel<false, true>), dim3((unsigned)(R * kRkQ)), dim3(kRkQThreads), 0, st, x, xh, plan_dev,
                   rk_base, n, k, key, is_biased, H, P, out_val, out_idx);
   else
-    CHOCO_KLAUNCH((randk_tile_kernel<false, false>), dim3((unsigned)R), dim3(kRkThreads), 0, st, x, xh, plan_dev,
+    CHOCO_KLAUNCH((randk_tile_kernel<false, false>), dim3((unsigned)(R * kRkQ)), dim3(kRkQThreads), 0, st, x, xh, plan_dev,
                   rk_base, n, k, key, is_biased, H, P, out_val, out_idx);
   profile_end("randk_tile", st);
   CHOCO_LAUNCHED("randk_tile_kernel");
