@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libchoco_codec.so")
 
 TOPK_STATUS_OFFSET = 0        # CHOCO_TOPK_STATUS_OFFSET
+TOPK_FALLBACKS_OFFSET = 4     # CHOCO_TOPK_FALLBACKS_OFFSET
 TOPK_STATUS_POLL_TIMEOUT = 1  # CHOCO_TOPK_STATUS_POLL_TIMEOUT
 
 _c_i32, _c_i64, _c_u64, _c_f32, _c_f64 = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
@@ -60,6 +61,12 @@ SIGNATURES = {
     "choco_qsgd_decode": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _c_i32, _c_i32, _vp, _vp]),
     "choco_qsgd_decompress_accumulate": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i32, _c_i64, _vp, _c_i32,
                                                   _c_i32, _c_i32, _vp, _vp, _vp]),
+    "choco_qsgd_norms": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _vp, _vp, _c_sz, _vp]),
+    "choco_gossip_qsgd_norms": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _vp, _c_i32, _vp, _vp, _c_sz, _vp]),
+    "choco_qsgd_quantize_range": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _c_i32, _c_i32, _vp, _c_u64, _c_u64,
+                                           _c_i64, _c_i64, _vp, _vp]),
+    "choco_qsgd_decompress_accumulate_range": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i32, _c_i64, _vp, _c_i32,
+                                                        _c_i32, _c_i32, _c_i64, _c_i64, _vp, _vp, _vp]),
     "choco_gossip_step": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _vp]),
     "choco_gossip_topk_compress": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_gossip_topk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _c_f32, _vp, _p_i64, _c_i32, _vp, _vp, _vp,

@@ -127,6 +127,23 @@ def check_topk_status(wait=True):
         st.check(wait=wait)
 
 
+def topk_fallback_count(dev=None, plan=None):
+    """Diagnostic: calls on this stream's flat top-k workspace that took the exact fallback,
+    or (plan=...) segments of that plan whose warm window missed (include/choco_codec.h
+    CHOCO_TOPK_FALLBACKS_OFFSET).  Synchronises the stream."""
+    dev = torch.device(dev) if dev is not None else torch.device("cuda", torch.cuda.current_device())
+    if plan is not None:
+        ws = plan.workspace(dev)
+    else:
+        with _ws_lock:
+            ws = _ws_cache.get((dev.index, torch.cuda.current_stream(dev).cuda_stream, "topk"))
+        if ws is None:
+            return 0
+    off = _lib.TOPK_FALLBACKS_OFFSET
+    torch.cuda.current_stream(dev).synchronize()
+    return int(ws[off:off + 4].view(torch.int32).item())
+
+
 def workspace_bytes():
     """Device bytes held by the cached scratch buffers (top-k: ~9 bytes per element of
     the largest flat input, sized for 288 GB HBM rather than packed)."""
@@ -724,6 +741,92 @@ def qsgd_accumulate(messages, weights, self_slot, n, q, memory, xhat_self=None, 
                                                           _ptr(xhat_self if slot >= 0 else None), _ptr(memory),
                                                           _stream(memory.device)),
                    "choco_qsgd_decompress_accumulate")
+
+
+# ---- chunked QSGD wire (include/choco_codec.h "Chunked QSGD wire")
+QSGD_RANGE_ALIGN = 8192
+
+
+def qsgd_chunks(n, chunks):
+    """`chunks` element ranges [(e0, e1)] covering [0, n), starts aligned to 8192."""
+    per = -(-int(n) // max(1, int(chunks)))
+    per = -(-per // QSGD_RANGE_ALIGN) * QSGD_RANGE_ALIGN
+    return [(e, min(e + per, n)) for e in range(0, n, per)]
+
+
+def qsgd_chunked_wire(n, q, nseg, chunks, dev):
+    """One chunked QSGD message [fp32 norms (16-B padded) | range 0 | range 1 | ...], each
+    range a self-contained [level plane | sign plane]; returns (message, norms view,
+    [(e0, e1, range view)])."""
+    hb = 4 * wire_header_words(nseg)
+    ranges = qsgd_chunks(n, chunks)
+    offs = [hb]
+    for e0, e1 in ranges:
+        offs.append(offs[-1] + qsgd_packed_bytes(e1 - e0, q))
+    msg = torch.empty(offs[-1], dtype=torch.uint8, device=dev)
+    msg[:hb].zero_()
+    parts = [(e0, e1, msg[offs[i]:offs[i + 1]]) for i, (e0, e1) in enumerate(ranges)]
+    return msg, msg[:hb].view(torch.float32)[:nseg], parts
+
+
+def qsgd_norms(x, xhat=None, seg_off=None, nseg=1, gossip=None, out=None):
+    """The QSGD norm pass alone (per-segment ||x - xhat||_2, fp64, rounded once);
+    `gossip=(memory, gamma)` applies the consensus step to x in the same pass."""
+    _require(x, torch.float32, "x")
+    if xhat is not None:
+        _require(xhat, torch.float32, "xhat")
+    dev = x.device
+    norms = out if out is not None else torch.empty(nseg, dtype=torch.float32, device=dev)
+    _require(norms, torch.float32, "norms")
+    L = lib()
+    ws = workspace(dev, "acc", L.choco_qsgd_workspace_size(nseg))
+    g = _gossip(gossip, x, xhat)
+    if g is not None:
+        _lib.check(L.choco_gossip_qsgd_norms(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1], x.numel(), _ptr(seg_off),
+                                             int(nseg), _ptr(norms), _ptr(ws), ws.numel(), _stream(dev)),
+                   "choco_gossip_qsgd_norms")
+    else:
+        _lib.check(L.choco_qsgd_norms(_ptr(x), _ptr(xhat), x.numel(), _ptr(seg_off), int(nseg), _ptr(norms),
+                                      _ptr(ws), ws.numel(), _stream(dev)), "choco_qsgd_norms")
+    return norms
+
+
+def qsgd_quantize_range(x, q, norms, e0, e1, packed_range, is_biased=False, xhat=None, seg_off=None, nseg=1,
+                        seed=0, offset=0):
+    """Quantize elements [e0, e1) into `packed_range` (qsgd_packed_bytes(e1 - e0, q) bytes)."""
+    _require(x, torch.float32, "x")
+    _require(norms, torch.float32, "norms")
+    _require(packed_range, torch.uint8, "packed_range")
+    if packed_range.numel() != qsgd_packed_bytes(e1 - e0, q):
+        raise RuntimeError("packed_range must hold qsgd_packed_bytes(e1 - e0, q) bytes")
+    _lib.check(lib().choco_qsgd_quantize_range(_ptr(x), _ptr(xhat), x.numel(), _ptr(seg_off), int(nseg), int(q),
+                                               1 if is_biased else 0, _ptr(norms), int(seed) & (2**64 - 1),
+                                               int(offset) & (2**64 - 1), int(e0), int(e1), _ptr(packed_range),
+                                               _stream(x.device)), "choco_qsgd_quantize_range")
+
+
+def qsgd_accumulate_range(messages, weights, self_slot, n, q, memory, e0, e1, xhat_self=None, is_biased=False,
+                          seg_off=None, nseg=1):
+    """qsgd_accumulate over elements [e0, e1); messages: list of (range message, norms)."""
+    _require(memory, torch.float32, "memory")
+    _check_layout(memory, xhat_self, n, seg_off, nseg)
+    if len(messages) != len(weights):
+        raise RuntimeError("one weight per message")
+    nbytes = qsgd_packed_bytes(e1 - e0, q)
+    for p, nm in messages:
+        _require(p, torch.uint8, "packed")
+        _require(nm, torch.float32, "norms")
+        if p.numel() != nbytes or nm.numel() != nseg:
+            raise RuntimeError(f"QSGD range message must hold {nbytes} bytes and {nseg} norms")
+    for c0, c1, slot in _msg_chunks(len(messages), int(self_slot)):
+        part = messages[c0:c1]
+        pp, keep1 = _lib.ptr_array([p.data_ptr() for p, _ in part])
+        nn, keep2 = _lib.ptr_array([nm.data_ptr() for _, nm in part])
+        ww, keep3 = _lib.f32_array([float(w) for w in weights[c0:c1]])
+        _lib.check(lib().choco_qsgd_decompress_accumulate_range(
+            pp, nn, ww, len(part), slot, int(n), _ptr(seg_off), int(nseg), int(q), 1 if is_biased else 0, int(e0),
+            int(e1), _ptr(xhat_self if slot >= 0 else None), _ptr(memory), _stream(memory.device)),
+            "choco_qsgd_decompress_accumulate_range")
 
 
 def qsgd_extrapolate(packed, norms, n, q, target, a, b, is_biased=False, seg_off=None, nseg=1):

@@ -401,18 +401,20 @@ __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, const int64_t* __restrict__ seg_off,
     int nseg, int s_levels, int biased, const float* __restrict__ norms, const float* __restrict__ u_in,
     uint64_t seed, uint64_t offset, uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
-    float* __restrict__ dense_out, int64_t ntiles) {
+    float* __restrict__ dense_out, int64_t tile_lo, int64_t tile_cnt, int64_t pad_e0, int64_t pad_len) {
   __shared__ int s_seg[2];
-  const int64_t tile = ntiles - 1 - (int64_t)blockIdx.x;  // reverse walk: Infinity-Cache hits
+  // tiles [tile_lo, tile_lo + tile_cnt) of the buffer, walked in reverse (Infinity-Cache hits)
+  const int64_t tile = tile_lo + tile_cnt - 1 - (int64_t)blockIdx.x;
   const int64_t t_e0 = tile * kQStreamTile;
   const int64_t t_e1 = std::min<int64_t>(t_e0 + kQStreamTile, n);
   const int sg0 = tile_seg(seg_off, nseg, t_e0, t_e1, s_seg);
   const bool uniform = s_seg[1] == sg0;
-  if (tile == ntiles - 1) {
-    // the wire is fully defined: zero the 16-byte padding tails of both planes
-    const int64_t groups = (n + kQPer - 1) / kQPer;
-    const int64_t lvl_used = groups * CW, lvl_end = (lvl_used + 15) / 16 * 16;
-    const int64_t sgn_used = groups, sgn_end = (sgn_used + 15) / 16 * 16;
+  if (blockIdx.x == 0) {
+    // the planes of elements [pad_e0, pad_e0 + pad_len) are fully defined: zero their
+    // 16-byte padding tails (the planes are indexed by absolute element group)
+    const int64_t g0 = pad_e0 / kQPer, groups = (pad_len + kQPer - 1) / kQPer;
+    const int64_t lvl_used = (g0 + groups) * CW, lvl_end = g0 * CW + (groups * CW + 15) / 16 * 16;
+    const int64_t sgn_used = g0 + groups, sgn_end = g0 + (groups + 15) / 16 * 16;
     for (int64_t b = lvl_used + threadIdx.x; b < lvl_end; b += kQThreads) lvl_plane[b] = 0;
     for (int64_t b = sgn_used + threadIdx.x; b < sgn_end; b += kQThreads) sign_plane[b] = 0;
   }
@@ -545,9 +547,10 @@ template <int CW, int NM, int MODE>
 __global__ __launch_bounds__(kQThreads) void qsgd_decode_kernel(QMsgs M, int64_t n,
                                                                 const int64_t* __restrict__ seg_off, int nseg,
                                                                 int s_levels, int biased,
-                                                                float* __restrict__ hat, float* __restrict__ mem) {
+                                                                float* __restrict__ hat, float* __restrict__ mem,
+                                                                int64_t blk_lo) {
   __shared__ int s_seg[2];
-  const int64_t t_e0 = (int64_t)blockIdx.x * kQTile;
+  const int64_t t_e0 = (blk_lo + (int64_t)blockIdx.x) * kQTile;
   const int64_t t_e1 = std::min<int64_t>(t_e0 + kQTile, n);
   const int sg0 = tile_seg(seg_off, nseg, t_e0, t_e1, s_seg);
   const bool uniform = s_seg[1] == sg0;
@@ -621,38 +624,40 @@ __global__ __launch_bounds__(kQThreads) void qsgd_decode_kernel(QMsgs M, int64_t
   }
 }
 
+// Elements [e0, e1) (e0 a multiple of kQTile; e1 a multiple of it or n).
 template <int CW, int NM, int MODE>
 static void launch_decode(const QMsgs& M, int64_t n, const int64_t* seg_off, int nseg, int s_levels, int biased,
-                          float* hat, float* mem, hipStream_t st) {
-  const unsigned grid = (unsigned)((n + kQTile - 1) / kQTile);
+                          float* hat, float* mem, hipStream_t st, int64_t e0, int64_t e1) {
+  const unsigned grid = (unsigned)((e1 - e0 + kQTile - 1) / kQTile);
   CHOCO_KLAUNCH((qsgd_decode_kernel<CW, NM, MODE>), dim3(grid), dim3(kQThreads), 0, st, M, n, seg_off, nseg,
-                     s_levels, biased, hat, mem);
+                     s_levels, biased, hat, mem, e0 / kQTile);
 }
 
 template <int CW, int MODE>
 static void launch_decode_nm(const QMsgs& M, int64_t n, const int64_t* seg_off, int nseg, int s_levels,
-                             int biased, float* hat, float* mem, hipStream_t st) {
+                             int biased, float* hat, float* mem, hipStream_t st, int64_t e0, int64_t e1) {
   switch (M.nmsg) {
-    case 1: launch_decode<CW, 1, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
-    case 2: launch_decode<CW, 2, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
-    case 3: launch_decode<CW, 3, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
-    case 4: launch_decode<CW, 4, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
-    case 5: launch_decode<CW, 5, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
-    case 6: launch_decode<CW, 6, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
-    case 7: launch_decode<CW, 7, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
-    default: launch_decode<CW, 8, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+    case 1: launch_decode<CW, 1, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st, e0, e1); break;
+    case 2: launch_decode<CW, 2, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st, e0, e1); break;
+    case 3: launch_decode<CW, 3, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st, e0, e1); break;
+    case 4: launch_decode<CW, 4, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st, e0, e1); break;
+    case 5: launch_decode<CW, 5, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st, e0, e1); break;
+    case 6: launch_decode<CW, 6, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st, e0, e1); break;
+    case 7: launch_decode<CW, 7, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st, e0, e1); break;
+    default: launch_decode<CW, 8, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st, e0, e1); break;
   }
 }
 
 template <int MODE>
 static void launch_decode_cw(int cw, const QMsgs& M, int64_t n, const int64_t* seg_off, int nseg, int s_levels,
-                             int biased, float* hat, float* mem, hipStream_t st) {
+                             int biased, float* hat, float* mem, hipStream_t st, int64_t e0 = 0, int64_t e1 = -1) {
+  if (e1 < 0) e1 = n;
   switch (cw) {
-    case 1: launch_decode_nm<1, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
-    case 2: launch_decode_nm<2, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
-    case 4: launch_decode_nm<4, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
-    case 8: launch_decode_nm<8, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
-    default: launch_decode_nm<16, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st); break;
+    case 1: launch_decode_nm<1, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st, e0, e1); break;
+    case 2: launch_decode_nm<2, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st, e0, e1); break;
+    case 4: launch_decode_nm<4, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st, e0, e1); break;
+    case 8: launch_decode_nm<8, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st, e0, e1); break;
+    default: launch_decode_nm<16, MODE>(M, n, seg_off, nseg, s_levels, biased, hat, mem, st, e0, e1); break;
   }
 }
 
@@ -669,57 +674,55 @@ CHOCO_API size_t choco_qsgd_workspace_size(int32_t nseg) {
   return 256 + align_up((size_t)(nseg > 0 ? nseg : 1) * sizeof(double), 256);
 }
 
-static int qsgd_compress(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
-                         int32_t q, int32_t is_biased, const float* norm_in, const float* u_in, uint64_t seed,
-                         uint64_t offset, uint8_t* packed, float* norms_out, float* dense_out, void* ws,
-                         size_t ws_bytes, hipStream_t st, Gossip gs) {
-  CHOCO_REQUIRE(x && packed, "null pointer argument");
-  CHOCO_REQUIRE(!gs.mem || (xhat && aligned16(gs.mem)), "the gossip step needs x_hat and a 16-byte aligned memory");
-  CHOCO_REQUIRE(q >= 1 && q <= 16, "quantize level q must be in [1, 16] (q = 32 is a passthrough), got %d", q);
+static int qsgd_check(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg) {
+  CHOCO_REQUIRE(x, "null pointer argument");
   CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
   CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
-  CHOCO_REQUIRE(aligned16(x) && (!xhat || aligned16(xhat)) && aligned16(packed) &&
-                    (!dense_out || aligned16(dense_out)),
-                "buffers must be 16-byte aligned");
+  CHOCO_REQUIRE(aligned16(x) && (!xhat || aligned16(xhat)), "buffers must be 16-byte aligned");
+  return CHOCO_OK;
+}
+
+// The norm pass (per-segment ||d||_2, fp64, rounded once); gs: the fused gossip step.
+static int qsgd_norms_launch(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
+                             float* norms_out, void* ws, size_t ws_bytes, hipStream_t st, Gossip gs) {
+  CHOCO_REQUIRE(!gs.mem || (xhat && aligned16(gs.mem)), "the gossip step needs x_hat and a 16-byte aligned memory");
+  CHOCO_REQUIRE(norms_out, "norms_out is required when norm_in is NULL");
+  CHOCO_REQUIRE(ws && ws_bytes >= choco_qsgd_workspace_size(nseg), "qsgd workspace too small");
+  const unsigned g1 = (unsigned)((n + kNormTile - 1) / kNormTile);
+  QsgdWs* w = static_cast<QsgdWs*>(ws);
+  profile_begin("qsgd_norm", st);
+  if (gs.mem)
+    CHOCO_KLAUNCH((qsgd_norm_kernel<true, true>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
+                  norms_out, w, gs);
+  else if (xhat)
+    CHOCO_KLAUNCH((qsgd_norm_kernel<true>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
+                  norms_out, w, gs);
+  else
+    CHOCO_KLAUNCH((qsgd_norm_kernel<false>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
+                  norms_out, w, gs);
+  profile_end("qsgd_norm", st);
+  CHOCO_LAUNCHED("qsgd_norm_kernel");
+  return CHOCO_OK;
+}
+
+// The quantize pass over elements [e0, e1) into planes indexed by ABSOLUTE element
+// group (lvl_plane / sign_plane point at element 0's group; a range call writes
+// only the groups of its elements, plus the 16-byte padding of a plane that ends
+// at e1).
+static int qsgd_quant_launch(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
+                             int32_t q, int32_t is_biased, const float* norms, const float* u_in, uint64_t seed,
+                             uint64_t offset, uint8_t* lvl_plane, uint8_t* sign_plane, float* dense_out,
+                             int64_t e0, int64_t e1, int64_t pad_e0, hipStream_t st) {
   const int cw = container_bits(q);
   const int s_levels = (1 << q) - 1;
-  const float* norms = norm_in;
-  if (!norms) {
-    CHOCO_REQUIRE(norms_out, "norms_out is required when norm_in is NULL");
-    CHOCO_REQUIRE(ws && ws_bytes >= choco_qsgd_workspace_size(nseg), "qsgd workspace too small");
-    const unsigned g1 = (unsigned)((n + kNormTile - 1) / kNormTile);
-    QsgdWs* w = static_cast<QsgdWs*>(ws);
-    profile_begin("qsgd_norm", st);
-    if (gs.mem)
-      CHOCO_KLAUNCH((qsgd_norm_kernel<true, true>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
-                    norms_out, w, gs);
-    else if (xhat)
-      CHOCO_KLAUNCH((qsgd_norm_kernel<true>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
-                    norms_out, w, gs);
-    else
-      CHOCO_KLAUNCH((qsgd_norm_kernel<false>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
-                    norms_out, w, gs);
-    profile_end("qsgd_norm", st);
-    CHOCO_LAUNCHED("qsgd_norm_kernel");
-    norms = norms_out;
-  } else {
-    // pinned norms (parity mode): no norm pass to fuse the gossip step into
-    if (gs.mem) {
-      const int rc = gossip_launch(const_cast<float*>(x), gs.mem, xhat, gs.gamma, n, st);
-      if (rc) return rc;
-    }
-    if (norms_out && norms_out != norm_in)
-      CHOCO_HIP(hipMemcpyAsync(norms_out, norm_in, sizeof(float) * nseg, hipMemcpyDeviceToDevice, st));
-  }
-  uint8_t* lvl_plane = packed;
-  uint8_t* sign_plane = packed + plane_bytes(n, cw);
-  const int64_t ntiles = (n + kQStreamTile - 1) / kQStreamTile;
+  const int64_t tile_lo = e0 / kQStreamTile;
+  const int64_t tile_cnt = (e1 - e0 + kQStreamTile - 1) / kQStreamTile;
   profile_begin("qsgd_quantize", st);
 #define CHOCO_Q(CWV)                                                                                          \
   case CWV:                                                                                                   \
-    CHOCO_KLAUNCH((qsgd_quant_kernel<CWV>), dim3((unsigned)ntiles), dim3(kQThreads), 0, st, x, xhat, n,      \
+    CHOCO_KLAUNCH((qsgd_quant_kernel<CWV>), dim3((unsigned)tile_cnt), dim3(kQThreads), 0, st, x, xhat, n,    \
                   seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane, sign_plane,        \
-                  dense_out, ntiles);                                                                         \
+                  dense_out, tile_lo, tile_cnt, pad_e0, e1 - pad_e0);                                         \
     break;
   switch (cw) {
     CHOCO_Q(1)
@@ -732,6 +735,50 @@ static int qsgd_compress(const float* x, const float* xhat, int64_t n, const int
   profile_end("qsgd_quantize", st);
   CHOCO_LAUNCHED("qsgd_quant_kernel");
   return CHOCO_OK;
+}
+
+static int qsgd_compress(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
+                         int32_t q, int32_t is_biased, const float* norm_in, const float* u_in, uint64_t seed,
+                         uint64_t offset, uint8_t* packed, float* norms_out, float* dense_out, void* ws,
+                         size_t ws_bytes, hipStream_t st, Gossip gs) {
+  CHOCO_REQUIRE(x && packed, "null pointer argument");
+  CHOCO_REQUIRE(q >= 1 && q <= 16, "quantize level q must be in [1, 16] (q = 32 is a passthrough), got %d", q);
+  if (int rc = qsgd_check(x, xhat, n, seg_off, nseg)) return rc;
+  CHOCO_REQUIRE(aligned16(packed) && (!dense_out || aligned16(dense_out)), "buffers must be 16-byte aligned");
+  const int cw = container_bits(q);
+  const float* norms = norm_in;
+  if (!norms) {
+    if (int rc = qsgd_norms_launch(x, xhat, n, seg_off, nseg, norms_out, ws, ws_bytes, st, gs)) return rc;
+    norms = norms_out;
+  } else {
+    // pinned norms (parity mode): no norm pass to fuse the gossip step into
+    CHOCO_REQUIRE(!gs.mem || (xhat && aligned16(gs.mem)), "the gossip step needs x_hat and a 16-byte aligned memory");
+    if (gs.mem) {
+      const int rc = gossip_launch(const_cast<float*>(x), gs.mem, xhat, gs.gamma, n, st);
+      if (rc) return rc;
+    }
+    if (norms_out && norms_out != norm_in)
+      CHOCO_HIP(hipMemcpyAsync(norms_out, norm_in, sizeof(float) * nseg, hipMemcpyDeviceToDevice, st));
+  }
+  return qsgd_quant_launch(x, xhat, n, seg_off, nseg, q, is_biased, norms, u_in, seed, offset, packed,
+                           packed + plane_bytes(n, cw), dense_out, 0, n, 0, st);
+}
+
+// A range [e0, e1) of a chunked wire: e0 a multiple of kQStreamTile, e1 one too or n.
+static int qsgd_range_ok(int64_t n, int64_t e0, int64_t e1) {
+  CHOCO_REQUIRE(e0 >= 0 && e0 < e1 && e1 <= n && e0 % kQStreamTile == 0 && (e1 % kQStreamTile == 0 || e1 == n),
+                "range [%lld, %lld) of n=%lld: e0 must be a multiple of %d, e1 one too or n", (long long)e0,
+                (long long)e1, (long long)n, kQStreamTile);
+  return CHOCO_OK;
+}
+
+// The planes of a range message (packed_range = [level plane | sign plane] of e1 - e0
+// elements, choco_qsgd_packed_bytes(e1 - e0, q) bytes) as absolute-group pointers.
+static void range_planes(const uint8_t* packed_range, int64_t e0, int64_t len, int cw, const uint8_t** lvl,
+                         const uint8_t** sgn) {
+  const uintptr_t base = reinterpret_cast<uintptr_t>(packed_range);
+  *lvl = reinterpret_cast<const uint8_t*>(base - (uintptr_t)((e0 / kQPer) * cw));
+  *sgn = reinterpret_cast<const uint8_t*>(base + (uintptr_t)plane_bytes(len, cw) - (uintptr_t)(e0 / kQPer));
 }
 
 CHOCO_API int choco_qsgd_compress(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
@@ -749,6 +796,72 @@ CHOCO_API int choco_gossip_qsgd_compress(float* x, const float* memory, const fl
   CHOCO_REQUIRE(memory != nullptr && xhat != nullptr, "the gossip step needs memory and x_hat");
   return qsgd_compress(x, xhat, n, seg_off, nseg, q, is_biased, nullptr, nullptr, seed, offset, packed, norms_out,
                        dense_out, ws, ws_bytes, as_stream(stream), Gossip{memory, gamma});
+}
+
+CHOCO_API int choco_qsgd_norms(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
+                               float* norms_out, void* ws, size_t ws_bytes, void* stream) {
+  if (int rc = qsgd_check(x, xhat, n, seg_off, nseg)) return rc;
+  return qsgd_norms_launch(x, xhat, n, seg_off, nseg, norms_out, ws, ws_bytes, as_stream(stream),
+                           Gossip{nullptr, 0.f});
+}
+
+CHOCO_API int choco_gossip_qsgd_norms(float* x, const float* memory, const float* xhat, float gamma, int64_t n,
+                                      const int64_t* seg_off, int32_t nseg, float* norms_out, void* ws,
+                                      size_t ws_bytes, void* stream) {
+  CHOCO_REQUIRE(memory != nullptr && xhat != nullptr, "the gossip step needs memory and x_hat");
+  if (int rc = qsgd_check(x, xhat, n, seg_off, nseg)) return rc;
+  return qsgd_norms_launch(x, xhat, n, seg_off, nseg, norms_out, ws, ws_bytes, as_stream(stream),
+                           Gossip{memory, gamma});
+}
+
+CHOCO_API int choco_qsgd_quantize_range(const float* x, const float* xhat, int64_t n, const int64_t* seg_off,
+                                        int32_t nseg, int32_t q, int32_t is_biased, const float* norms,
+                                        uint64_t seed, uint64_t offset, int64_t e0, int64_t e1,
+                                        uint8_t* packed_range, void* stream) {
+  CHOCO_REQUIRE(norms && packed_range, "null pointer argument");
+  CHOCO_REQUIRE(q >= 1 && q <= 16, "quantize level q must be in [1, 16], got %d", q);
+  if (int rc = qsgd_check(x, xhat, n, seg_off, nseg)) return rc;
+  if (int rc = qsgd_range_ok(n, e0, e1)) return rc;
+  CHOCO_REQUIRE(aligned16(packed_range), "packed_range must be 16-byte aligned");
+  const int cw = container_bits(q);
+  const uint8_t *lvl, *sgn;
+  range_planes(packed_range, e0, e1 - e0, cw, &lvl, &sgn);
+  return qsgd_quant_launch(x, xhat, n, seg_off, nseg, q, is_biased, norms, nullptr, seed, offset,
+                           const_cast<uint8_t*>(lvl), const_cast<uint8_t*>(sgn), nullptr, e0, e1, e0,
+                           as_stream(stream));
+}
+
+CHOCO_API int choco_qsgd_decompress_accumulate_range(const uint8_t* const* packed_list,
+                                                     const float* const* norms_list, const float* weights,
+                                                     int32_t nmsg, int32_t self_slot, int64_t n,
+                                                     const int64_t* seg_off, int32_t nseg, int32_t q,
+                                                     int32_t is_biased, int64_t e0, int64_t e1, float* xhat_self,
+                                                     float* memory, void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(packed_list && norms_list && weights && memory, "null pointer argument");
+  CHOCO_REQUIRE(nmsg >= 1 && nmsg <= kQMaxMsg, "nmsg must be in [1, %d]", kQMaxMsg);
+  CHOCO_REQUIRE(self_slot >= -1 && self_slot < nmsg, "bad self_slot");
+  CHOCO_REQUIRE(q >= 1 && q <= 16, "q must be in [1, 16]");
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
+  CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
+  CHOCO_REQUIRE(aligned16(memory) && (!xhat_self || aligned16(xhat_self)), "buffers must be 16-byte aligned");
+  if (int rc = qsgd_range_ok(n, e0, e1)) return rc;
+  const int cw = container_bits(q);
+  QMsgs M{};
+  for (int m = 0; m < nmsg; ++m) {
+    CHOCO_REQUIRE(packed_list[m] && norms_list[m], "null message pointer");
+    CHOCO_REQUIRE(aligned16(packed_list[m]), "packed messages must be 16-byte aligned");
+    range_planes(packed_list[m], e0, e1 - e0, cw, &M.lvl[m], &M.sgn[m]);
+    M.norms[m] = norms_list[m];
+    M.w[m] = weights[m];
+  }
+  M.nmsg = nmsg;
+  M.self_slot = self_slot;
+  profile_begin("qsgd_accumulate", st);
+  launch_decode_cw<1>(cw, M, n, seg_off, nseg, (1 << q) - 1, is_biased, xhat_self, memory, st, e0, e1);
+  profile_end("qsgd_accumulate", st);
+  CHOCO_LAUNCHED("qsgd_decode_kernel");
+  return CHOCO_OK;
 }
 
 CHOCO_API int choco_qsgd_decode(const uint8_t* packed, const float* norms, int64_t n, const int64_t* seg_off,

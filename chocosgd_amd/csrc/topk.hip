@@ -142,7 +142,10 @@ struct TopkBounds {
 // another kernel of call c still reads.
 struct TopkCtrl {
   uint32_t status;                               // sticky error bits (kStatus*), read by the host lazily
-  uint32_t pad0[15];
+  uint32_t fallbacks;                            // calls that took the exact fallback (diagnostic counter)
+  uint32_t cold_left;                            // warm-host calls still to sample their window in K2 (backoff)
+  uint32_t backoff;                              // cold run length after the next warm miss
+  uint32_t pad0[12];
   uint32_t overflow[2];                          // bit 0: a side list overflowed; bit 1: take the exact fallback
   uint32_t pad1[14];
   TopkBounds bounds[2];
@@ -150,6 +153,7 @@ struct TopkCtrl {
   uint32_t G[2][kNRep][kNBucket];                // replicated bucket suffix totals
 };
 static_assert(offsetof(TopkCtrl, status) == CHOCO_TOPK_STATUS_OFFSET, "status word at the documented offset");
+static_assert(offsetof(TopkCtrl, fallbacks) == CHOCO_TOPK_FALLBACKS_OFFSET, "fallback counter at the documented offset");
 constexpr uint32_t kStatusPollTimeout = 1u;    // a bounded wait of the exact fallback gave up: output invalid
 constexpr uint32_t kNoCandKey = 0x7F800000u;   // window that admits only inf / NaN keys (invalid bounds)
 
@@ -381,6 +385,7 @@ struct StreamSmem {
   uint32_t trash_i[64];
   union {
     uint2 pairs[kK2Waves * kPairsPerWave];  // (value bits, index) per candidate, per-wave regions
+    SampleHist sh;                          // the prologue's sample window (cold calls only)
   } u;
   uint32_t cmeta[kMaxTileChunks];  // per chunk: LDS start | LDS count << 16
   uint32_t ccnt[kMaxTileChunks + 1];  // per chunk: candidates; at tile end their exclusive prefix
@@ -782,6 +787,42 @@ __global__ __launch_bounds__(kK1Threads) void topk_bounds_kernel(const float* __
   STAMP(30000, 2);
 }
 
+// K1's window computed inside K2's prologue (a warm-host call on a cold run): every
+// workgroup takes the same sample and finds the same bounds.  The sample's loads queue
+// behind the first prefetch of 255 CUs, so this costs ~10 us against K1's ~7 -- paid
+// only on the calls of a cold run, never on a warm call.
+struct SampleView {
+  SampleHist& sh;
+  uint32_t* scratch;
+  uint32_t* bc;
+};
+template <bool XH, bool GS>
+CHOCO_DEV Buckets prologue_sample(const float* __restrict__ x, const float* __restrict__ xh, const Gossip& gs,
+                                  int64_t n, const SampleRanks& ranks, int lane, int w, SampleView& sv, bool* deg) {
+  static_assert(kK2Threads == kK1Threads, "the K1 sample geometry");
+  float4 s[kSampleLoads], sh[kSampleLoads], sm_[kSampleLoads];
+  load_sample<XH, GS>(x, xh, gs.mem, n, s, sh, sm_);
+  uint32_t kk[kSampleLoads * 4];
+#pragma unroll
+  for (int j = 0; j < kSampleLoads; ++j) {
+    float4 v = s[j];
+    if (GS) v = gossip4(v, sm_[j], sh[j], gs.gamma);
+    if (XH) { v.x -= sh[j].x; v.y -= sh[j].y; v.z -= sh[j].z; v.w -= sh[j].w; }
+    kk[4 * j + 0] = fkey(v.x); kk[4 * j + 1] = fkey(v.y); kk[4 * j + 2] = fkey(v.z); kk[4 * j + 3] = fkey(v.w);
+  }
+  uint32_t s_lo;
+  uint64_t s_hi_est;
+  sample_bounds(kk, ranks, lane, w, sv, s_lo, s_hi_est);
+  const Buckets bk = make_buckets(s_lo, s_hi_est, 0);
+  uint32_t nmaybe = 0;
+#pragma unroll
+  for (int j = 0; j < kSampleLoads * 4; ++j) nmaybe += (kk[j] >= bk.s_lo && kk[j] < bk.s_hi) ? 1u : 0u;
+  uint32_t tot_maybe;
+  block_excl_scan(nmaybe, sv.scratch, &tot_maybe);
+  *deg = tot_maybe > (uint32_t)(kSampleN / 4);
+  return bk;
+}
+
 // Random-k (MODE kHash): keys are uniform on [0, 2^31) and (s_lo, s_hi) come from
 // the binomial tails (host), passed as hs_lo / hs_hi.
 // GS (kData, XH): the fused gossip step -- the stream reads x, memory and xh,
@@ -791,7 +832,8 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
     uint32_t par, uint32_t side_cap, uint64_t seed, uint32_t hs_lo, uint64_t hs_hi, TopkCtrl* __restrict__ ctrl,
     uint32_t* __restrict__ cum_tab, uint32_t* __restrict__ cntw, uint32_t* __restrict__ side,
-    float* __restrict__ cval, uint32_t* __restrict__ cidx, uint32_t* __restrict__ tinfo, Gossip gs) {
+    float* __restrict__ cval, uint32_t* __restrict__ cidx, uint32_t* __restrict__ tinfo, Gossip gs,
+    SampleRanks ranks, uint32_t sample_if_cold) {
   static_assert(!GS || (MODE == kData && XH), "the gossip step needs x_hat and data keys");
   __shared__ StreamSmem sm;
   STAMP(1024 + blockIdx.x, 0);
@@ -830,15 +872,42 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     if (!GS) load_rows_full<XH>(ts, batch0(c), lane, A);
     if (kTwoChunks) load_rows_full<XH>(ts, batch0(c + kK2Waves), lane, B);
     else if (!kOneBatch && !XH) load_rows_full<XH>(ts, batch1(c), lane, B);
-    // this call's window: K1's sample (cold call) or the previous call's (warm call)
+    // this call's window: K1's sample (cold call), the previous call's (warm call), or --
+    // when the host skipped K1 but the window is stale or a warm miss put this workspace
+    // on a cold run (cold_left, set by K34) -- a sample taken here by every workgroup
     const TopkBounds W = ctrl->bounds[par];
-    const bool ok = W.valid != 0u && W.n == n && W.k == k && W.shift < 32u;
-    bk = ok ? make_buckets_from(W.s_lo, W.s_hi, W.shift, seed) : make_buckets_from(kNoCandKey, kNoCandKey, 0u, seed);
+    const uint32_t cold_left = ctrl->cold_left;
+    bool ok = W.valid != 0u && W.n == n && W.k == k && W.shift < 32u;
+    bool degenerate = false;
+    if (sample_if_cold && (!ok || cold_left != 0u)) {  // grid-uniform
+      SampleView sv{sm.u.sh, sm.scratch, sm.bc};
+      bool deg;
+      const Buckets sb = prologue_sample<XH, GS>(x, xh, gs, n, ranks, lane, w, sv, &deg);
+      __syncthreads();  // the union is the pairs region again
+      bk = make_buckets_from(sb.s_lo, sb.s_hi, sb.shift, seed);
+      ok = true;
+      degenerate = deg;
+      if (b == 0 && tid == 0) {  // K34 reads this call's window from the control block
+        TopkBounds& B = ctrl->bounds[par];
+        B.s_lo = sb.s_lo;
+        B.s_hi = sb.s_hi;
+        B.shift = sb.shift;
+        B.m1024 = 0u;
+        B.n = n;
+        B.k = k;
+        B.valid = 1u;
+        if (deg) atomicOr(&ctrl->overflow[par], 2u);
+      }
+    } else {
+      bk = ok ? make_buckets_from(W.s_lo, W.s_hi, W.shift, seed) : make_buckets_from(kNoCandKey, kNoCandKey, 0u, seed);
+      degenerate = (ctrl->overflow[par] & 2u) != 0u;
+    }
     // no window for this (n, k) (a workspace the host believed warm): the exact fallback
     if (!ok && b == 0 && tid == 0) atomicOr(&ctrl->overflow[par], 2u);
-    // K1 flagged a degenerate sample: K34 will take the exact fallback, which needs
-    // nothing from this kernel (with the fused gossip step the stream must still run)
-    if (!GS && (!ok || (ctrl->overflow[par] & 2u) != 0u)) return;
+    // a degenerate sample (K1's flag, or this prologue's): K34 will take the exact
+    // fallback, which needs nothing from this kernel (with the fused gossip step the
+    // stream must still run)
+    if (!GS && (!ok || degenerate)) return;
   } else {
     bk = make_buckets(hs_lo, hs_hi, seed);
   }
@@ -1561,6 +1630,7 @@ CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uin
 // window are extrapolated from its density (G[0] - k keys over [s_lo, T]).
 // Wave 0 of one workgroup; ~0.3 us, after that workgroup's emission.
 // ----------------------------------------------------------------------------
+constexpr uint32_t kColdMin = 32, kColdMax = 1024;  // cold-run lengths after a warm miss
 constexpr uint32_t kWarmM0 = 20;     // ~2 % of k (the bench's randn deltas drift ~0.1 %)
 constexpr uint32_t kWarmMMax = 512;  // 50 %
 CHOCO_DEV void next_window(const uint32_t* G, uint32_t s_lo, uint32_t s_hi, uint32_t shift, uint32_t m_prev,
@@ -1689,6 +1759,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   STAMP(26000 + b, 2);
   if (!fallback && fs.G[jstar] - fs.G[jstar + 1] > (uint32_t)kMCap) fallback = true;
   if (fallback) {
+    if (b == 0 && tid == 0) atomicAdd(&ctrl->fallbacks, 1u);
     // the sample's guess was off: the exact radix select over the whole input, shared
     // by every workgroup through the ticketed queue (wide_fallback)
     Src<MODE, XH> src{x, xh, seed};
@@ -1870,6 +1941,26 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   }
   // random-k windows come from the host each call: nothing for the next call to reuse
   if (MODE == kHash && b == 0 && tid == 0) ctrl->bounds[par ^ 1u].valid = 0u;
+  // Cold backoff: a call that took a carried window (m1024 != 0) and still missed puts
+  // the workspace on a run of `backoff` calls that sample their own window (in K1 or in
+  // K2's prologue), doubling per consecutive miss; warm hits halve it again.  A delta
+  // whose k-th key moves further than the window between calls (x_hat draining the top
+  // keys of a fixed x, the bench's fused step) then pays K1's sample instead of the
+  // exact fallback every call.
+  if (MODE == kData && b == 0 && tid == 0) {
+    const bool warm_call = fs.ctl[4] != 0u;
+    uint32_t bo = ctrl->backoff, cl = ctrl->cold_left;
+    if (warm_call && fallback) {
+      bo = min(max(2u * bo, kColdMin), kColdMax);
+      cl = bo;
+    } else if (warm_call) {
+      bo = max(bo / 2u, kColdMin);
+    } else if (cl != 0u) {
+      --cl;
+    }
+    ctrl->backoff = bo;
+    ctrl->cold_left = cl;
+  }
   STAMP(24576 + b, 2);
 }
 
@@ -1983,7 +2074,8 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   profile_begin("topk_stream", st);
   CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH, GS>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, k, L.tile, L.nb,
                 par, L.side_cap, seed, hs_lo, hs_hi, ctrl, cum, cntw, side, cval, cidx,
-                reinterpret_cast<uint32_t*>(base + L.off_tinfo), gs);
+                reinterpret_cast<uint32_t*>(base + L.off_tinfo), gs, sample_ranks(n, k),
+                (uint32_t)(MODE == kData && wc.warm ? 1 : 0));
   profile_end("topk_stream", st);
   CHOCO_LAUNCHED("topk_stream_kernel");
   profile_begin("topk_finish", st);
@@ -2109,7 +2201,8 @@ CHOCO_API int choco_dbg_stream_only(const float* x, int64_t n, int64_t k, void* 
                        reinterpret_cast<uint32_t*>(base + L.off_cum),
                        reinterpret_cast<uint32_t*>(base + L.off_cntw), reinterpret_cast<uint32_t*>(base + L.off_side),
                        reinterpret_cast<float*>(base + L.off_cval), reinterpret_cast<uint32_t*>(base + L.off_cidx),
-                       reinterpret_cast<uint32_t*>(base + L.off_tinfo), Gossip{nullptr, 0.f});
+                       reinterpret_cast<uint32_t*>(base + L.off_tinfo), Gossip{nullptr, 0.f}, SampleRanks{0u, 0u, 0u},
+                       0u);
   CHOCO_HIP(hipEventRecord(b, st));
   CHOCO_HIP(hipEventSynchronize(b));
   float ms = 0.f;

@@ -86,6 +86,7 @@ struct SegWs {
   float* cval;
   uint32_t* cidx;
   SegWin* win;
+  uint32_t* misses;  // the workspace's CHOCO_TOPK_FALLBACKS_OFFSET counter
 };
 
 struct SegLayout {
@@ -696,7 +697,8 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ plan, int nseg,
     const uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt, const uint32_t* __restrict__ tcount,
     uint32_t* __restrict__ hist3, const float* __restrict__ cval, const uint32_t* __restrict__ cidx,
-    float* __restrict__ out_val, int32_t* __restrict__ out_idx, SegWin* __restrict__ win) {
+    float* __restrict__ out_val, int32_t* __restrict__ out_idx, SegWin* __restrict__ win,
+    uint32_t* __restrict__ misses) {
   __shared__ uint32_t scratch[40];
   __shared__ ExactSmem es;
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
@@ -709,6 +711,7 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
   const uint32_t mode = WARM ? info[8 * c.s + 6] : (uint32_t)kSegSelect;
   if (mode == kSegMissed) {  // workgroup-uniform
     if (c.j != 0) return;
+    if (tid == 0) atomicAdd(misses, 1u);
     Src<kData, XH> src{x + c.R.off, XH ? xh + c.R.off : nullptr, 0};
     block_select_T(src, c.R.len, c.R.k, es);
     const uint32_t T = es.bc[0], r = es.bc[1], ties = es.bc[2];
@@ -838,10 +841,10 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
   profile_begin("topk_seg_emit", st);
   if (warm)
     CHOCO_KLAUNCH((seg_emit_kernel<true, XH>), dim3(ntile), dim3(kS4Threads), 0, st, x, xh, plan_dev, nseg, W.info,
-                  W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win);
+                  W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win, W.misses);
   else
     CHOCO_KLAUNCH((seg_emit_kernel<false, XH>), dim3(ntile), dim3(kS4Threads), 0, st, x, xh, plan_dev, nseg, W.info,
-                  W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win);
+                  W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win, W.misses);
   profile_end("topk_seg_emit", st);
   CHOCO_LAUNCHED("seg_emit_kernel");
   return CHOCO_OK;
@@ -879,7 +882,8 @@ static int segmented(const float* x, const float* xhat, const int64_t* plan_dev,
             reinterpret_cast<uint32_t*>(base + L.off_h3),
             reinterpret_cast<uint32_t*>(base + L.off_info), reinterpret_cast<uint32_t*>(base + L.off_cnt),
             reinterpret_cast<uint32_t*>(base + L.off_out), reinterpret_cast<float*>(base + L.off_cval),
-            reinterpret_cast<uint32_t*>(base + L.off_cidx), reinterpret_cast<SegWin*>(base + L.off_win)};
+            reinterpret_cast<uint32_t*>(base + L.off_cidx), reinterpret_cast<SegWin*>(base + L.off_win),
+            reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_FALLBACKS_OFFSET)};
     const bool warm = seg_claim_warm(base + L.off_win);
     int rc;
     if (gs.mem)

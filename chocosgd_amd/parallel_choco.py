@@ -229,12 +229,28 @@ class CHOCOSparsificationCompressor(_CHOCOBase):
 
 
 class CHOCOQuantizationCompressor(_CHOCOBase):
-    """QSGD  (parallel_choco_v.py:335-433)."""
+    """QSGD  (parallel_choco_v.py:335-433).
+
+    `exchange_chunks=C` (> 1, a constructor keyword every rank must pass alike) pipelines
+    the exchange (communication.py:259-262): the norm pass, then C element
+    ranges each quantized and SENT as soon as it is packed (the transfer of range c overlaps
+    the quantize of range c + 1), and uncompress decodes range c as soon as it has arrived
+    (overlapping the transfer of c + 1).  The wire is the chunked form of
+    codec.qsgd_chunked_wire; x_hat / memory are bit-identical to C = 1 (every element sees
+    the same messages in the same neighbour order).  `synced_message[rank]` is then the list
+    [norms header, range 0, range 1, ...]."""
+
+    def __init__(self, *args, **kargs):
+        super().__init__(*args, **kargs)
+        self.exchange_chunks = int(self.kargs.get("exchange_chunks", 1))
 
     def compress(self, sync_buffer):
         x, xh, lay = self._flat_inputs(sync_buffer)
         q = int(self.quantize_level)
         g = self._gossip(sync_buffer)
+        if q != 32 and self.exchange_chunks > 1:
+            return self._compress_chunked(sync_buffer, x, xh, lay, q, g)
+        sync_buffer.pop("chunked", None)
         if q == 32:  # the reference sends the raw delta (sparsification.py:118-119)
             if g is not None:
                 codec.gossip_step(x, g[0], xh, g[1])
@@ -248,12 +264,55 @@ class CHOCOQuantizationCompressor(_CHOCOBase):
         sync_buffer["n_bits"] = get_n_bits(x) * self.quantize_level / 32
         sync_buffer["n_bits_wire"] = 8 * message.numel()
 
+    def _compress_chunked(self, sync_buffer, x, xh, lay, q, g):
+        message, norms, parts = codec.qsgd_chunked_wire(lay.n, q, lay.nseg, self.exchange_chunks, x.device)
+        codec.qsgd_norms(x, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg, gossip=g, out=norms)
+        hb = 4 * _hdr_words(lay.nseg)
+        # the norms header leaves first; every range is posted right after its quantize launch,
+        # so its transfer (ordered after it on the stream) overlaps the next range's quantize
+        head = self._send(sync_buffer, message[:hb])
+        seed = _draw_seed()
+        posted = []
+        for e0, e1, part in parts:
+            codec.qsgd_quantize_range(x, q, norms, e0, e1, part, is_biased=self.is_biased, xhat=xh,
+                                      seg_off=lay.seg_off, nseg=lay.nseg, seed=seed)
+            posted.append(self._send(sync_buffer, part))
+        sync_buffer["chunked"] = (head, [(e0, e1) for e0, e1, _ in parts], posted)
+        sync_buffer["flatten_updates"] = TensorBuffer.from_flat(message, [(message.numel(),)])
+        sync_buffer["n_bits"] = get_n_bits(x) * self.quantize_level / 32  # nominal (parallel_choco_v.py:393)
+        sync_buffer["n_bits_wire"] = 8 * message.numel()
+
     def sync(self, sync_buffer):
+        if "chunked" in sync_buffer:  # posted by compress, range by range
+            (h_reqs, h_synced), _, posted = sync_buffer["chunked"]
+            sync_buffer["sync_reqs"] = h_reqs + [r for p in posted for r in p[0]]
+            sync_buffer["synced_message"] = {r: [h_synced[r]] + [p[1][r] for p in posted] for r in h_synced}
+            return
         reqs, synced = self._send(sync_buffer, sync_buffer["flatten_updates"].buffer)
         sync_buffer["sync_reqs"] = reqs
         sync_buffer["synced_message"] = synced
 
+    def _uncompress_chunked(self, sync_buffer, neighbor_hat_params, neighbors_info):
+        (h_reqs, h_synced), ranges, posted = sync_buffer["chunked"]
+        memory = neighbor_hat_params["memory"]
+        dev = memory.buffer.device
+        lay = _Layout.get(_seg_lens(sync_buffer["original_shapes"]), dev)
+        ranks = list(neighbors_info.keys())
+        weights = [neighbors_info[r] for r in ranks]
+        self_slot = self._self_slot(ranks, neighbor_hat_params)
+        xhat_self = neighbor_hat_params[ranks[self_slot]].buffer if self_slot >= 0 else None
+        self.aggregator_fn.complete_wait(h_reqs)
+        norms = [recover_device(h_synced[r], device=dev).view(torch.float32)[:lay.nseg].contiguous() for r in ranks]
+        for (e0, e1), (reqs, synced) in zip(ranges, posted):
+            self.aggregator_fn.complete_wait(reqs)  # this range only: later ones are still in flight
+            msgs = [(recover_device(synced[r], device=dev), nm) for r, nm in zip(ranks, norms)]
+            codec.qsgd_accumulate_range(msgs, weights, self_slot, lay.n, int(self.quantize_level), memory.buffer,
+                                        e0, e1, xhat_self=xhat_self, is_biased=self.is_biased,
+                                        seg_off=lay.seg_off, nseg=lay.nseg)
+
     def uncompress(self, sync_buffer, neighbor_hat_params, neighbors_info):
+        if "chunked" in sync_buffer:
+            return self._uncompress_chunked(sync_buffer, neighbor_hat_params, neighbors_info)
         self.aggregator_fn.complete_wait(sync_buffer["sync_reqs"])
         memory = neighbor_hat_params["memory"]
         dev = memory.buffer.device

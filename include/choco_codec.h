@@ -80,6 +80,9 @@ int choco_topk_set_warm_start(int32_t enable);
  * stuck producer cannot hang the GPU).  The caller reads it without blocking
  * (e.g. an async copy checked later), raises, and writes 0 back. */
 #define CHOCO_TOPK_STATUS_OFFSET 0
+/* Byte offset of a uint32 counter of calls (flat: the exact fallback; segmented: segments
+ * whose warm window missed) in the same workspaces: diagnostics, never reset by the codec. */
+#define CHOCO_TOPK_FALLBACKS_OFFSET 4
 #define CHOCO_TOPK_STATUS_POLL_TIMEOUT 1
 int choco_topk_compress(const float* x, const float* xhat, int64_t n, int64_t k,
                         float* out_val, int32_t* out_idx,
@@ -282,6 +285,30 @@ int choco_qsgd_decompress_accumulate(const uint8_t* const* packed_list,
 int choco_qsgd_decompress_extrapolate(const uint8_t* packed, const float* norms, int64_t n,
                                       const int64_t* seg_off, int32_t nseg, int32_t q, int32_t is_biased,
                                       float a, float b, float* target, void* stream);
+
+/* Chunked QSGD wire (the exchange pipelined with compress and decompress, SURVEY.md
+ * §8(e); parallel_choco.py exchange_chunks): the norm pass alone, then the quantize
+ * pass over element ranges [e0, e1), each range a self-contained message of
+ * choco_qsgd_packed_bytes(e1 - e0, q) bytes ([level plane | sign plane] of its own
+ * elements), and the receiver over the same ranges.  e0 must be a multiple of 8192
+ * (the uniform-stream tile), e1 one too or n.  A range's levels, signs and uniforms
+ * are exactly those of choco_qsgd_compress over the whole buffer (element e keeps its
+ * stream position), so the decoded values, and memory / xhat_self after all ranges,
+ * are bit-identical to the unchunked path; norms come from choco_qsgd_norms (or its
+ * gossip form, which also applies the consensus step to x). */
+int choco_qsgd_norms(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
+                     float* norms_out, void* ws, size_t ws_bytes, void* stream);
+int choco_gossip_qsgd_norms(float* x, const float* memory, const float* xhat, float gamma, int64_t n,
+                            const int64_t* seg_off, int32_t nseg, float* norms_out, void* ws, size_t ws_bytes,
+                            void* stream);
+int choco_qsgd_quantize_range(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
+                              int32_t q, int32_t is_biased, const float* norms, uint64_t seed, uint64_t offset,
+                              int64_t e0, int64_t e1, uint8_t* packed_range, void* stream);
+int choco_qsgd_decompress_accumulate_range(const uint8_t* const* packed_list, const float* const* norms_list,
+                                           const float* weights, int32_t nmsg, int32_t self_slot, int64_t n,
+                                           const int64_t* seg_off, int32_t nseg, int32_t q, int32_t is_biased,
+                                           int64_t e0, int64_t e1, float* xhat_self, float* memory,
+                                           void* stream);
 
 /* ------------------------------------------------------- gossip step
  * update_params_from_neighbor (pcode/optim/utils.py:67-72):

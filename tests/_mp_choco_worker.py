@@ -17,6 +17,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LENS = [3, 70_001, 5, 1_100_003, 17, 300]
 RATIO = 0.9
+CHUNKS = 4  # exchange_chunks of the *_chunked comm ops (ranges of 294,912 elements)
 
 
 def inputs(rank):
@@ -46,8 +47,10 @@ def _rank_main(rank, world, port, comm_op, outdir):
         parallel_choco._draw_seed = lambda: 1000 + rank  # pinned per-worker seeds (random-k, QSGD)
         nb = neighborhood(rank, world)
         agg = DecentralizedAggregation(rank, nb)
-        comp = CHOCOCompressor(aggregator=agg, comm_op=comm_op, comm_device="cpu", compress_ratio=RATIO,
-                               quantize_level=4, is_biased=False, backend="gloo", use_ipc=False)
+        chunks = CHUNKS if comm_op.endswith("_chunked") else 1
+        comp = CHOCOCompressor(aggregator=agg, comm_op=comm_op.replace("_chunked", ""), comm_device="cpu",
+                               compress_ratio=RATIO, quantize_level=4, is_biased=False, backend="gloo",
+                               use_ipc=False, exchange_chunks=chunks)
         x, xh, hat0, mem0 = inputs(rank)
 
         def split(a):
@@ -68,7 +71,11 @@ def _rank_main(rank, world, port, comm_op, outdir):
         torch.cuda.synchronize()
         out = {"hat": nhp[rank].buffer.cpu().numpy(), "mem": nhp["memory"].buffer.cpu().numpy()}
         for r, m in sb["synced_message"].items():
-            out[f"msg{r}"] = m.cpu().numpy()
+            if isinstance(m, list):  # chunked wire: [norms header, range 0, range 1, ...]
+                for i, part in enumerate(m):
+                    out[f"msg{r}_{i}"] = part.cpu().numpy()
+            else:
+                out[f"msg{r}"] = m.cpu().numpy()
         np.savez(os.path.join(outdir, f"rank{rank}.npz"), **out)
         dist.barrier()
     finally:

@@ -34,7 +34,8 @@ def _hdr(nseg):
 
 
 @pytest.mark.parametrize("comm_op,world", [("compress_top_k", 2), ("compress_top_k", 3), ("compress_random_k", 3),
-                                           ("sign", 2), ("sign", 3), ("quantize_qsgd", 3)])
+                                           ("sign", 2), ("sign", 3), ("quantize_qsgd", 3),
+                                           ("quantize_qsgd_chunked", 2), ("quantize_qsgd_chunked", 3)])
 def test_choco_round_across_processes(comm_op, world, tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_mp_choco_worker.py"), comm_op, str(world),
                         str(tmp_path)], capture_output=True, text=True, timeout=600)
@@ -65,6 +66,32 @@ def _verify_round(comm_op, world, tmp_path):
     # every worker's message, checked once against the oracle (as its neighbours received it)
     msgs = {}
     for q in range(world):
+        if comm_op.endswith("_chunked"):
+            # the chunked wire, re-assembled into the one-message layout (each range is a
+            # self-contained [level | sign] message of its own elements: checked against the
+            # oracle's packing of exactly those elements)
+            g = next(g for g in got if f"msg{q}_0" in g)
+            d = deltas[q]
+            hb = 4 * _hdr(nseg)
+            norms = g[f"msg{q}_0"][:hb].view(np.float32)[:nseg]
+            assert np.allclose(norms, O.l2_norms(d, lens), rtol=1e-6, atol=0)
+            u = O.qsgd_uniforms(n, 1000 + q, 0)
+            lvl, off = [], 0
+            for s, m in enumerate(lens):
+                lvl.append(O.qsgd_levels(d[off:off + m], 15, u[off:off + m], norms[s]))
+                off += m
+            lvl = np.concatenate(lvl)
+            per = -(-(-(-n // W.CHUNKS)) // 8192) * 8192
+            for i, e0 in enumerate(range(0, n, per)):
+                e1 = min(e0 + per, n)
+                assert np.array_equal(g[f"msg{q}_{i + 1}"], O.qsgd_pack(lvl[e0:e1], d[e0:e1], 4)), (q, i)
+            levels, neg = O.qsgd_unpack(O.qsgd_pack(lvl, d, 4), n, 4)
+            dec, off = [], 0
+            for s, m in enumerate(lens):
+                dec.append(O.qsgd_decode(levels[off:off + m], neg[off:off + m], norms[s], 15, m))
+                off += m
+            msgs[q] = np.concatenate(dec)
+            continue
         rcv = next(g[f"msg{q}"] for g in got if f"msg{q}" in g)
         d = deltas[q]
         if "top_k" in comm_op or "random_k" in comm_op:

@@ -325,6 +325,7 @@ def _check_topk(x, k, xh=None):
     ov, oi = O.topk(d, k)
     assert np.array_equal(host(idx).astype(np.int64), oi)
     assert same_bits(host(vals), ov)
+    return vals, idx
 
 
 @pytest.mark.parametrize("n", [3_000_000, 25_000_000])
@@ -394,6 +395,25 @@ def test_topk_warm_start_gossip_sequence():
         codec.sparse_accumulate(vals, idx, mem, 1.0, xhat_self=hat)
 
 
+def test_topk_warm_start_drained_delta():
+    """The CHOCO drain: x fixed, x_hat catching up with every call's top-k (the selected
+    entries of the delta become 0), so every call's k-th key is the previous call's ~2k-th.
+    Every call exact; the first warm miss puts the workspace on a cold run (K34's backoff:
+    the window is sampled in K2's prologue), so no later call takes the exact fallback."""
+    from chocosgd_amd import codec
+    n = 4_000_037
+    k = codec.topk_k(n, 0.99)
+    torch.cuda.synchronize()
+    codec.release_workspaces()  # a fresh workspace: cold first call, counter at 0
+    d = randn(n, 470)
+    counts = []
+    for step in range(12):
+        vals, idx = _check_topk(d, k)
+        d[idx.long()] = 0.0
+        counts.append(codec.topk_fallback_count())
+    assert counts[-1] <= 1, counts
+
+
 def test_topk_status_word_clean_after_calls():
     """No call of this module left the workspace status word set (bounded waits never gave up)."""
     from chocosgd_amd import codec
@@ -454,6 +474,7 @@ def _check_seg(x, plan, lens, ratio, xh=None):
     ov, oi, _ = O.topk_segmented(d, lens, ratio)
     assert np.array_equal(host(idx).astype(np.int64), oi)
     assert same_bits(host(vals), ov)
+    return vals, idx
 
 
 @pytest.mark.parametrize("layout", ["resnet20_cifar10", "resnet50_imagenet", "edges"])
@@ -475,6 +496,25 @@ def test_topk_segmented_warm_sequence(layout):
            randn(n, 505) * 1e-3, randn(n, 506), randn(n, 507)]
     for x in seq:
         _check_seg(x, plan, lens, ratio)
+
+
+def test_topk_segmented_warm_drained_delta():
+    """The drain on the segmented path (ResNet-50's layout): the selected entries of every
+    call are zeroed before the next.  Every call exact; windows that miss take S4's exact
+    one-workgroup select (the segmented path has no cold backoff yet, the miss
+    count is reported by codec.topk_fallback_count)."""
+    from chocosgd_amd import codec
+    lens = golden_json("layouts.json")["resnet50_imagenet"]
+    n = sum(lens)
+    ratio = 0.99
+    plan = codec.SegmentPlan(lens, ratio, torch.device(DEV))
+    d = randn(n, 540)
+    counts = []
+    for step in range(10):
+        vals, idx = _check_seg(d, plan, lens, ratio)
+        d[idx.long()] = 0.0
+        counts.append(codec.topk_fallback_count(plan=plan))
+    print("segment window misses per call (cumulative):", counts)
 
 
 def test_topk_segmented_warm_ratio0_and_half():
