@@ -1630,7 +1630,10 @@ CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uin
 // window are extrapolated from its density (G[0] - k keys over [s_lo, T]).
 // Wave 0 of one workgroup; ~0.3 us, after that workgroup's emission.
 // ----------------------------------------------------------------------------
-constexpr uint32_t kColdMin = 32, kColdMax = 1024;  // cold-run lengths after a warm miss
+// Cold-run lengths after a warm miss.  A miss costs the exact fallback (~0.6-0.75 ms at
+// 100M) against ~10 us saved per warm call, so a retry pays only if warm then holds for
+// ~60+ calls: the first run is 64 calls, doubling per consecutive miss.
+constexpr uint32_t kColdMin = 64, kColdMax = 4096;
 constexpr uint32_t kWarmM0 = 20;     // ~2 % of k (the bench's randn deltas drift ~0.1 %)
 constexpr uint32_t kWarmMMax = 512;  // 50 %
 CHOCO_DEV void next_window(const uint32_t* G, uint32_t s_lo, uint32_t s_hi, uint32_t shift, uint32_t m_prev,

@@ -86,7 +86,8 @@ struct SegWs {
   float* cval;
   uint32_t* cidx;
   SegWin* win;
-  uint32_t* misses;  // the workspace's CHOCO_TOPK_FALLBACKS_OFFSET counter
+  uint32_t* misses;     // the workspace's CHOCO_TOPK_FALLBACKS_OFFSET counter
+  uint32_t* miss_flag;  // pinned host word of the cold backoff (nullable)
 };
 
 struct SegLayout {
@@ -698,7 +699,7 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
     const uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt, const uint32_t* __restrict__ tcount,
     uint32_t* __restrict__ hist3, const float* __restrict__ cval, const uint32_t* __restrict__ cidx,
     float* __restrict__ out_val, int32_t* __restrict__ out_idx, SegWin* __restrict__ win,
-    uint32_t* __restrict__ misses) {
+    uint32_t* __restrict__ misses, uint32_t* __restrict__ miss_flag) {
   __shared__ uint32_t scratch[40];
   __shared__ ExactSmem es;
   const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
@@ -711,7 +712,10 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
   const uint32_t mode = WARM ? info[8 * c.s + 6] : (uint32_t)kSegSelect;
   if (mode == kSegMissed) {  // workgroup-uniform
     if (c.j != 0) return;
-    if (tid == 0) atomicAdd(misses, 1u);
+    if (tid == 0) {
+      atomicAdd(misses, 1u);
+      if (miss_flag) __hip_atomic_store(miss_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     Src<kData, XH> src{x + c.R.off, XH ? xh + c.R.off : nullptr, 0};
     block_select_T(src, c.R.len, c.R.k, es);
     const uint32_t T = es.bc[0], r = es.bc[1], ties = es.bc[2];
@@ -775,26 +779,59 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
 static int64_t plan_tiles(const int64_t* plan_host) { return plan_host[6]; }
 static int64_t plan_batched(const int64_t* plan_host) { return plan_host[7]; }
 
-// warm bookkeeping: per segmented workspace, whether an earlier call left windows
+// Warm bookkeeping per segmented workspace: whether an earlier call left windows, and a
+// cold backoff driven by the device.  S4 raises a flag in pinned host memory (a system-
+// scope store, no copy on the stream) when a segment's window missed; the host sees it
+// a few calls later (whenever that S4 has run) and then takes the cold sequence (S1 + S2,
+// two reads, never a miss) for a run of 64 calls, doubling per run that ends in a new
+// miss, up to 4096.  A stationary delta never raises the flag and never pays anything; a
+// delta whose k-th keys keep moving out of their windows (x_hat draining the top keys)
+// pays the second read instead of S4's one-workgroup exact select of every missed segment.
+struct SegState {
+  uint64_t calls = 0;
+  uint32_t cold_left = 0, backoff = 0;
+  uint32_t* flag = nullptr;  // pinned, mapped; the device writes 1 on a miss
+  uint32_t* flag_dev = nullptr;
+};
 static std::mutex g_seg_mu;
-static std::unordered_map<const void*, uint64_t> g_seg_calls;
-static bool seg_claim_warm(const void* ws) {
+static std::unordered_map<const void*, SegState> g_seg;
+static bool seg_claim_warm(const void* ws, uint32_t** flag_dev) {
   std::lock_guard<std::mutex> g(g_seg_mu);
-  auto it = g_seg_calls.find(ws);
-  if (it == g_seg_calls.end()) {
-    g_seg_calls.emplace(ws, 1u);
+  SegState& S = g_seg[ws];
+  if (!S.flag) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+      S.flag = static_cast<uint32_t*>(h);
+      *S.flag = 0u;
+      void* d = nullptr;
+      if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess) S.flag_dev = static_cast<uint32_t*>(d);
+    }
+  }
+  *flag_dev = S.flag_dev;  // (null: no backoff, warm as before)
+  const bool first = S.calls++ == 0;
+  if (S.flag && __atomic_load_n(S.flag, __ATOMIC_ACQUIRE) != 0u) {
+    __atomic_store_n(S.flag, 0u, __ATOMIC_RELEASE);
+    S.backoff = std::min<uint32_t>(std::max<uint32_t>(2u * S.backoff, 64u), 4096u);
+    S.cold_left = S.backoff;
+  }
+  if (first) return false;
+  if (S.cold_left != 0u) {
+    --S.cold_left;
     return false;
   }
-  ++it->second;
   return topk_warm_enabled();
 }
 void seg_forget(const void* ws, size_t bytes) {
   std::lock_guard<std::mutex> g(g_seg_mu);
   const char* lo = static_cast<const char*>(ws);
-  for (auto it = g_seg_calls.begin(); it != g_seg_calls.end();) {
+  for (auto it = g_seg.begin(); it != g_seg.end();) {
     const char* p = static_cast<const char*>(it->first);
-    if (p == lo || (p > lo && p < lo + bytes)) it = g_seg_calls.erase(it);
-    else ++it;
+    if (p == lo || (p > lo && p < lo + bytes)) {
+      if (it->second.flag) (void)hipHostFree(it->second.flag);  // (callers synchronise before a reset)
+      it = g_seg.erase(it);
+    } else {
+      ++it;
+    }
   }
 }
 
@@ -841,10 +878,10 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
   profile_begin("topk_seg_emit", st);
   if (warm)
     CHOCO_KLAUNCH((seg_emit_kernel<true, XH>), dim3(ntile), dim3(kS4Threads), 0, st, x, xh, plan_dev, nseg, W.info,
-                  W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win, W.misses);
+                  W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win, W.misses, W.miss_flag);
   else
     CHOCO_KLAUNCH((seg_emit_kernel<false, XH>), dim3(ntile), dim3(kS4Threads), 0, st, x, xh, plan_dev, nseg, W.info,
-                  W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win, W.misses);
+                  W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win, W.misses, W.miss_flag);
   profile_end("topk_seg_emit", st);
   CHOCO_LAUNCHED("seg_emit_kernel");
   return CHOCO_OK;
@@ -883,8 +920,8 @@ static int segmented(const float* x, const float* xhat, const int64_t* plan_dev,
             reinterpret_cast<uint32_t*>(base + L.off_info), reinterpret_cast<uint32_t*>(base + L.off_cnt),
             reinterpret_cast<uint32_t*>(base + L.off_out), reinterpret_cast<float*>(base + L.off_cval),
             reinterpret_cast<uint32_t*>(base + L.off_cidx), reinterpret_cast<SegWin*>(base + L.off_win),
-            reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_FALLBACKS_OFFSET)};
-    const bool warm = seg_claim_warm(base + L.off_win);
+            reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_FALLBACKS_OFFSET), nullptr};
+    const bool warm = seg_claim_warm(base + L.off_win, &W.miss_flag);
     int rc;
     if (gs.mem)
       rc = launch_batched<true, true>(x, xhat, plan_dev, plan_host, nseg, out_val, out_idx, W, warm, st, gs);
