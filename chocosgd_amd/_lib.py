@@ -45,6 +45,8 @@ SIGNATURES = {
     "choco_sign_words": (_c_i64, [_c_i64]),
     "choco_sign_workspace_size": (_c_sz, [_c_i32]),
     "choco_sign_compress": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
+    "choco_sign_compress_range": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _c_i64, _c_i64, _c_i32, _vp, _vp, _vp,
+                                           _c_sz, _vp]),
     "choco_sign_unpack": (_c_i32, [_vp, _c_i64, _vp, _vp]),
     "choco_sign_decompress_accumulate": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i32, _c_i64, _vp, _c_i32,
                                                   _vp, _vp, _vp, _c_sz, _vp]),
@@ -74,6 +76,8 @@ SIGNATURES = {
     "choco_gossip_randk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _c_f32, _vp, _p_i64, _c_i32, _c_u64, _c_u64,
                                                        _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_gossip_sign_compress": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _vp, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
+    "choco_gossip_sign_compress_range": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _vp, _c_i32, _c_i64, _c_i64,
+                                                  _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_gossip_qsgd_compress": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _vp, _c_i32, _c_i32, _c_i32, _c_u64,
                                             _c_u64, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_profile_enable": (_c_i32, [_c_i32]),

@@ -544,6 +544,45 @@ def sign_compress(x, xhat=None, seg_off=None, nseg=1, want_norms=True, gossip=No
     return packed, norms
 
 
+SIGN_RANGE_ALIGN = 1024  # words per pack workgroup (sign.hip kSignCols)
+
+
+def sign_chunks(n, chunks):
+    """`chunks` word ranges [(w0, w1)] covering [0, N'), starts aligned to 1024 words."""
+    words = sign_words(n)
+    per = -(-words // max(1, int(chunks)))
+    per = -(-per // SIGN_RANGE_ALIGN) * SIGN_RANGE_ALIGN
+    return [(w, min(w + per, words)) for w in range(0, words, per)]
+
+
+def sign_compress_range(x, w0, w1, finish, xhat=None, seg_off=None, nseg=1, gossip=None, out=None):
+    """Pack the words [w0, w1) of sign_compress's layout into out=(packed int32[N'], norms
+    f32[nseg] or None); the norms are written by the `finish` call, which must be the last
+    range of the message on this stream (include/choco_codec.h "Chunked sign pack")."""
+    _require(x, torch.float32, "x")
+    if xhat is not None:
+        _require(xhat, torch.float32, "xhat")
+    if seg_off is not None:
+        _require(seg_off, torch.int64, "seg_off")
+    n = x.numel()
+    dev = x.device
+    L = lib()
+    packed, norms = _out_views(out, sign_words(n), torch.int32, nseg, dev)
+    ws = workspace(dev, "acc", L.choco_sign_workspace_size(nseg))
+    g = _gossip(gossip, x, xhat)
+    fin = 1 if finish else 0
+    if g is not None:
+        _lib.check(L.choco_gossip_sign_compress_range(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1], n, _ptr(seg_off),
+                                                      int(nseg), int(w0), int(w1), fin, _ptr(packed), _ptr(norms),
+                                                      _ptr(ws), ws.numel(), _stream(dev)),
+                   "choco_gossip_sign_compress_range")
+    else:
+        _lib.check(L.choco_sign_compress_range(_ptr(x), _ptr(xhat), n, _ptr(seg_off), int(nseg), int(w0), int(w1),
+                                               fin, _ptr(packed), _ptr(norms), _ptr(ws), ws.numel(), _stream(dev)),
+                   "choco_sign_compress_range")
+    return packed, norms
+
+
 def sign_unpack(packed, n):
     _require(packed, torch.int32, "packed")
     out = torch.empty(n, dtype=torch.float32, device=packed.device)

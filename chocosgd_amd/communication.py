@@ -53,8 +53,14 @@ class DecentralizedAggregation(object):
         self.neighbor_ranks = [r for r in neighbors_info.keys() if r != rank]
         self.world_size = float(len(self.neighbor_ranks))
 
-    def _agg(self, data, op, force_wait=True):
-        local_data = {i: torch.empty_like(data) for i in self.neighbor_ranks}
+    def _agg(self, data, op, force_wait=True, out=None):
+        """`out` (this drop-in's addition, default None = the reference's behaviour):
+        {rank: buffer} to receive each neighbour's message into, e.g. slices of one
+        message posted range by range (CHOCOSignCompressor exchange_chunks)."""
+        if out is not None:
+            local_data = {i: out[i] for i in self.neighbor_ranks}
+        else:
+            local_data = {i: torch.empty_like(data) for i in self.neighbor_ranks}
         local_data[self.rank] = data
         reqs = []
         if self.neighbor_ranks:

@@ -82,6 +82,9 @@ CHOCO_DEV float4 ld_norm4(const float* p) {
   return *reinterpret_cast<const float4*>(p);
 }
 
+#ifndef CHOCO_QQUANT_REV  // 1: workgroups walk the tiles in reverse (A/B, r03 with two tiles per workgroup: forward 145-146 vs reverse 142-144 us)
+#define CHOCO_QQUANT_REV 1
+#endif
 #ifndef CHOCO_QQUANT_NT  // non-temporal loads in the quantize pass (off: the decode then runs 300 -> 270 us)
 #define CHOCO_QQUANT_NT 0
 #endif
@@ -404,7 +407,7 @@ __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
     float* __restrict__ dense_out, int64_t tile_lo, int64_t tile_cnt, int64_t pad_e0, int64_t pad_len) {
   __shared__ int s_seg[2];
   // tiles [tile_lo, tile_lo + tile_cnt) of the buffer, walked in reverse (Infinity-Cache hits)
-  const int64_t tile = tile_lo + tile_cnt - 1 - (int64_t)blockIdx.x;
+  const int64_t tile = CHOCO_QQUANT_REV ? tile_lo + tile_cnt - 1 - (int64_t)blockIdx.x : tile_lo + (int64_t)blockIdx.x;
   const int64_t t_e0 = tile * kQStreamTile;
   const int64_t t_e1 = std::min<int64_t>(t_e0 + kQStreamTile, n);
   const int sg0 = tile_seg(seg_off, nseg, t_e0, t_e1, s_seg);

@@ -145,14 +145,14 @@ template <bool XH, bool NORM, bool GS = false>
 __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t Np,
     const int64_t* __restrict__ seg_off, int nseg, uint32_t* __restrict__ packed, float* __restrict__ l1_out,
-    SignWs* __restrict__ ws, Gossip gs) {
+    SignWs* __restrict__ ws, Gossip gs, int64_t blk0, int finish) {
   static_assert(!GS || XH, "the gossip step needs x_hat");
   __shared__ int s_lo[32], s_hi[32];
   __shared__ double s_rows[kSignThreads / 64][32];
   __shared__ unsigned int s_flag;
   double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
   const int lane = lane_id(), w = threadIdx.x >> 6;
-  const int64_t J0 = (int64_t)blockIdx.x * kSignCols;
+  const int64_t J0 = (blk0 + (int64_t)blockIdx.x) * kSignCols;
   const int64_t j0 = J0 + 256 * w;
   const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
   if (NORM) row_segments(seg_off, nseg, n, Np, J0, s_lo, s_hi);
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
       }
       if (cur >= 0 && run != 0.0) unsafeAtomicAdd(&acc[cur], run);
     }
-    if (last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
+    if (finish && last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
       for (int q = threadIdx.x; q < nseg; q += blockDim.x) l1_out[q] = (float)atomic_exchange_double(&acc[q], 0.0);
       if (threadIdx.x == 0) __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -337,7 +337,8 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
                                                                   const float* __restrict__ xh, int64_t n,
                                                                   int64_t Np, uint32_t* __restrict__ packed,
                                                                   float* __restrict__ l1_out,
-                                                                  SignWs* __restrict__ ws, Gossip gs) {
+                                                                  SignWs* __restrict__ ws, Gossip gs, int64_t blk0,
+                                                                  int finish) {
   static_assert(!GS || XH, "the gossip step needs x_hat");
   constexpr int RU = GS ? CHOCO_SIGN_GS_RU : (XH ? 4 : 8);  // rows per group (more streams, more registers)
   constexpr int NG = 32 / RU;
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
   __shared__ unsigned int s_flag;
   double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
   const int lane = lane_id(), w = threadIdx.x >> 6;
-  const int64_t j0 = (int64_t)blockIdx.x * kSignCols + 256 * w;
+  const int64_t j0 = (blk0 + (int64_t)blockIdx.x) * kSignCols + 256 * w;
   const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
   // every row run of the wave (row 31's last float4 included) lies inside [0, n)
   const bool interior = ncol == 256 && (int64_t)31 * Np + j0 + 256 <= n;
@@ -453,7 +454,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
       for (int i = 0; i < kSignThreads / 64; ++i) tsum += s_red[i];
       if (tsum != 0.0) unsafeAtomicAdd(&acc[0], tsum);
     }
-    if (last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
+    if (finish && last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
       if (threadIdx.x == 0) {
         l1_out[0] = (float)atomic_exchange_double(&acc[0], 0.0);
         __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -961,17 +962,21 @@ CHOCO_API size_t choco_sign_workspace_size(int32_t nseg) {
 template <bool XH, bool NORM, bool GS>
 static void launch_pack(bool one, unsigned grid, hipStream_t st, const float* x, const float* xhat, int64_t n,
                         int64_t Np, const int64_t* seg_off, int32_t nseg, uint32_t* pk, float* l1, SignWs* w,
-                        Gossip gs) {
+                        Gossip gs, int64_t blk0, int finish) {
   if (one)
     CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, pk, l1,
-                  w, gs);
+                  w, gs, blk0, finish);
   else
     CHOCO_KLAUNCH((sign_pack_kernel<XH, NORM, GS>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, seg_off,
-                  nseg, pk, l1, w, gs);
+                  nseg, pk, l1, w, gs, blk0, finish);
 }
 
+// Packs words [w0, w1) (the whole buffer: 0, N').  The per-segment L1 sums of a range
+// stay in the workspace's fp64 accumulators; the `finish` launch (issued last) rounds
+// them to fp32 into l1_norms and zeroes the accumulators.
 static int sign_compress(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
-                         int32_t* packed, float* l1_norms, void* ws, size_t ws_bytes, hipStream_t st, Gossip gs) {
+                         int32_t* packed, float* l1_norms, void* ws, size_t ws_bytes, hipStream_t st, Gossip gs,
+                         int64_t w0 = 0, int64_t w1 = -1, bool finish = true) {
   CHOCO_REQUIRE(x && packed, "null pointer argument");
   CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
   CHOCO_REQUIRE(aligned16(x) && (!xhat || aligned16(xhat)) && aligned16(packed),
@@ -979,7 +984,11 @@ static int sign_compress(const float* x, const float* xhat, int64_t n, const int
   CHOCO_REQUIRE(!gs.mem || (xhat && aligned16(gs.mem)), "the gossip step needs x_hat and a 16-byte aligned memory");
   CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
   const int64_t Np = choco_sign_words(n);
-  const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
+  if (w1 < 0) w1 = Np;
+  CHOCO_REQUIRE(w0 >= 0 && w0 < w1 && w1 <= Np && w0 % kSignCols == 0 && (w1 % kSignCols == 0 || w1 == Np),
+                "word range must satisfy 0 <= w0 < w1 <= N', w0 a multiple of 1024, w1 one too or N'");
+  const unsigned grid = (unsigned)((w1 - w0 + kSignCols - 1) / kSignCols);
+  const int64_t blk0 = w0 / kSignCols;
   uint32_t* pk = reinterpret_cast<uint32_t*>(packed);
   SignWs* w = static_cast<SignWs*>(ws);
   if (l1_norms) {
@@ -987,20 +996,22 @@ static int sign_compress(const float* x, const float* xhat, int64_t n, const int
   }
   const bool one = nseg == 1 && n < (int64_t(1) << 30);  // one segment, buffer offsets: n * 4 < 2^32 bytes
   if (gs.mem && !CHOCO_SIGN_GS_FUSE) {
+    CHOCO_REQUIRE(w0 == 0 && w1 == Np, "the unfused gossip build packs whole buffers only");
     const int rc = gossip_launch(const_cast<float*>(x), gs.mem, xhat, gs.gamma, n, st);
     if (rc) return rc;
     gs.mem = nullptr;
   }
+  const int fin = finish ? 1 : 0;
   profile_begin("sign_pack", st);
   if (gs.mem) {
-    if (l1_norms) launch_pack<true, true, true>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs);
-    else launch_pack<true, false, true>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs);
+    if (l1_norms) launch_pack<true, true, true>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs, blk0, fin);
+    else launch_pack<true, false, true>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs, blk0, fin);
   } else if (xhat) {
-    if (l1_norms) launch_pack<true, true, false>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs);
-    else launch_pack<true, false, false>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs);
+    if (l1_norms) launch_pack<true, true, false>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs, blk0, fin);
+    else launch_pack<true, false, false>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs, blk0, fin);
   } else {
-    if (l1_norms) launch_pack<false, true, false>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs);
-    else launch_pack<false, false, false>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs);
+    if (l1_norms) launch_pack<false, true, false>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs, blk0, fin);
+    else launch_pack<false, false, false>(one, grid, st, x, xhat, n, Np, seg_off, nseg, pk, l1_norms, w, gs, blk0, fin);
   }
   profile_end("sign_pack", st);
   CHOCO_LAUNCHED("sign_pack_kernel");
@@ -1020,6 +1031,22 @@ CHOCO_API int choco_gossip_sign_compress(float* x, const float* memory, const fl
   CHOCO_REQUIRE(memory != nullptr && xhat != nullptr, "the gossip step needs memory and x_hat");
   return sign_compress(x, xhat, n, seg_off, nseg, packed, l1_norms, ws, ws_bytes, as_stream(stream),
                        Gossip{memory, gamma});
+}
+
+CHOCO_API int choco_sign_compress_range(const float* x, const float* xhat, int64_t n, const int64_t* seg_off,
+                                        int32_t nseg, int64_t w0, int64_t w1, int32_t finish, int32_t* packed,
+                                        float* l1_norms, void* ws, size_t ws_bytes, void* stream) {
+  return sign_compress(x, xhat, n, seg_off, nseg, packed, l1_norms, ws, ws_bytes, as_stream(stream),
+                       Gossip{nullptr, 0.f}, w0, w1, finish != 0);
+}
+
+CHOCO_API int choco_gossip_sign_compress_range(float* x, const float* memory, const float* xhat, float gamma,
+                                               int64_t n, const int64_t* seg_off, int32_t nseg, int64_t w0, int64_t w1,
+                                               int32_t finish, int32_t* packed, float* l1_norms, void* ws,
+                                               size_t ws_bytes, void* stream) {
+  CHOCO_REQUIRE(memory != nullptr && xhat != nullptr, "the gossip step needs memory and x_hat");
+  return sign_compress(x, xhat, n, seg_off, nseg, packed, l1_norms, ws, ws_bytes, as_stream(stream),
+                       Gossip{memory, gamma}, w0, w1, finish != 0);
 }
 
 CHOCO_API int choco_sign_unpack(const int32_t* packed, int64_t n, float* out, void* stream) {

@@ -134,10 +134,12 @@ class _CHOCOBase(object):
         g = sync_buffer.get("gossip")
         return None if g is None else (g[0], float(g[1]))
 
-    def _send(self, sync_buffer, message):
+    def _send(self, sync_buffer, message, out=None):
         if self.comm_device == "cpu":
             message = message.cpu().pin_memory()
-        return self.aggregator_fn._agg(message, op="get_raw_sync_data", force_wait=False)
+        if out is None:
+            return self.aggregator_fn._agg(message, op="get_raw_sync_data", force_wait=False)
+        return self.aggregator_fn._agg(message, op="get_raw_sync_data", force_wait=False, out=out)
 
     @staticmethod
     def _self_slot(ranks, neighbor_hat_params):
@@ -337,13 +339,30 @@ class CHOCOQuantizationCompressor(_CHOCOBase):
 
 
 class CHOCOSignCompressor(_CHOCOBase):
-    """sign + per-tensor L1 norm  (parallel_choco_v.py:436-558)."""
+    """sign + per-tensor L1 norm  (parallel_choco_v.py:436-558).
+
+    `exchange_chunks=C` (> 1, every rank alike) pipelines the send with the pack: the
+    words are packed in C column ranges and each range's words are posted as soon as its
+    pack is queued (its transfer overlaps the next range's pack); the norms header, complete
+    only after the last range, leaves last.  Every range of the (32, N') layout touches
+    every row's segments, so the receiver decodes after the whole message, as with C = 1
+    (include/choco_codec.h "Chunked sign pack").  Neighbours receive straight into one
+    message per rank, so the wire, `synced_message` and the decode are those of C = 1."""
+
+    def __init__(self, *args, **kargs):
+        super().__init__(*args, **kargs)
+        self.exchange_chunks = int(self.kargs.get("exchange_chunks", 1))
 
     def compress(self, sync_buffer):
         x, xh, lay = self._flat_inputs(sync_buffer)
         message, (signs, norms) = codec.sign_wire(lay.n, lay.nseg, x.device)  # written in place by the kernels
-        codec.sign_compress(x, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg, want_norms=True,
-                            gossip=self._gossip(sync_buffer), out=(signs, norms))
+        g = self._gossip(sync_buffer)
+        sync_buffer.pop("chunked", None)
+        if self.exchange_chunks > 1:
+            sync_buffer["chunked"] = self._pack_and_post(sync_buffer, x, xh, lay, g, message, signs, norms)
+        else:
+            codec.sign_compress(x, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg, want_norms=True, gossip=g,
+                                out=(signs, norms))
         sync_buffer["sign_message"] = message
         sync_buffer["flatten_norms"] = TensorBuffer.from_flat(norms, [() for _ in range(lay.nseg)])
         sync_buffer["flatten_directions"] = None  # the delta is never materialised (fused)
@@ -352,12 +371,31 @@ class CHOCOSignCompressor(_CHOCOBase):
         # nominal bits as in parallel_choco_v.py:492
         sync_buffer["n_bits"] = get_n_bits(norms) + get_n_bits(signs)
 
+    def _pack_and_post(self, sync_buffer, x, xh, lay, g, message, signs, norms):
+        hw = _hdr_words(lay.nseg)
+        peers = [r for r in self.aggregator_fn.neighbor_ranks]
+        host = self.comm_device == "cpu"
+        recv = {r: torch.empty(message.shape, dtype=message.dtype, device="cpu" if host else message.device,
+                               pin_memory=host) for r in peers}
+        ranges = codec.sign_chunks(lay.n, self.exchange_chunks)
+        reqs = []
+        for i, (w0, w1) in enumerate(ranges):
+            codec.sign_compress_range(x, w0, w1, i == len(ranges) - 1, xhat=xh, seg_off=lay.seg_off,
+                                      nseg=lay.nseg, gossip=g, out=(signs, norms))
+            r, _ = self._send(sync_buffer, message[hw + w0:hw + w1],
+                              out={p: recv[p][hw + w0:hw + w1] for p in peers})
+            reqs += r
+        r, _ = self._send(sync_buffer, message[:hw], out={p: recv[p][:hw] for p in peers})
+        recv[self.aggregator_fn.rank] = message
+        return reqs + r, recv
+
     def sync(self, sync_buffer):
         norms = sync_buffer["flatten_norms"].buffer
-        signs = sync_buffer["signs"]
         hw = _hdr_words(norms.numel())
-        message = sync_buffer["sign_message"]  # [norms | signs]: the two buffers above are views of it
-        reqs, synced = self._send(sync_buffer, message)
+        if "chunked" in sync_buffer:  # posted by compress, range by range
+            reqs, synced = sync_buffer["chunked"]
+        else:
+            reqs, synced = self._send(sync_buffer, sync_buffer["sign_message"])  # [norms | signs]
         sync_buffer["sync_reqs_1"] = reqs
         sync_buffer["sync_reqs_2"] = []
         sync_buffer["synced_message"] = synced

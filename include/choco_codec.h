@@ -192,6 +192,20 @@ int choco_sign_compress(const float* x, const float* xhat, int64_t n,
                         int32_t* packed, float* l1_norms,
                         void* ws, size_t ws_bytes, void* stream);
 
+/* Chunked sign pack (the exchange pipelined with compress, SURVEY.md §8(e);
+ * parallel_choco.py exchange_chunks): choco_sign_compress over the words [w0, w1) of the
+ * SAME layout (packed is the whole word array; w0 a multiple of 1024, w1 one too or N'),
+ * so each range's words can be sent as soon as its launch is queued.  The per-segment L1
+ * sums stay in the workspace's fp64 accumulators between calls; the call with finish = 1,
+ * issued LAST on the same stream and workspace, writes l1_norms and clears them.  A
+ * receiver needs the norms of every segment a range touches, and in the (32, N') layout
+ * every range touches every row's segments, so the norms header is sent last and the
+ * receiver decodes after the whole message (choco_sign_decompress_accumulate).
+ * Words and norms equal the whole-buffer call's (the norms up to fp64 summation order). */
+int choco_sign_compress_range(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
+                              int64_t w0, int64_t w1, int32_t finish, int32_t* packed, float* l1_norms,
+                              void* ws, size_t ws_bytes, void* stream);
+
 /* SignCompressor.unpacking (sparsification.py:147-163): +1.0 / -1.0 floats. */
 int choco_sign_unpack(const int32_t* packed, int64_t n, float* out, void* stream);
 
@@ -343,6 +357,9 @@ int choco_gossip_sign_compress(float* x, const float* memory, const float* xhat,
                                int64_t n, const int64_t* seg_off, int32_t nseg,
                                int32_t* packed, float* l1_norms,
                                void* ws, size_t ws_bytes, void* stream);
+int choco_gossip_sign_compress_range(float* x, const float* memory, const float* xhat, float gamma, int64_t n,
+                                     const int64_t* seg_off, int32_t nseg, int64_t w0, int64_t w1, int32_t finish,
+                                     int32_t* packed, float* l1_norms, void* ws, size_t ws_bytes, void* stream);
 int choco_gossip_qsgd_compress(float* x, const float* memory, const float* xhat, float gamma,
                                int64_t n, const int64_t* seg_off, int32_t nseg,
                                int32_t q, int32_t is_biased, uint64_t seed, uint64_t offset,

@@ -30,6 +30,18 @@ def _worker(rank, world, port, q):
             reqs, got = agg._agg(msg, op="get_raw_sync_data", force_wait=False)
             agg.complete_wait(reqs)
             res[str(dtype)] = {r: t.tolist() for r, t in got.items()}
+        # range-by-range posting into one receive buffer per neighbour (_agg out=, the
+        # chunked sign exchange): three slices, posted out of order
+        msg = torch.arange(101, dtype=torch.int32) * (rank + 1)
+        recv = {r: torch.full((101,), -1, dtype=torch.int32) for r in agg.neighbor_ranks}
+        reqs = []
+        for a, b in ((4, 40), (40, 101), (0, 4)):
+            rq, got = agg._agg(msg[a:b], op="get_raw_sync_data", force_wait=False,
+                               out={r: recv[r][a:b] for r in agg.neighbor_ranks})
+            assert all(got[r].data_ptr() == recv[r][a:b].data_ptr() for r in agg.neighbor_ranks)
+            reqs += rq
+        agg.complete_wait(reqs)
+        res["ranged"] = {r: t.tolist() for r, t in recv.items()}
         w = agg._agg(torch.full((4,), float(rank)), op="weighted", force_wait=True)
         res["weighted"] = w.tolist()
         q.put((rank, res))
@@ -57,5 +69,7 @@ def test_decentralized_exchange(world):
             assert sorted(got) == sorted(nb)
             for r in nb:
                 assert got[r] == (torch.arange(37) * (r + 1)).to(dtype).tolist()
+        for r, got in out[rank]["ranged"].items():
+            assert got == (torch.arange(101, dtype=torch.int32) * (r + 1)).tolist()
         exp = sum(float(r) * w for r, w in nb.items())
         assert all(abs(v - exp) < 1e-6 for v in out[rank]["weighted"])

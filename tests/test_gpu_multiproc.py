@@ -35,7 +35,8 @@ def _hdr(nseg):
 
 @pytest.mark.parametrize("comm_op,world", [("compress_top_k", 2), ("compress_top_k", 3), ("compress_random_k", 3),
                                            ("sign", 2), ("sign", 3), ("quantize_qsgd", 3),
-                                           ("quantize_qsgd_chunked", 2), ("quantize_qsgd_chunked", 3)])
+                                           ("quantize_qsgd_chunked", 2), ("quantize_qsgd_chunked", 3),
+                                           ("sign_chunked", 2), ("sign_chunked", 3)])
 def test_choco_round_across_processes(comm_op, world, tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_mp_choco_worker.py"), comm_op, str(world),
                         str(tmp_path)], capture_output=True, text=True, timeout=600)
@@ -66,7 +67,7 @@ def _verify_round(comm_op, world, tmp_path):
     # every worker's message, checked once against the oracle (as its neighbours received it)
     msgs = {}
     for q in range(world):
-        if comm_op.endswith("_chunked"):
+        if comm_op == "quantize_qsgd_chunked":
             # the chunked wire, re-assembled into the one-message layout (each range is a
             # self-contained [level | sign] message of its own elements: checked against the
             # oracle's packing of exactly those elements)
@@ -103,7 +104,7 @@ def _verify_round(comm_op, world, tmp_path):
             assert np.array_equal(rcv[K:].astype(np.int64), oi)
             assert same_bits(rcv[:K].view(np.float32), ov)
             msgs[q] = (ov, oi)
-        elif comm_op == "sign":
+        elif comm_op.startswith("sign"):  # sign_chunked: the same message, posted range by range
             hw = _hdr(nseg)
             norms = rcv[:hw].view(np.float32)[:nseg]
             assert np.array_equal(rcv[hw:], O.sign_pack(d))
@@ -133,7 +134,7 @@ def _verify_round(comm_op, world, tmp_path):
         if "top_k" in comm_op or "random_k" in comm_op:
             for q in ranks:
                 O.sparse_accumulate(hat if q == rank else None, mem, msgs[q][0], msgs[q][1], nb[q])
-        elif comm_op == "sign":
+        elif comm_op.startswith("sign"):
             O.sign_accumulate(hat, mem, [msgs[q] for q in ranks], [nb[q] for q in ranks], ranks.index(rank), lens)
         else:
             O.qsgd_accumulate(hat, mem, [msgs[q] for q in ranks], [nb[q] for q in ranks], ranks.index(rank))

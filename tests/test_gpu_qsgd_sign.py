@@ -169,6 +169,45 @@ def test_sign_segmented_norms(layout):
     assert np.allclose(host(norms), O.l1_norms(host(x), lens), rtol=1e-7, atol=0)
 
 
+@pytest.mark.parametrize("layout", ["one_segment", "resnet20_cifar10", "tiny_segments"])
+@pytest.mark.parametrize("chunks", [2, 3, 7])
+@pytest.mark.parametrize("fused", [False, True])
+def test_sign_compress_ranges(layout, chunks, fused):
+    """The chunked pack (choco_sign_compress_range, exchange_chunks): words bit-exact and
+    norms as the oracle's, x_new (fused consensus step) bit-identical to the whole-buffer
+    call; the finishing range leaves the accumulators clear for the next message."""
+    from chocosgd_amd import codec
+    if layout == "one_segment":
+        lens = [1_000_007]
+    elif layout == "tiny_segments":
+        lens = np.random.default_rng(1).integers(1, 3000, size=700).tolist()
+    else:
+        lens = golden_json("layouts.json")[layout]
+    n, nseg, so = sum(lens), len(lens), seg_table(lens)
+    x, xh, mem = randn(n, 41), randn(n, 42, 0.5), randn(n, 43)
+    gamma = 0.37
+    x_whole = x.clone()
+    if fused:
+        codec.gossip_step(x_whole, mem, xh, gamma)
+    d = host(x_whole) - host(xh)
+    ranges = codec.sign_chunks(n, chunks)
+    assert ranges[0][0] == 0 and ranges[-1][1] == codec.sign_words(n)
+    for rep in range(2):
+        xr = x.clone()
+        packed = torch.full((codec.sign_words(n),), -1, dtype=torch.int32, device=DEV)
+        norms = torch.full((nseg,), -1.0, device=DEV)
+        for i, (w0, w1) in enumerate(ranges):
+            codec.sign_compress_range(xr, w0, w1, i == len(ranges) - 1, xhat=xh, seg_off=so, nseg=nseg,
+                                      gossip=(mem, gamma) if fused else None, out=(packed, norms))
+        assert np.array_equal(host(packed), O.sign_pack(d)), rep
+        assert np.allclose(host(norms), O.l1_norms(d, lens), rtol=1e-7, atol=0), rep
+        if fused:
+            assert same_bits(host(xr), host(x_whole)), rep
+    with pytest.raises(RuntimeError, match="word range"):
+        codec.sign_compress_range(x, 512, codec.sign_words(n), True, xhat=xh, seg_off=so, nseg=nseg,
+                                  out=(packed, norms))
+
+
 def test_choco_sign_round_trip_golden():
     from chocosgd_amd import codec
     g = golden("choco_sign_mini")

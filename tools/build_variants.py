@@ -13,6 +13,8 @@ VARIANTS = {
     "acc_seg8": ["CHOCO_ACC_SEGF=8"],
     "acc_seg32": ["CHOCO_ACC_SEGF=32"],
     "qq_nt": ["CHOCO_QQUANT_NT=1"],
+    "qq_fwd": ["CHOCO_QQUANT_REV=0"],
+    "qq_fwd_nt": ["CHOCO_QQUANT_REV=0", "CHOCO_QQUANT_NT=1"],
     "qn_plain": ["CHOCO_QNORM_NT=0"],
     "sign_acc1": ["CHOCO_SIGN_ACC1=1"],
     "g_form0": ["CHOCO_GOSSIP_FORM=0"],
