@@ -51,7 +51,10 @@
 namespace choco {
 
 constexpr int kSegTile = 16384;                       // elements per tile
-constexpr int kSegThreads = 1024;                     // 4 rows of 1024 float4 = one tile
+#ifndef CHOCO_SEG_THREADS  // threads of the tile kernels S1 / S2 (rows of float4 per thread = 4096 / threads)
+#define CHOCO_SEG_THREADS 1024
+#endif
+constexpr int kSegThreads = CHOCO_SEG_THREADS;
 constexpr int kSegRows = kSegTile / (4 * kSegThreads);
 constexpr int kSegMaxTiles = 1024;                    // tiles per batched segment (S3: one per thread)
 constexpr int64_t kSegBatchMax = (int64_t)kSegTile * kSegMaxTiles;
@@ -181,19 +184,31 @@ CHOCO_DEV void tile_load_gossip(const float* __restrict__ x, const float* __rest
 CHOCO_DEV int tile_elem(int r, int q) { return r * 4 * kSegThreads + 4 * (int)threadIdx.x + q; }
 
 // Over hist[kH] in LDS or global memory (ascending key order), the bin holding
-// the rank-th largest entry and the rank inside it -> out[0], out[1].  Two bins
-// per thread of the kSegThreads workgroup; ends with a barrier.
-CHOCO_DEV void block_find_rank2k(uint32_t h0, uint32_t h1, uint32_t rank, uint32_t* scratch, uint32_t* out) {
+// the rank-th largest entry and the rank inside it -> out[0], out[1].  kBpt
+// consecutive bins per thread of the kSegThreads workgroup (hv[b] = bin kBpt*tid + b);
+// ends with a barrier.
+constexpr int kBpt = kH / kSegThreads;
+static_assert(kBpt * kSegThreads == kH, "whole bins per thread");
+CHOCO_DEV void block_find_rank(const uint32_t (&hv)[kBpt], uint32_t rank, uint32_t* scratch, uint32_t* out) {
   const int tid = threadIdx.x;
-  const uint32_t local = h0 + h1;
+  uint32_t local = 0;
+#pragma unroll
+  for (int b = 0; b < kBpt; ++b) local += hv[b];
   uint32_t total;
   const uint32_t pre = block_excl_scan(local, scratch, &total);
-  const uint32_t above = total - pre - local;  // entries in bins above my two
+  uint32_t above = total - pre - local;  // entries in bins above mine
   if (above < rank && rank <= above + local) {
-    if (rank <= above + h1) { out[0] = 2 * tid + 1; out[1] = rank - above; }
-    else { out[0] = 2 * tid; out[1] = rank - above - h1; }
+#pragma unroll
+    for (int b = kBpt - 1; b >= 0; --b) {
+      if (above < rank && rank <= above + hv[b]) { out[0] = kBpt * tid + b; out[1] = rank - above; }
+      above += hv[b];
+    }
   }
   __syncthreads();
+}
+CHOCO_DEV void load_bins(const uint32_t* h, uint32_t (&hv)[kBpt]) {
+#pragma unroll
+  for (int b = 0; b < kBpt; ++b) hv[b] = h[kBpt * threadIdx.x + b];
 }
 
 // ---------------------------------------------------------------- S1: coarse histogram (cold)
@@ -298,7 +313,9 @@ CHOCO_DEV void seg_exact_tile(const float (&v)[kSegRows][4], const TileCtx& c, u
           if (tile_elem(r, q) < c.tl && (key[r][q] & maskhi) == prefix)
             atomicAdd(&h[(key[r][q] >> shs[rd]) & dms[rd]], 1u);
       __syncthreads();
-      block_find_rank2k(h[2 * tid], h[2 * tid + 1], krem, scratch, bc);
+      uint32_t hv[kBpt];
+      load_bins(h, hv);
+      block_find_rank(hv, krem, scratch, bc);
       prefix |= bc[0] << shs[rd];
       maskhi |= dms[rd] << shs[rd];
       krem = bc[1];
@@ -351,10 +368,13 @@ CHOCO_DEV void seg_exact_tile(const float (&v)[kSegRows][4], const TileCtx& c, u
 // feed hist2 by bits 19..9.  Warm: the floor is the window's lo, every candidate
 // feeds hist2 by its window bin min((key - lo) >> sh, 2047); GS: the fused gossip
 // step happens here (the one read).
-// (8 waves per SIMD = two workgroups per CU: <= 64 VGPRs; one per CU measured ~10 us
-// slower at ResNet-50)
+// (8 waves per SIMD: <= 64 VGPRs; 2 x 1024 or 4 x 512 threads per CU.  Fewer
+// workgroups per CU measured ~10 us slower at ResNet-50)
 template <bool XH, bool WARM, bool GS = false>
-__global__ __launch_bounds__(kSegThreads, 8) void seg_collect_kernel(
+#ifndef CHOCO_SEG_WPE  // waves per SIMD the collect kernel is compiled for (VGPR budget 512 / WPE)
+#define CHOCO_SEG_WPE (kSegThreads == 1024 ? 8 : 6)
+#endif
+__global__ __launch_bounds__(kSegThreads, CHOCO_SEG_WPE) void seg_collect_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ plan, int nseg,
     const uint32_t* __restrict__ hist1, uint32_t* __restrict__ hist2, uint32_t* __restrict__ info,
     uint32_t* __restrict__ tilecnt, float* __restrict__ cval, uint32_t* __restrict__ cidx,
@@ -385,8 +405,9 @@ __global__ __launch_bounds__(kSegThreads, 8) void seg_collect_kernel(
     __syncthreads();
   } else {
     const uint32_t* __restrict__ g1 = hist1 + (int64_t)c.s * kH;
-    const uint32_t c0 = g1[2 * tid], c1 = g1[2 * tid + 1];
-    block_find_rank2k(c0, c1, (uint32_t)c.R.k, scratch, bc);
+    uint32_t hv[kBpt];
+    load_bins(g1, hv);
+    block_find_rank(hv, (uint32_t)c.R.k, scratch, bc);
     b1 = bc[0];
     if (c.j == 0 && tid == 0) {
       info[8 * c.s + 0] = b1;
