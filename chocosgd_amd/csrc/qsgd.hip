@@ -323,9 +323,13 @@ struct QDiv {
     const float q0 = t * y;
     const float r = fmaf(-q0, norm, t);
     slow = !(fast && ((q0 >= 0x1p-60f && q0 <= 0x1p7f) || t == 0.0f));
-    return t == 0.0f ? 0.0f : fmaf(r, y, q0);
+    return fmaf(r, y, q0);  // t = +0 (s * |d|): q0 = r = +0 -> +0, as 0 / norm
   }
 };
+
+// The container value of a level: NaN -> 0, levels >= s -> s (a pinned norm below
+// |d|), as one branch-free clamp (fmaxf(NaN, 0) = 0); levels are >= 0 and integral.
+CHOCO_DEV uint32_t level_code(float lvl, float sf) { return (uint32_t)fminf(fmaxf(lvl, 0.0f), sf); }
 
 // One quantized element: level (clamped container value, 0 for NaN), sign bit.
 CHOCO_DEV float qlevel(float lf, float u) {
@@ -357,7 +361,6 @@ __device__ __noinline__ void qsgd_quant_tile_slow(const float* __restrict__ x, c
                                                   uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
                                                   float* __restrict__ dense_out, int64_t tile, int sg0) {
   const float sf = (float)s_levels;
-  const uint32_t smax = (uint32_t)s_levels;
   const int64_t eb = tile * kQStreamTile + (int64_t)threadIdx.x * kQPer;
   Xoro128 rng;
   if (!u_in) rng.seed(qrng_key(seed, offset), ((uint64_t)tile << 8) | threadIdx.x);
@@ -379,7 +382,7 @@ __device__ __noinline__ void qsgd_quant_tile_slow(const float* __restrict__ x, c
         const QParam Q = qparam(norms, seg_off, n, s, s_levels, biased != 0);
         const float dv = dval(x, xh, e);
         const float lvl = qlevel((sf * fabsf(dv)) / Q.norm, uu[h]);  // s * x.abs() / norm
-        const uint32_t li = lvl == lvl ? (lvl >= sf ? smax : (uint32_t)lvl) : 0u;
+        const uint32_t li = level_code(lvl, sf);
         const int bp = (c + h) * CW;
         if (bp < 64) lacc[0] |= (uint64_t)li << bp; else lacc[1] |= (uint64_t)li << (bp - 64);
         sbits |= dv < 0.f ? (1u << (c + h)) : 0u;
@@ -422,7 +425,6 @@ __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
     for (int64_t b = sgn_used + threadIdx.x; b < sgn_end; b += kQThreads) sign_plane[b] = 0;
   }
   const float sf = (float)s_levels;
-  const uint32_t smax = (uint32_t)s_levels;
   const int64_t eb = t_e0 + (int64_t)threadIdx.x * kQPer;  // group g starts at eb + g * 2048
   constexpr int GS = kQThreads * kQPer;                    // 2048
   if (!uniform || t_e1 - t_e0 != kQStreamTile) {
@@ -493,21 +495,23 @@ __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
     }
     uint32_t lv[kQPer];
     uint32_t sbits = 0;
-    float outv[kQPer];
+    float lvlf[kQPer];
 #pragma unroll
     for (int c = 0; c < kQPer; ++c) {
-      const float lvl = qlevel(lf[c], u[g][c]);
-      if (dense) {
-        const float sg = d[g][c] > 0.f ? 1.0f : (d[g][c] < 0.f ? -1.0f : 0.0f);  // torch.sign (NaN -> 0)
-        outv[c] = (((P.scale * sg) * P.norm) * lvl) / sf;
-      }
-      lv[c] = lvl == lvl ? (lvl >= sf ? smax : (uint32_t)lvl) : 0u;
+      lvlf[c] = qlevel(lf[c], u[g][c]);
+      lv[c] = level_code(lvlf[c], sf);
       sbits |= d[g][c] < 0.f ? (1u << c) : 0u;
     }
     const int64_t t = e0 / kQPer;
     store_levels<CW>(lvl_plane, t, lv);
     sign_plane[t] = (uint8_t)sbits;
-    if (dense) {
+    if (dense) {  // one branch per group (a branch per element made the compiler shuffle the group's registers)
+      float outv[kQPer];
+#pragma unroll
+      for (int c = 0; c < kQPer; ++c) {
+        const float sg = d[g][c] > 0.f ? 1.0f : (d[g][c] < 0.f ? -1.0f : 0.0f);  // torch.sign (NaN -> 0)
+        outv[c] = (((P.scale * sg) * P.norm) * lvlf[c]) / sf;
+      }
       *reinterpret_cast<float4*>(dense_out + e0) = make_float4(outv[0], outv[1], outv[2], outv[3]);
       *reinterpret_cast<float4*>(dense_out + e0 + 4) = make_float4(outv[4], outv[5], outv[6], outv[7]);
     }
