@@ -68,7 +68,10 @@ constexpr int kRkWords = (int)(kRkTile / 32);            // 8192 bitmap words pe
 // 8 KB of LDS) with kRkQThreads threads of 8 words (256 bits) each: ~6 small
 // workgroups per CU instead of 1-2 large ones (382 tiles on 256 CUs left half the
 // CUs with two 1024-thread tiles and set the tail: 44.7 us at 100M).
-constexpr int kRkQ = 4;
+#ifndef CHOCO_RK_Q  // workgroups per tile (A/B knob)
+#define CHOCO_RK_Q 4
+#endif
+constexpr int kRkQ = CHOCO_RK_Q;
 constexpr int kRkQThreads = 256;
 constexpr int kRkQWords = kRkWords / kRkQ;               // 2048
 constexpr int kRkWpt = kRkQWords / kRkQThreads;          // 8 words (256 bits) per thread

@@ -14,6 +14,7 @@ VARIANTS = {
     "acc_seg32": ["CHOCO_ACC_SEGF=32"],
     "qq_nt": ["CHOCO_QQUANT_NT=1"],
     "qq_fwd": ["CHOCO_QQUANT_REV=0"],
+    "rk_q2": ["CHOCO_RK_Q=2"],
     "seg512_w6": ["CHOCO_SEG_THREADS=512", "CHOCO_SEG_WPE=6"],
     "seg512_w5": ["CHOCO_SEG_THREADS=512", "CHOCO_SEG_WPE=5"],
     "seg512_w4": ["CHOCO_SEG_THREADS=512", "CHOCO_SEG_WPE=4"],
