@@ -162,3 +162,19 @@ def test_get_n_bits():
     from chocosgd_amd.sparsification import get_n_bits
     assert get_n_bits(torch.zeros(10, dtype=torch.float32)) == 320
     assert get_n_bits(torch.zeros(10, dtype=torch.int32)) == 320
+
+
+@pytest.mark.parametrize("n", [1, 31, 32 * 1024, 32 * 1024 + 1, 1_000_007, 345_000_000])
+@pytest.mark.parametrize("chunks", [1, 2, 3, 7, 64])
+def test_chunked_wire_ranges(n, chunks):
+    """The chunked exchanges' ranges (host side): they tile the buffer in order, starts on
+    the kernels' alignment (QSGD: 8192 elements; sign: 1024 words), at most `chunks` of them."""
+    from chocosgd_amd import codec
+    for ranges, end, align in ((codec.qsgd_chunks(n, chunks), n, codec.QSGD_RANGE_ALIGN),
+                               (codec.sign_chunks(n, chunks), codec.sign_words(n), codec.SIGN_RANGE_ALIGN)):
+        assert 1 <= len(ranges) <= chunks
+        assert ranges[0][0] == 0 and ranges[-1][1] == end
+        for (a0, a1), (b0, _) in zip(ranges, ranges[1:]):
+            assert a1 == b0
+        for a0, a1 in ranges:
+            assert a0 < a1 and a0 % align == 0 and (a1 % align == 0 or a1 == end)
