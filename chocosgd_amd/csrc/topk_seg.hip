@@ -134,17 +134,17 @@ CHOCO_DEV TileCtx tile_ctx(const int64_t* __restrict__ plan, int nseg, int64_t b
 // The tile's values: row r, thread t <-> elements r * 4096 + 4t .. +3 (dword-
 // aligned buffer loads: x + start needs only 4-byte alignment; past the tile
 // the loads return zeros and the elements are masked by `valid`).
-template <bool XH>
+template <bool XH, bool NT = false>
 CHOCO_DEV void tile_load(const float* __restrict__ x, const float* __restrict__ xh, const TileCtx& c,
                          float (&v)[kSegRows][4]) {
   const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x + c.start, (uint32_t)c.tl * 4u);
   const __amdgpu_buffer_rsrc_t rh = buf_rsrc((XH ? xh : x) + c.start, (uint32_t)c.tl * 4u);
   float4 a[kSegRows], h[kSegRows];
 #pragma unroll
-  for (int r = 0; r < kSegRows; ++r) a[r] = ld_buf4<false>(rx, (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u);
+  for (int r = 0; r < kSegRows; ++r) a[r] = ld_buf4<NT>(rx, (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u);
   if (XH) {
 #pragma unroll
-    for (int r = 0; r < kSegRows; ++r) h[r] = ld_buf4<false>(rh, (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u);
+    for (int r = 0; r < kSegRows; ++r) h[r] = ld_buf4<NT>(rh, (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u);
   }
 #pragma unroll
   for (int r = 0; r < kSegRows; ++r) {
@@ -371,6 +371,9 @@ CHOCO_DEV void seg_exact_tile(const float (&v)[kSegRows][4], const TileCtx& c, u
 // (8 waves per SIMD: <= 64 VGPRs; 2 x 1024 or 4 x 512 threads per CU.  Fewer
 // workgroups per CU measured ~10 us slower at ResNet-50)
 template <bool XH, bool WARM, bool GS = false>
+#ifndef CHOCO_SEG_WARM_NT  // 1: W2's one read of the delta uses non-temporal loads
+#define CHOCO_SEG_WARM_NT 1
+#endif
 #ifndef CHOCO_SEG_WPE  // waves per SIMD the collect kernel is compiled for (VGPR budget 512 / WPE)
 #define CHOCO_SEG_WPE (kSegThreads == 1024 ? 8 : 6)
 #endif
@@ -389,7 +392,7 @@ __global__ __launch_bounds__(kSegThreads, CHOCO_SEG_WPE) void seg_collect_kernel
   const int tid = threadIdx.x;
   float v[kSegRows][4] = {};
   if (GS) tile_load_gossip<true>(x, xh, gs, c, v);  // in flight while the floor is found
-  else tile_load<XH>(x, xh, c, v);
+  else tile_load<XH, WARM && CHOCO_SEG_WARM_NT>(x, xh, c, v);  // warm: the only read of the call
   if (c.R.ntile == 1) {  // workgroup-uniform: the whole segment is here
     seg_exact_tile(v, c, h2, scratch, bc, rc_cnt, out_val, out_idx);
     return;
