@@ -114,6 +114,22 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_kernel(const float* __r
 #ifndef CHOCO_ACC_SEGF
 #define CHOCO_ACC_SEGF 16
 #endif
+#ifndef CHOCO_ACC_NT  // cache policy of the owner's segment RMW (A/B): 0 default, 1 nt stores, 2 nt loads + stores
+#define CHOCO_ACC_NT 0
+#endif
+CHOCO_DEV float4 acc_ld4(const float* p) {
+  if (CHOCO_ACC_NT >= 2) return ld_nt4(p);
+  return *reinterpret_cast<const float4*>(p);
+}
+CHOCO_DEV void acc_st4(float* p, float4 v) {
+  if (CHOCO_ACC_NT >= 1) {
+    choco_f32x4 f;
+    f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
+    __builtin_nontemporal_store(f, reinterpret_cast<choco_f32x4*>(p));
+  } else {
+    *reinterpret_cast<float4*>(p) = v;
+  }
+}
 constexpr int kSegF = CHOCO_ACC_SEGF;  // floats per owned segment (16: 64 B)
 constexpr int kSegL = kSegF / 4;       // lanes per update (one float4 each)
 constexpr int kSegShift = kSegF == 32 ? 5 : (kSegF == 16 ? 4 : 3);
@@ -141,10 +157,10 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_seg_kernel(const float*
       const bool full = base + 4 <= n;
       float hv[4] = {0.f, 0.f, 0.f, 0.f}, mv[4] = {0.f, 0.f, 0.f, 0.f};
       if (full) {
-        const float4 m4 = *reinterpret_cast<const float4*>(mem + base);
+        const float4 m4 = acc_ld4(mem + base);
         mv[0] = m4.x; mv[1] = m4.y; mv[2] = m4.z; mv[3] = m4.w;
         if (HS) {
-          const float4 h4 = *reinterpret_cast<const float4*>(hat + base);
+          const float4 h4 = acc_ld4(hat + base);
           hv[0] = h4.x; hv[1] = h4.y; hv[2] = h4.z; hv[3] = h4.w;
         }
       } else {
@@ -171,8 +187,8 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_seg_kernel(const float*
         }
       }
       if (full) {
-        *reinterpret_cast<float4*>(mem + base) = make_float4(mv[0], mv[1], mv[2], mv[3]);
-        if (HS) *reinterpret_cast<float4*>(hat + base) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+        acc_st4(mem + base, make_float4(mv[0], mv[1], mv[2], mv[3]));
+        if (HS) acc_st4(hat + base, make_float4(hv[0], hv[1], hv[2], hv[3]));
       } else {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {

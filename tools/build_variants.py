@@ -16,6 +16,8 @@ VARIANTS = {
     "qq_fwd": ["CHOCO_QQUANT_REV=0"],
     "rk_q2": ["CHOCO_RK_Q=2"],
     "seg_wnt0": ["CHOCO_SEG_WARM_NT=0"],
+    "acc_nt1": ["CHOCO_ACC_NT=1"],
+    "acc_nt2": ["CHOCO_ACC_NT=2"],
     "seg512_w6": ["CHOCO_SEG_THREADS=512", "CHOCO_SEG_WPE=6"],
     "seg512_w5": ["CHOCO_SEG_THREADS=512", "CHOCO_SEG_WPE=5"],
     "seg512_w4": ["CHOCO_SEG_THREADS=512", "CHOCO_SEG_WPE=4"],
