@@ -10,7 +10,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libchoco_codec.so")
+# CHOCO_CODEC_LIB: another build of the same ABI (the A/B variants of tools/build_variants.py)
+LIB_PATH = os.environ.get("CHOCO_CODEC_LIB") or os.path.join(_HERE, "lib", "libchoco_codec.so")
 
 TOPK_STATUS_OFFSET = 0        # CHOCO_TOPK_STATUS_OFFSET
 TOPK_FALLBACKS_OFFSET = 4     # CHOCO_TOPK_FALLBACKS_OFFSET

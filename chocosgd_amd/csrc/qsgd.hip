@@ -30,7 +30,11 @@ namespace choco {
 constexpr int kQThreads = 256;
 constexpr int kQPer = 8;                         // elements per thread in the quantize/decode passes
 constexpr int kQTile = kQThreads * kQPer;        // 2048
-constexpr int kNormTile = 32768;                 // elements per workgroup in the norm pass
+#ifndef CHOCO_QNORM_TILE  // elements per workgroup in the norm pass (a multiple of 8192)
+#define CHOCO_QNORM_TILE 32768
+#endif
+constexpr int kNormTile = CHOCO_QNORM_TILE;
+static_assert(kNormTile % 8192 == 0, "whole load rounds per norm tile");
 constexpr int kQMaxMsg = 8;
 
 struct QsgdWs {

@@ -18,6 +18,8 @@ VARIANTS = {
     "seg_wnt0": ["CHOCO_SEG_WARM_NT=0"],
     "acc_nt1": ["CHOCO_ACC_NT=1"],
     "acc_nt2": ["CHOCO_ACC_NT=2"],
+    "qn_t48k": ["CHOCO_QNORM_TILE=49152"],
+    "qn_t64k": ["CHOCO_QNORM_TILE=65536"],
     "seg512_w6": ["CHOCO_SEG_THREADS=512", "CHOCO_SEG_WPE=6"],
     "seg512_w5": ["CHOCO_SEG_THREADS=512", "CHOCO_SEG_WPE=5"],
     "seg512_w4": ["CHOCO_SEG_THREADS=512", "CHOCO_SEG_WPE=4"],
