@@ -30,8 +30,9 @@ namespace choco {
 constexpr int kQThreads = 256;
 constexpr int kQPer = 8;                         // elements per thread in the quantize/decode passes
 constexpr int kQTile = kQThreads * kQPer;        // 2048
-#ifndef CHOCO_QNORM_TILE  // elements per workgroup in the norm pass (a multiple of 8192)
-#define CHOCO_QNORM_TILE 32768
+#ifndef CHOCO_QNORM_TILE  // elements per workgroup in the norm pass (a multiple of 8192): 49152 -> ~2040
+                          // workgroups at 100M, one round of 8 per CU (r03 A/B: 32768 and 65536 slower)
+#define CHOCO_QNORM_TILE 49152
 #endif
 constexpr int kNormTile = CHOCO_QNORM_TILE;
 static_assert(kNormTile % 8192 == 0, "whole load rounds per norm tile");
