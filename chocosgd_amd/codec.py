@@ -69,52 +69,37 @@ def workspace(dev, kind, nbytes):
 
 
 class TopkStatus:
-    """Lazy check of a top-k workspace's sticky status word (include/choco_codec.h,
-    CHOCO_TOPK_STATUS_OFFSET): every `every`-th call queues a non-blocking copy of the
-    word to pinned host memory behind its launches (a 4-byte copy per call would sit in
-    the stream of every step); `check()` raises RuntimeError once such a copy has landed
-    nonzero -- the output of the call that set it is invalid -- and clears the word.
-    `check(wait=True)` copies and waits (end of training, checkpoints)."""
+    """Check of a top-k workspace's sticky status word (include/choco_codec.h,
+    CHOCO_TOPK_STATUS_OFFSET) through its pinned host mirror: the device raises the bits
+    there with a system-scope store, so `check()` -- called before every top-k call --
+    reads host memory only (no copy on the stream, no synchronisation) and raises
+    RuntimeError as soon as a call whose bounded fallback wait gave up has run on the GPU;
+    that call's output (and whatever was computed from it: the model state of a CHOCO step
+    that applied it) is invalid.  `check(wait=True)` first waits for the stream (teardown,
+    checkpoints).  Holds the workspace's address only, never the tensor: a dropped
+    workspace or SegmentPlan frees its device memory."""
 
-    def __init__(self, ws, every=16):
-        self.word = ws[_lib.TOPK_STATUS_OFFSET:_lib.TOPK_STATUS_OFFSET + 4].view(torch.int32)
-        self.host = torch.zeros(1, dtype=torch.int32).pin_memory()
-        self.event = None
-        self.every = every
-        self.calls = 0
-
-    def arm(self):
-        self.host.copy_(self.word, non_blocking=True)
-        self.event = torch.cuda.Event()
-        self.event.record(torch.cuda.current_stream(self.word.device))
-
-    def after_call(self):
-        self.calls += 1
-        if self.event is None and self.calls % self.every == 0:
-            self.arm()
+    def __init__(self, ws):
+        self.ptr = ws.data_ptr()
+        self.device = ws.device
 
     def check(self, wait=False):
-        if wait and self.event is None:
-            self.arm()
-        if self.event is None:
-            return
         if wait:
-            self.event.synchronize()
-        elif not self.event.query():
-            return
-        self.event = None
-        bad = int(self.host.item())
+            torch.cuda.current_stream(self.device).synchronize()
+        bad = int(lib().choco_topk_host_status(ctypes.c_void_p(self.ptr), 1, _stream(self.device)))
+        if bad < 0:
+            raise RuntimeError(f"choco_topk_host_status failed: {_lib.last_error()}")
         if bad:
-            self.word.zero_()
             raise RuntimeError(f"top-k: status word {bad:#x}: a bounded wait of the exact fallback gave up, so the "
-                               "output of an earlier call on this workspace is invalid")
+                               "output of an earlier call on this workspace is invalid (and every state it was "
+                               "applied to)")
 
 
 _status = {}
 
 
 def topk_status(ws):
-    """The TopkStatus of a workspace tensor (one per workspace)."""
+    """The TopkStatus of a workspace tensor (one per workspace address)."""
     st = _status.get(ws.data_ptr())
     if st is None:
         st = _status[ws.data_ptr()] = TopkStatus(ws)
@@ -224,7 +209,6 @@ def topk(x, k, xhat=None, out=None, gossip=None):
     else:
         _lib.check(L.choco_topk_compress(_ptr(x), _ptr(xhat), n, int(k), _ptr(vals), _ptr(idx), _ptr(ws),
                                          ws.numel(), _stream(dev)), "choco_topk_compress")
-    st.after_call()
     return vals, idx
 
 
@@ -335,7 +319,6 @@ def topk_segmented(x, plan, xhat=None, out=None, gossip=None):
         torch.cuda.synchronize(dev)
         plan.drop_workspace(dev)
         raise
-    st.after_call()
     return vals, idx
 
 

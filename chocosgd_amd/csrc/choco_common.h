@@ -348,11 +348,20 @@ enum TopkMode { kData = 0, kHash = 1 };
 size_t topk_ws_bytes(int64_t n);
 // gs.mem != nullptr: the gossip step is applied to x[0, n) first (fused into the
 // stream pass where the path has one); x is then written.
-// status: the sticky status word the exact fallback flags (nullptr: the workspace's own,
-// at CHOCO_TOPK_STATUS_OFFSET).
+// Where a call flags an invalid output (the exact fallback's bounded wait gave up): the
+// sticky device status word of a workspace (at CHOCO_TOPK_STATUS_OFFSET) and its pinned
+// host mirror (choco_topk_host_status), written with a system-scope store so the host
+// sees it without a copy or a synchronisation.  dev == nullptr: the call's own workspace.
+struct StatusSink {
+  uint32_t* dev;
+  uint32_t* host;
+};
+// the pinned, mapped host mirror of workspace ws's status word (device pointer; nullptr
+// if pinned memory is unavailable), allocated on first use
+uint32_t* host_status_dev(const void* ws);
 int topk_pipeline(int mode, const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                   float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes, hipStream_t st,
-                  Gossip gs = Gossip{nullptr, 0.f}, uint32_t* status = nullptr);
+                  Gossip gs = Gossip{nullptr, 0.f}, StatusSink status = StatusSink{nullptr, nullptr});
 // forget the warm-start records of the top-k workspaces in [ws, ws + bytes) (include/choco_codec.h)
 void topk_warm_forget(const void* ws, size_t bytes);
 void seg_forget(const void* ws, size_t bytes);  // ... of the segmented workspaces (topk_seg.hip)

@@ -1479,7 +1479,7 @@ template <int MODE, bool XH>
 CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
                              float scale, WideCtrl* W, uint32_t* __restrict__ gcnt, float* __restrict__ out_val,
                              int32_t* __restrict__ out_idx, int64_t idx_base, ExactSmem& es, uint32_t* s_tk,
-                             uint32_t* __restrict__ status, TopkBounds* next) {
+                             uint32_t* __restrict__ status, uint32_t* __restrict__ host_status, TopkBounds* next) {
   const int tid = threadIdx.x;
   const bool w0 = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;  // wave-uniform
   for (;;) {
@@ -1496,8 +1496,11 @@ CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uin
                          ld_sc1(&W->done[4]));
 #endif
     if (phase > 0) {
-      if (w0 && !wave0_poll_ge(&W->done[phase - 1], nb) && lane_id() == 0)
+      if (w0 && !wave0_poll_ge(&W->done[phase - 1], nb) && lane_id() == 0) {
         atomicOr(status, kStatusPollTimeout);
+        // the pinned host mirror: the host sees it at its next call, no copy, no sync
+        if (host_status) __hip_atomic_store(host_status, kStatusPollTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       __syncthreads();
     }
     const int64_t lo = (int64_t)t * tile, hi = min(lo + (int64_t)tile, n);
@@ -1696,7 +1699,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     const uint32_t* __restrict__ cntw, const uint32_t* __restrict__ side, const float* __restrict__ cval,
     const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
     int64_t idx_base, WideCtrl* __restrict__ wide, uint32_t* __restrict__ gcnt, uint32_t par,
-    uint32_t* __restrict__ status, const uint32_t* __restrict__ tinfo) {
+    uint32_t* __restrict__ status, uint32_t* __restrict__ host_status, const uint32_t* __restrict__ tinfo) {
   __shared__ FinSmem fs;
   __shared__ ExactSmem es;
   __shared__ uint32_t s_tk;
@@ -1767,7 +1770,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     // by every workgroup through the ticketed queue (wide_fallback)
     Src<MODE, XH> src{x, xh, seed};
     wide_fallback(src, n, k, tile, nb, scale, wide, gcnt, out_val, out_idx, idx_base, es, &s_tk, status,
-                  MODE == kData ? &ctrl->bounds[par ^ 1u] : nullptr);
+                  host_status, MODE == kData ? &ctrl->bounds[par ^ 1u] : nullptr);
   } else {
     // ---- thread t <-> tile t: bucket-j* key count and side-list offset
     uint32_t above = 0, cb = 0, off = 0;
@@ -2015,11 +2018,11 @@ static WarmClaim warm_claim(const void* ws, int64_t n, int64_t k, bool data) {
 // GS: the gossip step fused into K1's sample and K2's stream (x written by K2);
 // K34 and its exact fallback then read (x_new, xh).
 // status: where the exact fallback flags a bounded wait that gave up (the
-// workspace's own status word, or the segmented workspace's).
+// workspace's own status word and host mirror, or the segmented workspace's).
 template <int MODE, bool XH, bool GS = false>
 static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                        float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes,
-                       hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}, uint32_t* status = nullptr) {
+                       hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}, StatusSink status = StatusSink{nullptr, nullptr}) {
   if (k >= n) {
     const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
     profile_begin("topk_all", st);
@@ -2046,7 +2049,7 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   uint32_t* side = reinterpret_cast<uint32_t*>(base + L.off_side);
   float* cval = reinterpret_cast<float*>(base + L.off_cval);
   uint32_t* cidx = reinterpret_cast<uint32_t*>(base + L.off_cidx);
-  if (status == nullptr) status = &ctrl->status;
+  if (status.dev == nullptr) status = StatusSink{&ctrl->status, host_status_dev(ws)};
   uint32_t hs_lo = 0;
   uint64_t hs_hi = 0;
   if (MODE == kHash) {
@@ -2085,7 +2088,7 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   CHOCO_KLAUNCH((topk_finish_kernel<MODE, XH>), dim3(L.nb), dim3(kK4Threads), 0, st, x, xh, n, k, L.tile, L.nb,
                 L.side_cap, seed, scale, ctrl, cum, cntw, side, cval, cidx, out_val, out_idx, idx_base,
                 reinterpret_cast<WideCtrl*>(base + L.off_wide), reinterpret_cast<uint32_t*>(base + L.off_gcnt), par,
-                status, reinterpret_cast<const uint32_t*>(base + L.off_tinfo));
+                status.dev, status.host, reinterpret_cast<const uint32_t*>(base + L.off_tinfo));
   profile_end("topk_finish", st);
   CHOCO_LAUNCHED("topk_finish_kernel");
   return CHOCO_OK;
@@ -2094,7 +2097,7 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
 template <int MODE>
 static int dispatch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                          float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes,
-                         hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}, uint32_t* status = nullptr) {
+                         hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}, StatusSink status = StatusSink{nullptr, nullptr}) {
   CHOCO_REQUIRE(x != nullptr && out_val != nullptr && out_idx != nullptr, "null pointer argument");
   CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n must be in [1, 2^31-1), got %lld", (long long)n);
   CHOCO_REQUIRE(k >= 1 && k <= n, "k must be in [1, n], got k=%lld n=%lld", (long long)k, (long long)n);
@@ -2118,7 +2121,7 @@ static int dispatch_topk(const float* x, const float* xh, int64_t n, int64_t k, 
 
 int topk_pipeline(int mode, const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                   float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes, hipStream_t st,
-                  Gossip gs, uint32_t* status) {
+                  Gossip gs, StatusSink status) {
   if (mode == kHash)
     return dispatch_topk<kHash>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st, gs, status);
   return dispatch_topk<kData>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st, gs, status);
@@ -2126,13 +2129,60 @@ int topk_pipeline(int mode, const float* x, const float* xh, int64_t n, int64_t 
 
 bool topk_warm_enabled() { return g_warm_on.load(std::memory_order_relaxed); }
 
+// ---- pinned host mirrors of the workspaces' status words (choco_topk_host_status)
+struct HostStatus {
+  uint32_t* host;  // pinned, mapped, coherent
+  uint32_t* dev;   // its device address
+};
+static std::mutex g_hs_mu;
+static std::unordered_map<const void*, HostStatus> g_hs;
+
+uint32_t* host_status_dev(const void* ws) {
+  std::lock_guard<std::mutex> g(g_hs_mu);
+  auto it = g_hs.find(ws);
+  if (it != g_hs.end()) return it->second.dev;
+  HostStatus hs{nullptr, nullptr};
+  void* h = nullptr;
+  if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+    hs.host = static_cast<uint32_t*>(h);
+    __atomic_store_n(hs.host, 0u, __ATOMIC_RELEASE);
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess) hs.dev = static_cast<uint32_t*>(d);
+  }
+  g_hs.emplace(ws, hs);
+  return hs.dev;
+}
+
+static uint32_t host_status_read(const void* ws, bool clear) {
+  std::lock_guard<std::mutex> g(g_hs_mu);
+  auto it = g_hs.find(ws);
+  if (it == g_hs.end() || it->second.host == nullptr) return 0u;
+  const uint32_t v = __atomic_load_n(it->second.host, __ATOMIC_ACQUIRE);
+  if (clear && v != 0u) __atomic_store_n(it->second.host, 0u, __ATOMIC_RELEASE);
+  return v;
+}
+
 void topk_warm_forget(const void* ws, size_t bytes) {
-  std::lock_guard<std::mutex> g(g_warm_mu);
   const char* lo = static_cast<const char*>(ws);
-  for (auto it = g_warm.begin(); it != g_warm.end();) {
-    const char* p = static_cast<const char*>(it->first);
-    if (p == lo || (p > lo && p < lo + bytes)) it = g_warm.erase(it);
-    else ++it;
+  auto inside = [&](const void* q) {
+    const char* p = static_cast<const char*>(q);
+    return p == lo || (p > lo && p < lo + bytes);
+  };
+  {
+    std::lock_guard<std::mutex> g(g_warm_mu);
+    for (auto it = g_warm.begin(); it != g_warm.end();) {
+      if (inside(it->first)) it = g_warm.erase(it);
+      else ++it;
+    }
+  }
+  std::lock_guard<std::mutex> g(g_hs_mu);
+  for (auto it = g_hs.begin(); it != g_hs.end();) {
+    if (inside(it->first)) {
+      if (it->second.host) (void)hipHostFree(it->second.host);  // (callers synchronise before a reset)
+      it = g_hs.erase(it);
+    } else {
+      ++it;
+    }
   }
 }
 
@@ -2154,6 +2204,16 @@ CHOCO_API int choco_topk_workspace_reset(const void* ws, size_t ws_bytes) {
   seg_forget(ws, ws_bytes);
   randk_forget(ws, ws_bytes);
   return CHOCO_OK;
+}
+
+CHOCO_API int choco_topk_host_status(const void* ws, int32_t clear, void* stream) {
+  const uint32_t v = host_status_read(ws, clear != 0);
+  if (clear != 0 && v != 0u && ws != nullptr) {
+    // the device word too (sticky, at CHOCO_TOPK_STATUS_OFFSET), behind the stream's work
+    if (hipMemsetAsync(const_cast<void*>(ws), 0, sizeof(uint32_t), as_stream(stream)) != hipSuccess)
+      return fail(CHOCO_ERR_HIP, "hipMemsetAsync failed");
+  }
+  return (int32_t)v;
 }
 
 CHOCO_API int choco_topk_set_warm_start(int32_t enable) {

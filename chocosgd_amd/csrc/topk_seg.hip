@@ -966,7 +966,8 @@ static int segmented(const float* x, const float* xhat, const int64_t* plan_dev,
     const size_t fb = align_up(topk_ws_bytes(p[1]), 256);
     const int rc = topk_pipeline(kData, x + p[0], xhat ? xhat + p[0] : nullptr, p[1], p[2], 0, 1.0f,
                                  out_val + p[3], out_idx + p[3], p[0], base + fo, fb, st, gseg,
-                                 reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_STATUS_OFFSET));
+                                 StatusSink{reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_STATUS_OFFSET),
+                                            host_status_dev(ws)});
     if (rc) return rc;
     fo += fb;
   }

@@ -77,9 +77,17 @@ int choco_topk_set_warm_start(int32_t enable);
 /* Byte offset, in every top-k / random-k / segmented workspace, of a sticky uint32
  * status word.  Bit 0: a bounded wait inside the exact fallback gave up, so the
  * output of that call is invalid (never expected; the wait is bounded so that a
- * stuck producer cannot hang the GPU).  The caller reads it without blocking
- * (e.g. an async copy checked later), raises, and writes 0 back. */
+ * stuck producer cannot hang the GPU).  The device raises the same bits in a
+ * pinned host mirror of the word with a system-scope store, so
+ * choco_topk_host_status(ws, clear, stream) reads them with NO copy and NO
+ * synchronisation: a call issued after the failing call has run on the GPU sees
+ * them (the Python wrapper checks before every call and raises RuntimeError, the
+ * exception the reference's pipelines catch, parallel_choco_v.py:226-227).  It
+ * returns the bits (0: nothing raised); clear != 0 zeroes the mirror and queues a
+ * zero of the device word on `stream`.  The mirror is released with the workspace
+ * (choco_topk_workspace_reset). */
 #define CHOCO_TOPK_STATUS_OFFSET 0
+int choco_topk_host_status(const void* ws, int32_t clear, void* stream);
 /* Byte offset of a uint32 counter of calls (flat: the exact fallback; segmented: segments
  * whose warm window missed) in the same workspaces: diagnostics, never reset by the codec. */
 #define CHOCO_TOPK_FALLBACKS_OFFSET 4

@@ -416,17 +416,77 @@ def test_qsgd_uniform_stream_mapping():
     assert abs(u.mean() - 0.5) < 2e-3 and np.all(np.abs(h - 16384) < 5 * 128)
 
 
-def test_randk_indices_distinct_and_uniformish():
+def test_randk_indices_distinct_and_streams():
     n, k = 10000, 1000
-    counts = np.zeros(n)
     for seed in range(40):
         idx = O.randk_indices(n, k, seed)
         assert idx.size == k and np.unique(idx).size == k and np.all(np.diff(idx) > 0)
-        counts[idx] += 1
-    # each index selected ~ 40 * 0.1 = 4 times on average
-    assert 3.0 < counts.mean() < 5.0 and counts.max() < 20
+        assert idx[0] >= 0 and idx[-1] < n
     # (seed, offset) streams are distinct
     assert not np.array_equal(O.randk_indices(n, k, 7, 0), O.randk_indices(n, k, 7, 1))
+
+
+# Uniformity of the device sampler (randk.hip, restated in the oracle) against the law of
+# the reference's np.random.choice(n, k, replace=False) (sparsification.py:48): a uniform
+# k-subset.  Chi-square tests over fixed seeds (deterministic), rejected at p < 1e-4.
+_RK_P_MIN = 1e-4
+
+
+def _chi2_p(obs, exp, fpc=1.0):
+    from scipy import stats
+    obs, exp = np.asarray(obs, np.float64), np.asarray(exp, np.float64)
+    x = float(((obs - exp) ** 2 / exp).sum()) / fpc
+    return stats.chi2.sf(x, obs.size - 1)
+
+
+@pytest.mark.parametrize("N", [1 << 18, 1_000_000])
+def test_randk_position_residues_uniform(N):
+    """In-tile positions modulo 2^s, s = 1..8 (tiles are 2^18-aligned, so idx mod 2^s is the
+    in-tile position's residue): each residue class holds its share of the draws.  A uniform
+    k-subset's class counts are multivariate hypergeometric: chi-square with the finite
+    population correction (N - k) / (N - 1)."""
+    k, seeds = N // 64, 128
+    draws = [O.randk_indices(N, k, seed) for seed in range(seeds)]
+    for s in range(1, 9):
+        M = 1 << s
+        cnt = sum(np.bincount(i % M, minlength=M) for i in draws)
+        exp = np.array([len(range(r, N, M)) for r in range(M)]) * (k / N) * seeds
+        p = _chi2_p(cnt, exp, (N - k) / (N - 1))
+        assert p > _RK_P_MIN, (N, M, p)
+
+
+@pytest.mark.parametrize("N", [1 << 18, 1_000_000])
+def test_randk_gaps_geometric(N):
+    """Gaps between consecutive selected indices follow the geometric law of a uniform
+    k-subset for k << N: P(gap = g) = (1 - k/N)^(g-1) k/N (bins g = 1..128, tail pooled)."""
+    k, seeds = N // 64, 64
+    g = np.concatenate([np.diff(O.randk_indices(N, k, seed)) for seed in range(seeds)])
+    q = k / N
+    edges = np.array(list(range(1, 129)) + [1 << 40], dtype=np.float64)
+    obs = np.histogram(g, bins=edges)[0]
+    probs = (1 - q) ** (edges[:-1] - 1) - (1 - q) ** (edges[1:] - 1)
+    assert _chi2_p(obs, probs * g.size) > _RK_P_MIN
+
+
+@pytest.mark.parametrize("N", [1 << 18, 1_000_000])
+def test_randk_consecutive_draws_uncorrelated(N):
+    """Consecutive draws pi(j), pi(j + 1) of the sampler's bijections -- pi_N (the tile
+    counts) and the in-tile pi_L (the positions) -- are independent: correlation within
+    5 standard errors, and uniform joint cells on a 16 x 16 grid of the high bits and of
+    the low 4 bits (chi-square over 8 keys pooled)."""
+    k = N // 64
+    T = 1 << O.RK_TILE_BITS
+    grids_hi, grids_lo = np.zeros(256), np.zeros(256)
+    for seed in range(8):
+        K = O.rk_derive(O.randk_key(seed, 0), 0)
+        for L, key in ((N, K), (min(T, N), O.rk_derive(K, 8))):
+            y = O.rk_perm(np.arange(k), L, key)
+            a, b = y[:-1], y[1:]
+            assert abs(np.corrcoef(a, b)[0, 1]) < 5.0 / np.sqrt(a.size), (N, L, seed)
+            grids_hi += np.bincount((a * 16 // L) * 16 + b * 16 // L, minlength=256)
+            grids_lo += np.bincount((a % 16) * 16 + b % 16, minlength=256)
+    for grid in (grids_hi, grids_lo):
+        assert _chi2_p(grid, np.full(256, grid.sum() / 256)) > _RK_P_MIN
 
 
 @pytest.mark.parametrize("N", [1, 2, 3, 5, 17, 1000, 65537, 262144, 300001])

@@ -54,6 +54,8 @@ VARIANTS = {
     "k2t512": ["CHOCO_K2_TARGET=512"],
     "k2t768": ["CHOCO_K2_TARGET=768"],
     "k2t1024": ["CHOCO_K2_TARGET=1024"],
+    # every bounded wait of the exact fallback gives up at once: tools/status_probe.py
+    "poll1": ["CHOCO_POLL_BUDGET=1"],
 }
 
 
