@@ -136,6 +136,19 @@ def workspace_bytes():
         return sum(b.numel() for b in _ws_cache.values())
 
 
+def drop_workspace(dev, kind):
+    """Forget this stream's cached `kind` workspace (after a call sequence failed part-way:
+    e.g. the sign / QSGD accumulators of an interrupted chunked pack are no longer zero);
+    the next call allocates a fresh zero-filled one."""
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream, kind)
+    with _ws_lock:
+        buf = _ws_cache.pop(key, None)
+    if buf is not None:
+        torch.cuda.current_stream(dev).synchronize()
+        _status.pop(buf.data_ptr(), None)
+        lib().choco_topk_workspace_reset(_ptr(buf), buf.numel())
+
+
 def release_workspaces(dev=None):
     """Drop the cached scratch buffers (all devices, or `dev`) after synchronising the
     streams that used them; the next call on that stream allocates a fresh, zeroed one.

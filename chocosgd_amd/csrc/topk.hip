@@ -121,6 +121,25 @@ CHOCO_DEV void st_pol(T* p, T v) {
   }
 }
 
+// Hand-offs between workgroups of one launch use the fence-free form of
+// MI355X_MICROARCH.md "Valid forms" (row 1): every handed-off word is stored
+// write-through (relaxed agent-scope atomic store = sc1) and read with sc1 loads.
+CHOCO_DEV void st_sc1(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+CHOCO_DEV uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16-byte granules (the one-launch emission records): buffer_store/load_dwordx4 sc1,
+// observed untorn on gfx950 (the guide's R2 granule), so a record is its own flag.
+constexpr int kCpolSc1 = 16;  // gfx940+ cache-policy bit SC1 of a buffer instruction
+CHOCO_DEV void st_sc1_16(uint4* p, uint4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
+                                         buf_rsrc(p, 16u), 0, 0, kCpolSc1);
+}
+CHOCO_DEV uint4 ld_sc1_16(const uint4* p) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(buf_rsrc(p, 16u), 0, 0, kCpolSc1);
+  return __builtin_bit_cast(uint4, v);
+}
+
 enum TileMode { kTakeNone = 0, kTakeAll = 1, kTakePartial = 2 };
 
 // Candidate window of one call: keys >= s_lo are candidates, [s_lo, s_hi) is
@@ -145,7 +164,8 @@ struct TopkCtrl {
   uint32_t fallbacks;                            // calls that took the exact fallback (diagnostic counter)
   uint32_t cold_left;                            // warm-host calls still to sample their window in K2 (backoff)
   uint32_t backoff;                              // cold run length after the next warm miss
-  uint32_t pad0[12];
+  uint32_t arrive;                               // one-launch path: tiles done (the last resets it)
+  uint32_t pad0[11];
   uint32_t overflow[2];                          // bit 0: a side list overflowed; bit 1: take the exact fallback
   uint32_t pad1[14];
   TopkBounds bounds[2];
@@ -160,7 +180,7 @@ constexpr uint32_t kNoCandKey = 0x7F800000u;   // window that admits only inf / 
 struct TopkLayout {
   int64_t n;
   uint32_t tile, nb, side_cap;
-  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, off_wide, off_gcnt, off_tinfo, total;
+  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, off_wide, off_gcnt, off_tinfo, off_rec, total;
 };
 
 // Tile = ceil(n / kK2Target) rounded up to 32768 elements: one tile per CU, all
@@ -189,6 +209,7 @@ static TopkLayout topk_layout(int64_t n) {
   L.off_cidx = o;  o += align_up((size_t)L.nb * tile * 4, 256);   // ... and indices
   L.off_gcnt = o;  o += align_up((size_t)L.nb * 8, 256);              // ... its per-tile (#>T, #==T)
   L.off_tinfo = o; o += align_up((size_t)L.nb * 4, 256);              // per tile: candidates (compact) or ~0 (spilled)
+  L.off_rec = o;   o += align_up((size_t)L.nb * 16, 256);             // one-launch path: per-tile emission record
   L.total = o;
   return L;
 }
@@ -395,6 +416,7 @@ struct StreamSmem {
   uint32_t bc[8];
   uint32_t next_chunk;            // the tile's chunk counter (waves claim chunks)
   uint32_t spill;                 // some wave spilled pairs to global (tile end)
+  uint32_t m1024;                 // this call's window margin (0: a sampled window); one-launch path
 };
 
 // Unconditional float4 loads of kK2Unroll rows (no branch around a load: the
@@ -823,18 +845,42 @@ CHOCO_DEV Buckets prologue_sample(const float* __restrict__ x, const float* __re
   return bk;
 }
 
+// One-launch path (ONE): the stream kernel also selects and emits, no K34 (see
+// one_finish below).  Arguments of that tail, unused otherwise.
+struct WideCtrl;
+struct OneArgs {
+  uint4* rec;               // per tile: {output offset | kOneFallback, T, ties to take, epoch}
+  uint32_t epoch;           // this call's tag (never 0, unique per workspace within 2^32 calls)
+  float* out_val;
+  int32_t* out_idx;
+  int64_t idx_base;
+  float scale;
+  WideCtrl* wide;
+  uint32_t* gcnt;
+  uint32_t* status;
+  uint32_t* host_status;
+};
+template <int MODE, bool XH, bool GS>
+CHOCO_DEV void one_finish(const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k,
+                          uint32_t tile, uint32_t nb, uint32_t par, uint32_t side_cap, const Buckets& bk,
+                          TopkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ cum_tab,
+                          const uint32_t* __restrict__ side, const float* __restrict__ cval,
+                          const uint32_t* __restrict__ cidx, const OneArgs& oa, StreamSmem& sm, bool spilled,
+                          uint32_t nchunk);
+
 // Random-k (MODE kHash): keys are uniform on [0, 2^31) and (s_lo, s_hi) come from
 // the binomial tails (host), passed as hs_lo / hs_hi.
 // GS (kData, XH): the fused gossip step -- the stream reads x, memory and xh,
 // writes x_new back and selects on d = x_new - xh.
-template <int MODE, bool XH, bool GS = false>
+template <int MODE, bool XH, bool GS = false, bool ONE = false>
 __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
     uint32_t par, uint32_t side_cap, uint64_t seed, uint32_t hs_lo, uint64_t hs_hi, TopkCtrl* __restrict__ ctrl,
     uint32_t* __restrict__ cum_tab, uint32_t* __restrict__ cntw, uint32_t* __restrict__ side,
     float* __restrict__ cval, uint32_t* __restrict__ cidx, uint32_t* __restrict__ tinfo, Gossip gs,
-    SampleRanks ranks, uint32_t sample_if_cold) {
+    SampleRanks ranks, uint32_t sample_if_cold, OneArgs oa) {
   static_assert(!GS || (MODE == kData && XH), "the gossip step needs x_hat and data keys");
+  static_assert(!ONE || MODE == kData, "the one-launch path selects data keys");
   __shared__ StreamSmem sm;
   STAMP(1024 + blockIdx.x, 0);
   const int tid = threadIdx.x;
@@ -879,6 +925,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     const uint32_t cold_left = ctrl->cold_left;
     bool ok = W.valid != 0u && W.n == n && W.k == k && W.shift < 32u;
     bool degenerate = false;
+    uint32_t m1024 = 0;
     if (sample_if_cold && (!ok || cold_left != 0u)) {  // grid-uniform
       SampleView sv{sm.u.sh, sm.scratch, sm.bc};
       bool deg;
@@ -901,13 +948,21 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     } else {
       bk = ok ? make_buckets_from(W.s_lo, W.s_hi, W.shift, seed) : make_buckets_from(kNoCandKey, kNoCandKey, 0u, seed);
       degenerate = (ctrl->overflow[par] & 2u) != 0u;
+      m1024 = ok ? W.m1024 : 0u;
     }
+    if (ONE && tid == 0) sm.m1024 = m1024;
     // no window for this (n, k) (a workspace the host believed warm): the exact fallback
     if (!ok && b == 0 && tid == 0) atomicOr(&ctrl->overflow[par], 2u);
     // a degenerate sample (K1's flag, or this prologue's): K34 will take the exact
     // fallback, which needs nothing from this kernel (with the fused gossip step the
     // stream must still run)
-    if (!GS && (!ok || degenerate)) return;
+    if (!GS && (!ok || degenerate)) {
+      // one launch: every workgroup still arrives; the last one finds the overflow bit and
+      // the whole grid runs the exact fallback
+      if constexpr (ONE) one_finish<MODE, XH, GS>(x, xh, n, k, tile, nb, par, side_cap, bk, ctrl, cum_tab, side,
+                                                  cval, cidx, oa, sm, false, tile / (uint32_t)kChunk);
+      return;
+    }
   } else {
     bk = make_buckets(hs_lo, hs_hi, seed);
   }
@@ -1107,7 +1162,8 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     if (t == 0 && hsum > side_cap) atomicOr(&ctrl->overflow[par], 1u);
     if (t < kNBucket) {
       const uint32_t cum = t < kNMaybe ? sure + above + hv : sure;
-      cum_tab[b * kNBucket + jb] = cum;
+      if (ONE) st_sc1(&cum_tab[b * kNBucket + jb], cum);  // read by the last workgroup, same launch
+      else cum_tab[b * kNBucket + jb] = cum;
       atomicAdd(&ctrl->G[par][b & (kNRep - 1)][jb], cum);
       if (t < kNMaybe) sm.hist[jb] = above;  // counting-sort cursor of bucket jb (hist is dead now)
     }
@@ -1135,30 +1191,48 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
         if (key < bk.s_hi) {  // every candidate has key >= s_lo
           const uint32_t p = atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
           if (sort_lds) skeys[p] = key;
-          else if (p < side_cap) st_pol<CHOCO_K2_STORE>(&sd[p], key);
+          else if (p < side_cap) {
+            if (ONE) st_sc1(&sd[p], key);
+            else st_pol<CHOCO_K2_STORE>(&sd[p], key);
+          }
         }
       };
       // Store-only loop: no global load may follow the stores inside it (vmcnt
       // counts stores too, so a load's wait would wait for every store before it).
+      // (one launch: the pairs stay in LDS for this workgroup's own emission, unless the
+      // tile spilled -- then they join the spilled ones in the chunks' global slots)
+      const bool keep = ONE && !spilled;
       for (uint32_t j = h; j < lc; j += 32) {
         const uint2 pr = sm.u.pairs[ls + j];
-        st_pol<CHOCO_K2_STORE>(&ov[j], __uint_as_float(pr.x));
-        st_pol<CHOCO_K2_STORE>(&oi[j], pr.y);
+        if (!keep) {
+          st_pol<CHOCO_K2_STORE>(&ov[j], __uint_as_float(pr.x));
+          st_pol<CHOCO_K2_STORE>(&oi[j], pr.y);
+        }
         to_side(pr.x, pr.y);
       }
-      if (have && h == 0) cntw[(int64_t)b * nchunk + cc] = spilled ? cnt : (cc == 0 ? csum : 0u);
-      if (cc == 0 && lane == 0) tinfo[b] = spilled ? 0xFFFFFFFFu : csum;
+      if (!ONE) {
+        if (have && h == 0) cntw[(int64_t)b * nchunk + cc] = spilled ? cnt : (cc == 0 ? csum : 0u);
+        if (cc == 0 && lane == 0) tinfo[b] = spilled ? 0xFFFFFFFFu : csum;
+      }
       // rare (a wave's LDS region overflowed): this tile keeps per-chunk slot
       // ranges; the pairs spilled during the stream are only binned here
       for (uint32_t j = lc + h; j < cnt; j += 32) to_side(__float_as_uint(ov[j]), oi[j]);
     }
     if (sort_lds) {
       __syncthreads();
-      for (uint32_t i = (uint32_t)tid; i < hsum; i += kK2Threads) sd[i] = skeys[i];
+      for (uint32_t i = (uint32_t)tid; i < hsum; i += kK2Threads) {
+        if (ONE) st_sc1(&sd[i], skeys[i]);
+        else sd[i] = skeys[i];
+      }
     }
   }
   WSTAMP(32000 + b * 8 + 4 + (w >> 2), w & 3);
   STAMP(1024 + b, 3);
+  if constexpr (ONE) {
+    __syncthreads();  // the ring (sorted maybe keys) is read again below
+    one_finish<MODE, XH, GS>(x, xh, n, k, tile, nb, par, side_cap, bk, ctrl, cum_tab, side, cval, cidx, oa, sm,
+                             spilled, nchunk);
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -1326,10 +1400,6 @@ static_assert(kEmitRows * (kK4Threads / 64) == 128, "batch_ranks: wave 0 scans 2
 // behind which one lane adds to the counter; the consumer polls that counter.
 // No release fence: a buffer_wbl2 writes back the whole XCD L2 and cost
 // 10-30 us per tile in the middle of everyone else's stream (measured).
-CHOCO_DEV void st_sc1(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-CHOCO_DEV uint32_t ld_sc1(const uint32_t* p) {
-  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 
 // every wave's stores drained, the workgroup joined, one lane adds
@@ -1971,6 +2041,278 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
 }
 
 // ----------------------------------------------------------------------------
+// One-launch finish (warm calls, k small enough for every tile's pairs to stay in
+// LDS): the stream kernel's tail instead of K34 and its kernel boundary.
+//
+//   * every tile published its bucket suffix row (cum_tab) and its sorted maybe keys
+//     (side list) with write-through (sc1) stores and added its row into G, then
+//     draws an arrival ticket (one device-scope add per workgroup, after every wave's
+//     stores drained);
+//   * the LAST workgroup to arrive selects: G -> bucket j*, every tile's bucket-j*
+//     keys -> LDS -> radix select of T and the tie quota r, then every tile's
+//     (#key > T, #key == T) -> its output offset and the ties it takes; one 16-byte
+//     record per tile {offset, T, ties, epoch} (a write-through granule: the record
+//     is its own flag);
+//   * every other workgroup polls its record and then emits its tile's candidates
+//     in ascending index order straight from the LDS pairs the stream left there --
+//     the candidates never go to HBM and nothing is read twice.
+// All workgroups are resident when the last one arrives (each one's tile has been
+// streamed by then), so the waits cannot deadlock; they are still bounded (a wait
+// that gives up raises the status word).  A failed select (window missed, bucket
+// too large, side list overflow, degenerate sample) publishes kOneFallback: the
+// whole grid then runs the ticketed exact fallback (wide_fallback) as K34 would.
+// ----------------------------------------------------------------------------
+constexpr uint32_t kOneFallback = 0xFFFFFFFFu;
+constexpr uint32_t kOneTimeout = 0xFFFFFFFEu;
+constexpr int kOneMCap = 8192;   // bucket-j* keys selected in LDS (the dead entry ring: 32 KB)
+constexpr int kOneHist = 1024;   // radix digit of <= 10 bits per round
+#ifndef CHOCO_ONE_POLL_BUDGET  // diagnostic builds only
+#define CHOCO_ONE_POLL_BUDGET (1u << 22)
+#endif
+
+// Emission of this workgroup's tile from {out, T, take}: candidates in chunk order
+// (= ascending index), from LDS (cmeta runs) or -- a tile that spilled -- from the
+// chunks' global slots; key > T, or key == T among the tile's first `take` ties.
+template <int MODE, bool XH>
+CHOCO_DEV void one_emit(uint32_t out, uint32_t T, uint32_t take, int64_t tb, uint32_t nchunk, bool spilled,
+                        const float* __restrict__ cval, const uint32_t* __restrict__ cidx, const OneArgs& oa,
+                        StreamSmem& sm) {
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  uint32_t* cg = reinterpret_cast<uint32_t*>(&sm.ent_v[0][0]);  // per chunk: #gt, then output base
+  uint32_t* ce = cg + kMaxTileChunks;                             // per chunk: #eq, then ties before it
+  auto fetch = [&](uint32_t c, uint32_t j, uint32_t& vb, uint32_t& ix) {
+    if (!spilled) {
+      const uint2 pr = sm.u.pairs[(sm.cmeta[c] & 0xFFFFu) + j];
+      vb = pr.x;
+      ix = pr.y;
+    } else {
+      const int64_t o = tb + (int64_t)c * kChunk + j;
+      vb = ld_sc1(reinterpret_cast<const uint32_t*>(cval) + o);
+      ix = ld_sc1(cidx + o);
+    }
+  };
+  // 1. per chunk (a wave per chunk): candidates above T and at T
+  for (uint32_t c = (uint32_t)w; c < nchunk; c += kK2Waves) {
+    const uint32_t cnt = sm.ccnt[c + 1] - sm.ccnt[c];
+    uint32_t gt = 0, eq = 0;
+    for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
+      const uint32_t j = j0 + (uint32_t)lane;
+      uint32_t vb = 0, ix = 0;
+      if (j < cnt) fetch(c, j, vb, ix);
+      const uint32_t key = vb & 0x7fffffffu;
+      gt += (uint32_t)__popcll(ballot(j < cnt && key > T));
+      eq += (uint32_t)__popcll(ballot(j < cnt && key == T));
+    }
+    if (lane == 0) { cg[c] = gt; ce[c] = eq; }
+  }
+  __syncthreads();
+  // 2. chunk prefixes: ties before each chunk, then the selected count before it
+  {
+    const uint32_t c = (uint32_t)tid;  // nchunk <= kK2Threads on this path: a chunk per thread
+    const uint32_t gv = c < nchunk ? cg[c] : 0u, ev = c < nchunk ? ce[c] : 0u;
+    uint32_t gp, ep, gtot, etot;
+    block_excl_scan2(c < nchunk ? gv : 0u, c < nchunk ? ev : 0u, sm.scratch, &gp, &ep, &gtot, &etot);
+    const uint32_t tk = c < nchunk ? min(ev, take > ep ? take - ep : 0u) : 0u;
+    uint32_t sp, stot;
+    sp = block_excl_scan(c < nchunk ? gv + tk : 0u, sm.scratch, &stot);
+    if (c < nchunk) {
+      cg[c] = sp;
+      ce[c] = ep;
+    }
+  }
+  __syncthreads();
+  // 3. emission (a wave per chunk, ranks by ballot; stores contiguous per wave)
+  for (uint32_t c = (uint32_t)w; c < nchunk; c += kK2Waves) {
+    const uint32_t cnt = sm.ccnt[c + 1] - sm.ccnt[c];
+    uint32_t base = out + cg[c], eqb = ce[c];
+    for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
+      const uint32_t j = j0 + (uint32_t)lane;
+      uint32_t vb = 0, ix = 0;
+      if (j < cnt) fetch(c, j, vb, ix);
+      const uint32_t key = vb & 0x7fffffffu;
+      const bool iseq = j < cnt && key == T;
+      const uint64_t em = ballot(iseq);
+      const bool sel = (j < cnt && key > T) || (iseq && eqb + mask_prefix(em) < take);
+      const uint64_t sm_ = ballot(sel);
+      if (sel) {
+        const uint32_t pos = base + mask_prefix(sm_);
+        oa.out_val[pos] = __uint_as_float(vb) * oa.scale;
+        oa.out_idx[pos] = (int32_t)((int64_t)ix + oa.idx_base);
+      }
+      base += (uint32_t)__popcll(sm_);
+      eqb += (uint32_t)__popcll(em);
+    }
+  }
+}
+
+template <int MODE, bool XH, bool GS>
+CHOCO_DEV void one_finish(const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k,
+                          uint32_t tile, uint32_t nb, uint32_t par, uint32_t side_cap, const Buckets& bk,
+                          TopkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ cum_tab,
+                          const uint32_t* __restrict__ side, const float* __restrict__ cval,
+                          const uint32_t* __restrict__ cidx, const OneArgs& oa, StreamSmem& sm, bool spilled,
+                          uint32_t nchunk) {
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const uint32_t b = blockIdx.x;
+  const uint32_t ku = (uint32_t)k;
+  // ---- arrival: every wave's write-through stores and G adds have completed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  STAMP(24576 + b, 0);
+  if (tid == 0) sm.bc[0] = __hip_atomic_fetch_add(&ctrl->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  uint32_t* R = sm.bc + 4;  // this tile's record {out, T, take} (bc[4..6])
+  if (sm.bc[0] == nb - 1) {
+    // ================= the last workgroup: select T, publish every tile's record
+    STAMP(24576 + b, 1);
+    uint32_t* Gs = sm.hist;  // the bucket totals (the counting-sort cursors are dead)
+    uint32_t* keys = reinterpret_cast<uint32_t*>(&sm.ent_v[0][0]);
+    uint32_t* hist = sm.ent_i[0];  // kOneHist words
+    if (tid < kNBucket) {
+      uint32_t g = 0;
+#pragma unroll
+      for (int r = 0; r < kNRep; ++r) g += ld_sc1(&ctrl->G[par][r][tid]);
+      Gs[tid] = g;
+    }
+    if (tid == 0) {
+      sm.bc[1] = ld_sc1(&ctrl->overflow[par]);
+      sm.bc[2] = 0u;  // j*
+      st_sc1(&ctrl->arrive, 0u);  // every tile has arrived: ready for the next call
+    }
+    __syncthreads();
+    bool fb = sm.bc[1] != 0u || Gs[0] < ku || Gs[kNMaybe] >= ku;
+    if (!fb && tid < kNMaybe && Gs[tid] >= ku && Gs[tid + 1] < ku) sm.bc[2] = (uint32_t)tid;
+    __syncthreads();
+    const uint32_t jstar = sm.bc[2];
+    const uint32_t M = fb ? 0u : Gs[jstar] - Gs[jstar + 1];
+    if (M > (uint32_t)kOneMCap) fb = true;  // workgroup-uniform
+    STAMP(26000 + b, 0);
+    uint32_t T = 0, r = 0;
+    if (!fb) {
+      // thread t <-> tile t: its bucket-j* keys (side list, buckets stored high to low)
+      const bool mine = (uint32_t)tid < nb;
+      const uint32_t* row = cum_tab + (int64_t)(mine ? tid : 0) * kNBucket;
+      const uint32_t a = ld_sc1(row + jstar), c = ld_sc1(row + jstar + 1), su = ld_sc1(row + kNMaybe);
+      const uint32_t cb = mine ? a - c : 0u, off = c - su, above = mine ? c : 0u;
+      uint32_t Mk;  // == M (the tables and the totals describe the same keys)
+      const uint32_t kpos = block_excl_scan(cb, sm.scratch, &Mk);
+      Mk = min(Mk, (uint32_t)kOneMCap);
+      {
+        const uint32_t* src = side + (int64_t)(mine ? tid : 0) * side_cap + off;
+        for (uint32_t j0 = 0; j0 < cb; j0 += 8) {
+          uint32_t kv[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) kv[q] = j0 + q < cb ? ld_sc1(src + j0 + q) : 0u;
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (j0 + q < cb && kpos + j0 + q < (uint32_t)kOneMCap) keys[kpos + j0 + q] = kv[q];
+        }
+      }
+      STAMP(26000 + b, 1);
+      // radix select inside bucket j*: rel = key - base_j in [0, 2^shift), <= 10 bits a round
+      const uint32_t base_j = bk.s_lo + (jstar << bk.shift);
+      uint32_t prefix = 0, krem = ku - Gs[jstar + 1];  // 1 <= krem <= M
+      int sh = (int)bk.shift;
+      __syncthreads();  // the keys are in LDS
+      while (sh > 0) {
+        const int dsh = sh > 10 ? sh - 10 : 0;
+        const uint32_t dmask = (1u << (sh - dsh)) - 1u;
+        for (int i = tid; i <= (int)dmask; i += kK2Threads) hist[i] = 0u;
+        __syncthreads();
+        for (uint32_t j = tid; j < Mk; j += kK2Threads) {
+          const uint32_t rel = keys[j] - base_j;
+          if (sh >= 32 || (rel >> sh) == (prefix >> sh)) atomicAdd(&hist[(rel >> dsh) & dmask], 1u);
+        }
+        __syncthreads();
+        block_find_rank1k(hist, dmask + 1, krem, sm.scratch, sm.bc + 2);
+        prefix |= sm.bc[2] << dsh;
+        krem = sm.bc[3];
+        sh = dsh;
+      }
+      T = base_j + prefix;
+      r = krem;  // ties at T to take (>= 1)
+      STAMP(26000 + b, 2);
+      // per tile: #keys > T (every key above bucket j* is) and #keys == T
+      uint32_t gt = above, eq = 0;
+      for (uint32_t i = 0; i < cb; ++i) {
+        const uint32_t kk = keys[kpos + i];
+        gt += kk > T ? 1u : 0u;
+        eq += kk == T ? 1u : 0u;
+      }
+      uint32_t gpre, epre, gtot, etot;
+      block_excl_scan2(gt, eq, sm.scratch, &gpre, &epre, &gtot, &etot);
+      if (mine) {
+        const uint32_t taken = min(r, epre);  // ties taken by earlier tiles (lowest index first)
+        const uint32_t take = min(eq, r - taken);
+        const uint4 rec = make_uint4(gpre + taken, T, take, oa.epoch);
+        if ((uint32_t)tid == b) { R[0] = rec.x; R[1] = rec.y; R[2] = rec.z; }
+        else st_sc1_16(oa.rec + tid, rec);
+      }
+    } else {
+      if ((uint32_t)tid < nb) {
+        if ((uint32_t)tid == b) R[0] = kOneFallback;
+        else st_sc1_16(oa.rec + tid, make_uint4(kOneFallback, 0u, 0u, oa.epoch));
+      }
+      if (tid == 0) atomicAdd(&ctrl->fallbacks, 1u);
+    }
+    STAMP(26000 + b, 3);
+    // the next call's window and the cold backoff (as K34's workgroup 0 does)
+    if (!fb && w == 0) next_window(Gs, bk.s_lo, bk.s_hi, bk.shift, sm.m1024, T, n, k, &ctrl->bounds[par ^ 1u]);
+    if (tid == 0) {
+      const bool warm_call = sm.m1024 != 0u;
+      uint32_t bo = ctrl->backoff, cl = ctrl->cold_left;
+      if (warm_call && fb) {
+        bo = min(max(2u * bo, kColdMin), kColdMax);
+        cl = bo;
+      } else if (warm_call) {
+        bo = max(bo / 2u, kColdMin);
+      } else if (cl != 0u) {
+        --cl;
+      }
+      ctrl->backoff = bo;
+      ctrl->cold_left = cl;
+    }
+    __syncthreads();
+  } else {
+    // ================= every other workgroup: poll its record (wave 0)
+    if (w == 0) {
+      uint4 rec = make_uint4(0u, 0u, 0u, 0u);
+      bool ok = false;
+      for (uint32_t it = 0; it < (uint32_t)CHOCO_ONE_POLL_BUDGET; ++it) {
+        rec = ld_sc1_16(oa.rec + b);
+        if (__builtin_amdgcn_readfirstlane(rec.w) == oa.epoch) { ok = true; break; }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (!ok) {
+        rec.x = kOneTimeout;
+        if (lane == 0) {
+          atomicOr(oa.status, kStatusPollTimeout);
+          if (oa.host_status)
+            __hip_atomic_store(oa.host_status, kStatusPollTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      if (lane == 0) { R[0] = __builtin_amdgcn_readfirstlane(rec.x); R[1] = __builtin_amdgcn_readfirstlane(rec.y);
+                       R[2] = __builtin_amdgcn_readfirstlane(rec.z); }
+    }
+    __syncthreads();
+  }
+  STAMP(24576 + b, 1);
+  const uint32_t out = R[0], T = R[1], take = R[2];
+  __syncthreads();
+  if (out == kOneTimeout) return;  // (status raised: the output is invalid)
+  if (out == kOneFallback) {
+    // the exact select over the whole input, shared through the ticketed queue
+    ExactSmem& es = *reinterpret_cast<ExactSmem*>(&sm.ent_v[0][0]);
+    Src<MODE, XH> src{x, xh, 0};
+    wide_fallback(src, n, k, tile, nb, oa.scale, oa.wide, oa.gcnt, oa.out_val, oa.out_idx, oa.idx_base, es,
+                  sm.bc + 3, oa.status, oa.host_status, &ctrl->bounds[par ^ 1u]);
+    return;
+  }
+  one_emit<MODE, XH>(out, T, take, (int64_t)b * tile, nchunk, spilled, cval, cidx, oa, sm);
+  STAMP(24576 + b, 2);
+}
+
+// ----------------------------------------------------------------------------
 // host dispatch
 // ----------------------------------------------------------------------------
 size_t topk_ws_bytes(int64_t n) {
@@ -1992,6 +2334,21 @@ struct WarmEntry {
 static std::mutex g_warm_mu;
 static std::unordered_map<const void*, WarmEntry> g_warm;
 static std::atomic<bool> g_warm_on{true};
+// one-launch records are tagged with a library-wide call counter: a stale record (an
+// earlier call, any workspace at that address) never carries the current tag
+static std::atomic<uint32_t> g_epoch{0};
+static uint32_t next_epoch() {
+  uint32_t e = g_epoch.fetch_add(1, std::memory_order_relaxed) + 1u;
+  if (e == 0u) e = g_epoch.fetch_add(1, std::memory_order_relaxed) + 1u;  // 0 = a zero-filled record
+  return e;
+}
+// A/B knob (tools/build_variants.py): 0 keeps K2 + K34 on every call
+#ifndef CHOCO_ONE
+#define CHOCO_ONE 1
+#endif
+// The one-launch path keeps every tile's candidates in LDS (640 pairs per wave): taken when a
+// tile's share of k is at most 4096 (a sampled window holds ~1.7x k: ~440 per wave).
+constexpr int64_t kOneMaxTileK = 4096;
 
 struct WarmClaim {
   uint32_t par;
@@ -2077,11 +2434,28 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
     profile_end("topk_bounds", st);
     CHOCO_LAUNCHED("topk_bounds_kernel");
   }
+  const bool one = CHOCO_ONE && MODE == kData && wc.warm && L.nb > 1 && L.tile / kChunk <= (uint32_t)kK2Threads &&
+                   (double)k * (double)L.tile / (double)n <= (double)kOneMaxTileK;
+  if constexpr (MODE == kData) {
+    if (one) {
+      // the stream kernel selects and emits itself (one_finish): no K34, no boundary
+      const OneArgs oa{reinterpret_cast<uint4*>(base + L.off_rec), next_epoch(), out_val, out_idx, idx_base, scale,
+                       reinterpret_cast<WideCtrl*>(base + L.off_wide), reinterpret_cast<uint32_t*>(base + L.off_gcnt),
+                       status.dev, status.host};
+      profile_begin("topk_stream", st);
+      CHOCO_KLAUNCH((topk_stream_kernel<kData, XH, GS, true>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, k,
+                    L.tile, L.nb, par, L.side_cap, seed, hs_lo, hs_hi, ctrl, cum, cntw, side, cval, cidx,
+                    reinterpret_cast<uint32_t*>(base + L.off_tinfo), gs, sample_ranks(n, k), 1u, oa);
+      profile_end("topk_stream", st);
+      CHOCO_LAUNCHED("topk_stream_kernel");
+      return CHOCO_OK;
+    }
+  }
   profile_begin("topk_stream", st);
   CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH, GS>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, k, L.tile, L.nb,
                 par, L.side_cap, seed, hs_lo, hs_hi, ctrl, cum, cntw, side, cval, cidx,
                 reinterpret_cast<uint32_t*>(base + L.off_tinfo), gs, sample_ranks(n, k),
-                (uint32_t)(MODE == kData && wc.warm ? 1 : 0));
+                (uint32_t)(MODE == kData && wc.warm ? 1 : 0), OneArgs{});
   profile_end("topk_stream", st);
   CHOCO_LAUNCHED("topk_stream_kernel");
   profile_begin("topk_finish", st);
@@ -2265,7 +2639,7 @@ CHOCO_API int choco_dbg_stream_only(const float* x, int64_t n, int64_t k, void* 
                        reinterpret_cast<uint32_t*>(base + L.off_cntw), reinterpret_cast<uint32_t*>(base + L.off_side),
                        reinterpret_cast<float*>(base + L.off_cval), reinterpret_cast<uint32_t*>(base + L.off_cidx),
                        reinterpret_cast<uint32_t*>(base + L.off_tinfo), Gossip{nullptr, 0.f}, SampleRanks{0u, 0u, 0u},
-                       0u);
+                       0u, OneArgs{});
   CHOCO_HIP(hipEventRecord(b, st));
   CHOCO_HIP(hipEventSynchronize(b));
   float ms = 0.f;

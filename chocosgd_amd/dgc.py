@@ -20,9 +20,16 @@ strict_reference=True)` keeps the reference's three steps as methods:
   * `sync(values, indices)` -> (synced_message, message_size);
   * `recover_info(flatten_params, synced_message, message_size, lr)` -> params - lr *
     (sum of messages) / n_nodes.
-The momentum-factor masking of dgc.py:175-179 is optimizer state: `last_indices`
-holds the selected global indices for it.
+The momentum-factor masking of dgc.py:175-179 (`mask_momentum`) is optimizer state and
+is NOT applied here, in either mode: `last_indices` holds the selected global indices the
+optimizer needs for it.
+
+strict_reference=True multiplies the unselected memory by 255 every step, so the memory
+overflows to inf after ~16 steps and DGC top-k / random-k diverges -- as the reference
+does on the PyTorch it runs on; a one-time warning says so.
 """
+import warnings
+
 import torch
 
 from . import codec
@@ -30,6 +37,18 @@ from .communication import recover_device
 from .parallel_choco import _Layout
 from .sparsification import _draw_seed, get_n_bits
 from .tensor_buffer import flatten
+
+
+_warned = []
+
+
+def _warn_strict_once():
+    if not _warned:
+        _warned.append(True)
+        warnings.warn("DGCCodec(strict_reference=True) reproduces the reference's nmask = "
+                      "(~mask.byte()).float() = 255 / 254 (sparsification.py:33-38): the error-feedback "
+                      "memory grows 255x per step and overflows after ~16 steps; pass "
+                      "strict_reference=False for the intended 1 - mask", RuntimeWarning, stacklevel=3)
 
 
 class DGCCodec(object):
@@ -45,6 +64,8 @@ class DGCCodec(object):
         self.is_compress_op = "compress" in comm_op
         self.selected_shapes = None
         self.last_indices = None
+        if strict_reference and "compress" in comm_op:
+            _warn_strict_once()
 
     def compress(self, grads, memory_tb, compress_ratio):
         memory = memory_tb.buffer

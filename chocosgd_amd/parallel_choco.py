@@ -23,6 +23,8 @@ What changes underneath:
     (optim/utils.py:67-72) to `flatten_params` inside its own first pass
     (utils.fused_step drives it; include/choco_codec.h "fused gossip step").
 """
+import inspect
+
 import torch
 
 from . import codec
@@ -338,6 +340,50 @@ class CHOCOQuantizationCompressor(_CHOCOBase):
                               is_biased=self.is_biased, seg_off=lay.seg_off, nseg=lay.nseg)
 
 
+class _Reassembled(dict):
+    """{rank: [norms | words] message} of a chunked sign exchange over an aggregator without
+    `out=`: each neighbour's message is concatenated from its received ranges on first
+    access, i.e. after uncompress has waited for every request."""
+
+    def __init__(self, rank, message, head, parts):
+        super().__init__()
+        self._src = {r: (head[r], [p[r] for p in parts]) for r in head if r != rank}
+        self[rank] = message
+        for r in self._src:
+            dict.__setitem__(self, r, None)
+
+    def __getitem__(self, r):
+        v = dict.__getitem__(self, r)
+        if v is None:
+            h, ps = self._src[r]
+            v = torch.cat([h] + ps)
+            dict.__setitem__(self, r, v)
+        return v
+
+    def items(self):
+        return [(r, self[r]) for r in self.keys()]
+
+    def values(self):
+        return [self[r] for r in self.keys()]
+
+
+class _LazyMap(dict):
+    """{rank: fn(src[rank])}, evaluated on access."""
+
+    def __init__(self, src, fn):
+        super().__init__((r, None) for r in src.keys())
+        self._src, self._fn = src, fn
+
+    def __getitem__(self, r):
+        return self._fn(self._src[r])
+
+    def items(self):
+        return [(r, self[r]) for r in self.keys()]
+
+    def values(self):
+        return [self[r] for r in self.keys()]
+
+
 class CHOCOSignCompressor(_CHOCOBase):
     """sign + per-tensor L1 norm  (parallel_choco_v.py:436-558).
 
@@ -371,13 +417,44 @@ class CHOCOSignCompressor(_CHOCOBase):
         # nominal bits as in parallel_choco_v.py:492
         sync_buffer["n_bits"] = get_n_bits(norms) + get_n_bits(signs)
 
+    def _agg_takes_out(self):
+        """Whether the aggregator's _agg accepts `out=` (this package's DecentralizedAggregation
+        does; the reference's, communication.py:246, does not)."""
+        try:
+            ps = inspect.signature(self.aggregator_fn._agg).parameters
+        except (TypeError, ValueError):
+            return False
+        return "out" in ps or any(p.kind == p.VAR_KEYWORD for p in ps.values())
+
     def _pack_and_post(self, sync_buffer, x, xh, lay, g, message, signs, norms):
+        try:
+            return self._pack_and_post_ranges(sync_buffer, x, xh, lay, g, message, signs, norms)
+        except BaseException:
+            # the per-segment L1 sums of the ranges packed so far stay in the stream's
+            # accumulator workspace until the `finish` range clears them: drop it, so the next
+            # sign / QSGD call does not add stale sums into its norms
+            codec.drop_workspace(x.device, "acc")
+            raise
+
+    def _pack_and_post_ranges(self, sync_buffer, x, xh, lay, g, message, signs, norms):
         hw = _hdr_words(lay.nseg)
+        ranges = codec.sign_chunks(lay.n, self.exchange_chunks)
+        if not self._agg_takes_out():
+            # the reference's aggregator: every range travels as a message of its own (same
+            # posting order); uncompress re-assembles each neighbour's [norms | words]
+            parts, reqs = [], []
+            for i, (w0, w1) in enumerate(ranges):
+                codec.sign_compress_range(x, w0, w1, i == len(ranges) - 1, xhat=xh, seg_off=lay.seg_off,
+                                          nseg=lay.nseg, gossip=g, out=(signs, norms))
+                r, synced = self._send(sync_buffer, message[hw + w0:hw + w1])
+                reqs += r
+                parts.append(synced)
+            r, head = self._send(sync_buffer, message[:hw])
+            return reqs + r, _Reassembled(self.aggregator_fn.rank, message, head, parts)
         peers = [r for r in self.aggregator_fn.neighbor_ranks]
         host = self.comm_device == "cpu"
         recv = {r: torch.empty(message.shape, dtype=message.dtype, device="cpu" if host else message.device,
                                pin_memory=host) for r in peers}
-        ranges = codec.sign_chunks(lay.n, self.exchange_chunks)
         reqs = []
         for i, (w0, w1) in enumerate(ranges):
             codec.sign_compress_range(x, w0, w1, i == len(ranges) - 1, xhat=xh, seg_off=lay.seg_off,
@@ -402,8 +479,12 @@ class CHOCOSignCompressor(_CHOCOBase):
         # the reference's two received dicts (parallel_choco_v.py:521-522), as views of
         # the one message per rank: [fp32 norms (16-B padded) | int32 words]
         nseg = norms.numel()
-        sync_buffer["synced_flatten_norms"] = {r: m[:hw].view(torch.float32)[:nseg] for r, m in synced.items()}
-        sync_buffer["synced_signs"] = {r: m[hw:] for r, m in synced.items()}
+        if isinstance(synced, _Reassembled):  # assembled after uncompress's wait, not now
+            sync_buffer["synced_flatten_norms"] = _LazyMap(synced, lambda m: m[:hw].view(torch.float32)[:nseg])
+            sync_buffer["synced_signs"] = _LazyMap(synced, lambda m: m[hw:])
+        else:
+            sync_buffer["synced_flatten_norms"] = {r: m[:hw].view(torch.float32)[:nseg] for r, m in synced.items()}
+            sync_buffer["synced_signs"] = {r: m[hw:] for r, m in synced.items()}
 
     def uncompress(self, sync_buffer, neighbor_hat_params, neighbors_info):
         self.aggregator_fn.complete_wait(sync_buffer["sync_reqs_1"])

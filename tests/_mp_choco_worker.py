@@ -46,7 +46,14 @@ def _rank_main(rank, world, port, comm_op, outdir):
         from chocosgd_amd.tensor_buffer import TensorBuffer
         parallel_choco._draw_seed = lambda: 1000 + rank  # pinned per-worker seeds (random-k, QSGD)
         nb = neighborhood(rank, world)
-        agg = DecentralizedAggregation(rank, nb)
+        if comm_op.endswith("_refagg"):
+            class _RefAgg(DecentralizedAggregation):  # the reference's _agg signature (no out=)
+                def _agg(self, data, op, force_wait=True):
+                    return DecentralizedAggregation._agg(self, data, op, force_wait)
+            agg = _RefAgg(rank, nb)
+            comm_op = comm_op[:-len("_refagg")]
+        else:
+            agg = DecentralizedAggregation(rank, nb)
         chunks = CHUNKS if comm_op.endswith("_chunked") else 1
         comp = CHOCOCompressor(aggregator=agg, comm_op=comm_op.replace("_chunked", ""), comm_device="cpu",
                                compress_ratio=RATIO, quantize_level=4, is_biased=False, backend="gloo",
@@ -82,6 +89,75 @@ def _rank_main(rank, world, port, comm_op, outdir):
         dist.destroy_process_group()
 
 
+def grads_of(rank):
+    """Worker `rank`'s gradient, error-feedback memory and parameters (centralized consumers)."""
+    n = sum(LENS)
+    rng = np.random.default_rng(500 + rank)
+    g = rng.standard_normal(n).astype(np.float32)
+    mem = (rng.standard_normal(n) * 0.25).astype(np.float32)
+    params = rng.standard_normal(n).astype(np.float32)
+    return g, mem, params
+
+
+LR = 0.1
+
+
+def _rank_central(rank, world, port, comm_op, outdir):
+    """EF-signSGD / DGC through the centralized aggregator built as the reference builds it
+    (ef_sign_sgd.py:41-47, dgc.py:53-59: get_aggregators(cur_rank, world=ranks,
+    neighbors_info={r: 1 / n_nodes}, "centralized") -> communication.py:138-224), all-gathers
+    over gloo with comm_device="cpu"."""
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from chocosgd_amd.communication import get_aggregators
+        from chocosgd_amd.tensor_buffer import TensorBuffer
+        ranks = list(range(world))
+        agg = get_aggregators(cur_rank=rank, world=ranks, neighbors_info={r: 1.0 / world for r in ranks},
+                              aggregator_type="centralized")
+        g, mem, params = grads_of(rank)
+
+        def split(a):
+            t = torch.from_numpy(a).cuda()
+            out, p = [], 0
+            for m in LENS:
+                out.append(t[p:p + m].clone())
+                p += m
+            return out
+        out = {}
+        if comm_op == "efsign":
+            from chocosgd_amd.ef_sign import EFSignCompressor
+            comp = EFSignCompressor(rank=rank, world_size=world, aggregator=agg, comm_op="sign", comm_device="cpu",
+                                    use_ipc=False)
+            sb = comp.compress(TensorBuffer(split(g)))
+            out["local"] = sb["synced_grads_tb"].buffer.cpu().numpy()
+            comp.sync(sb)
+            out["out"] = comp.decompress(sb).buffer.cpu().numpy()
+            for r, m in enumerate(sb["synced_message"]):
+                out[f"msg{r}"] = m.cpu().numpy()
+        else:  # dgc_top_k: DGC's top-k with the reference's 255 / 254 memory mask (strict default)
+            from chocosgd_amd.dgc import DGCCodec
+            c = DGCCodec(world_aggregator=agg, comm_op="compress_top_k", comm_device="cpu", n_nodes=world)
+            memory = TensorBuffer(split(mem))
+            vals, idx, _ = c.compress(split(g), memory, RATIO)
+            synced, size = c.sync(vals, idx)
+            flat = torch.from_numpy(params).cuda()
+            out["params"] = c.recover_info(flat, synced, size, LR).cpu().numpy()
+            out["mem"] = memory.buffer.cpu().numpy()
+            for r, m in enumerate(synced):
+                out[f"msg{r}"] = m.cpu().numpy()
+        torch.cuda.synchronize()
+        np.savez(os.path.join(outdir, f"rank{rank}.npz"), **out)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
 def main():
     comm_op, world, outdir = sys.argv[1], int(sys.argv[2]), sys.argv[3]
     import multiprocessing as mp
@@ -90,7 +166,8 @@ def main():
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, comm_op, outdir)) for r in range(world)]
+    target = _rank_central if comm_op in ("efsign", "dgc_top_k") else _rank_main
+    procs = [ctx.Process(target=target, args=(r, world, port, comm_op, outdir)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -36,8 +36,12 @@ def _hdr(nseg):
 @pytest.mark.parametrize("comm_op,world", [("compress_top_k", 2), ("compress_top_k", 3), ("compress_random_k", 3),
                                            ("sign", 2), ("sign", 3), ("quantize_qsgd", 3),
                                            ("quantize_qsgd_chunked", 2), ("quantize_qsgd_chunked", 3),
-                                           ("sign_chunked", 2), ("sign_chunked", 3)])
+                                           ("sign_chunked", 2), ("sign_chunked", 3),
+                                           ("sign_chunked_refagg", 3)])
 def test_choco_round_across_processes(comm_op, world, tmp_path):
+    """(`*_refagg`: the aggregator has the reference's `_agg(data, op, force_wait)` signature,
+    without this package's `out=`: the chunked sign exchange posts each range as a message of
+    its own and re-assembles the neighbours' messages after the wait.)"""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_mp_choco_worker.py"), comm_op, str(world),
                         str(tmp_path)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
@@ -56,6 +60,64 @@ def test_parallel_choco_sync_process_ipc(comm_op, world, tmp_path):
                         str(tmp_path)], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
     _verify_round(comm_op, world, tmp_path)
+
+
+@pytest.mark.parametrize("comm_op,world", [("efsign", 2), ("efsign", 3), ("dgc_top_k", 3)])
+def test_centralized_aggregation_across_processes(comm_op, world, tmp_path):
+    """EF-signSGD and DGC through CentralizedAggregation across PROCESSES (all-gather over
+    gloo, comm_device="cpu"), the aggregator built exactly as the reference builds it
+    (ef_sign_sgd.py:41-47, dgc.py:53-59 -> communication.py:138-224); every rank's state is
+    checked against the oracle (EF-sign: ef_sign_sgd.py:167-219; DGC: dgc.py:153-252)."""
+    import torch
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_mp_choco_worker.py"), comm_op, str(world),
+                        str(tmp_path)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lens = W.LENS
+    nseg = len(lens)
+    got = [dict(np.load(tmp_path / f"rank{q}.npz")) for q in range(world)]
+    ins = [W.grads_of(q) for q in range(world)]
+    if comm_op == "efsign":
+        hw = _hdr(nseg)
+        for q in range(world):
+            g = ins[q][0]
+            norms = O.l1_norms(g, lens)
+            for rk in range(world):  # every rank received every rank's [norms | words], in rank order
+                m = got[rk][f"msg{q}"]
+                assert np.array_equal(m[hw:], O.sign_pack(g)), (rk, q)
+                assert np.allclose(m[:hw].view(np.float32)[:nseg], norms, rtol=1e-6, atol=0)
+        for me in range(world):
+            nm_me = got[me][f"msg{me}"][:hw].view(np.float32)[:nseg]
+            local = O.sign_local(ins[me][0], nm_me, lens)
+            assert same_bits(got[me]["local"], local), me
+            want = local.copy()
+            for q in range(world):
+                if q != me:
+                    m = got[me][f"msg{q}"]
+                    O.sign_axpy(want, m[hw:], m[:hw].view(np.float32)[:nseg], lens, 1.0, two_roundings=False)
+            assert same_bits(got[me]["out"], (want / np.float32(world)).astype(np.float32)), me
+        return
+    # DGC top-k: every rank's message = top-k of grad + memory; memory <- x * nmask (255 / 254)
+    msgs = []
+    for q in range(world):
+        g, mem, _ = ins[q]
+        x = (g + mem).astype(np.float32)
+        ov, oi, _ = O.topk_segmented(x, lens, W.RATIO)
+        K = ov.size
+        for rk in range(world):
+            m = got[rk][f"msg{q}"]
+            assert same_bits(m[:K].view(np.float32), ov) and np.array_equal(m[K:].astype(np.int64), oi), (rk, q)
+        want_mem = (x * np.float32(255.0)).astype(np.float32)
+        want_mem[oi] = (ov * np.float32(254.0)).astype(np.float32)
+        assert same_bits(got[q]["mem"], want_mem), q
+        msgs.append((ov, oi))
+    dev = torch.device("cuda", 0)
+    for me in range(world):
+        acc = np.zeros(sum(lens), dtype=np.float32)
+        for ov, oi in msgs:  # empty_grads[q_indices] += q_values, messages in rank order
+            acc[oi] = (acc[oi] + ov).astype(np.float32)
+        upd = torch.from_numpy(acc).to(dev) / torch.full((), float(world), dtype=torch.float32, device=dev)
+        want = torch.from_numpy(ins[me][2]).to(dev).add(upd, alpha=-W.LR).cpu().numpy()
+        assert same_bits(got[me]["params"], want), me
 
 
 def _verify_round(comm_op, world, tmp_path):

@@ -208,6 +208,48 @@ def test_sign_compress_ranges(layout, chunks, fused):
                                   out=(packed, norms))
 
 
+def test_sign_chunked_pack_interrupted_leaves_norms_clean():
+    """A chunked sign pack interrupted after its first range (the exchange raises) must not
+    leave per-segment L1 sums in the stream's accumulator: the next message's norms are the
+    oracle's (CHOCOSignCompressor drops the workspace on failure)."""
+    from chocosgd_amd import codec
+    from chocosgd_amd.parallel_choco import CHOCOCompressor
+    from chocosgd_amd.tensor_buffer import TensorBuffer
+    lens = [70_001, 5, 1_100_003, 300]
+    n, nseg, so = sum(lens), len(lens), seg_table(lens)
+
+    class _FailingAgg:
+        rank, neighbor_ranks = 0, [1]
+
+        def __init__(self):
+            self.calls = 0
+
+        def _agg(self, data, op, force_wait=True, out=None):
+            self.calls += 1
+            raise RuntimeError("exchange failed")
+
+    comp = CHOCOCompressor(aggregator=_FailingAgg(), comm_op="sign", comm_device="gpu", compress_ratio=0.0,
+                           quantize_level=32, is_biased=False, backend="nccl", use_ipc=False, exchange_chunks=4)
+    x, xh = randn(n, 51), randn(n, 52, 0.5)
+
+    def split(t):
+        out, p = [], 0
+        for m in lens:
+            out.append(t[p:p + m].clone())
+            p += m
+        return out
+    sb = {"original_shapes": [(torch.Size([m]), m) for m in lens],
+          "flatten_params": TensorBuffer(split(x)), "flatten_hat_params": TensorBuffer(split(xh))}
+    with pytest.raises(RuntimeError, match="exchange failed"):
+        comp.compress(sb)
+    assert comp.compressor_fn.aggregator_fn.calls == 1  # the first range was packed, then the send failed
+    x2, xh2 = randn(n, 53), randn(n, 54, 0.5)
+    packed, norms = codec.sign_compress(x2, xhat=xh2, seg_off=so, nseg=nseg)
+    d2 = host(x2) - host(xh2)
+    assert np.array_equal(host(packed), O.sign_pack(d2))
+    assert np.allclose(host(norms), O.l1_norms(d2, lens), rtol=1e-7, atol=0)
+
+
 def test_choco_sign_round_trip_golden():
     from chocosgd_amd import codec
     g = golden("choco_sign_mini")
