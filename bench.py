@@ -521,6 +521,8 @@ def main():
     elapsed = time.perf_counter() - t0
     codec.profile_enable(False)
     timed = stage_times(args.steps)
+    # calls that took the exact fallback so far (top-k: the flat workspace's counter)
+    fallbacks = codec.topk_fallback_count() if w.op == "topk" else None
 
     # untimed pass: every kernel, plus the exchange on its own events
     codec.profile_reset()
@@ -634,6 +636,7 @@ def main():
             "stage_bytes_note": bytes_note,
             "kernels_us": {k: round(v[1], 2) for k, v in untimed.items()},
             "exchange_us": round(exchange_us, 1),
+            "topk_fallbacks": fallbacks,
             "cold_start": cold_entry,
             "e2e": None,
             "cpu_baseline": None,

@@ -315,13 +315,34 @@ CHOCO_DEV int tile_seg(const int64_t* __restrict__ seg_off, int nseg, int64_t e0
 // pinned norm below |d|) takes the real division.  Checked against fp32 division on 3e9 (t, norm) pairs (random over
 // the guarded range + exhaustive t for 12 norm mantissas) and bit-exact against
 // the oracle in the GPU tests.
+#ifndef CHOCO_QCHECK  // 1: the quotient guard per 8-element group (A/B knob; 0: per element)
+#define CHOCO_QCHECK 1
+#endif
 struct QDiv {
   float norm, y;
   bool fast;
+  uint32_t tlo_m1;  // bits(T_lo) - 1, T_lo = 2^-60 norm (1 + 2^-20): t >= T_lo implies q0 >= 2^-60
   CHOCO_DEV void init(float nrm) {
     norm = nrm;
     y = 1.0f / nrm;
     fast = nrm >= 0x1p-30f && nrm <= 0x1p96f;
+    tlo_m1 = __float_as_uint(nrm * 0x1.00001p-60f) - 1u;
+  }
+  // Group form of quot()'s guard (CHOCO_QCHECK 1): instead of testing every element's q0
+  // against [2^-60, 2^7] (three compares and four scalar mask operations per element),
+  // the group keeps min(bits(t) - 1) and max(bits(q0)) in two VALU ops per element and
+  // tests them once.  Conservative: t != 0 with t < T_lo covers every q0 < 2^-60 (and
+  // some above it), bits(q0) > bits(2^7) covers q0 > 2^7, inf and NaN; a flagged group
+  // takes the IEEE division for all its elements, so the result is the same as quot()'s.
+  CHOCO_DEV float quot_nocheck(float t, uint32_t& tmin_m1, uint32_t& qmax) const {
+    const float q0 = t * y;
+    const float r = fmaf(-q0, norm, t);
+    tmin_m1 = min(tmin_m1, __float_as_uint(t) - 1u);
+    qmax = max(qmax, __float_as_uint(q0));
+    return fmaf(r, y, q0);
+  }
+  CHOCO_DEV bool group_slow(uint32_t tmin_m1, uint32_t qmax) const {
+    return !fast || tmin_m1 < tlo_m1 || qmax > 0x43000000u;
   }
   // returns t / norm; *slow set when this element needs the real division
   CHOCO_DEV float quot(float t, bool& slow) const {
@@ -486,6 +507,17 @@ __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
   for (int g = 0; g < kQG; ++g) {
     const int64_t e0 = eb + g * GS;
     float lf[kQPer];
+#if CHOCO_QCHECK
+    uint32_t tmin_m1 = 0xFFFFFFFFu, qmax = 0u;
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) lf[c] = D.quot_nocheck(sf * fabsf(d[g][c]), tmin_m1, qmax);  // s * x.abs() / norm
+    const bool gslow = D.group_slow(tmin_m1, qmax);
+    if (__builtin_expect(__ballot(gslow) != 0, 0)) {
+#pragma unroll
+      for (int c = 0; c < kQPer; ++c)
+        if (gslow) lf[c] = (sf * fabsf(d[g][c])) / P.norm;
+    }
+#else
     bool slow[kQPer];
     bool any = false;
 #pragma unroll
@@ -498,6 +530,7 @@ __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
       for (int c = 0; c < kQPer; ++c)
         if (slow[c]) lf[c] = (sf * fabsf(d[g][c])) / P.norm;
     }
+#endif
     uint32_t lv[kQPer];
     uint32_t sbits = 0;
     float lvlf[kQPer];

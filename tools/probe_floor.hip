@@ -477,6 +477,140 @@ __global__ __launch_bounds__(kThreads) void dynamic_emit(const float* __restrict
   if (tid == 0 && stamps) stamps[b * kStampW + 7] = home | (ns << 8);
 }
 
+// ------------------------------------------------------------------ strided static blocks
+// Workgroup b streams blocks b, b + nwg, b + 2 nwg, ... (32K elements each): every
+// workgroup's bytes are spread over the whole buffer (all address ranges), ordered by
+// per-block counts the last workgroup scans.  Tests whether the per-XCD spread of the
+// static tiles follows the address ranges (then this evens it out) or the XCD.
+struct StrSmem {
+  uint2 pairs[kWaves * kPairCap];
+  uint32_t cmeta[kMaxSlots * kBlkChunks];
+  uint32_t cpre[kMaxSlots * kBlkChunks];
+  uint32_t boff[kMaxSlots];
+  uint32_t scratch[40];
+  uint32_t bc[8];
+  uint32_t next;
+  uint32_t ovf;
+};
+__global__ __launch_bounds__(kThreads) void strided_emit(const float* __restrict__ x, long n, uint32_t nblk, float T,
+                                                         uint32_t* __restrict__ cnt_b, uint32_t* __restrict__ off_b,
+                                                         uint32_t* __restrict__ ctrl, uint32_t epoch,
+                                                         float* __restrict__ ov, uint32_t* __restrict__ oi,
+                                                         unsigned long long* stamps) {
+  __shared__ StrSmem sm;
+  stamp(stamps, 0);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t b = blockIdx.x, nwg = gridDim.x;
+  const uint32_t ns = (nblk - b + nwg - 1) / nwg;  // blocks of this workgroup
+  const uint32_t nch = ns * kBlkChunks;
+  const __amdgpu_buffer_rsrc_t r = rsrc(x, (uint32_t)(n * 4));
+  auto boff_of = [&](uint32_t c) -> uint32_t {
+    if (c >= nch) return 0xFFFFFFF0u;
+    const uint32_t blk = b + (c / kBlkChunks) * nwg;
+    return (blk * kBlk + (c % kBlkChunks) * kChunk) * 4u;
+  };
+  if (tid == 0) { sm.next = 2 * kWaves; sm.ovf = 0; }
+  uint32_t cA = w, cB = w + kWaves;
+  float4 A[kU], B[kU];
+  load8(r, boff_of(cA), lane, A);
+  load8(r, boff_of(cB), lane, B);
+  __syncthreads();
+  uint2* region = sm.pairs + w * kPairCap;
+  uint32_t fill = 0, ovf = 0;
+  auto chunk = [&](uint32_t c, const float4 (&R)[kU]) {
+    const uint32_t f0 = fill;
+    const uint32_t e0 = (b + (c / kBlkChunks) * nwg) * kBlk + (c % kBlkChunks) * kChunk;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) row_pairs(R[u], e0 + u * 256 + 4 * lane, T, region, fill, ovf);
+    if (lane == 0) sm.cmeta[c] = (w * kPairCap + f0) | ((fill - f0) << 16);
+  };
+  for (;;) {
+    if (cA >= nch) break;
+    uint32_t nA = 0;
+    if (lane == 0) nA = atomicAdd(&sm.next, 1u);
+    nA = __builtin_amdgcn_readfirstlane(nA);
+    chunk(cA, A);
+    load8(r, boff_of(nA), lane, A);
+    cA = nA;
+    if (cB >= nch) break;
+    uint32_t nB = 0;
+    if (lane == 0) nB = atomicAdd(&sm.next, 1u);
+    nB = __builtin_amdgcn_readfirstlane(nB);
+    chunk(cB, B);
+    load8(r, boff_of(nB), lane, B);
+    cB = nB;
+  }
+  if (ovf && lane == 0) atomicOr(&sm.ovf, 1u);
+  __syncthreads();
+  stamp(stamps, 1);
+  if ((uint32_t)tid < ns) {
+    uint32_t acc = 0;
+    for (int j = 0; j < kBlkChunks; ++j) {
+      const uint32_t c = tid * kBlkChunks + j;
+      sm.cpre[c] = acc;
+      acc += sm.cmeta[c] >> 16;
+    }
+    st_sc1(&cnt_b[b + tid * nwg], acc);
+  }
+  if (tid == 0 && sm.ovf) atomicOr(&ctrl[64], 1u);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) sm.bc[0] = __hip_atomic_fetch_add(&ctrl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  stamp(stamps, 2);
+  if (sm.bc[0] == nwg - 1) {
+    constexpr int kPer = 4;
+    uint32_t v[kPer], s = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const uint32_t i = tid * kPer + q;
+      v[q] = i < nblk ? ld_sc1(&cnt_b[i]) : 0u;
+      s += v[q];
+    }
+    uint32_t tot;
+    uint32_t o = block_excl(s, sm.scratch, &tot);
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const uint32_t i = tid * kPer + q;
+      if (i < nblk) st_sc1(&off_b[i], o);
+      o += v[q];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      st_sc1(&ctrl[0], 0u);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      st_sc1(&ctrl[32], epoch);
+    }
+  } else {
+    if (w == 0) {
+      for (uint32_t it = 0;; ++it) {
+        if (__builtin_amdgcn_readfirstlane(ld_sc1(&ctrl[32])) == epoch) break;
+        if (it == (1u << 22)) { if (lane == 0) atomicOr(&ctrl[64], 2u); break; }
+        __builtin_amdgcn_s_sleep(4);
+      }
+    }
+    __syncthreads();
+  }
+  if ((uint32_t)tid < ns) sm.boff[tid] = ld_sc1(&off_b[b + tid * nwg]);
+  __syncthreads();
+  stamp(stamps, 3);
+  const uint32_t h = lane & 31;
+  for (uint32_t c0 = 2u * w; c0 < nch; c0 += 2u * kWaves) {
+    const uint32_t c = c0 + (lane >> 5);
+    const uint32_t meta = c < nch ? sm.cmeta[c] : 0u;
+    const uint32_t st = meta & 0xFFFFu, cnt = meta >> 16;
+    const uint32_t base = c < nch ? sm.boff[c / kBlkChunks] + sm.cpre[c] : 0u;
+    for (uint32_t j = h; j < cnt; j += 32) {
+      const uint2 pr = sm.pairs[st + j];
+      ov[base + j] = __uint_as_float(pr.x);
+      oi[base + j] = pr.y;
+    }
+  }
+  stamp(stamps, 4);
+  if (tid == 0 && stamps) stamps[b * kStampW + 7] = xcc_id() | (ns << 8);
+}
+
 // ------------------------------------------------------------------ input + reference count
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
@@ -617,7 +751,10 @@ int main() {
   CK(hipMemcpy(hctrl, ctrl, sizeof(hctrl), hipMemcpyDeviceToHost));
   printf("dynamic overflow flag %u\n", hctrl[64]);
   const bool ok2 = verify("dynamic", bufs[0], n, T, (long)want[0], ov, oi);
-  if (!ok1 || !ok2) return 1;
+  strided_emit<<<nb, kThreads>>>(bufs[0], n, nblk, T, cnt, off, ctrl, epoch++, ov, oi, nullptr);
+  CK(hipDeviceSynchronize());
+  const bool ok3 = verify("strided", bufs[0], n, T, (long)want[0], ov, oi);
+  if (!ok1 || !ok2 || !ok3) return 1;
 
   for (int pass = 0; pass < 2; ++pass) {
     printf("-- pass %d\n", pass);
@@ -627,6 +764,9 @@ int main() {
     }, bytes);
     timed("dynamic: read + emit", [&](int i, int) {
       dynamic_emit<<<nwg, kThreads>>>(bufs[i], n, nblk, T, cnt, off, ctrl, epoch++, ov, oi, nullptr);
+    }, bytes);
+    timed("strided: read + emit", [&](int i, int) {
+      strided_emit<<<nb, kThreads>>>(bufs[i], n, nblk, T, cnt, off, ctrl, epoch++, ov, oi, nullptr);
     }, bytes);
   }
   for (int rep = 0; rep < 2; ++rep) {
@@ -641,6 +781,11 @@ int main() {
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(hst.data(), st, hst.size() * 8, hipMemcpyDeviceToHost));
     timeline("dynamic", hst.data(), nwg, true);
+    strided_emit<<<nb, kThreads>>>(bufs[1], n, nblk, T, cnt, off, ctrl, epoch++, ov, oi, nullptr);
+    strided_emit<<<nb, kThreads>>>(bufs[2], n, nblk, T, cnt, off, ctrl, epoch++, ov, oi, st);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(hst.data(), st, hst.size() * 8, hipMemcpyDeviceToHost));
+    timeline("strided", hst.data(), (int)nb, false);
   }
   return 0;
 }
