@@ -77,7 +77,7 @@ def main():
         k2 = k2[live]
         onef = t[24576:24576 + 1024][live]
         last = t[26000:26000 + 1024]
-        lw = np.nonzero(last[:, 0] > 0)[0]
+        lw = np.nonzero(last[:, 0] >= t[1024:1024 + 1024][live][:, 0].min())[0]  # this call's last workgroup
         t0 = k2[:, 0].min()
 
         def row(name, v):
@@ -92,13 +92,15 @@ def main():
               f"dispatch events (avg of {a.loop}): " + ", ".join(f"{nm} {v:.1f} us" for nm, v in ev.items() if v)
               + f"; in-kernel span (first start -> last stamp) {(last_end - t0) * TICK_US:.1f} us")
         te = t[22000:22000 + 1024][live]
+        rk = t[28000:28000 + 1024][live]
         wv = t[32000:32000 + 8 * 1024].reshape(1024, 8, 4)[live]
         last_wave = wv[:, :4, :].reshape(len(live), 16).max(1)
         row("start", k2[:, 0]); row("window known", k2[:, 1]); row("streamed (wave 0)", k2[:, 2])
         row("streamed (last wave)", last_wave)
         row("tile scans + G adds", te[:, 0]); row("pairs binned", te[:, 1]); row("tile end", k2[:, 3])
         row("arrived (before ticket)", onef[:, 0]); row("ticket returned", onef[:, 3])
-        row("record known", onef[:, 1]); row("emitted", onef[:, 2])
+        row("record known", onef[:, 1]); row("emit: pmap ready", rk[:, 0]); row("emit: ranks", rk[:, 1])
+        row("emitted", onef[:, 2])
         if lw.size:
             L = last[lw[0]]
             L2 = t[27000 + lw[0]]
