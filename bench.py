@@ -80,6 +80,9 @@ def parse():
                    help="gloo: messages staged through host memory (comm_device=cpu); lets ranks share a GPU")
     p.add_argument("--unfused", action="store_true",
                    help="step_* workloads: the consensus step as its own pass (the reference's order)")
+    p.add_argument("--fold", action="store_true",
+                   help="top-k: fold the self message's uncompress (x_hat, and memory when the self rank is first) "
+                        "into the compress emission (choco_topk_compress_accumulate)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the host-resident (PCIe-inclusive) leg")
     p.add_argument("--lib", default=None, help=argparse.SUPPRESS)
@@ -131,6 +134,10 @@ class Worker:
         self.peers = [r for r in self.ranks if r != rank]
         self.weights = [self.nb[r] for r in self.ranks]
         self.self_slot = self.ranks.index(rank)
+        # self-message fold (top-k): x_hat always; memory only when the self message is the
+        # first one applied to it (ascending rank order, parallel_choco_v.py:291-310)
+        self.fold = bool(args.fold) and self.op == "topk"
+        self.fold_mem = self.fold and self.self_slot == 0
         self.plan = None
         if self.op == "topk_seg":
             with open(os.path.join(ROOT, "tests", "golden", "layouts.json")) as f:
@@ -181,7 +188,8 @@ class Worker:
         if self.step_mode:
             self.compress_step()
         elif self.op == "topk":
-            c.topk(self.d, self.k, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]))
+            c.topk(self.d, self.k, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]),
+                   fold=self._fold_args())
         elif self.op == "topk_seg":
             c.topk_segmented(self.d, self.plan, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]))
         elif self.op == "randk":
@@ -203,12 +211,17 @@ class Worker:
             g = None
         if self.op == "topk":
             c.topk(self.x, self.k, xhat=self.hat, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]),
-                   gossip=g)
+                   gossip=g, fold=self._fold_args())
         elif self.op == "qsgd":
             c.qsgd_compress(self.x, self.param, xhat=self.hat, seed=12345 + self.rank, offset=self.step_id,
                             gossip=g, out=self.wire)
         else:
             c.sign_compress(self.x, xhat=self.hat, gossip=g, out=self.wire)
+
+    def _fold_args(self):
+        if not self.fold:
+            return None
+        return (self.hat, self.mem if self.fold_mem else None, self.weights[self.self_slot])
 
     def exchange(self):
         self.exchange_finish(self.exchange_start())
@@ -251,8 +264,10 @@ class Worker:
         msgs = [self.msg if r == self.rank else self.recv[r] for r in self.ranks]
         if self.op in ("topk", "topk_seg", "randk"):
             for r, m, w in zip(self.ranks, msgs, self.weights):
+                if r == self.rank and self.fold_mem:
+                    continue  # applied by the compress (the fold)
                 c.sparse_accumulate(m[:self.k].view(torch.float32), m[self.k:], self.mem, w,
-                                    xhat_self=self.hat if r == self.rank and not hat_done else None)
+                                    xhat_self=self.hat if r == self.rank and not (hat_done or self.fold) else None)
         elif self.op == "qsgd":
             parts = [(m[16:], m[:4].view(torch.float32)) for m in msgs]
             c.qsgd_accumulate(parts, self.weights, self.self_slot, self.n, self.param, self.mem, xhat_self=self.hat)
@@ -263,7 +278,7 @@ class Worker:
     def step(self):
         self.compress()
         works = self.exchange_start()
-        overlap = works is not None and self.op in ("topk", "topk_seg", "randk")
+        overlap = works is not None and self.op in ("topk", "topk_seg", "randk") and not self.fold
         if overlap:
             self.hat_self_update()
         self.exchange_finish(works)
@@ -284,6 +299,12 @@ class Worker:
         if self.op in ("topk", "topk_seg"):
             comp = 4 * n + 8 * self.k                    # read d once, write k (fp32 value, int32 index)
             dec = 8 * self.k * nm + 8 * self.k * (nm + 1)  # read each message; RMW mem per msg + x_hat (self)
+            if self.fold:
+                s = 1 if self.fold_mem else 0
+                comp += 8 * self.k * (1 + s)            # the self message's RMW of x_hat (+ memory) in the emission
+                dec = 8 * self.k * (nm - s) * 2           # the other messages: read + memory RMW
+                return comp, dec, ("compress 4n + 8k + 8k RMW of x_hat (+ 8k of memory when the self rank is "
+                                   "first: the fold); decompress 8k read + 8k memory RMW per other message")
             return comp, dec, "compress 4n + 8k; decompress 8k read per message + 8k RMW per touched buffer"
         if self.op == "randk":
             comp = 4 * self.k + 8 * self.k                # gather k values + write k pairs (the sampler reads none)
@@ -627,7 +648,7 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": w.label, "n_per_worker": w.n, "k_per_worker": w.k,
+            "config": {"workload": w.label + ("_fold" if w.fold else ""), "n_per_worker": w.n, "k_per_worker": w.k,
                        "graph": "self" if world == 1 else ("complete" if world == 2 else "ring"),
                        "messages_per_step": len(w.ranks), "backend": args.backend if world > 1 else None,
                        "step": "compress+exchange+decompress-accumulate", "parallelism": f"gossip{world}"},

@@ -34,6 +34,8 @@ SIGNATURES = {
     "choco_topk_set_warm_start": (_c_i32, [_c_i32]),
     "choco_topk_host_status": (_c_i32, [_vp, _c_i32, _vp]),
     "choco_topk_compress": (_c_i32, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+    "choco_topk_compress_accumulate": (_c_i32, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_f32, _vp, _c_sz,
+                                                _vp]),
     "choco_topk_segmented_plan_len": (_c_i64, [_p_i64, _c_i32]),
     "choco_topk_segmented_plan": (_c_i64, [_p_i64, _c_i32, _c_f64, _p_i64]),
     "choco_topk_segmented_workspace_size": (_c_sz, [_p_i64, _c_i32]),
@@ -73,6 +75,8 @@ SIGNATURES = {
                                                         _c_i32, _c_i32, _c_i64, _c_i64, _vp, _vp, _vp]),
     "choco_gossip_step": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _vp]),
     "choco_gossip_topk_compress": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
+    "choco_gossip_topk_compress_accumulate": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _c_i64, _vp, _vp, _c_i32,
+                                                       _c_f32, _vp, _c_sz, _vp]),
     "choco_gossip_topk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _c_f32, _vp, _p_i64, _c_i32, _vp, _vp, _vp,
                                                       _c_sz, _vp]),
     "choco_gossip_randk_compress_segmented": (_c_i32, [_vp, _vp, _vp, _c_f32, _vp, _p_i64, _c_i32, _c_u64, _c_u64,

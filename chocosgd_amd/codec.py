@@ -188,12 +188,17 @@ def topk_k(n, ratio):
     return int(lib().choco_topk_k(int(n), float(ratio)))
 
 
-def topk(x, k, xhat=None, out=None, gossip=None):
+def topk(x, k, xhat=None, out=None, gossip=None, fold=None):
     """Exact top-k by |x - xhat| (signed values, int32 indices, ascending index).
 
     `out=(values f32[k], indices i32[k])` writes into caller buffers (e.g. two views
     of one wire message) instead of allocating; `gossip=(memory, gamma)` fuses the
-    consensus step (x is updated in place first)."""
+    consensus step (x is updated in place first).  `fold=(hat_self, memory, weight)`
+    (either may be None) applies the self message's uncompress while the message is
+    emitted: hat_self[idx] += v, memory[idx] += weight * v.  Folding memory is only
+    bit-identical to the reference when the self rank is the first message applied to
+    memory (include/choco_codec.h, choco_topk_compress_accumulate).  With `gossip`,
+    hat_self must be xhat and memory the gossip memory (or None)."""
     _require(x, torch.float32, "x")
     if xhat is not None:
         _require(xhat, torch.float32, "xhat")
@@ -215,7 +220,28 @@ def topk(x, k, xhat=None, out=None, gossip=None):
     st = topk_status(ws)
     st.check()
     g = _gossip(gossip, x, xhat)
-    if g is not None:
+    if fold is not None:
+        fhat, fmem, fw = fold
+        for t, nm in ((fhat, "hat_self"), (fmem, "memory")):
+            if t is not None:
+                _require(t, torch.float32, nm)
+                if t.numel() != n:
+                    raise RuntimeError(f"{nm} and x must have the same number of elements")
+        if fhat is None and fmem is None:
+            raise RuntimeError("fold: hat_self and memory are both None")
+        if g is not None:
+            if fhat is None or fhat.data_ptr() != xhat.data_ptr():
+                raise RuntimeError("with gossip, the fold's hat_self must be xhat")
+            if fmem is not None and fmem.data_ptr() != g[0].data_ptr():
+                raise RuntimeError("with gossip, the folded memory must be the gossip memory")
+            _lib.check(L.choco_gossip_topk_compress_accumulate(
+                _ptr(x), _ptr(g[0]), _ptr(xhat), g[1], n, int(k), _ptr(vals), _ptr(idx), int(fmem is not None),
+                float(fw), _ptr(ws), ws.numel(), _stream(dev)), "choco_gossip_topk_compress_accumulate")
+        else:
+            _lib.check(L.choco_topk_compress_accumulate(
+                _ptr(x), _ptr(xhat), n, int(k), _ptr(vals), _ptr(idx), _ptr(fhat), _ptr(fmem), float(fw),
+                _ptr(ws), ws.numel(), _stream(dev)), "choco_topk_compress_accumulate")
+    elif g is not None:
         _lib.check(L.choco_gossip_topk_compress(_ptr(x), _ptr(g[0]), _ptr(xhat), g[1], n, int(k), _ptr(vals),
                                                 _ptr(idx), _ptr(ws), ws.numel(), _stream(dev)),
                    "choco_gossip_topk_compress")

@@ -428,8 +428,91 @@ __device__ __noinline__ void qsgd_quant_tile_slow(const float* __restrict__ x, c
   }
 }
 
+// The math and stores of one full single-segment tile whose deltas d are in registers
+// (thread t: its four 8-element groups e = tile * 8192 + g * 2048 + 8 t + c).
 template <int CW>
-__global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
+CHOCO_DEV void quant_tile_math(const float (&d)[kQG][kQPer], int64_t tile, int64_t n, const QParam& P,
+                               const QDiv& D, float sf, const float* __restrict__ u_in, uint64_t seed,
+                               uint64_t offset, uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
+                               float* __restrict__ dense_out) {
+  constexpr int GS = kQThreads * kQPer;  // 2048
+  const int64_t eb = tile * kQStreamTile + (int64_t)threadIdx.x * kQPer;
+  // the thread's uniform stream, drawn group by group in stream order (8 uniforms live at
+  // a time, not 32: the registers go to resident waves instead)
+  Xoro128 rng;
+  if (!u_in) rng.seed(qrng_key(seed, offset), ((uint64_t)tile << 8) | threadIdx.x);
+  const bool dense = dense_out != nullptr;
+#pragma unroll
+  for (int g = 0; g < kQG; ++g) {
+    const int64_t e0 = eb + g * GS;
+    float lf[kQPer];
+#if CHOCO_QCHECK
+    uint32_t tmin_m1 = 0xFFFFFFFFu, qmax = 0u;
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) lf[c] = D.quot_nocheck(sf * fabsf(d[g][c]), tmin_m1, qmax);  // s * x.abs() / norm
+    const bool gslow = D.group_slow(tmin_m1, qmax);
+    if (__builtin_expect(__ballot(gslow) != 0, 0)) {
+#pragma unroll
+      for (int c = 0; c < kQPer; ++c)
+        if (gslow) lf[c] = (sf * fabsf(d[g][c])) / P.norm;
+    }
+#else
+    bool slow[kQPer];
+    bool any = false;
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) {
+      lf[c] = D.quot(sf * fabsf(d[g][c]), slow[c]);  // s * x.abs() / norm
+      any |= slow[c];
+    }
+    if (__builtin_expect(__ballot(any) != 0, 0)) {
+#pragma unroll
+      for (int c = 0; c < kQPer; ++c)
+        if (slow[c]) lf[c] = (sf * fabsf(d[g][c])) / P.norm;
+    }
+#endif
+    float u[kQPer];
+    if (u_in) {
+      const float4 u0 = *reinterpret_cast<const float4*>(u_in + e0);
+      const float4 u1 = *reinterpret_cast<const float4*>(u_in + e0 + 4);
+      u[0] = u0.x; u[1] = u0.y; u[2] = u0.z; u[3] = u0.w;
+      u[4] = u1.x; u[5] = u1.y; u[6] = u1.z; u[7] = u1.w;
+    } else {
+#pragma unroll
+      for (int c = 0; c < kQPer; c += 2) rng.next2(u[c], u[c + 1]);
+    }
+    uint32_t lv[kQPer];
+    uint32_t sbits = 0;
+    float lvlf[kQPer];
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) {
+      lvlf[c] = qlevel(lf[c], u[c]);
+      lv[c] = level_code(lvlf[c], sf);
+      sbits |= d[g][c] < 0.f ? (1u << c) : 0u;
+    }
+    const int64_t t = e0 / kQPer;
+    store_levels<CW>(lvl_plane, t, lv);
+    sign_plane[t] = (uint8_t)sbits;
+    if (dense) {  // one branch per group (a branch per element made the compiler shuffle the group's registers)
+      float outv[kQPer];
+#pragma unroll
+      for (int c = 0; c < kQPer; ++c) {
+        const float sg = d[g][c] > 0.f ? 1.0f : (d[g][c] < 0.f ? -1.0f : 0.0f);  // torch.sign (NaN -> 0)
+        outv[c] = (((P.scale * sg) * P.norm) * lvlf[c]) / sf;
+      }
+      *reinterpret_cast<float4*>(dense_out + e0) = make_float4(outv[0], outv[1], outv[2], outv[3]);
+      *reinterpret_cast<float4*>(dense_out + e0 + 4) = make_float4(outv[4], outv[5], outv[6], outv[7]);
+    }
+  }
+}
+
+// Occupancy of the one-tile quantize kernel (waves per SIMD the compiler must allow; A/B
+// knob).  r04 same-box A/B at 100M: 4 -> 131 us, 6 -> 132, 8 -> 136 (more waves did not
+// hide more latency: the 64-VGPR build spills one float4).
+#ifndef CHOCO_QQ_WAVES
+#define CHOCO_QQ_WAVES 4
+#endif
+template <int CW, bool XH>
+__global__ __launch_bounds__(kQThreads, XH ? 4 : CHOCO_QQ_WAVES) void qsgd_quant_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, const int64_t* __restrict__ seg_off,
     int nseg, int s_levels, int biased, const float* __restrict__ norms, const float* __restrict__ u_in,
     uint64_t seed, uint64_t offset, uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
@@ -468,7 +551,7 @@ __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
       a[g][0] = ld_quant4(x + eb + g * GS);
       a[g][1] = ld_quant4(x + eb + g * GS + 4);
     }
-    if (xh) {
+    if constexpr (XH) {
 #pragma unroll
       for (int g = 0; g < kQG; ++g) {
         const float4 h0 = ld_quant4(xh + eb + g * GS), h1 = ld_quant4(xh + eb + g * GS + 4);
@@ -482,77 +565,91 @@ __global__ __launch_bounds__(kQThreads) void qsgd_quant_kernel(
       d[g][4] = a[g][1].x; d[g][5] = a[g][1].y; d[g][6] = a[g][1].z; d[g][7] = a[g][1].w;
     }
   }
-  float u[kQG][kQPer];
-  if (u_in) {
-#pragma unroll
-    for (int g = 0; g < kQG; ++g) {
-      const float4 u0 = *reinterpret_cast<const float4*>(u_in + eb + g * GS);
-      const float4 u1 = *reinterpret_cast<const float4*>(u_in + eb + g * GS + 4);
-      u[g][0] = u0.x; u[g][1] = u0.y; u[g][2] = u0.z; u[g][3] = u0.w;
-      u[g][4] = u1.x; u[g][5] = u1.y; u[g][6] = u1.z; u[g][7] = u1.w;
-    }
-  } else {
-    Xoro128 rng;
-    rng.seed(qrng_key(seed, offset), ((uint64_t)tile << 8) | threadIdx.x);
-#pragma unroll
-    for (int g = 0; g < kQG; ++g)
-#pragma unroll
-      for (int c = 0; c < kQPer; c += 2) rng.next2(u[g][c], u[g][c + 1]);
-  }
   const QParam P = qparam(norms, seg_off, n, sg0, s_levels, biased != 0);
   QDiv D;
   D.init(P.norm);
-  const bool dense = dense_out != nullptr;
+  quant_tile_math<CW>(d, tile, n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out);
+}
+
+// Single-segment buffers (the flat path, BASELINE cfg 3): a grid of resident workgroups
+// walks the full tiles from the end of the range backward (Infinity-Cache hits on the
+// tail the norm pass read last), workgroup b taking the (b + i G)-th tile from the end,
+// with the NEXT tile's loads issued before the current tile's math -- a wave's loads and
+// math overlap instead of alternating.  r04 counters on the one-tile kernel: waves waited
+// on memory 46 % of their cycles while VALU issue ran at ~37 % of the SIMDs' 2-cycle rate
+// (SQ_WAIT_ANY / SQ_WAVE_CYCLES, SQ_INSTS_VALU; profiles/r04_qsgd_sq_counters.txt).
+// Workgroup 0 also quantizes the range's partial last tile (tail_tile >= 0) and zeroes
+// the planes' padding.  Same uniforms and results as the one-tile kernel.
+template <int CW, bool XH>
+__global__ __launch_bounds__(kQThreads, 4) void qsgd_quant_loop_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, const int64_t* __restrict__ seg_off,
+    int s_levels, int biased, const float* __restrict__ norms, const float* __restrict__ u_in, uint64_t seed,
+    uint64_t offset, uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
+    float* __restrict__ dense_out, int64_t tile_lo, int64_t full_cnt, int64_t tail_tile, int64_t pad_e0,
+    int64_t pad_len) {
+  constexpr int GS = kQThreads * kQPer;  // 2048
+  if (blockIdx.x == 0) {
+    const int64_t g0 = pad_e0 / kQPer, groups = (pad_len + kQPer - 1) / kQPer;
+    const int64_t lvl_used = (g0 + groups) * CW, lvl_end = g0 * CW + (groups * CW + 15) / 16 * 16;
+    const int64_t sgn_used = g0 + groups, sgn_end = g0 + (groups + 15) / 16 * 16;
+    for (int64_t b = lvl_used + threadIdx.x; b < lvl_end; b += kQThreads) lvl_plane[b] = 0;
+    for (int64_t b = sgn_used + threadIdx.x; b < sgn_end; b += kQThreads) sign_plane[b] = 0;
+    if (tail_tile >= 0)
+      qsgd_quant_tile_slow<CW>(x, xh, n, seg_off, 1, s_levels, biased, norms, u_in, seed, offset, lvl_plane,
+                               sign_plane, dense_out, tail_tile, 0);
+  }
+  int64_t j = blockIdx.x;
+  if (j >= full_cnt) return;
+  const float sf = (float)s_levels;
+  const QParam P = qparam(norms, seg_off, n, 0, s_levels, biased != 0);
+  QDiv D;
+  D.init(P.norm);
+  auto tile_of = [&](int64_t jj) -> int64_t { return CHOCO_QQUANT_REV ? tile_lo + full_cnt - 1 - jj : tile_lo + jj; };
+  auto load = [&](int64_t tile, float4 (&a)[kQG][2], float4 (&h)[kQG][2]) {
+    const int64_t eb = tile * kQStreamTile + (int64_t)threadIdx.x * kQPer;
 #pragma unroll
-  for (int g = 0; g < kQG; ++g) {
-    const int64_t e0 = eb + g * GS;
-    float lf[kQPer];
-#if CHOCO_QCHECK
-    uint32_t tmin_m1 = 0xFFFFFFFFu, qmax = 0u;
-#pragma unroll
-    for (int c = 0; c < kQPer; ++c) lf[c] = D.quot_nocheck(sf * fabsf(d[g][c]), tmin_m1, qmax);  // s * x.abs() / norm
-    const bool gslow = D.group_slow(tmin_m1, qmax);
-    if (__builtin_expect(__ballot(gslow) != 0, 0)) {
-#pragma unroll
-      for (int c = 0; c < kQPer; ++c)
-        if (gslow) lf[c] = (sf * fabsf(d[g][c])) / P.norm;
+    for (int g = 0; g < kQG; ++g) {
+      a[g][0] = ld_quant4(x + eb + g * GS);
+      a[g][1] = ld_quant4(x + eb + g * GS + 4);
     }
-#else
-    bool slow[kQPer];
-    bool any = false;
+    if constexpr (XH) {
 #pragma unroll
-    for (int c = 0; c < kQPer; ++c) {
-      lf[c] = D.quot(sf * fabsf(d[g][c]), slow[c]);  // s * x.abs() / norm
-      any |= slow[c];
-    }
-    if (__builtin_expect(__ballot(any) != 0, 0)) {
-#pragma unroll
-      for (int c = 0; c < kQPer; ++c)
-        if (slow[c]) lf[c] = (sf * fabsf(d[g][c])) / P.norm;
-    }
-#endif
-    uint32_t lv[kQPer];
-    uint32_t sbits = 0;
-    float lvlf[kQPer];
-#pragma unroll
-    for (int c = 0; c < kQPer; ++c) {
-      lvlf[c] = qlevel(lf[c], u[g][c]);
-      lv[c] = level_code(lvlf[c], sf);
-      sbits |= d[g][c] < 0.f ? (1u << c) : 0u;
-    }
-    const int64_t t = e0 / kQPer;
-    store_levels<CW>(lvl_plane, t, lv);
-    sign_plane[t] = (uint8_t)sbits;
-    if (dense) {  // one branch per group (a branch per element made the compiler shuffle the group's registers)
-      float outv[kQPer];
-#pragma unroll
-      for (int c = 0; c < kQPer; ++c) {
-        const float sg = d[g][c] > 0.f ? 1.0f : (d[g][c] < 0.f ? -1.0f : 0.0f);  // torch.sign (NaN -> 0)
-        outv[c] = (((P.scale * sg) * P.norm) * lvlf[c]) / sf;
+      for (int g = 0; g < kQG; ++g) {
+        h[g][0] = ld_quant4(xh + eb + g * GS);
+        h[g][1] = ld_quant4(xh + eb + g * GS + 4);
       }
-      *reinterpret_cast<float4*>(dense_out + e0) = make_float4(outv[0], outv[1], outv[2], outv[3]);
-      *reinterpret_cast<float4*>(dense_out + e0 + 4) = make_float4(outv[4], outv[5], outv[6], outv[7]);
     }
+  };
+  float4 a[kQG][2], h[kQG][2];
+  load(tile_of(j), a, h);
+  for (;;) {
+    const int64_t jn = j + (int64_t)gridDim.x;
+    const bool more = jn < full_cnt;  // workgroup-uniform
+    float4 b[kQG][2], bh[kQG][2];
+    if (more) load(tile_of(jn), b, bh);
+    float d[kQG][kQPer];
+#pragma unroll
+    for (int g = 0; g < kQG; ++g) {
+      float4 v0 = a[g][0], v1 = a[g][1];
+      if constexpr (XH) {
+        v0 = sub4(v0, h[g][0]);
+        v1 = sub4(v1, h[g][1]);
+      }
+      d[g][0] = v0.x; d[g][1] = v0.y; d[g][2] = v0.z; d[g][3] = v0.w;
+      d[g][4] = v1.x; d[g][5] = v1.y; d[g][6] = v1.z; d[g][7] = v1.w;
+    }
+    quant_tile_math<CW>(d, tile_of(j), n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out);
+    if (!more) break;
+#pragma unroll
+    for (int g = 0; g < kQG; ++g) {
+      a[g][0] = b[g][0];
+      a[g][1] = b[g][1];
+      if constexpr (XH) {
+        h[g][0] = bh[g][0];
+        h[g][1] = bh[g][1];
+      }
+    }
+    j = jn;
   }
 }
 
@@ -754,6 +851,14 @@ static int qsgd_norms_launch(const float* x, const float* xhat, int64_t n, const
 // group (lvl_plane / sign_plane point at element 0's group; a range call writes
 // only the groups of its elements, plus the 16-byte padding of a plane that ends
 // at e1).
+// A/B knob: the looping quantize kernel for single-segment buffers (0: one tile per workgroup)
+#ifndef CHOCO_QQ_LOOP
+#define CHOCO_QQ_LOOP 1
+#endif
+#ifndef CHOCO_QQ_GRID  // resident workgroups of the looping kernel: 4 per CU (16 waves)
+#define CHOCO_QQ_GRID 1024
+#endif
+constexpr int64_t kQLoopGrid = CHOCO_QQ_GRID;
 static int qsgd_quant_launch(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
                              int32_t q, int32_t is_biased, const float* norms, const float* u_in, uint64_t seed,
                              uint64_t offset, uint8_t* lvl_plane, uint8_t* sign_plane, float* dense_out,
@@ -763,11 +868,41 @@ static int qsgd_quant_launch(const float* x, const float* xhat, int64_t n, const
   const int64_t tile_lo = e0 / kQStreamTile;
   const int64_t tile_cnt = (e1 - e0 + kQStreamTile - 1) / kQStreamTile;
   profile_begin("qsgd_quantize", st);
+  // (with x_hat the prefetch would need 64 more registers: the one-tile kernel, no spills)
+  if (CHOCO_QQ_LOOP && nseg <= 1 && !xhat) {
+    // full tiles of the range, and its partial last tile (the buffer's end)
+    const bool partial = (tile_lo + tile_cnt) * kQStreamTile > n;
+    const int64_t full_cnt = tile_cnt - (partial ? 1 : 0);
+    const int64_t tail_tile = partial ? tile_lo + tile_cnt - 1 : -1;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(full_cnt, kQLoopGrid));
+#define CHOCO_QL(CWV)                                                                                         \
+  case CWV:                                                                                                   \
+    CHOCO_KLAUNCH((qsgd_quant_loop_kernel<CWV, false>), dim3(grid), dim3(kQThreads), 0, st, x, nullptr, n,   \
+                  seg_off, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane, sign_plane, dense_out,   \
+                  tile_lo, full_cnt, tail_tile, pad_e0, e1 - pad_e0);                                         \
+    break;
+    switch (cw) {
+      CHOCO_QL(1)
+      CHOCO_QL(2)
+      CHOCO_QL(4)
+      CHOCO_QL(8)
+      CHOCO_QL(16)
+    }
+#undef CHOCO_QL
+    profile_end("qsgd_quantize", st);
+    CHOCO_LAUNCHED("qsgd_quant_loop_kernel");
+    return CHOCO_OK;
+  }
 #define CHOCO_Q(CWV)                                                                                          \
   case CWV:                                                                                                   \
-    CHOCO_KLAUNCH((qsgd_quant_kernel<CWV>), dim3((unsigned)tile_cnt), dim3(kQThreads), 0, st, x, xhat, n,    \
-                  seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane, sign_plane,        \
-                  dense_out, tile_lo, tile_cnt, pad_e0, e1 - pad_e0);                                         \
+    if (xhat)                                                                                                 \
+      CHOCO_KLAUNCH((qsgd_quant_kernel<CWV, true>), dim3((unsigned)tile_cnt), dim3(kQThreads), 0, st, x, xhat, \
+                    n, seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane, sign_plane,   \
+                    dense_out, tile_lo, tile_cnt, pad_e0, e1 - pad_e0);                                       \
+    else                                                                                                      \
+      CHOCO_KLAUNCH((qsgd_quant_kernel<CWV, false>), dim3((unsigned)tile_cnt), dim3(kQThreads), 0, st, x,     \
+                    nullptr, n, seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane,      \
+                    sign_plane, dense_out, tile_lo, tile_cnt, pad_e0, e1 - pad_e0);                           \
     break;
   switch (cw) {
     CHOCO_Q(1)

@@ -44,7 +44,6 @@
 #include <algorithm>
 #include <atomic>
 #include <mutex>
-#include <type_traits>
 #include <unordered_map>
 
 namespace choco {
@@ -67,29 +66,6 @@ constexpr int64_t kChunk = CHOCO_K2_CHUNK;
 static_assert(kTileQuant % kChunk == 0 && kChunk % (256 * kK2Unroll) == 0, "chunk geometry");
 static_assert(kChunk == 256 * kK2Unroll || kChunk == 512 * kK2Unroll, "a chunk is one or two load batches");
 constexpr int kMaybeCap = 65536;        // side-list capacity per tile (maybe keys)
-// One-launch path (one_finish): workgroup b streams the 32768-element blocks b, b + nb, ...
-constexpr int kOneBlock = 32768;        // elements per block
-constexpr int kOneLcpb = kChunk == 2048 ? 4 : 3;  // log2 chunks per block
-static_assert((int64_t)kOneBlock == kChunk << kOneLcpb, "block geometry");
-constexpr int kOneMaxBlk = 16;          // blocks per workgroup (n <= 16 * 256 blocks = 134M)
-constexpr int kOneSideCap = 2048;       // side-list capacity per block (6 %; a k = 1 % window holds ~0.5 %)
-// A/B knob: rotate the blocks of full rows (block l of workgroup b = l nb + (b + l) mod nb),
-// so that every XCD reads every residue of the block index mod 8 (0: block l nb + b)
-#ifndef CHOCO_ONE_ROT
-#define CHOCO_ONE_ROT 1
-#endif
-// block l of workgroup b (row l = blocks [l nb, l nb + nb); a partial last row unrotated)
-__host__ __device__ inline uint32_t one_block(uint32_t b, uint32_t l, uint32_t nb, uint32_t nblk) {
-  const bool full = (l + 1u) * nb <= nblk;
-  return l * nb + (CHOCO_ONE_ROT && full ? (b + l) % nb : b);
-}
-// its record slot: owner-major (a workgroup's records are one contiguous run)
-__host__ __device__ inline uint32_t one_rec_slot(uint32_t blk, uint32_t nb, uint32_t nblk) {
-  const uint32_t l = blk / nb, j = blk % nb;
-  const bool full = (l + 1u) * nb <= nblk;
-  const uint32_t owner = CHOCO_ONE_ROT && full ? (j + nb - l % nb) % nb : j;
-  return owner * (uint32_t)kOneMaxBlk + l;
-}
 constexpr int kNBucket = 256;           // 255 "maybe" buckets + 1 "sure"
 constexpr int kNMaybe = kNBucket - 1;
 constexpr int kNRep = 16;               // replicas of the global bucket totals
@@ -145,27 +121,6 @@ CHOCO_DEV void st_pol(T* p, T v) {
   }
 }
 
-// Hand-offs between workgroups of one launch use the fence-free form of
-// MI355X_MICROARCH.md "Valid forms" (row 1): every handed-off word is stored
-// write-through (relaxed agent-scope atomic store = sc1) and read with sc1 loads.
-CHOCO_DEV void st_sc1(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-CHOCO_DEV uint32_t ld_sc1(const uint32_t* p) {
-  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// 16-byte granules (the one-launch emission records): buffer_store/load_dwordx4 sc1,
-// observed untorn on gfx950 (the guide's R2 granule), so a record is its own flag.
-// The resource is the (wave-uniform) record array, the record a per-lane offset: a
-// per-lane resource would make the compiler loop over the wave's distinct values.
-constexpr int kCpolSc1 = 16;  // gfx940+ cache-policy bit SC1 of a buffer instruction
-CHOCO_DEV void st_sc1_16(__amdgpu_buffer_rsrc_t recs, uint32_t i, uint4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
-                                         recs, i * 16u, 0, kCpolSc1);
-}
-CHOCO_DEV uint4 ld_sc1_16(__amdgpu_buffer_rsrc_t recs, uint32_t i) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b128(recs, i * 16u, 0, kCpolSc1);
-  return __builtin_bit_cast(uint4, v);
-}
-
 enum TileMode { kTakeNone = 0, kTakeAll = 1, kTakePartial = 2 };
 
 // Candidate window of one call: keys >= s_lo are candidates, [s_lo, s_hi) is
@@ -190,8 +145,7 @@ struct TopkCtrl {
   uint32_t fallbacks;                            // calls that took the exact fallback (diagnostic counter)
   uint32_t cold_left;                            // warm-host calls still to sample their window in K2 (backoff)
   uint32_t backoff;                              // cold run length after the next warm miss
-  uint32_t arrive;                               // one-launch path: tiles done (the last resets it)
-  uint32_t pad0[11];
+  uint32_t pad0[12];
   uint32_t overflow[2];                          // bit 0: a side list overflowed; bit 1: take the exact fallback
   uint32_t pad1[14];
   TopkBounds bounds[2];
@@ -203,11 +157,27 @@ static_assert(offsetof(TopkCtrl, fallbacks) == CHOCO_TOPK_FALLBACKS_OFFSET, "fal
 constexpr uint32_t kStatusPollTimeout = 1u;    // a bounded wait of the exact fallback gave up: output invalid
 constexpr uint32_t kNoCandKey = 0x7F800000u;   // window that admits only inf / NaN keys (invalid bounds)
 
+// The self-message part of CHOCOSparsificationCompressor.uncompress (parallel_choco_v.py:
+// 307-310) folded into the emission of the message: hat[i] += q (hat != nullptr) and
+// mem[i] += w * q (mem != nullptr; two roundings, as choco_sparse_accumulate) for every
+// emitted (q, i).  hat may be the x_hat the call compresses against: nothing reads it
+// once emission starts (K34 emits from the candidate slots; the exact fallback's emission
+// phase starts after every read phase, and each element is read before it is written).
+struct Fold {
+  float* hat;
+  float* mem;
+  float w;
+  __host__ __device__ bool on() const { return hat != nullptr || mem != nullptr; }
+};
+CHOCO_DEV void fold_apply(const Fold& f, int64_t i, float q) {
+  if (f.hat) f.hat[i] = f.hat[i] + q;
+  if (f.mem) f.mem[i] = f.mem[i] + f.w * q;
+}
+
 struct TopkLayout {
   int64_t n;
   uint32_t tile, nb, side_cap;
-  uint32_t one_nb, one_nblk;  // one-launch geometry: workgroups, 32768-element blocks
-  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, off_wide, off_gcnt, off_tinfo, off_rec, total;
+  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, off_wide, off_gcnt, off_tinfo, total;
 };
 
 // Tile = ceil(n / kK2Target) rounded up to 32768 elements: one tile per CU, all
@@ -223,23 +193,19 @@ static TopkLayout topk_layout(int64_t n) {
   L.tile = (uint32_t)tile;
   L.nb = (uint32_t)((n + tile - 1) / tile);
   L.side_cap = (uint32_t)std::min<int64_t>(kMaybeCap, tile);
-  L.one_nblk = (uint32_t)((n + kOneBlock - 1) / kOneBlock);
-  L.one_nb = std::min<uint32_t>(L.one_nblk, (uint32_t)kK2Target);
-  const size_t rows = std::max<size_t>(L.nb, L.one_nblk);  // tiles, or one-launch blocks
   // A fixed header at the start of every top-k workspace (any n): the control block
   // and the exact-fallback queue (WideCtrl), whose counters rely on starting zeroed --
   // calls of different n sharing one workspace must not move them.
   size_t o = 0;
   L.off_ctrl = o;  o += align_up(sizeof(TopkCtrl), 256);
   L.off_wide = o;  o += kWideBytes;
-  L.off_cum = o;   o += align_up(rows * kNBucket * 4, 256);
+  L.off_cum = o;   o += align_up((size_t)L.nb * kNBucket * 4, 256);
   L.off_cntw = o;  o += align_up((size_t)L.nb * (tile / kChunk) * 4, 256);   // per-chunk candidate counts
-  L.off_side = o;  o += align_up(std::max<size_t>((size_t)L.nb * L.side_cap, (size_t)L.one_nblk * kOneSideCap) * 4, 256);
+  L.off_side = o;  o += align_up((size_t)L.nb * L.side_cap * 4, 256);
   L.off_cval = o;  o += align_up((size_t)L.nb * tile * 4, 256);   // candidate values, chunk slot ranges
   L.off_cidx = o;  o += align_up((size_t)L.nb * tile * 4, 256);   // ... and indices
-  L.off_gcnt = o;  o += align_up((size_t)std::max(L.nb, L.one_nb) * 8, 256);              // ... its per-tile (#>T, #==T)
+  L.off_gcnt = o;  o += align_up((size_t)L.nb * 8, 256);              // ... its per-tile (#>T, #==T)
   L.off_tinfo = o; o += align_up((size_t)L.nb * 4, 256);              // per tile: candidates (compact) or ~0 (spilled)
-  L.off_rec = o;   o += align_up((size_t)L.one_nb * kOneMaxBlk * 16, 256);  // one-launch path: per-block emission record
   L.total = o;
   return L;
 }
@@ -429,12 +395,7 @@ struct SampleHist {
   uint32_t list[kK2Waves][kListPerWave];
 };
 
-// MAXC: chunks per tile the tables hold.  The one-launch path streams <= kOneMaxBlk
-// strided blocks of 16 chunks per workgroup (256 chunks) and spends the LDS this saves
-// on per-block bucket histograms and its position map.
-constexpr int kPmapCap = 8192;  // one launch: tile candidates with an LDS position -> pair map
-template <int MAXC, bool ONE_>
-struct StreamSmemT {
+struct StreamSmem {
   float4 ent_v[kK2Waves][kEnt];   // staged lanes: the float4 row slice
   uint32_t ent_i[kK2Waves][kEnt]; // ... and the index of its first element
   float4 trash_v[64];             // per-lane sink of the branch-free batch writes (shared, never read)
@@ -443,21 +404,15 @@ struct StreamSmemT {
     uint2 pairs[kK2Waves * kPairsPerWave];  // (value bits, index) per candidate, per-wave regions
     SampleHist sh;                          // the prologue's sample window (cold calls only)
   } u;
-  uint32_t cmeta[MAXC];           // per chunk: LDS start | LDS count << 16
-  uint32_t ccnt[MAXC + 1];        // per chunk: candidates; at tile end their exclusive prefix
-  uint32_t hist[ONE_ ? kOneMaxBlk * kNBucket : kNBucket];  // maybe-key bucket counts (per block), then cursors
-  uint32_t gacc[ONE_ ? kNBucket : 1];  // one launch: the workgroup's bucket suffix counts, summed over blocks
+  uint32_t cmeta[kMaxTileChunks];  // per chunk: LDS start | LDS count << 16
+  uint32_t ccnt[kMaxTileChunks + 1];  // per chunk: candidates; at tile end their exclusive prefix
+  uint32_t hist[kNBucket];        // maybe-key bucket counts, then counting-sort cursors
   uint32_t cnt[kK2Waves];
   uint32_t scratch[40];
   uint32_t bc[8];
   uint32_t next_chunk;            // the tile's chunk counter (waves claim chunks)
   uint32_t spill;                 // some wave spilled pairs to global (tile end)
-  uint32_t m1024;                 // this call's window margin (0: a sampled window); one-launch path
-  uint16_t pmap[ONE_ ? kPmapCap : 2];  // one launch: tile candidate position -> pair (LDS index)
 };
-using StreamSmem = StreamSmemT<kMaxTileChunks, false>;
-constexpr int kOneMaxChunks = kOneMaxBlk << kOneLcpb;
-using StreamSmemOne = StreamSmemT<kOneMaxChunks, true>;
 
 // Unconditional float4 loads of kK2Unroll rows (no branch around a load: the
 // compiler's vmcnt accounting stays exact and all rows are in flight together),
@@ -529,7 +484,6 @@ struct WaveAcc {
   uint32_t lstart, lcnt;       // the current chunk's pairs kept in LDS: region offset, count
   uint32_t lfill;              // pairs in the wave's LDS region
   uint32_t cand;               // candidates, whole tile
-  uint32_t hoff;               // one launch: the current chunk's block histogram (block * kNBucket)
 };
 
 // Expand ring entries [eflushed, eflushed + nent) (nent <= 64, one per lane)
@@ -557,7 +511,7 @@ CHOCO_DEV void flush_entries(const Src<MODE, XH>& src, SM& sm, int w, int lane, 
     const uint32_t key = MODE == kData ? fkey(vv[q]) : (rank_hash(bk.seed, i0 + q) >> 1);
     ok[q] = have && (int64_t)i0 + q < bk.n && key >= bk.s_lo;
     nc += ok[q] ? 1u : 0u;
-    if (ok[q] && key < bk.s_hi) atomicAdd(&sm.hist[a.hoff + ((key - bk.s_lo) >> bk.shift)], 1u);
+    if (ok[q] && key < bk.s_hi) atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
   }
   if (MODE == kHash) {
 #pragma unroll
@@ -886,48 +840,19 @@ CHOCO_DEV Buckets prologue_sample(const float* __restrict__ x, const float* __re
   return bk;
 }
 
-// One-launch path (ONE): the stream kernel also selects and emits, no K34 (see
-// one_finish below).  Arguments of that tail, unused otherwise.
-struct WideCtrl;
-struct OneArgs {
-  uint4* rec;               // per block (owner-major): {output offset | kOneFallback, T, ties to take, epoch}
-  uint32_t epoch;           // this call's tag (never 0, unique per workspace within 2^32 calls)
-  float* out_val;
-  int32_t* out_idx;
-  int64_t idx_base;
-  float scale;
-  WideCtrl* wide;
-  uint32_t* gcnt;
-  uint32_t* status;
-  uint32_t* host_status;
-};
-template <int MODE, bool XH, bool GS>
-CHOCO_DEV void one_finish(const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k,
-                          uint32_t tile, uint32_t nb, uint32_t par, uint32_t side_cap, const Buckets& bk,
-                          TopkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ cum_tab,
-                          const uint32_t* __restrict__ side, const float* __restrict__ cval,
-                          const uint32_t* __restrict__ cidx, const OneArgs& oa, StreamSmemOne& sm, bool spilled,
-                          uint32_t nchunk, uint32_t nsb, uint32_t lcpb);
-template <int MODE>
-CHOCO_DEV bool one_tile_end(StreamSmemOne& sm, TopkCtrl* __restrict__ ctrl, uint32_t par,
-                            uint32_t* __restrict__ cum_tab, uint32_t* __restrict__ side, uint32_t cap_b, uint32_t nb,
-                            uint32_t b, uint32_t nsb, uint32_t nchunk, uint32_t tile, uint32_t lcpb,
-                            const Buckets& bk, float* __restrict__ cval, uint32_t* __restrict__ cidx, uint32_t nblk);
-
 // Random-k (MODE kHash): keys are uniform on [0, 2^31) and (s_lo, s_hi) come from
 // the binomial tails (host), passed as hs_lo / hs_hi.
 // GS (kData, XH): the fused gossip step -- the stream reads x, memory and xh,
 // writes x_new back and selects on d = x_new - xh.
-template <int MODE, bool XH, bool GS = false, bool ONE = false>
+template <int MODE, bool XH, bool GS = false>
 __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
     uint32_t par, uint32_t side_cap, uint64_t seed, uint32_t hs_lo, uint64_t hs_hi, TopkCtrl* __restrict__ ctrl,
     uint32_t* __restrict__ cum_tab, uint32_t* __restrict__ cntw, uint32_t* __restrict__ side,
     float* __restrict__ cval, uint32_t* __restrict__ cidx, uint32_t* __restrict__ tinfo, Gossip gs,
-    SampleRanks ranks, uint32_t sample_if_cold, OneArgs oa) {
+    SampleRanks ranks, uint32_t sample_if_cold) {
   static_assert(!GS || (MODE == kData && XH), "the gossip step needs x_hat and data keys");
-  static_assert(!ONE || MODE == kData, "the one-launch path selects data keys");
-  __shared__ std::conditional_t<ONE, StreamSmemOne, StreamSmem> sm;
+  __shared__ StreamSmem sm;
   STAMP(1024 + blockIdx.x, 0);
   const int tid = threadIdx.x;
   const int lane = lane_id();
@@ -937,29 +862,15 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   constexpr bool kOneBatch = kChunk == kStep;  // a chunk is one load batch (else: two, A and B)
   constexpr bool kTwoChunks = kOneBatch && MODE == kData && !XH;  // A and B hold the next two chunks
   static_assert(!GS || kOneBatch, "the gossip stream processes one-batch chunks");
-  // one launch: workgroup b streams the blocks b, b + nb, ... (`tile` = the block size);
-  // chunk c of the workgroup is chunk c % 16 of its block c / 16
-  const uint32_t nblk = ONE ? (uint32_t)((n + tile - 1) / tile) : 0u;
-  const uint32_t nsb = ONE ? (nblk - (uint32_t)b + nb - 1u) / nb : 1u;
-  const uint32_t nchunk = ONE ? nsb << kOneLcpb : tile / (uint32_t)kChunk;
-  auto chunk_e0 = [&](uint32_t cc) -> int64_t {
-    if constexpr (ONE)
-      return (int64_t)one_block((uint32_t)b, cc >> kOneLcpb, nb, nblk) * tile +
-             (int64_t)(cc & ((1u << kOneLcpb) - 1u)) * kChunk;
-    else
-      return b * (int64_t)tile + (int64_t)cc * kChunk;
-  };
+  const uint32_t nchunk = tile / (uint32_t)kChunk;
   Src<MODE, XH> src{x, xh, seed};
-  // resource-relative byte offset of a full chunk's first / second batch, or kNoChunk
-  // (resources based at the tile start; one launch: at the buffer start, n * 4 < 2^31)
-  const int64_t rb = ONE ? 0 : b * (int64_t)tile;
-  const int64_t tlen = ONE ? n : min((int64_t)tile, n - b * (int64_t)tile);
-  const TileRsrc ts{buf_rsrc(x + rb, (uint32_t)(tlen * 4)), buf_rsrc((XH ? xh : x) + rb, (uint32_t)(tlen * 4)),
-                    buf_rsrc((GS ? gs.mem : x) + rb, (uint32_t)(tlen * 4))};
+  // tile-relative byte offset of a full chunk's first / second batch, or kNoChunk
+  const int64_t tlen = min((int64_t)tile, n - b * (int64_t)tile);
+  const TileRsrc ts{buf_rsrc(x + b * (int64_t)tile, (uint32_t)(tlen * 4)),
+                    buf_rsrc((XH ? xh : x) + b * (int64_t)tile, (uint32_t)(tlen * 4)),
+                    buf_rsrc((GS ? gs.mem : x) + b * (int64_t)tile, (uint32_t)(tlen * 4))};
   auto batch0 = [&](uint32_t c) -> uint32_t {
-    if (c >= nchunk) return kNoChunk;
-    const int64_t e0 = chunk_e0(c) - rb;
-    return e0 + kChunk <= tlen ? (uint32_t)e0 * 4u : kNoChunk;
+    return (c < nchunk && (int64_t)(c + 1) * kChunk <= tlen) ? c * (uint32_t)kChunk * 4u : kNoChunk;
   };
   auto batch1 = [&](uint32_t c) -> uint32_t { return batch0(c) + (uint32_t)kStep * 4u; };
 
@@ -985,7 +896,6 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     const uint32_t cold_left = ctrl->cold_left;
     bool ok = W.valid != 0u && W.n == n && W.k == k && W.shift < 32u;
     bool degenerate = false;
-    uint32_t m1024 = 0;
     if (sample_if_cold && (!ok || cold_left != 0u)) {  // grid-uniform
       SampleView sv{sm.u.sh, sm.scratch, sm.bc};
       bool deg;
@@ -1008,26 +918,17 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     } else {
       bk = ok ? make_buckets_from(W.s_lo, W.s_hi, W.shift, seed) : make_buckets_from(kNoCandKey, kNoCandKey, 0u, seed);
       degenerate = (ctrl->overflow[par] & 2u) != 0u;
-      m1024 = ok ? W.m1024 : 0u;
     }
-    if (ONE && tid == 0) sm.m1024 = m1024;
     // no window for this (n, k) (a workspace the host believed warm): the exact fallback
     if (!ok && b == 0 && tid == 0) atomicOr(&ctrl->overflow[par], 2u);
     // a degenerate sample (K1's flag, or this prologue's): K34 will take the exact
     // fallback, which needs nothing from this kernel (with the fused gossip step the
     // stream must still run)
-    if (!GS && (!ok || degenerate)) {
-      // one launch: every workgroup still arrives; the last one finds the overflow bit and
-      // the whole grid runs the exact fallback
-      if constexpr (ONE)
-        one_finish<MODE, XH, GS>(x, xh, n, k, tile, nb, par, side_cap, bk, ctrl, cum_tab, side, cval, cidx, oa, sm,
-                                 false, nchunk, nsb, kOneLcpb);
-      return;
-    }
+    if (!GS && (!ok || degenerate)) return;
   } else {
     bk = make_buckets(hs_lo, hs_hi, seed);
   }
-  for (uint32_t i = (uint32_t)tid; i < (ONE ? nsb : 1u) * kNBucket; i += kK2Threads) sm.hist[i] = 0;
+  if (tid < kNBucket) sm.hist[tid] = 0;
   if (tid == 0) {
     sm.next_chunk = kTwoChunks ? 2 * kK2Waves : kK2Waves;
     sm.spill = 0;
@@ -1056,8 +957,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   // (hash mode, the partial chunk); ends with the chunk's bookkeeping.
   // `reload` refills R (the wave's next chunk) as soon as R is dead.
   auto run_chunk = [&](uint32_t cc, const float4 (&R)[kK2Unroll], auto&& reload) {
-    const int64_t cbeg = chunk_e0(cc);
-    if constexpr (ONE) a.hoff = (cc >> kOneLcpb) * (uint32_t)kNBucket;
+    const int64_t cbeg = tb + (int64_t)cc * kChunk;
     const int64_t cend = min(cbeg + kChunk, n);
     float* __restrict__ ov = cval + cbeg;
     uint32_t* __restrict__ oi = cidx + cbeg;
@@ -1184,15 +1084,6 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   STAMP(1024 + b, 2);
   WSTAMP(32000 + b * 8 + (w >> 2), w & 3);
   __syncthreads();
-  if constexpr (ONE) {
-    const bool spilled = one_tile_end<MODE>(sm, ctrl, par, cum_tab, side, side_cap, nb, (uint32_t)b, nsb, nchunk,
-                                            tile, kOneLcpb, bk, cval, cidx, nblk);
-    STAMP(22000 + b, 1);
-    __syncthreads();  // the ring (side keys, position map) is read again below
-    one_finish<MODE, XH, GS>(x, xh, n, k, tile, nb, par, side_cap, bk, ctrl, cum_tab, side, cval, cidx, oa, sm,
-                             spilled, nchunk, nsb, kOneLcpb);
-    return;
-  } else {
 
   // ---- end of tile: bucket suffix counts and the chunks' candidate prefix;
   // then the LDS pairs leave in one burst and the maybe keys are counting-sorted
@@ -1278,7 +1169,6 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       // ranges; the pairs spilled during the stream are only binned here
       for (uint32_t j = lc + h; j < cnt; j += 32) to_side(__float_as_uint(ov[j]), oi[j]);
     }
-    STAMP(22000 + b, 1);
     if (sort_lds) {
       __syncthreads();
       for (uint32_t i = (uint32_t)tid; i < hsum; i += kK2Threads) sd[i] = skeys[i];
@@ -1286,7 +1176,6 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   }
   WSTAMP(32000 + b * 8 + 4 + (w >> 2), w & 3);
   STAMP(1024 + b, 3);
-  }
 }
 
 // ----------------------------------------------------------------------------
@@ -1454,6 +1343,10 @@ static_assert(kEmitRows * (kK4Threads / 64) == 128, "batch_ranks: wave 0 scans 2
 // behind which one lane adds to the counter; the consumer polls that counter.
 // No release fence: a buffer_wbl2 writes back the whole XCD L2 and cost
 // 10-30 us per tile in the middle of everyone else's stream (measured).
+CHOCO_DEV void st_sc1(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+CHOCO_DEV uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 
 // every wave's stores drained, the workgroup joined, one lane adds
@@ -1600,7 +1493,7 @@ CHOCO_DEV void fallback_window(WideCtrl* W, int64_t n, int64_t k, ExactSmem& es,
 }
 
 template <int MODE, bool XH>
-CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
+CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uint32_t tile, uint32_t nb, const Fold& fold,
                              float scale, WideCtrl* W, uint32_t* __restrict__ gcnt, float* __restrict__ out_val,
                              int32_t* __restrict__ out_idx, int64_t idx_base, ExactSmem& es, uint32_t* s_tk,
                              uint32_t* __restrict__ status, uint32_t* __restrict__ host_status, TopkBounds* next) {
@@ -1717,6 +1610,7 @@ CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uin
             if (sel[c]) {
               out_val[pos] = vv[c] * scale;
               out_idx[pos] = (int32_t)(i0 + c + idx_base);
+              if (fold.on()) fold_apply(fold, i0 + c, vv[c] * scale);
               ++pos;
             }
           }
@@ -1824,12 +1718,13 @@ CHOCO_DEV void next_window(const uint32_t* G, uint32_t s_lo, uint32_t s_hi, uint
 
 template <int MODE, bool XH>
 __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
+    const float* x, const float* xh, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
     uint32_t side_cap, uint64_t seed, float scale, TopkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ cum_tab,
     const uint32_t* __restrict__ cntw, const uint32_t* __restrict__ side, const float* __restrict__ cval,
     const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
     int64_t idx_base, WideCtrl* __restrict__ wide, uint32_t* __restrict__ gcnt, uint32_t par,
-    uint32_t* __restrict__ status, uint32_t* __restrict__ host_status, const uint32_t* __restrict__ tinfo) {
+    uint32_t* __restrict__ status, uint32_t* __restrict__ host_status, const uint32_t* __restrict__ tinfo,
+    Fold fold) {
   __shared__ FinSmem fs;
   __shared__ ExactSmem es;
   __shared__ uint32_t s_tk;
@@ -1899,7 +1794,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     // the sample's guess was off: the exact radix select over the whole input, shared
     // by every workgroup through the ticketed queue (wide_fallback)
     Src<MODE, XH> src{x, xh, seed};
-    wide_fallback(src, n, k, tile, nb, scale, wide, gcnt, out_val, out_idx, idx_base, es, &s_tk, status,
+    wide_fallback(src, n, k, tile, nb, fold, scale, wide, gcnt, out_val, out_idx, idx_base, es, &s_tk, status,
                   host_status, MODE == kData ? &ctrl->bounds[par ^ 1u] : nullptr);
   } else {
     // ---- thread t <-> tile t: bucket-j* key count and side-list offset
@@ -2068,6 +1963,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
         if (sel[i] && out + rk[i] < ku) {  // (bounded: an inconsistent select cannot write past k)
           st_pol<CHOCO_K34_STORE>(&out_val[out + rk[i]], v[i] * scale);
           st_pol<CHOCO_K34_STORE>(&out_idx[out + rk[i]], (int32_t)((int64_t)idx[i] + idx_base));
+          if (fold.on()) fold_apply(fold, (int64_t)idx[i], v[i] * scale);
         }
       }
       out += nsel;
@@ -2101,567 +1997,6 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
 }
 
 // ----------------------------------------------------------------------------
-// One-launch path (warm calls, k small enough for every workgroup's pairs to stay
-// in LDS): the stream kernel selects and emits itself, no K34 and no boundary.
-//
-// Layout.  The buffer is cut into blocks of `tile` = 32768 elements; workgroup b
-// streams blocks b, b + nb, b + 2 nb, ... (strided: every workgroup's bytes come
-// from every address range -- measured in tools/probe_floor.hip: contiguous
-// 1.5 MB tiles end their streams up to ~10 us apart because some address ranges
-// read slower, strided blocks end within ~4 us).  Output order stays ascending
-// index: blocks are ordered by per-block offsets.
-//   * at its tile end every workgroup publishes, per block, the bucket suffix row
-//     (cum_tab) and the block's maybe keys counting-sorted by bucket (side list),
-//     both write-through (sc1), adds the sum of its rows into G, and draws an
-//     arrival ticket (one device-scope add, after every wave's stores drained);
-//   * the LAST workgroup to arrive selects: G -> bucket j*, every block's bucket-j*
-//     keys -> LDS (16-bit offsets in the bucket) -> radix select of T and the tie
-//     quota r, then every block's (#key > T, #key == T) -> its output offset and the
-//     ties it takes: one 16-byte record per block {offset, T, ties, epoch} (a
-//     write-through granule: the record is its own flag);
-//   * every other workgroup polls the records of its blocks and emits its pairs
-//     in ascending index order straight from LDS -- the candidates never go to HBM
-//     and nothing is read twice.
-// All workgroups are resident when the last one arrives (each one has streamed its
-// blocks by then), so the waits cannot deadlock; they are still bounded (a wait
-// that gives up raises the status word).  A failed select (window missed, bucket
-// too large, side list overflow, degenerate sample) publishes kOneFallback: the
-// whole grid then runs the ticketed exact fallback (wide_fallback) as K34 would.
-// ----------------------------------------------------------------------------
-constexpr uint32_t kOneFallback = 0xFFFFFFFFu;
-constexpr uint32_t kOneTimeout = 0xFFFFFFFEu;
-constexpr int kOneMCap = 16384;  // bucket-j* keys selected in LDS as 16-bit offsets (the dead entry ring: 32 KB)
-#ifndef CHOCO_ONE_POLL_BUDGET  // diagnostic builds only
-#define CHOCO_ONE_POLL_BUDGET (1u << 22)
-#endif
-// LDS words (in the entry ring's index half, dead after the stream) of the per-block
-// emission parameters: offset, ties to take, ties / selected before the block
-constexpr int kOneBout = 1024, kOneBtake = 1040, kOneBE = 1056, kOneBS = 1072, kOneBstart = 1088;
-
-// Exclusive scan inside each 256-thread group (4 waves) of the 1024-thread workgroup;
-// *total = the group's sum.  Two barriers.
-CHOCO_DEV uint32_t group256_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
-  const int l = lane_id();
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g0 = w & ~3;
-  const uint32_t inc = wave_incl_scan(v);
-  if (l == 63) scratch[w] = inc;
-  __syncthreads();
-  uint32_t base = 0, tot = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t s = scratch[g0 + q];
-    base += g0 + q < w ? s : 0u;
-    tot += s;
-  }
-  *total = tot;
-  __syncthreads();
-  return base + inc - v;
-}
-
-// The workgroup's tile end on the one-launch path; returns `spilled` (some wave's LDS
-// region overflowed: the tile's pairs are then in the chunks' global slots).
-template <int MODE>
-CHOCO_DEV bool one_tile_end(StreamSmemOne& sm, TopkCtrl* __restrict__ ctrl, uint32_t par,
-                            uint32_t* __restrict__ cum_tab, uint32_t* __restrict__ side, uint32_t cap_b, uint32_t nb,
-                            uint32_t b, uint32_t nsb, uint32_t nchunk, uint32_t tile, uint32_t lcpb,
-                            const Buckets& bk, float* __restrict__ cval, uint32_t* __restrict__ cidx, uint32_t nblk) {
-  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  // 1. the chunks' candidate prefix (block-major = ascending index per block) and the spill check
-  {
-    const uint32_t c = (uint32_t)tid;
-    const uint32_t cc = c < nchunk ? sm.ccnt[c] : 0u;
-    const bool sp = c < nchunk && cc != (sm.cmeta[c] >> 16);
-    if (ballot(sp) != 0ull && lane == 0) atomicOr(&sm.spill, 1u);
-    uint32_t csum;
-    const uint32_t cpre = block_excl_scan(cc, sm.scratch, &csum);
-    if (c < nchunk) sm.ccnt[c] = cpre;
-    if (c == 0) sm.ccnt[nchunk] = csum;
-    if (c < kNBucket) sm.gacc[c] = 0u;
-  }
-  __syncthreads();
-  const bool spilled = sm.spill != 0u;
-  // 2. per block (4 at a time, a 256-thread group each): bucket suffix counts -> the
-  //    block's cum row (write-through), counting-sort cursors, its share of G
-  for (uint32_t l0 = 0; l0 < nsb; l0 += 4) {  // workgroup-uniform
-    const uint32_t l = l0 + ((uint32_t)tid >> 8), jt = (uint32_t)tid & 255u;
-    const bool on = l < nsb;
-    const uint32_t jb = jt < (uint32_t)kNMaybe ? (uint32_t)kNMaybe - 1u - jt : (uint32_t)kNMaybe;
-    const uint32_t hv = on && jt < (uint32_t)kNMaybe ? sm.hist[l * kNBucket + jb] : 0u;
-    uint32_t hsum;
-    const uint32_t above = group256_excl_scan(hv, sm.scratch, &hsum);  // maybe keys in buckets > jb
-    if (on) {
-      const uint32_t cs = sm.ccnt[min((l + 1u) << lcpb, nchunk)] - sm.ccnt[l << lcpb];
-      const uint32_t sure = cs - hsum;
-      const uint32_t cum = jt < (uint32_t)kNMaybe ? sure + above + hv : sure;
-      st_sc1(&cum_tab[(int64_t)one_block(b, l, nb, nblk) * kNBucket + jb], cum);  // read by the last workgroup
-      atomicAdd(&sm.gacc[jb], cum);
-      if (jt < (uint32_t)kNMaybe) sm.hist[l * kNBucket + jb] = above;  // counting-sort cursor
-      if (jt == 0 && hsum > cap_b) atomicOr(&ctrl->overflow[par], 1u);
-    }
-  }
-  __syncthreads();
-  if (tid < kNBucket) atomicAdd(&ctrl->G[par][b & (kNRep - 1)][tid], sm.gacc[tid]);
-  // 3. the maybe keys -> their block's side list (write-through); the position map
-  //    (or, a tile that spilled: every pair to its chunk's global slots)
-  const uint32_t h = (uint32_t)lane & 31u;
-  for (uint32_t c0 = 2u * w; c0 < nchunk; c0 += 2u * kK2Waves) {
-    const uint32_t cc = c0 + ((uint32_t)lane >> 5);
-    const bool have = cc < nchunk;
-    const uint32_t l = cc >> lcpb;
-    const uint32_t meta = have ? sm.cmeta[cc] : 0u;
-    const uint32_t cp = have ? sm.ccnt[cc] : 0u, cnt = have ? sm.ccnt[cc + 1] - cp : 0u;
-    const uint32_t ls = meta & 0xFFFFu, lc = meta >> 16;
-    const uint32_t blk = have ? one_block(b, l, nb, nblk) : 0u;
-    const int64_t o = (int64_t)blk * tile + (int64_t)(cc & ((1u << lcpb) - 1u)) * kChunk;
-    float* __restrict__ ov = cval + o;
-    uint32_t* __restrict__ oi = cidx + o;
-    uint32_t* __restrict__ sd = side + (int64_t)blk * cap_b;
-    auto to_side = [&](uint32_t vb) {
-      const uint32_t key = vb & 0x7fffffffu;
-      if (key < bk.s_hi) {  // every candidate has key >= s_lo
-        const uint32_t p = atomicAdd(&sm.hist[l * kNBucket + ((key - bk.s_lo) >> bk.shift)], 1u);
-        if (p < cap_b) st_sc1(&sd[p], key);
-      }
-    };
-    for (uint32_t j = h; j < lc; j += 32) {
-      const uint2 pr = sm.u.pairs[ls + j];
-      if (spilled) {
-        ov[j] = __uint_as_float(pr.x);
-        oi[j] = pr.y;
-      } else if (cp + j < (uint32_t)kPmapCap) {
-        sm.pmap[cp + j] = (uint16_t)(ls + j);  // candidate cp + j of the workgroup (block-major, ascending)
-      }
-      to_side(pr.x);
-    }
-    for (uint32_t j = lc + h; j < cnt; j += 32) to_side(__float_as_uint(ov[j]));  // spilled during the stream
-  }
-  return spilled;
-}
-
-// Emission through the position map (the usual case: no spill, <= kPmapCap candidates,
-// one batch): K34's batch emission reading the pairs from LDS -- row i, thread t <->
-// position i * 1024 + t; block l of a position by binary search over the block starts;
-// ranks by ballot + one scan of the (row, wave) counts, offsets per block.
-template <int MODE>
-CHOCO_DEV void one_emit_map(uint32_t T, uint32_t tot, uint32_t nsb, bool any_take, const OneArgs& oa,
-                            StreamSmemOne& sm) {
-  static_assert(kPmapCap <= kK2Threads * kEmitRows, "one emission batch");
-  const int tid = threadIdx.x;
-  uint32_t* words = sm.ent_i[0];
-  uint32_t* cnt0 = words;
-  uint32_t* cnt1 = words + 160;
-  const uint32_t* bout = words + kOneBout;
-  const uint32_t* btake = words + kOneBtake;
-  uint32_t* bE = words + kOneBE;
-  uint32_t* bS = words + kOneBS;
-  const uint32_t* bstart = words + kOneBstart;  // [nsb + 1]
-  uint32_t vb[kEmitRows], ix[kEmitRows], bl[kEmitRows];
-  bool gtv[kEmitRows], eqv[kEmitRows], first[kEmitRows];
-#pragma unroll
-  for (int i = 0; i < kEmitRows; ++i) {
-    const uint32_t p = (uint32_t)(i * kK2Threads + tid);
-    const bool valid = p < tot;
-    const uint2 pr = sm.u.pairs[valid ? sm.pmap[p] : 0];
-    vb[i] = pr.x;
-    ix[i] = pr.y;
-    uint32_t lo = 0, hi = nsb - 1;  // the last block whose start is <= p
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1) >> 1;
-      if (bstart[mid] <= p) lo = mid; else hi = mid - 1;
-    }
-    bl[i] = lo;
-    first[i] = valid && bstart[lo] == p;
-    const uint32_t key = pr.x & 0x7fffffffu;
-    gtv[i] = valid && key > T;
-    eqv[i] = valid && key == T;
-  }
-  bool sel[kEmitRows];
-  uint32_t rk[kEmitRows];
-  if (any_take) {  // workgroup-uniform: some block takes ties at T (lowest index first)
-    batch_ranks(eqv, rk, cnt0);
-#pragma unroll
-    for (int i = 0; i < kEmitRows; ++i)
-      if (first[i]) bE[bl[i]] = rk[i];  // ties before the block
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kEmitRows; ++i) sel[i] = gtv[i] || (eqv[i] && rk[i] - bE[bl[i]] < btake[bl[i]]);
-  } else {
-#pragma unroll
-    for (int i = 0; i < kEmitRows; ++i) sel[i] = gtv[i];
-  }
-  batch_ranks(sel, rk, cnt1);
-#pragma unroll
-  for (int i = 0; i < kEmitRows; ++i)
-    if (first[i]) bS[bl[i]] = rk[i];  // selected before the block
-  __syncthreads();
-  STAMP(28000 + blockIdx.x, 1);
-#pragma unroll
-  for (int i = 0; i < kEmitRows; ++i) {
-    if (sel[i]) {
-      const uint32_t pos = bout[bl[i]] + rk[i] - bS[bl[i]];
-      oa.out_val[pos] = __uint_as_float(vb[i]) * oa.scale;
-      oa.out_idx[pos] = (int32_t)((int64_t)ix[i] + oa.idx_base);
-    }
-  }
-}
-
-// Emission walking the chunks (a tile that spilled, or more than kPmapCap candidates):
-// candidates from LDS (cmeta runs) or the chunks' global slots; a wave per chunk.
-template <int MODE>
-CHOCO_DEV void one_emit_chunks(uint32_t T, uint32_t nchunk, uint32_t lcpb, uint32_t b, uint32_t nb, uint32_t tile, int64_t n,
-                               bool spilled, const float* __restrict__ cval, const uint32_t* __restrict__ cidx,
-                               const OneArgs& oa, StreamSmemOne& sm) {
-  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  uint32_t* words = sm.ent_i[0];
-  const uint32_t* bout = words + kOneBout;
-  const uint32_t* btake = words + kOneBtake;
-  uint32_t* bE = words + kOneBE;
-  uint32_t* bS = words + kOneBS;
-  uint32_t* cg = reinterpret_cast<uint32_t*>(&sm.ent_v[0][0]);  // per chunk: #gt, then output base
-  uint32_t* ce = cg + kOneMaxChunks;                              // per chunk: #eq, then ties before it (in block)
-  auto fetch = [&](uint32_t c, uint32_t j, uint32_t& vb, uint32_t& ix) {
-    if (!spilled) {
-      const uint2 pr = sm.u.pairs[(sm.cmeta[c] & 0xFFFFu) + j];
-      vb = pr.x;
-      ix = pr.y;
-    } else {
-      const int64_t o = (int64_t)one_block(b, c >> lcpb, nb, (uint32_t)((n + tile - 1) / tile)) * tile +
-                        (int64_t)(c & ((1u << lcpb) - 1u)) * kChunk + j;
-      vb = ld_sc1(reinterpret_cast<const uint32_t*>(cval) + o);
-      ix = ld_sc1(cidx + o);
-    }
-  };
-  for (uint32_t c = (uint32_t)w; c < nchunk; c += kK2Waves) {
-    const uint32_t cnt = sm.ccnt[c + 1] - sm.ccnt[c];
-    uint32_t gt = 0, eq = 0;
-    for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
-      const uint32_t j = j0 + (uint32_t)lane;
-      uint32_t vb = 0, ix = 0;
-      if (j < cnt) fetch(c, j, vb, ix);
-      const uint32_t key = vb & 0x7fffffffu;
-      gt += (uint32_t)__popcll(ballot(j < cnt && key > T));
-      eq += (uint32_t)__popcll(ballot(j < cnt && key == T));
-    }
-    if (lane == 0) { cg[c] = gt; ce[c] = eq; }
-  }
-  __syncthreads();
-  {
-    const uint32_t c = (uint32_t)tid;  // nchunk <= kOneMaxChunks <= kK2Threads: a chunk per thread
-    const bool on = c < nchunk;
-    const uint32_t l = c >> lcpb;
-    const bool bfirst = on && (c & ((1u << lcpb) - 1u)) == 0u;
-    const uint32_t gv = on ? cg[c] : 0u, ev = on ? ce[c] : 0u;
-    uint32_t gp, ep, gtot, etot;
-    block_excl_scan2(gv, ev, sm.scratch, &gp, &ep, &gtot, &etot);
-    if (bfirst) bE[l] = ep;
-    __syncthreads();
-    const uint32_t epb = on ? ep - bE[l] : 0u;  // ties before the chunk, in its block
-    const uint32_t tk = on ? min(ev, btake[l] > epb ? btake[l] - epb : 0u) : 0u;
-    uint32_t stot;
-    const uint32_t sp = block_excl_scan(gv + tk, sm.scratch, &stot);
-    if (bfirst) bS[l] = sp;
-    __syncthreads();
-    if (on) {
-      cg[c] = bout[l] + sp - bS[l];
-      ce[c] = epb;
-    }
-  }
-  __syncthreads();
-  for (uint32_t c = (uint32_t)w; c < nchunk; c += kK2Waves) {
-    const uint32_t cnt = sm.ccnt[c + 1] - sm.ccnt[c];
-    const uint32_t take = btake[c >> lcpb];
-    uint32_t base = cg[c], eqb = ce[c];
-    for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
-      const uint32_t j = j0 + (uint32_t)lane;
-      uint32_t vb = 0, ix = 0;
-      if (j < cnt) fetch(c, j, vb, ix);
-      const uint32_t key = vb & 0x7fffffffu;
-      const bool iseq = j < cnt && key == T;
-      const uint64_t em = ballot(iseq);
-      const bool sel = (j < cnt && key > T) || (iseq && eqb + mask_prefix(em) < take);
-      const uint64_t smk = ballot(sel);
-      if (sel) {
-        const uint32_t pos = base + mask_prefix(smk);
-        oa.out_val[pos] = __uint_as_float(vb) * oa.scale;
-        oa.out_idx[pos] = (int32_t)((int64_t)ix + oa.idx_base);
-      }
-      base += (uint32_t)__popcll(smk);
-      eqb += (uint32_t)__popcll(em);
-    }
-  }
-}
-
-template <int MODE, bool XH, bool GS>
-CHOCO_DEV void one_finish(const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k,
-                          uint32_t tile, uint32_t nb, uint32_t par, uint32_t cap_b, const Buckets& bk,
-                          TopkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ cum_tab,
-                          const uint32_t* __restrict__ side, const float* __restrict__ cval,
-                          const uint32_t* __restrict__ cidx, const OneArgs& oa, StreamSmemOne& sm, bool spilled,
-                          uint32_t nchunk, uint32_t nsb, uint32_t lcpb) {
-  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  const uint32_t b = blockIdx.x;
-  const uint32_t ku = (uint32_t)k;
-  const uint32_t nblk = (uint32_t)((n + tile - 1) / tile);
-  uint32_t* words = sm.ent_i[0];
-  uint32_t* bout = words + kOneBout;
-  uint32_t* btake = words + kOneBtake;
-  // ---- arrival: every wave's write-through stores and G adds have completed
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  STAMP(24576 + b, 0);
-  if (tid == 0) sm.bc[0] = __hip_atomic_fetch_add(&ctrl->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  STAMP(24576 + b, 3);
-  // sm.bc[4]: T; sm.bc[5]: 0 ok / kOneFallback / kOneTimeout; sm.bc[6]: some block takes ties
-  constexpr int kPB = 4;  // blocks per thread in the last workgroup (nblk <= 4096)
-  const __amdgpu_buffer_rsrc_t recs = buf_rsrc(oa.rec, nb * (uint32_t)kOneMaxBlk * 16u);
-  if (sm.bc[0] == nb - 1) {
-    // ================= the last workgroup: select T, publish every block's record
-    uint32_t* Gs = sm.gacc;  // the bucket totals
-    uint16_t* keys = reinterpret_cast<uint16_t*>(&sm.ent_v[0][0]);  // bucket-j* key offsets
-    uint32_t* hist = words;  // <= 1024 digit bins (words [0, 1024))
-    if (tid < kNBucket) {
-      uint32_t g = 0;
-#pragma unroll
-      for (int r = 0; r < kNRep; ++r) g += ld_sc1(&ctrl->G[par][r][tid]);
-      Gs[tid] = g;
-    }
-    if (tid == 0) {
-      sm.bc[1] = ld_sc1(&ctrl->overflow[par]);
-      sm.bc[2] = 0u;  // j*
-      sm.bc[6] = 0u;
-      st_sc1(&ctrl->arrive, 0u);  // every workgroup has arrived: ready for the next call
-    }
-    __syncthreads();
-    bool fb = sm.bc[1] != 0u || Gs[0] < ku || Gs[kNMaybe] >= ku;
-    if (!fb && tid < kNMaybe && Gs[tid] >= ku && Gs[tid + 1] < ku) sm.bc[2] = (uint32_t)tid;
-    __syncthreads();
-    const uint32_t jstar = sm.bc[2];
-    const uint32_t M = fb ? 0u : Gs[jstar] - Gs[jstar + 1];
-    if (M > (uint32_t)kOneMCap || bk.shift > 16u) fb = true;  // workgroup-uniform
-    STAMP(26000 + b, 0);
-    uint32_t T = 0;
-    if (!fb) {
-      // thread t <-> blocks kPB t .. kPB t + kPB - 1: their bucket-j* keys (side lists,
-      // buckets stored high to low)
-      uint32_t cb[kPB], off[kPB], above[kPB], cbs = 0;
-#pragma unroll
-      for (int q = 0; q < kPB; ++q) {
-        const uint32_t blk = (uint32_t)tid * kPB + q;
-        const bool on = blk < nblk;
-        const uint32_t* row = cum_tab + (int64_t)(on ? blk : 0u) * kNBucket;
-        const uint32_t a = ld_sc1(row + jstar), c = ld_sc1(row + jstar + 1), su = ld_sc1(row + kNMaybe);
-        cb[q] = on ? a - c : 0u;
-        off[q] = c - su;
-        above[q] = on ? c : 0u;
-        cbs += cb[q];
-      }
-      uint32_t Mk;  // == M (the rows and the totals describe the same keys)
-      const uint32_t kp = block_excl_scan(cbs, sm.scratch, &Mk);
-      Mk = min(Mk, (uint32_t)kOneMCap);
-      // per block: its first key's position | its side-list offset << 15 (the per-block
-      // histograms are dead), then key j <-> thread j % 1024: its block by binary search,
-      // all loads of a thread in flight together (one round trip)
-      uint32_t* bpos = sm.hist;
-      {
-        uint32_t kq = kp;
-#pragma unroll
-        for (int q = 0; q < kPB; ++q) {
-          const uint32_t blk = (uint32_t)tid * kPB + q;
-          if (blk < nblk) bpos[blk] = min(kq, (uint32_t)kOneMCap) | (off[q] << 15);
-          kq += cb[q];
-        }
-      }
-      __syncthreads();
-      // the keys as offsets rel = key - base_j in [0, 2^shift), shift <= 16: 16 bits each
-      const uint32_t base_j = bk.s_lo + (jstar << bk.shift);
-      for (uint32_t j0 = 0; j0 < Mk; j0 += 4u * kK2Threads) {
-        uint32_t kv[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t j = j0 + (uint32_t)e * kK2Threads + (uint32_t)tid;
-          kv[e] = 0u;
-          if (j < Mk) {
-            uint32_t lo = 0, hi = nblk - 1u;  // the last block whose first key is <= j
-            while (lo < hi) {
-              const uint32_t mid = (lo + hi + 1u) >> 1;
-              if ((bpos[mid] & 0x7FFFu) <= j) lo = mid; else hi = mid - 1u;
-            }
-            const uint32_t bw = bpos[lo];
-            kv[e] = ld_sc1(side + (int64_t)lo * cap_b + (bw >> 15) + (j - (bw & 0x7FFFu)));
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t j = j0 + (uint32_t)e * kK2Threads + (uint32_t)tid;
-          if (j < Mk) keys[j] = (uint16_t)(kv[e] - base_j);
-        }
-      }
-      STAMP(26000 + b, 1);
-      // radix select inside bucket j*: <= 10 bits a round
-      uint32_t prefix = 0, krem = ku - Gs[jstar + 1];  // 1 <= krem <= M
-      int sh = (int)bk.shift;
-      __syncthreads();  // the keys are in LDS
-      while (sh > 0) {
-        const int dsh = sh > 10 ? sh - 10 : 0;
-        const uint32_t dmask = (1u << (sh - dsh)) - 1u;
-        for (int i = tid; i <= (int)dmask; i += kK2Threads) hist[i] = 0u;
-        __syncthreads();
-        for (uint32_t j = tid; j < Mk; j += kK2Threads) {
-          const uint32_t rel = keys[j];
-          if ((rel >> sh) == (prefix >> sh)) atomicAdd(&hist[(rel >> dsh) & dmask], 1u);
-        }
-        __syncthreads();
-        block_find_rank1k(hist, dmask + 1, krem, sm.scratch, sm.bc + 2);
-        prefix |= sm.bc[2] << dsh;
-        krem = sm.bc[3];
-        sh = dsh;
-      }
-      T = base_j + prefix;
-      const uint32_t r = krem;  // ties at T to take (>= 1)
-      STAMP(26000 + b, 2);
-      // per block: #keys > T (every key above bucket j* is) and #keys == T
-      uint32_t gt[kPB], eq[kPB], gts = 0, eqs = 0;
-      {
-        uint32_t kq = kp;
-#pragma unroll
-        for (int q = 0; q < kPB; ++q) {
-          gt[q] = above[q];
-          eq[q] = 0u;
-          for (uint32_t i = 0; i < cb[q]; ++i) {
-            const uint32_t rel = keys[min(kq + i, (uint32_t)kOneMCap - 1u)];
-            gt[q] += rel > prefix ? 1u : 0u;
-            eq[q] += rel == prefix ? 1u : 0u;
-          }
-          kq += cb[q];
-          gts += gt[q];
-          eqs += eq[q];
-        }
-      }
-      STAMP(27000 + b, 0);
-      uint32_t gpre, epre, gtot, etot;
-      block_excl_scan2(gts, eqs, sm.scratch, &gpre, &epre, &gtot, &etot);
-      STAMP(27000 + b, 1);
-#pragma unroll
-      for (int q = 0; q < kPB; ++q) {
-        const uint32_t blk = (uint32_t)tid * kPB + q;
-        const uint32_t taken = min(r, epre);  // ties taken by earlier blocks (lowest index first)
-        const uint32_t take = min(eq[q], r - taken);
-        if (blk < nblk) {
-          const uint4 rec = make_uint4(gpre + taken, T, take, oa.epoch);
-          const uint32_t slot = one_rec_slot(blk, nb, nblk);
-          if (slot / kOneMaxBlk == b) {  // one of this workgroup's blocks
-            bout[slot % kOneMaxBlk] = rec.x;
-            btake[slot % kOneMaxBlk] = take;
-            if (take) sm.bc[6] = 1u;
-          } else {
-            st_sc1_16(recs, slot, rec);
-          }
-        }
-        gpre += gt[q];
-        epre += eq[q];
-      }
-      if (tid == 0) { sm.bc[4] = T; sm.bc[5] = 0u; }
-    } else {
-#pragma unroll
-      for (int q = 0; q < kPB; ++q) {
-        const uint32_t blk = (uint32_t)tid * kPB + q;
-        const uint32_t slot = blk < nblk ? one_rec_slot(blk, nb, nblk) : 0u;
-        if (blk < nblk && slot / kOneMaxBlk != b) st_sc1_16(recs, slot, make_uint4(kOneFallback, 0u, 0u, oa.epoch));
-      }
-      if (tid == 0) {
-        sm.bc[5] = kOneFallback;
-        atomicAdd(&ctrl->fallbacks, 1u);
-        // why (diagnostic words in the control block's padding): overflow word, G[0], G[sure], M, j*
-        ctrl->pad0[0] = sm.bc[1];
-        ctrl->pad0[1] = Gs[0];
-        ctrl->pad0[2] = Gs[kNMaybe];
-        ctrl->pad0[3] = M;
-        ctrl->pad0[4] = jstar;
-      }
-    }
-    STAMP(26000 + b, 3);
-    // the next call's window and the cold backoff (as K34's workgroup 0 does)
-    if (!fb && w == 0) next_window(Gs, bk.s_lo, bk.s_hi, bk.shift, sm.m1024, T, n, k, &ctrl->bounds[par ^ 1u]);
-    if (tid == 0) {
-      const bool warm_call = sm.m1024 != 0u;
-      uint32_t bo = ctrl->backoff, cl = ctrl->cold_left;
-      if (warm_call && fb) {
-        bo = min(max(2u * bo, kColdMin), kColdMax);
-        cl = bo;
-      } else if (warm_call) {
-        bo = max(bo / 2u, kColdMin);
-      } else if (cl != 0u) {
-        --cl;
-      }
-      ctrl->backoff = bo;
-      ctrl->cold_left = cl;
-    }
-    __syncthreads();
-  } else {
-    // ================= every other workgroup: poll the records of its blocks (wave 0,
-    // lane l <-> its block l: one contiguous run of records)
-    if (w == 0) {
-      const bool mine = (uint32_t)lane < nsb;
-      uint4 rec = make_uint4(0u, 0u, 0u, 0u);
-      bool done = !mine;
-      for (uint32_t it = 0; it < (uint32_t)CHOCO_ONE_POLL_BUDGET; ++it) {
-        if (!done) {
-          rec = ld_sc1_16(recs, b * (uint32_t)kOneMaxBlk + (uint32_t)lane);
-          done = rec.w == oa.epoch;
-        }
-        if (ballot(!done) == 0ull) break;
-        __builtin_amdgcn_s_sleep(2);
-      }
-      const bool timeout = ballot(!done) != 0ull;
-      const bool fbk = ballot(done && mine && rec.x == kOneFallback) != 0ull;
-      if (mine) {
-        bout[lane] = rec.x;
-        btake[lane] = rec.z;
-      }
-      const bool anytake = ballot(mine && rec.z != 0u) != 0ull;
-      if (lane == 0) {
-        sm.bc[4] = rec.y;  // T (every record of a call carries it)
-        sm.bc[5] = timeout ? kOneTimeout : (fbk ? kOneFallback : 0u);
-        sm.bc[6] = anytake ? 1u : 0u;
-        if (timeout) {
-          atomicOr(oa.status, kStatusPollTimeout);
-          if (oa.host_status)
-            __hip_atomic_store(oa.host_status, kStatusPollTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
-    }
-    __syncthreads();
-  }
-  STAMP(24576 + b, 1);
-  const uint32_t T = sm.bc[4], state = sm.bc[5];
-  const bool any_take = sm.bc[6] != 0u;
-  __syncthreads();
-  if (state == kOneTimeout) return;  // (status raised: the output is invalid)
-  if (state == kOneFallback) {
-    // the exact select over the whole input, shared through the ticketed queue
-    ExactSmem& es = *reinterpret_cast<ExactSmem*>(&sm.ent_v[0][0]);
-    Src<MODE, XH> src{x, xh, 0};
-    const uint32_t wtile = (uint32_t)((n + nb - 1) / nb);
-    wide_fallback(src, n, k, wtile, nb, oa.scale, oa.wide, oa.gcnt, oa.out_val, oa.out_idx, oa.idx_base, es,
-                  sm.bc + 3, oa.status, oa.host_status, &ctrl->bounds[par ^ 1u]);
-    return;
-  }
-  const uint32_t tot = sm.ccnt[nchunk];
-  if (!spilled && tot <= (uint32_t)kPmapCap) {
-    uint32_t* bstart = words + kOneBstart;
-    if ((uint32_t)tid <= nsb) bstart[tid] = (uint32_t)tid < nsb ? sm.ccnt[(uint32_t)tid << lcpb] : tot;
-    __syncthreads();
-    STAMP(28000 + b, 0);
-    one_emit_map<MODE>(T, tot, nsb, any_take, oa, sm);
-  } else {
-    one_emit_chunks<MODE>(T, nchunk, lcpb, b, nb, tile, n, spilled, cval, cidx, oa, sm);
-  }
-  STAMP(24576 + b, 2);
-}
-
-// ----------------------------------------------------------------------------
 // host dispatch
 // ----------------------------------------------------------------------------
 size_t topk_ws_bytes(int64_t n) {
@@ -2683,22 +2018,6 @@ struct WarmEntry {
 static std::mutex g_warm_mu;
 static std::unordered_map<const void*, WarmEntry> g_warm;
 static std::atomic<bool> g_warm_on{true};
-// one-launch records are tagged with a library-wide call counter: a stale record (an
-// earlier call, any workspace at that address) never carries the current tag
-static std::atomic<uint32_t> g_epoch{0};
-static uint32_t next_epoch() {
-  uint32_t e = g_epoch.fetch_add(1, std::memory_order_relaxed) + 1u;
-  if (e == 0u) e = g_epoch.fetch_add(1, std::memory_order_relaxed) + 1u;  // 0 = a zero-filled record
-  return e;
-}
-// A/B knob (tools/build_variants.py "one1"): the one-launch path on warm calls.  Off: measured
-// 98-102 us against K2 + K34 = 83 us (profiles/r04_one_launch_stamps.txt).
-#ifndef CHOCO_ONE
-#define CHOCO_ONE 0
-#endif
-// The one-launch path keeps every workgroup's candidates in LDS (640 pairs per wave): taken when a
-// workgroup's share of k is at most 4096 (a sampled window holds ~1.7x k: ~440 per wave).
-constexpr int64_t kOneMaxTileK = 4096;
 
 struct WarmClaim {
   uint32_t par;
@@ -2729,14 +2048,22 @@ static WarmClaim warm_claim(const void* ws, int64_t n, int64_t k, bool data) {
 template <int MODE, bool XH, bool GS = false>
 static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                        float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes,
-                       hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}, StatusSink status = StatusSink{nullptr, nullptr}) {
+                       hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}, StatusSink status = StatusSink{nullptr, nullptr},
+                       Fold fold = Fold{nullptr, nullptr, 0.f}) {
+  // the one-workgroup / copy paths emit without a fold: the self message is then applied
+  // by the accumulate kernel after them (same arithmetic)
+  auto fold_after = [&]() -> int {
+    if (!fold.on()) return CHOCO_OK;
+    if (fold.mem) return choco_sparse_accumulate(out_val, out_idx, k, fold.hat, fold.mem, n, fold.w, nullptr, st);
+    return choco_sparse_accumulate(out_val, out_idx, k, nullptr, fold.hat, n, 1.0f, nullptr, st);
+  };
   if (k >= n) {
     const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
     profile_begin("topk_all", st);
     CHOCO_KLAUNCH((topk_all_kernel<XH>), dim3(g), dim3(256), 0, st, x, xh, n, scale, out_val, out_idx, idx_base);
     profile_end("topk_all", st);
     CHOCO_LAUNCHED("topk_all_kernel");
-    return CHOCO_OK;
+    return fold_after();
   }
   if (n <= kSmallN) {
     profile_begin("topk_exact", st);
@@ -2744,7 +2071,7 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
                        seed, scale, out_val, out_idx, idx_base);
     profile_end("topk_exact", st);
     CHOCO_LAUNCHED("topk_exact_kernel");
-    return CHOCO_OK;
+    return fold_after();
   }
   const TopkLayout L = topk_layout(n);
   CHOCO_REQUIRE(ws != nullptr && ws_bytes >= L.total, "top-k workspace too small: need %zu bytes, got %zu",
@@ -2784,39 +2111,18 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
     profile_end("topk_bounds", st);
     CHOCO_LAUNCHED("topk_bounds_kernel");
   }
-  // one launch: >= 2 workgroups, <= 16 blocks each, and a workgroup's share of k small
-  // enough for its pairs to stay in LDS
-  const uint32_t one_nsb = (L.one_nblk + L.one_nb - 1) / L.one_nb;
-  const bool one = CHOCO_ONE && MODE == kData && wc.warm && L.one_nb > 1 && one_nsb <= (uint32_t)kOneMaxBlk &&
-                   (double)k * (double)one_nsb * kOneBlock / (double)n <= (double)kOneMaxTileK;
-  if constexpr (MODE == kData && kChunk == 256 * kK2Unroll) {  // (the one-launch stream: one-batch chunks)
-    if (one) {
-      // the stream kernel selects and emits itself (one_finish): no K34, no boundary
-      const OneArgs oa{reinterpret_cast<uint4*>(base + L.off_rec), next_epoch(), out_val, out_idx, idx_base, scale,
-                       reinterpret_cast<WideCtrl*>(base + L.off_wide), reinterpret_cast<uint32_t*>(base + L.off_gcnt),
-                       status.dev, status.host};
-      profile_begin("topk_stream", st);
-      CHOCO_KLAUNCH((topk_stream_kernel<kData, XH, GS, true>), dim3(L.one_nb), dim3(kK2Threads), 0, st, x, xh, n,
-                    k, (uint32_t)kOneBlock, L.one_nb, par, (uint32_t)kOneSideCap, seed, hs_lo, hs_hi, ctrl, cum, cntw,
-                    side, cval, cidx,
-                    reinterpret_cast<uint32_t*>(base + L.off_tinfo), gs, sample_ranks(n, k), 1u, oa);
-      profile_end("topk_stream", st);
-      CHOCO_LAUNCHED("topk_stream_kernel");
-      return CHOCO_OK;
-    }
-  }
   profile_begin("topk_stream", st);
   CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH, GS>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, k, L.tile, L.nb,
                 par, L.side_cap, seed, hs_lo, hs_hi, ctrl, cum, cntw, side, cval, cidx,
                 reinterpret_cast<uint32_t*>(base + L.off_tinfo), gs, sample_ranks(n, k),
-                (uint32_t)(MODE == kData && wc.warm ? 1 : 0), OneArgs{});
+                (uint32_t)(MODE == kData && wc.warm ? 1 : 0));
   profile_end("topk_stream", st);
   CHOCO_LAUNCHED("topk_stream_kernel");
   profile_begin("topk_finish", st);
   CHOCO_KLAUNCH((topk_finish_kernel<MODE, XH>), dim3(L.nb), dim3(kK4Threads), 0, st, x, xh, n, k, L.tile, L.nb,
                 L.side_cap, seed, scale, ctrl, cum, cntw, side, cval, cidx, out_val, out_idx, idx_base,
                 reinterpret_cast<WideCtrl*>(base + L.off_wide), reinterpret_cast<uint32_t*>(base + L.off_gcnt), par,
-                status.dev, status.host, reinterpret_cast<const uint32_t*>(base + L.off_tinfo));
+                status.dev, status.host, reinterpret_cast<const uint32_t*>(base + L.off_tinfo), fold);
   profile_end("topk_finish", st);
   CHOCO_LAUNCHED("topk_finish_kernel");
   return CHOCO_OK;
@@ -2825,7 +2131,8 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
 template <int MODE>
 static int dispatch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                          float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes,
-                         hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}, StatusSink status = StatusSink{nullptr, nullptr}) {
+                         hipStream_t st, Gossip gs = Gossip{nullptr, 0.f}, StatusSink status = StatusSink{nullptr, nullptr},
+                         Fold fold = Fold{nullptr, nullptr, 0.f}) {
   CHOCO_REQUIRE(x != nullptr && out_val != nullptr && out_idx != nullptr, "null pointer argument");
   CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n must be in [1, 2^31-1), got %lld", (long long)n);
   CHOCO_REQUIRE(k >= 1 && k <= n, "k must be in [1, n], got k=%lld n=%lld", (long long)k, (long long)n);
@@ -2834,7 +2141,7 @@ static int dispatch_topk(const float* x, const float* xh, int64_t n, int64_t k, 
     CHOCO_REQUIRE(xh != nullptr && aligned4(gs.mem), "the gossip step needs x_hat and a 4-byte aligned memory");
     if (MODE == kData && k < n && n > kSmallN)
       return launch_topk<kData, true, true>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st,
-                                            gs, status);
+                                            gs, status, fold);
     // no full stream pass to fuse into (random-k gathers k elements; small n and
     // k == n are one-workgroup / copy paths): the standalone step, then the codec
     const int rc = gossip_launch(const_cast<float*>(x), gs.mem, xh, gs.gamma, n, st);
@@ -2842,9 +2149,9 @@ static int dispatch_topk(const float* x, const float* xh, int64_t n, int64_t k, 
   }
   if (xh)
     return launch_topk<MODE, true>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st,
-                                   Gossip{nullptr, 0.f}, status);
+                                   Gossip{nullptr, 0.f}, status, fold);
   return launch_topk<MODE, false>(x, xh, n, k, seed, scale, out_val, out_idx, idx_base, ws, ws_bytes, st,
-                                  Gossip{nullptr, 0.f}, status);
+                                  Gossip{nullptr, 0.f}, status, fold);
 }
 
 int topk_pipeline(int mode, const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
@@ -2954,6 +2261,25 @@ CHOCO_API int choco_topk_compress(const float* x, const float* xhat, int64_t n, 
   return dispatch_topk<kData>(x, xhat, n, k, 0, 1.0f, out_val, out_idx, 0, ws, ws_bytes, as_stream(stream));
 }
 
+CHOCO_API int choco_topk_compress_accumulate(const float* x, const float* xhat, int64_t n, int64_t k,
+                                             float* out_val, int32_t* out_idx, float* hat_self, float* memory,
+                                             float weight, void* ws, size_t ws_bytes, void* stream) {
+  CHOCO_REQUIRE(hat_self != nullptr || memory != nullptr, "nothing to fold into (hat_self and memory are NULL)");
+  CHOCO_REQUIRE((hat_self == nullptr || aligned4(hat_self)) && (memory == nullptr || aligned4(memory)),
+                "hat_self / memory must be 4-byte aligned");
+  return dispatch_topk<kData>(x, xhat, n, k, 0, 1.0f, out_val, out_idx, 0, ws, ws_bytes, as_stream(stream),
+                              Gossip{nullptr, 0.f}, StatusSink{nullptr, nullptr}, Fold{hat_self, memory, weight});
+}
+
+CHOCO_API int choco_gossip_topk_compress_accumulate(float* x, float* memory, float* xhat, float gamma, int64_t n,
+                                                    int64_t k, float* out_val, int32_t* out_idx, int32_t fold_memory,
+                                                    float weight, void* ws, size_t ws_bytes, void* stream) {
+  CHOCO_REQUIRE(memory != nullptr && xhat != nullptr, "the gossip step needs memory and x_hat");
+  return dispatch_topk<kData>(x, xhat, n, k, 0, 1.0f, out_val, out_idx, 0, ws, ws_bytes, as_stream(stream),
+                              Gossip{memory, gamma}, StatusSink{nullptr, nullptr},
+                              Fold{xhat, fold_memory ? memory : nullptr, weight});
+}
+
 CHOCO_API int choco_gossip_topk_compress(float* x, const float* memory, const float* xhat, float gamma, int64_t n,
                                          int64_t k, float* out_val, int32_t* out_idx, void* ws, size_t ws_bytes,
                                          void* stream) {
@@ -2993,7 +2319,7 @@ CHOCO_API int choco_dbg_stream_only(const float* x, int64_t n, int64_t k, void* 
                        reinterpret_cast<uint32_t*>(base + L.off_cntw), reinterpret_cast<uint32_t*>(base + L.off_side),
                        reinterpret_cast<float*>(base + L.off_cval), reinterpret_cast<uint32_t*>(base + L.off_cidx),
                        reinterpret_cast<uint32_t*>(base + L.off_tinfo), Gossip{nullptr, 0.f}, SampleRanks{0u, 0u, 0u},
-                       0u, OneArgs{});
+                       0u);
   CHOCO_HIP(hipEventRecord(b, st));
   CHOCO_HIP(hipEventSynchronize(b));
   float ms = 0.f;

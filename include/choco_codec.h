@@ -96,6 +96,23 @@ int choco_topk_compress(const float* x, const float* xhat, int64_t n, int64_t k,
                         float* out_val, int32_t* out_idx,
                         void* ws, size_t ws_bytes, void* stream);
 
+/* choco_topk_compress followed by the SELF message's part of
+ * CHOCOSparsificationCompressor.uncompress (parallel_choco_v.py:307-310), folded into
+ * the emission of the message (no second launch, no re-read of the message):
+ *   if hat_self != NULL:  hat_self[idx] += val
+ *   if memory   != NULL:  memory[idx]   += (float)weight * val
+ * with the arithmetic of choco_sparse_accumulate (at least one target non-NULL).
+ * hat_self may be xhat itself (the CHOCO case): it is written only after this call's
+ * last read of it.  The reference applies the messages to memory in ascending rank
+ * order (topology.py:161-162 get_neighborhood), so memory may be folded bit-identically
+ * only when the self rank comes first among the neighbours (rank 0 of a ring, or a
+ * single worker); pass memory = NULL otherwise and apply the self message to memory
+ * with choco_sparse_accumulate in its turn. */
+int choco_topk_compress_accumulate(const float* x, const float* xhat, int64_t n, int64_t k,
+                                   float* out_val, int32_t* out_idx, float* hat_self, float* memory,
+                                   float weight,
+                                   void* ws, size_t ws_bytes, void* stream);
+
 /* Per-segment top-k (one tensor per segment, as the reference loops over
  * parameter tensors): k_s = choco_topk_k(len_s, ratio), outputs concatenated in
  * segment order, indices GLOBAL (segment offset added in integer arithmetic --
@@ -352,6 +369,13 @@ int choco_gossip_step(float* x, const float* memory, const float* xhat, float ga
 int choco_gossip_topk_compress(float* x, const float* memory, const float* xhat, float gamma,
                                int64_t n, int64_t k, float* out_val, int32_t* out_idx,
                                void* ws, size_t ws_bytes, void* stream);
+/* The fused step + top-k + self-message fold: xhat[idx] += val, and memory[idx] +=
+ * (float)weight * val when fold_memory != 0 (the ordering rule of
+ * choco_topk_compress_accumulate). */
+int choco_gossip_topk_compress_accumulate(float* x, float* memory, float* xhat, float gamma,
+                                          int64_t n, int64_t k, float* out_val, int32_t* out_idx,
+                                          int32_t fold_memory, float weight,
+                                          void* ws, size_t ws_bytes, void* stream);
 int choco_gossip_topk_compress_segmented(float* x, const float* memory, const float* xhat, float gamma,
                                          const int64_t* plan_dev, const int64_t* plan_host, int32_t nseg,
                                          float* out_val, int32_t* out_idx,

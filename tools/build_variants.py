@@ -56,9 +56,10 @@ VARIANTS = {
     "k2t1024": ["CHOCO_K2_TARGET=1024"],
     # every bounded wait of the exact fallback gives up at once: tools/status_probe.py
     "poll1": ["CHOCO_POLL_BUDGET=1"],
-    "one1": ["CHOCO_ONE=1"],
-    "one1_rot0": ["CHOCO_ONE=1", "CHOCO_ONE_ROT=0"],
-    "stamps_one1": ["CHOCO_STAMPS=1", "CHOCO_ONE=1"],
+    "qq_loop0": ["CHOCO_QQ_LOOP=0"],
+    "qq_g512": ["CHOCO_QQ_GRID=512"],
+    "qq_g2048": ["CHOCO_QQ_GRID=2048"],
+    "qcheck0": ["CHOCO_QCHECK=0"],
 }
 
 
