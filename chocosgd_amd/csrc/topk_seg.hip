@@ -370,29 +370,43 @@ CHOCO_DEV void seg_exact_tile(const float (&v)[kSegRows][4], const TileCtx& c, u
 // step happens here (the one read).
 // (8 waves per SIMD: <= 64 VGPRs; 2 x 1024 or 4 x 512 threads per CU.  Fewer
 // workgroups per CU measured ~10 us slower at ResNet-50)
-template <bool XH, bool WARM, bool GS = false>
+// LOOP (warm, no gossip step): a grid of resident
+// workgroups (kSegLoopGrid, one per CU) walks the tiles b, b + G, ..., each issuing the
+// NEXT tile's loads before the current tile's histogram, scans and stores, so a CU's
+// loads and processing overlap instead of alternating round by round (r04 counters on the
+// one-tile-per-workgroup W2: waves waited 54 % of their cycles, VALU issue ~28-34 %).
+#ifndef CHOCO_SEG_LOOP  // A/B knob
+#define CHOCO_SEG_LOOP 1
+#endif
+#ifndef CHOCO_SEG_LOOP_WPE  // its VGPR budget: 4 waves per SIMD (128 VGPRs: the prefetch does not fit 64)
+#define CHOCO_SEG_LOOP_WPE 4
+#endif
+#ifndef CHOCO_SEG_LOOP_GRID  // one 16-wave workgroup per CU at 4 waves per SIMD
+#define CHOCO_SEG_LOOP_GRID (CHOCO_SEG_LOOP_WPE >= 8 ? 512 : 256)
+#endif
+constexpr int64_t kSegLoopGrid = CHOCO_SEG_LOOP_GRID;
+template <bool XH, bool WARM, bool GS = false, bool LOOP = false>
 #ifndef CHOCO_SEG_WARM_NT  // 1: W2's one read of the delta uses non-temporal loads
 #define CHOCO_SEG_WARM_NT 1
 #endif
 #ifndef CHOCO_SEG_WPE  // waves per SIMD the collect kernel is compiled for (VGPR budget 512 / WPE)
 #define CHOCO_SEG_WPE (kSegThreads == 1024 ? 8 : 6)
 #endif
-__global__ __launch_bounds__(kSegThreads, CHOCO_SEG_WPE) void seg_collect_kernel(
+__global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_WPE) void seg_collect_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ plan, int nseg,
     const uint32_t* __restrict__ hist1, uint32_t* __restrict__ hist2, uint32_t* __restrict__ info,
     uint32_t* __restrict__ tilecnt, float* __restrict__ cval, uint32_t* __restrict__ cidx,
-    const SegWin* __restrict__ win, Gossip gs, float* __restrict__ out_val, int32_t* __restrict__ out_idx) {
+    const SegWin* __restrict__ win, Gossip gs, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
+    int64_t ntile) {
   static_assert(!GS || (XH && WARM), "the gossip step is fused into S2 on the warm path only (S1 on the cold)");
+  static_assert(!LOOP || (WARM && !GS), "the looping collect is the warm path without the gossip step");
   __shared__ uint32_t h2[kH];
   __shared__ uint32_t scratch[40];
   __shared__ uint32_t bc[4];
   __shared__ uint32_t rc_cnt[kSegRows * (kSegThreads / 64) + 1];
   static_assert(kSegRows * (kSegThreads / 64) == 64, "one wave scans the (row, wave) counts");
-  const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
   const int tid = threadIdx.x;
-  float v[kSegRows][4] = {};
-  if (GS) tile_load_gossip<true>(x, xh, gs, c, v);  // in flight while the floor is found
-  else tile_load<XH, WARM && CHOCO_SEG_WARM_NT>(x, xh, c, v);  // warm: the only read of the call
+  auto process = [&](const float (&v)[kSegRows][4], const TileCtx& c, int64_t tb) {
   if (c.R.ntile == 1) {  // workgroup-uniform: the whole segment is here
     seg_exact_tile(v, c, h2, scratch, bc, rc_cnt, out_val, out_idx);
     return;
@@ -468,7 +482,54 @@ __global__ __launch_bounds__(kSegThreads, CHOCO_SEG_WPE) void seg_collect_kernel
   uint32_t* __restrict__ g2 = hist2 + (int64_t)c.s * kH;
   for (int i = tid; i < kH; i += kSegThreads)
     if (h2[i]) atomicAdd(&g2[i], h2[i]);
-  if (tid == 0) tilecnt[blockIdx.x] = rc_cnt[kSegRows * kW];
+  if (tid == 0) tilecnt[tb] = rc_cnt[kSegRows * kW];
+  };
+  if constexpr (!LOOP) {
+    const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+    float v[kSegRows][4] = {};
+    if (GS) tile_load_gossip<true>(x, xh, gs, c, v);  // in flight while the floor is found
+    else tile_load<XH, WARM && CHOCO_SEG_WARM_NT>(x, xh, c, v);  // warm: the only read of the call
+    process(v, c, blockIdx.x);
+  } else {
+    // the raw loads of a tile (x, and x_hat), formed into v only when the tile is processed,
+    // so that the next tile's loads stay in flight during this tile's work
+    auto issue = [&](const TileCtx& tc, float4 (&a)[kSegRows], float4 (&h)[kSegRows]) {
+      const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x + tc.start, (uint32_t)tc.tl * 4u);
+#pragma unroll
+      for (int r = 0; r < kSegRows; ++r)
+        a[r] = ld_buf4<CHOCO_SEG_WARM_NT>(rx, (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u);
+      if constexpr (XH) {
+        const __amdgpu_buffer_rsrc_t rh = buf_rsrc(xh + tc.start, (uint32_t)tc.tl * 4u);
+#pragma unroll
+        for (int r = 0; r < kSegRows; ++r)
+          h[r] = ld_buf4<CHOCO_SEG_WARM_NT>(rh, (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u);
+      }
+    };
+    int64_t b = blockIdx.x;
+    TileCtx c = tile_ctx(plan, nseg, b);
+    float4 a[kSegRows], h[kSegRows];
+    issue(c, a, h);
+    for (;;) {
+      const int64_t bn = b + (int64_t)gridDim.x;
+      const bool more = bn < ntile;  // workgroup-uniform
+      float v[kSegRows][4];
+#pragma unroll
+      for (int r = 0; r < kSegRows; ++r) {
+        v[r][0] = a[r].x; v[r][1] = a[r].y; v[r][2] = a[r].z; v[r][3] = a[r].w;
+        if constexpr (XH) { v[r][0] -= h[r].x; v[r][1] -= h[r].y; v[r][2] -= h[r].z; v[r][3] -= h[r].w; }
+      }
+      TileCtx cn = c;
+      if (more) {
+        cn = tile_ctx(plan, nseg, bn);
+        issue(cn, a, h);  // in flight during this tile's work
+      }
+      process(v, c, b);
+      if (!more) break;
+      __syncthreads();  // the LDS histogram and scan words are reused by the next tile
+      c = cn;
+      b = bn;
+    }
+  }
 }
 
 // ---------------------------------------------------------------- S3: exact T per segment
@@ -873,11 +934,16 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
     profile_begin("topk_seg_collect", st);
     CHOCO_KLAUNCH((seg_collect_kernel<XH, false, false>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev,
                   nseg, W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.win, Gossip{nullptr, 0.f}, out_val,
-                  out_idx);
+                  out_idx, (int64_t)ntile);
+  } else if (CHOCO_SEG_LOOP && !GS && ntile > (unsigned)kSegLoopGrid) {
+    profile_begin("topk_seg_collect", st);
+    CHOCO_KLAUNCH((seg_collect_kernel<XH, true, false, true>), dim3((unsigned)kSegLoopGrid), dim3(kSegThreads), 0,
+                  st, x, xh, plan_dev, nseg, W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.win, gs, out_val,
+                  out_idx, (int64_t)ntile);
   } else {
     profile_begin("topk_seg_collect", st);
     CHOCO_KLAUNCH((seg_collect_kernel<XH, true, GS>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg,
-                  W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.win, gs, out_val, out_idx);
+                  W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.win, gs, out_val, out_idx, (int64_t)ntile);
   }
   profile_end("topk_seg_collect", st);
   CHOCO_LAUNCHED("seg_collect_kernel");

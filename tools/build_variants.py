@@ -60,6 +60,9 @@ VARIANTS = {
     "qq_g512": ["CHOCO_QQ_GRID=512"],
     "qq_g2048": ["CHOCO_QQ_GRID=2048"],
     "qcheck0": ["CHOCO_QCHECK=0"],
+    "seg_loop0": ["CHOCO_SEG_LOOP=0"],
+    "seg_loop_w8": ["CHOCO_SEG_LOOP_WPE=8"],
+    "seg_loop_g512": ["CHOCO_SEG_LOOP_GRID=512"],
 }
 
 
