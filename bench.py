@@ -644,6 +644,18 @@ def main():
                         "dominant_kernel": dom_kernel,
                         "timed_in": (f"{dom_kernel}: timed region (dispatch-attached events); the stage's other "
                                      f"kernels: untimed pass right after" if in_timed else "untimed pass")}
+        # top-k: the measured floor of a single pass that is GIVEN the k-th key (tools/probe_floor.hip)
+        if roofline and w.op == "topk" and not w.fold and not w.step_mode and dom and dom["stage"] == "compress":
+            ff = os.path.join(ROOT, "profiles", "probe_floor.json")
+            if os.path.exists(ff):
+                with open(ff) as f:
+                    fl = json.load(f).get(f"topk:{w.n}:{w.k}")
+                if fl:
+                    roofline["known_t_floor"] = {
+                        "us": fl["known_t_floor_us"], "frac_of_peak": round(dom["algorithmic_bytes"] / (
+                            fl["known_t_floor_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                        "compress_vs_floor": round(fl["known_t_floor_us"] / dom["us_per_step"], 4),
+                        "source": fl["source"]}
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,

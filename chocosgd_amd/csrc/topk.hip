@@ -874,26 +874,61 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   };
   auto batch1 = [&](uint32_t c) -> uint32_t { return batch0(c) + (uint32_t)kStep * 4u; };
 
-  // ---- prologue: the wave's first chunk is chunk w (and with one-batch chunks
-  // its second is w + 16); both batches go out at once, then the bounds K1 left
-  // in the control block are read
+#ifndef CHOCO_K2_WINDOW_FIRST  // A/B knob: 0 reads the window behind the first batch (round 3)
+#define CHOCO_K2_WINDOW_FIRST 1
+#endif
+  // ---- prologue: the window words K1 / the previous call left in the control block
+  // are read FIRST, then the wave's first chunk w (and with one-batch chunks its second,
+  // w + 16) goes out.  vmcnt retires in order: read behind the first batches (~67 MB
+  // requested GPU-wide at once), the window arrived after all of them (~10 us) and no
+  // wave could start its first chunk or refill its buffers until then.
   uint32_t c = (uint32_t)w;
   float4 A[kK2Unroll], B[kK2Unroll];
   Buckets bk;
+  TopkBounds W{};
+  uint32_t cold_left = 0, ovf_now = 0;
+  if constexpr (MODE == kData && CHOCO_K2_WINDOW_FIRST) {
+    // ONE vector load, lane i <-> word i (bounds words 0..8, cold_left, overflow): issued
+    // before the batch, waited for (by the compiler, at the first readlane) behind it.
+    // (Separate scalar loads made the batch wait for their lgkmcnt; separate vector loads
+    // got a register reused as an address of the batch, which then waited for them.)
+    static_assert(offsetof(TopkBounds, valid) == 32, "bounds words 0..8: s_lo, s_hi, shift, m1024, n, k, valid");
+    const uint32_t* bw = reinterpret_cast<const uint32_t*>(&ctrl->bounds[par]);
+    const uint32_t* wsrc = lane < 9 ? bw + lane : (lane == 9 ? &ctrl->cold_left : &ctrl->overflow[par]);
+    const uint32_t wl = __hip_atomic_load(wsrc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" ::: "memory");  // (the batch's loads stay behind the window load)
+    if (!GS) load_rows_full<XH>(ts, batch0(c), lane, A);
+    if (kTwoChunks) load_rows_full<XH>(ts, batch0(c + kK2Waves), lane, B);
+    else if (!kOneBatch && !XH) load_rows_full<XH>(ts, batch1(c), lane, B);
+    asm volatile("" ::: "memory");
+    W.s_lo = __builtin_amdgcn_readlane(wl, 0);
+    W.s_hi = __builtin_amdgcn_readlane(wl, 1);
+    W.shift = __builtin_amdgcn_readlane(wl, 2);
+    W.m1024 = __builtin_amdgcn_readlane(wl, 3);
+    W.n = (int64_t)(((uint64_t)__builtin_amdgcn_readlane(wl, 5) << 32) | __builtin_amdgcn_readlane(wl, 4));
+    W.k = (int64_t)(((uint64_t)__builtin_amdgcn_readlane(wl, 7) << 32) | __builtin_amdgcn_readlane(wl, 6));
+    W.valid = __builtin_amdgcn_readlane(wl, 8);
+    cold_left = __builtin_amdgcn_readlane(wl, 9);
+    ovf_now = __builtin_amdgcn_readlane(wl, 10);
+  } else {
+    if constexpr (MODE == kData) {
+      if (!GS) load_rows_full<XH>(ts, batch0(c), lane, A);
+      if (kTwoChunks) load_rows_full<XH>(ts, batch0(c + kK2Waves), lane, B);
+      else if (!kOneBatch && !XH) load_rows_full<XH>(ts, batch1(c), lane, B);
+      W = ctrl->bounds[par];
+      cold_left = ctrl->cold_left;
+      ovf_now = ctrl->overflow[par];
+    }
+  }
   // the NEXT call's bucket totals and overflow word start from zero (no kernel of
   // this call reads them: this call's are G[par] / overflow[par])
   for (int i = (int)b * kK2Threads + tid; i < kNRep * kNBucket; i += (int)nb * kK2Threads)
     (&ctrl->G[par ^ 1u][0][0])[i] = 0u;
   if (b == 0 && tid == 0) ctrl->overflow[par ^ 1u] = 0u;
   if constexpr (MODE == kData) {
-    if (!GS) load_rows_full<XH>(ts, batch0(c), lane, A);
-    if (kTwoChunks) load_rows_full<XH>(ts, batch0(c + kK2Waves), lane, B);
-    else if (!kOneBatch && !XH) load_rows_full<XH>(ts, batch1(c), lane, B);
     // this call's window: K1's sample (cold call), the previous call's (warm call), or --
     // when the host skipped K1 but the window is stale or a warm miss put this workspace
     // on a cold run (cold_left, set by K34) -- a sample taken here by every workgroup
-    const TopkBounds W = ctrl->bounds[par];
-    const uint32_t cold_left = ctrl->cold_left;
     bool ok = W.valid != 0u && W.n == n && W.k == k && W.shift < 32u;
     bool degenerate = false;
     if (sample_if_cold && (!ok || cold_left != 0u)) {  // grid-uniform
@@ -917,7 +952,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       }
     } else {
       bk = ok ? make_buckets_from(W.s_lo, W.s_hi, W.shift, seed) : make_buckets_from(kNoCandKey, kNoCandKey, 0u, seed);
-      degenerate = (ctrl->overflow[par] & 2u) != 0u;
+      degenerate = (ovf_now & 2u) != 0u;
     }
     // no window for this (n, k) (a workspace the host believed warm): the exact fallback
     if (!ok && b == 0 && tid == 0) atomicOr(&ctrl->overflow[par], 2u);

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Combined pass: parity of everything changed this round, then same-box A/Bs
+# (QSGD looping quantize, segmented looping W2, K2 window-first).
+cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; O=gpurun_out/r4n; mkdir -p $O
+timeout -k 10 700 python -u -m pytest tests/test_gpu_qsgd_sign.py tests/test_gpu_baseline_sizes.py tests/test_gpu_topk.py tests/test_gpu_topk_fold.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; tail -2 $O/tests.log; [ $rc -ne 0 ] && { grep -E "FAIL|Error|assert" $O/tests.log | head -30; tail -40 $O/tests.log; exit $rc; }
+summ() { python3 -c "import json,sys; d=json.load(open('$1')); r=d['roofline']; print('$2', d['value'], d['ms_per_step'], r['stage'], r['frac'], d['kernels_us'])"; }
+ab() {  # workload variant...
+  wl=$1; shift
+  for v in "$@"; do
+    L=""; [ $v != default ] && L="--lib chocosgd_amd/lib/variants/lib_$v.so"
+    timeout -k 10 120 python bench.py --workload $wl --steps 10 --warmup 4 --no-cpu-baseline --no-e2e $L > $O/${wl}_$v.json 2>$O/${wl}_$v.err || { tail -5 $O/${wl}_$v.err; exit 1; }
+    summ $O/${wl}_$v.json ${wl}_$v
+  done
+}
+for rep in 1 2; do
+  ab topk default k2wf0
+  ab topk25m default k2wf0
+  ab qsgd default qq_loop0 qq_g512 qq_g2048
+  ab topk_r50 default seg_loop0 seg_loop_g512
+done
+timeout -k 10 120 python -u tools/stamps.py > $O/stamps.txt 2>&1; echo "stamps rc=$?"; grep -v amdgpu.ids $O/stamps.txt | head -40

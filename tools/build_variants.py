@@ -61,6 +61,7 @@ VARIANTS = {
     "qq_g2048": ["CHOCO_QQ_GRID=2048"],
     "qcheck0": ["CHOCO_QCHECK=0"],
     "seg_loop0": ["CHOCO_SEG_LOOP=0"],
+    "k2wf0": ["CHOCO_K2_WINDOW_FIRST=0"],
     "seg_loop_w8": ["CHOCO_SEG_LOOP_WPE=8"],
     "seg_loop_g512": ["CHOCO_SEG_LOOP_GRID=512"],
 }
