@@ -16,6 +16,10 @@ Deliberate differences (all documented in DESIGN.md):
     include/choco_codec.h) instead of
     torch.rand_like (sparsification.py:91); norms are fp64-accumulated (the
     reference's fp32 CPU norm drifts by up to 1e-2 relative at 1e8 elements).
+  * host (CPU) tensors are accepted as the reference accepts them (BASELINE cfg 1 runs
+    the sign compressor on CPU tensors): they are staged to the current ROCm device,
+    computed there by the same kernels and the results returned on the input's device.
+    Nothing is computed on the host.
 """
 import math
 
@@ -34,14 +38,27 @@ def _draw_seed():
     return int(torch.randint(0, 2**62, (1,)).item())
 
 
+def _on_device(t):
+    """(device tensor, the device results go back to): host tensors are staged to the
+    current ROCm device (the compute never runs on the host)."""
+    if t.is_cuda:
+        return t, None
+    return t.to(torch.device("cuda", torch.cuda.current_device())), t.device
+
+
+def _home(t, home):
+    return t if home is None else t.to(home)
+
+
 class SparsificationCompressor(object):
     """top-k / random-k  (sparsification.py:17-83)."""
 
     def get_top_k(self, x, ratio):
+        x, home = _on_device(x)
         x_data = x.view(-1)
         top_k = codec.topk_k(x_data.nelement(), ratio)
         values, indices = codec.topk(x_data, top_k)
-        return values, indices.long()
+        return _home(values, home), _home(indices.long(), home)
 
     def get_mask(self, flatten_arr, indices):
         # identical torch ops to sparsification.py:33-38 (including ~ on uint8)
@@ -51,10 +68,11 @@ class SparsificationCompressor(object):
         return mask.float(), (~mask).float()
 
     def get_random_k(self, x, ratio, is_biased=True):
+        x, home = _on_device(x)
         x_data = x.view(-1)
         top_k = codec.topk_k(x_data.nelement(), ratio)
         values, indices = codec.randk(x_data, top_k, _draw_seed(), is_biased=is_biased)
-        return values, indices.long()
+        return _home(values, home), _home(indices.long(), home)
 
     def compress(self, arr, op, compress_ratio, is_biased):
         if "top_k" in op:
@@ -88,14 +106,15 @@ class QuantizationCompressor(object):
         if not codec.is_pow2_minus1(int(s)):
             raise RuntimeError(f"QSGD level count s={s} must be 2^q - 1 with 1 <= q <= 16")
         q = int(round(math.log2(int(s) + 1)))
-        x_flat = x.reshape(-1).contiguous()
+        xd, home = _on_device(x)
+        x_flat = xd.reshape(-1).contiguous()
         _, _, dense = codec.qsgd_compress(x_flat, q, is_biased=is_biased, seed=_draw_seed(), want_dense=True)
-        return dense.view_as(x)
+        return _home(dense.view_as(xd), home)
 
     def qsgd_quantize_numpy(self, x, s, is_biased=False):
         """numpy in / numpy out; computed on the current ROCm device."""
-        t = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).cuda()
-        return self.get_qsgd(t, s, is_biased).cpu().numpy()
+        t = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32))
+        return self.get_qsgd(t, s, is_biased).numpy()
 
     def compress(self, arr, op, quantize_level, is_biased):
         if quantize_level != 32:
@@ -114,23 +133,27 @@ class SignCompressor(object):
 
     def packing(self, src_tensor):
         size = src_tensor.size()
-        packed, _ = codec.sign_compress(src_tensor.reshape(-1).contiguous(), want_norms=False)
-        return packed, size
+        src, home = _on_device(src_tensor)
+        packed, _ = codec.sign_compress(src.reshape(-1).contiguous(), want_norms=False)
+        return _home(packed, home), size
 
     def unpacking(self, src_tensor, src_tensor_size):
         n = self.element_num(src_tensor_size)
-        out = codec.sign_unpack(src_tensor.int().contiguous(), n)
-        return out.view(src_tensor_size)
+        src, home = _on_device(src_tensor)
+        out = codec.sign_unpack(src.int().contiguous(), n)
+        return _home(out.view(src_tensor_size), home)
 
     def majority_vote(self, src_tensor_list):
         """Per (row, word) majority of the voters' decoded signs; a tie encodes as "+"."""
         n = 32 * src_tensor_list[0].numel()
+        home = None if src_tensor_list[0].is_cuda else src_tensor_list[0].device
         total = None
         for t in src_tensor_list:
+            t, _ = _on_device(t)
             dec = codec.sign_unpack(t.int().contiguous(), n)
             total = dec if total is None else total + dec
         packed, _ = codec.sign_compress(total, want_norms=False)
-        return packed
+        return _home(packed, home)
 
     def element_num(self, size):
         num = 1

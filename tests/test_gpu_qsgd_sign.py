@@ -74,6 +74,29 @@ def test_qsgd_device_rng_matches_oracle(q, n):
     assert np.array_equal(host(packed), O.qsgd_pack(O.qsgd_levels(host(x), s, u, nrm), host(x), q))
 
 
+def test_qsgd_looping_quantize_and_ranges():
+    """The looping quantize kernel (single-segment buffers without x_hat: 1024 resident
+    workgroups walk the tiles backward with a one-tile prefetch) at a size where every
+    workgroup takes more than one tile plus a partial tail, whole-buffer and as chunked
+    ranges (range starts aligned to 8192, the last range ending in the partial tile):
+    bit-exact against the oracle."""
+    from chocosgd_amd import codec
+    n = 8192 * 1100 + 333
+    q, seed, offset = 4, 0x2468_ACE0, 3
+    x = randn(n, 515)
+    packed, norms, dense = codec.qsgd_compress(x, q, seed=seed, offset=offset, want_dense=True)
+    u = O.qsgd_uniforms(n, seed, offset)
+    s = 2 ** q - 1
+    nrm = host(norms)[0]
+    lvl = O.qsgd_levels(host(x), s, u, nrm)
+    assert same_bits(host(dense), O.qsgd_dense(host(x), s, u, nrm))
+    assert np.array_equal(host(packed), O.qsgd_pack(lvl, host(x), q))
+    for e0, e1 in codec.qsgd_chunks(n, 3):
+        part = torch.empty(codec.qsgd_packed_bytes(e1 - e0, q), dtype=torch.uint8, device=DEV)
+        codec.qsgd_quantize_range(x, q, norms, e0, e1, part, seed=seed, offset=offset)
+        assert np.array_equal(host(part), O.qsgd_pack(lvl[e0:e1], host(x)[e0:e1], q)), (e0, e1)
+
+
 def test_qsgd_zero_segment_nan():
     from chocosgd_amd import codec
     x = torch.zeros(64, device=DEV)
@@ -297,3 +320,25 @@ def test_gossip_golden():
     x = dev(g["x"])
     codec.gossip_step(x, dev(g["mem"]), dev(g["hat"]), float(g["gamma"]))
     assert same_bits(host(x), g["out"])
+
+
+def test_primitives_accept_host_tensors():
+    """BASELINE cfg 1 runs the reference's SignCompressor on CPU tensors: the drop-in
+    primitives accept host tensors (staged to the device, computed by the same kernels)
+    and return host tensors, equal to the oracle."""
+    from chocosgd_amd.sparsification import QuantizationCompressor, SignCompressor, SparsificationCompressor
+    n = 1_000_000
+    x = torch.from_numpy(np.random.default_rng(5).standard_normal(n).astype(np.float32))
+    sc = SignCompressor()
+    packed, size = sc.compress(x)
+    assert packed.device.type == "cpu" and size == x.size()
+    assert np.array_equal(packed.numpy(), O.sign_pack(x.numpy()))
+    dec = sc.uncompress(packed, size)
+    assert dec.device.type == "cpu"
+    assert np.array_equal(dec.numpy(), np.where(x.numpy() < 0, -1.0, 1.0).astype(np.float32))
+    vals, idx = SparsificationCompressor().get_top_k(x, 0.99)
+    assert vals.device.type == "cpu" and idx.device.type == "cpu"
+    ov, oi = O.topk(x.numpy(), O.topk_k(n, 0.99))
+    assert np.array_equal(idx.numpy(), oi) and same_bits(vals.numpy(), ov)
+    out = QuantizationCompressor().compress(x[:4099].clone(), "quantize_qsgd", 4, False)
+    assert out.device.type == "cpu" and out.shape == (4099,)
