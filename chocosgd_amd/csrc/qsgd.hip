@@ -853,7 +853,7 @@ static int qsgd_norms_launch(const float* x, const float* xhat, int64_t n, const
 // at e1).
 // A/B knob: the looping quantize kernel for single-segment buffers (0: one tile per workgroup)
 #ifndef CHOCO_QQ_LOOP
-#define CHOCO_QQ_LOOP 1
+#define CHOCO_QQ_LOOP 0
 #endif
 #ifndef CHOCO_QQ_GRID  // resident workgroups of the looping kernel: 4 per CU (16 waves)
 #define CHOCO_QQ_GRID 1024

@@ -875,7 +875,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   auto batch1 = [&](uint32_t c) -> uint32_t { return batch0(c) + (uint32_t)kStep * 4u; };
 
 #ifndef CHOCO_K2_WINDOW_FIRST  // A/B knob: 0 reads the window behind the first batch (round 3)
-#define CHOCO_K2_WINDOW_FIRST 1
+#define CHOCO_K2_WINDOW_FIRST 0
 #endif
   // ---- prologue: the window words K1 / the previous call left in the control block
   // are read FIRST, then the wave's first chunk w (and with one-batch chunks its second,

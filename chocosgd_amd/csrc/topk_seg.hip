@@ -376,7 +376,7 @@ CHOCO_DEV void seg_exact_tile(const float (&v)[kSegRows][4], const TileCtx& c, u
 // loads and processing overlap instead of alternating round by round (r04 counters on the
 // one-tile-per-workgroup W2: waves waited 54 % of their cycles, VALU issue ~28-34 %).
 #ifndef CHOCO_SEG_LOOP  // A/B knob
-#define CHOCO_SEG_LOOP 1
+#define CHOCO_SEG_LOOP 0
 #endif
 #ifndef CHOCO_SEG_LOOP_WPE  // its VGPR budget: 4 waves per SIMD (128 VGPRs: the prefetch does not fit 64)
 #define CHOCO_SEG_LOOP_WPE 4

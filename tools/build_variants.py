@@ -56,14 +56,16 @@ VARIANTS = {
     "k2t1024": ["CHOCO_K2_TARGET=1024"],
     # every bounded wait of the exact fallback gives up at once: tools/status_probe.py
     "poll1": ["CHOCO_POLL_BUDGET=1"],
-    "qq_loop0": ["CHOCO_QQ_LOOP=0"],
-    "qq_g512": ["CHOCO_QQ_GRID=512"],
-    "qq_g2048": ["CHOCO_QQ_GRID=2048"],
+    "qq_loop1": ["CHOCO_QQ_LOOP=1"],
+    "qq_loop1_g512": ["CHOCO_QQ_LOOP=1", "CHOCO_QQ_GRID=512"],
+    "qq_loop1_g2048": ["CHOCO_QQ_LOOP=1", "CHOCO_QQ_GRID=2048"],
     "qcheck0": ["CHOCO_QCHECK=0"],
-    "seg_loop0": ["CHOCO_SEG_LOOP=0"],
-    "k2wf0": ["CHOCO_K2_WINDOW_FIRST=0"],
-    "seg_loop_w8": ["CHOCO_SEG_LOOP_WPE=8"],
-    "seg_loop_g512": ["CHOCO_SEG_LOOP_GRID=512"],
+    "seg_loop1": ["CHOCO_SEG_LOOP=1"],
+    "k2wf1": ["CHOCO_K2_WINDOW_FIRST=1"],
+    # the three r04 changes together (parity run before they become defaults)
+    "r04_all": ["CHOCO_QQ_LOOP=1", "CHOCO_SEG_LOOP=1", "CHOCO_K2_WINDOW_FIRST=1"],
+    "seg_loop1_g512": ["CHOCO_SEG_LOOP=1", "CHOCO_SEG_LOOP_GRID=512"],
+    "stamps_wf1": ["CHOCO_STAMPS=1", "CHOCO_K2_WINDOW_FIRST=1"],
 }
 
 
