@@ -875,7 +875,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   auto batch1 = [&](uint32_t c) -> uint32_t { return batch0(c) + (uint32_t)kStep * 4u; };
 
 #ifndef CHOCO_K2_WINDOW_FIRST  // A/B knob: 0 reads the window behind the first batch (round 3)
-#define CHOCO_K2_WINDOW_FIRST 0
+#define CHOCO_K2_WINDOW_FIRST 1
 #endif
   // ---- prologue: the window words K1 / the previous call left in the control block
   // are read FIRST, then the wave's first chunk w (and with one-batch chunks its second,
@@ -1270,6 +1270,9 @@ CHOCO_DEV uint32_t chunk_run_starts(const uint32_t (&cw)[kCPT], uint32_t nchunk,
   return tot;
 }
 
+#ifndef CHOCO_K34_WAVE_SELECT  // A/B knob (r04: 1 = one wave, bit by bit, for <= 256 keys -- measured
+#define CHOCO_K34_WAVE_SELECT 0     // slower, 2.5 against 1.3 us for the ~160 keys of a warm bucket)
+#endif
 constexpr int kEmitR = 8;  // emission batch: kEmitR rows of kK4Threads candidate positions
 constexpr int kEmitRows = kEmitR;
 constexpr int kSelBits = 13;  // radix-select digit: one round for bucket widths <= 2^13
@@ -1346,13 +1349,17 @@ CHOCO_DEV int64_t cand_addr(const uint32_t* run_start, uint32_t nchunk, uint32_t
 // Exclusive ranks, in position order, of the flagged slots of one emission
 // batch (row-major: row i, then wave, then lane); returns the batch total.
 // `cnt` is one of two alternating LDS buffers; two barriers.
-CHOCO_DEV uint32_t batch_ranks(const bool (&f)[kEmitRows], uint32_t (&rk)[kEmitRows], uint32_t* cnt) {
+CHOCO_DEV uint32_t batch_ranks(const bool (&f)[kEmitRows], uint32_t (&rk)[kEmitRows], uint32_t* cnt,
+                               uint32_t nrows = kEmitRows) {
+  // rows >= nrows (workgroup-uniform) hold no position: no ballot, a zero count.
+  // (r04 A/B: every wave scanning the counts itself after ONE barrier was slower,
+  // 1.48 against 1.03 us in K34's stamps: wave 0 scans between two barriers)
   constexpr int kW = kK4Threads / 64;
   const int lane = lane_id(), w = threadIdx.x >> 6;
   uint64_t bm[kEmitRows];
 #pragma unroll
   for (int i = 0; i < kEmitRows; ++i) {
-    bm[i] = ballot(f[i]);
+    bm[i] = (uint32_t)i < nrows ? ballot(f[i]) : 0ull;
     if (lane == 0) cnt[i * kW + w] = (uint32_t)__popcll(bm[i]);
   }
   __syncthreads();
@@ -1907,6 +1914,40 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     const uint32_t base_j = s_lo + (jstar << shift);
     uint32_t prefix = 0, krem = ku - fs.G[jstar + 1];  // 1 <= krem <= M
     int sh = (int)shift;
+    if (CHOCO_K34_WAVE_SELECT && M <= 256u && shift <= 16u) {  // workgroup-uniform: the warm path's few keys
+      // ONE wave, bit by bit from the top: the keys (4 per lane) whose bits so far match
+      // T's, counted per bit with ballots -- no histogram, no block scan (r04 stamps: the
+      // LDS histogram + block rank took ~1.3 us for the ~160 keys of a warm bucket)
+      __syncthreads();  // the bucket keys are in LDS
+      if (tid < 64) {
+        uint32_t kv[4];
+        bool act[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t j = (uint32_t)tid + 64u * q;
+          act[q] = j < M;
+          kv[q] = act[q] ? fs.keys[j] - base_j : 0u;
+        }
+        for (int bit = sh - 1; bit >= 0; --bit) {
+          uint32_t c = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) c += (uint32_t)__popcll(ballot(act[q] && ((kv[q] >> bit) & 1u)));
+          const bool one = c >= krem;  // wave-uniform
+          if (one) prefix |= 1u << bit;
+          else krem -= c;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) act[q] = act[q] && (((kv[q] >> bit) & 1u) == (one ? 1u : 0u));
+        }
+        if (tid == 0) {
+          fs.bc[5] = prefix;
+          fs.bc[6] = krem;
+        }
+      }
+      __syncthreads();
+      prefix = fs.bc[5];
+      krem = fs.bc[6];
+      sh = 0;
+    }
     while (sh > 0) {
       const int dsh = sh > kSelBits ? sh - kSelBits : 0;
       const uint32_t dmask = (1u << (sh - dsh)) - 1u;
@@ -1928,6 +1969,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
       sh = dsh;
     }
     if (shift == 0) __syncthreads();  // the bucket keys are in LDS
+    STAMP(28000 + b, 3);
     STAMP(27000 + b, 0);
     const uint32_t T = base_j + prefix;
     const uint32_t r = krem;  // ties at T to take (>= 1)
@@ -1971,6 +2013,9 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
           idx[i] = cidx[addr[i]];
         }
       }
+      // rows holding positions (workgroup-uniform): a k = 1 % tile holds ~4,000 candidates,
+      // half of the batch's 8 rows
+      const uint32_t nrows = min((uint32_t)kEmitR, (tot - p0 + kK4Threads - 1) / kK4Threads);
       bool gtv[kEmitR], eqv[kEmitR];
 #pragma unroll
       for (int i = 0; i < kEmitR; ++i) {
@@ -1979,10 +2024,11 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
         gtv[i] = valid && key > T;
         eqv[i] = valid && key == T;
       }
+      STAMP(30000 + b, 0);
       bool sel[kEmitR];
       uint32_t rk[kEmitR];
       if (mode == kTakePartial) {  // workgroup-uniform
-        const uint32_t eq_total = batch_ranks(eqv, rk, fs.ecnt[eb]);
+        const uint32_t eq_total = batch_ranks(eqv, rk, fs.ecnt[eb], nrows);
         eb ^= 1;
 #pragma unroll
         for (int i = 0; i < kEmitR; ++i) sel[i] = gtv[i] || (eqv[i] && tie_run + rk[i] < r);
@@ -1991,10 +2037,12 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
 #pragma unroll
         for (int i = 0; i < kEmitR; ++i) sel[i] = gtv[i] || (eqv[i] && mode == kTakeAll);
       }
-      const uint32_t nsel = batch_ranks(sel, rk, fs.ecnt[eb]);
+      const uint32_t nsel = batch_ranks(sel, rk, fs.ecnt[eb], nrows);
       eb ^= 1;
+      STAMP(30000 + b, 1);
 #pragma unroll
       for (int i = 0; i < kEmitR; ++i) {
+        if ((uint32_t)i >= nrows) continue;  // workgroup-uniform
         if (sel[i] && out + rk[i] < ku) {  // (bounded: an inconsistent select cannot write past k)
           st_pol<CHOCO_K34_STORE>(&out_val[out + rk[i]], v[i] * scale);
           st_pol<CHOCO_K34_STORE>(&out_idx[out + rk[i]], (int32_t)((int64_t)idx[i] + idx_base));
@@ -2003,6 +2051,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
       }
       out += nsel;
     }
+    STAMP(30000 + b, 2);
     if (MODE == kData && b == 0 && tid < 64)
       next_window(fs.G, s_lo, fs.ctl[1], shift, fs.ctl[4], T, n, k, &ctrl->bounds[par ^ 1u]);
   }

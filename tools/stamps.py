@@ -124,7 +124,13 @@ def main():
     if len(q3):
         row("  (select histogram built)", q3[:, 2]); row("  (select rank found)", q3[:, 3])
     row("  T selected", q2[:, 0])
-    row("offsets known", k4[:, 1]); row("end", k4[:, 2])
+    row("offsets known", k4[:, 1])
+    q5 = t[30000:30000 + 1000]
+    q5 = q5[q5[:, 0] > 0]
+    if len(q5):
+        row("  (emission keys compared)", q5[:, 0]); row("  (emission ranks)", q5[:, 1])
+        row("  (emission stores issued)", q5[:, 2])
+    row("end", k4[:, 2])
 
 
 if __name__ == "__main__":
