@@ -386,6 +386,12 @@ CHOCO_DEV void seg_exact_tile(const float (&v)[kSegRows][4], const TileCtx& c, u
 #endif
 constexpr int64_t kSegLoopGrid = CHOCO_SEG_LOOP_GRID;
 template <bool XH, bool WARM, bool GS = false, bool LOOP = false>
+#ifndef CHOCO_SEG_SMALL_FIRST  // A/B knob: W2 / S2 take the single-tile segments' tiles first
+#define CHOCO_SEG_SMALL_FIRST 1
+#endif
+#ifndef CHOCO_SEG_WIN_FIRST  // A/B knob: 1 reads the window before the tile loads (r04: no gain, 28.5 vs 28.0 us)
+#define CHOCO_SEG_WIN_FIRST 0
+#endif
 #ifndef CHOCO_SEG_WARM_NT  // 1: W2's one read of the delta uses non-temporal loads
 #define CHOCO_SEG_WARM_NT 1
 #endif
@@ -397,7 +403,7 @@ __global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_
     const uint32_t* __restrict__ hist1, uint32_t* __restrict__ hist2, uint32_t* __restrict__ info,
     uint32_t* __restrict__ tilecnt, float* __restrict__ cval, uint32_t* __restrict__ cidx,
     const SegWin* __restrict__ win, Gossip gs, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
-    int64_t ntile) {
+    int64_t ntile, const int64_t* __restrict__ order) {
   static_assert(!GS || (XH && WARM), "the gossip step is fused into S2 on the warm path only (S1 on the cold)");
   static_assert(!LOOP || (WARM && !GS), "the looping collect is the warm path without the gossip step");
   __shared__ uint32_t h2[kH];
@@ -406,7 +412,8 @@ __global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_
   __shared__ uint32_t rc_cnt[kSegRows * (kSegThreads / 64) + 1];
   static_assert(kSegRows * (kSegThreads / 64) == 64, "one wave scans the (row, wave) counts");
   const int tid = threadIdx.x;
-  auto process = [&](const float (&v)[kSegRows][4], const TileCtx& c, int64_t tb) {
+  // `wpre`: the segment's window, read before the tile's loads were issued (warm)
+  auto process = [&](const float (&v)[kSegRows][4], const TileCtx& c, int64_t tb, const SegWin& wpre) {
   if (c.R.ntile == 1) {  // workgroup-uniform: the whole segment is here
     seg_exact_tile(v, c, h2, scratch, bc, rc_cnt, out_val, out_idx);
     return;
@@ -414,7 +421,7 @@ __global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_
   for (int i = tid; i < kH; i += kSegThreads) h2[i] = 0u;
   uint32_t floor_key, b1 = 0, sh = 0;
   if (WARM) {
-    const SegWin w = win[c.s];
+    const SegWin w = wpre;
     // no window (never expected after a cold call): no candidates -> S3a flags the miss
     floor_key = w.valid ? w.lo : 0xFFFFFFFFu;
     sh = w.valid ? min(w.sh, kWinShMax) : 0u;
@@ -485,11 +492,34 @@ __global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_
   if (tid == 0) tilecnt[tb] = rc_cnt[kSegRows * kW];
   };
   if constexpr (!LOOP) {
-    const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+    const int64_t tb = order ? order[blockIdx.x] : (int64_t)blockIdx.x;  // the tile this workgroup takes
+    const TileCtx c = tile_ctx(plan, nseg, tb);
+    // the window is read BEFORE the tile's loads go out: read behind them it arrived after
+    // every load queued ahead of it GPU-wide (K2's finding)
+    // (one lane-indexed vector load, lane i <-> word i: the compiler sinks a plain or
+    // scalar load of the window below the tile's loads)
+    SegWin wpre{};
+    uint32_t wl = 0;
+    if (WARM && CHOCO_SEG_WIN_FIRST) {
+      static_assert(sizeof(SegWin) == 16, "window: 4 words");
+      const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(win + c.s) + (lane_id() & 3);
+      wl = __hip_atomic_load(wsrc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("" ::: "memory");
     float v[kSegRows][4] = {};
     if (GS) tile_load_gossip<true>(x, xh, gs, c, v);  // in flight while the floor is found
     else tile_load<XH, WARM && CHOCO_SEG_WARM_NT>(x, xh, c, v);  // warm: the only read of the call
-    process(v, c, blockIdx.x);
+    asm volatile("" ::: "memory");
+    if (WARM && CHOCO_SEG_WIN_FIRST) {
+      uint32_t* wd = reinterpret_cast<uint32_t*>(&wpre);
+      wd[0] = __builtin_amdgcn_readlane(wl, 0);
+      wd[1] = __builtin_amdgcn_readlane(wl, 1);
+      wd[2] = __builtin_amdgcn_readlane(wl, 2);
+      wd[3] = __builtin_amdgcn_readlane(wl, 3);
+    } else if (WARM) {
+      wpre = win[c.s];
+    }
+    process(v, c, tb, wpre);
   } else {
     // the raw loads of a tile (x, and x_hat), formed into v only when the tile is processed,
     // so that the next tile's loads stay in flight during this tile's work
@@ -523,7 +553,7 @@ __global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_
         cn = tile_ctx(plan, nseg, bn);
         issue(cn, a, h);  // in flight during this tile's work
       }
-      process(v, c, b);
+      process(v, c, b, win[c.s]);
       if (!more) break;
       __syncthreads();  // the LDS histogram and scan words are reused by the next tile
       c = cn;
@@ -925,6 +955,9 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
                           int nseg, float* out_val, int32_t* out_idx, const SegWs& W, bool warm, hipStream_t st,
                           Gossip gs) {
   const unsigned ntile = (unsigned)plan_tiles(plan_host);
+  // the collect launches' dispatch order (choco_topk_segmented_plan: after the random-k table)
+  const int64_t rkb = (int64_t)kRow * nseg + plan_tiles(plan_host) + plan_batched(plan_host);  // (rk_base_of)
+  const int64_t* w2_order = CHOCO_SEG_SMALL_FIRST ? plan_dev + rkb + 1 + 4 * plan_host[rkb] : nullptr;
   if (!warm) {
     profile_begin("topk_seg_hist", st);
     CHOCO_KLAUNCH((seg_hist_kernel<XH, GS>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg, W.hist1,
@@ -934,16 +967,17 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
     profile_begin("topk_seg_collect", st);
     CHOCO_KLAUNCH((seg_collect_kernel<XH, false, false>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev,
                   nseg, W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.win, Gossip{nullptr, 0.f}, out_val,
-                  out_idx, (int64_t)ntile);
+                  out_idx, (int64_t)ntile, w2_order);
   } else if (CHOCO_SEG_LOOP && !GS && ntile > (unsigned)kSegLoopGrid) {
     profile_begin("topk_seg_collect", st);
     CHOCO_KLAUNCH((seg_collect_kernel<XH, true, false, true>), dim3((unsigned)kSegLoopGrid), dim3(kSegThreads), 0,
                   st, x, xh, plan_dev, nseg, W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.win, gs, out_val,
-                  out_idx, (int64_t)ntile);
+                  out_idx, (int64_t)ntile, nullptr);
   } else {
     profile_begin("topk_seg_collect", st);
     CHOCO_KLAUNCH((seg_collect_kernel<XH, true, GS>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg,
-                  W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.win, gs, out_val, out_idx, (int64_t)ntile);
+                  W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.win, gs, out_val, out_idx, (int64_t)ntile,
+                  w2_order);
   }
   profile_end("topk_seg_collect", st);
   CHOCO_LAUNCHED("seg_collect_kernel");
@@ -1069,7 +1103,7 @@ CHOCO_API int64_t choco_topk_segmented_plan_len(const int64_t* seg_off_host, int
   int64_t ntile, nbat;
   const int rc = seg_plan_scan(seg_off_host, nseg, &ntile, &nbat);
   if (rc) return rc;
-  return (int64_t)kRow * nseg + ntile + nbat + 1 + 4 * rk_plan_tiles(seg_off_host, nseg);
+  return (int64_t)kRow * nseg + ntile + nbat + 1 + 4 * rk_plan_tiles(seg_off_host, nseg) + ntile;
 }
 
 CHOCO_API int64_t choco_topk_segmented_plan(const int64_t* seg_off_host, int32_t nseg, double ratio,
@@ -1107,6 +1141,17 @@ CHOCO_API int64_t choco_topk_segmented_plan(const int64_t* seg_off_host, int32_t
       r += nt;
     }
     rk[0] = r;
+    // W2's dispatch order: the tiles of single-tile segments (selected exactly in W2 by a
+    // latency-bound three-round radix select) first, so that they overlap the streaming
+    // of the large segments' tiles instead of ending the launch
+    int64_t* order = rk + 1 + 4 * r;
+    int64_t q = 0;
+    for (int pass = 0; pass < 2; ++pass)
+      for (int s = 0; s < nseg; ++s) {
+        const int64_t* p = plan_host + (int64_t)kRow * s;
+        if ((p[5] == 1) != (pass == 0)) continue;
+        for (int64_t t = 0; t < p[5]; ++t) order[q++] = p[4] + t;
+      }
   }
   return out;
 }

@@ -123,7 +123,8 @@ int choco_topk_compress_accumulate(const float* x, const float* xhat, int64_t n,
  * choco_topk_segmented_plan_len(seg_off, nseg) entries from the HOST table
  * seg_off[nseg+1]: nseg rows of 8 {off, len, k_s, out_off, first tile, tiles, ., .}
  * (row 0's last two = total tiles, batched segments), then the tile -> segment
- * map, then the batched segment ids.  It returns K = sum k_s (the reference's
+ * map, then the batched segment ids, the random-k tile table (randk.hip) and the
+ * collect launch's tile order (single-tile segments first).  It returns K = sum k_s (the reference's
  * selected_shapes are the k_s, parallel_choco_v.py:245); ratio must be in [0, 1).
  * The caller keeps a DEVICE copy of the whole plan (plan_dev) and passes both on
  * every call.  x / xhat need only 4-byte alignment.  The workspace

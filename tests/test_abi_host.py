@@ -70,7 +70,7 @@ def test_segmented_plan(lib):
     tiles = [(m + 16383) // 16384 for m in lens]  # every ResNet-50 tensor is batched (< 16M)
     rk = [(m + (1 << 18) - 1) >> 18 for m in lens]  # random-k tiles of 2^18 (csrc/randk.hip)
     base = 8 * len(lens) + sum(tiles) + len(lens)
-    assert plen == base + 1 + 4 * sum(rk)
+    assert plen == base + 1 + 4 * sum(rk) + sum(tiles)
     plan = (ctypes.c_int64 * plen)()
     total = lib.choco_topk_segmented_plan(p_off, len(lens), 0.99,
                                           ctypes.cast(plan, ctypes.POINTER(ctypes.c_int64)))
@@ -90,16 +90,22 @@ def test_segmented_plan(lib):
     assert flat[8 * len(lens) + sum(tiles):base].tolist() == list(range(len(lens)))
     # the random-k tile table: [R] then {segment, tile in segment, first tile, tiles}
     assert flat[base] == sum(rk)
-    tab = flat[base + 1:].reshape(-1, 4)
+    tab = flat[base + 1:base + 1 + 4 * sum(rk)].reshape(-1, 4)
     first = np.concatenate([[0], np.cumsum(rk)[:-1]])
     assert tab[:, 0].tolist() == np.repeat(np.arange(len(lens)), rk).tolist()
     assert tab[:, 1].tolist() == [t for m in rk for t in range(m)]
     assert tab[:, 2].tolist() == np.repeat(first, rk).tolist()
     assert tab[:, 3].tolist() == np.repeat(rk, rk).tolist()
+    # the collect launch's dispatch order: the tiles of single-tile segments, then the rest
+    order = flat[base + 1 + 4 * sum(rk):]
+    t0 = np.concatenate([[0], np.cumsum(tiles)[:-1]])
+    small = [int(t0[s]) for s in range(len(lens)) if tiles[s] == 1]
+    rest = [int(t0[s]) + t for s in range(len(lens)) if tiles[s] > 1 for t in range(tiles[s])]
+    assert order.tolist() == small + rest
     # a segment over 16M elements is routed to the flat pipeline (no top-k tiles)
     big = np.array([0, 5, 5 + 20_000_000], dtype=np.int64)
     pb, keep2 = _lib.i64_array(big.tolist())
-    assert lib.choco_topk_segmented_plan_len(pb, 2) == 16 + 1 + 1 + 1 + 4 * (1 + 77)
+    assert lib.choco_topk_segmented_plan_len(pb, 2) == 16 + 1 + 1 + 1 + 4 * (1 + 77) + 1
     assert lib.choco_topk_segmented_plan(pb, 2, 1.5, None) < 0  # ratio outside [0, 1)
 
 

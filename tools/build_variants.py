@@ -61,6 +61,7 @@ VARIANTS = {
     "qq_loop1_g2048": ["CHOCO_QQ_LOOP=1", "CHOCO_QQ_GRID=2048"],
     "qcheck0": ["CHOCO_QCHECK=0"],
     "seg_loop1": ["CHOCO_SEG_LOOP=1"],
+    "seg_sf0": ["CHOCO_SEG_SMALL_FIRST=0"],
     "k2wf0": ["CHOCO_K2_WINDOW_FIRST=0"],
     "k34ws1": ["CHOCO_K34_WAVE_SELECT=1"],
     "seg_loop1_g512": ["CHOCO_SEG_LOOP=1", "CHOCO_SEG_LOOP_GRID=512"],
