@@ -50,6 +50,23 @@
 
 namespace choco {
 
+// Diagnostic phase stamps (tools/seg_stamps.py; never in the product build): slot t
+// (tile t) {dispatched, loads issued}, slot 2048 + t {flags, scanned, stored, exact}.
+#ifndef CHOCO_STAMPS
+#define CHOCO_STAMPS 0
+#endif
+#if CHOCO_STAMPS
+constexpr int kSgStampSlots = 4096;
+__device__ unsigned long long g_sg_stamps[kSgStampSlots][4];
+#define SGSTAMP(slot, j)                                                                       \
+  do {                                                                                        \
+    if (threadIdx.x == 0 && (slot) < kSgStampSlots) g_sg_stamps[(slot)][(j)] = wall_clock64(); \
+  } while (0)
+#else
+#define SGSTAMP(slot, j) \
+  do {                   \
+  } while (0)
+#endif
 constexpr int kSegTile = 16384;                       // elements per tile
 #ifndef CHOCO_SEG_THREADS  // threads of the tile kernels S1 / S2 (rows of float4 per thread = 4096 / threads)
 #define CHOCO_SEG_THREADS 1024
@@ -389,9 +406,6 @@ template <bool XH, bool WARM, bool GS = false, bool LOOP = false>
 #ifndef CHOCO_SEG_SMALL_FIRST  // A/B knob: W2 / S2 take the single-tile segments' tiles first
 #define CHOCO_SEG_SMALL_FIRST 1
 #endif
-#ifndef CHOCO_SEG_WIN_FIRST  // A/B knob: 1 reads the window before the tile loads (r04: no gain, 28.5 vs 28.0 us)
-#define CHOCO_SEG_WIN_FIRST 0
-#endif
 #ifndef CHOCO_SEG_WARM_NT  // 1: W2's one read of the delta uses non-temporal loads
 #define CHOCO_SEG_WARM_NT 1
 #endif
@@ -416,6 +430,7 @@ __global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_
   auto process = [&](const float (&v)[kSegRows][4], const TileCtx& c, int64_t tb, const SegWin& wpre) {
   if (c.R.ntile == 1) {  // workgroup-uniform: the whole segment is here
     seg_exact_tile(v, c, h2, scratch, bc, rc_cnt, out_val, out_idx);
+    SGSTAMP(2048 + tb, 3);
     return;
   }
   for (int i = tid; i < kH; i += kSegThreads) h2[i] = 0u;
@@ -465,6 +480,7 @@ __global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_
     lpre[r] = inc - cnt;
     if (lane == 63) rc_cnt[r * kW + w] = inc;
   }
+  SGSTAMP(2048 + tb, 0);
   __syncthreads();
   if (w == 0) {  // wave 0: exclusive scan of the kSegRows * kW = 64 counts (row-major)
     const uint32_t cv = rc_cnt[lane];
@@ -473,6 +489,7 @@ __global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_
     if (lane == 63) rc_cnt[kSegRows * kW] = inc;
   }
   __syncthreads();
+  SGSTAMP(2048 + tb, 1);
 #pragma unroll
   for (int r = 0; r < kSegRows; ++r) {
     uint32_t pos = rc_cnt[r * kW + w] + lpre[r];
@@ -490,36 +507,36 @@ __global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_
   for (int i = tid; i < kH; i += kSegThreads)
     if (h2[i]) atomicAdd(&g2[i], h2[i]);
   if (tid == 0) tilecnt[tb] = rc_cnt[kSegRows * kW];
+  SGSTAMP(2048 + tb, 2);
   };
   if constexpr (!LOOP) {
-    const int64_t tb = order ? order[blockIdx.x] : (int64_t)blockIdx.x;  // the tile this workgroup takes
-    const TileCtx c = tile_ctx(plan, nseg, tb);
-    // the window is read BEFORE the tile's loads go out: read behind them it arrived after
-    // every load queued ahead of it GPU-wide (K2's finding)
-    // (one lane-indexed vector load, lane i <-> word i: the compiler sinks a plain or
-    // scalar load of the window below the tile's loads)
-    SegWin wpre{};
-    uint32_t wl = 0;
-    if (WARM && CHOCO_SEG_WIN_FIRST) {
-      static_assert(sizeof(SegWin) == 16, "window: 4 words");
-      const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(win + c.s) + (lane_id() & 3);
-      wl = __hip_atomic_load(wsrc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the tile this workgroup takes; with the dispatch-order records its loads need only
+    // the record (the segment's row is read while they fly)
+    int64_t ta;
+    TileCtx c;
+    if (order) {
+      const int64_t* rec = order + 4 * (int64_t)blockIdx.x;
+      ta = rec[0];
+      c.s = (int)rec[1];
+      c.start = rec[2];
+      c.tl = (int)rec[3];
+      c.slot = ta * kSegTile;
+    } else {
+      ta = blockIdx.x;
+      c = tile_ctx(plan, nseg, ta);
     }
-    asm volatile("" ::: "memory");
+    SGSTAMP(ta, 0);
     float v[kSegRows][4] = {};
     if (GS) tile_load_gossip<true>(x, xh, gs, c, v);  // in flight while the floor is found
     else tile_load<XH, WARM && CHOCO_SEG_WARM_NT>(x, xh, c, v);  // warm: the only read of the call
-    asm volatile("" ::: "memory");
-    if (WARM && CHOCO_SEG_WIN_FIRST) {
-      uint32_t* wd = reinterpret_cast<uint32_t*>(&wpre);
-      wd[0] = __builtin_amdgcn_readlane(wl, 0);
-      wd[1] = __builtin_amdgcn_readlane(wl, 1);
-      wd[2] = __builtin_amdgcn_readlane(wl, 2);
-      wd[3] = __builtin_amdgcn_readlane(wl, 3);
-    } else if (WARM) {
-      wpre = win[c.s];
+    if (order) {
+      c.R = seg_row(plan, c.s);
+      c.j = ta - c.R.t0;
     }
-    process(v, c, tb, wpre);
+    SegWin wpre{};
+    if (WARM) wpre = win[c.s];
+    SGSTAMP(ta, 1);
+    process(v, c, ta, wpre);
   } else {
     // the raw loads of a tile (x, and x_hat), formed into v only when the tile is processed,
     // so that the next tile's loads stay in flight during this tile's work
@@ -1099,11 +1116,23 @@ static int64_t rk_plan_tiles(const int64_t* seg_off_host, int32_t nseg) {
   return R;
 }
 
+#if CHOCO_STAMPS
+// Diagnostic builds only: copy out (and clear) the segmented collect stamps.
+CHOCO_API int choco_dbg_seg_stamps(unsigned long long* host, size_t bytes) {
+  const size_t all = sizeof(unsigned long long) * kSgStampSlots * 4;
+  if (bytes > all) bytes = all;
+  if (host) CHOCO_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sg_stamps), bytes, 0, hipMemcpyDeviceToHost));
+  static unsigned long long zeros[kSgStampSlots * 4];
+  CHOCO_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sg_stamps), zeros, all, 0, hipMemcpyHostToDevice));
+  return CHOCO_OK;
+}
+#endif
+
 CHOCO_API int64_t choco_topk_segmented_plan_len(const int64_t* seg_off_host, int32_t nseg) {
   int64_t ntile, nbat;
   const int rc = seg_plan_scan(seg_off_host, nseg, &ntile, &nbat);
   if (rc) return rc;
-  return (int64_t)kRow * nseg + ntile + nbat + 1 + 4 * rk_plan_tiles(seg_off_host, nseg) + ntile;
+  return (int64_t)kRow * nseg + ntile + nbat + 1 + 4 * rk_plan_tiles(seg_off_host, nseg) + 4 * ntile;
 }
 
 CHOCO_API int64_t choco_topk_segmented_plan(const int64_t* seg_off_host, int32_t nseg, double ratio,
@@ -1141,16 +1170,25 @@ CHOCO_API int64_t choco_topk_segmented_plan(const int64_t* seg_off_host, int32_t
       r += nt;
     }
     rk[0] = r;
-    // W2's dispatch order: the tiles of single-tile segments (selected exactly in W2 by a
-    // latency-bound three-round radix select) first, so that they overlap the streaming
-    // of the large segments' tiles instead of ending the launch
+    // The collect launch's dispatch order, one record {tile, segment, first element,
+    // length} per workgroup: the tiles of single-tile segments (selected exactly in the
+    // collect by a latency-bound three-round radix select) first, so that they overlap
+    // the streaming of the large segments' tiles instead of ending the launch; and a
+    // workgroup's loads need ONE scalar round trip (r04 stamps: the three dependent plan
+    // lookups -- tile -> segment -> row -> start -- took up to 2 us per tile under load)
     int64_t* order = rk + 1 + 4 * r;
     int64_t q = 0;
     for (int pass = 0; pass < 2; ++pass)
       for (int s = 0; s < nseg; ++s) {
         const int64_t* p = plan_host + (int64_t)kRow * s;
         if ((p[5] == 1) != (pass == 0)) continue;
-        for (int64_t t = 0; t < p[5]; ++t) order[q++] = p[4] + t;
+        for (int64_t t = 0; t < p[5]; ++t) {
+          int64_t* e = order + 4 * q++;
+          e[0] = p[4] + t;
+          e[1] = s;
+          e[2] = p[0] + t * kSegTile;
+          e[3] = std::min<int64_t>(kSegTile, p[1] - t * kSegTile);
+        }
       }
   }
   return out;

@@ -70,7 +70,7 @@ def test_segmented_plan(lib):
     tiles = [(m + 16383) // 16384 for m in lens]  # every ResNet-50 tensor is batched (< 16M)
     rk = [(m + (1 << 18) - 1) >> 18 for m in lens]  # random-k tiles of 2^18 (csrc/randk.hip)
     base = 8 * len(lens) + sum(tiles) + len(lens)
-    assert plen == base + 1 + 4 * sum(rk) + sum(tiles)
+    assert plen == base + 1 + 4 * sum(rk) + 4 * sum(tiles)
     plan = (ctypes.c_int64 * plen)()
     total = lib.choco_topk_segmented_plan(p_off, len(lens), 0.99,
                                           ctypes.cast(plan, ctypes.POINTER(ctypes.c_int64)))
@@ -96,16 +96,18 @@ def test_segmented_plan(lib):
     assert tab[:, 1].tolist() == [t for m in rk for t in range(m)]
     assert tab[:, 2].tolist() == np.repeat(first, rk).tolist()
     assert tab[:, 3].tolist() == np.repeat(rk, rk).tolist()
-    # the collect launch's dispatch order: the tiles of single-tile segments, then the rest
-    order = flat[base + 1 + 4 * sum(rk):]
+    # the collect launch's dispatch order, {tile, segment, first element, length} per
+    # workgroup: the tiles of single-tile segments, then the rest
+    order = flat[base + 1 + 4 * sum(rk):].reshape(-1, 4)
     t0 = np.concatenate([[0], np.cumsum(tiles)[:-1]])
-    small = [int(t0[s]) for s in range(len(lens)) if tiles[s] == 1]
-    rest = [int(t0[s]) + t for s in range(len(lens)) if tiles[s] > 1 for t in range(tiles[s])]
-    assert order.tolist() == small + rest
+    segs = [s for s in range(len(lens)) if tiles[s] == 1] + [s for s in range(len(lens)) if tiles[s] > 1]
+    exp = [(int(t0[s]) + t, s, int(offs[s]) + t * 16384, min(16384, lens[s] - t * 16384))
+           for s in segs for t in range(tiles[s])]
+    assert [tuple(r) for r in order.tolist()] == exp
     # a segment over 16M elements is routed to the flat pipeline (no top-k tiles)
     big = np.array([0, 5, 5 + 20_000_000], dtype=np.int64)
     pb, keep2 = _lib.i64_array(big.tolist())
-    assert lib.choco_topk_segmented_plan_len(pb, 2) == 16 + 1 + 1 + 1 + 4 * (1 + 77) + 1
+    assert lib.choco_topk_segmented_plan_len(pb, 2) == 16 + 1 + 1 + 1 + 4 * (1 + 77) + 4
     assert lib.choco_topk_segmented_plan(pb, 2, 1.5, None) < 0  # ratio outside [0, 1)
 
 
