@@ -148,6 +148,20 @@ CHOCO_DEV TileCtx tile_ctx(const int64_t* __restrict__ plan, int nseg, int64_t b
   return c;
 }
 
+// The same from the plan's per-tile rows (a copy of the tile's segment row + the segment
+// id, 8 int64 per tile): ONE scalar round trip instead of two dependent ones
+CHOCO_DEV TileCtx tile_ctx_rows(const int64_t* __restrict__ trows, int64_t b) {
+  const int64_t* r = trows + 8 * b;
+  TileCtx c;
+  c.R = SegRow{r[0], r[1], r[2], r[3], r[4], r[5]};
+  c.s = (int)r[6];
+  c.j = b - c.R.t0;
+  c.start = c.R.off + c.j * kSegTile;
+  c.slot = b * kSegTile;
+  c.tl = (int)min((int64_t)kSegTile, c.R.len - c.j * kSegTile);
+  return c;
+}
+
 // The tile's values: row r, thread t <-> elements r * 4096 + 4t .. +3 (dword-
 // aligned buffer loads: x + start needs only 4-byte alignment; past the tile
 // the loads return zeros and the elements are masked by `valid`).
@@ -238,14 +252,14 @@ CHOCO_DEV void load_bins(const uint32_t* h, uint32_t (&hv)[kBpt]) {
 template <bool XH, bool GS = false>
 __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ xh,
-                                                               const int64_t* __restrict__ plan, int nseg,
+                                                               const int64_t* __restrict__ trows, int nseg,
                                                                uint32_t* __restrict__ hist1, Gossip gs) {
   static_assert(!GS || XH, "the gossip step needs x_hat");
   // histogram copies: wave w -> copy w % NC (CHOCO_S1_COPIES), or lane l -> copy
   // l % NC (CHOCO_S1_LANEC: same-bin lanes of ONE atomic instruction split over copies)
   constexpr int NC = CHOCO_S1_LANEC > 1 ? CHOCO_S1_LANEC : CHOCO_S1_COPIES;
   __shared__ uint32_t h[NC][kH];
-  const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+  const TileCtx c = tile_ctx_rows(trows, blockIdx.x);
   float v[kSegRows][4] = {};
   if (GS) tile_load_gossip<false>(x, xh, gs, c, v);
   else if (c.R.ntile == 1) return;  // a single-tile segment is selected in S2 (no histogram)
@@ -628,13 +642,13 @@ CHOCO_DEV void block_find_rank_g(const uint32_t* __restrict__ hist, uint32_t ran
 
 template <bool WARM>
 __global__ __launch_bounds__(kS3Threads) void seg_fine_kernel(
-    const int64_t* __restrict__ plan, int nseg, uint32_t* __restrict__ hist1, const uint32_t* __restrict__ hist2,
+    const int64_t* __restrict__ trows, int nseg, uint32_t* __restrict__ hist1, const uint32_t* __restrict__ hist2,
     uint32_t* __restrict__ hist3, uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt,
     const float* __restrict__ cval, const SegWin* __restrict__ win) {
   __shared__ uint32_t h3[kH3];
   __shared__ uint32_t scratch[40];
   __shared__ uint32_t bc[4];
-  const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+  const TileCtx c = tile_ctx_rows(trows, blockIdx.x);
   if (c.R.ntile == 1) return;  // selected in S2
   const int tid = threadIdx.x;
   const uint32_t cnt = tilecnt[blockIdx.x];
@@ -740,12 +754,12 @@ CHOCO_DEV void seg_next_window(const uint32_t* __restrict__ hist, uint32_t base,
 
 template <bool WARM>
 __global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
-    const int64_t* __restrict__ plan, int nseg, uint32_t* __restrict__ hist2, const uint32_t* __restrict__ hist3,
+    const int64_t* __restrict__ trows, int nseg, uint32_t* __restrict__ hist2, const uint32_t* __restrict__ hist3,
     uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt, const float* __restrict__ cval,
     uint32_t* __restrict__ tcount, SegWin* __restrict__ win) {
   __shared__ uint32_t scratch[40];
   __shared__ uint32_t bc[4];
-  const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+  const TileCtx c = tile_ctx_rows(trows, blockIdx.x);
   if (c.R.ntile == 1) return;  // selected in S2
   const int tid = threadIdx.x;
   const uint32_t cnt = tilecnt[blockIdx.x];
@@ -827,14 +841,14 @@ constexpr int kS4Per = kSegMaxTiles / kS4Threads;
 static_assert(kS4Per * kS4Threads == kSegMaxTiles, "S4 tile-count geometry");
 template <bool WARM, bool XH>
 __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ plan, int nseg,
+    const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ trows, int nseg,
     const uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt, const uint32_t* __restrict__ tcount,
     uint32_t* __restrict__ hist3, const float* __restrict__ cval, const uint32_t* __restrict__ cidx,
     float* __restrict__ out_val, int32_t* __restrict__ out_idx, SegWin* __restrict__ win,
     uint32_t* __restrict__ misses, uint32_t* __restrict__ miss_flag) {
   __shared__ uint32_t scratch[40];
   __shared__ ExactSmem es;
-  const TileCtx c = tile_ctx(plan, nseg, blockIdx.x);
+  const TileCtx c = tile_ctx_rows(trows, blockIdx.x);
   if (c.R.ntile == 1) return;  // selected in S2
   const int tid = threadIdx.x;
   if (c.j == 0) {  // every tile of the segment read hist3 in S3b: reset it for the next call
@@ -975,9 +989,11 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
   // the collect launches' dispatch order (choco_topk_segmented_plan: after the random-k table)
   const int64_t rkb = (int64_t)kRow * nseg + plan_tiles(plan_host) + plan_batched(plan_host);  // (rk_base_of)
   const int64_t* w2_order = CHOCO_SEG_SMALL_FIRST ? plan_dev + rkb + 1 + 4 * plan_host[rkb] : nullptr;
+  // the per-tile rows (after the dispatch records): S1 / S3 / S4 look their tile up in one round trip
+  const int64_t* trows = plan_dev + rkb + 1 + 4 * plan_host[rkb] + 4 * (int64_t)ntile;
   if (!warm) {
     profile_begin("topk_seg_hist", st);
-    CHOCO_KLAUNCH((seg_hist_kernel<XH, GS>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg, W.hist1,
+    CHOCO_KLAUNCH((seg_hist_kernel<XH, GS>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, trows, nseg, W.hist1,
                   gs);
     profile_end("topk_seg_hist", st);
     CHOCO_LAUNCHED("seg_hist_kernel");
@@ -1000,28 +1016,28 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
   CHOCO_LAUNCHED("seg_collect_kernel");
   profile_begin("topk_seg_fine", st);
   if (warm)
-    CHOCO_KLAUNCH((seg_fine_kernel<true>), dim3(ntile), dim3(kS3Threads), 0, st, plan_dev, nseg, W.hist1, W.hist2,
+    CHOCO_KLAUNCH((seg_fine_kernel<true>), dim3(ntile), dim3(kS3Threads), 0, st, trows, nseg, W.hist1, W.hist2,
                   W.hist3, W.info, W.tilecnt, W.cval, W.win);
   else
-    CHOCO_KLAUNCH((seg_fine_kernel<false>), dim3(ntile), dim3(kS3Threads), 0, st, plan_dev, nseg, W.hist1, W.hist2,
+    CHOCO_KLAUNCH((seg_fine_kernel<false>), dim3(ntile), dim3(kS3Threads), 0, st, trows, nseg, W.hist1, W.hist2,
                   W.hist3, W.info, W.tilecnt, W.cval, W.win);
   profile_end("topk_seg_fine", st);
   CHOCO_LAUNCHED("seg_fine_kernel");
   profile_begin("topk_seg_count", st);
   if (warm)
-    CHOCO_KLAUNCH((seg_count_kernel<true>), dim3(ntile), dim3(kS3Threads), 0, st, plan_dev, nseg, W.hist2, W.hist3,
+    CHOCO_KLAUNCH((seg_count_kernel<true>), dim3(ntile), dim3(kS3Threads), 0, st, trows, nseg, W.hist2, W.hist3,
                   W.info, W.tilecnt, W.cval, W.tcount, W.win);
   else
-    CHOCO_KLAUNCH((seg_count_kernel<false>), dim3(ntile), dim3(kS3Threads), 0, st, plan_dev, nseg, W.hist2, W.hist3,
+    CHOCO_KLAUNCH((seg_count_kernel<false>), dim3(ntile), dim3(kS3Threads), 0, st, trows, nseg, W.hist2, W.hist3,
                   W.info, W.tilecnt, W.cval, W.tcount, W.win);
   profile_end("topk_seg_count", st);
   CHOCO_LAUNCHED("seg_count_kernel");
   profile_begin("topk_seg_emit", st);
   if (warm)
-    CHOCO_KLAUNCH((seg_emit_kernel<true, XH>), dim3(ntile), dim3(kS4Threads), 0, st, x, xh, plan_dev, nseg, W.info,
+    CHOCO_KLAUNCH((seg_emit_kernel<true, XH>), dim3(ntile), dim3(kS4Threads), 0, st, x, xh, trows, nseg, W.info,
                   W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win, W.misses, W.miss_flag);
   else
-    CHOCO_KLAUNCH((seg_emit_kernel<false, XH>), dim3(ntile), dim3(kS4Threads), 0, st, x, xh, plan_dev, nseg, W.info,
+    CHOCO_KLAUNCH((seg_emit_kernel<false, XH>), dim3(ntile), dim3(kS4Threads), 0, st, x, xh, trows, nseg, W.info,
                   W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win, W.misses, W.miss_flag);
   profile_end("topk_seg_emit", st);
   CHOCO_LAUNCHED("seg_emit_kernel");
@@ -1132,7 +1148,7 @@ CHOCO_API int64_t choco_topk_segmented_plan_len(const int64_t* seg_off_host, int
   int64_t ntile, nbat;
   const int rc = seg_plan_scan(seg_off_host, nseg, &ntile, &nbat);
   if (rc) return rc;
-  return (int64_t)kRow * nseg + ntile + nbat + 1 + 4 * rk_plan_tiles(seg_off_host, nseg) + 4 * ntile;
+  return (int64_t)kRow * nseg + ntile + nbat + 1 + 4 * rk_plan_tiles(seg_off_host, nseg) + 4 * ntile + 8 * ntile;
 }
 
 CHOCO_API int64_t choco_topk_segmented_plan(const int64_t* seg_off_host, int32_t nseg, double ratio,
@@ -1190,6 +1206,17 @@ CHOCO_API int64_t choco_topk_segmented_plan(const int64_t* seg_off_host, int32_t
           e[3] = std::min<int64_t>(kSegTile, p[1] - t * kSegTile);
         }
       }
+    // per tile (tile-id order): its segment's row and the segment id
+    int64_t* trows = order + 4 * ntile;
+    for (int s = 0; s < nseg; ++s) {
+      const int64_t* p = plan_host + (int64_t)kRow * s;
+      for (int64_t t = 0; t < p[5]; ++t) {
+        int64_t* e = trows + 8 * (p[4] + t);
+        for (int i = 0; i < 6; ++i) e[i] = p[i];
+        e[6] = s;
+        e[7] = 0;
+      }
+    }
   }
   return out;
 }

@@ -1,6 +1,6 @@
 #!/bin/bash
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; O=gpurun_out/r4s; mkdir -p $O
-timeout -k 10 700 python -u -m pytest tests/test_gpu_topk.py tests/test_gpu_choco_api.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+timeout -k 10 700 python -u -m pytest tests/test_gpu_topk.py tests/test_gpu_choco_api.py tests/test_gpu_consumers.py tests/test_gpu_gossip_fused.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -2 $O/tests.log; [ $rc -ne 0 ] && { grep -E "FAIL|Error|assert" $O/tests.log | head -30; tail -40 $O/tests.log; exit $rc; }
 timeout -k 10 120 python -u tools/seg_stamps.py > $O/seg_stamps.txt 2>&1; echo "stamps rc=$?"; grep -v amdgpu.ids $O/seg_stamps.txt | head -14
 summ() { python3 -c "import json,sys; d=json.load(open('$1')); r=d['roofline']; print('$2', d['value'], d['ms_per_step'], r['stage'], r['frac'], d['kernels_us'])"; }

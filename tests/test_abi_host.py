@@ -70,7 +70,7 @@ def test_segmented_plan(lib):
     tiles = [(m + 16383) // 16384 for m in lens]  # every ResNet-50 tensor is batched (< 16M)
     rk = [(m + (1 << 18) - 1) >> 18 for m in lens]  # random-k tiles of 2^18 (csrc/randk.hip)
     base = 8 * len(lens) + sum(tiles) + len(lens)
-    assert plen == base + 1 + 4 * sum(rk) + 4 * sum(tiles)
+    assert plen == base + 1 + 4 * sum(rk) + 4 * sum(tiles) + 8 * sum(tiles)
     plan = (ctypes.c_int64 * plen)()
     total = lib.choco_topk_segmented_plan(p_off, len(lens), 0.99,
                                           ctypes.cast(plan, ctypes.POINTER(ctypes.c_int64)))
@@ -98,16 +98,22 @@ def test_segmented_plan(lib):
     assert tab[:, 3].tolist() == np.repeat(rk, rk).tolist()
     # the collect launch's dispatch order, {tile, segment, first element, length} per
     # workgroup: the tiles of single-tile segments, then the rest
-    order = flat[base + 1 + 4 * sum(rk):].reshape(-1, 4)
+    ob = base + 1 + 4 * sum(rk)
+    order = flat[ob:ob + 4 * sum(tiles)].reshape(-1, 4)
     t0 = np.concatenate([[0], np.cumsum(tiles)[:-1]])
     segs = [s for s in range(len(lens)) if tiles[s] == 1] + [s for s in range(len(lens)) if tiles[s] > 1]
     exp = [(int(t0[s]) + t, s, int(offs[s]) + t * 16384, min(16384, lens[s] - t * 16384))
            for s in segs for t in range(tiles[s])]
     assert [tuple(r) for r in order.tolist()] == exp
+    # per tile (tile-id order): its segment's row and the segment id
+    trows = flat[ob + 4 * sum(tiles):].reshape(-1, 8)
+    seg_of_tile = np.repeat(np.arange(len(lens)), tiles)
+    assert np.array_equal(trows[:, :6], rows[seg_of_tile, :6])
+    assert trows[:, 6].tolist() == seg_of_tile.tolist()
     # a segment over 16M elements is routed to the flat pipeline (no top-k tiles)
     big = np.array([0, 5, 5 + 20_000_000], dtype=np.int64)
     pb, keep2 = _lib.i64_array(big.tolist())
-    assert lib.choco_topk_segmented_plan_len(pb, 2) == 16 + 1 + 1 + 1 + 4 * (1 + 77) + 4
+    assert lib.choco_topk_segmented_plan_len(pb, 2) == 16 + 1 + 1 + 1 + 4 * (1 + 77) + 4 + 8
     assert lib.choco_topk_segmented_plan(pb, 2, 1.5, None) < 0  # ratio outside [0, 1)
 
 
