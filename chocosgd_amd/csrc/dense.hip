@@ -114,6 +114,9 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_kernel(const float* __r
 #ifndef CHOCO_ACC_SEGF
 #define CHOCO_ACC_SEGF 16
 #endif
+#ifndef CHOCO_ACC_NEXT  // A/B knob: 1 loads the next index and the value with the update's index
+#define CHOCO_ACC_NEXT 1
+#endif
 #ifndef CHOCO_ACC_NT  // cache policy of the owner's segment RMW (A/B): 0 default, 1 nt stores, 2 nt loads + stores
 #define CHOCO_ACC_NT 0
 #endif
@@ -148,6 +151,11 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_seg_kernel(const float*
   if (u < k) {
     const int64_t j = idx[u];
     const int64_t jp = u > 0 ? (int64_t)idx[u - 1] : -1;
+    // the next update's index and this update's value in the same round trip: most
+    // segments hold one update, so the leader then needs no third round trip to find
+    // that the next update is not its segment's
+    const int64_t jn = CHOCO_ACC_NEXT && u + 1 < k ? (int64_t)idx[u + 1] : -1;
+    const float v0 = CHOCO_ACC_NEXT ? val[u] : 0.f;
     const bool ok = j >= 0 && j < n;
     const int64_t seg = j >> kSegShift;
     if (l4 == 0) nbad += (ok ? 0u : 1u) + ((u > 0 && jp >= j) ? 1u : 0u);
@@ -174,9 +182,9 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_seg_kernel(const float*
       }
       int64_t je = j;
       for (int64_t e = u; e < k && e < u + kSegF; ++e) {
-        if (e != u) je = idx[e];
+        if (e != u) je = (CHOCO_ACC_NEXT && e == u + 1) ? jn : idx[e];
         if (je < 0 || je >= n || (je >> kSegShift) != seg) break;
-        const float v = val[e];
+        const float v = (CHOCO_ACC_NEXT && e == u) ? v0 : val[e];
         const int off = (int)(je - base);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {

@@ -17,6 +17,7 @@ VARIANTS = {
     "rk_q2": ["CHOCO_RK_Q=2"],
     "seg_wnt0": ["CHOCO_SEG_WARM_NT=0"],
     "acc_nt1": ["CHOCO_ACC_NT=1"],
+    "acc_next0": ["CHOCO_ACC_NEXT=0"],
     "acc_nt2": ["CHOCO_ACC_NT=2"],
     "qn_t48k": ["CHOCO_QNORM_TILE=49152"],
     "qn_t64k": ["CHOCO_QNORM_TILE=65536"],
