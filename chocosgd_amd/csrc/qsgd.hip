@@ -430,20 +430,28 @@ __device__ __noinline__ void qsgd_quant_tile_slow(const float* __restrict__ x, c
 
 // The math and stores of one full single-segment tile whose deltas d are in registers
 // (thread t: its four 8-element groups e = tile * 8192 + g * 2048 + 8 t + c).
-template <int CW>
-CHOCO_DEV void quant_tile_math(const float (&d)[kQG][kQPer], int64_t tile, int64_t n, const QParam& P,
+// NG groups g0 .. g0 + NG - 1 of stream `st` (the one-tile kernel: all four groups of
+// stream threadIdx.x; the half kernel: two groups, the second half's stream advanced past
+// the first half's eight steps).
+template <int CW, int NG = kQG>
+CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_t n, const QParam& P,
                                const QDiv& D, float sf, const float* __restrict__ u_in, uint64_t seed,
                                uint64_t offset, uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
-                               float* __restrict__ dense_out) {
+                               float* __restrict__ dense_out, int g0 = 0, int st = -1) {
   constexpr int GS = kQThreads * kQPer;  // 2048
-  const int64_t eb = tile * kQStreamTile + (int64_t)threadIdx.x * kQPer;
+  if (st < 0) st = (int)threadIdx.x;
+  const int64_t eb = tile * kQStreamTile + (int64_t)st * kQPer + (int64_t)g0 * GS;
   // the thread's uniform stream, drawn group by group in stream order (8 uniforms live at
   // a time, not 32: the registers go to resident waves instead)
   Xoro128 rng;
-  if (!u_in) rng.seed(qrng_key(seed, offset), ((uint64_t)tile << 8) | threadIdx.x);
+  if (!u_in) {
+    rng.seed(qrng_key(seed, offset), ((uint64_t)tile << 8) | (uint32_t)st);
+    float skip;
+    for (int i = 0; i < g0 * (kQPer / 2); ++i) rng.next2(skip, skip);  // wave-uniform (g0 per wave)
+  }
   const bool dense = dense_out != nullptr;
 #pragma unroll
-  for (int g = 0; g < kQG; ++g) {
+  for (int g = 0; g < NG; ++g) {
     const int64_t e0 = eb + g * GS;
     float lf[kQPer];
 #if CHOCO_QCHECK
@@ -511,8 +519,18 @@ CHOCO_DEV void quant_tile_math(const float (&d)[kQG][kQPer], int64_t tile, int64
 #ifndef CHOCO_QQ_WAVES
 #define CHOCO_QQ_WAVES 4
 #endif
-template <int CW, bool XH>
-__global__ __launch_bounds__(kQThreads, XH ? 4 : CHOCO_QQ_WAVES) void qsgd_quant_kernel(
+// H = 2: a 512-thread workgroup per tile, each stream's four groups split over two
+// threads (waves 0-3 take groups 0-1, waves 4-7 groups 2-3 after stepping their stream
+// past the first eight uniforms) -- half the registers per thread, twice the waves
+// resident, the same uniforms.  Occupancy of the H = 2 build: CHOCO_QQ_HWAVES.
+#ifndef CHOCO_QQ_HALF
+#define CHOCO_QQ_HALF 1
+#endif
+#ifndef CHOCO_QQ_HWAVES
+#define CHOCO_QQ_HWAVES 6
+#endif
+template <int CW, bool XH, int H>
+__global__ __launch_bounds__(kQThreads * H, H == 1 ? (XH ? 4 : CHOCO_QQ_WAVES) : CHOCO_QQ_HWAVES) void qsgd_quant_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, const int64_t* __restrict__ seg_off,
     int nseg, int s_levels, int biased, const float* __restrict__ norms, const float* __restrict__ u_in,
     uint64_t seed, uint64_t offset, uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
@@ -530,37 +548,41 @@ __global__ __launch_bounds__(kQThreads, XH ? 4 : CHOCO_QQ_WAVES) void qsgd_quant
     const int64_t g0 = pad_e0 / kQPer, groups = (pad_len + kQPer - 1) / kQPer;
     const int64_t lvl_used = (g0 + groups) * CW, lvl_end = g0 * CW + (groups * CW + 15) / 16 * 16;
     const int64_t sgn_used = g0 + groups, sgn_end = g0 + (groups + 15) / 16 * 16;
-    for (int64_t b = lvl_used + threadIdx.x; b < lvl_end; b += kQThreads) lvl_plane[b] = 0;
-    for (int64_t b = sgn_used + threadIdx.x; b < sgn_end; b += kQThreads) sign_plane[b] = 0;
+    for (int64_t b = lvl_used + threadIdx.x; b < lvl_end; b += kQThreads * H) lvl_plane[b] = 0;
+    for (int64_t b = sgn_used + threadIdx.x; b < sgn_end; b += kQThreads * H) sign_plane[b] = 0;
   }
   const float sf = (float)s_levels;
-  const int64_t eb = t_e0 + (int64_t)threadIdx.x * kQPer;  // group g starts at eb + g * 2048
-  constexpr int GS = kQThreads * kQPer;                    // 2048
+  constexpr int NG = kQG / H;                                // groups per thread
+  const int st = (int)(threadIdx.x % kQThreads);             // the thread's uniform stream
+  const int g0 = (int)(threadIdx.x / kQThreads) * NG;        // its first group (wave-uniform)
+  constexpr int GS = kQThreads * kQPer;                      // 2048
+  const int64_t eb = t_e0 + (int64_t)st * kQPer + (int64_t)g0 * GS;  // group g0 + g starts at eb + g * 2048
   if (!uniform || t_e1 - t_e0 != kQStreamTile) {
-    qsgd_quant_tile_slow<CW>(x, xh, n, seg_off, nseg, s_levels, biased, norms, u_in, seed, offset, lvl_plane,
-                             sign_plane, dense_out, tile, sg0);
+    if (threadIdx.x < kQThreads)  // (no barrier below: the second half leaves)
+      qsgd_quant_tile_slow<CW>(x, xh, n, seg_off, nseg, s_levels, biased, norms, u_in, seed, offset, lvl_plane,
+                               sign_plane, dense_out, tile, sg0);
     return;
   }
   // full one-segment tile: unconditional loads, all in flight (the delta's last
   // read: the norm pass read it first)
-  float d[kQG][kQPer];
+  float d[NG][kQPer];
   {
-    float4 a[kQG][2];
+    float4 a[NG][2];
 #pragma unroll
-    for (int g = 0; g < kQG; ++g) {
+    for (int g = 0; g < NG; ++g) {
       a[g][0] = ld_quant4(x + eb + g * GS);
       a[g][1] = ld_quant4(x + eb + g * GS + 4);
     }
     if constexpr (XH) {
 #pragma unroll
-      for (int g = 0; g < kQG; ++g) {
+      for (int g = 0; g < NG; ++g) {
         const float4 h0 = ld_quant4(xh + eb + g * GS), h1 = ld_quant4(xh + eb + g * GS + 4);
         a[g][0] = sub4(a[g][0], h0);
         a[g][1] = sub4(a[g][1], h1);
       }
     }
 #pragma unroll
-    for (int g = 0; g < kQG; ++g) {
+    for (int g = 0; g < NG; ++g) {
       d[g][0] = a[g][0].x; d[g][1] = a[g][0].y; d[g][2] = a[g][0].z; d[g][3] = a[g][0].w;
       d[g][4] = a[g][1].x; d[g][5] = a[g][1].y; d[g][6] = a[g][1].z; d[g][7] = a[g][1].w;
     }
@@ -568,7 +590,7 @@ __global__ __launch_bounds__(kQThreads, XH ? 4 : CHOCO_QQ_WAVES) void qsgd_quant
   const QParam P = qparam(norms, seg_off, n, sg0, s_levels, biased != 0);
   QDiv D;
   D.init(P.norm);
-  quant_tile_math<CW>(d, tile, n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out);
+  quant_tile_math<CW, NG>(d, tile, n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out, g0, st);
 }
 
 // Single-segment buffers (the flat path, BASELINE cfg 3): a grid of resident workgroups
@@ -859,6 +881,7 @@ static int qsgd_norms_launch(const float* x, const float* xhat, int64_t n, const
 #define CHOCO_QQ_GRID 1024
 #endif
 constexpr int64_t kQLoopGrid = CHOCO_QQ_GRID;
+constexpr int kQH = CHOCO_QQ_HALF ? 2 : 1;
 static int qsgd_quant_launch(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
                              int32_t q, int32_t is_biased, const float* norms, const float* u_in, uint64_t seed,
                              uint64_t offset, uint8_t* lvl_plane, uint8_t* sign_plane, float* dense_out,
@@ -896,13 +919,13 @@ static int qsgd_quant_launch(const float* x, const float* xhat, int64_t n, const
 #define CHOCO_Q(CWV)                                                                                          \
   case CWV:                                                                                                   \
     if (xhat)                                                                                                 \
-      CHOCO_KLAUNCH((qsgd_quant_kernel<CWV, true>), dim3((unsigned)tile_cnt), dim3(kQThreads), 0, st, x, xhat, \
-                    n, seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane, sign_plane,   \
-                    dense_out, tile_lo, tile_cnt, pad_e0, e1 - pad_e0);                                       \
-    else                                                                                                      \
-      CHOCO_KLAUNCH((qsgd_quant_kernel<CWV, false>), dim3((unsigned)tile_cnt), dim3(kQThreads), 0, st, x,     \
-                    nullptr, n, seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane,      \
+      CHOCO_KLAUNCH((qsgd_quant_kernel<CWV, true, kQH>), dim3((unsigned)tile_cnt), dim3(kQThreads * kQH), 0, st, \
+                    x, xhat, n, seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane,      \
                     sign_plane, dense_out, tile_lo, tile_cnt, pad_e0, e1 - pad_e0);                           \
+    else                                                                                                      \
+      CHOCO_KLAUNCH((qsgd_quant_kernel<CWV, false, kQH>), dim3((unsigned)tile_cnt), dim3(kQThreads * kQH), 0,  \
+                    st, x, nullptr, n, seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset,          \
+                    lvl_plane, sign_plane, dense_out, tile_lo, tile_cnt, pad_e0, e1 - pad_e0);                \
     break;
   switch (cw) {
     CHOCO_Q(1)

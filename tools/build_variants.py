@@ -66,6 +66,8 @@ VARIANTS = {
     "k2wf0": ["CHOCO_K2_WINDOW_FIRST=0"],
     "k34ws1": ["CHOCO_K34_WAVE_SELECT=1"],
     "seg_loop1_g512": ["CHOCO_SEG_LOOP=1", "CHOCO_SEG_LOOP_GRID=512"],
+    "qq_h0": ["CHOCO_QQ_HALF=0"],
+    "qq_hw8": ["CHOCO_QQ_HWAVES=8"],
 }
 
 
