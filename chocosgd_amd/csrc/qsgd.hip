@@ -433,7 +433,11 @@ __device__ __noinline__ void qsgd_quant_tile_slow(const float* __restrict__ x, c
 // NG groups g0 .. g0 + NG - 1 of stream `st` (the one-tile kernel: all four groups of
 // stream threadIdx.x; the half kernel: two groups, the second half's stream advanced past
 // the first half's eight steps).
-template <int CW, int NG = kQG>
+// UIN: the uniforms come from u_in (tests pin them) instead of the streams -- a template
+// flag, not a runtime test: a runtime branch around the u loads made the compiler wait
+// vmcnt(0) before every group's math, draining every load in flight (the prefetch of the
+// looping kernel included).
+template <int CW, int NG, bool UIN>
 CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_t n, const QParam& P,
                                const QDiv& D, float sf, const float* __restrict__ u_in, uint64_t seed,
                                uint64_t offset, uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
@@ -444,7 +448,7 @@ CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_
   // the thread's uniform stream, drawn group by group in stream order (8 uniforms live at
   // a time, not 32: the registers go to resident waves instead)
   Xoro128 rng;
-  if (!u_in) {
+  if constexpr (!UIN) {
     rng.seed(qrng_key(seed, offset), ((uint64_t)tile << 8) | (uint32_t)st);
     float skip;
     for (int i = 0; i < g0 * (kQPer / 2); ++i) rng.next2(skip, skip);  // wave-uniform (g0 per wave)
@@ -479,7 +483,7 @@ CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_
     }
 #endif
     float u[kQPer];
-    if (u_in) {
+    if constexpr (UIN) {
       const float4 u0 = *reinterpret_cast<const float4*>(u_in + e0);
       const float4 u1 = *reinterpret_cast<const float4*>(u_in + e0 + 4);
       u[0] = u0.x; u[1] = u0.y; u[2] = u0.z; u[3] = u0.w;
@@ -529,7 +533,7 @@ CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_
 #ifndef CHOCO_QQ_HWAVES
 #define CHOCO_QQ_HWAVES 6
 #endif
-template <int CW, bool XH, int H>
+template <int CW, bool XH, int H, bool UIN>
 __global__ __launch_bounds__(kQThreads * H, H == 1 ? (XH ? 4 : CHOCO_QQ_WAVES) : CHOCO_QQ_HWAVES) void qsgd_quant_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, const int64_t* __restrict__ seg_off,
     int nseg, int s_levels, int biased, const float* __restrict__ norms, const float* __restrict__ u_in,
@@ -590,7 +594,7 @@ __global__ __launch_bounds__(kQThreads * H, H == 1 ? (XH ? 4 : CHOCO_QQ_WAVES) :
   const QParam P = qparam(norms, seg_off, n, sg0, s_levels, biased != 0);
   QDiv D;
   D.init(P.norm);
-  quant_tile_math<CW, NG>(d, tile, n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out, g0, st);
+  quant_tile_math<CW, NG, UIN>(d, tile, n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out, g0, st);
 }
 
 // Single-segment buffers (the flat path, BASELINE cfg 3): a grid of resident workgroups
@@ -602,7 +606,7 @@ __global__ __launch_bounds__(kQThreads * H, H == 1 ? (XH ? 4 : CHOCO_QQ_WAVES) :
 // (SQ_WAIT_ANY / SQ_WAVE_CYCLES, SQ_INSTS_VALU; profiles/r04_qsgd_sq_counters.txt).
 // Workgroup 0 also quantizes the range's partial last tile (tail_tile >= 0) and zeroes
 // the planes' padding.  Same uniforms and results as the one-tile kernel.
-template <int CW, bool XH>
+template <int CW, bool XH, bool UIN>
 __global__ __launch_bounds__(kQThreads, 4) void qsgd_quant_loop_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, const int64_t* __restrict__ seg_off,
     int s_levels, int biased, const float* __restrict__ norms, const float* __restrict__ u_in, uint64_t seed,
@@ -660,7 +664,7 @@ __global__ __launch_bounds__(kQThreads, 4) void qsgd_quant_loop_kernel(
       d[g][0] = v0.x; d[g][1] = v0.y; d[g][2] = v0.z; d[g][3] = v0.w;
       d[g][4] = v1.x; d[g][5] = v1.y; d[g][6] = v1.z; d[g][7] = v1.w;
     }
-    quant_tile_math<CW>(d, tile_of(j), n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out);
+    quant_tile_math<CW, kQG, UIN>(d, tile_of(j), n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out);
     if (!more) break;
 #pragma unroll
     for (int g = 0; g < kQG; ++g) {
@@ -881,6 +885,8 @@ static int qsgd_norms_launch(const float* x, const float* xhat, int64_t n, const
 #define CHOCO_QQ_GRID 1024
 #endif
 constexpr int64_t kQLoopGrid = CHOCO_QQ_GRID;
+// split streams for the plain delta only: with x_hat (the gossip form) the one-stream
+// threads measured faster (r4u2: 151.5-153.4 against 154.8-157.6 us)
 constexpr int kQH = CHOCO_QQ_HALF ? 2 : 1;
 static int qsgd_quant_launch(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
                              int32_t q, int32_t is_biased, const float* norms, const float* u_in, uint64_t seed,
@@ -900,9 +906,14 @@ static int qsgd_quant_launch(const float* x, const float* xhat, int64_t n, const
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(full_cnt, kQLoopGrid));
 #define CHOCO_QL(CWV)                                                                                         \
   case CWV:                                                                                                   \
-    CHOCO_KLAUNCH((qsgd_quant_loop_kernel<CWV, false>), dim3(grid), dim3(kQThreads), 0, st, x, nullptr, n,   \
-                  seg_off, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane, sign_plane, dense_out,   \
-                  tile_lo, full_cnt, tail_tile, pad_e0, e1 - pad_e0);                                         \
+    if (u_in)                                                                                                 \
+      CHOCO_KLAUNCH((qsgd_quant_loop_kernel<CWV, false, true>), dim3(grid), dim3(kQThreads), 0, st, x,        \
+                    nullptr, n, seg_off, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane,            \
+                    sign_plane, dense_out, tile_lo, full_cnt, tail_tile, pad_e0, e1 - pad_e0);                \
+    else                                                                                                      \
+      CHOCO_KLAUNCH((qsgd_quant_loop_kernel<CWV, false, false>), dim3(grid), dim3(kQThreads), 0, st, x,       \
+                    nullptr, n, seg_off, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane,            \
+                    sign_plane, dense_out, tile_lo, full_cnt, tail_tile, pad_e0, e1 - pad_e0);                \
     break;
     switch (cw) {
       CHOCO_QL(1)
@@ -916,16 +927,18 @@ static int qsgd_quant_launch(const float* x, const float* xhat, int64_t n, const
     CHOCO_LAUNCHED("qsgd_quant_loop_kernel");
     return CHOCO_OK;
   }
+#define CHOCO_Q1(CWV, XHV, UINV)                                                                              \
+  CHOCO_KLAUNCH((qsgd_quant_kernel<CWV, XHV, XHV ? 1 : kQH, UINV>), dim3((unsigned)tile_cnt),                  \
+                dim3(kQThreads * (XHV ? 1 : kQH)), 0,                                                          \
+                st, x, xhat, n, seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane,      \
+                sign_plane, dense_out, tile_lo, tile_cnt, pad_e0, e1 - pad_e0)
 #define CHOCO_Q(CWV)                                                                                          \
   case CWV:                                                                                                   \
-    if (xhat)                                                                                                 \
-      CHOCO_KLAUNCH((qsgd_quant_kernel<CWV, true, kQH>), dim3((unsigned)tile_cnt), dim3(kQThreads * kQH), 0, st, \
-                    x, xhat, n, seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane,      \
-                    sign_plane, dense_out, tile_lo, tile_cnt, pad_e0, e1 - pad_e0);                           \
-    else                                                                                                      \
-      CHOCO_KLAUNCH((qsgd_quant_kernel<CWV, false, kQH>), dim3((unsigned)tile_cnt), dim3(kQThreads * kQH), 0,  \
-                    st, x, nullptr, n, seg_off, nseg, s_levels, is_biased, norms, u_in, seed, offset,          \
-                    lvl_plane, sign_plane, dense_out, tile_lo, tile_cnt, pad_e0, e1 - pad_e0);                \
+    if (xhat) {                                                                                               \
+      if (u_in) CHOCO_Q1(CWV, true, true); else CHOCO_Q1(CWV, true, false);                                   \
+    } else {                                                                                                  \
+      if (u_in) CHOCO_Q1(CWV, false, true); else CHOCO_Q1(CWV, false, false);                                 \
+    }                                                                                                         \
     break;
   switch (cw) {
     CHOCO_Q(1)
@@ -935,6 +948,7 @@ static int qsgd_quant_launch(const float* x, const float* xhat, int64_t n, const
     CHOCO_Q(16)
   }
 #undef CHOCO_Q
+#undef CHOCO_Q1
   profile_end("qsgd_quantize", st);
   CHOCO_LAUNCHED("qsgd_quant_kernel");
   return CHOCO_OK;

@@ -6,7 +6,7 @@ rc=$?; tail -1 $O/tests.log; [ $rc -ne 0 ] && { grep -E "FAIL|Error|assert" $O/t
 summ() { python3 -c "import json,sys; d=json.load(open('$1')); r=d['roofline']; print('$2', d['value'], d['ms_per_step'], r['stage'], r['frac'], d['kernels_us'])"; }
 for rep in 1 2 3; do
   for wl in qsgd step_qsgd; do
-    for v in default qq_h0 qq_hw6; do
+    for v in default qq_h0 qq_hw8 qq_loop1; do
       L=""; [ $v != default ] && L="--lib chocosgd_amd/lib/variants/lib_$v.so"
       timeout -k 10 120 python bench.py --workload $wl --steps 10 --warmup 4 --no-cpu-baseline --no-e2e $L > $O/${wl}_$v.json 2>$O/${wl}_$v.err || { tail -5 $O/${wl}_$v.err; exit 1; }
       summ $O/${wl}_$v.json ${wl}_$v
