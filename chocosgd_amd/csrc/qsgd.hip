@@ -679,6 +679,123 @@ __global__ __launch_bounds__(kQThreads, 4) void qsgd_quant_loop_kernel(
   }
 }
 
+// The ring quantize (single-segment buffers without x_hat, stream uniforms; CHOCO_QQ_RING):
+// the tile's loads land in LDS, not in registers, so a wave keeps the next units' loads in
+// flight while it computes.  A wave unit is one split-stream half tile (the H = 2 mapping:
+// 64 streams x 2 groups, 4 KiB); resident waves walk the units from the end of the range
+// backward, each with a ring of kQRingD unit slots in LDS filled by global_load_lds
+// (lane l's 16 bytes land at slot + 16 l: loads are issued so that lane l finds its own
+// eight elements of a group at the same offset of two 1 KiB pieces -- conflict-free reads).
+// No barrier: each wave reads only what it loaded.  The waits are counted here, not by
+// the compiler: before unit j's reads, the ops issued after unit j's loads may remain
+// (the later units' loads and the stores of the units computed since).
+#ifndef CHOCO_QQ_RING
+#define CHOCO_QQ_RING 0
+#endif
+#ifndef CHOCO_QQ_RING_D  // ring depth (unit slots per wave)
+#define CHOCO_QQ_RING_D 3
+#endif
+#ifndef CHOCO_QQ_RING_WGS  // resident 256-thread workgroups per CU
+#define CHOCO_QQ_RING_WGS 3
+#endif
+constexpr int kQRingD = CHOCO_QQ_RING_D;
+typedef __attribute__((address_space(3))) void* choco_lds_ptr;
+CHOCO_DEV void glds16(const float* g, float4* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(g, (choco_lds_ptr)lds_wave_base, 16, 0, 0);
+}
+template <int N>
+CHOCO_DEV void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// The lane's float4 of each of a unit's four 1 KiB pieces (p = the lane's float4 of
+// piece 0), after the wait: the compiler does not see the DMA's LDS writes, so the
+// reads are asm too (one wait for the four).
+CHOCO_DEV void lds_read_unit(const float4* p, float4 (&o)[4]) {
+  choco_f32x4 v0, v1, v2, v3;
+  const uint32_t a = (uint32_t)(uintptr_t)(choco_lds_ptr)p;
+  asm volatile(
+      "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\tds_read_b128 %2, %4 offset:2048\n\t"
+      "ds_read_b128 %3, %4 offset:3072\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)
+      : "v"(a)
+      : "memory");
+  o[0] = make_float4(v0.x, v0.y, v0.z, v0.w);
+  o[1] = make_float4(v1.x, v1.y, v1.z, v1.w);
+  o[2] = make_float4(v2.x, v2.y, v2.z, v2.w);
+  o[3] = make_float4(v3.x, v3.y, v3.z, v3.w);
+}
+
+template <int CW>
+__global__ __launch_bounds__(kQThreads, 3) void qsgd_quant_ring_kernel(
+    const float* __restrict__ x, int64_t n, const int64_t* __restrict__ seg_off, int s_levels, int biased,
+    const float* __restrict__ norms, uint64_t seed, uint64_t offset, uint8_t* __restrict__ lvl_plane,
+    uint8_t* __restrict__ sign_plane, float* __restrict__ dense_out, int64_t tile_lo, int64_t full_cnt,
+    int64_t tail_tile, int64_t pad_e0, int64_t pad_len) {
+  __shared__ float4 ring[kQThreads / 64][kQRingD][4][64];
+  constexpr int GS = kQThreads * kQPer;  // 2048
+  if (blockIdx.x == 0) {
+    const int64_t g0 = pad_e0 / kQPer, groups = (pad_len + kQPer - 1) / kQPer;
+    const int64_t lvl_used = (g0 + groups) * CW, lvl_end = g0 * CW + (groups * CW + 15) / 16 * 16;
+    const int64_t sgn_used = g0 + groups, sgn_end = g0 + (groups + 15) / 16 * 16;
+    for (int64_t b = lvl_used + threadIdx.x; b < lvl_end; b += kQThreads) lvl_plane[b] = 0;
+    for (int64_t b = sgn_used + threadIdx.x; b < sgn_end; b += kQThreads) sign_plane[b] = 0;
+    if (tail_tile >= 0)
+      qsgd_quant_tile_slow<CW>(x, nullptr, n, seg_off, 1, s_levels, biased, norms, nullptr, seed, offset,
+                               lvl_plane, sign_plane, dense_out, tail_tile, 0);
+  }
+  const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  const int64_t gw = (int64_t)blockIdx.x * (kQThreads / 64) + w, TW = (int64_t)gridDim.x * (kQThreads / 64);
+  const int64_t nunits = full_cnt * 8;
+  if (gw >= nunits) return;  // wave-uniform; no barrier below
+  const int64_t cnt = (nunits - gw + TW - 1) / TW;
+  const float sf = (float)s_levels;
+  const QParam P = qparam(norms, seg_off, n, 0, s_levels, biased != 0);
+  QDiv D;
+  D.init(P.norm);
+  // unit u: tile (from the end of the range) u >> 3, wave slot ws = u & 7 (streams
+  // 64 (ws & 3) .. +63, groups 2 (ws >> 2) .. +1)
+  auto unit_tile = [&](int64_t j) { return tile_lo + full_cnt - 1 - ((gw + j * TW) >> 3); };
+  auto unit_ws = [&](int64_t j) { return (int)((gw + j * TW) & 7); };
+  auto issue = [&](int64_t j) {
+    const int ws = unit_ws(j);
+    const float* base = x + unit_tile(j) * kQStreamTile + (int64_t)(ws & 3) * 512 + (int64_t)lane * kQPer +
+                        (int64_t)(ws >> 2) * 2 * GS;
+    float4(&slot)[4][64] = ring[w][(int)(j % kQRingD)];
+    glds16(base, slot[0]);
+    glds16(base + 4, slot[1]);
+    glds16(base + GS, slot[2]);
+    glds16(base + GS + 4, slot[3]);
+  };
+  const bool dense = dense_out != nullptr;
+#pragma unroll 1
+  for (int64_t j = 0; j < kQRingD - 1 && j < cnt; ++j) issue(j);
+#pragma unroll 1
+  for (int64_t j = 0; j < cnt; ++j) {
+    const bool more = j + kQRingD - 1 < cnt;
+    if (more) issue(j + kQRingD - 1);
+    // steady state: the D - 1 later units' loads (4 each) and the stores of the D - 1
+    // units computed since unit j's loads (4, or 8 with the dense output) may remain
+    if (more && j >= kQRingD - 1) {
+      if (dense) wait_vm<(kQRingD - 1) * 12>(); else wait_vm<(kQRingD - 1) * 8>();
+    } else {
+      wait_vm<0>();
+    }
+    const float4(&slot)[4][64] = ring[w][(int)(j % kQRingD)];
+    static_assert(sizeof(slot[0]) == 1024, "pieces of 1 KiB");
+    float4 a[4];
+    lds_read_unit(&slot[0][lane], a);
+    float d[2][kQPer];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      d[g][0] = a[2 * g].x; d[g][1] = a[2 * g].y; d[g][2] = a[2 * g].z; d[g][3] = a[2 * g].w;
+      d[g][4] = a[2 * g + 1].x; d[g][5] = a[2 * g + 1].y; d[g][6] = a[2 * g + 1].z; d[g][7] = a[2 * g + 1].w;
+    }
+    const int ws = unit_ws(j);
+    quant_tile_math<CW, 2, false>(d, unit_tile(j), n, P, D, sf, nullptr, seed, offset, lvl_plane, sign_plane,
+                                  dense_out, (ws >> 2) * 2, (ws & 3) * 64 + lane);
+  }
+}
+
 // ---------------------------------------------------------------- decode / accumulate
 struct QMsgs {
   const uint8_t* lvl[kQMaxMsg];
@@ -898,6 +1015,31 @@ static int qsgd_quant_launch(const float* x, const float* xhat, int64_t n, const
   const int64_t tile_cnt = (e1 - e0 + kQStreamTile - 1) / kQStreamTile;
   profile_begin("qsgd_quantize", st);
   // (with x_hat the prefetch would need 64 more registers: the one-tile kernel, no spills)
+  if (CHOCO_QQ_RING && nseg <= 1 && !xhat && !u_in) {
+    const bool partial = (tile_lo + tile_cnt) * kQStreamTile > n;
+    const int64_t full_cnt = tile_cnt - (partial ? 1 : 0);
+    const int64_t tail_tile = partial ? tile_lo + tile_cnt - 1 : -1;
+    const int64_t waves = full_cnt * 8;
+    const unsigned grid = (unsigned)std::max<int64_t>(
+        1, std::min<int64_t>((waves + 3) / 4, (int64_t)256 * CHOCO_QQ_RING_WGS));
+#define CHOCO_QR(CWV)                                                                                         \
+  case CWV:                                                                                                   \
+    CHOCO_KLAUNCH((qsgd_quant_ring_kernel<CWV>), dim3(grid), dim3(kQThreads), 0, st, x, n, seg_off, s_levels,  \
+                  is_biased, norms, seed, offset, lvl_plane, sign_plane, dense_out, tile_lo, full_cnt,         \
+                  tail_tile, pad_e0, e1 - pad_e0);                                                            \
+    break;
+    switch (cw) {
+      CHOCO_QR(1)
+      CHOCO_QR(2)
+      CHOCO_QR(4)
+      CHOCO_QR(8)
+      CHOCO_QR(16)
+    }
+#undef CHOCO_QR
+    profile_end("qsgd_quantize", st);
+    CHOCO_LAUNCHED("qsgd_quant_ring_kernel");
+    return CHOCO_OK;
+  }
   if (CHOCO_QQ_LOOP && nseg <= 1 && !xhat) {
     // full tiles of the range, and its partial last tile (the buffer's end)
     const bool partial = (tile_lo + tile_cnt) * kQStreamTile > n;

@@ -97,6 +97,30 @@ def test_qsgd_looping_quantize_and_ranges():
         assert np.array_equal(host(part), O.qsgd_pack(lvl[e0:e1], host(x)[e0:e1], q)), (e0, e1)
 
 
+def test_qsgd_quantize_many_units_per_wave():
+    """A size where every resident wave of the ring quantize (CHOCO_QQ_RING builds: loads
+    through LDS, waits counted by hand) walks ~8 units, so its steady-state waits run, with
+    and without the dense output (4 or 8 stores per unit in the count): the whole wire
+    and the dense values bit-exact against the oracle.  (Default builds: the one-tile
+    kernel at a 3000-tile size.)"""
+    from chocosgd_amd import codec
+    n = 8192 * 3000 + 333
+    q, seed, offset = 4, 0x1357_9BDF, 11
+    x = randn(n, 516)
+    packed_d, norms, dense = codec.qsgd_compress(x, q, seed=seed, offset=offset, want_dense=True)
+    packed, norms2, _ = codec.qsgd_compress(x, q, seed=seed, offset=offset)
+    u = O.qsgd_uniforms(n, seed, offset)
+    s = 2 ** q - 1
+    nrm = host(norms)[0]
+    assert host(norms2)[0] == nrm
+    xh = host(x)
+    lvl = O.qsgd_levels(xh, s, u, nrm)
+    want = O.qsgd_pack(lvl, xh, q)
+    assert np.array_equal(host(packed), want)
+    assert np.array_equal(host(packed_d), want)
+    assert same_bits(host(dense), O.qsgd_dense(xh, s, u, nrm))
+
+
 def test_qsgd_zero_segment_nan():
     from chocosgd_amd import codec
     x = torch.zeros(64, device=DEV)

@@ -67,6 +67,8 @@ VARIANTS = {
     "k34ws1": ["CHOCO_K34_WAVE_SELECT=1"],
     "seg_loop1_g512": ["CHOCO_SEG_LOOP=1", "CHOCO_SEG_LOOP_GRID=512"],
     "qq_h0": ["CHOCO_QQ_HALF=0"],
+    "qq_ring_d3w3": ["CHOCO_QQ_RING=1", "CHOCO_QQ_RING_D=3", "CHOCO_QQ_RING_WGS=3"],
+    "qq_ring_d2w4": ["CHOCO_QQ_RING=1", "CHOCO_QQ_RING_D=2", "CHOCO_QQ_RING_WGS=4"],
     "qq_hw8": ["CHOCO_QQ_HWAVES=8"],
 }
 
