@@ -296,14 +296,16 @@ CHOCO_DEV __host__ uint64_t qrng_key(uint64_t seed, uint64_t offset) {
 CHOCO_DEV float u24(uint32_t b24) { return (float)b24 * 5.9604644775390625e-08f; }
 
 // The uniforms themselves come from xoroshiro128+ (Blackman & Vigna 2018, the
-// a=24 b=16 c=37 parameters) run for 16 steps per 32-element STREAM, its state
+// a=24 b=16 c=37 parameters) run for 8 steps per 16-element STREAM, its state
 // seeded by SplitMix64 as its authors prescribe: stream `sid` starts at
 // (mix(key + (2 sid + 1) gamma), mix(key + (2 sid + 2) gamma)).  One step (two
 // 64-bit adds/xors/rotates, no multiply) yields two uniforms: bits 63..40 and
-// 39..16 of s0 + s1, * 2^-24.  Amortising the seeding over 32 elements takes the
-// generator from ~20 to ~8 VALU operations per element (the quantize pass is
-// VALU-bound).  Stream of element e (qsgd.hip kQStreamTile): tile T = e >> 13,
-// o = e & 8191, sid = (T << 8) | ((o >> 3) & 255), position (o >> 11) * 8 + (o & 7).
+// 39..16 of s0 + s1, * 2^-24.  Amortising the seeding over 16 elements takes the
+// generator from ~20 to ~9 VALU operations per element.  Stream of element e
+// (qsgd.hip kQStreamTile, qstream_id): tile T = e >> 13, o = e & 8191, group
+// g = o >> 11, sid = (T << 9) | ((g >> 1) << 8) | ((o >> 3) & 255), position
+// (g & 1) * 8 + (o & 7).  (Round 4: 16-element streams, so a thread that owns two of a
+// slot's four groups starts its own stream instead of stepping past another's.)
 CHOCO_DEV __host__ uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
 struct Xoro128 {
   uint64_t s0, s1;

@@ -372,6 +372,11 @@ CHOCO_DEV float qlevel(float lf, float u) {
 // IEEE division per element: 123 us at 100M with the tail re-read from the
 // Infinity Cache); see DESIGN.md §4 for the measured steps.
 constexpr int kQG = 4;                                  // groups per thread
+// The uniform stream of thread slot t's groups g, g + 1 (g even) of a tile: 16 uniforms
+// each, two streams per slot (choco_common.h Xoro128; oracle qsgd_uniforms_at).
+CHOCO_DEV uint64_t qstream_id(int64_t tile, int g, uint32_t t) {
+  return ((uint64_t)tile << 9) | ((uint64_t)(g >> 1) << 8) | t;
+}
 constexpr int kQStreamTile = kQThreads * kQPer * kQG;   // 8192 elements per workgroup
 static_assert(kQStreamTile == 8192, "the uniform-stream mapping (choco_common.h) assumes 8192-element tiles");
 
@@ -389,10 +394,10 @@ __device__ __noinline__ void qsgd_quant_tile_slow(const float* __restrict__ x, c
   const float sf = (float)s_levels;
   const int64_t eb = tile * kQStreamTile + (int64_t)threadIdx.x * kQPer;
   Xoro128 rng;
-  if (!u_in) rng.seed(qrng_key(seed, offset), ((uint64_t)tile << 8) | threadIdx.x);
   int s = sg0;
 #pragma unroll 1
   for (int g = 0; g < kQG; ++g) {
+    if (!u_in && (g & 1) == 0) rng.seed(qrng_key(seed, offset), qstream_id(tile, g, threadIdx.x));
     const int64_t e0 = eb + (int64_t)g * kQThreads * kQPer;
     uint64_t lacc[2] = {0, 0};  // 8 * CW <= 128 level bits
     uint32_t sbits = 0;
@@ -430,9 +435,8 @@ __device__ __noinline__ void qsgd_quant_tile_slow(const float* __restrict__ x, c
 
 // The math and stores of one full single-segment tile whose deltas d are in registers
 // (thread t: its four 8-element groups e = tile * 8192 + g * 2048 + 8 t + c).
-// NG groups g0 .. g0 + NG - 1 of stream `st` (the one-tile kernel: all four groups of
-// stream threadIdx.x; the half kernel: two groups, the second half's stream advanced past
-// the first half's eight steps).
+// NG groups g0 .. g0 + NG - 1 of thread slot `st` (the one-tile kernel: all four groups
+// of slot threadIdx.x, i.e. two streams; the split kernel: two groups, one stream).
 // UIN: the uniforms come from u_in (tests pin them) instead of the streams -- a template
 // flag, not a runtime test: a runtime branch around the u loads made the compiler wait
 // vmcnt(0) before every group's math, draining every load in flight (the prefetch of the
@@ -448,14 +452,12 @@ CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_
   // the thread's uniform stream, drawn group by group in stream order (8 uniforms live at
   // a time, not 32: the registers go to resident waves instead)
   Xoro128 rng;
-  if constexpr (!UIN) {
-    rng.seed(qrng_key(seed, offset), ((uint64_t)tile << 8) | (uint32_t)st);
-    float skip;
-    for (int i = 0; i < g0 * (kQPer / 2); ++i) rng.next2(skip, skip);  // wave-uniform (g0 per wave)
-  }
   const bool dense = dense_out != nullptr;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
+    if constexpr (!UIN) {
+      if (((g0 + g) & 1) == 0) rng.seed(qrng_key(seed, offset), qstream_id(tile, g0 + g, st));
+    }
     const int64_t e0 = eb + g * GS;
     float lf[kQPer];
 #if CHOCO_QCHECK

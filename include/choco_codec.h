@@ -280,9 +280,10 @@ int choco_sign_local_decode(const float* x, int64_t n, const int64_t* seg_off, i
  *   level   = floor(lf) + (u < lf - floor(lf)),  u = u_in[e] if given, else
  *             this codec's stream (the reference draws torch.rand_like,
  *             sparsification.py:91): key = splitmix64_mix(seed + (offset+1) *
- *             0xD1B54A32D192ED03); element e belongs to stream
- *             sid = ((e >> 13) << 8) | ((e & 8191) >> 3 & 255) at position
- *             p = ((e & 8191) >> 11) * 8 + (e & 7); stream sid is xoroshiro128+
+ *             0xD1B54A32D192ED03); with g = (e & 8191) >> 11, element e
+ *             belongs to stream sid = ((e >> 13) << 9) | ((g >> 1) << 8) |
+ *             ((e & 8191) >> 3 & 255) at position p = (g & 1) * 8 + (e & 7)
+ *             (16 uniforms per stream); stream sid is xoroshiro128+
  *             (a=24, b=16, c=37) started from (splitmix64_mix(z),
  *             splitmix64_mix(z + 0x9E3779B97F4A7C15)), z = key + (2 sid + 1) *
  *             0x9E3779B97F4A7C15; its output number p / 2, r = s0 + s1, gives

@@ -398,18 +398,20 @@ def _xoro_scalar_stream(key, sid, count):
 
 
 def test_qsgd_uniform_stream_mapping():
-    """The device stream layout (qsgd.hip kQStreamTile): element e is position
-    ((e & 8191) >> 11) * 8 + (e & 7) of stream ((e >> 13) << 8) | ((e & 8191) >> 3 & 255)."""
+    """The device stream layout (qsgd.hip qstream_id): with g = (e & 8191) >> 11, element e
+    is position (g & 1) * 8 + (e & 7) of stream ((e >> 13) << 9) | ((g >> 1) << 8) |
+    ((e & 8191) >> 3 & 255): 16 uniforms per stream, two streams per thread slot."""
     seed, offset = 0xABCDEF, 2
     key = O.qrng_key(seed, offset)
     for tile, t in ((0, 0), (0, 255), (3, 17)):
-        r = _xoro_scalar_stream(key, (tile << 8) | t, 16)
-        idx = np.array([tile * 8192 + g * 2048 + 8 * t + c for g in range(4) for c in range(8)])
-        want = []
-        for p in range(32):
-            v = r[p // 2]
-            want.append(((v >> 40) if p % 2 == 0 else (v >> 16) & 0xFFFFFF) * 2.0 ** -24)
-        assert np.array_equal(O.qsgd_uniforms_at(idx, seed, offset), np.array(want, dtype=np.float32))
+        for h in range(2):
+            r = _xoro_scalar_stream(key, (tile << 9) | (h << 8) | t, 8)
+            idx = np.array([tile * 8192 + g * 2048 + 8 * t + c for g in (2 * h, 2 * h + 1) for c in range(8)])
+            want = []
+            for p in range(16):
+                v = r[p // 2]
+                want.append(((v >> 40) if p % 2 == 0 else (v >> 16) & 0xFFFFFF) * 2.0 ** -24)
+            assert np.array_equal(O.qsgd_uniforms_at(idx, seed, offset), np.array(want, dtype=np.float32))
     # distribution: 2^20 uniforms, 64 bins within 5 sigma, mean 1/2
     u = O.qsgd_uniforms(1 << 20, 11, 0)
     h = np.bincount((u * 64).astype(np.int64), minlength=64)
