@@ -532,6 +532,15 @@ CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_
 #ifndef CHOCO_QQ_HALF
 #define CHOCO_QQ_HALF 1
 #endif
+#ifndef CHOCO_QQ_LOOP_ASM  // the looping kernel's prefetch as asm loads (see the kernel)
+#define CHOCO_QQ_LOOP_ASM 1
+#endif
+#ifndef CHOCO_QQ_DIAG_COAL
+#define CHOCO_QQ_DIAG_COAL 0
+#endif
+#ifndef CHOCO_QQ_DIAG_NOMATH
+#define CHOCO_QQ_DIAG_NOMATH 0
+#endif
 #ifndef CHOCO_QQ_HWAVES
 #define CHOCO_QQ_HWAVES 6
 #endif
@@ -576,8 +585,14 @@ __global__ __launch_bounds__(kQThreads * H, H == 1 ? (XH ? 4 : CHOCO_QQ_WAVES) :
     float4 a[NG][2];
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
+#if CHOCO_QQ_DIAG_COAL  // diagnostic only (wrong results): full-line loads, lane l at float4 l and 64 + l of its wave's run
+      const int64_t wb = eb - (int64_t)(st & 63) * kQPer;
+      a[g][0] = ld_quant4(x + wb + g * GS + 4 * (st & 63));
+      a[g][1] = ld_quant4(x + wb + g * GS + 256 + 4 * (st & 63));
+#else
       a[g][0] = ld_quant4(x + eb + g * GS);
       a[g][1] = ld_quant4(x + eb + g * GS + 4);
+#endif
     }
     if constexpr (XH) {
 #pragma unroll
@@ -596,7 +611,20 @@ __global__ __launch_bounds__(kQThreads * H, H == 1 ? (XH ? 4 : CHOCO_QQ_WAVES) :
   const QParam P = qparam(norms, seg_off, n, sg0, s_levels, biased != 0);
   QDiv D;
   D.init(P.norm);
+#if CHOCO_QQ_DIAG_NOMATH  // diagnostic only (wrong results): the loads and a sign-byte store, no math
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    uint32_t sb = 0;
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) sb |= d[g][c] < 0.f ? (1u << c) : 0u;
+#if CHOCO_QQ_DIAG_NOMATH == 2  // loads only (a store that never happens keeps them alive)
+    if (__float_as_uint(d[g][0]) == 0x7fc01234u)
+#endif
+    sign_plane[(eb + g * GS) / kQPer] = (uint8_t)sb;
+  }
+#else
   quant_tile_math<CW, NG, UIN>(d, tile, n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out, g0, st);
+#endif
 }
 
 // Single-segment buffers (the flat path, BASELINE cfg 3): a grid of resident workgroups
@@ -654,7 +682,23 @@ __global__ __launch_bounds__(kQThreads, 4) void qsgd_quant_loop_kernel(
     const int64_t jn = j + (int64_t)gridDim.x;
     const bool more = jn < full_cnt;  // workgroup-uniform
     float4 b[kQG][2], bh[kQG][2];
+#if CHOCO_QQ_LOOP_ASM
+    // the next tile's loads as asm: the compiler's wait pass does not see them, so it
+    // cannot make the current tile's math wait for them (it did: vmcnt at the loop head
+    // covered two of them); one counted wait after the math, tied to the registers
+    choco_f32x4 bq[kQG][2];
+    static_assert(!XH, "the asm prefetch covers the plain delta");
+    if (more) {
+      const int64_t ebn = tile_of(jn) * kQStreamTile + (int64_t)threadIdx.x * kQPer;
+#pragma unroll
+      for (int g = 0; g < kQG; ++g) {
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bq[g][0]) : "v"(x + ebn + g * GS) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bq[g][1]) : "v"(x + ebn + g * GS + 4) : "memory");
+      }
+    }
+#else
     if (more) load(tile_of(jn), b, bh);
+#endif
     float d[kQG][kQPer];
 #pragma unroll
     for (int g = 0; g < kQG; ++g) {
@@ -668,6 +712,18 @@ __global__ __launch_bounds__(kQThreads, 4) void qsgd_quant_loop_kernel(
     }
     quant_tile_math<CW, kQG, UIN>(d, tile_of(j), n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out);
     if (!more) break;
+#if CHOCO_QQ_LOOP_ASM
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(bq[0][0]), "+v"(bq[0][1]), "+v"(bq[1][0]), "+v"(bq[1][1]), "+v"(bq[2][0]), "+v"(bq[2][1]),
+                   "+v"(bq[3][0]), "+v"(bq[3][1])
+                 :
+                 : "memory");
+#pragma unroll
+    for (int g = 0; g < kQG; ++g) {
+      b[g][0] = make_float4(bq[g][0].x, bq[g][0].y, bq[g][0].z, bq[g][0].w);
+      b[g][1] = make_float4(bq[g][1].x, bq[g][1].y, bq[g][1].z, bq[g][1].w);
+    }
+#endif
 #pragma unroll
     for (int g = 0; g < kQG; ++g) {
       a[g][0] = b[g][0];

@@ -67,6 +67,19 @@ VARIANTS = {
     "k34ws1": ["CHOCO_K34_WAVE_SELECT=1"],
     "seg_loop1_g512": ["CHOCO_SEG_LOOP=1", "CHOCO_SEG_LOOP_GRID=512"],
     "qq_h0": ["CHOCO_QQ_HALF=0"],
+    # timing diagnostics only, WRONG results (never in a parity run)
+    "qqdiag_coal": ["CHOCO_QQ_DIAG_COAL=1"],
+    "qqdiag_nomath": ["CHOCO_QQ_DIAG_NOMATH=1"],
+    "qqdiag_coal_nomath": ["CHOCO_QQ_DIAG_COAL=1", "CHOCO_QQ_DIAG_NOMATH=1"],
+    "qqdiag_loadonly": ["CHOCO_QQ_DIAG_NOMATH=2"],
+    "qqdiag_nomath_nt": ["CHOCO_QQ_DIAG_NOMATH=1", "CHOCO_QQUANT_NT=1"],
+    "qqdiag_nomath_fwd": ["CHOCO_QQ_DIAG_NOMATH=1", "CHOCO_QQUANT_REV=0"],
+    "qqdiag_nomath_h0": ["CHOCO_QQ_DIAG_NOMATH=1", "CHOCO_QQ_HALF=0"],
+    "qq_nt_h": ["CHOCO_QQUANT_NT=1"],
+    "qn_plain_qq_nt": ["CHOCO_QNORM_NT=0", "CHOCO_QQUANT_NT=1"],
+    "qq_loop_asm": ["CHOCO_QQ_LOOP=1", "CHOCO_QQ_LOOP_ASM=1"],
+    "qq_loop_asm_g512": ["CHOCO_QQ_LOOP=1", "CHOCO_QQ_LOOP_ASM=1", "CHOCO_QQ_GRID=512"],
+    "qq_fwd_h": ["CHOCO_QQUANT_REV=0"],
     "qq_ring_d3w3": ["CHOCO_QQ_RING=1", "CHOCO_QQ_RING_D=3", "CHOCO_QQ_RING_WGS=3"],
     "qq_ring_d2w4": ["CHOCO_QQ_RING=1", "CHOCO_QQ_RING_D=2", "CHOCO_QQ_RING_WGS=4"],
     "qq_hw8": ["CHOCO_QQ_HWAVES=8"],
