@@ -292,6 +292,25 @@ class SegmentPlan:
                 buf = self._ws[key] = _new_workspace(dev, max(self.ws_bytes, 256))
             return buf
 
+    def __del__(self):
+        # The plan's workspaces go with it, and so does the codec's host-side state keyed by
+        # their addresses (warm windows, the pinned miss flag): a later workspace at the
+        # same address must not inherit it.  The device may still write the miss flag, so
+        # the devices are synchronised before it is freed.
+        try:
+            bufs = list(self._ws.values())
+            self._ws.clear()
+            if not bufs:
+                return
+            for d in {b.device.index for b in bufs}:
+                torch.cuda.synchronize(d)
+            L = lib()
+            for buf in bufs:
+                _status.pop(buf.data_ptr(), None)
+                L.choco_topk_workspace_reset(_ptr(buf), buf.numel())
+        except Exception:  # interpreter shutdown: the library or torch may be gone
+            pass
+
     def drop_workspace(self, dev):
         """Forget this plan's workspace on the current stream of `dev` (after a failed
         call: its histograms may not be zeroed any more); the next call starts cold on

@@ -318,6 +318,33 @@ def test_release_workspaces_then_recompute():
     assert np.array_equal(host(i2).astype(np.int64), oi)
 
 
+def test_dropped_plan_frees_its_workspace():
+    """A SegmentPlan that is garbage-collected takes its device workspaces with it (the
+    status registry holds addresses, not tensors) and the codec's host-side state keyed
+    by them; a new plan afterwards (possibly at the same address) starts cold and exact
+    (plans built per layout leaked their workspaces)."""
+    import gc
+    from chocosgd_amd import codec
+    lens = [300_000, 7, 1_200_000, 4096, 50_000]
+    x = randn(sum(lens), 91)
+    torch.cuda.synchronize()
+    gc.collect()
+    base = torch.cuda.memory_allocated()
+    for rep in range(3):
+        plan = codec.SegmentPlan(lens, 0.99, x.device)
+        for _ in range(2):  # cold, then warm (the miss flag is allocated)
+            vals, idx = codec.topk_segmented(x, plan)
+        torch.cuda.synchronize()
+        assert torch.cuda.memory_allocated() > base
+        ov, oi, ks = O.topk_segmented(host(x), lens, 0.99)
+        assert np.array_equal(host(idx).astype(np.int64), oi)
+        assert same_bits(host(vals), ov)
+        del plan, vals, idx
+        gc.collect()
+        torch.cuda.synchronize()
+        assert torch.cuda.memory_allocated() <= base, (rep, torch.cuda.memory_allocated(), base)
+
+
 def _check_topk(x, k, xh=None):
     from chocosgd_amd import codec
     vals, idx = codec.topk(x, k, xhat=xh)
