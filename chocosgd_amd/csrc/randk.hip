@@ -64,17 +64,20 @@ constexpr int kRkTileBits = 18;
 constexpr int64_t kRkTile = int64_t(1) << kRkTileBits;  // elements per tile: a 32 KB bitmap
 constexpr int kRkThreads = 1024;                         // R1
 constexpr int kRkWords = (int)(kRkTile / 32);            // 8192 bitmap words per tile
-// R2: kRkQ workgroups per tile, each one quarter of the tile's bitmap (2^16 bits,
-// 8 KB of LDS) with kRkQThreads threads of 8 words (256 bits) each: ~6 small
-// workgroups per CU instead of 1-2 large ones (382 tiles on 256 CUs left half the
-// CUs with two 1024-thread tiles and set the tail: 44.7 us at 100M).
+// R2: kRkQ workgroups per tile, each 1 / kRkQ of the tile's bitmap (8: 2^15 bits,
+// 4 KB of LDS) with kRkQThreads threads of kRkWpt words each: many small workgroups
+// per CU instead of 1-2 large ones (382 tiles on 256 CUs left half the CUs with two
+// 1024-thread tiles and set the tail: 44.7 us at 100M).  r04 same-box A/B (three
+// passes): R2 itself 41.6-41.7 (4) / 41.1-41.3 (8) / 41.8-43.3 us (16); the sparse
+// accumulate after it 78.7-79.3 / 77.4-77.7 / 76.1-76.9 us; step 0.1406-0.1415 /
+// 0.1384-0.1405 / 0.1385-0.1391 ms.
 #ifndef CHOCO_RK_Q  // workgroups per tile (A/B knob)
-#define CHOCO_RK_Q 4
+#define CHOCO_RK_Q 8
 #endif
 constexpr int kRkQ = CHOCO_RK_Q;
 constexpr int kRkQThreads = 256;
-constexpr int kRkQWords = kRkWords / kRkQ;               // 2048
-constexpr int kRkWpt = kRkQWords / kRkQThreads;          // 8 words (256 bits) per thread
+constexpr int kRkQWords = kRkWords / kRkQ;               // 1024 at kRkQ = 8
+constexpr int kRkWpt = kRkQWords / kRkQThreads;          // 4 words (128 bits) per thread at kRkQ = 8
 constexpr int kRkMaxSegTiles = (int)((int64_t(1) << 31) >> kRkTileBits);  // 8192 tiles of one segment
 constexpr int kRkGroups = 256;   // R1 workgroups drawing one segment's counts (count-matrix row length)
 constexpr int kRkList = 4096;    // R2: positions of a quarter listed in LDS (denser quarters emit per thread)
@@ -210,7 +213,7 @@ CHOCO_DEV uint32_t pick_word(const uint32_t (&w)[kRkWpt], int q) {  // w[q] by s
   return r;
 }
 
-// R2: one quarter of a tile -> the tile's count and output offset (its rows of H
+// R2: one quarter of a tile ("quarter": the 1 / kRkQ part a workgroup owns) -> the tile's count and output offset (its rows of H
 // and P), the quarter's bitmap (every draw of the tile is evaluated; the ones
 // below the quarter are counted, which places the quarter inside the tile without
 // any exchange between workgroups), the ordered emission with the gather.  Up to
@@ -282,7 +285,7 @@ __global__ __launch_bounds__(kRkQThreads) void randk_tile_kernel(const float* __
     block_excl_scan(nb, scratch, &below);  // (ends with a barrier: the bitmap is complete)
   }
   RKSTAMP(8192 + blockIdx.x, 2);
-  // thread t owns bits [256 t, 256 t + 256) of the quarter: rank of its first set bit
+  // thread t owns bits [32 kRkWpt t, 32 kRkWpt (t + 1)) of the quarter: rank of its first set bit
   uint32_t w[kRkWpt];
   uint32_t mine = 0;
 #pragma unroll

@@ -15,6 +15,8 @@ VARIANTS = {
     "qq_nt": ["CHOCO_QQUANT_NT=1"],
     "qq_fwd": ["CHOCO_QQUANT_REV=0"],
     "rk_q2": ["CHOCO_RK_Q=2"],
+    "rk_q8": ["CHOCO_RK_Q=8"],
+    "rk_q16": ["CHOCO_RK_Q=16"],
     "seg_wnt0": ["CHOCO_SEG_WARM_NT=0"],
     "acc_nt1": ["CHOCO_ACC_NT=1"],
     "acc_next0": ["CHOCO_ACC_NEXT=0"],
