@@ -82,10 +82,13 @@ class TopkStatus:
     def __init__(self, ws):
         self.ptr = ws.data_ptr()
         self.device = ws.device
+        # the stream the workspace belongs to (workspaces are per (device, stream): it is the
+        # current stream when the workspace is taken, codec.workspace / SegmentPlan.workspace)
+        self.stream = torch.cuda.current_stream(ws.device)
 
     def check(self, wait=False):
         if wait:
-            torch.cuda.current_stream(self.device).synchronize()
+            self.stream.synchronize()
         bad = int(lib().choco_topk_host_status(ctypes.c_void_p(self.ptr), 1, _stream(self.device)))
         if bad < 0:
             raise RuntimeError(f"choco_topk_host_status failed: {_lib.last_error()}")

@@ -2168,6 +2168,9 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   float* cval = reinterpret_cast<float*>(base + L.off_cval);
   uint32_t* cidx = reinterpret_cast<uint32_t*>(base + L.off_cidx);
   if (status.dev == nullptr) status = StatusSink{&ctrl->status, host_status_dev(ws)};
+  CHOCO_REQUIRE(status.host != nullptr,
+                "top-k: could not map the pinned host mirror of the workspace status word (hipHostMalloc / "
+                "hipHostGetDevicePointer failed), so a failed exact-fallback wait could not be reported");
   uint32_t hs_lo = 0;
   uint64_t hs_hi = 0;
   if (MODE == kHash) {
@@ -2260,14 +2263,17 @@ uint32_t* host_status_dev(const void* ws) {
   std::lock_guard<std::mutex> g(g_hs_mu);
   auto it = g_hs.find(ws);
   if (it != g_hs.end()) return it->second.dev;
-  HostStatus hs{nullptr, nullptr};
+  // A failure is not cached: this call fails (the callers raise), the next one retries.
+  // (A call that ran without the mirror could not report a bounded wait that gave up.)
   void* h = nullptr;
-  if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
-    hs.host = static_cast<uint32_t*>(h);
-    __atomic_store_n(hs.host, 0u, __ATOMIC_RELEASE);
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess) hs.dev = static_cast<uint32_t*>(d);
+  if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || d == nullptr) {
+    (void)hipHostFree(h);
+    return nullptr;
   }
+  HostStatus hs{static_cast<uint32_t*>(h), static_cast<uint32_t*>(d)};
+  __atomic_store_n(hs.host, 0u, __ATOMIC_RELEASE);
   g_hs.emplace(ws, hs);
   return hs.dev;
 }

@@ -1097,10 +1097,13 @@ static int segmented(const float* x, const float* xhat, const int64_t* plan_dev,
     if (p[5] != 0) continue;
     const Gossip gseg{gs.mem ? gs.mem + p[0] : nullptr, gs.gamma};
     const size_t fb = align_up(topk_ws_bytes(p[1]), 256);
+    uint32_t* hs = host_status_dev(ws);
+    CHOCO_REQUIRE(hs != nullptr,
+                  "top-k: could not map the pinned host mirror of the workspace status word (hipHostMalloc / "
+                  "hipHostGetDevicePointer failed), so a failed exact-fallback wait could not be reported");
     const int rc = topk_pipeline(kData, x + p[0], xhat ? xhat + p[0] : nullptr, p[1], p[2], 0, 1.0f,
                                  out_val + p[3], out_idx + p[3], p[0], base + fo, fb, st, gseg,
-                                 StatusSink{reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_STATUS_OFFSET),
-                                            host_status_dev(ws)});
+                                 StatusSink{reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_STATUS_OFFSET), hs});
     if (rc) return rc;
     fo += fb;
   }

@@ -12,7 +12,8 @@ op sequences, run with torch on the host cores:
   sign+norm : per-tensor L1 norm + SignCompressor.packing with the bit2byte
               step replaced by torch bit ops            (sparsification.py:129-163,
                                                          parallel_choco_v.py:476-558)
-Its outputs are checked against the numpy oracle in tests (same sets / values).
+Its outputs are checked against the reference's golden vectors in tests/test_torch_port.py
+(top-k sets, QSGD with the reference's draws, sign words, the three decompresses).
 Only tests/ and bench.py's cpu_baseline leg may import it.
 """
 import torch

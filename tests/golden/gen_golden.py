@@ -18,6 +18,7 @@ is this repo's convention ("parity unpinned" at that one boundary).
 
 Usage:  python tests/golden/gen_golden.py [generator ...]   (no argument: all)
 """
+import importlib
 import json
 import os
 import sys
@@ -649,6 +650,68 @@ def gen_ecd_all():
     gen_ecd("topk", "ecd_topk_mini_r09", MINI_LAYOUT, "compress_top_k", ratio=0.9)
     gen_ecd("qsgd", "ecd_qsgd_mini_q4", MINI_LAYOUT, "quantize_qsgd", qlevel=4)
     gen_ecd("sign", "ecd_sign_mini", MINI_LAYOUT, "sign")
+
+
+def ref_neighborhood(world, rank):
+    """neighbors_info as the reference's graphs give it: RingGraph for world > 2
+    (topology.py:186-202 mixing matrix, :295-299 get_neighborhood), CompleteGraph for
+    world 2 (topology.py:127,156-162); the constructors' process-group setup is skipped."""
+    topo = importlib.import_module("pcode.utils.topology")
+    if world == 2:
+        g = object.__new__(topo.CompleteGraph)
+        g._mixing_matrix = np.ones((world, world)) / world
+    else:
+        g = object.__new__(topo.RingGraph)
+        g._mixing_matrix, g._rho = g._compute_mixing_matrix_and_rho(world)
+    g._rank = rank
+    return {int(r): float(w) for r, w in g.get_neighborhood().items()}
+
+
+def gen_ring():
+    """A ring of 8 CHOCO workers through the reference (parallel_choco_v.py:229-332 top-k,
+    :476-558 sign): every worker compresses, then every worker uncompresses the messages of
+    ITS neighbourhood only (a strict subset of the world from rank 0's {0, 1, 7} on), so the
+    fixture pins the per-rank neighbour selection and order of a ring larger than 3.
+    Inputs come from tests/_ring.py (seeded); only the outputs are stored."""
+    sys.path.insert(0, os.path.dirname(OUT))
+    import _ring as R
+    nbs = {str(w): [[[r, wt] for r, wt in ref_neighborhood(w, q).items()] for q in range(w)]
+           for w in range(2, 9)}
+    with open(os.path.join(OUT, "ring_neighborhoods.json"), "w") as f:
+        json.dump(nbs, f)
+    print("wrote ring_neighborhoods.json")
+    W, lens = R.RING_WORLD, R.RING_LAYOUT
+    shapes = [(torch.Size([m]), m) for m in lens]
+    ins = [R.ring_inputs(r) for r in range(W)]
+    for kind, name, cls, op in (("topk", "choco_ring8_topk_r09", ref_pcv.CHOCOSparsificationCompressor,
+                                 "compress_top_k"),
+                                ("sign", "choco_ring8_sign", ref_pcv.CHOCOSignCompressor, "sign")):
+        sent, sbs = [], []
+        for r in range(W):
+            x, xh, _, _ = (torch.from_numpy(a) for a in ins[r])
+            comp = make_comp(cls, op, ratio=R.RING_RATIO)
+            sb = {"original_shapes": shapes, "flatten_params": TensorBuffer(split(x, lens)),
+                  "flatten_hat_params": TensorBuffer(split(xh, lens))}
+            comp.compress(sb)
+            comp.aggregator_fn = CaptureAgg()
+            comp.sync(sb)
+            sent.append(comp.aggregator_fn.sent)
+            sbs.append((comp, sb))
+        hat1, mem1 = [], []
+        for r in range(W):
+            nb = ref_neighborhood(W, r)
+            comp, sb = sbs[r]
+            nhp = {r: TensorBuffer(split(torch.from_numpy(ins[r][2]), lens)),
+                   "memory": TensorBuffer(split(torch.from_numpy(ins[r][3]), lens))}
+            comp.aggregator_fn = ReplayAgg([{q: sent[q][c] for q in nb} for c in range(len(sent[0]))])
+            comp.sync(sb)
+            comp.uncompress(sb, nhp, nb)
+            hat1.append(nhp[r].buffer.numpy().copy())
+            mem1.append(nhp["memory"].buffer.numpy().copy())
+        extra = {}
+        if kind == "sign":  # the reference's fp32 CPU L1 norms (SURVEY 0.4d drift), per worker
+            extra["norms"] = np.stack([sent[r][0].numpy() for r in range(W)])
+        save(name, layout=np.array(lens, dtype=np.int64), hat1=np.stack(hat1), mem1=np.stack(mem1), **extra)
 
 
 STEP_LAYOUT = MINI_LAYOUT + [1029, 3]

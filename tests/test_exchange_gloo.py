@@ -1,4 +1,5 @@
-"""Multi-process exchange (the CHOCO sync step) over gloo on CPU, world sizes 2 and 3."""
+"""Multi-process exchange (the CHOCO sync step) over gloo on CPU, world sizes 2, 3, 4 and 8
+(rings larger than 3: each rank exchanges with 2 of its N - 1 peers)."""
 import os
 import socket
 
@@ -49,7 +50,7 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_decentralized_exchange(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -67,6 +68,7 @@ def test_decentralized_exchange(world):
         for dtype in (torch.int32, torch.uint8):
             got = out[rank][str(dtype)]
             assert sorted(got) == sorted(nb)
+            assert len(nb) == min(world, 3)  # self + the two ring neighbours (both, for world 2)
             for r in nb:
                 assert got[r] == (torch.arange(37) * (r + 1)).to(dtype).tolist()
         for r, got in out[rank]["ranged"].items():

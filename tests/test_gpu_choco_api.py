@@ -269,3 +269,62 @@ def test_accumulate_more_than_8_messages(kind):
         O.qsgd_accumulate(h0, m0, decoded, w, self_slot)
     assert same_bits(host(hat), h0)
     assert same_bits(host(mem), m0)
+
+
+@pytest.mark.parametrize("kind,name", [("topk", "choco_ring8_topk_r09"), ("sign", "choco_ring8_sign")])
+def test_choco_ring8_api(kind, name):
+    """A ring of 8 workers through the drop-in (compress every worker, then uncompress every
+    worker's own RingGraph neighbourhood, a strict subset of the world) against the
+    reference's ring (tests/golden gen_ring): top-k bit-exact; sign within the reference's
+    fp32 CPU norm drift (test_choco_sign_api_close), and bit-exact with its norms pinned
+    through the fused receiver."""
+    import os
+    import sys
+    from conftest import ROOT, golden_json
+    from chocosgd_amd import codec
+    from chocosgd_amd.parallel_choco import CHOCOCompressor
+    from chocosgd_amd.tensor_buffer import TensorBuffer
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _ring as R
+    g = golden(name)
+    lens = g["layout"].tolist()
+    W = R.RING_WORLD
+    nbs = golden_json("ring_neighborhoods.json")[str(W)]
+    shapes = [(torch.Size([m]), m) for m in lens]
+    ins = [R.ring_inputs(r) for r in range(W)]
+    op = "compress_top_k" if kind == "topk" else "sign"
+    args = dict(aggregator=None, comm_op=op, comm_device="gpu", compress_ratio=R.RING_RATIO, quantize_level=4,
+                is_biased=False, backend="nccl", use_ipc=False)
+    sent, comps = [], []
+    for r in range(W):
+        comp = CHOCOCompressor(**args)
+        sb = {"original_shapes": shapes, "flatten_params": TensorBuffer(_split(dev(ins[r][0]), lens)),
+              "flatten_hat_params": TensorBuffer(_split(dev(ins[r][1]), lens))}
+        comp.compress(sb)
+        comp.compressor_fn.aggregator_fn = CaptureAgg()
+        comp.sync(sb)
+        sent.append(comp.compressor_fn.aggregator_fn.sent)
+        comps.append((comp, sb))
+    for r in range(W):
+        nb = {int(q): float(x) for q, x in nbs[r]}
+        comp, sb = comps[r]
+        nhp = {r: TensorBuffer(_split(dev(ins[r][2]), lens)), "memory": TensorBuffer(_split(dev(ins[r][3]), lens))}
+        comp.compressor_fn.aggregator_fn = ReplayAgg([{q: sent[q][c] for q in nb} for c in range(len(sent[0]))])
+        comp.sync(sb)
+        comp.uncompress(sb, nhp, nb)
+        if kind == "topk":
+            assert same_bits(host(nhp[r].buffer), g["hat1"][r]), r
+            assert same_bits(host(nhp["memory"].buffer), g["mem1"][r]), r
+            continue
+        assert np.allclose(host(nhp[r].buffer), g["hat1"][r], rtol=1e-5, atol=1e-6), r
+        assert np.allclose(host(nhp["memory"].buffer), g["mem1"][r], rtol=1e-5, atol=1e-6), r
+        # the same neighbourhood through the fused receiver with the reference's norms
+        ranks = list(nb)
+        hw = (len(lens) + 3) // 4 * 4
+        parts = [(sent[q][0][hw:], dev(g["norms"][q])) for q in ranks]
+        hat, mem = dev(ins[r][2]), dev(ins[r][3])
+        lay_off = torch.tensor([0] + list(np.cumsum(lens)), dtype=torch.int64, device=DEV)
+        codec.sign_accumulate(parts, [nb[q] for q in ranks], ranks.index(r), sum(lens), mem, xhat_self=hat,
+                              seg_off=lay_off, nseg=len(lens))
+        assert same_bits(host(hat), g["hat1"][r]), r
+        assert same_bits(host(mem), g["mem1"][r]), r

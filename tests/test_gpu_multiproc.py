@@ -1,5 +1,5 @@
 """The CHOCO gossip round across PROCESSES: CHOCOCompressor compress -> sync ->
-uncompress on 2 and 3 ranks sharing the one GPU, exchanging through the
+uncompress on 2, 3, 4 and 8 ranks sharing the one GPU, exchanging through the
 reference's DecentralizedAggregation over gloo with comm_device="cpu"
 (communication.py:246-291, parallel_choco_v.py:262-310).  Every worker's
 x_hat / memory is compared with the oracle's round over the same inputs.
@@ -14,7 +14,7 @@ import sys
 import numpy as np
 import pytest
 
-from conftest import ROOT, same_bits
+from conftest import ROOT, golden_json, same_bits
 from oracle import choco_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -23,10 +23,9 @@ import _mp_choco_worker as W  # noqa: E402
 
 
 def _neighborhood(rank, world):
-    if world == 2:
-        return {0: 0.5, 1: 0.5}
-    ranks = sorted({(rank - 1) % world, rank, (rank + 1) % world})
-    return {r: 1.0 / 3 for r in ranks}
+    """The reference's own mixing-matrix row (RingGraph / CompleteGraph, generated from
+    topology.py:122-299 into tests/golden/ring_neighborhoods.json)."""
+    return {int(r): float(w) for r, w in golden_json("ring_neighborhoods.json")[str(world)][rank]}
 
 
 def _hdr(nseg):
@@ -35,6 +34,10 @@ def _hdr(nseg):
 
 @pytest.mark.parametrize("comm_op,world", [("compress_top_k", 2), ("compress_top_k", 3), ("compress_random_k", 3),
                                            ("sign", 2), ("sign", 3), ("quantize_qsgd", 3),
+                                           # rings larger than 3 (cfg 4 / 5 are 8-worker rings): every
+                                           # rank exchanges with 2 of N - 1 peers and skips the rest
+                                           ("compress_top_k", 4), ("sign", 4), ("quantize_qsgd", 4),
+                                           ("compress_top_k", 8), ("sign_chunked", 4),
                                            ("quantize_qsgd_chunked", 2), ("quantize_qsgd_chunked", 3),
                                            ("sign_chunked", 2), ("sign_chunked", 3),
                                            ("sign_chunked_refagg", 3)])

@@ -2,7 +2,7 @@
 choco_gossip_topk_compress_accumulate) -- the top-k message plus x_hat += q and
 memory += w q applied while the message is emitted -- against the unfused sequence
 (topk, then choco_sparse_accumulate of the self message, parallel_choco_v.py:307-310)
-and the oracle, bit for bit, on every emission path: K34 (cold and warm calls), the
+and the oracle (the message, and x_hat / memory directly), bit for bit, on every emission path: K34 (cold and warm calls), the
 exact fallback inside K34 (tie-heavy and all-equal inputs), the one-workgroup path
 (n <= 65536) and k == n."""
 import numpy as np
@@ -48,6 +48,7 @@ def test_topk_fold_matches_unfused(kind, n, ratio, fold_memory):
     x, hat, mem = _inputs(kind, n, 600 + n % 991)
     hat_a, mem_a = hat.clone(), mem.clone()
     hat_b, mem_b = hat.clone(), mem.clone()
+    h_o, m_o = host(hat), host(mem)  # the oracle's x_hat / memory (direct, not only transitive)
     for call in range(3):  # cold, then warm calls (the window carried in the workspace)
         d = (host(x) - host(hat_a)).astype(np.float32)
         va, ia = codec.topk(x, k, xhat=hat_a, fold=(hat_a, mem_a if fold_memory else None, w))
@@ -62,6 +63,9 @@ def test_topk_fold_matches_unfused(kind, n, ratio, fold_memory):
         else:
             codec.sparse_accumulate(va, ia, mem_a, w)  # memory's self update in its turn
             assert same_bits(host(mem_a), host(mem_b)), call
+        O.sparse_accumulate(h_o, m_o, ov, oi, w)
+        assert same_bits(host(hat_a), h_o), call
+        assert same_bits(host(mem_a), m_o), call
         x += 0.01 * randn(n, 7 + call)  # the next call compresses a moved delta
 
 
@@ -96,8 +100,9 @@ def test_gossip_topk_fold_sequence(fold_memory):
     mem = hat + 0.05 * torch.randn(n, generator=g, device=DEV)
     xa, hat_a, mem_a = x.clone(), hat.clone(), mem.clone()
     xb, hat_b, mem_b = x.clone(), hat.clone(), mem.clone()
+    h_o, m_o = host(hat), host(mem)
     for step in range(5):
-        xo = O.gossip_step(host(xa), host(mem_a), host(hat_a), 0.9)
+        xo = O.gossip_step(host(xa), m_o, h_o, 0.9)
         d = (xo - host(hat_a)).astype(np.float32)
         va, ia = codec.topk(xa, k, xhat=hat_a, gossip=(mem_a, 0.9), fold=(hat_a, mem_a if fold_memory else None, 1.0))
         vb, ib = codec.topk(xb, k, xhat=hat_b, gossip=(mem_b, 0.9))
@@ -109,3 +114,5 @@ def test_gossip_topk_fold_sequence(fold_memory):
         assert np.array_equal(host(ia).astype(np.int64), oi)
         assert same_bits(host(va), ov)
         assert same_bits(host(hat_a), host(hat_b)) and same_bits(host(mem_a), host(mem_b))
+        O.sparse_accumulate(h_o, m_o, ov, oi, 1.0)
+        assert same_bits(host(hat_a), h_o) and same_bits(host(mem_a), m_o)

@@ -1,9 +1,12 @@
 """Pin the numpy oracle against golden vectors produced by the REFERENCE itself
 (tests/golden/gen_golden.py imports dl_code/pcode).  CPU only."""
+import os
+import sys
+
 import numpy as np
 import pytest
 
-from conftest import golden, golden_json, same_bits
+from conftest import ROOT, golden, golden_json, same_bits
 from oracle import choco_oracle as O
 
 TOPK_CASES = ["topk_n1000_r09", "topk_n65536_r099", "topk_n262144_r099", "topk_n30011_r09", "topk_n50_k1",
@@ -561,3 +564,54 @@ def test_oracle_segmented_randk():
     assert same_bits(v, d[i])
     # the flat draw is segment 0 of the same key
     assert np.array_equal(O.randk_indices(1000, 100, 42), O.randk_segment_indices(1000, 100, O.rk_derive(O.randk_key(42), 0)))
+
+
+# ---------------------------------------------------------------------------- ring > 3
+def test_ring_neighborhoods_match_reference_graphs():
+    """communication.neighborhood against the reference's own RingGraph (world > 2) /
+    CompleteGraph (world 2) rows, generated from topology.py:122-299: same ranks, same
+    ascending order, same float64 weights -- including worlds 4..8, where a rank's
+    neighbourhood is a strict subset of the world."""
+    from chocosgd_amd.communication import neighborhood
+    tab = golden_json("ring_neighborhoods.json")
+    for w, rows in tab.items():
+        for rank, row in enumerate(rows):
+            got = neighborhood(rank, int(w))
+            assert list(got.items()) == [(int(r), float(x)) for r, x in row], (w, rank)
+
+
+def _ring_replay(kind, g):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _ring as R
+    lens = g["layout"].tolist()
+    W = R.RING_WORLD
+    nbs = golden_json("ring_neighborhoods.json")[str(W)]
+    ins = [R.ring_inputs(r) for r in range(W)]
+    msgs = []
+    for r in range(W):
+        d = (ins[r][0] - ins[r][1]).astype(np.float32)
+        if kind == "topk":
+            vals, idx, _ = O.topk_segmented(d, lens, R.RING_RATIO)
+            msgs.append((vals, idx))
+        else:
+            assert np.allclose(O.l1_norms(d, lens), g["norms"][r], rtol=1e-5, atol=0)
+            msgs.append((O.sign_pack(d), g["norms"][r]))  # the reference's fp32 norms pinned
+    for r in range(W):
+        hat, mem = ins[r][2].copy(), ins[r][3].copy()
+        ranks = [int(q) for q, _ in nbs[r]]
+        weights = [float(x) for _, x in nbs[r]]
+        if kind == "topk":
+            for q, wq in zip(ranks, weights):
+                O.sparse_accumulate(hat if q == r else None, mem, msgs[q][0], msgs[q][1], wq)
+        else:
+            O.sign_accumulate(hat, mem, [msgs[q] for q in ranks], weights, ranks.index(r), lens)
+        assert same_bits(hat, g["hat1"][r]), (kind, r)
+        assert same_bits(mem, g["mem1"][r]), (kind, r)
+
+
+@pytest.mark.parametrize("kind,name", [("topk", "choco_ring8_topk_r09"), ("sign", "choco_ring8_sign")])
+def test_choco_ring8_round(kind, name):
+    """A ring of 8 through the reference (every worker's x_hat / memory after uncompress of
+    its own neighbourhood's messages, parallel_choco_v.py:291-310 / :549-558): the oracle,
+    replaying each rank's neighbourhood from the reference's RingGraph, is bit-exact."""
+    _ring_replay(kind, golden(name))
