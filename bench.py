@@ -59,10 +59,10 @@ GAMMA = 0.9  # consensus_stepsize (parameters.py:126 default)
 # kernels (profile names) of each stage
 STAGES = {
     "topk": (["topk_bounds", "topk_stream", "topk_finish", "topk_exact", "topk_all"],
-             ["sparse_accumulate"]),
+             ["sparse_accumulate", "sparse_split", "sparse_acc_multi"]),
     "topk_seg": (["topk_seg_hist", "topk_seg_collect", "topk_seg_fine", "topk_seg_count", "topk_seg_emit",
-                  "topk_bounds", "topk_stream", "topk_finish"], ["sparse_accumulate"]),
-    "randk": (["randk_count", "randk_tile"], ["sparse_accumulate"]),
+                  "topk_bounds", "topk_stream", "topk_finish"], ["sparse_accumulate", "sparse_split", "sparse_acc_multi"]),
+    "randk": (["randk_count", "randk_tile"], ["sparse_accumulate", "sparse_split", "sparse_acc_multi"]),
     "qsgd": (["qsgd_norm", "qsgd_quantize"], ["qsgd_accumulate"]),
     "sign": (["sign_pack"], ["sign_accumulate"]),
 }
@@ -83,6 +83,12 @@ def parse():
     p.add_argument("--fold", action="store_true",
                    help="top-k: fold the self message's uncompress (x_hat, and memory when the self rank is first) "
                         "into the compress emission (choco_topk_compress_accumulate)")
+    p.add_argument("--ring3-loopback", action="store_true",
+                   help="sparse codecs on one GPU: each step applies the self message plus two neighbour messages "
+                        "(compressed from other resident deltas, no exchange) -- a ring worker's receive (cfg 4)")
+    p.add_argument("--accumulate", default="multi", choices=["multi", "per_message"],
+                   help="sparse receive: one sweep over all messages (choco_sparse_accumulate_multi) or one "
+                        "choco_sparse_accumulate launch per message (the A/B)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the host-resident (PCIe-inclusive) leg")
     p.add_argument("--lib", default=None, help=argparse.SUPPRESS)
@@ -176,6 +182,35 @@ class Worker:
             self.msg = torch.zeros(4 + codec.sign_words(self.n), dtype=torch.int32, device=dev)
             self.wire = (self.msg[4:], self.msg[:4].view(torch.float32)[:1])
         self.recv = {r: torch.empty_like(self.msg) for r in self.peers}
+        self.accumulate = args.accumulate
+        self.loop_sets = None
+        if args.ring3_loopback:
+            if self.op not in ("topk", "topk_seg", "randk") or world != 1:
+                raise SystemExit("--ring3-loopback: sparse workloads at --gpus 1 only")
+            # a ring worker's neighbourhood {r-1, r, r+1} (weights 1/3, the self message second):
+            # the two neighbour messages come from other deltas, compressed once per rotation slot
+            self.ranks, self.self_slot = ["left", rank, "right"], 1
+            self.weights = [1.0 / 3] * 3
+            self.fold_mem = False
+            self.loop_sets = []
+            for j in range(len(self.ds)):
+                pair = {}
+                for side, sd in (("left", 5000 + 2 * j), ("right", 5001 + 2 * j)):
+                    gj = torch.Generator(device=dev).manual_seed(sd)
+                    dj = torch.randn(self.n, generator=gj, device=dev)
+                    m = torch.empty_like(self.msg)
+                    vv, ii = m[:self.k].view(torch.float32), m[self.k:]
+                    if self.op == "topk":
+                        codec.topk(dj, self.k, out=(vv, ii))
+                    elif self.op == "topk_seg":
+                        codec.topk_segmented(dj, self.plan, out=(vv, ii))
+                    else:
+                        codec.randk(dj, self.k, seed=777 + sd, offset=0, out=(vv, ii))
+                    pair[side] = m
+                    del dj
+                self.loop_sets.append(pair)
+            self.recv = self.loop_sets[0]
+            self.label += "_ring3_loopback"
         if self.backend == "gloo":
             self.msg_h = torch.empty(self.msg.shape, dtype=self.msg.dtype).pin_memory()
             self.recv_h = {r: torch.empty_like(self.msg_h).pin_memory() for r in self.peers}
@@ -185,6 +220,8 @@ class Worker:
         c = self.codec
         torch = self.torch
         self.d = self.ds[self.step_id % len(self.ds)]
+        if self.loop_sets:
+            self.recv = self.loop_sets[self.step_id % len(self.loop_sets)]
         if self.step_mode:
             self.compress_step()
         elif self.op == "topk":
@@ -263,11 +300,20 @@ class Worker:
         torch = self.torch
         msgs = [self.msg if r == self.rank else self.recv[r] for r in self.ranks]
         if self.op in ("topk", "topk_seg", "randk"):
-            for r, m, w in zip(self.ranks, msgs, self.weights):
-                if r == self.rank and self.fold_mem:
-                    continue  # applied by the compress (the fold)
+            # the self message's memory update is skipped when the fold applied it; x_hat takes
+            # it here unless the overlap (hat_done) or the fold did
+            items = [(r, m, w) for r, m, w in zip(self.ranks, msgs, self.weights)
+                     if not (r == self.rank and self.fold_mem)]
+            want_hat = not (hat_done or self.fold)
+            if self.accumulate == "multi":
+                slot = next((i for i, (r, _, _) in enumerate(items) if r == self.rank), -1) if want_hat else -1
+                c.sparse_accumulate_multi([(m[:self.k].view(torch.float32), m[self.k:]) for _, m, _ in items],
+                                          [w for _, _, w in items], self.mem, self_slot=slot,
+                                          xhat_self=self.hat if slot >= 0 else None)
+                return
+            for r, m, w in items:
                 c.sparse_accumulate(m[:self.k].view(torch.float32), m[self.k:], self.mem, w,
-                                    xhat_self=self.hat if r == self.rank and not (hat_done or self.fold) else None)
+                                    xhat_self=self.hat if r == self.rank and want_hat else None)
         elif self.op == "qsgd":
             parts = [(m[16:], m[:4].view(torch.float32)) for m in msgs]
             c.qsgd_accumulate(parts, self.weights, self.self_slot, self.n, self.param, self.mem, xhat_self=self.hat)
@@ -328,10 +374,12 @@ class Worker:
         if self.op not in ("topk", "topk_seg", "randk"):
             return None
         torch = self.torch
-        segs = 0
-        for m in [self.msg] + [self.recv[r] for r in self.peers]:
-            segs += int(torch.unique(m[self.k:].long() // 16).numel())
-        own = int(torch.unique(self.msg[self.k:].long() // 16).numel())
+        ms = [self.msg] + [self.recv[r] for r in self.ranks if r != self.rank]
+        own = int(torch.unique(self.msg[self.k:].long() // 16).numel())  # x_hat: the self message's lines
+        if self.accumulate == "multi":  # memory: every line touched by any message, once
+            segs = int(torch.unique(torch.cat([m[self.k:].long() // 16 for m in ms])).numel())
+        else:
+            segs = sum(int(torch.unique(m[self.k:].long() // 16).numel()) for m in ms)
         return 8 * self.k * len(self.ranks) + 128 * (segs + own)
 
 
@@ -661,7 +709,9 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": w.label + ("_fold" if w.fold else ""), "n_per_worker": w.n, "k_per_worker": w.k,
-                       "graph": "self" if world == 1 else ("complete" if world == 2 else "ring"),
+                       "graph": ("ring3_loopback" if w.loop_sets else "self") if world == 1 else (
+                           "complete" if world == 2 else "ring"),
+                       "accumulate": w.accumulate if w.op in ("topk", "topk_seg", "randk") else None,
                        "messages_per_step": len(w.ranks), "backend": args.backend if world > 1 else None,
                        "step": "compress+exchange+decompress-accumulate", "parallelism": f"gossip{world}"},
             "roofline": roofline,

@@ -46,6 +46,9 @@ SIGNATURES = {
                                                 _c_sz, _vp]),
     "choco_gather": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_f32, _vp, _vp]),
     "choco_sparse_accumulate": (_c_i32, [_vp, _vp, _c_i64, _vp, _vp, _c_i64, _c_f32, _vp, _vp]),
+    "choco_sparse_accumulate_multi_workspace_size": (_c_sz, [_c_i64, _c_i32]),
+    "choco_sparse_accumulate_multi": (_c_i32, [_pp, _pp, _p_i64, _p_f32, _c_i32, _c_i32, _vp, _vp, _c_i64, _vp,
+                                               _c_sz, _vp, _vp]),
     "choco_sign_words": (_c_i64, [_c_i64]),
     "choco_sign_workspace_size": (_c_sz, [_c_i32]),
     "choco_sign_compress": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),

@@ -15,81 +15,25 @@ namespace choco {
 
 constexpr int kEwThreads = 256;
 
-__global__ __launch_bounds__(kEwThreads) void gossip_kernel(float* __restrict__ x, const float* __restrict__ mem,
-                                                            const float* __restrict__ hat, float gamma, int64_t n) {
-  const int64_t stride = (int64_t)gridDim.x * kEwThreads * 4;
-  for (int64_t e = ((int64_t)blockIdx.x * kEwThreads + threadIdx.x) * 4; e < n; e += stride) {
-    if (e + 3 < n) {
-      float4 a = *reinterpret_cast<const float4*>(x + e);
-      const float4 m = *reinterpret_cast<const float4*>(mem + e);
-      const float4 h = *reinterpret_cast<const float4*>(hat + e);
-      a.x = a.x + gamma * (m.x - h.x);
-      a.y = a.y + gamma * (m.y - h.y);
-      a.z = a.z + gamma * (m.z - h.z);
-      a.w = a.w + gamma * (m.w - h.w);
-      *reinterpret_cast<float4*>(x + e) = a;
-    } else {
-      for (int64_t i = e; i < n; ++i) x[i] = x[i] + gamma * (mem[i] - hat[i]);
-    }
-  }
-}
-
-// Scattered read-modify-write of x_hat and memory at the message's (sorted,
-// distinct) indices.  Each thread takes kAccU updates (strided by the block, so
-// the index/value reads stay coalesced) and issues all their loads before any
-// store.  Default 1: with cold lines (the bench step) the full grid's memory-level
-// parallelism wins (U = 16: 82 -> 88 us); with MALL-hot lines U = 16 wins (73 -> 59 us).
-#ifndef CHOCO_ACC_U
-#define CHOCO_ACC_U 1
-#endif
-constexpr int kAccU = CHOCO_ACC_U;
-// An index outside [0, n) (a corrupt message, or a peer with another layout) is
-// skipped and counted into *bad (nullable) -- the reference's index_put raises
-// IndexError there; the host checks the count lazily (codec.py).
+// Scattered read-modify-write of x_hat and memory at the message's indices, one
+// update per thread: the form for buffers that are not 16-byte aligned (the segment
+// form below needs whole float4).  An index outside [0, n) (a corrupt message, or a peer
+// with another layout) is skipped and counted into *bad (nullable) -- the reference's
+// index_put raises IndexError there; the host checks the count lazily (codec.py).
 __global__ __launch_bounds__(kEwThreads) void sparse_acc_kernel(const float* __restrict__ val,
                                                                 const int32_t* __restrict__ idx, int64_t k,
                                                                 float* __restrict__ hat, float* __restrict__ mem,
                                                                 int64_t n, float w, uint32_t* __restrict__ bad) {
-  const int64_t base = (int64_t)blockIdx.x * kEwThreads * kAccU + threadIdx.x;
-  uint32_t nbad = 0;
-  if (base + (int64_t)(kAccU - 1) * kEwThreads < k) {
-    int64_t j[kAccU];
-    float v[kAccU], h[kAccU], m[kAccU];
-    bool ok[kAccU];
-#pragma unroll
-    for (int u = 0; u < kAccU; ++u) {
-      j[u] = idx[base + u * kEwThreads];
-      v[u] = val[base + u * kEwThreads];
-      ok[u] = j[u] >= 0 && j[u] < n;
-      nbad += ok[u] ? 0u : 1u;
-      if (!ok[u]) j[u] = 0;
-    }
-#pragma unroll
-    for (int u = 0; u < kAccU; ++u) {
-      if (hat) h[u] = hat[j[u]];
-      m[u] = mem[j[u]];
-    }
-#pragma unroll
-    for (int u = 0; u < kAccU; ++u) {
-      if (!ok[u]) continue;
-      if (hat) hat[j[u]] = h[u] + v[u];
-      mem[j[u]] = m[u] + w * v[u];
-    }
-  } else {
-    for (int u = 0; u < kAccU; ++u) {
-      const int64_t i = base + u * kEwThreads;
-      if (i >= k) break;
-      const int64_t jj = idx[i];
-      if (jj < 0 || jj >= n) {
-        ++nbad;
-        continue;
-      }
-      const float vv = val[i];
-      if (hat) hat[jj] = hat[jj] + vv;
-      mem[jj] = mem[jj] + w * vv;
-    }
+  const int64_t i = (int64_t)blockIdx.x * kEwThreads + threadIdx.x;
+  if (i >= k) return;
+  const int64_t jj = idx[i];
+  if (jj < 0 || jj >= n) {
+    if (bad) atomicAdd(bad, 1u);
+    return;
   }
-  if (bad && nbad) atomicAdd(bad, nbad);
+  const float vv = val[i];
+  if (hat) hat[jj] = hat[jj] + vv;
+  mem[jj] = mem[jj] + w * vv;
 }
 
 // Segment-owner form (default).  A message's indices are strictly ascending
@@ -108,35 +52,13 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_kernel(const float* __r
 // of that step may already be wrong when the host reports the bad count
 // (IndexGuard, one step later; INTEGRATION.md "corrupt messages").  Messages
 // from this codec are always ascending.
-#ifndef CHOCO_ACC_MODE
-#define CHOCO_ACC_MODE 1
-#endif
-#ifndef CHOCO_ACC_SEGF
-#define CHOCO_ACC_SEGF 16
-#endif
-#ifndef CHOCO_ACC_NEXT  // A/B knob: 1 loads the next index and the value with the update's index
-#define CHOCO_ACC_NEXT 1
-#endif
-#ifndef CHOCO_ACC_NT  // cache policy of the owner's segment RMW (A/B): 0 default, 1 nt stores, 2 nt loads + stores
-#define CHOCO_ACC_NT 0
-#endif
-CHOCO_DEV float4 acc_ld4(const float* p) {
-  if (CHOCO_ACC_NT >= 2) return ld_nt4(p);
-  return *reinterpret_cast<const float4*>(p);
-}
-CHOCO_DEV void acc_st4(float* p, float4 v) {
-  if (CHOCO_ACC_NT >= 1) {
-    choco_f32x4 f;
-    f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
-    __builtin_nontemporal_store(f, reinterpret_cast<choco_f32x4*>(p));
-  } else {
-    *reinterpret_cast<float4*>(p) = v;
-  }
-}
-constexpr int kSegF = CHOCO_ACC_SEGF;  // floats per owned segment (16: 64 B)
+// Measured and not kept (same-box A/Bs, r03/r04; git history): owner granules of 32 / 128 B
+// and per-element updates (80-99 against 77.5-80 us), non-temporal segment loads / stores.
+CHOCO_DEV float4 acc_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+CHOCO_DEV void acc_st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+constexpr int kSegF = 16;              // floats per owned segment (64 B)
 constexpr int kSegL = kSegF / 4;       // lanes per update (one float4 each)
-constexpr int kSegShift = kSegF == 32 ? 5 : (kSegF == 16 ? 4 : 3);
-static_assert((1 << kSegShift) == kSegF, "segment of 8, 16 or 32 floats");
+constexpr int kSegShift = 4;
 
 template <bool HS>
 __global__ __launch_bounds__(kEwThreads) void sparse_acc_seg_kernel(const float* __restrict__ val,
@@ -154,8 +76,8 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_seg_kernel(const float*
     // the next update's index and this update's value in the same round trip: most
     // segments hold one update, so the leader then needs no third round trip to find
     // that the next update is not its segment's
-    const int64_t jn = CHOCO_ACC_NEXT && u + 1 < k ? (int64_t)idx[u + 1] : -1;
-    const float v0 = CHOCO_ACC_NEXT ? val[u] : 0.f;
+    const int64_t jn = u + 1 < k ? (int64_t)idx[u + 1] : -1;
+    const float v0 = val[u];
     const bool ok = j >= 0 && j < n;
     const int64_t seg = j >> kSegShift;
     if (l4 == 0) nbad += (ok ? 0u : 1u) + ((u > 0 && jp >= j) ? 1u : 0u);
@@ -182,9 +104,9 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_seg_kernel(const float*
       }
       int64_t je = j;
       for (int64_t e = u; e < k && e < u + kSegF; ++e) {
-        if (e != u) je = (CHOCO_ACC_NEXT && e == u + 1) ? jn : idx[e];
+        if (e != u) je = e == u + 1 ? jn : idx[e];
         if (je < 0 || je >= n || (je >> kSegShift) != seg) break;
-        const float v = (CHOCO_ACC_NEXT && e == u) ? v0 : val[e];
+        const float v = e == u ? v0 : val[e];
         const int off = (int)(je - base);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -209,6 +131,182 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_seg_kernel(const float*
     }
   }
   if (bad && nbad) atomicAdd(bad, nbad);
+}
+
+// ----------------------------------------------------------------------------
+// Multi-message receive (the per-neighbour loop of CHOCOSparsificationCompressor.
+// uncompress, parallel_choco_v.py:291-310, for memory): memory[i] += w_m * v_m for
+// every message m IN ORDER, as ONE sweep.  The index space is cut into ranges of
+// kMRange elements (256 segments of 64 B); a range's workgroup
+//   1. reads where each message's updates for the range start and end (a split table
+//      written by sparse_split_kernel: one pass over the messages' indices),
+//   2. loads those updates (first 256 per message in registers) and marks the 64-B
+//      segments they touch,
+//   3. loads every touched segment of memory ONCE into LDS (a quad of lanes per
+//      segment: whole-line float4 loads),
+//   4. applies the messages one after the other in LDS (indices are unique inside a
+//      message, so no two lanes of one message meet; a barrier between messages keeps
+//      the per-element order of the reference),
+//   5. writes the touched segments back whole.
+// A line hit by several messages is read and written once per step instead of once per
+// message (at k = 1 %, ~15 % of a ring-3 memory's touched lines), and the launches of
+// the per-message kernels collapse into two.
+// ----------------------------------------------------------------------------
+constexpr int kMaxMsgs = 8;
+constexpr int kMRShift = 12;
+constexpr int64_t kMRange = int64_t(1) << kMRShift;   // elements per range
+constexpr int kMSegs = (int)(kMRange / 16);          // 64-B segments per range = threads
+static_assert(kMSegs == kEwThreads, "one thread per segment of the range");
+struct MsgSet {
+  const float* val[kMaxMsgs];
+  const int32_t* idx[kMaxMsgs];
+  int64_t k[kMaxMsgs];
+  float w[kMaxMsgs];
+};
+
+// starts[m][q] = first update of message m with index >= q * kMRange (q = 0 .. nR),
+// for an ascending message.  Thread per update u (and u = k as the sentinel): writes
+// the ranges (range(u-1), range(u)].  Indices out of [0, n) and non-ascending pairs are
+// counted into *bad (then some entries may keep an earlier call's value: the sweep
+// clamps them and skips updates outside its range, so it stays in bounds).
+__global__ __launch_bounds__(kEwThreads) void sparse_split_kernel(MsgSet ms, int64_t n, int64_t nR,
+                                                                  int32_t* __restrict__ starts,
+                                                                  uint32_t* __restrict__ bad) {
+  const int m = blockIdx.y;
+  const int64_t k = ms.k[m];
+  const int32_t* __restrict__ idx = ms.idx[m];
+  int32_t* __restrict__ st = starts + (int64_t)m * (nR + 1);
+  uint32_t nbad = 0;
+  for (int64_t u = (int64_t)blockIdx.x * kEwThreads + threadIdx.x; u <= k; u += (int64_t)gridDim.x * kEwThreads) {
+    const int64_t j = u < k ? (int64_t)idx[u] : n;
+    const int64_t jp = u > 0 ? (int64_t)idx[u - 1] : -1;
+    const int64_t rq = u < k ? (j < 0 ? 0 : min(j >> kMRShift, nR)) : nR;
+    const int64_t rp = u > 0 ? (jp < 0 ? 0 : min(jp >> kMRShift, nR)) : -1;
+    if (u < k) nbad += ((j < 0 || j >= n) ? 1u : 0u) + ((u > 0 && jp >= j) ? 1u : 0u);
+    for (int64_t q = rp + 1; q <= rq; ++q) st[q] = (int32_t)u;
+  }
+  if (bad && nbad) atomicAdd(bad, nbad);
+}
+
+__global__ __launch_bounds__(kEwThreads) void sparse_acc_multi_kernel(MsgSet ms, int nmsg, float* __restrict__ mem,
+                                                                      int64_t n, int64_t nR,
+                                                                      const int32_t* __restrict__ starts) {
+  __shared__ float4 stage[kMSegs][4];   // the range's touched segments, compacted (16 KiB)
+  __shared__ uint8_t touched[kMSegs];
+  __shared__ uint8_t slot_of[kMSegs];
+  __shared__ uint8_t seg_of[kMSegs];
+  __shared__ uint32_t wsum[kEwThreads / 64];
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const int64_t r = blockIdx.x;
+  const int64_t r0 = r << kMRShift;
+  const int64_t r1 = min(r0 + kMRange, n);
+  touched[tid] = 0;
+  // this range's update span per message (workgroup-uniform: scalar loads)
+  int32_t beg[kMaxMsgs], cnt[kMaxMsgs];
+#pragma unroll
+  for (int m = 0; m < kMaxMsgs; ++m) {
+    beg[m] = 0;
+    cnt[m] = 0;
+    if (m < nmsg) {
+      const int32_t* st = starts + (int64_t)m * (nR + 1);
+      const int64_t k = ms.k[m];
+      const int64_t b = min(max((int64_t)st[r], (int64_t)0), k);
+      const int64_t e = min(max((int64_t)st[r + 1], b), k);
+      beg[m] = (int32_t)b;
+      cnt[m] = (int32_t)(e - b);
+    }
+  }
+  // the first 256 updates of every message in registers (the common case: ~41 per
+  // message per range at k = 1 %); -1 = none / outside this range
+  int32_t ji[kMaxMsgs];
+  float vv[kMaxMsgs];
+#pragma unroll
+  for (int m = 0; m < kMaxMsgs; ++m) {
+    ji[m] = -1;
+    vv[m] = 0.f;
+    if (m < nmsg && tid < cnt[m]) {
+      const int64_t j = ms.idx[m][beg[m] + tid];
+      vv[m] = ms.val[m][beg[m] + tid];
+      ji[m] = (j >= r0 && j < r1) ? (int32_t)(j - r0) : -1;
+    }
+  }
+  __syncthreads();  // touched[] cleared
+#pragma unroll
+  for (int m = 0; m < kMaxMsgs; ++m) {
+    if (m < nmsg) {
+      if (ji[m] >= 0) touched[ji[m] >> 4] = 1;
+      for (int32_t u = tid + kEwThreads; u < cnt[m]; u += kEwThreads) {  // dense messages
+        const int64_t j = ms.idx[m][beg[m] + u];
+        if (j >= r0 && j < r1) touched[(j - r0) >> 4] = 1;
+      }
+    }
+  }
+  __syncthreads();
+  // compact the touched segments: slot = rank among them
+  const bool t = touched[tid] != 0;
+  const uint64_t bm = ballot(t);
+  if (lane == 0) wsum[wv] = (uint32_t)__popcll(bm);
+  __syncthreads();
+  uint32_t base = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < kEwThreads / 64; ++i) {
+    base += i < wv ? wsum[i] : 0u;
+    total += wsum[i];
+  }
+  if (t) {
+    const uint32_t s = base + mask_prefix(bm);
+    slot_of[tid] = (uint8_t)s;
+    seg_of[s] = (uint8_t)tid;
+  }
+  __syncthreads();
+  // load the touched segments: a quad per segment, lane l4 its float4
+  const int q = tid >> 2, l4 = tid & 3;
+  for (uint32_t s = q; s < total; s += kEwThreads / 4) {
+    const int64_t e = r0 + (int64_t)seg_of[s] * 16 + 4 * l4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e + 4 <= n) {
+      v = *reinterpret_cast<const float4*>(mem + e);
+    } else {
+      if (e < n) v.x = mem[e];
+      if (e + 1 < n) v.y = mem[e + 1];
+      if (e + 2 < n) v.z = mem[e + 2];
+    }
+    stage[s][l4] = v;
+  }
+  __syncthreads();
+  float* sf = reinterpret_cast<float*>(&stage[0][0]);
+  // the messages in order; inside one message every index is distinct
+#pragma unroll
+  for (int m = 0; m < kMaxMsgs; ++m) {
+    if (m < nmsg) {
+      const float w = ms.w[m];
+      if (ji[m] >= 0) {
+        float* p = sf + (int)slot_of[ji[m] >> 4] * 16 + (ji[m] & 15);
+        *p = *p + w * vv[m];
+      }
+      for (int32_t u = tid + kEwThreads; u < cnt[m]; u += kEwThreads) {
+        const int64_t j = ms.idx[m][beg[m] + u];
+        if (j >= r0 && j < r1) {
+          const int jl = (int)(j - r0);
+          float* p = sf + (int)slot_of[jl >> 4] * 16 + (jl & 15);
+          *p = *p + w * ms.val[m][beg[m] + u];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // write the touched segments back whole
+  for (uint32_t s = q; s < total; s += kEwThreads / 4) {
+    const int64_t e = r0 + (int64_t)seg_of[s] * 16 + 4 * l4;
+    const float4 v = stage[s][l4];
+    if (e + 4 <= n) {
+      *reinterpret_cast<float4*>(mem + e) = v;
+    } else {
+      if (e < n) mem[e] = v.x;
+      if (e + 1 < n) mem[e + 1] = v.y;
+      if (e + 2 < n) mem[e + 2] = v.z;
+    }
+  }
 }
 
 __global__ __launch_bounds__(kEwThreads) void gather_kernel(const float* __restrict__ x, const float* __restrict__ xh,
@@ -244,18 +342,12 @@ static unsigned ew_grid(int64_t work, int per_thread) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 8192));
 }
 
-// One-shot form: each thread owns kGossipU float4 of every stream (no grid-stride
-// loop), all loads issued before any arithmetic; `nt` policy knob for the A/B.
-#ifndef CHOCO_GOSSIP_FORM  // 0: grid-stride gossip_kernel; 1: one-shot gossipu_kernel
-#define CHOCO_GOSSIP_FORM 1
-#endif
-#ifndef CHOCO_GOSSIP_U  // measured at 100M (tools/gossip_probe.py): U=4 + nt 258 us (6.2 TB/s)
-#define CHOCO_GOSSIP_U 4    // against 320 us for the grid-stride form and 291 us for U=2 plain
-#endif
-#ifndef CHOCO_GOSSIP_NT
-#define CHOCO_GOSSIP_NT 1
-#endif
-constexpr int kGossipU = CHOCO_GOSSIP_U;
+// The consensus step x += gamma (memory - x_hat), one-shot form: each thread owns
+// kGossipU float4 of every stream (no grid-stride loop), all loads issued before any
+// arithmetic, non-temporal loads and stores.  Measured at 100M (tools/gossip_probe.py):
+// U = 4 + nt 258 us (6.2 TB/s) against 320 us for a grid-stride form and 291 us for U = 2
+// plain.
+constexpr int kGossipU = 4;
 __global__ __launch_bounds__(kEwThreads) void gossipu_kernel(float* __restrict__ x, const float* __restrict__ mem,
                                                              const float* __restrict__ hat, float gamma, int64_t n) {
   const int64_t e0 = ((int64_t)blockIdx.x * kEwThreads * kGossipU + threadIdx.x) * 4;
@@ -264,26 +356,16 @@ __global__ __launch_bounds__(kEwThreads) void gossipu_kernel(float* __restrict__
     float4 a[kGossipU], m[kGossipU], h[kGossipU];
 #pragma unroll
     for (int u = 0; u < kGossipU; ++u) {
-      if (CHOCO_GOSSIP_NT) {
-        a[u] = ld_nt4(x + e0 + u * kStep);
-        m[u] = ld_nt4(mem + e0 + u * kStep);
-        h[u] = ld_nt4(hat + e0 + u * kStep);
-      } else {
-        a[u] = *reinterpret_cast<const float4*>(x + e0 + u * kStep);
-        m[u] = *reinterpret_cast<const float4*>(mem + e0 + u * kStep);
-        h[u] = *reinterpret_cast<const float4*>(hat + e0 + u * kStep);
-      }
+      a[u] = ld_nt4(x + e0 + u * kStep);
+      m[u] = ld_nt4(mem + e0 + u * kStep);
+      h[u] = ld_nt4(hat + e0 + u * kStep);
     }
 #pragma unroll
     for (int u = 0; u < kGossipU; ++u) {
       const float4 v = gossip4(a[u], m[u], h[u], gamma);
-      if (CHOCO_GOSSIP_NT) {
-        choco_f32x4 f;
-        f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
-        __builtin_nontemporal_store(f, reinterpret_cast<choco_f32x4*>(x + e0 + u * kStep));
-      } else {
-        *reinterpret_cast<float4*>(x + e0 + u * kStep) = v;
-      }
+      choco_f32x4 f;
+      f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
+      __builtin_nontemporal_store(f, reinterpret_cast<choco_f32x4*>(x + e0 + u * kStep));
     }
   } else {
     for (int u = 0; u < kGossipU; ++u)
@@ -308,13 +390,9 @@ int gossip_launch(float* x, const float* mem, const float* xh, float gamma, int6
   CHOCO_REQUIRE(aligned4(x) && aligned4(mem) && aligned4(xh), "buffers must be 4-byte aligned");
   profile_begin("gossip_step", st);
   if (aligned16(x) && aligned16(mem) && aligned16(xh)) {
-    if (CHOCO_GOSSIP_FORM == 1) {
-      const int64_t per = (int64_t)kEwThreads * 4 * kGossipU;
-      CHOCO_KLAUNCH(gossipu_kernel, dim3((unsigned)((n + per - 1) / per)), dim3(kEwThreads), 0, st, x, mem, xh,
-                    gamma, n);
-    } else {
-      CHOCO_KLAUNCH(gossip_kernel, dim3(ew_grid(n, 4)), dim3(kEwThreads), 0, st, x, mem, xh, gamma, n);
-    }
+    const int64_t per = (int64_t)kEwThreads * 4 * kGossipU;
+    CHOCO_KLAUNCH(gossipu_kernel, dim3((unsigned)((n + per - 1) / per)), dim3(kEwThreads), 0, st, x, mem, xh,
+                  gamma, n);
   } else {
     CHOCO_KLAUNCH(gossip1_kernel, dim3(ew_grid(n, 1)), dim3(kEwThreads), 0, st, x, mem, xh, gamma, n);
   }
@@ -340,7 +418,7 @@ CHOCO_API int choco_sparse_accumulate(const float* val, const int32_t* idx, int6
   CHOCO_REQUIRE(n > 0, "n must be positive");
   if (k <= 0) return CHOCO_OK;
   profile_begin("sparse_accumulate", st);
-  if (CHOCO_ACC_MODE == 1 && aligned16(memory) && (!xhat_self || aligned16(xhat_self))) {
+  if (aligned16(memory) && (!xhat_self || aligned16(xhat_self))) {
     const unsigned g = (unsigned)((kSegL * k + kEwThreads - 1) / kEwThreads);
     if (xhat_self)
       CHOCO_KLAUNCH((sparse_acc_seg_kernel<true>), dim3(g), dim3(kEwThreads), 0, st, val, idx, k, xhat_self, memory,
@@ -349,12 +427,74 @@ CHOCO_API int choco_sparse_accumulate(const float* val, const int32_t* idx, int6
       CHOCO_KLAUNCH((sparse_acc_seg_kernel<false>), dim3(g), dim3(kEwThreads), 0, st, val, idx, k, xhat_self,
                     memory, n, weight, bad_count);
   } else {
-    CHOCO_KLAUNCH(sparse_acc_kernel,
-                  dim3((unsigned)((k + (int64_t)kEwThreads * kAccU - 1) / ((int64_t)kEwThreads * kAccU))),
-                  dim3(kEwThreads), 0, st, val, idx, k, xhat_self, memory, n, weight, bad_count);
+    CHOCO_KLAUNCH(sparse_acc_kernel, dim3((unsigned)((k + kEwThreads - 1) / kEwThreads)), dim3(kEwThreads), 0, st,
+                  val, idx, k, xhat_self, memory, n, weight, bad_count);
   }
   profile_end("sparse_accumulate", st);
   CHOCO_LAUNCHED("sparse_acc_kernel");
+  return CHOCO_OK;
+}
+
+CHOCO_API size_t choco_sparse_accumulate_multi_workspace_size(int64_t n, int32_t nmsg) {
+  const int64_t nR = (std::max<int64_t>(n, 1) + kMRange - 1) / kMRange;
+  return align_up((size_t)std::max(nmsg, 1) * (size_t)(nR + 1) * 4, 256);
+}
+
+CHOCO_API int choco_sparse_accumulate_multi(const float* const* vals, const int32_t* const* idxs, const int64_t* ks,
+                                            const float* weights, int32_t nmsg, int32_t self_slot, float* xhat_self,
+                                            float* memory, int64_t n, void* ws, size_t ws_bytes,
+                                            uint32_t* bad_count, void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(vals && idxs && ks && weights && memory, "null pointer argument");
+  CHOCO_REQUIRE(nmsg >= 1 && nmsg <= kMaxMsgs, "nmsg must be in [1, %d], got %d", kMaxMsgs, (int)nmsg);
+  CHOCO_REQUIRE(self_slot >= -1 && self_slot < nmsg, "self_slot out of range");
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n must be in [1, 2^31-1)");
+  const int64_t nR = (n + kMRange - 1) / kMRange;
+  MsgSet ms{};
+  bool sweep = aligned16(memory) && n >= kMRange;
+  for (int m = 0; m < nmsg; ++m) {
+    CHOCO_REQUIRE(ks[m] >= 0 && ks[m] < (int64_t)INT32_MAX, "message %d: k out of range", m);
+    CHOCO_REQUIRE(ks[m] == 0 || (vals[m] && idxs[m]), "message %d: null values / indices", m);
+    ms.val[m] = vals[m];
+    ms.idx[m] = idxs[m];
+    ms.k[m] = ks[m];
+    ms.w[m] = weights[m];
+    // the split writes (range(u-1), range(u)] per update: long runs of empty ranges would
+    // serialise in one thread, so sparse messages (< one update per range) take the
+    // per-message kernels
+    sweep = sweep && ks[m] >= nR;
+  }
+  if (!sweep) {
+    for (int m = 0; m < nmsg; ++m) {
+      const int rc = choco_sparse_accumulate(vals[m], idxs[m], ks[m], m == self_slot ? xhat_self : nullptr, memory, n,
+                                             weights[m], bad_count, stream);
+      if (rc) return rc;
+    }
+    return CHOCO_OK;
+  }
+  const size_t need = choco_sparse_accumulate_multi_workspace_size(n, nmsg);
+  CHOCO_REQUIRE(ws != nullptr && ws_bytes >= need, "multi-message accumulate workspace too small: need %zu, got %zu",
+                need, ws_bytes);
+  int32_t* starts = static_cast<int32_t*>(ws);
+  if (self_slot >= 0 && xhat_self != nullptr && ks[self_slot] > 0) {
+    // x_hat takes the self message only (parallel_choco_v.py:307-308): hat + 1.0f * v == hat + v
+    // (its bad indices are counted by the split below)
+    const int rc = choco_sparse_accumulate(vals[self_slot], idxs[self_slot], ks[self_slot], nullptr, xhat_self, n, 1.0f,
+                                           nullptr, stream);
+    if (rc) return rc;
+  }
+  int64_t kmax = 0;
+  for (int m = 0; m < nmsg; ++m) kmax = std::max(kmax, ks[m]);
+  profile_begin("sparse_split", st);
+  CHOCO_KLAUNCH(sparse_split_kernel, dim3((unsigned)std::min<int64_t>((kmax + kEwThreads) / kEwThreads, 4096), nmsg),
+                dim3(kEwThreads), 0, st, ms, n, nR, starts, bad_count);
+  profile_end("sparse_split", st);
+  CHOCO_LAUNCHED("sparse_split_kernel");
+  profile_begin("sparse_acc_multi", st);
+  CHOCO_KLAUNCH(sparse_acc_multi_kernel, dim3((unsigned)nR), dim3(kEwThreads), 0, st, ms, (int)nmsg, memory, n, nR,
+                starts);
+  profile_end("sparse_acc_multi", st);
+  CHOCO_LAUNCHED("sparse_acc_multi_kernel");
   return CHOCO_OK;
 }
 

@@ -30,11 +30,9 @@ namespace choco {
 constexpr int kQThreads = 256;
 constexpr int kQPer = 8;                         // elements per thread in the quantize/decode passes
 constexpr int kQTile = kQThreads * kQPer;        // 2048
-#ifndef CHOCO_QNORM_TILE  // elements per workgroup in the norm pass (a multiple of 8192): 49152 -> ~2040
-                          // workgroups at 100M, one round of 8 per CU (r03 A/B: 32768 and 65536 slower)
-#define CHOCO_QNORM_TILE 49152
-#endif
-constexpr int kNormTile = CHOCO_QNORM_TILE;
+// elements per workgroup in the norm pass (a multiple of 8192): 49152 -> ~2040 workgroups
+// at 100M, one round of 8 per CU (r03 A/B: 32768 and 65536 slower)
+constexpr int kNormTile = 49152;
 static_assert(kNormTile % 8192 == 0, "whole load rounds per norm tile");
 constexpr int kQMaxMsg = 8;
 
@@ -75,48 +73,26 @@ CHOCO_DEV QParam qparam(const float* __restrict__ norms, const int64_t* __restri
   return p;
 }
 
-// Non-temporal loads in the norm pass (default; 0 for A/B runs): they keep the
-// previous decode's dirty Infinity-Cache lines from being written back in the
-// middle of this stream (bench step: 120 -> 72 us), though the decode then
-// meets them itself.
-#ifndef CHOCO_QNORM_NT
-#define CHOCO_QNORM_NT 1
-#endif
-CHOCO_DEV float4 ld_norm4(const float* p) {
-  if (CHOCO_QNORM_NT) return ld_nt4(p);
-  return *reinterpret_cast<const float4*>(p);
-}
+// Non-temporal loads in the norm pass: they keep the previous decode's dirty
+// Infinity-Cache lines from being written back in the middle of this stream (bench
+// step: 120 -> 72 us), though the decode then meets them itself.
+CHOCO_DEV float4 ld_norm4(const float* p) { return ld_nt4(p); }
 
-#ifndef CHOCO_QQUANT_REV  // 1: workgroups walk the tiles in reverse (A/B, r03 with two tiles per workgroup: forward 145-146 vs reverse 142-144 us)
-#define CHOCO_QQUANT_REV 1
-#endif
-#ifndef CHOCO_QQUANT_NT  // non-temporal loads in the quantize pass (off: the decode then runs 300 -> 270 us)
-#define CHOCO_QQUANT_NT 0
-#endif
-CHOCO_DEV float4 ld_quant4(const float* p) {
-  if (CHOCO_QQUANT_NT) return ld_nt4(p);
-  return *reinterpret_cast<const float4*>(p);
-}
+// The quantize pass reads with the default policy (non-temporal loads measured: the
+// decode after it then runs 270 -> 300 us) and its workgroups walk the tiles in reverse
+// (Infinity-Cache hits on the tail the norm pass read last; r03 A/B forward 145-146 vs
+// reverse 142-144 us).
+CHOCO_DEV float4 ld_quant4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-// The fused gossip step's xh loads and x_new stores in the norm pass:
-// non-temporal (default; measured at 100M in the step: norm 343 -> 315 us, step
-// 0.827 -> 0.785 ms) or plain (A/B knob: lets the quantize pass's backward walk
-// hit the Infinity Cache, but the dirty lines cost more than that saves).
-#ifndef CHOCO_QNORM_GS_NT
-#define CHOCO_QNORM_GS_NT 1
-#endif
-CHOCO_DEV float4 ld_gs4(const float* p) {
-  if (CHOCO_QNORM_GS_NT) return ld_nt4(p);
-  return *reinterpret_cast<const float4*>(p);
-}
+// The fused gossip step's xh loads and x_new stores in the norm pass: non-temporal
+// (measured at 100M in the step: norm 343 -> 315 us, step 0.827 -> 0.785 ms; plain lets
+// the quantize pass's backward walk hit the Infinity Cache, but the dirty lines cost
+// more than that saves).
+CHOCO_DEV float4 ld_gs4(const float* p) { return ld_nt4(p); }
 CHOCO_DEV void st_gs4(float* p, float4 v) {
-  if (CHOCO_QNORM_GS_NT) {
-    choco_f32x4 f;
-    f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
-    __builtin_nontemporal_store(f, reinterpret_cast<choco_f32x4*>(p));
-  } else {
-    *reinterpret_cast<float4*>(p) = v;
-  }
+  choco_f32x4 f;
+  f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
+  __builtin_nontemporal_store(f, reinterpret_cast<choco_f32x4*>(p));
 }
 
 // ---------------------------------------------------------------- pass 1: norms
@@ -315,9 +291,6 @@ CHOCO_DEV int tile_seg(const int64_t* __restrict__ seg_off, int nseg, int64_t e0
 // pinned norm below |d|) takes the real division.  Checked against fp32 division on 3e9 (t, norm) pairs (random over
 // the guarded range + exhaustive t for 12 norm mantissas) and bit-exact against
 // the oracle in the GPU tests.
-#ifndef CHOCO_QCHECK  // 1: the quotient guard per 8-element group (A/B knob; 0: per element)
-#define CHOCO_QCHECK 1
-#endif
 struct QDiv {
   float norm, y;
   bool fast;
@@ -328,12 +301,13 @@ struct QDiv {
     fast = nrm >= 0x1p-30f && nrm <= 0x1p96f;
     tlo_m1 = __float_as_uint(nrm * 0x1.00001p-60f) - 1u;
   }
-  // Group form of quot()'s guard (CHOCO_QCHECK 1): instead of testing every element's q0
+  // The guard, per 8-element group: instead of testing every element's q0
   // against [2^-60, 2^7] (three compares and four scalar mask operations per element),
   // the group keeps min(bits(t) - 1) and max(bits(q0)) in two VALU ops per element and
   // tests them once.  Conservative: t != 0 with t < T_lo covers every q0 < 2^-60 (and
   // some above it), bits(q0) > bits(2^7) covers q0 > 2^7, inf and NaN; a flagged group
-  // takes the IEEE division for all its elements, so the result is the same as quot()'s.
+  // takes the IEEE division for all its elements, so the result is the same as a per-element
+  // guard's (q0 in [2^-60, 2^7] or t == 0, norm in range).
   CHOCO_DEV float quot_nocheck(float t, uint32_t& tmin_m1, uint32_t& qmax) const {
     const float q0 = t * y;
     const float r = fmaf(-q0, norm, t);
@@ -343,13 +317,6 @@ struct QDiv {
   }
   CHOCO_DEV bool group_slow(uint32_t tmin_m1, uint32_t qmax) const {
     return !fast || tmin_m1 < tlo_m1 || qmax > 0x43000000u;
-  }
-  // returns t / norm; *slow set when this element needs the real division
-  CHOCO_DEV float quot(float t, bool& slow) const {
-    const float q0 = t * y;
-    const float r = fmaf(-q0, norm, t);
-    slow = !(fast && ((q0 >= 0x1p-60f && q0 <= 0x1p7f) || t == 0.0f));
-    return fmaf(r, y, q0);  // t = +0 (s * |d|): q0 = r = +0 -> +0, as 0 / norm
   }
 };
 
@@ -460,7 +427,6 @@ CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_
     }
     const int64_t e0 = eb + g * GS;
     float lf[kQPer];
-#if CHOCO_QCHECK
     uint32_t tmin_m1 = 0xFFFFFFFFu, qmax = 0u;
 #pragma unroll
     for (int c = 0; c < kQPer; ++c) lf[c] = D.quot_nocheck(sf * fabsf(d[g][c]), tmin_m1, qmax);  // s * x.abs() / norm
@@ -470,20 +436,6 @@ CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_
       for (int c = 0; c < kQPer; ++c)
         if (gslow) lf[c] = (sf * fabsf(d[g][c])) / P.norm;
     }
-#else
-    bool slow[kQPer];
-    bool any = false;
-#pragma unroll
-    for (int c = 0; c < kQPer; ++c) {
-      lf[c] = D.quot(sf * fabsf(d[g][c]), slow[c]);  // s * x.abs() / norm
-      any |= slow[c];
-    }
-    if (__builtin_expect(__ballot(any) != 0, 0)) {
-#pragma unroll
-      for (int c = 0; c < kQPer; ++c)
-        if (slow[c]) lf[c] = (sf * fabsf(d[g][c])) / P.norm;
-    }
-#endif
     float u[kQPer];
     if constexpr (UIN) {
       const float4 u0 = *reinterpret_cast<const float4*>(u_in + e0);
@@ -519,40 +471,24 @@ CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_
   }
 }
 
-// Occupancy of the one-tile quantize kernel (waves per SIMD the compiler must allow; A/B
-// knob).  r04 same-box A/B at 100M: 4 -> 131 us, 6 -> 132, 8 -> 136 (more waves did not
-// hide more latency: the 64-VGPR build spills one float4).
-#ifndef CHOCO_QQ_WAVES
-#define CHOCO_QQ_WAVES 4
-#endif
-// H = 2: a 512-thread workgroup per tile, each stream's four groups split over two
-// threads (waves 0-3 take groups 0-1, waves 4-7 groups 2-3 after stepping their stream
-// past the first eight uniforms) -- half the registers per thread, twice the waves
-// resident, the same uniforms.  Occupancy of the H = 2 build: CHOCO_QQ_HWAVES.
-#ifndef CHOCO_QQ_HALF
-#define CHOCO_QQ_HALF 1
-#endif
-#ifndef CHOCO_QQ_LOOP_ASM  // the looping kernel's prefetch as asm loads (see the kernel)
-#define CHOCO_QQ_LOOP_ASM 1
-#endif
-#ifndef CHOCO_QQ_DIAG_COAL
-#define CHOCO_QQ_DIAG_COAL 0
-#endif
-#ifndef CHOCO_QQ_DIAG_NOMATH
-#define CHOCO_QQ_DIAG_NOMATH 0
-#endif
-#ifndef CHOCO_QQ_HWAVES
-#define CHOCO_QQ_HWAVES 6
-#endif
+// Occupancy of the one-tile quantize kernel (waves per SIMD the compiler must allow).
+// r04 same-box A/B at 100M: 4 -> 131 us, 6 -> 132, 8 -> 136 (more waves did not hide
+// more latency: the 64-VGPR build spills one float4).
+constexpr int kQQWaves = 4;
+// H = 2 (the plain delta): a 512-thread workgroup per tile, each stream's four groups
+// split over two threads (waves 0-3 take groups 0-1, waves 4-7 groups 2-3 after stepping
+// their stream past the first eight uniforms) -- half the registers per thread, twice
+// the waves resident, the same uniforms; compiled for 6 waves per SIMD.
+constexpr int kQQHWaves = 6;
 template <int CW, bool XH, int H, bool UIN>
-__global__ __launch_bounds__(kQThreads * H, H == 1 ? (XH ? 4 : CHOCO_QQ_WAVES) : CHOCO_QQ_HWAVES) void qsgd_quant_kernel(
+__global__ __launch_bounds__(kQThreads * H, H == 1 ? kQQWaves : kQQHWaves) void qsgd_quant_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, const int64_t* __restrict__ seg_off,
     int nseg, int s_levels, int biased, const float* __restrict__ norms, const float* __restrict__ u_in,
     uint64_t seed, uint64_t offset, uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
     float* __restrict__ dense_out, int64_t tile_lo, int64_t tile_cnt, int64_t pad_e0, int64_t pad_len) {
   __shared__ int s_seg[2];
   // tiles [tile_lo, tile_lo + tile_cnt) of the buffer, walked in reverse (Infinity-Cache hits)
-  const int64_t tile = CHOCO_QQUANT_REV ? tile_lo + tile_cnt - 1 - (int64_t)blockIdx.x : tile_lo + (int64_t)blockIdx.x;
+  const int64_t tile = tile_lo + tile_cnt - 1 - (int64_t)blockIdx.x;
   const int64_t t_e0 = tile * kQStreamTile;
   const int64_t t_e1 = std::min<int64_t>(t_e0 + kQStreamTile, n);
   const int sg0 = tile_seg(seg_off, nseg, t_e0, t_e1, s_seg);
@@ -585,14 +521,8 @@ __global__ __launch_bounds__(kQThreads * H, H == 1 ? (XH ? 4 : CHOCO_QQ_WAVES) :
     float4 a[NG][2];
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-#if CHOCO_QQ_DIAG_COAL  // diagnostic only (wrong results): full-line loads, lane l at float4 l and 64 + l of its wave's run
-      const int64_t wb = eb - (int64_t)(st & 63) * kQPer;
-      a[g][0] = ld_quant4(x + wb + g * GS + 4 * (st & 63));
-      a[g][1] = ld_quant4(x + wb + g * GS + 256 + 4 * (st & 63));
-#else
       a[g][0] = ld_quant4(x + eb + g * GS);
       a[g][1] = ld_quant4(x + eb + g * GS + 4);
-#endif
     }
     if constexpr (XH) {
 #pragma unroll
@@ -611,247 +541,7 @@ __global__ __launch_bounds__(kQThreads * H, H == 1 ? (XH ? 4 : CHOCO_QQ_WAVES) :
   const QParam P = qparam(norms, seg_off, n, sg0, s_levels, biased != 0);
   QDiv D;
   D.init(P.norm);
-#if CHOCO_QQ_DIAG_NOMATH  // diagnostic only (wrong results): the loads and a sign-byte store, no math
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    uint32_t sb = 0;
-#pragma unroll
-    for (int c = 0; c < kQPer; ++c) sb |= d[g][c] < 0.f ? (1u << c) : 0u;
-#if CHOCO_QQ_DIAG_NOMATH == 2  // loads only (a store that never happens keeps them alive)
-    if (__float_as_uint(d[g][0]) == 0x7fc01234u)
-#endif
-    sign_plane[(eb + g * GS) / kQPer] = (uint8_t)sb;
-  }
-#else
   quant_tile_math<CW, NG, UIN>(d, tile, n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out, g0, st);
-#endif
-}
-
-// Single-segment buffers (the flat path, BASELINE cfg 3): a grid of resident workgroups
-// walks the full tiles from the end of the range backward (Infinity-Cache hits on the
-// tail the norm pass read last), workgroup b taking the (b + i G)-th tile from the end,
-// with the NEXT tile's loads issued before the current tile's math -- a wave's loads and
-// math overlap instead of alternating.  r04 counters on the one-tile kernel: waves waited
-// on memory 46 % of their cycles while VALU issue ran at ~37 % of the SIMDs' 2-cycle rate
-// (SQ_WAIT_ANY / SQ_WAVE_CYCLES, SQ_INSTS_VALU; profiles/r04_qsgd_sq_counters.txt).
-// Workgroup 0 also quantizes the range's partial last tile (tail_tile >= 0) and zeroes
-// the planes' padding.  Same uniforms and results as the one-tile kernel.
-template <int CW, bool XH, bool UIN>
-__global__ __launch_bounds__(kQThreads, 4) void qsgd_quant_loop_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, int64_t n, const int64_t* __restrict__ seg_off,
-    int s_levels, int biased, const float* __restrict__ norms, const float* __restrict__ u_in, uint64_t seed,
-    uint64_t offset, uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
-    float* __restrict__ dense_out, int64_t tile_lo, int64_t full_cnt, int64_t tail_tile, int64_t pad_e0,
-    int64_t pad_len) {
-  constexpr int GS = kQThreads * kQPer;  // 2048
-  if (blockIdx.x == 0) {
-    const int64_t g0 = pad_e0 / kQPer, groups = (pad_len + kQPer - 1) / kQPer;
-    const int64_t lvl_used = (g0 + groups) * CW, lvl_end = g0 * CW + (groups * CW + 15) / 16 * 16;
-    const int64_t sgn_used = g0 + groups, sgn_end = g0 + (groups + 15) / 16 * 16;
-    for (int64_t b = lvl_used + threadIdx.x; b < lvl_end; b += kQThreads) lvl_plane[b] = 0;
-    for (int64_t b = sgn_used + threadIdx.x; b < sgn_end; b += kQThreads) sign_plane[b] = 0;
-    if (tail_tile >= 0)
-      qsgd_quant_tile_slow<CW>(x, xh, n, seg_off, 1, s_levels, biased, norms, u_in, seed, offset, lvl_plane,
-                               sign_plane, dense_out, tail_tile, 0);
-  }
-  int64_t j = blockIdx.x;
-  if (j >= full_cnt) return;
-  const float sf = (float)s_levels;
-  const QParam P = qparam(norms, seg_off, n, 0, s_levels, biased != 0);
-  QDiv D;
-  D.init(P.norm);
-  auto tile_of = [&](int64_t jj) -> int64_t { return CHOCO_QQUANT_REV ? tile_lo + full_cnt - 1 - jj : tile_lo + jj; };
-  auto load = [&](int64_t tile, float4 (&a)[kQG][2], float4 (&h)[kQG][2]) {
-    const int64_t eb = tile * kQStreamTile + (int64_t)threadIdx.x * kQPer;
-#pragma unroll
-    for (int g = 0; g < kQG; ++g) {
-      a[g][0] = ld_quant4(x + eb + g * GS);
-      a[g][1] = ld_quant4(x + eb + g * GS + 4);
-    }
-    if constexpr (XH) {
-#pragma unroll
-      for (int g = 0; g < kQG; ++g) {
-        h[g][0] = ld_quant4(xh + eb + g * GS);
-        h[g][1] = ld_quant4(xh + eb + g * GS + 4);
-      }
-    }
-  };
-  float4 a[kQG][2], h[kQG][2];
-  load(tile_of(j), a, h);
-  for (;;) {
-    const int64_t jn = j + (int64_t)gridDim.x;
-    const bool more = jn < full_cnt;  // workgroup-uniform
-    float4 b[kQG][2], bh[kQG][2];
-#if CHOCO_QQ_LOOP_ASM
-    // the next tile's loads as asm: the compiler's wait pass does not see them, so it
-    // cannot make the current tile's math wait for them (it did: vmcnt at the loop head
-    // covered two of them); one counted wait after the math, tied to the registers
-    choco_f32x4 bq[kQG][2];
-    static_assert(!XH, "the asm prefetch covers the plain delta");
-    if (more) {
-      const int64_t ebn = tile_of(jn) * kQStreamTile + (int64_t)threadIdx.x * kQPer;
-#pragma unroll
-      for (int g = 0; g < kQG; ++g) {
-        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bq[g][0]) : "v"(x + ebn + g * GS) : "memory");
-        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bq[g][1]) : "v"(x + ebn + g * GS + 4) : "memory");
-      }
-    }
-#else
-    if (more) load(tile_of(jn), b, bh);
-#endif
-    float d[kQG][kQPer];
-#pragma unroll
-    for (int g = 0; g < kQG; ++g) {
-      float4 v0 = a[g][0], v1 = a[g][1];
-      if constexpr (XH) {
-        v0 = sub4(v0, h[g][0]);
-        v1 = sub4(v1, h[g][1]);
-      }
-      d[g][0] = v0.x; d[g][1] = v0.y; d[g][2] = v0.z; d[g][3] = v0.w;
-      d[g][4] = v1.x; d[g][5] = v1.y; d[g][6] = v1.z; d[g][7] = v1.w;
-    }
-    quant_tile_math<CW, kQG, UIN>(d, tile_of(j), n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out);
-    if (!more) break;
-#if CHOCO_QQ_LOOP_ASM
-    asm volatile("s_waitcnt vmcnt(0)"
-                 : "+v"(bq[0][0]), "+v"(bq[0][1]), "+v"(bq[1][0]), "+v"(bq[1][1]), "+v"(bq[2][0]), "+v"(bq[2][1]),
-                   "+v"(bq[3][0]), "+v"(bq[3][1])
-                 :
-                 : "memory");
-#pragma unroll
-    for (int g = 0; g < kQG; ++g) {
-      b[g][0] = make_float4(bq[g][0].x, bq[g][0].y, bq[g][0].z, bq[g][0].w);
-      b[g][1] = make_float4(bq[g][1].x, bq[g][1].y, bq[g][1].z, bq[g][1].w);
-    }
-#endif
-#pragma unroll
-    for (int g = 0; g < kQG; ++g) {
-      a[g][0] = b[g][0];
-      a[g][1] = b[g][1];
-      if constexpr (XH) {
-        h[g][0] = bh[g][0];
-        h[g][1] = bh[g][1];
-      }
-    }
-    j = jn;
-  }
-}
-
-// The ring quantize (single-segment buffers without x_hat, stream uniforms; CHOCO_QQ_RING):
-// the tile's loads land in LDS, not in registers, so a wave keeps the next units' loads in
-// flight while it computes.  A wave unit is one split-stream half tile (the H = 2 mapping:
-// 64 streams x 2 groups, 4 KiB); resident waves walk the units from the end of the range
-// backward, each with a ring of kQRingD unit slots in LDS filled by global_load_lds
-// (lane l's 16 bytes land at slot + 16 l: loads are issued so that lane l finds its own
-// eight elements of a group at the same offset of two 1 KiB pieces -- conflict-free reads).
-// No barrier: each wave reads only what it loaded.  The waits are counted here, not by
-// the compiler: before unit j's reads, the ops issued after unit j's loads may remain
-// (the later units' loads and the stores of the units computed since).
-#ifndef CHOCO_QQ_RING
-#define CHOCO_QQ_RING 0
-#endif
-#ifndef CHOCO_QQ_RING_D  // ring depth (unit slots per wave)
-#define CHOCO_QQ_RING_D 3
-#endif
-#ifndef CHOCO_QQ_RING_WGS  // resident 256-thread workgroups per CU
-#define CHOCO_QQ_RING_WGS 3
-#endif
-constexpr int kQRingD = CHOCO_QQ_RING_D;
-typedef __attribute__((address_space(3))) void* choco_lds_ptr;
-CHOCO_DEV void glds16(const float* g, float4* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(g, (choco_lds_ptr)lds_wave_base, 16, 0, 0);
-}
-template <int N>
-CHOCO_DEV void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-// The lane's float4 of each of a unit's four 1 KiB pieces (p = the lane's float4 of
-// piece 0), after the wait: the compiler does not see the DMA's LDS writes, so the
-// reads are asm too (one wait for the four).
-CHOCO_DEV void lds_read_unit(const float4* p, float4 (&o)[4]) {
-  choco_f32x4 v0, v1, v2, v3;
-  const uint32_t a = (uint32_t)(uintptr_t)(choco_lds_ptr)p;
-  asm volatile(
-      "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\tds_read_b128 %2, %4 offset:2048\n\t"
-      "ds_read_b128 %3, %4 offset:3072\n\ts_waitcnt lgkmcnt(0)"
-      : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)
-      : "v"(a)
-      : "memory");
-  o[0] = make_float4(v0.x, v0.y, v0.z, v0.w);
-  o[1] = make_float4(v1.x, v1.y, v1.z, v1.w);
-  o[2] = make_float4(v2.x, v2.y, v2.z, v2.w);
-  o[3] = make_float4(v3.x, v3.y, v3.z, v3.w);
-}
-
-template <int CW>
-__global__ __launch_bounds__(kQThreads, 3) void qsgd_quant_ring_kernel(
-    const float* __restrict__ x, int64_t n, const int64_t* __restrict__ seg_off, int s_levels, int biased,
-    const float* __restrict__ norms, uint64_t seed, uint64_t offset, uint8_t* __restrict__ lvl_plane,
-    uint8_t* __restrict__ sign_plane, float* __restrict__ dense_out, int64_t tile_lo, int64_t full_cnt,
-    int64_t tail_tile, int64_t pad_e0, int64_t pad_len) {
-  __shared__ float4 ring[kQThreads / 64][kQRingD][4][64];
-  constexpr int GS = kQThreads * kQPer;  // 2048
-  if (blockIdx.x == 0) {
-    const int64_t g0 = pad_e0 / kQPer, groups = (pad_len + kQPer - 1) / kQPer;
-    const int64_t lvl_used = (g0 + groups) * CW, lvl_end = g0 * CW + (groups * CW + 15) / 16 * 16;
-    const int64_t sgn_used = g0 + groups, sgn_end = g0 + (groups + 15) / 16 * 16;
-    for (int64_t b = lvl_used + threadIdx.x; b < lvl_end; b += kQThreads) lvl_plane[b] = 0;
-    for (int64_t b = sgn_used + threadIdx.x; b < sgn_end; b += kQThreads) sign_plane[b] = 0;
-    if (tail_tile >= 0)
-      qsgd_quant_tile_slow<CW>(x, nullptr, n, seg_off, 1, s_levels, biased, norms, nullptr, seed, offset,
-                               lvl_plane, sign_plane, dense_out, tail_tile, 0);
-  }
-  const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
-  const int64_t gw = (int64_t)blockIdx.x * (kQThreads / 64) + w, TW = (int64_t)gridDim.x * (kQThreads / 64);
-  const int64_t nunits = full_cnt * 8;
-  if (gw >= nunits) return;  // wave-uniform; no barrier below
-  const int64_t cnt = (nunits - gw + TW - 1) / TW;
-  const float sf = (float)s_levels;
-  const QParam P = qparam(norms, seg_off, n, 0, s_levels, biased != 0);
-  QDiv D;
-  D.init(P.norm);
-  // unit u: tile (from the end of the range) u >> 3, wave slot ws = u & 7 (streams
-  // 64 (ws & 3) .. +63, groups 2 (ws >> 2) .. +1)
-  auto unit_tile = [&](int64_t j) { return tile_lo + full_cnt - 1 - ((gw + j * TW) >> 3); };
-  auto unit_ws = [&](int64_t j) { return (int)((gw + j * TW) & 7); };
-  auto issue = [&](int64_t j) {
-    const int ws = unit_ws(j);
-    const float* base = x + unit_tile(j) * kQStreamTile + (int64_t)(ws & 3) * 512 + (int64_t)lane * kQPer +
-                        (int64_t)(ws >> 2) * 2 * GS;
-    float4(&slot)[4][64] = ring[w][(int)(j % kQRingD)];
-    glds16(base, slot[0]);
-    glds16(base + 4, slot[1]);
-    glds16(base + GS, slot[2]);
-    glds16(base + GS + 4, slot[3]);
-  };
-  const bool dense = dense_out != nullptr;
-#pragma unroll 1
-  for (int64_t j = 0; j < kQRingD - 1 && j < cnt; ++j) issue(j);
-#pragma unroll 1
-  for (int64_t j = 0; j < cnt; ++j) {
-    const bool more = j + kQRingD - 1 < cnt;
-    if (more) issue(j + kQRingD - 1);
-    // steady state: the D - 1 later units' loads (4 each) and the stores of the D - 1
-    // units computed since unit j's loads (4, or 8 with the dense output) may remain
-    if (more && j >= kQRingD - 1) {
-      if (dense) wait_vm<(kQRingD - 1) * 12>(); else wait_vm<(kQRingD - 1) * 8>();
-    } else {
-      wait_vm<0>();
-    }
-    const float4(&slot)[4][64] = ring[w][(int)(j % kQRingD)];
-    static_assert(sizeof(slot[0]) == 1024, "pieces of 1 KiB");
-    float4 a[4];
-    lds_read_unit(&slot[0][lane], a);
-    float d[2][kQPer];
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      d[g][0] = a[2 * g].x; d[g][1] = a[2 * g].y; d[g][2] = a[2 * g].z; d[g][3] = a[2 * g].w;
-      d[g][4] = a[2 * g + 1].x; d[g][5] = a[2 * g + 1].y; d[g][6] = a[2 * g + 1].z; d[g][7] = a[2 * g + 1].w;
-    }
-    const int ws = unit_ws(j);
-    quant_tile_math<CW, 2, false>(d, unit_tile(j), n, P, D, sf, nullptr, seed, offset, lvl_plane, sign_plane,
-                                  dense_out, (ws >> 2) * 2, (ws & 3) * 64 + lane);
-  }
 }
 
 // ---------------------------------------------------------------- decode / accumulate
@@ -872,18 +562,7 @@ CHOCO_DEV float qdecode(uint32_t level, bool neg, const QParam& P, float sf) {
   return (((P.scale * sg) * P.norm) * lvl) / sf;
 }
 
-#ifndef CHOCO_QDEC_ST_NT  // non-temporal x_hat / memory stores in the decode (A/B knob)
-#define CHOCO_QDEC_ST_NT 0
-#endif
-CHOCO_DEV void st_dec4(float* p, float4 v) {
-  if (CHOCO_QDEC_ST_NT) {
-    choco_f32x4 f;
-    f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
-    __builtin_nontemporal_store(f, reinterpret_cast<choco_f32x4*>(p));
-  } else {
-    *reinterpret_cast<float4*>(p) = v;
-  }
-}
+CHOCO_DEV void st_dec4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 // MODE 0: out = decode(msg 0); MODE 1: accumulate all messages into hat/mem.
 template <int CW, int NM, int MODE>
@@ -1052,17 +731,12 @@ static int qsgd_norms_launch(const float* x, const float* xhat, int64_t n, const
 // group (lvl_plane / sign_plane point at element 0's group; a range call writes
 // only the groups of its elements, plus the 16-byte padding of a plane that ends
 // at e1).
-// A/B knob: the looping quantize kernel for single-segment buffers (0: one tile per workgroup)
-#ifndef CHOCO_QQ_LOOP
-#define CHOCO_QQ_LOOP 0
-#endif
-#ifndef CHOCO_QQ_GRID  // resident workgroups of the looping kernel: 4 per CU (16 waves)
-#define CHOCO_QQ_GRID 1024
-#endif
-constexpr int64_t kQLoopGrid = CHOCO_QQ_GRID;
 // split streams for the plain delta only: with x_hat (the gossip form) the one-stream
-// threads measured faster (r4u2: 151.5-153.4 against 154.8-157.6 us)
-constexpr int kQH = CHOCO_QQ_HALF ? 2 : 1;
+// threads measured faster (r4u2: 151.5-153.4 against 154.8-157.6 us).  Measured slower and
+// removed from the source (git history: r04): a looping kernel with the next tile's loads
+// in flight (141-147 us, also with its prefetch as asm loads), an LDS-DMA ring (149-156 us)
+// -- against 122-128 us for this one-tile kernel.
+constexpr int kQH = 2;
 static int qsgd_quant_launch(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg,
                              int32_t q, int32_t is_biased, const float* norms, const float* u_in, uint64_t seed,
                              uint64_t offset, uint8_t* lvl_plane, uint8_t* sign_plane, float* dense_out,
@@ -1072,61 +746,6 @@ static int qsgd_quant_launch(const float* x, const float* xhat, int64_t n, const
   const int64_t tile_lo = e0 / kQStreamTile;
   const int64_t tile_cnt = (e1 - e0 + kQStreamTile - 1) / kQStreamTile;
   profile_begin("qsgd_quantize", st);
-  // (with x_hat the prefetch would need 64 more registers: the one-tile kernel, no spills)
-  if (CHOCO_QQ_RING && nseg <= 1 && !xhat && !u_in) {
-    const bool partial = (tile_lo + tile_cnt) * kQStreamTile > n;
-    const int64_t full_cnt = tile_cnt - (partial ? 1 : 0);
-    const int64_t tail_tile = partial ? tile_lo + tile_cnt - 1 : -1;
-    const int64_t waves = full_cnt * 8;
-    const unsigned grid = (unsigned)std::max<int64_t>(
-        1, std::min<int64_t>((waves + 3) / 4, (int64_t)256 * CHOCO_QQ_RING_WGS));
-#define CHOCO_QR(CWV)                                                                                         \
-  case CWV:                                                                                                   \
-    CHOCO_KLAUNCH((qsgd_quant_ring_kernel<CWV>), dim3(grid), dim3(kQThreads), 0, st, x, n, seg_off, s_levels,  \
-                  is_biased, norms, seed, offset, lvl_plane, sign_plane, dense_out, tile_lo, full_cnt,         \
-                  tail_tile, pad_e0, e1 - pad_e0);                                                            \
-    break;
-    switch (cw) {
-      CHOCO_QR(1)
-      CHOCO_QR(2)
-      CHOCO_QR(4)
-      CHOCO_QR(8)
-      CHOCO_QR(16)
-    }
-#undef CHOCO_QR
-    profile_end("qsgd_quantize", st);
-    CHOCO_LAUNCHED("qsgd_quant_ring_kernel");
-    return CHOCO_OK;
-  }
-  if (CHOCO_QQ_LOOP && nseg <= 1 && !xhat) {
-    // full tiles of the range, and its partial last tile (the buffer's end)
-    const bool partial = (tile_lo + tile_cnt) * kQStreamTile > n;
-    const int64_t full_cnt = tile_cnt - (partial ? 1 : 0);
-    const int64_t tail_tile = partial ? tile_lo + tile_cnt - 1 : -1;
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(full_cnt, kQLoopGrid));
-#define CHOCO_QL(CWV)                                                                                         \
-  case CWV:                                                                                                   \
-    if (u_in)                                                                                                 \
-      CHOCO_KLAUNCH((qsgd_quant_loop_kernel<CWV, false, true>), dim3(grid), dim3(kQThreads), 0, st, x,        \
-                    nullptr, n, seg_off, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane,            \
-                    sign_plane, dense_out, tile_lo, full_cnt, tail_tile, pad_e0, e1 - pad_e0);                \
-    else                                                                                                      \
-      CHOCO_KLAUNCH((qsgd_quant_loop_kernel<CWV, false, false>), dim3(grid), dim3(kQThreads), 0, st, x,       \
-                    nullptr, n, seg_off, s_levels, is_biased, norms, u_in, seed, offset, lvl_plane,            \
-                    sign_plane, dense_out, tile_lo, full_cnt, tail_tile, pad_e0, e1 - pad_e0);                \
-    break;
-    switch (cw) {
-      CHOCO_QL(1)
-      CHOCO_QL(2)
-      CHOCO_QL(4)
-      CHOCO_QL(8)
-      CHOCO_QL(16)
-    }
-#undef CHOCO_QL
-    profile_end("qsgd_quantize", st);
-    CHOCO_LAUNCHED("qsgd_quant_loop_kernel");
-    return CHOCO_OK;
-  }
 #define CHOCO_Q1(CWV, XHV, UINV)                                                                              \
   CHOCO_KLAUNCH((qsgd_quant_kernel<CWV, XHV, XHV ? 1 : kQH, UINV>), dim3((unsigned)tile_cnt),                  \
                 dim3(kQThreads * (XHV ? 1 : kQH)), 0,                                                          \

@@ -71,10 +71,7 @@ constexpr int kRkWords = (int)(kRkTile / 32);            // 8192 bitmap words pe
 // passes): R2 itself 41.6-41.7 (4) / 41.1-41.3 (8) / 41.8-43.3 us (16); the sparse
 // accumulate after it 78.7-79.3 / 77.4-77.7 / 76.1-76.9 us; step 0.1406-0.1415 /
 // 0.1384-0.1405 / 0.1385-0.1391 ms.
-#ifndef CHOCO_RK_Q  // workgroups per tile (A/B knob)
-#define CHOCO_RK_Q 8
-#endif
-constexpr int kRkQ = CHOCO_RK_Q;
+constexpr int kRkQ = 8;  // workgroups per tile (4: 41.6 us, 16: no better; r04)
 constexpr int kRkQThreads = 256;
 constexpr int kRkQWords = kRkWords / kRkQ;               // 1024 at kRkQ = 8
 constexpr int kRkWpt = kRkQWords / kRkQThreads;          // 4 words (128 bits) per thread at kRkQ = 8

@@ -321,15 +321,6 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
 // bytes): the row offset is a wave-uniform SGPR operand and the lane offset
 // one VGPR, so the 2 x RU loads in flight need no 64-bit address registers.
 
-#ifndef CHOCO_SIGN_GS_RU  // rows per group with the fused gossip step (3 streams)
-#define CHOCO_SIGN_GS_RU 8
-#endif
-#ifndef CHOCO_SIGN_GS_FUSE  // 0: the standalone consensus step, then the x - x_hat pack (A/B)
-#define CHOCO_SIGN_GS_FUSE 1
-#endif
-#ifndef CHOCO_SIGN_NT  // non-temporal loads in the one-segment pack
-#define CHOCO_SIGN_NT 1
-#endif
 // GS: the fused gossip step -- x, memory and xh rows in flight, x_new stored back
 // (each lane owns its float4 of every row run: no overlap), d = x_new - xh.
 template <bool XH, bool NORM, bool GS = false>
@@ -340,7 +331,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
                                                                   SignWs* __restrict__ ws, Gossip gs, int64_t blk0,
                                                                   int finish) {
   static_assert(!GS || XH, "the gossip step needs x_hat");
-  constexpr int RU = GS ? CHOCO_SIGN_GS_RU : (XH ? 4 : 8);  // rows per group (more streams, more registers)
+  constexpr int RU = GS ? 8 : (XH ? 4 : 8);  // rows per group (more streams, more registers)
   constexpr int NG = 32 / RU;
   __shared__ double s_red[kSignThreads / 64];
   __shared__ unsigned int s_flag;
@@ -363,14 +354,14 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
   };
   auto load_group = [&](int g, Group& G) {
 #pragma unroll
-    for (int u = 0; u < RU; ++u) G.x[u] = ld_buf4s<CHOCO_SIGN_NT>(rx, voff, row_off(g * RU + u));
+    for (int u = 0; u < RU; ++u) G.x[u] = ld_buf4s<true>(rx, voff, row_off(g * RU + u));
     if (XH) {
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.h[u] = ld_buf4s<CHOCO_SIGN_NT>(rh, voff, row_off(g * RU + u));
+      for (int u = 0; u < RU; ++u) G.h[u] = ld_buf4s<true>(rh, voff, row_off(g * RU + u));
     }
     if (GS) {
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.m[u] = ld_buf4s<CHOCO_SIGN_NT>(rm, voff, row_off(g * RU + u));
+      for (int u = 0; u < RU; ++u) G.m[u] = ld_buf4s<true>(rm, voff, row_off(g * RU + u));
     }
   };
   uint32_t wd[4] = {0u, 0u, 0u, 0u};
@@ -542,19 +533,14 @@ CHOCO_DEV float seg_scale(const SignMsgs& M, int q, const int64_t* __restrict__ 
   return nm / (float)numel;
 }
 
-#ifndef CHOCO_SIGN_ACC_RU  // rows per load group in the receiver (A/B knob)
-#define CHOCO_SIGN_ACC_RU 4
-#endif
+constexpr int kSAccRU = 4;  // rows per load group in the receiver
 // Rows of the (32, N') view one receiver workgroup covers (32 / kSAccRows workgroups
 // per 1024-column block).  Block L -> (column block, row block) keeps the row blocks
 // of one column block on ONE XCD (linear ids congruent mod 8), so their word loads
 // hit that XCD's L2.
-#ifndef CHOCO_SIGN_ACC_RG
-#define CHOCO_SIGN_ACC_RG 8
-#endif
-constexpr int kSAccRows = CHOCO_SIGN_ACC_RG;
+constexpr int kSAccRows = 8;
 constexpr int kSAccRB = 32 / kSAccRows;  // row blocks per column block
-static_assert(kSAccRows % CHOCO_SIGN_ACC_RU == 0 && 32 % kSAccRows == 0, "row blocking");
+static_assert(kSAccRows % kSAccRU == 0 && 32 % kSAccRows == 0, "row blocking");
 CHOCO_DEV void sign_acc_block(uint32_t L, int64_t& cb, int& rb) {
   if (kSAccRB == 1) {
     cb = L;
@@ -604,7 +590,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
   }
   // interior workgroups: unconditional loads keep all RU rows in flight
   const bool interior = ncol == 256 && (int64_t)31 * Np + j0 + 260 <= n;
-  constexpr int RU = CHOCO_SIGN_ACC_RU;
+  constexpr int RU = kSAccRU;
   bool all_uniform = true;
 #pragma unroll
   for (int r = 0; r < kSAccRows; ++r) all_uniform &= s_lo[rb + r] == s_hi[rb + r];
@@ -791,128 +777,9 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
   }
 }
 
-// One-segment receiver (nseg == 1, the flat buffer; n * 4 < 2^32 bytes).  A wave
-// owns 1024 consecutive columns (words) as 4 sub-runs of 256: lane l holds words
-// j0 + 256s + 4l .. +3 of every message, so in row r its elements are the 1024
-// CONSECUTIVE floats r*N' + j0 .. +1023 -- 4 KiB runs instead of 1 KiB ones.
-// Every lane loads and stores the float4 at its OWN element offset with
-// dword-aligned buffer loads / stores (N' = 2 mod 4 at both BASELINE sizes, so
-// half the rows start 8 B off a 16-B boundary): no realigning shuffle, no tail
-// element, and a line shared with the neighbouring wave only at the two ends of
-// each 4 KiB run.  Rows go in pairs with two pairs in flight (A/B).
-// Measured SLOWER than the column-tile receiver (1208 vs 1127 us at 345M, one
-// message): the dword-aligned 16-B stores cost more than the longer runs save.
-// Kept as a diagnostic variant (CHOCO_SIGN_ACC1=1).
-#ifndef CHOCO_SIGN_ACC1
-#define CHOCO_SIGN_ACC1 0
-#endif
-constexpr int kSA1Cols = 1024;               // columns per wave
-constexpr int kSA1Waves = 4;
-constexpr int kSA1WgCols = kSA1Cols * kSA1Waves;
-constexpr int kSA1RU = 2;                    // rows per group
-
-
-template <int NM, bool HS>
-__global__ __launch_bounds__(64 * kSA1Waves) void sign_accumulate1_kernel(SignMsgs M, int64_t n, int64_t Np,
-                                                                          float* __restrict__ hat,
-                                                                          float* __restrict__ mem) {
-  const int lane = lane_id(), w = threadIdx.x >> 6;
-  const int64_t j0 = (int64_t)blockIdx.x * kSA1WgCols + (int64_t)w * kSA1Cols;
-  if (j0 >= Np) return;  // wave-uniform; no workgroup barrier in this kernel
-  const int ncol = (int)std::min<int64_t>(kSA1Cols, Np - j0);
-  float sc[kMaxMsg];
-#pragma unroll
-  for (int q = 0; q < NM; ++q) sc[q] = M.norms[q][0] / (float)n;  // (norm / numel), exact per message
-  uint32_t wd[NM][4][4];
-#pragma unroll
-  for (int q = 0; q < NM; ++q)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int64_t j = j0 + 256 * s + 4 * lane;
-      if (j + 3 < Np) {
-        const uint4 v = *reinterpret_cast<const uint4*>(M.packed[q] + j);
-        wd[q][s][0] = v.x; wd[q][s][1] = v.y; wd[q][s][2] = v.z; wd[q][s][3] = v.w;
-      } else {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) wd[q][s][c] = (j + c < Np) ? M.packed[q][j + c] : 0u;
-      }
-    }
-  auto apply = [&](int r, int s, float4 h4, float4 m4, float4& ho, float4& mo) {
-    float hv[4] = {h4.x, h4.y, h4.z, h4.w}, mv[4] = {m4.x, m4.y, m4.z, m4.w};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-#pragma unroll
-      for (int q = 0; q < NM; ++q) {
-        const float u = ((wd[q][s][c] >> r) & 1u) ? -sc[q] : sc[q];
-        if (HS && q == M.self_slot) hv[c] = hv[c] + u;
-        mv[c] = sign_axpy(M, q, u, mv[c]);  // torch add_(u, alpha=w) fuses on CPU (verified)
-      }
-    }
-    ho = make_float4(hv[0], hv[1], hv[2], hv[3]);
-    mo = make_float4(mv[0], mv[1], mv[2], mv[3]);
-  };
-  const bool interior = ncol == kSA1Cols && (int64_t)31 * Np + j0 + kSA1Cols <= n;
-  if (interior) {
-    const __amdgpu_buffer_rsrc_t rm = buf_rsrc(mem, (uint32_t)(n * 4));
-    const __amdgpu_buffer_rsrc_t rh = buf_rsrc(HS ? hat : mem, (uint32_t)(n * 4));
-    const uint32_t voff = 16u * (uint32_t)lane;
-    auto row_off = [&](int r) -> uint32_t { return (uint32_t)(((int64_t)r * Np + j0) * 4); };  // wave-uniform
-    auto load = [&](int g, float4 (&Mr)[kSA1RU][4], float4 (&Hr)[kSA1RU][4]) {
-#pragma unroll
-      for (int u = 0; u < kSA1RU; ++u)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          Mr[u][s] = ld_buf4s<false>(rm, voff + 1024u * s, row_off(g * kSA1RU + u));
-          if (HS) Hr[u][s] = ld_buf4s<false>(rh, voff + 1024u * s, row_off(g * kSA1RU + u));
-        }
-    };
-    auto proc = [&](int g, const float4 (&Mr)[kSA1RU][4], const float4 (&Hr)[kSA1RU][4]) {
-#pragma unroll
-      for (int u = 0; u < kSA1RU; ++u)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          float4 ho, mo;
-          apply(g * kSA1RU + u, s, HS ? Hr[u][s] : Mr[u][s], Mr[u][s], ho, mo);
-          st_buf4s(rm, voff + 1024u * s, row_off(g * kSA1RU + u), mo);
-          if (HS) st_buf4s(rh, voff + 1024u * s, row_off(g * kSA1RU + u), ho);
-        }
-    };
-    constexpr int NG = 32 / kSA1RU;
-    float4 MA[kSA1RU][4], HA[kSA1RU][4], MB[kSA1RU][4], HB[kSA1RU][4];
-    load(0, MA, HA);
-    load(1, MB, HB);
-#pragma unroll 1
-    for (int g = 0; g < NG; g += 2) {
-      proc(g, MA, HA);
-      if (g + 2 < NG) load(g + 2, MA, HA);
-      proc(g + 1, MB, HB);
-      if (g + 3 < NG) load(g + 3, MB, HB);
-    }
-    return;
-  }
-  // the last waves: guarded element path
-#pragma unroll 1
-  for (int r = 0; r < 32; ++r) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int col = 256 * s + 4 * lane;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int64_t e = (int64_t)r * Np + j0 + col + c;
-        if (col + c >= ncol || e >= n) continue;
-        float h = HS ? hat[e] : 0.f, m = mem[e];
-#pragma unroll
-        for (int q = 0; q < NM; ++q) {
-          const float u = ((wd[q][s][c] >> r) & 1u) ? -sc[q] : sc[q];
-          if (HS && q == M.self_slot) h = h + u;
-          m = sign_axpy(M, q, u, m);
-        }
-        mem[e] = m;
-        if (HS) hat[e] = h;
-      }
-    }
-  }
-}
+// (A one-segment receiver with 4 KiB row runs per wave and dword-aligned 16-B stores
+// measured slower than the column-tile receiver, 1208 vs 1127 us at 345M, one message:
+// removed, git history r03.)
 
 // DeepSqueezeSignCompressor.compress's local copy of the message
 // (deep_squeeze.py:416-422): out = (norm_s * torch.sign(x)) / numel_s -- sign(0) = 0
@@ -995,12 +862,6 @@ static int sign_compress(const float* x, const float* xhat, int64_t n, const int
     CHOCO_REQUIRE(ws && ws_bytes >= choco_sign_workspace_size(nseg), "sign workspace too small");
   }
   const bool one = nseg == 1 && n < (int64_t(1) << 30);  // one segment, buffer offsets: n * 4 < 2^32 bytes
-  if (gs.mem && !CHOCO_SIGN_GS_FUSE) {
-    CHOCO_REQUIRE(w0 == 0 && w1 == Np, "the unfused gossip build packs whole buffers only");
-    const int rc = gossip_launch(const_cast<float*>(x), gs.mem, xhat, gs.gamma, n, st);
-    if (rc) return rc;
-    gs.mem = nullptr;
-  }
   const int fin = finish ? 1 : 0;
   profile_begin("sign_pack", st);
   if (gs.mem) {
@@ -1086,32 +947,6 @@ CHOCO_API int choco_sign_decompress_accumulate(const int32_t* const* packed_list
   const int64_t Np = choco_sign_words(n);
   const unsigned grid = sign_acc_grid(Np);
   profile_begin("sign_accumulate", st);
-  if (nseg == 1 && n < (int64_t(1) << 30) && CHOCO_SIGN_ACC1) {
-    const unsigned g1 = (unsigned)((Np + kSA1WgCols - 1) / kSA1WgCols);
-#define CHOCO_SIGN_ACC1_CASE(NM)                                                                            \
-  case NM:                                                                                                  \
-    if (self_slot >= 0 && xhat_self)                                                                        \
-      CHOCO_KLAUNCH((sign_accumulate1_kernel<NM, true>), dim3(g1), dim3(64 * kSA1Waves), 0, st, M, n, Np,   \
-                    xhat_self, memory);                                                                     \
-    else                                                                                                    \
-      CHOCO_KLAUNCH((sign_accumulate1_kernel<NM, false>), dim3(g1), dim3(64 * kSA1Waves), 0, st, M, n, Np,  \
-                    xhat_self, memory);                                                                     \
-    break;
-    switch (nmsg) {
-      CHOCO_SIGN_ACC1_CASE(1)
-      CHOCO_SIGN_ACC1_CASE(2)
-      CHOCO_SIGN_ACC1_CASE(3)
-      CHOCO_SIGN_ACC1_CASE(4)
-      CHOCO_SIGN_ACC1_CASE(5)
-      CHOCO_SIGN_ACC1_CASE(6)
-      CHOCO_SIGN_ACC1_CASE(7)
-      CHOCO_SIGN_ACC1_CASE(8)
-    }
-#undef CHOCO_SIGN_ACC1_CASE
-    profile_end("sign_accumulate", st);
-    CHOCO_LAUNCHED("sign_accumulate1_kernel");
-    return CHOCO_OK;
-  }
 #define CHOCO_SIGN_ACC(NM)                                                                                 \
   case NM:                                                                                                  \
     if (self_slot >= 0 && xhat_self)                                                                        \

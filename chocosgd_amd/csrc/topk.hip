@@ -50,21 +50,13 @@ namespace choco {
 
 constexpr int kK2Threads = 1024;          // 16 waves, each a contiguous range of the tile
 constexpr int kK2Waves = kK2Threads / 64;
-// Diagnostic knob (tools/build_variants.py): tiles per launch.
-#ifndef CHOCO_K2_TARGET  // one workgroup per CU (256 CUs): no two tiles compete on a CU
-#define CHOCO_K2_TARGET 256
-#endif
 constexpr int kK2Unroll = 8;            // float4 rows per wave per load batch (8 KiB in flight)
-constexpr int64_t kK2Target = CHOCO_K2_TARGET;
+constexpr int64_t kK2Target = 256;      // tiles per launch: one workgroup per CU, no two tiles compete on a CU
 constexpr int64_t kTileQuant = (int64_t)kK2Waves * kK2Unroll * 256;   // 32768 elements
 static_assert(kK2Target <= 1024, "K34 keeps one tile per thread");
-// Elements a wave claims at a time (LDS counter): one load batch (2048) or two.
-#ifndef CHOCO_K2_CHUNK
-#define CHOCO_K2_CHUNK 2048
-#endif
-constexpr int64_t kChunk = CHOCO_K2_CHUNK;
-static_assert(kTileQuant % kChunk == 0 && kChunk % (256 * kK2Unroll) == 0, "chunk geometry");
-static_assert(kChunk == 256 * kK2Unroll || kChunk == 512 * kK2Unroll, "a chunk is one or two load batches");
+// Elements a wave claims at a time (LDS counter): one load batch.
+constexpr int64_t kChunk = 256 * kK2Unroll;
+static_assert(kTileQuant % kChunk == 0, "chunk geometry");
 constexpr int kMaybeCap = 65536;        // side-list capacity per tile (maybe keys)
 constexpr int kNBucket = 256;           // 255 "maybe" buckets + 1 "sure"
 constexpr int kNMaybe = kNBucket - 1;
@@ -98,28 +90,6 @@ __device__ unsigned long long g_stamps[kStampSlots][4];
   do {                  \
   } while (0)
 #endif
-
-// Diagnostic knobs: cache policy of the stream kernel's candidate/side stores
-// and of the finish kernel's output stores (0 plain, 1 nt, 2 sc1 write-through).
-#ifndef CHOCO_K2_STORE
-#define CHOCO_K2_STORE 0
-#endif
-#ifndef CHOCO_K34_PREFETCH
-#define CHOCO_K34_PREFETCH 2
-#endif
-#ifndef CHOCO_K34_STORE
-#define CHOCO_K34_STORE 0
-#endif
-template <int POL, class T>
-CHOCO_DEV void st_pol(T* p, T v) {
-  if constexpr (POL == 1) {
-    __builtin_nontemporal_store(v, p);
-  } else if constexpr (POL == 2) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    *p = v;
-  }
-}
 
 enum TileMode { kTakeNone = 0, kTakeAll = 1, kTakePartial = 2 };
 
@@ -243,10 +213,7 @@ __global__ __launch_bounds__(256) void topk_all_kernel(const float* __restrict__
 // without a grid-wide hand-off.  Both bounds are heuristics that K34 verifies
 // (G[0] >= k, G[sure] < k); any k/n works.
 // ----------------------------------------------------------------------------
-#ifndef CHOCO_SAMPLE_RUNS
-#define CHOCO_SAMPLE_RUNS 64
-#endif
-constexpr int kSampleRuns = CHOCO_SAMPLE_RUNS;  // runs of 256 contiguous elements
+constexpr int kSampleRuns = 64;  // runs of 256 contiguous elements
 constexpr int kSampleN = kSampleRuns * 256;                  // 16384 at 64 runs
 constexpr int kK1Threads = 1024;                              // the bounds kernel: one workgroup
 constexpr int kSampleLoads = kSampleRuns * 64 / kK1Threads;  // float4 per thread (4)
@@ -426,9 +393,6 @@ struct StreamSmem {
 // evicted (and written back) in the middle of the stream.  Measured in the
 // bench step (the previous step's sparse accumulate leaves ~120 MB dirty):
 // K2 130 -> 83 us; back to back, cold caches: 89.6 -> 82.9 us.
-#ifndef CHOCO_STREAM_NT
-#define CHOCO_STREAM_NT 1
-#endif
 constexpr uint32_t kNoChunk = 0x80000000u;  // > any tile's bytes (tile <= 2^31 / 256 elements)
 struct TileRsrc {
   __amdgpu_buffer_rsrc_t x, xh, m;  // m: the gossip step's memory (GS only)
@@ -437,11 +401,11 @@ struct TileRsrc {
 template <bool XH>
 CHOCO_DEV void load_rows_full(const TileRsrc& ts, uint32_t boff, int lane, float4 (&r)[kK2Unroll]) {
 #pragma unroll
-  for (int u = 0; u < kK2Unroll; ++u) r[u] = ld_buf4<CHOCO_STREAM_NT>(ts.x, boff + (u * 256 + 4 * lane) * 4);
+  for (int u = 0; u < kK2Unroll; ++u) r[u] = ld_buf4<true>(ts.x, boff + (u * 256 + 4 * lane) * 4);
   if (XH) {
 #pragma unroll
     for (int u = 0; u < kK2Unroll; ++u) {
-      const float4 h = ld_buf4<CHOCO_STREAM_NT>(ts.xh, boff + (u * 256 + 4 * lane) * 4);
+      const float4 h = ld_buf4<true>(ts.xh, boff + (u * 256 + 4 * lane) * 4);
       r[u].x -= h.x; r[u].y -= h.y; r[u].z -= h.z; r[u].w -= h.w;
     }
   }
@@ -452,21 +416,18 @@ CHOCO_DEV void load_rows_full(const TileRsrc& ts, uint32_t boff, int lane, float
 // does not exist loads zeros and its stores are dropped: out of the resource's
 // range), and r = x_new - xh.  No cross-chunk prefetch: three streams per wave
 // keep 24 KiB in flight, 16 waves per CU are plenty to cover the latency.
-#ifndef CHOCO_GS_STORE_NT  // cache policy of the x_new stores (A/B knob)
-#define CHOCO_GS_STORE_NT 1
-#endif
 CHOCO_DEV void gossip_rows(const TileRsrc& ts, uint32_t boff, int lane, float gamma, float4 (&r)[kK2Unroll]) {
   float4 M[kK2Unroll], H[kK2Unroll];
 #pragma unroll
-  for (int u = 0; u < kK2Unroll; ++u) r[u] = ld_buf4<CHOCO_STREAM_NT>(ts.x, boff + (u * 256 + 4 * lane) * 4);
+  for (int u = 0; u < kK2Unroll; ++u) r[u] = ld_buf4<true>(ts.x, boff + (u * 256 + 4 * lane) * 4);
 #pragma unroll
-  for (int u = 0; u < kK2Unroll; ++u) M[u] = ld_buf4<CHOCO_STREAM_NT>(ts.m, boff + (u * 256 + 4 * lane) * 4);
+  for (int u = 0; u < kK2Unroll; ++u) M[u] = ld_buf4<true>(ts.m, boff + (u * 256 + 4 * lane) * 4);
 #pragma unroll
-  for (int u = 0; u < kK2Unroll; ++u) H[u] = ld_buf4<CHOCO_STREAM_NT>(ts.xh, boff + (u * 256 + 4 * lane) * 4);
+  for (int u = 0; u < kK2Unroll; ++u) H[u] = ld_buf4<true>(ts.xh, boff + (u * 256 + 4 * lane) * 4);
 #pragma unroll
   for (int u = 0; u < kK2Unroll; ++u) {
     const float4 xn = gossip4(r[u], M[u], H[u], gamma);
-    st_buf4<CHOCO_GS_STORE_NT>(ts.x, boff + (u * 256 + 4 * lane) * 4, xn);
+    st_buf4<1>(ts.x, boff + (u * 256 + 4 * lane) * 4, xn);
     r[u] = sub4(xn, H[u]);
   }
 }
@@ -859,9 +820,8 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   const int w = tid >> 6;
   const int64_t b = blockIdx.x;
   constexpr int64_t kStep = 256 * kK2Unroll;
-  constexpr bool kOneBatch = kChunk == kStep;  // a chunk is one load batch (else: two, A and B)
-  constexpr bool kTwoChunks = kOneBatch && MODE == kData && !XH;  // A and B hold the next two chunks
-  static_assert(!GS || kOneBatch, "the gossip stream processes one-batch chunks");
+  static_assert(kChunk == kStep, "a chunk is one load batch");
+  constexpr bool kTwoChunks = MODE == kData && !XH;  // A and B hold the next two chunks
   const uint32_t nchunk = tile / (uint32_t)kChunk;
   Src<MODE, XH> src{x, xh, seed};
   // tile-relative byte offset of a full chunk's first / second batch, or kNoChunk
@@ -872,11 +832,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   auto batch0 = [&](uint32_t c) -> uint32_t {
     return (c < nchunk && (int64_t)(c + 1) * kChunk <= tlen) ? c * (uint32_t)kChunk * 4u : kNoChunk;
   };
-  auto batch1 = [&](uint32_t c) -> uint32_t { return batch0(c) + (uint32_t)kStep * 4u; };
 
-#ifndef CHOCO_K2_WINDOW_FIRST  // A/B knob: 0 reads the window behind the first batch (round 3)
-#define CHOCO_K2_WINDOW_FIRST 1
-#endif
   // ---- prologue: the window words K1 / the previous call left in the control block
   // are read FIRST, then the wave's first chunk w (and with one-batch chunks its second,
   // w + 16) goes out.  vmcnt retires in order: read behind the first batches (~67 MB
@@ -887,7 +843,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   Buckets bk;
   TopkBounds W{};
   uint32_t cold_left = 0, ovf_now = 0;
-  if constexpr (MODE == kData && CHOCO_K2_WINDOW_FIRST) {
+  if constexpr (MODE == kData) {
     // ONE vector load, lane i <-> word i (bounds words 0..8, cold_left, overflow): issued
     // before the batch, waited for (by the compiler, at the first readlane) behind it.
     // (Separate scalar loads made the batch wait for their lgkmcnt; separate vector loads
@@ -899,7 +855,6 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     asm volatile("" ::: "memory");  // (the batch's loads stay behind the window load)
     if (!GS) load_rows_full<XH>(ts, batch0(c), lane, A);
     if (kTwoChunks) load_rows_full<XH>(ts, batch0(c + kK2Waves), lane, B);
-    else if (!kOneBatch && !XH) load_rows_full<XH>(ts, batch1(c), lane, B);
     asm volatile("" ::: "memory");
     W.s_lo = __builtin_amdgcn_readlane(wl, 0);
     W.s_hi = __builtin_amdgcn_readlane(wl, 1);
@@ -910,15 +865,6 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     W.valid = __builtin_amdgcn_readlane(wl, 8);
     cold_left = __builtin_amdgcn_readlane(wl, 9);
     ovf_now = __builtin_amdgcn_readlane(wl, 10);
-  } else {
-    if constexpr (MODE == kData) {
-      if (!GS) load_rows_full<XH>(ts, batch0(c), lane, A);
-      if (kTwoChunks) load_rows_full<XH>(ts, batch0(c + kK2Waves), lane, B);
-      else if (!kOneBatch && !XH) load_rows_full<XH>(ts, batch1(c), lane, B);
-      W = ctrl->bounds[par];
-      cold_left = ctrl->cold_left;
-      ovf_now = ctrl->overflow[par];
-    }
   }
   // the NEXT call's bucket totals and overflow word start from zero (no kernel of
   // this call reads them: this call's are G[par] / overflow[par])
@@ -1049,7 +995,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       });
       cB = nB;
     }
-  } else if constexpr (kOneBatch) {
+  } else {
     // one buffer (two input streams: x - xh is formed at load time; hash mode: no loads)
     while (c < nchunk) {
       const uint32_t nn = claim_chunk(sm, lane);
@@ -1059,61 +1005,6 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       });
       c = nn;
     }
-  } else {
-  uint32_t nx = claim_chunk(sm, lane);
-  while (c < nchunk) {
-    const uint32_t nn = claim_chunk(sm, lane);  // used after this chunk
-    const int64_t cbeg = tb + (int64_t)c * kChunk;
-    const int64_t cend = min(cbeg + kChunk, n);
-    float* __restrict__ ov = cval + cbeg;
-    uint32_t* __restrict__ oi = cidx + cbeg;
-    a.estaged = a.eflushed = a.staged = a.lcnt = 0u;
-    a.lstart = a.lfill;
-    if (cbeg + kChunk <= n) {
-      if constexpr (MODE == kData && !XH) {
-        // double-buffered: A and B hold this chunk; each is refilled with the
-        // next chunk's batch as soon as it has been processed
-        process_batch<XH>(src, A, cbeg, cend, sm, w, lane, a, ov, oi, bk,
-                          [&] { load_rows_full<XH>(ts, batch0(nx), lane, A); });
-        process_batch<XH>(src, B, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk,
-                          [&] { load_rows_full<XH>(ts, batch1(nx), lane, B); });
-      } else if constexpr (MODE == kData) {
-        // two input streams: one batch (16 KiB per wave) at a time
-        process_batch<XH>(src, A, cbeg, cend, sm, w, lane, a, ov, oi, bk, [&] {
-          load_rows_full<XH>(ts, (uint32_t)(cbeg - b * (int64_t)tile + kStep) * 4u, lane, A);
-        });
-        process_batch<XH>(src, A, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk,
-                          [&] { load_rows_full<XH>(ts, batch0(nx), lane, A); });
-      } else {
-        process_rows_hash<MODE, XH>(src, cbeg, cend, sm, w, lane, a, ov, oi, bk);
-        process_rows_hash<MODE, XH>(src, cbeg + kStep, cend, sm, w, lane, a, ov, oi, bk);
-      }
-    } else {
-      // the buffer's last, partial chunk (or an empty one past n): guarded rows
-      for (int64_t base = cbeg; base < cend; base += 256) {
-        const int64_t i = base + 4 * lane;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (MODE == kData) {
-          float tt[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            tt[q] = (i + q < cend) ? (GS ? src.val_gossip(i + q, gs) : src.val(i + q)) : 0.f;
-          v = make_float4(tt[0], tt[1], tt[2], tt[3]);
-        }
-        process_row<MODE, XH, true>(src, v, i, cend, sm, w, lane, a, ov, oi, bk);
-      }
-      // the buffer's last chunk: every later chunk is past n, nothing to prefetch
-    }
-    // the chunk's remaining entries (< 64)
-    const uint32_t rest = a.estaged - a.eflushed;
-    if (rest) flush_entries<MODE, XH>(src, sm, w, lane, a, rest, ov, oi, bk);
-    if (lane == 0) {
-      sm.ccnt[c] = a.staged;
-      sm.cmeta[c] = (w * kPairsPerWave + a.lstart) | (a.lcnt << 16);
-    }
-    c = nx;
-    nx = nn;
-  }
   }
   if (lane == 0) sm.cnt[w] = a.cand;  // wave-uniform
   STAMP(1024 + b, 2);
@@ -1187,15 +1078,15 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
         if (key < bk.s_hi) {  // every candidate has key >= s_lo
           const uint32_t p = atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
           if (sort_lds) skeys[p] = key;
-          else if (p < side_cap) st_pol<CHOCO_K2_STORE>(&sd[p], key);
+          else if (p < side_cap) sd[p] = key;
         }
       };
       // Store-only loop: no global load may follow the stores inside it (vmcnt
       // counts stores too, so a load's wait would wait for every store before it).
       for (uint32_t j = h; j < lc; j += 32) {
         const uint2 pr = sm.u.pairs[ls + j];
-        st_pol<CHOCO_K2_STORE>(&ov[j], __uint_as_float(pr.x));
-        st_pol<CHOCO_K2_STORE>(&oi[j], pr.y);
+        ov[j] = __uint_as_float(pr.x);
+        oi[j] = pr.y;
         to_side(pr.x, pr.y);
       }
       if (have && h == 0) cntw[(int64_t)b * nchunk + cc] = spilled ? cnt : (cc == 0 ? csum : 0u);
@@ -1270,9 +1161,6 @@ CHOCO_DEV uint32_t chunk_run_starts(const uint32_t (&cw)[kCPT], uint32_t nchunk,
   return tot;
 }
 
-#ifndef CHOCO_K34_WAVE_SELECT  // A/B knob (r04: 1 = one wave, bit by bit, for <= 256 keys -- measured
-#define CHOCO_K34_WAVE_SELECT 0     // slower, 2.5 against 1.3 us for the ~160 keys of a warm bucket)
-#endif
 constexpr int kEmitR = 8;  // emission batch: kEmitR rows of kK4Threads candidate positions
 constexpr int kEmitRows = kEmitR;
 constexpr int kSelBits = 13;  // radix-select digit: one round for bucket widths <= 2^13
@@ -1422,9 +1310,6 @@ struct WideCtrl {
 };
 static_assert(sizeof(WideCtrl) == kWideBytes && kWideBytes % 256 == 0, "topk_layout reserves WideCtrl");
 constexpr int kWidePhases = 5;
-#ifndef CHOCO_WIDE_DEBUG  // printf trace of the fallback queue (diagnostic builds)
-#define CHOCO_WIDE_DEBUG 0
-#endif
 constexpr int kWideU = 4;  // float4 loads per stream per thread in flight
 
 // Queue hand-offs made by ALL lanes of wave 0 (no lane-divergent region inside the
@@ -1549,11 +1434,6 @@ CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uin
     if (tk >= (uint32_t)kWidePhases * nb) break;  // workgroup-uniform
     const int phase = (int)(tk / nb);
     const uint32_t t = tk % nb;
-#if CHOCO_WIDE_DEBUG
-    if (tid == 0) printf("wg %d ticket %u phase %d tile %u done %u %u %u %u %u\n", (int)blockIdx.x, tk, phase, t,
-                         ld_sc1(&W->done[0]), ld_sc1(&W->done[1]), ld_sc1(&W->done[2]), ld_sc1(&W->done[3]),
-                         ld_sc1(&W->done[4]));
-#endif
     if (phase > 0) {
       if (w0 && !wave0_poll_ge(&W->done[phase - 1], nb) && lane_id() == 0) {
         atomicOr(status, kStatusPollTimeout);
@@ -1570,10 +1450,6 @@ CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uin
       const uint32_t dm = wide_mask(phase);
       for (int i = tid; i < 2048; i += kK4Threads) es.hist[i] = 0u;
       __syncthreads();
-#if CHOCO_WIDE_DEBUG
-      if (tid == 0) printf("wg %d item %u: digits done, tile [%lld, %lld)\n", (int)blockIdx.x, tk, (long long)lo,
-                           (long long)hi);
-#endif
       const int lane = lane_id();
       wide_tile(src, lo, hi, [&](int64_t, int nin, const uint32_t (&kk)[4], const float (&)[4]) {
 #pragma unroll
@@ -1592,17 +1468,8 @@ CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uin
         }
       });
       __syncthreads();
-#if CHOCO_WIDE_DEBUG
-      if (tid == 0) printf("wg %d item %u: histogram done\n", (int)blockIdx.x, tk);
-#endif
       for (int i = tid; i < 2048; i += kK4Threads)
         if (es.hist[i]) __hip_atomic_fetch_add(&W->hist[phase][i], es.hist[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if CHOCO_WIDE_DEBUG
-      if (es.hist[1008] && tid == 1008) printf("wg %d item %u: flushed bin 1008 += %u\n", (int)blockIdx.x, tk, es.hist[1008]);
-      if (tid == 0) printf("wg %d item %u: flush loop done (thread 0)\n", (int)blockIdx.x, tk);
-      __syncthreads();
-      if (tid == 0) printf("wg %d item %u: barrier after flush\n", (int)blockIdx.x, tk);
-#endif
     } else {
       const uint32_t T = prefix;  // all digits known: T = the k-th largest key, krem = ties to take
       const uint32_t r = krem;
@@ -1664,9 +1531,6 @@ CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uin
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (w0) wave0_fetch_add(&W->done[phase], 1u);
-#if CHOCO_WIDE_DEBUG
-    if (tid == 0) printf("wg %d item %u published\n", (int)blockIdx.x, tk);
-#endif
   }
   // the last workgroup out resets the queue for the next call
   if (w0) {
@@ -1880,16 +1744,6 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
       uint32_t kv[kG];
 #pragma unroll
       for (int q = 0; q < kG; ++q) kv[q] = (uint32_t)q * kK4Threads < M ? side[ka[q]] : 0u;  // clamped slots
-      // The first emission batch's loads go out now, BEHIND the key loads: the
-      // vmcnt counter is in order, so waiting for the keys does not wait for
-      // them, and they land while T is being selected.
-      if (CHOCO_K34_PREFETCH == 1) {
-#pragma unroll
-        for (int i = 0; i < kEmitR; ++i) {
-          v[i] = cval[addr[i]];
-          idx[i] = cidx[addr[i]];
-        }
-      }
       STAMP(28000 + b, 1);
       __syncthreads();  // the tile map (= histogram) is dead before the select clears it
 #pragma unroll
@@ -1897,9 +1751,10 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
         const uint32_t i = (uint32_t)tid + (uint32_t)q * kK4Threads;
         if (i < M) fs.keys[i] = kv[q];
       }
-      if (CHOCO_K34_PREFETCH == 2) {
-        // late prefetch: the first emission batch goes out once the keys are in,
-        // so it does not queue in front of other workgroups' key gathers
+      {
+        // late prefetch: the first emission batch goes out once the keys are in, so it
+        // does not queue in front of other workgroups' key gathers (issued behind the key
+        // loads instead, measured slower), and lands while T is being selected
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < kEmitR; ++i) {
@@ -1914,40 +1769,6 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     const uint32_t base_j = s_lo + (jstar << shift);
     uint32_t prefix = 0, krem = ku - fs.G[jstar + 1];  // 1 <= krem <= M
     int sh = (int)shift;
-    if (CHOCO_K34_WAVE_SELECT && M <= 256u && shift <= 16u) {  // workgroup-uniform: the warm path's few keys
-      // ONE wave, bit by bit from the top: the keys (4 per lane) whose bits so far match
-      // T's, counted per bit with ballots -- no histogram, no block scan (r04 stamps: the
-      // LDS histogram + block rank took ~1.3 us for the ~160 keys of a warm bucket)
-      __syncthreads();  // the bucket keys are in LDS
-      if (tid < 64) {
-        uint32_t kv[4];
-        bool act[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t j = (uint32_t)tid + 64u * q;
-          act[q] = j < M;
-          kv[q] = act[q] ? fs.keys[j] - base_j : 0u;
-        }
-        for (int bit = sh - 1; bit >= 0; --bit) {
-          uint32_t c = 0;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) c += (uint32_t)__popcll(ballot(act[q] && ((kv[q] >> bit) & 1u)));
-          const bool one = c >= krem;  // wave-uniform
-          if (one) prefix |= 1u << bit;
-          else krem -= c;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) act[q] = act[q] && (((kv[q] >> bit) & 1u) == (one ? 1u : 0u));
-        }
-        if (tid == 0) {
-          fs.bc[5] = prefix;
-          fs.bc[6] = krem;
-        }
-      }
-      __syncthreads();
-      prefix = fs.bc[5];
-      krem = fs.bc[6];
-      sh = 0;
-    }
     while (sh > 0) {
       const int dsh = sh > kSelBits ? sh - kSelBits : 0;
       const uint32_t dmask = (1u << (sh - dsh)) - 1u;
@@ -2004,7 +1825,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     // ties' ranks first, only when ties at T are split).
     int eb = 0;  // alternating rank buffer
     for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads * kEmitR) {
-      if (p0 != 0 || !CHOCO_K34_PREFETCH) {  // workgroup-uniform: batches after the prefetched first one
+      if (p0 != 0) {  // workgroup-uniform: batches after the prefetched first one
 #pragma unroll
         for (int i = 0; i < kEmitR; ++i) addr[i] = cand_addr(fs.run_start, nchunk, tot, p0 + i * kK4Threads + tid, tb, compact);
 #pragma unroll
@@ -2044,8 +1865,8 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
       for (int i = 0; i < kEmitR; ++i) {
         if ((uint32_t)i >= nrows) continue;  // workgroup-uniform
         if (sel[i] && out + rk[i] < ku) {  // (bounded: an inconsistent select cannot write past k)
-          st_pol<CHOCO_K34_STORE>(&out_val[out + rk[i]], v[i] * scale);
-          st_pol<CHOCO_K34_STORE>(&out_idx[out + rk[i]], (int32_t)((int64_t)idx[i] + idx_base));
+          out_val[out + rk[i]] = v[i] * scale;
+          out_idx[out + rk[i]] = (int32_t)((int64_t)idx[i] + idx_base);
           if (fold.on()) fold_apply(fold, (int64_t)idx[i], v[i] * scale);
         }
       }

@@ -68,10 +68,7 @@ __device__ unsigned long long g_sg_stamps[kSgStampSlots][4];
   } while (0)
 #endif
 constexpr int kSegTile = 16384;                       // elements per tile
-#ifndef CHOCO_SEG_THREADS  // threads of the tile kernels S1 / S2 (rows of float4 per thread = 4096 / threads)
-#define CHOCO_SEG_THREADS 1024
-#endif
-constexpr int kSegThreads = CHOCO_SEG_THREADS;
+constexpr int kSegThreads = 1024;  // threads of the tile kernels S1 / S2 (rows of float4 per thread = 4096 / threads)
 constexpr int kSegRows = kSegTile / (4 * kSegThreads);
 constexpr int kSegMaxTiles = 1024;                    // tiles per batched segment (S3: one per thread)
 constexpr int64_t kSegBatchMax = (int64_t)kSegTile * kSegMaxTiles;
@@ -243,31 +240,23 @@ CHOCO_DEV void load_bins(const uint32_t* h, uint32_t (&hv)[kBpt]) {
 }
 
 // ---------------------------------------------------------------- S1: coarse histogram (cold)
-#ifndef CHOCO_S1_COPIES
-#define CHOCO_S1_COPIES 1
-#endif
-#ifndef CHOCO_S1_LANEC
-#define CHOCO_S1_LANEC 1
-#endif
 template <bool XH, bool GS = false>
 __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ xh,
                                                                const int64_t* __restrict__ trows, int nseg,
                                                                uint32_t* __restrict__ hist1, Gossip gs) {
   static_assert(!GS || XH, "the gossip step needs x_hat");
-  // histogram copies: wave w -> copy w % NC (CHOCO_S1_COPIES), or lane l -> copy
-  // l % NC (CHOCO_S1_LANEC: same-bin lanes of ONE atomic instruction split over copies)
-  constexpr int NC = CHOCO_S1_LANEC > 1 ? CHOCO_S1_LANEC : CHOCO_S1_COPIES;
-  __shared__ uint32_t h[NC][kH];
+  // one LDS histogram (per-wave or per-lane copies measured no faster, r04)
+  __shared__ uint32_t h[kH];
   const TileCtx c = tile_ctx_rows(trows, blockIdx.x);
   float v[kSegRows][4] = {};
   if (GS) tile_load_gossip<false>(x, xh, gs, c, v);
   else if (c.R.ntile == 1) return;  // a single-tile segment is selected in S2 (no histogram)
   else tile_load<XH>(x, xh, c, v);
   if (c.R.ntile == 1) return;  // (GS: its consensus step is applied; S2 selects it)
-  for (int i = threadIdx.x; i < NC * kH; i += kSegThreads) (&h[0][0])[i] = 0u;
+  for (int i = threadIdx.x; i < kH; i += kSegThreads) h[i] = 0u;
   __syncthreads();
-  uint32_t* __restrict__ hw = h[CHOCO_S1_LANEC > 1 ? lane_id() % NC : (threadIdx.x >> 6) % NC];
+  uint32_t* __restrict__ hw = h;
 #pragma unroll
   for (int r = 0; r < kSegRows; ++r)
 #pragma unroll
@@ -278,9 +267,7 @@ __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __re
   __syncthreads();
   uint32_t* __restrict__ g = hist1 + (int64_t)c.s * kH;
   for (int i = threadIdx.x; i < kH; i += kSegThreads) {
-    uint32_t t = 0;
-#pragma unroll
-    for (int k = 0; k < NC; ++k) t += h[k][i];
+    const uint32_t t = h[i];
     if (t) atomicAdd(&g[i], t);
   }
 }
@@ -399,41 +386,20 @@ CHOCO_DEV void seg_exact_tile(const float (&v)[kSegRows][4], const TileCtx& c, u
 // feed hist2 by bits 19..9.  Warm: the floor is the window's lo, every candidate
 // feeds hist2 by its window bin min((key - lo) >> sh, 2047); GS: the fused gossip
 // step happens here (the one read).
-// (8 waves per SIMD: <= 64 VGPRs; 2 x 1024 or 4 x 512 threads per CU.  Fewer
-// workgroups per CU measured ~10 us slower at ResNet-50)
-// LOOP (warm, no gossip step): a grid of resident
-// workgroups (kSegLoopGrid, one per CU) walks the tiles b, b + G, ..., each issuing the
-// NEXT tile's loads before the current tile's histogram, scans and stores, so a CU's
-// loads and processing overlap instead of alternating round by round (r04 counters on the
-// one-tile-per-workgroup W2: waves waited 54 % of their cycles, VALU issue ~28-34 %).
-#ifndef CHOCO_SEG_LOOP  // A/B knob
-#define CHOCO_SEG_LOOP 0
-#endif
-#ifndef CHOCO_SEG_LOOP_WPE  // its VGPR budget: 4 waves per SIMD (128 VGPRs: the prefetch does not fit 64)
-#define CHOCO_SEG_LOOP_WPE 4
-#endif
-#ifndef CHOCO_SEG_LOOP_GRID  // one 16-wave workgroup per CU at 4 waves per SIMD
-#define CHOCO_SEG_LOOP_GRID (CHOCO_SEG_LOOP_WPE >= 8 ? 512 : 256)
-#endif
-constexpr int64_t kSegLoopGrid = CHOCO_SEG_LOOP_GRID;
-template <bool XH, bool WARM, bool GS = false, bool LOOP = false>
-#ifndef CHOCO_SEG_SMALL_FIRST  // A/B knob: W2 / S2 take the single-tile segments' tiles first
-#define CHOCO_SEG_SMALL_FIRST 1
-#endif
-#ifndef CHOCO_SEG_WARM_NT  // 1: W2's one read of the delta uses non-temporal loads
-#define CHOCO_SEG_WARM_NT 1
-#endif
-#ifndef CHOCO_SEG_WPE  // waves per SIMD the collect kernel is compiled for (VGPR budget 512 / WPE)
-#define CHOCO_SEG_WPE (kSegThreads == 1024 ? 8 : 6)
-#endif
-__global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_WPE) void seg_collect_kernel(
+// (8 waves per SIMD: <= 64 VGPRs; 2 x 1024 threads per CU.  Fewer workgroups per CU
+// measured ~10 us slower at ResNet-50; a looping collect with the next tile's loads in
+// flight (one workgroup per CU, 128 VGPRs) 40 against 29.5 us: removed, git history r04.)
+// W2's one read of the delta uses non-temporal loads; W2 / S2 take the single-tile
+// segments' tiles first (the plan's dispatch records).
+constexpr int kSegWpe = kSegThreads == 1024 ? 8 : 6;  // waves per SIMD (VGPR budget 512 / WPE)
+template <bool XH, bool WARM, bool GS = false>
+__global__ __launch_bounds__(kSegThreads, kSegWpe) void seg_collect_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ plan, int nseg,
     const uint32_t* __restrict__ hist1, uint32_t* __restrict__ hist2, uint32_t* __restrict__ info,
     uint32_t* __restrict__ tilecnt, float* __restrict__ cval, uint32_t* __restrict__ cidx,
     const SegWin* __restrict__ win, Gossip gs, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
     int64_t ntile, const int64_t* __restrict__ order) {
   static_assert(!GS || (XH && WARM), "the gossip step is fused into S2 on the warm path only (S1 on the cold)");
-  static_assert(!LOOP || (WARM && !GS), "the looping collect is the warm path without the gossip step");
   __shared__ uint32_t h2[kH];
   __shared__ uint32_t scratch[40];
   __shared__ uint32_t bc[4];
@@ -523,7 +489,7 @@ __global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_
   if (tid == 0) tilecnt[tb] = rc_cnt[kSegRows * kW];
   SGSTAMP(2048 + tb, 2);
   };
-  if constexpr (!LOOP) {
+  {
     // the tile this workgroup takes; with the dispatch-order records its loads need only
     // the record (the segment's row is read while they fly)
     int64_t ta;
@@ -542,7 +508,7 @@ __global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_
     SGSTAMP(ta, 0);
     float v[kSegRows][4] = {};
     if (GS) tile_load_gossip<true>(x, xh, gs, c, v);  // in flight while the floor is found
-    else tile_load<XH, WARM && CHOCO_SEG_WARM_NT>(x, xh, c, v);  // warm: the only read of the call
+    else tile_load<XH, WARM>(x, xh, c, v);  // warm: the only read of the call (non-temporal)
     if (order) {
       c.R = seg_row(plan, c.s);
       c.j = ta - c.R.t0;
@@ -551,45 +517,6 @@ __global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_
     if (WARM) wpre = win[c.s];
     SGSTAMP(ta, 1);
     process(v, c, ta, wpre);
-  } else {
-    // the raw loads of a tile (x, and x_hat), formed into v only when the tile is processed,
-    // so that the next tile's loads stay in flight during this tile's work
-    auto issue = [&](const TileCtx& tc, float4 (&a)[kSegRows], float4 (&h)[kSegRows]) {
-      const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x + tc.start, (uint32_t)tc.tl * 4u);
-#pragma unroll
-      for (int r = 0; r < kSegRows; ++r)
-        a[r] = ld_buf4<CHOCO_SEG_WARM_NT>(rx, (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u);
-      if constexpr (XH) {
-        const __amdgpu_buffer_rsrc_t rh = buf_rsrc(xh + tc.start, (uint32_t)tc.tl * 4u);
-#pragma unroll
-        for (int r = 0; r < kSegRows; ++r)
-          h[r] = ld_buf4<CHOCO_SEG_WARM_NT>(rh, (uint32_t)(r * 4 * kSegThreads + 4 * threadIdx.x) * 4u);
-      }
-    };
-    int64_t b = blockIdx.x;
-    TileCtx c = tile_ctx(plan, nseg, b);
-    float4 a[kSegRows], h[kSegRows];
-    issue(c, a, h);
-    for (;;) {
-      const int64_t bn = b + (int64_t)gridDim.x;
-      const bool more = bn < ntile;  // workgroup-uniform
-      float v[kSegRows][4];
-#pragma unroll
-      for (int r = 0; r < kSegRows; ++r) {
-        v[r][0] = a[r].x; v[r][1] = a[r].y; v[r][2] = a[r].z; v[r][3] = a[r].w;
-        if constexpr (XH) { v[r][0] -= h[r].x; v[r][1] -= h[r].y; v[r][2] -= h[r].z; v[r][3] -= h[r].w; }
-      }
-      TileCtx cn = c;
-      if (more) {
-        cn = tile_ctx(plan, nseg, bn);
-        issue(cn, a, h);  // in flight during this tile's work
-      }
-      process(v, c, b, win[c.s]);
-      if (!more) break;
-      __syncthreads();  // the LDS histogram and scan words are reused by the next tile
-      c = cn;
-      b = bn;
-    }
   }
 }
 
@@ -604,10 +531,7 @@ __global__ __launch_bounds__(kSegThreads, LOOP ? CHOCO_SEG_LOOP_WPE : CHOCO_SEG_
 //   S3b seg_count: T_s from hist3[s]; this tile's (#key > T_s, #key == T_s);
 //                  tile 0: the next call's window.
 // S4 then places each tile from the counts of the tiles before it.
-#ifndef CHOCO_S3_THREADS
-#define CHOCO_S3_THREADS 256
-#endif
-constexpr int kS3Threads = CHOCO_S3_THREADS;
+constexpr int kS3Threads = 256;
 constexpr int kH3 = 512;  // bits 8..0 (cold) / the low sh <= 9 bits of a window bin (warm)
 enum SegMode { kSegSelect = 0, kSegMissed = 1, kSegAll = 2 };
 
@@ -833,10 +757,7 @@ __global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
 // workgroups resident).  A warm segment whose window missed: tile 0 selects the
 // whole segment exactly (select.h; the segment's candidates were not all kept)
 // and re-centres the window on its T.
-#ifndef CHOCO_S4_THREADS
-#define CHOCO_S4_THREADS 256
-#endif
-constexpr int kS4Threads = CHOCO_S4_THREADS;
+constexpr int kS4Threads = 256;
 constexpr int kS4Per = kSegMaxTiles / kS4Threads;
 static_assert(kS4Per * kS4Threads == kSegMaxTiles, "S4 tile-count geometry");
 template <bool WARM, bool XH>
@@ -988,7 +909,7 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
   const unsigned ntile = (unsigned)plan_tiles(plan_host);
   // the collect launches' dispatch order (choco_topk_segmented_plan: after the random-k table)
   const int64_t rkb = (int64_t)kRow * nseg + plan_tiles(plan_host) + plan_batched(plan_host);  // (rk_base_of)
-  const int64_t* w2_order = CHOCO_SEG_SMALL_FIRST ? plan_dev + rkb + 1 + 4 * plan_host[rkb] : nullptr;
+  const int64_t* w2_order = plan_dev + rkb + 1 + 4 * plan_host[rkb];
   // the per-tile rows (after the dispatch records): S1 / S3 / S4 look their tile up in one round trip
   const int64_t* trows = plan_dev + rkb + 1 + 4 * plan_host[rkb] + 4 * (int64_t)ntile;
   if (!warm) {
@@ -1001,11 +922,6 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
     CHOCO_KLAUNCH((seg_collect_kernel<XH, false, false>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev,
                   nseg, W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.win, Gossip{nullptr, 0.f}, out_val,
                   out_idx, (int64_t)ntile, w2_order);
-  } else if (CHOCO_SEG_LOOP && !GS && ntile > (unsigned)kSegLoopGrid) {
-    profile_begin("topk_seg_collect", st);
-    CHOCO_KLAUNCH((seg_collect_kernel<XH, true, false, true>), dim3((unsigned)kSegLoopGrid), dim3(kSegThreads), 0,
-                  st, x, xh, plan_dev, nseg, W.hist1, W.hist2, W.info, W.tilecnt, W.cval, W.cidx, W.win, gs, out_val,
-                  out_idx, (int64_t)ntile, nullptr);
   } else {
     profile_begin("topk_seg_collect", st);
     CHOCO_KLAUNCH((seg_collect_kernel<XH, true, GS>), dim3(ntile), dim3(kSegThreads), 0, st, x, xh, plan_dev, nseg,

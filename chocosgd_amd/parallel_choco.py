@@ -214,14 +214,18 @@ class CHOCOSparsificationCompressor(_CHOCOBase):
             msg = sync_buffer["wire_message"]
             codec.sparse_accumulate(msg[:K].view(torch.float32), msg[K:], hat, 1.0, guard=guard)
         self.aggregator_fn.complete_wait(sync_buffer["sync_reqs"])
+        # every message into memory in ONE sweep, in neighbors_info order (each touched line
+        # of memory read and written once per step, not once per message; bit-identical to
+        # the reference's per-neighbour loop)
+        msgs, weights, slot, hat = [], [], -1, None
         for rank, weight in neighbors_info.items():
             hat_params = neighbor_hat_params[rank if rank in neighbor_hat_params else "memory"]
             msg = recover_device(sync_buffer["synced_message"][rank], device=hat_params.buffer.device)
-            q_values = msg[:K].view(torch.float32)
-            q_indices = msg[K:]
-            own = rank in neighbor_hat_params and not hat_early
-            codec.sparse_accumulate(q_values, q_indices, memory.buffer, weight,
-                                    xhat_self=hat_params.buffer if own else None, guard=guard)
+            if rank in neighbor_hat_params and not hat_early:
+                slot, hat = len(msgs), hat_params.buffer
+            msgs.append((msg[:K].view(torch.float32), msg[K:]))
+            weights.append(weight)
+        codec.sparse_accumulate_multi(msgs, weights, memory.buffer, self_slot=slot, xhat_self=hat, guard=guard)
         # out-of-range indices of an EARLIER step (lazy, no sync), reported once this step's
         # messages are applied; pipeline() prints it as the reference prints its RuntimeErrors
         guard.check_then_arm()
