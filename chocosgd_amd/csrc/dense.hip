@@ -450,41 +450,49 @@ CHOCO_API int choco_sparse_accumulate_multi(const float* const* vals, const int3
   CHOCO_REQUIRE(self_slot >= -1 && self_slot < nmsg, "self_slot out of range");
   CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n must be in [1, 2^31-1)");
   const int64_t nR = (n + kMRange - 1) / kMRange;
+  // the non-empty messages, in order (an empty message changes nothing)
   MsgSet ms{};
+  int nm = 0, slot = -1;
   bool sweep = aligned16(memory) && n >= kMRange;
   for (int m = 0; m < nmsg; ++m) {
     CHOCO_REQUIRE(ks[m] >= 0 && ks[m] < (int64_t)INT32_MAX, "message %d: k out of range", m);
-    CHOCO_REQUIRE(ks[m] == 0 || (vals[m] && idxs[m]), "message %d: null values / indices", m);
-    ms.val[m] = vals[m];
-    ms.idx[m] = idxs[m];
-    ms.k[m] = ks[m];
-    ms.w[m] = weights[m];
+    if (ks[m] == 0) continue;
+    CHOCO_REQUIRE(vals[m] && idxs[m], "message %d: null values / indices", m);
+    if (m == self_slot) slot = nm;
+    ms.val[nm] = vals[m];
+    ms.idx[nm] = idxs[m];
+    ms.k[nm] = ks[m];
+    ms.w[nm] = weights[m];
     // the split writes (range(u-1), range(u)] per update: long runs of empty ranges would
     // serialise in one thread, so sparse messages (< one update per range) take the
     // per-message kernels
     sweep = sweep && ks[m] >= nR;
+    ++nm;
   }
+  if (nm == 0) return CHOCO_OK;
   if (!sweep) {
-    for (int m = 0; m < nmsg; ++m) {
-      const int rc = choco_sparse_accumulate(vals[m], idxs[m], ks[m], m == self_slot ? xhat_self : nullptr, memory, n,
-                                             weights[m], bad_count, stream);
+    for (int m = 0; m < nm; ++m) {
+      const int rc = choco_sparse_accumulate(ms.val[m], ms.idx[m], ms.k[m], m == slot ? xhat_self : nullptr, memory, n,
+                                             ms.w[m], bad_count, stream);
       if (rc) return rc;
     }
     return CHOCO_OK;
   }
+  nmsg = nm;
+  self_slot = slot;
   const size_t need = choco_sparse_accumulate_multi_workspace_size(n, nmsg);
   CHOCO_REQUIRE(ws != nullptr && ws_bytes >= need, "multi-message accumulate workspace too small: need %zu, got %zu",
                 need, ws_bytes);
   int32_t* starts = static_cast<int32_t*>(ws);
-  if (self_slot >= 0 && xhat_self != nullptr && ks[self_slot] > 0) {
+  if (self_slot >= 0 && xhat_self != nullptr) {
     // x_hat takes the self message only (parallel_choco_v.py:307-308): hat + 1.0f * v == hat + v
     // (its bad indices are counted by the split below)
-    const int rc = choco_sparse_accumulate(vals[self_slot], idxs[self_slot], ks[self_slot], nullptr, xhat_self, n, 1.0f,
-                                           nullptr, stream);
+    const int rc = choco_sparse_accumulate(ms.val[self_slot], ms.idx[self_slot], ms.k[self_slot], nullptr, xhat_self,
+                                           n, 1.0f, nullptr, stream);
     if (rc) return rc;
   }
   int64_t kmax = 0;
-  for (int m = 0; m < nmsg; ++m) kmax = std::max(kmax, ks[m]);
+  for (int m = 0; m < nmsg; ++m) kmax = std::max(kmax, ms.k[m]);
   profile_begin("sparse_split", st);
   CHOCO_KLAUNCH(sparse_split_kernel, dim3((unsigned)std::min<int64_t>((kmax + kEwThreads) / kEwThreads, 4096), nmsg),
                 dim3(kEwThreads), 0, st, ms, n, nR, starts, bad_count);
