@@ -96,6 +96,13 @@ def parse():
     return p.parse_args()
 
 
+def traffic_key(args):
+    """The workload key of profiles/pmc_traffic.json (tools/pmc_traffic.py's 3rd argument)."""
+    if args.ring3_loopback:
+        return f"{args.workload}_ring3_{args.accumulate}"
+    return args.workload
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -680,7 +687,7 @@ def main():
         if os.path.exists(tf) and dom:
             with open(tf) as f:
                 tab = json.load(f)
-            ks = [f"{k}:{args.workload}:{w.n}" for k in dom["kernels"]]
+            ks = [f"{k}:{traffic_key(args)}:{w.n}" for k in dom["kernels"]]
             if all(k in tab for k in ks):
                 traffic = int(sum(tab[k]["bytes"] for k in ks))
         roofline = None

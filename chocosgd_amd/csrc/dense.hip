@@ -470,6 +470,8 @@ CHOCO_API int choco_sparse_accumulate_multi(const float* const* vals, const int3
     ++nm;
   }
   if (nm == 0) return CHOCO_OK;
+  // one message: the segment-owner kernel applies x_hat and memory in the same pass
+  if (nm == 1) sweep = false;
   if (!sweep) {
     for (int m = 0; m < nm; ++m) {
       const int rc = choco_sparse_accumulate(ms.val[m], ms.idx[m], ms.k[m], m == slot ? xhat_self : nullptr, memory, n,

@@ -1564,8 +1564,7 @@ constexpr uint32_t kColdMin = 64, kColdMax = 4096;
 constexpr uint32_t kWarmM0 = 20;     // ~2 % of k (the bench's randn deltas drift ~0.1 %)
 constexpr uint32_t kWarmMMax = 512;  // 50 %
 CHOCO_DEV void next_window(const uint32_t* G, uint32_t s_lo, uint32_t s_hi, uint32_t shift, uint32_t m_prev,
-                           uint32_t T, int64_t n, int64_t k, TopkBounds* __restrict__ out,
-                           uint32_t* __restrict__ hint) {
+                           uint32_t T, int64_t n, int64_t k, TopkBounds* __restrict__ out) {
   const int lane = lane_id();
   const double kd = (double)k;
   uint32_t m = kWarmM0;
@@ -1621,12 +1620,6 @@ CHOCO_DEV void next_window(const uint32_t* G, uint32_t s_lo, uint32_t s_hi, uint
   out->n = n;
   out->k = k;
   out->valid = 1u;
-  // the bucket this call's T falls into in the next window: the host passes it to a later
-  // call's K34 as its guess of j* (topk_finish_kernel `jhint`), through pinned memory
-  if (hint) {
-    const uint64_t jp = (uint64_t)T >= x_lo ? std::min<uint64_t>(((uint64_t)T - x_lo) >> sh, kNMaybe - 1) : 0u;
-    __hip_atomic_store(hint, (uint32_t)jp + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
 }
 
 template <int MODE, bool XH>
@@ -1637,7 +1630,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
     int64_t idx_base, WideCtrl* __restrict__ wide, uint32_t* __restrict__ gcnt, uint32_t par,
     uint32_t* __restrict__ status, uint32_t* __restrict__ host_status, const uint32_t* __restrict__ tinfo,
-    Fold fold, uint32_t jhint, uint32_t* __restrict__ hint_out) {
+    Fold fold) {
   __shared__ FinSmem fs;
   __shared__ ExactSmem es;
   __shared__ uint32_t s_tk;
@@ -1668,19 +1661,6 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   const bool mine_tile = tid < (int)nb;
   const uint32_t* row = cum_tab + (int64_t)(mine_tile ? tid : 0) * kNBucket;  // clamped: loads unconditional
   const uint32_t sure_t = row[kNMaybe];
-  // The j* hint (an earlier call's T in this call's window, jhint = bucket + 1; 0: none):
-  // twelve table words around it ride in this first round trip, so a hit needs no table
-  // trip after j* is known (a miss loads the two words as before).
-#ifndef CHOCO_K34_HINT  // r05 A/B knob (tools/build_variants.py k34_nohint); removed once measured
-#define CHOCO_K34_HINT 1
-#endif
-  const bool hinted = CHOCO_K34_HINT && MODE == kData && jhint != 0u;
-  const uint32_t bs = hinted ? (uint32_t)min(max((int)jhint - 1 - 4, 0), kNBucket - 12) & ~3u : 0u;
-  uint4 band[3];
-  if (hinted) {
-#pragma unroll
-    for (int q = 0; q < 3; ++q) band[q] = *reinterpret_cast<const uint4*>(row + bs + 4 * q);
-  }
   uint32_t g[kNRep];
   if (tid < kNBucket) {
 #pragma unroll
@@ -1726,24 +1706,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     // ---- thread t <-> tile t: bucket-j* key count and side-list offset
     uint32_t above = 0, cb = 0, off = 0;
     {
-      uint32_t a, c;
-      if (hinted && jstar >= bs && jstar + 1 < bs + 12) {  // workgroup-uniform: the hint hit
-        const uint32_t bw[12] = {band[0].x, band[0].y, band[0].z, band[0].w, band[1].x, band[1].y,
-                                 band[1].z, band[1].w, band[2].x, band[2].y, band[2].z, band[2].w};
-        a = bw[0];
-        c = bw[1];
-#pragma unroll
-        for (int i = 1; i < 11; ++i) {
-          if (jstar - bs == (uint32_t)i) {
-            a = bw[i];
-            c = bw[i + 1];
-          }
-        }
-      } else {
-        a = row[jstar];
-        c = row[jstar + 1];
-      }
-      const uint32_t s = sure_t;
+      const uint32_t a = row[jstar], c = row[jstar + 1], s = sure_t;
       if (mine_tile) {
         above = c;
         cb = a - c;   // keys of bucket j* in this tile
@@ -1911,7 +1874,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     }
     STAMP(30000 + b, 2);
     if (MODE == kData && b == 0 && tid < 64)
-      next_window(fs.G, s_lo, fs.ctl[1], shift, fs.ctl[4], T, n, k, &ctrl->bounds[par ^ 1u], hint_out);
+      next_window(fs.G, s_lo, fs.ctl[1], shift, fs.ctl[4], T, n, k, &ctrl->bounds[par ^ 1u]);
   }
   // random-k windows come from the host each call: nothing for the next call to reuse
   if (MODE == kHash && b == 0 && tid == 0) ctrl->bounds[par ^ 1u].valid = 0u;
@@ -1982,8 +1945,6 @@ static WarmClaim warm_claim(const void* ws, int64_t n, int64_t k, bool data) {
   e.calls += 1;
   return c;
 }
-
-static uint32_t host_hint_read(const void* ws);  // the pinned block's j* hint (below)
 
 // GS: the gossip step fused into K1's sample and K2's stream (x written by K2);
 // K34 and its exact fallback then read (x_new, xh).
@@ -2065,17 +2026,11 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
                 (uint32_t)(MODE == kData && wc.warm ? 1 : 0));
   profile_end("topk_stream", st);
   CHOCO_LAUNCHED("topk_stream_kernel");
-  // the j* hint a previous call left in this workspace's pinned block (word 1): read without
-  // a synchronisation, so it may be a few calls old -- a guess, checked on the device
-  uint32_t* mirror = host_status_dev(ws);
-  CHOCO_REQUIRE(mirror != nullptr, "top-k: could not map the pinned host block of the workspace");
-  const uint32_t jhint = (MODE == kData && wc.warm) ? host_hint_read(ws) : 0u;
   profile_begin("topk_finish", st);
   CHOCO_KLAUNCH((topk_finish_kernel<MODE, XH>), dim3(L.nb), dim3(kK4Threads), 0, st, x, xh, n, k, L.tile, L.nb,
                 L.side_cap, seed, scale, ctrl, cum, cntw, side, cval, cidx, out_val, out_idx, idx_base,
                 reinterpret_cast<WideCtrl*>(base + L.off_wide), reinterpret_cast<uint32_t*>(base + L.off_gcnt), par,
-                status.dev, status.host, reinterpret_cast<const uint32_t*>(base + L.off_tinfo), fold, jhint,
-                MODE == kData ? mirror + 1 : nullptr);
+                status.dev, status.host, reinterpret_cast<const uint32_t*>(base + L.off_tinfo), fold);
   profile_end("topk_finish", st);
   CHOCO_LAUNCHED("topk_finish_kernel");
   return CHOCO_OK;
@@ -2139,18 +2094,9 @@ uint32_t* host_status_dev(const void* ws) {
     return nullptr;
   }
   HostStatus hs{static_cast<uint32_t*>(h), static_cast<uint32_t*>(d)};
-  __atomic_store_n(hs.host + 1, 0u, __ATOMIC_RELAXED);  // no j* hint yet
   __atomic_store_n(hs.host, 0u, __ATOMIC_RELEASE);
   g_hs.emplace(ws, hs);
   return hs.dev;
-}
-
-// word 1 of the block: the last j* hint a K34 of this workspace wrote (0: none yet)
-static uint32_t host_hint_read(const void* ws) {
-  std::lock_guard<std::mutex> g(g_hs_mu);
-  auto it = g_hs.find(ws);
-  if (it == g_hs.end() || it->second.host == nullptr) return 0u;
-  return __atomic_load_n(it->second.host + 1, __ATOMIC_RELAXED);
 }
 
 static uint32_t host_status_read(const void* ws, bool clear) {

@@ -13,8 +13,6 @@ VARIANTS = {
     "stamps": ["CHOCO_STAMPS=1"],
     # every bounded wait of the exact fallback gives up at once: tools/status_probe.py
     "poll1": ["CHOCO_POLL_BUDGET=1"],
-    # r05 A/B: K34 without the j* hint (the table-word trip after j* on every call)
-    "k34_nohint": ["CHOCO_K34_HINT=0"],
 }
 
 
