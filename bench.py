@@ -59,10 +59,10 @@ GAMMA = 0.9  # consensus_stepsize (parameters.py:126 default)
 # kernels (profile names) of each stage
 STAGES = {
     "topk": (["topk_bounds", "topk_stream", "topk_finish", "topk_exact", "topk_all"],
-             ["sparse_accumulate", "sparse_split", "sparse_acc_multi"]),
+             ["sparse_accumulate"]),
     "topk_seg": (["topk_seg_hist", "topk_seg_collect", "topk_seg_fine", "topk_seg_count", "topk_seg_emit",
-                  "topk_bounds", "topk_stream", "topk_finish"], ["sparse_accumulate", "sparse_split", "sparse_acc_multi"]),
-    "randk": (["randk_count", "randk_tile"], ["sparse_accumulate", "sparse_split", "sparse_acc_multi"]),
+                  "topk_bounds", "topk_stream", "topk_finish"], ["sparse_accumulate"]),
+    "randk": (["randk_count", "randk_tile"], ["sparse_accumulate"]),
     "qsgd": (["qsgd_norm", "qsgd_quantize"], ["qsgd_accumulate"]),
     "sign": (["sign_pack"], ["sign_accumulate"]),
 }
@@ -86,9 +86,6 @@ def parse():
     p.add_argument("--ring3-loopback", action="store_true",
                    help="sparse codecs on one GPU: each step applies the self message plus two neighbour messages "
                         "(compressed from other resident deltas, no exchange) -- a ring worker's receive (cfg 4)")
-    p.add_argument("--accumulate", default="multi", choices=["multi", "per_message"],
-                   help="sparse receive: one sweep over all messages (choco_sparse_accumulate_multi) or one "
-                        "choco_sparse_accumulate launch per message (the A/B)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the host-resident (PCIe-inclusive) leg")
     p.add_argument("--lib", default=None, help=argparse.SUPPRESS)
@@ -99,7 +96,7 @@ def parse():
 def traffic_key(args):
     """The workload key of profiles/pmc_traffic.json (tools/pmc_traffic.py's 3rd argument)."""
     if args.ring3_loopback:
-        return f"{args.workload}_ring3_{args.accumulate}"
+        return f"{args.workload}_ring3"
     return args.workload
 
 
@@ -189,7 +186,6 @@ class Worker:
             self.msg = torch.zeros(4 + codec.sign_words(self.n), dtype=torch.int32, device=dev)
             self.wire = (self.msg[4:], self.msg[:4].view(torch.float32)[:1])
         self.recv = {r: torch.empty_like(self.msg) for r in self.peers}
-        self.accumulate = args.accumulate
         self.loop_sets = None
         if args.ring3_loopback:
             if self.op not in ("topk", "topk_seg", "randk") or world != 1:
@@ -312,15 +308,10 @@ class Worker:
             items = [(r, m, w) for r, m, w in zip(self.ranks, msgs, self.weights)
                      if not (r == self.rank and self.fold_mem)]
             want_hat = not (hat_done or self.fold)
-            if self.accumulate == "multi":
-                slot = next((i for i, (r, _, _) in enumerate(items) if r == self.rank), -1) if want_hat else -1
-                c.sparse_accumulate_multi([(m[:self.k].view(torch.float32), m[self.k:]) for _, m, _ in items],
-                                          [w for _, _, w in items], self.mem, self_slot=slot,
-                                          xhat_self=self.hat if slot >= 0 else None)
-                return
-            for r, m, w in items:
-                c.sparse_accumulate(m[:self.k].view(torch.float32), m[self.k:], self.mem, w,
-                                    xhat_self=self.hat if r == self.rank and want_hat else None)
+            slot = next((i for i, (r, _, _) in enumerate(items) if r == self.rank), -1) if want_hat else -1
+            c.sparse_accumulate_multi([(m[:self.k].view(torch.float32), m[self.k:]) for _, m, _ in items],
+                                      [w for _, _, w in items], self.mem, self_slot=slot,
+                                      xhat_self=self.hat if slot >= 0 else None)
         elif self.op == "qsgd":
             parts = [(m[16:], m[:4].view(torch.float32)) for m in msgs]
             c.qsgd_accumulate(parts, self.weights, self.self_slot, self.n, self.param, self.mem, xhat_self=self.hat)
@@ -383,10 +374,7 @@ class Worker:
         torch = self.torch
         ms = [self.msg] + [self.recv[r] for r in self.ranks if r != self.rank]
         own = int(torch.unique(self.msg[self.k:].long() // 16).numel())  # x_hat: the self message's lines
-        if self.accumulate == "multi":  # memory: every line touched by any message, once
-            segs = int(torch.unique(torch.cat([m[self.k:].long() // 16 for m in ms])).numel())
-        else:
-            segs = sum(int(torch.unique(m[self.k:].long() // 16).numel()) for m in ms)
+        segs = sum(int(torch.unique(m[self.k:].long() // 16).numel()) for m in ms)
         return 8 * self.k * len(self.ranks) + 128 * (segs + own)
 
 
@@ -718,7 +706,6 @@ def main():
             "config": {"workload": w.label + ("_fold" if w.fold else ""), "n_per_worker": w.n, "k_per_worker": w.k,
                        "graph": ("ring3_loopback" if w.loop_sets else "self") if world == 1 else (
                            "complete" if world == 2 else "ring"),
-                       "accumulate": w.accumulate if w.op in ("topk", "topk_seg", "randk") else None,
                        "messages_per_step": len(w.ranks), "backend": args.backend if world > 1 else None,
                        "step": "compress+exchange+decompress-accumulate", "parallelism": f"gossip{world}"},
             "roofline": roofline,

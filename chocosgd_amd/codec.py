@@ -498,10 +498,10 @@ MAX_SPARSE_MSGS = 8  # messages per choco_sparse_accumulate_multi call
 
 
 def sparse_accumulate_multi(messages, weights, memory, self_slot=-1, xhat_self=None, guard=None):
-    """Every message of a receive step in ONE sweep (include/choco_codec.h
+    """Every message of a receive step in ONE call (include/choco_codec.h
     choco_sparse_accumulate_multi): for m in order, x_hat[idx_m] += v_m (m == self_slot,
     xhat_self given) and memory[idx_m] += weights[m] * v_m -- bit-identical to one
-    sparse_accumulate per message in that order.  messages: [(values f32, indices i32)];
+    sparse_accumulate per message in that order (the per-message kernels run it).  messages: [(values f32, indices i32)];
     any count (chunks of MAX_SPARSE_MSGS, applied in order)."""
     _require(memory, torch.float32, "memory")
     if len(messages) != len(weights):
@@ -522,13 +522,14 @@ def sparse_accumulate_multi(messages, weights, memory, self_slot=-1, xhat_self=N
         part = messages[c0:c0 + MAX_SPARSE_MSGS]
         m = len(part)
         slot = self_slot - c0 if (xhat_self is not None and c0 <= self_slot < c0 + m) else -1
-        ws = workspace(dev, "accm", L.choco_sparse_accumulate_multi_workspace_size(n, m))
+        nws = L.choco_sparse_accumulate_multi_workspace_size(n, m)
+        ws = workspace(dev, "accm", nws) if nws else None
         vp, keep1 = _lib.ptr_array([v.data_ptr() for v, _ in part])
         ip, keep2 = _lib.ptr_array([i.data_ptr() for _, i in part])
         kp, keep3 = _lib.i64_array([v.numel() for v, _ in part])
         wp, keep4 = _lib.f32_array([float(w) for w in weights[c0:c0 + m]])
         _lib.check(L.choco_sparse_accumulate_multi(vp, ip, kp, wp, m, slot, _ptr(xhat_self if slot >= 0 else None),
-                                                   _ptr(memory), n, _ptr(ws), ws.numel(),
+                                                   _ptr(memory), n, _ptr(ws), ws.numel() if ws is not None else 0,
                                                    _ptr(guard.word) if guard is not None else ctypes.c_void_p(0),
                                                    _stream(dev)),
                    "choco_sparse_accumulate_multi")

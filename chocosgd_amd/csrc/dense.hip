@@ -133,181 +133,14 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_seg_kernel(const float*
   if (bad && nbad) atomicAdd(bad, nbad);
 }
 
-// ----------------------------------------------------------------------------
-// Multi-message receive (the per-neighbour loop of CHOCOSparsificationCompressor.
-// uncompress, parallel_choco_v.py:291-310, for memory): memory[i] += w_m * v_m for
-// every message m IN ORDER, as ONE sweep.  The index space is cut into ranges of
-// kMRange elements (256 segments of 64 B); a range's workgroup
-//   1. reads where each message's updates for the range start and end (a split table
-//      written by sparse_split_kernel: one pass over the messages' indices),
-//   2. loads those updates (first 256 per message in registers) and marks the 64-B
-//      segments they touch,
-//   3. loads every touched segment of memory ONCE into LDS (a quad of lanes per
-//      segment: whole-line float4 loads),
-//   4. applies the messages one after the other in LDS (indices are unique inside a
-//      message, so no two lanes of one message meet; a barrier between messages keeps
-//      the per-element order of the reference),
-//   5. writes the touched segments back whole.
-// A line hit by several messages is read and written once per step instead of once per
-// message (at k = 1 %, ~15 % of a ring-3 memory's touched lines), and the launches of
-// the per-message kernels collapse into two.
-// ----------------------------------------------------------------------------
+// (A merged multi-message receive -- one sweep over 8192-element ranges applying every
+// neighbour's message to each touched 64-B line of memory once, after a split pass over
+// the messages' indices -- was built and measured in r05 (git history): ring-3 loopback at
+// k = 1 %, line traffic 477 -> 422 MB per step, but 160 against 156 us per step: the sweep
+// ran at the per-message kernels' scattered line rate (~2.9-3.1 TB/s) and the split pass
+// cost more than the lines saved.  choco_sparse_accumulate_multi applies the messages with
+// the per-message kernels.)
 constexpr int kMaxMsgs = 8;
-constexpr int kMRShift = 12;
-constexpr int64_t kMRange = int64_t(1) << kMRShift;   // elements per range
-constexpr int kMSegs = (int)(kMRange / 16);          // 64-B segments per range = threads
-static_assert(kMSegs == kEwThreads, "one thread per segment of the range");
-struct MsgSet {
-  const float* val[kMaxMsgs];
-  const int32_t* idx[kMaxMsgs];
-  int64_t k[kMaxMsgs];
-  float w[kMaxMsgs];
-};
-
-// starts[m][q] = first update of message m with index >= q * kMRange (q = 0 .. nR),
-// for an ascending message.  Thread per update u (and u = k as the sentinel): writes
-// the ranges (range(u-1), range(u)].  Indices out of [0, n) and non-ascending pairs are
-// counted into *bad (then some entries may keep an earlier call's value: the sweep
-// clamps them and skips updates outside its range, so it stays in bounds).
-__global__ __launch_bounds__(kEwThreads) void sparse_split_kernel(MsgSet ms, int64_t n, int64_t nR,
-                                                                  int32_t* __restrict__ starts,
-                                                                  uint32_t* __restrict__ bad) {
-  const int m = blockIdx.y;
-  const int64_t k = ms.k[m];
-  const int32_t* __restrict__ idx = ms.idx[m];
-  int32_t* __restrict__ st = starts + (int64_t)m * (nR + 1);
-  uint32_t nbad = 0;
-  for (int64_t u = (int64_t)blockIdx.x * kEwThreads + threadIdx.x; u <= k; u += (int64_t)gridDim.x * kEwThreads) {
-    const int64_t j = u < k ? (int64_t)idx[u] : n;
-    const int64_t jp = u > 0 ? (int64_t)idx[u - 1] : -1;
-    const int64_t rq = u < k ? (j < 0 ? 0 : min(j >> kMRShift, nR)) : nR;
-    const int64_t rp = u > 0 ? (jp < 0 ? 0 : min(jp >> kMRShift, nR)) : -1;
-    if (u < k) nbad += ((j < 0 || j >= n) ? 1u : 0u) + ((u > 0 && jp >= j) ? 1u : 0u);
-    for (int64_t q = rp + 1; q <= rq; ++q) st[q] = (int32_t)u;
-  }
-  if (bad && nbad) atomicAdd(bad, nbad);
-}
-
-__global__ __launch_bounds__(kEwThreads) void sparse_acc_multi_kernel(MsgSet ms, int nmsg, float* __restrict__ mem,
-                                                                      int64_t n, int64_t nR,
-                                                                      const int32_t* __restrict__ starts) {
-  __shared__ float4 stage[kMSegs][4];   // the range's touched segments, compacted (16 KiB)
-  __shared__ uint8_t touched[kMSegs];
-  __shared__ uint8_t slot_of[kMSegs];
-  __shared__ uint8_t seg_of[kMSegs];
-  __shared__ uint32_t wsum[kEwThreads / 64];
-  const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-  const int64_t r = blockIdx.x;
-  const int64_t r0 = r << kMRShift;
-  const int64_t r1 = min(r0 + kMRange, n);
-  touched[tid] = 0;
-  // this range's update span per message (workgroup-uniform: scalar loads)
-  int32_t beg[kMaxMsgs], cnt[kMaxMsgs];
-#pragma unroll
-  for (int m = 0; m < kMaxMsgs; ++m) {
-    beg[m] = 0;
-    cnt[m] = 0;
-    if (m < nmsg) {
-      const int32_t* st = starts + (int64_t)m * (nR + 1);
-      const int64_t k = ms.k[m];
-      const int64_t b = min(max((int64_t)st[r], (int64_t)0), k);
-      const int64_t e = min(max((int64_t)st[r + 1], b), k);
-      beg[m] = (int32_t)b;
-      cnt[m] = (int32_t)(e - b);
-    }
-  }
-  // the first 256 updates of every message in registers (the common case: ~41 per
-  // message per range at k = 1 %); -1 = none / outside this range
-  int32_t ji[kMaxMsgs];
-  float vv[kMaxMsgs];
-#pragma unroll
-  for (int m = 0; m < kMaxMsgs; ++m) {
-    ji[m] = -1;
-    vv[m] = 0.f;
-    if (m < nmsg && tid < cnt[m]) {
-      const int64_t j = ms.idx[m][beg[m] + tid];
-      vv[m] = ms.val[m][beg[m] + tid];
-      ji[m] = (j >= r0 && j < r1) ? (int32_t)(j - r0) : -1;
-    }
-  }
-  __syncthreads();  // touched[] cleared
-#pragma unroll
-  for (int m = 0; m < kMaxMsgs; ++m) {
-    if (m < nmsg) {
-      if (ji[m] >= 0) touched[ji[m] >> 4] = 1;
-      for (int32_t u = tid + kEwThreads; u < cnt[m]; u += kEwThreads) {  // dense messages
-        const int64_t j = ms.idx[m][beg[m] + u];
-        if (j >= r0 && j < r1) touched[(j - r0) >> 4] = 1;
-      }
-    }
-  }
-  __syncthreads();
-  // compact the touched segments: slot = rank among them
-  const bool t = touched[tid] != 0;
-  const uint64_t bm = ballot(t);
-  if (lane == 0) wsum[wv] = (uint32_t)__popcll(bm);
-  __syncthreads();
-  uint32_t base = 0, total = 0;
-#pragma unroll
-  for (int i = 0; i < kEwThreads / 64; ++i) {
-    base += i < wv ? wsum[i] : 0u;
-    total += wsum[i];
-  }
-  if (t) {
-    const uint32_t s = base + mask_prefix(bm);
-    slot_of[tid] = (uint8_t)s;
-    seg_of[s] = (uint8_t)tid;
-  }
-  __syncthreads();
-  // load the touched segments: a quad per segment, lane l4 its float4
-  const int q = tid >> 2, l4 = tid & 3;
-  for (uint32_t s = q; s < total; s += kEwThreads / 4) {
-    const int64_t e = r0 + (int64_t)seg_of[s] * 16 + 4 * l4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e + 4 <= n) {
-      v = *reinterpret_cast<const float4*>(mem + e);
-    } else {
-      if (e < n) v.x = mem[e];
-      if (e + 1 < n) v.y = mem[e + 1];
-      if (e + 2 < n) v.z = mem[e + 2];
-    }
-    stage[s][l4] = v;
-  }
-  __syncthreads();
-  float* sf = reinterpret_cast<float*>(&stage[0][0]);
-  // the messages in order; inside one message every index is distinct
-#pragma unroll
-  for (int m = 0; m < kMaxMsgs; ++m) {
-    if (m < nmsg) {
-      const float w = ms.w[m];
-      if (ji[m] >= 0) {
-        float* p = sf + (int)slot_of[ji[m] >> 4] * 16 + (ji[m] & 15);
-        *p = *p + w * vv[m];
-      }
-      for (int32_t u = tid + kEwThreads; u < cnt[m]; u += kEwThreads) {
-        const int64_t j = ms.idx[m][beg[m] + u];
-        if (j >= r0 && j < r1) {
-          const int jl = (int)(j - r0);
-          float* p = sf + (int)slot_of[jl >> 4] * 16 + (jl & 15);
-          *p = *p + w * ms.val[m][beg[m] + u];
-        }
-      }
-      __syncthreads();
-    }
-  }
-  // write the touched segments back whole
-  for (uint32_t s = q; s < total; s += kEwThreads / 4) {
-    const int64_t e = r0 + (int64_t)seg_of[s] * 16 + 4 * l4;
-    const float4 v = stage[s][l4];
-    if (e + 4 <= n) {
-      *reinterpret_cast<float4*>(mem + e) = v;
-    } else {
-      if (e < n) mem[e] = v.x;
-      if (e + 1 < n) mem[e + 1] = v.y;
-      if (e + 2 < n) mem[e + 2] = v.z;
-    }
-  }
-}
 
 __global__ __launch_bounds__(kEwThreads) void gather_kernel(const float* __restrict__ x, const float* __restrict__ xh,
                                                             const int64_t* __restrict__ idx, int64_t k, float scale,
@@ -436,75 +269,27 @@ CHOCO_API int choco_sparse_accumulate(const float* val, const int32_t* idx, int6
 }
 
 CHOCO_API size_t choco_sparse_accumulate_multi_workspace_size(int64_t n, int32_t nmsg) {
-  const int64_t nR = (std::max<int64_t>(n, 1) + kMRange - 1) / kMRange;
-  return align_up((size_t)std::max(nmsg, 1) * (size_t)(nR + 1) * 4, 256);
+  (void)n;
+  (void)nmsg;
+  return 0;  // no scratch: the messages are applied by the per-message kernels
 }
 
 CHOCO_API int choco_sparse_accumulate_multi(const float* const* vals, const int32_t* const* idxs, const int64_t* ks,
                                             const float* weights, int32_t nmsg, int32_t self_slot, float* xhat_self,
                                             float* memory, int64_t n, void* ws, size_t ws_bytes,
                                             uint32_t* bad_count, void* stream) {
-  hipStream_t st = as_stream(stream);
+  (void)ws;
+  (void)ws_bytes;
   CHOCO_REQUIRE(vals && idxs && ks && weights && memory, "null pointer argument");
   CHOCO_REQUIRE(nmsg >= 1 && nmsg <= kMaxMsgs, "nmsg must be in [1, %d], got %d", kMaxMsgs, (int)nmsg);
   CHOCO_REQUIRE(self_slot >= -1 && self_slot < nmsg, "self_slot out of range");
-  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n must be in [1, 2^31-1)");
-  const int64_t nR = (n + kMRange - 1) / kMRange;
-  // the non-empty messages, in order (an empty message changes nothing)
-  MsgSet ms{};
-  int nm = 0, slot = -1;
-  bool sweep = aligned16(memory) && n >= kMRange;
   for (int m = 0; m < nmsg; ++m) {
     CHOCO_REQUIRE(ks[m] >= 0 && ks[m] < (int64_t)INT32_MAX, "message %d: k out of range", m);
-    if (ks[m] == 0) continue;
-    CHOCO_REQUIRE(vals[m] && idxs[m], "message %d: null values / indices", m);
-    if (m == self_slot) slot = nm;
-    ms.val[nm] = vals[m];
-    ms.idx[nm] = idxs[m];
-    ms.k[nm] = ks[m];
-    ms.w[nm] = weights[m];
-    // the split writes (range(u-1), range(u)] per update: long runs of empty ranges would
-    // serialise in one thread, so sparse messages (< one update per range) take the
-    // per-message kernels
-    sweep = sweep && ks[m] >= nR;
-    ++nm;
-  }
-  if (nm == 0) return CHOCO_OK;
-  // one message: the segment-owner kernel applies x_hat and memory in the same pass
-  if (nm == 1) sweep = false;
-  if (!sweep) {
-    for (int m = 0; m < nm; ++m) {
-      const int rc = choco_sparse_accumulate(ms.val[m], ms.idx[m], ms.k[m], m == slot ? xhat_self : nullptr, memory, n,
-                                             ms.w[m], bad_count, stream);
-      if (rc) return rc;
-    }
-    return CHOCO_OK;
-  }
-  nmsg = nm;
-  self_slot = slot;
-  const size_t need = choco_sparse_accumulate_multi_workspace_size(n, nmsg);
-  CHOCO_REQUIRE(ws != nullptr && ws_bytes >= need, "multi-message accumulate workspace too small: need %zu, got %zu",
-                need, ws_bytes);
-  int32_t* starts = static_cast<int32_t*>(ws);
-  if (self_slot >= 0 && xhat_self != nullptr) {
-    // x_hat takes the self message only (parallel_choco_v.py:307-308): hat + 1.0f * v == hat + v
-    // (its bad indices are counted by the split below)
-    const int rc = choco_sparse_accumulate(ms.val[self_slot], ms.idx[self_slot], ms.k[self_slot], nullptr, xhat_self,
-                                           n, 1.0f, nullptr, stream);
+    if (ks[m] == 0) continue;  // an empty message changes nothing
+    const int rc = choco_sparse_accumulate(vals[m], idxs[m], ks[m], m == self_slot ? xhat_self : nullptr, memory, n,
+                                           weights[m], bad_count, stream);
     if (rc) return rc;
   }
-  int64_t kmax = 0;
-  for (int m = 0; m < nmsg; ++m) kmax = std::max(kmax, ms.k[m]);
-  profile_begin("sparse_split", st);
-  CHOCO_KLAUNCH(sparse_split_kernel, dim3((unsigned)std::min<int64_t>((kmax + kEwThreads) / kEwThreads, 4096), nmsg),
-                dim3(kEwThreads), 0, st, ms, n, nR, starts, bad_count);
-  profile_end("sparse_split", st);
-  CHOCO_LAUNCHED("sparse_split_kernel");
-  profile_begin("sparse_acc_multi", st);
-  CHOCO_KLAUNCH(sparse_acc_multi_kernel, dim3((unsigned)nR), dim3(kEwThreads), 0, st, ms, (int)nmsg, memory, n, nR,
-                starts);
-  profile_end("sparse_acc_multi", st);
-  CHOCO_LAUNCHED("sparse_acc_multi_kernel");
   return CHOCO_OK;
 }
 

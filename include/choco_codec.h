@@ -194,20 +194,17 @@ int choco_sparse_accumulate(const float* val, const int32_t* idx, int64_t k,
                             float* xhat_self, float* memory, int64_t n, float weight,
                             uint32_t* bad_count, void* stream);
 
-/* Every neighbour's message in ONE receive sweep: the per-neighbour loop of
+/* Every neighbour's message of a receive step in ONE call: the per-neighbour loop of
  * CHOCOSparsificationCompressor.uncompress (parallel_choco_v.py:291-310) --
  *   for m in 0 .. nmsg-1 (neighbors_info order):
  *     if m == self_slot and xhat_self != NULL:  xhat_self[idx_m] += val_m
  *     memory[idx_m] += (float)weights[m] * val_m
- * bit-identical to nmsg choco_sparse_accumulate calls in that order.  vals / idxs / ks /
- * weights are HOST arrays of nmsg (1..8) entries (device pointers inside); indices
- * ascending per message, as this codec's wire carries them.  Each touched 64-B line of
- * memory is read and written once for all messages (a split pass over the indices, then
- * one sweep over 4096-element ranges); x_hat takes the self message in its own launch.
- * Messages with fewer than one update per 4096 elements, or an unaligned memory, take
- * the per-message kernels.  Workspace: choco_sparse_accumulate_multi_workspace_size(n,
- * nmsg) bytes (no zeroing contract).  Out-of-range / non-ascending indices are counted
- * into *bad_count (nullable) and skipped inside the sweep. */
+ * bit-identical to nmsg choco_sparse_accumulate calls in that order (which is how it runs:
+ * a merged sweep that applies all messages to each touched line of memory once measured
+ * slower).  vals / idxs / ks / weights are HOST arrays of nmsg (1..8) entries
+ * (device pointers inside).  Workspace: choco_sparse_accumulate_multi_workspace_size(n,
+ * nmsg) bytes (0: none).  Out-of-range / non-ascending indices are counted into
+ * *bad_count (nullable), as by choco_sparse_accumulate. */
 size_t choco_sparse_accumulate_multi_workspace_size(int64_t n, int32_t nmsg);
 int choco_sparse_accumulate_multi(const float* const* vals, const int32_t* const* idxs, const int64_t* ks,
                                   const float* weights, int32_t nmsg, int32_t self_slot, float* xhat_self,

@@ -1,5 +1,5 @@
-"""GPU parity: the multi-message receive sweep (choco_sparse_accumulate_multi) against the
-oracle's per-message sequence (parallel_choco_v.py:291-310: for each (rank, weight) in
+"""GPU parity: the one-call receive of all messages (choco_sparse_accumulate_multi) against
+the oracle's per-message sequence (parallel_choco_v.py:291-310: for each (rank, weight) in
 neighbors_info, x_hat[idx] += v for the self rank, memory[idx] += weight * v), bit for
 bit: messages whose indices share 64-B lines and elements, ranges with more than 256
 updates, ragged n, more than 8 messages, the per-message path (sparse messages, an

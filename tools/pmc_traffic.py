@@ -28,8 +28,6 @@ KERNELS = {
     "topk_seg_count": ("seg_count_kernel", 2.0),
     "topk_seg_emit": ("seg_emit_kernel", 2.0),
     "sparse_accumulate": ("sparse_acc_seg_kernel", 1.0),
-    "sparse_split": ("sparse_split_kernel", 2.0),
-    "sparse_acc_multi": ("sparse_acc_multi_kernel", 1.0),  # scattered line RMW: raw count
     "randk_count": ("randk_count_kernel", 1.0),
     "randk_tile": ("randk_tile_kernel", 1.0),  # 4-B gathers: raw count (uncalibrated, like the accumulate)
     "qsgd_norm": ("qsgd_norm_kernel", 2.0),
