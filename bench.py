@@ -86,6 +86,9 @@ def parse():
     p.add_argument("--ring3-loopback", action="store_true",
                    help="sparse codecs on one GPU: each step applies the self message plus two neighbour messages "
                         "(compressed from other resident deltas, no exchange) -- a ring worker's receive (cfg 4)")
+    p.add_argument("--defer-receive", action="store_true",
+                   help="step_* workloads: apply each step's received messages inside the NEXT step's first pass "
+                        "(receive + consensus step + first compress pass in one kernel; same x / x_hat / memory)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true", help="skip the host-resident (PCIe-inclusive) leg")
     p.add_argument("--lib", default=None, help=argparse.SUPPRESS)
@@ -137,6 +140,14 @@ class Worker:
         self.unfused = self.step_mode and args.unfused
         if self.unfused:
             self.label += "_unfused"
+        self.defer = self.step_mode and args.defer_receive and not self.unfused
+        if args.defer_receive and not self.defer:
+            raise SystemExit("--defer-receive: step_* workloads without --unfused only")
+        if self.defer:
+            if self.op not in ("qsgd", "sign"):
+                raise SystemExit("--defer-receive: step_qsgd / step_sign only")
+            self.label += "_deferred_receive"
+        self.pending = None  # (messages, weights, self slot) the next step's first pass applies
         self.backend = args.backend
         self.rank, self.world, self.dev = rank, world, dev
         self.nb = neighborhood(rank, world)
@@ -186,6 +197,9 @@ class Worker:
             self.msg = torch.zeros(4 + codec.sign_words(self.n), dtype=torch.int32, device=dev)
             self.wire = (self.msg[4:], self.msg[:4].view(torch.float32)[:1])
         self.recv = {r: torch.empty_like(self.msg) for r in self.peers}
+        # deferred sign receive: this step's words are packed in the pass that reads the previous
+        # step's (own) message, so the own message alternates between two buffers
+        self.msg_pp = [self.msg, torch.zeros_like(self.msg)] if (self.defer and self.op == "sign") else None
         self.loop_sets = None
         if args.ring3_loopback:
             if self.op not in ("topk", "topk_seg", "randk") or world != 1:
@@ -252,9 +266,23 @@ class Worker:
         if self.op == "topk":
             c.topk(self.x, self.k, xhat=self.hat, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]),
                    gossip=g, fold=self._fold_args())
+        elif self.op == "qsgd" and self.pending is not None:
+            # the previous step's receive + this step's consensus step + norm pass, one kernel
+            parts, weights, slot = self.pending
+            self.pending = None
+            c.qsgd_recv_gossip_norms(parts, weights, slot, self.x, self.mem, self.hat, GAMMA, self.param,
+                                     out=self.wire[1])
+            c.qsgd_compress(self.x, self.param, xhat=self.hat, norm_in=self.wire[1], seed=12345 + self.rank,
+                            offset=self.step_id, out=self.wire)
         elif self.op == "qsgd":
             c.qsgd_compress(self.x, self.param, xhat=self.hat, seed=12345 + self.rank, offset=self.step_id,
                             gossip=g, out=self.wire)
+        elif self.pending is not None:  # sign: receive + consensus step + pack, one kernel
+            parts, weights, slot = self.pending
+            self.pending = None
+            self.msg = self.msg_pp[self.step_id % 2]
+            self.wire = (self.msg[4:], self.msg[:4].view(torch.float32)[:1])
+            c.sign_recv_gossip_compress(parts, weights, slot, self.x, self.mem, self.hat, GAMMA, out=self.wire)
         else:
             c.sign_compress(self.x, xhat=self.hat, gossip=g, out=self.wire)
 
@@ -313,10 +341,16 @@ class Worker:
                                       [w for _, _, w in items], self.mem, self_slot=slot,
                                       xhat_self=self.hat if slot >= 0 else None)
         elif self.op == "qsgd":
-            parts = [(m[16:], m[:4].view(torch.float32)) for m in msgs]
+            parts = [(m[16:], m[:4].view(torch.float32)[:1]) for m in msgs]
+            if self.defer:  # applied by the next step's first pass
+                self.pending = (parts, list(self.weights), self.self_slot)
+                return
             c.qsgd_accumulate(parts, self.weights, self.self_slot, self.n, self.param, self.mem, xhat_self=self.hat)
         else:
             parts = [(m[4:], m[:1].view(torch.float32)) for m in msgs]
+            if self.defer:  # applied by the next step's pass
+                self.pending = (parts, list(self.weights), self.self_slot)
+                return
             c.sign_accumulate(parts, self.weights, self.self_slot, self.n, self.mem, xhat_self=self.hat)
 
     def step(self):
@@ -336,6 +370,14 @@ class Worker:
             comp, dec, note = self._codec_bytes(n, nm)
             # the consensus step reads x, memory, x_hat and writes x (16n) in place of the
             # 4n read of a resident delta: the compulsory bytes of the fused pass
+            if self.defer:
+                # the receive runs inside the next step's first pass: one stage whose compulsory
+                # bytes are x, x_hat, memory read and written once (24n), every message read, and
+                # this step's message written
+                wire = comp - 4 * n
+                return 24 * n + nm * (wire - 4) + wire, 0, (
+                    "deferred receive: x, x_hat, memory read + written once (24n) + each received message + "
+                    "this step's message (QSGD: the quantize pass's second read of x, x_hat is not counted)")
             return comp + 12 * n, dec, "consensus step + compress 16n + codec output; " + note
         return self._codec_bytes(n, nm)
 
@@ -540,7 +582,7 @@ def main():
     w = Worker(args, rank, world, dev)
     comp_k, dec_k = STAGES[w.op]
     if w.step_mode:
-        comp_k = comp_k + ["gossip_step"]
+        comp_k = comp_k + ["gossip_step", "qsgd_recv_norm", "sign_recv_pack"]
 
     def barrier():
         torch.cuda.synchronize()

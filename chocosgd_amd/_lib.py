@@ -57,6 +57,8 @@ SIGNATURES = {
     "choco_sign_unpack": (_c_i32, [_vp, _c_i64, _vp, _vp]),
     "choco_sign_decompress_accumulate": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i32, _c_i64, _vp, _c_i32,
                                                   _vp, _vp, _vp, _c_sz, _vp]),
+    "choco_sign_recv_gossip_compress": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i32, _vp, _vp, _vp, _c_f32, _c_i64,
+                                                 _vp, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_sign_decompress_axpy": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i64, _vp, _c_i32, _c_i32, _vp, _vp]),
     "choco_sign_decompress_extrapolate": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _c_f32, _c_f32, _vp, _vp]),
     "choco_qsgd_decompress_extrapolate": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _c_i32, _c_i32, _c_f32, _c_f32,
@@ -71,6 +73,8 @@ SIGNATURES = {
     "choco_qsgd_decompress_accumulate": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i32, _c_i64, _vp, _c_i32,
                                                   _c_i32, _c_i32, _vp, _vp, _vp]),
     "choco_qsgd_norms": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _vp, _vp, _c_sz, _vp]),
+    "choco_qsgd_recv_gossip_norms": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i32, _vp, _vp, _vp, _c_f32, _c_i64, _vp,
+                                              _c_i32, _c_i32, _c_i32, _vp, _vp, _c_sz, _vp]),
     "choco_gossip_qsgd_norms": (_c_i32, [_vp, _vp, _vp, _c_f32, _c_i64, _vp, _c_i32, _vp, _vp, _c_sz, _vp]),
     "choco_qsgd_quantize_range": (_c_i32, [_vp, _vp, _c_i64, _vp, _c_i32, _c_i32, _c_i32, _vp, _c_u64, _c_u64,
                                            _c_i64, _c_i64, _vp, _vp]),

@@ -727,6 +727,51 @@ def sign_accumulate(messages, weights, self_slot, n, memory, xhat_self=None, seg
                    "choco_sign_decompress_accumulate")
 
 
+def sign_recv_gossip_compress(messages, weights, self_slot, x, memory, xhat, gamma, seg_off=None, nseg=1,
+                              out=None):
+    """The deferred receive fused into the next step's pass (include/choco_codec.h
+    choco_sign_recv_gossip_compress): the previous step's messages [(packed, norms)] into
+    x_hat (self_slot) and memory in order, then x += gamma (memory - x_hat), then this step's
+    message (packed signs of x - x_hat, L1 norms) -- returned, or written to
+    `out=(packed, norms)`, which must not be one of `messages`' buffers.  More than 8
+    messages: the leading chunks are applied by sign_accumulate first (same order)."""
+    _require(x, torch.float32, "x")
+    _require(xhat, torch.float32, "xhat")
+    _require(memory, torch.float32, "memory")
+    n = x.numel()
+    _check_layout(memory, xhat, n, seg_off, nseg)
+    if len(messages) != len(weights) or not messages:
+        raise RuntimeError("one weight per message, at least one message")
+    words = sign_words(n)
+    for p, nm in messages:
+        _require(p, torch.int32, "packed")
+        _require(nm, torch.float32, "norms")
+        if p.numel() != words or nm.numel() != nseg:
+            raise RuntimeError(f"sign message must hold {words} words and {nseg} norms")
+    dev = x.device
+    if out is not None:
+        packed, norms = _out_views(out, words, torch.int32, nseg, dev)
+    else:
+        packed = torch.empty(words, dtype=torch.int32, device=dev)
+        norms = torch.empty(nseg, dtype=torch.float32, device=dev)
+    head = len(messages) - MAX_FUSED_MSGS
+    if head > 0:  # leading messages first, in order
+        sign_accumulate(messages[:head], weights[:head], self_slot, n, memory,
+                        xhat_self=xhat if 0 <= self_slot < head else None, seg_off=seg_off, nseg=nseg)
+        messages, weights, self_slot = messages[head:], weights[head:], self_slot - head
+    slot = self_slot if 0 <= self_slot < len(messages) else -1
+    L = lib()
+    ws = workspace(dev, "acc", L.choco_sign_workspace_size(nseg))
+    pp, keep1 = _lib.ptr_array([p.data_ptr() for p, _ in messages])
+    nn, keep2 = _lib.ptr_array([nm.data_ptr() for _, nm in messages])
+    ww, keep3 = _lib.f32_array([float(w) for w in weights])
+    _lib.check(L.choco_sign_recv_gossip_compress(pp, nn, ww, len(messages), slot, _ptr(x), _ptr(memory), _ptr(xhat),
+                                                 float(gamma), n, _ptr(seg_off), int(nseg), _ptr(packed),
+                                                 _ptr(norms), _ptr(ws), ws.numel(), _stream(dev)),
+               "choco_sign_recv_gossip_compress")
+    return packed, norms
+
+
 def sign_axpy(messages, weights, n, target, seg_off=None, nseg=1, two_roundings=False):
     """target += w_m * decode(m) for each (packed, norms) message in order -- the receiver of
     the DCD / DeepSqueeze sign compressors; `two_roundings` selects torch's add_(w * u)
@@ -912,6 +957,46 @@ def qsgd_norms(x, xhat=None, seg_off=None, nseg=1, gossip=None, out=None):
     else:
         _lib.check(L.choco_qsgd_norms(_ptr(x), _ptr(xhat), x.numel(), _ptr(seg_off), int(nseg), _ptr(norms),
                                       _ptr(ws), ws.numel(), _stream(dev)), "choco_qsgd_norms")
+    return norms
+
+
+def qsgd_recv_gossip_norms(messages, weights, self_slot, x, memory, xhat, gamma, q, is_biased=False, seg_off=None,
+                           nseg=1, out=None):
+    """The deferred receive fused into the next step's first pass (include/choco_codec.h
+    choco_qsgd_recv_gossip_norms): the previous step's messages [(packed, norms)] into x_hat
+    (self_slot) and memory in order, then x += gamma (memory - x_hat), then this step's
+    per-segment norms of x - x_hat (returned, or written to `out`).  More than 8 messages:
+    the leading chunks are applied by qsgd_accumulate first (same order, same results)."""
+    _require(x, torch.float32, "x")
+    _require(xhat, torch.float32, "xhat")
+    _check_layout(memory, xhat, x.numel(), seg_off, nseg)
+    n = x.numel()
+    if len(messages) != len(weights) or not messages:
+        raise RuntimeError("one weight per message, at least one message")
+    nbytes = qsgd_packed_bytes(n, q)
+    for p, nm in messages:
+        _require(p, torch.uint8, "packed")
+        _require(nm, torch.float32, "norms")
+        if p.numel() != nbytes or nm.numel() != nseg:
+            raise RuntimeError(f"QSGD message must hold {nbytes} bytes and {nseg} norms")
+    dev = x.device
+    norms = out if out is not None else torch.empty(nseg, dtype=torch.float32, device=dev)
+    _require(norms, torch.float32, "norms")
+    head = len(messages) - MAX_FUSED_MSGS
+    if head > 0:  # leading messages first, in order
+        qsgd_accumulate(messages[:head], weights[:head], self_slot, n, q, memory, xhat_self=xhat,
+                        is_biased=is_biased, seg_off=seg_off, nseg=nseg)
+        messages, weights, self_slot = messages[head:], weights[head:], self_slot - head
+    slot = self_slot if 0 <= self_slot < len(messages) else -1
+    L = lib()
+    ws = workspace(dev, "acc", L.choco_qsgd_workspace_size(nseg))
+    pp, keep1 = _lib.ptr_array([p.data_ptr() for p, _ in messages])
+    nn, keep2 = _lib.ptr_array([nm.data_ptr() for _, nm in messages])
+    ww, keep3 = _lib.f32_array([float(w) for w in weights])
+    _lib.check(L.choco_qsgd_recv_gossip_norms(pp, nn, ww, len(messages), slot, _ptr(x), _ptr(memory), _ptr(xhat),
+                                              float(gamma), n, _ptr(seg_off), int(nseg), int(q),
+                                              1 if is_biased else 0, _ptr(norms), _ptr(ws), ws.numel(),
+                                              _stream(dev)), "choco_qsgd_recv_gossip_norms")
     return norms
 
 

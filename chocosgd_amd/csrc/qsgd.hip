@@ -35,6 +35,7 @@ constexpr int kQTile = kQThreads * kQPer;        // 2048
 constexpr int kNormTile = 49152;
 static_assert(kNormTile % 8192 == 0, "whole load rounds per norm tile");
 constexpr int kQMaxMsg = 8;
+constexpr int kAccRep = 8;  // replicas of the fp64 norm accumulators (the fused receive pass)
 
 struct QsgdWs {
   unsigned int ticket;
@@ -250,6 +251,37 @@ CHOCO_DEV void store_levels(uint8_t* __restrict__ plane, int64_t t, const uint32
     if (CW == 2) reinterpret_cast<uint16_t*>(plane)[t] = (uint16_t)acc;
     if (CW == 1) plane[t] = (uint8_t)acc;
   }
+}
+
+// A group's packed levels as loaded (CW * 8 bits: 1 to 4 words) and one level of them: the
+// fused receive keeps the packed form in registers (8 unpacked levels per message and group
+// did not fit).
+template <int CW>
+struct LevelWords {
+  uint32_t w[CW == 16 ? 4 : (CW == 8 ? 2 : 1)];
+};
+template <int CW>
+CHOCO_DEV LevelWords<CW> load_level_words(const uint8_t* __restrict__ plane, int64_t t) {
+  LevelWords<CW> r;
+  if (CW == 16) {
+    const uint4 v = reinterpret_cast<const uint4*>(plane)[t];
+    r.w[0] = v.x; r.w[CW == 16 ? 1 : 0] = v.y; r.w[CW == 16 ? 2 : 0] = v.z; r.w[CW == 16 ? 3 : 0] = v.w;
+  } else if (CW == 8) {
+    const uint2 v = reinterpret_cast<const uint2*>(plane)[t];
+    r.w[0] = v.x; r.w[CW == 8 ? 1 : 0] = v.y;
+  } else if (CW == 4) {
+    r.w[0] = reinterpret_cast<const uint32_t*>(plane)[t];
+  } else if (CW == 2) {
+    r.w[0] = reinterpret_cast<const uint16_t*>(plane)[t];
+  } else {
+    r.w[0] = plane[t];
+  }
+  return r;
+}
+template <int CW>
+CHOCO_DEV uint32_t level_of(const LevelWords<CW>& r, int c) {
+  const int bit = c * CW;
+  return (r.w[bit >> 5] >> (bit & 31)) & ((CW == 16 ? 0x10000u : (1u << CW)) - 1u);
 }
 
 template <int CW>
@@ -646,6 +678,175 @@ __global__ __launch_bounds__(kQThreads) void qsgd_decode_kernel(QMsgs M, int64_t
   }
 }
 
+// ---------------------------------------------------------------- deferred receive, fused
+// The previous step's receive (CHOCOQuantizationCompressor.uncompress, parallel_choco_v.py:
+// 430-433: x_hat += q_self, memory += w * q per message in neighbors_info order), this
+// step's consensus step (update_params_from_neighbor, optim/utils.py:67-72: x += gamma
+// (memory - x_hat)) and this step's norm pass (per-segment ||x_new - x_hat||_2, fp64) in
+// ONE pass over x, x_hat and memory.  Every step is elementwise, so the results are those of
+// the decode, gossip and norm passes run one after the other; the step's SGD update of x
+// comes first, as in ParallelCHOCO_V.step (apply_gradient, then the previous gossip's join).
+// Thread t: kRG 8-element groups (the planes' groups) t_e0 + g * 2048 + 8 t; every load of
+// both groups in flight before any arithmetic.  fp64 sums go to kAccRep replicas of the
+// per-segment accumulators (workgroup b -> replica b & 7: 24K workgroups at 100M would
+// otherwise queue on one address); the last workgroup sums the replicas.
+constexpr int kRG = 2;
+constexpr int kRTile = kQTile * kRG;  // 4096 elements per workgroup
+template <int CW, int NM>
+__global__ __launch_bounds__(kQThreads) void qsgd_recv_gossip_norm_kernel(
+    QMsgs M, int64_t n, const int64_t* __restrict__ seg_off, int nseg, int s_levels, int biased,
+    float* __restrict__ x, float* __restrict__ hat, float* __restrict__ mem, float gamma,
+    QsgdWs* __restrict__ ws, float* __restrict__ norms_out) {
+  __shared__ int s_seg[2];
+  __shared__ double s_red[kQThreads / 64];
+  __shared__ unsigned int s_flag;
+  double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
+  double* __restrict__ rep = acc + (size_t)(blockIdx.x & (kAccRep - 1)) * (size_t)nseg;
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int64_t t_e0 = (int64_t)blockIdx.x * kRTile;
+  const int64_t t_e1 = std::min<int64_t>(t_e0 + kRTile, n);
+  const int sg0 = tile_seg(seg_off, nseg, t_e0, t_e1, s_seg);
+  const bool uniform = s_seg[1] == sg0;
+  const float sf = (float)s_levels;
+  const bool has_self = M.self_slot >= 0;
+  float xv[kRG][kQPer], hv[kRG][kQPer], mv[kRG][kQPer];
+  LevelWords<CW> lw[kRG][NM];
+  uint32_t sb[kRG][NM];
+  // ---- loads of both groups (a group past n is skipped; the buffer's last group is partial)
+#pragma unroll
+  for (int g = 0; g < kRG; ++g) {
+    const int64_t e0 = t_e0 + (int64_t)g * kQTile + (int64_t)tid * kQPer;
+    if (e0 >= n) continue;
+    if (e0 + kQPer <= n) {
+      const float4 a0 = *reinterpret_cast<const float4*>(x + e0), a1 = *reinterpret_cast<const float4*>(x + e0 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(hat + e0), b1 = *reinterpret_cast<const float4*>(hat + e0 + 4);
+      const float4 c0 = *reinterpret_cast<const float4*>(mem + e0), c1 = *reinterpret_cast<const float4*>(mem + e0 + 4);
+      xv[g][0] = a0.x; xv[g][1] = a0.y; xv[g][2] = a0.z; xv[g][3] = a0.w;
+      xv[g][4] = a1.x; xv[g][5] = a1.y; xv[g][6] = a1.z; xv[g][7] = a1.w;
+      hv[g][0] = b0.x; hv[g][1] = b0.y; hv[g][2] = b0.z; hv[g][3] = b0.w;
+      hv[g][4] = b1.x; hv[g][5] = b1.y; hv[g][6] = b1.z; hv[g][7] = b1.w;
+      mv[g][0] = c0.x; mv[g][1] = c0.y; mv[g][2] = c0.z; mv[g][3] = c0.w;
+      mv[g][4] = c1.x; mv[g][5] = c1.y; mv[g][6] = c1.z; mv[g][7] = c1.w;
+    } else {
+#pragma unroll
+      for (int c = 0; c < kQPer; ++c) {
+        const bool in = e0 + c < n;
+        xv[g][c] = in ? x[e0 + c] : 0.f;
+        hv[g][c] = in ? hat[e0 + c] : 0.f;
+        mv[g][c] = in ? mem[e0 + c] : 0.f;
+      }
+    }
+    const int64_t t = e0 / kQPer;
+#pragma unroll
+    for (int q = 0; q < NM; ++q) {
+      lw[g][q] = load_level_words<CW>(M.lvl[q], t);
+      sb[g][q] = M.sgn[q][t];
+    }
+  }
+  // ---- receive, consensus step, stores, sums of squares
+  double p = 0.0;         // uniform tile: this thread's sum
+  int run_s = -1;         // otherwise: the current segment run and its sum
+  double run_p = 0.0;
+#pragma unroll
+  for (int g = 0; g < kRG; ++g) {
+    const int64_t e0 = t_e0 + (int64_t)g * kQTile + (int64_t)tid * kQPer;
+    if (e0 >= n) continue;
+    QParam P[NM];
+#pragma unroll
+    for (int q = 0; q < NM; ++q) P[q] = qparam(M.norms[q], seg_off, n, sg0, s_levels, biased != 0);
+    int s = sg0;
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) {
+      const int64_t e = e0 + c;
+      if (!uniform && e < n) {
+        while (s + 1 < nseg && seg_off[s + 1] <= e) ++s;
+#pragma unroll
+        for (int q = 0; q < NM; ++q) P[q] = qparam(M.norms[q], seg_off, n, s, s_levels, biased != 0);
+      }
+#pragma unroll
+      for (int q = 0; q < NM; ++q) {
+        const float v = qdecode(level_of<CW>(lw[g][q], c), (sb[g][q] >> c) & 1u, P[q], sf);
+        if (has_self && q == M.self_slot) hv[g][c] = hv[g][c] + v;  // hat_params.buffer += q_values
+        const float wv = M.w[q] * v;                                  // weight * q_values (rounded)
+        mv[g][c] = mv[g][c] + wv;                                     // memory += ...
+      }
+      xv[g][c] = gossip1(xv[g][c], mv[g][c], hv[g][c], gamma);
+      const double d = (double)(xv[g][c] - hv[g][c]);
+      if (e < n) {
+        if (uniform) {
+          p += d * d;
+        } else {
+          if (s != run_s) {
+            if (run_s >= 0 && run_p != 0.0) unsafeAtomicAdd(&rep[run_s], run_p);
+            run_s = s;
+            run_p = 0.0;
+          }
+          run_p += d * d;
+        }
+      }
+    }
+    if (e0 + kQPer <= n) {
+      *reinterpret_cast<float4*>(x + e0) = make_float4(xv[g][0], xv[g][1], xv[g][2], xv[g][3]);
+      *reinterpret_cast<float4*>(x + e0 + 4) = make_float4(xv[g][4], xv[g][5], xv[g][6], xv[g][7]);
+      *reinterpret_cast<float4*>(mem + e0) = make_float4(mv[g][0], mv[g][1], mv[g][2], mv[g][3]);
+      *reinterpret_cast<float4*>(mem + e0 + 4) = make_float4(mv[g][4], mv[g][5], mv[g][6], mv[g][7]);
+      if (has_self) {
+        *reinterpret_cast<float4*>(hat + e0) = make_float4(hv[g][0], hv[g][1], hv[g][2], hv[g][3]);
+        *reinterpret_cast<float4*>(hat + e0 + 4) = make_float4(hv[g][4], hv[g][5], hv[g][6], hv[g][7]);
+      }
+    } else {
+      for (int c = 0; c < kQPer && e0 + c < n; ++c) {
+        x[e0 + c] = xv[g][c];
+        mem[e0 + c] = mv[g][c];
+        if (has_self) hat[e0 + c] = hv[g][c];
+      }
+    }
+  }
+  if (uniform) {
+    p = wave_sum(p);
+    if (lane == 0) s_red[w] = p;
+    __syncthreads();
+    if (tid == 0) {
+      double t = 0.0;
+      for (int i = 0; i < kQThreads / 64; ++i) t += s_red[i];
+      if (t != 0.0) unsafeAtomicAdd(&rep[sg0], t);
+    }
+  } else if (run_s >= 0 && run_p != 0.0) {
+    unsafeAtomicAdd(&rep[run_s], run_p);
+  }
+  if (last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
+    for (int q = threadIdx.x; q < nseg; q += blockDim.x) {
+      double t = 0.0;
+      for (int r = 0; r < kAccRep; ++r) t += atomic_exchange_double(&acc[(size_t)r * nseg + q], 0.0);
+      norms_out[q] = (float)sqrt(t);
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <int CW>
+static void launch_recv_gossip(const QMsgs& M, int64_t n, const int64_t* seg_off, int nseg, int s_levels,
+                               int biased, float* x, float* hat, float* mem, float gamma, QsgdWs* ws, float* norms,
+                               hipStream_t st) {
+  const unsigned grid = (unsigned)((n + kRTile - 1) / kRTile);
+#define CHOCO_RG(NMV)                                                                                     \
+  case NMV:                                                                                               \
+    CHOCO_KLAUNCH((qsgd_recv_gossip_norm_kernel<CW, NMV>), dim3(grid), dim3(kQThreads), 0, st, M, n, seg_off, \
+                  nseg, s_levels, biased, x, hat, mem, gamma, ws, norms);                                 \
+    break;
+  switch (M.nmsg) {
+    CHOCO_RG(1)
+    CHOCO_RG(2)
+    CHOCO_RG(3)
+    CHOCO_RG(4)
+    CHOCO_RG(5)
+    CHOCO_RG(6)
+    CHOCO_RG(7)
+    CHOCO_RG(8)
+  }
+#undef CHOCO_RG
+}
+
 // Elements [e0, e1) (e0 a multiple of kQTile; e1 a multiple of it or n).
 template <int CW, int NM, int MODE>
 static void launch_decode(const QMsgs& M, int64_t n, const int64_t* seg_off, int nseg, int s_levels, int biased,
@@ -693,7 +894,9 @@ CHOCO_API int64_t choco_qsgd_packed_bytes(int64_t n, int32_t q) {
 }
 
 CHOCO_API size_t choco_qsgd_workspace_size(int32_t nseg) {
-  return 256 + align_up((size_t)(nseg > 0 ? nseg : 1) * sizeof(double), 256);
+  // the ticket, then kAccRep replicas of the per-segment fp64 accumulators (the norm pass
+  // uses replica 0; the fused receive pass all of them)
+  return 256 + align_up((size_t)kAccRep * (size_t)(nseg > 0 ? nseg : 1) * sizeof(double), 256);
 }
 
 static int qsgd_check(const float* x, const float* xhat, int64_t n, const int64_t* seg_off, int32_t nseg) {
@@ -949,6 +1152,46 @@ CHOCO_API int choco_qsgd_decompress_accumulate(const uint8_t* const* packed_list
   launch_decode_cw<1>(cw, M, n, seg_off, nseg, (1 << q) - 1, is_biased, xhat_self, memory, st);
   profile_end("qsgd_accumulate", st);
   CHOCO_LAUNCHED("qsgd_decode_kernel");
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_qsgd_recv_gossip_norms(const uint8_t* const* packed_list, const float* const* norms_list,
+                                           const float* weights, int32_t nmsg, int32_t self_slot, float* x,
+                                           float* memory, float* xhat, float gamma, int64_t n,
+                                           const int64_t* seg_off, int32_t nseg, int32_t q, int32_t is_biased,
+                                           float* norms_out, void* ws, size_t ws_bytes, void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(packed_list && norms_list && weights && x && memory && xhat && norms_out, "null pointer argument");
+  CHOCO_REQUIRE(nmsg >= 1 && nmsg <= kQMaxMsg, "nmsg must be in [1, %d]", kQMaxMsg);
+  CHOCO_REQUIRE(self_slot >= -1 && self_slot < nmsg, "bad self_slot");
+  CHOCO_REQUIRE(q >= 1 && q <= 16, "q must be in [1, 16]");
+  if (int rc = qsgd_check(x, xhat, n, seg_off, nseg)) return rc;
+  CHOCO_REQUIRE(aligned16(memory), "buffers must be 16-byte aligned");
+  CHOCO_REQUIRE(ws && ws_bytes >= choco_qsgd_workspace_size(nseg), "qsgd workspace too small");
+  const int cw = container_bits(q);
+  QMsgs M{};
+  for (int m = 0; m < nmsg; ++m) {
+    CHOCO_REQUIRE(packed_list[m] && norms_list[m], "null message pointer");
+    CHOCO_REQUIRE(aligned16(packed_list[m]), "packed messages must be 16-byte aligned");
+    M.lvl[m] = packed_list[m];
+    M.sgn[m] = packed_list[m] + plane_bytes(n, cw);
+    M.norms[m] = norms_list[m];
+    M.w[m] = weights[m];
+  }
+  M.nmsg = nmsg;
+  M.self_slot = self_slot;
+  const int s_levels = (1 << q) - 1;
+  QsgdWs* w = static_cast<QsgdWs*>(ws);
+  profile_begin("qsgd_recv_norm", st);
+  switch (cw) {
+    case 1: launch_recv_gossip<1>(M, n, seg_off, nseg, s_levels, is_biased, x, xhat, memory, gamma, w, norms_out, st); break;
+    case 2: launch_recv_gossip<2>(M, n, seg_off, nseg, s_levels, is_biased, x, xhat, memory, gamma, w, norms_out, st); break;
+    case 4: launch_recv_gossip<4>(M, n, seg_off, nseg, s_levels, is_biased, x, xhat, memory, gamma, w, norms_out, st); break;
+    case 8: launch_recv_gossip<8>(M, n, seg_off, nseg, s_levels, is_biased, x, xhat, memory, gamma, w, norms_out, st); break;
+    default: launch_recv_gossip<16>(M, n, seg_off, nseg, s_levels, is_biased, x, xhat, memory, gamma, w, norms_out, st); break;
+  }
+  profile_end("qsgd_recv_norm", st);
+  CHOCO_LAUNCHED("qsgd_recv_gossip_norm_kernel");
   return CHOCO_OK;
 }
 

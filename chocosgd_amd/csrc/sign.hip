@@ -781,6 +781,173 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
 // measured slower than the column-tile receiver, 1208 vs 1127 us at 345M, one message:
 // removed, git history r03.)
 
+// Deferred receive (one segment): the previous step's messages, this step's consensus
+// step and this step's pack in ONE pass over x, x_hat and memory.
+// ParallelCHOCO_V.step (parallel_choco_v.py:104-155) runs uncompress (:548-558: per
+// message u = (norm / numel) * sign; x_hat += u for the self rank, memory += w * u in
+// neighbors_info order), then update_params_from_neighbor (optim/utils.py:67-72) and the
+// next compress; every element's chain here is exactly that sequence's (sign_apply,
+// gossip1, the pack's x_new - x_hat), so x, x_hat, memory and the words are bit-identical
+// to sign_accumulate_kernel + sign_pack1_kernel<.., GS>.  The column tiles are
+// sign_pack1_kernel's: lane l owns words j0+4l..+3 of every message and of the output, so
+// row r's float4 at the lane's run offset is exactly bit r of its words (no realignment).
+// Rows go in groups of 4 with two groups in flight (x, x_hat, memory of 8 rows).
+#ifndef CHOCO_SRP_RU
+#define CHOCO_SRP_RU 4
+#endif
+#ifndef CHOCO_SRP_NTS
+#define CHOCO_SRP_NTS 1
+#endif
+#ifndef CHOCO_SRP_NTL
+#define CHOCO_SRP_NTL 1
+#endif
+#ifndef CHOCO_SRP_WPE
+#define CHOCO_SRP_WPE 1
+#endif
+template <int NM, bool HS>
+__global__ __launch_bounds__(kSignThreads) __attribute__((amdgpu_waves_per_eu(CHOCO_SRP_WPE))) void sign_recv_pack1_kernel(SignMsgs M, float* __restrict__ x,
+                                                                       float* __restrict__ xh,
+                                                                       float* __restrict__ mem, float gamma,
+                                                                       int64_t n, int64_t Np,
+                                                                       uint32_t* __restrict__ packed,
+                                                                       float* __restrict__ l1_out,
+                                                                       SignWs* __restrict__ ws) {
+  constexpr int RU = CHOCO_SRP_RU;
+  constexpr int NG = 32 / RU;
+  constexpr bool NTL = CHOCO_SRP_NTL, NTS = CHOCO_SRP_NTS;
+  __shared__ double s_red[kSignThreads / 64];
+  __shared__ unsigned int s_flag;
+  double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int64_t j0 = (int64_t)blockIdx.x * kSignCols + 256 * w;
+  const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
+  const bool interior = ncol == 256 && (int64_t)31 * Np + j0 + 256 <= n;
+  // this lane's words of every message and the per-message scale (norm / numel)
+  uint32_t in[NM][4];
+  float sc[NM];
+  {
+    const int64_t j = j0 + 4 * lane;
+#pragma unroll
+    for (int q = 0; q < NM; ++q) {
+      sc[q] = M.norms[q][0] / (float)n;
+      if (j + 3 < Np) {
+        const uint4 t = *reinterpret_cast<const uint4*>(M.packed[q] + j);
+        in[q][0] = t.x; in[q][1] = t.y; in[q][2] = t.z; in[q][3] = t.w;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) in[q][c] = (j + c < Np) ? M.packed[q][j + c] : 0u;
+      }
+    }
+  }
+  // one element of row r, word column c: receive, consensus step; returns x_new - x_hat
+  auto elem = [&](int r, int c, float& xv, float& hv, float& mv) -> float {
+#pragma unroll
+    for (int q = 0; q < NM; ++q) {
+      const float u = ((in[q][c] >> r) & 1u) ? -sc[q] : sc[q];
+      if (HS && q == M.self_slot) hv = hv + u;
+      mv = fmaf(M.w[q], u, mv);
+    }
+    xv = gossip1(xv, mv, hv, gamma);
+    return xv - hv;
+  };
+  uint32_t wd[4] = {0u, 0u, 0u, 0u};
+  double p = 0.0;
+  if (interior) {
+    const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x, (uint32_t)(n * 4));
+    const __amdgpu_buffer_rsrc_t rh = buf_rsrc(xh, (uint32_t)(n * 4));
+    const __amdgpu_buffer_rsrc_t rm = buf_rsrc(mem, (uint32_t)(n * 4));
+    const uint32_t voff = 16u * (uint32_t)lane;
+    auto row_off = [&](int r) -> uint32_t { return (uint32_t)(((int64_t)r * Np + j0) * 4); };
+    struct Group {
+      float4 x[RU], h[RU], m[RU];
+    };
+    auto load_group = [&](int g, Group& G) {
+#pragma unroll
+      for (int u = 0; u < RU; ++u) G.x[u] = ld_buf4s<NTL>(rx, voff, row_off(g * RU + u));
+#pragma unroll
+      for (int u = 0; u < RU; ++u) G.h[u] = ld_buf4s<NTL>(rh, voff, row_off(g * RU + u));
+#pragma unroll
+      for (int u = 0; u < RU; ++u) G.m[u] = ld_buf4s<NTL>(rm, voff, row_off(g * RU + u));
+    };
+    auto proc_group = [&](int g, Group& G) {
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int r = g * RU + u;
+        float xv[4] = {G.x[u].x, G.x[u].y, G.x[u].z, G.x[u].w};
+        float hv[4] = {G.h[u].x, G.h[u].y, G.h[u].z, G.h[u].w};
+        float mv[4] = {G.m[u].x, G.m[u].y, G.m[u].z, G.m[u].w};
+        float v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = elem(r, c, xv[c], hv[c], mv[c]);
+        // non-temporal: none of the three is re-read by this step
+        st_buf4s<NTS>(rx, voff, row_off(r), make_float4(xv[0], xv[1], xv[2], xv[3]));
+        st_buf4s<NTS>(rm, voff, row_off(r), make_float4(mv[0], mv[1], mv[2], mv[3]));
+        if (HS) st_buf4s<NTS>(rh, voff, row_off(r), make_float4(hv[0], hv[1], hv[2], hv[3]));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wd[c] |= (v[c] < 0.f ? 1u : 0u) << r;
+        p += ((double)fabsf(v[0]) + (double)fabsf(v[1])) + ((double)fabsf(v[2]) + (double)fabsf(v[3]));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    Group A, B;
+    load_group(0, A);
+    load_group(1, B);
+#pragma unroll
+    for (int g = 0; g < NG; g += 2) {
+      proc_group(g, A);
+      if (g + 2 < NG) load_group(g + 2, A);
+      proc_group(g + 1, B);
+      if (g + 3 < NG) load_group(g + 3, B);
+    }
+  } else {
+#pragma unroll 1
+    for (int r = 0; r < 32; ++r) {
+      const int64_t s = (int64_t)r * Np + j0 + 4 * lane;
+      float tt[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int64_t e = s + c;
+        tt[c] = 0.f;
+        if (4 * lane + c < ncol && e < n) {
+          float xv = x[e], hv = xh[e], mv = mem[e];
+          tt[c] = elem(r, c, xv, hv, mv);
+          x[e] = xv;
+          mem[e] = mv;
+          if (HS) xh[e] = hv;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wd[c] |= (tt[c] < 0.f ? 1u : 0u) << r;
+      p += ((double)fabsf(tt[0]) + (double)fabsf(tt[1])) + ((double)fabsf(tt[2]) + (double)fabsf(tt[3]));
+    }
+  }
+  {
+    const int64_t j = j0 + 4 * lane;
+    if (j + 3 < Np) {
+      *reinterpret_cast<uint4*>(packed + j) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (j + c < Np) packed[j + c] = wd[c];
+    }
+  }
+  p = wave_sum(p);
+  if (lane == 0) s_red[w] = p;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tsum = 0.0;
+#pragma unroll
+    for (int i = 0; i < kSignThreads / 64; ++i) tsum += s_red[i];
+    if (tsum != 0.0) unsafeAtomicAdd(&acc[0], tsum);
+  }
+  if (last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
+    if (threadIdx.x == 0) {
+      l1_out[0] = (float)atomic_exchange_double(&acc[0], 0.0);
+      __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // DeepSqueezeSignCompressor.compress's local copy of the message
 // (deep_squeeze.py:416-422): out = (norm_s * torch.sign(x)) / numel_s -- sign(0) = 0
 // and NaN stays NaN, unlike the wire's decode (zero encodes as "+").  One float4
@@ -969,6 +1136,71 @@ CHOCO_API int choco_sign_decompress_accumulate(const int32_t* const* packed_list
 #undef CHOCO_SIGN_ACC
   profile_end("sign_accumulate", st);
   CHOCO_LAUNCHED("sign_accumulate_kernel");
+  return CHOCO_OK;
+}
+
+CHOCO_API int choco_sign_recv_gossip_compress(const int32_t* const* packed_list, const float* const* norms_list,
+                                              const float* weights, int32_t nmsg, int32_t self_slot, float* x,
+                                              float* memory, float* xhat, float gamma, int64_t n,
+                                              const int64_t* seg_off, int32_t nseg, int32_t* packed,
+                                              float* l1_norms, void* ws, size_t ws_bytes, void* stream) {
+  hipStream_t st = as_stream(stream);
+  CHOCO_REQUIRE(packed_list && norms_list && weights && x && memory && xhat && packed && l1_norms,
+                "null pointer argument");
+  CHOCO_REQUIRE(nmsg >= 1 && nmsg <= kMaxMsg, "nmsg must be in [1, %d]", kMaxMsg);
+  CHOCO_REQUIRE(self_slot >= -1 && self_slot < nmsg, "bad self_slot");
+  CHOCO_REQUIRE(n > 0 && n < (int64_t)INT32_MAX, "n out of range");
+  CHOCO_REQUIRE(nseg >= 1 && (nseg == 1 || seg_off), "need seg_off for nseg > 1");
+  CHOCO_REQUIRE(aligned16(x) && aligned16(memory) && aligned16(xhat) && aligned16(packed),
+                "x/memory/xhat/packed must be 16-byte aligned");
+  CHOCO_REQUIRE(ws && ws_bytes >= choco_sign_workspace_size(nseg), "sign workspace too small");
+  for (int q = 0; q < nmsg; ++q) {
+    CHOCO_REQUIRE(packed_list[q] && norms_list[q], "null message pointer");
+    CHOCO_REQUIRE(packed_list[q] != packed, "the output words must not alias a message being applied");
+  }
+  const bool one = nseg == 1 && n < (int64_t(1) << 30);
+  if (!one) {  // segmented layouts: the receive and the fused consensus step + pack as two kernels
+    int rc = choco_sign_decompress_accumulate(packed_list, norms_list, weights, nmsg, self_slot, n, seg_off, nseg,
+                                              self_slot >= 0 ? xhat : nullptr, memory, nullptr, 0, stream);
+    if (rc != CHOCO_OK) return rc;
+    return choco_gossip_sign_compress(x, memory, xhat, gamma, n, seg_off, nseg, packed, l1_norms, ws, ws_bytes,
+                                      stream);
+  }
+  SignMsgs M{};
+  for (int q = 0; q < nmsg; ++q) {
+    M.packed[q] = reinterpret_cast<const uint32_t*>(packed_list[q]);
+    M.norms[q] = norms_list[q];
+    M.w[q] = weights[q];
+  }
+  M.nmsg = nmsg;
+  M.self_slot = self_slot;
+  const int64_t Np = choco_sign_words(n);
+  const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
+  uint32_t* pk = reinterpret_cast<uint32_t*>(packed);
+  SignWs* w = static_cast<SignWs*>(ws);
+  profile_begin("sign_recv_pack", st);
+#define CHOCO_SIGN_RECV(NM)                                                                                     \
+  case NM:                                                                                                      \
+    if (self_slot >= 0)                                                                                         \
+      CHOCO_KLAUNCH((sign_recv_pack1_kernel<NM, true>), dim3(grid), dim3(kSignThreads), 0, st, M, x, xhat,     \
+                    memory, gamma, n, Np, pk, l1_norms, w);                                                     \
+    else                                                                                                        \
+      CHOCO_KLAUNCH((sign_recv_pack1_kernel<NM, false>), dim3(grid), dim3(kSignThreads), 0, st, M, x, xhat,    \
+                    memory, gamma, n, Np, pk, l1_norms, w);                                                     \
+    break;
+  switch (nmsg) {
+    CHOCO_SIGN_RECV(1)
+    CHOCO_SIGN_RECV(2)
+    CHOCO_SIGN_RECV(3)
+    CHOCO_SIGN_RECV(4)
+    CHOCO_SIGN_RECV(5)
+    CHOCO_SIGN_RECV(6)
+    CHOCO_SIGN_RECV(7)
+    CHOCO_SIGN_RECV(8)
+  }
+#undef CHOCO_SIGN_RECV
+  profile_end("sign_recv_pack", st);
+  CHOCO_LAUNCHED("sign_recv_pack1_kernel");
   return CHOCO_OK;
 }
 

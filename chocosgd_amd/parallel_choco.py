@@ -21,7 +21,11 @@ What changes underneath:
   * optional input key `gossip` = (memory buffer, consensus_stepsize): compress
     first applies ParallelCHOCO_V.step's update_params_from_neighbor
     (optim/utils.py:67-72) to `flatten_params` inside its own first pass
-    (utils.fused_step drives it; include/choco_codec.h "fused gossip step").
+    (utils.fused_step drives it; include/choco_codec.h "fused gossip step");
+  * optional input key `defer_receive` (QSGD, sign): uncompress keeps the received
+    messages and the NEXT compress applies them in the same pass as its consensus step
+    (include/choco_codec.h "deferred receive"); x_hat / memory lag by one step until that
+    compress or `flush_receive()` (utils.fused_step(defer_receive=True) drives it).
 """
 import inspect
 
@@ -97,6 +101,9 @@ class CHOCOCompressor(object):
     def uncompress(self, *args, **kargs):
         return self.compressor_fn.uncompress(*args, **kargs)
 
+    def flush_receive(self):
+        return self.compressor_fn.flush_receive()
+
 
 class _CHOCOBase(object):
     def __init__(self, aggregator, comm_op, comm_device, compress_ratio, quantize_level, is_biased, backend,
@@ -112,6 +119,9 @@ class _CHOCOBase(object):
         self.kargs = kargs
         # the reference binds the current stream here (parallel_choco_v.py:214-218)
         self.gossip_stream = torch.cuda.current_stream()
+        # deferred receive: (messages, weights, self slot, memory, x_hat_i, layout) that the
+        # next compress applies in its first pass (or flush_receive() applies alone)
+        self._pending = None
 
     def pipeline(self, sync_buffer, neighbor_hat_params, neighbors_info):
         with torch.cuda.stream(self.gossip_stream):
@@ -142,6 +152,35 @@ class _CHOCOBase(object):
         if out is None:
             return self.aggregator_fn._agg(message, op="get_raw_sync_data", force_wait=False)
         return self.aggregator_fn._agg(message, op="get_raw_sync_data", force_wait=False, out=out)
+
+    # deferred receive ---------------------------------------------------------
+    def _defer(self, parts, weights, self_slot, memory, xhat_self, lay):
+        if self._pending is not None:
+            raise RuntimeError("deferred receive: the previous step's messages were never applied")
+        self._pending = (parts, weights, self_slot, memory, xhat_self, lay)
+
+    def _take_pending(self, x, xh, g, lay):
+        """The pending receive if this compress can apply it in its first pass (the
+        consensus step fused, x_hat_i itself -- not a copy -- as flatten_hat_params);
+        otherwise it is applied on its own first (flush_receive), and None."""
+        pend = self._pending
+        if pend is None:
+            return None
+        parts, weights, slot, memory, xhat_self, play = pend
+        if g is None or play is not lay:
+            self.flush_receive()
+            return None
+        if g[0].data_ptr() != memory.data_ptr() or (slot >= 0 and xh.data_ptr() != xhat_self.data_ptr()):
+            raise RuntimeError("deferred receive: the next compress must take the same memory buffer and x_hat_i "
+                               "itself as flatten_hat_params (utils.fused_step(defer_receive=True))")
+        self._pending = None
+        return parts, weights, slot
+
+    def flush_receive(self):
+        """Apply a deferred receive now (before reading x_hat / memory between steps)."""
+        pend, self._pending = self._pending, None
+        if pend is not None:
+            self._apply(*pend)
 
     @staticmethod
     def _self_slot(ranks, neighbor_hat_params):
@@ -256,6 +295,8 @@ class CHOCOQuantizationCompressor(_CHOCOBase):
         x, xh, lay = self._flat_inputs(sync_buffer)
         q = int(self.quantize_level)
         g = self._gossip(sync_buffer)
+        if q == 32 or self.exchange_chunks > 1:
+            self.flush_receive()  # (never deferred on these paths)
         if q != 32 and self.exchange_chunks > 1:
             return self._compress_chunked(sync_buffer, x, xh, lay, q, g)
         sync_buffer.pop("chunked", None)
@@ -265,8 +306,18 @@ class CHOCOQuantizationCompressor(_CHOCOBase):
             message = torch.sub(x, xh).view(torch.uint8)
         else:
             message, out = codec.qsgd_wire(lay.n, q, lay.nseg, x.device)  # written in place by the kernels
-            codec.qsgd_compress(x, q, is_biased=self.is_biased, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg,
-                                seed=_draw_seed(), gossip=g, out=out)
+            pend = self._take_pending(x, xh, g, lay)
+            if pend is not None:
+                # the previous step's receive + the consensus step + the norm pass, one kernel;
+                # then the quantize pass with those norms
+                codec.qsgd_recv_gossip_norms(pend[0], pend[1], pend[2], x, g[0], xh, g[1], q,
+                                             is_biased=self.is_biased, seg_off=lay.seg_off, nseg=lay.nseg,
+                                             out=out[1])
+                codec.qsgd_compress(x, q, is_biased=self.is_biased, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg,
+                                    norm_in=out[1], seed=_draw_seed(), out=out)
+            else:
+                codec.qsgd_compress(x, q, is_biased=self.is_biased, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg,
+                                    seed=_draw_seed(), gossip=g, out=out)
         sync_buffer["flatten_updates"] = TensorBuffer.from_flat(message, [(message.numel(),)])
         # nominal bits as in parallel_choco_v.py:393
         sync_buffer["n_bits"] = get_n_bits(x) * self.quantize_level / 32
@@ -340,8 +391,13 @@ class CHOCOQuantizationCompressor(_CHOCOBase):
             return
         hb = 4 * _hdr_words(lay.nseg)
         parts = [(m[hb:], m[:hb].view(torch.float32)[:lay.nseg].contiguous()) for m in msgs]
-        codec.qsgd_accumulate(parts, weights, self_slot, lay.n, q, memory.buffer, xhat_self=xhat_self,
-                              is_biased=self.is_biased, seg_off=lay.seg_off, nseg=lay.nseg)
+        if sync_buffer.get("defer_receive"):  # applied by the next compress's first pass
+            return self._defer(parts, weights, self_slot, memory.buffer, xhat_self, lay)
+        self._apply(parts, weights, self_slot, memory.buffer, xhat_self, lay)
+
+    def _apply(self, parts, weights, self_slot, memory, xhat_self, lay):
+        codec.qsgd_accumulate(parts, weights, self_slot, lay.n, int(self.quantize_level), memory,
+                              xhat_self=xhat_self, is_biased=self.is_biased, seg_off=lay.seg_off, nseg=lay.nseg)
 
 
 class _Reassembled(dict):
@@ -409,10 +465,16 @@ class CHOCOSignCompressor(_CHOCOBase):
         g = self._gossip(sync_buffer)
         sync_buffer.pop("chunked", None)
         if self.exchange_chunks > 1:
+            self.flush_receive()  # (never deferred on this path)
             sync_buffer["chunked"] = self._pack_and_post(sync_buffer, x, xh, lay, g, message, signs, norms)
         else:
-            codec.sign_compress(x, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg, want_norms=True, gossip=g,
-                                out=(signs, norms))
+            pend = self._take_pending(x, xh, g, lay)
+            if pend is not None:  # the previous step's receive + the consensus step + the pack, one pass
+                codec.sign_recv_gossip_compress(pend[0], pend[1], pend[2], x, g[0], xh, g[1], seg_off=lay.seg_off,
+                                                nseg=lay.nseg, out=(signs, norms))
+            else:
+                codec.sign_compress(x, xhat=xh, seg_off=lay.seg_off, nseg=lay.nseg, want_norms=True, gossip=g,
+                                    out=(signs, norms))
         sync_buffer["sign_message"] = message
         sync_buffer["flatten_norms"] = TensorBuffer.from_flat(norms, [() for _ in range(lay.nseg)])
         sync_buffer["flatten_directions"] = None  # the delta is never materialised (fused)
@@ -505,5 +567,10 @@ class CHOCOSignCompressor(_CHOCOBase):
             nm = recover_device(sync_buffer["synced_flatten_norms"][r], device=dev).contiguous()
             sg = recover_device(sync_buffer["synced_signs"][r], device=dev)
             parts.append((sg, nm))
-        codec.sign_accumulate(parts, weights, self_slot, lay.n, memory.buffer, xhat_self=xhat_self,
-                              seg_off=lay.seg_off, nseg=lay.nseg)
+        if sync_buffer.get("defer_receive") and "chunked" not in sync_buffer:  # the next compress applies them
+            return self._defer(parts, weights, self_slot, memory.buffer, xhat_self, lay)
+        self._apply(parts, weights, self_slot, memory.buffer, xhat_self, lay)
+
+    def _apply(self, parts, weights, self_slot, memory, xhat_self, lay):
+        codec.sign_accumulate(parts, weights, self_slot, lay.n, memory, xhat_self=xhat_self, seg_off=lay.seg_off,
+                              nseg=lay.nseg)

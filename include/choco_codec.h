@@ -273,6 +273,22 @@ int choco_sign_decompress_accumulate(const int32_t* const* packed_list,
  * DCDSignCompressor.uncompress, dcd_psgd.py:442-446, w = 1); 1 -> target + (w * u)
  * (torch add_(w * u): DeepSqueezeSignCompressor.uncompress, deep_squeeze.py:481-488,
  * w = consensus_stepsize * (w_r - [r == self])).  u = (norms[m][s] / numel_s) * sign. */
+/* The deferred receive fused into the next step's pass (sign): the previous step's
+ * messages applied exactly as choco_sign_decompress_accumulate (x_hat += u_self, memory =
+ * fmaf(w, u, memory) in order; CHOCOSignCompressor.uncompress, parallel_choco_v.py:
+ * 548-558), then this step's consensus step x += gamma (memory - x_hat) (optim/utils.py:
+ * 67-72), then this step's message: packed signs of x - x_hat and l1_norms[s] -- ONE pass
+ * over x, x_hat and memory (nseg == 1; a segmented layout runs the receive and
+ * choco_gossip_sign_compress as two kernels).  Bit-identical x, x_hat, memory and words
+ * to that sequence.  packed must not alias a message's words (l1_norms may alias a
+ * message's norms: every workgroup reads them before the last one writes).  nmsg 1..8;
+ * ws as for choco_sign_compress. */
+int choco_sign_recv_gossip_compress(const int32_t* const* packed_list, const float* const* norms_list,
+                                    const float* weights, int32_t nmsg, int32_t self_slot, float* x,
+                                    float* memory, float* xhat, float gamma, int64_t n,
+                                    const int64_t* seg_off, int32_t nseg, int32_t* packed,
+                                    float* l1_norms, void* ws, size_t ws_bytes, void* stream);
+
 int choco_sign_decompress_axpy(const int32_t* const* packed_list, const float* const* norms_list,
                                const float* weights, int32_t nmsg, int64_t n,
                                const int64_t* seg_off, int32_t nseg, int32_t two_roundings,
@@ -337,6 +353,23 @@ int choco_qsgd_decompress_accumulate(const uint8_t* const* packed_list,
                                      int64_t n, const int64_t* seg_off, int32_t nseg,
                                      int32_t q, int32_t is_biased,
                                      float* xhat_self, float* memory, void* stream);
+
+/* The deferred receive fused into the next step's first pass (QSGD): the previous step's
+ * messages applied exactly as choco_qsgd_decompress_accumulate (x_hat += q_self, memory +=
+ * w * q in order; CHOCOQuantizationCompressor.uncompress, parallel_choco_v.py:430-433),
+ * then this step's consensus step x += gamma (memory - x_hat) (optim/utils.py:67-72), then
+ * norms_out[s] = ||x - x_hat||_2 per segment (fp64, rounded once) -- ONE pass over x,
+ * x_hat and memory instead of the decode, gossip and norm passes; bit-identical x, x_hat
+ * and memory.  Quantize this step's message afterwards with choco_qsgd_compress(...,
+ * norm_in = norms_out, ...).  Valid wherever the receive of step t-1 and the consensus
+ * step of step t are adjacent (ParallelCHOCO_V.step: apply_gradient, then the previous
+ * gossip's join, then update_params_from_neighbor).  nmsg 1..8; ws as for
+ * choco_qsgd_norms (choco_qsgd_workspace_size(nseg)). */
+int choco_qsgd_recv_gossip_norms(const uint8_t* const* packed_list, const float* const* norms_list,
+                                 const float* weights, int32_t nmsg, int32_t self_slot, float* x,
+                                 float* memory, float* xhat, float gamma, int64_t n,
+                                 const int64_t* seg_off, int32_t nseg, int32_t q, int32_t is_biased,
+                                 float* norms_out, void* ws, size_t ws_bytes, void* stream);
 
 /* ECDQuantizationCompressor.uncompress (ecd_psgd.py:415-423) for one message:
  * target = fmaf(b, decode(m), target * a)   (hat.mul_(a).add_(q, alpha=b)). */

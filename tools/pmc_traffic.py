@@ -32,6 +32,7 @@ KERNELS = {
     "randk_tile": ("randk_tile_kernel", 1.0),  # 4-B gathers: raw count (uncalibrated, like the accumulate)
     "qsgd_norm": ("qsgd_norm_kernel", 2.0),
     "qsgd_quantize": ("qsgd_quant_kernel", 2.0),
+    "qsgd_recv_norm": ("qsgd_recv_gossip_norm_kernel", 2.0),
     "qsgd_accumulate": ("qsgd_decode_kernel", 2.0),
     "sign_pack": ("sign_pack", 2.0),
     "sign_accumulate": ("sign_accumulate_kernel", 2.0),
