@@ -791,30 +791,21 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
 // to sign_accumulate_kernel + sign_pack1_kernel<.., GS>.  The column tiles are
 // sign_pack1_kernel's: lane l owns words j0+4l..+3 of every message and of the output, so
 // row r's float4 at the lane's run offset is exactly bit r of its words (no realignment).
-// Rows go in groups of 4 with two groups in flight (x, x_hat, memory of 8 rows).
-#ifndef CHOCO_SRP_RU
-#define CHOCO_SRP_RU 4
-#endif
-#ifndef CHOCO_SRP_NTS
-#define CHOCO_SRP_NTS 1
-#endif
-#ifndef CHOCO_SRP_NTL
-#define CHOCO_SRP_NTL 1
-#endif
-#ifndef CHOCO_SRP_WPE
-#define CHOCO_SRP_WPE 1
-#endif
+// Rows go in groups of 4 with two groups in flight (x, x_hat, memory of 8 rows), loads and
+// stores non-temporal.  Same-box A/B at 345M, one message (ms per step, two repeats): this
+// 1.962 / 1.970; temporal stores 2.121 / 2.108; temporal loads + stores 1.989 / 1.986;
+// 2-row groups (131 VGPRs, 3 waves) 1.995 / 2.001; 3 waves forced 1.963 / 2.009; 8-row
+// groups (1 wave) 1.927 / 1.968 -- no knob moves it: variants removed.
 template <int NM, bool HS>
-__global__ __launch_bounds__(kSignThreads) __attribute__((amdgpu_waves_per_eu(CHOCO_SRP_WPE))) void sign_recv_pack1_kernel(SignMsgs M, float* __restrict__ x,
+__global__ __launch_bounds__(kSignThreads) void sign_recv_pack1_kernel(SignMsgs M, float* __restrict__ x,
                                                                        float* __restrict__ xh,
                                                                        float* __restrict__ mem, float gamma,
                                                                        int64_t n, int64_t Np,
                                                                        uint32_t* __restrict__ packed,
                                                                        float* __restrict__ l1_out,
                                                                        SignWs* __restrict__ ws) {
-  constexpr int RU = CHOCO_SRP_RU;
+  constexpr int RU = 4;
   constexpr int NG = 32 / RU;
-  constexpr bool NTL = CHOCO_SRP_NTL, NTS = CHOCO_SRP_NTS;
   __shared__ double s_red[kSignThreads / 64];
   __shared__ unsigned int s_flag;
   double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
@@ -863,11 +854,11 @@ __global__ __launch_bounds__(kSignThreads) __attribute__((amdgpu_waves_per_eu(CH
     };
     auto load_group = [&](int g, Group& G) {
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.x[u] = ld_buf4s<NTL>(rx, voff, row_off(g * RU + u));
+      for (int u = 0; u < RU; ++u) G.x[u] = ld_buf4s<true>(rx, voff, row_off(g * RU + u));
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.h[u] = ld_buf4s<NTL>(rh, voff, row_off(g * RU + u));
+      for (int u = 0; u < RU; ++u) G.h[u] = ld_buf4s<true>(rh, voff, row_off(g * RU + u));
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.m[u] = ld_buf4s<NTL>(rm, voff, row_off(g * RU + u));
+      for (int u = 0; u < RU; ++u) G.m[u] = ld_buf4s<true>(rm, voff, row_off(g * RU + u));
     };
     auto proc_group = [&](int g, Group& G) {
 #pragma unroll
@@ -880,9 +871,9 @@ __global__ __launch_bounds__(kSignThreads) __attribute__((amdgpu_waves_per_eu(CH
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[c] = elem(r, c, xv[c], hv[c], mv[c]);
         // non-temporal: none of the three is re-read by this step
-        st_buf4s<NTS>(rx, voff, row_off(r), make_float4(xv[0], xv[1], xv[2], xv[3]));
-        st_buf4s<NTS>(rm, voff, row_off(r), make_float4(mv[0], mv[1], mv[2], mv[3]));
-        if (HS) st_buf4s<NTS>(rh, voff, row_off(r), make_float4(hv[0], hv[1], hv[2], hv[3]));
+        st_buf4s<true>(rx, voff, row_off(r), make_float4(xv[0], xv[1], xv[2], xv[3]));
+        st_buf4s<true>(rm, voff, row_off(r), make_float4(mv[0], mv[1], mv[2], mv[3]));
+        if (HS) st_buf4s<true>(rh, voff, row_off(r), make_float4(hv[0], hv[1], hv[2], hv[3]));
 #pragma unroll
         for (int c = 0; c < 4; ++c) wd[c] |= (v[c] < 0.f ? 1u : 0u) << r;
         p += ((double)fabsf(v[0]) + (double)fabsf(v[1])) + ((double)fabsf(v[2]) + (double)fabsf(v[3]));

@@ -13,13 +13,6 @@ VARIANTS = {
     "stamps": ["CHOCO_STAMPS=1"],
     # every bounded wait of the exact fallback gives up at once: tools/status_probe.py
     "poll1": ["CHOCO_POLL_BUDGET=1"],
-    # deferred sign receive (sign_recv_pack1_kernel): rows per group, nt loads / stores, waves per EU
-    "srp_nts0": ["CHOCO_SRP_NTS=0"],
-    "srp_nt00": ["CHOCO_SRP_NTS=0", "CHOCO_SRP_NTL=0"],
-    "srp_ru2": ["CHOCO_SRP_RU=2"],
-    "srp_ru2_nts0": ["CHOCO_SRP_RU=2", "CHOCO_SRP_NTS=0"],
-    "srp_wpe3": ["CHOCO_SRP_WPE=3"],
-    "srp_ru8": ["CHOCO_SRP_RU=8"],
 }
 
 
