@@ -60,8 +60,8 @@ GAMMA = 0.9  # consensus_stepsize (parameters.py:126 default)
 STAGES = {
     "topk": (["topk_bounds", "topk_stream", "topk_finish", "topk_exact", "topk_all"],
              ["sparse_accumulate"]),
-    "topk_seg": (["topk_seg_hist", "topk_seg_collect", "topk_seg_fine", "topk_seg_count", "topk_seg_emit",
-                  "topk_bounds", "topk_stream", "topk_finish"], ["sparse_accumulate"]),
+    "topk_seg": (["topk_seg_hist", "topk_seg_collect", "topk_seg_fine", "topk_seg_count", "topk_seg_bin",
+                  "topk_seg_emit", "topk_bounds", "topk_stream", "topk_finish"], ["sparse_accumulate"]),
     "randk": (["randk_count", "randk_tile"], ["sparse_accumulate"]),
     "qsgd": (["qsgd_norm", "qsgd_quantize"], ["qsgd_accumulate"]),
     "sign": (["sign_pack"], ["sign_accumulate"]),

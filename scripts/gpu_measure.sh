@@ -1,24 +1,29 @@
 # Round measurement for the workloads in $WLS: PMC FETCH/WRITE passes (-> profiles/
 # pmc_traffic.json), a rocprofv3 --kernel-trace --stats run, then the bench line (CPU
 # baseline included).  Summaries land in gpurun_out/measure/; copy what is judged
-# into profiles/.
+# into profiles/.  A workload "name+defer" runs with --defer-receive, "name+ring3" with
+# --ring3-loopback (PMC key name_ring3, bench.traffic_key).
 set -o pipefail
 cd $GRAFT_REPO_ROOT; O=gpurun_out/measure; mkdir -p $O; export TMPDIR=/tmp
-for wl in $WLS; do
-  B="bench.py --workload $wl --steps 3 --warmup 2 --no-cpu-baseline --no-e2e"
+for spec in $WLS; do
+  wl=${spec%%+*}; mode=""; [ "$spec" != "$wl" ] && mode=${spec#*+}
+  F=""; key=$wl; tag=$wl
+  [ "$mode" = defer ] && { F="--defer-receive"; tag=${wl}_deferred; }
+  [ "$mode" = ring3 ] && { F="--ring3-loopback"; key=${wl}_ring3; tag=${wl}_ring3; }
+  B="bench.py --workload $wl $F --steps 3 --warmup 2 --no-cpu-baseline --no-e2e"
   rm -rf /tmp/pf /tmp/pw
-  timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d /tmp/pf -o f -- python3 $B > $O/pmcf_$wl.log 2>&1 \
-    || { tail -5 $O/pmcf_$wl.log; exit 1; }
-  timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d /tmp/pw -o w -- python3 $B > $O/pmcw_$wl.log 2>&1 \
-    || { tail -5 $O/pmcw_$wl.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d /tmp/pf -o f -- python3 $B > $O/pmcf_$tag.log 2>&1 \
+    || { tail -5 $O/pmcf_$tag.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d /tmp/pw -o w -- python3 $B > $O/pmcw_$tag.log 2>&1 \
+    || { tail -5 $O/pmcw_$tag.log; exit 1; }
   N=$(python3 -c "import bench; print(bench.WORKLOADS['$wl'][1] if '$wl' != 'topk_r50' else 25557032)")
-  python3 tools/pmc_traffic.py /tmp/pf /tmp/pw $wl $N > $O/pmc_$wl.txt || exit 1
+  python3 tools/pmc_traffic.py /tmp/pf /tmp/pw $key $N > $O/pmc_$tag.txt || exit 1
   rm -rf /tmp/pk
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/pk -o k -- python3 bench.py --workload $wl --steps 20 \
-    --warmup 5 --no-cpu-baseline --no-e2e > $O/prof_$wl.json 2> $O/prof_$wl.err || { tail -5 $O/prof_$wl.err; exit 1; }
-  cp $(find /tmp/pk -name "*kernel_stats.csv" | head -1) $O/${R:-r03}_${wl}_kernel_stats.csv || exit 1
-  timeout -k 10 300 python3 bench.py --workload $wl > $O/bench_$wl.json 2> $O/bench_$wl.err \
-    || { tail -5 $O/bench_$wl.err; exit 1; }
-  echo "$wl done: $(python3 -c "import json; d=json.loads(open('$O/bench_$wl.json').read().splitlines()[-1]); r=d['roofline']; print(d['value'], d['ms_per_step'], r['stage'], r['frac'], r['traffic'])")"
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/pk -o k -- python3 bench.py --workload $wl $F \
+    --steps 20 --warmup 5 --no-cpu-baseline --no-e2e > $O/prof_$tag.json 2> $O/prof_$tag.err || { tail -5 $O/prof_$tag.err; exit 1; }
+  cp $(find /tmp/pk -name "*kernel_stats.csv" | head -1) $O/${R:-r05}_${tag}_kernel_stats.csv || exit 1
+  timeout -k 10 300 python3 bench.py --workload $wl $F > $O/bench_$tag.json 2> $O/bench_$tag.err \
+    || { tail -5 $O/bench_$tag.err; exit 1; }
+  echo "$tag done: $(python3 -c "import json; d=json.loads(open('$O/bench_$tag.json').read().splitlines()[-1]); r=d['roofline']; print(d['value'], d['ms_per_step'], r['stage'], r['frac'], r['traffic'])")"
 done
 cp profiles/pmc_traffic.json $O/pmc_traffic.json

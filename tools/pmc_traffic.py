@@ -26,7 +26,8 @@ KERNELS = {
     "topk_seg_collect": ("seg_collect_kernel", 2.0),
     "topk_seg_fine": ("seg_fine_kernel", 2.0),
     "topk_seg_count": ("seg_count_kernel", 2.0),
-    "topk_seg_emit": ("seg_emit_kernel", 2.0),
+    "topk_seg_bin": ("seg_bin_kernel", 2.0),
+    "topk_seg_emit": ("seg_emit", 2.0),  # seg_emit_kernel (cold) / seg_emit_w_kernel (warm)
     "sparse_accumulate": ("sparse_acc_seg_kernel", 1.0),
     "randk_count": ("randk_count_kernel", 1.0),
     "randk_tile": ("randk_tile_kernel", 1.0),  # 4-B gathers: raw count (uncalibrated, like the accumulate)
@@ -36,7 +37,8 @@ KERNELS = {
     "qsgd_accumulate": ("qsgd_decode_kernel", 2.0),
     "sign_pack": ("sign_pack", 2.0),
     "sign_accumulate": ("sign_accumulate_kernel", 2.0),
-    "gossip_step": ("gossip", 2.0),
+    "sign_recv_pack": ("sign_recv_pack1_kernel", 2.0),
+    "gossip_step": ("::gossip", 2.0),  # gossip1_kernel / gossipu_kernel (not qsgd_recv_gossip_norm_kernel)
 }
 
 
