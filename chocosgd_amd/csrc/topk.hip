@@ -281,7 +281,7 @@ CHOCO_DEV void load_sample(const float* __restrict__ x, const float* __restrict_
                            int64_t n, float4 (&s)[kSampleLoads], float4 (&h)[kSampleLoads],
                            float4 (&m)[kSampleLoads]) {
   const int64_t stride4 = ((n - 256) / (kSampleRuns - 1)) >> 2;  // float4 between run starts
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = wave_id();
   // one 1 KiB buffer resource per run (wave-uniform base): dword-aligned 16-B
   // buffer loads, so x / xh need only 4-byte alignment (unaligned segments)
 #pragma unroll
@@ -874,10 +874,13 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   if constexpr (MODE == kData) {
     // this call's window: K1's sample (cold call), the previous call's (warm call), or --
     // when the host skipped K1 but the window is stale or a warm miss put this workspace
-    // on a cold run (cold_left, set by K34) -- a sample taken here by every workgroup
+    // on a cold run (cold_left, set by K34) -- a sample taken here by every workgroup.
+    // Never with the fused gossip step (GS): the workgroups write x_new as they stream, so
+    // a workgroup that starts late could sample some x_new and derive other buckets than
+    // the rest (a wrong selection, undetected); the host runs K1 instead (launch_topk).
     bool ok = W.valid != 0u && W.n == n && W.k == k && W.shift < 32u;
     bool degenerate = false;
-    if (sample_if_cold && (!ok || cold_left != 0u)) {  // grid-uniform
+    if (!GS && sample_if_cold && (!ok || cold_left != 0u)) {  // grid-uniform
       SampleView sv{sm.u.sh, sm.scratch, sm.bc};
       bool deg;
       const Buckets sb = prologue_sample<XH, GS>(x, xh, gs, n, ranks, lane, w, sv, &deg);
@@ -1630,7 +1633,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
     int64_t idx_base, WideCtrl* __restrict__ wide, uint32_t* __restrict__ gcnt, uint32_t par,
     uint32_t* __restrict__ status, uint32_t* __restrict__ host_status, const uint32_t* __restrict__ tinfo,
-    Fold fold) {
+    Fold fold, uint32_t* __restrict__ cold_host) {
   __shared__ FinSmem fs;
   __shared__ ExactSmem es;
   __shared__ uint32_t s_tk;
@@ -1897,6 +1900,8 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     }
     ctrl->backoff = bo;
     ctrl->cold_left = cl;
+    // (the host launches K1 for fused-gossip calls on a cold run: launch_topk)
+    if (cold_host) __hip_atomic_store(cold_host, cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   STAMP(24576 + b, 2);
 }
@@ -1950,6 +1955,8 @@ static WarmClaim warm_claim(const void* ws, int64_t n, int64_t k, bool data) {
 // K34 and its exact fallback then read (x_new, xh).
 // status: where the exact fallback flags a bounded wait that gave up (the
 // workspace's own status word and host mirror, or the segmented workspace's).
+static uint32_t host_cold_left(const void* ws);
+
 template <int MODE, bool XH, bool GS = false>
 static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, uint64_t seed, float scale,
                        float* out_val, int32_t* out_idx, int64_t idx_base, void* ws, size_t ws_bytes,
@@ -2006,13 +2013,23 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   }
   const WarmClaim wc = warm_claim(ws, n, k, MODE == kData);
   const uint32_t par = wc.par;
+  // Fused gossip step: K2 cannot sample its own window (x is rewritten while it streams),
+  // so a warm call on a cold run (K34's backoff, mirrored to the host) runs K1 first.
+  uint32_t* cold_host = nullptr;
+  bool warm = wc.warm;
+  if (GS && MODE == kData) {
+    uint32_t* mir = host_status_dev(ws);
+    CHOCO_REQUIRE(mir != nullptr, "top-k: could not map the pinned host mirror of the workspace");
+    cold_host = mir + 1;
+    if (warm && host_cold_left(ws) != 0u) warm = false;
+  }
   if (MODE == kHash && !wc.known) {
     // this call's bucket totals and overflow word start from zero (K1 does it in data mode)
     CHOCO_REQUIRE(hipMemsetAsync(&ctrl->G[par][0][0], 0, sizeof(ctrl->G[par]), st) == hipSuccess &&
                       hipMemsetAsync(&ctrl->overflow[par], 0, sizeof(uint32_t), st) == hipSuccess,
                   "hipMemsetAsync failed");
   }
-  if (MODE == kData && !wc.warm) {
+  if (MODE == kData && !warm) {
     profile_begin("topk_bounds", st);
     CHOCO_KLAUNCH((topk_bounds_kernel<XH, GS>), dim3(1), dim3(kK1Threads), 0, st, x, xh, n, k, par,
                   sample_ranks(n, k), ctrl, gs);
@@ -2023,14 +2040,14 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH, GS>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, k, L.tile, L.nb,
                 par, L.side_cap, seed, hs_lo, hs_hi, ctrl, cum, cntw, side, cval, cidx,
                 reinterpret_cast<uint32_t*>(base + L.off_tinfo), gs, sample_ranks(n, k),
-                (uint32_t)(MODE == kData && wc.warm ? 1 : 0));
+                (uint32_t)(MODE == kData && warm && !GS ? 1 : 0));
   profile_end("topk_stream", st);
   CHOCO_LAUNCHED("topk_stream_kernel");
   profile_begin("topk_finish", st);
   CHOCO_KLAUNCH((topk_finish_kernel<MODE, XH>), dim3(L.nb), dim3(kK4Threads), 0, st, x, xh, n, k, L.tile, L.nb,
                 L.side_cap, seed, scale, ctrl, cum, cntw, side, cval, cidx, out_val, out_idx, idx_base,
                 reinterpret_cast<WideCtrl*>(base + L.off_wide), reinterpret_cast<uint32_t*>(base + L.off_gcnt), par,
-                status.dev, status.host, reinterpret_cast<const uint32_t*>(base + L.off_tinfo), fold);
+                status.dev, status.host, reinterpret_cast<const uint32_t*>(base + L.off_tinfo), fold, cold_host);
   profile_end("topk_finish", st);
   CHOCO_LAUNCHED("topk_finish_kernel");
   return CHOCO_OK;
@@ -2094,9 +2111,19 @@ uint32_t* host_status_dev(const void* ws) {
     return nullptr;
   }
   HostStatus hs{static_cast<uint32_t*>(h), static_cast<uint32_t*>(d)};
+  __atomic_store_n(hs.host + 1, 0u, __ATOMIC_RELEASE);  // word 1: K34's cold-run mirror (fused gossip)
   __atomic_store_n(hs.host, 0u, __ATOMIC_RELEASE);
   g_hs.emplace(ws, hs);
   return hs.dev;
+}
+
+// The cold-run length K34 mirrors to host word 1 of the workspace's mirror (fused-gossip
+// calls only; as of the last call that has completed).
+static uint32_t host_cold_left(const void* ws) {
+  std::lock_guard<std::mutex> g(g_hs_mu);
+  auto it = g_hs.find(ws);
+  if (it == g_hs.end() || it->second.host == nullptr) return 0u;
+  return __atomic_load_n(it->second.host + 1, __ATOMIC_ACQUIRE);
 }
 
 static uint32_t host_status_read(const void* ws, bool clear) {

@@ -67,9 +67,11 @@ __device__ unsigned long long g_sg_stamps[kSgStampSlots][4];
   do {                   \
   } while (0)
 #endif
-constexpr int kSegTile = 16384;                       // elements per tile
-constexpr int kSegThreads = 1024;  // threads of the tile kernels S1 / S2 (rows of float4 per thread = 4096 / threads)
-constexpr int kSegRows = kSegTile / (4 * kSegThreads);
+constexpr int kSegThreads = 1024;  // threads of the tile kernels S1 / S2
+// rows of float4 per thread.  Same-box A/B at ResNet-50 (compress us, three passes):
+// 4 rows (16384-element tiles) 40.0-40.4, 5 rows 40.0-40.4, 6 rows 42.2-42.6 (spills).
+constexpr int kSegRows = 4;
+constexpr int kSegTile = kSegRows * 4 * kSegThreads;  // elements per tile
 constexpr int kSegMaxTiles = 1024;                    // tiles per batched segment (S3: one per thread)
 constexpr int64_t kSegBatchMax = (int64_t)kSegTile * kSegMaxTiles;
 constexpr int kRow = 8;                               // plan row width (int64)
@@ -105,11 +107,13 @@ struct SegWs {
   SegWin* win;
   uint32_t* misses;     // the workspace's CHOCO_TOPK_FALLBACKS_OFFSET counter
   uint32_t* miss_flag;  // pinned host word of the cold backoff (nullable)
+  uint2* blist;         // warm: per tile, its keys in the k-th key's window bin ({key, count} x kTileList)
 };
 
 struct SegLayout {
-  size_t off_h1, off_h2, off_h3, off_info, off_cnt, off_out, off_cval, off_cidx, off_win, total;
+  size_t off_h1, off_h2, off_h3, off_info, off_cnt, off_out, off_cval, off_cidx, off_win, off_blist, total;
 };
+constexpr int kTileList = 4;  // warm: a tile's distinct keys in the k-th key's window bin kept for S4w
 
 static SegLayout seg_layout(int nseg, int64_t ntile) {
   SegLayout L{};
@@ -123,6 +127,7 @@ static SegLayout seg_layout(int nseg, int64_t ntile) {
   L.off_cval = o; o += align_up((size_t)ntile * kSegTile * 4, 256);
   L.off_cidx = o; o += align_up((size_t)ntile * kSegTile * 4, 256);
   L.off_win = o;  o += align_up((size_t)nseg * sizeof(SegWin), 256);
+  L.off_blist = o; o += align_up((size_t)ntile * kTileList * sizeof(uint2), 256);
   L.total = o;
   return L;
 }
@@ -280,6 +285,28 @@ __global__ __launch_bounds__(kSegThreads) void seg_hist_kernel(const float* __re
 // work: their k-th key moves by many ranks from call to call, so a warm window would
 // miss often.  Exclusive ranks of the set bits of `bits` in row-major order (row r,
 // wave, lane, element q) -> base[r] (+ popc of the lane's lower bits); two barriers.
+// Wave 0: exclusive scan of the NC (row, wave) counts in rc[0, NC) (row-major), the
+// total -> rc[NC]; NC <= 128 (two counts per lane above 64).
+template <int NC>
+CHOCO_DEV void wave0_scan_counts(uint32_t* rc) {
+  static_assert(NC <= 128, "two counts per lane at most");
+  const int lane = lane_id();
+  if constexpr (NC <= 64) {
+    const uint32_t cv = lane < NC ? rc[lane] : 0u;
+    const uint32_t inc = wave_incl_scan(cv);
+    if (lane < NC) rc[lane] = inc - cv;
+    if (lane == 63) rc[NC] = inc;
+  } else {
+    const int i0 = 2 * lane, i1 = 2 * lane + 1;
+    const uint32_t c0 = i0 < NC ? rc[i0] : 0u, c1 = i1 < NC ? rc[i1] : 0u;
+    const uint32_t inc = wave_incl_scan(c0 + c1);
+    const uint32_t ex = inc - (c0 + c1);
+    if (i0 < NC) rc[i0] = ex;
+    if (i1 < NC) rc[i1] = ex + c0;
+    if (lane == 63) rc[NC] = inc;
+  }
+}
+
 CHOCO_DEV void tile_ranks(const uint32_t (&bits)[kSegRows], uint32_t (&base)[kSegRows], uint32_t* rc_cnt,
                           uint32_t* total) {
   constexpr int kW = kSegThreads / 64;
@@ -292,12 +319,7 @@ CHOCO_DEV void tile_ranks(const uint32_t (&bits)[kSegRows], uint32_t (&base)[kSe
     if (lane == 63) rc_cnt[r * kW + w] = inc;
   }
   __syncthreads();
-  if (w == 0) {
-    const uint32_t cv = rc_cnt[lane];
-    const uint32_t inc = wave_incl_scan(cv);
-    rc_cnt[lane] = inc - cv;
-    if (lane == 63) rc_cnt[kSegRows * kW] = inc;
-  }
+  if (w == 0) wave0_scan_counts<kSegRows * kW>(rc_cnt);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kSegRows; ++r) base[r] += rc_cnt[r * kW + w];
@@ -404,7 +426,6 @@ __global__ __launch_bounds__(kSegThreads, kSegWpe) void seg_collect_kernel(
   __shared__ uint32_t scratch[40];
   __shared__ uint32_t bc[4];
   __shared__ uint32_t rc_cnt[kSegRows * (kSegThreads / 64) + 1];
-  static_assert(kSegRows * (kSegThreads / 64) == 64, "one wave scans the (row, wave) counts");
   const int tid = threadIdx.x;
   // `wpre`: the segment's window, read before the tile's loads were issued (warm)
   auto process = [&](const float (&v)[kSegRows][4], const TileCtx& c, int64_t tb, const SegWin& wpre) {
@@ -462,12 +483,7 @@ __global__ __launch_bounds__(kSegThreads, kSegWpe) void seg_collect_kernel(
   }
   SGSTAMP(2048 + tb, 0);
   __syncthreads();
-  if (w == 0) {  // wave 0: exclusive scan of the kSegRows * kW = 64 counts (row-major)
-    const uint32_t cv = rc_cnt[lane];
-    const uint32_t inc = wave_incl_scan(cv);
-    rc_cnt[lane] = inc - cv;
-    if (lane == 63) rc_cnt[kSegRows * kW] = inc;
-  }
+  if (w == 0) wave0_scan_counts<kSegRows * kW>(rc_cnt);  // the (row, wave) counts, row-major
   __syncthreads();
   SGSTAMP(2048 + tb, 1);
 #pragma unroll
@@ -636,18 +652,26 @@ __global__ __launch_bounds__(kS3Threads) void seg_fine_kernel(
 // 4 sqrt(k) + 8: the k-th key of a small segment moves by many ranks from one
 // call to the next), bin-rounded outward; a window wider than 2048 << kWinShMax
 // keys is centred on T instead.
+constexpr int kWinPer = kH / kS3Threads;  // hist bins per thread of seg_next_window
+CHOCO_DEV void seg_next_window_v(const uint32_t (&hv)[kWinPer], uint32_t base, uint32_t shb, uint32_t above,
+                                 uint32_t k, uint32_t T, SegWin* __restrict__ out, uint32_t* scratch);
 CHOCO_DEV void seg_next_window(const uint32_t* __restrict__ hist, uint32_t base, uint32_t shb, uint32_t above,
                                uint32_t k, uint32_t T, SegWin* __restrict__ out, uint32_t* scratch) {
-  constexpr int PER = kH / kS3Threads;
+  uint32_t hv[kWinPer];
+#pragma unroll
+  for (int j = 0; j < kWinPer; ++j) hv[j] = hist[threadIdx.x * kWinPer + j];
+  seg_next_window_v(hv, base, shb, above, k, T, out, scratch);
+}
+// the same over bins already in registers (hv[j] = bin tid * kWinPer + j)
+CHOCO_DEV void seg_next_window_v(const uint32_t (&hv)[kWinPer], uint32_t base, uint32_t shb, uint32_t above,
+                                 uint32_t k, uint32_t T, SegWin* __restrict__ out, uint32_t* scratch) {
+  constexpr int PER = kWinPer;
   const int tid = threadIdx.x;
   const uint64_t delta = (uint64_t)(0.03 * (double)k + 4.0 * sqrt((double)k)) + 8u;
   const uint64_t lo_t = (uint64_t)k + delta, hi_t = (uint64_t)k > delta ? (uint64_t)k - delta : 0u;
-  uint32_t hv[PER], local = 0;
+  uint32_t local = 0;
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    hv[j] = hist[tid * PER + j];
-    local += hv[j];
-  }
+  for (int j = 0; j < PER; ++j) local += hv[j];
   uint32_t total;
   const uint32_t pre = block_excl_scan(local, scratch, &total);
   // C(j) = #keys >= base + (j << shb) = above + total - (keys in bins below j)
@@ -749,6 +773,146 @@ __global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
   }
 }
 
+// ---------------------------------------------------------------- S3w: warm bin + list
+// Warm calls: the k-th key's window bin b2 and the rank inside it from the complete
+// hist2[s] (as S3a), then this tile's candidates ABOVE bin b2 counted and those IN bin b2
+// kept: the window's 2048 bins hold ~1-2 keys each near the k-th one, so a tile holds
+// none or one or two.  S4w takes T from those kept keys directly: no fine-histogram pass
+// over every tile's candidates (S3a) and no per-tile count against T (S3b) -- one launch
+// less.  Every load of the tile (its count, the window, its 8 bins of hist2, its first
+// 1024 candidates) goes out in ONE round trip; the kept keys go to the tile's own
+// kTileList slots as {key, 1} (no atomics) -- or, when the tile has more keys in bin b2
+// than slots (ties), as {key, count} of its distinct keys from an LDS histogram of the
+// bin's low sh bits -- and tcount[b] = {#above b2, #slots used}.  Tile 0 records the
+// window it used (info 0/1: S4w re-writes win[s] for the next call) and b2 / rank / mode
+// (info 3/4/6).  A tile with more than kTileList DISTINCT keys in bin b2 sends its
+// segment to S4w's exact select (not counted as a window miss).
+// Kept over the round-4 sequence S3a + S3b + S4 (same-box A/B, profiles/r05_ab_summary.txt).
+template <int PER>
+CHOCO_DEV void block_find_rank_v(const uint32_t (&hv)[PER], uint32_t rank, uint32_t* scratch, uint32_t* out) {
+  // block_find_rank_g over bins already in registers (hv[j] = bin tid * PER + j)
+  const int tid = threadIdx.x;
+  uint32_t local = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) local += hv[j];
+  uint32_t total;
+  const uint32_t pre = block_excl_scan(local, scratch, &total);
+  const uint32_t above = total - pre - local;
+  if (tid == 0) out[2] = total;
+  if (above < rank && rank <= above + local) {
+    uint32_t acc = above;
+#pragma unroll
+    for (int j = PER - 1; j >= 0; --j) {
+      if (acc < rank && rank <= acc + hv[j]) { out[0] = (uint32_t)(tid * PER + j); out[1] = rank - acc; }
+      acc += hv[j];
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kS3Threads) void seg_bin_kernel(
+    const int64_t* __restrict__ trows, const uint32_t* __restrict__ hist2, uint32_t* __restrict__ info,
+    const uint32_t* __restrict__ tilecnt, const float* __restrict__ cval, const SegWin* __restrict__ win,
+    uint32_t* __restrict__ tcount, uint2* __restrict__ blist) {
+  __shared__ uint32_t scratch[40];
+  __shared__ uint32_t bc[4];
+  __shared__ uint32_t h3[kH3];
+  const TileCtx c = tile_ctx_rows(trows, blockIdx.x);
+  if (c.R.ntile == 1) return;  // selected in S2
+  const int tid = threadIdx.x;
+  constexpr int PER = kH / kS3Threads;
+  constexpr int U = 4;
+  static_assert(PER == 8, "two 16-byte loads of hist2 per thread");
+  // ---- every load of the tile in one round trip
+  const uint32_t cnt = tilecnt[blockIdx.x];
+  const SegWin w = win[c.s];
+  uint32_t hv[PER];
+  {
+    const uint4* h4 = reinterpret_cast<const uint4*>(hist2 + (int64_t)c.s * kH + tid * PER);
+    const uint4 a = h4[0], b = h4[1];
+    hv[0] = a.x; hv[1] = a.y; hv[2] = a.z; hv[3] = a.w; hv[4] = b.x; hv[5] = b.y; hv[6] = b.z; hv[7] = b.w;
+  }
+  float cv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) cv[u] = cval[c.slot + u * kS3Threads + tid];  // (inside the tile's slots; masked below)
+  if (tid < 4) bc[tid] = 0u;
+  __syncthreads();
+  const uint32_t lo = w.lo, sh = min(w.sh, kWinShMax);
+  const uint32_t rank = (uint32_t)c.R.k;
+  block_find_rank_v<PER>(hv, rank, scratch, bc);
+  const uint32_t b2 = bc[0];
+  uint32_t mode = kSegSelect;
+  if (c.R.k >= c.R.len) mode = kSegAll;
+  else if (!w.valid || bc[2] < rank || b2 == (uint32_t)(kH - 1)) mode = kSegMissed;  // T below the window or in its clamped top
+  if (c.j == 0 && tid == 0) {
+    info[8 * c.s + 0] = lo;
+    info[8 * c.s + 1] = sh;
+    info[8 * c.s + 3] = b2;
+    info[8 * c.s + 4] = bc[1];  // rank of the k-th key inside bin b2
+    info[8 * c.s + 6] = mode;
+  }
+  uint32_t gt = 0, nin = 0;
+  if (mode == kSegSelect) {  // workgroup-uniform
+    uint2* __restrict__ L = blist + (int64_t)blockIdx.x * kTileList;
+    for (uint32_t i0 = 0; i0 < cnt; i0 += U * kS3Threads) {  // workgroup-uniform
+      uint32_t key[U], inb = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = i0 + u * kS3Threads + tid;
+        key[u] = i0 == 0 ? fkey(cv[u]) : (i < cnt ? fkey(cval[c.slot + i]) : 0u);
+        const uint32_t bin = min((key[u] - lo) >> sh, (uint32_t)(kH - 1));  // (every candidate has key >= lo)
+        gt += (i < cnt && bin > b2) ? 1u : 0u;
+        inb |= (i < cnt && bin == b2) ? (1u << u) : 0u;
+      }
+      uint32_t nb;
+      uint32_t pos = nin + block_excl_scan((uint32_t)__popc(inb), scratch, &nb);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if ((inb >> u) & 1u) {
+          if (pos < (uint32_t)kTileList) L[pos] = make_uint2(key[u], 1u);
+          ++pos;
+        }
+      }
+      nin += nb;
+    }
+    if (nin > (uint32_t)kTileList) {  // workgroup-uniform (ties): {key, count} of the distinct keys
+      const uint32_t fmask = (1u << sh) - 1u;
+      for (int i = tid; i < kH3; i += kS3Threads) h3[i] = 0u;
+      __syncthreads();
+      for (uint32_t i = tid; i < cnt; i += kS3Threads) {
+        const uint32_t key = fkey(cval[c.slot + i]);
+        if (min((key - lo) >> sh, (uint32_t)(kH - 1)) == b2) atomicAdd(&h3[(key - lo) & fmask], 1u);
+      }
+      __syncthreads();
+      constexpr int P3 = kH3 / kS3Threads;
+      uint32_t hc[P3], nz = 0;
+#pragma unroll
+      for (int q = 0; q < P3; ++q) {
+        hc[q] = h3[tid * P3 + q];
+        nz += hc[q] ? 1u : 0u;
+      }
+      uint32_t nd;
+      uint32_t pos = block_excl_scan(nz, scratch, &nd);
+#pragma unroll
+      for (int q = 0; q < P3; ++q) {
+        if (hc[q]) {
+          if (pos < (uint32_t)kTileList) L[pos] = make_uint2(lo + (b2 << sh) + (uint32_t)(tid * P3 + q), hc[q]);
+          ++pos;
+        }
+      }
+      nin = nd;  // > kTileList: more distinct keys than slots (S4w selects the segment exactly)
+    }
+  } else if (mode == kSegAll) {
+    gt = tid == 0 ? cnt : 0u;
+  }
+  uint32_t gtot;
+  block_excl_scan(gt, scratch, &gtot);
+  if (tid == 0) {  // {#candidates above bin b2 (kSegAll: all of them), #slots used}
+    tcount[2 * blockIdx.x] = gtot;
+    tcount[2 * blockIdx.x + 1] = nin;
+  }
+}
+
 // ---------------------------------------------------------------- S4: ordered emission
 // The tile's output offset and tie share from the counts of the segment's
 // earlier tiles (<= kSegMaxTiles - 1: kS4Per per thread), then the ordered
@@ -842,6 +1006,201 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
   }
 }
 
+// S4w (warm, after S3w): every tile's (#above b2, #in b2) counts and kept keys of its
+// segment are loaded in one round trip (with the tile's first 256 candidates), T is taken
+// from the kept keys -- histogrammed by their low sh bits in LDS (bins of one key), the
+// rank inside bin b2 located -- and the tile's offset is the earlier tiles' counts above
+// b2 plus their kept keys above / at T; then the ordered emission as S4.  One extra
+// workgroup per segment (the first nseg of the grid, so they start first) derives the
+// same T and writes the next call's window from hist2, then zeroes hist2 (every S3w tile
+// has read it) -- off the tiles' chains.  Missed windows and tie overflows: tile 0
+// selects the segment exactly.
+template <bool XH>
+__global__ __launch_bounds__(kS4Threads) void seg_emit_w_kernel(
+    const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ plan,
+    const int64_t* __restrict__ trows, uint32_t nseg, const uint32_t* __restrict__ info,
+    const uint32_t* __restrict__ tilecnt, const uint32_t* __restrict__ tcount, uint32_t* __restrict__ hist2,
+    const float* __restrict__ cval, const uint32_t* __restrict__ cidx, float* __restrict__ out_val,
+    int32_t* __restrict__ out_idx, SegWin* __restrict__ win, uint32_t* __restrict__ misses,
+    uint32_t* __restrict__ miss_flag, const uint2* __restrict__ blist) {
+  __shared__ uint32_t scratch[40];
+  __shared__ uint32_t h3[kH3];
+  __shared__ uint32_t bc[4];
+  __shared__ uint32_t s_ovf, s_me;
+  __shared__ ExactSmem es;
+  const int tid = threadIdx.x;
+  const bool segwg = blockIdx.x < nseg;  // workgroup-uniform: a segment's window workgroup
+  const int64_t b = (int64_t)blockIdx.x - nseg;  // the tile (tile workgroups)
+  TileCtx c;
+  if (segwg) {
+    c.s = (int)blockIdx.x;
+    c.R = seg_row(plan, c.s);
+    if (c.R.ntile <= 1) return;  // single-tile (selected in S2) or flat-pipeline segment
+    c.j = -1;
+    c.slot = 0;
+    c.start = c.R.off;
+    c.tl = 0;
+  } else {
+    c = tile_ctx_rows(trows, b);
+    if (c.R.ntile == 1) return;  // selected in S2
+  }
+  // ---- one round trip: the segment's info, every tile's counts and kept keys, this
+  // tile's count and first 256 candidates
+  const uint32_t* I = info + 8 * c.s;
+  const uint32_t mode = I[6];
+  const uint32_t lo = I[0], sh = I[1], b2 = I[3], rb = I[4];
+  uint32_t tg[kS4Per], tn[kS4Per];
+  uint2 kk[kS4Per][kTileList];  // {key, count}
+#pragma unroll
+  for (int q = 0; q < kS4Per; ++q) {
+    const int t = q * kS4Threads + tid;
+    tg[q] = tn[q] = 0u;
+#pragma unroll
+    for (int i = 0; i < kTileList; ++i) kk[q][i] = make_uint2(0u, 0u);
+    if (t < c.R.ntile) {
+      const int64_t tb = c.R.t0 + t;
+      const uint2 p = reinterpret_cast<const uint2*>(tcount)[tb];
+      tg[q] = p.x;
+      tn[q] = p.y;
+      const uint4* k4 = reinterpret_cast<const uint4*>(blist + tb * kTileList);
+      static_assert(kTileList == 4, "two 16-byte loads of kept keys per tile");
+      const uint4 a = k4[0], b = k4[1];
+      kk[q][0] = make_uint2(a.x, a.y); kk[q][1] = make_uint2(a.z, a.w);
+      kk[q][2] = make_uint2(b.x, b.y); kk[q][3] = make_uint2(b.z, b.w);
+    }
+  }
+  const uint32_t cnt = segwg ? 0u : tilecnt[b];
+  float v0 = 0.f;
+  uint32_t ix0 = 0u;
+  uint32_t hv[kWinPer] = {};  // (segment workgroups: hist2 for the next window, in the same trip)
+  uint32_t* __restrict__ g2 = hist2 + (int64_t)c.s * kH;
+  if (!segwg) {
+    v0 = cval[c.slot + tid];  // (inside the tile's slots; masked by cnt below)
+    ix0 = cidx[c.slot + tid];
+  } else {
+    static_assert(kWinPer == 8, "two 16-byte loads of hist2 per thread");
+    const uint4* h4 = reinterpret_cast<const uint4*>(g2 + tid * kWinPer);
+    const uint4 a = h4[0], bb = h4[1];
+    hv[0] = a.x; hv[1] = a.y; hv[2] = a.z; hv[3] = a.w; hv[4] = bb.x; hv[5] = bb.y; hv[6] = bb.z; hv[7] = bb.w;
+  }
+  bool ovf = false;
+#pragma unroll
+  for (int q = 0; q < kS4Per; ++q) ovf |= tn[q] > (uint32_t)kTileList;
+  // (one barrier for the overflow flag, the LDS histogram's reset and bc)
+  if (tid == 0) s_ovf = 0u;
+  for (int i = tid; i < kH3; i += kS4Threads) h3[i] = 0u;
+  if (tid < 4) bc[tid] = 0u;
+  __syncthreads();
+  if (ovf) s_ovf = 1u;
+  __syncthreads();
+  const bool overflow = mode == kSegSelect && s_ovf != 0u;
+  if (mode == kSegMissed || overflow) {  // workgroup-uniform: tile 0 selects the segment exactly
+    if (c.j != 0) return;
+    if (tid == 0 && mode == kSegMissed) {
+      atomicAdd(misses, 1u);
+      if (miss_flag) __hip_atomic_store(miss_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    Src<kData, XH> src{x + c.R.off, XH ? xh + c.R.off : nullptr, 0};
+    block_select_T(src, c.R.len, c.R.k, es);
+    const uint32_t T = es.bc[0], r = es.bc[1], ties = es.bc[2];
+    __syncthreads();
+    block_emit(src, c.R.len, T, r, ties, 1.0f, out_val + c.R.out_off, out_idx + c.R.out_off, c.R.off, es);
+    if (overflow) {  // the window held T: the next one from this call's hist2, as usual
+      seg_next_window(g2, lo, sh, 0u, (uint32_t)c.R.k, T, &win[c.s], scratch);
+      __syncthreads();
+    } else if (tid == 0) {  // re-centred on T
+      win[c.s] = SegWin{T > (1u << 18) ? T - (1u << 18) : 0u, kWinShMax, 1u, 0u};
+    }
+    for (int i = tid; i < kH; i += kS4Threads) g2[i] = 0u;
+    return;
+  }
+  // ---- T and the ties at it to take, from the kept keys (mode kSegAll: every candidate)
+  uint32_t T = 0, r = 0;
+  if (mode == kSegSelect) {  // workgroup-uniform
+    const uint32_t fmask = (1u << sh) - 1u;
+#pragma unroll
+    for (int q = 0; q < kS4Per; ++q)
+#pragma unroll
+      for (int i = 0; i < kTileList; ++i)
+        if ((uint32_t)i < tn[q]) atomicAdd(&h3[(kk[q][i].x - lo) & fmask], kk[q][i].y);
+    __syncthreads();
+    block_find_rank_g<kH3 / kS4Threads>(h3, rb, scratch, bc);
+    T = lo + (b2 << sh) + bc[0];
+    r = bc[1];
+  }
+  if (segwg) {  // the next call's window (this call's hist2: the window's own bins), then hist2 reset
+    if (mode == kSegSelect) {
+      seg_next_window_v(hv, lo, sh, 0u, (uint32_t)c.R.k, T, &win[c.s], scratch);
+      __syncthreads();
+    } else if (tid == 0) {
+      win[c.s] = SegWin{0u, kWinShMax, 1u, 0u};
+    }
+    for (int i = tid; i < kH; i += kS4Threads) g2[i] = 0u;
+    return;
+  }
+  // ---- offsets: the earlier tiles' candidates above bin b2 and their kept keys above / at
+  // T; this tile's kept keys at T (its ties)
+  uint32_t g = 0u, le = 0u;
+#pragma unroll
+  for (int q = 0; q < kS4Per; ++q) {
+    const int t = q * kS4Threads + tid;
+    uint32_t above = 0u, at = 0u;
+    if (mode == kSegSelect) {
+#pragma unroll
+      for (int i = 0; i < kTileList; ++i) {
+        above += ((uint32_t)i < tn[q] && kk[q][i].x > T) ? kk[q][i].y : 0u;
+        at += ((uint32_t)i < tn[q] && kk[q][i].x == T) ? kk[q][i].y : 0u;
+      }
+    }
+    if (t < c.j) {
+      g += tg[q] + above;
+      le += at;
+    } else if (t == c.j) {
+      s_me = at;  // (one thread; read after the scan's barriers)
+    }
+  }
+  uint32_t gp, ep, gsum, lesum;
+  block_excl_scan2(g, le, scratch, &gp, &ep, &gsum, &lesum);
+  const uint32_t mesum = s_me;
+  const uint32_t taken = min(r, lesum);  // ties taken by earlier tiles (lowest index first)
+  const uint32_t o = gsum + taken;
+  const uint32_t quota = min(mesum, r - taken);
+  const bool all_ties = quota == mesum;
+  float* __restrict__ ov = out_val + c.R.out_off + o;
+  int32_t* __restrict__ oi = out_idx + c.R.out_off + o;
+  const uint32_t room = (uint32_t)c.R.k - min(o, (uint32_t)c.R.k);  // (bounded: never past the segment's k)
+  uint32_t run = 0, tie_run = 0;
+  for (uint32_t p0 = 0; p0 < cnt; p0 += kS4Threads) {  // workgroup-uniform
+    const uint32_t p = p0 + tid;
+    const bool valid = p < cnt;
+    const float v = p0 == 0 ? v0 : (valid ? cval[c.slot + p] : 0.f);
+    const uint32_t ix = p0 == 0 ? ix0 : (valid ? cidx[c.slot + p] : 0u);
+    const uint32_t key = fkey(v);
+    const bool gt = valid && (mode == kSegAll || key > T), eq = valid && mode != kSegAll && key == T;
+    bool sel;
+    if (all_ties || quota == 0u) {
+      sel = gt || (eq && all_ties);
+    } else {
+      uint32_t ntie;
+      const uint32_t trank = tie_run + block_excl_scan(eq ? 1u : 0u, scratch, &ntie);
+      sel = gt || (eq && trank < quota);
+      tie_run += ntie;
+    }
+    uint32_t nsel;
+    const uint32_t pos = run + block_excl_scan(sel ? 1u : 0u, scratch, &nsel);
+    if (sel && pos < room) {
+      ov[pos] = v;
+      oi[pos] = (int32_t)ix;
+    }
+    run += nsel;
+  }
+}
+
+#ifndef CHOCO_SEG_W3
+#define CHOCO_SEG_W3 1
+#endif
+constexpr bool kSegW3 = CHOCO_SEG_W3 != 0;
+
 // ---------------------------------------------------------------- host side
 static int64_t plan_tiles(const int64_t* plan_host) { return plan_host[6]; }
 static int64_t plan_batched(const int64_t* plan_host) { return plan_host[7]; }
@@ -930,6 +1289,20 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
   }
   profile_end("topk_seg_collect", st);
   CHOCO_LAUNCHED("seg_collect_kernel");
+  if (warm && kSegW3) {
+    profile_begin("topk_seg_bin", st);
+    CHOCO_KLAUNCH(seg_bin_kernel, dim3(ntile), dim3(kS3Threads), 0, st, trows, W.hist2, W.info, W.tilecnt, W.cval,
+                  W.win, W.tcount, W.blist);
+    profile_end("topk_seg_bin", st);
+    CHOCO_LAUNCHED("seg_bin_kernel");
+    profile_begin("topk_seg_emit", st);
+    CHOCO_KLAUNCH((seg_emit_w_kernel<XH>), dim3(ntile + (unsigned)nseg), dim3(kS4Threads), 0, st, x, xh, plan_dev,
+                  trows, (uint32_t)nseg, W.info, W.tilecnt, W.tcount, W.hist2, W.cval, W.cidx, out_val, out_idx, W.win, W.misses,
+                  W.miss_flag, W.blist);
+    profile_end("topk_seg_emit", st);
+    CHOCO_LAUNCHED("seg_emit_w_kernel");
+    return CHOCO_OK;
+  }
   profile_begin("topk_seg_fine", st);
   if (warm)
     CHOCO_KLAUNCH((seg_fine_kernel<true>), dim3(ntile), dim3(kS3Threads), 0, st, trows, nseg, W.hist1, W.hist2,
@@ -993,7 +1366,8 @@ static int segmented(const float* x, const float* xhat, const int64_t* plan_dev,
             reinterpret_cast<uint32_t*>(base + L.off_info), reinterpret_cast<uint32_t*>(base + L.off_cnt),
             reinterpret_cast<uint32_t*>(base + L.off_out), reinterpret_cast<float*>(base + L.off_cval),
             reinterpret_cast<uint32_t*>(base + L.off_cidx), reinterpret_cast<SegWin*>(base + L.off_win),
-            reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_FALLBACKS_OFFSET), nullptr};
+            reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_FALLBACKS_OFFSET), nullptr,
+            reinterpret_cast<uint2*>(base + L.off_blist)};
     const bool warm = seg_claim_warm(base + L.off_win, &W.miss_flag);
     int rc;
     if (gs.mem)

@@ -605,3 +605,21 @@ def test_topk_segmented_gossip_warm_sequence():
         assert np.array_equal(host(idx).astype(np.int64), oi)
         assert same_bits(host(vals), ov)
         codec.sparse_accumulate(vals, idx, mem, 1.0, xhat_self=hat)
+
+
+def test_topk_segmented_warm_bin_list_overflow():
+    """Warm calls on tie-heavy tensors (values on a 1/8 grid): the k-th key's window bin holds
+    thousands of equal keys, more than the bin list takes (topk_seg.hip kListCap), so the
+    segment is selected exactly in S4w -- every call exact, and not counted as a window
+    miss (the window itself holds T)."""
+    from chocosgd_amd import codec
+    lens = [1_000_000, 500_000, 40_000, 33]
+    n = sum(lens)
+    plan = codec.SegmentPlan(lens, 0.99, torch.device(DEV))
+    counts = []
+    for step in range(5):
+        g = torch.Generator(device=DEV).manual_seed(560 + step)
+        x = torch.round(torch.randn(n, generator=g, device=DEV) * 8) / 8
+        _check_seg(x, plan, lens, 0.99)
+        counts.append(codec.topk_fallback_count(plan=plan))
+    assert counts[-1] == counts[1], counts

@@ -13,11 +13,10 @@ VARIANTS = {
     "stamps": ["CHOCO_STAMPS=1"],
     # every bounded wait of the exact fallback gives up at once: tools/status_probe.py
     "poll1": ["CHOCO_POLL_BUDGET=1"],
-    # segmented top-k tiles of 5 / 6 rows of float4 per thread (20480 / 24576 elements)
-    "seg5": ["CHOCO_SEG_ROWS=5"],
-    "seg6": ["CHOCO_SEG_ROWS=6"],
     # warm segmented tail: S3a + S3b + S4 (the round-4 sequence) instead of S3w + S4w
     "segw0": ["CHOCO_SEG_W3=0"],
+    # the sign packs' row offsets as a VGPR-derived scalar offset (round 4): readfirstlane loops
+    "sgn_old": ["CHOCO_SIGN_OLD_ROWS=1"],
 }
 
 
