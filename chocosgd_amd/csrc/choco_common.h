@@ -138,10 +138,6 @@ CHOCO_DEV float4 sub4(float4 a, float4 b) { return make_float4(a.x - b.x, a.y - 
 int gossip_launch(float* x, const float* mem, const float* xh, float gamma, int64_t n, hipStream_t st);
 
 CHOCO_DEV int lane_id() { return __lane_id(); }
-// The wave's index in the workgroup as a wave-uniform (SGPR) value: offsets derived from
-// it can be a buffer instruction's scalar soffset (threadIdx.x >> 6 alone is a VGPR to the
-// compiler, which then wraps every such buffer access in a readfirstlane loop).
-CHOCO_DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 // number of set bits of `mask` strictly below this lane
 CHOCO_DEV uint32_t mask_prefix(uint64_t mask) {

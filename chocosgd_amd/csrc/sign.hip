@@ -29,13 +29,6 @@
 
 namespace choco {
 
-#if CHOCO_SIGN_OLD_ROWS  // (A/B only: round 4's row offsets, a VGPR-derived scalar offset per buffer access)
-#define SROW(voff, ro) voff, ro
-#define SIGN_WAVE() ((int)(threadIdx.x >> 6))
-#else  // the row offset in the VGPR offset: no readfirstlane loop around each access
-#define SROW(voff, ro) (voff) + (ro), 0u
-#define SIGN_WAVE() wave_id()
-#endif
 constexpr int kSignThreads = 256;
 constexpr int kSignCols = 1024;  // words per workgroup
 
@@ -158,7 +151,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
   __shared__ double s_rows[kSignThreads / 64][32];
   __shared__ unsigned int s_flag;
   double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
-  const int lane = lane_id(), w = SIGN_WAVE();
+  const int lane = lane_id(), w = threadIdx.x >> 6;
   const int64_t J0 = (blk0 + (int64_t)blockIdx.x) * kSignCols;
   const int64_t j0 = J0 + 256 * w;
   const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
@@ -343,7 +336,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
   __shared__ double s_red[kSignThreads / 64];
   __shared__ unsigned int s_flag;
   double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
-  const int lane = lane_id(), w = SIGN_WAVE();
+  const int lane = lane_id(), w = threadIdx.x >> 6;
   const int64_t j0 = (blk0 + (int64_t)blockIdx.x) * kSignCols + 256 * w;
   const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
   // every row run of the wave (row 31's last float4 included) lies inside [0, n)
@@ -361,14 +354,14 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
   };
   auto load_group = [&](int g, Group& G) {
 #pragma unroll
-    for (int u = 0; u < RU; ++u) G.x[u] = ld_buf4s<true>(rx, SROW(voff, row_off(g * RU + u)));
+    for (int u = 0; u < RU; ++u) G.x[u] = ld_buf4s<true>(rx, voff, row_off(g * RU + u));
     if (XH) {
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.h[u] = ld_buf4s<true>(rh, SROW(voff, row_off(g * RU + u)));
+      for (int u = 0; u < RU; ++u) G.h[u] = ld_buf4s<true>(rh, voff, row_off(g * RU + u));
     }
     if (GS) {
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.m[u] = ld_buf4s<true>(rm, SROW(voff, row_off(g * RU + u)));
+      for (int u = 0; u < RU; ++u) G.m[u] = ld_buf4s<true>(rm, voff, row_off(g * RU + u));
     }
   };
   uint32_t wd[4] = {0u, 0u, 0u, 0u};
@@ -380,7 +373,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
         G.x[u] = gossip4(G.x[u], G.m[u], G.h[u], gs.gamma);
         // non-temporal: x_new is not re-read by this step, and dirty Infinity-Cache
         // lines would be written back in the middle of the receiver's pass
-        st_buf4s<true>(rx, SROW(voff, row_off(g * RU + u)), G.x[u]);
+        st_buf4s<true>(rx, voff, row_off(g * RU + u), G.x[u]);
       }
     }
 #pragma unroll
@@ -465,7 +458,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
 __global__ __launch_bounds__(kSignThreads) void sign_unpack_kernel(const uint32_t* __restrict__ packed,
                                                                    int64_t n, int64_t Np,
                                                                    float* __restrict__ out) {
-  const int lane = lane_id(), w = SIGN_WAVE();
+  const int lane = lane_id(), w = threadIdx.x >> 6;
   const int64_t j0 = (int64_t)blockIdx.x * kSignCols + 256 * w;
   const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
   if (ncol == 0) return;
@@ -569,7 +562,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
                                                                        float* __restrict__ mem) {
   __shared__ int s_lo[32], s_hi[32];
   __shared__ float s_sc[kMaxMsg][32];
-  const int lane = lane_id(), w = SIGN_WAVE();
+  const int lane = lane_id(), w = threadIdx.x >> 6;
   int64_t cb;
   int rb;
   sign_acc_block(blockIdx.x, cb, rb);
@@ -816,7 +809,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_recv_pack1_kernel(SignMsgs 
   __shared__ double s_red[kSignThreads / 64];
   __shared__ unsigned int s_flag;
   double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
-  const int lane = lane_id(), w = SIGN_WAVE();
+  const int lane = lane_id(), w = threadIdx.x >> 6;
   const int64_t j0 = (int64_t)blockIdx.x * kSignCols + 256 * w;
   const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
   const bool interior = ncol == 256 && (int64_t)31 * Np + j0 + 256 <= n;
@@ -861,11 +854,11 @@ __global__ __launch_bounds__(kSignThreads) void sign_recv_pack1_kernel(SignMsgs 
     };
     auto load_group = [&](int g, Group& G) {
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.x[u] = ld_buf4s<true>(rx, SROW(voff, row_off(g * RU + u)));
+      for (int u = 0; u < RU; ++u) G.x[u] = ld_buf4s<true>(rx, voff, row_off(g * RU + u));
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.h[u] = ld_buf4s<true>(rh, SROW(voff, row_off(g * RU + u)));
+      for (int u = 0; u < RU; ++u) G.h[u] = ld_buf4s<true>(rh, voff, row_off(g * RU + u));
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.m[u] = ld_buf4s<true>(rm, SROW(voff, row_off(g * RU + u)));
+      for (int u = 0; u < RU; ++u) G.m[u] = ld_buf4s<true>(rm, voff, row_off(g * RU + u));
     };
     auto proc_group = [&](int g, Group& G) {
 #pragma unroll
@@ -878,9 +871,9 @@ __global__ __launch_bounds__(kSignThreads) void sign_recv_pack1_kernel(SignMsgs 
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[c] = elem(r, c, xv[c], hv[c], mv[c]);
         // non-temporal: none of the three is re-read by this step
-        st_buf4s<true>(rx, SROW(voff, row_off(r)), make_float4(xv[0], xv[1], xv[2], xv[3]));
-        st_buf4s<true>(rm, SROW(voff, row_off(r)), make_float4(mv[0], mv[1], mv[2], mv[3]));
-        if (HS) st_buf4s<true>(rh, SROW(voff, row_off(r)), make_float4(hv[0], hv[1], hv[2], hv[3]));
+        st_buf4s<true>(rx, voff, row_off(r), make_float4(xv[0], xv[1], xv[2], xv[3]));
+        st_buf4s<true>(rm, voff, row_off(r), make_float4(mv[0], mv[1], mv[2], mv[3]));
+        if (HS) st_buf4s<true>(rh, voff, row_off(r), make_float4(hv[0], hv[1], hv[2], hv[3]));
 #pragma unroll
         for (int c = 0; c < 4; ++c) wd[c] |= (v[c] < 0.f ? 1u : 0u) << r;
         p += ((double)fabsf(v[0]) + (double)fabsf(v[1])) + ((double)fabsf(v[2]) + (double)fabsf(v[3]));

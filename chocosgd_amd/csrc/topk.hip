@@ -281,7 +281,7 @@ CHOCO_DEV void load_sample(const float* __restrict__ x, const float* __restrict_
                            int64_t n, float4 (&s)[kSampleLoads], float4 (&h)[kSampleLoads],
                            float4 (&m)[kSampleLoads]) {
   const int64_t stride4 = ((n - 256) / (kSampleRuns - 1)) >> 2;  // float4 between run starts
-  const int lane = threadIdx.x & 63, w = wave_id();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   // one 1 KiB buffer resource per run (wave-uniform base): dword-aligned 16-B
   // buffer loads, so x / xh need only 4-byte alignment (unaligned segments)
 #pragma unroll

@@ -15,8 +15,6 @@ VARIANTS = {
     "poll1": ["CHOCO_POLL_BUDGET=1"],
     # warm segmented tail: S3a + S3b + S4 (the round-4 sequence) instead of S3w + S4w
     "segw0": ["CHOCO_SEG_W3=0"],
-    # the sign packs' row offsets as a VGPR-derived scalar offset (round 4): readfirstlane loops
-    "sgn_old": ["CHOCO_SIGN_OLD_ROWS=1"],
 }
 
 
