@@ -26,17 +26,20 @@
 //                     #== T_s); tile 0 of the segment writes the NEXT call's window.
 //   S4 seg_emit     : offset and tie share from the segment's earlier tiles, then
 //                     the ordered compaction of the tile's candidates.
-// WARM (four launches, ONE read): each segment carries a window [lo_s, lo_s +
+// WARM (three launches, ONE read): each segment carries a window [lo_s, lo_s +
 // 2048 << sh_s) from the previous call (around that call's T_s, margins at
 // k_s (1 +- m_s) keys), so
 //   W2 seg_collect  : candidates key >= lo_s, compacted; their window bin
 //                     min((key - lo_s) >> sh_s, 2047) -> hist2[s]  (no S1);
-//   S3a / S3b / S4  : as above with (window bin, low sh_s bits) in place of
-//                     (b2, bits 8..0).  A segment whose T_s is not inside its
-//                     window (fewer than k_s candidates, or T_s in the clamped
-//                     top bin) is flagged in S3a and selected exactly by ONE
-//                     workgroup in S4 (slow, correct), which also re-centres its
-//                     window; k_s >= len_s segments take every element.
+//   S3w seg_bin     : the k_s-th key's window bin b2 from hist2[s]; the tile's
+//                     count above b2 and its (few) keys IN b2, kept per tile;
+//   S4w seg_emit_w  : T_s from the kept keys, offsets, ordered compaction; one
+//                     workgroup per segment writes the next call's window.
+//                     A segment whose T_s is not inside its window (fewer than
+//                     k_s candidates, or T_s in the clamped top bin) is flagged
+//                     in S3w and selected exactly by ONE workgroup in S4w (slow,
+//                     correct), which also re-centres its window; k_s >= len_s
+//                     segments take every element.
 // Every histogram is reset by the first tile of its segment in the launch after
 // its last reader.  Segments over 16M elements take the flat pipeline (topk.hip),
 // each in its own workspace (its own warm window).
@@ -580,11 +583,11 @@ CHOCO_DEV void block_find_rank_g(const uint32_t* __restrict__ hist, uint32_t ran
   __syncthreads();
 }
 
-template <bool WARM>
+// (cold calls; warm calls take S3w + S4w below)
 __global__ __launch_bounds__(kS3Threads) void seg_fine_kernel(
     const int64_t* __restrict__ trows, int nseg, uint32_t* __restrict__ hist1, const uint32_t* __restrict__ hist2,
     uint32_t* __restrict__ hist3, uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt,
-    const float* __restrict__ cval, const SegWin* __restrict__ win) {
+    const float* __restrict__ cval) {
   __shared__ uint32_t h3[kH3];
   __shared__ uint32_t scratch[40];
   __shared__ uint32_t bc[4];
@@ -595,35 +598,18 @@ __global__ __launch_bounds__(kS3Threads) void seg_fine_kernel(
   for (int i = tid; i < kH3; i += kS3Threads) h3[i] = 0u;
   if (tid < 4) bc[tid] = 0u;
   __syncthreads();
-  uint32_t lo = 0, sh = 0, b1 = 0;
-  uint32_t rank;
-  if (WARM) {
-    const SegWin w = win[c.s];
-    lo = w.lo;
-    sh = min(w.sh, kWinShMax);
-    rank = (uint32_t)c.R.k;
-  } else {
-    b1 = info[8 * c.s + 0];
-    rank = info[8 * c.s + 1];
-  }
+  const uint32_t b1 = info[8 * c.s + 0], rank = info[8 * c.s + 1];
   block_find_rank_g<kH / kS3Threads>(hist2 + (int64_t)c.s * kH, rank, scratch, bc);
   const uint32_t b2 = bc[0];
-  uint32_t mode = kSegSelect;
-  if (WARM) {
-    if (c.R.k >= c.R.len) mode = kSegAll;
-    else if (bc[2] < rank || b2 == (uint32_t)(kH - 1)) mode = kSegMissed;  // T below the window or in its clamped top
-  }
   if (c.j == 0 && tid == 0) {
     info[8 * c.s + 3] = b2;
     info[8 * c.s + 4] = bc[1];  // rank of the k-th key inside that bin
-    info[8 * c.s + 6] = mode;
   }
-  if (!WARM && c.j == 0) {  // every tile of the segment read hist1 in S2: reset it for the next call
+  if (c.j == 0) {  // every tile of the segment read hist1 in S2: reset it for the next call
     uint32_t* __restrict__ g1 = hist1 + (int64_t)c.s * kH;
     for (int i = tid; i < kH; i += kS3Threads) g1[i] = 0u;
   }
-  if (mode != kSegSelect) return;  // workgroup-uniform
-  const uint32_t fmask = WARM ? (1u << sh) - 1u : (uint32_t)(kH3 - 1);
+  const uint32_t fmask = (uint32_t)(kH3 - 1);
   constexpr int U = 4;
   for (uint32_t i0 = 0; i0 < cnt; i0 += U * kS3Threads) {  // workgroup-uniform
     uint32_t key[U];
@@ -635,8 +621,8 @@ __global__ __launch_bounds__(kS3Threads) void seg_fine_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + u * kS3Threads + tid;
-      const bool in = WARM ? (key[u] - lo) >> sh == b2 : key[u] >> 9 == ((b1 << 11) | b2);
-      const uint32_t f = WARM ? (key[u] - lo) & fmask : key[u] & fmask;
+      const bool in = key[u] >> 9 == ((b1 << 11) | b2);
+      const uint32_t f = key[u] & fmask;
       if (i < cnt && in) atomicAdd(&h3[f], 1u);
     }
   }
@@ -700,7 +686,7 @@ CHOCO_DEV void seg_next_window_v(const uint32_t (&hv)[kWinPer], uint32_t base, u
   }
 }
 
-template <bool WARM>
+// (cold calls)
 __global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
     const int64_t* __restrict__ trows, int nseg, uint32_t* __restrict__ hist2, const uint32_t* __restrict__ hist3,
     uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt, const float* __restrict__ cval,
@@ -711,42 +697,23 @@ __global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
   if (c.R.ntile == 1) return;  // selected in S2
   const int tid = threadIdx.x;
   const uint32_t cnt = tilecnt[blockIdx.x];
-  const uint32_t mode = WARM ? info[8 * c.s + 6] : (uint32_t)kSegSelect;
-  const uint32_t b2 = info[8 * c.s + 3], kc = info[8 * c.s + 4];
-  SegWin w{0u, 9u, 0u, 0u};
-  uint32_t b1 = 0;
-  if (WARM) {
-    w = win[c.s];
-    w.sh = min(w.sh, kWinShMax);
-  } else {
-    b1 = info[8 * c.s + 0];
-  }
-  uint32_t T = 0;
-  if (mode == kSegSelect) {  // workgroup-uniform
-    block_find_rank_g<kH3 / kS3Threads>(hist3 + (int64_t)c.s * kH3, kc, scratch, bc);
-    T = WARM ? w.lo + (b2 << w.sh) + bc[0] : ((b1 << 20) | (b2 << 9) | bc[0]);
-  }
+  const uint32_t b2 = info[8 * c.s + 3], kc = info[8 * c.s + 4], b1 = info[8 * c.s + 0];
+  block_find_rank_g<kH3 / kS3Threads>(hist3 + (int64_t)c.s * kH3, kc, scratch, bc);
+  const uint32_t T = (b1 << 20) | (b2 << 9) | bc[0];
   if (c.j == 0) {
-    if (tid == 0 && mode == kSegSelect) {
+    if (tid == 0) {
       info[8 * c.s + 2] = T;
       info[8 * c.s + 5] = bc[1];  // ties at T to take (>= 1)
     }
-    uint32_t* __restrict__ g2 = hist2 + (int64_t)c.s * kH;  // read by every tile in S3a
-    if (mode == kSegSelect) {
-      // the next call's window, from this call's hist2 (cold: bits 19..9 inside b1,
-      // with the keys of the bins above b1; warm: the window's own bins)
-      const uint32_t base = WARM ? w.lo : (b1 << 20);
-      const uint32_t shb = WARM ? w.sh : 9u;
-      const uint32_t above = WARM ? 0u : (uint32_t)c.R.k - info[8 * c.s + 1];
-      seg_next_window(g2, base, shb, above, (uint32_t)c.R.k, T, &win[c.s], scratch);
-      __syncthreads();
-    } else if (mode == kSegAll && tid == 0) {
-      win[c.s] = SegWin{0u, kWinShMax, 1u, 0u};
-    }
+    // the next call's window, from this call's hist2 (bits 19..9 inside b1, with the keys
+    // of the bins above b1); hist2 was read by every tile in S3a
+    uint32_t* __restrict__ g2 = hist2 + (int64_t)c.s * kH;
+    seg_next_window(g2, b1 << 20, 9u, (uint32_t)c.R.k - info[8 * c.s + 1], (uint32_t)c.R.k, T, &win[c.s], scratch);
+    __syncthreads();
     for (int i = tid; i < kH; i += kS3Threads) g2[i] = 0u;
   }
   uint32_t gt = 0, eq = 0;
-  if (mode == kSegSelect) {
+  {
     constexpr int U = 4;
     for (uint32_t i0 = 0; i0 < cnt; i0 += U * kS3Threads) {  // workgroup-uniform
       uint32_t key[U];
@@ -762,8 +729,6 @@ __global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
         eq += (i < cnt && key[u] == T) ? 1u : 0u;
       }
     }
-  } else if (mode == kSegAll) {
-    gt = tid == 0 ? cnt : 0u;
   }
   uint32_t g0, e0, gtot, etot;
   block_excl_scan2(gt, eq, scratch, &g0, &e0, &gtot, &etot);
@@ -918,21 +883,15 @@ __global__ __launch_bounds__(kS3Threads) void seg_bin_kernel(
 // earlier tiles (<= kSegMaxTiles - 1: kS4Per per thread), then the ordered
 // compaction of its candidates (a few hundred at k = 1 %: one or two rounds).
 // Latency-bound like S3: 256-thread workgroups (cheaper block scans, more
-// workgroups resident).  A warm segment whose window missed: tile 0 selects the
-// whole segment exactly (select.h; the segment's candidates were not all kept)
-// and re-centres the window on its T.
+// workgroups resident).  (Cold calls; warm calls take S4w below.)
 constexpr int kS4Threads = 256;
 constexpr int kS4Per = kSegMaxTiles / kS4Threads;
 static_assert(kS4Per * kS4Threads == kSegMaxTiles, "S4 tile-count geometry");
-template <bool WARM, bool XH>
 __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
-    const float* __restrict__ x, const float* __restrict__ xh, const int64_t* __restrict__ trows, int nseg,
-    const uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt, const uint32_t* __restrict__ tcount,
-    uint32_t* __restrict__ hist3, const float* __restrict__ cval, const uint32_t* __restrict__ cidx,
-    float* __restrict__ out_val, int32_t* __restrict__ out_idx, SegWin* __restrict__ win,
-    uint32_t* __restrict__ misses, uint32_t* __restrict__ miss_flag) {
+    const int64_t* __restrict__ trows, const uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt,
+    const uint32_t* __restrict__ tcount, uint32_t* __restrict__ hist3, const float* __restrict__ cval,
+    const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx) {
   __shared__ uint32_t scratch[40];
-  __shared__ ExactSmem es;
   const TileCtx c = tile_ctx_rows(trows, blockIdx.x);
   if (c.R.ntile == 1) return;  // selected in S2
   const int tid = threadIdx.x;
@@ -940,22 +899,7 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
     uint32_t* __restrict__ g3 = hist3 + (int64_t)c.s * kH3;
     for (int i = tid; i < kH3; i += kS4Threads) g3[i] = 0u;
   }
-  const uint32_t mode = WARM ? info[8 * c.s + 6] : (uint32_t)kSegSelect;
-  if (mode == kSegMissed) {  // workgroup-uniform
-    if (c.j != 0) return;
-    if (tid == 0) {
-      atomicAdd(misses, 1u);
-      if (miss_flag) __hip_atomic_store(miss_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    Src<kData, XH> src{x + c.R.off, XH ? xh + c.R.off : nullptr, 0};
-    block_select_T(src, c.R.len, c.R.k, es);
-    const uint32_t T = es.bc[0], r = es.bc[1], ties = es.bc[2];
-    __syncthreads();
-    block_emit(src, c.R.len, T, r, ties, 1.0f, out_val + c.R.out_off, out_idx + c.R.out_off, c.R.off, es);
-    if (tid == 0) win[c.s] = SegWin{T > (1u << 18) ? T - (1u << 18) : 0u, kWinShMax, 1u, 0u};
-    return;
-  }
-  const uint32_t T = info[8 * c.s + 2], r = mode == kSegAll ? 0u : info[8 * c.s + 5];
+  const uint32_t T = info[8 * c.s + 2], r = info[8 * c.s + 5];
   const uint32_t cnt = tilecnt[blockIdx.x];
   const uint32_t ev = tcount[2 * blockIdx.x + 1];
   uint32_t o, quota;
@@ -986,7 +930,7 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
     const float v = valid ? cval[c.slot + p] : 0.f;
     const uint32_t ix = valid ? cidx[c.slot + p] : 0u;
     const uint32_t key = fkey(v);
-    const bool gt = valid && (mode == kSegAll || key > T), eq = valid && mode != kSegAll && key == T;
+    const bool gt = valid && key > T, eq = valid && key == T;
     bool sel;
     if (all_ties || quota == 0u) {
       sel = gt || (eq && all_ties);
@@ -1196,11 +1140,6 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_w_kernel(
   }
 }
 
-#ifndef CHOCO_SEG_W3
-#define CHOCO_SEG_W3 1
-#endif
-constexpr bool kSegW3 = CHOCO_SEG_W3 != 0;
-
 // ---------------------------------------------------------------- host side
 static int64_t plan_tiles(const int64_t* plan_host) { return plan_host[6]; }
 static int64_t plan_batched(const int64_t* plan_host) { return plan_host[7]; }
@@ -1289,7 +1228,7 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
   }
   profile_end("topk_seg_collect", st);
   CHOCO_LAUNCHED("seg_collect_kernel");
-  if (warm && kSegW3) {
+  if (warm) {
     profile_begin("topk_seg_bin", st);
     CHOCO_KLAUNCH(seg_bin_kernel, dim3(ntile), dim3(kS3Threads), 0, st, trows, W.hist2, W.info, W.tilecnt, W.cval,
                   W.win, W.tcount, W.blist);
@@ -1303,31 +1242,20 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
     CHOCO_LAUNCHED("seg_emit_w_kernel");
     return CHOCO_OK;
   }
+  // cold calls: S3a, S3b, S4
   profile_begin("topk_seg_fine", st);
-  if (warm)
-    CHOCO_KLAUNCH((seg_fine_kernel<true>), dim3(ntile), dim3(kS3Threads), 0, st, trows, nseg, W.hist1, W.hist2,
-                  W.hist3, W.info, W.tilecnt, W.cval, W.win);
-  else
-    CHOCO_KLAUNCH((seg_fine_kernel<false>), dim3(ntile), dim3(kS3Threads), 0, st, trows, nseg, W.hist1, W.hist2,
-                  W.hist3, W.info, W.tilecnt, W.cval, W.win);
+  CHOCO_KLAUNCH(seg_fine_kernel, dim3(ntile), dim3(kS3Threads), 0, st, trows, nseg, W.hist1, W.hist2, W.hist3,
+                W.info, W.tilecnt, W.cval);
   profile_end("topk_seg_fine", st);
   CHOCO_LAUNCHED("seg_fine_kernel");
   profile_begin("topk_seg_count", st);
-  if (warm)
-    CHOCO_KLAUNCH((seg_count_kernel<true>), dim3(ntile), dim3(kS3Threads), 0, st, trows, nseg, W.hist2, W.hist3,
-                  W.info, W.tilecnt, W.cval, W.tcount, W.win);
-  else
-    CHOCO_KLAUNCH((seg_count_kernel<false>), dim3(ntile), dim3(kS3Threads), 0, st, trows, nseg, W.hist2, W.hist3,
-                  W.info, W.tilecnt, W.cval, W.tcount, W.win);
+  CHOCO_KLAUNCH(seg_count_kernel, dim3(ntile), dim3(kS3Threads), 0, st, trows, nseg, W.hist2, W.hist3, W.info,
+                W.tilecnt, W.cval, W.tcount, W.win);
   profile_end("topk_seg_count", st);
   CHOCO_LAUNCHED("seg_count_kernel");
   profile_begin("topk_seg_emit", st);
-  if (warm)
-    CHOCO_KLAUNCH((seg_emit_kernel<true, XH>), dim3(ntile), dim3(kS4Threads), 0, st, x, xh, trows, nseg, W.info,
-                  W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win, W.misses, W.miss_flag);
-  else
-    CHOCO_KLAUNCH((seg_emit_kernel<false, XH>), dim3(ntile), dim3(kS4Threads), 0, st, x, xh, trows, nseg, W.info,
-                  W.tilecnt, W.tcount, W.hist3, W.cval, W.cidx, out_val, out_idx, W.win, W.misses, W.miss_flag);
+  CHOCO_KLAUNCH(seg_emit_kernel, dim3(ntile), dim3(kS4Threads), 0, st, trows, W.info, W.tilecnt, W.tcount,
+                W.hist3, W.cval, W.cidx, out_val, out_idx);
   profile_end("topk_seg_emit", st);
   CHOCO_LAUNCHED("seg_emit_kernel");
   return CHOCO_OK;

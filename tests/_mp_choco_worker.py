@@ -31,7 +31,49 @@ def inputs(rank):
     return x, xh, hat0, mem0
 
 
+DEFER_STEPS = 4
+GAMMA = 0.5
+
+
+def _defer_steps(rank, comp, nb, split, state, outdir, dist, torch):
+    """`*_defer`: DEFER_STEPS fused CHOCO steps (sync_buffer["gossip"], x_hat_i itself as
+    flatten_hat_params) twice over the same start state -- the receive applied at once, then
+    deferred into the next step's first pass (sync_buffer["defer_receive"]) and flushed at the
+    end; x after every step and the final x_hat / memory are saved for both runs."""
+    from chocosgd_amd.tensor_buffer import TensorBuffer
+    x0, hat0, mem0 = state
+    shapes = [(torch.Size([m]), m) for m in LENS]
+    out = {}
+    for tag, defer in (("now", False), ("deferred", True)):
+        x = TensorBuffer(split(x0))
+        nhp = {rank: TensorBuffer(split(hat0)), "memory": TensorBuffer(split(mem0))}
+        for step in range(DEFER_STEPS):
+            sb = {"original_shapes": shapes, "flatten_params": x, "flatten_hat_params": nhp[rank],
+                  "gossip": (nhp["memory"].buffer, GAMMA)}
+            if defer:
+                sb["defer_receive"] = True
+            with torch.cuda.stream(comp.compressor_fn.gossip_stream):
+                comp.compress(sb)
+                comp.sync(sb)
+                comp.uncompress(sb, nhp, nb)
+            torch.cuda.synchronize()
+            out[f"{tag}_x{step}"] = x.buffer.cpu().numpy()
+        comp.flush_receive()
+        torch.cuda.synchronize()
+        out[f"{tag}_hat"] = nhp[rank].buffer.cpu().numpy()
+        out[f"{tag}_mem"] = nhp["memory"].buffer.cpu().numpy()
+        dist.barrier()
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), **out)
+    dist.barrier()
+
+
 def _rank_main(rank, world, port, comm_op, outdir):
+    global LENS
+    defer_steps = comm_op.endswith("_defer")
+    comm_op = comm_op[:-len("_defer")] if defer_steps else comm_op
+    if comm_op == "sign1":  # one segment: the single-kernel deferred sign receive
+        LENS = [sum(LENS)]
+        comm_op = "sign"
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -67,6 +109,8 @@ def _rank_main(rank, world, port, comm_op, outdir):
                 out.append(t[p:p + m].clone())
                 p += m
             return out
+        if defer_steps:
+            return _defer_steps(rank, comp, nb, split, (x, hat0, mem0), outdir, dist, torch)
         sb = {"original_shapes": [(torch.Size([m]), m) for m in LENS],
               "flatten_params": TensorBuffer(split(x)), "flatten_hat_params": TensorBuffer(split(xh))}
         nhp = {rank: TensorBuffer(split(hat0)), "memory": TensorBuffer(split(mem0))}

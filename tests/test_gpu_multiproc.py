@@ -123,6 +123,26 @@ def test_centralized_aggregation_across_processes(comm_op, world, tmp_path):
         assert same_bits(got[me]["params"], want), me
 
 
+@pytest.mark.parametrize("comm_op,world", [("quantize_qsgd_defer", 3), ("sign_defer", 3), ("sign1_defer", 3),
+                                           ("sign1_defer", 4)])
+def test_deferred_receive_across_processes(comm_op, world, tmp_path):
+    """utils.fused_step's deferred receive across PROCESSES (gloo, comm_device="cpu"): every
+    rank runs DEFER_STEPS fused CHOCO steps twice from the same state -- receive applied at
+    once, then deferred into the next step's first pass and flushed at the end -- and x after
+    every step, x_hat and memory must be the same bits (`sign1`: one segment, the
+    single-kernel receive; `sign`: six segments, receive + fused pack)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_mp_choco_worker.py"), comm_op, str(world),
+                        str(tmp_path)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    for q in range(world):
+        g = dict(np.load(tmp_path / f"rank{q}.npz"))
+        for s in range(W.DEFER_STEPS):
+            assert same_bits(g[f"deferred_x{s}"], g[f"now_x{s}"]), (q, s)
+        assert same_bits(g["deferred_hat"], g["now_hat"]), q
+        assert same_bits(g["deferred_mem"], g["now_mem"]), q
+        assert not np.array_equal(g["now_x0"], g[f"now_x{W.DEFER_STEPS - 1}"])  # the steps moved x
+
+
 def _verify_round(comm_op, world, tmp_path):
     lens, nseg = W.LENS, len(W.LENS)
     n = sum(lens)

@@ -623,3 +623,36 @@ def test_topk_segmented_warm_bin_list_overflow():
         _check_seg(x, plan, lens, 0.99)
         counts.append(codec.topk_fallback_count(plan=plan))
     assert counts[-1] == counts[1], counts
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_topk_segmented_warm_random_layouts(seed):
+    """Random layouts (single-tile and multi-tile tensors, tile-edge lengths) through a run of
+    warm calls whose data changes in kind -- drift, a sign flip, a few huge entries, a block
+    of zeros, quantised values (ties at the k-th key), a tensor made all equal -- every call
+    exact against the oracle (the warm tail's kept keys, their tie counts, the overflow and
+    missed-window paths)."""
+    from chocosgd_amd import codec
+    rng = np.random.default_rng(seed)
+    lens = [int(v) for v in rng.choice([1, 7, 300, 16383, 16384, 16385, 40_000, 131_072, 250_001], size=9)]
+    lens += [int(rng.integers(20_000, 600_000))]
+    n = sum(lens)
+    ratio = float(rng.choice([0.9, 0.99, 0.999]))
+    plan = codec.SegmentPlan(lens, ratio, torch.device(DEV))
+    base = randn(n, seed)
+    seq = [base, base * 0.97 + randn(n, seed + 1, 0.05), -base]
+    spikes = base.clone()
+    spikes[torch.from_numpy(rng.choice(n, 50, replace=False)).to(DEV)] = 1e6
+    seq.append(spikes)
+    zeros = base.clone()
+    zeros[: n // 3] = 0.0
+    seq.append(zeros)
+    seq.append(torch.round(base * 8) / 8)
+    flat = base.clone()
+    off = int(np.sum(lens[:-1]))
+    flat[off:] = 0.25  # the last tensor all equal: every key ties at T
+    seq.append(flat)
+    seq.append(randn(n, seed + 2))
+    for x in seq:
+        _check_seg(x, plan, lens, ratio)
+        _check_seg(x, plan, lens, ratio, xh=randn(n, seed + 3, 0.01))

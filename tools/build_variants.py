@@ -13,8 +13,9 @@ VARIANTS = {
     "stamps": ["CHOCO_STAMPS=1"],
     # every bounded wait of the exact fallback gives up at once: tools/status_probe.py
     "poll1": ["CHOCO_POLL_BUDGET=1"],
-    # warm segmented tail: S3a + S3b + S4 (the round-4 sequence) instead of S3w + S4w
-    "segw0": ["CHOCO_SEG_W3=0"],
+    # the deferred QSGD receive's stores: all non-temporal / memory non-temporal (default: plain)
+    "qrg1": ["CHOCO_QRG_ST=1"],
+    "qrg2": ["CHOCO_QRG_ST=2"],
 }
 
 
