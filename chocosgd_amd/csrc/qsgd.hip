@@ -786,22 +786,15 @@ __global__ __launch_bounds__(kQThreads) void qsgd_recv_gossip_norm_kernel(
       }
     }
     if (e0 + kQPer <= n) {
-#ifndef CHOCO_QRG_ST
-#define CHOCO_QRG_ST 0
-#endif
-      // (A/B: 0 plain stores, 1 all non-temporal, 2 memory non-temporal)
-      auto st = [](float* p, float4 v, bool nt) {
-        if (nt) st_gs4(p, v);
-        else *reinterpret_cast<float4*>(p) = v;
-      };
-      constexpr bool kNtX = CHOCO_QRG_ST == 1, kNtM = CHOCO_QRG_ST >= 1;
-      st(x + e0, make_float4(xv[g][0], xv[g][1], xv[g][2], xv[g][3]), kNtX);
-      st(x + e0 + 4, make_float4(xv[g][4], xv[g][5], xv[g][6], xv[g][7]), kNtX);
-      st(mem + e0, make_float4(mv[g][0], mv[g][1], mv[g][2], mv[g][3]), kNtM);
-      st(mem + e0 + 4, make_float4(mv[g][4], mv[g][5], mv[g][6], mv[g][7]), kNtM);
+      // (plain stores: non-temporal x / x_hat / memory, or memory alone, measured the same
+      // in the deferred step, profiles/r05_ab_summary.txt item 11)
+      *reinterpret_cast<float4*>(x + e0) = make_float4(xv[g][0], xv[g][1], xv[g][2], xv[g][3]);
+      *reinterpret_cast<float4*>(x + e0 + 4) = make_float4(xv[g][4], xv[g][5], xv[g][6], xv[g][7]);
+      *reinterpret_cast<float4*>(mem + e0) = make_float4(mv[g][0], mv[g][1], mv[g][2], mv[g][3]);
+      *reinterpret_cast<float4*>(mem + e0 + 4) = make_float4(mv[g][4], mv[g][5], mv[g][6], mv[g][7]);
       if (has_self) {
-        st(hat + e0, make_float4(hv[g][0], hv[g][1], hv[g][2], hv[g][3]), kNtX);
-        st(hat + e0 + 4, make_float4(hv[g][4], hv[g][5], hv[g][6], hv[g][7]), kNtX);
+        *reinterpret_cast<float4*>(hat + e0) = make_float4(hv[g][0], hv[g][1], hv[g][2], hv[g][3]);
+        *reinterpret_cast<float4*>(hat + e0 + 4) = make_float4(hv[g][4], hv[g][5], hv[g][6], hv[g][7]);
       }
     } else {
       for (int c = 0; c < kQPer && e0 + c < n; ++c) {

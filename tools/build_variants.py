@@ -13,9 +13,6 @@ VARIANTS = {
     "stamps": ["CHOCO_STAMPS=1"],
     # every bounded wait of the exact fallback gives up at once: tools/status_probe.py
     "poll1": ["CHOCO_POLL_BUDGET=1"],
-    # the deferred QSGD receive's stores: all non-temporal / memory non-temporal (default: plain)
-    "qrg1": ["CHOCO_QRG_ST=1"],
-    "qrg2": ["CHOCO_QRG_ST=2"],
 }
 
 
