@@ -1020,7 +1020,9 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   // candidates are written COMPACTLY, chunk after chunk from the tile start
   // (full lines; cntw then says "one run": [total, 0, 0, ...]), and the sorted
   // side list is staged in LDS and copied out coalesced.  Scattered partial-line
-  // stores while other CUs still stream cost ~0.5 us per MB (HBM turnaround).
+  // stores while other CUs still stream cost ~0.5 us per MB (HBM turnaround): each wave
+  // writing its chunks' pairs as its own stream ends (per-chunk slots) took K2 71 -> 96 us
+  // and K34 11 -> 15 us at 100M (same-box A/B, round 5: removed).
   uint32_t hsum, csum;
   bool spilled;
   {
