@@ -582,7 +582,7 @@ def main():
     w = Worker(args, rank, world, dev)
     comp_k, dec_k = STAGES[w.op]
     if w.step_mode:
-        comp_k = comp_k + ["gossip_step", "qsgd_recv_norm", "sign_recv_pack"]
+        comp_k = comp_k + ["gossip_step", "qsgd_recv_norm", "sign_recv_pack", "sign_planes"]
 
     def barrier():
         torch.cuda.synchronize()

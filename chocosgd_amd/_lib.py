@@ -57,6 +57,7 @@ SIGNATURES = {
     "choco_sign_unpack": (_c_i32, [_vp, _c_i64, _vp, _vp]),
     "choco_sign_decompress_accumulate": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i32, _c_i64, _vp, _c_i32,
                                                   _vp, _vp, _vp, _c_sz, _vp]),
+    "choco_sign_recv_workspace_size": (_c_sz, [_c_i64, _c_i32, _c_i32]),
     "choco_sign_recv_gossip_compress": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i32, _vp, _vp, _vp, _c_f32, _c_i64,
                                                  _vp, _c_i32, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_sign_decompress_axpy": (_c_i32, [_pp, _pp, _p_f32, _c_i32, _c_i64, _vp, _c_i32, _c_i32, _vp, _vp]),

@@ -761,7 +761,8 @@ def sign_recv_gossip_compress(messages, weights, self_slot, x, memory, xhat, gam
         messages, weights, self_slot = messages[head:], weights[head:], self_slot - head
     slot = self_slot if 0 <= self_slot < len(messages) else -1
     L = lib()
-    ws = workspace(dev, "acc", L.choco_sign_workspace_size(nseg))
+    # (its own workspace: the accumulator block plus bit planes of the messages and the output)
+    ws = workspace(dev, "signrecv", L.choco_sign_recv_workspace_size(n, nseg, len(messages)))
     pp, keep1 = _lib.ptr_array([p.data_ptr() for p, _ in messages])
     nn, keep2 = _lib.ptr_array([nm.data_ptr() for _, nm in messages])
     ww, keep3 = _lib.f32_array([float(w) for w in weights])

@@ -777,163 +777,237 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
   }
 }
 
-// (A one-segment receiver with 4 KiB row runs per wave and dword-aligned 16-B stores
-// measured slower than the column-tile receiver, 1208 vs 1127 us at 345M, one message:
-// removed, git history r03.)
+// ---------------------------------------------------------------- the receive in row runs
+// Deferred receive (one segment) over ROW RUNS of the (32, N') view instead of column
+// tiles: a workgroup streams 4096 consecutive columns of ONE row -- 16 KiB contiguous of
+// x, x_hat and memory each, the access shape of a flat stream -- and needs bit r of 4096
+// consecutive words of every message.  Those come from bit PLANES: plane[r][p] bit b =
+// word 32 p + b bit r, made from each message by a 32 x 32 bit transpose per 32 words
+// (sign_to_planes_kernel), and this step's words are made back from the output planes
+// the same way (sign_from_planes_kernel).  The transposes read and write n / 8 bytes per
+// message; the row runs save the column tiles' 32 separate row streams per workgroup.
+constexpr int kPlaneThreads = 256;
+constexpr int kRowRun = 4096;      // columns per workgroup of the row-run receive
+static_assert(kRowRun == 4 * 4 * kSignThreads, "four float4 per thread per run");
+__host__ __device__ inline int64_t plane_words(int64_t Np) { return (Np + 31) / 32; }
 
-// Deferred receive (one segment): the previous step's messages, this step's consensus
-// step and this step's pack in ONE pass over x, x_hat and memory.
-// ParallelCHOCO_V.step (parallel_choco_v.py:104-155) runs uncompress (:548-558: per
-// message u = (norm / numel) * sign; x_hat += u for the self rank, memory += w * u in
-// neighbors_info order), then update_params_from_neighbor (optim/utils.py:67-72) and the
-// next compress; every element's chain here is exactly that sequence's (sign_apply,
-// gossip1, the pack's x_new - x_hat), so x, x_hat, memory and the words are bit-identical
-// to sign_accumulate_kernel + sign_pack1_kernel<.., GS>.  The column tiles are
-// sign_pack1_kernel's: lane l owns words j0+4l..+3 of every message and of the output, so
-// row r's float4 at the lane's run offset is exactly bit r of its words (no realignment).
-// Rows go in groups of 4 with two groups in flight (x, x_hat, memory of 8 rows), loads and
-// stores non-temporal.  Same-box A/B at 345M, one message (ms per step, two repeats): this
-// 1.962 / 1.970; temporal stores 2.121 / 2.108; temporal loads + stores 1.989 / 1.986;
-// 2-row groups (131 VGPRs, 3 waves) 1.995 / 2.001; 3 waves forced 1.963 / 2.009; 8-row
-// groups (1 wave) 1.927 / 1.968 -- no knob moves it: variants removed.
+// In place: w[r] bit b <-> w[b] bit r (LSB-first), five rounds of masked block swaps.
+CHOCO_DEV void transpose32(uint32_t (&w)[32]) {
+  const uint32_t masks[5] = {0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int m = 16 >> k;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      if ((i & m) == 0) {
+        const uint32_t t = ((w[i] >> m) ^ w[i + m]) & masks[k];
+        w[i + m] ^= t;
+        w[i] ^= t << m;
+      }
+    }
+  }
+}
+
+// words (Np) -> planes [32][P]: thread t <-> 32-word block t
+__global__ __launch_bounds__(kPlaneThreads) void sign_to_planes_kernel(const uint32_t* __restrict__ words, int64_t Np,
+                                                                       uint32_t* __restrict__ planes) {
+  const int64_t P = plane_words(Np);
+  const int64_t p = (int64_t)blockIdx.x * kPlaneThreads + threadIdx.x;
+  if (p >= P) return;
+  uint32_t w[32];
+  const int64_t j0 = 32 * p;
+  if (j0 + 32 <= Np) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(words + j0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint4 t = s4[q];
+      w[4 * q] = t.x; w[4 * q + 1] = t.y; w[4 * q + 2] = t.z; w[4 * q + 3] = t.w;
+    }
+  } else {
+#pragma unroll
+    for (int b = 0; b < 32; ++b) w[b] = j0 + b < Np ? words[j0 + b] : 0u;
+  }
+  transpose32(w);
+#pragma unroll
+  for (int r = 0; r < 32; ++r) planes[(int64_t)r * P + p] = w[r];
+}
+
+// planes [32][P] -> words (Np)
+__global__ __launch_bounds__(kPlaneThreads) void sign_from_planes_kernel(const uint32_t* __restrict__ planes,
+                                                                         int64_t Np, uint32_t* __restrict__ words) {
+  const int64_t P = plane_words(Np);
+  const int64_t p = (int64_t)blockIdx.x * kPlaneThreads + threadIdx.x;
+  if (p >= P) return;
+  uint32_t w[32];
+#pragma unroll
+  for (int r = 0; r < 32; ++r) w[r] = planes[(int64_t)r * P + p];
+  transpose32(w);
+  const int64_t j0 = 32 * p;
+  if (j0 + 32 <= Np) {
+    uint4* d4 = reinterpret_cast<uint4*>(words + j0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) d4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  } else {
+#pragma unroll
+    for (int b = 0; b < 32; ++b)
+      if (j0 + b < Np) words[j0 + b] = w[b];
+  }
+}
+
+struct PlaneMsgs {
+  const uint32_t* planes[kMaxMsg];  // [32][P] per message
+  const float* norms[kMaxMsg];
+  float w[kMaxMsg];
+  int self_slot;
+};
+
+constexpr int kRowRep = 8;  // replicas of the fp64 L1 accumulator
+// Workgroup i <-> run i, row-major over the (32, N') view, i.e. the flat element order: row
+// r = i / nrun, columns [J, J + 4096) with J = (i % nrun) * 4096.  Thread t takes the float4
+// at columns J + 1024 c + 4 t (c = 0..3): every load and store instruction of a wave is one
+// contiguous 1 KiB.  Its 4 message bits per float4 are a nibble of a plane word; the 4-bit
+// output nibbles of 8 lanes are OR-ed into one plane word (3 xor shuffles).  Every element's
+// chain is the unfused sequence's (sign_apply, gossip1, the pack's x_new - x_hat), so x,
+// x_hat, memory and the words are bit-identical to sign_accumulate_kernel +
+// sign_pack1_kernel<.., GS> (parallel_choco_v.py:548-558, optim/utils.py:67-72, :476-506).
+// Same-box A/B at 345M, one message, step_sign --defer-receive (ms per step, two repeats):
+// this 1.628 / 1.626; non-temporal loads and stores 1.767 / 1.758; a 2048-workgroup
+// grid-stride loop 1.915 / 1.914 (non-temporal 1.994 / 2.036; 1024 workgroups 2.033 /
+// 2.030); round 5's column-tile receive (32 rows of a 1024-word block per workgroup,
+// non-temporal, 8 rows in flight) 1.983 / 1.984: removed, git history r05.
 template <int NM, bool HS>
-__global__ __launch_bounds__(kSignThreads) void sign_recv_pack1_kernel(SignMsgs M, float* __restrict__ x,
-                                                                       float* __restrict__ xh,
-                                                                       float* __restrict__ mem, float gamma,
-                                                                       int64_t n, int64_t Np,
-                                                                       uint32_t* __restrict__ packed,
-                                                                       float* __restrict__ l1_out,
-                                                                       SignWs* __restrict__ ws) {
-  constexpr int RU = 4;
-  constexpr int NG = 32 / RU;
+__global__ __launch_bounds__(kSignThreads) void sign_recv_rows_kernel(PlaneMsgs M, float* __restrict__ x,
+                                                                      float* __restrict__ xh,
+                                                                      float* __restrict__ mem, float gamma,
+                                                                      int64_t n, int64_t Np,
+                                                                      uint32_t* __restrict__ out_planes,
+                                                                      float* __restrict__ l1_out,
+                                                                      SignWs* __restrict__ ws) {
   __shared__ double s_red[kSignThreads / 64];
   __shared__ unsigned int s_flag;
   double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
-  const int lane = lane_id(), w = threadIdx.x >> 6;
-  const int64_t j0 = (int64_t)blockIdx.x * kSignCols + 256 * w;
-  const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
-  const bool interior = ncol == 256 && (int64_t)31 * Np + j0 + 256 <= n;
-  // this lane's words of every message and the per-message scale (norm / numel)
-  uint32_t in[NM][4];
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const int64_t P = plane_words(Np);
+  const int64_t nrun = (Np + kRowRun - 1) / kRowRun;
+  const uint32_t nib_sh = 4u * (uint32_t)(tid & 7);
   float sc[NM];
-  {
-    const int64_t j = j0 + 4 * lane;
 #pragma unroll
-    for (int q = 0; q < NM; ++q) {
-      sc[q] = M.norms[q][0] / (float)n;
-      if (j + 3 < Np) {
-        const uint4 t = *reinterpret_cast<const uint4*>(M.packed[q] + j);
-        in[q][0] = t.x; in[q][1] = t.y; in[q][2] = t.z; in[q][3] = t.w;
-      } else {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) in[q][c] = (j + c < Np) ? M.packed[q][j + c] : 0u;
-      }
-    }
-  }
-  // one element of row r, word column c: receive, consensus step; returns x_new - x_hat
-  auto elem = [&](int r, int c, float& xv, float& hv, float& mv) -> float {
-#pragma unroll
-    for (int q = 0; q < NM; ++q) {
-      const float u = ((in[q][c] >> r) & 1u) ? -sc[q] : sc[q];
-      if (HS && q == M.self_slot) hv = hv + u;
-      mv = fmaf(M.w[q], u, mv);
-    }
-    xv = gossip1(xv, mv, hv, gamma);
-    return xv - hv;
-  };
-  uint32_t wd[4] = {0u, 0u, 0u, 0u};
+  for (int q = 0; q < NM; ++q) sc[q] = M.norms[q][0] / (float)n;
+  const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x, (uint32_t)(n * 4));
+  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(xh, (uint32_t)(n * 4));
+  const __amdgpu_buffer_rsrc_t rm = buf_rsrc(mem, (uint32_t)(n * 4));
   double p = 0.0;
-  if (interior) {
-    const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x, (uint32_t)(n * 4));
-    const __amdgpu_buffer_rsrc_t rh = buf_rsrc(xh, (uint32_t)(n * 4));
-    const __amdgpu_buffer_rsrc_t rm = buf_rsrc(mem, (uint32_t)(n * 4));
-    const uint32_t voff = 16u * (uint32_t)lane;
-    auto row_off = [&](int r) -> uint32_t { return (uint32_t)(((int64_t)r * Np + j0) * 4); };
-    struct Group {
-      float4 x[RU], h[RU], m[RU];
-    };
-    auto load_group = [&](int g, Group& G) {
+  {
+    const int64_t i = blockIdx.x;
+    const int r = (int)(i / nrun);
+    const int64_t J = (i - (int64_t)r * nrun) * kRowRun;
+    const int64_t e0 = (int64_t)r * Np + J;  // the run's first element
+    const bool full = J + kRowRun <= Np && e0 + kRowRun <= n;
+    uint32_t bits[4][NM];
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.x[u] = ld_buf4s<true>(rx, voff, row_off(g * RU + u));
+    for (int c = 0; c < 4; ++c) {
+      const int64_t pw = (J + 1024 * c) / 32 + (tid >> 3);
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.h[u] = ld_buf4s<true>(rh, voff, row_off(g * RU + u));
-#pragma unroll
-      for (int u = 0; u < RU; ++u) G.m[u] = ld_buf4s<true>(rm, voff, row_off(g * RU + u));
-    };
-    auto proc_group = [&](int g, Group& G) {
-#pragma unroll
-      for (int u = 0; u < RU; ++u) {
-        const int r = g * RU + u;
-        float xv[4] = {G.x[u].x, G.x[u].y, G.x[u].z, G.x[u].w};
-        float hv[4] = {G.h[u].x, G.h[u].y, G.h[u].z, G.h[u].w};
-        float mv[4] = {G.m[u].x, G.m[u].y, G.m[u].z, G.m[u].w};
-        float v[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = elem(r, c, xv[c], hv[c], mv[c]);
-        // non-temporal: none of the three is re-read by this step
-        st_buf4s<true>(rx, voff, row_off(r), make_float4(xv[0], xv[1], xv[2], xv[3]));
-        st_buf4s<true>(rm, voff, row_off(r), make_float4(mv[0], mv[1], mv[2], mv[3]));
-        if (HS) st_buf4s<true>(rh, voff, row_off(r), make_float4(hv[0], hv[1], hv[2], hv[3]));
-#pragma unroll
-        for (int c = 0; c < 4; ++c) wd[c] |= (v[c] < 0.f ? 1u : 0u) << r;
-        p += ((double)fabsf(v[0]) + (double)fabsf(v[1])) + ((double)fabsf(v[2]) + (double)fabsf(v[3]));
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    Group A, B;
-    load_group(0, A);
-    load_group(1, B);
-#pragma unroll
-    for (int g = 0; g < NG; g += 2) {
-      proc_group(g, A);
-      if (g + 2 < NG) load_group(g + 2, A);
-      proc_group(g + 1, B);
-      if (g + 3 < NG) load_group(g + 3, B);
+      for (int q = 0; q < NM; ++q) bits[c][q] = pw < P ? M.planes[q][(int64_t)r * P + pw] >> nib_sh : 0u;
     }
-  } else {
-#pragma unroll 1
-    for (int r = 0; r < 32; ++r) {
-      const int64_t s = (int64_t)r * Np + j0 + 4 * lane;
-      float tt[4];
+    float4 xv[4], hv[4], mv[4];
+    if (full) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const int64_t e = s + c;
-        tt[c] = 0.f;
-        if (4 * lane + c < ncol && e < n) {
-          float xv = x[e], hv = xh[e], mv = mem[e];
-          tt[c] = elem(r, c, xv, hv, mv);
-          x[e] = xv;
-          mem[e] = mv;
-          if (HS) xh[e] = hv;
-        }
+        const uint32_t off = (uint32_t)((e0 + 1024 * c + 4 * tid) * 4);
+        xv[c] = ld_buf4<false>(rx, off);
+        hv[c] = ld_buf4<false>(rh, off);
+        mv[c] = ld_buf4<false>(rm, off);
       }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) wd[c] |= (tt[c] < 0.f ? 1u : 0u) << r;
-      p += ((double)fabsf(tt[0]) + (double)fabsf(tt[1])) + ((double)fabsf(tt[2]) + (double)fabsf(tt[3]));
-    }
-  }
-  {
-    const int64_t j = j0 + 4 * lane;
-    if (j + 3 < Np) {
-      *reinterpret_cast<uint4*>(packed + j) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
     } else {
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (j + c < Np) packed[j + c] = wd[c];
+      for (int c = 0; c < 4; ++c) {
+        float tx[4], th[4], tm[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t jj = J + 1024 * c + 4 * tid + k;
+          const bool in = jj < Np && e0 - J + jj < n;
+          tx[k] = in ? x[e0 - J + jj] : 0.f;
+          th[k] = in ? xh[e0 - J + jj] : 0.f;
+          tm[k] = in ? mem[e0 - J + jj] : 0.f;
+        }
+        xv[c] = make_float4(tx[0], tx[1], tx[2], tx[3]);
+        hv[c] = make_float4(th[0], th[1], th[2], th[3]);
+        mv[c] = make_float4(tm[0], tm[1], tm[2], tm[3]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float a[4] = {xv[c].x, xv[c].y, xv[c].z, xv[c].w};
+      float h[4] = {hv[c].x, hv[c].y, hv[c].z, hv[c].w};
+      float m[4] = {mv[c].x, mv[c].y, mv[c].z, mv[c].w};
+      uint32_t nib = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int q = 0; q < NM; ++q) {
+          const float u = ((bits[c][q] >> k) & 1u) ? -sc[q] : sc[q];
+          if (HS && q == M.self_slot) h[k] = h[k] + u;
+          m[k] = fmaf(M.w[q], u, m[k]);
+        }
+        a[k] = gossip1(a[k], m[k], h[k], gamma);
+        const float d = a[k] - h[k];
+        const int64_t jj = J + 1024 * c + 4 * tid + k;
+        const bool in = full || (jj < Np && e0 - J + jj < n);
+        nib |= (in && d < 0.f ? 1u : 0u) << k;
+        if (in) p += (double)fabsf(d);
+      }
+      xv[c] = make_float4(a[0], a[1], a[2], a[3]);
+      hv[c] = make_float4(h[0], h[1], h[2], h[3]);
+      mv[c] = make_float4(m[0], m[1], m[2], m[3]);
+      uint32_t wd = nib << nib_sh;
+      wd |= __shfl_xor(wd, 1);
+      wd |= __shfl_xor(wd, 2);
+      wd |= __shfl_xor(wd, 4);
+      const int64_t pw = (J + 1024 * c) / 32 + (tid >> 3);
+      if ((tid & 7) == 0 && pw < P) out_planes[(int64_t)r * P + pw] = wd;
+    }
+    if (full) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t off = (uint32_t)((e0 + 1024 * c + 4 * tid) * 4);
+        st_buf4s<false>(rx, off, 0u, xv[c]);
+        st_buf4s<false>(rm, off, 0u, mv[c]);
+        if (HS) st_buf4s<false>(rh, off, 0u, hv[c]);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float a[4] = {xv[c].x, xv[c].y, xv[c].z, xv[c].w};
+        const float h[4] = {hv[c].x, hv[c].y, hv[c].z, hv[c].w};
+        const float m[4] = {mv[c].x, mv[c].y, mv[c].z, mv[c].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t jj = J + 1024 * c + 4 * tid + k;
+          if (jj < Np && e0 - J + jj < n) {
+            x[e0 - J + jj] = a[k];
+            mem[e0 - J + jj] = m[k];
+            if (HS) xh[e0 - J + jj] = h[k];
+          }
+        }
+      }
     }
   }
+  // the L1 norm: fp64 per thread, per workgroup, one of kRowRep replicas
   p = wave_sum(p);
-  if (lane == 0) s_red[w] = p;
+  if (lane == 0) s_red[wv] = p;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double tsum = 0.0;
+  if (tid == 0) {
+    double t = 0.0;
 #pragma unroll
-    for (int i = 0; i < kSignThreads / 64; ++i) tsum += s_red[i];
-    if (tsum != 0.0) unsafeAtomicAdd(&acc[0], tsum);
+    for (int i = 0; i < kSignThreads / 64; ++i) t += s_red[i];
+    if (t != 0.0) unsafeAtomicAdd(&acc[blockIdx.x & (kRowRep - 1)], t);
   }
   if (last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
-    if (threadIdx.x == 0) {
-      l1_out[0] = (float)atomic_exchange_double(&acc[0], 0.0);
+    if (tid == 0) {
+      double t = 0.0;
+      for (int i = 0; i < kRowRep; ++i) t += atomic_exchange_double(&acc[i], 0.0);
+      l1_out[0] = (float)t;
       __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -1130,6 +1204,13 @@ CHOCO_API int choco_sign_decompress_accumulate(const int32_t* const* packed_list
   return CHOCO_OK;
 }
 
+CHOCO_API size_t choco_sign_recv_workspace_size(int64_t n, int32_t nseg, int32_t nmsg) {
+  if (nseg > 1 || n >= (int64_t(1) << 30)) return choco_sign_workspace_size(nseg);  // the two-kernel form
+  const int64_t Np = choco_sign_words(n > 0 ? n : 1);
+  const size_t pb = align_up((size_t)32 * (size_t)plane_words(Np) * 4, 256);
+  return choco_sign_workspace_size(1) + (size_t)((nmsg > 0 ? nmsg : 1) + 1) * pb;
+}
+
 CHOCO_API int choco_sign_recv_gossip_compress(const int32_t* const* packed_list, const float* const* norms_list,
                                               const float* weights, int32_t nmsg, int32_t self_slot, float* x,
                                               float* memory, float* xhat, float gamma, int64_t n,
@@ -1157,41 +1238,57 @@ CHOCO_API int choco_sign_recv_gossip_compress(const int32_t* const* packed_list,
     return choco_gossip_sign_compress(x, memory, xhat, gamma, n, seg_off, nseg, packed, l1_norms, ws, ws_bytes,
                                       stream);
   }
-  SignMsgs M{};
+  const int64_t Np = choco_sign_words(n);
+  uint32_t* pk = reinterpret_cast<uint32_t*>(packed);
+  SignWs* w = static_cast<SignWs*>(ws);
+  CHOCO_REQUIRE(ws_bytes >= choco_sign_recv_workspace_size(n, nseg, nmsg),
+                "sign receive workspace too small: need choco_sign_recv_workspace_size(n, nseg, nmsg) bytes");
+  const int64_t P = plane_words(Np);
+  const size_t pb = align_up((size_t)32 * (size_t)P * 4, 256);
+  char* wb = static_cast<char*>(ws) + choco_sign_workspace_size(1);
+  const unsigned gp = (unsigned)((P + kPlaneThreads - 1) / kPlaneThreads);
+  PlaneMsgs M{};
+  profile_begin("sign_planes", st);
   for (int q = 0; q < nmsg; ++q) {
-    M.packed[q] = reinterpret_cast<const uint32_t*>(packed_list[q]);
+    uint32_t* pl = reinterpret_cast<uint32_t*>(wb + (size_t)q * pb);
+    CHOCO_KLAUNCH(sign_to_planes_kernel, dim3(gp), dim3(kPlaneThreads), 0, st,
+                  reinterpret_cast<const uint32_t*>(packed_list[q]), Np, pl);
+    M.planes[q] = pl;
     M.norms[q] = norms_list[q];
     M.w[q] = weights[q];
   }
-  M.nmsg = nmsg;
+  profile_end("sign_planes", st);
+  CHOCO_LAUNCHED("sign_to_planes_kernel");
   M.self_slot = self_slot;
-  const int64_t Np = choco_sign_words(n);
-  const unsigned grid = (unsigned)((Np + kSignCols - 1) / kSignCols);
-  uint32_t* pk = reinterpret_cast<uint32_t*>(packed);
-  SignWs* w = static_cast<SignWs*>(ws);
+  uint32_t* outp = reinterpret_cast<uint32_t*>(wb + (size_t)nmsg * pb);
+  const unsigned grid = (unsigned)(32 * ((Np + kRowRun - 1) / kRowRun));  // one workgroup per run
   profile_begin("sign_recv_pack", st);
-#define CHOCO_SIGN_RECV(NM)                                                                                     \
-  case NM:                                                                                                      \
-    if (self_slot >= 0)                                                                                         \
-      CHOCO_KLAUNCH((sign_recv_pack1_kernel<NM, true>), dim3(grid), dim3(kSignThreads), 0, st, M, x, xhat,     \
-                    memory, gamma, n, Np, pk, l1_norms, w);                                                     \
-    else                                                                                                        \
-      CHOCO_KLAUNCH((sign_recv_pack1_kernel<NM, false>), dim3(grid), dim3(kSignThreads), 0, st, M, x, xhat,    \
-                    memory, gamma, n, Np, pk, l1_norms, w);                                                     \
+#define CHOCO_SRR_CASE(NM)                                                                               \
+  case NM:                                                                                               \
+    if (self_slot >= 0)                                                                                  \
+      CHOCO_KLAUNCH((sign_recv_rows_kernel<NM, true>), dim3(grid), dim3(kSignThreads), 0, st, M, x, xhat, \
+                    memory, gamma, n, Np, outp, l1_norms, w);                                            \
+    else                                                                                                 \
+      CHOCO_KLAUNCH((sign_recv_rows_kernel<NM, false>), dim3(grid), dim3(kSignThreads), 0, st, M, x,      \
+                    xhat, memory, gamma, n, Np, outp, l1_norms, w);                                      \
     break;
   switch (nmsg) {
-    CHOCO_SIGN_RECV(1)
-    CHOCO_SIGN_RECV(2)
-    CHOCO_SIGN_RECV(3)
-    CHOCO_SIGN_RECV(4)
-    CHOCO_SIGN_RECV(5)
-    CHOCO_SIGN_RECV(6)
-    CHOCO_SIGN_RECV(7)
-    CHOCO_SIGN_RECV(8)
+    CHOCO_SRR_CASE(1)
+    CHOCO_SRR_CASE(2)
+    CHOCO_SRR_CASE(3)
+    CHOCO_SRR_CASE(4)
+    CHOCO_SRR_CASE(5)
+    CHOCO_SRR_CASE(6)
+    CHOCO_SRR_CASE(7)
+    CHOCO_SRR_CASE(8)
   }
-#undef CHOCO_SIGN_RECV
+#undef CHOCO_SRR_CASE
   profile_end("sign_recv_pack", st);
-  CHOCO_LAUNCHED("sign_recv_pack1_kernel");
+  CHOCO_LAUNCHED("sign_recv_rows_kernel");
+  profile_begin("sign_planes", st);
+  CHOCO_KLAUNCH(sign_from_planes_kernel, dim3(gp), dim3(kPlaneThreads), 0, st, outp, Np, pk);
+  profile_end("sign_planes", st);
+  CHOCO_LAUNCHED("sign_from_planes_kernel");
   return CHOCO_OK;
 }
 

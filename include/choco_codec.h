@@ -282,7 +282,13 @@ int choco_sign_decompress_accumulate(const int32_t* const* packed_list,
  * choco_gossip_sign_compress as two kernels).  Bit-identical x, x_hat, memory and words
  * to that sequence.  packed must not alias a message's words (l1_norms may alias a
  * message's norms: every workgroup reads them before the last one writes).  nmsg 1..8;
- * ws as for choco_sign_compress. */
+ * ws of choco_sign_recv_workspace_size(n, nseg, nmsg) bytes (one segment: the pass runs over
+ * row runs of the (32, N') view, the messages and the output words as bit planes). */
+/* Workspace bytes of choco_sign_recv_gossip_compress for n elements in nseg segments and
+ * nmsg messages (one segment: the accumulator block plus bit planes of every message and of
+ * the output; several: choco_sign_workspace_size(nseg)). */
+size_t choco_sign_recv_workspace_size(int64_t n, int32_t nseg, int32_t nmsg);
+
 int choco_sign_recv_gossip_compress(const int32_t* const* packed_list, const float* const* norms_list,
                                     const float* weights, int32_t nmsg, int32_t self_slot, float* x,
                                     float* memory, float* xhat, float gamma, int64_t n,

@@ -161,6 +161,27 @@ def test_sign_recv_gossip_compress_matches_sequence(case):
     assert np.allclose(host(nb), exact, rtol=1e-6, atol=0) and np.allclose(host(na), exact, rtol=1e-6, atol=0)
 
 
+@pytest.mark.parametrize("n", [1, 7, 32, 33, 1_023, 32 * 4_096 + 1, 32 * 4_097 + 5, 32 * 8_192 - 3])
+def test_sign_recv_gossip_compress_small_and_ragged(n):
+    """Sizes at the edges of the receive's layout: fewer words than one 32-word plane block,
+    word counts one past a 4096-column run, a last row shorter than the others -- against
+    the unfused sequence and the oracle's pack, bit for bit."""
+    from chocosgd_amd import codec
+    nmsg, self_slot, weights = 2, 0, [0.5, 0.25]
+    msgs = _sign_msgs(n, nmsg, None, 1)
+    x, hat, mem = _state(n, 5)
+    xa, ha, ma = x.clone(), hat.clone(), mem.clone()
+    xb, hb, mb = x.clone(), hat.clone(), mem.clone()
+    codec.sign_accumulate(msgs, weights, self_slot, n, ma, xhat_self=ha)
+    pa, na = codec.sign_compress(xa, xhat=ha, gossip=(ma, GAMMA))
+    pb, nb = codec.sign_recv_gossip_compress(msgs, weights, self_slot, xb, mb, hb, GAMMA)
+    assert same_bits(host(xb), host(xa)) and same_bits(host(hb), host(ha)) and same_bits(host(mb), host(ma))
+    assert torch.equal(pb, pa)
+    d = (host(xb) - host(hb)).astype(np.float32)
+    assert np.array_equal(host(pb), O.sign_pack(d))
+    assert np.allclose(host(nb), O.l1_norms(d, [n]), rtol=1e-6, atol=0)
+
+
 def test_sign_recv_gossip_compress_repeated_steps():
     """Deferred sign steps (own message double-buffered, as bench.py --defer-receive) against
     the unfused sequence over several steps: the L1 accumulator is left clean each call."""

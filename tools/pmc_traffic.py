@@ -37,7 +37,8 @@ KERNELS = {
     "qsgd_accumulate": ("qsgd_decode_kernel", 2.0),
     "sign_pack": ("sign_pack", 2.0),
     "sign_accumulate": ("sign_accumulate_kernel", 2.0),
-    "sign_recv_pack": ("sign_recv_pack1_kernel", 2.0),
+    "sign_recv_pack": ("sign_recv_rows_kernel", 2.0),
+    "sign_planes": ("planes_kernel", 2.0),
     "gossip_step": ("::gossip", 2.0),  # gossip1_kernel / gossipu_kernel (not qsgd_recv_gossip_norm_kernel)
 }
 
