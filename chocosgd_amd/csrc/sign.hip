@@ -808,49 +808,82 @@ CHOCO_DEV void transpose32(uint32_t (&w)[32]) {
   }
 }
 
-// words (Np) -> planes [32][P]: thread t <-> 32-word block t
-__global__ __launch_bounds__(kPlaneThreads) void sign_to_planes_kernel(const uint32_t* __restrict__ words, int64_t Np,
-                                                                       uint32_t* __restrict__ planes) {
-  const int64_t P = plane_words(Np);
-  const int64_t p = (int64_t)blockIdx.x * kPlaneThreads + threadIdx.x;
-  if (p >= P) return;
-  uint32_t w[32];
-  const int64_t j0 = 32 * p;
-  if (j0 + 32 <= Np) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(words + j0);
+// Both transposes stage a workgroup's 8192 words (256 32-word blocks) through LDS, so the
+// word side is read / written as contiguous uint4 rows (a stride-33 layout: the per-block
+// accesses are bank-conflict free), and thread t transposes block t in registers; the plane
+// side is 32 coalesced rows of 256 words.
+constexpr int kPlaneWords = 32 * kPlaneThreads;  // words per transpose workgroup
+constexpr int kPlaneLds = 33 * kPlaneThreads;
+
+CHOCO_DEV void words_to_lds(const uint32_t* __restrict__ words, int64_t Np, int64_t base, uint32_t* s) {
+  const bool a16 = (reinterpret_cast<uintptr_t>(words) & 15u) == 0;  // (a message may be a view)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const uint4 t = s4[q];
-      w[4 * q] = t.x; w[4 * q + 1] = t.y; w[4 * q + 2] = t.z; w[4 * q + 3] = t.w;
+  for (int i = 0; i < kPlaneWords / 4 / kPlaneThreads; ++i) {
+    const int wl = 4 * ((int)threadIdx.x + kPlaneThreads * i);
+    uint32_t v[4];
+    if (a16 && base + wl + 4 <= Np) {
+      const uint4 t = *reinterpret_cast<const uint4*>(words + base + wl);
+      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = base + wl + c < Np ? words[base + wl + c] : 0u;
     }
-  } else {
 #pragma unroll
-    for (int b = 0; b < 32; ++b) w[b] = j0 + b < Np ? words[j0 + b] : 0u;
+    for (int c = 0; c < 4; ++c) s[((wl + c) >> 5) * 33 + ((wl + c) & 31)] = v[c];
   }
-  transpose32(w);
+}
+
+struct PlaneSrc {
+  const uint32_t* words[kMaxMsg];
+  uint32_t* planes[kMaxMsg];
+};
+
+// words (Np) -> planes [32][P] of message blockIdx.y
+__global__ __launch_bounds__(kPlaneThreads) void sign_to_planes_kernel(PlaneSrc S, int64_t Np) {
+  __shared__ uint32_t s[kPlaneLds];
+  const int64_t P = plane_words(Np);
+  const int64_t base = (int64_t)blockIdx.x * kPlaneWords;
+  words_to_lds(S.words[blockIdx.y], Np, base, s);
+  __syncthreads();
+  uint32_t w[32];
 #pragma unroll
-  for (int r = 0; r < 32; ++r) planes[(int64_t)r * P + p] = w[r];
+  for (int b = 0; b < 32; ++b) w[b] = s[threadIdx.x * 33 + b];
+  transpose32(w);
+  const int64_t p = (int64_t)blockIdx.x * kPlaneThreads + threadIdx.x;
+  uint32_t* __restrict__ planes = S.planes[blockIdx.y];
+  if (p < P) {
+#pragma unroll
+    for (int r = 0; r < 32; ++r) planes[(int64_t)r * P + p] = w[r];
+  }
 }
 
 // planes [32][P] -> words (Np)
 __global__ __launch_bounds__(kPlaneThreads) void sign_from_planes_kernel(const uint32_t* __restrict__ planes,
                                                                          int64_t Np, uint32_t* __restrict__ words) {
+  __shared__ uint32_t s[kPlaneLds];
   const int64_t P = plane_words(Np);
   const int64_t p = (int64_t)blockIdx.x * kPlaneThreads + threadIdx.x;
-  if (p >= P) return;
   uint32_t w[32];
 #pragma unroll
-  for (int r = 0; r < 32; ++r) w[r] = planes[(int64_t)r * P + p];
+  for (int r = 0; r < 32; ++r) w[r] = p < P ? planes[(int64_t)r * P + p] : 0u;
   transpose32(w);
-  const int64_t j0 = 32 * p;
-  if (j0 + 32 <= Np) {
-    uint4* d4 = reinterpret_cast<uint4*>(words + j0);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) d4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-  } else {
+  for (int b = 0; b < 32; ++b) s[threadIdx.x * 33 + b] = w[b];
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kPlaneWords;
 #pragma unroll
-    for (int b = 0; b < 32; ++b)
-      if (j0 + b < Np) words[j0 + b] = w[b];
+  for (int i = 0; i < kPlaneWords / 4 / kPlaneThreads; ++i) {
+    const int wl = 4 * ((int)threadIdx.x + kPlaneThreads * i);
+    uint32_t v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = s[((wl + c) >> 5) * 33 + ((wl + c) & 31)];
+    if (base + wl + 4 <= Np) {
+      *reinterpret_cast<uint4*>(words + base + wl) = make_uint4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (base + wl + c < Np) words[base + wl + c] = v[c];
+    }
   }
 }
 
@@ -1248,15 +1281,17 @@ CHOCO_API int choco_sign_recv_gossip_compress(const int32_t* const* packed_list,
   char* wb = static_cast<char*>(ws) + choco_sign_workspace_size(1);
   const unsigned gp = (unsigned)((P + kPlaneThreads - 1) / kPlaneThreads);
   PlaneMsgs M{};
-  profile_begin("sign_planes", st);
+  PlaneSrc S{};
   for (int q = 0; q < nmsg; ++q) {
     uint32_t* pl = reinterpret_cast<uint32_t*>(wb + (size_t)q * pb);
-    CHOCO_KLAUNCH(sign_to_planes_kernel, dim3(gp), dim3(kPlaneThreads), 0, st,
-                  reinterpret_cast<const uint32_t*>(packed_list[q]), Np, pl);
+    S.words[q] = reinterpret_cast<const uint32_t*>(packed_list[q]);
+    S.planes[q] = pl;
     M.planes[q] = pl;
     M.norms[q] = norms_list[q];
     M.w[q] = weights[q];
   }
+  profile_begin("sign_planes", st);
+  CHOCO_KLAUNCH(sign_to_planes_kernel, dim3(gp, (unsigned)nmsg), dim3(kPlaneThreads), 0, st, S, Np);
   profile_end("sign_planes", st);
   CHOCO_LAUNCHED("sign_to_planes_kernel");
   M.self_slot = self_slot;
