@@ -102,3 +102,58 @@ def test_qsgd_100M_levels_wire_decode():
     assert lvl.max() >= 1  # non-trivial levels are present in the sample
     dec = codec.qsgd_decode(packed, norms, n, q)
     assert same_bits(host(dec[torch.from_numpy(idx).to(DEV)]), O.qsgd_dense(d, s, u, nrm))
+
+
+@pytest.mark.parametrize("nmsg", [1, 3])
+def test_sign_345M_deferred_receive_matches_sequence(nmsg):
+    """cfg 5's deferred receive at full size: choco_sign_recv_gossip_compress (row runs over bit
+    planes) against sign_accumulate + the gossip-fused pack on the same inputs, compared whole on
+    the device -- x, x_hat, memory and the words bit for bit, the L1 norm to rtol 1e-6.  (The
+    sequence itself is pinned against the oracle at small sizes: test_gpu_deferred_receive.py.)"""
+    from chocosgd_amd import codec
+    n = 345_000_000
+    gamma = 0.5
+    msgs = [codec.sign_compress(randn(n, 2100 + q, 0.5)) for q in range(nmsg)]
+    weights = [1.0 / 3.0 + 0.125 * q for q in range(nmsg)]
+    self_slot = nmsg // 2
+    x, xh, mem = randn(n, 2010), randn(n, 2011, 0.25), randn(n, 2012, 0.1)
+    xa, ha, ma = x, xh, mem
+    xb, hb, mb = x.clone(), xh.clone(), mem.clone()
+    codec.sign_accumulate(msgs, weights, self_slot, n, ma, xhat_self=ha)
+    pa, na = codec.sign_compress(xa, xhat=ha, gossip=(ma, gamma))
+    pb, nb = codec.sign_recv_gossip_compress(msgs, weights, self_slot, xb, mb, hb, gamma)
+    assert torch.equal(xb.view(torch.int32), xa.view(torch.int32))
+    assert torch.equal(hb.view(torch.int32), ha.view(torch.int32))
+    assert torch.equal(mb.view(torch.int32), ma.view(torch.int32))
+    assert torch.equal(pb, pa)
+    assert abs(float(nb[0]) - float(na[0])) <= 1e-6 * abs(float(na[0]))
+    del msgs, x, xh, mem, xb, hb, mb
+    codec.release_workspaces()
+    torch.cuda.empty_cache()
+
+
+def test_qsgd_100M_deferred_receive_matches_sequence():
+    """cfg 3's deferred receive at full size (q = 4, three messages): choco_qsgd_recv_gossip_norms
+    against qsgd_accumulate + the consensus step + the norm pass, compared whole on the device --
+    x, x_hat, memory bit for bit, the norm to rtol 1e-6 -- and the next message from either."""
+    from chocosgd_amd import codec
+    n, q, nmsg, gamma = 100_000_000, 4, 3, 0.5
+    msgs = [codec.qsgd_compress(randn(n, 2200 + r), q, seed=r, offset=3)[:2] for r in range(nmsg)]
+    weights = [1.0 / nmsg] * nmsg
+    x, xh, mem = randn(n, 2020), randn(n, 2021, 0.25), randn(n, 2022, 0.1)
+    xa, ha, ma = x, xh, mem
+    xb, hb, mb = x.clone(), xh.clone(), mem.clone()
+    codec.qsgd_accumulate(msgs, weights, 1, n, q, ma, xhat_self=ha)
+    codec.gossip_step(xa, ma, ha, gamma)
+    na = codec.qsgd_norms(xa, xhat=ha)
+    nb = codec.qsgd_recv_gossip_norms(msgs, weights, 1, xb, mb, hb, gamma, q)
+    assert torch.equal(xb.view(torch.int32), xa.view(torch.int32))
+    assert torch.equal(hb.view(torch.int32), ha.view(torch.int32))
+    assert torch.equal(mb.view(torch.int32), ma.view(torch.int32))
+    assert abs(float(nb[0]) - float(na[0])) <= 1e-6 * abs(float(na[0]))
+    pa = codec.qsgd_compress(xa, q, xhat=ha, norm_in=nb, seed=9, offset=1)[0]
+    pb = codec.qsgd_compress(xb, q, xhat=hb, norm_in=nb, seed=9, offset=1)[0]
+    assert torch.equal(pa, pb)
+    del msgs, x, xh, mem, xb, hb, mb
+    codec.release_workspaces()
+    torch.cuda.empty_cache()
