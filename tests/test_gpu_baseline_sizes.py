@@ -104,14 +104,14 @@ def test_qsgd_100M_levels_wire_decode():
     assert same_bits(host(dec[torch.from_numpy(idx).to(DEV)]), O.qsgd_dense(d, s, u, nrm))
 
 
-@pytest.mark.parametrize("nmsg", [1, 3])
-def test_sign_345M_deferred_receive_matches_sequence(nmsg):
+@pytest.mark.parametrize("n,nmsg", [(345_000_000, 1), (345_000_000, 3), ((1 << 30) - 1, 1), (1 << 30, 1)])
+def test_sign_345M_deferred_receive_matches_sequence(n, nmsg):
     """cfg 5's deferred receive at full size: choco_sign_recv_gossip_compress (row runs over bit
     planes) against sign_accumulate + the gossip-fused pack on the same inputs, compared whole on
-    the device -- x, x_hat, memory and the words bit for bit, the L1 norm to rtol 1e-6.  (The
-    sequence itself is pinned against the oracle at small sizes: test_gpu_deferred_receive.py.)"""
+    the device -- x, x_hat, memory and the words bit for bit, the L1 norm to rtol 1e-6; also the
+    largest one-pass size (2^30 - 1: 32-bit buffer offsets) and the first two-kernel one (2^30).
+    (The sequence itself is pinned against the oracle at small sizes: test_gpu_deferred_receive.py.)"""
     from chocosgd_amd import codec
-    n = 345_000_000
     gamma = 0.5
     msgs = [codec.sign_compress(randn(n, 2100 + q, 0.5)) for q in range(nmsg)]
     weights = [1.0 / 3.0 + 0.125 * q for q in range(nmsg)]
