@@ -53,6 +53,9 @@ WORKLOADS = {
     "step_topk": ("topk", 100_000_000, 0.99, "choco_step_gossip_topk_k1pct"),
     "step_sign": ("sign", 345_000_000, None, "choco_step_gossip_sign_norm"),
     "step_qsgd": ("qsgd", 100_000_000, 4, "choco_step_gossip_qsgd_q4"),
+    # the drop-in's per-tensor layout (ResNet-50's 161 tensors, create_optimizer.py:15-24)
+    "step_sign_r50": ("sign", 25_557_032, None, "choco_step_gossip_sign_norm_resnet50_161seg"),
+    "step_qsgd_r50": ("qsgd", 25_557_032, 4, "choco_step_gossip_qsgd_q4_resnet50_161seg"),
 }
 GAMMA = 0.9  # consensus_stepsize (parameters.py:126 default)
 
@@ -160,11 +163,19 @@ class Worker:
         self.fold = bool(args.fold) and self.op == "topk"
         self.fold_mem = self.fold and self.self_slot == 0
         self.plan = None
-        if self.op == "topk_seg":
+        self.seg_off, self.nseg = None, 1  # per-tensor layout of the dense codecs (_r50 workloads)
+        if self.op == "topk_seg" or args.workload.endswith("_r50"):
             with open(os.path.join(ROOT, "tests", "golden", "layouts.json")) as f:
                 lens = json.load(f)["resnet50_imagenet"]
-            self.plan = codec.SegmentPlan(lens, self.param, dev)
             n = sum(lens)
+            if self.op == "topk_seg":
+                self.plan = codec.SegmentPlan(lens, self.param, dev)
+            else:
+                if args.n:
+                    raise SystemExit("--n: not with a per-tensor layout")
+                self.seg_off = torch.tensor([0] + [int(v) for v in torch.tensor(lens).cumsum(0)], dtype=torch.int64,
+                                            device=dev)
+                self.nseg = len(lens)
         self.n = args.n or n
         g = torch.Generator(device=dev).manual_seed(1000 + rank)
         # The worker's delta x - x_hat.  Consecutive steps compress different
@@ -189,13 +200,10 @@ class Worker:
         elif self.op == "topk_seg":
             self.k = self.plan.k_total
             self.msg = torch.empty(2 * self.k, dtype=torch.int32, device=dev)
-        elif self.op == "qsgd":
-            nbytes = codec.qsgd_packed_bytes(self.n, self.param)
-            self.msg = torch.zeros(16 + nbytes, dtype=torch.uint8, device=dev)   # [norm (16 B) | planes]
-            self.wire = (self.msg[16:], self.msg[:4].view(torch.float32)[:1])  # compress writes in place
-        else:
-            self.msg = torch.zeros(4 + codec.sign_words(self.n), dtype=torch.int32, device=dev)
-            self.wire = (self.msg[4:], self.msg[:4].view(torch.float32)[:1])
+        elif self.op == "qsgd":  # [norms (16-B padded) | planes]; compress writes in place
+            self.msg, self.wire = codec.qsgd_wire(self.n, self.param, self.nseg, dev)
+        else:  # [norms (16-B padded) | words]
+            self.msg, self.wire = codec.sign_wire(self.n, self.nseg, dev)
         self.recv = {r: torch.empty_like(self.msg) for r in self.peers}
         # deferred sign receive: this step's words are packed in the pass that reads the previous
         # step's (own) message, so the own message alternates between two buffers
@@ -251,9 +259,10 @@ class Worker:
             c.randk(self.d, self.k, seed=12345 + self.rank, offset=self.step_id,
                     out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]))
         elif self.op == "qsgd":
-            c.qsgd_compress(self.d, self.param, seed=12345 + self.rank, offset=self.step_id, out=self.wire)
+            c.qsgd_compress(self.d, self.param, seed=12345 + self.rank, offset=self.step_id, out=self.wire,
+                            **self._seg())
         else:
-            c.sign_compress(self.d, out=self.wire)
+            c.sign_compress(self.d, out=self.wire, **self._seg())
         self.step_id += 1
 
     def compress_step(self):
@@ -271,20 +280,31 @@ class Worker:
             parts, weights, slot = self.pending
             self.pending = None
             c.qsgd_recv_gossip_norms(parts, weights, slot, self.x, self.mem, self.hat, GAMMA, self.param,
-                                     out=self.wire[1])
+                                     out=self.wire[1], **self._seg())
             c.qsgd_compress(self.x, self.param, xhat=self.hat, norm_in=self.wire[1], seed=12345 + self.rank,
-                            offset=self.step_id, out=self.wire)
+                            offset=self.step_id, out=self.wire, **self._seg())
         elif self.op == "qsgd":
             c.qsgd_compress(self.x, self.param, xhat=self.hat, seed=12345 + self.rank, offset=self.step_id,
-                            gossip=g, out=self.wire)
+                            gossip=g, out=self.wire, **self._seg())
         elif self.pending is not None:  # sign: receive + consensus step + pack, one kernel
             parts, weights, slot = self.pending
             self.pending = None
             self.msg = self.msg_pp[self.step_id % 2]
-            self.wire = (self.msg[4:], self.msg[:4].view(torch.float32)[:1])
-            c.sign_recv_gossip_compress(parts, weights, slot, self.x, self.mem, self.hat, GAMMA, out=self.wire)
+            self.wire = self._parts(self.msg)
+            c.sign_recv_gossip_compress(parts, weights, slot, self.x, self.mem, self.hat, GAMMA, out=self.wire,
+                                        **self._seg())
         else:
-            c.sign_compress(self.x, xhat=self.hat, gossip=g, out=self.wire)
+            c.sign_compress(self.x, xhat=self.hat, gossip=g, out=self.wire, **self._seg())
+
+    def _seg(self):
+        return {"seg_off": self.seg_off, "nseg": self.nseg} if self.nseg > 1 else {}
+
+    def _parts(self, m):
+        """(payload, norms) views of a dense codec's wire message (codec.sign_wire / qsgd_wire)."""
+        hw = self.codec.wire_header_words(self.nseg)
+        if self.op == "qsgd":
+            return m[4 * hw:], m[:4 * hw].view(self.torch.float32)[:self.nseg]
+        return m[hw:], m[:hw].view(self.torch.float32)[:self.nseg]
 
     def _fold_args(self):
         if not self.fold:
@@ -341,17 +361,19 @@ class Worker:
                                       [w for _, _, w in items], self.mem, self_slot=slot,
                                       xhat_self=self.hat if slot >= 0 else None)
         elif self.op == "qsgd":
-            parts = [(m[16:], m[:4].view(torch.float32)[:1]) for m in msgs]
+            parts = [self._parts(m) for m in msgs]
             if self.defer:  # applied by the next step's first pass
                 self.pending = (parts, list(self.weights), self.self_slot)
                 return
-            c.qsgd_accumulate(parts, self.weights, self.self_slot, self.n, self.param, self.mem, xhat_self=self.hat)
+            c.qsgd_accumulate(parts, self.weights, self.self_slot, self.n, self.param, self.mem, xhat_self=self.hat,
+                              **self._seg())
         else:
-            parts = [(m[4:], m[:1].view(torch.float32)) for m in msgs]
+            parts = [self._parts(m) for m in msgs]
             if self.defer:  # applied by the next step's pass
                 self.pending = (parts, list(self.weights), self.self_slot)
                 return
-            c.sign_accumulate(parts, self.weights, self.self_slot, self.n, self.mem, xhat_self=self.hat)
+            c.sign_accumulate(parts, self.weights, self.self_slot, self.n, self.mem, xhat_self=self.hat,
+                              **self._seg())
 
     def step(self):
         self.compress()

@@ -31,9 +31,16 @@ constexpr int kQThreads = 256;
 constexpr int kQPer = 8;                         // elements per thread in the quantize/decode passes
 constexpr int kQTile = kQThreads * kQPer;        // 2048
 // elements per workgroup in the norm pass (a multiple of 8192): 49152 -> ~2040 workgroups
-// at 100M, one round of 8 per CU (r03 A/B: 32768 and 65536 slower)
+// at 100M, one round of 8 per CU (r03 A/B: 32768 and 65536 slower); smaller inputs take
+// smaller tiles down to 8192, so that the grid still has ~2048 workgroups (norm_tile)
 constexpr int kNormTile = 49152;
-static_assert(kNormTile % 8192 == 0, "whole load rounds per norm tile");
+constexpr int kNormTileMin = 8192;
+static int64_t norm_tile(int64_t n) {
+  const int64_t t = (n / 2048 + kNormTileMin - 1) / kNormTileMin * kNormTileMin;  // 100M: 49152
+  return std::min<int64_t>(kNormTile, std::max<int64_t>(kNormTileMin, t));
+}
+constexpr int kNormSegLds = 64;  // a tile spanning fewer segments sums them in LDS first
+static_assert(kNormTile % kNormTileMin == 0 && kNormTileMin % 8192 == 0, "whole load rounds per norm tile");
 constexpr int kQMaxMsg = 8;
 constexpr int kAccRep = 8;  // replicas of the fp64 norm accumulators (the fused receive pass)
 
@@ -104,7 +111,7 @@ __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __res
                                                               const float* __restrict__ xh, int64_t n,
                                                               const int64_t* __restrict__ seg_off, int nseg,
                                                               float* __restrict__ norms_out,
-                                                              QsgdWs* __restrict__ ws, Gossip gs) {
+                                                              QsgdWs* __restrict__ ws, Gossip gs, int64_t tile) {
   static_assert(!GS || XH, "the gossip step needs x_hat");
   // one element's delta (and, GS, its gossip step)
   auto dv = [&](int64_t i) -> float {
@@ -117,51 +124,92 @@ __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __res
   };
   __shared__ int s_seg[2];
   __shared__ double s_red[kQThreads / 64];
+  __shared__ double s_sacc[kNormSegLds];
   __shared__ unsigned int s_flag;
   double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  const int64_t t0 = (int64_t)blockIdx.x * kNormTile;
-  const int64_t t1 = std::min<int64_t>(t0 + kNormTile, n);
-  if (tid == 0) {
-    s_seg[0] = nseg > 1 ? seg_of(seg_off, nseg, t0) : 0;
-    s_seg[1] = nseg > 1 ? seg_of(seg_off, nseg, t1 - 1) : 0;
-  }
-  __syncthreads();
-  const int sg0 = s_seg[0], sg1 = s_seg[1];
-  if (sg0 == sg1) {
-    double p = 0.0;
-    constexpr int U = 8;  // float4 loads in flight per thread
-    if (t1 - t0 == kNormTile) {
-      // full tile: unconditional loads (no branch around a load -> all U stay in flight)
-      for (int64_t e0 = t0 + 4 * tid; e0 < t1; e0 += 4 * kQThreads * U) {
-        float4 a[U];
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = std::min<int64_t>(t0 + tile, n);
+  // The tile's first and last segments (binary searches by one thread; a full tile looks them
+  // up while its first loads are in flight).  A uniform tile sums per thread; otherwise each
+  // thread follows the segment of its current element (its elements ascend) with a running
+  // sum, added to the tile's LDS sums (or the global ones) at each boundary.
+  int sg0 = 0, sg1 = 0, s = 0;
+  bool uniform = true, lds = true;  // workgroup-uniform
+  int64_t s_end = t1;
+  double p = 0.0, run_p = 0.0;
+  auto lookup = [&]() {
+    if (tid == 0) {
+      s_seg[0] = nseg > 1 ? seg_of(seg_off, nseg, t0) : 0;
+      s_seg[1] = nseg > 1 ? seg_of(seg_off, nseg, t1 - 1) : 0;
+    }
+    if (tid < kNormSegLds) s_sacc[tid] = 0.0;
+    __syncthreads();
+    sg0 = s_seg[0];
+    sg1 = s_seg[1];
+    uniform = sg0 == sg1;
+    lds = sg1 - sg0 < kNormSegLds;
+    s = sg0;
+    s_end = uniform ? t1 : seg_off[sg0 + 1];
+  };
+  auto flush = [&]() {
+    if (run_p != 0.0) {
+      if (lds) atomicAdd(&s_sacc[s - sg0], run_p);
+      else unsafeAtomicAdd(&acc[s], run_p);
+    }
+    run_p = 0.0;
+  };
+  auto add4 = [&](int64_t e, const float4& a) {
+    if (uniform) {
+      p += (double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z + (double)a.w * a.w;
+      return;
+    }
+    const float av[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
-        for (int u = 0; u < U; ++u) a[u] = ld_norm4(x + e0 + (int64_t)u * 4 * kQThreads);
-        if (GS) {
-          float4 h[U], m[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) m[u] = ld_norm4(gs.mem + e0 + (int64_t)u * 4 * kQThreads);
-#pragma unroll
-          for (int u = 0; u < U; ++u) h[u] = ld_gs4(xh + e0 + (int64_t)u * 4 * kQThreads);
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const float4 xn = gossip4(a[u], m[u], h[u], gs.gamma);
-            st_gs4(const_cast<float*>(x) + e0 + (int64_t)u * 4 * kQThreads, xn);
-            a[u] = sub4(xn, h[u]);
-          }
-        } else if (XH) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const float4 h = ld_norm4(xh + e0 + (int64_t)u * 4 * kQThreads);
-            a[u].x -= h.x; a[u].y -= h.y; a[u].z -= h.z; a[u].w -= h.w;
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          p += (double)a[u].x * a[u].x + (double)a[u].y * a[u].y + (double)a[u].z * a[u].z +
-               (double)a[u].w * a[u].w;
+    for (int c = 0; c < 4; ++c) {
+      if (e + c >= t1) break;
+      if (e + c >= s_end) {
+        flush();
+        do {
+          ++s;
+          s_end = seg_off[s + 1];
+        } while (e + c >= s_end);
       }
-    } else
+      run_p += (double)av[c] * av[c];
+    }
+  };
+  constexpr int U = 8;  // float4 loads in flight per thread
+  if (t1 - t0 == tile) {
+    // full tile: unconditional loads (no branch around a load -> all U stay in flight)
+    for (int64_t e0 = t0 + 4 * tid; e0 < t1; e0 += 4 * kQThreads * U) {
+      float4 a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) a[u] = ld_norm4(x + e0 + (int64_t)u * 4 * kQThreads);
+      if (e0 == t0 + 4 * tid) lookup();  // first round (every thread of a full tile runs the same rounds)
+      if (GS) {
+        float4 h[U], m[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) m[u] = ld_norm4(gs.mem + e0 + (int64_t)u * 4 * kQThreads);
+#pragma unroll
+        for (int u = 0; u < U; ++u) h[u] = ld_gs4(xh + e0 + (int64_t)u * 4 * kQThreads);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float4 xn = gossip4(a[u], m[u], h[u], gs.gamma);
+          st_gs4(const_cast<float*>(x) + e0 + (int64_t)u * 4 * kQThreads, xn);
+          a[u] = sub4(xn, h[u]);
+        }
+      } else if (XH) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float4 h = ld_norm4(xh + e0 + (int64_t)u * 4 * kQThreads);
+          a[u].x -= h.x; a[u].y -= h.y; a[u].z -= h.z; a[u].w -= h.w;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) add4(e0 + (int64_t)u * 4 * kQThreads, a[u]);
+    }
+  } else {
+    lookup();
     for (int64_t e0 = t0 + 4 * tid; e0 < t1; e0 += 4 * kQThreads * U) {
       float4 a[U];
 #pragma unroll
@@ -180,10 +228,10 @@ __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __res
         }
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        p += (double)a[u].x * a[u].x + (double)a[u].y * a[u].y + (double)a[u].z * a[u].z +
-             (double)a[u].w * a[u].w;
+      for (int u = 0; u < U; ++u) add4(e0 + (int64_t)u * 4 * kQThreads, a[u]);
     }
+  }
+  if (uniform) {
     p = wave_sum(p);
     if (lane == 0) s_red[w] = p;
     __syncthreads();
@@ -193,36 +241,10 @@ __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __res
       if (t != 0.0) unsafeAtomicAdd(&acc[sg0], t);
     }
   } else {
-    // segment boundaries inside the tile: per-wave segmented reduction
-    for (int64_t base = t0 + 256 * w; base < t1; base += 256 * (kQThreads / 64)) {
-      const int64_t e = base + 4 * lane;
-      double v[4];
-      int sg[4];
-      int lo = 0x7fffffff, hi = -1;
-      for (int c = 0; c < 4; ++c) {
-        sg[c] = -1;
-        v[c] = 0.0;
-        if (e + c < t1) {
-          const double d = dv(e + c);
-          v[c] = d * d;
-          int s = sg0;
-          while (s + 1 < nseg && seg_off[s + 1] <= e + c) ++s;
-          sg[c] = s;
-          lo = min(lo, s);
-          hi = max(hi, s);
-        }
-      }
-      for (int o = 32; o > 0; o >>= 1) {
-        lo = min(lo, __shfl_xor(lo, o));
-        hi = max(hi, __shfl_xor(hi, o));
-      }
-      for (int q = lo; q <= hi; ++q) {
-        double p = 0.0;
-        for (int c = 0; c < 4; ++c)
-          if (sg[c] == q) p += v[c];
-        p = wave_sum(p);
-        if (lane == 0 && p != 0.0) unsafeAtomicAdd(&acc[q], p);
-      }
+    flush();
+    if (lds) {
+      __syncthreads();
+      if (tid <= sg1 - sg0 && s_sacc[tid] != 0.0) unsafeAtomicAdd(&acc[sg0 + tid], s_sacc[tid]);
     }
   }
   if (last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
@@ -915,18 +937,19 @@ static int qsgd_norms_launch(const float* x, const float* xhat, int64_t n, const
   CHOCO_REQUIRE(!gs.mem || (xhat && aligned16(gs.mem)), "the gossip step needs x_hat and a 16-byte aligned memory");
   CHOCO_REQUIRE(norms_out, "norms_out is required when norm_in is NULL");
   CHOCO_REQUIRE(ws && ws_bytes >= choco_qsgd_workspace_size(nseg), "qsgd workspace too small");
-  const unsigned g1 = (unsigned)((n + kNormTile - 1) / kNormTile);
+  const int64_t tile = norm_tile(n);
+  const unsigned g1 = (unsigned)((n + tile - 1) / tile);
   QsgdWs* w = static_cast<QsgdWs*>(ws);
   profile_begin("qsgd_norm", st);
   if (gs.mem)
     CHOCO_KLAUNCH((qsgd_norm_kernel<true, true>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
-                  norms_out, w, gs);
+                  norms_out, w, gs, tile);
   else if (xhat)
     CHOCO_KLAUNCH((qsgd_norm_kernel<true>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
-                  norms_out, w, gs);
+                  norms_out, w, gs, tile);
   else
     CHOCO_KLAUNCH((qsgd_norm_kernel<false>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
-                  norms_out, w, gs);
+                  norms_out, w, gs, tile);
   profile_end("qsgd_norm", st);
   CHOCO_LAUNCHED("qsgd_norm_kernel");
   return CHOCO_OK;

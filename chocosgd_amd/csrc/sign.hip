@@ -155,8 +155,6 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
   const int64_t J0 = (blk0 + (int64_t)blockIdx.x) * kSignCols;
   const int64_t j0 = J0 + 256 * w;
   const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
-  if (NORM) row_segments(seg_off, nseg, n, Np, J0, s_lo, s_hi);
-  __syncthreads();
 
   uint32_t wd[4] = {0u, 0u, 0u, 0u};
   // Interior workgroups (every row run, incl. the tail float4, inside [0, n)) use
@@ -205,6 +203,11 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
         }
       }
     }
+  }
+  if (r0 == 0) {
+    // the rows' segments, looked up (binary searches) while the first group's loads are in flight
+    if (NORM) row_segments(seg_off, nseg, n, Np, J0, s_lo, s_hi);
+    __syncthreads();
   }
 #pragma unroll
   for (int u = 0; u < RU; ++u) {
@@ -323,21 +326,32 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
 
 // GS: the fused gossip step -- x, memory and xh rows in flight, x_new stored back
 // (each lane owns its float4 of every row run: no overlap), d = x_new - xh.
-template <bool XH, bool NORM, bool GS = false>
+// SEG (per-tensor norms, NORM only): the 32 rows' segments over the workgroup's 1024
+// columns are looked up while the first two groups' loads are in flight; a lane keeps one
+// running sum while consecutive rows stay in one segment, and a wave sum goes to the
+// workgroup's LDS per-segment sums when the segment changes (a row across a boundary: one
+// wave sum per segment in it); the workgroup adds its LDS sums to the global ones.
+constexpr int kPackSegLds = 1024;  // segments of one workgroup's rows summed in LDS (more: global atomics)
+template <bool XH, bool NORM, bool GS = false, bool SEG = false, int RUV = 0>
 __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* __restrict__ x,
                                                                   const float* __restrict__ xh, int64_t n,
                                                                   int64_t Np, uint32_t* __restrict__ packed,
                                                                   float* __restrict__ l1_out,
                                                                   SignWs* __restrict__ ws, Gossip gs, int64_t blk0,
-                                                                  int finish) {
+                                                                  int finish, const int64_t* __restrict__ seg_off,
+                                                                  int nseg) {
   static_assert(!GS || XH, "the gossip step needs x_hat");
-  constexpr int RU = GS ? 8 : (XH ? 4 : 8);  // rows per group (more streams, more registers)
+  static_assert(!SEG || NORM, "segments only matter to the norms");
+  constexpr int RU = RUV ? RUV : (GS ? 8 : (XH ? 4 : 8));  // rows per group (more streams, more registers)
   constexpr int NG = 32 / RU;
   __shared__ double s_red[kSignThreads / 64];
   __shared__ unsigned int s_flag;
+  __shared__ int s_lo[SEG ? 32 : 1], s_hi[SEG ? 32 : 1];
+  __shared__ double s_sacc[SEG ? kPackSegLds : 1];
   double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
   const int lane = lane_id(), w = threadIdx.x >> 6;
-  const int64_t j0 = (blk0 + (int64_t)blockIdx.x) * kSignCols + 256 * w;
+  const int64_t J0 = (blk0 + (int64_t)blockIdx.x) * kSignCols;
+  const int64_t j0 = J0 + 256 * w;
   const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
   // every row run of the wave (row 31's last float4 included) lies inside [0, n)
   const bool interior = ncol == 256 && (int64_t)31 * Np + j0 + 256 <= n;
@@ -366,6 +380,72 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
   };
   uint32_t wd[4] = {0u, 0u, 0u, 0u};
   double p = 0.0;
+  // SEG: the rows' segments (s_lo / s_hi), the workgroup's first one and whether its
+  // segment span fits the LDS sums; a lane's running sum belongs to segment `cur`
+  int sbase = 0;
+  bool slds = true;
+  int cur = -1;
+  auto seg_lookup = [&]() {
+    if (SEG) {
+      row_segments(seg_off, nseg, n, Np, J0, s_lo, s_hi);
+      __syncthreads();
+      int lo = s_lo[0] >= 0 ? s_lo[0] : 0, hi = 0;
+      for (int r = 31; r >= 0; --r)
+        if (s_hi[r] >= 0) { hi = s_hi[r]; break; }
+      sbase = lo;
+      slds = hi - lo < kPackSegLds;
+      if (slds)
+        for (int i = threadIdx.x; i <= hi - lo; i += kSignThreads) s_sacc[i] = 0.0;
+      __syncthreads();
+    }
+  };
+  auto seg_add = [&](int sg, double v) {  // lane 0 of a wave
+    if (v == 0.0) return;
+    if (slds) atomicAdd(&s_sacc[sg - sbase], v);
+    else unsafeAtomicAdd(&acc[sg], v);
+  };
+  auto seg_flush = [&]() {  // wave-uniform
+    if (cur >= 0) {
+      const double t = wave_sum(p);
+      if (lane == 0) seg_add(cur, t);
+    }
+    p = 0.0;
+  };
+  // one row's |d| (valid elements only) into the norms
+  auto seg_row = [&](int r, const float (&v)[4], uint32_t valid) {
+    if (!SEG) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if ((valid >> c) & 1u) p += (double)fabsf(v[c]);
+      return;
+    }
+    const int lo = s_lo[r], hi = s_hi[r];
+    if (lo < 0) return;  // (a row run past n)
+    if (lo == hi) {      // wave-uniform
+      if (lo != cur) {
+        seg_flush();
+        cur = lo;
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if ((valid >> c) & 1u) p += (double)fabsf(v[c]);
+      return;
+    }
+    seg_flush();
+    cur = -1;
+    const int64_t e = (int64_t)r * Np + j0 + 4 * lane;
+    int sg[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) sg[c] = ((valid >> c) & 1u) ? seg_walk(seg_off, nseg, lo, e + c) : -1;
+    for (int q = lo; q <= hi; ++q) {
+      double t = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (sg[c] == q) t += (double)fabsf(v[c]);
+      t = wave_sum(t);
+      if (lane == 0) seg_add(q, t);
+    }
+  };
   auto proc_group = [&](int g, Group& G) {
     if (GS) {
 #pragma unroll
@@ -383,7 +463,10 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
       const float v[4] = {R.x, R.y, R.z, R.w};
 #pragma unroll
       for (int c = 0; c < 4; ++c) wd[c] |= (v[c] < 0.f ? 1u : 0u) << r;
-      if (NORM) p += ((double)fabsf(v[0]) + (double)fabsf(v[1])) + ((double)fabsf(v[2]) + (double)fabsf(v[3]));
+      if (NORM) {
+        if (SEG) seg_row(r, v, 15u);
+        else p += ((double)fabsf(v[0]) + (double)fabsf(v[1])) + ((double)fabsf(v[2]) + (double)fabsf(v[3]));
+      }
       __builtin_amdgcn_sched_barrier(0);  // row by row: hoisted fp64 conversions of a whole group cost registers
     }
   };
@@ -393,6 +476,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
     Group A, B;
     load_group(0, A);
     load_group(1, B);
+    seg_lookup();
 #pragma unroll
     for (int g = 0; g < NG; g += 2) {
       proc_group(g, A);
@@ -402,6 +486,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
     }
   } else {
     // the last workgroups: guarded element loads, one row at a time
+    seg_lookup();
 #pragma unroll 1
     for (int r = 0; r < 32; ++r) {
       const int64_t s = (int64_t)r * Np + j0 + 4 * lane;
@@ -422,7 +507,16 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c) wd[c] |= (tt[c] < 0.f ? 1u : 0u) << r;
-      if (NORM) p += ((double)fabsf(tt[0]) + (double)fabsf(tt[1])) + ((double)fabsf(tt[2]) + (double)fabsf(tt[3]));
+      if (NORM) {
+        if (SEG) {
+          uint32_t valid = 0;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) valid |= (4 * lane + c < ncol && s + c < n ? 1u : 0u) << c;
+          seg_row(r, tt, valid);
+        } else {
+          p += ((double)fabsf(tt[0]) + (double)fabsf(tt[1])) + ((double)fabsf(tt[2]) + (double)fabsf(tt[3]));
+        }
+      }
     }
   }
   {
@@ -435,7 +529,21 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
         if (j + c < Np) packed[j + c] = wd[c];
     }
   }
-  if (NORM) {
+  if (NORM && SEG) {
+    seg_flush();
+    __syncthreads();
+    if (slds) {
+      int hi = 0;
+      for (int r = 31; r >= 0; --r)
+        if (s_hi[r] >= 0) { hi = s_hi[r]; break; }
+      for (int i = threadIdx.x; i <= hi - sbase; i += kSignThreads)
+        if (s_sacc[i] != 0.0) unsafeAtomicAdd(&acc[sbase + i], s_sacc[i]);
+    }
+    if (finish && last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
+      for (int q = threadIdx.x; q < nseg; q += kSignThreads) l1_out[q] = (float)atomic_exchange_double(&acc[q], 0.0);
+      if (threadIdx.x == 0) __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else if (NORM) {
     p = wave_sum(p);
     if (lane == 0) s_red[w] = p;
     __syncthreads();
@@ -836,6 +944,8 @@ CHOCO_DEV void words_to_lds(const uint32_t* __restrict__ words, int64_t Np, int6
 struct PlaneSrc {
   const uint32_t* words[kMaxMsg];
   uint32_t* planes[kMaxMsg];
+  double* acc;  // the receive's fp64 accumulators, zeroed here: their place in the workspace
+  int nacc;     // moves with nseg, so an earlier call's planes may lie where they are now
 };
 
 // words (Np) -> planes [32][P] of message blockIdx.y
@@ -843,6 +953,8 @@ __global__ __launch_bounds__(kPlaneThreads) void sign_to_planes_kernel(PlaneSrc 
   __shared__ uint32_t s[kPlaneLds];
   const int64_t P = plane_words(Np);
   const int64_t base = (int64_t)blockIdx.x * kPlaneWords;
+  if (blockIdx.x == 0 && blockIdx.y == 0)
+    for (int i = threadIdx.x; i < S.nacc; i += kPlaneThreads) S.acc[i] = 0.0;
   words_to_lds(S.words[blockIdx.y], Np, base, s);
   __syncthreads();
   uint32_t w[32];
@@ -894,7 +1006,8 @@ struct PlaneMsgs {
   int self_slot;
 };
 
-constexpr int kRowRep = 8;  // replicas of the fp64 L1 accumulator
+constexpr int kRowRep = 8;      // replicas of the fp64 L1 accumulators (workgroup b -> replica b & 7)
+constexpr int kRowSegLds = 64;  // a run spanning fewer segments sums them in LDS first
 // Workgroup i <-> run i, row-major over the (32, N') view, i.e. the flat element order: row
 // r = i / nrun, columns [J, J + 4096) with J = (i % nrun) * 4096.  Thread t takes the float4
 // at columns J + 1024 c + 4 t (c = 0..3): every load and store instruction of a wave is one
@@ -908,24 +1021,38 @@ constexpr int kRowRep = 8;  // replicas of the fp64 L1 accumulator
 // grid-stride loop 1.915 / 1.914 (non-temporal 1.994 / 2.036; 1024 workgroups 2.033 /
 // 2.030); round 5's column-tile receive (32 rows of a 1024-word block per workgroup,
 // non-temporal, 8 rows in flight) 1.983 / 1.984: removed, git history r05.
-template <int NM, bool HS>
+// SEG (per-tensor layouts, create_optimizer.py:15-24): element e decodes with its segment's
+// norm / numel (seg_scale) and adds |d| to its segment's L1 sum.  The run's first and last
+// segments are looked up (binary search) while its loads are in flight; a run inside one
+// segment (nearly all of them) runs the flat code with that segment's scales, a run across
+// boundaries walks them per element and sums per segment (in LDS when it spans fewer than
+// kRowSegLds segments).
+template <int NM, bool HS, bool SEG>
 __global__ __launch_bounds__(kSignThreads) void sign_recv_rows_kernel(PlaneMsgs M, float* __restrict__ x,
                                                                       float* __restrict__ xh,
                                                                       float* __restrict__ mem, float gamma,
                                                                       int64_t n, int64_t Np,
+                                                                      const int64_t* __restrict__ seg_off, int nseg,
                                                                       uint32_t* __restrict__ out_planes,
                                                                       float* __restrict__ l1_out,
                                                                       SignWs* __restrict__ ws) {
   __shared__ double s_red[kSignThreads / 64];
+  __shared__ double s_sacc[SEG ? kRowSegLds : 1];
+  __shared__ int s_seg[2];
   __shared__ unsigned int s_flag;
   double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
+  double* __restrict__ rep = acc + (size_t)(blockIdx.x & (kRowRep - 1)) * (size_t)(SEG ? nseg : 1);
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const int64_t P = plane_words(Np);
   const int64_t nrun = (Np + kRowRun - 1) / kRowRun;
   const uint32_t nib_sh = 4u * (uint32_t)(tid & 7);
   float sc[NM];
+  if (!SEG) {
 #pragma unroll
-  for (int q = 0; q < NM; ++q) sc[q] = M.norms[q][0] / (float)n;
+    for (int q = 0; q < NM; ++q) sc[q] = M.norms[q][0] / (float)n;
+  }
+  int s0 = 0, s1 = 0;  // SEG: the run's first and last segments
+  bool uni = true;     // the run inside one segment (workgroup-uniform)
   const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x, (uint32_t)(n * 4));
   const __amdgpu_buffer_rsrc_t rh = buf_rsrc(xh, (uint32_t)(n * 4));
   const __amdgpu_buffer_rsrc_t rm = buf_rsrc(mem, (uint32_t)(n * 4));
@@ -969,6 +1096,25 @@ __global__ __launch_bounds__(kSignThreads) void sign_recv_rows_kernel(PlaneMsgs 
         mv[c] = make_float4(tm[0], tm[1], tm[2], tm[3]);
       }
     }
+    int64_t s_beg = 0, s_end = n;  // SEG: the current segment's [start, end)
+    if (SEG) {
+      if (tid == 0) {
+        const int64_t elast = std::min<int64_t>(e0 + std::min<int64_t>(kRowRun, Np - J), n) - 1;
+        s_seg[0] = e0 < n ? seg_of(seg_off, nseg, e0) : 0;
+        s_seg[1] = e0 < n ? seg_of(seg_off, nseg, elast) : 0;
+      }
+      if (tid < kRowSegLds) s_sacc[tid] = 0.0;
+      __syncthreads();
+      s0 = s_seg[0];
+      s1 = s_seg[1];
+      s_beg = seg_off[s0];
+      s_end = seg_off[s0 + 1];
+#pragma unroll
+      for (int q = 0; q < NM; ++q) sc[q] = M.norms[q][s0] / (float)(s_end - s_beg);  // seg_scale
+    }
+    uni = !SEG || s0 == s1;
+    int s = s0, run_s = -1;
+    double run_p = 0.0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       float a[4] = {xv[c].x, xv[c].y, xv[c].z, xv[c].w};
@@ -977,6 +1123,17 @@ __global__ __launch_bounds__(kSignThreads) void sign_recv_rows_kernel(PlaneMsgs 
       uint32_t nib = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
+        const int64_t jj = J + 1024 * c + 4 * tid + k;
+        const bool in = full || (jj < Np && e0 - J + jj < n);
+        if (SEG && !uni && in && e0 - J + jj >= s_end) {  // the next segment(s) (increasing e)
+          do {
+            ++s;
+            s_beg = s_end;
+            s_end = seg_off[s + 1];
+          } while (e0 - J + jj >= s_end);
+#pragma unroll
+          for (int q = 0; q < NM; ++q) sc[q] = M.norms[q][s] / (float)(s_end - s_beg);
+        }
 #pragma unroll
         for (int q = 0; q < NM; ++q) {
           const float u = ((bits[c][q] >> k) & 1u) ? -sc[q] : sc[q];
@@ -985,10 +1142,22 @@ __global__ __launch_bounds__(kSignThreads) void sign_recv_rows_kernel(PlaneMsgs 
         }
         a[k] = gossip1(a[k], m[k], h[k], gamma);
         const float d = a[k] - h[k];
-        const int64_t jj = J + 1024 * c + 4 * tid + k;
-        const bool in = full || (jj < Np && e0 - J + jj < n);
         nib |= (in && d < 0.f ? 1u : 0u) << k;
-        if (in) p += (double)fabsf(d);
+        if (in) {
+          if (uni) {
+            p += (double)fabsf(d);
+          } else {
+            if (s != run_s) {
+              if (run_s >= 0 && run_p != 0.0) {
+                if (s1 - s0 < kRowSegLds) atomicAdd(&s_sacc[run_s - s0], run_p);
+                else unsafeAtomicAdd(&rep[run_s], run_p);
+              }
+              run_s = s;
+              run_p = 0.0;
+            }
+            run_p += (double)fabsf(d);
+          }
+        }
       }
       xv[c] = make_float4(a[0], a[1], a[2], a[3]);
       hv[c] = make_float4(h[0], h[1], h[2], h[3]);
@@ -1025,24 +1194,35 @@ __global__ __launch_bounds__(kSignThreads) void sign_recv_rows_kernel(PlaneMsgs 
         }
       }
     }
+    if (SEG && !uni) {  // workgroup-uniform
+      if (run_s >= 0 && run_p != 0.0) {
+        if (s1 - s0 < kRowSegLds) atomicAdd(&s_sacc[run_s - s0], run_p);
+        else unsafeAtomicAdd(&rep[run_s], run_p);
+      }
+      __syncthreads();
+      if (s1 - s0 < kRowSegLds && tid <= s1 - s0 && s_sacc[tid] != 0.0) unsafeAtomicAdd(&rep[s0 + tid], s_sacc[tid]);
+    }
   }
-  // the L1 norm: fp64 per thread, per workgroup, one of kRowRep replicas
-  p = wave_sum(p);
-  if (lane == 0) s_red[wv] = p;
-  __syncthreads();
-  if (tid == 0) {
-    double t = 0.0;
-#pragma unroll
-    for (int i = 0; i < kSignThreads / 64; ++i) t += s_red[i];
-    if (t != 0.0) unsafeAtomicAdd(&acc[blockIdx.x & (kRowRep - 1)], t);
-  }
-  if (last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
+  // the L1 norm: fp64 per thread, per workgroup, into one of kRowRep replicas
+  if (uni) {  // workgroup-uniform
+    p = wave_sum(p);
+    if (lane == 0) s_red[wv] = p;
+    __syncthreads();
     if (tid == 0) {
       double t = 0.0;
-      for (int i = 0; i < kRowRep; ++i) t += atomic_exchange_double(&acc[i], 0.0);
-      l1_out[0] = (float)t;
-      __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int i = 0; i < kSignThreads / 64; ++i) t += s_red[i];
+      if (t != 0.0) unsafeAtomicAdd(&rep[s0], t);
     }
+  }
+  if (last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
+    const int ns = SEG ? nseg : 1;
+    for (int q = tid; q < ns; q += kSignThreads) {
+      double t = 0.0;
+      for (int i = 0; i < kRowRep; ++i) t += atomic_exchange_double(&acc[(size_t)i * ns + q], 0.0);
+      l1_out[q] = (float)t;
+    }
+    if (tid == 0) __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1091,13 +1271,28 @@ CHOCO_API size_t choco_sign_workspace_size(int32_t nseg) {
   return 256 + align_up((size_t)(nseg > 0 ? nseg : 1) * sizeof(double), 256);
 }
 
+// Same-box A/B, ResNet-50 layout (25.6M, 161 tensors; 780 workgroups), fused step: 4-row groups
+// 112.5 / 112.3 us against 135.3 / 134.7 in 8-row groups (profiles/r05_ab_summary.txt item 16)
+constexpr int kPackSmallGrid = 2048;
 template <bool XH, bool NORM, bool GS>
 static void launch_pack(bool one, unsigned grid, hipStream_t st, const float* x, const float* xhat, int64_t n,
                         int64_t Np, const int64_t* seg_off, int32_t nseg, uint32_t* pk, float* l1, SignWs* w,
                         Gossip gs, int64_t blk0, int finish) {
-  if (one)
-    CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, pk, l1,
-                  w, gs, blk0, finish);
+  // a grid of under kPackSmallGrid workgroups (the ~25M-element buffers of one model) runs the
+  // fused step in groups of 4 rows: more waves per CU instead of more rows in flight per wave
+  const bool small = GS && grid < (unsigned)kPackSmallGrid;
+  if (one && small && NORM && nseg > 1)
+    CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS, NORM, 4>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
+                  pk, l1, w, gs, blk0, finish, seg_off, nseg);
+  else if (one && small)
+    CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS, false, 4>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
+                  pk, l1, w, gs, blk0, finish, seg_off, nseg);
+  else if (one && NORM && nseg > 1)
+    CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS, NORM>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, pk,
+                  l1, w, gs, blk0, finish, seg_off, nseg);
+  else if (one)
+    CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS, false>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, pk,
+                  l1, w, gs, blk0, finish, seg_off, nseg);
   else
     CHOCO_KLAUNCH((sign_pack_kernel<XH, NORM, GS>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, seg_off,
                   nseg, pk, l1, w, gs, blk0, finish);
@@ -1126,7 +1321,7 @@ static int sign_compress(const float* x, const float* xhat, int64_t n, const int
   if (l1_norms) {
     CHOCO_REQUIRE(ws && ws_bytes >= choco_sign_workspace_size(nseg), "sign workspace too small");
   }
-  const bool one = nseg == 1 && n < (int64_t(1) << 30);  // one segment, buffer offsets: n * 4 < 2^32 bytes
+  const bool one = n < (int64_t(1) << 30);  // the one-pass column kernel: buffer offsets, n * 4 < 2^32 bytes
   const int fin = finish ? 1 : 0;
   profile_begin("sign_pack", st);
   if (gs.mem) {
@@ -1237,11 +1432,17 @@ CHOCO_API int choco_sign_decompress_accumulate(const int32_t* const* packed_list
   return CHOCO_OK;
 }
 
+// ticket block, kRowRep replicas of the per-segment fp64 L1 sums, then the bit planes of the
+// messages and of the output (sign_recv_rows_kernel)
+static size_t sign_recv_acc_bytes(int32_t nseg) {
+  return 256 + align_up((size_t)kRowRep * (size_t)(nseg > 0 ? nseg : 1) * sizeof(double), 256);
+}
+
 CHOCO_API size_t choco_sign_recv_workspace_size(int64_t n, int32_t nseg, int32_t nmsg) {
-  if (nseg > 1 || n >= (int64_t(1) << 30)) return choco_sign_workspace_size(nseg);  // the two-kernel form
+  if (n >= (int64_t(1) << 30)) return choco_sign_workspace_size(nseg);  // the two-kernel form
   const int64_t Np = choco_sign_words(n > 0 ? n : 1);
   const size_t pb = align_up((size_t)32 * (size_t)plane_words(Np) * 4, 256);
-  return choco_sign_workspace_size(1) + (size_t)((nmsg > 0 ? nmsg : 1) + 1) * pb;
+  return sign_recv_acc_bytes(nseg) + (size_t)((nmsg > 0 ? nmsg : 1) + 1) * pb;
 }
 
 CHOCO_API int choco_sign_recv_gossip_compress(const int32_t* const* packed_list, const float* const* norms_list,
@@ -1263,8 +1464,9 @@ CHOCO_API int choco_sign_recv_gossip_compress(const int32_t* const* packed_list,
     CHOCO_REQUIRE(packed_list[q] && norms_list[q], "null message pointer");
     CHOCO_REQUIRE(packed_list[q] != packed, "the output words must not alias a message being applied");
   }
-  const bool one = nseg == 1 && n < (int64_t(1) << 30);
-  if (!one) {  // segmented layouts: the receive and the fused consensus step + pack as two kernels
+  if (n >= (int64_t(1) << 30)) {  // past 32-bit buffer offsets: the receive, then the fused consensus step + pack
+    // (the pack's accumulators may hold an earlier row-run call's planes: zero them)
+    CHOCO_HIP(hipMemsetAsync(static_cast<char*>(ws) + 256, 0, (size_t)nseg * sizeof(double), st));
     int rc = choco_sign_decompress_accumulate(packed_list, norms_list, weights, nmsg, self_slot, n, seg_off, nseg,
                                               self_slot >= 0 ? xhat : nullptr, memory, nullptr, 0, stream);
     if (rc != CHOCO_OK) return rc;
@@ -1278,10 +1480,12 @@ CHOCO_API int choco_sign_recv_gossip_compress(const int32_t* const* packed_list,
                 "sign receive workspace too small: need choco_sign_recv_workspace_size(n, nseg, nmsg) bytes");
   const int64_t P = plane_words(Np);
   const size_t pb = align_up((size_t)32 * (size_t)P * 4, 256);
-  char* wb = static_cast<char*>(ws) + choco_sign_workspace_size(1);
+  char* wb = static_cast<char*>(ws) + sign_recv_acc_bytes(nseg);
   const unsigned gp = (unsigned)((P + kPlaneThreads - 1) / kPlaneThreads);
   PlaneMsgs M{};
   PlaneSrc S{};
+  S.acc = reinterpret_cast<double*>(static_cast<char*>(ws) + 256);
+  S.nacc = kRowRep * nseg;
   for (int q = 0; q < nmsg; ++q) {
     uint32_t* pl = reinterpret_cast<uint32_t*>(wb + (size_t)q * pb);
     S.words[q] = reinterpret_cast<const uint32_t*>(packed_list[q]);
@@ -1298,14 +1502,22 @@ CHOCO_API int choco_sign_recv_gossip_compress(const int32_t* const* packed_list,
   uint32_t* outp = reinterpret_cast<uint32_t*>(wb + (size_t)nmsg * pb);
   const unsigned grid = (unsigned)(32 * ((Np + kRowRun - 1) / kRowRun));  // one workgroup per run
   profile_begin("sign_recv_pack", st);
-#define CHOCO_SRR_CASE(NM)                                                                               \
-  case NM:                                                                                               \
-    if (self_slot >= 0)                                                                                  \
-      CHOCO_KLAUNCH((sign_recv_rows_kernel<NM, true>), dim3(grid), dim3(kSignThreads), 0, st, M, x, xhat, \
-                    memory, gamma, n, Np, outp, l1_norms, w);                                            \
-    else                                                                                                 \
-      CHOCO_KLAUNCH((sign_recv_rows_kernel<NM, false>), dim3(grid), dim3(kSignThreads), 0, st, M, x,      \
-                    xhat, memory, gamma, n, Np, outp, l1_norms, w);                                      \
+#define CHOCO_SRR_LAUNCH(NM, HS, SEG)                                                                    \
+  CHOCO_KLAUNCH((sign_recv_rows_kernel<NM, HS, SEG>), dim3(grid), dim3(kSignThreads), 0, st, M, x, xhat, memory, \
+                gamma, n, Np, seg_off, nseg, outp, l1_norms, w)
+#define CHOCO_SRR_CASE(NM)                         \
+  case NM:                                         \
+    if (nseg > 1) {                                \
+      if (self_slot >= 0)                          \
+        CHOCO_SRR_LAUNCH(NM, true, true);          \
+      else                                         \
+        CHOCO_SRR_LAUNCH(NM, false, true);         \
+    } else {                                       \
+      if (self_slot >= 0)                          \
+        CHOCO_SRR_LAUNCH(NM, true, false);         \
+      else                                         \
+        CHOCO_SRR_LAUNCH(NM, false, false);        \
+    }                                              \
     break;
   switch (nmsg) {
     CHOCO_SRR_CASE(1)
@@ -1318,6 +1530,7 @@ CHOCO_API int choco_sign_recv_gossip_compress(const int32_t* const* packed_list,
     CHOCO_SRR_CASE(8)
   }
 #undef CHOCO_SRR_CASE
+#undef CHOCO_SRR_LAUNCH
   profile_end("sign_recv_pack", st);
   CHOCO_LAUNCHED("sign_recv_rows_kernel");
   profile_begin("sign_planes", st);

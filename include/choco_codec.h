@@ -278,15 +278,15 @@ int choco_sign_decompress_accumulate(const int32_t* const* packed_list,
  * fmaf(w, u, memory) in order; CHOCOSignCompressor.uncompress, parallel_choco_v.py:
  * 548-558), then this step's consensus step x += gamma (memory - x_hat) (optim/utils.py:
  * 67-72), then this step's message: packed signs of x - x_hat and l1_norms[s] -- ONE pass
- * over x, x_hat and memory (nseg == 1; a segmented layout runs the receive and
+ * over x, x_hat and memory, per-tensor layouts included (n >= 2^30 runs the receive and
  * choco_gossip_sign_compress as two kernels).  Bit-identical x, x_hat, memory and words
  * to that sequence.  packed must not alias a message's words (l1_norms may alias a
  * message's norms: every workgroup reads them before the last one writes).  nmsg 1..8;
- * ws of choco_sign_recv_workspace_size(n, nseg, nmsg) bytes (one segment: the pass runs over
- * row runs of the (32, N') view, the messages and the output words as bit planes). */
+ * ws of choco_sign_recv_workspace_size(n, nseg, nmsg) bytes (the pass runs over row runs of
+ * the (32, N') view, the messages and the output words as bit planes). */
 /* Workspace bytes of choco_sign_recv_gossip_compress for n elements in nseg segments and
- * nmsg messages (one segment: the accumulator block plus bit planes of every message and of
- * the output; several: choco_sign_workspace_size(nseg)). */
+ * nmsg messages (the per-segment accumulators plus bit planes of every message and of the
+ * output; n >= 2^30: choco_sign_workspace_size(nseg)). */
 size_t choco_sign_recv_workspace_size(int64_t n, int32_t nseg, int32_t nmsg);
 
 int choco_sign_recv_gossip_compress(const int32_t* const* packed_list, const float* const* norms_list,

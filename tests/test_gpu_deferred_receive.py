@@ -125,18 +125,22 @@ def _sign_msgs(n, nmsg, seg_off, nseg):
 
 
 @pytest.mark.parametrize("case", ["flat", "odd_n", "one_message", "eight_messages", "ten_messages", "no_self",
-                                  "segmented"])
+                                  "segmented", "resnet20", "tiny_segments", "segmented_no_self"])
 def test_sign_recv_gossip_compress_matches_sequence(case):
     """choco_sign_recv_gossip_compress (CHOCOSignCompressor.uncompress, parallel_choco_v.py:548-558,
     then the consensus step and the next compress, :476-506) against sign_accumulate +
     the gossip-fused pack, and against the oracle, bit for bit (norms: the exact fp64 L1
     norms rounded once, rtol 1e-6)."""
     from chocosgd_amd import codec
-    lens = {"segmented": [3, 70_001, 5, 400_003]}.get(case)
+    # tiny_segments: 300 segments of 1-13 elements in the first runs (more than kRowSegLds in one
+    # run: the global per-segment sums), then large ones
+    lens = {"segmented": [3, 70_001, 5, 400_003], "segmented_no_self": [4097, 1, 250_000, 9],
+            "resnet20": golden_json("layouts.json")["resnet20_cifar10"],
+            "tiny_segments": [1 + (i * 7) % 13 for i in range(300)] + [65_536, 3, 200_001]}.get(case)
     n = sum(lens) if lens else {"flat": 4_000_000, "odd_n": 1_234_567}.get(case, 777_777)
     seg_off, nseg = _seg(lens)
     nmsg = {"one_message": 1, "eight_messages": 8, "ten_messages": 10}.get(case, 3)
-    self_slot = -1 if case == "no_self" else min(1, nmsg - 1)
+    self_slot = -1 if case in ("no_self", "segmented_no_self") else min(1, nmsg - 1)
     weights = [0.25 + 0.5 / (q + 1) for q in range(nmsg)]
     msgs = _sign_msgs(n, nmsg, seg_off, nseg)
     x, hat, mem = _state(n, 21 + nmsg)
@@ -182,6 +186,24 @@ def test_sign_recv_gossip_compress_small_and_ragged(n):
     assert np.allclose(host(nb), O.l1_norms(d, [n]), rtol=1e-6, atol=0)
 
 
+def test_sign_recv_workspace_reuse_across_layouts():
+    """One cached receive workspace over calls whose accumulators and planes sit at different
+    offsets (flat, 4 segments, 65 segments, flat again; largest n first so it is never
+    reallocated): each call's norms are the exact per-segment L1 norms."""
+    from chocosgd_amd import codec
+    for lens in ([1_000_003], [3, 70_001, 5, 400_003], golden_json("layouts.json")["resnet20_cifar10"],
+                 [1_000_003], [1 + (i * 7) % 13 for i in range(300)] + [65_536]):
+        n = sum(lens)
+        seg_off, nseg = _seg(lens if len(lens) > 1 else None)
+        msgs = _sign_msgs(n, 2, seg_off, nseg)
+        x, hat, mem = _state(n, 31)
+        pb, nb = codec.sign_recv_gossip_compress(msgs, [0.5, 0.25], 0, x, mem, hat, GAMMA, seg_off=seg_off,
+                                                 nseg=nseg)
+        d = (host(x) - host(hat)).astype(np.float32)
+        assert np.array_equal(host(pb), O.sign_pack(d))
+        assert np.allclose(host(nb), O.l1_norms(d, lens), rtol=1e-6, atol=0)
+
+
 def test_sign_recv_gossip_compress_repeated_steps():
     """Deferred sign steps (own message double-buffered, as bench.py --defer-receive) against
     the unfused sequence over several steps: the L1 accumulator is left clean each call."""
@@ -218,7 +240,8 @@ def test_sign_recv_gossip_compress_rejects_aliased_output():
         codec.sign_recv_gossip_compress(msgs, [0.5, 0.5], 0, x, mem, hat, GAMMA, out=msgs[0])
 
 
-@pytest.mark.parametrize("lens", [[37, 40_000, 5, 123_457], [163_499]])
+@pytest.mark.parametrize("lens", [[37, 40_000, 5, 123_457], [163_499], golden_json("layouts.json")["resnet20_cifar10"]],
+                         ids=["ragged", "flat", "resnet20"])
 @pytest.mark.parametrize("comm_op", ["quantize_qsgd", "sign"])
 def test_fused_step_defer_receive_drop_in(comm_op, lens):
     """utils.fused_step(defer_receive=True) through the drop-in CHOCOCompressor against
