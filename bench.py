@@ -56,6 +56,7 @@ WORKLOADS = {
     # the drop-in's per-tensor layout (ResNet-50's 161 tensors, create_optimizer.py:15-24)
     "step_sign_r50": ("sign", 25_557_032, None, "choco_step_gossip_sign_norm_resnet50_161seg"),
     "step_qsgd_r50": ("qsgd", 25_557_032, 4, "choco_step_gossip_qsgd_q4_resnet50_161seg"),
+    "step_topk_r50": ("topk_seg", 25_557_032, 0.99, "choco_step_gossip_topk_k1pct_resnet50_161seg"),
 }
 GAMMA = 0.9  # consensus_stepsize (parameters.py:126 default)
 
@@ -275,6 +276,9 @@ class Worker:
         if self.op == "topk":
             c.topk(self.x, self.k, xhat=self.hat, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]),
                    gossip=g, fold=self._fold_args())
+        elif self.op == "topk_seg":
+            c.topk_segmented(self.x, self.plan, xhat=self.hat,
+                             out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]), gossip=g)
         elif self.op == "qsgd" and self.pending is not None:
             # the previous step's receive + this step's consensus step + norm pass, one kernel
             parts, weights, slot = self.pending
