@@ -57,6 +57,8 @@ WORKLOADS = {
     "step_sign_r50": ("sign", 25_557_032, None, "choco_step_gossip_sign_norm_resnet50_161seg"),
     "step_qsgd_r50": ("qsgd", 25_557_032, 4, "choco_step_gossip_qsgd_q4_resnet50_161seg"),
     "step_topk_r50": ("topk_seg", 25_557_032, 0.99, "choco_step_gossip_topk_k1pct_resnet50_161seg"),
+    "sign_r50": ("sign", 25_557_032, None, "sign_norm_resnet50_161seg"),
+    "qsgd_r50": ("qsgd", 25_557_032, 4, "qsgd_q4_resnet50_161seg"),
 }
 GAMMA = 0.9  # consensus_stepsize (parameters.py:126 default)
 

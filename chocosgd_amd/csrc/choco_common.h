@@ -276,6 +276,19 @@ CHOCO_DEV int seg_of(const int64_t* __restrict__ seg_off, int nseg, int64_t e) {
   return lo;
 }
 
+// The workgroup stages seg_off[0 .. nseg] in LDS (`lds`: room for kSegLdsCap entries) when it
+// fits, so that its segment lookups are LDS binary searches behind ONE global round trip
+// (a search in global memory is ~log2(nseg) dependent ones); returns the table to search.
+// Every thread calls it (workgroup-uniform nseg); ends with a barrier.
+constexpr int kSegLdsCap = 1024;
+CHOCO_DEV const int64_t* stage_seg_off(const int64_t* __restrict__ seg_off, int nseg, int64_t* lds) {
+  const bool fits = nseg + 1 <= kSegLdsCap;
+  if (fits)
+    for (int i = threadIdx.x; i <= nseg; i += blockDim.x) lds[i] = seg_off[i];
+  __syncthreads();
+  return fits ? lds : seg_off;
+}
+
 // ---------------------------------------------------------------- RNG
 // SplitMix64 (Steele, Lea & Flood, OOPSLA 2014; passes BigCrush): the output
 // function of the splitmix64 generator, used in counter mode -- the value at

@@ -414,25 +414,39 @@ __device__ __noinline__ void qsgd_quant_tile_slow(const float* __restrict__ x, c
                                                   float* __restrict__ dense_out, int64_t tile, int sg0) {
   const float sf = (float)s_levels;
   const int64_t eb = tile * kQStreamTile + (int64_t)threadIdx.x * kQPer;
+  // every delta of the thread first (independent loads, all in flight), then the math
+  float dvv[kQG][kQPer];
+#pragma unroll
+  for (int g = 0; g < kQG; ++g)
+#pragma unroll
+    for (int c = 0; c < kQPer; ++c) {
+      const int64_t e = eb + (int64_t)g * kQThreads * kQPer + c;
+      dvv[g][c] = e < n ? dval(x, xh, e) : 0.f;
+    }
   Xoro128 rng;
-  int s = sg0;
-#pragma unroll 1
+  int s = sg0, qs = -1;
+  QParam Q;
+#pragma unroll
   for (int g = 0; g < kQG; ++g) {
     if (!u_in && (g & 1) == 0) rng.seed(qrng_key(seed, offset), qstream_id(tile, g, threadIdx.x));
     const int64_t e0 = eb + (int64_t)g * kQThreads * kQPer;
     uint64_t lacc[2] = {0, 0};  // 8 * CW <= 128 level bits
     uint32_t sbits = 0;
-#pragma unroll 1
+#pragma unroll
     for (int c = 0; c < kQPer; c += 2) {
       float uu[2];
       if (!u_in) rng.next2(uu[0], uu[1]);
+#pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int64_t e = e0 + c + h;
         if (e >= n) continue;
         if (u_in) uu[h] = u_in[e];
         while (s + 1 < nseg && seg_off[s + 1] <= e) ++s;
-        const QParam Q = qparam(norms, seg_off, n, s, s_levels, biased != 0);
-        const float dv = dval(x, xh, e);
+        if (s != qs) {  // the segment's parameters, once per segment
+          Q = qparam(norms, seg_off, n, s, s_levels, biased != 0);
+          qs = s;
+        }
+        const float dv = dvv[g][c + h];
         const float lvl = qlevel((sf * fabsf(dv)) / Q.norm, uu[h]);  // s * x.abs() / norm
         const uint32_t li = level_code(lvl, sf);
         const int bp = (c + h) * CW;
@@ -462,11 +476,21 @@ __device__ __noinline__ void qsgd_quant_tile_slow(const float* __restrict__ x, c
 // flag, not a runtime test: a runtime branch around the u loads made the compiler wait
 // vmcnt(0) before every group's math, draining every load in flight (the prefetch of the
 // looping kernel included).
-template <int CW, int NG, bool UIN>
-CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_t n, const QParam& P,
-                               const QDiv& D, float sf, const float* __restrict__ u_in, uint64_t seed,
+// SEGT: a full tile across tensor boundaries.  Each 8-element group takes its own segment's
+// parameters (walked from the tile's first segment through the LDS table `so`: a thread's
+// groups ascend); a group that itself straddles a boundary divides per element with its
+// element's norm (the same correctly rounded quotients).
+struct QSegs {
+  const int64_t* so;  // seg_off (LDS copy)
+  const float* nm;    // norms (LDS copy)
+  int nseg, sg0, s_levels;
+  bool biased;
+};
+template <int CW, int NG, bool UIN, bool SEGT = false>
+CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_t n, const QParam& P0,
+                               const QDiv& D0, float sf, const float* __restrict__ u_in, uint64_t seed,
                                uint64_t offset, uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
-                               float* __restrict__ dense_out, int g0 = 0, int st = -1) {
+                               float* __restrict__ dense_out, int g0 = 0, int st = -1, const QSegs* SG = nullptr) {
   constexpr int GS = kQThreads * kQPer;  // 2048
   if (st < 0) st = (int)threadIdx.x;
   const int64_t eb = tile * kQStreamTile + (int64_t)st * kQPer + (int64_t)g0 * GS;
@@ -474,12 +498,25 @@ CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_
   // a time, not 32: the registers go to resident waves instead)
   Xoro128 rng;
   const bool dense = dense_out != nullptr;
+  QParam P = P0;
+  QDiv D = D0;
+  int s = SEGT ? SG->sg0 : 0;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     if constexpr (!UIN) {
       if (((g0 + g) & 1) == 0) rng.seed(qrng_key(seed, offset), qstream_id(tile, g0 + g, st));
     }
     const int64_t e0 = eb + g * GS;
+    bool straddle = false;
+    if constexpr (SEGT) {
+      const int s_prev = s;
+      while (s + 1 < SG->nseg && SG->so[s + 1] <= e0) ++s;
+      if (s != s_prev || g == 0) {
+        P = qparam(SG->nm, SG->so, n, s, SG->s_levels, SG->biased);
+        D.init(P.norm);
+      }
+      straddle = s + 1 < SG->nseg && SG->so[s + 1] <= e0 + kQPer - 1;
+    }
     float lf[kQPer];
     uint32_t tmin_m1 = 0xFFFFFFFFu, qmax = 0u;
 #pragma unroll
@@ -489,6 +526,20 @@ CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_
 #pragma unroll
       for (int c = 0; c < kQPer; ++c)
         if (gslow) lf[c] = (sf * fabsf(d[g][c])) / P.norm;
+    }
+    float escale[SEGT ? kQPer : 1], enorm[SEGT ? kQPer : 1];  // (SEGT, straddling group: per element)
+    if constexpr (SEGT) {
+      if (straddle) {
+        int se = s;
+#pragma unroll
+        for (int c = 0; c < kQPer; ++c) {
+          while (se + 1 < SG->nseg && SG->so[se + 1] <= e0 + c) ++se;
+          const QParam Q = qparam(SG->nm, SG->so, n, se, SG->s_levels, SG->biased);
+          lf[c] = (sf * fabsf(d[g][c])) / Q.norm;
+          escale[c] = Q.scale;
+          enorm[c] = Q.norm;
+        }
+      }
     }
     float u[kQPer];
     if constexpr (UIN) {
@@ -517,7 +568,14 @@ CHOCO_DEV void quant_tile_math(const float (&d)[NG][kQPer], int64_t tile, int64_
 #pragma unroll
       for (int c = 0; c < kQPer; ++c) {
         const float sg = d[g][c] > 0.f ? 1.0f : (d[g][c] < 0.f ? -1.0f : 0.0f);  // torch.sign (NaN -> 0)
-        outv[c] = (((P.scale * sg) * P.norm) * lvlf[c]) / sf;
+        float sc = P.scale, nr = P.norm;
+        if constexpr (SEGT) {
+          if (straddle) {
+            sc = escale[c];
+            nr = enorm[c];
+          }
+        }
+        outv[c] = (((sc * sg) * nr) * lvlf[c]) / sf;
       }
       *reinterpret_cast<float4*>(dense_out + e0) = make_float4(outv[0], outv[1], outv[2], outv[3]);
       *reinterpret_cast<float4*>(dense_out + e0 + 4) = make_float4(outv[4], outv[5], outv[6], outv[7]);
@@ -541,11 +599,43 @@ __global__ __launch_bounds__(kQThreads * H, H == 1 ? kQQWaves : kQQHWaves) void 
     uint64_t seed, uint64_t offset, uint8_t* __restrict__ lvl_plane, uint8_t* __restrict__ sign_plane,
     float* __restrict__ dense_out, int64_t tile_lo, int64_t tile_cnt, int64_t pad_e0, int64_t pad_len) {
   __shared__ int s_seg[2];
+  __shared__ int64_t s_so[kSegLdsCap];
+  __shared__ float s_nm[kSegLdsCap];
   // tiles [tile_lo, tile_lo + tile_cnt) of the buffer, walked in reverse (Infinity-Cache hits)
   const int64_t tile = tile_lo + tile_cnt - 1 - (int64_t)blockIdx.x;
   const int64_t t_e0 = tile * kQStreamTile;
   const int64_t t_e1 = std::min<int64_t>(t_e0 + kQStreamTile, n);
-  const int sg0 = tile_seg(seg_off, nseg, t_e0, t_e1, s_seg);
+  const bool full = t_e1 - t_e0 == kQStreamTile;
+  constexpr int NG = kQG / H;                                // groups per thread
+  const int st = (int)(threadIdx.x % kQThreads);             // the thread's uniform stream
+  const int g0 = (int)(threadIdx.x / kQThreads) * NG;        // its first group (wave-uniform)
+  constexpr int GS = kQThreads * kQPer;                      // 2048
+  const int64_t eb = t_e0 + (int64_t)st * kQPer + (int64_t)g0 * GS;  // group g0 + g starts at eb + g * 2048
+  // a full tile's loads go out first (the delta's last read: the norm pass read it first);
+  // a per-tensor layout's segment lookup then runs while they are in flight
+  float4 a[NG][2], hq[XH ? NG : 1][2];
+  if (full) {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      a[g][0] = ld_quant4(x + eb + g * GS);
+      a[g][1] = ld_quant4(x + eb + g * GS + 4);
+    }
+    if constexpr (XH) {
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        hq[g][0] = ld_quant4(xh + eb + g * GS);
+        hq[g][1] = ld_quant4(xh + eb + g * GS + 4);
+      }
+    }
+  }
+  // (the norms ride along with the table: the tile's parameters then need no further round trip)
+  const float* nm = norms;
+  if (nseg > 1 && nseg + 1 <= kSegLdsCap) {
+    for (int i = threadIdx.x; i < nseg; i += blockDim.x) s_nm[i] = norms[i];
+    nm = s_nm;
+  }
+  const int64_t* so = nseg > 1 ? stage_seg_off(seg_off, nseg, s_so) : seg_off;
+  const int sg0 = tile_seg(so, nseg, t_e0, t_e1, s_seg);
   const bool uniform = s_seg[1] == sg0;
   if (blockIdx.x == 0) {
     // the planes of elements [pad_e0, pad_e0 + pad_len) are fully defined: zero their
@@ -557,33 +647,20 @@ __global__ __launch_bounds__(kQThreads * H, H == 1 ? kQQWaves : kQQHWaves) void 
     for (int64_t b = sgn_used + threadIdx.x; b < sgn_end; b += kQThreads * H) sign_plane[b] = 0;
   }
   const float sf = (float)s_levels;
-  constexpr int NG = kQG / H;                                // groups per thread
-  const int st = (int)(threadIdx.x % kQThreads);             // the thread's uniform stream
-  const int g0 = (int)(threadIdx.x / kQThreads) * NG;        // its first group (wave-uniform)
-  constexpr int GS = kQThreads * kQPer;                      // 2048
-  const int64_t eb = t_e0 + (int64_t)st * kQPer + (int64_t)g0 * GS;  // group g0 + g starts at eb + g * 2048
-  if (!uniform || t_e1 - t_e0 != kQStreamTile) {
+  if (!full) {
     if (threadIdx.x < kQThreads)  // (no barrier below: the second half leaves)
-      qsgd_quant_tile_slow<CW>(x, xh, n, seg_off, nseg, s_levels, biased, norms, u_in, seed, offset, lvl_plane,
+      qsgd_quant_tile_slow<CW>(x, xh, n, so, nseg, s_levels, biased, norms, u_in, seed, offset, lvl_plane,
                                sign_plane, dense_out, tile, sg0);
     return;
   }
-  // full one-segment tile: unconditional loads, all in flight (the delta's last
-  // read: the norm pass read it first)
+  // full one-segment tile
   float d[NG][kQPer];
   {
-    float4 a[NG][2];
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      a[g][0] = ld_quant4(x + eb + g * GS);
-      a[g][1] = ld_quant4(x + eb + g * GS + 4);
-    }
     if constexpr (XH) {
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
-        const float4 h0 = ld_quant4(xh + eb + g * GS), h1 = ld_quant4(xh + eb + g * GS + 4);
-        a[g][0] = sub4(a[g][0], h0);
-        a[g][1] = sub4(a[g][1], h1);
+        a[g][0] = sub4(a[g][0], hq[g][0]);
+        a[g][1] = sub4(a[g][1], hq[g][1]);
       }
     }
 #pragma unroll
@@ -592,10 +669,16 @@ __global__ __launch_bounds__(kQThreads * H, H == 1 ? kQQWaves : kQQHWaves) void 
       d[g][4] = a[g][1].x; d[g][5] = a[g][1].y; d[g][6] = a[g][1].z; d[g][7] = a[g][1].w;
     }
   }
-  const QParam P = qparam(norms, seg_off, n, sg0, s_levels, biased != 0);
+  const QParam P = qparam(nm, so, n, sg0, s_levels, biased != 0);
   QDiv D;
   D.init(P.norm);
-  quant_tile_math<CW, NG, UIN>(d, tile, n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out, g0, st);
+  if (uniform) {
+    quant_tile_math<CW, NG, UIN>(d, tile, n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out, g0, st);
+  } else {
+    const QSegs SG{so, nm, nseg, sg0, s_levels, biased != 0};
+    quant_tile_math<CW, NG, UIN, true>(d, tile, n, P, D, sf, u_in, seed, offset, lvl_plane, sign_plane, dense_out,
+                                       g0, st, &SG);
+  }
 }
 
 // ---------------------------------------------------------------- decode / accumulate

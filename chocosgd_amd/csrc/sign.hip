@@ -331,6 +331,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
 // running sum while consecutive rows stay in one segment, and a wave sum goes to the
 // workgroup's LDS per-segment sums when the segment changes (a row across a boundary: one
 // wave sum per segment in it); the workgroup adds its LDS sums to the global ones.
+constexpr int kRowRep = 8;  // replicas of the fp64 L1 accumulators (workgroup b -> replica b & 7)
 constexpr int kPackSegLds = 1024;  // segments of one workgroup's rows summed in LDS (more: global atomics)
 template <bool XH, bool NORM, bool GS = false, bool SEG = false, int RUV = 0>
 __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* __restrict__ x,
@@ -348,6 +349,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
   __shared__ unsigned int s_flag;
   __shared__ int s_lo[SEG ? 32 : 1], s_hi[SEG ? 32 : 1];
   __shared__ double s_sacc[SEG ? kPackSegLds : 1];
+  __shared__ int64_t s_so[SEG ? kSegLdsCap : 1];
   double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
   const int lane = lane_id(), w = threadIdx.x >> 6;
   const int64_t J0 = (blk0 + (int64_t)blockIdx.x) * kSignCols;
@@ -385,10 +387,13 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
   int sbase = 0;
   bool slds = true;
   int cur = -1;
+  int lo_v = 0, hi_v = 0;  // lane l: row (l & 31)'s first and last segment (read back with readlane)
   auto seg_lookup = [&]() {
     if (SEG) {
-      row_segments(seg_off, nseg, n, Np, J0, s_lo, s_hi);
+      row_segments(stage_seg_off(seg_off, nseg, s_so), nseg, n, Np, J0, s_lo, s_hi);
       __syncthreads();
+      lo_v = s_lo[lane & 31];
+      hi_v = s_hi[lane & 31];
       int lo = s_lo[0] >= 0 ? s_lo[0] : 0, hi = 0;
       for (int r = 31; r >= 0; --r)
         if (s_hi[r] >= 0) { hi = s_hi[r]; break; }
@@ -399,10 +404,12 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
       __syncthreads();
     }
   };
+  // the global sums: kRowRep replicas (workgroup b -> replica b & 7), summed by the finish
+  double* __restrict__ rep = acc + (size_t)(blockIdx.x & (kRowRep - 1)) * (size_t)(SEG ? nseg : 1);
   auto seg_add = [&](int sg, double v) {  // lane 0 of a wave
     if (v == 0.0) return;
     if (slds) atomicAdd(&s_sacc[sg - sbase], v);
-    else unsafeAtomicAdd(&acc[sg], v);
+    else unsafeAtomicAdd(&rep[sg], v);
   };
   auto seg_flush = [&]() {  // wave-uniform
     if (cur >= 0) {
@@ -419,7 +426,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
         if ((valid >> c) & 1u) p += (double)fabsf(v[c]);
       return;
     }
-    const int lo = s_lo[r], hi = s_hi[r];
+    const int lo = __builtin_amdgcn_readlane(lo_v, r), hi = __builtin_amdgcn_readlane(hi_v, r);
     if (lo < 0) return;  // (a row run past n)
     if (lo == hi) {      // wave-uniform
       if (lo != cur) {
@@ -537,10 +544,14 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
       for (int r = 31; r >= 0; --r)
         if (s_hi[r] >= 0) { hi = s_hi[r]; break; }
       for (int i = threadIdx.x; i <= hi - sbase; i += kSignThreads)
-        if (s_sacc[i] != 0.0) unsafeAtomicAdd(&acc[sbase + i], s_sacc[i]);
+        if (s_sacc[i] != 0.0) unsafeAtomicAdd(&rep[sbase + i], s_sacc[i]);
     }
     if (finish && last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
-      for (int q = threadIdx.x; q < nseg; q += kSignThreads) l1_out[q] = (float)atomic_exchange_double(&acc[q], 0.0);
+      for (int q = threadIdx.x; q < nseg; q += kSignThreads) {
+        double t = 0.0;
+        for (int i = 0; i < kRowRep; ++i) t += atomic_exchange_double(&acc[(size_t)i * nseg + q], 0.0);
+        l1_out[q] = (float)t;
+      }
       if (threadIdx.x == 0) __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   } else if (NORM) {
@@ -1006,7 +1017,6 @@ struct PlaneMsgs {
   int self_slot;
 };
 
-constexpr int kRowRep = 8;      // replicas of the fp64 L1 accumulators (workgroup b -> replica b & 7)
 constexpr int kRowSegLds = 64;  // a run spanning fewer segments sums them in LDS first
 // Workgroup i <-> run i, row-major over the (32, N') view, i.e. the flat element order: row
 // r = i / nrun, columns [J, J + 4096) with J = (i % nrun) * 4096.  Thread t takes the float4
@@ -1268,7 +1278,9 @@ using namespace choco;
 CHOCO_API int64_t choco_sign_words(int64_t n) { return (n + 31) / 32; }
 
 CHOCO_API size_t choco_sign_workspace_size(int32_t nseg) {
-  return 256 + align_up((size_t)(nseg > 0 ? nseg : 1) * sizeof(double), 256);
+  // the ticket block, then kRowRep replicas of the per-segment fp64 L1 sums (the one-pass
+  // pack's per-tensor form spreads its workgroups' atomics over them)
+  return 256 + align_up((size_t)kRowRep * (size_t)(nseg > 0 ? nseg : 1) * sizeof(double), 256);
 }
 
 // Same-box A/B, ResNet-50 layout (25.6M, 161 tensors; 780 workgroups), fused step: 4-row groups

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-5 GPU pass AJ: the QSGD quantize with the tile's norms staged with the segment table -- QSGD tests, then
+# per-tensor and flat QSGD rounds (twice).
+cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; O=gpurun_out/r5aj; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_qsgd_sign.py tests/test_gpu_deferred_receive.py tests/test_gpu_consumers.py \
+  -x -q -p no:cacheprovider --timeout 240 --timeout-method thread > $O/tests.log 2>&1; rc=$?
+tail -2 $O/tests.log; [ $rc -ne 0 ] && { grep -E "FAIL|Error|assert" $O/tests.log | head -30; exit $rc; }
+for rep in 1 2; do
+for spec in qsgd_r50 "qsgd --n 25557032" step_qsgd_r50 "step_qsgd --n 25557032" qsgd; do
+  timeout -k 10 300 python bench.py --workload $spec --no-cpu-baseline --no-e2e > $O/b.json 2> $O/b.err || { tail -20 $O/b.err; exit 1; }
+  python -c "import json; d=json.load(open('$O/b.json')); print('$spec', d['ms_per_step'], d['roofline']['frac'], d['kernels_us'])"
+done
+done
