@@ -59,6 +59,7 @@ WORKLOADS = {
     "step_topk_r50": ("topk_seg", 25_557_032, 0.99, "choco_step_gossip_topk_k1pct_resnet50_161seg"),
     "sign_r50": ("sign", 25_557_032, None, "sign_norm_resnet50_161seg"),
     "qsgd_r50": ("qsgd", 25_557_032, 4, "qsgd_q4_resnet50_161seg"),
+    "randk_r50": ("randk_seg", 25_557_032, 0.99, "randk_k1pct_resnet50_161seg"),
 }
 GAMMA = 0.9  # consensus_stepsize (parameters.py:126 default)
 
@@ -69,6 +70,7 @@ STAGES = {
     "topk_seg": (["topk_seg_hist", "topk_seg_collect", "topk_seg_fine", "topk_seg_count", "topk_seg_bin",
                   "topk_seg_emit", "topk_bounds", "topk_stream", "topk_finish"], ["sparse_accumulate"]),
     "randk": (["randk_count", "randk_tile"], ["sparse_accumulate"]),
+    "randk_seg": (["randk_count", "randk_tile"], ["sparse_accumulate"]),
     "qsgd": (["qsgd_norm", "qsgd_quantize"], ["qsgd_accumulate"]),
     "sign": (["sign_pack"], ["sign_accumulate"]),
 }
@@ -167,11 +169,11 @@ class Worker:
         self.fold_mem = self.fold and self.self_slot == 0
         self.plan = None
         self.seg_off, self.nseg = None, 1  # per-tensor layout of the dense codecs (_r50 workloads)
-        if self.op == "topk_seg" or args.workload.endswith("_r50"):
+        if self.op in ("topk_seg", "randk_seg") or args.workload.endswith("_r50"):
             with open(os.path.join(ROOT, "tests", "golden", "layouts.json")) as f:
                 lens = json.load(f)["resnet50_imagenet"]
             n = sum(lens)
-            if self.op == "topk_seg":
+            if self.op in ("topk_seg", "randk_seg"):
                 self.plan = codec.SegmentPlan(lens, self.param, dev)
             else:
                 if args.n:
@@ -200,7 +202,7 @@ class Worker:
         if self.op in ("topk", "randk"):
             self.k = codec.topk_k(self.n, self.param)
             self.msg = torch.empty(2 * self.k, dtype=torch.int32, device=dev)
-        elif self.op == "topk_seg":
+        elif self.op in ("topk_seg", "randk_seg"):
             self.k = self.plan.k_total
             self.msg = torch.empty(2 * self.k, dtype=torch.int32, device=dev)
         elif self.op == "qsgd":  # [norms (16-B padded) | planes]; compress writes in place
@@ -257,6 +259,9 @@ class Worker:
                    fold=self._fold_args())
         elif self.op == "topk_seg":
             c.topk_segmented(self.d, self.plan, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]))
+        elif self.op == "randk_seg":
+            c.randk_segmented(self.d, self.plan, seed=12345 + self.rank, offset=self.step_id,
+                              out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]))
         elif self.op == "randk":
             # one seed per worker, the step number as the stream offset (include/choco_codec.h)
             c.randk(self.d, self.k, seed=12345 + self.rank, offset=self.step_id,
@@ -356,7 +361,7 @@ class Worker:
         c = self.codec
         torch = self.torch
         msgs = [self.msg if r == self.rank else self.recv[r] for r in self.ranks]
-        if self.op in ("topk", "topk_seg", "randk"):
+        if self.op in ("topk", "topk_seg", "randk", "randk_seg"):
             # the self message's memory update is skipped when the fold applied it; x_hat takes
             # it here unless the overlap (hat_done) or the fold did
             items = [(r, m, w) for r, m, w in zip(self.ranks, msgs, self.weights)
@@ -384,7 +389,7 @@ class Worker:
     def step(self):
         self.compress()
         works = self.exchange_start()
-        overlap = works is not None and self.op in ("topk", "topk_seg", "randk") and not self.fold
+        overlap = works is not None and self.op in ("topk", "topk_seg", "randk", "randk_seg") and not self.fold
         if overlap:
             self.hat_self_update()
         self.exchange_finish(works)
@@ -420,7 +425,7 @@ class Worker:
                 return comp, dec, ("compress 4n + 8k + 8k RMW of x_hat (+ 8k of memory when the self rank is "
                                    "first: the fold); decompress 8k read + 8k memory RMW per other message")
             return comp, dec, "compress 4n + 8k; decompress 8k read per message + 8k RMW per touched buffer"
-        if self.op == "randk":
+        if self.op in ("randk", "randk_seg"):
             comp = 4 * self.k + 8 * self.k                # gather k values + write k pairs (the sampler reads none)
             dec = 8 * self.k * nm + 8 * self.k * (nm + 1)
             return comp, dec, "compress 4k gather + 8k; decompress as top-k"
@@ -439,7 +444,7 @@ class Worker:
     def granule_bytes_decompress(self):
         """Sparse accumulate at HBM access granularity: every touched 64-B segment of
         x_hat / memory is read and written whole (the bound a scattered RMW really pays)."""
-        if self.op not in ("topk", "topk_seg", "randk"):
+        if self.op not in ("topk", "topk_seg", "randk", "randk_seg"):
             return None
         torch = self.torch
         ms = [self.msg] + [self.recv[r] for r in self.ranks if r != self.rank]
@@ -542,8 +547,8 @@ def cpu_baseline(w):
     def make_codec(m, hat, mem, d_fixed):
         def wrap(f):
             return (lambda: f(d_fixed)) if d_fixed is not None else f
-        if w.op in ("topk", "topk_seg", "randk"):
-            if w.op == "randk":
+        if w.op in ("topk", "topk_seg", "randk", "randk_seg"):
+            if w.op in ("randk", "randk_seg"):
                 return wrap(lambda d: P.sparse_decompress(hat, mem, *P.randk_compress(d, w.param), 1.0))
             return wrap(lambda d: P.sparse_decompress(hat, mem, *P.topk_compress(d, w.param), 1.0))
         if w.op == "qsgd":
@@ -553,6 +558,7 @@ def cpu_baseline(w):
     what = {"topk": "top-k (torch.topk) compress + self decompress",
             "topk_seg": "top-k (torch.topk, flat) compress + self decompress",
             "randk": "random-k (np.random.choice) compress + self decompress",
+            "randk_seg": "random-k (np.random.choice, flat) compress + self decompress",
             "qsgd": f"QSGD q={w.param} compress + self decompress",
             "sign": "sign + L1 norm compress + self decompress"}[w.op]
     if w.step_mode:
