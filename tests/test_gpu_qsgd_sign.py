@@ -149,29 +149,37 @@ def test_choco_qsgd_round_trip_golden():
     assert same_bits(host(mem), g["mem1"])
 
 
-@pytest.mark.parametrize("layout", ["resnet20_cifar10", "resnet50_imagenet"])
-def test_qsgd_segmented_layout_norms_and_levels(layout):
+@pytest.mark.parametrize("layout,biased", [("resnet20_cifar10", False), ("resnet50_imagenet", False),
+                                           ("tiny", False), ("tiny", True)])
+def test_qsgd_segmented_layout_norms_and_levels(layout, biased):
+    """Per-tensor QSGD against the oracle: norms, levels (dense output) and the decode.  "tiny":
+    300 tensors of 1-13 elements between larger ones, so that 8-element groups and 8192-element
+    tiles straddle boundaries (the quantize's per-group and per-element segment parameters);
+    biased: the per-tensor scale too."""
     from chocosgd_amd import codec
-    lens = golden_json("layouts.json")[layout]
+    if layout == "tiny":
+        lens = [20_000] + [1 + (i * 7) % 13 for i in range(300)] + [9_000, 3, 70_001]
+    else:
+        lens = golden_json("layouts.json")[layout]
     n = sum(lens)
     x, xh = randn(n, 21), randn(n, 22, 0.3)
     so = seg_table(lens)
-    packed, norms, dense = codec.qsgd_compress(x, 4, xhat=xh, seg_off=so, nseg=len(lens), seed=9, offset=1,
-                                               want_dense=True)
+    packed, norms, dense = codec.qsgd_compress(x, 4, is_biased=biased, xhat=xh, seg_off=so, nseg=len(lens), seed=9,
+                                               offset=1, want_dense=True)
     d = host(x) - host(xh)
     ref = O.l2_norms(d, lens)
     assert np.allclose(host(norms), ref, rtol=1e-6, atol=0)
     u = O.qsgd_uniforms(n, 9, 1)
     off, outs = 0, []
     for s, m in enumerate(lens):
-        outs.append(O.qsgd_dense(d[off:off + m], 15, u[off:off + m], host(norms)[s]))
+        outs.append(O.qsgd_dense(d[off:off + m], 15, u[off:off + m], host(norms)[s], is_biased=biased))
         off += m
     assert same_bits(host(dense), np.concatenate(outs))
-    dec = codec.qsgd_decode(packed, norms, n, 4, seg_off=so, nseg=len(lens))
+    dec = codec.qsgd_decode(packed, norms, n, 4, is_biased=biased, seg_off=so, nseg=len(lens))
     levels, neg = O.qsgd_unpack(host(packed), n, 4)  # the oracle's decode of the wire itself
     off, want = 0, []
     for s, m in enumerate(lens):
-        want.append(O.qsgd_decode(levels[off:off + m], neg[off:off + m], host(norms)[s], 15, m))
+        want.append(O.qsgd_decode(levels[off:off + m], neg[off:off + m], host(norms)[s], 15, m, is_biased=biased))
         off += m
     assert same_bits(host(dec), np.concatenate(want))
     assert same_bits(host(dense), np.concatenate(want))
