@@ -333,8 +333,11 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack_kernel(
 // wave sum per segment in it); the workgroup adds its LDS sums to the global ones.
 constexpr int kRowRep = 8;  // replicas of the fp64 L1 accumulators (workgroup b -> replica b & 7)
 constexpr int kPackSegLds = 1024;  // segments of one workgroup's rows summed in LDS (more: global atomics)
-template <bool XH, bool NORM, bool GS = false, bool SEG = false, int RUV = 0>
-__global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* __restrict__ x,
+// RS = 2 (small grids): eight waves per workgroup, waves w and w + 4 take rows 0-15 and 16-31
+// of the same 256 columns (twice the waves resident per column block); the upper half's
+// words are OR-ed in through LDS.
+template <bool XH, bool NORM, bool GS = false, bool SEG = false, int RUV = 0, int RS = 1>
+__global__ __launch_bounds__(kSignThreads * RS) void sign_pack1_kernel(const float* __restrict__ x,
                                                                   const float* __restrict__ xh, int64_t n,
                                                                   int64_t Np, uint32_t* __restrict__ packed,
                                                                   float* __restrict__ l1_out,
@@ -344,16 +347,21 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
   static_assert(!GS || XH, "the gossip step needs x_hat");
   static_assert(!SEG || NORM, "segments only matter to the norms");
   constexpr int RU = RUV ? RUV : (GS ? 8 : (XH ? 4 : 8));  // rows per group (more streams, more registers)
-  constexpr int NG = 32 / RU;
-  __shared__ double s_red[kSignThreads / 64];
+  constexpr int kT = kSignThreads * RS;                     // threads per workgroup
+  constexpr int NR = 32 / RS;                               // rows per wave
+  constexpr int NG = NR / RU;
+  static_assert(NG >= 2 && NG % 2 == 0, "groups go in A/B pairs");
+  __shared__ double s_red[kT / 64];
+  __shared__ uint4 s_wd[RS > 1 ? 4 : 1][64];
   __shared__ unsigned int s_flag;
   __shared__ int s_lo[SEG ? 32 : 1], s_hi[SEG ? 32 : 1];
   __shared__ double s_sacc[SEG ? kPackSegLds : 1];
   __shared__ int64_t s_so[SEG ? kSegLdsCap : 1];
   double* __restrict__ acc = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
   const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int wq = w & 3, rs0 = (w >> 2) * NR;  // the wave's 256 columns and first row
   const int64_t J0 = (blk0 + (int64_t)blockIdx.x) * kSignCols;
-  const int64_t j0 = J0 + 256 * w;
+  const int64_t j0 = J0 + 256 * wq;
   const int ncol = (int)std::max<int64_t>(0, std::min<int64_t>(256, Np - j0));
   // every row run of the wave (row 31's last float4 included) lies inside [0, n)
   const bool interior = ncol == 256 && (int64_t)31 * Np + j0 + 256 <= n;
@@ -370,14 +378,14 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
   };
   auto load_group = [&](int g, Group& G) {
 #pragma unroll
-    for (int u = 0; u < RU; ++u) G.x[u] = ld_buf4s<true>(rx, voff, row_off(g * RU + u));
+    for (int u = 0; u < RU; ++u) G.x[u] = ld_buf4s<true>(rx, voff, row_off(rs0 + g * RU + u));
     if (XH) {
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.h[u] = ld_buf4s<true>(rh, voff, row_off(g * RU + u));
+      for (int u = 0; u < RU; ++u) G.h[u] = ld_buf4s<true>(rh, voff, row_off(rs0 + g * RU + u));
     }
     if (GS) {
 #pragma unroll
-      for (int u = 0; u < RU; ++u) G.m[u] = ld_buf4s<true>(rm, voff, row_off(g * RU + u));
+      for (int u = 0; u < RU; ++u) G.m[u] = ld_buf4s<true>(rm, voff, row_off(rs0 + g * RU + u));
     }
   };
   uint32_t wd[4] = {0u, 0u, 0u, 0u};
@@ -400,7 +408,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
       sbase = lo;
       slds = hi - lo < kPackSegLds;
       if (slds)
-        for (int i = threadIdx.x; i <= hi - lo; i += kSignThreads) s_sacc[i] = 0.0;
+        for (int i = threadIdx.x; i <= hi - lo; i += kT) s_sacc[i] = 0.0;
       __syncthreads();
     }
   };
@@ -460,12 +468,12 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
         G.x[u] = gossip4(G.x[u], G.m[u], G.h[u], gs.gamma);
         // non-temporal: x_new is not re-read by this step, and dirty Infinity-Cache
         // lines would be written back in the middle of the receiver's pass
-        st_buf4s<true>(rx, voff, row_off(g * RU + u), G.x[u]);
+        st_buf4s<true>(rx, voff, row_off(rs0 + g * RU + u), G.x[u]);
       }
     }
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
-      const int r = g * RU + u;
+      const int r = rs0 + g * RU + u;
       const float4 R = XH ? sub4(G.x[u], G.h[u]) : G.x[u];
       const float v[4] = {R.x, R.y, R.z, R.w};
 #pragma unroll
@@ -495,7 +503,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
     // the last workgroups: guarded element loads, one row at a time
     seg_lookup();
 #pragma unroll 1
-    for (int r = 0; r < 32; ++r) {
+    for (int r = rs0; r < rs0 + NR; ++r) {
       const int64_t s = (int64_t)r * Np + j0 + 4 * lane;
       float tt[4];
 #pragma unroll
@@ -526,7 +534,15 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
       }
     }
   }
-  {
+  if (RS > 1) {  // the upper rows' bits through LDS
+    if (w >= 4) s_wd[wq][lane] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    __syncthreads();
+    if (w < 4) {
+      const uint4 o = s_wd[wq][lane];
+      wd[0] |= o.x; wd[1] |= o.y; wd[2] |= o.z; wd[3] |= o.w;
+    }
+  }
+  if (w < 4) {
     const int64_t j = j0 + 4 * lane;
     if (j + 3 < Np) {
       *reinterpret_cast<uint4*>(packed + j) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
@@ -543,11 +559,11 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
       int hi = 0;
       for (int r = 31; r >= 0; --r)
         if (s_hi[r] >= 0) { hi = s_hi[r]; break; }
-      for (int i = threadIdx.x; i <= hi - sbase; i += kSignThreads)
+      for (int i = threadIdx.x; i <= hi - sbase; i += kT)
         if (s_sacc[i] != 0.0) unsafeAtomicAdd(&rep[sbase + i], s_sacc[i]);
     }
     if (finish && last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
-      for (int q = threadIdx.x; q < nseg; q += kSignThreads) {
+      for (int q = threadIdx.x; q < nseg; q += kT) {
         double t = 0.0;
         for (int i = 0; i < kRowRep; ++i) t += atomic_exchange_double(&acc[(size_t)i * nseg + q], 0.0);
         l1_out[q] = (float)t;
@@ -561,7 +577,7 @@ __global__ __launch_bounds__(kSignThreads) void sign_pack1_kernel(const float* _
     if (threadIdx.x == 0) {
       double tsum = 0.0;
 #pragma unroll
-      for (int i = 0; i < kSignThreads / 64; ++i) tsum += s_red[i];
+      for (int i = 0; i < kT / 64; ++i) tsum += s_red[i];
       if (tsum != 0.0) unsafeAtomicAdd(&acc[0], tsum);
     }
     if (finish && last_block_ticket_atomics(&ws->ticket, gridDim.x, &s_flag)) {
@@ -1286,19 +1302,29 @@ CHOCO_API size_t choco_sign_workspace_size(int32_t nseg) {
 // Same-box A/B, ResNet-50 layout (25.6M, 161 tensors; 780 workgroups), fused step: 4-row groups
 // 112.5 / 112.3 us against 135.3 / 134.7 in 8-row groups (profiles/r05_ab_summary.txt item 16)
 constexpr int kPackSmallGrid = 2048;
+// Row split on those grids, same box (profiles/r05_ab_summary.txt item 18): flat 25.6M pack 35.4 ->
+// 26.7 us, fused step 100.8 -> 85.3, ResNet-50's fused step 104 -> 95.6
+constexpr int kPackRS = 2;
 template <bool XH, bool NORM, bool GS>
 static void launch_pack(bool one, unsigned grid, hipStream_t st, const float* x, const float* xhat, int64_t n,
                         int64_t Np, const int64_t* seg_off, int32_t nseg, uint32_t* pk, float* l1, SignWs* w,
                         Gossip gs, int64_t blk0, int finish) {
-  // a grid of under kPackSmallGrid workgroups (the ~25M-element buffers of one model) runs the
-  // fused step in groups of 4 rows: more waves per CU instead of more rows in flight per wave
-  const bool small = GS && grid < (unsigned)kPackSmallGrid;
-  if (one && small && NORM && nseg > 1)
-    CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS, NORM, 4>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
-                  pk, l1, w, gs, blk0, finish, seg_off, nseg);
+  // a grid of under kPackSmallGrid workgroups (the ~25M-element buffers of one model) splits each
+  // column block's rows over two waves, and runs the fused step in groups of 4 rows: more
+  // waves per CU instead of more rows in flight per wave
+  const bool small = grid < (unsigned)kPackSmallGrid;
+  if (one && small && GS && NORM && nseg > 1)
+    CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS, NORM, 4, kPackRS>), dim3(grid), dim3(kPackRS * kSignThreads), 0, st, x, xhat,
+                  n, Np, pk, l1, w, gs, blk0, finish, seg_off, nseg);
+  else if (one && small && GS)
+    CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS, false, 4, kPackRS>), dim3(grid), dim3(kPackRS * kSignThreads), 0, st, x, xhat,
+                  n, Np, pk, l1, w, gs, blk0, finish, seg_off, nseg);
+  else if (one && small && NORM && nseg > 1)
+    CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS, NORM, 0, kPackRS>), dim3(grid), dim3(kPackRS * kSignThreads), 0, st, x, xhat,
+                  n, Np, pk, l1, w, gs, blk0, finish, seg_off, nseg);
   else if (one && small)
-    CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS, false, 4>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np,
-                  pk, l1, w, gs, blk0, finish, seg_off, nseg);
+    CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS, false, 0, kPackRS>), dim3(grid), dim3(kPackRS * kSignThreads), 0, st, x, xhat,
+                  n, Np, pk, l1, w, gs, blk0, finish, seg_off, nseg);
   else if (one && NORM && nseg > 1)
     CHOCO_KLAUNCH((sign_pack1_kernel<XH, NORM, GS, NORM>), dim3(grid), dim3(kSignThreads), 0, st, x, xhat, n, Np, pk,
                   l1, w, gs, blk0, finish, seg_off, nseg);
