@@ -200,10 +200,14 @@ def test_gossip_randk_segmented():
     assert same_bits(host(v), ov)
 
 
-@pytest.mark.parametrize("lens", [[1_000_003], [4_194_304], [3, 70_001, 5, 1_200_003, 17, 301], [33, 31, 2_000_000]])
+MANY = np.random.default_rng(6).integers(1, 40, size=1500).tolist() + [300_000]  # past the LDS tables
+
+
+@pytest.mark.parametrize("lens", [[1_000_003], [4_194_304], [3, 70_001, 5, 1_200_003, 17, 301], [33, 31, 2_000_000],
+                                  MANY], ids=["flat", "flat4m", "ragged", "small_first", "many"])
 def test_gossip_sign(lens):
-    """One-segment pack (per-lane own float4s) and the multi-segment pack (realigned
-    float4s: x_new is stored only for the wave's own elements)."""
+    """The one-pass pack with the step fused, one segment and per-tensor norms (small grids: rows
+    split over two waves; "many": more tensors than its LDS tables hold)."""
     from chocosgd_amd import codec
     n = sum(lens)
     x, mem, hat = _inputs(n, 9)
@@ -216,7 +220,7 @@ def test_gossip_sign(lens):
     assert np.allclose(host(norms), O.l1_norms(d, lens), rtol=1e-6, atol=0)
 
 
-@pytest.mark.parametrize("lens", [[2_000_003], [3, 70_001, 5, 1_200_003]])
+@pytest.mark.parametrize("lens", [[2_000_003], [3, 70_001, 5, 1_200_003], MANY], ids=["flat", "ragged", "many"])
 def test_gossip_qsgd(lens):
     """The norm pass with the step fused; levels and signs on the wire vs the oracle with
     the device norms and the device uniforms (SplitMix64)."""

@@ -150,7 +150,7 @@ def test_choco_qsgd_round_trip_golden():
 
 
 @pytest.mark.parametrize("layout,biased", [("resnet20_cifar10", False), ("resnet50_imagenet", False),
-                                           ("tiny", False), ("tiny", True)])
+                                           ("tiny", False), ("tiny", True), ("many", False)])
 def test_qsgd_segmented_layout_norms_and_levels(layout, biased):
     """Per-tensor QSGD against the oracle: norms, levels (dense output) and the decode.  "tiny":
     300 tensors of 1-13 elements between larger ones, so that 8-element groups and 8192-element
@@ -159,6 +159,8 @@ def test_qsgd_segmented_layout_norms_and_levels(layout, biased):
     from chocosgd_amd import codec
     if layout == "tiny":
         lens = [20_000] + [1 + (i * 7) % 13 for i in range(300)] + [9_000, 3, 70_001]
+    elif layout == "many":  # more tensors than the kernels' LDS tables hold (their global fallbacks)
+        lens = np.random.default_rng(5).integers(1, 40, size=1500).tolist() + [50_000]
     else:
         lens = golden_json("layouts.json")[layout]
     n = sum(lens)
