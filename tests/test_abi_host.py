@@ -58,7 +58,22 @@ def test_sizes_and_formats(lib):
     # candidate entries (float4 + int32 per 4 elements) dominate: 5 bytes per element
     assert lib.choco_topk_workspace_size(100_000_000) > 5 * 100_000_000
     assert lib.choco_topk_workspace_size(1000) >= 256
-    assert lib.choco_sign_workspace_size(161) >= 256 + 161 * 8
+    assert lib.choco_sign_workspace_size(161) >= 256 + 8 * 161 * 8  # 8 replicas of the per-segment sums
+
+
+def test_sign_receive_workspace_sizes(lib):
+    """choco_sign_recv_workspace_size: the accumulators plus bit planes of every message and of
+    the output (n/8 bytes each, 32 x ceil(N'/32) words), growing with n, nseg and nmsg; past
+    2^30 elements the two-kernel form's sign workspace."""
+    for n in [1, 33, 4096 * 32 + 1, 345_000_000]:
+        P = (O.sign_words(n) + 31) // 32
+        for nseg in [1, 161]:
+            for nmsg in [1, 3, 8]:
+                sz = lib.choco_sign_recv_workspace_size(n, nseg, nmsg)
+                assert sz >= 256 + 8 * nseg * 8 + (nmsg + 1) * 32 * P * 4
+                assert sz % 256 == 0
+                assert lib.choco_sign_recv_workspace_size(n, nseg, nmsg + 1) > sz
+    assert lib.choco_sign_recv_workspace_size(1 << 30, 5, 3) == lib.choco_sign_workspace_size(5)
 
 
 def test_segmented_plan(lib):
