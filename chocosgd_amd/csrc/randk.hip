@@ -217,6 +217,12 @@ CHOCO_DEV uint32_t pick_word(const uint32_t (&w)[kRkWpt], int q) {  // w[q] by s
 // kRkList positions are listed in LDS in ascending order and gathered by
 // consecutive lanes (coalesced stores, kRkGU loads in flight per thread); denser
 // quarters emit per thread.
+// A gathered element, non-temporal: with default-policy loads the 1M scattered lines of a
+// 100M gather allocate in the Infinity Cache and push out the lines the step's accumulate left
+// dirty, whose write-back then meets the gather.  Same-box A/B (r05_ab_summary.txt item 19):
+// R2 41.0 -> 30.3 us, the random-k step 0.1373 -> 0.1262 ms; ResNet-50 layout unchanged.
+CHOCO_DEV float rk_ld(const float* p) { return __builtin_nontemporal_load(p); }
+
 template <bool FLAT, bool XH>
 __global__ __launch_bounds__(kRkQThreads) void randk_tile_kernel(const float* __restrict__ x, const float* __restrict__ xh,
                                                                  const int64_t* __restrict__ plan, int64_t rk_base,
@@ -324,7 +330,7 @@ __global__ __launch_bounds__(kRkQThreads) void randk_tile_kernel(const float* __
         const uint32_t i = i0 + (uint32_t)u * kRkQThreads + (uint32_t)tid;
         const int64_t e = gbase + pos[u];
         v[u] = 0.f;
-        if (i < cq) v[u] = XH ? x[e] - xh[e] : x[e];
+        if (i < cq) v[u] = XH ? rk_ld(x + e) - rk_ld(xh + e) : rk_ld(x + e);
       }
 #pragma unroll
       for (int u = 0; u < kRkGU; ++u) {
@@ -357,7 +363,7 @@ __global__ __launch_bounds__(kRkQThreads) void randk_tile_kernel(const float* __
         v[i] = 0.f;
         if (ok[i]) {
           const int64_t e = gbase + pos[i];
-          v[i] = XH ? x[e] - xh[e] : x[e];
+          v[i] = XH ? rk_ld(x + e) - rk_ld(xh + e) : rk_ld(x + e);
         }
       }
 #pragma unroll
