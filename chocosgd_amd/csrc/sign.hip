@@ -729,6 +729,9 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
   bool all_uniform = true;
 #pragma unroll
   for (int r = 0; r < kSAccRows; ++r) all_uniform &= s_lo[rb + r] == s_hi[rb + r];
+  // (Buffer loads at each lane's own run offset, as sign_pack1_kernel -- no tail loads, no
+  // realigning shuffle -- measured slower here: 1212-1222 against 1153-1155 us at 345M, fused
+  // step 1140-1157 against 1065-1066; r05_ab_summary.txt item 20.)
   if (interior && all_uniform) {
     // fast path: no segment lookups, no global memory op besides the prefetch and the stores
     for (int r0 = rb; r0 < rb + kSAccRows; r0 += RU) {
