@@ -699,6 +699,8 @@ CHOCO_DEV float qdecode(uint32_t level, bool neg, const QParam& P, float sf) {
   return (((P.scale * sg) * P.norm) * lvl) / sf;
 }
 
+// (non-temporal stores: whole steps within noise, qsgd 0.4735-0.4770 against 0.4735-0.4804 ms;
+// r05_ab_summary.txt item 21)
 CHOCO_DEV void st_dec4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 // MODE 0: out = decode(msg 0); MODE 1: accumulate all messages into hat/mem.
