@@ -56,7 +56,8 @@ __global__ __launch_bounds__(kEwThreads) void sparse_acc_kernel(const float* __r
 // and per-element updates (80-99 against 77.5-80 us), non-temporal segment loads / stores;
 // r05: one thread per update with return-less float atomics, agent or workgroup scope, 97 /
 // 103 us against 77 (top-k / random-k at k = 1M); non-temporal segment stores (whole steps
-// within 1 %) or loads + stores (+3.5-6 us here; random-k's step -3.6 %, top-k's +3.7 %).
+// within 1 %), loads + stores (+3.5-6 us here; random-k's step -3.6 %, top-k's +3.7 %), or
+// loads alone (+3-6 us; the fused top-k step's next stream +30 us): r05_ab_summary.txt 15, 22.
 CHOCO_DEV float4 acc_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 CHOCO_DEV void acc_st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 constexpr int kSegF = 16;              // floats per owned segment (64 B)
