@@ -690,7 +690,28 @@ static unsigned sign_acc_grid(int64_t Np) {
   const int64_t ncb = (Np + kSignCols - 1) / kSignCols;
   return kSAccRB == 1 ? (unsigned)ncb : (unsigned)((ncb + 7) / 8 * 8 * kSAccRB);
 }
-template <int NM, bool HS>
+// NT (large buffers, n >= kSaccNtMin: x_hat and memory far beyond the 256 MB Infinity Cache):
+// the interior rows' loads and stores non-temporal, so the receive does not leave dirty lines
+// in the cache for the next step's pack to meet.  Same-box A/B (r05_ab_summary.txt item 23):
+// `sign` (345M) 1.351-1.370 against 1.415-1.468 ms per step; at ResNet-50's 25.6M, whose x_hat
+// and memory fit the cache, non-temporal was 11 % slower (plain kept there).
+constexpr int64_t kSaccNtMin = int64_t(1) << 25;
+template <bool NT>
+CHOCO_DEV float4 sacc_ld4(const float* p) {
+  if (NT) return ld_nt4(p);
+  return *reinterpret_cast<const float4*>(p);
+}
+template <bool NT>
+CHOCO_DEV void sacc_st4(float* p, float4 v) {
+  if (NT) {
+    choco_f32x4 f;
+    f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
+    __builtin_nontemporal_store(f, reinterpret_cast<choco_f32x4*>(p));
+    return;
+  }
+  *reinterpret_cast<float4*>(p) = v;
+}
+template <int NM, bool HS, bool NT = false>
 __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs M, int64_t n, int64_t Np,
                                                                        const int64_t* __restrict__ seg_off,
                                                                        int nseg, float* __restrict__ hat,
@@ -739,10 +760,10 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         const int64_t A = ((int64_t)(r0 + u) * Np + j0) & ~(int64_t)3;
-        pm[u] = *reinterpret_cast<const float4*>(mem + A + 4 * lane);
+        pm[u] = sacc_ld4<NT>(mem + A + 4 * lane);
         tm[u] = *reinterpret_cast<const float4*>(mem + A + 256);
         if (HS) {
-          ph[u] = *reinterpret_cast<const float4*>(hat + A + 4 * lane);
+          ph[u] = sacc_ld4<NT>(hat + A + 4 * lane);
           th[u] = *reinterpret_cast<const float4*>(hat + A + 256);
         }
       }
@@ -769,8 +790,8 @@ __global__ __launch_bounds__(kSignThreads) void sign_accumulate_kernel(SignMsgs 
 #pragma unroll
         for (int c = 0; c < 4; ++c) sign_apply<NM>(M, sc, x8, 4 + c - m, hv[c], mv[c]);
         if (lane != 0 || m == 0) {
-          *reinterpret_cast<float4*>(mem + e) = make_float4(mv[0], mv[1], mv[2], mv[3]);
-          if (HS) *reinterpret_cast<float4*>(hat + e) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+          sacc_st4<NT>(mem + e, make_float4(mv[0], mv[1], mv[2], mv[3]));
+          if (HS) sacc_st4<NT>(hat + e, make_float4(hv[0], hv[1], hv[2], hv[3]));
         } else {
 #pragma unroll
           for (int c = 1; c < 4; ++c) {  // lane 0: elements before the run belong to the previous wave
@@ -1448,15 +1469,24 @@ CHOCO_API int choco_sign_decompress_accumulate(const int32_t* const* packed_list
   const int64_t Np = choco_sign_words(n);
   const unsigned grid = sign_acc_grid(Np);
   profile_begin("sign_accumulate", st);
-#define CHOCO_SIGN_ACC(NM)                                                                                 \
-  case NM:                                                                                                  \
-    if (self_slot >= 0 && xhat_self)                                                                        \
-      CHOCO_KLAUNCH((sign_accumulate_kernel<NM, true>), dim3(grid), dim3(kSignThreads), 0, st, M, n,   \
-                         Np, seg_off, nseg, xhat_self, memory);                                             \
-    else                                                                                                    \
-      CHOCO_KLAUNCH((sign_accumulate_kernel<NM, false>), dim3(grid), dim3(kSignThreads), 0, st, M, n,  \
-                         Np, seg_off, nseg, xhat_self, memory);                                             \
+#define CHOCO_SIGN_ACC_L(NM, HS, NT)                                                                          \
+  CHOCO_KLAUNCH((sign_accumulate_kernel<NM, HS, NT>), dim3(grid), dim3(kSignThreads), 0, st, M, n, Np, seg_off, \
+                nseg, xhat_self, memory)
+#define CHOCO_SIGN_ACC(NM)                                       \
+  case NM:                                                       \
+    if (self_slot >= 0 && xhat_self) {                           \
+      if (nt)                                                    \
+        CHOCO_SIGN_ACC_L(NM, true, true);                        \
+      else                                                       \
+        CHOCO_SIGN_ACC_L(NM, true, false);                       \
+    } else {                                                     \
+      if (nt)                                                    \
+        CHOCO_SIGN_ACC_L(NM, false, true);                       \
+      else                                                       \
+        CHOCO_SIGN_ACC_L(NM, false, false);                      \
+    }                                                            \
     break;
+  const bool nt = n >= kSaccNtMin;
   switch (nmsg) {
     CHOCO_SIGN_ACC(1)
     CHOCO_SIGN_ACC(2)
@@ -1468,6 +1498,7 @@ CHOCO_API int choco_sign_decompress_accumulate(const int32_t* const* packed_list
     CHOCO_SIGN_ACC(8)
   }
 #undef CHOCO_SIGN_ACC
+#undef CHOCO_SIGN_ACC_L
   profile_end("sign_accumulate", st);
   CHOCO_LAUNCHED("sign_accumulate_kernel");
   return CHOCO_OK;
