@@ -700,7 +700,9 @@ CHOCO_DEV float qdecode(uint32_t level, bool neg, const QParam& P, float sf) {
 }
 
 // (non-temporal stores: whole steps within noise, qsgd 0.4735-0.4770 against 0.4735-0.4804 ms;
-// r05_ab_summary.txt item 21)
+// loads + stores: the decode 271 -> 300 us, qsgd 0.475-0.480 -> 0.489-0.493 ms; r05_ab_summary.txt
+// items 21, 24)
+CHOCO_DEV float4 qdec_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 CHOCO_DEV void st_dec4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 // MODE 0: out = decode(msg 0); MODE 1: accumulate all messages into hat/mem.
@@ -724,12 +726,12 @@ __global__ __launch_bounds__(kQThreads) void qsgd_decode_kernel(QMsgs M, int64_t
   const bool has_self = MODE == 1 && M.self_slot >= 0 && hat != nullptr;
   if (MODE == 1) {
     if (full) {
-      const float4 a0 = *reinterpret_cast<const float4*>(mem + e0);
-      const float4 a1 = *reinterpret_cast<const float4*>(mem + e0 + 4);
+      const float4 a0 = qdec_ld4(mem + e0);
+      const float4 a1 = qdec_ld4(mem + e0 + 4);
       mv[0] = a0.x; mv[1] = a0.y; mv[2] = a0.z; mv[3] = a0.w; mv[4] = a1.x; mv[5] = a1.y; mv[6] = a1.z; mv[7] = a1.w;
       if (has_self) {
-        const float4 b0 = *reinterpret_cast<const float4*>(hat + e0);
-        const float4 b1 = *reinterpret_cast<const float4*>(hat + e0 + 4);
+        const float4 b0 = qdec_ld4(hat + e0);
+        const float4 b1 = qdec_ld4(hat + e0 + 4);
         hv[0] = b0.x; hv[1] = b0.y; hv[2] = b0.z; hv[3] = b0.w; hv[4] = b1.x; hv[5] = b1.y; hv[6] = b1.z; hv[7] = b1.w;
       }
     } else {
