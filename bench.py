@@ -76,7 +76,7 @@ STAGES = {
 }
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -101,7 +101,10 @@ def parse():
     p.add_argument("--no-e2e", action="store_true", help="skip the host-resident (PCIe-inclusive) leg")
     p.add_argument("--lib", default=None, help=argparse.SUPPRESS)
     p.add_argument("--no-kernel-events", action="store_true", help=argparse.SUPPRESS)  # diagnostic
-    return p.parse_args()
+    p.add_argument("--dist-timeout", type=float, default=300.0,
+                   help="seconds for init_process_group and every collective before a rank gives up")
+    p.add_argument("--die-before-exchange", type=int, default=None, help=argparse.SUPPRESS)  # launcher test
+    return p.parse_args(argv)
 
 
 def traffic_key(args):
@@ -119,19 +122,59 @@ def _free_port():
     return port
 
 
-def spawn_ranks(n):
+def rank_exit_code(rc):
+    """A child's return code as this launcher's exit code: 0 only for 0.  Popen reports a
+    rank killed by signal s as -s, which max() over return codes would have hidden; it maps
+    to 128 + s, as a shell reports it."""
+    if rc is None or rc == 0:
+        return 0 if rc == 0 else 1
+    return 128 - rc if rc < 0 else rc
+
+
+def wait_ranks(procs, poll_s=0.2):
+    """Wait for every rank; on the first one that fails (non-zero exit or a signal),
+    terminate its siblings (then kill those that ignore it) so none is left blocked in a
+    collective, and return that rank's exit code.  0 when all ranks exit 0."""
+    first = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and first == 0:
+                first = rank_exit_code(rc)
+                print(f"bench.py: rank pid {p.pid} exited with {rc}; stopping {len(live)} sibling rank(s)",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+                deadline = time.time() + 10.0
+                for q in live:
+                    try:
+                        q.wait(timeout=max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                live = []
+                break
+        if live:
+            time.sleep(poll_s)
+    return first
+
+
+def spawn_ranks(n, argv=None):
     """`python bench.py --gpus N` with no launcher: one child process per rank, started
-    before this process makes any GPU call (it never makes one); exits with the worst rc."""
+    before this process makes any GPU call (it never makes one).  Returns 0 only when every
+    rank exits 0; the first failing rank (exit code or signal) stops the others."""
     port = str(_free_port())
     procs = []
+    argv = sys.argv[1:] if argv is None else argv
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rc = 0
-    for p in procs:
-        rc = max(rc, p.wait())
-    return rc
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    return wait_ranks(procs)
 
 
 class Worker:
@@ -591,6 +634,14 @@ def cpu_baseline(w):
             "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(), "usable_cpus": usable, "rows": rows}
 
 
+def _bench_device(torch, local):
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        raise SystemExit("bench.py: no GPU visible (the codec has no CPU path)")
+    torch.cuda.set_device(local % ndev)
+    return torch.device("cuda", local % ndev)
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -600,15 +651,27 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = torch.cuda.device_count()
-    torch.cuda.set_device(local % ndev)
-    dev = torch.device("cuda", local % ndev)
+    dev = None
     if world > 1:
+        import datetime
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # bounded: a rank that never arrives (or dies) fails the others instead of hanging them
+        tmo = datetime.timedelta(seconds=args.dist_timeout)
         if args.backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+            dev = _bench_device(torch, local)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.init_process_group("gloo", rank=rank, world_size=world, timeout=tmo)
+        if args.die_before_exchange is not None:
+            # launcher test (tests/test_bench_launcher.py): one rank aborts, the others block in
+            # the first collective, as a rank killed before the exchange leaves them
+            if rank == args.die_before_exchange:
+                import signal
+                os.kill(os.getpid(), signal.SIGABRT)
+            dist.barrier()
+            raise SystemExit("bench.py: --die-before-exchange: the barrier returned")
+    if dev is None:
+        dev = _bench_device(torch, local)
     from chocosgd_amd import _lib, codec
     if args.lib:
         _lib.load(args.lib)

@@ -287,8 +287,14 @@ CHOCO_API int choco_sparse_accumulate_multi(const float* const* vals, const int3
   CHOCO_REQUIRE(vals && idxs && ks && weights && memory, "null pointer argument");
   CHOCO_REQUIRE(nmsg >= 1 && nmsg <= kMaxMsgs, "nmsg must be in [1, %d], got %d", kMaxMsgs, (int)nmsg);
   CHOCO_REQUIRE(self_slot >= -1 && self_slot < nmsg, "self_slot out of range");
+  CHOCO_REQUIRE(n > 0, "n must be positive");
+  // every message is checked before the first launch: a bad message m must not leave
+  // messages 0..m-1 applied (a retry would apply them twice)
   for (int m = 0; m < nmsg; ++m) {
     CHOCO_REQUIRE(ks[m] >= 0 && ks[m] < (int64_t)INT32_MAX, "message %d: k out of range", m);
+    CHOCO_REQUIRE(ks[m] == 0 || (vals[m] != nullptr && idxs[m] != nullptr), "message %d: null pointer", m);
+  }
+  for (int m = 0; m < nmsg; ++m) {
     if (ks[m] == 0) continue;  // an empty message changes nothing
     const int rc = choco_sparse_accumulate(vals[m], idxs[m], ks[m], m == self_slot ? xhat_self : nullptr, memory, n,
                                            weights[m], bad_count, stream);

@@ -1532,9 +1532,15 @@ CHOCO_API int choco_sign_recv_gossip_compress(const int32_t* const* packed_list,
   CHOCO_REQUIRE(aligned16(x) && aligned16(memory) && aligned16(xhat) && aligned16(packed),
                 "x/memory/xhat/packed must be 16-byte aligned");
   CHOCO_REQUIRE(ws && ws_bytes >= choco_sign_workspace_size(nseg), "sign workspace too small");
-  for (int q = 0; q < nmsg; ++q) {
-    CHOCO_REQUIRE(packed_list[q] && norms_list[q], "null message pointer");
-    CHOCO_REQUIRE(packed_list[q] != packed, "the output words must not alias a message being applied");
+  {
+    // the output words must not overlap any message's words (the row-run pass reads the
+    // message planes while it writes the output): a range test, not a start-pointer test
+    const int64_t nw = choco_sign_words(n);
+    for (int q = 0; q < nmsg; ++q) {
+      CHOCO_REQUIRE(packed_list[q] && norms_list[q], "null message pointer");
+      CHOCO_REQUIRE(packed + nw <= packed_list[q] || packed_list[q] + nw <= packed,
+                    "the output words overlap message %d's words", q);
+    }
   }
   if (n >= (int64_t(1) << 30)) {  // past 32-bit buffer offsets: the receive, then the fused consensus step + pack
     // (the pack's accumulators may hold an earlier row-run call's planes: zero them)

@@ -159,15 +159,34 @@ class _CHOCOBase(object):
             raise RuntimeError("deferred receive: the previous step's messages were never applied")
         self._pending = (parts, weights, self_slot, memory, xhat_self, lay)
 
+    def _require_fused_consensus(self, g):
+        """A pending receive may only be applied by a compress whose first pass runs the
+        consensus step itself (then that pass reads x_hat / memory after the receive).  With
+        the consensus step run outside (g is None: the reference's ParallelCHOCO_V.step),
+        recover_params and update_params_from_neighbor have already read the stale x_hat and
+        memory, so x and this step's message would silently diverge from the reference."""
+        if self._pending is not None and g is None:
+            raise RuntimeError("deferred receive pending: call compressor.flush_receive() before recover_params / "
+                               "update_params_from_neighbor (the previous step ran with defer_receive=True)")
+
+    def _flush_before_pass(self, g):
+        """Compress paths that never take a receive into their own pass: apply a pending one
+        first (valid only with the consensus step fused into this compress)."""
+        self._require_fused_consensus(g)
+        self.flush_receive()
+
     def _take_pending(self, x, xh, g, lay):
         """The pending receive if this compress can apply it in its first pass (the
         consensus step fused, x_hat_i itself -- not a copy -- as flatten_hat_params);
-        otherwise it is applied on its own first (flush_receive), and None."""
+        otherwise it is applied on its own first (flush_receive; the fused consensus step
+        then reads the updated x_hat / memory), and None.  Raises when the consensus step
+        is not fused into this compress (_require_fused_consensus)."""
         pend = self._pending
         if pend is None:
             return None
+        self._require_fused_consensus(g)
         parts, weights, slot, memory, xhat_self, play = pend
-        if g is None or play is not lay:
+        if play is not lay:
             self.flush_receive()
             return None
         if g[0].data_ptr() != memory.data_ptr() or (slot >= 0 and xh.data_ptr() != xhat_self.data_ptr()):
@@ -177,10 +196,12 @@ class _CHOCOBase(object):
         return parts, weights, slot
 
     def flush_receive(self):
-        """Apply a deferred receive now (before reading x_hat / memory between steps)."""
+        """Apply a deferred receive now (before reading x_hat / memory between steps).  It runs
+        on the gossip stream, where the pending messages, memory and x_hat were written."""
         pend, self._pending = self._pending, None
         if pend is not None:
-            self._apply(*pend)
+            with torch.cuda.stream(self.gossip_stream):
+                self._apply(*pend)
 
     @staticmethod
     def _self_slot(ranks, neighbor_hat_params):
@@ -253,9 +274,9 @@ class CHOCOSparsificationCompressor(_CHOCOBase):
             msg = sync_buffer["wire_message"]
             codec.sparse_accumulate(msg[:K].view(torch.float32), msg[K:], hat, 1.0, guard=guard)
         self.aggregator_fn.complete_wait(sync_buffer["sync_reqs"])
-        # every message into memory in ONE sweep, in neighbors_info order (each touched line
-        # of memory read and written once per step, not once per message; bit-identical to
-        # the reference's per-neighbour loop)
+        # every message applied by ONE call that runs the per-message kernels in neighbors_info
+        # order (bit-identical to the reference's per-neighbour loop); a merged one-sweep form
+        # was measured slower and removed ("Sparse accumulate")
         msgs, weights, slot, hat = [], [], -1, None
         for rank, weight in neighbors_info.items():
             hat_params = neighbor_hat_params[rank if rank in neighbor_hat_params else "memory"]
@@ -296,7 +317,7 @@ class CHOCOQuantizationCompressor(_CHOCOBase):
         q = int(self.quantize_level)
         g = self._gossip(sync_buffer)
         if q == 32 or self.exchange_chunks > 1:
-            self.flush_receive()  # (never deferred on these paths)
+            self._flush_before_pass(g)  # (never deferred on these paths)
         if q != 32 and self.exchange_chunks > 1:
             return self._compress_chunked(sync_buffer, x, xh, lay, q, g)
         sync_buffer.pop("chunked", None)
@@ -465,7 +486,7 @@ class CHOCOSignCompressor(_CHOCOBase):
         g = self._gossip(sync_buffer)
         sync_buffer.pop("chunked", None)
         if self.exchange_chunks > 1:
-            self.flush_receive()  # (never deferred on this path)
+            self._flush_before_pass(g)  # (never deferred on this path)
             sync_buffer["chunked"] = self._pack_and_post(sync_buffer, x, xh, lay, g, message, signs, norms)
         else:
             pend = self._take_pending(x, xh, g, lay)

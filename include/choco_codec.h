@@ -370,7 +370,10 @@ int choco_qsgd_decompress_accumulate(const uint8_t* const* packed_list,
  * norm_in = norms_out, ...).  Valid wherever the receive of step t-1 and the consensus
  * step of step t are adjacent (ParallelCHOCO_V.step: apply_gradient, then the previous
  * gossip's join, then update_params_from_neighbor).  nmsg 1..8; ws as for
- * choco_qsgd_norms (choco_qsgd_workspace_size(nseg)). */
+ * choco_qsgd_norms (choco_qsgd_workspace_size(nseg)).  norms_out MAY alias a message's
+ * norms (e.g. the pending self message's header, reused as this step's): every workgroup
+ * reads the message norms before it takes the last-workgroup ticket, and only the last
+ * workgroup writes norms_out.  The level / sign planes must not overlap x, x_hat or memory. */
 int choco_qsgd_recv_gossip_norms(const uint8_t* const* packed_list, const float* const* norms_list,
                                  const float* weights, int32_t nmsg, int32_t self_slot, float* x,
                                  float* memory, float* xhat, float gamma, int64_t n,
