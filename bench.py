@@ -92,8 +92,16 @@ def parse(argv=None):
                    help="top-k: fold the self message's uncompress (x_hat, and memory when the self rank is first) "
                         "into the compress emission (choco_topk_compress_accumulate)")
     p.add_argument("--ring3-loopback", action="store_true",
-                   help="sparse codecs on one GPU: each step applies the self message plus two neighbour messages "
-                        "(compressed from other resident deltas, no exchange) -- a ring worker's receive (cfg 4)")
+                   help="one GPU: each step applies the self message plus two neighbour messages, no exchange -- a "
+                        "ring worker's receive (cfg 4).  topk/randk workloads: the neighbours' messages are compressed "
+                        "once from other resident deltas; step_* workloads: they are this worker's own messages of "
+                        "the two previous steps (same codec, same magnitudes, other index sets)")
+    p.add_argument("--grad-lr", type=float, default=0.1,
+                   help="step_* workloads: apply_gradient (optim/utils.py:13-47, no momentum / weight decay) "
+                        "x -= lr * g at the start of every step; 0 = off (round-5 steps)")
+    p.add_argument("--grad-scale", type=float, default=0.01,
+                   help="step_* workloads: the synthetic gradient g ~ N(0, scale^2), a fresh seeded draw every step "
+                        "(with the gradient on, x_hat and memory start as copies of x, as the reference's do)")
     p.add_argument("--defer-receive", action="store_true",
                    help="step_* workloads: apply each step's received messages inside the NEXT step's first pass "
                         "(receive + consensus step + first compress pass in one kernel; same x / x_hat / memory)")
@@ -233,8 +241,15 @@ class Worker:
             # x, x_hat, memory resident; x moves every step (the consensus step), so every
             # step selects a new index set
             self.x = torch.randn(self.n, generator=g, device=dev)
-            self.hat = self.x + 0.1 * torch.randn(self.n, generator=g, device=dev)
-            self.mem = self.hat + 0.05 * torch.randn(self.n, generator=g, device=dev)
+            if args.grad_lr > 0:
+                # the reference's start: x_hat_i and memory are copies of the parameters
+                # (parallel_choco_v.py:94-97); the gradient then drives the delta
+                self.hat = self.x.clone()
+                self.mem = self.x.clone()
+            else:
+                # round 5's synthetic state (no gradient: the delta would stay 0)
+                self.hat = self.x + 0.1 * torch.randn(self.n, generator=g, device=dev)
+                self.mem = self.hat + 0.05 * torch.randn(self.n, generator=g, device=dev)
             self.ds = [self.x]
         else:
             self.ds = [torch.randn(self.n, generator=g, device=dev) for _ in range(max(1, args.nbuf))]
@@ -257,9 +272,23 @@ class Worker:
         # step's (own) message, so the own message alternates between two buffers
         self.msg_pp = [self.msg, torch.zeros_like(self.msg)] if (self.defer and self.op == "sign") else None
         self.loop_sets = None
-        if args.ring3_loopback:
+        self.ring_msgs = None
+        if args.ring3_loopback and self.step_mode:
+            if world != 1:
+                raise SystemExit("--ring3-loopback: --gpus 1 only")
+            # a ring worker's neighbourhood {r-1, r, r+1} (weights 1/3, the self message second);
+            # the neighbours' messages are this worker's own of steps t-1 and t-2: four message
+            # buffers in rotation (the deferred receive still reads step t-1's while step t writes)
+            self.ranks, self.self_slot = ["left", rank, "right"], 1
+            self.weights = [1.0 / 3] * 3
+            self.fold, self.fold_mem = False, False
+            self.ring_msgs = [self.msg] + [torch.zeros_like(self.msg) for _ in range(3)]
+            self.msg_pp = None
+            self.recv = {"left": self.ring_msgs[3], "right": self.ring_msgs[2]}
+            self.label += "_ring3_loopback"
+        elif args.ring3_loopback:
             if self.op not in ("topk", "topk_seg", "randk") or world != 1:
-                raise SystemExit("--ring3-loopback: sparse workloads at --gpus 1 only")
+                raise SystemExit("--ring3-loopback: sparse workloads (or step_*) at --gpus 1 only")
             # a ring worker's neighbourhood {r-1, r, r+1} (weights 1/3, the self message second):
             # the two neighbour messages come from other deltas, compressed once per rotation slot
             self.ranks, self.self_slot = ["left", rank, "right"], 1
@@ -284,6 +313,14 @@ class Worker:
                 self.loop_sets.append(pair)
             self.recv = self.loop_sets[0]
             self.label += "_ring3_loopback"
+        # apply_gradient (optim/utils.py:13-47; momentum and weight decay 0): x -= lr * g at the
+        # start of every step, g a FRESH seeded draw N(0, scale^2) each step
+        self.grads, self.grad_lr, self.grad_scale, self.grad_events = None, 0.0, 0.0, None
+        if self.step_mode and args.grad_lr > 0:
+            self.grad_gen = torch.Generator(device=dev).manual_seed(3000 + rank)
+            self.grads = torch.empty(self.n, device=dev)
+            self.grad_lr, self.grad_scale = args.grad_lr, args.grad_scale
+            self.label += f"_grad_lr{args.grad_lr:g}_scale{args.grad_scale:g}"
         if self.backend == "gloo":
             self.msg_h = torch.empty(self.msg.shape, dtype=self.msg.dtype).pin_memory()
             self.recv_h = {r: torch.empty_like(self.msg_h).pin_memory() for r in self.peers}
@@ -295,7 +332,23 @@ class Worker:
         self.d = self.ds[self.step_id % len(self.ds)]
         if self.loop_sets:
             self.recv = self.loop_sets[self.step_id % len(self.loop_sets)]
+        if self.ring_msgs:
+            t = self.step_id
+            self.msg = self.ring_msgs[t % 4]
+            if self.op in ("qsgd", "sign"):
+                self.wire = self._parts(self.msg)
+            self.recv = {"left": self.ring_msgs[(t - 1) % 4], "right": self.ring_msgs[(t - 2) % 4]}
         if self.step_mode:
+            if self.grads is not None:
+                ev = None
+                if self.grad_events is not None:
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record()
+                self.grads.normal_(0.0, self.grad_scale, generator=self.grad_gen)
+                self.x.add_(self.grads, alpha=-self.grad_lr)
+                if ev:
+                    ev[1].record()
+                    self.grad_events.append(ev)
             self.compress_step()
         elif self.op == "topk":
             c.topk(self.d, self.k, out=(self.msg[:self.k].view(torch.float32), self.msg[self.k:]),
@@ -343,8 +396,9 @@ class Worker:
         elif self.pending is not None:  # sign: receive + consensus step + pack, one kernel
             parts, weights, slot = self.pending
             self.pending = None
-            self.msg = self.msg_pp[self.step_id % 2]
-            self.wire = self._parts(self.msg)
+            if self.msg_pp:
+                self.msg = self.msg_pp[self.step_id % 2]
+                self.wire = self._parts(self.msg)
             c.sign_recv_gossip_compress(parts, weights, slot, self.x, self.mem, self.hat, GAMMA, out=self.wire,
                                         **self._seg())
         else:
@@ -437,6 +491,40 @@ class Worker:
             self.hat_self_update()
         self.exchange_finish(works)
         self.decompress(hat_done=overlap)
+
+    def warm_counters(self):
+        """Counters behind the warm-start hit rate (top-k): sample launches, K2 prologue
+        samples, exact fallbacks / segment window misses, calls.  None for other codecs."""
+        c = self.codec
+        from chocosgd_amd import _lib
+        if self.op == "topk":
+            return {"calls": c.launch_count("topk_stream"), "k1_sample_launches": c.launch_count("topk_bounds"),
+                    "k2_prologue_samples": c.topk_workspace_word(_lib.TOPK_K2_SAMPLES_OFFSET),
+                    "exact_fallbacks": c.topk_workspace_word(_lib.TOPK_FALLBACKS_OFFSET)}
+        if self.op == "topk_seg":
+            return {"calls": c.launch_count("topk_seg_collect"), "s1_cold_passes": c.launch_count("topk_seg_hist"),
+                    "segment_window_misses": c.topk_workspace_word(_lib.TOPK_FALLBACKS_OFFSET, plan=self.plan)}
+        return None
+
+    def warm_rates(self, before, steps):
+        """Per-step rates of warm_counters() over the timed region, and the warm-call share."""
+        if before is None:
+            return None
+        after = self.warm_counters()
+        d = {k: after[k] - before[k] for k in after}
+        calls = max(d["calls"], 1)
+        if self.op == "topk":
+            cold = d["k1_sample_launches"] + d["k2_prologue_samples"] + d["exact_fallbacks"]
+            note = ("warm = took the previous call's window without a fallback; cold = a K1 sample launch, a K2 "
+                    "prologue sample (cold run after a warm miss) or an exact fallback")
+        else:
+            cold = d["s1_cold_passes"]
+            note = ("warm = one read against the segments' carried windows (W2); cold = the S1 + S2 sequence "
+                    "(cold run after a window miss); segment_window_misses counts segments, not calls")
+        r = {k + "_per_step": round(v / steps, 3) for k, v in d.items()}
+        r["warm_call_share"] = round(max(0.0, 1.0 - cold / calls), 3)
+        r["note"] = note
+        return r
 
     def stage_bytes(self):
         """Algorithmic HBM bytes per step of each stage, and the
@@ -715,6 +803,7 @@ def main():
     dom_kernel = max((k for k in dom_k if k in pre), key=lambda k: pre[k][0], default=None)
     codec.profile_reset()
     codec.profile_filter([dom_kernel] if dom_kernel else dom_k)
+    warm0 = w.warm_counters()  # (synchronises: before the timed region)
     codec.profile_enable(not args.no_kernel_events)
     barrier()
     t0 = time.perf_counter()
@@ -726,6 +815,7 @@ def main():
     timed = stage_times(args.steps)
     # calls that took the exact fallback so far (top-k: the flat workspace's counter)
     fallbacks = codec.topk_fallback_count() if w.op == "topk" else None
+    warm_start = w.warm_rates(warm0, args.steps)
 
     # untimed pass: every kernel, plus the exchange on its own events
     codec.profile_reset()
@@ -733,6 +823,8 @@ def main():
     codec.profile_enable(True)
     npass = min(args.steps, 10)
     ex_ms = []
+    if w.grads is not None:
+        w.grad_events = []
     for _ in range(npass):
         w.compress()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -745,6 +837,10 @@ def main():
     codec.profile_enable(False)
     untimed = stage_times(npass)
     exchange_us = statistics.median(a.elapsed_time(b) * 1e3 for a, b in ex_ms) if w.peers else 0.0
+    grad_us = None
+    if w.grad_events:
+        grad_us = statistics.median(a.elapsed_time(b) * 1e3 for a, b in w.grad_events)
+        w.grad_events = None
     # top-k: the same compress with the warm start off (every call samples its window
     # in K1 / reads twice in the segmented path), beside the warm numbers above
     cold = None
@@ -853,6 +949,12 @@ def main():
             "kernels_us": {k: round(v[1], 2) for k, v in untimed.items()},
             "exchange_us": round(exchange_us, 1),
             "topk_fallbacks": fallbacks,
+            "warm_start": warm_start,
+            "apply_gradient": None if grad_us is None else {
+                "us": round(grad_us, 1), "lr": args.grad_lr, "scale": args.grad_scale,
+                "note": "g ~ N(0, scale^2) drawn fresh each step, then x -= lr * g (optim/utils.py:13-47, no "
+                        "momentum / weight decay): torch ops inside the timed step (ms_per_step includes them); not "
+                        "part of the codec stages"},
             "cold_start": cold_entry,
             "e2e": None,
             "cpu_baseline": None,

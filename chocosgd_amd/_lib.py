@@ -15,6 +15,8 @@ LIB_PATH = os.environ.get("CHOCO_CODEC_LIB") or os.path.join(_HERE, "lib", "libc
 
 TOPK_STATUS_OFFSET = 0        # CHOCO_TOPK_STATUS_OFFSET
 TOPK_FALLBACKS_OFFSET = 4     # CHOCO_TOPK_FALLBACKS_OFFSET
+TOPK_COLD_LEFT_OFFSET = 8     # CHOCO_TOPK_COLD_LEFT_OFFSET
+TOPK_K2_SAMPLES_OFFSET = 16   # CHOCO_TOPK_K2_SAMPLES_OFFSET
 TOPK_STATUS_POLL_TIMEOUT = 1  # CHOCO_TOPK_STATUS_POLL_TIMEOUT
 
 _c_i32, _c_i64, _c_u64, _c_f32, _c_f64 = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
@@ -98,6 +100,7 @@ SIGNATURES = {
     "choco_profile_filter": (_c_i32, [ctypes.c_char_p]),
     "choco_profile_read": (_c_i32, [ctypes.c_char_p, ctypes.POINTER(_c_f64), ctypes.POINTER(_c_i64)]),
     "choco_profile_reset": (_c_i32, []),
+    "choco_launch_count": (_c_i64, [ctypes.c_char_p]),
 }
 
 _lib = None

@@ -1082,5 +1082,25 @@ def profile_reset():
     lib().choco_profile_reset()
 
 
+def launch_count(name):
+    """Launches of kernel `name` since the library was loaded (counted with profiling off)."""
+    return int(lib().choco_launch_count(name.encode()))
+
+
+def topk_workspace_word(off, dev=None, plan=None):
+    """Diagnostic: the uint32 at byte `off` of this stream's flat top-k workspace (or of
+    `plan`'s segmented one); include/choco_codec.h CHOCO_TOPK_*_OFFSET.  Synchronises."""
+    dev = torch.device(dev) if dev is not None else torch.device("cuda", torch.cuda.current_device())
+    if plan is not None:
+        ws = plan.workspace(dev)
+    else:
+        with _ws_lock:
+            ws = _ws_cache.get((dev.index, torch.cuda.current_stream(dev).cuda_stream, "topk"))
+        if ws is None:
+            return 0
+    torch.cuda.current_stream(dev).synchronize()
+    return int(ws[off:off + 4].view(torch.int32).item())
+
+
 def is_pow2_minus1(s):
     return s >= 1 and (s + 1) & s == 0 and int(math.log2(s + 1)) <= 16

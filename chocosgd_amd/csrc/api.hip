@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <atomic>
 #include <map>
+#include <unordered_map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -44,9 +45,17 @@ static std::vector<std::string> g_filter;  // only these kernel names are timed 
 static std::vector<hipEvent_t> g_free_ev;  // events are reused: no create/destroy per launch
 
 static thread_local ProfArm g_armed{nullptr, nullptr};
+// launches per kernel name, counted whether or not timing is on (choco_launch_count: the
+// bench's warm-hit rates; names are the string literals of the call sites)
+static std::mutex g_cnt_mu;
+static std::unordered_map<const char*, int64_t> g_launches;
 
 void profile_begin(const char* name, hipStream_t) {
   g_armed = ProfArm{nullptr, nullptr};
+  {
+    std::lock_guard<std::mutex> g(g_cnt_mu);
+    ++g_launches[name];
+  }
   if (!g_prof_on.load(std::memory_order_relaxed)) return;
   std::lock_guard<std::mutex> g(g_prof_mu);
   if (!g_filter.empty() && std::find(g_filter.begin(), g_filter.end(), std::string(name)) == g_filter.end()) return;
@@ -137,6 +146,14 @@ CHOCO_API int choco_profile_read(const char* name, double* total_ms, int64_t* co
   if (total_ms) *total_ms = it == g_acc.end() ? 0.0 : it->second.first;
   if (count) *count = it == g_acc.end() ? 0 : it->second.second;
   return CHOCO_OK;
+}
+
+CHOCO_API int64_t choco_launch_count(const char* name) {
+  std::lock_guard<std::mutex> g(g_cnt_mu);
+  int64_t n = 0;
+  for (const auto& e : g_launches)
+    if (name && strcmp(e.first, name) == 0) n += e.second;
+  return n;
 }
 
 CHOCO_API int choco_profile_reset(void) {

@@ -38,13 +38,10 @@ struct SignWs {
   // double acc[nseg] follows at offset 256
 };
 
-template <bool NT = false>
-CHOCO_DEV void st_buf4s(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, float4 v) {
-  choco_f32x4 f;
-  f.x = v.x; f.y = v.y; f.z = v.z; f.w = v.w;
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, f), r,
-                                         voff, soff, NT ? 2 : 0);
-}
+// (16-B stores go through choco_common.h's st_buf4: soffset is always the constant 0.  A
+// 16-B buffer store with an SGPR soffset gets no wait state from the compiler before a VALU
+// overwrites its data registers, and on gfx950 it can then store the new values -- DESIGN.md
+// section 4, "The r5m wrong stores"; tests/test_isa_hazards.py checks the built library.)
 
 CHOCO_DEV void load4g(const float* __restrict__ x, const float* __restrict__ xh, int64_t e, int64_t n,
                       float (&v)[4]) {
@@ -467,8 +464,21 @@ __global__ __launch_bounds__(kSignThreads * RS) void sign_pack1_kernel(const flo
       for (int u = 0; u < RU; ++u) {
         G.x[u] = gossip4(G.x[u], G.m[u], G.h[u], gs.gamma);
         // non-temporal: x_new is not re-read by this step, and dirty Infinity-Cache
-        // lines would be written back in the middle of the receiver's pass
-        st_buf4s<true>(rx, voff, row_off(rs0 + g * RU + u), G.x[u]);
+        // lines would be written back in the middle of the receiver's pass.
+        // The row offset goes in the VGPR offset, soffset 0: a 16-B buffer store whose
+        // soffset is an SGPR gets no wait state from the compiler before a VALU overwrites
+        // its data registers, and on gfx950 such a store can write the NEW values (the r5m
+        // wrong x / memory stores; DESIGN.md section 4, tests/test_isa_hazards.py).
+#if CHOCO_AB_SIGN_ST_SOFF  // (A/B only, round 6: round 5's scalar-offset store)
+        {
+          choco_f32x4 f;
+          f.x = G.x[u].x; f.y = G.x[u].y; f.z = G.x[u].z; f.w = G.x[u].w;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, f),
+                                                 rx, voff, row_off(rs0 + g * RU + u), 2);
+        }
+#else
+        st_buf4<true>(rx, voff + row_off(rs0 + g * RU + u), G.x[u]);
+#endif
       }
     }
 #pragma unroll
@@ -1223,9 +1233,9 @@ __global__ __launch_bounds__(kSignThreads) void sign_recv_rows_kernel(PlaneMsgs 
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const uint32_t off = (uint32_t)((e0 + 1024 * c + 4 * tid) * 4);
-        st_buf4s<false>(rx, off, 0u, xv[c]);
-        st_buf4s<false>(rm, off, 0u, mv[c]);
-        if (HS) st_buf4s<false>(rh, off, 0u, hv[c]);
+        st_buf4<false>(rx, off, xv[c]);
+        st_buf4<false>(rm, off, mv[c]);
+        if (HS) st_buf4<false>(rh, off, hv[c]);
       }
     } else {
 #pragma unroll
@@ -1539,7 +1549,7 @@ CHOCO_API int choco_sign_recv_gossip_compress(const int32_t* const* packed_list,
     for (int q = 0; q < nmsg; ++q) {
       CHOCO_REQUIRE(packed_list[q] && norms_list[q], "null message pointer");
       CHOCO_REQUIRE(packed + nw <= packed_list[q] || packed_list[q] + nw <= packed,
-                    "the output words overlap message %d's words", q);
+                    "the output words alias (overlap) message %d's words", q);
     }
   }
   if (n >= (int64_t(1) << 30)) {  // past 32-bit buffer offsets: the receive, then the fused consensus step + pack

@@ -115,7 +115,8 @@ struct TopkCtrl {
   uint32_t fallbacks;                            // calls that took the exact fallback (diagnostic counter)
   uint32_t cold_left;                            // warm-host calls still to sample their window in K2 (backoff)
   uint32_t backoff;                              // cold run length after the next warm miss
-  uint32_t pad0[12];
+  uint32_t k2_samples;                           // calls whose K2 took its window from its own sample (diagnostic)
+  uint32_t pad0[11];
   uint32_t overflow[2];                          // bit 0: a side list overflowed; bit 1: take the exact fallback
   uint32_t pad1[14];
   TopkBounds bounds[2];
@@ -124,6 +125,8 @@ struct TopkCtrl {
 };
 static_assert(offsetof(TopkCtrl, status) == CHOCO_TOPK_STATUS_OFFSET, "status word at the documented offset");
 static_assert(offsetof(TopkCtrl, fallbacks) == CHOCO_TOPK_FALLBACKS_OFFSET, "fallback counter at the documented offset");
+static_assert(offsetof(TopkCtrl, cold_left) == CHOCO_TOPK_COLD_LEFT_OFFSET, "cold-run word at the documented offset");
+static_assert(offsetof(TopkCtrl, k2_samples) == CHOCO_TOPK_K2_SAMPLES_OFFSET, "K2 sample counter at the documented offset");
 constexpr uint32_t kStatusPollTimeout = 1u;    // a bounded wait of the exact fallback gave up: output invalid
 constexpr uint32_t kNoCandKey = 0x7F800000u;   // window that admits only inf / NaN keys (invalid bounds)
 
@@ -898,6 +901,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
         B.k = k;
         B.valid = 1u;
         if (deg) atomicOr(&ctrl->overflow[par], 2u);
+        ctrl->k2_samples += 1u;  // (this call's only writer of the word)
       }
     } else {
       bk = ok ? make_buckets_from(W.s_lo, W.s_hi, W.shift, seed) : make_buckets_from(kNoCandKey, kNoCandKey, 0u, seed);

@@ -91,6 +91,12 @@ int choco_topk_host_status(const void* ws, int32_t clear, void* stream);
 /* Byte offset of a uint32 counter of calls (flat: the exact fallback; segmented: segments
  * whose warm window missed) in the same workspaces: diagnostics, never reset by the codec. */
 #define CHOCO_TOPK_FALLBACKS_OFFSET 4
+/* Flat workspaces only, diagnostics: the uint32 cold-run length (calls left that take a
+ * sampled window after a warm window missed) and a uint32 counter of calls whose stream
+ * kernel took that sample itself (never with the fused consensus step, whose x changes
+ * under the stream: the host then runs the separate sample kernel first). */
+#define CHOCO_TOPK_COLD_LEFT_OFFSET 8
+#define CHOCO_TOPK_K2_SAMPLES_OFFSET 16
 #define CHOCO_TOPK_STATUS_POLL_TIMEOUT 1
 int choco_topk_compress(const float* x, const float* xhat, int64_t n, int64_t k,
                         float* out_val, int32_t* out_idx,
@@ -473,6 +479,10 @@ int choco_profile_enable(int32_t on);
 int choco_profile_filter(const char* names);
 int choco_profile_read(const char* name, double* total_ms, int64_t* count);
 int choco_profile_reset(void);
+/* Launches of the named kernel since the library was loaded, counted whether or not
+ * profiling is enabled (diagnostic: the bench's per-step warm-hit rates, e.g. how many
+ * "topk_bounds" sample launches or "topk_seg_hist" cold passes a step took). */
+int64_t choco_launch_count(const char* name);
 
 #ifdef __cplusplus
 }

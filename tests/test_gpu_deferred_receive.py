@@ -238,6 +238,14 @@ def test_sign_recv_gossip_compress_rejects_aliased_output():
     x, hat, mem = _state(n, 3)
     with pytest.raises(RuntimeError, match="alias"):
         codec.sign_recv_gossip_compress(msgs, [0.5, 0.5], 0, x, mem, hat, GAMMA, out=msgs[0])
+    # a PARTIAL overlap (the output words start inside message 1's words) is refused too
+    words, norms = msgs[1]
+    big = torch.zeros(words.numel() + 64, dtype=torch.int32, device=DEV)
+    big[:words.numel()].copy_(words)
+    shifted = (big[:words.numel()], norms)
+    out = (big[32:32 + words.numel()], torch.empty_like(norms))
+    with pytest.raises(RuntimeError, match="alias"):
+        codec.sign_recv_gossip_compress([msgs[0], shifted], [0.5, 0.5], 0, x, mem, hat, GAMMA, out=out)
 
 
 @pytest.mark.parametrize("lens", [[37, 40_000, 5, 123_457], [163_499], golden_json("layouts.json")["resnet20_cifar10"]],

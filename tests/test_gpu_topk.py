@@ -453,6 +453,61 @@ def test_topk_warm_start_gossip_sequence():
         codec.sparse_accumulate(vals, idx, mem, 1.0, xhat_self=hat)
 
 
+def _ws_word(off):
+    from chocosgd_amd import codec
+    return codec.topk_workspace_word(off)
+
+
+def test_topk_fused_gossip_cold_run_takes_host_k1():
+    """Deterministic check of the round-5 race fix: a fused-gossip
+    call on a workspace that a warm miss put on a cold run must take its window from the
+    host-launched sample kernel (K1), never from K2's own prologue sample (K2 rewrites x
+    while it streams).  At 25M: (1) a cold fused call; (2) a warm fused call whose delta is
+    1000x larger, so the carried window misses (exact fallback, cold run started and
+    mirrored to the host); (3) a fused call on the cold run: K1 runs (profile count), K2's
+    sample counter does not move, the output is exact.  Then (4) the same cold run WITHOUT
+    the fused step samples inside K2 (the counter moves), so the counter is live."""
+    from chocosgd_amd import _lib, codec
+    n = 25_000_000
+    k = codec.topk_k(n, 0.99)
+    torch.cuda.synchronize()
+    codec.release_workspaces()
+    g = torch.Generator(device=DEV).manual_seed(4711)
+    x = torch.randn(n, generator=g, device=DEV)
+    hat = x + 0.1 * torch.randn(n, generator=g, device=DEV)
+    mem = hat + 0.05 * torch.randn(n, generator=g, device=DEV)
+
+    def fused_call(xx, mm, hh, expect_k1):
+        xa = O.gossip_step(host(xx), host(mm), host(hh), 0.9)
+        d = (xa - host(hh)).astype(np.float32)
+        codec.profile_reset()
+        codec.profile_enable(True)
+        vals, idx = codec.topk(xx, k, xhat=hh, gossip=(mm, 0.9))
+        torch.cuda.synchronize()
+        codec.profile_enable(False)
+        assert codec.profile_read("topk_bounds")[1] == (1 if expect_k1 else 0)
+        assert same_bits(host(xx), xa)
+        ov, oi = O.topk(d, k)
+        assert np.array_equal(host(idx).astype(np.int64), oi)
+        assert same_bits(host(vals), ov)
+
+    fused_call(x, mem, hat, expect_k1=True)                       # (1) cold: K1
+    s0 = _ws_word(_lib.TOPK_K2_SAMPLES_OFFSET)
+    f0 = _ws_word(_lib.TOPK_FALLBACKS_OFFSET)
+    mem.mul_(1000.0)
+    fused_call(x, mem, hat, expect_k1=False)                      # (2) warm window, misses
+    assert _ws_word(_lib.TOPK_FALLBACKS_OFFSET) == f0 + 1
+    assert _ws_word(_lib.TOPK_COLD_LEFT_OFFSET) >= 64             # the cold run (K34's backoff)
+    fused_call(x, mem, hat, expect_k1=True)                       # (3) cold run, fused: host K1
+    assert _ws_word(_lib.TOPK_K2_SAMPLES_OFFSET) == s0            # K2 never sampled
+    # (4) the same cold run without the fused step: K2 samples its own window
+    vals, idx = codec.topk(x, k, xhat=hat)
+    torch.cuda.synchronize()
+    assert _ws_word(_lib.TOPK_K2_SAMPLES_OFFSET) == s0 + 1
+    ov, oi = O.topk((host(x) - host(hat)).astype(np.float32), k)
+    assert np.array_equal(host(idx).astype(np.int64), oi)
+
+
 def test_topk_warm_start_drained_delta():
     """The CHOCO drain: x fixed, x_hat catching up with every call's top-k (the selected
     entries of the delta become 0), so every call's k-th key is the previous call's ~2k-th.

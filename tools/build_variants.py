@@ -13,6 +13,8 @@ VARIANTS = {
     "stamps": ["CHOCO_STAMPS=1"],
     # every bounded wait of the exact fallback gives up at once: tools/status_probe.py
     "poll1": ["CHOCO_POLL_BUDGET=1"],
+    # round 6 A/B: the fused sign pack's x store with the row offset as soffset (round 5)
+    "st_soff": ["CHOCO_AB_SIGN_ST_SOFF=1"],
 }
 
 
