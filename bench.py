@@ -102,6 +102,10 @@ def parse(argv=None):
     p.add_argument("--grad-scale", type=float, default=0.01,
                    help="step_* workloads: the synthetic gradient g ~ N(0, scale^2), a fresh seeded draw every step "
                         "(with the gradient on, x_hat and memory start as copies of x, as the reference's do)")
+    p.add_argument("--burn-in", type=int, default=None,
+                   help="step_* workloads with the gradient on: untimed steps run before the warm-up, so the timed "
+                        "steps are those of a running training job, not its first few (default 200; the delta "
+                        "starts at 0 and its k-th key moves by large factors over the first ~50 steps)")
     p.add_argument("--defer-receive", action="store_true",
                    help="step_* workloads: apply each step's received messages inside the NEXT step's first pass "
                         "(receive + consensus step + first compress pass in one kernel; same x / x_hat / memory)")
@@ -783,6 +787,9 @@ def main():
                 out[name] = (t / steps * 1e3, t / c * 1e3, c / steps)  # us per step, us per launch, launches/step
         return out
 
+    burn = args.burn_in if args.burn_in is not None else (200 if (w.step_mode and w.grads is not None) else 0)
+    for _ in range(burn):  # untimed: the steady state of a training run (step_* workloads)
+        w.step()
     # warm-up; its last steps time every kernel to find the dominant stage
     codec.profile_reset()
     for i in range(args.warmup):
@@ -950,6 +957,7 @@ def main():
             "exchange_us": round(exchange_us, 1),
             "topk_fallbacks": fallbacks,
             "warm_start": warm_start,
+            "burn_in_steps": burn,
             "apply_gradient": None if grad_us is None else {
                 "us": round(grad_us, 1), "lr": args.grad_lr, "scale": args.grad_scale,
                 "note": "g ~ N(0, scale^2) drawn fresh each step, then x -= lr * g (optim/utils.py:13-47, no "

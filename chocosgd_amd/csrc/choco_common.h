@@ -139,6 +139,20 @@ int gossip_launch(float* x, const float* mem, const float* xh, float gamma, int6
 
 CHOCO_DEV int lane_id() { return __lane_id(); }
 
+// Drift-aware warm windows (top-k, flat K34 and segmented S3b / S4w): the key drift to
+// extrapolate the next call's window by -- the last move T - t_prev when it has the sign
+// of the move before it (d_prev), clamped to the smaller of the two.  A steady drift of the
+// k-th key (the delta's scale growing or shrinking from step to step, as in a training
+// run) is followed; noise, whose moves alternate in sign, is not.  Keys are |v| bits, so a
+// key shift is a relative change of the value.
+CHOCO_DEV int32_t window_drift(uint32_t T, uint32_t t_prev, uint32_t d_prev_bits, bool valid) {
+  if (!valid || t_prev == 0u) return 0;
+  const int64_t dn = (int64_t)T - (int64_t)t_prev, dp = (int64_t)(int32_t)d_prev_bits;
+  if (dp == 0 || dn == 0 || (dn > 0) != (dp > 0)) return 0;
+  const int64_t m = dn > 0 ? (dn < dp ? dn : dp) : (dn > dp ? dn : dp);
+  return (int32_t)(m > (1ll << 30) ? (1ll << 30) : (m < -(1ll << 30) ? -(1ll << 30) : m));
+}
+
 // number of set bits of `mask` strictly below this lane
 CHOCO_DEV uint32_t mask_prefix(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),

@@ -116,7 +116,14 @@ struct TopkCtrl {
   uint32_t cold_left;                            // warm-host calls still to sample their window in K2 (backoff)
   uint32_t backoff;                              // cold run length after the next warm miss
   uint32_t k2_samples;                           // calls whose K2 took its window from its own sample (diagnostic)
-  uint32_t pad0[11];
+  // drift tracking (K34, workgroup 0): the previous call's exact k-th key, the key drift
+  // between the two calls before it, the window the previous call prepared for this one
+  // (the "shadow": on a cold run, would it have held this call's k-th key?) and for which
+  // (n, k), and the cold-run calls in a row whose k-th key the shadow held
+  uint32_t t_prev;
+  uint32_t d_prev;                               // int32 bits
+  uint32_t sh_lo, sh_hi, sh_nk, sh_hits;
+  uint32_t pad0[5];
   uint32_t overflow[2];                          // bit 0: a side list overflowed; bit 1: take the exact fallback
   uint32_t pad1[14];
   TopkBounds bounds[2];
@@ -828,6 +835,16 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   const uint32_t nchunk = tile / (uint32_t)kChunk;
   Src<MODE, XH> src{x, xh, seed};
   // tile-relative byte offset of a full chunk's first / second batch, or kNoChunk
+#if CHOCO_AB_K2_STRIDED
+  // (A/B timing only, round 6: workgroup b streams the 32768-element blocks b, b + nb, ...;
+  // the output is the right set in the wrong order)
+  auto gchunk = [&](uint32_t c) -> int64_t { return ((int64_t)b + (int64_t)nb * (c >> 4)) * 16 + (c & 15); };
+  const TileRsrc ts{buf_rsrc(x, (uint32_t)(n * 4)), buf_rsrc(XH ? xh : x, (uint32_t)(n * 4)),
+                    buf_rsrc(GS ? gs.mem : x, (uint32_t)(n * 4))};
+  auto batch0 = [&](uint32_t c) -> uint32_t {
+    return (c < nchunk && (gchunk(c) + 1) * kChunk <= n) ? (uint32_t)(gchunk(c) * kChunk * 4) : kNoChunk;
+  };
+#else
   const int64_t tlen = min((int64_t)tile, n - b * (int64_t)tile);
   const TileRsrc ts{buf_rsrc(x + b * (int64_t)tile, (uint32_t)(tlen * 4)),
                     buf_rsrc((XH ? xh : x) + b * (int64_t)tile, (uint32_t)(tlen * 4)),
@@ -835,6 +852,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   auto batch0 = [&](uint32_t c) -> uint32_t {
     return (c < nchunk && (int64_t)(c + 1) * kChunk <= tlen) ? c * (uint32_t)kChunk * 4u : kNoChunk;
   };
+#endif
 
   // ---- prologue: the window words K1 / the previous call left in the control block
   // are read FIRST, then the wave's first chunk w (and with one-batch chunks its second,
@@ -945,7 +963,11 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   // (hash mode, the partial chunk); ends with the chunk's bookkeeping.
   // `reload` refills R (the wave's next chunk) as soon as R is dead.
   auto run_chunk = [&](uint32_t cc, const float4 (&R)[kK2Unroll], auto&& reload) {
+#if CHOCO_AB_K2_STRIDED
+    const int64_t cbeg = gchunk(cc) * kChunk;
+#else
     const int64_t cbeg = tb + (int64_t)cc * kChunk;
+#endif
     const int64_t cend = min(cbeg + kChunk, n);
     float* __restrict__ ov = cval + cbeg;
     uint32_t* __restrict__ oi = cidx + cbeg;
@@ -1094,8 +1116,13 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       // counts stores too, so a load's wait would wait for every store before it).
       for (uint32_t j = h; j < lc; j += 32) {
         const uint2 pr = sm.u.pairs[ls + j];
+#if CHOCO_AB_K2_NTST  // (A/B only, round 6: the burst non-temporal)
+        __builtin_nontemporal_store(__uint_as_float(pr.x), &ov[j]);
+        __builtin_nontemporal_store(pr.y, &oi[j]);
+#else
         ov[j] = __uint_as_float(pr.x);
         oi[j] = pr.y;
+#endif
         to_side(pr.x, pr.y);
       }
       if (have && h == 0) cntw[(int64_t)b * nchunk + cc] = spilled ? cnt : (cc == 0 ? csum : 0u);
@@ -1106,7 +1133,11 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     }
     if (sort_lds) {
       __syncthreads();
+#if CHOCO_AB_K2_NTST
+      for (uint32_t i = (uint32_t)tid; i < hsum; i += kK2Threads) __builtin_nontemporal_store(skeys[i], &sd[i]);
+#else
       for (uint32_t i = (uint32_t)tid; i < hsum; i += kK2Threads) sd[i] = skeys[i];
+#endif
     }
   }
   WSTAMP(32000 + b * 8 + 4 + (w >> 2), w & 3);
@@ -1182,7 +1213,7 @@ struct FinSmem {
   uint32_t run_start[kMaxTileChunks + 1];
   uint32_t scratch[40];
   uint32_t bc[8];
-  uint32_t ctl[8];  // this call's window (s_lo, s_hi, shift), overflow word, margin m1024
+  uint32_t ctl[16];  // this call's window (s_lo, s_hi, shift), overflow word, margin m1024; drift words
 };
 static_assert(kK2Target <= kK4Threads, "K34 keeps one tile per thread");
 
@@ -1570,10 +1601,15 @@ CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uin
 // 100M) against ~10 us saved per warm call, so a retry pays only if warm then holds for
 // ~60+ calls: the first run is 64 calls, doubling per consecutive miss.
 constexpr uint32_t kColdMin = 64, kColdMax = 4096;
+constexpr uint32_t kShadowExit = 2;  // cold-run calls in a row whose k-th key the carried window would have held
+CHOCO_DEV uint32_t nk_tag(int64_t n, int64_t k) {
+  return ((uint32_t)n * 2654435761u) ^ ((uint32_t)k * 40503u) ^ (uint32_t)((uint64_t)k >> 32) ^ 1u;
+}
+// (window_drift: choco_common.h)
 constexpr uint32_t kWarmM0 = 20;     // ~2 % of k (the bench's randn deltas drift ~0.1 %)
 constexpr uint32_t kWarmMMax = 512;  // 50 %
 CHOCO_DEV void next_window(const uint32_t* G, uint32_t s_lo, uint32_t s_hi, uint32_t shift, uint32_t m_prev,
-                           uint32_t T, int64_t n, int64_t k, TopkBounds* __restrict__ out) {
+                           uint32_t T, int64_t n, int64_t k, int32_t drift, TopkBounds* __restrict__ out) {
   const int lane = lane_id();
   const double kd = (double)k;
   uint32_t m = kWarmM0;
@@ -1618,6 +1654,12 @@ CHOCO_DEV void next_window(const uint32_t* G, uint32_t s_lo, uint32_t s_hi, uint
     const double dh = C >= fmax(kd / 1024.0, 16.0) ? 2.0 * D * need / C + (double)(1u << shift)
                                                    : 2.0 * (double)w0 + D;
     x_hi = (uint64_t)fmin((double)s_hi + dh, 2147483648.0);
+  }
+  // drift-aware: both edges follow the k-th key's steady drift (window_drift)
+  if (drift != 0) {
+    const int64_t lo2 = (int64_t)x_lo + drift, hi2 = (int64_t)x_hi + drift;
+    x_lo = (uint64_t)std::max<int64_t>(0, lo2);
+    x_hi = (uint64_t)std::min<int64_t>(2147483648ll, std::max<int64_t>(hi2, (int64_t)x_lo + 1));
   }
   const uint64_t width = x_hi > x_lo + kNMaybe ? x_hi - x_lo : (uint64_t)kNMaybe;
   uint32_t sh = 0;
@@ -1664,8 +1706,9 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   {
     const TopkBounds& Bw = ctrl->bounds[par];
     const uint32_t* src = tid == 0 ? &Bw.s_lo : tid == 1 ? &Bw.s_hi : tid == 2 ? &Bw.shift
-                        : tid == 3 ? &ctrl->overflow[par] : &Bw.m1024;
-    if (tid < 5) cword = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        : tid == 3 ? &ctrl->overflow[par] : tid == 4 ? &Bw.m1024
+                        : tid < 11 ? &ctrl->t_prev + (tid - 5) : &Bw.m1024;  // t_prev, d_prev, sh_lo, sh_hi, sh_nk, sh_hits
+    if (tid < 11) cword = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const bool mine_tile = tid < (int)nb;
   const uint32_t* row = cum_tab + (int64_t)(mine_tile ? tid : 0) * kNBucket;  // clamped: loads unconditional
@@ -1675,7 +1718,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
 #pragma unroll
     for (int r = 0; r < kNRep; ++r) g[r] = ctrl->G[par][r][tid];
   }
-  if (tid < 5) fs.ctl[tid] = cword;  // s_lo, s_hi, shift, overflow, m1024
+  if (tid < 11) fs.ctl[tid] = cword;  // s_lo, s_hi, shift, overflow, m1024, t_prev, d_prev, sh_lo, sh_hi, sh_nk, sh_hits
   const uint32_t tot = compact ? ti : chunk_run_starts(cw, nchunk, fs.run_start, fs.scratch);
   if (compact) __syncthreads();  // fs.ctl (chunk_run_starts ends with this barrier)
   const uint32_t s_lo = fs.ctl[0], shift = fs.ctl[2], overflow = fs.ctl[3];
@@ -1704,6 +1747,8 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   const uint32_t jstar = fs.bc[4];
   STAMP(26000 + b, 2);
   if (!fallback && fs.G[jstar] - fs.G[jstar + 1] > (uint32_t)kMCap) fallback = true;
+  uint32_t T_exact = 0;  // (workgroup 0's tail: this call's exact k-th key on the select path)
+  const uint32_t nk = nk_tag(n, k);
   if (fallback) {
     if (b == 0 && tid == 0) atomicAdd(&ctrl->fallbacks, 1u);
     // the sample's guess was off: the exact radix select over the whole input, shared
@@ -1803,6 +1848,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     STAMP(27000 + b, 0);
     const uint32_t T = base_j + prefix;
     const uint32_t r = krem;  // ties at T to take (>= 1)
+    T_exact = T;
     // ---- per tile: #keys > T (every key above bucket j* is) and #keys == T
     uint32_t gt = above, eq = 0;
     for (uint32_t i0 = 0; i0 < cb; i0 += 8) {  // 8 independent LDS reads per round trip
@@ -1883,7 +1929,8 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     }
     STAMP(30000 + b, 2);
     if (MODE == kData && b == 0 && tid < 64)
-      next_window(fs.G, s_lo, fs.ctl[1], shift, fs.ctl[4], T, n, k, &ctrl->bounds[par ^ 1u]);
+      next_window(fs.G, s_lo, fs.ctl[1], shift, fs.ctl[4], T, n, k,
+                  window_drift(T, fs.ctl[5], fs.ctl[6], fs.ctl[9] == nk), &ctrl->bounds[par ^ 1u]);
   }
   // random-k windows come from the host each call: nothing for the next call to reuse
   if (MODE == kHash && b == 0 && tid == 0) ctrl->bounds[par ^ 1u].valid = 0u;
@@ -1895,17 +1942,40 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   // exact fallback every call.
   if (MODE == kData && b == 0 && tid == 0) {
     const bool warm_call = fs.ctl[4] != 0u;
-    uint32_t bo = ctrl->backoff, cl = ctrl->cold_left;
+    uint32_t bo = ctrl->backoff, cl = ctrl->cold_left, hits = fs.ctl[10];
+    // the shadow: would the window the previous call prepared have held this k-th key?
+    const bool shadow_hit = !fallback && fs.ctl[9] == nk && fs.ctl[7] <= T_exact && T_exact < fs.ctl[8];
     if (warm_call && fallback) {
       bo = min(max(2u * bo, kColdMin), kColdMax);
       cl = bo;
+      hits = 0u;
     } else if (warm_call) {
       bo = max(bo / 2u, kColdMin);
+      hits = 0u;
     } else if (cl != 0u) {
       --cl;
+      // a cold run ends early once the carried (drift-aware) windows would have held the
+      // k-th key kShadowExit calls in a row: the drift that caused the miss is followed now
+      hits = shadow_hit ? hits + 1u : 0u;
+      if (hits >= kShadowExit) {
+        cl = 0u;
+        hits = 0u;
+      }
     }
     ctrl->backoff = bo;
     ctrl->cold_left = cl;
+    ctrl->sh_hits = hits;
+    if (!fallback) {  // the drift words and the shadow for the next call
+      ctrl->d_prev = (fs.ctl[9] == nk && fs.ctl[5] != 0u) ? T_exact - fs.ctl[5] : 0u;
+      ctrl->t_prev = T_exact;
+      ctrl->sh_lo = ctrl->bounds[par ^ 1u].s_lo;  // (written by this thread in next_window)
+      ctrl->sh_hi = ctrl->bounds[par ^ 1u].s_hi;
+      ctrl->sh_nk = nk;
+    } else {
+      ctrl->t_prev = 0u;
+      ctrl->d_prev = 0u;
+      ctrl->sh_nk = 0u;
+    }
     // (the host launches K1 for fused-gossip calls on a cold run: launch_topk)
     if (cold_host) __hip_atomic_store(cold_host, cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }

@@ -95,10 +95,16 @@ CHOCO_DEV SegRow seg_row(const int64_t* __restrict__ plan, int s) {
   return SegRow{p[0], p[1], p[2], p[3], p[4], p[5]};
 }
 
-// A segment's warm window: candidates key >= lo, bins of 2^sh keys.
+// A segment's warm window: candidates key >= lo, bins of 2^sh keys; and the drift words
+// (the exact k-th key of the call that wrote it, and its move from the call before:
+// window_drift extrapolates the next window by them).
 struct SegWin {
   uint32_t lo, sh, valid, pad;
+  uint32_t tprev, dprev, pad2[2];
 };
+CHOCO_DEV SegWin seg_win(uint32_t lo, uint32_t sh, uint32_t T, const SegWin& old) {
+  return SegWin{lo, sh, 1u, 0u, T, (old.valid && old.tprev) ? T - old.tprev : 0u, {0u, 0u}};
+}
 
 // info[8 s + i]: 0 b1 (cold), 1 rank inside b1 (cold), 2 T, 3 bin of the k-th key
 // (S3a), 4 rank inside that bin, 5 ties at T to take, 6 mode (0 select, 1 window
@@ -110,6 +116,7 @@ struct SegWs {
   SegWin* win;
   uint32_t* misses;     // the workspace's CHOCO_TOPK_FALLBACKS_OFFSET counter
   uint32_t* miss_flag;  // pinned host word of the cold backoff (nullable)
+  unsigned long long* shadow;  // pinned host counter of cold calls' window checks (nullable; seg_count_kernel)
   uint2* blist;         // warm: per tile, its keys in the k-th key's window bin ({key, count} x kTileList)
 };
 
@@ -640,17 +647,21 @@ __global__ __launch_bounds__(kS3Threads) void seg_fine_kernel(
 // keys is centred on T instead.
 constexpr int kWinPer = kH / kS3Threads;  // hist bins per thread of seg_next_window
 CHOCO_DEV void seg_next_window_v(const uint32_t (&hv)[kWinPer], uint32_t base, uint32_t shb, uint32_t above,
-                                 uint32_t k, uint32_t T, SegWin* __restrict__ out, uint32_t* scratch);
+                                 uint32_t k, uint32_t T, const SegWin& old, SegWin* __restrict__ out,
+                                 uint32_t* scratch);
 CHOCO_DEV void seg_next_window(const uint32_t* __restrict__ hist, uint32_t base, uint32_t shb, uint32_t above,
-                               uint32_t k, uint32_t T, SegWin* __restrict__ out, uint32_t* scratch) {
+                               uint32_t k, uint32_t T, const SegWin& old, SegWin* __restrict__ out,
+                               uint32_t* scratch) {
   uint32_t hv[kWinPer];
 #pragma unroll
   for (int j = 0; j < kWinPer; ++j) hv[j] = hist[threadIdx.x * kWinPer + j];
-  seg_next_window_v(hv, base, shb, above, k, T, out, scratch);
+  seg_next_window_v(hv, base, shb, above, k, T, old, out, scratch);
 }
-// the same over bins already in registers (hv[j] = bin tid * kWinPer + j)
+// the same over bins already in registers (hv[j] = bin tid * kWinPer + j).  `old` is the
+// window the call used or the previous call prepared (its drift words; window_drift).
 CHOCO_DEV void seg_next_window_v(const uint32_t (&hv)[kWinPer], uint32_t base, uint32_t shb, uint32_t above,
-                                 uint32_t k, uint32_t T, SegWin* __restrict__ out, uint32_t* scratch) {
+                                 uint32_t k, uint32_t T, const SegWin& old, SegWin* __restrict__ out,
+                                 uint32_t* scratch) {
   constexpr int PER = kWinPer;
   const int tid = threadIdx.x;
   const uint64_t delta = (uint64_t)(0.03 * (double)k + 4.0 * sqrt((double)k)) + 8u;
@@ -674,23 +685,31 @@ CHOCO_DEV void seg_next_window_v(const uint32_t (&hv)[kWinPer], uint32_t base, u
   if (tid == 0) {
     uint64_t x_lo = (uint64_t)base + ((uint64_t)(nlo ? nlo - 1u : 0u) << shb);
     uint64_t x_hi = (uint64_t)base + ((uint64_t)nhi << shb);
+    const int32_t drift = window_drift(T, old.tprev, old.dprev, old.valid != 0u);
+    if (drift != 0) {  // both edges follow the k-th key's steady drift
+      const int64_t lo2 = (int64_t)x_lo + drift, hi2 = (int64_t)x_hi + drift;
+      x_lo = (uint64_t)(lo2 > 0 ? lo2 : 0);
+      x_hi = (uint64_t)(hi2 > (int64_t)x_lo + 1 ? (hi2 < (1ll << 31) ? hi2 : (1ll << 31)) : (int64_t)x_lo + 1);
+    }
     uint32_t sh = 0;
     while (((uint64_t)kH << sh) < x_hi - x_lo && sh < kWinShMax) ++sh;
     if (((uint64_t)kH << sh) < x_hi - x_lo) {  // too wide for the finest bins: centre on T
       sh = kWinShMax;
       x_lo = T > (1u << 18) ? (uint64_t)T - (1u << 18) : 0u;
     }
-    out->lo = (uint32_t)x_lo;
-    out->sh = sh;
-    out->valid = 1u;
+    *out = seg_win((uint32_t)x_lo, sh, T, old);
   }
 }
 
 // (cold calls)
+// shadow: on a cold call, tile 0 of each segment also checks whether the window the
+// previous call prepared (still in win[s]) would have held this call's T_s, and adds
+// (miss << 32) | 1 to a 64-bit counter in pinned host memory (one system-scope atomic per
+// segment): the host ends a cold run once two calls' worth of checks came without a miss.
 __global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
     const int64_t* __restrict__ trows, int nseg, uint32_t* __restrict__ hist2, const uint32_t* __restrict__ hist3,
     uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt, const float* __restrict__ cval,
-    uint32_t* __restrict__ tcount, SegWin* __restrict__ win) {
+    uint32_t* __restrict__ tcount, SegWin* __restrict__ win, unsigned long long* __restrict__ shadow) {
   __shared__ uint32_t scratch[40];
   __shared__ uint32_t bc[4];
   const TileCtx c = tile_ctx_rows(trows, blockIdx.x);
@@ -708,7 +727,14 @@ __global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
     // the next call's window, from this call's hist2 (bits 19..9 inside b1, with the keys
     // of the bins above b1); hist2 was read by every tile in S3a
     uint32_t* __restrict__ g2 = hist2 + (int64_t)c.s * kH;
-    seg_next_window(g2, b1 << 20, 9u, (uint32_t)c.R.k - info[8 * c.s + 1], (uint32_t)c.R.k, T, &win[c.s], scratch);
+    const SegWin old = win[c.s];  // the window the previous call prepared (read before it is replaced)
+    __syncthreads();
+    if (tid == 0 && shadow) {
+      const bool hit = old.valid && old.lo <= T && (uint64_t)T < (uint64_t)old.lo + ((uint64_t)(kH - 1) << min(old.sh, kWinShMax));
+      __hip_atomic_fetch_add(shadow, (hit ? 0ull : (1ull << 32)) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    seg_next_window(g2, b1 << 20, 9u, (uint32_t)c.R.k - info[8 * c.s + 1], (uint32_t)c.R.k, T, old, &win[c.s],
+                    scratch);
     __syncthreads();
     for (int i = tid; i < kH; i += kS3Threads) g2[i] = 0u;
   }
@@ -1018,6 +1044,8 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_w_kernel(
   uint32_t ix0 = 0u;
   uint32_t hv[kWinPer] = {};  // (segment workgroups: hist2 for the next window, in the same trip)
   uint32_t* __restrict__ g2 = hist2 + (int64_t)c.s * kH;
+  SegWin old{};  // (segment workgroups and tile 0: the window this call used, for its drift words)
+  if (segwg || c.j == 0) old = win[c.s];
   if (!segwg) {
     v0 = cval[c.slot + tid];  // (inside the tile's slots; masked by cnt below)
     ix0 = cidx[c.slot + tid];
@@ -1050,10 +1078,10 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_w_kernel(
     __syncthreads();
     block_emit(src, c.R.len, T, r, ties, 1.0f, out_val + c.R.out_off, out_idx + c.R.out_off, c.R.off, es);
     if (overflow) {  // the window held T: the next one from this call's hist2, as usual
-      seg_next_window(g2, lo, sh, 0u, (uint32_t)c.R.k, T, &win[c.s], scratch);
+      seg_next_window(g2, lo, sh, 0u, (uint32_t)c.R.k, T, old, &win[c.s], scratch);
       __syncthreads();
     } else if (tid == 0) {  // re-centred on T
-      win[c.s] = SegWin{T > (1u << 18) ? T - (1u << 18) : 0u, kWinShMax, 1u, 0u};
+      win[c.s] = seg_win(T > (1u << 18) ? T - (1u << 18) : 0u, kWinShMax, T, old);
     }
     for (int i = tid; i < kH; i += kS4Threads) g2[i] = 0u;
     return;
@@ -1074,10 +1102,10 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_w_kernel(
   }
   if (segwg) {  // the next call's window (this call's hist2: the window's own bins), then hist2 reset
     if (mode == kSegSelect) {
-      seg_next_window_v(hv, lo, sh, 0u, (uint32_t)c.R.k, T, &win[c.s], scratch);
+      seg_next_window_v(hv, lo, sh, 0u, (uint32_t)c.R.k, T, old, &win[c.s], scratch);
       __syncthreads();
     } else if (tid == 0) {
-      win[c.s] = SegWin{0u, kWinShMax, 1u, 0u};
+      win[c.s] = SegWin{0u, kWinShMax, 1u, 0u, 0u, 0u, {0u, 0u}};
     }
     for (int i = tid; i < kH; i += kS4Threads) g2[i] = 0u;
     return;
@@ -1152,35 +1180,65 @@ static int64_t plan_batched(const int64_t* plan_host) { return plan_host[7]; }
 // miss, up to 4096.  A stationary delta never raises the flag and never pays anything; a
 // delta whose k-th keys keep moving out of their windows (x_hat draining the top keys)
 // pays the second read instead of S4's one-workgroup exact select of every missed segment.
+// A cold run ends early when the windows the cold calls prepare would have held their
+// successors' k-th keys: S3b of every cold call checks, per multi-tile segment, the window
+// the previous call left (drift-aware, window_drift) against its exact T and counts
+// (misses << 32 | checks) in the same pinned page; two cold calls' worth of checks with no
+// miss end the run (the drift that caused the miss is followed now).
 struct SegState {
   uint64_t calls = 0;
   uint32_t cold_left = 0, backoff = 0;
-  uint32_t* flag = nullptr;  // pinned, mapped; the device writes 1 on a miss
+  uint32_t* flag = nullptr;  // pinned, mapped; word 0: the device writes 1 on a miss; words 2-3: shadow counter
   uint32_t* flag_dev = nullptr;
+  uint32_t last_checks = 0, last_misses = 0, clean = 0;
 };
+constexpr uint32_t kSegShadowExit = 2;
+static uint64_t seg_shadow_read(const SegState& S) {
+  return S.flag ? __atomic_load_n(reinterpret_cast<uint64_t*>(S.flag + 2), __ATOMIC_ACQUIRE) : 0ull;
+}
 static std::mutex g_seg_mu;
 static std::unordered_map<const void*, SegState> g_seg;
-static bool seg_claim_warm(const void* ws, uint32_t** flag_dev) {
+static bool seg_claim_warm(const void* ws, uint32_t nmulti, uint32_t** flag_dev, unsigned long long** shadow_dev) {
   std::lock_guard<std::mutex> g(g_seg_mu);
   SegState& S = g_seg[ws];
   if (!S.flag) {
     void* h = nullptr;
     if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
       S.flag = static_cast<uint32_t*>(h);
-      *S.flag = 0u;
+      for (int i = 0; i < 16; ++i) __atomic_store_n(S.flag + i, 0u, __ATOMIC_RELEASE);
       void* d = nullptr;
       if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess) S.flag_dev = static_cast<uint32_t*>(d);
     }
   }
   *flag_dev = S.flag_dev;  // (null: no backoff, warm as before)
+  *shadow_dev = S.flag_dev ? reinterpret_cast<unsigned long long*>(S.flag_dev + 2) : nullptr;
   const bool first = S.calls++ == 0;
   if (S.flag && __atomic_load_n(S.flag, __ATOMIC_ACQUIRE) != 0u) {
     __atomic_store_n(S.flag, 0u, __ATOMIC_RELEASE);
     S.backoff = std::min<uint32_t>(std::max<uint32_t>(2u * S.backoff, 64u), 4096u);
     S.cold_left = S.backoff;
+    const uint64_t v = seg_shadow_read(S);  // checks from before this run do not count
+    S.last_checks = (uint32_t)v;
+    S.last_misses = (uint32_t)(v >> 32);
+    S.clean = 0u;
   }
   if (first) return false;
   if (S.cold_left != 0u) {
+    if (S.flag && nmulti > 0u) {
+      const uint64_t v = seg_shadow_read(S);
+      const uint32_t dc = (uint32_t)v - S.last_checks, dm = (uint32_t)(v >> 32) - S.last_misses;
+      if (dc >= nmulti) {  // at least one more cold call's checks have landed
+        S.clean = dm == 0u ? S.clean + dc / nmulti : 0u;
+        S.last_checks = (uint32_t)v;
+        S.last_misses = (uint32_t)(v >> 32);
+      }
+      if (S.clean >= kSegShadowExit) {
+        S.cold_left = 0u;
+        S.clean = 0u;
+        S.backoff = std::max<uint32_t>(S.backoff / 2u, 64u);
+        return topk_warm_enabled();
+      }
+    }
     --S.cold_left;
     return false;
   }
@@ -1250,7 +1308,7 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
   CHOCO_LAUNCHED("seg_fine_kernel");
   profile_begin("topk_seg_count", st);
   CHOCO_KLAUNCH(seg_count_kernel, dim3(ntile), dim3(kS3Threads), 0, st, trows, nseg, W.hist2, W.hist3, W.info,
-                W.tilecnt, W.cval, W.tcount, W.win);
+                W.tilecnt, W.cval, W.tcount, W.win, W.shadow);
   profile_end("topk_seg_count", st);
   CHOCO_LAUNCHED("seg_count_kernel");
   profile_begin("topk_seg_emit", st);
@@ -1294,9 +1352,11 @@ static int segmented(const float* x, const float* xhat, const int64_t* plan_dev,
             reinterpret_cast<uint32_t*>(base + L.off_info), reinterpret_cast<uint32_t*>(base + L.off_cnt),
             reinterpret_cast<uint32_t*>(base + L.off_out), reinterpret_cast<float*>(base + L.off_cval),
             reinterpret_cast<uint32_t*>(base + L.off_cidx), reinterpret_cast<SegWin*>(base + L.off_win),
-            reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_FALLBACKS_OFFSET), nullptr,
+            reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_FALLBACKS_OFFSET), nullptr, nullptr,
             reinterpret_cast<uint2*>(base + L.off_blist)};
-    const bool warm = seg_claim_warm(base + L.off_win, &W.miss_flag);
+    uint32_t nmulti = 0;  // segments with windows (multi-tile, batched): the shadow checks per cold call
+    for (int s = 0; s < nseg; ++s) nmulti += plan_host[(int64_t)kRow * s + 5] > 1 ? 1u : 0u;
+    const bool warm = seg_claim_warm(base + L.off_win, nmulti, &W.miss_flag, &W.shadow);
     int rc;
     if (gs.mem)
       rc = launch_batched<true, true>(x, xhat, plan_dev, plan_host, nseg, out_val, out_idx, W, warm, st, gs);
