@@ -711,3 +711,64 @@ def test_topk_segmented_warm_random_layouts(seed):
     for x in seq:
         _check_seg(x, plan, lens, ratio)
         _check_seg(x, plan, lens, ratio, xh=randn(n, seed + 3, 0.01))
+
+
+def _ties_data(n, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return torch.round(torch.randn(n, generator=g, device=DEV) * 4096) / 4096  # ~100 ties per value near T
+
+
+@pytest.mark.parametrize("n", [16_777_216, 16_789_561, 33_554_431, 100_000_000])
+@pytest.mark.parametrize("ratio", [0.99, 0.985])
+@pytest.mark.parametrize("kind", ["randn", "ties", "xhat"])
+def test_topk_block_layout_exact(n, ratio, kind):
+    """The strided block layout (csrc/topk.hip BLK: stream workgroup b takes the 32768-element
+    blocks b, b + 256, ...; K34B places every block) on its whole range -- the first size it
+    serves (2^24: 512 blocks), a partial last chunk and block, 2^25 - 1, the north-star 100M --
+    at k = 1 % and 1.5 % (<= n / 64), on Gaussian data, on tie-heavy data (the k-th value
+    shared by ~100 elements: ties split inside one block), and on a delta x - x_hat; then the
+    same call with the tile layout.  Both bit-exact against the oracle, warm calls included."""
+    from chocosgd_amd import codec
+    lib = codec.lib()
+    k = codec.topk_k(n, ratio)
+    x = _ties_data(n, 61) if kind == "ties" else randn(n, 62)
+    xh = randn(n, 63, 0.5) if kind == "xhat" else None
+    d = host(x) if xh is None else (host(x) - host(xh)).astype(np.float32)
+    ov, oi = O.topk(d, k)
+    try:
+        for blocks in (1, 1, 0):  # cold, then warm, then the tile layout
+            lib.choco_topk_set_block_layout(blocks)
+            vals, idx = codec.topk(x, k, xhat=xh)
+            assert np.array_equal(host(idx).astype(np.int64), oi), blocks
+            assert same_bits(host(vals), ov), blocks
+    finally:
+        lib.choco_topk_set_block_layout(1)
+
+
+def test_topk_block_layout_gossip_and_drain():
+    """The block layout with the fused consensus step over a warm sequence (x, memory, x_hat
+    evolve; every call exact, x_new bit-identical), then the CHOCO drain on a fixed delta
+    (every call's k-th key moves: windows miss, the exact fallback and the cold run run on
+    the block layout too)."""
+    from chocosgd_amd import codec
+    n = 20_000_003
+    k = codec.topk_k(n, 0.99)
+    torch.cuda.synchronize()
+    codec.release_workspaces()
+    g = torch.Generator(device=DEV).manual_seed(64)
+    x = torch.randn(n, generator=g, device=DEV)
+    hat = x + 0.1 * torch.randn(n, generator=g, device=DEV)
+    mem = hat + 0.05 * torch.randn(n, generator=g, device=DEV)
+    for step in range(4):
+        xa = O.gossip_step(host(x), host(mem), host(hat), 0.9)
+        d = (xa - host(hat)).astype(np.float32)
+        vals, idx = codec.topk(x, k, xhat=hat, gossip=(mem, 0.9))
+        assert same_bits(host(x), xa)
+        ov, oi = O.topk(d, k)
+        assert np.array_equal(host(idx).astype(np.int64), oi)
+        assert same_bits(host(vals), ov)
+        codec.sparse_accumulate(vals, idx, mem, 1.0, xhat_self=hat)
+    dd = randn(n, 65)
+    for step in range(5):
+        vals, idx = _check_topk(dd, k)
+        dd[idx.long()] = 0.0

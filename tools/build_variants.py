@@ -19,6 +19,10 @@ VARIANTS = {
     "k2strided": ["CHOCO_AB_K2_STRIDED=1"],
     # round 6 A/B: K2's tile-end burst (pairs, side list) with non-temporal stores
     "k2ntst": ["CHOCO_AB_K2_NTST=1"],
+    # round 6 A/B (timing only, wrong output): K34B without the per-block loads / the block search
+    "k34b_nogt": ["CHOCO_AB_K34B_NOGT=1"],
+    "k34b_nosearch": ["CHOCO_AB_K34B_NOSEARCH=1"],
+    "k34b_both": ["CHOCO_AB_K34B_NOGT=1", "CHOCO_AB_K34B_NOSEARCH=1"],
     "k2strided_ntst": ["CHOCO_AB_K2_STRIDED=1", "CHOCO_AB_K2_NTST=1"],
 }
 
