@@ -113,8 +113,6 @@ def parse(argv=None):
     p.add_argument("--no-e2e", action="store_true", help="skip the host-resident (PCIe-inclusive) leg")
     p.add_argument("--lib", default=None, help=argparse.SUPPRESS)
     p.add_argument("--no-kernel-events", action="store_true", help=argparse.SUPPRESS)  # diagnostic
-    p.add_argument("--no-block-layout", action="store_true",
-                   help="top-k: stream contiguous tiles instead of strided blocks (choco_topk_set_block_layout(0))")
     p.add_argument("--dist-timeout", type=float, default=300.0,
                    help="seconds for init_process_group and every collective before a rank gives up")
     p.add_argument("--die-before-exchange", type=int, default=None, help=argparse.SUPPRESS)  # launcher test
@@ -770,8 +768,6 @@ def main():
     if args.lib:
         _lib.load(args.lib)
     codec.lib()
-    if args.no_block_layout:
-        codec.lib().choco_topk_set_block_layout(0)
     w = Worker(args, rank, world, dev)
     comp_k, dec_k = STAGES[w.op]
     if w.step_mode:

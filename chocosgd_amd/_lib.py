@@ -34,7 +34,6 @@ SIGNATURES = {
     "choco_topk_workspace_size": (_c_sz, [_c_i64]),
     "choco_topk_workspace_reset": (_c_i32, [_vp, _c_sz]),
     "choco_topk_set_warm_start": (_c_i32, [_c_i32]),
-    "choco_topk_set_block_layout": (_c_i32, [_c_i32]),
     "choco_topk_host_status": (_c_i32, [_vp, _c_i32, _vp]),
     "choco_topk_compress": (_c_i32, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "choco_topk_compress_accumulate": (_c_i32, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_f32, _vp, _c_sz,

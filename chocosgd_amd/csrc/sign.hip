@@ -469,16 +469,7 @@ __global__ __launch_bounds__(kSignThreads * RS) void sign_pack1_kernel(const flo
         // soffset is an SGPR gets no wait state from the compiler before a VALU overwrites
         // its data registers, and on gfx950 such a store can write the NEW values (the r5m
         // wrong x / memory stores; DESIGN.md section 4, tests/test_isa_hazards.py).
-#if CHOCO_AB_SIGN_ST_SOFF  // (A/B only, round 6: round 5's scalar-offset store)
-        {
-          choco_f32x4 f;
-          f.x = G.x[u].x; f.y = G.x[u].y; f.z = G.x[u].z; f.w = G.x[u].w;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, f),
-                                                 rx, voff, row_off(rs0 + g * RU + u), 2);
-        }
-#else
         st_buf4<true>(rx, voff + row_off(rs0 + g * RU + u), G.x[u]);
-#endif
       }
     }
 #pragma unroll

@@ -57,12 +57,6 @@ static_assert(kK2Target <= 1024, "K34 keeps one tile per thread");
 // Elements a wave claims at a time (LDS counter): one load batch.
 constexpr int64_t kChunk = 256 * kK2Unroll;
 static_assert(kTileQuant % kChunk == 0, "chunk geometry");
-// the strided block layout (BLK, StreamSmemT): blocks of 16 chunks
-constexpr int kBlkChunks = 16;
-constexpr int64_t kBlkElems = (int64_t)kChunk * kBlkChunks;  // 32768
-constexpr int kMaxBlk = 16;          // blocks per K2 workgroup (n <= kMaxNB * 32768 = 134M)
-constexpr int kMaxNB = 4096;         // blocks per buffer
-constexpr int kBlkSideCap = 65536;   // 8-byte side entries {key, block} per K2 workgroup
 constexpr int kMaybeCap = 65536;        // side-list capacity per tile (maybe keys)
 constexpr int kNBucket = 256;           // 255 "maybe" buckets + 1 "sure"
 constexpr int kNMaybe = kNBucket - 1;
@@ -163,19 +157,8 @@ CHOCO_DEV void fold_apply(const Fold& f, int64_t i, float q) {
 struct TopkLayout {
   int64_t n;
   uint32_t tile, nb, side_cap;
-  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, off_wide, off_gcnt, off_tinfo;
-  size_t off_bcum, off_side2;  // the block layout's per-block suffix counts and {key, block} side lists
-  size_t total;
+  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, off_wide, off_gcnt, off_tinfo, total;
 };
-// The block layout (BLK) serves the data path for 2^24 <= n <= kMaxNB * 32768 (~134M) and
-// k <= n / 64 (a K2 workgroup's candidates must fit its LDS pair regions); the grid is then
-// kK2Target workgroups.  choco_topk_set_block_layout(0) turns it off (A/B, tests).
-constexpr int64_t kBlkMinN = 512 * kBlkElems;
-static std::atomic<bool> g_topk_blocks{true};
-static bool topk_blocks_fit(int64_t n) { return n >= kBlkMinN && n <= (int64_t)kMaxNB * kBlkElems; }
-static bool topk_blocks_apply(int64_t n, int64_t k) {
-  return g_topk_blocks.load(std::memory_order_relaxed) && topk_blocks_fit(n) && k <= n / 64;
-}
 
 // Tile = ceil(n / kK2Target) rounded up to 32768 elements: one tile per CU, all
 // resident at once (few tiles also keep K3's table reads short).  A tile's side
@@ -196,20 +179,13 @@ static TopkLayout topk_layout(int64_t n) {
   size_t o = 0;
   L.off_ctrl = o;  o += align_up(sizeof(TopkCtrl), 256);
   L.off_wide = o;  o += kWideBytes;
-  const size_t rows = std::max<size_t>(L.nb, (size_t)kK2Target);  // (the block layout's grid is kK2Target)
-  L.off_cum = o;   o += align_up(rows * kNBucket * 4, 256);
+  L.off_cum = o;   o += align_up((size_t)L.nb * kNBucket * 4, 256);
   L.off_cntw = o;  o += align_up((size_t)L.nb * (tile / kChunk) * 4, 256);   // per-chunk candidate counts
   L.off_side = o;  o += align_up((size_t)L.nb * L.side_cap * 4, 256);
   L.off_cval = o;  o += align_up((size_t)L.nb * tile * 4, 256);   // candidate values, chunk slot ranges
   L.off_cidx = o;  o += align_up((size_t)L.nb * tile * 4, 256);   // ... and indices
-  L.off_gcnt = o;  o += align_up(rows * 8, 256);                     // ... its per-tile (#>T, #==T)
+  L.off_gcnt = o;  o += align_up((size_t)L.nb * 8, 256);              // ... its per-tile (#>T, #==T)
   L.off_tinfo = o; o += align_up((size_t)L.nb * 4, 256);              // per tile: candidates (compact) or ~0 (spilled)
-  L.off_bcum = L.off_side2 = o;
-  if (topk_blocks_fit(n)) {
-    const size_t nblk = (size_t)((n + kBlkElems - 1) / kBlkElems);
-    L.off_bcum = o;  o += align_up(nblk * kNBucket * 2, 256);
-    L.off_side2 = o; o += align_up((size_t)kK2Target * kBlkSideCap * 8, 256);
-  }
   L.total = o;
   return L;
 }
@@ -396,16 +372,7 @@ struct SampleHist {
   uint32_t list[kK2Waves][kListPerWave];
 };
 
-// The strided block layout (BLK, round 6): the buffer is cut into blocks of 16 chunks
-// (32768 elements) and K2 workgroup b streams the blocks b, b + G, b + 2G, ... (G = the
-// grid): at any time the whole chip reads one ~32 MB window of the buffer instead of 256
-// separate tile streams, which evened out the XCDs' stream ends (tools/probe_floor.hip,
-// profiles/r04_probe_floor.txt: per-XCD medians within 4 us against 11).  Each block's
-// candidates are stored compactly at the block's own slots and its bucket counts go to a
-// per-block table, so K34B places every block by a scan over all blocks.
-
-template <bool BLK>
-struct StreamSmemT {
+struct StreamSmem {
   float4 ent_v[kK2Waves][kEnt];   // staged lanes: the float4 row slice
   uint32_t ent_i[kK2Waves][kEnt]; // ... and the index of its first element
   float4 trash_v[64];             // per-lane sink of the branch-free batch writes (shared, never read)
@@ -414,24 +381,15 @@ struct StreamSmemT {
     uint2 pairs[kK2Waves * kPairsPerWave];  // (value bits, index) per candidate, per-wave regions
     SampleHist sh;                          // the prologue's sample window (cold calls only)
   } u;
-  static constexpr int kCh = BLK ? kMaxBlk * kBlkChunks : kMaxTileChunks;
-  uint32_t cmeta[kCh];            // per chunk: LDS start | LDS count << 16
-  uint32_t ccnt[kCh + 1];         // per chunk: candidates; at tile end their exclusive prefix (BLK: in the block)
-  uint32_t hist[kNBucket];        // maybe-key bucket counts (tile layout), then counting-sort cursors
-  uint32_t bh[BLK ? kMaxBlk : 1][kNBucket / 2];  // BLK: per block, bucket counts as 16-bit pairs, then suffix counts
-  uint32_t btot[BLK ? kMaxBlk : 1];              // BLK: candidates per block
+  uint32_t cmeta[kMaxTileChunks];  // per chunk: LDS start | LDS count << 16
+  uint32_t ccnt[kMaxTileChunks + 1];  // per chunk: candidates; at tile end their exclusive prefix
+  uint32_t hist[kNBucket];        // maybe-key bucket counts, then counting-sort cursors
   uint32_t cnt[kK2Waves];
   uint32_t scratch[40];
   uint32_t bc[8];
   uint32_t next_chunk;            // the tile's chunk counter (waves claim chunks)
   uint32_t spill;                 // some wave spilled pairs to global (tile end)
 };
-using StreamSmem = StreamSmemT<false>;
-// a maybe key of bucket j, counted per tile (tile layout) or per block (BLK)
-CHOCO_DEV void hist_count(StreamSmemT<false>& sm, uint32_t, uint32_t j) { atomicAdd(&sm.hist[j], 1u); }
-CHOCO_DEV void hist_count(StreamSmemT<true>& sm, uint32_t blk, uint32_t j) {
-  atomicAdd(&sm.bh[blk][j >> 1], (j & 1u) ? 65536u : 1u);  // (a block holds <= 32768 keys: no carry)
-}
 
 // Unconditional float4 loads of kK2Unroll rows (no branch around a load: the
 // compiler's vmcnt accounting stays exact and all rows are in flight together),
@@ -497,7 +455,6 @@ struct WaveAcc {
   uint32_t lstart, lcnt;       // the current chunk's pairs kept in LDS: region offset, count
   uint32_t lfill;              // pairs in the wave's LDS region
   uint32_t cand;               // candidates, whole tile
-  uint32_t blk;                // BLK: the current chunk's block (workgroup-local index)
 };
 
 // Expand ring entries [eflushed, eflushed + nent) (nent <= 64, one per lane)
@@ -525,7 +482,7 @@ CHOCO_DEV void flush_entries(const Src<MODE, XH>& src, SM& sm, int w, int lane, 
     const uint32_t key = MODE == kData ? fkey(vv[q]) : (rank_hash(bk.seed, i0 + q) >> 1);
     ok[q] = have && (int64_t)i0 + q < bk.n && key >= bk.s_lo;
     nc += ok[q] ? 1u : 0u;
-    if (ok[q] && key < bk.s_hi) hist_count(sm, a.blk, (key - bk.s_lo) >> bk.shift);
+    if (ok[q] && key < bk.s_hi) atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
   }
   if (MODE == kHash) {
 #pragma unroll
@@ -858,20 +815,15 @@ CHOCO_DEV Buckets prologue_sample(const float* __restrict__ x, const float* __re
 // the binomial tails (host), passed as hs_lo / hs_hi.
 // GS (kData, XH): the fused gossip step -- the stream reads x, memory and xh,
 // writes x_new back and selects on d = x_new - xh.
-// BLK: the strided block layout (StreamSmemT above): nb = the grid G, workgroup b streams
-// blocks b, b + G, ...; `blk_cum` gets each block's bucket suffix counts (uint16[256] per
-// block), `side2` the maybe keys as {key, block-local index}; tile / cntw / side / tinfo
-// are unused.  Requires n < 2^30 (whole-buffer resources) and <= kMaxNB blocks.
-template <int MODE, bool XH, bool GS = false, bool BLK = false>
+template <int MODE, bool XH, bool GS = false>
 __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     const float* __restrict__ x, const float* __restrict__ xh, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
     uint32_t par, uint32_t side_cap, uint64_t seed, uint32_t hs_lo, uint64_t hs_hi, TopkCtrl* __restrict__ ctrl,
     uint32_t* __restrict__ cum_tab, uint32_t* __restrict__ cntw, uint32_t* __restrict__ side,
     float* __restrict__ cval, uint32_t* __restrict__ cidx, uint32_t* __restrict__ tinfo, Gossip gs,
-    SampleRanks ranks, uint32_t sample_if_cold, uint16_t* __restrict__ blk_cum, uint2* __restrict__ side2) {
+    SampleRanks ranks, uint32_t sample_if_cold) {
   static_assert(!GS || (MODE == kData && XH), "the gossip step needs x_hat and data keys");
-  static_assert(!BLK || MODE == kData, "the block layout is the data path");
-  __shared__ StreamSmemT<BLK> sm;
+  __shared__ StreamSmem sm;
   STAMP(1024 + blockIdx.x, 0);
   const int tid = threadIdx.x;
   const int lane = lane_id();
@@ -880,23 +832,14 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   constexpr int64_t kStep = 256 * kK2Unroll;
   static_assert(kChunk == kStep, "a chunk is one load batch");
   constexpr bool kTwoChunks = MODE == kData && !XH;  // A and B hold the next two chunks
+  const uint32_t nchunk = tile / (uint32_t)kChunk;
   Src<MODE, XH> src{x, xh, seed};
-  // BLK: this workgroup's blocks b, b + nb, ...; its chunk c is chunk (c & 15) of its block c >> 4
-  const uint32_t nblk_all = BLK ? (uint32_t)((n + kBlkElems - 1) / kBlkElems) : 0u;
-  const uint32_t nbk = BLK ? ((uint32_t)b < nblk_all ? (nblk_all - (uint32_t)b + nb - 1) / nb : 0u) : 0u;
-  const uint32_t nchunk = BLK ? nbk * (uint32_t)kBlkChunks : tile / (uint32_t)kChunk;
-  auto gchunk = [&](uint32_t c) -> int64_t {  // BLK: the global chunk index of local chunk c
-    return ((int64_t)b + (int64_t)nb * (c >> 4)) * kBlkChunks + (c & 15);
-  };
-  // byte offset of a full chunk's batch in the resources (tile-relative, or whole-buffer
-  // with BLK), or kNoChunk
-  const int64_t tlen = BLK ? n : min((int64_t)tile, n - b * (int64_t)tile);
-  const int64_t rbase = BLK ? 0 : b * (int64_t)tile;
-  const TileRsrc ts{buf_rsrc(x + rbase, (uint32_t)(tlen * 4)), buf_rsrc((XH ? xh : x) + rbase, (uint32_t)(tlen * 4)),
-                    buf_rsrc((GS ? gs.mem : x) + rbase, (uint32_t)(tlen * 4))};
+  // tile-relative byte offset of a full chunk's first / second batch, or kNoChunk
+  const int64_t tlen = min((int64_t)tile, n - b * (int64_t)tile);
+  const TileRsrc ts{buf_rsrc(x + b * (int64_t)tile, (uint32_t)(tlen * 4)),
+                    buf_rsrc((XH ? xh : x) + b * (int64_t)tile, (uint32_t)(tlen * 4)),
+                    buf_rsrc((GS ? gs.mem : x) + b * (int64_t)tile, (uint32_t)(tlen * 4))};
   auto batch0 = [&](uint32_t c) -> uint32_t {
-    if constexpr (BLK)
-      return (c < nchunk && (gchunk(c) + 1) * kChunk <= n) ? (uint32_t)(gchunk(c) * kChunk * 4) : kNoChunk;
     return (c < nchunk && (int64_t)(c + 1) * kChunk <= tlen) ? c * (uint32_t)kChunk * 4u : kNoChunk;
   };
 
@@ -981,8 +924,6 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     bk = make_buckets(hs_lo, hs_hi, seed);
   }
   if (tid < kNBucket) sm.hist[tid] = 0;
-  if constexpr (BLK)
-    for (int i = tid; i < kMaxBlk * (kNBucket / 2); i += kK2Threads) (&sm.bh[0][0])[i] = 0u;
   if (tid == 0) {
     sm.next_chunk = kTwoChunks ? 2 * kK2Waves : kK2Waves;
     sm.spill = 0;
@@ -1011,8 +952,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   // (hash mode, the partial chunk); ends with the chunk's bookkeeping.
   // `reload` refills R (the wave's next chunk) as soon as R is dead.
   auto run_chunk = [&](uint32_t cc, const float4 (&R)[kK2Unroll], auto&& reload) {
-    const int64_t cbeg = BLK ? gchunk(cc) * kChunk : tb + (int64_t)cc * kChunk;
-    a.blk = cc >> 4;
+    const int64_t cbeg = tb + (int64_t)cc * kChunk;
     const int64_t cend = min(cbeg + kChunk, n);
     float* __restrict__ ov = cval + cbeg;
     uint32_t* __restrict__ oi = cidx + cbeg;
@@ -1084,106 +1024,6 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
   STAMP(1024 + b, 2);
   WSTAMP(32000 + b * 8 + (w >> 2), w & 3);
   __syncthreads();
-
-  if constexpr (BLK) {
-    // ---- end of the workgroup's stream, block layout: per block its chunks' candidate
-    // prefix and total, its bucket suffix counts (-> blk_cum, read by K34B for every block),
-    // the workgroup's totals (-> cum_tab row, G); then the LDS pairs leave in one burst to
-    // each block's compact slots [block * 32768, ...) and the maybe keys are counting-sorted
-    // into the side list as {key, block} (K34B attributes bucket-j* keys to blocks).
-    {
-      const uint32_t t = (uint32_t)tid;
-      const uint32_t cc = t < nchunk ? sm.ccnt[t] : 0u;
-      const bool sp = t < nchunk && cc != (sm.cmeta[t] >> 16);
-      uint32_t inc = cc;  // inclusive scan inside the 16-lane rows (a block's 16 chunks)
-      inc += dpp_u32<0x111>(inc);
-      inc += dpp_u32<0x112>(inc);
-      inc += dpp_u32<0x114>(inc);
-      inc += dpp_u32<0x118>(inc);
-      const uint32_t btot = __shfl(inc, lane | 15);
-      if (t < nchunk) sm.ccnt[t] = inc - cc;  // the chunk's first slot inside its block
-      if ((t & 15u) == 0u && t < nchunk) sm.btot[t >> 4] = btot;
-      if (ballot(sp) != 0ull && lane == 0) atomicOr(&sm.spill, 1u);
-    }
-    __syncthreads();
-    if (sm.spill != 0u) {  // workgroup-uniform: a wave's LDS region overflowed (dense input): exact fallback
-      if (tid == 0) atomicOr(&ctrl->overflow[par], 2u);
-      return;
-    }
-    {
-      const uint32_t i = (uint32_t)w;  // wave w <-> block w (kMaxBlk == kK2Waves)
-      static_assert(kMaxBlk == kK2Waves, "one block per wave at the stream end");
-      if (i < nbk) {
-        const uint32_t p0 = sm.bh[i][2 * lane], p1 = sm.bh[i][2 * lane + 1];
-        const uint32_t h0 = p0 & 0xFFFFu, h1 = p0 >> 16, h2 = p1 & 0xFFFFu, h3 = p1 >> 16;  // buckets 4l..4l+3
-        const uint32_t loc = h0 + h1 + h2 + h3;
-        const uint32_t rinc = wave_incl_scan(__shfl(loc, 63 - lane));
-        const uint32_t suf = __shfl(rinc, 63 - lane);                   // maybe keys in buckets >= 4l
-        const uint32_t sure = sm.btot[i] - __builtin_amdgcn_readlane(rinc, 63);
-        const uint32_t c0 = sure + suf, c1 = c0 - h0, c2 = c1 - h1, c3 = c2 - h2;  // #candidates in buckets >= j
-        const uint2 pk = make_uint2(c0 | (c1 << 16), c2 | (c3 << 16));        // (<= 32768 each)
-        const uint32_t gb = (uint32_t)b + nb * i;
-        reinterpret_cast<uint2*>(blk_cum + (size_t)gb * kNBucket)[lane] = pk;
-        sm.bh[i][2 * lane] = pk.x;
-        sm.bh[i][2 * lane + 1] = pk.y;
-      }
-    }
-    __syncthreads();
-    {
-      // thread t <-> bucket t: the workgroup's suffix counts (cum_tab row, G), and the
-      // counting-sort cursor of maybe bucket t (maybe keys in buckets > t)
-      const int t = tid;
-      auto cum16 = [&](uint32_t q, int j) -> uint32_t { return (sm.bh[q][j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
-      if (t < kNBucket) {
-        uint32_t wc = 0, wc1 = 0, ws = 0;
-        for (uint32_t q = 0; q < nbk; ++q) {
-          wc += cum16(q, t);
-          wc1 += t + 1 < kNBucket ? cum16(q, t + 1) : 0u;
-          ws += cum16(q, kNBucket - 1);
-        }
-        cum_tab[b * kNBucket + t] = wc;
-        atomicAdd(&ctrl->G[par][b & (kNRep - 1)][t], wc);
-        if (t < kNMaybe) sm.hist[t] = wc1 - ws;
-        if (t == 0) sm.bc[0] = wc - ws;  // the workgroup's maybe keys
-      }
-    }
-    __syncthreads();
-    const uint32_t hsum = sm.bc[0];
-    if (tid == 0 && hsum > side_cap) atomicOr(&ctrl->overflow[par], 1u);
-    {
-      uint2* __restrict__ sd = side2 + (size_t)b * side_cap;
-      uint2* __restrict__ skeys = reinterpret_cast<uint2*>(&sm.ent_v[0][0]);  // the ring is dead now
-      const bool sort_lds = hsum <= (uint32_t)(sizeof(sm.ent_v) / sizeof(uint2));
-      const uint32_t h = (uint32_t)lane & 31u;
-      // a half wave per chunk; store-only loop (no load may follow a store inside it)
-      for (uint32_t c0 = 2u * w; c0 < nchunk; c0 += 2u * kK2Waves) {
-        const uint32_t cc = c0 + ((uint32_t)lane >> 5);
-        const bool have = cc < nchunk;
-        const uint32_t meta = have ? sm.cmeta[cc] : 0u;
-        const uint32_t ls = meta & 0xFFFFu, lc = meta >> 16;
-        const uint32_t bi = cc >> 4;
-        const int64_t o = ((int64_t)b + (int64_t)nb * bi) * kBlkElems + (have ? sm.ccnt[cc] : 0u);
-        float* __restrict__ ov = cval + o;
-        uint32_t* __restrict__ oi = cidx + o;
-        for (uint32_t j = h; j < lc; j += 32) {
-          const uint2 pr = sm.u.pairs[ls + j];
-          ov[j] = __uint_as_float(pr.x);
-          oi[j] = pr.y;
-          const uint32_t key = pr.x & 0x7fffffffu;
-          if (key < bk.s_hi) {  // every candidate has key >= s_lo
-            const uint32_t p = atomicAdd(&sm.hist[(key - bk.s_lo) >> bk.shift], 1u);
-            if (sort_lds) skeys[p] = make_uint2(key, bi);
-            else if (p < side_cap) sd[p] = make_uint2(key, bi);
-          }
-        }
-      }
-      if (sort_lds) {
-        __syncthreads();
-        for (uint32_t i = (uint32_t)tid; i < hsum; i += kK2Threads) sd[i] = skeys[i];
-      }
-    }
-    return;
-  }
 
   // ---- end of tile: bucket suffix counts and the chunks' candidate prefix;
   // then the LDS pairs leave in one burst and the maybe keys are counting-sorted
@@ -1261,13 +1101,8 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
       // counts stores too, so a load's wait would wait for every store before it).
       for (uint32_t j = h; j < lc; j += 32) {
         const uint2 pr = sm.u.pairs[ls + j];
-#if CHOCO_AB_K2_NTST  // (A/B only, round 6: the burst non-temporal)
-        __builtin_nontemporal_store(__uint_as_float(pr.x), &ov[j]);
-        __builtin_nontemporal_store(pr.y, &oi[j]);
-#else
         ov[j] = __uint_as_float(pr.x);
         oi[j] = pr.y;
-#endif
         to_side(pr.x, pr.y);
       }
       if (have && h == 0) cntw[(int64_t)b * nchunk + cc] = spilled ? cnt : (cc == 0 ? csum : 0u);
@@ -1278,11 +1113,7 @@ __global__ __launch_bounds__(kK2Threads, 4) void topk_stream_kernel(
     }
     if (sort_lds) {
       __syncthreads();
-#if CHOCO_AB_K2_NTST
-      for (uint32_t i = (uint32_t)tid; i < hsum; i += kK2Threads) __builtin_nontemporal_store(skeys[i], &sd[i]);
-#else
       for (uint32_t i = (uint32_t)tid; i < hsum; i += kK2Threads) sd[i] = skeys[i];
-#endif
     }
   }
   WSTAMP(32000 + b * 8 + 4 + (w >> 2), w & 3);
@@ -1821,56 +1652,6 @@ CHOCO_DEV void next_window(const uint32_t* G, uint32_t s_lo, uint32_t s_hi, uint
   out->valid = 1u;
 }
 
-// Workgroup 0's tail on the data path (K34 / K34B, thread 0): the cold backoff, the
-// shadow check that ends a cold run early, and the drift words and shadow for the next call.
-// Stores only: every value it reads came in the first round trip (ctl: s_lo, s_hi, shift,
-// overflow, m1024, t_prev, d_prev, sh_lo, sh_hi, sh_nk, sh_hits, backoff, cold_left).
-// Cold backoff: a call that took a carried window (m1024 != 0) and still missed puts
-// the workspace on a run of `backoff` calls that sample their own window (in K1 or in
-// K2's prologue), doubling per consecutive miss; warm hits halve it again.  A delta
-// whose k-th key moves further than the window between calls (x_hat draining the top
-// keys of a fixed x) then pays K1's sample instead of the exact fallback every call.
-CHOCO_DEV void finish_tail(TopkCtrl* __restrict__ ctrl, const uint32_t* ctl, bool fallback, uint32_t T_exact,
-                         uint32_t nk, uint32_t nw_lo, uint32_t nw_hi, uint32_t* __restrict__ cold_host) {
-  const bool warm_call = ctl[4] != 0u;
-  uint32_t bo = ctl[11], cl = ctl[12], hits = ctl[10];
-  // the shadow: would the window the previous call prepared have held this k-th key?
-  const bool shadow_hit = !fallback && ctl[9] == nk && ctl[7] <= T_exact && T_exact < ctl[8];
-  if (warm_call && fallback) {
-    bo = min(max(2u * bo, kColdMin), kColdMax);
-    cl = bo;
-    hits = 0u;
-  } else if (warm_call) {
-    bo = max(bo / 2u, kColdMin);
-    hits = 0u;
-  } else if (cl != 0u) {
-    --cl;
-    // a cold run ends early once the carried (drift-aware) windows would have held the
-    // k-th key kShadowExit calls in a row: the drift that caused the miss is followed now
-    hits = shadow_hit ? hits + 1u : 0u;
-    if (hits >= kShadowExit) {
-      cl = 0u;
-      hits = 0u;
-    }
-  }
-  ctrl->backoff = bo;
-  ctrl->cold_left = cl;
-  ctrl->sh_hits = hits;
-  if (!fallback) {  // the drift words and the shadow for the next call
-    ctrl->d_prev = (ctl[9] == nk && ctl[5] != 0u) ? T_exact - ctl[5] : 0u;
-    ctrl->t_prev = T_exact;
-    ctrl->sh_lo = nw_lo;  // (this thread's next_window)
-    ctrl->sh_hi = nw_hi;
-    ctrl->sh_nk = nk;
-  } else {
-    ctrl->t_prev = 0u;
-    ctrl->d_prev = 0u;
-    ctrl->sh_nk = 0u;
-  }
-  // (the host launches K1 for fused-gossip calls on a cold run: launch_topk)
-  if (cold_host) __hip_atomic_store(cold_host, cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 template <int MODE, bool XH>
 __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     const float* x, const float* xh, int64_t n, int64_t k, uint32_t tile, uint32_t nb,
@@ -2136,294 +1917,52 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   }
   // random-k windows come from the host each call: nothing for the next call to reuse
   if (MODE == kHash && b == 0 && tid == 0) ctrl->bounds[par ^ 1u].valid = 0u;
-  if (MODE == kData && b == 0 && tid == 0) finish_tail(ctrl, fs.ctl, fallback, T_exact, nk, nw_lo, nw_hi, cold_host);
+  // Cold backoff: a call that took a carried window (m1024 != 0) and still missed puts
+  // the workspace on a run of `backoff` calls that sample their own window (in K1 or in
+  // K2's prologue), doubling per consecutive miss; warm hits halve it again.  A delta
+  // whose k-th key moves further than the window between calls (x_hat draining the top
+  // keys of a fixed x, the bench's fused step) then pays K1's sample instead of the
+  // exact fallback every call.
+  if (MODE == kData && b == 0 && tid == 0) {
+    const bool warm_call = fs.ctl[4] != 0u;
+    uint32_t bo = fs.ctl[11], cl = fs.ctl[12], hits = fs.ctl[10];
+    // the shadow: would the window the previous call prepared have held this k-th key?
+    const bool shadow_hit = !fallback && fs.ctl[9] == nk && fs.ctl[7] <= T_exact && T_exact < fs.ctl[8];
+    if (warm_call && fallback) {
+      bo = min(max(2u * bo, kColdMin), kColdMax);
+      cl = bo;
+      hits = 0u;
+    } else if (warm_call) {
+      bo = max(bo / 2u, kColdMin);
+      hits = 0u;
+    } else if (cl != 0u) {
+      --cl;
+      // a cold run ends early once the carried (drift-aware) windows would have held the
+      // k-th key kShadowExit calls in a row: the drift that caused the miss is followed now
+      hits = shadow_hit ? hits + 1u : 0u;
+      if (hits >= kShadowExit) {
+        cl = 0u;
+        hits = 0u;
+      }
+    }
+    ctrl->backoff = bo;
+    ctrl->cold_left = cl;
+    ctrl->sh_hits = hits;
+    if (!fallback) {  // the drift words and the shadow for the next call
+      ctrl->d_prev = (fs.ctl[9] == nk && fs.ctl[5] != 0u) ? T_exact - fs.ctl[5] : 0u;
+      ctrl->t_prev = T_exact;
+      ctrl->sh_lo = nw_lo;  // (this thread's next_window)
+      ctrl->sh_hi = nw_hi;
+      ctrl->sh_nk = nk;
+    } else {
+      ctrl->t_prev = 0u;
+      ctrl->d_prev = 0u;
+      ctrl->sh_nk = 0u;
+    }
+    // (the host launches K1 for fused-gossip calls on a cold run: launch_topk)
+    if (cold_host) __hip_atomic_store(cold_host, cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   STAMP(24576 + b, 2);
-}
-
-// ----------------------------------------------------------------------------
-// K34B: the finish of the block layout (BLK); one workgroup per K2 workgroup
-//
-// The select is K34's: every workgroup finds bucket j* from the totals, gathers every K2
-// workgroup's bucket-j* side entries -- {key, block} -- into LDS, and selects T and the
-// tie quota r.  The placement is per BLOCK (the output order is the index order, and K2
-// workgroup b streamed blocks b, b + G, ...): each block's count above T is its suffix
-// count above bucket j* (blk_cum, one 2-byte load per block) plus its bucket-j* keys
-// above T, its ties its bucket-j* keys at T; one scan over all blocks (<= 4 per thread)
-// gives every block its output offset and tie rank.  Then each workgroup emits its own
-// blocks' candidates (compact per block) in one pass over its position sequence: a
-// position's block by a search of the workgroup's <= 16 run starts, its output slot =
-// the block's first output slot + its rank among the selected positions of the block.
-// ----------------------------------------------------------------------------
-struct FinBSmem {
-  uint32_t keys[kMCap];
-  uint32_t kbase[kK4Threads];  // per K2 workgroup: side index of its first bucket-j* entry - its first slot
-  uint32_t ecnt[2][kEmitRows * (kK4Threads / 64) + 1];
-  uint32_t hist[1 << kSelBits];
-  uint32_t G[kNBucket];
-  uint32_t bcnt[kMaxNB];       // per block: its bucket-j* keys above T | at T << 16
-  uint32_t run[kMaxBlk + 1];   // this workgroup's blocks: first position in its candidate sequence
-  uint32_t bout[kMaxBlk];      // ... first output slot - selected positions of the earlier blocks
-  uint32_t btie[kMaxBlk];      // ... global tie rank of the first tie - ties of the earlier blocks
-  uint32_t bmode[kMaxBlk];     // ... ties at T: none / all / partly taken
-  uint32_t bsel[kMaxBlk], beq[kMaxBlk];
-  uint32_t scratch[40];
-  uint32_t bc[8];
-  uint32_t ctl[16];
-};
-
-template <bool XH>
-__global__ __launch_bounds__(kK4Threads) void topk_finish_blk_kernel(
-    const float* x, const float* xh, int64_t n, int64_t k, uint32_t nb, uint32_t side_cap, float scale,
-    TopkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ cum_tab, const uint16_t* __restrict__ blk_cum,
-    const uint2* __restrict__ side2, const float* __restrict__ cval, const uint32_t* __restrict__ cidx,
-    float* __restrict__ out_val, int32_t* __restrict__ out_idx, int64_t idx_base, WideCtrl* __restrict__ wide,
-    uint32_t* __restrict__ gcnt, uint32_t par, uint32_t* __restrict__ status, uint32_t* __restrict__ host_status,
-    Fold fold, uint32_t* __restrict__ cold_host) {
-  __shared__ FinBSmem fs;
-  __shared__ ExactSmem es;
-  __shared__ uint32_t s_tk;
-  const int tid = threadIdx.x;
-  const int lane = lane_id();
-  const int64_t b = blockIdx.x;
-  const uint32_t ku = (uint32_t)k;
-  const uint32_t NB = (uint32_t)((n + kBlkElems - 1) / kBlkElems);
-  const uint32_t nbk = (uint32_t)b < NB ? (NB - (uint32_t)b + nb - 1) / nb : 0u;
-  // ---- first round trip, every load independent: control words, the totals, every K2
-  // workgroup's "sure" count, the sizes of this workgroup's blocks
-  uint32_t cword = 0;
-  {
-    const TopkBounds& Bw = ctrl->bounds[par];
-    const uint32_t* src = tid == 0 ? &Bw.s_lo : tid == 1 ? &Bw.s_hi : tid == 2 ? &Bw.shift
-                        : tid == 3 ? &ctrl->overflow[par] : tid == 4 ? &Bw.m1024
-                        : tid < 11 ? &ctrl->t_prev + (tid - 5)
-                        : tid == 11 ? &ctrl->backoff : &ctrl->cold_left;
-    if (tid < 13) cword = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  const bool mine_wg = tid < (int)nb;
-  const uint32_t* row = cum_tab + (int64_t)(mine_wg ? tid : 0) * kNBucket;  // clamped: loads unconditional
-  const uint32_t sure_t = row[kNMaybe];
-  uint32_t g[kNRep];
-  if (tid < kNBucket) {
-#pragma unroll
-    for (int r = 0; r < kNRep; ++r) g[r] = ctrl->G[par][r][tid];
-  }
-  const uint32_t bsz = (uint32_t)tid < nbk ? blk_cum[(size_t)((uint32_t)b + nb * (uint32_t)tid) * kNBucket] : 0u;
-  for (int i = tid; i < kMaxNB; i += kK4Threads) fs.bcnt[i] = 0u;
-  if (tid < 13) fs.ctl[tid] = cword;
-  if (tid < kNBucket) {
-    uint32_t sum = 0;
-#pragma unroll
-    for (int r = 0; r < kNRep; ++r) sum += g[r];
-    fs.G[tid] = sum;
-  }
-  if (tid == 0) fs.bc[4] = 0;
-  if (tid < 64) {  // wave 0: run starts of this workgroup's blocks (nbk <= 16), run[nbk] = total
-    const uint32_t inc = wave_incl_scan(bsz);
-    if ((uint32_t)lane <= nbk) fs.run[lane] = inc - bsz;
-  }
-  __syncthreads();
-  const uint32_t s_lo = fs.ctl[0], shift = fs.ctl[2], overflow = fs.ctl[3];
-  const uint32_t tot = fs.run[nbk];
-  bool fallback = overflow != 0 || fs.G[0] < ku || fs.G[kNMaybe] >= ku;
-  if (!fallback && tid < kNMaybe && fs.G[tid] >= ku && fs.G[tid + 1] < ku) fs.bc[4] = tid;
-  __syncthreads();
-  const uint32_t jstar = fs.bc[4];
-  if (!fallback && fs.G[jstar] - fs.G[jstar + 1] > (uint32_t)kMCap) fallback = true;
-  uint32_t T_exact = 0, nw_lo = 0, nw_hi = 0;
-  const uint32_t nk = nk_tag(n, k);
-  if (fallback) {
-    if (b == 0 && tid == 0) atomicAdd(&ctrl->fallbacks, 1u);
-    Src<kData, XH> src{x, xh, 0};
-    const uint32_t tile_fb = (uint32_t)((n + nb - 1) / nb);
-    wide_fallback(src, n, k, tile_fb, nb, fold, scale, wide, gcnt, out_val, out_idx, idx_base, es, &s_tk, status,
-                  host_status, &ctrl->bounds[par ^ 1u]);
-  } else {
-    // ---- second round trip: per K2 workgroup its bucket-j* entries and their side offset;
-    // per block its candidates above bucket j*
-    uint32_t cb = 0, off = 0;
-    {
-      const uint32_t a = row[jstar], c = row[jstar + 1];
-      if (mine_wg) {
-        cb = a - c;        // bucket-j* entries of K2 workgroup tid
-        off = c - sure_t;  // their side-list offset (buckets stored high to low)
-      }
-    }
-    constexpr int kBPT = kMaxNB / kK4Threads;  // blocks per thread (block = tid * kBPT + q)
-    uint32_t gtb[kBPT];
-#pragma unroll
-    for (int q = 0; q < kBPT; ++q) {
-      const uint32_t gbq = (uint32_t)tid * kBPT + q;
-#if CHOCO_AB_K34B_NOGT  // (A/B timing only: one row instead of every block's)
-      gtb[q] = gbq < NB ? blk_cum[(size_t)(gbq & 7) * kNBucket + jstar + 1] : 0u;
-#else
-      gtb[q] = gbq < NB ? blk_cum[(size_t)gbq * kNBucket + jstar + 1] : 0u;
-#endif
-    }
-    uint32_t M;
-    const uint32_t kpos = block_excl_scan(cb, fs.scratch, &M);  // M = G[j*] - G[j*+1]
-    // every K2 workgroup's bucket-j* entries -> keys[0, M) (slot -> workgroup map in the
-    // select histogram, not in use yet), kept in registers with their blocks
-    uint16_t* tmap = reinterpret_cast<uint16_t*>(fs.hist);
-    fs.kbase[tid] = (uint32_t)(mine_wg ? tid : 0) * side_cap + off - kpos;  // mod 2^32
-    for (uint32_t j = 0; j < cb; ++j) tmap[kpos + j] = (uint16_t)tid;
-    __syncthreads();
-    constexpr int kG = kMCap / kK4Threads;
-    uint32_t kv[kG], kb[kG];
-#pragma unroll
-    for (int q = 0; q < kG; ++q) {
-      kv[q] = 0u;
-      kb[q] = 0u;
-      if ((uint32_t)q * kK4Threads < M) {  // workgroup-uniform
-        const uint32_t i = min((uint32_t)tid + (uint32_t)q * kK4Threads, M - 1u);
-        const uint32_t t = tmap[i];
-        const uint2 e = side2[fs.kbase[t] + i];
-        kv[q] = e.x;
-        kb[q] = t + nb * e.y;  // the entry's block
-      }
-    }
-    __syncthreads();  // the slot map (= histogram) is dead before the select clears it
-#pragma unroll
-    for (int q = 0; q < kG; ++q) {
-      const uint32_t i = (uint32_t)tid + (uint32_t)q * kK4Threads;
-      if (i < M) fs.keys[i] = kv[q];
-    }
-    // ---- radix select inside bucket j* (K34's)
-    const uint32_t base_j = s_lo + (jstar << shift);
-    uint32_t prefix = 0, krem = ku - fs.G[jstar + 1];  // 1 <= krem <= M
-    int sh = (int)shift;
-    while (sh > 0) {
-      const int dsh = sh > kSelBits ? sh - kSelBits : 0;
-      const uint32_t dmask = (1u << (sh - dsh)) - 1u;
-      const bool narrow = dmask < (uint32_t)kK4Threads;
-      for (int i = tid; i < (narrow ? (int)dmask + 1 : (1 << kSelBits)); i += kK4Threads) fs.hist[i] = 0;
-      __syncthreads();
-      for (uint32_t j = tid; j < M; j += kK4Threads) {
-        const uint32_t rel = fs.keys[j] - base_j;
-        if (sh >= 32 || (rel >> sh) == (prefix >> sh)) atomicAdd(&fs.hist[(rel >> dsh) & dmask], 1u);
-      }
-      __syncthreads();
-      if (narrow) block_find_rank1k(fs.hist, dmask + 1, krem, fs.scratch, fs.bc + 5);
-      else block_find_rank8k(fs.hist, krem, fs.scratch, fs.bc + 5);
-      prefix |= fs.bc[5] << dsh;
-      krem = fs.bc[6];
-      sh = dsh;
-    }
-    const uint32_t T = base_j + prefix;
-    const uint32_t r = krem;  // ties at T to take (>= 1)
-    T_exact = T;
-    // ---- per block: its bucket-j* entries above / at T
-#pragma unroll
-    for (int q = 0; q < kG; ++q) {
-      const uint32_t i = (uint32_t)tid + (uint32_t)q * kK4Threads;
-      if (i < M && kv[q] >= T) atomicAdd(&fs.bcnt[kb[q]], kv[q] > T ? 1u : 65536u);
-    }
-    __syncthreads();
-    // ---- every block's (#> T, #== T) in index order -> output offsets and tie ranks
-    uint32_t gts[kBPT], eqs[kBPT], gsum = 0, esum = 0;
-#pragma unroll
-    for (int q = 0; q < kBPT; ++q) {
-      const uint32_t gbq = (uint32_t)tid * kBPT + q;
-      const uint32_t v = gbq < NB ? fs.bcnt[gbq] : 0u;
-      gts[q] = gtb[q] + (v & 0xFFFFu);
-      eqs[q] = v >> 16;
-      gsum += gts[q];
-      esum += eqs[q];
-    }
-    uint32_t gpre, epre, gtot, etot;
-    block_excl_scan2(gsum, esum, fs.scratch, &gpre, &epre, &gtot, &etot);
-#pragma unroll
-    for (int q = 0; q < kBPT; ++q) {
-      const uint32_t gbq = (uint32_t)tid * kBPT + q;
-      if (gbq < NB && gbq % nb == (uint32_t)b) {
-        const uint32_t i = gbq / nb;
-        const uint32_t taken = epre >= r ? 0u : min(eqs[q], r - epre);  // ties taken in this block
-        fs.bout[i] = gpre + min(r, epre);
-        fs.btie[i] = epre;
-        fs.bsel[i] = gts[q] + taken;
-        fs.beq[i] = eqs[q];
-        fs.bmode[i] = taken == 0u ? kTakeNone : (taken == eqs[q] ? kTakeAll : kTakePartial);
-      }
-      gpre += gts[q];
-      epre += eqs[q];
-    }
-    __syncthreads();
-    if (tid == 0) {  // relative to this workgroup's position sequence
-      uint32_t sb = 0, tb = 0, part = 0;
-      for (uint32_t i = 0; i < nbk; ++i) {
-        fs.bout[i] -= sb;
-        fs.btie[i] -= tb;
-        sb += fs.bsel[i];
-        tb += fs.beq[i];
-        part |= fs.bmode[i] == kTakePartial ? 1u : 0u;
-      }
-      fs.bc[7] = part;
-    }
-    __syncthreads();
-    // ---- emission: batches of kEmitRows x kK4Threads positions of this workgroup's sequence
-    const bool partial = fs.bc[7] != 0u;
-    uint32_t wsel = 0, wtie = 0;
-    int eb = 0;
-    for (uint32_t p0 = 0; p0 < tot; p0 += kK4Threads * kEmitR) {
-      float v[kEmitR];
-      uint32_t idx[kEmitR], bi[kEmitR];
-#pragma unroll
-      for (int i = 0; i < kEmitR; ++i) {
-        const uint32_t p = p0 + (uint32_t)i * kK4Threads + tid;
-        uint32_t lo = 0, hi = nbk - 1;  // the block of position p: the last run start <= p
-#if CHOCO_AB_K34B_NOSEARCH  // (A/B timing only)
-        lo = min(p >> 9, hi);
-        while (lo > 0 && fs.run[lo] > p) --lo;  // (keeps p - run[lo] >= 0: the slot stays inside the block)
-#else
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi + 1) >> 1;
-          if (fs.run[mid] <= p) lo = mid; else hi = mid - 1;
-        }
-#endif
-        bi[i] = lo;
-        const int64_t addr = p < tot ? ((int64_t)b + (int64_t)nb * lo) * kBlkElems + (p - fs.run[lo]) : 0;
-        v[i] = cval[addr];
-        idx[i] = cidx[addr];
-      }
-      const uint32_t nrows = min((uint32_t)kEmitR, (tot - p0 + kK4Threads - 1) / kK4Threads);
-      bool gtv[kEmitR], eqv[kEmitR];
-#pragma unroll
-      for (int i = 0; i < kEmitR; ++i) {
-        const bool valid = p0 + (uint32_t)i * kK4Threads + tid < tot;
-        const uint32_t key = fkey(v[i]);
-        gtv[i] = valid && key > T;
-        eqv[i] = valid && key == T;
-      }
-      bool sel[kEmitR];
-      uint32_t rk[kEmitR];
-      if (partial) {  // workgroup-uniform: the block holding the r-th tie is one of ours
-        const uint32_t eq_total = batch_ranks(eqv, rk, fs.ecnt[eb], nrows);
-        eb ^= 1;
-#pragma unroll
-        for (int i = 0; i < kEmitR; ++i) sel[i] = gtv[i] || (eqv[i] && fs.btie[bi[i]] + wtie + rk[i] < r);
-        wtie += eq_total;
-      } else {
-#pragma unroll
-        for (int i = 0; i < kEmitR; ++i) sel[i] = gtv[i] || (eqv[i] && fs.bmode[bi[i]] == kTakeAll);
-      }
-      const uint32_t nsel = batch_ranks(sel, rk, fs.ecnt[eb], nrows);
-      eb ^= 1;
-#pragma unroll
-      for (int i = 0; i < kEmitR; ++i) {
-        if ((uint32_t)i >= nrows) continue;  // workgroup-uniform
-        const uint32_t o = fs.bout[bi[i]] + wsel + rk[i];
-        if (sel[i] && o < ku) {  // (bounded: an inconsistent select cannot write past k)
-          out_val[o] = v[i] * scale;
-          out_idx[o] = (int32_t)((int64_t)idx[i] + idx_base);
-          if (fold.on()) fold_apply(fold, (int64_t)idx[i], v[i] * scale);
-        }
-      }
-      wsel += nsel;
-    }
-    if (b == 0 && tid < 64)
-      next_window(fs.G, s_lo, fs.ctl[1], shift, fs.ctl[4], T, n, k,
-                  window_drift(T, fs.ctl[5], fs.ctl[6], fs.ctl[9] == nk), &ctrl->bounds[par ^ 1u], nw_lo, nw_hi);
-  }
-  if (b == 0 && tid == 0) finish_tail(ctrl, fs.ctl, fallback, T_exact, nk, nw_lo, nw_hi, cold_host);
 }
 
 // ----------------------------------------------------------------------------
@@ -2556,33 +2095,11 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
     profile_end("topk_bounds", st);
     CHOCO_LAUNCHED("topk_bounds_kernel");
   }
-  uint16_t* bcum = reinterpret_cast<uint16_t*>(base + L.off_bcum);
-  uint2* side2 = reinterpret_cast<uint2*>(base + L.off_side2);
-  if constexpr (MODE == kData) {
-    if (topk_blocks_apply(n, k)) {  // the strided block layout: K2 (BLK) + K34B
-      const uint32_t G = (uint32_t)kK2Target;
-      profile_begin("topk_stream", st);
-      CHOCO_KLAUNCH((topk_stream_kernel<kData, XH, GS, true>), dim3(G), dim3(kK2Threads), 0, st, x, xh, n, k, L.tile,
-                    G, par, (uint32_t)kBlkSideCap, seed, hs_lo, hs_hi, ctrl, cum, cntw, side, cval, cidx,
-                    reinterpret_cast<uint32_t*>(base + L.off_tinfo), gs, sample_ranks(n, k),
-                    (uint32_t)(warm && !GS ? 1 : 0), bcum, side2);
-      profile_end("topk_stream", st);
-      CHOCO_LAUNCHED("topk_stream_kernel");
-      profile_begin("topk_finish", st);
-      CHOCO_KLAUNCH((topk_finish_blk_kernel<XH>), dim3(G), dim3(kK4Threads), 0, st, x, xh, n, k, G,
-                    (uint32_t)kBlkSideCap, scale, ctrl, cum, bcum, side2, cval, cidx, out_val, out_idx, idx_base,
-                    reinterpret_cast<WideCtrl*>(base + L.off_wide), reinterpret_cast<uint32_t*>(base + L.off_gcnt),
-                    par, status.dev, status.host, fold, cold_host);
-      profile_end("topk_finish", st);
-      CHOCO_LAUNCHED("topk_finish_blk_kernel");
-      return CHOCO_OK;
-    }
-  }
   profile_begin("topk_stream", st);
   CHOCO_KLAUNCH((topk_stream_kernel<MODE, XH, GS>), dim3(L.nb), dim3(kK2Threads), 0, st, x, xh, n, k, L.tile, L.nb,
                 par, L.side_cap, seed, hs_lo, hs_hi, ctrl, cum, cntw, side, cval, cidx,
                 reinterpret_cast<uint32_t*>(base + L.off_tinfo), gs, sample_ranks(n, k),
-                (uint32_t)(MODE == kData && warm && !GS ? 1 : 0), bcum, side2);
+                (uint32_t)(MODE == kData && warm && !GS ? 1 : 0));
   profile_end("topk_stream", st);
   CHOCO_LAUNCHED("topk_stream_kernel");
   profile_begin("topk_finish", st);
@@ -2736,11 +2253,6 @@ CHOCO_API int choco_topk_set_warm_start(int32_t enable) {
   return CHOCO_OK;
 }
 
-CHOCO_API int choco_topk_set_block_layout(int32_t enable) {
-  g_topk_blocks.store(enable != 0);
-  return CHOCO_OK;
-}
-
 CHOCO_API int choco_topk_compress(const float* x, const float* xhat, int64_t n, int64_t k, float* out_val,
                                   int32_t* out_idx, void* ws, size_t ws_bytes, void* stream) {
   return dispatch_topk<kData>(x, xhat, n, k, 0, 1.0f, out_val, out_idx, 0, ws, ws_bytes, as_stream(stream));
@@ -2804,7 +2316,7 @@ CHOCO_API int choco_dbg_stream_only(const float* x, int64_t n, int64_t k, void* 
                        reinterpret_cast<uint32_t*>(base + L.off_cntw), reinterpret_cast<uint32_t*>(base + L.off_side),
                        reinterpret_cast<float*>(base + L.off_cval), reinterpret_cast<uint32_t*>(base + L.off_cidx),
                        reinterpret_cast<uint32_t*>(base + L.off_tinfo), Gossip{nullptr, 0.f}, SampleRanks{0u, 0u, 0u},
-                       0u, nullptr, nullptr);
+                       0u);
   CHOCO_HIP(hipEventRecord(b, st));
   CHOCO_HIP(hipEventSynchronize(b));
   float ms = 0.f;

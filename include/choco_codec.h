@@ -74,11 +74,6 @@ size_t choco_topk_workspace_size(int64_t n);
  * the warm path off library-wide (every call samples). */
 int choco_topk_workspace_reset(const void* ws, size_t ws_bytes);
 int choco_topk_set_warm_start(int32_t enable);
-/* Flat calls with 2^24 <= n <= 2^27 and k <= n / 64 stream the buffer in strided 32768-
- * element blocks (stream workgroup b takes blocks b, b + 256, ...; per-block placement);
- * other calls stream contiguous tiles.  Same output either way.  enable = 0 turns the block
- * layout off library-wide (A/B and tests). */
-int choco_topk_set_block_layout(int32_t enable);
 /* Byte offset, in every top-k / random-k / segmented workspace, of a sticky uint32
  * status word.  Bit 0: a bounded wait inside the exact fallback gave up, so the
  * output of that call is invalid (never expected; the wait is bounded so that a

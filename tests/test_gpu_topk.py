@@ -721,35 +721,27 @@ def _ties_data(n, seed):
 @pytest.mark.parametrize("n", [16_777_216, 16_789_561, 33_554_431, 100_000_000])
 @pytest.mark.parametrize("ratio", [0.99, 0.985])
 @pytest.mark.parametrize("kind", ["randn", "ties", "xhat"])
-def test_topk_block_layout_exact(n, ratio, kind):
-    """The strided block layout (csrc/topk.hip BLK: stream workgroup b takes the 32768-element
-    blocks b, b + 256, ...; K34B places every block) on its whole range -- the first size it
-    serves (2^24: 512 blocks), a partial last chunk and block, 2^25 - 1, the north-star 100M --
-    at k = 1 % and 1.5 % (<= n / 64), on Gaussian data, on tie-heavy data (the k-th value
-    shared by ~100 elements: ties split inside one block), and on a delta x - x_hat; then the
-    same call with the tile layout.  Both bit-exact against the oracle, warm calls included."""
+def test_topk_large_exact_cold_and_warm(n, ratio, kind):
+    """The flat pipeline from 2^24 (a partial last chunk and tile at 2^24 + 12345, 2^25 - 1)
+    to the north-star 100M, at k = 1 % and 1.5 %, on Gaussian data, on tie-heavy data (the
+    k-th value shared by ~100 elements: ties split inside one tile), and on a delta
+    x - x_hat; a cold call then a warm call, bit-exact against the oracle."""
     from chocosgd_amd import codec
-    lib = codec.lib()
     k = codec.topk_k(n, ratio)
     x = _ties_data(n, 61) if kind == "ties" else randn(n, 62)
     xh = randn(n, 63, 0.5) if kind == "xhat" else None
     d = host(x) if xh is None else (host(x) - host(xh)).astype(np.float32)
     ov, oi = O.topk(d, k)
-    try:
-        for blocks in (1, 1, 0):  # cold, then warm, then the tile layout
-            lib.choco_topk_set_block_layout(blocks)
-            vals, idx = codec.topk(x, k, xhat=xh)
-            assert np.array_equal(host(idx).astype(np.int64), oi), blocks
-            assert same_bits(host(vals), ov), blocks
-    finally:
-        lib.choco_topk_set_block_layout(1)
+    for _ in range(2):  # cold, then warm
+        vals, idx = codec.topk(x, k, xhat=xh)
+        assert np.array_equal(host(idx).astype(np.int64), oi)
+        assert same_bits(host(vals), ov)
 
 
-def test_topk_block_layout_gossip_and_drain():
-    """The block layout with the fused consensus step over a warm sequence (x, memory, x_hat
-    evolve; every call exact, x_new bit-identical), then the CHOCO drain on a fixed delta
-    (every call's k-th key moves: windows miss, the exact fallback and the cold run run on
-    the block layout too)."""
+def test_topk_gossip_and_drain_20m():
+    """The fused consensus step over a warm sequence at 20M (x, memory, x_hat evolve; every
+    call exact, x_new bit-identical), then the CHOCO drain on a fixed delta (every call's
+    k-th key moves: windows miss, the exact fallback and the cold run)."""
     from chocosgd_amd import codec
     n = 20_000_003
     k = codec.topk_k(n, 0.99)
