@@ -152,6 +152,17 @@ CHOCO_DEV int32_t window_drift(uint32_t T, uint32_t t_prev, uint32_t d_prev_bits
   const int64_t m = dn > 0 ? (dn < dp ? dn : dp) : (dn > dp ? dn : dp);
   return (int32_t)(m > (1ll << 30) ? (1ll << 30) : (m < -(1ll << 30) ? -(1ll << 30) : m));
 }
+// Whether the drift the previous call proposed (cand_bits, from its own last two moves) would
+// have predicted this call's k-th key T better than the previous key t_prev did: a steady
+// drift passes, a stationary noisy key (whose moves revert) does not.
+// The caller keeps a streak of such calls and applies the drift from kDriftTrust on.
+constexpr uint32_t kDriftTrust = 2;
+CHOCO_DEV bool drift_trusted(uint32_t T, uint32_t t_prev, uint32_t cand_bits, bool valid) {
+  if (!valid || t_prev == 0u || cand_bits == 0u) return false;
+  const int64_t e_static = (int64_t)T - (int64_t)t_prev;
+  const int64_t e_drift = e_static - (int64_t)(int32_t)cand_bits;
+  return (e_drift < 0 ? -e_drift : e_drift) < (e_static < 0 ? -e_static : e_static);
+}
 
 // number of set bits of `mask` strictly below this lane
 CHOCO_DEV uint32_t mask_prefix(uint64_t mask) {

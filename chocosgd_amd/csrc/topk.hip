@@ -123,7 +123,9 @@ struct TopkCtrl {
   uint32_t t_prev;
   uint32_t d_prev;                               // int32 bits
   uint32_t sh_lo, sh_hi, sh_nk, sh_hits;
-  uint32_t pad0[5];
+  uint32_t d_cand;                               // the drift window_drift proposed last call (int32 bits)
+  uint32_t d_trust;                              // calls in a row whose proposed drift beat the static key
+  uint32_t pad0[3];
   uint32_t overflow[2];                          // bit 0: a side list overflowed; bit 1: take the exact fallback
   uint32_t pad1[14];
   TopkBounds bounds[2];
@@ -1687,8 +1689,9 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     const uint32_t* src = tid == 0 ? &Bw.s_lo : tid == 1 ? &Bw.s_hi : tid == 2 ? &Bw.shift
                         : tid == 3 ? &ctrl->overflow[par] : tid == 4 ? &Bw.m1024
                         : tid < 11 ? &ctrl->t_prev + (tid - 5)  // t_prev, d_prev, sh_lo, sh_hi, sh_nk, sh_hits
-                        : tid == 11 ? &ctrl->backoff : &ctrl->cold_left;
-    if (tid < 13) cword = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        : tid == 11 ? &ctrl->backoff : tid == 12 ? &ctrl->cold_left
+                        : tid == 13 ? &ctrl->d_cand : &ctrl->d_trust;
+    if (tid < 15) cword = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const bool mine_tile = tid < (int)nb;
   const uint32_t* row = cum_tab + (int64_t)(mine_tile ? tid : 0) * kNBucket;  // clamped: loads unconditional
@@ -1698,9 +1701,9 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
 #pragma unroll
     for (int r = 0; r < kNRep; ++r) g[r] = ctrl->G[par][r][tid];
   }
-  // s_lo, s_hi, shift, overflow, m1024, t_prev, d_prev, sh_lo, sh_hi, sh_nk, sh_hits, backoff, cold_left
-  // (workgroup 0's tail then issues stores only)
-  if (tid < 13) fs.ctl[tid] = cword;
+  // s_lo, s_hi, shift, overflow, m1024, t_prev, d_prev, sh_lo, sh_hi, sh_nk, sh_hits, backoff, cold_left,
+  // d_cand, d_trust (workgroup 0's tail then issues stores only)
+  if (tid < 15) fs.ctl[tid] = cword;
   const uint32_t tot = compact ? ti : chunk_run_starts(cw, nchunk, fs.run_start, fs.scratch);
   if (compact) __syncthreads();  // fs.ctl (chunk_run_starts ends with this barrier)
   const uint32_t s_lo = fs.ctl[0], shift = fs.ctl[2], overflow = fs.ctl[3];
@@ -1731,6 +1734,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
   if (!fallback && fs.G[jstar] - fs.G[jstar + 1] > (uint32_t)kMCap) fallback = true;
   uint32_t T_exact = 0;  // (workgroup 0's tail: this call's exact k-th key on the select path)
   uint32_t nw_lo = 0, nw_hi = 0;  // ... and the window it prepared for the next call
+  uint32_t trust = 0;             // ... and the drift-trust streak
   const uint32_t nk = nk_tag(n, k);
   if (fallback) {
     if (b == 0 && tid == 0) atomicAdd(&ctrl->fallbacks, 1u);
@@ -1913,7 +1917,9 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     STAMP(30000 + b, 2);
     if (MODE == kData && b == 0 && tid < 64)
       next_window(fs.G, s_lo, fs.ctl[1], shift, fs.ctl[4], T, n, k,
-                  window_drift(T, fs.ctl[5], fs.ctl[6], fs.ctl[9] == nk), &ctrl->bounds[par ^ 1u], nw_lo, nw_hi);
+                  (trust = drift_trusted(T, fs.ctl[5], fs.ctl[13], fs.ctl[9] == nk) ? min(fs.ctl[14] + 1u, 15u) : 0u)
+                          >= kDriftTrust ? window_drift(T, fs.ctl[5], fs.ctl[6], fs.ctl[9] == nk) : 0,
+                  &ctrl->bounds[par ^ 1u], nw_lo, nw_hi);
   }
   // random-k windows come from the host each call: nothing for the next call to reuse
   if (MODE == kHash && b == 0 && tid == 0) ctrl->bounds[par ^ 1u].valid = 0u;
@@ -1954,10 +1960,14 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
       ctrl->sh_lo = nw_lo;  // (this thread's next_window)
       ctrl->sh_hi = nw_hi;
       ctrl->sh_nk = nk;
+      ctrl->d_cand = (uint32_t)window_drift(T_exact, fs.ctl[5], fs.ctl[6], fs.ctl[9] == nk);
+      ctrl->d_trust = trust;
     } else {
       ctrl->t_prev = 0u;
       ctrl->d_prev = 0u;
       ctrl->sh_nk = 0u;
+      ctrl->d_cand = 0u;
+      ctrl->d_trust = 0u;
     }
     // (the host launches K1 for fused-gossip calls on a cold run: launch_topk)
     if (cold_host) __hip_atomic_store(cold_host, cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -100,10 +100,12 @@ CHOCO_DEV SegRow seg_row(const int64_t* __restrict__ plan, int s) {
 // window_drift extrapolates the next window by them).
 struct SegWin {
   uint32_t lo, sh, valid, pad;
-  uint32_t tprev, dprev, pad2[2];
+  uint32_t tprev, dprev, cand, trust;  // cand: the drift window_drift proposed when this window was
+                                       // written; trust: the calls in a row it beat the static key
 };
-CHOCO_DEV SegWin seg_win(uint32_t lo, uint32_t sh, uint32_t T, const SegWin& old) {
-  return SegWin{lo, sh, 1u, 0u, T, (old.valid && old.tprev) ? T - old.tprev : 0u, {0u, 0u}};
+CHOCO_DEV SegWin seg_win(uint32_t lo, uint32_t sh, uint32_t T, const SegWin& old, uint32_t cand = 0u,
+                         uint32_t trust = 0u) {
+  return SegWin{lo, sh, 1u, 0u, T, (old.valid && old.tprev) ? T - old.tprev : 0u, cand, trust};
 }
 
 // info[8 s + i]: 0 b1 (cold), 1 rank inside b1 (cold), 2 T, 3 bin of the k-th key
@@ -116,7 +118,8 @@ struct SegWs {
   SegWin* win;
   uint32_t* misses;     // the workspace's CHOCO_TOPK_FALLBACKS_OFFSET counter
   uint32_t* miss_flag;  // pinned host word of the cold backoff (nullable)
-  unsigned long long* shadow;  // pinned host counter of cold calls' window checks (nullable; seg_count_kernel)
+  unsigned long long* shadow;       // device counter of cold calls' window checks (misses << 32 | checks)
+  unsigned long long* shadow_host;  // its pinned host copy, written once per cold call by S4 (nullable)
   uint2* blist;         // warm: per tile, its keys in the k-th key's window bin ({key, count} x kTileList)
 };
 
@@ -125,9 +128,11 @@ struct SegLayout {
 };
 constexpr int kTileList = 4;  // warm: a tile's distinct keys in the k-th key's window bin kept for S4w
 
+constexpr size_t kSegShadowOffset = 64;  // in the header: the cold calls' 64-bit window-check counter
 static SegLayout seg_layout(int nseg, int64_t ntile) {
   SegLayout L{};
-  size_t o = 256;  // [0, 256): the sticky status word (CHOCO_TOPK_STATUS_OFFSET) of the whole call
+  size_t o = 256;  // [0, 256): the sticky status word (CHOCO_TOPK_STATUS_OFFSET) of the whole call, the
+                   // miss counter (CHOCO_TOPK_FALLBACKS_OFFSET), the shadow counter (kSegShadowOffset)
   L.off_h1 = o;   o += align_up((size_t)nseg * kH * 4, 256);
   L.off_h2 = o;   o += align_up((size_t)nseg * kH * 4, 256);
   L.off_h3 = o;   o += align_up((size_t)nseg * 512 * 4, 256);
@@ -685,7 +690,12 @@ CHOCO_DEV void seg_next_window_v(const uint32_t (&hv)[kWinPer], uint32_t base, u
   if (tid == 0) {
     uint64_t x_lo = (uint64_t)base + ((uint64_t)(nlo ? nlo - 1u : 0u) << shb);
     uint64_t x_hi = (uint64_t)base + ((uint64_t)nhi << shb);
-    const int32_t drift = window_drift(T, old.tprev, old.dprev, old.valid != 0u);
+    // trusted drift: applied only when the previous candidate predicted this T better than
+    // the key it started from (a steady drift; on a stationary, noisy k-th key the
+    // extrapolated noise only widens the misses)
+    const int32_t cand = window_drift(T, old.tprev, old.dprev, old.valid != 0u);
+    const uint32_t trust = drift_trusted(T, old.tprev, old.cand, old.valid != 0u) ? min(old.trust + 1u, 15u) : 0u;
+    const int32_t drift = trust >= kDriftTrust ? cand : 0;
     if (drift != 0) {  // both edges follow the k-th key's steady drift
       const int64_t lo2 = (int64_t)x_lo + drift, hi2 = (int64_t)x_hi + drift;
       x_lo = (uint64_t)(lo2 > 0 ? lo2 : 0);
@@ -697,15 +707,16 @@ CHOCO_DEV void seg_next_window_v(const uint32_t (&hv)[kWinPer], uint32_t base, u
       sh = kWinShMax;
       x_lo = T > (1u << 18) ? (uint64_t)T - (1u << 18) : 0u;
     }
-    *out = seg_win((uint32_t)x_lo, sh, T, old);
+    *out = seg_win((uint32_t)x_lo, sh, T, old, (uint32_t)cand, trust);
   }
 }
 
 // (cold calls)
 // shadow: on a cold call, tile 0 of each segment also checks whether the window the
 // previous call prepared (still in win[s]) would have held this call's T_s, and adds
-// (miss << 32) | 1 to a 64-bit counter in pinned host memory (one system-scope atomic per
-// segment): the host ends a cold run once two calls' worth of checks came without a miss.
+// (miss << 32) | 1 to a 64-bit device counter; S4 copies it to pinned host memory once per
+// call (a system-scope atomic per segment took S3b 5 -> 49 us); the host ends a cold run
+// once two calls' worth of checks came without a miss.
 __global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
     const int64_t* __restrict__ trows, int nseg, uint32_t* __restrict__ hist2, const uint32_t* __restrict__ hist3,
     uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt, const float* __restrict__ cval,
@@ -731,7 +742,7 @@ __global__ __launch_bounds__(kS3Threads) void seg_count_kernel(
     __syncthreads();
     if (tid == 0 && shadow) {
       const bool hit = old.valid && old.lo <= T && (uint64_t)T < (uint64_t)old.lo + ((uint64_t)(kH - 1) << min(old.sh, kWinShMax));
-      __hip_atomic_fetch_add(shadow, (hit ? 0ull : (1ull << 32)) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_fetch_add(shadow, (hit ? 0ull : (1ull << 32)) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     seg_next_window(g2, b1 << 20, 9u, (uint32_t)c.R.k - info[8 * c.s + 1], (uint32_t)c.R.k, T, old, &win[c.s],
                     scratch);
@@ -916,8 +927,12 @@ static_assert(kS4Per * kS4Threads == kSegMaxTiles, "S4 tile-count geometry");
 __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
     const int64_t* __restrict__ trows, const uint32_t* __restrict__ info, const uint32_t* __restrict__ tilecnt,
     const uint32_t* __restrict__ tcount, uint32_t* __restrict__ hist3, const float* __restrict__ cval,
-    const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx) {
+    const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
+    unsigned long long* __restrict__ shadow, unsigned long long* __restrict__ shadow_host) {
   __shared__ uint32_t scratch[40];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && shadow_host)  // S3b's checks of this call are complete
+    __hip_atomic_store(shadow_host, __hip_atomic_load(shadow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const TileCtx c = tile_ctx_rows(trows, blockIdx.x);
   if (c.R.ntile == 1) return;  // selected in S2
   const int tid = threadIdx.x;
@@ -1105,7 +1120,7 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_w_kernel(
       seg_next_window_v(hv, lo, sh, 0u, (uint32_t)c.R.k, T, old, &win[c.s], scratch);
       __syncthreads();
     } else if (tid == 0) {
-      win[c.s] = SegWin{0u, kWinShMax, 1u, 0u, 0u, 0u, {0u, 0u}};
+      win[c.s] = SegWin{0u, kWinShMax, 1u, 0u, 0u, 0u, 0u, 0u};
     }
     for (int i = tid; i < kH; i += kS4Threads) g2[i] = 0u;
     return;
@@ -1198,7 +1213,7 @@ static uint64_t seg_shadow_read(const SegState& S) {
 }
 static std::mutex g_seg_mu;
 static std::unordered_map<const void*, SegState> g_seg;
-static bool seg_claim_warm(const void* ws, uint32_t nmulti, uint32_t** flag_dev, unsigned long long** shadow_dev) {
+static bool seg_claim_warm(const void* ws, uint32_t nmulti, uint32_t** flag_dev, unsigned long long** shadow_host) {
   std::lock_guard<std::mutex> g(g_seg_mu);
   SegState& S = g_seg[ws];
   if (!S.flag) {
@@ -1211,7 +1226,7 @@ static bool seg_claim_warm(const void* ws, uint32_t nmulti, uint32_t** flag_dev,
     }
   }
   *flag_dev = S.flag_dev;  // (null: no backoff, warm as before)
-  *shadow_dev = S.flag_dev ? reinterpret_cast<unsigned long long*>(S.flag_dev + 2) : nullptr;
+  *shadow_host = S.flag_dev ? reinterpret_cast<unsigned long long*>(S.flag_dev + 2) : nullptr;
   const bool first = S.calls++ == 0;
   if (S.flag && __atomic_load_n(S.flag, __ATOMIC_ACQUIRE) != 0u) {
     __atomic_store_n(S.flag, 0u, __ATOMIC_RELEASE);
@@ -1313,7 +1328,7 @@ static int launch_batched(const float* x, const float* xh, const int64_t* plan_d
   CHOCO_LAUNCHED("seg_count_kernel");
   profile_begin("topk_seg_emit", st);
   CHOCO_KLAUNCH(seg_emit_kernel, dim3(ntile), dim3(kS4Threads), 0, st, trows, W.info, W.tilecnt, W.tcount,
-                W.hist3, W.cval, W.cidx, out_val, out_idx);
+                W.hist3, W.cval, W.cidx, out_val, out_idx, W.shadow, W.shadow_host);
   profile_end("topk_seg_emit", st);
   CHOCO_LAUNCHED("seg_emit_kernel");
   return CHOCO_OK;
@@ -1352,11 +1367,12 @@ static int segmented(const float* x, const float* xhat, const int64_t* plan_dev,
             reinterpret_cast<uint32_t*>(base + L.off_info), reinterpret_cast<uint32_t*>(base + L.off_cnt),
             reinterpret_cast<uint32_t*>(base + L.off_out), reinterpret_cast<float*>(base + L.off_cval),
             reinterpret_cast<uint32_t*>(base + L.off_cidx), reinterpret_cast<SegWin*>(base + L.off_win),
-            reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_FALLBACKS_OFFSET), nullptr, nullptr,
+            reinterpret_cast<uint32_t*>(base + CHOCO_TOPK_FALLBACKS_OFFSET), nullptr,
+            reinterpret_cast<unsigned long long*>(base + kSegShadowOffset), nullptr,
             reinterpret_cast<uint2*>(base + L.off_blist)};
     uint32_t nmulti = 0;  // segments with windows (multi-tile, batched): the shadow checks per cold call
     for (int s = 0; s < nseg; ++s) nmulti += plan_host[(int64_t)kRow * s + 5] > 1 ? 1u : 0u;
-    const bool warm = seg_claim_warm(base + L.off_win, nmulti, &W.miss_flag, &W.shadow);
+    const bool warm = seg_claim_warm(base + L.off_win, nmulti, &W.miss_flag, &W.shadow_host);
     int rc;
     if (gs.mem)
       rc = launch_batched<true, true>(x, xhat, plan_dev, plan_host, nseg, out_val, out_idx, W, warm, st, gs);
