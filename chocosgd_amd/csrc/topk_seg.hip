@@ -1198,8 +1198,8 @@ static int64_t plan_batched(const int64_t* plan_host) { return plan_host[7]; }
 // A cold run ends early when the windows the cold calls prepare would have held their
 // successors' k-th keys: S3b of every cold call checks, per multi-tile segment, the window
 // the previous call left (drift-aware, window_drift) against its exact T and counts
-// (misses << 32 | checks) in the same pinned page; two cold calls' worth of checks with no
-// miss end the run (the drift that caused the miss is followed now).
+// (misses << 32 | checks) in the same pinned page; one cold call's worth of checks with no
+// miss ends the run (the drift that caused the miss is followed now).
 struct SegState {
   uint64_t calls = 0;
   uint32_t cold_left = 0, backoff = 0;
@@ -1207,7 +1207,7 @@ struct SegState {
   uint32_t* flag_dev = nullptr;
   uint32_t last_checks = 0, last_misses = 0, clean = 0;
 };
-constexpr uint32_t kSegShadowExit = 2;
+constexpr uint32_t kSegShadowExit = 1;  // (2: warm share 0.90 against 0.967, profiles/r06_ab_summary.txt item 10)
 static uint64_t seg_shadow_read(const SegState& S) {
   return S.flag ? __atomic_load_n(reinterpret_cast<uint64_t*>(S.flag + 2), __ATOMIC_ACQUIRE) : 0ull;
 }
