@@ -120,10 +120,16 @@ def parse(argv=None):
 
 
 def traffic_key(args):
-    """The workload key of profiles/pmc_traffic.json (tools/pmc_traffic.py's 3rd argument)."""
+    """The workload key of profiles/pmc_traffic.json (tools/pmc_traffic.py's 3rd argument;
+    scripts/gpu_measure.sh derives it from the same flags)."""
+    key = args.workload
     if args.ring3_loopback:
-        return f"{args.workload}_ring3"
-    return args.workload
+        key += "_ring3"
+    if getattr(args, "defer_receive", False):
+        key += "_deferred"
+    if args.workload.startswith("step_") and getattr(args, "grad_lr", 0.1) <= 0:
+        key += "_nograd"
+    return key
 
 
 def _free_port():

@@ -60,7 +60,10 @@ static_assert(kTileQuant % kChunk == 0, "chunk geometry");
 constexpr int kMaybeCap = 65536;        // side-list capacity per tile (maybe keys)
 constexpr int kNBucket = 256;           // 255 "maybe" buckets + 1 "sure"
 constexpr int kNMaybe = kNBucket - 1;
-constexpr int kNRep = 16;               // replicas of the global bucket totals
+// Replicas of the global bucket totals (K2's tile ends add to replica b & 3; every K34
+// workgroup reads all of them in its first round trip).  Same-box A/B, round 6
+// (profiles/r06_ab_summary.txt item 11): 16 replicas K34 11.48-11.66 us, 4 replicas 11.07-11.38 us.
+constexpr int kNRep = 4;
 constexpr int kMCap = 16384;            // max keys of bucket j* selected in LDS
 constexpr size_t kWideBytes = 4 * (64 + 3 * 2048);  // sizeof(WideCtrl), rounded to 256 below
 constexpr int kK4Threads = 1024;
