@@ -8,7 +8,11 @@ of the sparse accumulate (4-B gathers; the correction is uncalibrated there, so
 its raw count is kept).  Writes profiles/pmc_traffic.json
 {"<profile name>:<workload>:<n>": {...}}, the keys bench.py reads.
 
-    python tools/pmc_traffic.py <fetch_dir> <write_dir> <workload> <n>
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <workload> <n> [--tail M]
+
+--tail M: the median over each kernel's LAST M dispatches only (the step workloads'
+200 burn-in steps run in the same process, and their early calls -- the delta growing
+from 0, exact fallbacks -- are not the steady state the bench line times).
 """
 import collections
 import csv
@@ -43,29 +47,40 @@ KERNELS = {
 }
 
 
-def per_dispatch(root, counter, kernel):
+def per_dispatch(root, counter, kernel, tail=0):
+    """The counter's per-dispatch totals (sorted), of the last `tail` dispatches if tail > 0."""
     vals = collections.defaultdict(float)
     for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for r in csv.DictReader(f):
                 if r["Counter_Name"] == counter and kernel in r.get("Kernel_Name", ""):
-                    vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
-    return sorted(vals.values())
+                    vals[int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+    ids = sorted(vals)
+    if tail > 0:
+        ids = ids[-tail:]
+    return sorted(vals[i] for i in ids), len(vals)
 
 
 def main():
-    fdir, wdir, workload, n = sys.argv[1:5]
+    argv = sys.argv[1:]
+    tail = 0
+    if "--tail" in argv:
+        i = argv.index("--tail")
+        tail = int(argv[i + 1])
+        del argv[i:i + 2]
+    fdir, wdir, workload, n = argv[:4]
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
     data = json.load(open(path)) if os.path.exists(path) else {}
     for name, (kernel, corr) in KERNELS.items():
-        f = per_dispatch(fdir, "FETCH_SIZE", kernel)
-        w = per_dispatch(wdir, "WRITE_SIZE", kernel)
+        f, nf = per_dispatch(fdir, "FETCH_SIZE", kernel, tail)
+        w, nw = per_dispatch(wdir, "WRITE_SIZE", kernel, tail)
         if not f or not w:
             continue
         fmed, wmed = f[len(f) // 2], w[len(w) // 2]
         out = {"fetch_bytes": corr * fmed * 1024, "write_bytes": wmed * 1024}
         out["bytes"] = out["fetch_bytes"] + out["write_bytes"]
-        out["note"] = (f"median over {len(f)}/{len(w)} dispatches; FETCH_SIZE x{corr:g} "
+        over = f"the last {len(f)}/{len(w)} of {nf}/{nw}" if tail else f"{len(f)}/{len(w)}"
+        out["note"] = (f"median over {over} dispatches; FETCH_SIZE x{corr:g} "
                        f"({'gfx950 streaming-read correction' if corr != 1 else 'scattered: raw'}) + WRITE_SIZE, "
                        "KB units x1024")
         key = f"{name}:{workload}:{n}"
