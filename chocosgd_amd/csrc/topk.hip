@@ -23,7 +23,7 @@
 //                     the candidate buffer.  Tile end: the "maybe" keys
 //                     (key < s_hi) are bucket-counted and counting-sorted into a
 //                     per-tile side list; per-tile bucket suffix counts go to a
-//                     [tile][256] table and to 16 replicated global totals.
+//                     [tile][256] table and to kNRep replicated global totals.
 //   K34 topk_finish : one workgroup per tile.  Each finds the bucket j* of the
 //                     k-th key from the totals, copies every tile's bucket-j*
 //                     keys (a few thousand) into LDS, radix-selects T and the tie
@@ -31,13 +31,14 @@
 //                     compacts its own tile's candidates into the final
 //                     ascending-index output.
 //   If the sample's guess was off (too few candidates, T in the "sure" range,
-//   bucket j* larger than LDS, or a side list overflowed), K34's workgroup 0
-//   runs an exact single-workgroup radix select over the full input instead
-//   (correct, slow, data-dependent only).
+//   bucket j* larger than LDS, or a side list overflowed), every K34 workgroup
+//   joins an exact radix select over the full input instead (wide.h: a ticketed
+//   queue of per-tile passes; correct, ~5 reads of the input).
 // Small n (<= kSmallN) uses an exact radix select (block_topk_exact) in one
 // workgroup; per-tensor (segmented) calls are batched in topk_seg.hip.
 #include "choco_common.h"
 #include "select.h"
+#include "wide.h"
 
 #include <math.h>
 #include <stddef.h>
@@ -65,7 +66,6 @@ constexpr int kNMaybe = kNBucket - 1;
 // (profiles/r06_ab_summary.txt item 11): 16 replicas K34 11.48-11.66 us, 4 replicas 11.07-11.38 us.
 constexpr int kNRep = 4;
 constexpr int kMCap = 16384;            // max keys of bucket j* selected in LDS
-constexpr size_t kWideBytes = 4 * (64 + 3 * 2048);  // sizeof(WideCtrl), rounded to 256 below
 constexpr int kK4Threads = 1024;
 constexpr int64_t kSmallN = 65536;
 constexpr int kExactThreads = 1024;
@@ -139,7 +139,6 @@ static_assert(offsetof(TopkCtrl, status) == CHOCO_TOPK_STATUS_OFFSET, "status wo
 static_assert(offsetof(TopkCtrl, fallbacks) == CHOCO_TOPK_FALLBACKS_OFFSET, "fallback counter at the documented offset");
 static_assert(offsetof(TopkCtrl, cold_left) == CHOCO_TOPK_COLD_LEFT_OFFSET, "cold-run word at the documented offset");
 static_assert(offsetof(TopkCtrl, k2_samples) == CHOCO_TOPK_K2_SAMPLES_OFFSET, "K2 sample counter at the documented offset");
-constexpr uint32_t kStatusPollTimeout = 1u;    // a bounded wait of the exact fallback gave up: output invalid
 constexpr uint32_t kNoCandKey = 0x7F800000u;   // window that admits only inf / NaN keys (invalid bounds)
 
 // The self-message part of CHOCOSparsificationCompressor.uncompress (parallel_choco_v.py:
@@ -162,7 +161,7 @@ CHOCO_DEV void fold_apply(const Fold& f, int64_t i, float q) {
 struct TopkLayout {
   int64_t n;
   uint32_t tile, nb, side_cap;
-  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, off_wide, off_gcnt, off_tinfo, total;
+  size_t off_ctrl, off_cum, off_cntw, off_side, off_cval, off_cidx, off_wide, off_gcnt, off_thist, off_tinfo, total;
 };
 
 // Tile = ceil(n / kK2Target) rounded up to 32768 elements: one tile per CU, all
@@ -190,6 +189,7 @@ static TopkLayout topk_layout(int64_t n) {
   L.off_cval = o;  o += align_up((size_t)L.nb * tile * 4, 256);   // candidate values, chunk slot ranges
   L.off_cidx = o;  o += align_up((size_t)L.nb * tile * 4, 256);   // ... and indices
   L.off_gcnt = o;  o += align_up((size_t)L.nb * 8, 256);              // ... its per-tile (#>T, #==T)
+  L.off_thist = o; o += align_up((size_t)L.nb * 512 * 4, 256);        // ... and per-tile last-digit histograms
   L.off_tinfo = o; o += align_up((size_t)L.nb * 4, 256);              // per tile: candidates (compact) or ~0 (spilled)
   L.total = o;
   return L;
@@ -306,29 +306,6 @@ CHOCO_DEV void load_sample(const float* __restrict__ x, const float* __restrict_
     if (XH) h[j] = ld_buf4<false>(buf_rsrc(xh + run0, 1024u), 16u * (uint32_t)lane);
     if (GS) m[j] = ld_buf4<false>(buf_rsrc(mem + run0, 1024u), 16u * (uint32_t)lane);
   }
-}
-
-// Over hist[2048] in LDS (ascending key order), the bins holding the r0-th and
-// r1-th largest entries and the ranks inside them -> out[0..1], out[2..3] (a
-// rank of 0 is skipped).  Every thread of the kK2Threads workgroup calls it.
-CHOCO_DEV void block_find_two(const uint32_t* hist, uint32_t r0, uint32_t r1, uint32_t* scratch, uint32_t* out) {
-  static_assert(kK2Threads * 2 == 2048, "two bins per thread");
-  const int tid = threadIdx.x;
-  const uint32_t h0 = hist[2 * tid], h1 = hist[2 * tid + 1];
-  const uint32_t local = h0 + h1;
-  uint32_t total;
-  const uint32_t pre = block_excl_scan(local, scratch, &total);
-  const uint32_t above = total - pre - local;  // entries in bins above my two
-  const uint32_t rs[2] = {r0, r1};
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const uint32_t r = rs[q];
-    if (r != 0u && above < r && r <= above + local) {
-      if (r <= above + h1) { out[2 * q] = 2 * tid + 1; out[2 * q + 1] = r - above; }
-      else { out[2 * q] = 2 * tid; out[2 * q + 1] = r - above - h1; }
-    }
-  }
-  __syncthreads();
 }
 
 // ----------------------------------------------------------------------------
@@ -1287,134 +1264,6 @@ CHOCO_DEV uint32_t batch_ranks(const bool (&f)[kEmitRows], uint32_t (&rk)[kEmitR
 }
 static_assert(kEmitRows * (kK4Threads / 64) == 128, "batch_ranks: wave 0 scans 2 counts per lane");
 
-// Hand-offs between workgroups (bounds, tile tables, side lists) use the
-// fence-free form of MI355X_MICROARCH.md "Valid forms": every handed-off word is
-// stored write-through (relaxed agent-scope atomic store = sc1) and read with
-// sc1 loads; each storing wave drains (vmcnt(0)) before a workgroup barrier,
-// behind which one lane adds to the counter; the consumer polls that counter.
-// No release fence: a buffer_wbl2 writes back the whole XCD L2 and cost
-// 10-30 us per tile in the middle of everyone else's stream (measured).
-CHOCO_DEV void st_sc1(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-CHOCO_DEV uint32_t ld_sc1(const uint32_t* p) {
-  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-
-// every wave's stores drained, the workgroup joined, one lane adds
-CHOCO_DEV void publish_add(uint32_t* counter) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// ----------------------------------------------------------------------------
-// Wide exact fallback (K34, when the sample's bucket guess failed: bucket j* larger
-// than LDS -- tie clusters, exact zeros where x = x_hat --, too few candidates, or a
-// side list overflow).  Instead of one workgroup radix-selecting the whole input,
-// every K34 workgroup takes TICKETS from a work queue of 5 * nb items:
-//   phases 0-2: histogram of one tile's keys for radix digit 0/1/2 (bits 30..20,
-//               19..9, 8..0; only keys matching the digits found so far),
-//   phase 3   : one tile's (#key > T, #key == T),
-//   phase 4   : one tile's ordered emission at its offset (counts of earlier tiles).
-// An item of phase p waits until every item of phase p-1 is done; those are held by
-// workgroups that drew earlier tickets and are therefore running, so the queue is
-// deadlock-free whatever number of workgroups is resident.  The digits are
-// re-derived from the global histograms by whoever needs them (a 2048-bin scan).
-// The last workgroup to leave resets the queue and zeroes the histograms.
-// Five streaming passes over the input by all CUs instead of ~4 by one CU.
-// ----------------------------------------------------------------------------
-struct WideCtrl {
-  uint32_t ticket, exitc, pad0[6];
-  uint32_t done[8];  // items completed per phase
-  uint32_t pad1[48];
-  uint32_t hist[3][2048];
-};
-static_assert(sizeof(WideCtrl) == kWideBytes && kWideBytes % 256 == 0, "topk_layout reserves WideCtrl");
-constexpr int kWidePhases = 5;
-constexpr int kWideU = 4;  // float4 loads per stream per thread in flight
-
-// Queue hand-offs made by ALL lanes of wave 0 (no lane-divergent region inside the
-// ticket loop: with `if (threadIdx.x == 0)` around the atomic and the poll, the
-// compiler split the loop so that wave 0 executed extra barriers -- measured hang).
-CHOCO_DEV uint32_t wave0_fetch_add(uint32_t* p, uint32_t v) {
-  const uint32_t r = __hip_atomic_fetch_add(p, lane_id() == 0 ? v : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return __builtin_amdgcn_readfirstlane(r);
-}
-// Bounded: false when the budget ran out (a stuck producer must not hang the GPU;
-// the caller flags the call's output invalid in the workspace status word).
-#ifndef CHOCO_POLL_BUDGET  // diagnostic builds only (tools/build_variants.py "poll1")
-#define CHOCO_POLL_BUDGET (1u << 22)
-#endif
-CHOCO_DEV bool wave0_poll_ge(const uint32_t* p, uint32_t want) {
-  for (uint32_t it = 0; it < (uint32_t)CHOCO_POLL_BUDGET; ++it) {
-    if (__builtin_amdgcn_readfirstlane(ld_sc1(p)) >= want) return true;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  return __builtin_amdgcn_readfirstlane(ld_sc1(p)) >= want;
-}
-
-CHOCO_DEV constexpr int wide_shift(int r) { return r == 0 ? 20 : (r == 1 ? 9 : 0); }
-CHOCO_DEV constexpr uint32_t wide_mask(int r) { return r == 2 ? 511u : 2047u; }
-
-// Digits 0 .. upto-1 from the global histograms -> (prefix, maskhi, krem).
-CHOCO_DEV void wide_digits(WideCtrl* W, int upto, uint32_t k, ExactSmem& es, uint32_t& prefix, uint32_t& maskhi,
-                           uint32_t& krem) {
-  prefix = 0u;
-  maskhi = 0u;
-  krem = k;
-  for (int r = 0; r < upto; ++r) {
-    for (int i = threadIdx.x; i < 2048; i += blockDim.x) es.hist[i] = ld_sc1(&W->hist[r][i]);
-    __syncthreads();
-    block_find_two(es.hist, krem, 0u, es.scratch, es.bc);
-    const uint32_t bin = es.bc[0];
-    krem = es.bc[1];
-    prefix |= bin << wide_shift(r);
-    maskhi |= wide_mask(r) << wide_shift(r);
-    __syncthreads();
-  }
-}
-
-// The keys (and values) of tile [lo, hi) row by row (a row = 4 consecutive elements
-// per thread, kK4Threads * 4 per row, kWideU rows' loads in flight):
-// fn(i0, n_in, keys[4], vals[4]) for every row, by every thread (block-uniform).
-template <int MODE, bool XH, class F>
-CHOCO_DEV void wide_tile(const Src<MODE, XH>& src, int64_t lo, int64_t hi, F&& fn) {
-  const uint32_t len = (uint32_t)(hi - lo);
-  const __amdgpu_buffer_rsrc_t rx = buf_rsrc(src.x + lo, len * 4u);
-  const __amdgpu_buffer_rsrc_t rh = buf_rsrc((XH ? src.xh : src.x) + lo, len * 4u);
-  constexpr uint32_t kStep = kK4Threads * 4u;
-  for (uint32_t b0 = 0; b0 < len; b0 += kStep * kWideU) {
-    float4 v[kWideU], h[kWideU];
-#pragma unroll
-    for (int u = 0; u < kWideU; ++u) {
-      const uint32_t off = (b0 + (uint32_t)u * kStep + 4u * threadIdx.x) * 4u;
-      if (MODE == kData) {
-        v[u] = ld_buf4<true>(rx, off);
-        if (XH) h[u] = ld_buf4<true>(rh, off);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kWideU; ++u) {
-      if (b0 + (uint32_t)u * kStep >= len) break;  // block-uniform
-      const uint32_t e0 = b0 + (uint32_t)u * kStep + 4u * threadIdx.x;
-      float vv[4] = {0.f, 0.f, 0.f, 0.f};
-      uint32_t kk[4];
-      if (MODE == kData) {
-        const float4 d = XH ? sub4(v[u], h[u]) : v[u];
-        vv[0] = d.x; vv[1] = d.y; vv[2] = d.z; vv[3] = d.w;
-      }
-      const int nin = e0 >= len ? 0 : (int)min(4u, len - e0);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int64_t i = lo + e0 + c;
-        if (MODE == kHash && c < nin) vv[c] = src.val(i);
-        kk[c] = c < nin ? src.key_of(i, vv[c]) : 0u;
-      }
-      fn(lo + (int64_t)e0, nin, kk, vv);
-    }
-  }
-}
-
 // The next call's window after a fallback: keys at count levels k (1 +- 1/8) from the
 // complete coarse histogram hist[0] (key >> 20 of every key), bin-rounded outward.
 CHOCO_DEV void fallback_window(WideCtrl* W, int64_t n, int64_t k, ExactSmem& es, TopkBounds* next) {
@@ -1440,130 +1289,25 @@ CHOCO_DEV void fallback_window(WideCtrl* W, int64_t n, int64_t k, ExactSmem& es,
   __syncthreads();
 }
 
+// The exact select over the whole input, shared by every K34 workgroup (wide.h), when
+// the sample's guess failed; workgroup 0's item for tile 0 also writes the next window.
 template <int MODE, bool XH>
 CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uint32_t tile, uint32_t nb, const Fold& fold,
-                             float scale, WideCtrl* W, uint32_t* __restrict__ gcnt, float* __restrict__ out_val,
+                             float scale, WideCtrl* W, uint32_t* __restrict__ gcnt, uint32_t* __restrict__ thist,
+                             float* __restrict__ out_val,
                              int32_t* __restrict__ out_idx, int64_t idx_base, ExactSmem& es, uint32_t* s_tk,
                              uint32_t* __restrict__ status, uint32_t* __restrict__ host_status, TopkBounds* next) {
-  const int tid = threadIdx.x;
-  const bool w0 = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;  // wave-uniform
-  for (;;) {
-    if (w0) *s_tk = wave0_fetch_add(&W->ticket, 1u);  // every lane of wave 0 writes the same value
-    __syncthreads();
-    const uint32_t tk = __builtin_amdgcn_readfirstlane(*s_tk);
-    __syncthreads();
-    if (tk >= (uint32_t)kWidePhases * nb) break;  // workgroup-uniform
-    const int phase = (int)(tk / nb);
-    const uint32_t t = tk % nb;
-    if (phase > 0) {
-      if (w0 && !wave0_poll_ge(&W->done[phase - 1], nb) && lane_id() == 0) {
-        atomicOr(status, kStatusPollTimeout);
-        // the pinned host mirror: the host sees it at its next call, no copy, no sync
-        if (host_status) __hip_atomic_store(host_status, kStatusPollTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      __syncthreads();
-    }
-    const int64_t lo = (int64_t)t * tile, hi = min(lo + (int64_t)tile, n);
-    uint32_t prefix, maskhi, krem;
-    wide_digits(W, phase < 3 ? phase : 3, (uint32_t)k, es, prefix, maskhi, krem);
-    if (phase < 3) {
-      const int sh = wide_shift(phase);
-      const uint32_t dm = wide_mask(phase);
-      for (int i = tid; i < 2048; i += kK4Threads) es.hist[i] = 0u;
-      __syncthreads();
-      const int lane = lane_id();
-      wide_tile(src, lo, hi, [&](int64_t, int nin, const uint32_t (&kk)[4], const float (&)[4]) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          // tie-heavy inputs put most lanes in one bin: the lanes of the wave's first
-          // bin add with one atomic, the rest one by one
-          const bool on = c < nin && (kk[c] & maskhi) == prefix;
-          const uint32_t bin = (kk[c] >> sh) & dm;
-          const uint64_t live = ballot(on);
-          if (live == 0ull) continue;  // wave-uniform
-          const int first = __builtin_ctzll(live);
-          const uint32_t b0 = __builtin_amdgcn_readlane(bin, first);
-          const uint64_t same = ballot(on && bin == b0);
-          if (lane == first) atomicAdd(&es.hist[b0], (uint32_t)__popcll(same));
-          if (on && bin != b0) atomicAdd(&es.hist[bin], 1u);
-        }
+  wide_select<kK4Threads, 4>(  // 4 float4 rows per stream in flight
+
+      src, n, k, tile, nb, W, gcnt, thist, es, s_tk, status, host_status,
+      [&](uint32_t) {
+        if (next != nullptr) fallback_window(W, n, k, es, next);
+      },
+      [&](uint32_t pos, int64_t i, float v) {
+        out_val[pos] = v * scale;
+        out_idx[pos] = (int32_t)(i + idx_base);
+        if (fold.on()) fold_apply(fold, i, v * scale);
       });
-      __syncthreads();
-      for (int i = tid; i < 2048; i += kK4Threads)
-        if (es.hist[i]) __hip_atomic_fetch_add(&W->hist[phase][i], es.hist[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      const uint32_t T = prefix;  // all digits known: T = the k-th largest key, krem = ties to take
-      const uint32_t r = krem;
-      if (phase == 3 && t == 0 && next != nullptr) fallback_window(W, n, k, es, next);
-      if (phase == 3) {
-        uint32_t gt = 0, eq = 0;
-        wide_tile(src, lo, hi, [&](int64_t, int nin, const uint32_t (&kk)[4], const float (&)[4]) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            gt += (c < nin && kk[c] > T) ? 1u : 0u;
-            eq += (c < nin && kk[c] == T) ? 1u : 0u;
-          }
-        });
-        uint32_t gtot, etot, gp, ep;
-        block_excl_scan2(gt, eq, es.scratch, &gp, &ep, &gtot, &etot);
-        if (w0) { st_sc1(&gcnt[2 * t], gtot); st_sc1(&gcnt[2 * t + 1], etot); }  // same value from every lane
-      } else {
-        // this tile's output offset and tie start: counts of the tiles before it
-        const bool mine = (uint32_t)tid < nb;
-        const uint32_t gv = mine && (uint32_t)tid < t ? ld_sc1(&gcnt[2 * tid]) : 0u;
-        const uint32_t ev = mine && (uint32_t)tid < t ? ld_sc1(&gcnt[2 * tid + 1]) : 0u;
-        uint32_t gp, ep, gtot, etot;
-        block_excl_scan2(gv, ev, es.scratch, &gp, &ep, &gtot, &etot);
-        const uint32_t taken = min(r, etot);  // ties taken by the earlier tiles
-        uint32_t out = gtot + taken, tie_run = etot;
-        // ordered compaction, row by row: ties by global rank (lowest index first)
-        wide_tile(src, lo, hi, [&](int64_t i0, int nin, const uint32_t (&kk)[4], const float (&vv)[4]) {
-          uint32_t neq = 0;
-#pragma unroll
-          for (int c = 0; c < 4; ++c) neq += (c < nin && kk[c] == T) ? 1u : 0u;
-          uint32_t tp, tt;
-          tp = block_excl_scan(neq, es.scratch, &tt);
-          bool sel[4];
-          uint32_t ns = 0, q = tie_run + tp;
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const bool in = c < nin;
-            const bool eqc = in && kk[c] == T;
-            sel[c] = (in && kk[c] > T) || (eqc && q < r);
-            q += eqc ? 1u : 0u;
-            ns += sel[c] ? 1u : 0u;
-          }
-          uint32_t st;
-          uint32_t pos = out + block_excl_scan(ns, es.scratch, &st);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            if (sel[c]) {
-              out_val[pos] = vv[c] * scale;
-              out_idx[pos] = (int32_t)(i0 + c + idx_base);
-              if (fold.on()) fold_apply(fold, i0 + c, vv[c] * scale);
-              ++pos;
-            }
-          }
-          out += st;
-          tie_run += tt;
-        });
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (w0) wave0_fetch_add(&W->done[phase], 1u);
-  }
-  // the last workgroup out resets the queue for the next call
-  if (w0) {
-    const uint32_t e = wave0_fetch_add(&W->exitc, 1u);
-    *s_tk = e == nb - 1 ? 1u : 0u;
-  }
-  __syncthreads();
-  if (*s_tk) {
-    for (int i = tid; i < 3 * 2048; i += kK4Threads) st_sc1(&W->hist[0][0] + i, 0u);
-    if (tid < 8) st_sc1(&W->done[tid], 0u);
-    if (tid == 0) { st_sc1(&W->ticket, 0u); st_sc1(&W->exitc, 0u); }
-  }
 }
 
 // ----------------------------------------------------------------------------
@@ -1663,8 +1407,8 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     uint32_t side_cap, uint64_t seed, float scale, TopkCtrl* __restrict__ ctrl, const uint32_t* __restrict__ cum_tab,
     const uint32_t* __restrict__ cntw, const uint32_t* __restrict__ side, const float* __restrict__ cval,
     const uint32_t* __restrict__ cidx, float* __restrict__ out_val, int32_t* __restrict__ out_idx,
-    int64_t idx_base, WideCtrl* __restrict__ wide, uint32_t* __restrict__ gcnt, uint32_t par,
-    uint32_t* __restrict__ status, uint32_t* __restrict__ host_status, const uint32_t* __restrict__ tinfo,
+    int64_t idx_base, WideCtrl* __restrict__ wide, uint32_t* __restrict__ gcnt, uint32_t* __restrict__ thist,
+    uint32_t par, uint32_t* __restrict__ status, uint32_t* __restrict__ host_status, const uint32_t* __restrict__ tinfo,
     Fold fold, uint32_t* __restrict__ cold_host) {
   __shared__ FinSmem fs;
   __shared__ ExactSmem es;
@@ -1744,7 +1488,7 @@ __global__ __launch_bounds__(kK4Threads) void topk_finish_kernel(
     // the sample's guess was off: the exact radix select over the whole input, shared
     // by every workgroup through the ticketed queue (wide_fallback)
     Src<MODE, XH> src{x, xh, seed};
-    wide_fallback(src, n, k, tile, nb, fold, scale, wide, gcnt, out_val, out_idx, idx_base, es, &s_tk, status,
+    wide_fallback(src, n, k, tile, nb, fold, scale, wide, gcnt, thist, out_val, out_idx, idx_base, es, &s_tk, status,
                   host_status, MODE == kData ? &ctrl->bounds[par ^ 1u] : nullptr);
   } else {
     // ---- thread t <-> tile t: bucket-j* key count and side-list offset
@@ -2118,8 +1862,9 @@ static int launch_topk(const float* x, const float* xh, int64_t n, int64_t k, ui
   profile_begin("topk_finish", st);
   CHOCO_KLAUNCH((topk_finish_kernel<MODE, XH>), dim3(L.nb), dim3(kK4Threads), 0, st, x, xh, n, k, L.tile, L.nb,
                 L.side_cap, seed, scale, ctrl, cum, cntw, side, cval, cidx, out_val, out_idx, idx_base,
-                reinterpret_cast<WideCtrl*>(base + L.off_wide), reinterpret_cast<uint32_t*>(base + L.off_gcnt), par,
-                status.dev, status.host, reinterpret_cast<const uint32_t*>(base + L.off_tinfo), fold, cold_host);
+                reinterpret_cast<WideCtrl*>(base + L.off_wide), reinterpret_cast<uint32_t*>(base + L.off_gcnt),
+                reinterpret_cast<uint32_t*>(base + L.off_thist), par, status.dev, status.host,
+                reinterpret_cast<const uint32_t*>(base + L.off_tinfo), fold, cold_host);
   profile_end("topk_finish", st);
   CHOCO_LAUNCHED("topk_finish_kernel");
   return CHOCO_OK;

@@ -594,8 +594,8 @@ def _check_seg(x, plan, lens, ratio, xh=None):
 def test_topk_segmented_warm_sequence(layout):
     """Warm segmented calls (one read: each segment's window from the previous call):
     drifting data, then windows that are badly wrong -- x100, all zeros (k_s-th key 0),
-    tie-heavy, x1e-3, back to random -- every call exact (misses take the exact
-    one-workgroup fallback in S4 and re-centre the window)."""
+    tie-heavy, x1e-3, back to random -- every call exact (a missed segment is selected
+    exactly by its tile workgroups together in S4w, which re-centres its window)."""
     from chocosgd_amd import codec
     lens = ([16383, 16384, 16385, 1, 3, 700_001, 32768, 2_500_007] if layout == "edges"
             else golden_json("layouts.json")[layout])
@@ -614,9 +614,10 @@ def test_topk_segmented_warm_sequence(layout):
 def test_topk_segmented_warm_drained_delta():
     """The drain on the segmented path (ResNet-50's layout): the selected entries of every
     call are zeroed before the next.  Every call exact; the first call whose windows miss
-    (S4's exact one-workgroup select) raises the miss flag, and the host then takes the
-    cold sequence (S1 + S2) for a run of calls: no later window misses (each call here is
-    synchronised, so the flag is seen at the very next call)."""
+    (S4w's shared exact select) raises the miss flag, an isolated miss stays warm, and the
+    second one within kSegMissGap calls sends the host to the cold sequence (S1 + S2) for a
+    run of calls: no later window misses (each call here is synchronised, so each flag is
+    seen at the very next call)."""
     from chocosgd_amd import codec
     lens = golden_json("layouts.json")["resnet50_imagenet"]
     n = sum(lens)
@@ -628,7 +629,67 @@ def test_topk_segmented_warm_drained_delta():
         vals, idx = _check_seg(d, plan, lens, ratio)
         d[idx.long()] = 0.0
         counts.append(codec.topk_fallback_count(plan=plan))
-    assert counts[-1] == counts[1], counts
+    assert counts[-1] == counts[2], counts
+
+
+def test_topk_segmented_warm_miss_shared_select_max_segment():
+    """A missed window in the largest batched segment (1024 tiles, kSegBatchMax elements):
+    its 1024 tile workgroups select it together in S4w (wide.h, the segment's own queue;
+    phase 4's offsets sum up to 1023 earlier tiles over 256 threads) -- T far above the
+    window (x100), far below it (x1e-3), tie clusters (the kept-key lists overflow), all
+    exact, each queue reset for the next miss."""
+    from chocosgd_amd import codec
+    lens = [16384 * 1024, 16385, 5]
+    n = sum(lens)
+    ratio = 0.99
+    plan = codec.SegmentPlan(lens, ratio, torch.device(DEV))
+    base = randn(n, 570)
+    g = torch.Generator(device=DEV).manual_seed(571)
+    ties = torch.round(torch.randn(n, generator=g, device=DEV) * 8) / 8
+    misses = []
+    # (each call is synchronised here: an isolated miss stays warm, a second one within 32
+    # calls starts a cold run that ends after one call whose prepared window would have held)
+    for x in (base, base, base * 100, base * 100, base * 100, base * 1e-3, base * 1e-3, base * 1e-3, ties, ties,
+              base):
+        _check_seg(x, plan, lens, ratio)
+        misses.append(codec.topk_fallback_count(plan=plan))
+    assert misses[-1] > misses[1], misses  # the shared select ran
+    codec.check_topk_status(wait=True)
+
+
+def test_topk_segmented_gossip_warm_miss():
+    """The consensus step fused into W2 and then a missed window (the delta x100 in one
+    warm step): S4w's shared select reads x_new as W2 left it; x and the selection exact."""
+    from chocosgd_amd import codec
+    lens = golden_json("layouts.json")["resnet50_imagenet"]
+    n = sum(lens)
+    plan = codec.SegmentPlan(lens, 0.99, torch.device(DEV))
+    g = torch.Generator(device=DEV).manual_seed(580)
+    x = torch.randn(n, generator=g, device=DEV)
+    hat = x + 0.1 * torch.randn(n, generator=g, device=DEV)
+    mem = hat + 0.05 * torch.randn(n, generator=g, device=DEV)
+    prev_clean, before, checked = False, None, False
+    for step in range(12):
+        s1 = codec.launch_count("topk_seg_hist")  # the cold sequence's first launch
+        m0 = codec.topk_fallback_count(plan=plan)
+        jump = prev_clean and before is None  # after a warm call without a miss the host stays warm
+        if jump:
+            x = hat + 100.0 * (x - hat)
+            before = m0
+        xa = O.gossip_step(host(x), host(mem), host(hat), 0.9)
+        vals, idx = codec.topk_segmented(x, plan, xhat=hat, gossip=(mem, 0.9))
+        assert same_bits(host(x), xa)
+        ov, oi, _ = O.topk_segmented((xa - host(hat)).astype(np.float32), lens, 0.99)
+        assert np.array_equal(host(idx).astype(np.int64), oi)
+        assert same_bits(host(vals), ov)
+        warm = codec.launch_count("topk_seg_hist") == s1
+        if jump:
+            assert warm and codec.topk_fallback_count(plan=plan) > before  # warm, and its windows missed
+            checked = True
+        prev_clean = warm and codec.topk_fallback_count(plan=plan) == m0
+        codec.sparse_accumulate(vals, idx, mem, 1.0, xhat_self=hat)
+    assert checked
+    codec.check_topk_status(wait=True)
 
 
 def test_topk_segmented_warm_ratio0_and_half():
