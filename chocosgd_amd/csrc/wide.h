@@ -293,10 +293,10 @@ CHOCO_DEV void wide_select(const Src<MODE, XH>& src, int64_t n, int64_t k, uint3
           uint32_t pos = out + block_excl_scan(ns, es.scratch, &st);
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            if (sel[c]) {
-              emit(pos, i0 + c, vv[c]);
-              ++pos;
-            }
+            // (bounded: a wait that gave up leaves the counts unreliable -- the call is flagged
+            // invalid, and nothing may be written past the range's k outputs)
+            if (sel[c] && pos < (uint64_t)k) emit(pos, i0 + c, vv[c]);
+            pos += sel[c] ? 1u : 0u;
           }
           out += st;
           tie_run += tt;
