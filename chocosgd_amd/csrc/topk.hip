@@ -1297,9 +1297,9 @@ CHOCO_DEV void wide_fallback(const Src<MODE, XH>& src, int64_t n, int64_t k, uin
                              float* __restrict__ out_val,
                              int32_t* __restrict__ out_idx, int64_t idx_base, ExactSmem& es, uint32_t* s_tk,
                              uint32_t* __restrict__ status, uint32_t* __restrict__ host_status, TopkBounds* next) {
-  wide_select<kK4Threads, 4>(  // 4 float4 rows per stream in flight
-
-      src, n, k, tile, nb, W, gcnt, thist, es, s_tk, status, host_status,
+  wide_select<kK4Threads>(
+      RangeTiles<kK4Threads, 4, MODE, XH>{src, n, tile},  // 4 float4 rows per stream in flight
+      k, nb, W, gcnt, thist, es, s_tk, status, host_status,
       [&](uint32_t) {
         if (next != nullptr) fallback_window(W, n, k, es, next);
       },

@@ -576,7 +576,10 @@ __global__ __launch_bounds__(kSegThreads, kSegWpe) void seg_collect_kernel(
 // S4 then places each tile from the counts of the tiles before it.
 constexpr int kS3Threads = 256;
 constexpr int kH3 = 512;  // bits 8..0 (cold) / the low sh <= 9 bits of a window bin (warm)
-enum SegMode { kSegSelect = 0, kSegMissed = 1, kSegAll = 2 };
+// kSegMissed: T below the window (fewer candidates than k) or no window: the shared exact
+// select reads the segment; kSegMissedHigh: T above the window's top bin -- every key >= T is
+// a candidate, so the shared select reads the tiles' candidate lists only.
+enum SegMode { kSegSelect = 0, kSegMissed = 1, kSegAll = 2, kSegMissedHigh = 3 };
 
 // Over hist[nb] in global memory (ascending key order), the bin holding the
 // rank-th largest entry and the rank inside it -> out[0], out[1], and the
@@ -857,7 +860,8 @@ __global__ __launch_bounds__(kS3Threads) void seg_bin_kernel(
   const uint32_t b2 = bc[0];
   uint32_t mode = kSegSelect;
   if (c.R.k >= c.R.len) mode = kSegAll;
-  else if (!w.valid || bc[2] < rank || b2 == (uint32_t)(kH - 1)) mode = kSegMissed;  // T below the window or in its clamped top
+  else if (!w.valid || bc[2] < rank) mode = kSegMissed;  // T below the window (or none)
+  else if (b2 == (uint32_t)(kH - 1)) mode = kSegMissedHigh;  // T in the window's clamped top bin
   if (c.j == 0 && tid == 0) {
     info[8 * c.s + 0] = lo;
     info[8 * c.s + 1] = sh;
@@ -1003,6 +1007,47 @@ __global__ __launch_bounds__(kS4Threads) void seg_emit_kernel(
   }
 }
 
+// The shared select's reader over the tiles' candidate lists (W2's compaction: values and
+// global indices in index order, tilecnt[b] of them at slot b * kSegTile): the missed
+// segments whose k-th key lies above the window hold every key >= T among them.
+template <int NT, int U>
+struct CandTiles {
+  const float* __restrict__ cval;
+  const uint32_t* __restrict__ cidx;
+  const uint32_t* __restrict__ tilecnt;
+  int64_t t0;  // the segment's first tile
+  template <class F>
+  CHOCO_DEV void operator()(uint32_t t, F&& fn) const {
+    const int64_t b = t0 + t;
+    const uint32_t cnt = tilecnt[b];
+    const __amdgpu_buffer_rsrc_t rv = buf_rsrc(cval + b * kSegTile, cnt * 4u);
+    const __amdgpu_buffer_rsrc_t ri = buf_rsrc(reinterpret_cast<const float*>(cidx) + b * kSegTile, cnt * 4u);
+    constexpr uint32_t kStep = NT * 4u;
+    for (uint32_t b0 = 0; b0 < cnt; b0 += kStep * U) {  // workgroup-uniform
+      float4 v[U], q[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t off = (b0 + (uint32_t)u * kStep + 4u * threadIdx.x) * 4u;
+        v[u] = ld_buf4<false>(rv, off);
+        q[u] = ld_buf4<false>(ri, off);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (b0 + (uint32_t)u * kStep >= cnt) break;  // block-uniform
+        const uint32_t e0 = b0 + (uint32_t)u * kStep + 4u * threadIdx.x;
+        const int nin = e0 >= cnt ? 0 : (int)min(4u, cnt - e0);
+        const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        const int64_t ii[4] = {(int64_t)__float_as_uint(q[u].x), (int64_t)__float_as_uint(q[u].y),
+                               (int64_t)__float_as_uint(q[u].z), (int64_t)__float_as_uint(q[u].w)};
+        uint32_t kk[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) kk[c] = c < nin ? fkey(vv[c]) : 0u;
+        fn(nin, kk, vv, ii);
+      }
+    }
+  }
+};
+
 // S4w (warm, after S3w): every tile's (#above b2, #in b2) counts and kept keys of its
 // segment are loaded in one round trip (with the tile's first 256 candidates), T is taken
 // from the kept keys -- histogrammed by their low sh bits in LDS (bins of one key), the
@@ -1095,45 +1140,56 @@ __global__ __launch_bounds__(kS4Threads, 7) void seg_emit_w_kernel(
   if (ovf) s_ovf = 1u;
   __syncthreads();
   const bool overflow = mode == kSegSelect && s_ovf != 0u;
-  if (mode == kSegMissed || overflow) {  // workgroup-uniform: the segment's tiles select it exactly together
-    if (segwg) return;
-    if (c.j == 0 && tid == 0 && mode == kSegMissed) {
+  if (mode == kSegMissed || mode == kSegMissedHigh || overflow) {  // workgroup-uniform: the segment's tiles
+    if (segwg) return;                                                // select it exactly together
+    if (c.j == 0 && tid == 0 && mode != kSegSelect) {
       atomicAdd(misses, 1u);
       if (miss_flag) __hip_atomic_store(miss_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    Src<kData, XH> src{x + c.R.off, XH ? xh + c.R.off : nullptr, 0};
-    // (2 rows in flight, and the launch bounds hold S4w at 7 waves per SIMD: the shared
-    // select is the rare branch of this kernel)
-    wide_select<kS4Threads, 2>(
-        src, c.R.len, c.R.k, (uint32_t)kSegTile, (uint32_t)c.R.ntile, wide + c.s, wcnt + 2 * c.R.t0,
-        whist + 512 * c.R.t0, es, &s_tk, status, host_status,
-        [&](uint32_t T) {  // (every thread of the workgroup that learnt T; no other reader of win / hist2 is left)
-          const SegWin prev = win[c.s];
-          if (overflow) {  // the window held T: the next one from this call's hist2, as usual
-            seg_next_window(g2, lo, sh, 0u, (uint32_t)c.R.k, T, prev, &win[c.s], scratch);
-          } else {
-            // missed: the next window from this select's digit-1 histogram -- the keys of T's
-            // coarse bin (key >> 20) in bins of 2^9 keys, with the keys of the coarse bins
-            // above it -- at the usual count levels around k (a blind window centred on T
-            // with the widest bins overflowed its bin lists on the next call)
-            const WideCtrl* Wd = wide + c.s;
-            const uint32_t d0 = T >> 20;
-            uint32_t a = 0u;
-            for (int i = tid; i < kH; i += kS4Threads) a += (uint32_t)i > d0 ? ld_sc1(&Wd->hist[0][i]) : 0u;
-            uint32_t above;
-            block_excl_scan(a, scratch, &above);
-            uint32_t hv[kWinPer];
+    auto on_T = [&](uint32_t T) {  // (every thread of the workgroup that learnt T; no other reader of win / hist2 is left)
+      const SegWin prev = win[c.s];
+      if (overflow) {  // the window held T: the next one from this call's hist2, as usual
+        seg_next_window(g2, lo, sh, 0u, (uint32_t)c.R.k, T, prev, &win[c.s], scratch);
+      } else {
+        // missed: the next window from this select's digit-1 histogram -- the keys of T's
+        // coarse bin (key >> 20) in bins of 2^9 keys, with the keys of the coarse bins above
+        // it -- at the usual count levels around k (a blind window centred on T with the
+        // widest bins overflowed its bin lists on the next call).  (Over candidate lists the
+        // counts below the old window's floor are short: the level k + delta then lands at
+        // the coarse bin's floor or the old floor, a wider window.)
+        const WideCtrl* Wd = wide + c.s;
+        const uint32_t d0 = T >> 20;
+        uint32_t a = 0u;
+        for (int i = tid; i < kH; i += kS4Threads) a += (uint32_t)i > d0 ? ld_sc1(&Wd->hist[0][i]) : 0u;
+        uint32_t above;
+        block_excl_scan(a, scratch, &above);
+        uint32_t hv[kWinPer];
 #pragma unroll
-            for (int j = 0; j < kWinPer; ++j) hv[j] = ld_sc1(&Wd->hist[1][tid * kWinPer + j]);
-            seg_next_window_v(hv, d0 << 20, 9u, above, (uint32_t)c.R.k, T, prev, &win[c.s], scratch);
-          }
-          __syncthreads();
-          for (int i = tid; i < kH; i += kS4Threads) g2[i] = 0u;
-        },
-        [&](uint32_t pos, int64_t i, float v) {
-          out_val[c.R.out_off + pos] = v;
-          out_idx[c.R.out_off + pos] = (int32_t)(i + c.R.off);
-        });
+        for (int j = 0; j < kWinPer; ++j) hv[j] = ld_sc1(&Wd->hist[1][tid * kWinPer + j]);
+        seg_next_window_v(hv, d0 << 20, 9u, above, (uint32_t)c.R.k, T, prev, &win[c.s], scratch);
+      }
+      __syncthreads();
+      for (int i = tid; i < kH; i += kS4Threads) g2[i] = 0u;
+    };
+    // (2 rows in flight over the segment, 1 over the candidate lists -- a few hundred per
+    // tile, one row; the launch bounds hold S4w at 7 waves per SIMD without spills: the
+    // shared select is the rare branch of this kernel)
+    if (mode == kSegMissed) {
+      Src<kData, XH> src{x + c.R.off, XH ? xh + c.R.off : nullptr, 0};
+      wide_select<kS4Threads>(RangeTiles<kS4Threads, 2, kData, XH>{src, c.R.len, (uint32_t)kSegTile}, c.R.k,
+                              (uint32_t)c.R.ntile, wide + c.s, wcnt + 2 * c.R.t0, whist + 512 * c.R.t0, es, &s_tk,
+                              status, host_status, on_T, [&](uint32_t pos, int64_t i, float v) {
+                                out_val[c.R.out_off + pos] = v;
+                                out_idx[c.R.out_off + pos] = (int32_t)(i + c.R.off);
+                              });
+    } else {  // every key >= T is among the candidates: select over the tiles' candidate lists
+      wide_select<kS4Threads>(CandTiles<kS4Threads, 1>{cval, cidx, tilecnt, c.R.t0}, c.R.k, (uint32_t)c.R.ntile,
+                              wide + c.s, wcnt + 2 * c.R.t0, whist + 512 * c.R.t0, es, &s_tk, status, host_status,
+                              on_T, [&](uint32_t pos, int64_t ix, float v) {
+                                out_val[c.R.out_off + pos] = v;
+                                out_idx[c.R.out_off + pos] = (int32_t)ix;
+                              });
+    }
     return;
   }
   // ---- T and the ties at it to take, from the kept keys (mode kSegAll: every candidate)

@@ -174,15 +174,34 @@ CHOCO_DEV void wide_tile(const Src<MODE, XH>& src, int64_t lo, int64_t hi, F&& f
   }
 }
 
-// The shared select over src[0, n) in nb tiles of `tile` elements, by exactly nb
-// workgroups of NT threads, U rows of loads in flight per stream.  gcnt: 2 words per
-// tile, thist: 512 words per tile (phase 2 -> phase 3 -> phase 4).
+// A tile reader of wide_select: reader(t, fn) calls fn(n_in, keys[4], vals[4], idx[4]) for
+// every row of tile t, by every thread (block-uniform rows); idx is what emit() receives.
+// RangeTiles: src[0, n) in tiles of `tile` elements, idx the element index.
+template <int NT, int U, int MODE, bool XH>
+struct RangeTiles {
+  Src<MODE, XH> src;
+  int64_t n;
+  uint32_t tile;
+  template <class F>
+  CHOCO_DEV void operator()(uint32_t t, F&& fn) const {
+    const int64_t lo = (int64_t)t * tile, hi = min(lo + (int64_t)tile, n);
+    wide_tile<NT, U>(src, lo, hi, [&](int64_t i0, int nin, const uint32_t (&kk)[4], const float (&vv)[4]) {
+      const int64_t ii[4] = {i0, i0 + 1, i0 + 2, i0 + 3};
+      fn(nin, kk, vv, ii);
+    });
+  }
+};
+
+// The shared select over the nb tiles of `reader` (k outputs), by exactly nb workgroups
+// of NT threads.  gcnt: 2 words per tile, thist: 512 words per tile (phase 2 -> phase 3
+// -> phase 4).
 // on_T(T): called by every thread of the workgroup that runs tile 0's phase-3 item,
 // once T is known (the caller's next window; W->hist still holds this call's digits).
-// emit(pos, i, v): every selected element, pos its rank in the output (ascending i).
-template <int NT, int U, int MODE, bool XH, class OnT, class Emit>
-CHOCO_DEV void wide_select(const Src<MODE, XH>& src, int64_t n, int64_t k, uint32_t tile, uint32_t nb, WideCtrl* W,
-                           uint32_t* __restrict__ gcnt, uint32_t* __restrict__ thist, ExactSmem& es, uint32_t* s_tk, uint32_t* __restrict__ status,
+// emit(pos, idx, v): every selected element, pos its rank in the output (tile order, and
+// row order inside a tile: ascending index for both readers).
+template <int NT, class Reader, class OnT, class Emit>
+CHOCO_DEV void wide_select(const Reader& reader, int64_t k, uint32_t nb, WideCtrl* W, uint32_t* __restrict__ gcnt,
+                           uint32_t* __restrict__ thist, ExactSmem& es, uint32_t* s_tk, uint32_t* __restrict__ status,
                            uint32_t* __restrict__ host_status, OnT&& on_T, Emit&& emit) {
   const int tid = threadIdx.x;
   const bool w0 = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;  // wave-uniform
@@ -204,7 +223,6 @@ CHOCO_DEV void wide_select(const Src<MODE, XH>& src, int64_t n, int64_t k, uint3
       }
       __syncthreads();
     }
-    const int64_t lo = (int64_t)t * tile, hi = min(lo + (int64_t)tile, n);
     const int need = phase < 3 ? phase : 3;
     wide_digits<NT>(W, have, need, es, prefix, maskhi, krem);
     have = max(have, need);
@@ -215,7 +233,7 @@ CHOCO_DEV void wide_select(const Src<MODE, XH>& src, int64_t n, int64_t k, uint3
       __syncthreads();
       const int lane = lane_id();
       uint32_t above = 0u;  // (phase 2: keys above the first two digits' prefix)
-      wide_tile<NT, U>(src, lo, hi, [&](int64_t, int nin, const uint32_t (&kk)[4], const float (&)[4]) {
+      reader(t, [&](int nin, const uint32_t (&kk)[4], const float (&)[4], const int64_t (&)[4]) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           above += (c < nin && (kk[c] & maskhi) > prefix) ? 1u : 0u;
@@ -273,7 +291,7 @@ CHOCO_DEV void wide_select(const Src<MODE, XH>& src, int64_t n, int64_t k, uint3
         const uint32_t taken = min(r, etot);  // ties taken by the earlier tiles
         uint32_t out = gtot + taken, tie_run = etot;
         // ordered compaction, row by row: ties by global rank (lowest index first)
-        wide_tile<NT, U>(src, lo, hi, [&](int64_t i0, int nin, const uint32_t (&kk)[4], const float (&vv)[4]) {
+        reader(t, [&](int nin, const uint32_t (&kk)[4], const float (&vv)[4], const int64_t (&ii)[4]) {
           uint32_t neq = 0;
 #pragma unroll
           for (int c = 0; c < 4; ++c) neq += (c < nin && kk[c] == T) ? 1u : 0u;
@@ -295,7 +313,7 @@ CHOCO_DEV void wide_select(const Src<MODE, XH>& src, int64_t n, int64_t k, uint3
           for (int c = 0; c < 4; ++c) {
             // (bounded: a wait that gave up leaves the counts unreliable -- the call is flagged
             // invalid, and nothing may be written past the range's k outputs)
-            if (sel[c] && pos < (uint64_t)k) emit(pos, i0 + c, vv[c]);
+            if (sel[c] && pos < (uint64_t)k) emit(pos, ii[c], vv[c]);
             pos += sel[c] ? 1u : 0u;
           }
           out += st;
