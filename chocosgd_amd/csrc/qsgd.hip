@@ -106,6 +106,9 @@ CHOCO_DEV void st_gs4(float* p, float4 v) {
 // ---------------------------------------------------------------- pass 1: norms
 // GS: the fused gossip step (x_new = x + gamma (memory - xh) written back, the
 // norm is of d = x_new - xh; the quantize pass then reads (x_new, xh)).
+// (A flat instantiation without the segment code, as qsgd_decode_kernel's, measured: the
+// fused gossip form 145 -> 106 VGPRs but 297-300 -> 304-305 us at 100M, the plain one 69.6-70.2
+// -> 69.2-69.5 us; not kept, profiles/r06_ab_summary.txt item 16.)
 template <bool XH, bool GS = false>
 __global__ __launch_bounds__(kQThreads) void qsgd_norm_kernel(const float* __restrict__ x,
                                                               const float* __restrict__ xh, int64_t n,
@@ -706,7 +709,10 @@ CHOCO_DEV float4 qdec_ld4(const float* p) { return *reinterpret_cast<const float
 CHOCO_DEV void st_dec4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 // MODE 0: out = decode(msg 0); MODE 1: accumulate all messages into hat/mem.
-template <int CW, int NM, int MODE>
+// SEG: a per-tensor layout (nseg > 1); the flat instantiation drops the segment lookups and
+// the per-element segment walk (3-message decode 96 -> 59 VGPRs: the ring step's receive
+// at 100M 330-333 -> 295 us, profiles/r06_ab_summary.txt item 16).
+template <int CW, int NM, int MODE, bool SEG>
 __global__ __launch_bounds__(kQThreads) void qsgd_decode_kernel(QMsgs M, int64_t n,
                                                                 const int64_t* __restrict__ seg_off, int nseg,
                                                                 int s_levels, int biased,
@@ -715,8 +721,8 @@ __global__ __launch_bounds__(kQThreads) void qsgd_decode_kernel(QMsgs M, int64_t
   __shared__ int s_seg[2];
   const int64_t t_e0 = (blk_lo + (int64_t)blockIdx.x) * kQTile;
   const int64_t t_e1 = std::min<int64_t>(t_e0 + kQTile, n);
-  const int sg0 = tile_seg(seg_off, nseg, t_e0, t_e1, s_seg);
-  const bool uniform = s_seg[1] == sg0;
+  const int sg0 = SEG ? tile_seg(seg_off, nseg, t_e0, t_e1, s_seg) : 0;
+  const bool uniform = !SEG || s_seg[1] == sg0;
   const int64_t e0 = t_e0 + (int64_t)threadIdx.x * kQPer;
   if (e0 >= n) return;
   const float sf = (float)s_levels;
@@ -801,7 +807,7 @@ __global__ __launch_bounds__(kQThreads) void qsgd_decode_kernel(QMsgs M, int64_t
 // otherwise queue on one address); the last workgroup sums the replicas.
 constexpr int kRG = 2;
 constexpr int kRTile = kQTile * kRG;  // 4096 elements per workgroup
-template <int CW, int NM>
+template <int CW, int NM, bool SEG>  // (SEG: as qsgd_decode_kernel)
 __global__ __launch_bounds__(kQThreads) void qsgd_recv_gossip_norm_kernel(
     QMsgs M, int64_t n, const int64_t* __restrict__ seg_off, int nseg, int s_levels, int biased,
     float* __restrict__ x, float* __restrict__ hat, float* __restrict__ mem, float gamma,
@@ -814,8 +820,8 @@ __global__ __launch_bounds__(kQThreads) void qsgd_recv_gossip_norm_kernel(
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const int64_t t_e0 = (int64_t)blockIdx.x * kRTile;
   const int64_t t_e1 = std::min<int64_t>(t_e0 + kRTile, n);
-  const int sg0 = tile_seg(seg_off, nseg, t_e0, t_e1, s_seg);
-  const bool uniform = s_seg[1] == sg0;
+  const int sg0 = SEG ? tile_seg(seg_off, nseg, t_e0, t_e1, s_seg) : 0;
+  const bool uniform = !SEG || s_seg[1] == sg0;
   const float sf = (float)s_levels;
   const bool has_self = M.self_slot >= 0;
   float xv[kRG][kQPer], hv[kRG][kQPer], mv[kRG][kQPer];
@@ -940,10 +946,14 @@ static void launch_recv_gossip(const QMsgs& M, int64_t n, const int64_t* seg_off
                                int biased, float* x, float* hat, float* mem, float gamma, QsgdWs* ws, float* norms,
                                hipStream_t st) {
   const unsigned grid = (unsigned)((n + kRTile - 1) / kRTile);
-#define CHOCO_RG(NMV)                                                                                     \
-  case NMV:                                                                                               \
-    CHOCO_KLAUNCH((qsgd_recv_gossip_norm_kernel<CW, NMV>), dim3(grid), dim3(kQThreads), 0, st, M, n, seg_off, \
-                  nseg, s_levels, biased, x, hat, mem, gamma, ws, norms);                                 \
+#define CHOCO_RG(NMV)                                                                                      \
+  case NMV:                                                                                                \
+    if (nseg > 1)                                                                                          \
+      CHOCO_KLAUNCH((qsgd_recv_gossip_norm_kernel<CW, NMV, true>), dim3(grid), dim3(kQThreads), 0, st, M, n, \
+                    seg_off, nseg, s_levels, biased, x, hat, mem, gamma, ws, norms);                       \
+    else                                                                                                   \
+      CHOCO_KLAUNCH((qsgd_recv_gossip_norm_kernel<CW, NMV, false>), dim3(grid), dim3(kQThreads), 0, st, M,   \
+                    n, seg_off, nseg, s_levels, biased, x, hat, mem, gamma, ws, norms);                    \
     break;
   switch (M.nmsg) {
     CHOCO_RG(1)
@@ -963,8 +973,12 @@ template <int CW, int NM, int MODE>
 static void launch_decode(const QMsgs& M, int64_t n, const int64_t* seg_off, int nseg, int s_levels, int biased,
                           float* hat, float* mem, hipStream_t st, int64_t e0, int64_t e1) {
   const unsigned grid = (unsigned)((e1 - e0 + kQTile - 1) / kQTile);
-  CHOCO_KLAUNCH((qsgd_decode_kernel<CW, NM, MODE>), dim3(grid), dim3(kQThreads), 0, st, M, n, seg_off, nseg,
-                     s_levels, biased, hat, mem, e0 / kQTile);
+  if (nseg > 1)
+    CHOCO_KLAUNCH((qsgd_decode_kernel<CW, NM, MODE, true>), dim3(grid), dim3(kQThreads), 0, st, M, n, seg_off, nseg,
+                  s_levels, biased, hat, mem, e0 / kQTile);
+  else
+    CHOCO_KLAUNCH((qsgd_decode_kernel<CW, NM, MODE, false>), dim3(grid), dim3(kQThreads), 0, st, M, n, seg_off, nseg,
+                  s_levels, biased, hat, mem, e0 / kQTile);
 }
 
 template <int CW, int MODE>
@@ -1028,7 +1042,7 @@ static int qsgd_norms_launch(const float* x, const float* xhat, int64_t n, const
   const unsigned g1 = (unsigned)((n + tile - 1) / tile);
   QsgdWs* w = static_cast<QsgdWs*>(ws);
   profile_begin("qsgd_norm", st);
-  if (gs.mem)
+if (gs.mem)
     CHOCO_KLAUNCH((qsgd_norm_kernel<true, true>), dim3(g1), dim3(kQThreads), 0, st, x, xhat, n, seg_off, nseg,
                   norms_out, w, gs, tile);
   else if (xhat)
